@@ -1,0 +1,170 @@
+#!/usr/bin/env python
+"""fedmi headline benchmark (BASELINE.json): rounds/s + samples/s/client,
+2-conv CNN (LeNet) FedAvg at 1/2/4/8 MI355X clients.
+
+One process per GPU = one federated client (torchrun launches N ranks).
+A *step* is one federated round with the reference's semantics
+(SURVEY.md §6 / BASELINE.md "Round time"):
+
+  1. local epoch: one pass over this client's strided 1/N shard of the 50,000
+     training images at batch 128 with RandomCrop+HFlip augmentation, SGD
+     (lr 0.1, momentum 0.9, wd 5e-4)   [fused HIP kernels, hipGraph replay]
+  2. FedAvg of the full model across clients   [RCCL all-reduce over xGMI]
+  3. every client evaluates the global model on the full 10,000-image test set
+  4. the global model is persisted as Primary/optimizedModel.pth (rank 0) and
+     every client checkpoint as checkpoint/<client>.pth ({'net','acc','epoch'}),
+     flushed to disk inside the timed region.
+
+Total work per round is fixed (50k samples split over N clients) -> strong
+scaling.  ``value`` is the whole-job training throughput (samples/s summed over
+clients = 50,000 x rounds/s); rounds/s and samples/s/client are reported too.
+Data: synthetic CIFAR-shaped uint8 images, random-init weights.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+# Reference (CPU-measured) rounds/s with LeNet at N clients.
+BASELINE_ROUNDS_PER_S = {1: 0.373, 2: 0.428, 4: 0.436, 8: 0.426}
+N_TRAIN, N_TEST, BATCH = 50000, 10000, 128
+
+
+def _baseline_samples_per_s(n: int) -> float:
+    key = min(BASELINE_ROUNDS_PER_S, key=lambda k: abs(k - n))
+    return BASELINE_ROUNDS_PER_S[key] * N_TRAIN
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20, help="timed federated rounds")
+    ap.add_argument("--warmup", type=int, default=3, help="untimed rounds")
+    ap.add_argument("--model", default="lenet")
+    ap.add_argument("--compress", default="none", choices=["none", "topk", "int8"],
+                    help="-c Y data-plane compression of the FedAvg update")
+    ap.add_argument("--topk-ratio", type=float, default=0.01)
+    ap.add_argument("--no-eval", action="store_true", help="skip per-round eval (NOT the headline config)")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--ckpt-dir", default=None)
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run",
+              file=sys.stderr)
+        return 2
+    if not torch.cuda.is_available():
+        print("[bench] no GPU visible", file=sys.stderr)
+        return 2
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+
+    from fedmi.ckpt import AsyncCheckpointWriter, OPTIMIZED_MODEL, client_ckpt_path, mount_dir
+    from fedmi.engine import build_trainer
+    from fedmi.engine.base import TrainerConfig
+    from fedmi.engine.data import make_dataset, strided_schedule
+    from fedmi.parallel.fedavg import FedAvg, broadcast_state_
+    from fedmi.parallel.compress import make_compressor
+
+    data = make_dataset("synthetic-cifar10", device=device, n_train=N_TRAIN, n_test=N_TEST, seed=0)
+    cfg = TrainerConfig(seed=17, use_graph=not args.no_graph)
+    trainer = build_trainer(args.model, data, device, cfg)
+    broadcast_state_(trainer, 0)                     # one shared init (reference quirk A7 fixed)
+    trainer.set_schedule(*strided_schedule(N_TRAIN, BATCH, rank, world))
+    agg = FedAvg(compressor=make_compressor(args.compress, args.topk_ratio, trainer))
+
+    root = Path(args.ckpt_dir or tempfile.mkdtemp(prefix="fedmi_bench_"))
+    prim = mount_dir(root, primary=True) if rank == 0 else None
+    cpath = client_ckpt_path(root, f"client{rank}")
+    writer = AsyncCheckpointWriter()
+
+    def one_round(r: int) -> None:
+        trainer.train_epoch()
+        agg.average(trainer)
+        if not args.no_eval:
+            trainer.evaluate()
+        sd = trainer.state_dict()
+        if prim is not None:
+            writer.submit(prim / OPTIMIZED_MODEL, sd, acc=1, epoch=r + 1)
+        writer.submit(cpath, sd, acc=1, epoch=r + 1)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local_rank])
+        torch.cuda.synchronize(device)
+
+    for r in range(args.warmup):
+        one_round(r)
+    writer.flush()
+    barrier()
+    t0 = time.perf_counter()
+    for r in range(args.warmup, args.warmup + args.steps):
+        one_round(r)
+    writer.flush()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    T = float(elapsed.item())
+
+    tr_stats = trainer.train_stats()
+    ev_stats = trainer.eval_stats() if not args.no_eval else None
+    rounds_per_s = args.steps / T
+    value = rounds_per_s * N_TRAIN
+    out = {
+        "metric": "rounds/sec + samples/sec/client, 2-conv CNN FedAvg at 1/2/4/8 MI355X clients",
+        "value": round(value, 3),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(T / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": round(value / _baseline_samples_per_s(world), 3),
+        "dtype": "bf16",
+        "data": "synthetic (CIFAR-shaped uint8 50k/10k, class-structured), random-init weights",
+        "config": {"model": args.model, "global_batch": BATCH * world, "seq_len": None,
+                   "parallelism": f"fedavg-dp{world}", "per_client_batch": BATCH,
+                   "local_epochs_per_round": 1, "eval_per_round": not args.no_eval,
+                   "aggregation": "rccl-allreduce" + ("" if args.compress == "none" else f"+{args.compress}"),
+                   "hip_graph": not args.no_graph},
+        "rounds_per_sec": round(rounds_per_s, 4),
+        "samples_per_sec_per_client": round(value / world, 3),
+        "baseline_rounds_per_sec": BASELINE_ROUNDS_PER_S.get(world),
+        "last_round": {"train_loss": round(tr_stats.loss, 4), "train_acc": round(tr_stats.acc, 3),
+                       **({"test_loss": round(ev_stats.loss, 4), "test_acc": round(ev_stats.acc, 3)}
+                          if ev_stats else {})},
+        "allreduce_ms_last": round(agg.timer.last_ms, 4),
+    }
+    writer.close()
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            Path(args.json_out).write_text(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,200 @@
+// fedmi — Python bindings for the native runtime and HIP kernels.
+//
+// Device memory is owned by PyTorch tensors (caching allocator); the native
+// side receives raw device pointers and the torch stream handle, so every
+// launch is ordered on torch's current stream and can be graph-captured.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <vector>
+
+#include "kernels/lenet_layout.h"
+#include "runtime/lenet_engine.h"
+
+namespace py = pybind11;
+
+namespace fedmi {
+void launch_lenet_conv_fwd(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*, int,
+                           bf16*, bf16*, int, bf16*, uint8_t*, uint8_t*);
+void launch_lenet_fc_head(hipStream_t, const bf16*, const bf16*, int, const int*, int, int, const bf16*, const float*,
+                          float*, float*, lenet::Stats*);
+void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const float*, const bf16*,
+                           const uint8_t*, const uint8_t*, const bf16*, float*);
+void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, const float*, int, float, float, float, int*);
+void launch_lenet_pack(hipStream_t, const float*, bf16*);
+void launch_sgd_flat(hipStream_t, float*, const float*, float*, long, float, float, float, float, int, int);
+int fedavg_max_inputs();
+void launch_fedavg_reduce(hipStream_t, const float* const*, const float*, int, float*, long);
+void launch_scale(hipStream_t, float*, long, float);
+size_t select_state_bytes();
+int compact_chunk();
+void launch_ef_delta(hipStream_t, const float*, const float*, const float*, float*, long);
+void launch_topk(hipStream_t, const float*, long, int, void*, int*, int*, float*, float*);
+void launch_scatter_add_scaled(hipStream_t, float*, const int*, const float*, long, float, long);
+void launch_quant_int8(hipStream_t, const float*, long, signed char*, float*, float*);
+void launch_dequant_accum(hipStream_t, const signed char*, const float*, int, long, float*, float);
+}  // namespace fedmi
+
+using namespace fedmi;
+
+template <typename T>
+static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static void check_last(const char* what) { check_hip(hipGetLastError(), what); }
+
+static LeNetBuffers buffers_from(const py::dict& d) {
+  auto get = [&](const char* k) -> uintptr_t { return d.contains(k) ? d[k].cast<uintptr_t>() : 0; };
+  LeNetBuffers b;
+  b.train_images = P<const uint8_t>(get("train_images"));
+  b.train_labels = P<const int>(get("train_labels"));
+  b.n_train = d.contains("n_train") ? d["n_train"].cast<int>() : 0;
+  b.params = P<float>(get("params"));
+  b.mom = P<float>(get("mom"));
+  b.pk = P<bf16>(get("pk"));
+  b.act2 = P<bf16>(get("act2"));
+  b.act2_rows = d.contains("act2_rows") ? d["act2_rows"].cast<int>() : 0;
+  b.act2T = P<bf16>(get("act2T"));
+  b.pool1 = P<bf16>(get("pool1"));
+  b.am1 = P<uint8_t>(get("am1"));
+  b.am2 = P<uint8_t>(get("am2"));
+  b.dact2 = P<float>(get("dact2"));
+  b.conv_slab = P<float>(get("conv_slab"));
+  b.fc_slab = P<float>(get("fc_slab"));
+  b.train_stats = P<lenet::Stats>(get("train_stats"));
+  b.eval_stats = P<lenet::Stats>(get("eval_stats"));
+  b.round_ctr = P<int>(get("round_ctr"));
+  return b;
+}
+
+PYBIND11_MODULE(_fedmi_native, m) {
+  m.doc() = "fedmi native runtime: fused LeNet HIP kernels, graph executor, flat-buffer and compression kernels (gfx950)";
+
+  m.def("lenet_layout", []() {
+    using namespace lenet;
+    py::dict d;
+    d["P_C1W"] = P_C1W; d["P_C1B"] = P_C1B; d["P_C2W"] = P_C2W; d["P_C2B"] = P_C2B;
+    d["P_F1W"] = P_F1W; d["P_F1B"] = P_F1B; d["P_F2W"] = P_F2W; d["P_F2B"] = P_F2B;
+    d["P_F3W"] = P_F3W; d["P_F3B"] = P_F3B; d["P_TOTAL"] = P_TOTAL;
+    d["CS"] = CS; d["FS"] = FS; d["PK_TOTAL"] = PK_TOTAL; d["F0"] = F0; d["F0P"] = F0P; d["NP1"] = NP1;
+    d["MAX_TRAIN_BATCH"] = MAX_TRAIN_BATCH; d["FC_SPW"] = FC_SPW; d["MAX_FC_WG"] = MAX_FC_WG;
+    d["IMG_BYTES"] = IMG_BYTES; d["STATS_BYTES"] = (int)sizeof(Stats);
+    return d;
+  });
+
+  py::class_<SgdConfig>(m, "SgdConfig")
+      .def(py::init<>())
+      .def_readwrite("lr", &SgdConfig::lr)
+      .def_readwrite("momentum", &SgdConfig::momentum)
+      .def_readwrite("weight_decay", &SgdConfig::weight_decay);
+
+  py::class_<LeNetEngine>(m, "LeNetEngine")
+      .def(py::init([](const py::dict& bufs, float lr, float momentum, float wd, uint32_t seed, bool augment) {
+             SgdConfig c;
+             c.lr = lr; c.momentum = momentum; c.weight_decay = wd;
+             return new LeNetEngine(buffers_from(bufs), c, seed, augment);
+           }),
+           py::arg("buffers"), py::arg("lr"), py::arg("momentum"), py::arg("weight_decay"), py::arg("seed"),
+           py::arg("augment"))
+      .def("set_schedule", &LeNetEngine::set_schedule)
+      .def("schedule_len", &LeNetEngine::schedule_len)
+      .def("step", [](LeNetEngine& e, uintptr_t st, int start, int nb, bool bump) { e.step(S(st), start, nb, bump); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("run_epoch", [](LeNetEngine& e, uintptr_t st, bool use_graph) { e.run_epoch(S(st), use_graph); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("eval", [](LeNetEngine& e, uintptr_t st, uintptr_t images, uintptr_t labels, int n) {
+             e.eval(S(st), P<const uint8_t>(images), P<const int>(labels), n);
+           }, py::call_guard<py::gil_scoped_release>())
+      .def("pack", [](LeNetEngine& e, uintptr_t st) { e.pack(S(st)); }, py::call_guard<py::gil_scoped_release>())
+      .def("set_sgd", [](LeNetEngine& e, float lr, float m, float wd) {
+             SgdConfig c; c.lr = lr; c.momentum = m; c.weight_decay = wd; e.set_sgd(c);
+           })
+      .def("graph_ready", &LeNetEngine::graph_ready);
+
+  // ---- raw LeNet kernels (numerics tests drive them one by one) -------------
+  m.def("lenet_conv_fwd", [](uintptr_t st, uintptr_t images, int base, int nb, uintptr_t pk, uintptr_t params,
+                             uint32_t seed, uintptr_t round_ctr, int augment, uintptr_t act2, uintptr_t act2T,
+                             int tstride, uintptr_t pool1, uintptr_t am1, uintptr_t am2) {
+    launch_lenet_conv_fwd(S(st), P<const uint8_t>(images), base, nb, P<const bf16>(pk), P<const float>(params), seed,
+                          P<const int>(round_ctr), augment, P<bf16>(act2), P<bf16>(act2T), tstride, P<bf16>(pool1),
+                          P<uint8_t>(am1), P<uint8_t>(am2));
+    check_last("lenet_conv_fwd");
+  });
+  m.def("lenet_fc_head", [](uintptr_t st, uintptr_t act2, uintptr_t act2T, int tstride, uintptr_t labels, int nb,
+                            int train, uintptr_t pk, uintptr_t params, uintptr_t dact2, uintptr_t fc_slab,
+                            uintptr_t stats) {
+    launch_lenet_fc_head(S(st), P<const bf16>(act2), P<const bf16>(act2T), tstride, P<const int>(labels), nb, train,
+                         P<const bf16>(pk), P<const float>(params), P<float>(dact2), P<float>(fc_slab),
+                         P<lenet::Stats>(stats));
+    check_last("lenet_fc_head");
+  });
+  m.def("lenet_conv_bwd", [](uintptr_t st, uintptr_t images, int base, int nb, uint32_t seed, uintptr_t round_ctr,
+                             int augment, uintptr_t dact2, uintptr_t pool1, uintptr_t am1, uintptr_t am2,
+                             uintptr_t pk, uintptr_t conv_slab) {
+    launch_lenet_conv_bwd(S(st), P<const uint8_t>(images), base, nb, seed, P<const int>(round_ctr), augment,
+                          P<const float>(dact2), P<const bf16>(pool1), P<const uint8_t>(am1), P<const uint8_t>(am2),
+                          P<const bf16>(pk), P<float>(conv_slab));
+    check_last("lenet_conv_bwd");
+  });
+  m.def("lenet_sgd", [](uintptr_t st, uintptr_t params, uintptr_t mom, uintptr_t pk, uintptr_t conv_slab, int n_conv,
+                        uintptr_t fc_slab, int n_fc, float lr, float mo, float wd, uintptr_t round_ctr) {
+    launch_lenet_sgd(S(st), P<float>(params), P<float>(mom), P<bf16>(pk), P<const float>(conv_slab), n_conv,
+                     P<const float>(fc_slab), n_fc, lr, mo, wd, P<int>(round_ctr));
+    check_last("lenet_sgd");
+  });
+  m.def("lenet_pack", [](uintptr_t st, uintptr_t params, uintptr_t pk) {
+    launch_lenet_pack(S(st), P<const float>(params), P<bf16>(pk));
+    check_last("lenet_pack");
+  });
+
+  // ---- flat-buffer ops --------------------------------------------------------
+  m.def("sgd_flat", [](uintptr_t st, uintptr_t p, uintptr_t g, uintptr_t buf, long n, float lr, float mo, float wd,
+                       float damp, bool nesterov, bool first) {
+    launch_sgd_flat(S(st), P<float>(p), P<const float>(g), P<float>(buf), n, lr, mo, wd, damp, nesterov ? 1 : 0,
+                    first ? 1 : 0);
+    check_last("sgd_flat");
+  });
+  m.def("fedavg_max_inputs", &fedavg_max_inputs);
+  m.def("fedavg_reduce", [](uintptr_t st, const std::vector<uintptr_t>& ins, const std::vector<float>& w, uintptr_t out,
+                            long n) {
+    if (ins.size() != w.size() || ins.empty() || (int)ins.size() > fedavg_max_inputs())
+      throw std::invalid_argument("fedavg_reduce: bad inputs");
+    std::vector<const float*> ptrs;
+    for (auto p : ins) ptrs.push_back(P<const float>(p));
+    launch_fedavg_reduce(S(st), ptrs.data(), w.data(), (int)ins.size(), P<float>(out), n);
+    check_last("fedavg_reduce");
+  });
+  m.def("scale", [](uintptr_t st, uintptr_t x, long n, float a) {
+    launch_scale(S(st), P<float>(x), n, a);
+    check_last("scale");
+  });
+
+  // ---- compression ---------------------------------------------------------------
+  m.def("select_state_bytes", &select_state_bytes);
+  m.def("compact_chunk", &compact_chunk);
+  m.def("ef_delta", [](uintptr_t st, uintptr_t local, uintptr_t global, uintptr_t residual, uintptr_t d, long n) {
+    launch_ef_delta(S(st), P<const float>(local), P<const float>(global), P<const float>(residual), P<float>(d), n);
+    check_last("ef_delta");
+  });
+  m.def("topk", [](uintptr_t st, uintptr_t d, long n, int k, uintptr_t state, uintptr_t counts, uintptr_t idx,
+                   uintptr_t val, uintptr_t residual) {
+    if (k <= 0 || k > n) throw std::invalid_argument("topk: need 0 < k <= n");
+    launch_topk(S(st), P<const float>(d), n, k, P<void>(state), P<int>(counts), P<int>(idx), P<float>(val),
+                P<float>(residual));
+    check_last("topk");
+  });
+  m.def("scatter_add_scaled", [](uintptr_t st, uintptr_t out, uintptr_t idx, uintptr_t val, long m_, float scale, long n) {
+    launch_scatter_add_scaled(S(st), P<float>(out), P<const int>(idx), P<const float>(val), m_, scale, n);
+    check_last("scatter_add_scaled");
+  });
+  m.def("quant_int8", [](uintptr_t st, uintptr_t d, long n, uintptr_t q, uintptr_t scales, uintptr_t residual) {
+    launch_quant_int8(S(st), P<const float>(d), n, P<signed char>(q), P<float>(scales), P<float>(residual));
+    check_last("quant_int8");
+  });
+  m.def("dequant_accum", [](uintptr_t st, uintptr_t q, uintptr_t scales, int R, long n, uintptr_t out, float scale) {
+    launch_dequant_accum(S(st), P<const signed char>(q), P<const float>(scales), R, n, P<float>(out), scale);
+    check_last("dequant_accum");
+  });
+}

@@ -1,0 +1,162 @@
+"""Checkpoint format, directory layout and an asynchronous writer.
+
+Format (byte-compatible with the reference): ``torch.save({'net': state_dict,
+'acc': number, 'epoch': int})`` with un-prefixed keys and CPU fp32 tensors
+(src/main.py:160-165, src/server.py:174-179).  fedmi stores the real round in
+``epoch`` so a promoted backup or restarted coordinator resumes instead of
+restarting at round 0 (reference quirk A8, src/server.py:64 TODO).
+
+Layout (relative to the process CWD or an explicit root):
+  coordinator:  Primary/ | Backup/  ->  test_<rank>.pth, optimizedModel.pth
+  client:       checkpoint/<address>.pth
+"""
+from __future__ import annotations
+
+import base64
+import io
+import os
+import queue
+import threading
+from collections import OrderedDict
+from pathlib import Path
+from typing import Dict, Optional
+
+import torch
+
+OPTIMIZED_MODEL = "optimizedModel.pth"
+
+
+def mount_dir(root: Path | str, primary: bool) -> Path:
+    d = Path(root) / ("Primary" if primary else "Backup")
+    d.mkdir(parents=True, exist_ok=True)
+    return d
+
+
+def client_ckpt_path(root: Path | str, address: str) -> Path:
+    d = Path(root) / "checkpoint"
+    d.mkdir(parents=True, exist_ok=True)          # reference crashes if missing (quirk A13)
+    return d / f"{address}.pth"
+
+
+def make_checkpoint(state_dict, acc=1, epoch: int = 0) -> dict:
+    net = OrderedDict()
+    for k, v in state_dict.items():
+        k = k[7:] if k.startswith("module.") else k   # never DataParallel-prefixed (quirk A1)
+        net[k] = v.detach().to("cpu", copy=True).contiguous()
+    return {"net": net, "acc": acc, "epoch": int(epoch)}
+
+
+def to_bytes(ckpt: dict) -> bytes:
+    buf = io.BytesIO()
+    torch.save(ckpt, buf)
+    return buf.getvalue()
+
+
+def from_bytes(data: bytes) -> dict:
+    # weights_only: never execute anything from a checkpoint received over the wire
+    return torch.load(io.BytesIO(data), map_location="cpu", weights_only=True)
+
+
+def to_b64(data: bytes) -> str:
+    return base64.b64encode(data).decode("ascii")
+
+
+def from_b64(text) -> bytes:
+    return base64.b64decode(text)
+
+
+def atomic_write(path: Path | str, data: bytes) -> None:
+    path = Path(path)
+    path.parent.mkdir(parents=True, exist_ok=True)
+    tmp = path.with_name(path.name + f".tmp{os.getpid()}.{threading.get_ident()}")
+    with open(tmp, "wb") as f:
+        f.write(data)
+    os.replace(tmp, path)
+
+
+def save(path: Path | str, ckpt: dict) -> None:
+    atomic_write(path, to_bytes(ckpt))
+
+
+def load(path: Path | str) -> dict:
+    with open(path, "rb") as f:
+        return from_bytes(f.read())
+
+
+def read_epoch(path: Path | str) -> Optional[int]:
+    try:
+        return int(load(path).get("epoch", 0))
+    except (FileNotFoundError, RuntimeError, EOFError, ValueError):
+        return None
+
+
+class AsyncCheckpointWriter:
+    """Serialise + write checkpoints off the critical path.
+
+    ``submit`` snapshots the device tensors into pinned host memory with a
+    non-blocking copy on the current stream and records an event; the writer
+    thread waits for that event, then ``torch.save``s atomically.  The GPU
+    stream never blocks on file I/O.
+    """
+
+    def __init__(self, max_pending: int = 4):
+        self._q: "queue.Queue" = queue.Queue(maxsize=max_pending)
+        self._err: Optional[BaseException] = None
+        self._pinned: Dict[str, torch.Tensor] = {}
+        self._pin_lock = threading.Lock()
+        self._t = threading.Thread(target=self._run, name="fedmi-ckpt-writer", daemon=True)
+        self._t.start()
+        self.written = 0
+
+    def _snapshot(self, state_dict):
+        out = OrderedDict()
+        ev = None
+        for k, v in state_dict.items():
+            v = v.detach()
+            if v.is_cuda:
+                host = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+                host.copy_(v, non_blocking=True)
+                out[k] = host
+                if ev is None:
+                    ev = torch.cuda.Event()
+            else:
+                out[k] = v.clone()
+        if ev is not None:
+            ev.record()
+        return out, ev
+
+    def submit(self, path: Path | str, state_dict, acc=1, epoch: int = 0, on_done=None) -> None:
+        if self._err:
+            raise RuntimeError("checkpoint writer failed") from self._err
+        snap, ev = self._snapshot(state_dict)
+        self._q.put((Path(path), snap, ev, acc, epoch, on_done))
+
+    def _run(self):
+        while True:
+            item = self._q.get()
+            if item is None:
+                self._q.task_done()
+                return
+            path, snap, ev, acc, epoch, on_done = item
+            try:
+                if ev is not None:
+                    ev.synchronize()
+                data = to_bytes({"net": snap, "acc": acc, "epoch": int(epoch)})
+                atomic_write(path, data)
+                self.written += 1
+                if on_done is not None:
+                    on_done(path, data)
+            except BaseException as e:  # pragma: no cover
+                self._err = e
+            finally:
+                self._q.task_done()
+
+    def flush(self) -> None:
+        self._q.join()
+        if self._err:
+            raise RuntimeError("checkpoint writer failed") from self._err
+
+    def close(self) -> None:
+        self.flush()
+        self._q.put(None)
+        self._t.join(timeout=10)

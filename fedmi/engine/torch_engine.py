@@ -1,0 +1,175 @@
+"""Generic local trainer for any model of the zoo (PyTorch autograd for the
+layers, fedmi flat buffers + native fused SGD on GPU).
+
+All parameters live in ONE flat fp32 buffer (``p.data`` are views), all
+gradients in one flat grad buffer and all floating BN buffers in a second flat
+buffer, so FedAvg is a single collective over :meth:`float_state` and the SGD
+update is a single ``sgd_flat`` launch instead of 4 ops per tensor.
+On CPU the identical update is done with torch ops (reference semantics).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import List
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .. import native
+from ..models import build_model
+from .base import EpochStats, LocalTrainer, TrainerConfig
+from .data import FedDataset, ImageSet, augment_normalize
+
+
+class FlatState:
+    """Re-home a module's parameters / floating buffers into contiguous storage."""
+
+    def __init__(self, model: nn.Module, device: torch.device):
+        self.model = model
+        params = [p for p in model.parameters()]
+        n = sum(p.numel() for p in params)
+        self.n_params = n
+        fbufs = [(m, k, b) for m in model.modules() for k, b in m._buffers.items()
+                 if b is not None and b.is_floating_point()]
+        nb = sum(b.numel() for _, _, b in fbufs)
+        # one storage: [params | float buffers]; params are aligned to 16 B for the vector kernels
+        self.flat = torch.zeros(n + nb, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(n, dtype=torch.float32, device=device)
+        self.mom = torch.zeros(n, dtype=torch.float32, device=device)
+        off = 0
+        for p in params:
+            k = p.numel()
+            self.flat[off:off + k].copy_(p.data.reshape(-1))
+            p.data = self.flat[off:off + k].view_as(p)
+            p.grad = self.grad[off:off + k].view_as(p)
+            off += k
+        for m, key, b in fbufs:
+            k = b.numel()
+            self.flat[off:off + k].copy_(b.reshape(-1))
+            m._buffers[key] = self.flat[off:off + k].view_as(b)
+            off += k
+        self.ibufs = [(m, k, b) for m in model.modules() for k, b in m._buffers.items()
+                      if b is not None and not b.is_floating_point()]
+
+    @property
+    def params(self) -> torch.Tensor:
+        return self.flat[:self.n_params]
+
+
+class TorchTrainer(LocalTrainer):
+    def __init__(self, model_name: str, data: FedDataset, device: torch.device,
+                 cfg: TrainerConfig = TrainerConfig(), init_state=None, model_kwargs=None):
+        self.model_name = model_name
+        self.cfg = cfg
+        self._device = torch.device(device)
+        torch.manual_seed(cfg.seed)
+        model = build_model(model_name, **(model_kwargs or {}))
+        if init_state is not None:
+            model.load_state_dict(init_state)
+        self.model = model.to(self._device)
+        self.fs = FlatState(self.model, self._device)
+        self.train_set = data.train.to(self._device)
+        self.test_set = data.test.to(self._device)
+        self.mean, self.std = data.mean, data.std
+        self.augment = bool(data.augment and cfg.augment)
+        self.round_idx = 0
+        self._starts: List[int] = []
+        self._sizes: List[int] = []
+        self._tstats = torch.zeros(3, dtype=torch.float64, device=self._device)
+        self._estats = torch.zeros(3, dtype=torch.float64, device=self._device)
+        self._nat = native.require() if self._device.type == "cuda" and not native.force_torch_path() else None
+
+    @property
+    def device(self) -> torch.device:
+        return self._device
+
+    # ---- state -------------------------------------------------------------------
+    def state_dict(self):
+        return OrderedDict(self.model.state_dict())
+
+    def load_state_dict(self, sd) -> None:
+        cleaned = OrderedDict((k[7:] if k.startswith("module.") else k, v) for k, v in sd.items())
+        with torch.no_grad():
+            own = self.model.state_dict()
+            for k, v in cleaned.items():
+                own[k].copy_(v.to(own[k].device, own[k].dtype))
+
+    def float_state(self) -> torch.Tensor:
+        return self.fs.flat
+
+    def int_state(self) -> List[torch.Tensor]:
+        return [b for _, _, b in self.fs.ibufs]
+
+    def momentum_state(self) -> torch.Tensor:
+        return self.fs.mom
+
+    # ---- data ----------------------------------------------------------------------
+    def set_schedule(self, starts, sizes) -> None:
+        self._starts, self._sizes = list(map(int, starts)), list(map(int, sizes))
+
+    def set_train_data(self, data: ImageSet) -> None:
+        self.train_set = data.to(self._device)
+
+    def _batch(self, start: int, nb: int):
+        x = self.train_set.x[start:start + nb]
+        gidx = np.arange(start, start + nb) if self.augment else None
+        xin = augment_normalize(x, gidx, self.cfg.seed & 0xFFFFFFFF, self.round_idx, self.mean, self.std)
+        return xin, self.train_set.y[start:start + nb].long()
+
+    # ---- compute -------------------------------------------------------------------
+    def _sgd(self) -> None:
+        c = self.cfg
+        fs = self.fs
+        if self._nat is not None:
+            self._nat.sgd_flat(native.stream_handle(self._device), fs.params.data_ptr(), fs.grad.data_ptr(),
+                               fs.mom.data_ptr(), fs.n_params, c.lr, c.momentum, c.weight_decay, 0.0, False, False)
+        else:
+            with torch.no_grad():
+                d = fs.grad.add(fs.params, alpha=c.weight_decay)
+                fs.mom.mul_(c.momentum).add_(d)
+                fs.params.sub_(fs.mom, alpha=c.lr)
+
+    def train_step(self, start: int, nb: int) -> torch.Tensor:
+        x, y = self._batch(start, nb)
+        self.fs.grad.zero_()
+        out = self.model(x)
+        loss = F.cross_entropy(out, y)
+        loss.backward()
+        self._sgd()
+        with torch.no_grad():
+            self._tstats[0] += loss.detach().double() * nb
+            self._tstats[1] += (out.argmax(1) == y).sum()
+            self._tstats[2] += nb
+        return loss
+
+    def train_epoch(self) -> None:
+        self.model.train()
+        self._tstats.zero_()
+        for s, n in zip(self._starts, self._sizes):
+            self.train_step(s, n)
+        if self._starts:
+            self.round_idx += 1
+
+    def train_stats(self) -> EpochStats:
+        v = self._tstats.cpu().tolist()
+        return EpochStats(v[0], int(v[1]), int(v[2]))
+
+    @torch.no_grad()
+    def evaluate(self) -> None:
+        self.model.eval()
+        self._estats.zero_()
+        n = len(self.test_set)
+        bs = self.cfg.eval_batch_size
+        for s in range(0, n, bs):
+            x = augment_normalize(self.test_set.x[s:s + bs], None, 0, 0, self.mean, self.std)
+            y = self.test_set.y[s:s + bs].long()
+            out = self.model(x)
+            self._estats[0] += F.cross_entropy(out, y, reduction="sum").double()
+            self._estats[1] += (out.argmax(1) == y).sum()
+            self._estats[2] += y.numel()
+
+    def eval_stats(self) -> EpochStats:
+        v = self._estats.cpu().tolist()
+        return EpochStats(v[0], int(v[1]), int(v[2]))

@@ -1,0 +1,158 @@
+"""``-c Y``: compressed FedAvg updates on the data plane.
+
+Reference -c Y = gRPC gzip of base64 fp32 checkpoints (src/server.py:103-107,
+src/client.py:39-43): 0.98-0.99x of the raw size at 16 ms-3 s of CPU per
+message.  fedmi keeps the flag (and gzip on the gRPC control
+channel) and compresses the *update* instead:
+
+* ``topk``  — each client sends the k largest-magnitude entries of
+  d = (w_local - w_global) + e (error feedback e carries the rest to the next
+  round); selection is an exact radix select on the GPU
+  (csrc/kernels/compress.hip); (idx, val) pairs are all-gathered over RCCL and
+  scatter-added into the global model.  Payload per client: 8k bytes.
+* ``int8``  — per-256-element absmax int8 quantisation with error feedback;
+  payload n + 4n/256 bytes (~3.9x smaller than fp32).
+
+After aggregation every client holds w_global' = w_global + mean(sparse d),
+exactly like dense FedAvg when k = n.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import native
+
+
+def _world(group) -> int:
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+
+def _all_gather_flat(t: torch.Tensor, group) -> torch.Tensor:
+    w = _world(group)
+    if w == 1:
+        return t.clone()
+    out = torch.empty((w,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+    if t.is_cuda:
+        dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=group)
+    else:
+        dist.all_gather(list(out.unbind(0)), t.contiguous(), group=group)
+    return out
+
+
+class _EFCompressor:
+    def __init__(self, trainer):
+        x = trainer.float_state()
+        self.n = x.numel()
+        self.dev = x.device
+        self.global_ref = x.detach().clone()
+        self.residual = torch.zeros_like(self.global_ref)
+        self.d = torch.empty_like(self.global_ref)
+        self._nat = native.require() if x.is_cuda else None
+        self.bytes_sent = 0
+
+    def reset(self, trainer) -> None:
+        """Re-anchor on the trainer's current model (after a resync/load)."""
+        self.global_ref.copy_(trainer.float_state())
+        self.residual.zero_()
+
+    def _delta(self, x: torch.Tensor) -> None:
+        if self._nat is not None:
+            self._nat.ef_delta(native.stream_handle(self.dev), x.data_ptr(), self.global_ref.data_ptr(),
+                               self.residual.data_ptr(), self.d.data_ptr(), self.n)
+        else:
+            torch.sub(x, self.global_ref, out=self.d)
+            self.d.add_(self.residual)
+
+
+class TopKCompressor(_EFCompressor):
+    def __init__(self, trainer, ratio: float = 0.01):
+        super().__init__(trainer)
+        self.k = max(1, min(self.n, int(round(self.n * ratio))))
+        self.idx = torch.empty(self.k, dtype=torch.int32, device=self.dev)
+        self.val = torch.empty(self.k, dtype=torch.float32, device=self.dev)
+        if self._nat is not None:
+            self.state = torch.zeros(self._nat.select_state_bytes(), dtype=torch.uint8, device=self.dev)
+            nblk = (self.n + self._nat.compact_chunk() - 1) // self._nat.compact_chunk()
+            self.counts = torch.zeros(2 * nblk, dtype=torch.int32, device=self.dev)
+
+    def compress(self, x: torch.Tensor) -> None:
+        self._delta(x)
+        if self._nat is not None:
+            self._nat.topk(native.stream_handle(self.dev), self.d.data_ptr(), self.n, self.k, self.state.data_ptr(),
+                           self.counts.data_ptr(), self.idx.data_ptr(), self.val.data_ptr(),
+                           self.residual.data_ptr())
+        else:
+            sel = self.d.abs().topk(self.k, sorted=False).indices
+            self.idx.copy_(sel.to(torch.int32))
+            self.val.copy_(self.d[sel])
+            self.residual.copy_(self.d)
+            self.residual[sel] = 0.0
+
+    def aggregate(self, trainer, group=None) -> None:
+        x = trainer.float_state()
+        self.compress(x)
+        w = _world(group)
+        idx_all = _all_gather_flat(self.idx, group).view(-1)
+        val_all = _all_gather_flat(self.val, group).view(-1)
+        self.bytes_sent += 8 * self.k
+        if self._nat is not None:
+            self._nat.scatter_add_scaled(native.stream_handle(self.dev), self.global_ref.data_ptr(),
+                                         idx_all.data_ptr(), val_all.data_ptr(), idx_all.numel(), 1.0 / w, self.n)
+        else:
+            self.global_ref.index_add_(0, idx_all.long(), val_all / w)
+        x.copy_(self.global_ref)
+
+
+class Int8Compressor(_EFCompressor):
+    CHUNK = 256
+
+    def __init__(self, trainer):
+        super().__init__(trainer)
+        self.nchunks = (self.n + self.CHUNK - 1) // self.CHUNK
+        self.q = torch.empty(self.n, dtype=torch.int8, device=self.dev)
+        self.scales = torch.empty(self.nchunks, dtype=torch.float32, device=self.dev)
+
+    def compress(self, x: torch.Tensor) -> None:
+        self._delta(x)
+        if self._nat is not None:
+            self._nat.quant_int8(native.stream_handle(self.dev), self.d.data_ptr(), self.n, self.q.data_ptr(),
+                                 self.scales.data_ptr(), self.residual.data_ptr())
+        else:
+            pad = torch.zeros(self.nchunks * self.CHUNK, device=self.dev)
+            pad[:self.n] = self.d
+            blocks = pad.view(self.nchunks, self.CHUNK)
+            amax = blocks.abs().amax(1)
+            s = torch.where(amax > 0, amax / 127.0, torch.ones_like(amax))
+            q = torch.round(blocks / s[:, None]).clamp_(-127, 127)
+            self.q.copy_(q.view(-1)[:self.n].to(torch.int8))
+            self.scales.copy_(s)
+            self.residual.copy_(self.d - (q * s[:, None]).view(-1)[:self.n])
+
+    def aggregate(self, trainer, group=None) -> None:
+        x = trainer.float_state()
+        self.compress(x)
+        w = _world(group)
+        q_all = _all_gather_flat(self.q, group)
+        s_all = _all_gather_flat(self.scales, group)
+        self.bytes_sent += self.n + 4 * self.nchunks
+        if self._nat is not None:
+            self._nat.dequant_accum(native.stream_handle(self.dev), q_all.data_ptr(), s_all.data_ptr(), w, self.n,
+                                    self.global_ref.data_ptr(), 1.0 / w)
+        else:
+            idx = torch.arange(self.n, device=self.dev) // self.CHUNK
+            deq = q_all.float() * s_all[:, idx]
+            self.global_ref.add_(deq.sum(0) / w)
+        x.copy_(self.global_ref)
+
+
+def make_compressor(kind: Optional[str], ratio: float, trainer):
+    if kind in (None, "", "none", "n", "N"):
+        return None
+    if kind in ("topk", "Y", "y"):
+        return TopKCompressor(trainer, ratio)
+    if kind == "int8":
+        return Int8Compressor(trainer)
+    raise ValueError(f"unknown compression {kind!r}")

@@ -1,0 +1,105 @@
+"""Numerics of the flat-buffer and compression HIP kernels vs PyTorch fp32."""
+import numpy as np
+import pytest
+import torch
+
+from fedmi import native
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def nat(gpu_device):
+    return native.require()
+
+
+def S():
+    return native.stream_handle()
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 100003])
+def test_sgd_flat(nat, gpu_device, n):
+    torch.manual_seed(n)
+    p = torch.randn(n, device=gpu_device)
+    g = torch.randn(n, device=gpu_device)
+    b = torch.randn(n, device=gpu_device)
+    pr, br = p.clone(), b.clone()
+    nat.sgd_flat(S(), p.data_ptr(), g.data_ptr(), b.data_ptr(), n, 0.1, 0.9, 5e-4, 0.0, False, False)
+    d = g + 5e-4 * pr
+    br = 0.9 * br + d
+    pr = pr - 0.1 * br
+    torch.cuda.synchronize()
+    assert torch.allclose(b, br, rtol=1e-6, atol=1e-6)
+    assert torch.allclose(p, pr, rtol=1e-6, atol=1e-6)
+
+
+def test_fedavg_reduce(nat, gpu_device):
+    n = 62006
+    xs = [torch.randn(n, device=gpu_device) for _ in range(5)]
+    w = [0.2] * 5
+    out = torch.empty(n, device=gpu_device)
+    nat.fedavg_reduce(S(), [x.data_ptr() for x in xs], w, out.data_ptr(), n)
+    torch.cuda.synchronize()
+    assert torch.allclose(out, torch.stack(xs).mean(0), atol=1e-6)
+
+
+@pytest.mark.parametrize("n,k", [(62006, 620), (5000, 1), (5000, 5000), (1 << 20, 10000)])
+def test_topk_exact(nat, gpu_device, n, k):
+    torch.manual_seed(k)
+    d = torch.randn(n, device=gpu_device)
+    d[::97] = 0.0
+    state = torch.zeros(nat.select_state_bytes(), dtype=torch.uint8, device=gpu_device)
+    nblk = (n + nat.compact_chunk() - 1) // nat.compact_chunk()
+    counts = torch.zeros(2 * nblk, dtype=torch.int32, device=gpu_device)
+    idx = torch.full((k,), -1, dtype=torch.int32, device=gpu_device)
+    val = torch.zeros(k, device=gpu_device)
+    res = torch.empty(n, device=gpu_device)
+    nat.topk(S(), d.data_ptr(), n, k, state.data_ptr(), counts.data_ptr(), idx.data_ptr(), val.data_ptr(),
+             res.data_ptr())
+    torch.cuda.synchronize()
+    assert int(idx.min()) >= 0
+    assert len(set(idx.tolist())) == k
+    ref_vals = d.abs().topk(k).values
+    got = val.abs().sort(descending=True).values
+    assert torch.equal(got, ref_vals)
+    assert torch.equal(d[idx.long()], val)
+    # residual keeps exactly the unselected entries
+    mask = torch.ones(n, dtype=torch.bool, device=gpu_device)
+    mask[idx.long()] = False
+    assert torch.equal(res[mask], d[mask])
+    assert res[~mask].abs().sum().item() == 0
+
+
+def test_scatter_add_scaled(nat, gpu_device):
+    n = 1000
+    out = torch.zeros(n, device=gpu_device)
+    idx = torch.tensor([1, 5, 5, 999], dtype=torch.int32, device=gpu_device)
+    val = torch.tensor([1.0, 2.0, 3.0, 4.0], device=gpu_device)
+    nat.scatter_add_scaled(S(), out.data_ptr(), idx.data_ptr(), val.data_ptr(), 4, 0.5, n)
+    torch.cuda.synchronize()
+    exp = torch.zeros(n, device=gpu_device)
+    exp[1], exp[5], exp[999] = 0.5, 2.5, 2.0
+    assert torch.equal(out, exp)
+
+
+def test_int8_roundtrip(nat, gpu_device):
+    n = 62006
+    torch.manual_seed(1)
+    d = torch.randn(n, device=gpu_device)
+    nch = (n + 255) // 256
+    q = torch.empty(n, dtype=torch.int8, device=gpu_device)
+    sc = torch.empty(nch, device=gpu_device)
+    res = torch.empty(n, device=gpu_device)
+    nat.quant_int8(S(), d.data_ptr(), n, q.data_ptr(), sc.data_ptr(), res.data_ptr())
+    out = torch.zeros(n, device=gpu_device)
+    nat.dequant_accum(S(), q.data_ptr(), sc.data_ptr(), 1, n, out.data_ptr(), 1.0)
+    torch.cuda.synchronize()
+    # reference quantizer
+    pad = torch.zeros(nch * 256, device=gpu_device)
+    pad[:n] = d
+    amax = pad.view(nch, 256).abs().amax(1)
+    s_ref = torch.where(amax > 0, amax / 127, torch.ones_like(amax))
+    assert torch.allclose(sc, s_ref)
+    deq = (torch.round(pad.view(nch, 256) / s_ref[:, None]).clamp(-127, 127) * s_ref[:, None]).view(-1)[:n]
+    assert torch.allclose(out, deq, atol=1e-6)
+    assert torch.allclose(res, d - deq, atol=1e-6)
