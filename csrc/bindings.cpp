@@ -17,12 +17,14 @@ namespace py = pybind11;
 
 namespace fedmi {
 void launch_lenet_conv_fwd(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*, int,
-                           bf16*, bf16*, int, bf16*, uint8_t*, uint8_t*);
-void launch_lenet_fc_head(hipStream_t, const bf16*, const bf16*, int, const int*, int, int, const bf16*, const float*,
-                          float*, float*, lenet::Stats*);
-void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const float*, const bf16*,
-                           const uint8_t*, const uint8_t*, const bf16*, float*);
-void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, const float*, int, float, float, float, int*);
+                           bf16*, bf16*, int, bf16*, uint8_t*, uint8_t*, lenet::Stats*);
+void launch_lenet_fc_head(hipStream_t, const bf16*, const int*, int, int, const bf16*, const float*, bf16*, bf16*,
+                          float*, lenet::Stats*);
+void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const bf16*, const bf16*,
+                           const bf16*, const bf16*, const bf16*, const uint8_t*, const uint8_t*, const bf16*, float*,
+                           float*);
+void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, const float*, const float*, int, float,
+                      float, float, int*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
 void launch_sgd_flat(hipStream_t, float*, const float*, float*, long, float, float, float, float, int, int);
 int fedavg_max_inputs();
@@ -60,8 +62,10 @@ static LeNetBuffers buffers_from(const py::dict& d) {
   b.pool1 = P<bf16>(get("pool1"));
   b.am1 = P<uint8_t>(get("am1"));
   b.am2 = P<uint8_t>(get("am2"));
-  b.dact2 = P<float>(get("dact2"));
+  b.dZ1 = P<bf16>(get("dZ1"));
+  b.dZ1T = P<bf16>(get("dZ1T"));
   b.conv_slab = P<float>(get("conv_slab"));
+  b.fc1w_grad = P<float>(get("fc1w_grad"));
   b.fc_slab = P<float>(get("fc_slab"));
   b.train_stats = P<lenet::Stats>(get("train_stats"));
   b.eval_stats = P<lenet::Stats>(get("eval_stats"));
@@ -78,7 +82,7 @@ PYBIND11_MODULE(_fedmi_native, m) {
     d["P_C1W"] = P_C1W; d["P_C1B"] = P_C1B; d["P_C2W"] = P_C2W; d["P_C2B"] = P_C2B;
     d["P_F1W"] = P_F1W; d["P_F1B"] = P_F1B; d["P_F2W"] = P_F2W; d["P_F2B"] = P_F2B;
     d["P_F3W"] = P_F3W; d["P_F3B"] = P_F3B; d["P_TOTAL"] = P_TOTAL;
-    d["CS"] = CS; d["FS"] = FS; d["PK_TOTAL"] = PK_TOTAL; d["F0"] = F0; d["F0P"] = F0P; d["NP1"] = NP1;
+    d["CS"] = CS; d["FS"] = FS; d["F1W_N"] = F1W_N; d["DZ1_LD"] = DZ1_LD; d["N_DW1_WG"] = N_DW1_WG; d["PK_TOTAL"] = PK_TOTAL; d["F0"] = F0; d["F0P"] = F0P; d["NP1"] = NP1;
     d["MAX_TRAIN_BATCH"] = MAX_TRAIN_BATCH; d["FC_SPW"] = FC_SPW; d["MAX_FC_WG"] = MAX_FC_WG;
     d["IMG_BYTES"] = IMG_BYTES; d["STATS_BYTES"] = (int)sizeof(Stats);
     return d;
@@ -100,7 +104,10 @@ PYBIND11_MODULE(_fedmi_native, m) {
            py::arg("augment"))
       .def("set_schedule", &LeNetEngine::set_schedule)
       .def("schedule_len", &LeNetEngine::schedule_len)
-      .def("step", [](LeNetEngine& e, uintptr_t st, int start, int nb, bool bump) { e.step(S(st), start, nb, bump); },
+      .def("step", [](LeNetEngine& e, uintptr_t st, int start, int nb, bool bump, bool reset) {
+             e.step(S(st), start, nb, bump, reset);
+           }, py::arg("stream"), py::arg("start"), py::arg("nb"), py::arg("bump_round") = false,
+           py::arg("reset_stats") = false,
            py::call_guard<py::gil_scoped_release>())
       .def("run_epoch", [](LeNetEngine& e, uintptr_t st, bool use_graph) { e.run_epoch(S(st), use_graph); },
            py::call_guard<py::gil_scoped_release>())
@@ -116,32 +123,34 @@ PYBIND11_MODULE(_fedmi_native, m) {
   // ---- raw LeNet kernels (numerics tests drive them one by one) -------------
   m.def("lenet_conv_fwd", [](uintptr_t st, uintptr_t images, int base, int nb, uintptr_t pk, uintptr_t params,
                              uint32_t seed, uintptr_t round_ctr, int augment, uintptr_t act2, uintptr_t act2T,
-                             int tstride, uintptr_t pool1, uintptr_t am1, uintptr_t am2) {
+                             int tstride, uintptr_t pool1, uintptr_t am1, uintptr_t am2, uintptr_t zero_stats) {
     launch_lenet_conv_fwd(S(st), P<const uint8_t>(images), base, nb, P<const bf16>(pk), P<const float>(params), seed,
                           P<const int>(round_ctr), augment, P<bf16>(act2), P<bf16>(act2T), tstride, P<bf16>(pool1),
-                          P<uint8_t>(am1), P<uint8_t>(am2));
+                          P<uint8_t>(am1), P<uint8_t>(am2), P<lenet::Stats>(zero_stats));
     check_last("lenet_conv_fwd");
   });
-  m.def("lenet_fc_head", [](uintptr_t st, uintptr_t act2, uintptr_t act2T, int tstride, uintptr_t labels, int nb,
-                            int train, uintptr_t pk, uintptr_t params, uintptr_t dact2, uintptr_t fc_slab,
-                            uintptr_t stats) {
-    launch_lenet_fc_head(S(st), P<const bf16>(act2), P<const bf16>(act2T), tstride, P<const int>(labels), nb, train,
-                         P<const bf16>(pk), P<const float>(params), P<float>(dact2), P<float>(fc_slab),
+  m.def("lenet_fc_head", [](uintptr_t st, uintptr_t act2, uintptr_t labels, int nb, int train, uintptr_t pk,
+                            uintptr_t params, uintptr_t dZ1, uintptr_t dZ1T, uintptr_t fc_slab, uintptr_t stats) {
+    launch_lenet_fc_head(S(st), P<const bf16>(act2), P<const int>(labels), nb, train, P<const bf16>(pk),
+                         P<const float>(params), P<bf16>(dZ1), P<bf16>(dZ1T), P<float>(fc_slab),
                          P<lenet::Stats>(stats));
     check_last("lenet_fc_head");
   });
   m.def("lenet_conv_bwd", [](uintptr_t st, uintptr_t images, int base, int nb, uint32_t seed, uintptr_t round_ctr,
-                             int augment, uintptr_t dact2, uintptr_t pool1, uintptr_t am1, uintptr_t am2,
-                             uintptr_t pk, uintptr_t conv_slab) {
+                             int augment, uintptr_t act2, uintptr_t act2T, uintptr_t dZ1, uintptr_t dZ1T,
+                             uintptr_t pool1, uintptr_t am1, uintptr_t am2, uintptr_t pk, uintptr_t conv_slab,
+                             uintptr_t fc1w_grad) {
     launch_lenet_conv_bwd(S(st), P<const uint8_t>(images), base, nb, seed, P<const int>(round_ctr), augment,
-                          P<const float>(dact2), P<const bf16>(pool1), P<const uint8_t>(am1), P<const uint8_t>(am2),
-                          P<const bf16>(pk), P<float>(conv_slab));
+                          P<const bf16>(act2), P<const bf16>(act2T), P<const bf16>(dZ1), P<const bf16>(dZ1T),
+                          P<const bf16>(pool1), P<const uint8_t>(am1), P<const uint8_t>(am2), P<const bf16>(pk),
+                          P<float>(conv_slab), P<float>(fc1w_grad));
     check_last("lenet_conv_bwd");
   });
   m.def("lenet_sgd", [](uintptr_t st, uintptr_t params, uintptr_t mom, uintptr_t pk, uintptr_t conv_slab, int n_conv,
-                        uintptr_t fc_slab, int n_fc, float lr, float mo, float wd, uintptr_t round_ctr) {
+                        uintptr_t fc1w_grad, uintptr_t fc_slab, int n_fc, float lr, float mo, float wd,
+                        uintptr_t round_ctr) {
     launch_lenet_sgd(S(st), P<float>(params), P<float>(mom), P<bf16>(pk), P<const float>(conv_slab), n_conv,
-                     P<const float>(fc_slab), n_fc, lr, mo, wd, P<int>(round_ctr));
+                     P<const float>(fc1w_grad), P<const float>(fc_slab), n_fc, lr, mo, wd, P<int>(round_ctr));
     check_last("lenet_sgd");
   });
   m.def("lenet_pack", [](uintptr_t st, uintptr_t params, uintptr_t pk) {

@@ -22,10 +22,13 @@ constexpr int NPOS2 = O2 * O2;           // 100
 constexpr int F0 = C2 * P2 * P2;         // 400 flattened features
 constexpr int F0P = 416;                 // act2 row stride (13 k-steps of 32)
 constexpr int F1 = 120, F2 = 84, NCLS = 10;
-constexpr int K1 = CIN * 25, K1P = 96;   // conv1 reduction dim (pad to 3x32)
-constexpr int K2 = C1 * 25, K2P = 160;   // conv2 reduction dim (pad to 5x32)
-constexpr int KDG = C2 * 25, KDGP = 416; // conv2 dgrad reduction (o,r,s)
 constexpr int IMG_BYTES = CIN * IMG * IMG;  // 3072 (uint8 CHW, CIFAR format)
+
+// MFMA reduction dims (K) of the channels-last implicit GEMMs.
+//   conv1 fwd: k = g*8 + t, g = r*3 + s/2 (15 groups + 1 pad), t = (s&1)*4 + c (c<3)
+//   conv2 fwd: k = (r*5+s)*8 + c (c<6), 25 groups -> 200, pad 224
+//   conv2 dgrad: k = (r*5+s)*16 + o, 400, pad 416
+constexpr int K1C = 128, K2C = 224, KDG = 400, KDGP = 416;
 
 // ---- master parameters (fp32, state_dict order) ----------------------------
 constexpr int P_C1W = 0;                 // conv1.weight [6,3,5,5]
@@ -40,30 +43,35 @@ constexpr int P_F3W = 61156;             // fc3.weight   [10,84]
 constexpr int P_F3B = 61996;             // fc3.bias     [10]
 constexpr int P_TOTAL = 62006;
 
-// Gradient slabs: per-sample conv slab covers params [0, CS); per-FC-workgroup
-// slab covers params [P_F1W, P_TOTAL).  The SGD kernel reduces the slabs
-// (split-K combine at the next kernel boundary, no atomics, deterministic).
+// Gradient staging (combined by the SGD kernel at the next kernel boundary:
+// deterministic, no global atomics):
+//   conv_slab [nb][CS]      per-sample grads of params [0, P_F1W)
+//   fc1w_grad [48000]       complete fc1.weight grad (one writer per element)
+//   fc_slab   [nfc][FS]     per-FC-workgroup grads of params [P_F1B, P_TOTAL)
 constexpr int CS = P_F1W;                // 2872
-constexpr int FS = P_TOTAL - P_F1W;      // 59134
+constexpr int FS = P_TOTAL - P_F1B;      // 11134
+constexpr int F1W_N = P_F1B - P_F1W;     // 48000
 
 // ---- packed bf16 operand images (written by the SGD/pack kernels) ----------
 // Each image is laid out so a lane's 8 consecutive K elements of an MFMA
 // operand fragment are one 16-byte load.  Padding is zero and never written.
-constexpr int PK_W1C  = 0;                      // [16 o][96 k]      conv1 B
-constexpr int PK_W2C  = PK_W1C + 16 * K1P;      // [16 o][160 k]     conv2 B
-constexpr int PK_W2DG = PK_W2C + 16 * K2P;      // [16 c][416 (o,r,s)] conv2 dgrad B
-constexpr int PK_FC1  = PK_W2DG + 16 * KDGP;    // [128 n][416 f]    fc1 fwd B
-constexpr int PK_FC1T = PK_FC1 + 128 * F0P;     // [400 f][128 n]    fc1 dgrad B
-constexpr int PK_FC2  = PK_FC1T + F0 * 128;     // [96 n][128 f]     fc2 fwd B
-constexpr int PK_FC2T = PK_FC2 + 96 * 128;      // [128 f][96 n]     fc2 dgrad B
-constexpr int PK_FC3  = PK_FC2T + 128 * 96;     // [16 n][96 f]      fc3 fwd B
-constexpr int PK_FC3T = PK_FC3 + 16 * 96;       // [96 f][32 n]      fc3 dgrad B
-constexpr int PK_TOTAL = PK_FC3T + 96 * 32;     // 144384 bf16
+constexpr int PK_W1C  = 0;                      // [16 o][128 k]       conv1 B
+constexpr int PK_W2C  = PK_W1C + 16 * K1C;      // [16 o][224 k]       conv2 B
+constexpr int PK_W2DG = PK_W2C + 16 * K2C;      // [16 c][416 (r,s,o)] conv2 dgrad B
+constexpr int PK_FC1  = PK_W2DG + 16 * KDGP;    // [128 n][416 f]      fc1 fwd B
+constexpr int PK_FC1T = PK_FC1 + 128 * F0P;     // [400 f][128 n]      fc1 dgrad B
+constexpr int PK_FC2  = PK_FC1T + F0 * 128;     // [96 n][128 f]       fc2 fwd B
+constexpr int PK_FC2T = PK_FC2 + 96 * 128;      // [128 f][96 n]       fc2 dgrad B
+constexpr int PK_FC3  = PK_FC2T + 128 * 96;     // [16 n][96 f]        fc3 fwd B
+constexpr int PK_FC3T = PK_FC3 + 16 * 96;       // [96 f][32 n]        fc3 dgrad B
+constexpr int PK_TOTAL = PK_FC3T + 96 * 32;
 
 // ---- training-step geometry -------------------------------------------------
 constexpr int MAX_TRAIN_BATCH = 128;     // reference batch (src/main.py:140)
-constexpr int FC_SPW = 32;               // samples per FC-head workgroup
+constexpr int FC_SPW = 16;               // samples per FC-head workgroup (one MFMA row tile)
 constexpr int MAX_FC_WG = MAX_TRAIN_BATCH / FC_SPW;
+constexpr int DZ1_LD = 128;              // dZ1 [B][128] and dZ1T [128][B] (B = 128)
+constexpr int N_DW1_WG = F0 / 16;        // 25 fc1-wgrad workgroups appended to the conv-bwd grid
 
 // Stats block written by the FC-head kernel (float/int atomics).
 struct Stats {

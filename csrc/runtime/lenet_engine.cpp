@@ -10,13 +10,14 @@ using lenet::Stats;
 
 // launchers (csrc/kernels/lenet_kernels.hip)
 void launch_lenet_conv_fwd(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t,
-                           const int*, int, bf16*, bf16*, int, bf16*, uint8_t*, uint8_t*);
-void launch_lenet_fc_head(hipStream_t, const bf16*, const bf16*, int, const int*, int, int, const bf16*,
-                          const float*, float*, float*, Stats*);
-void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const float*,
-                           const bf16*, const uint8_t*, const uint8_t*, const bf16*, float*);
-void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, const float*, int, float, float,
-                      float, int*);
+                           const int*, int, bf16*, bf16*, int, bf16*, uint8_t*, uint8_t*, lenet::Stats*);
+void launch_lenet_fc_head(hipStream_t, const bf16*, const int*, int, int, const bf16*, const float*, bf16*, bf16*,
+                          float*, Stats*);
+void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const bf16*, const bf16*,
+                           const bf16*, const bf16*, const bf16*, const uint8_t*, const uint8_t*, const bf16*, float*,
+                           float*);
+void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, const float*, const float*, int, float,
+                      float, float, int*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
 
 void check_hip(hipError_t e, const char* what) {
@@ -25,8 +26,8 @@ void check_hip(hipError_t e, const char* what) {
 
 LeNetEngine::LeNetEngine(const LeNetBuffers& b, SgdConfig sgd, uint32_t seed, bool augment)
     : b_(b), sgd_(sgd), seed_(seed), augment_(augment) {
-  if (!b.params || !b.mom || !b.pk || !b.act2 || !b.act2T || !b.pool1 || !b.am1 || !b.am2 || !b.dact2 ||
-      !b.conv_slab || !b.fc_slab || !b.train_stats || !b.eval_stats || !b.round_ctr)
+  if (!b.params || !b.mom || !b.pk || !b.act2 || !b.act2T || !b.pool1 || !b.am1 || !b.am2 || !b.dZ1 || !b.dZ1T ||
+      !b.conv_slab || !b.fc1w_grad || !b.fc_slab || !b.train_stats || !b.eval_stats || !b.round_ctr)
     throw std::invalid_argument("LeNetEngine: missing device buffer");
   if (b.act2_rows < lenet::MAX_TRAIN_BATCH) throw std::invalid_argument("LeNetEngine: act2_rows < 128");
   check_hip(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -60,26 +61,26 @@ void LeNetEngine::set_sgd(SgdConfig sgd) {
   drop_graph();
 }
 
-void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round) {
+void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round, bool reset_stats) {
   using namespace lenet;
   if (nb <= 0 || nb > MAX_TRAIN_BATCH || start < 0 || start + nb > b_.n_train)
     throw std::invalid_argument("LeNetEngine::step: batch out of range");
   const int aug = augment_ ? 1 : 0;
   launch_lenet_conv_fwd(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug, b_.act2,
-                        b_.act2T, MAX_TRAIN_BATCH, b_.pool1, b_.am1, b_.am2);
-  launch_lenet_fc_head(st, b_.act2, b_.act2T, MAX_TRAIN_BATCH, b_.train_labels + start, nb, 1, b_.pk,
-                       b_.params, b_.dact2, b_.fc_slab, b_.train_stats);
-  launch_lenet_conv_bwd(st, b_.train_images, start, nb, seed_, b_.round_ctr, aug, b_.dact2, b_.pool1, b_.am1,
-                        b_.am2, b_.pk, b_.conv_slab);
-  launch_lenet_sgd(st, b_.params, b_.mom, b_.pk, b_.conv_slab, nb, b_.fc_slab, (nb + FC_SPW - 1) / FC_SPW,
-                   sgd_.lr, sgd_.momentum, sgd_.weight_decay, bump_round ? b_.round_ctr : nullptr);
+                        b_.act2T, MAX_TRAIN_BATCH, b_.pool1, b_.am1, b_.am2, reset_stats ? b_.train_stats : nullptr);
+  launch_lenet_fc_head(st, b_.act2, b_.train_labels + start, nb, 1, b_.pk, b_.params, b_.dZ1, b_.dZ1T,
+                       b_.fc_slab, b_.train_stats);
+  launch_lenet_conv_bwd(st, b_.train_images, start, nb, seed_, b_.round_ctr, aug, b_.act2, b_.act2T, b_.dZ1,
+                        b_.dZ1T, b_.pool1, b_.am1, b_.am2, b_.pk, b_.conv_slab, b_.fc1w_grad);
+  launch_lenet_sgd(st, b_.params, b_.mom, b_.pk, b_.conv_slab, nb, b_.fc1w_grad, b_.fc_slab,
+                   (nb + FC_SPW - 1) / FC_SPW, sgd_.lr, sgd_.momentum, sgd_.weight_decay,
+                   bump_round ? b_.round_ctr : nullptr);
   check_hip(hipGetLastError(), "LeNetEngine::step launch");
 }
 
 void LeNetEngine::enqueue_epoch(hipStream_t st) {
-  check_hip(hipMemsetAsync(b_.train_stats, 0, sizeof(Stats), st), "memset stats");
   const size_t n = starts_.size();
-  for (size_t i = 0; i < n; ++i) step(st, starts_[i], sizes_[i], i + 1 == n);
+  for (size_t i = 0; i < n; ++i) step(st, starts_[i], sizes_[i], i + 1 == n, i == 0);
 }
 
 void LeNetEngine::run_epoch(hipStream_t st, bool use_graph) {
@@ -110,11 +111,9 @@ void LeNetEngine::run_epoch(hipStream_t st, bool use_graph) {
 void LeNetEngine::eval(hipStream_t st, const uint8_t* images, const int* labels, int n) {
   using namespace lenet;
   if (n <= 0 || n > b_.act2_rows) throw std::invalid_argument("LeNetEngine::eval: n exceeds act2 capacity");
-  check_hip(hipMemsetAsync(b_.eval_stats, 0, sizeof(Stats), st), "memset eval stats");
   launch_lenet_conv_fwd(st, images, 0, n, b_.pk, b_.params, seed_, b_.round_ctr, 0, b_.act2, nullptr, 0,
-                        nullptr, nullptr, nullptr);
-  launch_lenet_fc_head(st, b_.act2, nullptr, 0, labels, n, 0, b_.pk, b_.params, nullptr, nullptr,
-                       b_.eval_stats);
+                        nullptr, nullptr, nullptr, b_.eval_stats);
+  launch_lenet_fc_head(st, b_.act2, labels, n, 0, b_.pk, b_.params, nullptr, nullptr, nullptr, b_.eval_stats);
   check_hip(hipGetLastError(), "LeNetEngine::eval launch");
 }
 

@@ -27,8 +27,10 @@ struct LeNetBuffers {
   bf16* pool1 = nullptr;         // [MAX_TRAIN_BATCH][NP1]
   uint8_t* am1 = nullptr;        // [MAX_TRAIN_BATCH][NP1]
   uint8_t* am2 = nullptr;        // [MAX_TRAIN_BATCH][F0]
-  float* dact2 = nullptr;        // [MAX_TRAIN_BATCH][F0]
+  bf16* dZ1 = nullptr;           // [MAX_TRAIN_BATCH][DZ1_LD]
+  bf16* dZ1T = nullptr;          // [DZ1_LD][MAX_TRAIN_BATCH]
   float* conv_slab = nullptr;    // [MAX_TRAIN_BATCH][CS]
+  float* fc1w_grad = nullptr;    // [F1W_N]
   float* fc_slab = nullptr;      // [MAX_FC_WG][FS]
   lenet::Stats* train_stats = nullptr;
   lenet::Stats* eval_stats = nullptr;
@@ -51,7 +53,7 @@ class LeNetEngine {
   int schedule_len() const { return (int)starts_.size(); }
 
   // One SGD step (eager launches) on samples [start, start+nb).
-  void step(hipStream_t st, int start, int nb, bool bump_round);
+  void step(hipStream_t st, int start, int nb, bool bump_round, bool reset_stats = false);
   // One local epoch over the schedule; graph replay when use_graph.
   void run_epoch(hipStream_t st, bool use_graph);
   // Forward + CE/accuracy over n samples of an image set (eval mode).

@@ -1,0 +1,99 @@
+"""Client process: ``python -m fedmi.cli.client -a host:port ...``.
+
+Reference-compatible flags (src/client.py:55-71 + the flags of the imported
+src/main.py:20-28): ``-a/--address`` (listen address AND checkpoint name),
+``-c/--compressFlag Y``, ``-r/--resume``, ``--lr``.  One client = one GPU:
+``--device cuda:N`` (default: LOCAL_RANK / first GPU, CPU if none).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import sys
+import threading
+
+import torch
+
+from ..control.client_agent import ClientAgent, serve_client
+from ..engine import build_trainer
+from ..engine.base import TrainerConfig
+from ..engine.data import label_shard_indices, make_dataset
+from ..parallel.compress import make_compressor
+from ..parallel.fedavg import FedAvg
+from ..parallel.group import GroupManager
+from ..utils.metrics import MetricsLog, log
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description="fedmi federated client (one GPU)")
+    ap.add_argument("-c", "--compressFlag", help="'Y': gzip gRPC + compressed (top-k) FedAvg updates")
+    ap.add_argument("-a", "--address", default="temp", help="listen address host:port (also the checkpoint name)")
+    ap.add_argument("-r", "--resume", action="store_true", help="resume from checkpoint/<address>.pth")
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--model", default="lenet")
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--agg", default="collective", choices=["collective", "grpc"])
+    ap.add_argument("--backend", default="auto", help="data-plane backend: nccl (RCCL) | gloo | auto")
+    ap.add_argument("--data", default="synthetic-cifar10",
+                    help="synthetic-cifar10 | synthetic-mnist | cifar10-bin:<dir>")
+    ap.add_argument("--n-train", type=int, default=None)
+    ap.add_argument("--n-test", type=int, default=None)
+    ap.add_argument("--batch-size", type=int, default=128)
+    ap.add_argument("--seed", type=int, default=0, help="model-init / augmentation seed (same on all clients)")
+    ap.add_argument("--data-seed", type=int, default=0)
+    ap.add_argument("--noniid", type=int, default=0, help="label shards per client (0 = reference strided IID)")
+    ap.add_argument("--client-index", type=int, default=0)
+    ap.add_argument("--num-clients", type=int, default=1)
+    ap.add_argument("--compress", default=None, choices=["none", "topk", "int8"],
+                    help="update compression (default: topk when -c Y)")
+    ap.add_argument("--topk-ratio", type=float, default=0.01)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--root", default=".")
+    ap.add_argument("--metrics", default=None)
+    ap.add_argument("--quiet", action="store_true")
+    return ap
+
+
+def pick_device(spec: str) -> torch.device:
+    if spec != "auto":
+        return torch.device(spec)
+    if torch.cuda.is_available():
+        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    return torch.device("cpu")
+
+
+def main(argv=None) -> int:
+    a = build_parser().parse_args(argv)
+    gzip = a.compressFlag == "Y"
+    dev = pick_device(a.device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")   # surface peer loss as an error
+    log(f"client {a.address}", f"Client is running on {a.address} ({dev}); Compression {a.compressFlag} enabled")
+    data = make_dataset(a.data, device=dev, n_train=a.n_train, n_test=a.n_test, seed=a.data_seed)
+    cfg = TrainerConfig(lr=a.lr, batch_size=a.batch_size, seed=a.seed, use_graph=not a.no_graph)
+    trainer = build_trainer(a.model, data, dev, cfg)
+    if a.noniid > 0:
+        shards = label_shard_indices(data.train.y.cpu().numpy(), a.num_clients, a.noniid, seed=a.data_seed)
+        trainer.set_train_data(data.train.subset(shards[a.client_index]))
+    backend = a.backend if a.backend != "auto" else ("nccl" if dev.type == "cuda" else "gloo")
+    comp_kind = a.compress if a.compress is not None else ("topk" if gzip else "none")
+    fedavg = FedAvg(compressor=make_compressor(comp_kind, a.topk_ratio, trainer))
+    agent = ClientAgent(trainer, a.address, root=a.root, agg=a.agg, group=GroupManager(backend, dev),
+                        fedavg=fedavg, batch_size=a.batch_size, local_shard=a.noniid > 0, resume=a.resume,
+                        metrics=MetricsLog(a.metrics), verbose=not a.quiet)
+    server, port = serve_client(agent, a.address, gzip=gzip)
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    signal.signal(signal.SIGINT, lambda *_: stop.set())
+    while not stop.is_set():
+        stop.wait(0.5)
+    server.stop(grace=1.0)
+    if agent.group is not None:
+        agent.group.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,191 @@
+"""Client agent: the ``federated.Trainer`` servicer run by every client.
+
+Reference: src/client.py:15-35 (+ the import-time trainer in src/main.py).
+
+  StartTrain(rank, world) -> one local epoch on this client's shard, then
+      * ``agg="grpc"`` (reference semantics): reply = base64(checkpoint of the
+        LOCAL model); the coordinator averages and sends it back (SendModel);
+      * ``agg="collective"`` (fedmi default): FedAvg happens right here as an
+        RCCL all-reduce among the clients (rank/world from the request, the
+        data-plane generation + rendezvous store from gRPC metadata); every
+        client evaluates the global model; only rank 0 uploads the (already
+        averaged) checkpoint so the coordinator can persist/replicate it.
+  SendModel(b64 checkpoint) -> install it (resync / grpc-mode broadcast), persist,
+      evaluate.
+  HeartBeat() -> status 1.
+
+Fixes vs the reference: one lock serialises RPCs that touch the model
+(quirk: concurrent StartTrain/SendModel raced on one global net), requests
+from a coordinator with an older *term* are rejected (split-brain fencing),
+checkpoints are never ``module.``-prefixed, the checkpoint dir is created.
+"""
+from __future__ import annotations
+
+import threading
+import time
+from pathlib import Path
+from typing import Optional
+
+import grpc
+
+from .. import ckpt as ck
+from ..engine.base import LocalTrainer
+from ..engine.data import contiguous_schedule, strided_schedule
+from ..parallel.fedavg import FedAvg
+from ..parallel.group import GroupManager, Membership
+from ..utils.metrics import MetricsLog, Timer, log
+from ..wire import proto as P
+
+META_TERM = "x-fedmi-term"
+META_ROUND = "x-fedmi-round"
+META_GEN = "x-fedmi-gen"
+META_STORE = "x-fedmi-store"
+
+
+def metadata_dict(context) -> dict:
+    try:
+        return {k: v for k, v in (context.invocation_metadata() or ())}
+    except Exception:
+        return {}
+
+
+class ClientAgent(P.TrainerServicer):
+    def __init__(self, trainer: LocalTrainer, address: str, *, root: str | Path = ".", agg: str = "collective",
+                 group: Optional[GroupManager] = None, fedavg: Optional[FedAvg] = None, batch_size: int = 128,
+                 local_shard: bool = False, resume: bool = False, metrics: Optional[MetricsLog] = None,
+                 verbose: bool = True):
+        if agg not in ("collective", "grpc"):
+            raise ValueError(f"agg must be 'collective' or 'grpc', not {agg!r}")
+        self.trainer = trainer
+        self.address = address
+        self.agg = agg
+        self.group = group
+        self.fedavg = fedavg or FedAvg()
+        self.batch = batch_size
+        self.local_shard = local_shard          # non-IID: the client owns its data, rank does not pick batches
+        self.metrics = metrics or MetricsLog()
+        self.verbose = verbose
+        self.lock = threading.RLock()
+        self.max_term = 0
+        self.round = 0
+        self.ckpt_path = ck.client_ckpt_path(root, address.replace("/", "_"))
+        if resume and self.ckpt_path.exists():
+            c = ck.load(self.ckpt_path)
+            trainer.load_state_dict(c["net"])
+            self.round = int(c.get("epoch", 0))
+            self._log(f"resumed from {self.ckpt_path} (epoch {self.round})")
+        else:
+            # reference bootstrap: persist the initial model (src/main.py:231-239)
+            ck.save(self.ckpt_path, ck.make_checkpoint(trainer.state_dict(), acc=1, epoch=self.round))
+
+    def _log(self, msg: str) -> None:
+        if self.verbose:
+            log(f"client {self.address}", msg)
+
+    # ---- helpers ------------------------------------------------------------------
+    def _fence(self, meta: dict, context) -> None:
+        term = int(meta.get(META_TERM, "0") or 0)
+        if term and term < self.max_term:
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION,
+                          f"stale coordinator term {term} < {self.max_term}")
+        self.max_term = max(self.max_term, term)
+
+    def _schedule(self, rank: int, world: int):
+        n = len(self.trainer.train_set)
+        if self.local_shard:
+            return contiguous_schedule(n, self.batch)
+        return strided_schedule(n, self.batch, rank, world)
+
+    def _persist(self, acc, epoch: int) -> bytes:
+        data = ck.to_bytes(ck.make_checkpoint(self.trainer.state_dict(), acc=acc, epoch=epoch))
+        ck.atomic_write(self.ckpt_path, data)
+        return data
+
+    # ---- RPCs ---------------------------------------------------------------------
+    def StartTrain(self, request, context):
+        meta = metadata_dict(context)
+        with self.lock:
+            self._fence(meta, context)
+            rank, world = int(request.rank), int(request.world)
+            if world <= 0 or not 0 <= rank < world:
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"bad rank/world {rank}/{world}")
+            rnd = int(meta.get(META_ROUND, self.round + 1) or self.round + 1)
+            t = Timer()
+            self.trainer.set_schedule(*self._schedule(rank, world))
+            self.trainer.train_epoch()
+            tr = self.trainer.train_stats()
+            t_train = t.ms()
+            rec = {"role": "client", "address": self.address, "round": rnd, "rank": rank, "world": world,
+                   "agg": self.agg, **tr.as_dict("train"), "train_ms": t_train}
+            if self.agg == "collective":
+                gen = int(meta.get(META_GEN, "0") or 0)
+                host, _, port = (meta.get(META_STORE) or "127.0.0.1:0").rpartition(":")
+                if self.group is not None:
+                    self.group.ensure(Membership(gen, rank, world, host, int(port)))
+                elif world > 1:
+                    context.abort(grpc.StatusCode.FAILED_PRECONDITION, "collective aggregation needs a GroupManager")
+                t2 = Timer()
+                self.fedavg.average(self.trainer)
+                rec["allreduce_ms"] = t2.ms()
+                self.trainer.evaluate()
+                ev = self.trainer.eval_stats()
+                rec.update(ev.as_dict("test"))
+                self.round = rnd
+                data = self._persist(ev.acc, rnd)
+                message = ck.to_b64(data) if rank == 0 else ""
+            else:
+                self.round = rnd
+                data = self._persist(tr.acc, rnd)
+                message = ck.to_b64(data)
+            rec["round_ms"] = t.ms()
+            self.metrics.write(**rec)
+            self._log(f"round {rnd} rank {rank}/{world}: train loss {tr.loss:.4f} acc {tr.acc:.2f}%"
+                      + (f" | test acc {rec['test_acc']:.2f}%" if "test_acc" in rec else ""))
+            try:
+                context.set_trailing_metadata((("x-fedmi-client-round", str(self.round)),
+                                               ("x-fedmi-train-loss", f"{tr.loss:.6f}"),
+                                               ("x-fedmi-test-acc", f"{rec.get('test_acc', -1):.4f}")))
+            except Exception:
+                pass
+            return P.TrainReply(message=message)
+
+    def SendModel(self, request, context):
+        meta = metadata_dict(context)
+        with self.lock:
+            self._fence(meta, context)
+            data = ck.from_b64(request.model)
+            c = ck.from_bytes(data)
+            self.trainer.load_state_dict(c["net"])
+            comp = getattr(self.fedavg, "compressor", None)
+            if comp is not None:
+                comp.reset(self.trainer)
+            ck.atomic_write(self.ckpt_path, data)
+            self.round = max(self.round, int(c.get("epoch", 0) or 0))
+            self.trainer.evaluate()
+            ev = self.trainer.eval_stats()
+            self.metrics.write(role="client", address=self.address, event="send_model", round=self.round,
+                               **ev.as_dict("test"))
+            self._log(f"installed model (epoch {self.round}): test loss {ev.loss:.4f} acc {ev.acc:.2f}%")
+            return P.SendModelReply(reply="success")
+
+    def HeartBeat(self, request, context):
+        return P.HeartBeatResponse(status=1)
+
+
+def serve_client(agent: ClientAgent, address: str, gzip: bool = False, max_workers: int = 10):
+    """Start the client's gRPC server (reference src/client.py:38-52); returns the server."""
+    server = P.make_server(max_workers=max_workers, gzip=gzip)
+    P.add_TrainerServicer_to_server(agent, server)
+    port = server.add_insecure_port(address)
+    if port == 0:
+        raise RuntimeError(f"could not bind {address}")
+    server.start()
+    return server, port
+
+
+def wait_forever(server, stop: Optional[threading.Event] = None) -> None:
+    try:
+        while stop is None or not stop.is_set():
+            time.sleep(0.5)
+    finally:
+        server.stop(grace=1.0)

@@ -1,0 +1,283 @@
+"""Coordinator: drives federated rounds over the ``federated.Trainer`` RPCs.
+
+Reference: ``run()`` / ``trainThreadFunc`` / ``allreduce()`` /
+``sendOptimizedModel`` / ``checkClientStatus`` in src/server.py:51-179.
+
+Per round (synchronous, one local epoch per client, like the reference):
+  live clients get StartTrain(rank=i, world=#live) in parallel, with a deadline;
+  * ``agg="collective"``: clients all-reduce among themselves (RCCL); the
+    coordinator persists rank 0's averaged checkpoint;
+  * ``agg="grpc"``: reference parameter-server path — replies are written to
+    ``<mount>/test_<rank>.pth``, averaged (only the replies of THIS round), the
+    result saved and SendModel'ed back.
+  ``<mount>/optimizedModel.pth`` is replicated to the backup asynchronously.
+
+Fixes vs the reference: deadlines on every RPC (A3),
+world = live clients only and no stale-file averaging (A5/A6), the round is
+persisted in the checkpoint's ``epoch`` and resumed (A8), a lock-guarded
+membership table (races in §5.2), a monotonic *term* sent as metadata so
+clients fence off a stale coordinator (split brain), and the rejoin tracker
+is a daemon thread that stops with the coordinator.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import threading
+import time
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Dict, List, Optional
+
+import grpc
+import torch
+
+from .. import ckpt as ck
+from ..parallel.group import StoreHost
+from ..utils.metrics import MetricsLog, Timer, log
+from ..wire import proto as P
+from .client_agent import META_GEN, META_ROUND, META_STORE, META_TERM
+
+
+@dataclass
+class CoordinatorConfig:
+    clients: List[str] = field(default_factory=lambda: ["localhost:50051", "localhost:50052"])
+    rounds: int = 20                     # src/server.py:120
+    agg: str = "collective"              # "collective" (RCCL among clients) | "grpc" (reference)
+    gzip: bool = False                   # -c Y on the control channel (src/server.py:103-107)
+    root: str = "."
+    primary: bool = True                 # mount dir Primary/ vs Backup/
+    train_timeout_s: float = 600.0
+    rpc_timeout_s: float = 30.0
+    heartbeat_s: float = 1.0             # rejoin probe period (src/server.py:81)
+    store_host: str = "127.0.0.1"
+    store_port: int = 0
+    backup_address: Optional[str] = None
+    min_clients: int = 1
+    round_pause_s: float = 0.0
+
+
+def fedavg_state_dicts(sds: List[dict], weights: Optional[List[float]] = None) -> "OrderedDict[str, torch.Tensor]":
+    """Uniform (or weighted) average of every entry (reference src/server.py:163-171).
+
+    Integer buffers stay integer: floor of the mean, which equals the
+    reference's float mean truncated back to int64 on load.
+    """
+    if not sds:
+        raise ValueError("no state dicts to average")
+    n = len(sds)
+    w = weights or [1.0 / n] * n
+    out = OrderedDict()
+    for k in sds[0]:
+        vals = [sd[k] for sd in sds]
+        if vals[0].is_floating_point():
+            acc = torch.zeros_like(vals[0], dtype=torch.float32)
+            for wi, v in zip(w, vals):
+                acc.add_(v.float(), alpha=wi)
+            out[k] = acc.to(vals[0].dtype)
+        else:
+            out[k] = torch.div(sum(v.long() for v in vals), n, rounding_mode="floor").to(vals[0].dtype)
+    return out
+
+
+class _Member:
+    __slots__ = ("address", "active", "channel", "stub")
+
+    def __init__(self, address: str, gzip: bool):
+        self.address = address
+        self.active = True
+        self.channel = P.make_channel(address, gzip=gzip)
+        self.stub = P.TrainerStub(self.channel)
+
+    def reconnect(self, gzip: bool) -> None:
+        try:
+            self.channel.close()
+        except Exception:
+            pass
+        self.channel = P.make_channel(self.address, gzip=gzip)
+        self.stub = P.TrainerStub(self.channel)
+
+
+class Coordinator:
+    def __init__(self, cfg: CoordinatorConfig, metrics: Optional[MetricsLog] = None, role: str = "primary",
+                 term: Optional[int] = None):
+        self.cfg = cfg
+        self.role = role
+        self.metrics = metrics or MetricsLog()
+        self.term = term if term is not None else time.time_ns()
+        self.mount = ck.mount_dir(cfg.root, cfg.primary)
+        self.model_path = self.mount / ck.OPTIMIZED_MODEL
+        self._lock = threading.Lock()
+        self.members: "OrderedDict[str, _Member]" = OrderedDict((a, _Member(a, cfg.gzip)) for a in cfg.clients)
+        self.stop_event = threading.Event()
+        self.generation = 0
+        self._last_live: Optional[tuple] = None
+        self.round = ck.read_epoch(self.model_path) or 0          # resume (quirk A8)
+        self.latest_model: Optional[bytes] = self.model_path.read_bytes() if self.model_path.exists() else None
+        self.store = StoreHost(cfg.store_host, cfg.store_port) if cfg.agg == "collective" else None
+        self._pool = cf.ThreadPoolExecutor(max_workers=max(4, 2 * len(self.members)), thread_name_prefix="fedmi-rpc")
+        self._replicator = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fedmi-replica")
+        self._backup = None
+        if cfg.backup_address:
+            self._backup = P.TrainerStub(P.make_channel(cfg.backup_address))
+        self._tracker: Optional[threading.Thread] = None
+        self.round_times: List[float] = []
+
+    # ---- logging / membership -------------------------------------------------
+    def _log(self, msg: str) -> None:
+        log(f"{self.role} coordinator", msg)
+
+    def live(self) -> List[str]:
+        with self._lock:
+            return [a for a, m in self.members.items() if m.active]
+
+    def _mark(self, address: str, active: bool) -> None:
+        with self._lock:
+            m = self.members.get(address)
+            if m is not None and m.active != active:
+                m.active = active
+                self._log(f"client {address} -> {'active' if active else 'INACTIVE'}")
+
+    def client_status(self) -> Dict[str, bool]:
+        with self._lock:
+            return {a: m.active for a, m in self.members.items()}
+
+    def _meta(self, round_no: int):
+        md = [(META_TERM, str(self.term)), (META_ROUND, str(round_no)), (META_GEN, str(self.generation))]
+        if self.store is not None:
+            md.append((META_STORE, f"{self.store.host}:{self.store.port}"))
+        return md
+
+    # ---- model persistence / replication --------------------------------------
+    def _install_global(self, data: bytes) -> None:
+        ck.atomic_write(self.model_path, data)
+        self.latest_model = data
+        if self._backup is not None:
+            self._replicator.submit(self._replicate, data)
+
+    def _replicate(self, data: bytes) -> None:
+        try:
+            self._backup.SendModel(P.SendModelRequest(model=ck.to_b64(data)), timeout=self.cfg.rpc_timeout_s,
+                                   metadata=[(META_TERM, str(self.term))])
+        except grpc.RpcError as e:
+            self._log(f"backup replication failed: {e.code().name}")
+
+    def _send_model(self, address: str, data_b64: str) -> bool:
+        m = self.members[address]
+        try:
+            m.stub.SendModel(P.SendModelRequest(model=data_b64), timeout=self.cfg.train_timeout_s,
+                             metadata=[(META_TERM, str(self.term))])
+            return True
+        except grpc.RpcError as e:
+            self._log(f"SendModel to {address} failed: {e.code().name}")
+            self._mark(address, False)
+            return False
+
+    # ---- one round ------------------------------------------------------------------
+    def run_round(self) -> bool:
+        live = self.live()
+        if len(live) < max(1, self.cfg.min_clients):
+            time.sleep(self.cfg.heartbeat_s)
+            return False
+        if tuple(live) != self._last_live:
+            self.generation += 1                      # new data-plane group for a new member set
+            self._last_live = tuple(live)
+        world = len(live)
+        rnd = self.round + 1
+        self._log(f"Starting round {rnd} with {world} client(s) (gen {self.generation})")
+        t = Timer()
+        md = self._meta(rnd)
+        futs = {}
+        for rank, addr in enumerate(live):
+            stub = self.members[addr].stub
+            futs[addr] = (rank, stub.StartTrain.future(P.TrainRequest(rank=rank, world=world),
+                                                       timeout=self.cfg.train_timeout_s, metadata=md))
+        replies, failed, client_rounds = {}, [], []
+        for addr, (rank, f) in futs.items():
+            try:
+                replies[rank] = f.result().message
+                tm = dict(f.trailing_metadata() or ())
+                if "x-fedmi-client-round" in tm:
+                    client_rounds.append(int(tm["x-fedmi-client-round"]))
+            except grpc.RpcError as e:
+                self._log(f"StartTrain on {addr} failed: {e.code().name} {e.details() or ''}".strip())
+                failed.append(addr)
+                self._mark(addr, False)
+        t_train = t.ms()
+        ok = False
+        if self.cfg.agg == "collective":
+            if failed:
+                # the survivors' all-reduce for this round is not trustworthy: redo with a new group
+                self._log(f"round {rnd} aborted ({len(failed)} client(s) lost); regrouping")
+            else:
+                msg = replies.get(0) or next((v for v in replies.values() if v), "")
+                if msg:
+                    self._install_global(ck.from_b64(msg))
+                ok = True
+        else:
+            good = {r: ck.from_b64(m) for r, m in replies.items() if m}
+            if good:
+                for r, data in good.items():
+                    ck.atomic_write(self.mount / f"test_{r}.pth", data)
+                sds = [ck.from_bytes(d)["net"] for d in good.values()]
+                avg = fedavg_state_dicts(sds)
+                data = ck.to_bytes(ck.make_checkpoint(avg, acc=1, epoch=rnd))
+                self._install_global(data)
+                b64 = ck.to_b64(data)
+                sends = [self._pool.submit(self._send_model, a, b64) for a in live if a not in failed]
+                for s in sends:
+                    s.result()
+                ok = True
+        if ok:
+            self.round = max([rnd] + client_rounds)
+        dt = t.ms()
+        self.round_times.append(dt)
+        self.metrics.write(role=self.role, event="round", round=rnd, ok=ok, world=world, generation=self.generation,
+                           failed=failed, train_ms=t_train, round_ms=dt, term=self.term)
+        if self.cfg.round_pause_s:
+            time.sleep(self.cfg.round_pause_s)
+        return ok
+
+    # ---- rejoin tracker (src/server.py:78-101) --------------------------------------
+    def _track(self) -> None:
+        while not self.stop_event.wait(self.cfg.heartbeat_s):
+            with self._lock:
+                inactive = [a for a, m in self.members.items() if not m.active]
+            for addr in inactive:
+                m = self.members[addr]
+                m.reconnect(self.cfg.gzip)
+                try:
+                    r = m.stub.HeartBeat(P.Request(), timeout=self.cfg.rpc_timeout_s)
+                except grpc.RpcError:
+                    continue
+                if r.status == 1:
+                    if self.latest_model is not None:
+                        if not self._send_model(addr, ck.to_b64(self.latest_model)):
+                            continue
+                    self._mark(addr, True)
+
+    def start_tracker(self) -> None:
+        if self._tracker is None:
+            self._tracker = threading.Thread(target=self._track, name="fedmi-tracker", daemon=True)
+            self._tracker.start()
+
+    # ---- lifecycle ------------------------------------------------------------------
+    def run(self) -> None:
+        self.start_tracker()
+        self._log(f"term {self.term}, resuming at round {self.round}, clients {list(self.members)}")
+        while self.round < self.cfg.rounds and not self.stop_event.is_set():
+            self.run_round()
+        self._log(f"finished at round {self.round}")
+
+    def stop(self) -> None:
+        self.stop_event.set()
+
+    def close(self) -> None:
+        self.stop()
+        self._replicator.shutdown(wait=True)
+        self._pool.shutdown(wait=False, cancel_futures=True)
+        for m in self.members.values():
+            try:
+                m.channel.close()
+            except Exception:
+                pass

@@ -1,0 +1,67 @@
+"""Shared test helpers (ports, subprocess clients, small CPU trainers)."""
+from __future__ import annotations
+
+import os
+import socket
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def small_trainer(model="mlp", n_train=512, n_test=256, seed=0, lr=0.05):
+    from fedmi.engine import build_trainer
+    from fedmi.engine.base import TrainerConfig
+    from fedmi.engine.data import make_dataset
+
+    spec = "synthetic-mnist" if model == "mlp" else "synthetic-cifar10"
+    data = make_dataset(spec, device="cpu", n_train=n_train, n_test=n_test, seed=0)
+    return build_trainer(model, data, torch.device("cpu"), TrainerConfig(lr=lr, seed=seed, eval_batch_size=256))
+
+
+def spawn_client(address: str, root: Path, *extra: str, log_path: Path | None = None) -> subprocess.Popen:
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, "-m", "fedmi.cli.client", "-a", address, "--device", "cpu", "--root", str(root),
+           "--quiet", *extra]
+    out = open(log_path, "w") if log_path else subprocess.DEVNULL
+    return subprocess.Popen(cmd, env=env, cwd=str(root), stdout=out, stderr=subprocess.STDOUT,
+                            start_new_session=True)
+
+
+def wait_heartbeat(address: str, timeout: float = 60.0) -> None:
+    from fedmi.wire import proto as P
+
+    stub = P.TrainerStub(P.make_channel(address))
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            if stub.HeartBeat(P.Request(), timeout=1.0).status == 1:
+                return
+        except Exception:
+            time.sleep(0.2)
+    raise TimeoutError(f"client {address} did not come up")
+
+
+def stop_proc(p: subprocess.Popen) -> None:
+    if p.poll() is None:
+        try:
+            os.killpg(p.pid, 15)
+        except ProcessLookupError:
+            return
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, 9)
+            p.wait(timeout=10)
