@@ -10,6 +10,7 @@
 #include <stdint.h>
 #include <vector>
 
+#include "kernels/common.h"
 #include "kernels/lenet_layout.h"
 #include "runtime/lenet_engine.h"
 
@@ -18,11 +19,12 @@ namespace py = pybind11;
 namespace fedmi {
 void launch_lenet_conv_fwd(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*, int,
                            bf16*, bf16*, int, bf16*, uint8_t*, uint8_t*, lenet::Stats*);
-void launch_lenet_fc_head(hipStream_t, const bf16*, const int*, int, int, const bf16*, const float*, bf16*, bf16*,
+void launch_lenet_fc_head(hipStream_t, const bf16*, const int*, int, int, const bf16*, const float*, float*, bf16*,
                           float*, lenet::Stats*);
-void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const bf16*, const bf16*,
-                           const bf16*, const bf16*, const bf16*, const uint8_t*, const uint8_t*, const bf16*, float*,
-                           float*);
+void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const float*, const bf16*,
+                           const bf16*, const bf16*, const uint8_t*, const uint8_t*, const bf16*, float*, float*);
+bool stamps_enabled();
+void read_stamps(unsigned long long*, bool);
 void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, const float*, const float*, int, float,
                       float, float, int*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
@@ -62,7 +64,7 @@ static LeNetBuffers buffers_from(const py::dict& d) {
   b.pool1 = P<bf16>(get("pool1"));
   b.am1 = P<uint8_t>(get("am1"));
   b.am2 = P<uint8_t>(get("am2"));
-  b.dZ1 = P<bf16>(get("dZ1"));
+  b.dact2 = P<float>(get("dact2"));
   b.dZ1T = P<bf16>(get("dZ1T"));
   b.conv_slab = P<float>(get("conv_slab"));
   b.fc1w_grad = P<float>(get("fc1w_grad"));
@@ -73,7 +75,15 @@ static LeNetBuffers buffers_from(const py::dict& d) {
   return b;
 }
 
-PYBIND11_MODULE(_fedmi_native, m) {
+static void fedmi_bind(py::module_& m) {
+  m.def("stamps_enabled", &stamps_enabled);
+  m.def("read_stamps", [](bool clear) {
+    const size_t n = (size_t)FEDMI_STAMP_KERNELS * FEDMI_STAMP_WGS * FEDMI_STAMP_SLOTS;
+    std::vector<unsigned long long> buf(n, 0ull);
+    read_stamps(buf.data(), clear);
+    return py::bytes(reinterpret_cast<const char*>(buf.data()), n * sizeof(unsigned long long));
+  }, py::arg("clear") = true);
+  m.attr("STAMP_SHAPE") = py::make_tuple(FEDMI_STAMP_KERNELS, FEDMI_STAMP_WGS, FEDMI_STAMP_SLOTS);
   m.doc() = "fedmi native runtime: fused LeNet HIP kernels, graph executor, flat-buffer and compression kernels (gfx950)";
 
   m.def("lenet_layout", []() {
@@ -130,20 +140,19 @@ PYBIND11_MODULE(_fedmi_native, m) {
     check_last("lenet_conv_fwd");
   });
   m.def("lenet_fc_head", [](uintptr_t st, uintptr_t act2, uintptr_t labels, int nb, int train, uintptr_t pk,
-                            uintptr_t params, uintptr_t dZ1, uintptr_t dZ1T, uintptr_t fc_slab, uintptr_t stats) {
+                            uintptr_t params, uintptr_t dact2, uintptr_t dZ1T, uintptr_t fc_slab, uintptr_t stats) {
     launch_lenet_fc_head(S(st), P<const bf16>(act2), P<const int>(labels), nb, train, P<const bf16>(pk),
-                         P<const float>(params), P<bf16>(dZ1), P<bf16>(dZ1T), P<float>(fc_slab),
+                         P<const float>(params), P<float>(dact2), P<bf16>(dZ1T), P<float>(fc_slab),
                          P<lenet::Stats>(stats));
     check_last("lenet_fc_head");
   });
   m.def("lenet_conv_bwd", [](uintptr_t st, uintptr_t images, int base, int nb, uint32_t seed, uintptr_t round_ctr,
-                             int augment, uintptr_t act2, uintptr_t act2T, uintptr_t dZ1, uintptr_t dZ1T,
-                             uintptr_t pool1, uintptr_t am1, uintptr_t am2, uintptr_t pk, uintptr_t conv_slab,
-                             uintptr_t fc1w_grad) {
+                             int augment, uintptr_t dact2, uintptr_t act2T, uintptr_t dZ1T, uintptr_t pool1,
+                             uintptr_t am1, uintptr_t am2, uintptr_t pk, uintptr_t conv_slab, uintptr_t fc1w_grad) {
     launch_lenet_conv_bwd(S(st), P<const uint8_t>(images), base, nb, seed, P<const int>(round_ctr), augment,
-                          P<const bf16>(act2), P<const bf16>(act2T), P<const bf16>(dZ1), P<const bf16>(dZ1T),
-                          P<const bf16>(pool1), P<const uint8_t>(am1), P<const uint8_t>(am2), P<const bf16>(pk),
-                          P<float>(conv_slab), P<float>(fc1w_grad));
+                          P<const float>(dact2), P<const bf16>(act2T), P<const bf16>(dZ1T), P<const bf16>(pool1),
+                          P<const uint8_t>(am1), P<const uint8_t>(am2), P<const bf16>(pk), P<float>(conv_slab),
+                          P<float>(fc1w_grad));
     check_last("lenet_conv_bwd");
   });
   m.def("lenet_sgd", [](uintptr_t st, uintptr_t params, uintptr_t mom, uintptr_t pk, uintptr_t conv_slab, int n_conv,
@@ -207,3 +216,9 @@ PYBIND11_MODULE(_fedmi_native, m) {
     check_last("dequant_accum");
   });
 }
+
+#ifdef FEDMI_STAMPS
+PYBIND11_MODULE(_fedmi_native_stamps, m) { fedmi_bind(m); }
+#else
+PYBIND11_MODULE(_fedmi_native, m) { fedmi_bind(m); }
+#endif

@@ -50,3 +50,20 @@ FEDMI_DEV float wave_sum(float v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
+
+// ---- optional per-phase timestamps (diagnostic build: -DFEDMI_STAMPS) -------
+// Lane 0 of each workgroup records s_memtime at phase boundaries (after the
+// phase's barrier), so phase shares can be read without a profiler.
+#define FEDMI_STAMP_KERNELS 4
+#define FEDMI_STAMP_WGS 1024
+#define FEDMI_STAMP_SLOTS 8
+#ifdef FEDMI_STAMPS
+extern __device__ unsigned long long fedmi_stamps[FEDMI_STAMP_KERNELS][FEDMI_STAMP_WGS][FEDMI_STAMP_SLOTS];
+#define FEDMI_STAMP(k, i)                                                                   \
+  do {                                                                                      \
+    if (threadIdx.x == 0 && blockIdx.x < FEDMI_STAMP_WGS)                                   \
+      fedmi_stamps[k][blockIdx.x][i] = __builtin_amdgcn_s_memtime();                        \
+  } while (0)
+#else
+#define FEDMI_STAMP(k, i) do {} while (0)
+#endif

@@ -31,6 +31,10 @@
 
 using namespace lenet;
 
+#ifdef FEDMI_STAMPS
+__device__ unsigned long long fedmi_stamps[FEDMI_STAMP_KERNELS][FEDMI_STAMP_WGS][FEDMI_STAMP_SLOTS];
+#endif
+
 namespace {
 
 constexpr int NT = 512;         // threads per workgroup (8 waves) for K1/K2/K3
@@ -102,10 +106,10 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
     uint8_t* __restrict__ am2_out,  // [nb][F0]  or null
     Stats* __restrict__ zero_stats) // stats block to reset before K2 accumulates (or null)
 {
-  // LDS: raw u8 | x channels-last [36][40][4] bf16 | conv1 out f32 [6][784]
-  //      | pool1 channels-last [14][14][8] bf16 | conv2 out f32 [16][100]
+  // LDS: raw u8 | x channels-last [36][40][4] bf16 | conv1 out f32 channels-last [784][8]
+  //      | pool1 channels-last [14][14][8] bf16 | conv2 out f32 channels-last [100][16]
   constexpr int XCL = 36 * 40 * 4, P1CL = 14 * 14 * 8;
-  constexpr int O_X = 3072, O_C1 = O_X + XCL * 2, O_P1 = O_C1 + C1 * NPOS1 * 4, O_C2 = O_P1 + P1CL * 2;
+  constexpr int O_X = 3072, O_C1 = O_X + XCL * 2, O_P1 = O_C1 + NPOS1 * 8 * 4, O_C2 = O_P1 + P1CL * 2;
   __shared__ __attribute__((aligned(16))) unsigned char smem[O_C2 + C2 * NPOS2 * 4];
   uint8_t* raw = smem;
   bf16* xcl = reinterpret_cast<bf16*>(smem + O_X);
@@ -121,8 +125,10 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
   // Reset the statistics the following FC-head launch accumulates into (a kernel
   // write instead of a memset node: ordered by the K1 -> K2 boundary in the graph).
   if (zero_stats != nullptr && s == 0 && tid == 0) *zero_stats = Stats{0.f, 0, 0, 0};
+  FEDMI_STAMP(0, 0);
 
   load_raw(images + (size_t)gidx * IMG_BYTES, raw);
+  zero_lds(xcl, XCL * 2);   // channel 3 and the right/bottom pad stay zero
   // conv1 weights (B fragments) + per-lane group offsets, while the image lands
   bf16x8 wb1[4];
   int go1[4];
@@ -134,12 +140,12 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
   }
   const Aug a = aug_params(augment, seed, round_ctr, gidx);
   __syncthreads();
-  for (int e = tid; e < XCL; e += NT) {
-    const int y = e / 160, rem = e - y * 160, x = rem >> 2, c = rem & 3;
-    const float v = (c < 3 && y < IMG && x < IMG) ? aug_pixel(raw, a, c, y, x) : 0.f;
-    xcl[e] = (bf16)v;
+  for (int e = tid; e < IMG_BYTES; e += NT) {   // lanes walk x: raw reads broadcast within a dword
+    const int c = e >> 10, y = (e >> 5) & 31, x = e & 31;
+    xcl[(y * 40 + x) * 4 + c] = (bf16)aug_pixel(raw, a, c, y, x);
   }
   __syncthreads();
+  FEDMI_STAMP(0, 1);
 
   // ---- conv1: M = 784 positions (49 tiles), N = 6 (pad 16), K = 128 (4 steps)
   {
@@ -153,7 +159,7 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
       for (int ks = 0; ks < 4; ++ks) acc = mfma16(ld8_b64x2(xb + go1[ks]), wb1[ks], acc);
       if (n16 < C1) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c1[n16 * NPOS1 + t * 16 + rq + r] = fmaxf(acc[r] + bias, 0.f);
+        for (int r = 0; r < 4; ++r) c1[(t * 16 + rq + r) * 8 + n16] = fmaxf(acc[r] + bias, 0.f);
       }
     }
   }
@@ -166,6 +172,7 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
     go2[ks] = g < 25 ? ((g / 5) * P1 + (g % 5)) * 8 : 0;
   }
   __syncthreads();
+  FEDMI_STAMP(0, 2);
 
   // ---- maxpool2 #1 (+ argmax code: 0=(0,0) 1=(0,1) 2=(1,0) 3=(1,1), first max wins)
   for (int e = tid; e < P1CL; e += NT) {
@@ -173,11 +180,11 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
     bf16 mb = (bf16)0.f;
     if (c < C1) {
       const int py = pos / P1, px = pos - py * P1;
-      const float* w = c1 + c * NPOS1 + (2 * py) * O1 + 2 * px;
+      const float* w = c1 + ((2 * py) * O1 + 2 * px) * 8 + c;
       float m = w[0]; int am = 0;
-      if (w[1] > m) { m = w[1]; am = 1; }
-      if (w[O1] > m) { m = w[O1]; am = 2; }
-      if (w[O1 + 1] > m) { m = w[O1 + 1]; am = 3; }
+      if (w[8] > m) { m = w[8]; am = 1; }
+      if (w[O1 * 8] > m) { m = w[O1 * 8]; am = 2; }
+      if (w[O1 * 8 + 8] > m) { m = w[O1 * 8 + 8]; am = 3; }
       mb = (bf16)m;
       if (pool1_out) {
         pool1_out[(size_t)s * NP1 + c * 196 + pos] = mb;
@@ -187,6 +194,7 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
     p1cl[e] = mb;
   }
   __syncthreads();
+  FEDMI_STAMP(0, 3);
 
   // ---- conv2: M = 100 positions (7 tiles), N = 16, K = 224 (7 steps)
   if (wave < 7) {
@@ -202,51 +210,58 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int p = t * 16 + rq + r;
-      if (p < NPOS2) c2[n16 * NPOS2 + p] = fmaxf(acc[r] + bias, 0.f);
+      if (p < NPOS2) c2[p * 16 + n16] = fmaxf(acc[r] + bias, 0.f);
     }
   }
   __syncthreads();
+  FEDMI_STAMP(0, 4);
 
   // ---- maxpool2 #2 -> flattened act2 row (torch .view order: o*25 + py*5 + px)
   for (int e = tid; e < F0P; e += NT) {
     bf16 mb = (bf16)0.f;
     if (e < F0) {
       const int o = e / 25, rem = e - o * 25, py = rem / P2, px = rem - py * P2;
-      const float* w = c2 + o * NPOS2 + (2 * py) * O2 + 2 * px;
+      const float* w = c2 + ((2 * py) * O2 + 2 * px) * 16 + o;
       float m = w[0]; int am = 0;
-      if (w[1] > m) { m = w[1]; am = 1; }
-      if (w[O2] > m) { m = w[O2]; am = 2; }
-      if (w[O2 + 1] > m) { m = w[O2 + 1]; am = 3; }
+      if (w[16] > m) { m = w[16]; am = 1; }
+      if (w[O2 * 16] > m) { m = w[O2 * 16]; am = 2; }
+      if (w[O2 * 16 + 16] > m) { m = w[O2 * 16 + 16]; am = 3; }
       mb = (bf16)m;
       if (am2_out) am2_out[(size_t)s * F0 + e] = (uint8_t)am;
     }
     act2[(size_t)s * F0P + e] = mb;
     if (act2T) act2T[(size_t)e * tstride + s] = mb;
   }
+  FEDMI_STAMP(0, 5);
 }
 
 // ---------------------------------------------------------------------------
 // K2: FC head, 16 samples per workgroup (one MFMA row tile), 8 waves.
 //   fwd: H1 = relu(X W1^T + b1), H2 = relu(H1 W2^T + b2), Z = H2 W3^T + b3
 //   CE:  loss/acc counters; dZ = (softmax - onehot) / nb  (mean reduction)
-//   bwd: dW3/db3, dH2, dW2/db2, dH1 -> dZ1 (+db1).  dZ1 goes to global for K3.
-// Wgrad GEMMs reduce over samples (K = 32, samples 16..31 zero), so the
-// activations are also kept sample-contiguous ("T" images) in LDS.
+//   bwd: dW3/db3, dH2, dW2/db2, dH1 -> dZ1 (+db1), dX = dZ1 W1 (masked by the
+//        pool2 ReLU) -> d(pool2) for K3; dZ1^T to global for the fc1 wgrad.
+// Every global operand is prefetched into registers at kernel entry or right
+// after fc1 so no phase waits on a cold L2/HBM round trip.  Wgrad GEMMs
+// reduce over samples (K = 32, samples 16..31 zero), so activations are also
+// kept sample-contiguous ("T" images) in LDS.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void lenet_fc_head(
     const bf16* __restrict__ act2,   // [nb][F0P]
     const int* __restrict__ labels,  // labels of this batch (already offset)
     int nb, int train,
     const bf16* __restrict__ pk, const float* __restrict__ params,
-    bf16* __restrict__ dZ1,          // [128][DZ1_LD]  (train)
-    bf16* __restrict__ dZ1T,         // [128][DZ1_LD]  (train)
-    float* __restrict__ fc_slab,     // [grid][FS]     (train)
+    float* __restrict__ dact2,       // [128][F0]       (train)
+    bf16* __restrict__ dZ1T,         // [128][DZ1_LD]   (train)
+    float* __restrict__ fc_slab,     // [grid][FS]      (train)
     Stats* __restrict__ stats)
 {
+  __shared__ __attribute__((aligned(16))) bf16 sX[16 * F0P];
   __shared__ __attribute__((aligned(16))) bf16 sH1[16 * 128], sH1T[128 * 32];
   __shared__ __attribute__((aligned(16))) bf16 sH2[16 * 96], sH2T[96 * 32];
   __shared__ __attribute__((aligned(16))) bf16 sdZ3[16 * 32], sdZ3T[16 * 32];
   __shared__ __attribute__((aligned(16))) bf16 sdZ2[16 * 96], sdZ2T[96 * 32];
+  __shared__ __attribute__((aligned(16))) bf16 sdZ1[16 * 128];
   __shared__ float sZ[16 * 16];
   __shared__ float sdb[128 + 96 + 16];
 
@@ -255,55 +270,89 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
   const int s0 = blockIdx.x * FC_SPW;
   const int ns = min(FC_SPW, nb - s0);
   if (ns <= 0) return;
+  FEDMI_STAMP(1, 0);
+
+  // ---- prefetch fc1 operands (13 k-steps) and the fc2/fc3 forward weights
+  // All loads are unconditional with clamped addresses (a per-load select on a
+  // runtime condition makes hipcc branch around each load and wait vmcnt(0)).
+  const bool valid = n16 < ns;
+  bf16x8 af[13], bfr[13];
+  {
+    const bf16* xa = act2 + (size_t)(s0 + (valid ? n16 : 0)) * F0P + kq;
+    const bf16* wb = pk + PK_FC1 + (wave * 16 + n16) * F0P + kq;
+#pragma unroll
+    for (int ks = 0; ks < 13; ++ks) {
+      af[ks] = ld8(xa + ks * 32);
+      bfr[ks] = ld8(wb + ks * 32);
+    }
+  }
+  bf16x8 w2f[4], w3f[3];
+  const int nf1 = wave * 16 + n16;
+  const int nf2 = (wave < 6 ? wave : 0) * 16 + n16;
+  const float b1 = params[P_F1B + min(nf1, F1 - 1)];
+  const float b2 = params[P_F2B + min(nf2, F2 - 1)];
+  const float b3 = params[P_F3B + min(n16, NCLS - 1)];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) w2f[ks] = ld8(pk + PK_FC2 + nf2 * 128 + ks * 32 + kq);
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) w3f[ks] = ld8(pk + PK_FC3 + n16 * 96 + ks * 32 + kq);
+  if (!valid) {
+#pragma unroll
+    for (int ks = 0; ks < 13; ++ks) af[ks] = zero8();
+  }
 
   zero_lds(sH1T, sizeof(sH1T));
   zero_lds(sH2T, sizeof(sH2T));
+  zero_lds(sdZ3, sizeof(sdZ3));
   zero_lds(sdZ3T, sizeof(sdZ3T));
   zero_lds(sdZ2T, sizeof(sdZ2T));
   for (int e = tid; e < 240; e += NT) sdb[e] = 0.f;
 
-  // ---- fc1 fwd: wave w -> output tile n in [16w, 16w+16); K = 416 (13 steps)
-  {
-    const bool valid = n16 < ns;
-    const bf16* xa = act2 + (size_t)(s0 + (valid ? n16 : 0)) * F0P + kq;
-    const bf16* wb = pk + PK_FC1 + (wave * 16 + n16) * F0P + kq;
-    bf16x8 af[13], bfr[13];
+  // ---- fc1 fwd: wave w -> outputs [16w, 16w+16); K = 416 (13 steps)
+  f32x4 acc1 = zero4();
 #pragma unroll
-    for (int ks = 0; ks < 13; ++ks) {
-      af[ks] = valid ? ld8(xa + ks * 32) : zero8();
-      bfr[ks] = ld8(wb + ks * 32);
-    }
-    f32x4 acc = zero4();
+  for (int ks = 0; ks < 13; ++ks) acc1 = mfma16(af[ks], bfr[ks], acc1);
+  if (wave == 0) {   // keep X (this tile's act2 rows) for the dX ReLU mask
 #pragma unroll
-    for (int ks = 0; ks < 13; ++ks) acc = mfma16(af[ks], bfr[ks], acc);
-    const int n = wave * 16 + n16;
-    const float b = n < F1 ? params[P_F1B + n] : 0.f;
-    __syncthreads();   // T images zeroed before they are written
+    for (int ks = 0; ks < 13; ++ks) *reinterpret_cast<bf16x8*>(sX + n16 * F0P + ks * 32 + kq) = af[ks];
+  }
+  // backward weights: dH2 task (q in {w, w+8} intersect [6,12)), dH1 tile w, dX tiles w + 8j
+  bf16x8 w3t, w2t[3], wxt[4][4];
+  const int q5 = wave >= 6 ? wave : wave + 8;          // this wave's dH2 task (valid if < 12)
+  if (train) {
+    w3t = ld8(pk + PK_FC3T + ((min(q5, 11) - 6) * 16 + n16) * 32 + kq);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int sr = rq + r;
-      const float hv = (n < F1 && sr < ns) ? fmaxf(acc[r] + b, 0.f) : 0.f;
-      sH1[sr * 128 + n] = (bf16)hv;
-      sH1T[n * 32 + sr] = (bf16)hv;
+    for (int ks = 0; ks < 3; ++ks) w2t[ks] = ld8(pk + PK_FC2T + nf1 * 96 + ks * 32 + kq);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = min(wave + 8 * j, F0 / 16 - 1);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) wxt[j][ks] = ld8(pk + PK_FC1T + (t * 16 + n16) * 128 + ks * 32 + kq);
     }
   }
+  __syncthreads();   // T images zeroed (and sX written) before use
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int sr = rq + r;
+    const float hv = (nf1 < F1 && sr < ns) ? fmaxf(acc1[r] + b1, 0.f) : 0.f;
+    sH1[sr * 128 + nf1] = (bf16)hv;
+    sH1T[nf1 * 32 + sr] = (bf16)hv;
+  }
   __syncthreads();
+  FEDMI_STAMP(1, 1);
 
   // ---- fc2 fwd: waves 0..5 -> 16 outputs each; K = 128 (4 steps)
   if (wave < 6) {
     const bf16* ha = sH1 + n16 * 128 + kq;
-    const bf16* wb = pk + PK_FC2 + (wave * 16 + n16) * 128 + kq;
     f32x4 acc = zero4();
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) acc = mfma16(ld8(ha + ks * 32), ld8(wb + ks * 32), acc);
-    const int n = wave * 16 + n16;
-    const float b = n < F2 ? params[P_F2B + n] : 0.f;
+    for (int ks = 0; ks < 4; ++ks) acc = mfma16(ld8(ha + ks * 32), w2f[ks], acc);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int sr = rq + r;
-      const float hv = (n < F2 && sr < ns) ? fmaxf(acc[r] + b, 0.f) : 0.f;
-      sH2[sr * 96 + n] = (bf16)hv;
-      sH2T[n * 32 + sr] = (bf16)hv;
+      const float hv = (nf1 < F2 && sr < ns) ? fmaxf(acc[r] + b2, 0.f) : 0.f;
+      sH2[sr * 96 + nf1] = (bf16)hv;
+      sH2T[nf1 * 32 + sr] = (bf16)hv;
     }
   }
   __syncthreads();
@@ -311,15 +360,14 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
   // ---- fc3 fwd: logits [16 x 16]; K = 96 (3 steps)
   if (wave == 0) {
     const bf16* ha = sH2 + n16 * 96 + kq;
-    const bf16* wb = pk + PK_FC3 + n16 * 96 + kq;
     f32x4 acc = zero4();
 #pragma unroll
-    for (int ks = 0; ks < 3; ++ks) acc = mfma16(ld8(ha + ks * 32), ld8(wb + ks * 32), acc);
-    const float b = n16 < NCLS ? params[P_F3B + n16] : 0.f;
+    for (int ks = 0; ks < 3; ++ks) acc = mfma16(ld8(ha + ks * 32), w3f[ks], acc);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sZ[(rq + r) * 16 + n16] = acc[r] + b;
+    for (int r = 0; r < 4; ++r) sZ[(rq + r) * 16 + n16] = acc[r] + b3;
   }
   __syncthreads();
+  FEDMI_STAMP(1, 2);
 
   // ---- cross-entropy (mean over the batch nb), accuracy, dZ3
   if (wave == 0) {
@@ -351,15 +399,14 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
 #pragma unroll
         for (int n = 0; n < NCLS; ++n) dz[n] = 0.f;
       }
-      if (train) {
+      if (train) {   // sdZ3 / sdZ3T were zeroed at entry: write the 10 live entries only
 #pragma unroll
-        for (int n = 0; n < 32; ++n) {
-          const float v = n < NCLS ? dz[n < NCLS ? n : 0] : 0.f;
-          sdZ3[sr * 32 + n] = (bf16)v;
-          if (n < 16) sdZ3T[n * 32 + sr] = (bf16)v;
+        for (int n = 0; n < NCLS; ++n) {
+          const bf16 v = (bf16)dz[n];
+          sdZ3[sr * 32 + n] = v;
+          sdZ3T[n * 32 + sr] = v;
+          sZ[sr * 16 + n] = dz[n];   // fp32 dZ3 for db3
         }
-#pragma unroll
-        for (int n = 0; n < NCLS; ++n) sZ[sr * 16 + n] = dz[n];   // fp32 dZ3 for db3
       }
     }
     loss = wave_sum(loss);
@@ -372,6 +419,7 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
   }
   if (!train) return;
   __syncthreads();
+  FEDMI_STAMP(1, 3);
 
   float* slab = fc_slab + (size_t)blockIdx.x * FS;
   constexpr int OF3W = P_F3W - P_F1B, OF2W = P_F2W - P_F1B;
@@ -382,7 +430,7 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
     sdb[224 + tid] = acc;
   }
 
-  // ---- dW3 (6 tiles) and dH2 = dZ3 . W3 (6 tiles)
+  // ---- dW3 (tasks 0..5) and dH2 = dZ3 . W3 (tasks 6..11)
   for (int q = wave; q < 12; q += NW) {
     if (q < 6) {
       const int ft = q;
@@ -394,7 +442,7 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
       }
     } else {
       const int f = (q - 6) * 16 + n16;
-      const f32x4 acc = mfma16(ld8(sdZ3 + n16 * 32 + kq), ld8(pk + PK_FC3T + f * 32 + kq), zero4());
+      const f32x4 acc = mfma16(ld8(sdZ3 + n16 * 32 + kq), w3t, zero4());
       float colsum = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -410,40 +458,58 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
     }
   }
   __syncthreads();
+  FEDMI_STAMP(1, 4);
 
-  // ---- dW2 = dZ2^T H1 (48 tiles) and dH1 = dZ2 . W2 (8 tiles) -> dZ1
-  for (int q = wave; q < 56; q += NW) {
-    if (q < 48) {
-      const int mt = q >> 3, ft = q & 7;
-      const f32x4 acc = mfma16(ld8(sdZ2T + (mt * 16 + n16) * 32 + kq), ld8(sH1T + (ft * 16 + n16) * 32 + kq), zero4());
+  // ---- dW2 = dZ2^T H1 (48 tiles) and dH1 = dZ2 . W2 (tile = wave) -> dZ1
+  for (int q = wave; q < 48; q += NW) {
+    const int mt = q >> 3, ft = q & 7;
+    const f32x4 acc = mfma16(ld8(sdZ2T + (mt * 16 + n16) * 32 + kq), ld8(sH1T + (ft * 16 + n16) * 32 + kq), zero4());
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = mt * 16 + rq + r, f = ft * 16 + n16;
-        if (n < F2 && f < F1) slab[OF2W + n * F1 + f] = acc[r];
-      }
-    } else {
-      const int f = (q - 48) * 16 + n16;
-      const bf16* za = sdZ2 + n16 * 96 + kq;
-      const bf16* wb = pk + PK_FC2T + f * 96 + kq;
+    for (int r = 0; r < 4; ++r) {
+      const int n = mt * 16 + rq + r, f = ft * 16 + n16;
+      if (n < F2 && f < F1) slab[OF2W + n * F1 + f] = acc[r];
+    }
+  }
+  {
+    const int f = nf1;
+    const bf16* za = sdZ2 + n16 * 96 + kq;
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) acc = mfma16(ld8(za + ks * 32), w2t[ks], acc);
+    float colsum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int sr = rq + r;
+      const float g = (f < F1 && (float)sH1[sr * 128 + f] > 0.f) ? acc[r] : 0.f;
+      const bf16 gb = (bf16)g;
+      sdZ1[sr * 128 + f] = gb;
+      dZ1T[(size_t)f * DZ1_LD + s0 + sr] = gb;
+      colsum += g;
+    }
+    colsum += __shfl_xor(colsum, 16, 64);
+    colsum += __shfl_xor(colsum, 32, 64);
+    if (lane < 16 && f < F1) atomicAdd(&sdb[f], colsum);
+  }
+  __syncthreads();
+  FEDMI_STAMP(1, 5);
+
+  // ---- dX = dZ1 . W1 (25 tiles, K = 128), masked by the pool2 ReLU -> d(pool2)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int t = wave + 8 * j;
+    if (t < F0 / 16) {
+      const int f = t * 16 + n16;
+      const bf16* za = sdZ1 + n16 * 128 + kq;
       f32x4 acc = zero4();
 #pragma unroll
-      for (int ks = 0; ks < 3; ++ks) acc = mfma16(ld8(za + ks * 32), ld8(wb + ks * 32), acc);
-      float colsum = 0.f;
+      for (int ks = 0; ks < 4; ++ks) acc = mfma16(ld8(za + ks * 32), wxt[j][ks], acc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int sr = rq + r;
-        const float g = (f < F1 && (float)sH1[sr * 128 + f] > 0.f) ? acc[r] : 0.f;
-        const bf16 gb = (bf16)g;
-        dZ1[(size_t)(s0 + sr) * DZ1_LD + f] = gb;
-        dZ1T[(size_t)f * DZ1_LD + s0 + sr] = gb;
-        colsum += g;
+        if (sr < ns) dact2[(size_t)(s0 + sr) * F0 + f] = (float)sX[sr * F0P + f] > 0.f ? acc[r] : 0.f;
       }
-      colsum += __shfl_xor(colsum, 16, 64);
-      colsum += __shfl_xor(colsum, 32, 64);
-      if (lane < 16 && f < F1) atomicAdd(&sdb[f], colsum);
     }
   }
-  __syncthreads();
   for (int e = tid; e < F1; e += NT) slab[e] = sdb[e];                       // fc1.bias
   for (int e = tid; e < F2; e += NT) slab[P_F2B - P_F1B + e] = sdb[128 + e];
   if (tid < NCLS) slab[P_F3B - P_F1B + tid] = sdb[224 + tid];
@@ -455,17 +521,19 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
       dZ1T[(size_t)f * DZ1_LD + c] = (bf16)0.f;
     }
   }
+  FEDMI_STAMP(1, 6);
 }
 
 // ---------------------------------------------------------------------------
 // K3: conv stack backward (one workgroup per sample) + fc1 wgrad workgroups.
+// All per-sample inputs and the conv2 dgrad weights are staged into LDS with
+// 16-byte loads at entry; every MFMA operand afterwards is an LDS read.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void lenet_conv_bwd(
     const uint8_t* __restrict__ images, int sample_base, int nb,
     uint32_t seed, const int* __restrict__ round_ctr, int augment,
-    const bf16* __restrict__ act2,         // [nb][F0P]
+    const float* __restrict__ dact2,       // [nb][F0]   d(pool2), ReLU-masked
     const bf16* __restrict__ act2T,        // [F0P][128]
-    const bf16* __restrict__ dZ1,          // [128][128]
     const bf16* __restrict__ dZ1T,         // [128][128]
     const bf16* __restrict__ pool1,        // [nb][NP1]
     const uint8_t* __restrict__ am1,       // [nb][NP1]
@@ -474,15 +542,15 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
     float* __restrict__ conv_slab,         // [nb][CS]
     float* __restrict__ fc1w_grad)         // [F1W_N]
 {
-  // LDS carve (bytes)
   constexpr int XSH = 5 * 3 * 32 * 32;        // x shifted copies [s][c][y][x']
   constexpr int P1SH = 5 * 6 * 14 * 16;       // pool1 shifted copies [s][c][y][x']
   constexpr int DY2W = 16 * 160;              // conv2 out-grad [o][i*16+j]
   constexpr int DY2C = 18 * 18 * 16;          // conv2 out-grad channels-last, 4-px zero border
   constexpr int DY1 = 6 * 896;                // conv1 out-grad [o][i*32+j]
-  constexpr int O_RAW = 0, O_XSH = 3072, O_P1SH = O_XSH + XSH * 2, O_DY2W = O_P1SH + P1SH * 2,
-                O_DY2C = O_DY2W + DY2W * 2, O_DY1 = O_DY2C + DY2C * 2, O_DX = O_DY1 + DY1 * 2,
-                O_DW1 = O_DX + F0 * 4, O_DB = O_DW1 + 16 * 80 * 4, O_END = O_DB + 32 * 4;
+  constexpr int O_RAW = 0, O_P1R = 3072, O_AM1 = O_P1R + 2368, O_AM2 = O_AM1 + 1184, O_DX = O_AM2 + 416,
+                O_WDG = O_DX + F0 * 4, O_XSH = O_WDG + 16 * KDGP * 2, O_P1SH = O_XSH + XSH * 2,
+                O_DY2W = O_P1SH + P1SH * 2, O_DY2C = O_DY2W + DY2W * 2, O_DY1 = O_DY2C + DY2C * 2,
+                O_DW1 = O_DY1 + DY1 * 2, O_DB = O_DW1 + 16 * 80 * 4, O_END = O_DB + 32 * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem[O_END];
 
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
@@ -495,8 +563,16 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
     const int nks = (nb + 31) >> 5;
     const bf16* ap = dZ1T + (wave * 16 + n16) * DZ1_LD + kq;
     const bf16* bp = act2T + (size_t)(e * 16 + n16) * MAX_TRAIN_BATCH + kq;
+    bf16x8 a[4], b[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {   // always load all 4 k-steps (columns >= nb of dZ1T are zero)
+      a[ks] = ld8(ap + ks * 32);
+      b[ks] = ld8(bp + ks * 32);
+    }
+    (void)nks;
     f32x4 acc = zero4();
-    for (int ks = 0; ks < nks; ++ks) acc = mfma16(ld8(ap + ks * 32), ld8(bp + ks * 32), acc);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) acc = mfma16(a[ks], b[ks], acc);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = wave * 16 + rq + r;
@@ -506,69 +582,82 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
   }
 
   uint8_t* raw = smem + O_RAW;
+  bf16* p1r = reinterpret_cast<bf16*>(smem + O_P1R);
+  uint8_t* am1s = smem + O_AM1;
+  uint8_t* am2s = smem + O_AM2;
+  float* dxs = reinterpret_cast<float*>(smem + O_DX);
+  bf16* wdg = reinterpret_cast<bf16*>(smem + O_WDG);
   bf16* xsh = reinterpret_cast<bf16*>(smem + O_XSH);
   bf16* p1sh = reinterpret_cast<bf16*>(smem + O_P1SH);
   bf16* dY2w = reinterpret_cast<bf16*>(smem + O_DY2W);
   bf16* dY2c = reinterpret_cast<bf16*>(smem + O_DY2C);
   bf16* dY1 = reinterpret_cast<bf16*>(smem + O_DY1);
-  float* dx = reinterpret_cast<float*>(smem + O_DX);
-  float* dW1acc = reinterpret_cast<float*>(smem + O_DW1);
   float* db = reinterpret_cast<float*>(smem + O_DB);
 
   const int s = blockIdx.x;
   const int gidx = sample_base + s;
+  FEDMI_STAMP(2, 0);
 
-  load_raw(images + (size_t)gidx * IMG_BYTES, raw);
+  // ---- stage everything this sample needs (16-B loads; 8-B for the argmax row)
+  {
+    constexpr int N_RAW = IMG_BYTES / 16, N_P1 = NP1 * 2 / 16, N_AM1 = NP1 / 8, N_AM2 = F0 / 16,
+                  N_DX = F0 * 4 / 16, N_WDG = 16 * KDGP * 2 / 16;
+    constexpr int E1 = N_RAW, E2 = E1 + N_P1, E3 = E2 + N_AM1, E4 = E3 + N_AM2, E5 = E4 + N_DX, E6 = E5 + N_WDG;
+    const uint4* img4 = reinterpret_cast<const uint4*>(images + (size_t)gidx * IMG_BYTES);
+    const uint4* p14 = reinterpret_cast<const uint4*>(pool1 + (size_t)s * NP1);
+    const uint2* am12 = reinterpret_cast<const uint2*>(am1 + (size_t)s * NP1);
+    const uint4* am24 = reinterpret_cast<const uint4*>(am2 + (size_t)s * F0);
+    const uint4* dx4 = reinterpret_cast<const uint4*>(dact2 + (size_t)s * F0);
+    const uint4* wdg4 = reinterpret_cast<const uint4*>(pk + PK_W2DG);
+    for (int e = tid; e < E6; e += NT) {
+      if (e < E1) reinterpret_cast<uint4*>(raw)[e] = img4[e];
+      else if (e < E2) reinterpret_cast<uint4*>(p1r)[e - E1] = p14[e - E1];
+      else if (e < E3) reinterpret_cast<uint2*>(am1s)[e - E2] = am12[e - E2];
+      else if (e < E4) reinterpret_cast<uint4*>(am2s)[e - E3] = am24[e - E3];
+      else if (e < E5) reinterpret_cast<uint4*>(dxs)[e - E4] = dx4[e - E4];
+      else reinterpret_cast<uint4*>(wdg)[e - E5] = wdg4[e - E5];
+    }
+  }
   zero_lds(dY2w, DY2W * 2);
   zero_lds(dY2c, DY2C * 2);
   zero_lds(dY1, DY1 * 2);
-  for (int e = tid; e < 16 * 80; e += NT) dW1acc[e] = 0.f;
+  zero_lds(xsh, XSH * 2);      // tails of the shifted copies (x' + s beyond the row) stay zero
+  zero_lds(p1sh, P1SH * 2);
   if (tid < 32) db[tid] = 0.f;
-  // pool1 shifted copies straight from global (one writer per element)
-  for (int e = tid; e < P1SH; e += NT) {
-    const int xp = e & 15, rest = e >> 4, y = rest % 14, sc = rest / 14, c = sc % 6, sh = sc / 6;
-    const int xx = xp + sh;
-    p1sh[e] = (xx < P1) ? pool1[(size_t)s * NP1 + c * 196 + y * P1 + xx] : (bf16)0.f;
-  }
+  const Aug a = aug_params(augment, seed, round_ctr, gidx);
+  __syncthreads();
+  FEDMI_STAMP(2, 1);
 
-  // ---- d(pool2) = dZ1[s] . W1 (masked by the pool2 ReLU): M = 1 (of 16), N = 400, K = 128
-  {
-    const bf16x8 z = zero8();
-    bf16x8 af[4];
+  // each augmented pixel / pooled value is computed once and stored into its 5
+  // column-shifted copies: copy s holds element x at column x - s
+  for (int e = tid; e < IMG_BYTES; e += NT) {
+    const int c = e >> 10, y = (e >> 5) & 31, x = e & 31;
+    const bf16 v = (bf16)aug_pixel(raw, a, c, y, x);
+    bf16* row = xsh + (c * 32 + y) * 32 + x;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) af[ks] = n16 == 0 ? ld8(dZ1 + (size_t)s * DZ1_LD + ks * 32 + kq) : z;
-    for (int nt = wave; nt < F0 / 16; nt += NW) {
-      const int f = nt * 16 + n16;
-      const bf16* wb = pk + PK_FC1T + f * 128 + kq;
-      f32x4 acc = zero4();
+    for (int sh = 0; sh < 5; ++sh)
+      if (x >= sh) row[sh * (3 * 32 * 32) - sh] = v;
+  }
+  for (int e = tid; e < NP1; e += NT) {
+    const int c = e / 196, rem = e - c * 196, y = rem / P1, x = rem - y * P1;
+    const bf16 v = p1r[e];
+    bf16* row = p1sh + (c * 14 + y) * 16 + x;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) acc = mfma16(af[ks], ld8(wb + ks * 32), acc);
-      if (lane < 16) dx[f] = (float)act2[(size_t)s * F0P + f] > 0.f ? acc[0] : 0.f;
-    }
+    for (int sh = 0; sh < 5; ++sh)
+      if (x >= sh) row[sh * (6 * 14 * 16) - sh] = v;
   }
-  __syncthreads();   // raw image, dx, zeroed buffers visible
-
-  // x shifted copies (augmented, normalised)
-  {
-    const Aug a = aug_params(augment, seed, round_ctr, gidx);
-    for (int e = tid; e < XSH; e += NT) {
-      const int xp = e & 31, y = (e >> 5) & 31, sc = e >> 10, c = sc % 3, sh = sc / 3;
-      const int xx = xp + sh;
-      xsh[e] = (bf16)(xx < IMG ? aug_pixel(raw, a, c, y, xx) : 0.f);
-    }
-  }
-  // pool2 / relu backward: route each pooled grad to its argmax position
   for (int f = tid; f < F0; f += NT) {
     const int o = f / 25, rem = f - o * 25, py = rem / P2, px = rem - py * P2;
-    const int am = am2[(size_t)s * F0 + f];
+    const int am = am2s[f];
     const int y = 2 * py + (am >> 1), x = 2 * px + (am & 1);
-    const float g = dx[f];
+    const float g = dxs[f];
     const bf16 gb = (bf16)g;
     dY2w[o * 160 + y * 16 + x] = gb;
     dY2c[((y + 4) * 18 + (x + 4)) * 16 + o] = gb;
     atomicAdd(&db[o], g);
   }
   __syncthreads();
+  FEDMI_STAMP(2, 2);
 
   float* slab = conv_slab + (size_t)s * CS;
 
@@ -593,84 +682,73 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
 
   // ---- conv2 dgrad: dP1[c][pos] = sum_(r,s,o) dY2[o][y-r][x-s] W2[o][c][r][s]
   //      M = 196 positions (13 tiles), N = 6 (pad 16), K = 416 (13 steps)
-  {
-    for (int t = wave; t < 13; t += NW) {
-      int pos = t * 16 + n16;
-      if (pos >= 196) pos = 0;
-      const int y = pos / P1, x = pos - y * P1;
-      const bf16* wb = pk + PK_W2DG + n16 * KDGP + kq;
-      f32x4 acc = zero4();
+  int koff[13];   // per-lane K-group offsets into dY2c relative to the output position
 #pragma unroll
-      for (int ks = 0; ks < 13; ++ks) {
-        const int G = ks * 4 + (lane >> 4), g = G >> 1;
-        int off = 0;
-        if (g < 25) {
-          const int r = g / 5, sc = g - r * 5;
-          off = ((y - r + 4) * 18 + (x - sc + 4)) * 16 + (G & 1) * 8;
-        }
-        acc = mfma16(ld8(dY2c + off), ld8(wb + ks * 32), acc);
-      }
-      if (n16 < C1) {
-        const int c = n16;
-        float csum = 0.f;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int p = t * 16 + rq + rr;
-          if (p < 196) {
-            const int py = p / P1, px = p - py * P1;
-            const float pooled = (float)p1sh[(c * 14 + py) * 16 + px];
-            const float g = pooled > 0.f ? acc[rr] : 0.f;
-            const int am = am1[(size_t)s * NP1 + c * 196 + p];
-            const int yy = 2 * py + (am >> 1), xx = 2 * px + (am & 1);
-            dY1[c * 896 + yy * 32 + xx] = (bf16)g;
-            csum += g;
-          }
-        }
-        atomicAdd(&db[16 + c], csum);
-      }
-    }
+  for (int ks = 0; ks < 13; ++ks) {
+    const int G = ks * 4 + (lane >> 4), g = G >> 1;
+    const int r = g / 5, sc = g - r * 5;
+    koff[ks] = g < 25 ? (-r * 18 - sc) * 16 + (G & 1) * 8 : 0;   // pad group: weight 0, any in-bounds read
   }
-  __syncthreads();
-
-  // ---- conv1 wgrad: dW1[o][k'] = sum_p dY1[o][p] * im2col(x)[p][k']
-  //      M = 16 (o < 6), N = 75 (5 tiles), K = 896 (p' = i*32 + j: step = row i)
-  //      K split over the 8 waves, combined with LDS float atomics.
-  {
-    const bf16* bb[5];
+  for (int t = wave; t < 13; t += NW) {
+    int pos = t * 16 + n16;
+    if (pos >= 196) pos = 0;
+    const int y = pos / P1, x = pos - y * P1;
+    const bf16* gb = dY2c + ((y + 4) * 18 + (x + 4)) * 16;
+    const bf16* wb = wdg + n16 * KDGP + kq;
+    f32x4 acc = zero4();
 #pragma unroll
-    for (int nt = 0; nt < 5; ++nt) {
-      const int kk = nt * 16 + n16;
-      const int kc = kk < 75 ? kk : 0;
-      const int c = kc / 25, rs = kc - c * 25, r = rs / 5, sc = rs - r * 5;
-      bb[nt] = xsh + ((sc * 3 + c) * 32 + r) * 32 + kq;
-    }
-    f32x4 acc[5];
-#pragma unroll
-    for (int nt = 0; nt < 5; ++nt) acc[nt] = zero4();
-    const bf16x8 z = zero8();
-    for (int ks = wave; ks < O1; ks += NW) {
-      const bf16x8 a = n16 < C1 ? ld8(dY1 + n16 * 896 + ks * 32 + kq) : z;
-#pragma unroll
-      for (int nt = 0; nt < 5; ++nt) acc[nt] = mfma16(a, ld8(bb[nt] + ks * 32), acc[nt]);
-    }
-#pragma unroll
-    for (int nt = 0; nt < 5; ++nt) {
+    for (int ks = 0; ks < 13; ++ks) acc = mfma16(ld8(gb + koff[ks]), ld8(wb + ks * 32), acc);
+    if (n16 < C1) {
+      const int c = n16;
+      float csum = 0.f;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const int o = rq + rr, kk = nt * 16 + n16;
-        if (o < C1 && kk < 75) atomicAdd(&dW1acc[o * 80 + kk], acc[nt][rr]);
+        const int p = t * 16 + rq + rr;
+        if (p < 196) {
+          const int py = p / P1, px = p - py * P1;
+          const float pooled = (float)p1r[c * 196 + p];
+          const float g = pooled > 0.f ? acc[rr] : 0.f;
+          const int am = am1s[c * 196 + p];
+          const int yy = 2 * py + (am >> 1), xx = 2 * px + (am & 1);
+          dY1[c * 896 + yy * 32 + xx] = (bf16)g;
+          csum += g;
+        }
       }
+      atomicAdd(&db[16 + c], csum);
     }
   }
   __syncthreads();
-  for (int e = tid; e < C1 * 75; e += NT) {
-    const int o = e / 75, kk = e - o * 75;
-    slab[P_C1W + e] = dW1acc[o * 80 + kk];
+  FEDMI_STAMP(2, 3);
+
+  // ---- conv1 wgrad: dW1[o][k'] = sum_p dY1[o][p] * im2col(x)[p][k']
+  //      M = 16 (o < 6), N = 75 (5 tiles: one per wave 0..4), K = 896 (p' = i*32 + j,
+  //      28 steps = conv1 output rows); each wave owns its tile: no cross-wave combine.
+  if (wave < 5) {
+    const int kk = wave * 16 + n16;
+    const int kc = kk < 75 ? kk : 0;
+    const int c = kc / 25, rs = kc - c * 25, r = rs / 5, sc = rs - r * 5;
+    const bf16* bb = xsh + ((sc * 3 + c) * 32 + r) * 32 + kq;
+    const bf16* ab = dY1 + min(n16, C1 - 1) * 896 + kq;
+    const bool arow = n16 < C1;
+    f32x4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll 2
+    for (int ks = 0; ks < O1; ks += 2) {
+      bf16x8 a0 = ld8(ab + ks * 32), a1 = ld8(ab + ks * 32 + 32);
+      if (!arow) { a0 = zero8(); a1 = zero8(); }
+      acc0 = mfma16(a0, ld8(bb + ks * 32), acc0);
+      acc1 = mfma16(a1, ld8(bb + ks * 32 + 32), acc1);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int o = rq + rr;
+      if (o < C1 && kk < 75) slab[P_C1W + o * 75 + kk] = acc0[rr] + acc1[rr];
+    }
   }
+  FEDMI_STAMP(2, 4);
   if (tid < C1) slab[P_C1B + tid] = db[16 + tid];
   if (tid < C2) slab[P_C2B + tid] = db[tid];
+  FEDMI_STAMP(2, 5);
 }
-
 // ---------------------------------------------------------------------------
 // Packing: fp32 master -> bf16 MFMA operand images.
 // ---------------------------------------------------------------------------
@@ -719,11 +797,10 @@ constexpr int SGD_NA = (CS + 15) / 16;           // 180
 constexpr int SGD_NB = (F1W_N + 255) / 256;      // 188
 constexpr int SGD_NC = (FS + 255) / 256;         // 44
 
-FEDMI_DEV void sgd_update(int i, float grad, float* __restrict__ params, float* __restrict__ mom,
-                          bf16* __restrict__ pk, float lr, float momentum, float wd) {
-  const float p = params[i];
+FEDMI_DEV void sgd_apply(int i, float grad, float p, float m, float* __restrict__ params, float* __restrict__ mom,
+                         bf16* __restrict__ pk, float lr, float momentum, float wd) {
   const float d = grad + wd * p;
-  const float b = momentum * mom[i] + d;
+  const float b = momentum * m + d;
   const float np = p - lr * b;
   mom[i] = b;
   params[i] = np;
@@ -739,9 +816,12 @@ __global__ __launch_bounds__(256) void lenet_sgd(
 {
   __shared__ float red[16][17];
   const int b = blockIdx.x, tid = threadIdx.x;
+  FEDMI_STAMP(3, 0);
   if (b < SGD_NA) {
     const int pl = tid & 15, g = tid >> 4;
     const int i = b * 16 + pl;
+    float p = 0.f, m = 0.f;
+    if (g == 0 && i < CS) { p = params[i]; m = mom[i]; }      // issued before the slab sweep
     float sum = 0.f;
     if (i < CS)
       for (int q = g; q < n_conv; q += 16) sum += conv_slab[(size_t)q * CS + i];
@@ -751,20 +831,26 @@ __global__ __launch_bounds__(256) void lenet_sgd(
       float tot = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) tot += red[q][pl];
-      sgd_update(i, tot, params, mom, pk, lr, momentum, wd);
+      sgd_apply(i, tot, p, m, params, mom, pk, lr, momentum, wd);
     }
   } else if (b < SGD_NA + SGD_NB) {
     const int j = (b - SGD_NA) * 256 + tid;
-    if (j < F1W_N) sgd_update(P_F1W + j, fc1w_grad[j], params, mom, pk, lr, momentum, wd);
+    if (j < F1W_N) {
+      const int i = P_F1W + j;
+      sgd_apply(i, fc1w_grad[j], params[i], mom[i], params, mom, pk, lr, momentum, wd);
+    }
   } else {
     const int j = (b - SGD_NA - SGD_NB) * 256 + tid;
     if (j < FS) {
+      const int i = P_F1B + j;
+      const float p = params[i], m = mom[i];
       float sum = 0.f;
       for (int q = 0; q < n_fc; ++q) sum += fc_slab[(size_t)q * FS + j];
-      sgd_update(P_F1B + j, sum, params, mom, pk, lr, momentum, wd);
+      sgd_apply(i, sum, p, m, params, mom, pk, lr, momentum, wd);
     }
   }
   if (round_ctr && b == 0 && tid == 0) atomicAdd(round_ctr, 1);
+  FEDMI_STAMP(3, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -782,22 +868,21 @@ void launch_lenet_conv_fwd(hipStream_t st, const uint8_t* images, int sample_bas
 }
 
 void launch_lenet_fc_head(hipStream_t st, const bf16* act2, const int* labels, int nb, int train,
-                          const bf16* pk, const float* params, bf16* dZ1, bf16* dZ1T, float* fc_slab,
+                          const bf16* pk, const float* params, float* dact2, bf16* dZ1T, float* fc_slab,
                           Stats* stats) {
   if (nb <= 0) return;
   const int grid = (nb + FC_SPW - 1) / FC_SPW;
   hipLaunchKernelGGL(lenet_fc_head, dim3(grid), dim3(NT), 0, st, act2, labels, nb, train, pk, params,
-                     dZ1, dZ1T, fc_slab, stats);
+                     dact2, dZ1T, fc_slab, stats);
 }
 
 void launch_lenet_conv_bwd(hipStream_t st, const uint8_t* images, int sample_base, int nb,
-                           uint32_t seed, const int* round_ctr, int augment, const bf16* act2,
-                           const bf16* act2T, const bf16* dZ1, const bf16* dZ1T, const bf16* pool1,
-                           const uint8_t* am1, const uint8_t* am2, const bf16* pk, float* conv_slab,
-                           float* fc1w_grad) {
+                           uint32_t seed, const int* round_ctr, int augment, const float* dact2,
+                           const bf16* act2T, const bf16* dZ1T, const bf16* pool1, const uint8_t* am1,
+                           const uint8_t* am2, const bf16* pk, float* conv_slab, float* fc1w_grad) {
   if (nb <= 0) return;
   hipLaunchKernelGGL(lenet_conv_bwd, dim3(nb + N_DW1_WG), dim3(NT), 0, st, images, sample_base, nb, seed,
-                     round_ctr, augment, act2, act2T, dZ1, dZ1T, pool1, am1, am2, pk, conv_slab, fc1w_grad);
+                     round_ctr, augment, dact2, act2T, dZ1T, pool1, am1, am2, pk, conv_slab, fc1w_grad);
 }
 
 void launch_lenet_sgd(hipStream_t st, float* params, float* mom, bf16* pk, const float* conv_slab,
@@ -805,6 +890,28 @@ void launch_lenet_sgd(hipStream_t st, float* params, float* mom, bf16* pk, const
                       float momentum, float wd, int* round_ctr) {
   hipLaunchKernelGGL(lenet_sgd, dim3(SGD_NA + SGD_NB + SGD_NC), dim3(256), 0, st, params, mom, pk,
                      conv_slab, n_conv, fc1w_grad, fc_slab, n_fc, lr, momentum, wd, round_ctr);
+}
+
+bool stamps_enabled() {
+#ifdef FEDMI_STAMPS
+  return true;
+#else
+  return false;
+#endif
+}
+
+// Copy (and optionally clear) the per-phase s_memtime stamps of the diagnostic build.
+void read_stamps(unsigned long long* host, bool clear) {
+#ifdef FEDMI_STAMPS
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(fedmi_stamps), sizeof(fedmi_stamps), 0, hipMemcpyDeviceToHost);
+  if (clear) {
+    static unsigned long long zeros[FEDMI_STAMP_KERNELS][FEDMI_STAMP_WGS][FEDMI_STAMP_SLOTS];
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(fedmi_stamps), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
+  }
+#else
+  (void)host;
+  (void)clear;
+#endif
 }
 
 void launch_lenet_pack(hipStream_t st, const float* params, bf16* pk) {

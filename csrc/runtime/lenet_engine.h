@@ -27,7 +27,7 @@ struct LeNetBuffers {
   bf16* pool1 = nullptr;         // [MAX_TRAIN_BATCH][NP1]
   uint8_t* am1 = nullptr;        // [MAX_TRAIN_BATCH][NP1]
   uint8_t* am2 = nullptr;        // [MAX_TRAIN_BATCH][F0]
-  bf16* dZ1 = nullptr;           // [MAX_TRAIN_BATCH][DZ1_LD]
+  float* dact2 = nullptr;        // [MAX_TRAIN_BATCH][F0]  d(pool2) from the FC head
   bf16* dZ1T = nullptr;          // [DZ1_LD][MAX_TRAIN_BATCH]
   float* conv_slab = nullptr;    // [MAX_TRAIN_BATCH][CS]
   float* fc1w_grad = nullptr;    // [F1W_N]

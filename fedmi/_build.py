@@ -34,9 +34,13 @@ SOURCES = [
 HEADERS = sorted(CSRC.rglob("*.h"))
 
 
-def ext_path() -> Path:
+VARIANTS = {"": [], "stamps": ["-DFEDMI_STAMPS"]}
+
+
+def ext_path(variant: str = "") -> Path:
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    return PKG / f"_fedmi_native{suffix}"
+    name = "_fedmi_native" + (f"_{variant}" if variant else "")
+    return PKG / f"{name}{suffix}"
 
 
 def _hipcc() -> str:
@@ -46,21 +50,24 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build fedmi native code)")
 
 
-def _stamp() -> str:
+def _stamp(variant: str = "") -> str:
     h = hashlib.sha256()
     h.update(ARCH.encode())
+    h.update(variant.encode())
     for p in SOURCES + HEADERS + [Path(__file__)]:
         h.update(p.name.encode())
         h.update(p.read_bytes())
     return h.hexdigest()
 
 
-def _compile(src: Path) -> Path:
+def _compile(src: Path, variant: str = "") -> Path:
     import pybind11
 
-    obj = BUILD / (src.stem + ".o")
+    bdir = BUILD.with_name(BUILD.name + (f"_{variant}" if variant else ""))
+    bdir.mkdir(parents=True, exist_ok=True)
+    obj = bdir / (src.stem + ".o")
     cmd = [
-        _hipcc(), "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
+        _hipcc(), "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", *VARIANTS[variant],
         "-Wno-unused-result", "-I", str(CSRC),
         "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"],
         "-c", str(src), "-o", str(obj),
@@ -73,17 +80,18 @@ def _compile(src: Path) -> Path:
     return obj
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
-    out = ext_path()
-    stamp_file = BUILD / "stamp"
-    stamp = _stamp()
+def build(force: bool = False, jobs: int = 4, verbose: bool = True, variant: str = "") -> Path:
+    out = ext_path(variant)
+    bdir = BUILD.with_name(BUILD.name + (f"_{variant}" if variant else ""))
+    stamp_file = bdir / "stamp"
+    stamp = _stamp(variant)
     if not force and out.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
         if verbose:
             print(f"[fedmi build] up to date: {out.name}")
         return out
-    BUILD.mkdir(parents=True, exist_ok=True)
+    bdir.mkdir(parents=True, exist_ok=True)
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(_compile, SOURCES))
+        objs = list(ex.map(lambda src: _compile(src, variant), SOURCES))
     tmp = out.with_suffix(".tmp.so")
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp)]
     proc = subprocess.run(cmd, capture_output=True, text=True)
@@ -100,8 +108,11 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--stamps", action="store_true", help="also build the per-phase timestamp diagnostic variant")
     a = ap.parse_args(argv)
     build(force=a.force, jobs=a.jobs)
+    if a.stamps:
+        build(force=a.force, jobs=a.jobs, variant="stamps")
     return 0
 
 

@@ -156,9 +156,10 @@ def _synthetic_images(n: int, shape, n_classes: int, seed: int, device, split: i
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
         noise = torch.randn(e - s, c, h, w, generator=gd, device=device) * 0.3
-        # contrast/noise chosen so the reference recipe (SGD lr 0.1, m 0.9) trains LeNet stably
-        # to a CIFAR-like ~60 % (fp32 torch: loss 1.6 after 6 epochs) instead of diverging
-        img = templates[labels_d[s:e]] * 0.15 + 0.425 + noise
+        # contrast/noise chosen so the reference recipe (SGD lr 0.1, m 0.9, no BN) trains
+        # LeNet stably for 24+ epochs (fp32 torch: ~50 % test acc, loss ~1.77); higher
+        # contrast makes that recipe diverge to a dead network after ~12 epochs
+        img = templates[labels_d[s:e]] * 0.12 + 0.44 + noise
         out[s:e] = (img.clamp_(0, 1) * 255.0).round_().to(torch.uint8)
     return ImageSet(out, labels_d.to(torch.int32))
 

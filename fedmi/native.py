@@ -23,8 +23,10 @@ def _load():
     with _lock:
         if _mod is not None or _err is not None:
             return
+        variant = os.environ.get("FEDMI_NATIVE_VARIANT", "")
+        name = "fedmi._fedmi_native" + (f"_{variant}" if variant else "")
         try:
-            _mod = importlib.import_module("fedmi._fedmi_native")
+            _mod = importlib.import_module(name)
         except Exception as e:  # pragma: no cover - depends on build state
             _err = e
 

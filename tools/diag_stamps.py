@@ -1,0 +1,58 @@
+"""Per-phase cycle breakdown of the fused LeNet step (diagnostic stamps build).
+
+Run with FEDMI_NATIVE_VARIANT=stamps (the -DFEDMI_STAMPS extension).  Executes a
+few warm-up steps, then one eager step of 128 samples, and prints, per kernel,
+the median (and max) cycles each workgroup spent in every phase, plus the
+spread of workgroup start times.
+"""
+import os
+import sys
+from pathlib import Path
+
+os.environ.setdefault("FEDMI_NATIVE_VARIANT", "stamps")
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from fedmi import native  # noqa: E402
+from fedmi.engine.base import TrainerConfig  # noqa: E402
+from fedmi.engine.data import make_dataset  # noqa: E402
+from fedmi.engine.lenet_native import LeNetNativeTrainer  # noqa: E402
+
+NAMES = {
+    0: ("conv_fwd", ["stage+aug", "conv1", "pool1", "conv2", "pool2+store"]),
+    1: ("fc_head", ["prefetch+fc1", "fc2+fc3", "CE", "dW3/dH2", "dW2/dH1", "dX+slab"]),
+    2: ("conv_bwd", ["stage", "shift+scatter", "c2 wgrad+dgrad", "c1 wgrad", "slab store"]),
+    3: ("sgd", ["all"]),
+}
+NWG = {0: 128, 1: 8, 2: 128, 3: 412}
+
+
+def main():
+    nat = native.require()
+    assert nat.stamps_enabled(), "not the stamps build"
+    dev = torch.device("cuda", 0)
+    ds = make_dataset("synthetic-cifar10", device=dev, n_train=4096, n_test=1024)
+    tr = LeNetNativeTrainer(ds, dev, TrainerConfig(seed=1))
+    for i in range(8):
+        tr.train_step(128 * i, 128)
+    torch.cuda.synchronize()
+    nat.read_stamps(True)
+    tr.train_step(0, 128)
+    torch.cuda.synchronize()
+    st = np.frombuffer(nat.read_stamps(True), dtype=np.uint64).reshape(nat.STAMP_SHAPE).astype(np.int64)
+    for k, (name, phases) in NAMES.items():
+        a = st[k, :NWG[k], :len(phases) + 1]
+        a = a[a[:, 0] > 0]
+        d = np.diff(a, axis=1)
+        tot = a[:, -1] - a[:, 0]
+        starts = a[:, 0] - a[:, 0].min()
+        print(f"{name:9s} wgs={len(a):4d} total med {np.median(tot):8.0f} max {tot.max():8.0f} cyc | "
+              f"start spread {starts.max():7d} cyc")
+        for j, ph in enumerate(phases):
+            print(f"    {ph:16s} med {np.median(d[:, j]):8.0f}  max {d[:, j].max():8.0f}")
+
+
+if __name__ == "__main__":
+    main()

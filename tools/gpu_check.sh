@@ -18,6 +18,8 @@ for st in $STAGES; do
            echo "bench rc=$rc" >> gpurun_out/summary.txt; tail -3 gpurun_out/bench.log >> gpurun_out/summary.txt; ok_or_stop $rc ;;
     diag)  timeout -k 10 400 python tools/diag_convergence.py ${DIAG_EPOCHS:-4} > gpurun_out/diag.log 2>&1; rc=$?
            echo "diag rc=$rc" >> gpurun_out/summary.txt; tail -6 gpurun_out/diag.log >> gpurun_out/summary.txt; ok_or_stop $rc ;;
+    stamps) timeout -k 10 300 env FEDMI_NATIVE_VARIANT=stamps python tools/diag_stamps.py > gpurun_out/stamps.log 2>&1; rc=$?
+           echo "stamps rc=$rc" >> gpurun_out/summary.txt; cat gpurun_out/stamps.log >> gpurun_out/summary.txt; ok_or_stop $rc ;;
     prof)  (cd /tmp && export TMPDIR=/tmp && true); export TMPDIR=/tmp
            timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 > gpurun_out/prof.log 2>&1; rc=$?
            echo "prof rc=$rc" >> gpurun_out/summary.txt; ok_or_stop $rc ;;
