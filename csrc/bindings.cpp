@@ -19,8 +19,9 @@ namespace py = pybind11;
 namespace fedmi {
 void launch_lenet_conv_fwd(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*, int,
                            bf16*, bf16*, int, bf16*, uint8_t*, uint8_t*, lenet::Stats*);
-void launch_lenet_fc_head(hipStream_t, const bf16*, const int*, int, int, const bf16*, const float*, float*, bf16*,
-                          float*, lenet::Stats*);
+void launch_lenet_fc1_fwd(hipStream_t, const bf16*, int, const bf16*, const float*, bf16*);
+void launch_lenet_fc_tail(hipStream_t, const bf16*, const bf16*, const int*, int, int, const bf16*, const float*, float*,
+                          bf16*, float*, lenet::Stats*);
 void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const float*, const bf16*,
                            const bf16*, const bf16*, const uint8_t*, const uint8_t*, const bf16*, float*, float*);
 bool stamps_enabled();
@@ -61,6 +62,7 @@ static LeNetBuffers buffers_from(const py::dict& d) {
   b.act2 = P<bf16>(get("act2"));
   b.act2_rows = d.contains("act2_rows") ? d["act2_rows"].cast<int>() : 0;
   b.act2T = P<bf16>(get("act2T"));
+  b.h1 = P<bf16>(get("h1"));
   b.pool1 = P<bf16>(get("pool1"));
   b.am1 = P<uint8_t>(get("am1"));
   b.am2 = P<uint8_t>(get("am2"));
@@ -139,11 +141,14 @@ static void fedmi_bind(py::module_& m) {
                           P<uint8_t>(am1), P<uint8_t>(am2), P<lenet::Stats>(zero_stats));
     check_last("lenet_conv_fwd");
   });
+  // FC head = fc1 forward (tiled) + FC tail; kept as one entry point for the tests
   m.def("lenet_fc_head", [](uintptr_t st, uintptr_t act2, uintptr_t labels, int nb, int train, uintptr_t pk,
-                            uintptr_t params, uintptr_t dact2, uintptr_t dZ1T, uintptr_t fc_slab, uintptr_t stats) {
-    launch_lenet_fc_head(S(st), P<const bf16>(act2), P<const int>(labels), nb, train, P<const bf16>(pk),
-                         P<const float>(params), P<float>(dact2), P<bf16>(dZ1T), P<float>(fc_slab),
-                         P<lenet::Stats>(stats));
+                            uintptr_t params, uintptr_t h1, uintptr_t dact2, uintptr_t dZ1T, uintptr_t fc_slab,
+                            uintptr_t stats) {
+    launch_lenet_fc1_fwd(S(st), P<const bf16>(act2), nb, P<const bf16>(pk), P<const float>(params), P<bf16>(h1));
+    launch_lenet_fc_tail(S(st), P<const bf16>(h1), P<const bf16>(act2), P<const int>(labels), nb, train,
+                         P<const bf16>(pk), P<const float>(params), P<float>(dact2), P<bf16>(dZ1T),
+                         P<float>(fc_slab), P<lenet::Stats>(stats));
     check_last("lenet_fc_head");
   });
   m.def("lenet_conv_bwd", [](uintptr_t st, uintptr_t images, int base, int nb, uint32_t seed, uintptr_t round_ctr,

@@ -1,7 +1,7 @@
 // fedmi — fused LeNet training/eval kernels for MI355X (gfx950, CDNA4).
 //
 // One local SGD step of the reference (src/main.py:146-151: zero_grad,
-// forward, CE loss, backward, SGD(m=0.9, wd=5e-4)) is FOUR launches:
+// forward, CE loss, backward, SGD(m=0.9, wd=5e-4)) is FIVE launches:
 //
 //   K1 lenet_conv_fwd   one 8-wave workgroup per sample: uint8 image ->
 //                       on-device RandomCrop(32,pad4)+HFlip+Normalize
@@ -9,12 +9,14 @@
 //                       image: one 16-B read per operand fragment) +bias+ReLU
 //                       -> maxpool2 -> conv2 (MFMA) +bias+ReLU -> maxpool2.
 //                       Saves pooled activations + 2-bit argmax codes.
-//   K2 lenet_fc_head    16 samples (one MFMA row tile) per workgroup: fc1/fc2/
-//                       fc3 forward, cross-entropy + accuracy counters, FC
-//                       backward down to dZ1 (fc2/fc3 wgrad + bias grads).
-//                       Also the eval head (train=0).
-//   K3 lenet_conv_bwd   one workgroup per sample: d(pool2) = dZ1.W1 (MFMA),
-//                       maxpool/ReLU backward by argmax, conv2 wgrad + dgrad,
+//   K2a lenet_fc1_fwd   fc1 forward tiled 16 samples x 16 outputs (the fc1
+//                       weight image is streamed by 8 column workgroups).
+//   K2b lenet_fc_tail   16 samples per row group: fc2/fc3 forward, cross-
+//                       entropy + accuracy counters, FC backward (fc2/fc3 wgrad,
+//                       bias grads, dZ1) and dX = dZ1.W1 split 4 ways over
+//                       workgroups.  Also the eval head (train=0).
+//   K3 lenet_conv_bwd   one workgroup per sample: maxpool/ReLU backward by
+//                       argmax, conv2 wgrad + dgrad,
 //                       conv1 wgrad (MFMA; the im2col operands come from
 //                       5 column-shifted LDS copies so every fragment is one
 //                       aligned 16-B read).  25 extra workgroups of the same
@@ -236,27 +238,75 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
 }
 
 // ---------------------------------------------------------------------------
-// K2: FC head, 16 samples per workgroup (one MFMA row tile), 8 waves.
-//   fwd: H1 = relu(X W1^T + b1), H2 = relu(H1 W2^T + b2), Z = H2 W3^T + b3
-//   CE:  loss/acc counters; dZ = (softmax - onehot) / nb  (mean reduction)
-//   bwd: dW3/db3, dH2, dW2/db2, dH1 -> dZ1 (+db1), dX = dZ1 W1 (masked by the
-//        pool2 ReLU) -> d(pool2) for K3; dZ1^T to global for the fc1 wgrad.
-// Every global operand is prefetched into registers at kernel entry or right
-// after fc1 so no phase waits on a cold L2/HBM round trip.  Wgrad GEMMs
-// reduce over samples (K = 32, samples 16..31 zero), so activations are also
-// kept sample-contiguous ("T" images) in LDS.
+// K2a: fc1 forward, tiled over (16-sample row tile) x (16-output column tile)
+// so the 106 KB fc1 weight image is streamed by 8 column workgroups instead of
+// every row-group workgroup (per-CU bandwidth, not FLOPs, bounds this GEMM).
+// 4 waves split K = 416 (13 steps) and combine through LDS.
+//   H1[s][n] = relu(X[s] . W1[n] + b1[n])   -> global bf16 [rows][128]
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void lenet_fc_head(
+__global__ __launch_bounds__(256) void lenet_fc1_fwd(
     const bf16* __restrict__ act2,   // [nb][F0P]
+    int nb, const bf16* __restrict__ pk, const float* __restrict__ params,
+    bf16* __restrict__ h1)           // [nb rounded to 16][128]
+{
+  __shared__ float red[4][16][17];
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
+  const int nt = blockIdx.x & 7, mt = blockIdx.x >> 3;
+  const int row = mt * 16 + n16;
+  const bool valid = row < nb;
+  const bf16* xa = act2 + (size_t)(valid ? row : 0) * F0P + kq;
+  const bf16* wb = pk + PK_FC1 + (nt * 16 + n16) * F0P + kq;
+  bf16x8 a[4], b[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {                 // k-steps wave, wave+4, wave+8, wave+12 (<13)
+    const int ks = min(wave + 4 * j, 12);
+    a[j] = ld8(xa + ks * 32);
+    b[j] = ld8(wb + ks * 32);
+  }
+  const int n = nt * 16 + (threadIdx.x & 15);
+  const float bias = params[P_F1B + min(n, F1 - 1)];
+  if (!valid) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = zero8();
+  }
+  f32x4 acc = zero4();
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (wave + 4 * j < 13) acc = mfma16(a[j], b[j], acc);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][rq + r][n16] = acc[r];
+  __syncthreads();
+  const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
+  const int srow = mt * 16 + r;
+  if (srow < nb) {
+    const float v = red[0][r][c] + red[1][r][c] + red[2][r][c] + red[3][r][c] + bias;
+    h1[(size_t)srow * 128 + n] = (bf16)((n < F1) ? fmaxf(v, 0.f) : 0.f);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K2b: FC tail, 16 samples per row group, 8 waves; in training each row group
+// is split over 4 workgroups that each produce a quarter of dX = dZ1 . W1
+// (the 100 KB fc1^T image is streamed 4-way in parallel).  The cheap middle of
+// the head (fc2, fc3, CE, fc3/fc2 backward, dZ1) is recomputed by the 4
+// workgroups; only quarter 0 publishes stats, slabs and dZ1^T.
+//   fwd: H2 = relu(H1 W2^T + b2), Z = H2 W3^T + b3; CE + accuracy counters
+//   bwd: dW3/db3, dZ2, dW2/db2, dZ1 (+db1) -> dZ1^T (global), dX (masked by the
+//        pool2 ReLU) -> d(pool2) for K3.
+// Every global operand is prefetched into registers at entry.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void lenet_fc_tail(
+    const bf16* __restrict__ h1,     // [nb][128]  relu(fc1) from K2a
+    const bf16* __restrict__ act2,   // [nb][F0P]  (for the dX mask)
     const int* __restrict__ labels,  // labels of this batch (already offset)
     int nb, int train,
     const bf16* __restrict__ pk, const float* __restrict__ params,
     float* __restrict__ dact2,       // [128][F0]       (train)
     bf16* __restrict__ dZ1T,         // [128][DZ1_LD]   (train)
-    float* __restrict__ fc_slab,     // [grid][FS]      (train)
+    float* __restrict__ fc_slab,     // [row groups][FS] (train)
     Stats* __restrict__ stats)
 {
-  __shared__ __attribute__((aligned(16))) bf16 sX[16 * F0P];
   __shared__ __attribute__((aligned(16))) bf16 sH1[16 * 128], sH1T[128 * 32];
   __shared__ __attribute__((aligned(16))) bf16 sH2[16 * 96], sH2T[96 * 32];
   __shared__ __attribute__((aligned(16))) bf16 sdZ3[16 * 32], sdZ3T[16 * 32];
@@ -267,38 +317,45 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
 
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
   const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
-  const int s0 = blockIdx.x * FC_SPW;
+  const int nq = train ? 4 : 1;
+  const int mt = blockIdx.x / nq, q = blockIdx.x - mt * nq;
+  const int s0 = mt * FC_SPW;
   const int ns = min(FC_SPW, nb - s0);
   if (ns <= 0) return;
+  const bool lead = q == 0;                        // publishes stats, slabs and dZ1^T
   FEDMI_STAMP(1, 0);
 
-  // ---- prefetch fc1 operands (13 k-steps) and the fc2/fc3 forward weights
-  // All loads are unconditional with clamped addresses (a per-load select on a
-  // runtime condition makes hipcc branch around each load and wait vmcnt(0)).
-  const bool valid = n16 < ns;
-  bf16x8 af[13], bfr[13];
-  {
-    const bf16* xa = act2 + (size_t)(s0 + (valid ? n16 : 0)) * F0P + kq;
-    const bf16* wb = pk + PK_FC1 + (wave * 16 + n16) * F0P + kq;
-#pragma unroll
-    for (int ks = 0; ks < 13; ++ks) {
-      af[ks] = ld8(xa + ks * 32);
-      bfr[ks] = ld8(wb + ks * 32);
-    }
+  // ---- prefetch: H1 tile, fc2/fc3 weights + biases, backward weights, dX tile + mask
+  uint4 h1v = make_uint4(0, 0, 0, 0);
+  if (tid < 16 * 128 / 8) {
+    const int r = tid >> 4;
+    h1v = reinterpret_cast<const uint4*>(h1 + (size_t)(s0 + min(r, ns - 1)) * 128)[tid & 15];
+    if (r >= ns) h1v = make_uint4(0, 0, 0, 0);
   }
-  bf16x8 w2f[4], w3f[3];
   const int nf1 = wave * 16 + n16;
   const int nf2 = (wave < 6 ? wave : 0) * 16 + n16;
-  const float b1 = params[P_F1B + min(nf1, F1 - 1)];
   const float b2 = params[P_F2B + min(nf2, F2 - 1)];
   const float b3 = params[P_F3B + min(n16, NCLS - 1)];
+  bf16x8 w2f[4], w3f[3];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) w2f[ks] = ld8(pk + PK_FC2 + nf2 * 128 + ks * 32 + kq);
 #pragma unroll
   for (int ks = 0; ks < 3; ++ks) w3f[ks] = ld8(pk + PK_FC3 + n16 * 96 + ks * 32 + kq);
-  if (!valid) {
+  const int q5 = wave >= 6 ? wave : wave + 8;      // this wave's dH2 task (valid if < 12)
+  // dX tiles of this quarter: 25 tiles split 7/6/6/6
+  const int t0 = q == 0 ? 0 : 7 + 6 * (q - 1), t1 = q == 0 ? 7 : t0 + 6;
+  const int tx = t0 + wave;                        // this wave's dX tile (valid if < t1)
+  const int fx = min(tx, F0 / 16 - 1) * 16 + n16;
+  bf16x8 w3t, w2t[3], wxt[4];
+  float xm[4];
+  if (train) {
+    w3t = ld8(pk + PK_FC3T + ((min(q5, 11) - 6) * 16 + n16) * 32 + kq);
 #pragma unroll
-    for (int ks = 0; ks < 13; ++ks) af[ks] = zero8();
+    for (int ks = 0; ks < 3; ++ks) w2t[ks] = ld8(pk + PK_FC2T + nf1 * 96 + ks * 32 + kq);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) wxt[ks] = ld8(pk + PK_FC1T + fx * 128 + ks * 32 + kq);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xm[r] = (float)act2[(size_t)(s0 + min(rq + r, ns - 1)) * F0P + fx];
   }
 
   zero_lds(sH1T, sizeof(sH1T));
@@ -307,38 +364,12 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
   zero_lds(sdZ3T, sizeof(sdZ3T));
   zero_lds(sdZ2T, sizeof(sdZ2T));
   for (int e = tid; e < 240; e += NT) sdb[e] = 0.f;
-
-  // ---- fc1 fwd: wave w -> outputs [16w, 16w+16); K = 416 (13 steps)
-  f32x4 acc1 = zero4();
-#pragma unroll
-  for (int ks = 0; ks < 13; ++ks) acc1 = mfma16(af[ks], bfr[ks], acc1);
-  if (wave == 0) {   // keep X (this tile's act2 rows) for the dX ReLU mask
-#pragma unroll
-    for (int ks = 0; ks < 13; ++ks) *reinterpret_cast<bf16x8*>(sX + n16 * F0P + ks * 32 + kq) = af[ks];
-  }
-  // backward weights: dH2 task (q in {w, w+8} intersect [6,12)), dH1 tile w, dX tiles w + 8j
-  bf16x8 w3t, w2t[3], wxt[4][4];
-  const int q5 = wave >= 6 ? wave : wave + 8;          // this wave's dH2 task (valid if < 12)
-  if (train) {
-    w3t = ld8(pk + PK_FC3T + ((min(q5, 11) - 6) * 16 + n16) * 32 + kq);
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks) w2t[ks] = ld8(pk + PK_FC2T + nf1 * 96 + ks * 32 + kq);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = min(wave + 8 * j, F0 / 16 - 1);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) wxt[j][ks] = ld8(pk + PK_FC1T + (t * 16 + n16) * 128 + ks * 32 + kq);
-    }
-  }
-  __syncthreads();   // T images zeroed (and sX written) before use
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int sr = rq + r;
-    const float hv = (nf1 < F1 && sr < ns) ? fmaxf(acc1[r] + b1, 0.f) : 0.f;
-    sH1[sr * 128 + nf1] = (bf16)hv;
-    sH1T[nf1 * 32 + sr] = (bf16)hv;
-  }
+  if (tid < 16 * 128 / 8) reinterpret_cast<uint4*>(sH1)[tid] = h1v;
   __syncthreads();
+  for (int e = tid; e < 16 * 128; e += NT) {       // sample-contiguous copy for the dW2 GEMM
+    const int r = e >> 7, c = e & 127;
+    sH1T[c * 32 + r] = sH1[e];
+  }
   FEDMI_STAMP(1, 1);
 
   // ---- fc2 fwd: waves 0..5 -> 16 outputs each; K = 128 (4 steps)
@@ -350,9 +381,9 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int sr = rq + r;
-      const float hv = (nf1 < F2 && sr < ns) ? fmaxf(acc[r] + b2, 0.f) : 0.f;
-      sH2[sr * 96 + nf1] = (bf16)hv;
-      sH2T[nf1 * 32 + sr] = (bf16)hv;
+      const float hv = (nf2 < F2 && sr < ns) ? fmaxf(acc[r] + b2, 0.f) : 0.f;
+      sH2[sr * 96 + nf2] = (bf16)hv;
+      sH2T[nf2 * 32 + sr] = (bf16)hv;
     }
   }
   __syncthreads();
@@ -411,7 +442,7 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
     }
     loss = wave_sum(loss);
     corr = wave_sum(corr);
-    if (lane == 0) {
+    if (lane == 0 && lead) {
       atomicAdd(&stats->loss_sum, loss);
       atomicAdd(&stats->correct, (int)(corr + 0.5f));
       atomicAdd(&stats->count, ns);
@@ -421,19 +452,20 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
   __syncthreads();
   FEDMI_STAMP(1, 3);
 
-  float* slab = fc_slab + (size_t)blockIdx.x * FS;
+  float* slab = fc_slab + (size_t)mt * FS;
   constexpr int OF3W = P_F3W - P_F1B, OF2W = P_F2W - P_F1B;
 
-  if (tid < NCLS) {   // db3
+  if (tid < NCLS && lead) {   // db3
     float acc = 0.f;
     for (int sr = 0; sr < 16; ++sr) acc += sZ[sr * 16 + tid];
     sdb[224 + tid] = acc;
   }
 
-  // ---- dW3 (tasks 0..5) and dH2 = dZ3 . W3 (tasks 6..11)
-  for (int q = wave; q < 12; q += NW) {
-    if (q < 6) {
-      const int ft = q;
+  // ---- dW3 (tasks 0..5, lead only) and dH2 = dZ3 . W3 (tasks 6..11)
+  for (int qq = wave; qq < 12; qq += NW) {
+    if (qq < 6) {
+      if (!lead) continue;
+      const int ft = qq;
       const f32x4 acc = mfma16(ld8(sdZ3T + n16 * 32 + kq), ld8(sH2T + (ft * 16 + n16) * 32 + kq), zero4());
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -441,7 +473,7 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
         if (n < NCLS && f < F2) slab[OF3W + n * F2 + f] = acc[r];
       }
     } else {
-      const int f = (q - 6) * 16 + n16;
+      const int f = (qq - 6) * 16 + n16;
       const f32x4 acc = mfma16(ld8(sdZ3 + n16 * 32 + kq), w3t, zero4());
       float colsum = 0.f;
 #pragma unroll
@@ -460,14 +492,16 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
   __syncthreads();
   FEDMI_STAMP(1, 4);
 
-  // ---- dW2 = dZ2^T H1 (48 tiles) and dH1 = dZ2 . W2 (tile = wave) -> dZ1
-  for (int q = wave; q < 48; q += NW) {
-    const int mt = q >> 3, ft = q & 7;
-    const f32x4 acc = mfma16(ld8(sdZ2T + (mt * 16 + n16) * 32 + kq), ld8(sH1T + (ft * 16 + n16) * 32 + kq), zero4());
+  // ---- dW2 = dZ2^T H1 (48 tiles, lead only) and dH1 = dZ2 . W2 (tile = wave) -> dZ1
+  if (lead) {
+    for (int qq = wave; qq < 48; qq += NW) {
+      const int mt2 = qq >> 3, ft = qq & 7;
+      const f32x4 acc = mfma16(ld8(sdZ2T + (mt2 * 16 + n16) * 32 + kq), ld8(sH1T + (ft * 16 + n16) * 32 + kq), zero4());
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = mt * 16 + rq + r, f = ft * 16 + n16;
-      if (n < F2 && f < F1) slab[OF2W + n * F1 + f] = acc[r];
+      for (int r = 0; r < 4; ++r) {
+        const int n = mt2 * 16 + rq + r, f = ft * 16 + n16;
+        if (n < F2 && f < F1) slab[OF2W + n * F1 + f] = acc[r];
+      }
     }
   }
   {
@@ -483,7 +517,7 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
       const float g = (f < F1 && (float)sH1[sr * 128 + f] > 0.f) ? acc[r] : 0.f;
       const bf16 gb = (bf16)g;
       sdZ1[sr * 128 + f] = gb;
-      dZ1T[(size_t)f * DZ1_LD + s0 + sr] = gb;
+      if (lead) dZ1T[(size_t)f * DZ1_LD + s0 + sr] = gb;
       colsum += g;
     }
     colsum += __shfl_xor(colsum, 16, 64);
@@ -493,37 +527,33 @@ __global__ __launch_bounds__(NT) void lenet_fc_head(
   __syncthreads();
   FEDMI_STAMP(1, 5);
 
-  // ---- dX = dZ1 . W1 (25 tiles, K = 128), masked by the pool2 ReLU -> d(pool2)
+  // ---- dX = dZ1 . W1 for this quarter's tiles (K = 128), masked by the pool2 ReLU
+  if (tx < t1) {
+    const bf16* za = sdZ1 + n16 * 128 + kq;
+    f32x4 acc = zero4();
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int t = wave + 8 * j;
-    if (t < F0 / 16) {
-      const int f = t * 16 + n16;
-      const bf16* za = sdZ1 + n16 * 128 + kq;
-      f32x4 acc = zero4();
+    for (int ks = 0; ks < 4; ++ks) acc = mfma16(ld8(za + ks * 32), wxt[ks], acc);
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) acc = mfma16(ld8(za + ks * 32), wxt[j][ks], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int sr = rq + r;
-        if (sr < ns) dact2[(size_t)(s0 + sr) * F0 + f] = (float)sX[sr * F0P + f] > 0.f ? acc[r] : 0.f;
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int sr = rq + r;
+      if (sr < ns) dact2[(size_t)(s0 + sr) * F0 + fx] = xm[r] > 0.f ? acc[r] : 0.f;
     }
   }
-  for (int e = tid; e < F1; e += NT) slab[e] = sdb[e];                       // fc1.bias
-  for (int e = tid; e < F2; e += NT) slab[P_F2B - P_F1B + e] = sdb[128 + e];
-  if (tid < NCLS) slab[P_F3B - P_F1B + tid] = sdb[224 + tid];
-  // the last workgroup zeroes dZ1T columns [nb, 128): they are K-padding of the fc1 wgrad
-  if (s0 + FC_SPW >= nb) {
-    const int pad = DZ1_LD - nb;
-    for (int e = tid; e < 128 * pad; e += NT) {
-      const int f = e / pad, c = nb + (e - f * pad);
-      dZ1T[(size_t)f * DZ1_LD + c] = (bf16)0.f;
+  if (lead) {
+    for (int e = tid; e < F1; e += NT) slab[e] = sdb[e];                       // fc1.bias
+    for (int e = tid; e < F2; e += NT) slab[P_F2B - P_F1B + e] = sdb[128 + e];
+    if (tid < NCLS) slab[P_F3B - P_F1B + tid] = sdb[224 + tid];
+    // the last row group zeroes dZ1T columns [nb, 128): K-padding of the fc1 wgrad
+    if (s0 + FC_SPW >= nb) {
+      const int pad = DZ1_LD - nb;
+      for (int e = tid; e < 128 * pad; e += NT) {
+        const int f = e / pad, c = nb + (e - f * pad);
+        dZ1T[(size_t)f * DZ1_LD + c] = (bf16)0.f;
+      }
     }
   }
   FEDMI_STAMP(1, 6);
 }
-
 // ---------------------------------------------------------------------------
 // K3: conv stack backward (one workgroup per sample) + fc1 wgrad workgroups.
 // All per-sample inputs and the conv2 dgrad weights are staged into LDS with
@@ -867,13 +897,19 @@ void launch_lenet_conv_fwd(hipStream_t st, const uint8_t* images, int sample_bas
                      seed, round_ctr, augment, act2, act2T, tstride, pool1, am1, am2, zero_stats);
 }
 
-void launch_lenet_fc_head(hipStream_t st, const bf16* act2, const int* labels, int nb, int train,
+void launch_lenet_fc1_fwd(hipStream_t st, const bf16* act2, int nb, const bf16* pk, const float* params, bf16* h1) {
+  if (nb <= 0) return;
+  const int mtiles = (nb + FC_SPW - 1) / FC_SPW;
+  hipLaunchKernelGGL(lenet_fc1_fwd, dim3(mtiles * 8), dim3(256), 0, st, act2, nb, pk, params, h1);
+}
+
+void launch_lenet_fc_tail(hipStream_t st, const bf16* h1, const bf16* act2, const int* labels, int nb, int train,
                           const bf16* pk, const float* params, float* dact2, bf16* dZ1T, float* fc_slab,
                           Stats* stats) {
   if (nb <= 0) return;
-  const int grid = (nb + FC_SPW - 1) / FC_SPW;
-  hipLaunchKernelGGL(lenet_fc_head, dim3(grid), dim3(NT), 0, st, act2, labels, nb, train, pk, params,
-                     dact2, dZ1T, fc_slab, stats);
+  const int mtiles = (nb + FC_SPW - 1) / FC_SPW;
+  hipLaunchKernelGGL(lenet_fc_tail, dim3(mtiles * (train ? 4 : 1)), dim3(NT), 0, st, h1, act2, labels, nb, train,
+                     pk, params, dact2, dZ1T, fc_slab, stats);
 }
 
 void launch_lenet_conv_bwd(hipStream_t st, const uint8_t* images, int sample_base, int nb,

@@ -11,8 +11,9 @@ using lenet::Stats;
 // launchers (csrc/kernels/lenet_kernels.hip)
 void launch_lenet_conv_fwd(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t,
                            const int*, int, bf16*, bf16*, int, bf16*, uint8_t*, uint8_t*, lenet::Stats*);
-void launch_lenet_fc_head(hipStream_t, const bf16*, const int*, int, int, const bf16*, const float*, float*, bf16*,
-                          float*, Stats*);
+void launch_lenet_fc1_fwd(hipStream_t, const bf16*, int, const bf16*, const float*, bf16*);
+void launch_lenet_fc_tail(hipStream_t, const bf16*, const bf16*, const int*, int, int, const bf16*, const float*, float*,
+                          bf16*, float*, Stats*);
 void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const float*, const bf16*,
                            const bf16*, const bf16*, const uint8_t*, const uint8_t*, const bf16*, float*, float*);
 void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, const float*, const float*, int, float,
@@ -25,7 +26,7 @@ void check_hip(hipError_t e, const char* what) {
 
 LeNetEngine::LeNetEngine(const LeNetBuffers& b, SgdConfig sgd, uint32_t seed, bool augment)
     : b_(b), sgd_(sgd), seed_(seed), augment_(augment) {
-  if (!b.params || !b.mom || !b.pk || !b.act2 || !b.act2T || !b.pool1 || !b.am1 || !b.am2 || !b.dact2 || !b.dZ1T ||
+  if (!b.params || !b.mom || !b.pk || !b.act2 || !b.act2T || !b.pool1 || !b.am1 || !b.am2 || !b.h1 || !b.dact2 || !b.dZ1T ||
       !b.conv_slab || !b.fc1w_grad || !b.fc_slab || !b.train_stats || !b.eval_stats || !b.round_ctr)
     throw std::invalid_argument("LeNetEngine: missing device buffer");
   if (b.act2_rows < lenet::MAX_TRAIN_BATCH) throw std::invalid_argument("LeNetEngine: act2_rows < 128");
@@ -67,7 +68,8 @@ void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round, bool 
   const int aug = augment_ ? 1 : 0;
   launch_lenet_conv_fwd(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug, b_.act2,
                         b_.act2T, MAX_TRAIN_BATCH, b_.pool1, b_.am1, b_.am2, reset_stats ? b_.train_stats : nullptr);
-  launch_lenet_fc_head(st, b_.act2, b_.train_labels + start, nb, 1, b_.pk, b_.params, b_.dact2, b_.dZ1T,
+  launch_lenet_fc1_fwd(st, b_.act2, nb, b_.pk, b_.params, b_.h1);
+  launch_lenet_fc_tail(st, b_.h1, b_.act2, b_.train_labels + start, nb, 1, b_.pk, b_.params, b_.dact2, b_.dZ1T,
                        b_.fc_slab, b_.train_stats);
   launch_lenet_conv_bwd(st, b_.train_images, start, nb, seed_, b_.round_ctr, aug, b_.dact2, b_.act2T, b_.dZ1T,
                         b_.pool1, b_.am1, b_.am2, b_.pk, b_.conv_slab, b_.fc1w_grad);
@@ -112,7 +114,8 @@ void LeNetEngine::eval(hipStream_t st, const uint8_t* images, const int* labels,
   if (n <= 0 || n > b_.act2_rows) throw std::invalid_argument("LeNetEngine::eval: n exceeds act2 capacity");
   launch_lenet_conv_fwd(st, images, 0, n, b_.pk, b_.params, seed_, b_.round_ctr, 0, b_.act2, nullptr, 0,
                         nullptr, nullptr, nullptr, b_.eval_stats);
-  launch_lenet_fc_head(st, b_.act2, labels, n, 0, b_.pk, b_.params, nullptr, nullptr, nullptr, b_.eval_stats);
+  launch_lenet_fc1_fwd(st, b_.act2, n, b_.pk, b_.params, b_.h1);
+  launch_lenet_fc_tail(st, b_.h1, b_.act2, labels, n, 0, b_.pk, b_.params, nullptr, nullptr, nullptr, b_.eval_stats);
   check_hip(hipGetLastError(), "LeNetEngine::eval launch");
 }
 

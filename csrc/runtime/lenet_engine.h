@@ -24,6 +24,7 @@ struct LeNetBuffers {
   bf16* act2 = nullptr;          // [act2_rows][F0P]
   int act2_rows = 0;
   bf16* act2T = nullptr;         // [F0P][MAX_TRAIN_BATCH]
+  bf16* h1 = nullptr;            // [act2_rows][128]  relu(fc1)
   bf16* pool1 = nullptr;         // [MAX_TRAIN_BATCH][NP1]
   uint8_t* am1 = nullptr;        // [MAX_TRAIN_BATCH][NP1]
   uint8_t* am2 = nullptr;        // [MAX_TRAIN_BATCH][F0]

@@ -62,6 +62,7 @@ class LeNetNativeTrainer(LocalTrainer):
             self.act2_rows = max(B, len(self.test_set))
             self.act2 = z(self.act2_rows, L["F0P"], dt=torch.bfloat16)
             self.act2T = z(L["F0P"], B, dt=torch.bfloat16)
+            self.h1 = z(self.act2_rows + 16, 128, dt=torch.bfloat16)
             self.pool1 = z(B, L["NP1"], dt=torch.bfloat16)
             self.am1 = z(B, L["NP1"], dt=torch.uint8)
             self.am2 = z(B, L["F0"], dt=torch.uint8)
@@ -75,7 +76,7 @@ class LeNetNativeTrainer(LocalTrainer):
         self._bufs = dict(
             train_images=_ptr(self.train_set.x), train_labels=_ptr(self.train_set.y), n_train=len(self.train_set),
             params=_ptr(self.params), mom=_ptr(self.mom), pk=_ptr(self.pk), act2=_ptr(self.act2),
-            act2_rows=self.act2_rows, act2T=_ptr(self.act2T), pool1=_ptr(self.pool1), am1=_ptr(self.am1),
+            act2_rows=self.act2_rows, act2T=_ptr(self.act2T), h1=_ptr(self.h1), pool1=_ptr(self.pool1), am1=_ptr(self.am1),
             am2=_ptr(self.am2), dact2=_ptr(self.dact2), dZ1T=_ptr(self.dZ1T), conv_slab=_ptr(self.conv_slab),
             fc1w_grad=_ptr(self.fc1w_grad), fc_slab=_ptr(self.fc_slab), train_stats=_ptr(self.stats[0]), eval_stats=_ptr(self.stats[1]),
             round_ctr=_ptr(self.round_ctr))

@@ -60,7 +60,8 @@ def _run_grad(nat, tr, start, nb, augment):
                        tr.stats[0].data_ptr())
     labels = tr.train_set.y[start:]
     nat.lenet_fc_head(s, tr.act2.data_ptr(), labels.data_ptr(), nb, 1, tr.pk.data_ptr(), tr.params.data_ptr(),
-                      tr.dact2.data_ptr(), tr.dZ1T.data_ptr(), tr.fc_slab.data_ptr(), tr.stats[0].data_ptr())
+                      tr.h1.data_ptr(), tr.dact2.data_ptr(), tr.dZ1T.data_ptr(), tr.fc_slab.data_ptr(),
+                      tr.stats[0].data_ptr())
     nat.lenet_conv_bwd(s, tr.train_set.x.data_ptr(), start, nb, SEED, tr.round_ctr.data_ptr(), int(augment),
                        tr.dact2.data_ptr(), tr.act2T.data_ptr(), tr.dZ1T.data_ptr(), tr.pool1.data_ptr(),
                        tr.am1.data_ptr(), tr.am2.data_ptr(), tr.pk.data_ptr(), tr.conv_slab.data_ptr(),
@@ -205,6 +206,7 @@ def test_step_stagewise_matches_torch(env, start, nb, augment):
     y = ds.train.y[start:start + nb].long()
     # ---- K2: FC head, kernel rounding points (H1, H2, dZ3, dZ2, dZ1 in bf16)
     h1 = _bf(torch.relu(X @ W1.t() + sd["fc1.bias"]))
+    assert rel(tr.h1[:nb, :120].float(), h1) < 1e-2
     h2 = _bf(torch.relu(h1 @ W2.t() + sd["fc2.bias"]))
     z = h2 @ W3.t() + sd["fc3.bias"]
     dz = (torch.softmax(z, 1) - F.one_hot(y, 10).float()) / nb

@@ -22,11 +22,11 @@ from fedmi.engine.lenet_native import LeNetNativeTrainer  # noqa: E402
 
 NAMES = {
     0: ("conv_fwd", ["stage+aug", "conv1", "pool1", "conv2", "pool2+store"]),
-    1: ("fc_head", ["prefetch+fc1", "fc2+fc3", "CE", "dW3/dH2", "dW2/dH1", "dX+slab"]),
+    1: ("fc_tail", ["prefetch+H1", "fc2+fc3", "CE", "dW3/dH2", "dW2/dH1", "dX+slab"]),
     2: ("conv_bwd", ["stage", "shift+scatter", "c2 wgrad+dgrad", "c1 wgrad", "slab store"]),
     3: ("sgd", ["all"]),
 }
-NWG = {0: 128, 1: 8, 2: 128, 3: 412}
+NWG = {0: 128, 1: 32, 2: 128, 3: 412}
 
 
 def main():
