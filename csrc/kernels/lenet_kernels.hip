@@ -39,8 +39,12 @@ __device__ unsigned long long fedmi_stamps[FEDMI_STAMP_KERNELS][FEDMI_STAMP_WGS]
 
 namespace {
 
-constexpr int NT = 512;         // threads per workgroup (8 waves) for K1/K2/K3
-constexpr int NW = NT / 64;
+constexpr int NT_FWD = 512;     // conv forward (K1): 8 waves (measured faster than 16)
+constexpr int NW_FWD = NT_FWD / 64;
+constexpr int NT_CONV = 1024;   // conv backward (K3): 16 waves
+constexpr int NW_CONV = NT_CONV / 64;
+constexpr int NT_FC = 512;      // FC tail (K2b): 8 waves
+constexpr int NW_FC = NT_FC / 64;
 
 __constant__ float kMean[3] = {0.4914f, 0.4822f, 0.4465f};
 __constant__ float kInvStd[3] = {1.f / 0.2023f, 1.f / 0.1994f, 1.f / 0.2010f};
@@ -96,7 +100,7 @@ FEDMI_DEV void zero_lds(void* p, int bytes) {
 // ---------------------------------------------------------------------------
 // K1: conv stack forward, one 8-wave workgroup per sample.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void lenet_conv_fwd(
+__global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
     const uint8_t* __restrict__ images, int sample_base, int nb,
     const bf16* __restrict__ pk, const float* __restrict__ params,
     uint32_t seed, const int* __restrict__ round_ctr, int augment,
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
   }
   const Aug a = aug_params(augment, seed, round_ctr, gidx);
   __syncthreads();
-  for (int e = tid; e < IMG_BYTES; e += NT) {   // lanes walk x: raw reads broadcast within a dword
+  for (int e = tid; e < IMG_BYTES; e += NT_FWD) {   // lanes walk x: raw reads broadcast within a dword
     const int c = e >> 10, y = (e >> 5) & 31, x = e & 31;
     xcl[(y * 40 + x) * 4 + c] = (bf16)aug_pixel(raw, a, c, y, x);
   }
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
   // ---- conv1: M = 784 positions (49 tiles), N = 6 (pad 16), K = 128 (4 steps)
   {
     const float bias = n16 < C1 ? params[P_C1B + n16] : 0.f;
-    for (int t = wave; t < NPOS1 / 16; t += NW) {
+    for (int t = wave; t < NPOS1 / 16; t += NW_FWD) {
       const int pos = t * 16 + n16;
       const int py = pos / O1, px = pos - py * O1;
       const bf16* xb = xcl + (py * 40 + px) * 4;
@@ -177,7 +181,7 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
   FEDMI_STAMP(0, 2);
 
   // ---- maxpool2 #1 (+ argmax code: 0=(0,0) 1=(0,1) 2=(1,0) 3=(1,1), first max wins)
-  for (int e = tid; e < P1CL; e += NT) {
+  for (int e = tid; e < P1CL; e += NT_FWD) {
     const int pos = e >> 3, c = e & 7;
     bf16 mb = (bf16)0.f;
     if (c < C1) {
@@ -219,7 +223,7 @@ __global__ __launch_bounds__(NT) void lenet_conv_fwd(
   FEDMI_STAMP(0, 4);
 
   // ---- maxpool2 #2 -> flattened act2 row (torch .view order: o*25 + py*5 + px)
-  for (int e = tid; e < F0P; e += NT) {
+  for (int e = tid; e < F0P; e += NT_FWD) {
     bf16 mb = (bf16)0.f;
     if (e < F0) {
       const int o = e / 25, rem = e - o * 25, py = rem / P2, px = rem - py * P2;
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(256) void lenet_fc1_fwd(
 //        pool2 ReLU) -> d(pool2) for K3.
 // Every global operand is prefetched into registers at entry.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void lenet_fc_tail(
+__global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
     const bf16* __restrict__ h1,     // [nb][128]  relu(fc1) from K2a
     const bf16* __restrict__ act2,   // [nb][F0P]  (for the dX mask)
     const int* __restrict__ labels,  // labels of this batch (already offset)
@@ -363,10 +367,10 @@ __global__ __launch_bounds__(NT) void lenet_fc_tail(
   zero_lds(sdZ3, sizeof(sdZ3));
   zero_lds(sdZ3T, sizeof(sdZ3T));
   zero_lds(sdZ2T, sizeof(sdZ2T));
-  for (int e = tid; e < 240; e += NT) sdb[e] = 0.f;
+  for (int e = tid; e < 240; e += NT_FC) sdb[e] = 0.f;
   if (tid < 16 * 128 / 8) reinterpret_cast<uint4*>(sH1)[tid] = h1v;
   __syncthreads();
-  for (int e = tid; e < 16 * 128; e += NT) {       // sample-contiguous copy for the dW2 GEMM
+  for (int e = tid; e < 16 * 128; e += NT_FC) {       // sample-contiguous copy for the dW2 GEMM
     const int r = e >> 7, c = e & 127;
     sH1T[c * 32 + r] = sH1[e];
   }
@@ -462,7 +466,7 @@ __global__ __launch_bounds__(NT) void lenet_fc_tail(
   }
 
   // ---- dW3 (tasks 0..5, lead only) and dH2 = dZ3 . W3 (tasks 6..11)
-  for (int qq = wave; qq < 12; qq += NW) {
+  for (int qq = wave; qq < 12; qq += NW_FC) {
     if (qq < 6) {
       if (!lead) continue;
       const int ft = qq;
@@ -494,7 +498,7 @@ __global__ __launch_bounds__(NT) void lenet_fc_tail(
 
   // ---- dW2 = dZ2^T H1 (48 tiles, lead only) and dH1 = dZ2 . W2 (tile = wave) -> dZ1
   if (lead) {
-    for (int qq = wave; qq < 48; qq += NW) {
+    for (int qq = wave; qq < 48; qq += NW_FC) {
       const int mt2 = qq >> 3, ft = qq & 7;
       const f32x4 acc = mfma16(ld8(sdZ2T + (mt2 * 16 + n16) * 32 + kq), ld8(sH1T + (ft * 16 + n16) * 32 + kq), zero4());
 #pragma unroll
@@ -540,13 +544,13 @@ __global__ __launch_bounds__(NT) void lenet_fc_tail(
     }
   }
   if (lead) {
-    for (int e = tid; e < F1; e += NT) slab[e] = sdb[e];                       // fc1.bias
-    for (int e = tid; e < F2; e += NT) slab[P_F2B - P_F1B + e] = sdb[128 + e];
+    for (int e = tid; e < F1; e += NT_FC) slab[e] = sdb[e];                       // fc1.bias
+    for (int e = tid; e < F2; e += NT_FC) slab[P_F2B - P_F1B + e] = sdb[128 + e];
     if (tid < NCLS) slab[P_F3B - P_F1B + tid] = sdb[224 + tid];
     // the last row group zeroes dZ1T columns [nb, 128): K-padding of the fc1 wgrad
     if (s0 + FC_SPW >= nb) {
       const int pad = DZ1_LD - nb;
-      for (int e = tid; e < 128 * pad; e += NT) {
+      for (int e = tid; e < 128 * pad; e += NT_FC) {
         const int f = e / pad, c = nb + (e - f * pad);
         dZ1T[(size_t)f * DZ1_LD + c] = (bf16)0.f;
       }
@@ -559,7 +563,7 @@ __global__ __launch_bounds__(NT) void lenet_fc_tail(
 // All per-sample inputs and the conv2 dgrad weights are staged into LDS with
 // 16-byte loads at entry; every MFMA operand afterwards is an LDS read.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void lenet_conv_bwd(
+__global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
     const uint8_t* __restrict__ images, int sample_base, int nb,
     uint32_t seed, const int* __restrict__ round_ctr, int augment,
     const float* __restrict__ dact2,       // [nb][F0]   d(pool2), ReLU-masked
@@ -572,15 +576,22 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
     float* __restrict__ conv_slab,         // [nb][CS]
     float* __restrict__ fc1w_grad)         // [F1W_N]
 {
-  constexpr int XSH = 5 * 3 * 32 * 32;        // x shifted copies [s][c][y][x']
+  // Operand images are padded so the 16 lanes of an MFMA fragment read land on
+  // distinct 16-byte bank groups (strides in 16-B units: coprime with 16 or
+  // chosen so the (c, r, s) im2col column index maps to distinct groups).
+  constexpr int XROW = 40, XS_C = 32 * XROW + 72, XS_S = 3 * XS_C + 48;   // xsh[s][c][y][x']: units 5 / 169 / 513
+  constexpr int XSH = 5 * XS_S;
   constexpr int P1SH = 5 * 6 * 14 * 16;       // pool1 shifted copies [s][c][y][x']
   constexpr int DY2W = 16 * 160;              // conv2 out-grad [o][i*16+j]
-  constexpr int DY2C = 18 * 18 * 16;          // conv2 out-grad channels-last, 4-px zero border
-  constexpr int DY1 = 6 * 896;                // conv1 out-grad [o][i*32+j]
+  constexpr int DY2S = 24;                    // conv2 out-grad channels-last position stride (3 units)
+  constexpr int DY2C = 18 * 18 * DY2S;        // 4-px zero border
+  constexpr int DY1S = 904;                   // conv1 out-grad row stride [o][i*32+j] (113 units)
+  constexpr int DY1 = 6 * DY1S;
+  constexpr int WDGS = KDGP + 8;              // conv2 dgrad weight row stride (53 units)
   constexpr int O_RAW = 0, O_P1R = 3072, O_AM1 = O_P1R + 2368, O_AM2 = O_AM1 + 1184, O_DX = O_AM2 + 416,
-                O_WDG = O_DX + F0 * 4, O_XSH = O_WDG + 16 * KDGP * 2, O_P1SH = O_XSH + XSH * 2,
+                O_WDG = O_DX + F0 * 4, O_XSH = O_WDG + 16 * WDGS * 2, O_P1SH = O_XSH + XSH * 2,
                 O_DY2W = O_P1SH + P1SH * 2, O_DY2C = O_DY2W + DY2W * 2, O_DY1 = O_DY2C + DY2C * 2,
-                O_DW1 = O_DY1 + DY1 * 2, O_DB = O_DW1 + 16 * 80 * 4, O_END = O_DB + 32 * 4;
+                O_DW1 = O_DY1 + DY1 * 2, O_DB = O_DW1 + 3 * 6 * 80 * 4, O_END = O_DB + 32 * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem[O_END];
 
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
@@ -589,7 +600,7 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
   if ((int)blockIdx.x >= nb) {
     // ---- fc1.weight grad: dW1[n][f] = sum_s dZ1[s][n] X[s][f], f in [16e, 16e+16)
     const int e = blockIdx.x - nb;
-    if (e >= N_DW1_WG) return;
+    if (e >= N_DW1_WG || wave >= 8) return;     // 8 row tiles of 16 outputs
     const int nks = (nb + 31) >> 5;
     const bf16* ap = dZ1T + (wave * 16 + n16) * DZ1_LD + kq;
     const bf16* bp = act2T + (size_t)(e * 16 + n16) * MAX_TRAIN_BATCH + kq;
@@ -623,6 +634,7 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
   bf16* dY2c = reinterpret_cast<bf16*>(smem + O_DY2C);
   bf16* dY1 = reinterpret_cast<bf16*>(smem + O_DY1);
   float* db = reinterpret_cast<float*>(smem + O_DB);
+  float* w1part = reinterpret_cast<float*>(smem + O_DW1);   // conv1 wgrad K-split partials [3][6][80]
 
   const int s = blockIdx.x;
   const int gidx = sample_base + s;
@@ -639,13 +651,16 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
     const uint4* am24 = reinterpret_cast<const uint4*>(am2 + (size_t)s * F0);
     const uint4* dx4 = reinterpret_cast<const uint4*>(dact2 + (size_t)s * F0);
     const uint4* wdg4 = reinterpret_cast<const uint4*>(pk + PK_W2DG);
-    for (int e = tid; e < E6; e += NT) {
+    for (int e = tid; e < E6; e += NT_CONV) {
       if (e < E1) reinterpret_cast<uint4*>(raw)[e] = img4[e];
       else if (e < E2) reinterpret_cast<uint4*>(p1r)[e - E1] = p14[e - E1];
       else if (e < E3) reinterpret_cast<uint2*>(am1s)[e - E2] = am12[e - E2];
       else if (e < E4) reinterpret_cast<uint4*>(am2s)[e - E3] = am24[e - E3];
       else if (e < E5) reinterpret_cast<uint4*>(dxs)[e - E4] = dx4[e - E4];
-      else reinterpret_cast<uint4*>(wdg)[e - E5] = wdg4[e - E5];
+      else {   // padded rows: 52 x 16 B per weight row
+        const int w = e - E5, row = w / (KDGP / 8), col = w - row * (KDGP / 8);
+        reinterpret_cast<uint4*>(wdg + row * WDGS)[col] = wdg4[w];
+      }
     }
   }
   zero_lds(dY2w, DY2W * 2);
@@ -660,15 +675,15 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
 
   // each augmented pixel / pooled value is computed once and stored into its 5
   // column-shifted copies: copy s holds element x at column x - s
-  for (int e = tid; e < IMG_BYTES; e += NT) {
+  for (int e = tid; e < IMG_BYTES; e += NT_CONV) {
     const int c = e >> 10, y = (e >> 5) & 31, x = e & 31;
     const bf16 v = (bf16)aug_pixel(raw, a, c, y, x);
-    bf16* row = xsh + (c * 32 + y) * 32 + x;
+    bf16* row = xsh + c * XS_C + y * XROW + x;
 #pragma unroll
     for (int sh = 0; sh < 5; ++sh)
-      if (x >= sh) row[sh * (3 * 32 * 32) - sh] = v;
+      if (x >= sh) row[sh * XS_S - sh] = v;
   }
-  for (int e = tid; e < NP1; e += NT) {
+  for (int e = tid; e < NP1; e += NT_CONV) {
     const int c = e / 196, rem = e - c * 196, y = rem / P1, x = rem - y * P1;
     const bf16 v = p1r[e];
     bf16* row = p1sh + (c * 14 + y) * 16 + x;
@@ -676,14 +691,14 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
     for (int sh = 0; sh < 5; ++sh)
       if (x >= sh) row[sh * (6 * 14 * 16) - sh] = v;
   }
-  for (int f = tid; f < F0; f += NT) {
+  for (int f = tid; f < F0; f += NT_CONV) {
     const int o = f / 25, rem = f - o * 25, py = rem / P2, px = rem - py * P2;
     const int am = am2s[f];
     const int y = 2 * py + (am >> 1), x = 2 * px + (am & 1);
     const float g = dxs[f];
     const bf16 gb = (bf16)g;
     dY2w[o * 160 + y * 16 + x] = gb;
-    dY2c[((y + 4) * 18 + (x + 4)) * 16 + o] = gb;
+    dY2c[((y + 4) * 18 + (x + 4)) * DY2S + o] = gb;
     atomicAdd(&db[o], g);
   }
   __syncthreads();
@@ -693,7 +708,8 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
 
   // ---- conv2 wgrad: dW2[o][k'] = sum_p dY2[o][p] * im2col(pool1)[p][k']
   //      M = 16 (o), N = 150 (10 tiles), K = 160 (p' = i*16 + j, 5 steps)
-  for (int t = wave; t < 10; t += NW) {
+  // task map over 16 waves: dgrad tile t -> wave t (t < 13), wgrad tile t -> wave (13 + t) % 16
+  for (int t = (wave + 3) & 15; t < 10; t += NW_CONV) {
     const int kk = t * 16 + n16;
     const int kc = kk < 150 ? kk : 0;
     const int c = kc / 25, rs = kc - c * 25, r = rs / 5, sc = rs - r * 5;
@@ -717,14 +733,14 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
   for (int ks = 0; ks < 13; ++ks) {
     const int G = ks * 4 + (lane >> 4), g = G >> 1;
     const int r = g / 5, sc = g - r * 5;
-    koff[ks] = g < 25 ? (-r * 18 - sc) * 16 + (G & 1) * 8 : 0;   // pad group: weight 0, any in-bounds read
+    koff[ks] = g < 25 ? (-r * 18 - sc) * DY2S + (G & 1) * 8 : 0;   // pad group: weight 0, any in-bounds read
   }
-  for (int t = wave; t < 13; t += NW) {
+  for (int t = wave; t < 13; t += NW_CONV) {
     int pos = t * 16 + n16;
     if (pos >= 196) pos = 0;
     const int y = pos / P1, x = pos - y * P1;
-    const bf16* gb = dY2c + ((y + 4) * 18 + (x + 4)) * 16;
-    const bf16* wb = wdg + n16 * KDGP + kq;
+    const bf16* gb = dY2c + ((y + 4) * 18 + (x + 4)) * DY2S;
+    const bf16* wb = wdg + min(n16, C1) * WDGS + kq;     // rows >= 6 are zero: share row 6 (broadcast)
     f32x4 acc = zero4();
 #pragma unroll
     for (int ks = 0; ks < 13; ++ks) acc = mfma16(ld8(gb + koff[ks]), ld8(wb + ks * 32), acc);
@@ -740,7 +756,7 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
           const float g = pooled > 0.f ? acc[rr] : 0.f;
           const int am = am1s[c * 196 + p];
           const int yy = 2 * py + (am >> 1), xx = 2 * px + (am & 1);
-          dY1[c * 896 + yy * 32 + xx] = (bf16)g;
+          dY1[c * DY1S + yy * 32 + xx] = (bf16)g;
           csum += g;
         }
       }
@@ -751,30 +767,43 @@ __global__ __launch_bounds__(NT) void lenet_conv_bwd(
   FEDMI_STAMP(2, 3);
 
   // ---- conv1 wgrad: dW1[o][k'] = sum_p dY1[o][p] * im2col(x)[p][k']
-  //      M = 16 (o < 6), N = 75 (5 tiles: one per wave 0..4), K = 896 (p' = i*32 + j,
-  //      28 steps = conv1 output rows); each wave owns its tile: no cross-wave combine.
-  if (wave < 5) {
-    const int kk = wave * 16 + n16;
-    const int kc = kk < 75 ? kk : 0;
+  //      M = 16 (o < 6), N = 75 (5 tiles), K = 896 (p' = i*32 + j, 28 steps = conv1
+  //      output rows) split in 3 parts: 15 waves = 5 tiles x 3 K-parts, then a
+  //      deterministic 3-way combine through LDS.
+  if (wave < 15) {
+    const int nt = wave % 5, part = wave / 5;
+    const int ks0 = part * 10, ks1 = min(ks0 + 10, O1);
+    const int kk = nt * 16 + n16;
+    const int kc = kk < 75 ? kk : kk - 64;                 // pad columns: distinct bank groups, result dropped
     const int c = kc / 25, rs = kc - c * 25, r = rs / 5, sc = rs - r * 5;
-    const bf16* bb = xsh + ((sc * 3 + c) * 32 + r) * 32 + kq;
-    const bf16* ab = dY1 + min(n16, C1 - 1) * 896 + kq;
+    const bf16* bb = xsh + sc * XS_S + c * XS_C + r * XROW + kq;
+    const bf16* ab = dY1 + min(n16, C1 - 1) * DY1S + kq;
     const bool arow = n16 < C1;
     f32x4 acc0 = zero4(), acc1 = zero4();
-#pragma unroll 2
-    for (int ks = 0; ks < O1; ks += 2) {
+    int ks = ks0;
+    for (; ks + 1 < ks1; ks += 2) {
       bf16x8 a0 = ld8(ab + ks * 32), a1 = ld8(ab + ks * 32 + 32);
       if (!arow) { a0 = zero8(); a1 = zero8(); }
-      acc0 = mfma16(a0, ld8(bb + ks * 32), acc0);
-      acc1 = mfma16(a1, ld8(bb + ks * 32 + 32), acc1);
+      acc0 = mfma16(a0, ld8(bb + ks * XROW), acc0);
+      acc1 = mfma16(a1, ld8(bb + (ks + 1) * XROW), acc1);
+    }
+    if (ks < ks1) {
+      bf16x8 a0 = ld8(ab + ks * 32);
+      if (!arow) a0 = zero8();
+      acc0 = mfma16(a0, ld8(bb + ks * XROW), acc0);
     }
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int o = rq + rr;
-      if (o < C1 && kk < 75) slab[P_C1W + o * 75 + kk] = acc0[rr] + acc1[rr];
+      if (o < C1 && kk < 75) w1part[(part * 6 + o) * 80 + kk] = acc0[rr] + acc1[rr];
     }
   }
+  __syncthreads();
   FEDMI_STAMP(2, 4);
+  for (int e = tid; e < C1 * 75; e += NT_CONV) {
+    const int o = e / 75, kk = e - o * 75;
+    slab[P_C1W + e] = w1part[o * 80 + kk] + w1part[(6 + o) * 80 + kk] + w1part[(12 + o) * 80 + kk];
+  }
   if (tid < C1) slab[P_C1B + tid] = db[16 + tid];
   if (tid < C2) slab[P_C2B + tid] = db[tid];
   FEDMI_STAMP(2, 5);
@@ -893,7 +922,7 @@ void launch_lenet_conv_fwd(hipStream_t st, const uint8_t* images, int sample_bas
                            int augment, bf16* act2, bf16* act2T, int tstride, bf16* pool1,
                            uint8_t* am1, uint8_t* am2, Stats* zero_stats) {
   if (nb <= 0) return;
-  hipLaunchKernelGGL(lenet_conv_fwd, dim3(nb), dim3(NT), 0, st, images, sample_base, nb, pk, params,
+  hipLaunchKernelGGL(lenet_conv_fwd, dim3(nb), dim3(NT_FWD), 0, st, images, sample_base, nb, pk, params,
                      seed, round_ctr, augment, act2, act2T, tstride, pool1, am1, am2, zero_stats);
 }
 
@@ -908,7 +937,7 @@ void launch_lenet_fc_tail(hipStream_t st, const bf16* h1, const bf16* act2, cons
                           Stats* stats) {
   if (nb <= 0) return;
   const int mtiles = (nb + FC_SPW - 1) / FC_SPW;
-  hipLaunchKernelGGL(lenet_fc_tail, dim3(mtiles * (train ? 4 : 1)), dim3(NT), 0, st, h1, act2, labels, nb, train,
+  hipLaunchKernelGGL(lenet_fc_tail, dim3(mtiles * (train ? 4 : 1)), dim3(NT_FC), 0, st, h1, act2, labels, nb, train,
                      pk, params, dact2, dZ1T, fc_slab, stats);
 }
 
@@ -917,7 +946,7 @@ void launch_lenet_conv_bwd(hipStream_t st, const uint8_t* images, int sample_bas
                            const bf16* act2T, const bf16* dZ1T, const bf16* pool1, const uint8_t* am1,
                            const uint8_t* am2, const bf16* pk, float* conv_slab, float* fc1w_grad) {
   if (nb <= 0) return;
-  hipLaunchKernelGGL(lenet_conv_bwd, dim3(nb + N_DW1_WG), dim3(NT), 0, st, images, sample_base, nb, seed,
+  hipLaunchKernelGGL(lenet_conv_bwd, dim3(nb + N_DW1_WG), dim3(NT_CONV), 0, st, images, sample_base, nb, seed,
                      round_ctr, augment, dact2, act2T, dZ1T, pool1, am1, am2, pk, conv_slab, fc1w_grad);
 }
 

@@ -101,6 +101,9 @@ class LocalTrainer(abc.ABC):
     def device(self) -> torch.device:
         ...
 
+    def set_lr(self, lr: float) -> None:
+        raise NotImplementedError
+
     def synchronize(self) -> None:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)

@@ -12,6 +12,7 @@ from __future__ import annotations
 from collections import OrderedDict
 from typing import List, Optional
 
+import dataclasses
 import torch
 
 from .. import native
@@ -44,7 +45,7 @@ class LeNetNativeTrainer(LocalTrainer):
         nat = native.require()
         self._nat = nat
         self.L = L = nat.lenet_layout()
-        self.cfg = cfg
+        self.cfg = dataclasses.replace(cfg)   # private copy: set_lr mutates it
         self._device = device
         self.round_idx = 0
         with torch.cuda.device(device):
@@ -159,3 +160,8 @@ class LeNetNativeTrainer(LocalTrainer):
 
     def reset_momentum(self) -> None:
         self.mom.zero_()
+
+    def set_lr(self, lr: float) -> None:
+        """New learning rate (re-captures the epoch graph on the next train_epoch)."""
+        self.cfg.lr = float(lr)
+        self.engine.set_sgd(self.cfg.lr, self.cfg.momentum, self.cfg.weight_decay)

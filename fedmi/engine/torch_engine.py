@@ -12,6 +12,7 @@ from __future__ import annotations
 from collections import OrderedDict
 from typing import List
 
+import dataclasses
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -62,7 +63,7 @@ class TorchTrainer(LocalTrainer):
     def __init__(self, model_name: str, data: FedDataset, device: torch.device,
                  cfg: TrainerConfig = TrainerConfig(), init_state=None, model_kwargs=None):
         self.model_name = model_name
-        self.cfg = cfg
+        self.cfg = dataclasses.replace(cfg)   # private copy: set_lr mutates it
         self._device = torch.device(device)
         torch.manual_seed(cfg.seed)
         model = build_model(model_name, **(model_kwargs or {}))
@@ -173,3 +174,6 @@ class TorchTrainer(LocalTrainer):
     def eval_stats(self) -> EpochStats:
         v = self._estats.cpu().tolist()
         return EpochStats(v[0], int(v[1]), int(v[2]))
+
+    def set_lr(self, lr: float) -> None:
+        self.cfg.lr = float(lr)
