@@ -44,6 +44,8 @@ void launch_dequant_accum(hipStream_t, const signed char*, const float*, int, lo
 
 using namespace fedmi;
 
+void fedmi_bind_cnn(py::module_& m);   // bindings_cnn.cpp
+
 template <typename T>
 static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
 static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
@@ -78,6 +80,7 @@ static LeNetBuffers buffers_from(const py::dict& d) {
 }
 
 static void fedmi_bind(py::module_& m) {
+  fedmi_bind_cnn(m);
   m.def("stamps_enabled", &stamps_enabled);
   m.def("read_stamps", [](bool clear) {
     const size_t n = (size_t)FEDMI_STAMP_KERNELS * FEDMI_STAMP_WGS * FEDMI_STAMP_SLOTS;

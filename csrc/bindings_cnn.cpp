@@ -1,0 +1,171 @@
+// fedmi — Python bindings for the CNN-zoo kernels (implicit-GEMM conv, BN,
+// classifier head, input prep).  Raw device pointers + torch stream handle,
+// like the rest of the extension; every call is graph-capturable.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "kernels/common.h"
+
+namespace py = pybind11;
+
+namespace fedmi {
+struct ConvShape {
+  int N, H, W, C, Cw, O, P, Q, R, S, st, pad;
+};
+void launch_conv_fwd(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, const float*);
+void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*);
+void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int);
+long conv_wgrad_ws_floats(const ConvShape&);
+void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int);
+
+struct BNDesc {
+  const float* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
+  float* smean; float* sinv; const float* shift;
+};
+struct BNBwdDesc {
+  const bf16* dya; const bf16* dyb; const bf16* y;
+  const bf16* za; const float* meanA; const float* invA; const float* gammaA; float* dgammaA; float* dbetaA; bf16* dza;
+  const bf16* zb; const float* meanB; const float* invB; const float* gammaB; float* dgammaB; float* dbetaB; bf16* dzb;
+  bf16* gout;
+  float* shiftA; float* shiftB;
+};
+struct DwShape {
+  int N, H, W, C, R, S, st, pad;
+};
+void launch_dw_fwd(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, float*, const float*);
+void launch_dw_dgrad(hipStream_t, const DwShape&, const bf16*, const float*, bf16*);
+long dw_wgrad_ws_floats(const DwShape&);
+void launch_dw_wgrad(hipStream_t, const DwShape&, const bf16*, const bf16*, float*, float*, long, int);
+void launch_prep_input(hipStream_t, const uint8_t*, int, const int*, int, int, uint32_t, const int*, bf16*);
+void launch_sched_next(hipStream_t, const int*, int*, int*);
+void launch_bn_apply(hipStream_t, const bf16*, const BNDesc&, const bf16*, const BNDesc*, const bf16*, bf16*, int, int,
+                     float, float, int, int);
+void launch_bn_bwd(hipStream_t, const BNBwdDesc&, float*, int, int);
+void launch_head(hipStream_t, const bf16*, const int*, int, const int*, int, int, int, int, const float*,
+                 const float*, float*, float*, bf16*, float*, float*, float*, int);
+}  // namespace fedmi
+
+using namespace fedmi;
+
+namespace {
+template <typename T>
+T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+void check(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+ConvShape shape_from(const py::tuple& t) {
+  if (t.size() != 12) throw std::invalid_argument("conv shape: (N,H,W,C,Cw,O,P,Q,R,S,stride,pad)");
+  ConvShape s;
+  int* f = &s.N;
+  for (int i = 0; i < 12; ++i) f[i] = t[i].cast<int>();
+  return s;
+}
+
+uintptr_t dget(const py::dict& d, const char* k) {
+  return d.contains(k) && !d[k].is_none() ? d[k].cast<uintptr_t>() : 0;
+}
+
+DwShape dw_from(const py::tuple& t) {
+  if (t.size() != 8) throw std::invalid_argument("dwconv shape: (N,H,W,C,R,S,stride,pad)");
+  DwShape s;
+  int* f = &s.N;
+  for (int i = 0; i < 8; ++i) f[i] = t[i].cast<int>();
+  return s;
+}
+
+BNDesc bn_from(const py::dict& d) {
+  return BNDesc{P<const float>(dget(d, "stats")), P<const float>(dget(d, "gamma")), P<const float>(dget(d, "beta")),
+                P<float>(dget(d, "rmean")),       P<float>(dget(d, "rvar")),        P<long long>(dget(d, "nbt")),
+                P<float>(dget(d, "smean")),       P<float>(dget(d, "sinv")),        P<const float>(dget(d, "shift"))};
+}
+}  // namespace
+
+void fedmi_bind_cnn(py::module_& m) {
+  m.def("conv_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
+                       uintptr_t shift) {
+    launch_conv_fwd(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(w), P<bf16>(y), P<float>(stats),
+                    P<const float>(shift));
+    check("conv_fwd");
+  });
+  m.def("conv_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx) {
+    launch_conv_dgrad(S(st), shape_from(shp), P<const bf16>(dy), P<const bf16>(w), P<bf16>(dx));
+    check("conv_dgrad");
+  });
+  m.def("conv_wgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws,
+                         long ws_floats, int splits, int accumulate) {
+    launch_conv_wgrad(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(dy), P<float>(dw), P<float>(ws),
+                      ws_floats, splits, accumulate);
+    check("conv_wgrad");
+  });
+  m.def("conv_wgrad_ws_floats", [](const py::tuple& shp) { return conv_wgrad_ws_floats(shape_from(shp)); });
+  m.def("conv_pack", [](uintptr_t st, uintptr_t w, uintptr_t wr, int O, int Cw, int C, int RS) {
+    launch_conv_pack(S(st), P<const float>(w), P<bf16>(wr), O, Cw, C, RS);
+    check("conv_pack");
+  });
+  m.def("dw_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
+                     uintptr_t shift) {
+    launch_dw_fwd(S(st), dw_from(shp), P<const bf16>(x), P<const float>(w), P<bf16>(y), P<float>(stats),
+                  P<const float>(shift));
+    check("dw_fwd");
+  });
+  m.def("dw_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx) {
+    launch_dw_dgrad(S(st), dw_from(shp), P<const bf16>(dy), P<const float>(w), P<bf16>(dx));
+    check("dw_dgrad");
+  });
+  m.def("dw_wgrad_ws_floats", [](const py::tuple& shp) { return dw_wgrad_ws_floats(dw_from(shp)); });
+  m.def("dw_wgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws,
+                       long ws_floats, int accumulate) {
+    launch_dw_wgrad(S(st), dw_from(shp), P<const bf16>(x), P<const bf16>(dy), P<float>(dw), P<float>(ws), ws_floats,
+                    accumulate);
+    check("dw_wgrad");
+  });
+  m.def("prep_input", [](uintptr_t st, uintptr_t images, int base, uintptr_t dbase, int nb, int augment,
+                         uint32_t seed, uintptr_t round_ctr, uintptr_t out) {
+    launch_prep_input(S(st), P<const uint8_t>(images), base, P<const int>(dbase), nb, augment, seed,
+                      P<const int>(round_ctr), P<bf16>(out));
+    check("prep_input");
+  });
+  m.def("sched_next", [](uintptr_t st, uintptr_t sched, uintptr_t counter, uintptr_t cur) {
+    launch_sched_next(S(st), P<const int>(sched), P<int>(counter), P<int>(cur));
+    check("sched_next");
+  });
+  m.def("bn_apply", [](uintptr_t st, uintptr_t z, const py::dict& a, uintptr_t z2, py::object b, uintptr_t res,
+                       uintptr_t y, int M, int C, float eps, float mom, int train, int relu) {
+    BNDesc bd{};
+    const bool has_b = !b.is_none();
+    if (has_b) bd = bn_from(b.cast<py::dict>());
+    launch_bn_apply(S(st), P<const bf16>(z), bn_from(a), P<const bf16>(z2), has_b ? &bd : nullptr, P<const bf16>(res),
+                    P<bf16>(y), M, C, eps, mom, train, relu);
+    check("bn_apply");
+  });
+  m.def("bn_bwd", [](uintptr_t st, const py::dict& d, uintptr_t red, int M, int C) {
+    BNBwdDesc b{P<const bf16>(dget(d, "dya")),     P<const bf16>(dget(d, "dyb")),     P<const bf16>(dget(d, "y")),
+                P<const bf16>(dget(d, "za")),      P<const float>(dget(d, "meanA")),  P<const float>(dget(d, "invA")),
+                P<const float>(dget(d, "gammaA")), P<float>(dget(d, "dgammaA")),      P<float>(dget(d, "dbetaA")),
+                P<bf16>(dget(d, "dza")),           P<const bf16>(dget(d, "zb")),      P<const float>(dget(d, "meanB")),
+                P<const float>(dget(d, "invB")),   P<const float>(dget(d, "gammaB")), P<float>(dget(d, "dgammaB")),
+                P<float>(dget(d, "dbetaB")),       P<bf16>(dget(d, "dzb")),           P<bf16>(dget(d, "gout")),
+                P<float>(dget(d, "shiftA")),       P<float>(dget(d, "shiftB"))};
+    if (!b.dya || !b.za || !b.meanA || !b.invA || !b.gammaA || !b.dza) throw std::invalid_argument("bn_bwd: missing A");
+    launch_bn_bwd(S(st), b, P<float>(red), M, C);
+    check("bn_bwd");
+  });
+  m.def("head", [](uintptr_t st, uintptr_t y, uintptr_t labels, int base, uintptr_t dbase, int N, int HW, int C, int J,
+                   uintptr_t W, uintptr_t b, uintptr_t pooled, uintptr_t dlog, uintptr_t dy, uintptr_t stats,
+                   uintptr_t dW, uintptr_t db, int train) {
+    launch_head(S(st), P<const bf16>(y), P<const int>(labels), base, P<const int>(dbase), N, HW, C, J, P<const float>(W),
+                P<const float>(b), P<float>(pooled), P<float>(dlog), P<bf16>(dy), P<float>(stats), P<float>(dW),
+                P<float>(db), train);
+    check("head");
+  });
+}

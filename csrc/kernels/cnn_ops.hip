@@ -1,0 +1,458 @@
+// fedmi — memory-bound companions of the implicit-GEMM convolution for the
+// CIFAR CNN zoo (ResNet family first), all on NHWC bf16 activations:
+//
+//  * prep_input:     uint8 NCHW image batch -> RandomCrop(32, pad 4) + HFlip +
+//                    Normalize (src/main.py:36-41, on-device counter RNG shared
+//                    with the LeNet engine) -> bf16 NHWC, channels padded to 8.
+//  * bn_apply:       training BatchNorm from the batch statistics the conv
+//                    epilogue accumulated (sum, sum of squares) or eval BN
+//                    from running stats; running-stat momentum update and
+//                    num_batches_tracked += 1 (torch BatchNorm2d semantics);
+//                    fused residual (identity or a second BN branch: the
+//                    projection shortcut) and ReLU.
+//  * bn_bwd_reduce / bn_bwd_apply: BatchNorm backward through the ReLU mask,
+//                    for one or two BN branches sharing the same output grad,
+//                    with an optional second incoming grad (residual fan-in);
+//                    writes dgamma/dbeta into the flat gradient buffer.
+//  * head_fwd_bwd / head_wgrad: global average pool + linear + softmax CE
+//                    (+ correct count) and its backward, deterministic weight
+//                    gradient (no atomics across samples).
+//
+// Reference parity: native_batch_norm(_backward), relu/threshold_backward,
+// add, avg_pool2d(4), addmm/mm, _log_softmax + nll_loss of SURVEY.md §2.4b
+// (src/models/resnet.py:14-104, src/main.py:146-156).
+#include <stdexcept>
+
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+
+__constant__ float cMean[3] = {0.4914f, 0.4822f, 0.4465f};
+__constant__ float cInvStd[3] = {1.f / 0.2023f, 1.f / 0.1994f, 1.f / 0.2010f};
+
+FEDMI_DEV void load8f(const bf16* p, float* v) {
+  const bf16x8v b = *reinterpret_cast<const bf16x8v*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)b[j];
+}
+FEDMI_DEV void store8f(bf16* p, const float* v) {
+  bf16x8v b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = (bf16)v[j];
+  *reinterpret_cast<bf16x8v*>(p) = b;
+}
+
+// ---------------------------------------------------------------------------
+// dbase (optional): device-side batch start added to ``base``, so one captured
+// graph serves every batch of an epoch (see sched_next_kernel).
+__global__ __launch_bounds__(256) void prep_input_kernel(const uint8_t* __restrict__ images, int base,
+                                                         const int* __restrict__ dbase, int nb, int augment,
+                                                         uint32_t seed, const int* __restrict__ round_ctr,
+                                                         bf16* __restrict__ out) {
+  // one thread per output pixel: 8 channels (3 real + 5 zero) = one 16-B store
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nb * 1024) return;
+  const int s = t >> 10, y = (t >> 5) & 31, x = t & 31;
+  const int gidx = base + (dbase ? dbase[0] : 0) + s;
+  int i0 = 4, j0 = 4, flip = 0;
+  if (augment) {
+    const uint32_t h = hash3(seed, (uint32_t)round_ctr[0], (uint32_t)gidx);
+    i0 = (int)(h % 9u); j0 = (int)((h >> 8) % 9u); flip = (int)((h >> 16) & 1u);
+  }
+  const int sy = y + i0 - 4, sx = (flip ? 31 - x : x) + j0 - 4;
+  const bool in = sy >= 0 && sy < 32 && sx >= 0 && sx < 32;
+  const uint8_t* img = images + (size_t)gidx * 3072 + (in ? sy * 32 + sx : 0);
+  float v[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) v[c] = 0.f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float px = (float)img[c * 1024];
+    v[c] = ((in ? px : 0.f) * (1.f / 255.f) - cMean[c]) * cInvStd[c];
+  }
+  store8f(out + (size_t)t * 8, v);
+}
+
+// ---------------------------------------------------------------------------
+struct BNArgs {
+  const float* stats;     // [2][C]: sum, sum of squares over M rows (train)
+  const float* gamma;
+  const float* beta;
+  float* rmean;           // running stats (updated in train mode, read in eval)
+  float* rvar;
+  long long* nbt;         // num_batches_tracked
+  float* smean;           // saved batch mean / invstd for the backward
+  float* sinv;
+  const float* shift;     // the sums in ``stats`` are of (z - shift[c]) (null: 0)
+};
+
+// per-channel scale/shift into LDS; block 0 also commits the running stats
+FEDMI_DEV void bn_coeffs(const BNArgs& a, int C, int M, float eps, float mom, int train, float* sc, float* sh) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float mean, inv;
+    if (train) {
+      const float ms = a.stats[c] / (float)M;   // mean of (z - shift)
+      const float var = fmaxf(a.stats[C + c] / (float)M - ms * ms, 0.f);
+      mean = ms + (a.shift ? a.shift[c] : 0.f);
+      inv = rsqrtf(var + eps);
+      if (blockIdx.x == 0) {
+        a.smean[c] = mean;
+        a.sinv[c] = inv;
+        if (a.rmean) {
+          a.rmean[c] = (1.f - mom) * a.rmean[c] + mom * mean;
+          a.rvar[c] = (1.f - mom) * a.rvar[c] + mom * var * ((float)M / (float)max(M - 1, 1));
+        }
+      }
+    } else {
+      mean = a.rmean[c];
+      inv = rsqrtf(a.rvar[c] + eps);
+    }
+    sc[c] = a.gamma[c] * inv;
+    sh[c] = a.beta[c] - mean * sc[c];
+  }
+  if (train && blockIdx.x == 0 && threadIdx.x == 0 && a.nbt) a.nbt[0] += 1;
+}
+
+// y = act(bnA(z) [+ res | + bnB(z2)])      res_mode: 0 none, 1 identity residual, 2 second BN branch
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ z, BNArgs A, const bf16* __restrict__ z2,
+                                                       BNArgs B, const bf16* __restrict__ res, bf16* __restrict__ y,
+                                                       int M, int C, float eps, float mom, int train, int relu,
+                                                       int res_mode) {
+  extern __shared__ float co[];   // [4][C]
+  float* sc = co;
+  float* sh = co + C;
+  float* sc2 = co + 2 * C;
+  float* sh2 = co + 3 * C;
+  bn_coeffs(A, C, M, eps, mom, train, sc, sh);
+  if (res_mode == 2) bn_coeffs(B, C, M, eps, mom, train, sc2, sh2);
+  __syncthreads();
+  const int VR = C >> 3;
+  const long nv = (long)M * VR;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % VR) * 8;
+    float v[8];
+    load8f(z + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[c0 + j] + sh[c0 + j];
+    if (res_mode == 1) {
+      float r[8];
+      load8f(res + i * 8, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    } else if (res_mode == 2) {
+      float r[8];
+      load8f(z2 + i * 8, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j] * sc2[c0 + j] + sh2[c0 + j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+    }
+    store8f(y + i * 8, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// BN backward. g = (dya [+ dyb]) * (y > 0 if relu).  Per channel:
+//   red[0] = sum g,  red[1] = sum g * xhatA,  red[2] = sum g * xhatB
+struct BwdIn {
+  const bf16* dya;
+  const bf16* dyb;        // optional second incoming grad (residual fan-in)
+  const bf16* y;          // forward output (ReLU mask) or null
+  const bf16* za;
+  const float* meanA;
+  const float* invA;
+  const bf16* zb;         // optional second BN branch (projection shortcut)
+  const float* meanB;
+  const float* invB;
+};
+
+FEDMI_DEV void load_g(const BwdIn& in, long i, float* g) {
+  load8f(in.dya + i * 8, g);
+  if (in.dyb) {
+    float t[8];
+    load8f(in.dyb + i * 8, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] += t[j];
+  }
+  if (in.y) {
+    float t[8];
+    load8f(in.y + i * 8, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = t[j] > 0.f ? g[j] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BwdIn in, float* __restrict__ red, int M, int C,
+                                                            int rows_per_block) {
+  __shared__ float part[3][256][8];
+  const int VR = C >> 3;                 // host: blockDim.x % VR == 0
+  const int cg = threadIdx.x % VR, rstep = blockDim.x / VR, r0 = threadIdx.x / VR;
+  const int c0 = cg * 8;
+  float ma[8], ia[8], mb[8], ib[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ma[j] = in.meanA[c0 + j]; ia[j] = in.invA[c0 + j];
+    mb[j] = in.zb ? in.meanB[c0 + j] : 0.f; ib[j] = in.zb ? in.invB[c0 + j] : 0.f;
+  }
+  float s0[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = s2[j] = 0.f;
+  const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
+  for (int r = rb + r0; r < re; r += rstep) {
+    const long i = (long)r * VR + cg;
+    float g[8], z[8];
+    load_g(in, i, g);
+    load8f(in.za + i * 8, z);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s0[j] += g[j];
+      s1[j] += g[j] * (z[j] - ma[j]) * ia[j];
+    }
+    if (in.zb) {
+      load8f(in.zb + i * 8, z);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s2[j] += g[j] * (z[j] - mb[j]) * ib[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    part[0][threadIdx.x][j] = s0[j];
+    part[1][threadIdx.x][j] = s1[j];
+    part[2][threadIdx.x][j] = s2[j];
+  }
+  __syncthreads();
+  // threads < 3*C: one (quantity, channel) sum over the rstep partials
+  for (int e = threadIdx.x; e < 3 * C; e += blockDim.x) {
+    const int qn = e / C, c = e - qn * C;
+    if (qn == 2 && !in.zb) continue;
+    const int g = c >> 3, j = c & 7;
+    float s = 0.f;
+    for (int t = g; t < (int)blockDim.x; t += VR) s += part[qn][t][j];
+    unsafeAtomicAdd(red + qn * C + c, s);
+  }
+}
+
+struct BwdOut {
+  bf16* dza;              // grad wrt za (conv output of branch A)
+  bf16* dzb;              // grad wrt zb (branch B) or null
+  bf16* gout;             // masked incoming grad g (identity-shortcut grad) or null
+  float* dgammaA;
+  float* dbetaA;
+  float* dgammaB;
+  float* dbetaB;
+  const float* gammaA;
+  const float* gammaB;
+  float* shiftA;          // <- this step's batch mean: the next step's statistics shift
+  float* shiftB;
+};
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdIn in, BwdOut out, const float* __restrict__ red,
+                                                           int M, int C) {
+  extern __shared__ float co[];   // [6][C]: kA, bA, cA, kB, bB, cB  (dz = k*g + b*xhat + c)
+  const float invM = 1.f / (float)M;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float sg = red[c], sgx = red[C + c];
+    const float scA = out.gammaA[c] * in.invA[c];
+    // dz = scA * (g - sg/M - xhat * sgx/M),  xhat = (z - mean) * inv
+    co[c] = scA;
+    co[C + c] = -scA * sgx * invM * in.invA[c];
+    co[2 * C + c] = -scA * sg * invM + scA * sgx * invM * in.invA[c] * in.meanA[c];
+    if (blockIdx.x == 0) {
+      out.dgammaA[c] = sgx;
+      out.dbetaA[c] = sg;
+      if (out.shiftA) out.shiftA[c] = in.meanA[c];
+    }
+    if (in.zb) {
+      const float sgx2 = red[2 * C + c];
+      const float scB = out.gammaB[c] * in.invB[c];
+      co[3 * C + c] = scB;
+      co[4 * C + c] = -scB * sgx2 * invM * in.invB[c];
+      co[5 * C + c] = -scB * sg * invM + scB * sgx2 * invM * in.invB[c] * in.meanB[c];
+      if (blockIdx.x == 0) {
+        out.dgammaB[c] = sgx2;
+        out.dbetaB[c] = sg;
+        if (out.shiftB) out.shiftB[c] = in.meanB[c];
+      }
+    }
+  }
+  __syncthreads();
+  const int VR = C >> 3;
+  const long nv = (long)M * VR;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % VR) * 8;
+    float g[8], z[8], d[8];
+    load_g(in, i, g);
+    if (out.gout) store8f(out.gout + i * 8, g);
+    load8f(in.za + i * 8, z);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = co[c0 + j] * g[j] + co[C + c0 + j] * z[j] + co[2 * C + c0 + j];
+    store8f(out.dza + i * 8, d);
+    if (in.zb) {
+      load8f(in.zb + i * 8, z);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = co[3 * C + c0 + j] * g[j] + co[4 * C + c0 + j] * z[j] + co[5 * C + c0 + j];
+      store8f(out.dzb + i * 8, d);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Classifier head: y [N][HW][C] -> avgpool -> linear (J <= 16) -> CE.
+// One workgroup per sample. Stats layout as lenet::Stats {loss_sum, correct, count, pad}.
+__global__ __launch_bounds__(256) void head_fwd_bwd_kernel(const bf16* __restrict__ y, const int* __restrict__ labels,
+                                                           int base, const int* __restrict__ dbase, int HW, int C, int J, const float* __restrict__ W,
+                                                           const float* __restrict__ b, float* __restrict__ pooled,
+                                                           float* __restrict__ dlog, bf16* __restrict__ dy,
+                                                           float* __restrict__ stats, int N, int train) {
+  extern __shared__ float sm[];   // pooled[C], logits[16], dl[16]
+  float* pl = sm;
+  float* lg = sm + C;
+  float* dl = lg + 16;
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16* yn = y + (size_t)n * HW * C;
+  const float invHW = 1.f / (float)HW;
+  for (int c = tid; c < C; c += 256) {
+    float s = 0.f;
+    for (int p = 0; p < HW; ++p) s += (float)yn[(size_t)p * C + c];
+    pl[c] = s * invHW;
+    if (train) pooled[(size_t)n * C + c] = s * invHW;
+  }
+  __syncthreads();
+  for (int j = wave; j < J; j += 4) {
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += W[(size_t)j * C + c] * pl[c];
+    s = wave_sum(s);
+    if (lane == 0) lg[j] = s + b[j];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int lab = labels[base + (dbase ? dbase[0] : 0) + n];
+    float mx = lg[0];
+    int am = 0;
+    for (int j = 1; j < J; ++j)
+      if (lg[j] > mx) { mx = lg[j]; am = j; }
+    float se = 0.f;
+    for (int j = 0; j < J; ++j) se += __expf(lg[j] - mx);
+    const float lse = mx + __logf(se);
+    atomicAdd(stats, lse - lg[lab]);
+    atomicAdd(reinterpret_cast<int*>(stats) + 1, am == lab ? 1 : 0);
+    atomicAdd(reinterpret_cast<int*>(stats) + 2, 1);
+    for (int j = 0; j < J; ++j) {
+      const float p = __expf(lg[j] - lse);
+      dl[j] = (p - (j == lab ? 1.f : 0.f)) / (float)N;
+      if (train) dlog[(size_t)n * J + j] = dl[j];
+    }
+  }
+  if (!train) return;
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float s = 0.f;
+    for (int j = 0; j < J; ++j) s += W[(size_t)j * C + c] * dl[j];
+    pl[c] = s * invHW;   // reuse: d pooled / HW
+  }
+  __syncthreads();
+  bf16* dyn = dy + (size_t)n * HW * C;
+  for (int e = tid; e < HW * C; e += 256) dyn[e] = (bf16)pl[e % C];
+}
+
+// dW[j][c] = sum_n dlog[n][j] * pooled[n][c];  db[j] = sum_n dlog[n][j]
+__global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict__ pooled, const float* __restrict__ dlog,
+                                                         int N, int C, int J, float* __restrict__ dW,
+                                                         float* __restrict__ db) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < J * C) {
+    const int j = e / C, c = e - j * C;
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += dlog[(size_t)n * J + j] * pooled[(size_t)n * C + c];
+    dW[e] = s;
+  } else if (e < J * C + J) {
+    const int j = e - J * C;
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += dlog[(size_t)n * J + j];
+    db[j] = s;
+  }
+}
+
+// cur[0] = sched[counter[0]++]  (first node of a captured training step)
+__global__ void sched_next_kernel(const int* __restrict__ sched, int* __restrict__ counter, int* __restrict__ cur) {
+  if (threadIdx.x == 0) {
+    const int i = counter[0];
+    cur[0] = sched[i];
+    counter[0] = i + 1;
+  }
+}
+
+int grid_for(long nv) { return (int)std::min<long>((nv + 255) / 256, 2048); }
+
+}  // namespace
+
+namespace fedmi {
+
+struct BNDesc {
+  const float* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
+  float* smean; float* sinv; const float* shift;
+};
+
+static BNArgs to_args(const BNDesc& d) {
+  return BNArgs{d.stats, d.gamma, d.beta, d.rmean, d.rvar, d.nbt, d.smean, d.sinv, d.shift};
+}
+
+void launch_prep_input(hipStream_t st, const uint8_t* images, int base, const int* dbase, int nb, int augment,
+                       uint32_t seed, const int* round_ctr, bf16* out) {
+  hipLaunchKernelGGL(prep_input_kernel, dim3((nb * 1024 + 255) / 256), dim3(256), 0, st, images, base, dbase, nb,
+                     augment, seed, round_ctr, out);
+}
+
+void launch_sched_next(hipStream_t st, const int* sched, int* counter, int* cur) {
+  hipLaunchKernelGGL(sched_next_kernel, dim3(1), dim3(64), 0, st, sched, counter, cur);
+}
+
+void launch_bn_apply(hipStream_t st, const bf16* z, const BNDesc& a, const bf16* z2, const BNDesc* b, const bf16* res,
+                     bf16* y, int M, int C, float eps, float mom, int train, int relu) {
+  if (C % 8) throw std::invalid_argument("bn_apply: C % 8 != 0");
+  const int res_mode = b ? 2 : (res ? 1 : 0);
+  const BNArgs bb = b ? to_args(*b) : BNArgs{};
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((long)M * (C / 8))), dim3(256), 4 * C * sizeof(float), st, z,
+                     to_args(a), z2, bb, res, y, M, C, eps, mom, train, relu, res_mode);
+}
+
+struct BNBwdDesc {
+  const bf16* dya; const bf16* dyb; const bf16* y;
+  const bf16* za; const float* meanA; const float* invA; const float* gammaA; float* dgammaA; float* dbetaA; bf16* dza;
+  const bf16* zb; const float* meanB; const float* invB; const float* gammaB; float* dgammaB; float* dbetaB; bf16* dzb;
+  bf16* gout;
+  float* shiftA; float* shiftB;
+};
+
+// red: [3][C] fp32 accumulator, must be zero on entry (callers zero all BN
+// accumulators of a step with one fill, keeping memset nodes out of graphs)
+void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, float* red, int M, int C) {
+  const int VR = C / 8;
+  if (C % 8 || VR > 256) throw std::invalid_argument("bn_bwd: need C % 8 == 0 and C <= 2048");
+  const int tb = (256 / VR) * VR;   // block size a multiple of C/8: fixed channel group per thread
+  BwdIn in{d.dya, d.dyb, d.y, d.za, d.meanA, d.invA, d.zb, d.meanB, d.invB};
+  BwdOut out{d.dza, d.dzb, d.gout, d.dgammaA, d.dbetaA, d.dgammaB, d.dbetaB, d.gammaA, d.gammaB, d.shiftA, d.shiftB};
+  // ~2 row-blocks per CU worth of work, >= 64 rows each
+  const int rows_per_block = std::max(64, (M + 511) / 512);
+  const int nblk = (M + rows_per_block - 1) / rows_per_block;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(tb), 0, st, in, red, M, C, rows_per_block);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for((long)M * VR)), dim3(256), 6 * C * sizeof(float), st, in, out,
+                     red, M, C);
+}
+
+void launch_head(hipStream_t st, const bf16* y, const int* labels, int base, const int* dbase, int N, int HW, int C, int J,
+                 const float* W, const float* b, float* pooled, float* dlog, bf16* dy, float* stats, float* dW,
+                 float* db, int train) {
+  if (J > 16) throw std::invalid_argument("head: at most 16 classes");
+  hipLaunchKernelGGL(head_fwd_bwd_kernel, dim3(N), dim3(256), (C + 32) * sizeof(float), st, y, labels, base, dbase, HW, C,
+                     J, W, b, pooled, dlog, dy, stats, N, train);
+  if (train)
+    hipLaunchKernelGGL(head_wgrad_kernel, dim3((J * C + J + 255) / 256), dim3(256), 0, st, pooled, dlog, N, C, J, dW,
+                       db);
+}
+
+}  // namespace fedmi

@@ -1,0 +1,583 @@
+// fedmi — implicit-GEMM 2-D convolution on gfx950 MFMA (bf16 in, fp32 acc).
+//
+// One kernel template serves the three convolution GEMMs of training, all on
+// NHWC (channels-last) bf16 activations and an [O][R][S][C] bf16 weight image
+// ("W_rsc", packed from the fp32 master [O][C][R][S] by conv_pack_weights):
+//
+//   FWD    Y[m=(n,p,q)][o]     = sum_{k=(r,s,c)} X[n][p*st-pad+r][q*st-pad+s][c] * W[o][r][s][c]
+//   DGRAD  dX[m=(n,h,w)][c]    = sum_{k=(r,s,o)} dY[n][(h+pad-r)/st][(w+pad-s)/st][o] * W[o][r][s][c]
+//   WGRAD  dW[o][j=(r,s,c)]   += sum_{k=m=(n,p,q)} dY[m][o] * X[n][p*st-pad+r][q*st-pad+s][c]   (split-K)
+//
+// Tiles: BM x BN output tile, BK = 64, 256 threads = 4 waves in a 2x2 grid,
+// each wave (BM/2) x (BN/2) of 16x16 MFMA sub-tiles (v_mfma_f32_16x16x32_bf16).
+// Operands are staged global -> registers -> LDS (double-buffered LDS, one
+// barrier per K step, the next tile's loads in flight behind the MFMAs).
+// Each operand tile is stored in the layout it has in global memory:
+//   * "KC"  (K contiguous: im2col rows of X / dY, W_rsc rows)  -> [rows][BK+8]
+//     image, MFMA fragments read with ds_read_b128 (16-B row reads; the +8
+//     element pad makes the 16 rows of a fragment hit distinct bank groups).
+//   * "MNC" (M/N contiguous: weight columns for DGRAD, pixel-major dY / X for
+//     WGRAD) -> [BK][cols] image with a 32-byte-segment XOR swizzle, fragments
+//     read with ds_read_b64_tr_b16 (gfx950 hardware transpose; conflict-free
+//     for the swizzle below).
+// So no operand is ever transposed in registers or through extra buffers.
+//
+// Epilogues: FWD writes bf16 Y and (optionally) per-channel sum / sum-of-
+// squares for the following BatchNorm (training batch statistics fused into
+// the conv); DGRAD writes bf16 dX; WGRAD atomically adds the
+// fp32 partial into the PyTorch-layout [O][C][R][S] gradient (split-K over
+// output pixels, gridDim.z splits).
+//
+// Reference parity: these are the convolution / convolution_backward ops of
+// every zoo model (src/models/resnet.py:14-104 etc.).
+#include <algorithm>
+#include <stdexcept>
+
+#include "common.h"
+
+namespace {
+
+struct FastDiv {   // q = x / d for 0 <= x < 2^31 (Granlund-Montgomery)
+  uint32_t d, m, s;
+};
+FEDMI_DEV uint32_t fdiv(uint32_t x, const FastDiv& f) { return (__umulhi(x, f.m) + x) >> f.s; }
+
+struct ConvGeom {
+  int N, H, W, C;          // input (C = padded channel count, % 8 == 0)
+  int O, P, Q;             // output channels / spatial
+  int R, S, st, pad;
+  int M, NC, K;            // GEMM rows / cols / reduction for the launched mode
+  int Cw;                  // channel count of the fp32 master weight (unpadded; WGRAD epilogue)
+  // DGRAD sub-pixel phase (stride 2: one launch per output parity (ph, pw), each
+  // summing only the taps r = r0 + 2i, s = s0 + 2j that land on that parity;
+  // stride 1: ph = pw = 0, r0 = s0 = 0, nr = R, ns = S, Hp = H, Wp = W)
+  int ph, pw, r0, s0, nr, ns, Hp, Wp;
+  FastDiv dC, dO, dS, dQ, dPQ, dW, dHW, dNS, dWp, dHWp;
+};
+
+enum { FWD = 0, DGRAD = 1, WGRAD = 2 };
+constexpr int BK = 64;
+constexpr int KC_LD = BK + 8;   // KC image row stride (elements): 144 B = 9 x 16 B
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+FEDMI_DEV uint4 zero_u4() { return make_uint4(0u, 0u, 0u, 0u); }
+FEDMI_DEV uint4 ld16(const bf16* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// MNC image: [BK rows][COLS] bf16, 32-byte segments XOR-swizzled by row so that
+// a ds_read_b64_tr_b16 (per 32-lane half: rows k0..k0+3 and k0+8..k0+11 of one
+// 16-column block) touches 64 distinct banks.
+template <int COLS>
+FEDMI_DEV int mnc_off(int row, int col) {
+  if constexpr (COLS == 128) {
+    const int f = (row & 3) | (((row >> 3) & 1) << 2);
+    return row * 128 + ((((col >> 4) ^ f)) << 4) + (col & 15);
+  } else {   // 64
+    const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+    return row * 64 + ((((col >> 4) ^ f)) << 4) + (col & 15);
+  }
+}
+
+// Fragment readers (16x16x32 operand of rows/cols [i0, i0+16), k in [kk*32, kk*32+32)).
+FEDMI_DEV bf16x8 frag_kc(const bf16* img, int i0, int kk, int lane) {
+  return *reinterpret_cast<const bf16x8*>(img + (i0 + (lane & 15)) * KC_LD + kk * 32 + (lane >> 4) * 8);
+}
+
+template <int COLS>
+FEDMI_DEV bf16x8 frag_mnc(const bf16* img, int i0, int kk, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int row0 = kk * 32 + 8 * g + q;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const bf16* a0 = img + mnc_off<COLS>(row0, i0 + 4 * p);
+  const bf16* a1 = img + mnc_off<COLS>(row0 + 4, i0 + 4 * p);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  // whole-vector bit casts: per-element short->bf16 casts of the tr16 result were
+  // miscompiled (elements 2,3 duplicated from 0,1)
+  const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo);
+  const bf16x4 h4 = __builtin_bit_cast(bf16x4, hi);
+  return __builtin_shufflevector(l4, h4, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// ---------------------------------------------------------------------------
+// Per-thread operand loaders. Each thread owns NCH 16-byte chunks of each
+// operand tile per K step; the chunk -> (row, k-chunk) map is fixed across the
+// K loop, so per-row decode work is hoisted out of it.
+// ---------------------------------------------------------------------------
+template <int MODE, int BM, int BN>
+struct Loader {
+  static constexpr int NA = BM * BK / 8 / 256;   // chunks per thread, A
+  static constexpr int NB = BN * BK / 8 / 256;
+  // A rows (KC: FWD/DGRAD) or k-rows (MNC: WGRAD)
+  int a_row[NA], a_kc[NA];
+  int a_n[NA], a_h[NA], a_w[NA];   // FWD: n, p*st-pad, q*st-pad ; DGRAD: n, h+pad, w+pad
+  bool a_ok[NA];
+  int b_row[NB], b_kc[NB];
+  int b_r[NB], b_s[NB], b_c[NB];   // WGRAD: fixed (r,s,c) of the column chunk
+  bool b_ok[NB];
+
+  FEDMI_DEV void init(const ConvGeom& g, int m0, int n0, int tid) {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      const int c = tid + 256 * u;
+      if constexpr (MODE == WGRAD) {          // MNC: [BK][BM]
+        a_row[u] = c / (BM / 8);
+        a_kc[u] = c % (BM / 8);
+        a_ok[u] = m0 + a_kc[u] * 8 < g.M;     // o chunk in range (O % 8 == 0)
+      } else {                                // KC: [BM][BK]
+        a_row[u] = c >> 3;
+        a_kc[u] = c & 7;
+        const int m = m0 + a_row[u];
+        a_ok[u] = m < g.M;
+        const uint32_t mm = a_ok[u] ? m : 0;
+        if constexpr (MODE == FWD) {
+          const uint32_t n = fdiv(mm, g.dPQ), pq = mm - n * g.P * g.Q;
+          const uint32_t p = fdiv(pq, g.dQ), q = pq - p * g.Q;
+          a_n[u] = n; a_h[u] = p * g.st - g.pad; a_w[u] = q * g.st - g.pad;
+        } else {   // DGRAD: row -> (n, hh, ww) of this phase -> input pixel (h, w)
+          const uint32_t n = fdiv(mm, g.dHWp), hw = mm - n * g.Hp * g.Wp;
+          const uint32_t hh = fdiv(hw, g.dWp), ww = hw - hh * g.Wp;
+          a_n[u] = n; a_h[u] = hh * g.st + g.ph + g.pad; a_w[u] = ww * g.st + g.pw + g.pad;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int c = tid + 256 * u;
+      if constexpr (MODE == FWD) {            // KC: [BN][BK] rows o
+        b_row[u] = c >> 3;
+        b_kc[u] = c & 7;
+        b_ok[u] = n0 + b_row[u] < g.NC;
+      } else {                                // MNC: [BK][BN]
+        b_row[u] = c / (BN / 8);
+        b_kc[u] = c % (BN / 8);
+        const int j = n0 + b_kc[u] * 8;
+        b_ok[u] = j < g.NC;
+        if constexpr (MODE == WGRAD) {
+          const uint32_t jj = b_ok[u] ? j : 0;
+          const uint32_t rs = fdiv(jj, g.dC), cc = jj - rs * g.C;
+          const uint32_t r = fdiv(rs, g.dS), s = rs - r * g.S;
+          b_r[u] = r; b_s[u] = s; b_c[u] = cc;
+        }
+      }
+    }
+  }
+
+  // Load the K step starting at k0 into registers (unconditional loads from a
+  // clamped address, then select: no per-load branches).
+  FEDMI_DEV void load(const ConvGeom& g, const bf16* __restrict__ x, const bf16* __restrict__ w,
+                      const bf16* __restrict__ dy, int k0, int m0, int n0, uint4* ra, uint4* rb) const {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      if constexpr (MODE == FWD) {
+        const int k = k0 + a_kc[u] * 8;
+        const uint32_t rs = fdiv(k, g.dC), cc = k - rs * g.C;
+        const uint32_t r = fdiv(rs, g.dS), s = rs - r * g.S;
+        const int h = a_h[u] + (int)r, ww = a_w[u] + (int)s;
+        const bool ok = a_ok[u] && k < g.K && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+        const long off = ok ? (((long)a_n[u] * g.H + h) * g.W + ww) * g.C + cc : 0;
+        const uint4 v = ld16(x + off);
+        ra[u] = ok ? v : zero_u4();
+      } else if constexpr (MODE == DGRAD) {
+        const int k = k0 + a_kc[u] * 8;
+        const uint32_t t = fdiv(k, g.dO), o = k - t * g.O;
+        const uint32_t i = fdiv(t, g.dNS), j = t - i * g.ns;
+        const int r = g.r0 + (int)i * g.st, s = g.s0 + (int)j * g.st;
+        int y = a_h[u] - r, xx = a_w[u] - s;   // divisible by st by the phase's tap choice
+        bool ok = a_ok[u] && k < g.K && y >= 0 && xx >= 0;
+        if (g.st == 2) { y >>= 1; xx >>= 1; }
+        ok = ok && y < g.P && xx < g.Q;
+        const long off = ok ? (((long)a_n[u] * g.P + y) * g.Q + xx) * g.O + o : 0;
+        const uint4 v = ld16(dy + off);
+        ra[u] = ok ? v : zero_u4();
+      } else {   // WGRAD A: dY[m][o], k-row = pixel
+        const int m = k0 + a_row[u];
+        const bool ok = a_ok[u] && m < g.K;
+        const long off = ok ? (long)m * g.O + m0 + a_kc[u] * 8 : 0;
+        const uint4 v = ld16(dy + off);
+        ra[u] = ok ? v : zero_u4();
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      if constexpr (MODE == FWD) {   // W_rsc[o][k]
+        const int k = k0 + b_kc[u] * 8;
+        const bool ok = b_ok[u] && k < g.K;
+        const long off = ok ? (long)(n0 + b_row[u]) * g.K + k : 0;
+        const uint4 v = ld16(w + off);
+        rb[u] = ok ? v : zero_u4();
+      } else if constexpr (MODE == DGRAD) {   // k-row = (tap, o), cols c: W_rsc[o][r][s][c]
+        const int k = k0 + b_row[u];
+        const uint32_t kk = k < g.K ? k : 0;
+        const uint32_t t = fdiv(kk, g.dO), o = kk - t * g.O;
+        const uint32_t i = fdiv(t, g.dNS), j = t - i * g.ns;
+        const int rs = (g.r0 + (int)i * g.st) * g.S + g.s0 + (int)j * g.st;
+        const bool ok = b_ok[u] && k < g.K;
+        const long off = ok ? ((long)o * g.R * g.S + rs) * g.C + n0 + b_kc[u] * 8 : 0;
+        const uint4 v = ld16(w + off);
+        rb[u] = ok ? v : zero_u4();
+      } else {   // WGRAD B: k-row = pixel m=(n,p,q), cols (r,s,c)
+        const int m = k0 + b_row[u];
+        const uint32_t mm = m < g.K ? m : 0;
+        const uint32_t n = fdiv(mm, g.dPQ), pq = mm - n * g.P * g.Q;
+        const uint32_t p = fdiv(pq, g.dQ), q = pq - p * g.Q;
+        const int h = (int)(p * g.st) - g.pad + b_r[u], ww = (int)(q * g.st) - g.pad + b_s[u];
+        const bool ok = b_ok[u] && m < g.K && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+        const long off = ok ? (((long)n * g.H + h) * g.W + ww) * g.C + b_c[u] : 0;
+        const uint4 v = ld16(x + off);
+        rb[u] = ok ? v : zero_u4();
+      }
+    }
+  }
+
+  FEDMI_DEV void store(bf16* As, bf16* Bs, const uint4* ra, const uint4* rb) const {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      bf16* d = (MODE == WGRAD) ? As + mnc_off<BM>(a_row[u], a_kc[u] * 8) : As + a_row[u] * KC_LD + a_kc[u] * 8;
+      *reinterpret_cast<uint4*>(d) = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      bf16* d = (MODE == FWD) ? Bs + b_row[u] * KC_LD + b_kc[u] * 8 : Bs + mnc_off<BN>(b_row[u], b_kc[u] * 8);
+      *reinterpret_cast<uint4*>(d) = rb[u];
+    }
+  }
+};
+
+template <int MODE, int BM, int BN>
+__global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                  const bf16* __restrict__ dy, bf16* __restrict__ out,
+                                                  float* __restrict__ gout, float* __restrict__ stats,
+                                                  const float* __restrict__ shift, ConvGeom g,
+                                                  int ksteps_per_split) {
+  constexpr int A_IMG = (MODE == WGRAD) ? BK * BM : BM * KC_LD;
+  constexpr int B_IMG = (MODE == FWD) ? BN * KC_LD : BK * BN;
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_IMG + B_IMG)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = (g.NC + BN - 1) / BN;
+  const int tile_n = blockIdx.x % ntn, tile_m = blockIdx.x / ntn;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int wm0 = (wave >> 1) * WM, wn0 = (wave & 1) * WN;
+
+  const int ksteps = (g.K + BK - 1) / BK;
+  const int kb = blockIdx.z * ksteps_per_split;
+  const int ke = min(ksteps, kb + ksteps_per_split);
+  if (MODE == WGRAD && kb >= ke) return;   // (never launched: every split owns >= 1 step)
+
+  Loader<MODE, BM, BN> L;
+  L.init(g, m0, n0, tid);
+  uint4 ra[Loader<MODE, BM, BN>::NA], rb[Loader<MODE, BM, BN>::NB];
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+
+  if (kb < ke) {   // a DGRAD phase with no taps (1x1 stride 2, odd parity) just writes zeros
+    L.load(g, x, w, dy, kb * BK, m0, n0, ra, rb);
+    L.store(smem, smem + A_IMG, ra, rb);
+  }
+  __syncthreads();
+
+  for (int t = kb; t < ke; ++t) {
+    const int buf = (t - kb) & 1;
+    const bf16* As = smem + buf * (A_IMG + B_IMG);
+    const bf16* Bs = As + A_IMG;
+    const bool more = t + 1 < ke;
+    if (more) L.load(g, x, w, dy, (t + 1) * BK, m0, n0, ra, rb);
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = (MODE == WGRAD) ? frag_mnc<BM>(As, wm0 + 16 * i, kk, lane) : frag_kc(As, wm0 + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = (MODE == FWD) ? frag_kc(Bs, wn0 + 16 * j, kk, lane) : frag_mnc<BN>(Bs, wn0 + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    if (more) {
+      bf16* Ad = smem + (buf ^ 1) * (A_IMG + B_IMG);
+      L.store(Ad, Ad + A_IMG, ra, rb);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  if constexpr (MODE == WGRAD) {
+    // fp32 partial of this K split -> workspace [split][O][R*S*C] (natural GEMM
+    // layout, plain stores); conv_wgrad_reduce sums the splits and permutes
+    // into the PyTorch [O][Cw][R][S] gradient.
+    float* ws = gout + (long)blockIdx.z * g.M * g.NC;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn0 + 16 * j + col_l;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int o = m0 + wm0 + 16 * i + row_l + e;
+          if (o < g.M && col < g.NC) ws[(long)o * g.NC + col] = acc[i][j][e];
+        }
+    }
+  } else {
+    // Stage the bf16 tile through LDS, then 16-byte row stores; FWD also sums
+    // each column (BatchNorm batch statistics) with one atomic per column per WG.
+    constexpr int CT_LD = BN + 8;
+    bf16* ct = smem;
+    float* red = reinterpret_cast<float*>(smem + BM * CT_LD);   // [256/BN parts][2][BN]
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          ct[(wm0 + 16 * i + row_l + e) * CT_LD + wn0 + 16 * j + col_l] = (bf16)acc[i][j][e];
+    __syncthreads();
+    constexpr int CPR = BN / 8;   // 16-B chunks per tile row
+    for (int c = tid; c < BM * CPR; c += 256) {
+      const int row = c / CPR, cc = c % CPR;
+      const int m = m0 + row, col = n0 + cc * 8;
+      long orow = m;
+      if (MODE == DGRAD && g.st != 1) {   // phase row -> input pixel row
+        const uint32_t n = fdiv(m, g.dHWp), hw = m - n * g.Hp * g.Wp;
+        const uint32_t hh = fdiv(hw, g.dWp), ww = hw - hh * g.Wp;
+        orow = ((long)n * g.H + hh * g.st + g.ph) * g.W + ww * g.st + g.pw;
+      }
+      if (m < g.M && col < g.NC)
+        *reinterpret_cast<uint4*>(out + orow * g.NC + col) = *reinterpret_cast<const uint4*>(ct + row * CT_LD + cc * 8);
+    }
+    if (MODE == FWD && stats != nullptr) {
+      // sums of (y - shift[c]): shift = the previous step's batch mean of this
+      // BN (kept by bn_bwd), so E[d^2] - E[d]^2 does not cancel catastrophically
+      constexpr int PARTS = 256 / BN;
+      const int col = tid % BN, part = tid / BN;
+      const int rows = min(BM, g.M - m0);
+      const float sh = (shift != nullptr && n0 + col < g.NC) ? shift[n0 + col] : 0.f;
+      float s1 = 0.f, s2 = 0.f;
+      for (int r = part; r < rows; r += PARTS) {
+        const float v = (float)ct[r * CT_LD + col] - sh;   // statistics of the values the next layer reads
+        s1 += v;
+        s2 += v * v;
+      }
+      red[(part * 2) * BN + col] = s1;
+      red[(part * 2 + 1) * BN + col] = s2;
+      __syncthreads();
+      if (tid < 2 * BN) {
+        const int q = tid / BN, cl = tid % BN;
+        float t = 0.f;
+#pragma unroll
+        for (int pp = 0; pp < PARTS; ++pp) t += red[(pp * 2 + q) * BN + cl];
+        if (n0 + cl < g.NC) unsafeAtomicAdd(stats + q * g.NC + n0 + cl, t);
+      }
+    }
+  }
+}
+
+// dW[o][c][r][s] (+)= sum_z ws[z][o][(r*S + s)*C + c]     (c < Cw)
+__global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict__ ws, int splits, int O, int C, int Cw,
+                                                         int RS, float* __restrict__ dw, int accumulate) {
+  const long total = (long)O * Cw * RS;
+  const long plane = (long)O * RS * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int rs = i % RS;
+    const long t = i / RS;
+    const int c = t % Cw, o = t / Cw;
+    const long src = ((long)o * RS + rs) * C + c;
+    float v = accumulate ? dw[i] : 0.f;
+    for (int z = 0; z < splits; ++z) v += ws[z * plane + src];
+    dw[i] = v;
+  }
+}
+
+// W fp32 [O][Cw][R][S] -> W_rsc bf16 [O][R][S][C]   (C = Cw padded to 8; pad = 0)
+__global__ __launch_bounds__(256) void conv_pack_kernel(const float* __restrict__ w, bf16* __restrict__ wr, int O, int Cw,
+                                                        int C, int RS) {
+  const long total = (long)O * RS * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = i % C;
+    const long t = i / C;
+    const int rs = t % RS, o = t / RS;
+    wr[i] = c < Cw ? (bf16)w[((long)o * Cw + c) * RS + rs] : (bf16)0.f;
+  }
+}
+
+FastDiv make_div(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
+  return f;
+}
+
+}  // namespace
+
+namespace fedmi {
+
+struct ConvShape {
+  int N, H, W, C, Cw, O, P, Q, R, S, st, pad;
+};
+
+static ConvGeom make_geom(const ConvShape& s) {
+  ConvGeom g{};
+  g.N = s.N; g.H = s.H; g.W = s.W; g.C = s.C; g.O = s.O; g.P = s.P; g.Q = s.Q;
+  g.R = s.R; g.S = s.S; g.st = s.st; g.pad = s.pad; g.Cw = s.Cw;
+  g.dC = make_div(s.C); g.dO = make_div(s.O); g.dS = make_div(s.S); g.dQ = make_div(s.Q);
+  g.dPQ = make_div(s.P * s.Q); g.dW = make_div(s.W); g.dHW = make_div(s.H * s.W);
+  g.ph = g.pw = 0; g.r0 = g.s0 = 0; g.nr = s.R; g.ns = s.S; g.Hp = s.H; g.Wp = s.W;
+  g.dNS = make_div(s.S); g.dWp = make_div(s.W); g.dHWp = make_div(s.H * s.W);
+  return g;
+}
+
+static void check_shape(const ConvShape& s) {
+  if (s.C % 8 || s.O % 8 || s.C < s.Cw || s.st < 1 || s.st > 2 || s.R < 1 || s.S < 1)
+    throw std::invalid_argument("conv_igemm: need C % 8 == 0, O % 8 == 0, stride 1|2");
+  if (s.P != (s.H + 2 * s.pad - s.R) / s.st + 1 || s.Q != (s.W + 2 * s.pad - s.S) / s.st + 1)
+    throw std::invalid_argument("conv_igemm: inconsistent output size");
+  if ((long)s.N * s.H * s.W * s.C >= (1l << 31) || (long)s.N * s.P * s.Q * s.O >= (1l << 31))
+    throw std::invalid_argument("conv_igemm: tensor too large for 32-bit index math");
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+struct TileCfg {
+  int BM, BN;
+};
+
+static TileCfg pick_tiles(int M, int NC) {
+  const int cus = num_cus();
+  const int BN = NC <= 64 ? 64 : 128;
+  const long t128 = (long)((M + 127) / 128) * ((NC + BN - 1) / BN);
+  return TileCfg{(M > 64 && t128 >= cus) ? 128 : 64, BN};
+}
+
+template <int MODE, int BM, int BN>
+static void launch_tiled(hipStream_t st, dim3 grid, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy,
+                         bf16* out, float* gout, float* stats, const float* shift, int kps) {
+  hipLaunchKernelGGL((conv_igemm<MODE, BM, BN>), grid, dim3(256), 0, st, x, w, dy, out, gout, stats, shift, g, kps);
+}
+
+template <int MODE>
+static void launch_mode(hipStream_t st, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy, bf16* out,
+                        float* gout, float* stats, int splits, const float* shift = nullptr) {
+  const TileCfg t = pick_tiles(g.M, g.NC);
+  const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
+  const int ksteps = (g.K + BK - 1) / BK;
+  if (MODE != WGRAD) splits = 1;
+  splits = std::max(1, std::min(splits, ksteps));
+  const int kps = std::max(1, (ksteps + splits - 1) / splits);
+  splits = std::max(1, (ksteps + kps - 1) / kps);
+  dim3 grid((unsigned)tiles, 1, (unsigned)splits);
+  if (t.BM == 128 && t.BN == 128) launch_tiled<MODE, 128, 128>(st, grid, g, x, w, dy, out, gout, stats, shift, kps);
+  else if (t.BM == 128) launch_tiled<MODE, 128, 64>(st, grid, g, x, w, dy, out, gout, stats, shift, kps);
+  else if (t.BN == 128) launch_tiled<MODE, 64, 128>(st, grid, g, x, w, dy, out, gout, stats, shift, kps);
+  else launch_tiled<MODE, 64, 64>(st, grid, g, x, w, dy, out, gout, stats, shift, kps);
+}
+
+// K-split count for the weight gradient: about two workgroups per CU, at least
+// 8 K steps per split, and a bounded workspace.
+static int wgrad_splits(const ConvGeom& g, long ws_cap_floats) {
+  const TileCfg t = pick_tiles(g.M, g.NC);
+  const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
+  const int ksteps = (g.K + BK - 1) / BK;
+  long sp = (2l * num_cus() + tiles - 1) / tiles;
+  sp = std::min<long>(sp, std::max(1, ksteps / 8));
+  if (ws_cap_floats > 0) sp = std::min<long>(sp, ws_cap_floats / ((long)g.M * g.NC));
+  sp = std::max<long>(1, sp);
+  const int kps = (int)((ksteps + sp - 1) / sp);
+  return (ksteps + kps - 1) / kps;
+}
+
+// Y[N,P,Q,O] = conv(X[N,H,W,C], W_rsc); stats (optional) += [sum | sumsq] of (Y - shift) per output channel.
+void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf16* wrsc, bf16* y, float* stats,
+                     const float* shift) {
+  check_shape(s);
+  ConvGeom g = make_geom(s);
+  g.M = s.N * s.P * s.Q; g.NC = s.O; g.K = s.R * s.S * s.C;
+  launch_mode<FWD>(st, g, x, wrsc, nullptr, y, nullptr, stats, 1, shift);
+}
+
+// dX[N,H,W,C] = conv_transpose(dY[N,P,Q,O], W_rsc)   (every element written).
+// Stride 2 runs as 4 sub-pixel phases so no MFMA multiplies a structural zero.
+void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const bf16* wrsc, bf16* dx) {
+  check_shape(s);
+  ConvGeom g = make_geom(s);
+  g.NC = s.C;
+  if (s.st == 1) {
+    g.M = s.N * s.H * s.W; g.K = s.R * s.S * s.O;
+    launch_mode<DGRAD>(st, g, nullptr, wrsc, dy, dx, nullptr, nullptr, 1);
+    return;
+  }
+  for (int ph = 0; ph < 2; ++ph)
+    for (int pw = 0; pw < 2; ++pw) {
+      ConvGeom q = g;
+      q.ph = ph; q.pw = pw;
+      q.r0 = (ph + s.pad) & 1; q.s0 = (pw + s.pad) & 1;
+      q.nr = std::max(0, (s.R - q.r0 + 1) / 2); q.ns = std::max(0, (s.S - q.s0 + 1) / 2);
+      q.Hp = (s.H - ph + 1) / 2; q.Wp = (s.W - pw + 1) / 2;
+      if (q.Hp <= 0 || q.Wp <= 0) continue;
+      q.dNS = make_div(std::max(q.ns, 1)); q.dWp = make_div(q.Wp); q.dHWp = make_div(q.Hp * q.Wp);
+      q.M = s.N * q.Hp * q.Wp; q.K = q.nr * q.ns * s.O;
+      launch_mode<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, 1);
+    }
+}
+
+static ConvGeom wgrad_geom(const ConvShape& s) {
+  check_shape(s);
+  ConvGeom g = make_geom(s);
+  g.M = s.O; g.NC = s.R * s.S * s.C; g.K = s.N * s.P * s.Q;
+  return g;
+}
+
+// Workspace (floats) launch_conv_wgrad needs for this shape with automatic splits.
+long conv_wgrad_ws_floats(const ConvShape& s) {
+  const ConvGeom g = wgrad_geom(s);
+  return (long)wgrad_splits(g, 0) * g.M * g.NC;
+}
+
+// dW[O][Cw][R][S] (fp32, PyTorch layout) = (or +=) X^T dY.  ``ws`` holds
+// ws_floats floats; splits <= 0 picks automatically within that capacity.
+void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const bf16* dy, float* dw, float* ws,
+                       long ws_floats, int splits, int accumulate) {
+  const ConvGeom g = wgrad_geom(s);
+  const long plane = (long)g.M * g.NC;
+  if (ws_floats < plane) throw std::invalid_argument("conv_wgrad: workspace smaller than one O x RSC plane");
+  if (splits <= 0) splits = wgrad_splits(g, ws_floats);
+  const int ksteps = (g.K + BK - 1) / BK;
+  splits = std::max(1, std::min<int>(splits, ksteps));
+  const int kps = (ksteps + splits - 1) / splits;
+  splits = (ksteps + kps - 1) / kps;
+  if ((long)splits * plane > ws_floats) throw std::invalid_argument("conv_wgrad: workspace too small for splits");
+  launch_mode<WGRAD>(st, g, x, nullptr, dy, nullptr, ws, nullptr, splits);
+  const long total = (long)s.O * s.Cw * s.R * s.S;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(conv_wgrad_reduce, dim3(blocks), dim3(256), 0, st, ws, splits, s.O, s.C, s.Cw, s.R * s.S, dw,
+                     accumulate);
+}
+
+void launch_conv_pack(hipStream_t st, const float* w, bf16* wrsc, int O, int Cw, int C, int RS) {
+  const long total = (long)O * RS * C;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(conv_pack_kernel, dim3(blocks), dim3(256), 0, st, w, wrsc, O, Cw, C, RS);
+}
+
+}  // namespace fedmi

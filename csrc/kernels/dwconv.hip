@@ -1,0 +1,271 @@
+// fedmi — depthwise 2-D convolution (groups == channels) on NHWC bf16, the
+// MobileNet / MobileNetV2 / EfficientNet / ShuffleNet / PNASNet building block
+// (src/models/mobilenet.py:11-23, mobilenetv2.py:11-37, ...).
+//
+// Depthwise work has K = R*S (9 for 3x3) per output: no reduction dimension
+// for MFMA to chew on, so these are VALU kernels built around 16-byte
+// channel vectors: one thread owns 8 consecutive channels of one pixel, the
+// R*S taps stream through registers, and the per-channel filter taps are
+// loaded once per thread.  Memory-bound by design (HBM roofline), with the
+// BatchNorm batch statistics of the output fused into the forward epilogue.
+//
+//   fwd    y[n,p,q,c]  = sum_rs x[n, p*st-pad+r, q*st-pad+s, c] * w[c,r,s]
+//   dgrad  dx[n,h,w,c] = sum_rs dy[n, (h+pad-r)/st, (w+pad-s)/st, c] * w[c,r,s]
+//   wgrad  dw[c,r,s]   = sum_npq dy[n,p,q,c] * x[n, p*st-pad+r, q*st-pad+s, c]
+//          (per-block partials -> workspace -> deterministic reduce)
+#include <algorithm>
+#include <stdexcept>
+
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+
+struct DwGeom {
+  int N, H, W, C, P, Q, R, S, st, pad;
+};
+
+FEDMI_DEV void ld8f(const bf16* p, float* v) {
+  const bf16x8v b = *reinterpret_cast<const bf16x8v*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)b[j];
+}
+
+constexpr int MAXRS = 49;   // up to 7x7 (PNASNet)
+
+// Filter taps staged in LDS as [tap][C] fp32 (8 consecutive channels = 32 B).
+FEDMI_DEV void stage_taps(const float* __restrict__ w, float* wl, int C, int RS) {
+  for (int i = threadIdx.x; i < C * RS; i += blockDim.x) {
+    const int c = i / RS, t = i - c * RS;
+    wl[t * C + c] = w[i];
+  }
+}
+
+// one thread per (output pixel, 8-channel group); the block size is a multiple
+// of C/8, so the grid stride is too and a thread's channel group is fixed
+__global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                     bf16* __restrict__ y, float* __restrict__ stats,
+                                                     const float* __restrict__ shift, DwGeom g) {
+  extern __shared__ float wl[];   // [RS][C]
+  __shared__ float red[2][256][8];
+  const int VC = g.C >> 3, RS = g.R * g.S;
+  stage_taps(w, wl, g.C, RS);
+  __syncthreads();
+  const long total = (long)g.N * g.P * g.Q * VC;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  const int c0 = (int)(threadIdx.x % VC) * 8;
+  float sh[8];   // statistics are of (y - shift): see conv_igemm's epilogue
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sh[j] = shift ? shift[c0 + j] : 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long pix = i / VC;
+    const int q = pix % g.Q;
+    const long t2 = pix / g.Q;
+    const int p = t2 % g.P, n = t2 / g.P;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int r = 0; r < g.R; ++r) {
+      const int h = p * g.st - g.pad + r;
+      if ((unsigned)h >= (unsigned)g.H) continue;
+      for (int s = 0; s < g.S; ++s) {
+        const int ww = q * g.st - g.pad + s;
+        if ((unsigned)ww >= (unsigned)g.W) continue;
+        float v[8];
+        ld8f(x + (((long)n * g.H + h) * g.W + ww) * g.C + c0, v);
+        const float* wt = wl + (r * g.S + s) * g.C + c0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[j] * wt[j];
+      }
+    }
+    bf16x8v o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = (bf16)acc[j];
+      const float vb = (float)o[j] - sh[j];
+      s1[j] += vb;
+      s2[j] += vb * vb;
+    }
+    *reinterpret_cast<bf16x8v*>(y + pix * g.C + c0) = o;
+  }
+  if (stats == nullptr) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[0][threadIdx.x][j] = s1[j]; red[1][threadIdx.x][j] = s2[j]; }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 2 * g.C; e += blockDim.x) {   // threads t == grp (mod VC) own group grp
+    const int qn = e / g.C, c = e - qn * g.C;
+    const int grp = c >> 3, j = c & 7;
+    float sum = 0.f;
+    for (int t = grp; t < (int)blockDim.x; t += VC) sum += red[qn][t][j];
+    unsafeAtomicAdd(stats + qn * g.C + c, sum);
+  }
+}
+
+// one thread per (input pixel, 8-channel group): gather form, no atomics
+__global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16* __restrict__ dy, const float* __restrict__ w,
+                                                       bf16* __restrict__ dx, DwGeom g) {
+  extern __shared__ float wl[];
+  const int VC = g.C >> 3;
+  stage_taps(w, wl, g.C, g.R * g.S);
+  __syncthreads();
+  const long total = (long)g.N * g.H * g.W * VC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % VC) * 8;
+    const long pix = i / VC;
+    const int wq = pix % g.W;
+    const long t2 = pix / g.W;
+    const int h = t2 % g.H, n = t2 / g.H;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int r = 0; r < g.R; ++r) {
+      int y = h + g.pad - r;
+      if (y < 0 || y % g.st) continue;
+      y /= g.st;
+      if (y >= g.P) continue;
+      for (int s = 0; s < g.S; ++s) {
+        int xx = wq + g.pad - s;
+        if (xx < 0 || xx % g.st) continue;
+        xx /= g.st;
+        if (xx >= g.Q) continue;
+        float v[8];
+        ld8f(dy + (((long)n * g.P + y) * g.Q + xx) * g.C + c0, v);
+        const float* wt = wl + (r * g.S + s) * g.C + c0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[j] * wt[j];
+      }
+    }
+    bf16x8v o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)acc[j];
+    *reinterpret_cast<bf16x8v*>(dx + pix * g.C + c0) = o;
+  }
+}
+
+// Partial weight gradients: block b sums a contiguous range of output pixels
+// for ALL channel groups (thread -> fixed group), writes ws[b][C][RS].
+template <int RS>
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                       float* __restrict__ ws, DwGeom g, int pix_per_block) {
+  const int VC = g.C >> 3;   // host: blockDim.x % VC == 0
+  const int cg = threadIdx.x % VC, lane_pix = threadIdx.x / VC, pstep = blockDim.x / VC;
+  const int c0 = cg * 8;
+  const long npix = (long)g.N * g.P * g.Q;
+  const long pb = (long)blockIdx.x * pix_per_block, pe = std::min<long>(npix, pb + pix_per_block);
+  float acc[RS][8];
+#pragma unroll
+  for (int t = 0; t < RS; ++t)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[t][j] = 0.f;
+  for (long pix = pb + lane_pix; pix < pe; pix += pstep) {
+    const int q = pix % g.Q;
+    const long t2 = pix / g.Q;
+    const int p = t2 % g.P, n = t2 / g.P;
+    float d[8];
+    ld8f(dy + pix * g.C + c0, d);
+#pragma unroll
+    for (int t = 0; t < RS; ++t) {
+      const int r = t / g.S, s = t - r * g.S;
+      const int h = p * g.st - g.pad + r, ww = q * g.st - g.pad + s;
+      const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+      float v[8];
+      ld8f(x + (ok ? (((long)n * g.H + h) * g.W + ww) * g.C + c0 : c0), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[t][j] += ok ? v[j] * d[j] : 0.f;
+    }
+  }
+  // reduce the pstep threads sharing a channel group through LDS, one tap at a time
+  __shared__ float red[256][8];
+  float* out = ws + (long)blockIdx.x * g.C * RS;
+#pragma unroll
+  for (int t = 0; t < RS; ++t) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = acc[t][j];
+    __syncthreads();
+    for (int c = threadIdx.x; c < g.C; c += blockDim.x) {
+      const int grp = c >> 3, j = c & 7;
+      float sum = 0.f;
+      for (int tt = grp; tt < (int)blockDim.x; tt += VC) sum += red[tt][j];
+      out[(long)c * RS + t] = sum;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void dw_wgrad_reduce(const float* __restrict__ ws, int nblk, int n,
+                                                       float* __restrict__ dw, int accumulate) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    float v = accumulate ? dw[i] : 0.f;
+    for (int b = 0; b < nblk; ++b) v += ws[(long)b * n + i];
+    dw[i] = v;
+  }
+}
+
+int blocks_for(long items, int tb = 256) { return (int)std::max<long>(1, std::min<long>((items + tb - 1) / tb, 4096)); }
+
+// largest multiple of C/8 that fits in 256 threads
+int block_threads(int C) { const int vc = C / 8; return (256 / vc) * vc; }
+
+}  // namespace
+
+namespace fedmi {
+
+struct DwShape {
+  int N, H, W, C, R, S, st, pad;
+};
+
+static DwGeom dw_geom(const DwShape& s) {
+  if (s.C % 8 || s.C / 8 > 256) throw std::invalid_argument("dwconv: need C % 8 == 0 and C <= 2048");
+  if (s.R != s.S || (s.R != 3 && s.R != 5 && s.R != 7)) throw std::invalid_argument("dwconv: square 3/5/7 kernels");
+  if ((long)s.C * s.R * s.S * 4 > 128 * 1024) throw std::invalid_argument("dwconv: filter image exceeds LDS");
+  DwGeom g{s.N, s.H, s.W, s.C, (s.H + 2 * s.pad - s.R) / s.st + 1, (s.W + 2 * s.pad - s.S) / s.st + 1,
+           s.R, s.S, s.st, s.pad};
+  return g;
+}
+
+// w: fp32 [C][1][R][S] (PyTorch depthwise layout, used directly)
+void launch_dw_fwd(hipStream_t st, const DwShape& s, const bf16* x, const float* w, bf16* y, float* stats,
+                   const float* shift) {
+  const DwGeom g = dw_geom(s);
+  const long items = (long)g.N * g.P * g.Q * (g.C / 8);
+  const int tb = block_threads(g.C);
+  hipLaunchKernelGGL(dw_fwd_kernel, dim3(blocks_for(items, tb)), dim3(tb), g.C * g.R * g.S * sizeof(float), st, x, w,
+                     y, stats, shift, g);
+}
+
+void launch_dw_dgrad(hipStream_t st, const DwShape& s, const bf16* dy, const float* w, bf16* dx) {
+  const DwGeom g = dw_geom(s);
+  const long items = (long)g.N * g.H * g.W * (g.C / 8);
+  hipLaunchKernelGGL(dw_dgrad_kernel, dim3(blocks_for(items)), dim3(256), g.C * g.R * g.S * sizeof(float), st, dy, w,
+                     dx, g);
+}
+
+static int dw_wgrad_blocks(const DwGeom& g) {
+  const long npix = (long)g.N * g.P * g.Q;
+  return (int)std::max<long>(1, std::min<long>(512, (npix + 63) / 64));
+}
+
+long dw_wgrad_ws_floats(const DwShape& s) {
+  const DwGeom g = dw_geom(s);
+  return (long)dw_wgrad_blocks(g) * g.C * g.R * g.S;
+}
+
+void launch_dw_wgrad(hipStream_t st, const DwShape& s, const bf16* x, const bf16* dy, float* dw, float* ws,
+                     long ws_floats, int accumulate) {
+  const DwGeom g = dw_geom(s);
+  const int nblk = dw_wgrad_blocks(g);
+  const int n = g.C * g.R * g.S;
+  if ((long)nblk * n > ws_floats) throw std::invalid_argument("dw_wgrad: workspace too small");
+  const long npix = (long)g.N * g.P * g.Q;
+  const int ppb = (int)((npix + nblk - 1) / nblk);
+  const int tb = block_threads(g.C);
+  if (g.R == 3) hipLaunchKernelGGL(dw_wgrad_kernel<9>, dim3(nblk), dim3(tb), 0, st, x, dy, ws, g, ppb);
+  else if (g.R == 5) hipLaunchKernelGGL(dw_wgrad_kernel<25>, dim3(nblk), dim3(tb), 0, st, x, dy, ws, g, ppb);
+  else hipLaunchKernelGGL(dw_wgrad_kernel<49>, dim3(nblk), dim3(tb), 0, st, x, dy, ws, g, ppb);
+  hipLaunchKernelGGL(dw_wgrad_reduce, dim3(blocks_for(n)), dim3(256), 0, st, ws, nblk, n, dw, accumulate);
+}
+
+}  // namespace fedmi

@@ -28,8 +28,12 @@ SOURCES = [
     CSRC / "kernels" / "lenet_kernels.hip",
     CSRC / "kernels" / "flat_ops.hip",
     CSRC / "kernels" / "compress.hip",
+    CSRC / "kernels" / "conv_igemm.hip",
+    CSRC / "kernels" / "cnn_ops.hip",
+    CSRC / "kernels" / "dwconv.hip",
     CSRC / "runtime" / "lenet_engine.cpp",
     CSRC / "bindings.cpp",
+    CSRC / "bindings_cnn.cpp",
 ]
 HEADERS = sorted(CSRC.rglob("*.h"))
 

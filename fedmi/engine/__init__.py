@@ -8,16 +8,27 @@ from .base import EpochStats, LocalTrainer, TrainerConfig
 from .data import FedDataset
 
 
+# zoo models with a native (hand-written HIP) training engine on the GPU
+NATIVE_CNNS = ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "mobilenet", "mobilenetv2")
+
+
 def build_trainer(model: str, data: FedDataset, device, cfg: TrainerConfig = TrainerConfig(),
                   init_state=None) -> LocalTrainer:
-    """LeNet on a GPU -> fused HIP engine (mandatory, no silent fallback); else PyTorch engine."""
+    """On a GPU: LeNet -> fused HIP engine; ResNet / MobileNet / MobileNetV2 -> the implicit-GEMM +
+    BN-fused HIP engine (mandatory, no silent fallback).  Other zoo models and CPU runs -> the
+    generic PyTorch engine (flat buffers + native fused SGD on GPU)."""
     device = torch.device(device)
     from ..models import _canon
 
-    if _canon(model) == "lenet" and device.type == "cuda" and not native.force_torch_path():
-        from .lenet_native import LeNetNativeTrainer
+    if device.type == "cuda" and not native.force_torch_path():
+        if _canon(model) == "lenet":
+            from .lenet_native import LeNetNativeTrainer
 
-        return LeNetNativeTrainer(data, device, cfg, init_state=init_state)
+            return LeNetNativeTrainer(data, device, cfg, init_state=init_state)
+        if _canon(model) in NATIVE_CNNS and tuple(data.train.x.shape[1:]) == (3, 32, 32):
+            from .cnn_native import CNNNativeTrainer
+
+            return CNNNativeTrainer(model, data, device, cfg, init_state=init_state)
     from .torch_engine import TorchTrainer
 
     kw = {}

@@ -1,0 +1,493 @@
+"""Native HIP engine for the BatchNorm CNN families of the zoo:
+
+* ResNet-18/34 (BasicBlock) and ResNet-50/101/152 (Bottleneck), src/models/resnet.py:14-124
+* MobileNet (depthwise-separable, the reference's default model), src/models/mobilenet.py:11-52
+* MobileNetV2 (inverted residuals), src/models/mobilenetv2.py:11-77
+
+The zoo ``nn.Module`` is only the parameter/buffer container (its
+``state_dict`` keeps the reference key names and lives in fedmi's flat fp32
+buffers); the training step is an explicit schedule of fedmi kernels on NHWC
+bf16 activations.  A network is a list of *blocks*; a block is a chain of
+*units* (conv or depthwise conv -> BatchNorm -> optional ReLU) whose last BN is
+fused with the block's shortcut (none / identity residual / projection
+conv+BN) and output ReLU in one ``bn_apply`` launch:
+
+  forward   prep_input (crop/flip/normalize, device-side batch start)
+            -> per unit: conv (implicit-GEMM MFMA, BN batch statistics summed in
+               the epilogue) or depthwise conv (VALU, same fused statistics)
+               -> bn_apply (+residual / +projection BN, +ReLU)
+            -> head (global avgpool + linear + CE + dlogits)
+  backward  per block, reversed: bn_bwd (ReLU mask, both BN branches, residual
+            fan-in of two incoming grads) -> wgrad (split-K partials into a
+            workspace, one reduce into the flat grad buffer) -> dgrad
+  update    one multi-tensor SGD launch over the flat fp32 master, then the
+            bf16 [O][R][S][C] weight images of the dense convs are repacked
+
+Each training step is captured once per batch size into a HIP graph
+(``torch.cuda.CUDAGraph``) and replayed for every batch of the epoch (the
+batch start comes from a device-side schedule).  All activations stay
+resident, sized for max(train batch, eval batch) rows.
+"""
+from __future__ import annotations
+
+import dataclasses
+from collections import OrderedDict
+from typing import Dict, List, Optional
+
+import torch
+from torch import nn
+
+from .. import native
+from ..models import build_model
+from ..models.zoo.mobile import DWSeparable, InvertedResidual, MobileNet, MobileNetV2
+from ..models.zoo.residual import BasicBlock, Bottleneck, ResNet
+from ..ops import cnn, conv
+from .base import EpochStats, LocalTrainer, TrainerConfig
+from .data import FedDataset, ImageSet
+from .torch_engine import FlatState
+
+BN_EPS = 1e-5
+BN_MOM = 0.1
+
+
+class _Unit:
+    """conv (dense or depthwise, no bias) + BatchNorm2d (+ ReLU), with its device buffers."""
+
+    def __init__(self, c: nn.Conv2d, bn: nn.BatchNorm2d, in_hw: int, relu: bool, rows: int, dev,
+                 need_y: bool = True, c_in_pad: Optional[int] = None, act_dtype=torch.bfloat16):
+        assert c.bias is None and c.dilation == (1, 1)
+        self.conv, self.bn, self.relu = c, bn, relu
+        self.depthwise = c.groups > 1
+        if self.depthwise and not (c.groups == c.in_channels == c.out_channels):
+            raise TypeError("grouped (non-depthwise) convolutions are not supported by the native engine")
+        self.O, self.Cw, self.R, self.S = c.weight.shape
+        if self.depthwise:
+            self.Cw = c.in_channels
+        self.C = c_in_pad or conv.pad8(self.Cw)
+        self.stride, self.pad = c.stride[0], c.padding[0]
+        self.H = in_hw
+        self.P = (in_hw + 2 * self.pad - self.R) // self.stride + 1
+        n_out = rows * self.P * self.P * self.O
+        bf = dict(dtype=act_dtype, device=dev)
+        self.wr = None if self.depthwise else torch.empty(self.O, self.R, self.S, self.C, dtype=torch.bfloat16,
+                                                          device=dev)
+        self.z = torch.empty(n_out, **bf)                            # conv output (pre-BN)
+        self.y = torch.empty(n_out, **bf) if need_y else None        # BN(+ReLU) output inside a block
+        self.dz = torch.empty(n_out, **bf)                           # grad wrt z
+        self.dy = torch.empty(n_out, **bf) if need_y else None       # grad wrt y
+        self.smean = torch.empty(self.O, device=dev)
+        self.sinv = torch.empty(self.O, device=dev)
+        self.shift = torch.zeros(self.O, device=dev)   # previous batch mean: stats are sums of (z - shift)
+
+    def view(self, t: torch.Tensor, nb: int) -> torch.Tensor:
+        return t[: nb * self.P * self.P * self.O].view(nb, self.P, self.P, self.O)
+
+    def bn_args(self, stats) -> dict:
+        b = self.bn
+        return cnn.bn_desc(stats, b.weight, b.bias, b.running_mean, b.running_var, b.num_batches_tracked,
+                           self.smean, self.sinv, self.shift)
+
+    def in_shape(self, nb: int):
+        return (nb, self.H, self.H, self.C)
+
+    def ws_floats(self, nb: int) -> int:
+        if self.depthwise:
+            return conv.dwconv_ws_floats(self.in_shape(nb), self.R, self.stride, self.pad)
+        return conv.wgrad_ws_floats(self.in_shape(nb), self.O, self.R, self.S, self.stride, self.pad, self.Cw)
+
+    # ---- launches
+    def fwd(self, x: torch.Tensor, nb: int, stats) -> None:
+        sh = self.shift if stats is not None else None
+        if self.depthwise:
+            conv.dwconv_fwd(x, self.conv.weight, self.stride, self.pad, stats=stats, out=self.view(self.z, nb),
+                            shift=sh)
+        else:
+            conv.conv2d_fwd(x, self.wr, self.stride, self.pad, Cw=self.Cw, stats=stats, out=self.view(self.z, nb),
+                            shift=sh)
+
+    def wgrad(self, x: torch.Tensor, nb: int, ws: torch.Tensor) -> None:
+        dz = self.view(self.dz, nb)
+        if self.depthwise:
+            conv.dwconv_wgrad(x, dz, self.R, self.stride, self.pad, out=self.conv.weight.grad, ws=ws)
+        else:
+            conv.conv2d_wgrad(x, dz, self.R, self.S, self.stride, self.pad, Cw=self.Cw, out=self.conv.weight.grad,
+                              ws=ws)
+
+    def dgrad(self, nb: int, out: torch.Tensor) -> torch.Tensor:
+        dz = self.view(self.dz, nb)
+        if self.depthwise:
+            return conv.dwconv_dgrad(dz, self.conv.weight, self.in_shape(nb), self.stride, self.pad, out=out)
+        return conv.conv2d_dgrad(dz, self.wr, self.in_shape(nb), self.stride, self.pad, Cw=self.Cw, out=out)
+
+    def pack(self) -> None:
+        if not self.depthwise:
+            conv.pack_weight(self.conv.weight.data, self.C, out=self.wr)
+
+
+class _Block:
+    """Chain of units; the last unit's BN is fused with the shortcut and the output ReLU."""
+
+    def __init__(self, pairs, relus, in_hw: int, cin: int, rows: int, dev, shortcut: str = "none",
+                 proj=None, out_relu: bool = True, first: bool = False, act_dtype=torch.bfloat16):
+        self.main: List[_Unit] = []
+        hw = in_hw
+        for i, ((c, bn), r) in enumerate(zip(pairs, relus)):
+            last = i == len(pairs) - 1
+            u = _Unit(c, bn, hw, relu=r, rows=rows, dev=dev, need_y=not last,
+                      c_in_pad=8 if first and i == 0 else None, act_dtype=act_dtype)
+            self.main.append(u)
+            hw = u.P
+        self.in_hw, self.cin, self.out_hw = in_hw, cin, hw
+        self.cout = self.main[-1].O
+        self.shortcut = shortcut            # "none" | "identity" | "proj"
+        self.proj = (_Unit(proj[0], proj[1], in_hw, relu=False, rows=rows, dev=dev, need_y=False,
+                           act_dtype=act_dtype) if proj else None)
+        self.out_relu = out_relu
+        self.first = first                  # network input block: no input gradient
+        bf = dict(dtype=act_dtype, device=dev)
+        self.out = torch.empty(rows * hw * hw * self.cout, **bf)
+        n_in = rows * in_hw * in_hw * cin
+        self.din_a = None if first else torch.empty(n_in, **bf)
+        self.din_b = torch.empty(n_in, **bf) if shortcut != "none" else None
+
+    def units(self) -> List[_Unit]:
+        return self.main + ([self.proj] if self.proj else [])
+
+    def out_view(self, nb: int) -> torch.Tensor:
+        return self.out[: nb * self.out_hw * self.out_hw * self.cout].view(nb, self.out_hw, self.out_hw, self.cout)
+
+    def in_view(self, t: torch.Tensor, nb: int) -> torch.Tensor:
+        return t[: nb * self.in_hw * self.in_hw * self.cin].view(nb, self.in_hw, self.in_hw, self.cin)
+
+
+# ---------------------------------------------------------------------------- network plans
+def _plan_resnet(m: ResNet, rows, dev, dt) -> List[_Block]:
+    blocks = [_Block([(m.conv1, m.bn1)], [True], 32, 8, rows, dev, first=True, act_dtype=dt)]
+    hw, c = blocks[0].out_hw, blocks[0].cout
+    for layer in (m.layer1, m.layer2, m.layer3, m.layer4):
+        for blk in layer:
+            if isinstance(blk, BasicBlock):
+                pairs = [(blk.conv1, blk.bn1), (blk.conv2, blk.bn2)]
+            elif isinstance(blk, Bottleneck):
+                pairs = [(blk.conv1, blk.bn1), (blk.conv2, blk.bn2), (blk.conv3, blk.bn3)]
+            else:
+                raise TypeError(type(blk).__name__)
+            relus = [True] * (len(pairs) - 1) + [False]
+            proj = (blk.shortcut[0], blk.shortcut[1]) if len(blk.shortcut) else None
+            b = _Block(pairs, relus, hw, c, rows, dev, shortcut="proj" if proj else "identity", proj=proj,
+                       out_relu=True, act_dtype=dt)
+            blocks.append(b)
+            hw, c = b.out_hw, b.cout
+    return blocks
+
+
+def _plan_mobilenet(m: MobileNet, rows, dev, dt) -> List[_Block]:
+    blocks = [_Block([(m.conv1, m.bn1)], [True], 32, 8, rows, dev, first=True, act_dtype=dt)]
+    hw, c = blocks[0].out_hw, blocks[0].cout
+    for blk in m.layers:
+        assert isinstance(blk, DWSeparable)
+        b = _Block([(blk.conv1, blk.bn1), (blk.conv2, blk.bn2)], [True, True], hw, c, rows, dev, out_relu=True,
+                   act_dtype=dt)
+        blocks.append(b)
+        hw, c = b.out_hw, b.cout
+    return blocks
+
+
+def _plan_mobilenetv2(m: MobileNetV2, rows, dev, dt) -> List[_Block]:
+    blocks = [_Block([(m.conv1, m.bn1)], [True], 32, 8, rows, dev, first=True, act_dtype=dt)]
+    hw, c = blocks[0].out_hw, blocks[0].cout
+    for blk in m.layers:
+        assert isinstance(blk, InvertedResidual)
+        pairs = [(blk.conv1, blk.bn1), (blk.conv2, blk.bn2), (blk.conv3, blk.bn3)]
+        if blk.stride != 1:
+            short, proj = "none", None
+        elif len(blk.shortcut):
+            short, proj = "proj", (blk.shortcut[0], blk.shortcut[1])
+        else:
+            short, proj = "identity", None
+        b = _Block(pairs, [True, True, False], hw, c, rows, dev, shortcut=short, proj=proj, out_relu=False,
+                   act_dtype=dt)
+        blocks.append(b)
+        hw, c = b.out_hw, b.cout
+    blocks.append(_Block([(m.conv2, m.bn2)], [True], hw, c, rows, dev, out_relu=True, act_dtype=dt))
+    return blocks
+
+
+PLANS = {ResNet: _plan_resnet, MobileNet: _plan_mobilenet, MobileNetV2: _plan_mobilenetv2}
+
+
+def supports(model: nn.Module) -> bool:
+    return type(model) in PLANS
+
+
+class CNNNativeTrainer(LocalTrainer):
+    def __init__(self, model_name: str, data: FedDataset, device: torch.device, cfg: TrainerConfig = TrainerConfig(),
+                 init_state=None, act_dtype=torch.bfloat16):
+        """``act_dtype`` other than bf16 only works under fedmi.ops.emulate (wiring tests)."""
+        self._nat = native.require()
+        self._device = device = torch.device(device)
+        self.cfg = dataclasses.replace(cfg)
+        self.model_name = model_name
+        torch.manual_seed(cfg.seed)
+        model = build_model(model_name)
+        if type(model) not in PLANS:
+            raise TypeError(f"{model_name}: no native plan (ResNet, MobileNet, MobileNetV2 are supported)")
+        if init_state is not None:
+            model.load_state_dict(init_state)
+        self.model = model.to(device)
+        self.fs = FlatState(self.model, device)
+        self.train_set = data.train.to(device)
+        self.test_set = data.test.to(device)
+        self.augment = bool(data.augment and cfg.augment)
+        if tuple(self.train_set.x.shape[1:]) != (3, 32, 32):
+            raise ValueError("native CNN engine expects CIFAR-shaped uint8 [N,3,32,32] data")
+        for s in (self.train_set, self.test_set):
+            if s.y.dtype != torch.int32:
+                s.y = s.y.to(torch.int32)
+        self.eval_bs = min(cfg.eval_batch_size, 500)
+        self.rows = R = max(cfg.batch_size, self.eval_bs)
+        self.blocks = PLANS[type(model)](self.model, R, device, act_dtype)
+        last = self.blocks[-1]
+        self.head_hw, self.head_c = last.out_hw, last.cout
+        self.units: List[_Unit] = [u for b in self.blocks for u in b.units()]
+        # per-step accumulators: BN batch stats [2][O] and BN-backward sums [3][O], one fill each
+        self.stats_all = torch.zeros(sum(2 * u.O for u in self.units), device=device)
+        self.red_all = torch.zeros(sum(3 * u.O for u in self.units), device=device)
+        so = ro = 0
+        for u in self.units:
+            u.stats = self.stats_all[so:so + 2 * u.O].view(2, u.O)
+            u.red = self.red_all[ro:ro + 3 * u.O].view(3, u.O)
+            so += 2 * u.O
+            ro += 3 * u.O
+        B = cfg.batch_size
+        self.wgrad_ws = torch.empty(max(u.ws_floats(B) for u in self.units), device=device)
+        self.xin = torch.empty(R, 32, 32, 8, dtype=act_dtype, device=device)
+        self.dhead = torch.empty(R * self.head_hw * self.head_hw * self.head_c, dtype=act_dtype, device=device)
+        self.pooled = torch.empty(R, self.head_c, device=device)
+        self.dlog = torch.empty(R, self.model.linear.out_features, device=device)
+        self.stats = torch.zeros(2, 4, device=device)        # [train, eval] x {loss, correct, count, pad}
+        self.round_ctr = torch.zeros(4, dtype=torch.int32, device=device)
+        self.sched = torch.zeros(1, dtype=torch.int32, device=device)
+        self.counter = torch.zeros(1, dtype=torch.int32, device=device)
+        self.cur = torch.zeros(1, dtype=torch.int32, device=device)
+        self.ebase = torch.zeros(1, dtype=torch.int32, device=device)
+        self._starts: List[int] = []
+        self._sizes: List[int] = []
+        self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        self.round_idx = 0
+        self.pack()
+
+    # ---- state ---------------------------------------------------------------------
+    @property
+    def device(self) -> torch.device:
+        return self._device
+
+    def state_dict(self):
+        return OrderedDict((k, v.detach()) for k, v in self.model.state_dict().items())
+
+    def load_state_dict(self, sd) -> None:
+        with torch.no_grad():
+            own = self.model.state_dict()
+            for k, v in sd.items():
+                own[k].copy_(v.to(own[k].device, own[k].dtype).view(own[k].shape))
+        self.after_aggregate()
+
+    def float_state(self) -> torch.Tensor:
+        return self.fs.flat
+
+    def int_state(self) -> List[torch.Tensor]:
+        return [b for _, _, b in self.fs.ibufs]
+
+    def momentum_state(self) -> torch.Tensor:
+        return self.fs.mom
+
+    def after_aggregate(self) -> None:
+        self.pack()
+
+    def set_lr(self, lr: float) -> None:
+        self.cfg.lr = float(lr)
+        self._graphs.clear()
+
+    def pack(self) -> None:
+        for u in self.units:
+            u.pack()
+
+    # ---- data ----------------------------------------------------------------------------
+    def set_schedule(self, starts, sizes) -> None:
+        starts, sizes = list(map(int, starts)), list(map(int, sizes))
+        n = len(self.train_set)
+        for s, b in zip(starts, sizes):
+            if not (0 < b <= self.cfg.batch_size) or s < 0 or s + b > n:
+                raise ValueError(f"schedule: batch ({s}, {b}) out of range")
+        self._starts, self._sizes = starts, sizes
+        self.sched = torch.tensor(starts or [0], dtype=torch.int32, device=self._device)
+        self._graphs.clear()
+
+    def set_train_data(self, data: ImageSet) -> None:
+        self.train_set = data.to(self._device)
+        if self.train_set.y.dtype != torch.int32:
+            self.train_set.y = self.train_set.y.to(torch.int32)
+        self._starts, self._sizes = [], []
+        self._graphs.clear()
+
+    # ---- kernel schedule ---------------------------------------------------------------------
+    def _bn(self, u: _Unit, z: torch.Tensor, y: torch.Tensor, train: bool, relu: bool, **kw) -> torch.Tensor:
+        return cnn.bn_apply(z, u.bn_args(u.stats), y, train, relu, eps=BN_EPS, momentum=BN_MOM, **kw)
+
+    def _forward(self, nb: int, train: bool, images: torch.Tensor, labels: torch.Tensor, dbase, stats_row: int):
+        x = cnn.prep_input(images, 0, nb, self.augment and train, self.cfg.seed, self.round_ctr,
+                           out=self.xin[:nb], dbase=dbase)
+        a = x
+        for b in self.blocks:
+            h = a
+            for v in b.main[:-1]:
+                v.fwd(h, nb, v.stats if train else None)
+                h = self._bn(v, v.view(v.z, nb), v.view(v.y, nb), train, v.relu)
+            last = b.main[-1]
+            last.fwd(h, nb, last.stats if train else None)
+            out = b.out_view(nb)
+            z = last.view(last.z, nb)
+            if b.shortcut == "proj":
+                p = b.proj
+                p.fwd(a, nb, p.stats if train else None)
+                self._bn(last, z, out, train, b.out_relu, z2=p.view(p.z, nb), b=p.bn_args(p.stats))
+            elif b.shortcut == "identity":
+                self._bn(last, z, out, train, b.out_relu, res=a)
+            else:
+                self._bn(last, z, out, train, b.out_relu)
+            a = out
+        lin = self.model.linear
+        hd = self.dhead[: a.numel()].view_as(a)
+        cnn.head(a, labels, 0, lin.weight, lin.bias, self.stats[stats_row], train, self.pooled[:nb], self.dlog[:nb],
+                 hd if train else None, lin.weight.grad if train else None, lin.bias.grad if train else None,
+                 dbase=dbase)
+        return x, hd
+
+    @staticmethod
+    def _bn_bwd(u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None) -> None:
+        kw = {}
+        if zb is not None:
+            kw = dict(zb=zb.view(zb.z, nb), b=zb.bn_args(None), dgamma_b=zb.bn.weight.grad,
+                      dbeta_b=zb.bn.bias.grad, dzb=zb.view(zb.dz, nb))
+        cnn.bn_bwd(dya, u.view(u.z, nb), u.bn_args(None), u.bn.weight.grad, u.bn.bias.grad, u.view(u.dz, nb), u.red,
+                   dyb=dyb, y=y, gout=gout, **kw)
+
+    def _backward(self, nb: int, x: torch.Tensor, dhead: torch.Tensor) -> None:
+        dya, dyb = dhead, None
+        ws = self.wgrad_ws
+        for i in range(len(self.blocks) - 1, -1, -1):
+            b = self.blocks[i]
+            a_in = x if b.first else self.blocks[i - 1].out_view(nb)
+            last = b.main[-1]
+            din_b = b.in_view(b.din_b, nb) if b.din_b is not None else None
+            self._bn_bwd(last, nb, dya, dyb, b.out_view(nb) if b.out_relu else None, zb=b.proj,
+                         gout=din_b if b.shortcut == "identity" else None)
+            for j in range(len(b.main) - 1, -1, -1):
+                v = b.main[j]
+                xin = b.main[j - 1].view(b.main[j - 1].y, nb) if j > 0 else a_in
+                v.wgrad(xin, nb, ws)
+                if j > 0:
+                    w = b.main[j - 1]
+                    v.dgrad(nb, w.view(w.dy, nb))
+                    self._bn_bwd(w, nb, w.view(w.dy, nb), None, w.view(w.y, nb) if w.relu else None)
+                elif not b.first:
+                    v.dgrad(nb, b.in_view(b.din_a, nb))
+            if b.proj is not None:
+                b.proj.wgrad(a_in, nb, ws)
+                b.proj.dgrad(nb, din_b)
+            if not b.first:
+                dya = b.in_view(b.din_a, nb)
+                dyb = din_b
+
+    def _sgd(self) -> None:
+        c, fs = self.cfg, self.fs
+        self._nat.sgd_flat(native.stream_handle(self._device), fs.params.data_ptr(), fs.grad.data_ptr(),
+                           fs.mom.data_ptr(), fs.n_params, c.lr, c.momentum, c.weight_decay, 0.0, False, False)
+        self.pack()
+
+    def _forward_backward(self, nb: int) -> None:
+        # every gradient entry is overwritten (wgrad reduce, BN dgamma/dbeta, head): no grad zeroing
+        self.stats_all.zero_()
+        self.red_all.zero_()
+        x, dh = self._forward(nb, True, self.train_set.x, self.train_set.y, self.cur, 0)
+        self._backward(nb, x, dh)
+
+    def _train_step(self, nb: int) -> None:
+        """One SGD step on the batch at sched[counter] (device-side)."""
+        cnn.sched_next(self.sched, self.counter, self.cur)
+        self._forward_backward(nb)
+        self._sgd()
+
+    def grads_for_batch(self, start: int, nb: int) -> None:
+        """Forward + backward of one batch WITHOUT the update (tests / diagnostics); grads in fs.grad."""
+        self.model.train()
+        self.cur.fill_(start)
+        self._forward_backward(nb)
+
+    # ---- compute ------------------------------------------------------------------------------
+    def train_epoch(self) -> None:
+        if not self._starts:
+            return
+        self.model.train()
+        self.stats[0].zero_()
+        self.counter.zero_()
+        if not self.cfg.use_graph:
+            for nb in self._sizes:
+                self._train_step(nb)
+        else:
+            for nb in self._sizes:
+                g = self._graphs.get(("train", nb))
+                if g is None:
+                    g = self._capture(nb)
+                g.replay()
+        self.round_ctr[0] += 1
+        self.round_idx += 1
+
+    def _capture(self, nb: int) -> torch.cuda.CUDAGraph:
+        # a warm-up eager step precedes capture; snapshot and restore everything it touches
+        saved = (self.fs.flat.clone(), self.fs.mom.clone(), [b.clone() for b in self.int_state()],
+                 self.counter.clone(), self.stats.clone())
+        s = torch.cuda.Stream(self._device)
+        s.wait_stream(torch.cuda.current_stream(self._device))
+        with torch.cuda.stream(s):
+            self._train_step(nb)
+        torch.cuda.current_stream(self._device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self._train_step(nb)
+        with torch.no_grad():
+            self.fs.flat.copy_(saved[0])
+            self.fs.mom.copy_(saved[1])
+            for b, v in zip(self.int_state(), saved[2]):
+                b.copy_(v)
+            self.counter.copy_(saved[3])
+            self.stats.copy_(saved[4])
+        self.pack()
+        self._graphs[("train", nb)] = g
+        return g
+
+    def train_stats(self) -> EpochStats:
+        return self._read_stats(0)
+
+    def _read_stats(self, i: int) -> EpochStats:
+        row = self.stats[i].cpu()
+        iv = row.view(torch.int32)
+        return EpochStats(float(row[0]), int(iv[1]), int(iv[2]))
+
+    @torch.no_grad()
+    def evaluate(self) -> None:
+        self.model.eval()
+        self.stats[1].zero_()
+        n = len(self.test_set)
+        bs = self.eval_bs
+        for s in range(0, n, bs):
+            nb = min(bs, n - s)
+            self.ebase.fill_(s)
+            self._forward(nb, False, self.test_set.x, self.test_set.y, self.ebase, 1)
+
+    def eval_stats(self) -> EpochStats:
+        return self._read_stats(1)
+
+
+# backwards-compatible name
+ResNetNativeTrainer = CNNNativeTrainer

@@ -1,0 +1,102 @@
+"""BatchNorm / classifier-head / input-prep kernels (csrc/kernels/cnn_ops.hip).
+
+All activations NHWC bf16 flattened to ``[M, C]`` rows (M = N*H*W).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .. import native
+
+
+def _p(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def prep_input(images_u8: torch.Tensor, base: int, nb: int, augment: bool, seed: int, round_ctr: torch.Tensor,
+               out: Optional[torch.Tensor] = None, dbase: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """uint8 [Ntot, 3, 32, 32] rows [base, base+nb) -> augmented, normalised bf16 [nb, 32, 32, 8].
+
+    ``dbase`` (int32 device scalar) is added to ``base`` on the device (graph replays); the caller
+    guarantees base + dbase + nb <= Ntot in that case (schedules are validated when set).
+    """
+    if images_u8.dtype != torch.uint8 or tuple(images_u8.shape[1:]) != (3, 32, 32):
+        raise ValueError("prep_input: expects uint8 [N, 3, 32, 32]")
+    if dbase is None and (base < 0 or base + nb > images_u8.shape[0]):
+        raise ValueError("prep_input: batch out of range")
+    if out is None:
+        out = torch.empty(nb, 32, 32, 8, dtype=torch.bfloat16, device=images_u8.device)
+    native.require().prep_input(native.stream_handle(images_u8.device), images_u8.data_ptr(), base, _p(dbase), nb,
+                                int(augment), seed & 0xFFFFFFFF, round_ctr.data_ptr(), out.data_ptr())
+    return out
+
+
+def sched_next(sched: torch.Tensor, counter: torch.Tensor, cur: torch.Tensor) -> None:
+    """cur = sched[counter++] on the device."""
+    native.require().sched_next(native.stream_handle(sched.device), sched.data_ptr(), counter.data_ptr(),
+                                cur.data_ptr())
+
+
+class BNParams:
+    """One BatchNorm2d's device tensors (train-time batch stats + params + running/saved stats)."""
+
+    __slots__ = ("stats", "gamma", "beta", "rmean", "rvar", "nbt", "smean", "sinv", "shift")
+
+    def __init__(self, stats=None, gamma=None, beta=None, rmean=None, rvar=None, nbt=None, smean=None, sinv=None,
+                 shift=None):
+        self.stats, self.gamma, self.beta = stats, gamma, beta
+        self.rmean, self.rvar, self.nbt = rmean, rvar, nbt
+        self.smean, self.sinv = smean, sinv
+        # ``stats`` hold sums of (z - shift); bn_bwd stores this step's batch mean into ``shift``
+        self.shift = shift
+
+    def ptrs(self) -> dict:
+        return {k: _p(getattr(self, k)) for k in self.__slots__}
+
+
+def bn_desc(stats=None, gamma=None, beta=None, rmean=None, rvar=None, nbt=None, smean=None, sinv=None,
+            shift=None) -> BNParams:
+    return BNParams(stats, gamma, beta, rmean, rvar, nbt, smean, sinv, shift)
+
+
+def bn_apply(z: torch.Tensor, a: BNParams, y: torch.Tensor, train: bool, relu: bool,
+             z2: Optional[torch.Tensor] = None, b: Optional[BNParams] = None, res: Optional[torch.Tensor] = None,
+             eps: float = 1e-5, momentum: float = 0.1) -> torch.Tensor:
+    """y = act(BN_a(z) [+ res | + BN_b(z2)]) over [M, C] rows; train mode commits running stats."""
+    C = z.shape[-1]
+    M = z.numel() // C
+    native.require().bn_apply(native.stream_handle(z.device), z.data_ptr(), a.ptrs(), _p(z2),
+                              b.ptrs() if b is not None else None, _p(res), y.data_ptr(), M, C, eps, momentum,
+                              int(train), int(relu))
+    return y
+
+
+def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Tensor, dbeta_a: torch.Tensor,
+           dza: torch.Tensor, red: torch.Tensor, dyb: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None,
+           zb: Optional[torch.Tensor] = None, b: Optional[BNParams] = None, dgamma_b=None, dbeta_b=None, dzb=None,
+           gout: Optional[torch.Tensor] = None) -> None:
+    """BatchNorm backward through an optional ReLU mask (``y``: forward output) for one or two BN
+    branches sharing the incoming grad g = dya (+ dyb).  Writes dz for each branch, dgamma/dbeta,
+    and optionally g itself (``gout``, the identity-shortcut grad).  ``red``: [3, C] fp32, ZERO on entry."""
+    C = za.shape[-1]
+    M = za.numel() // C
+    if red.numel() < 3 * C:
+        raise ValueError("bn_bwd: scratch too small")
+    d = dict(dya=_p(dya), dyb=_p(dyb), y=_p(y), za=_p(za), meanA=_p(a.smean), invA=_p(a.sinv), gammaA=_p(a.gamma),
+             dgammaA=_p(dgamma_a), dbetaA=_p(dbeta_a), dza=_p(dza), gout=_p(gout), shiftA=_p(a.shift))
+    if zb is not None:
+        d.update(zb=_p(zb), meanB=_p(b.smean), invB=_p(b.sinv), gammaB=_p(b.gamma), dgammaB=_p(dgamma_b),
+                 dbetaB=_p(dbeta_b), dzb=_p(dzb), shiftB=_p(b.shift))
+    native.require().bn_bwd(native.stream_handle(red.device), d, red.data_ptr(), M, C)
+
+
+def head(y: torch.Tensor, labels: torch.Tensor, base: int, W: torch.Tensor, b: torch.Tensor, stats: torch.Tensor,
+         train: bool, pooled=None, dlog=None, dy=None, dW=None, db=None, dbase=None) -> None:
+    N, H, Wd, C = y.shape
+    J = W.shape[0]
+    native.require().head(native.stream_handle(y.device), y.data_ptr(), labels.data_ptr(), base, _p(dbase), N,
+                          H * Wd, C, J,
+                          W.data_ptr(), b.data_ptr(), _p(pooled), _p(dlog), _p(dy), stats.data_ptr(), _p(dW), _p(db),
+                          int(train))

@@ -1,0 +1,198 @@
+"""Implicit-GEMM convolution on MFMA (csrc/kernels/conv_igemm.hip), NHWC bf16.
+
+Functional wrappers over the native launches: they allocate outputs, check
+shapes on the host (a kernel never sees an operand that disagrees with its
+grid) and launch on torch's current stream.  Activations are channels-last
+``[N, H, W, C]`` bf16 with ``C % 8 == 0`` (the network input is padded from 3
+to 8 channels by :func:`fedmi.ops.cnn.prep_input`); weights are packed from the
+fp32 PyTorch master ``[O, Cw, R, S]`` into ``[O, R, S, C]`` bf16.
+
+Reference ops: ``convolution`` / ``convolution_backward`` of every zoo model
+(e.g. src/models/resnet.py:14-70).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from .. import native
+
+
+def pad8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+def out_hw(h: int, w: int, r: int, s: int, stride: int, pad: int) -> Tuple[int, int]:
+    return (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
+
+
+def shape_tuple(x_shape, O: int, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None):
+    """(N, H, W, C, Cw, O, P, Q, R, S, stride, pad) as the native launchers expect."""
+    N, H, W, C = (int(v) for v in x_shape)
+    P, Q = out_hw(H, W, R, S, stride, pad)
+    if C % 8 or O % 8:
+        raise ValueError(f"conv: channels must be multiples of 8 (C={C}, O={O})")
+    if stride not in (1, 2):
+        raise ValueError("conv: stride 1 or 2")
+    return (N, H, W, C, int(Cw if Cw is not None else C), int(O), P, Q, int(R), int(S), int(stride), int(pad))
+
+
+def _check(t: torch.Tensor, dtype, name: str):
+    if t.dtype != dtype or not t.is_cuda or not t.is_contiguous():
+        raise ValueError(f"{name}: expected contiguous {dtype} CUDA tensor, got {t.dtype} {t.device}")
+
+
+def pack_weight(w: torch.Tensor, c_pad: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 [O, Cw, R, S] -> bf16 [O, R, S, C] (C = Cw rounded up to 8, zero pad)."""
+    O, Cw, R, S = w.shape
+    C = c_pad or pad8(Cw)
+    if out is None:
+        out = torch.empty(O, R, S, C, dtype=torch.bfloat16, device=w.device)
+    _check(w, torch.float32, "pack_weight.w")
+    native.require().conv_pack(native.stream_handle(w.device), w.data_ptr(), out.data_ptr(), O, Cw, C, R * S)
+    return out
+
+
+def conv2d_fwd(x: torch.Tensor, wrsc: torch.Tensor, stride: int, pad: int, Cw: Optional[int] = None,
+               stats: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+               shift: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y[N,P,Q,O] = conv(x[N,H,W,C]); ``stats`` ([2, O] fp32) += per-channel sum / sum of squares of
+    (y - shift) (``shift``: [O] fp32 or None = 0)."""
+    _check(x, torch.bfloat16, "conv2d_fwd.x")
+    _check(wrsc, torch.bfloat16, "conv2d_fwd.w")
+    O, R, S, C = wrsc.shape
+    if C != x.shape[3]:
+        raise ValueError(f"conv2d_fwd: weight C={C} vs input C={x.shape[3]}")
+    shp = shape_tuple(x.shape, O, R, S, stride, pad, Cw)
+    N, P, Q = shp[0], shp[6], shp[7]
+    if out is None:
+        out = torch.empty(N, P, Q, O, dtype=torch.bfloat16, device=x.device)
+    elif tuple(out.shape) != (N, P, Q, O):
+        raise ValueError("conv2d_fwd: bad out shape")
+    if stats is not None and (stats.numel() != 2 * O or stats.dtype != torch.float32):
+        raise ValueError("conv2d_fwd: stats must be [2, O] fp32")
+    native.require().conv_fwd(native.stream_handle(x.device), shp, x.data_ptr(), wrsc.data_ptr(), out.data_ptr(),
+                              stats.data_ptr() if stats is not None else 0,
+                              shift.data_ptr() if shift is not None else 0)
+    return out
+
+
+def conv2d_dgrad(dy: torch.Tensor, wrsc: torch.Tensor, x_shape, stride: int, pad: int, Cw: Optional[int] = None,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx[N,H,W,C] from dy[N,P,Q,O]."""
+    _check(dy, torch.bfloat16, "conv2d_dgrad.dy")
+    O, R, S, C = wrsc.shape
+    shp = shape_tuple(x_shape, O, R, S, stride, pad, Cw)
+    if tuple(dy.shape) != (shp[0], shp[6], shp[7], O):
+        raise ValueError(f"conv2d_dgrad: dy shape {tuple(dy.shape)} vs expected {(shp[0], shp[6], shp[7], O)}")
+    if out is None:
+        out = torch.empty(*x_shape, dtype=torch.bfloat16, device=dy.device)
+    native.require().conv_dgrad(native.stream_handle(dy.device), shp, dy.data_ptr(), wrsc.data_ptr(), out.data_ptr())
+    return out
+
+
+_WS: dict = {}
+
+
+def wgrad_workspace(device, floats: int) -> torch.Tensor:
+    """Per-device fp32 split-K workspace for conv2d_wgrad (grown outside graph capture only)."""
+    dev = torch.device(device)
+    ws = _WS.get(dev)
+    if ws is None or ws.numel() < floats:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("conv2d_wgrad: workspace must be reserved before graph capture "
+                               "(call wgrad_workspace(dev, wgrad_ws_floats(...)) first)")
+        ws = torch.empty(max(floats, 1 << 20), dtype=torch.float32, device=dev)
+        _WS[dev] = ws
+    return ws
+
+
+def wgrad_ws_floats(x_shape, O: int, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None) -> int:
+    return int(native.require().conv_wgrad_ws_floats(shape_tuple(x_shape, O, R, S, stride, pad, Cw)))
+
+
+def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None,
+                 out: Optional[torch.Tensor] = None, accumulate: bool = False, splits: int = 0,
+                 ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dW fp32 [O, Cw, R, S] (PyTorch layout).  ``accumulate`` adds into ``out`` instead of overwriting.
+
+    Split-K partials go to a workspace (plain stores) and one reduce launch sums
+    them into ``out`` — no fp32 atomics on the gradient.
+    """
+    _check(x, torch.bfloat16, "conv2d_wgrad.x")
+    _check(dy, torch.bfloat16, "conv2d_wgrad.dy")
+    O = dy.shape[3]
+    shp = shape_tuple(x.shape, O, R, S, stride, pad, Cw)
+    if tuple(dy.shape) != (shp[0], shp[6], shp[7], O):
+        raise ValueError("conv2d_wgrad: dy shape mismatch")
+    if out is None:
+        out = torch.empty(O, shp[4], R, S, dtype=torch.float32, device=x.device)
+        accumulate = False
+    if tuple(out.shape) != (O, shp[4], R, S) or out.dtype != torch.float32:
+        raise ValueError("conv2d_wgrad: out must be fp32 [O, Cw, R, S]")
+    nat = native.require()
+    if ws is None:
+        need = max(nat.conv_wgrad_ws_floats(shp), splits * O * R * S * shp[3])
+        ws = wgrad_workspace(x.device, need)
+    nat.conv_wgrad(native.stream_handle(x.device), shp, x.data_ptr(), dy.data_ptr(), out.data_ptr(), ws.data_ptr(),
+                   ws.numel(), splits, int(accumulate))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Depthwise convolution (csrc/kernels/dwconv.hip): groups == channels, weights
+# used directly in the PyTorch fp32 layout [C, 1, R, S].
+def _dw_shape(x_shape, R: int, stride: int, pad: int):
+    N, H, W, C = (int(v) for v in x_shape)
+    if C % 8 or C > 2048:
+        raise ValueError(f"dwconv: C={C} must be a multiple of 8 and <= 2048")
+    return (N, H, W, C, int(R), int(R), int(stride), int(pad))
+
+
+def dwconv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats: Optional[torch.Tensor] = None,
+               out: Optional[torch.Tensor] = None, shift: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _check(x, torch.bfloat16, "dwconv_fwd.x")
+    _check(w, torch.float32, "dwconv_fwd.w")
+    C, one, R, S = w.shape
+    if one != 1 or C != x.shape[3] or R != S:
+        raise ValueError("dwconv_fwd: weight must be [C, 1, R, R]")
+    shp = _dw_shape(x.shape, R, stride, pad)
+    P, Q = out_hw(shp[1], shp[2], R, R, stride, pad)
+    if out is None:
+        out = torch.empty(shp[0], P, Q, C, dtype=torch.bfloat16, device=x.device)
+    native.require().dw_fwd(native.stream_handle(x.device), shp, x.data_ptr(), w.data_ptr(), out.data_ptr(),
+                            stats.data_ptr() if stats is not None else 0,
+                            shift.data_ptr() if shift is not None else 0)
+    return out
+
+
+def dwconv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _check(dy, torch.bfloat16, "dwconv_dgrad.dy")
+    shp = _dw_shape(x_shape, w.shape[2], stride, pad)
+    if out is None:
+        out = torch.empty(*x_shape, dtype=torch.bfloat16, device=dy.device)
+    native.require().dw_dgrad(native.stream_handle(dy.device), shp, dy.data_ptr(), w.data_ptr(), out.data_ptr())
+    return out
+
+
+def dwconv_ws_floats(x_shape, R: int, stride: int, pad: int) -> int:
+    return int(native.require().dw_wgrad_ws_floats(_dw_shape(x_shape, R, stride, pad)))
+
+
+def dwconv_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, stride: int, pad: int, out: Optional[torch.Tensor] = None,
+                 accumulate: bool = False, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _check(x, torch.bfloat16, "dwconv_wgrad.x")
+    _check(dy, torch.bfloat16, "dwconv_wgrad.dy")
+    shp = _dw_shape(x.shape, R, stride, pad)
+    C = shp[3]
+    if out is None:
+        out = torch.empty(C, 1, R, R, dtype=torch.float32, device=x.device)
+        accumulate = False
+    nat = native.require()
+    if ws is None:
+        ws = wgrad_workspace(x.device, nat.dw_wgrad_ws_floats(shp))
+    nat.dw_wgrad(native.stream_handle(x.device), shp, x.data_ptr(), dy.data_ptr(), out.data_ptr(), ws.data_ptr(),
+                 ws.numel(), int(accumulate))
+    return out

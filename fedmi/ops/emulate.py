@@ -1,0 +1,284 @@
+"""PyTorch emulation of the fedmi CNN kernels (tests and debugging only).
+
+Every function here has the signature and buffer semantics of its native
+counterpart in :mod:`fedmi.ops.conv` / :mod:`fedmi.ops.cnn` (NHWC bf16
+activations, fp32 stats, outputs written in place) but computes with plain
+torch ops, so the native engines' *wiring* — which buffer feeds which launch,
+residual fan-in, BN branch pairing, running-stat updates — can be verified on
+a CPU-only host.  :func:`emulated` swaps them in for the duration of a
+``with`` block.  Never used on a GPU run: the native paths fail loudly when
+the extension is missing instead of falling back here.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import cnn, conv
+
+_BF = torch.bfloat16
+
+
+def _nchw(t: torch.Tensor) -> torch.Tensor:
+    return t.permute(0, 3, 1, 2).float()
+
+
+def _nhwc_into(out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+    out.copy_(t.permute(0, 2, 3, 1).to(out.dtype))
+    return out
+
+
+# packed image -> fp32 master it was packed from: the emulated convolutions use
+# the master weights, so an fp32-activation run is exact up to fp32 rounding
+_MASTER: dict = {}
+
+
+@torch.no_grad()
+def pack_weight(w, c_pad=None, out=None):
+    O, Cw, R, S = w.shape
+    C = c_pad or conv.pad8(Cw)
+    img = torch.zeros(O, R, S, C, dtype=_BF, device=w.device)
+    img[..., :Cw] = w.permute(0, 2, 3, 1).to(_BF)
+    if out is None:
+        out = img
+    else:
+        out.copy_(img)
+    _MASTER[out.data_ptr()] = w
+    return out
+
+
+def _w_from_img(wr: torch.Tensor, Cw: Optional[int]) -> torch.Tensor:
+    m = _MASTER.get(wr.data_ptr())
+    w = m.float() if m is not None and m.shape[2:] == wr.shape[1:3] else wr.permute(0, 3, 1, 2).float()
+    return w if Cw is None else w[:, :Cw]
+
+
+def _stats_add(stats, y_bf16_nhwc, shift=None):
+    if stats is not None:
+        v = y_bf16_nhwc.float().reshape(-1, y_bf16_nhwc.shape[-1])
+        if shift is not None:
+            v = v - shift
+        stats.view(2, -1)[0] += v.sum(0)
+        stats.view(2, -1)[1] += (v * v).sum(0)
+
+
+@torch.no_grad()
+def conv2d_fwd(x, wrsc, stride, pad, Cw=None, stats=None, out=None, shift=None):
+    Cw = Cw or x.shape[3]
+    y = F.conv2d(_nchw(x)[:, :Cw], _w_from_img(wrsc, Cw), stride=stride, padding=pad)
+    if out is None:
+        out = torch.empty(y.shape[0], y.shape[2], y.shape[3], y.shape[1], dtype=_BF, device=x.device)
+    _nhwc_into(out, y)
+    _stats_add(stats, out, shift)
+    return out
+
+
+@torch.no_grad()
+def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None):
+    N, H, W, C = x_shape
+    Cw = Cw or C
+    dx = torch.nn.grad.conv2d_input((N, Cw, H, W), _w_from_img(wrsc, Cw), _nchw(dy), stride=stride, padding=pad)
+    full = torch.zeros(N, C, H, W, device=dy.device)
+    full[:, :Cw] = dx
+    if out is None:
+        out = torch.empty(*x_shape, dtype=_BF, device=dy.device)
+    return _nhwc_into(out, full)
+
+
+@torch.no_grad()
+def conv2d_wgrad(x, dy, R, S, stride, pad, Cw=None, out=None, accumulate=False, splits=0, ws=None):
+    Cw = Cw or x.shape[3]
+    O = dy.shape[3]
+    dw = torch.nn.grad.conv2d_weight(_nchw(x)[:, :Cw], (O, Cw, R, S), _nchw(dy), stride=stride, padding=pad)
+    if out is None:
+        return dw
+    if accumulate:
+        out += dw
+    else:
+        out.copy_(dw)
+    return out
+
+
+def wgrad_ws_floats(*a, **k):
+    return 1
+
+
+@torch.no_grad()
+def dwconv_fwd(x, w, stride, pad, stats=None, out=None, shift=None):
+    C = x.shape[3]
+    y = F.conv2d(_nchw(x), w.float(), stride=stride, padding=pad, groups=C)
+    if out is None:
+        out = torch.empty(y.shape[0], y.shape[2], y.shape[3], C, dtype=_BF, device=x.device)
+    _nhwc_into(out, y)
+    _stats_add(stats, out, shift)
+    return out
+
+
+@torch.no_grad()
+def dwconv_dgrad(dy, w, x_shape, stride, pad, out=None):
+    N, H, W, C = x_shape
+    dx = torch.nn.grad.conv2d_input((N, C, H, W), w.float(), _nchw(dy), stride=stride, padding=pad, groups=C)
+    if out is None:
+        out = torch.empty(*x_shape, dtype=_BF, device=dy.device)
+    return _nhwc_into(out, dx)
+
+
+@torch.no_grad()
+def dwconv_wgrad(x, dy, R, stride, pad, out=None, accumulate=False, ws=None):
+    C = x.shape[3]
+    dw = torch.nn.grad.conv2d_weight(_nchw(x), (C, 1, R, R), _nchw(dy), stride=stride, padding=pad, groups=C)
+    if out is None:
+        return dw
+    if accumulate:
+        out += dw
+    else:
+        out.copy_(dw)
+    return out
+
+
+def dwconv_ws_floats(*a, **k):
+    return 1
+
+
+@torch.no_grad()
+def prep_input(images_u8, base, nb, augment, seed, round_ctr, out=None, dbase=None):
+    import numpy as np
+
+    from ..engine.data import augment_normalize
+
+    b = base + (int(dbase.view(-1)[0]) if dbase is not None else 0)
+    gidx = np.arange(b, b + nb) if augment else None
+    x = augment_normalize(images_u8[b:b + nb], gidx, seed, int(round_ctr.view(-1)[0]))
+    full = torch.zeros(nb, 8, 32, 32, device=images_u8.device)
+    full[:, :3] = x
+    if out is None:
+        out = torch.empty(nb, 32, 32, 8, dtype=_BF, device=images_u8.device)
+    return _nhwc_into(out, full)
+
+
+@torch.no_grad()
+def sched_next(sched, counter, cur):
+    i = int(counter.view(-1)[0])
+    cur.view(-1)[0] = sched.view(-1)[i]
+    counter.view(-1)[0] = i + 1
+
+
+def _coeffs(p: "cnn.BNParams", M: int, train: bool, eps: float, mom: float):
+    if train:
+        ms = p.stats.view(2, -1)[0] / M
+        var = torch.clamp(p.stats.view(2, -1)[1] / M - ms * ms, min=0.0)
+        mean = ms + (p.shift if p.shift is not None else 0.0)
+        inv = torch.rsqrt(var + eps)
+        p.smean.copy_(mean)
+        p.sinv.copy_(inv)
+        if p.rmean is not None:
+            p.rmean.mul_(1 - mom).add_(mom * mean)
+            p.rvar.mul_(1 - mom).add_(mom * var * M / max(M - 1, 1))
+        if p.nbt is not None:
+            p.nbt += 1
+    else:
+        mean, inv = p.rmean, torch.rsqrt(p.rvar + eps)
+    sc = p.gamma * inv
+    return sc, p.beta - mean * sc
+
+
+@torch.no_grad()
+def bn_apply(z, a, y, train, relu, z2=None, b=None, res=None, eps=1e-5, momentum=0.1):
+    C = z.shape[-1]
+    M = z.numel() // C
+    sc, sh = _coeffs(a, M, train, eps, momentum)
+    v = z.float().reshape(M, C) * sc + sh
+    if b is not None:
+        sc2, sh2 = _coeffs(b, M, train, eps, momentum)
+        v = v + z2.float().reshape(M, C) * sc2 + sh2
+    elif res is not None:
+        v = v + res.float().reshape(M, C)
+    if relu:
+        v = torch.relu(v)
+    y.copy_(v.reshape(y.shape).to(y.dtype))
+    return y
+
+
+@torch.no_grad()
+def bn_bwd(dya, za, a, dgamma_a, dbeta_a, dza, red, dyb=None, y=None, zb=None, b=None, dgamma_b=None,
+           dbeta_b=None, dzb=None, gout=None):
+    C = za.shape[-1]
+    M = za.numel() // C
+    g = dya.float().reshape(M, C)
+    if dyb is not None:
+        g = g + dyb.float().reshape(M, C)
+    if y is not None:
+        g = torch.where(y.float().reshape(M, C) > 0, g, torch.zeros_like(g))
+    if gout is not None:
+        gout.copy_(g.reshape(gout.shape).to(gout.dtype))
+    sg = g.sum(0)
+    for z, p, dg, db, dz in ((za, a, dgamma_a, dbeta_a, dza), (zb, b, dgamma_b, dbeta_b, dzb)):
+        if z is None:
+            continue
+        xhat = (z.float().reshape(M, C) - p.smean) * p.sinv
+        sgx = (g * xhat).sum(0)
+        dg.copy_(sgx)
+        db.copy_(sg)
+        if p.shift is not None:
+            p.shift.copy_(p.smean)
+        d = p.gamma * p.sinv * (g - sg / M - xhat * sgx / M)
+        dz.copy_(d.reshape(dz.shape).to(dz.dtype))
+
+
+@torch.no_grad()
+def head(y, labels, base, W, b, stats, train, pooled=None, dlog=None, dy=None, dW=None, db=None, dbase=None):
+    N, H, Wd, C = y.shape
+    base = base + (int(dbase.view(-1)[0]) if dbase is not None else 0)
+    lab = labels[base:base + N].long()
+    pl = y.float().reshape(N, H * Wd, C).mean(1)
+    logits = pl @ W.t() + b
+    lse = torch.logsumexp(logits, 1)
+    stats[0] += float((lse - logits.gather(1, lab[:, None])[:, 0]).sum())
+    iv = stats.view(torch.int32)
+    iv[1] += int((logits.argmax(1) == lab).sum())
+    iv[2] += N
+    if not train:
+        return
+    dl = (torch.softmax(logits, 1) - F.one_hot(lab, W.shape[0]).float()) / N
+    pooled.copy_(pl)
+    dlog.copy_(dl)
+    dW.copy_(dl.t() @ pl)
+    db.copy_(dl.sum(0))
+    dp = (dl @ W) / (H * Wd)
+    dy.copy_(dp[:, None, None, :].expand(N, H, Wd, C).to(dy.dtype))
+
+
+class _NativeStub:
+    """Stands in for the extension module under emulation: only flat SGD is needed."""
+
+    @staticmethod
+    def sgd_flat(st, p, g, buf, n, lr, m, wd, damp, nesterov, first):
+        raise RuntimeError("emulated engine: use the torch update path")
+
+
+@contextlib.contextmanager
+def emulated():
+    """Swap fedmi.ops kernels (and native.require) for their torch emulations."""
+    from .. import native
+
+    saved = []
+
+    def swap(mod, name, fn):
+        saved.append((mod, name, getattr(mod, name)))
+        setattr(mod, name, fn)
+
+    for name in ("pack_weight", "conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
+                 "dwconv_dgrad", "dwconv_wgrad", "dwconv_ws_floats"):
+        swap(conv, name, globals()[name])
+    for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "head"):
+        swap(cnn, name, globals()[name])
+    swap(native, "require", lambda: _NativeStub())
+    swap(native, "stream_handle", lambda device=None: 0)
+    try:
+        yield
+    finally:
+        for mod, name, fn in reversed(saved):
+            setattr(mod, name, fn)

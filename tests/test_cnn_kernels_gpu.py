@@ -1,0 +1,227 @@
+"""Implicit-GEMM conv (fwd / dgrad / wgrad), BatchNorm fwd/bwd and the
+classifier head vs PyTorch fp32 references on the same bf16-rounded inputs."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fedmi.ops import cnn, conv
+
+pytestmark = pytest.mark.gpu
+
+# (N, H, W, Cw, O, R, stride, pad): ResNet-18 CIFAR shapes at reduced batch + edge cases
+SHAPES = [
+    (4, 32, 32, 3, 64, 3, 1, 1),       # stem (input padded 3 -> 8 channels)
+    (4, 32, 32, 64, 64, 3, 1, 1),      # layer1
+    (4, 32, 32, 64, 128, 3, 2, 1),     # layer2 downsample
+    (4, 32, 32, 64, 128, 1, 2, 0),     # projection shortcut
+    (8, 8, 8, 256, 512, 3, 2, 1),      # layer4 downsample
+    (16, 4, 4, 512, 512, 3, 1, 1),     # layer4
+    (3, 7, 5, 24, 40, 3, 1, 1),        # odd spatial, partial tiles
+    (2, 9, 9, 16, 8, 5, 2, 2),         # 5x5 stride 2
+]
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / (b.abs().max() + 1e-6))
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _make(shape, dev, seed=0):
+    N, H, W, Cw, O, R, st, pad = shape
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(N, Cw, H, W, generator=g).to(dev).bfloat16().float()
+    w = (torch.randn(O, Cw, R, R, generator=g) / (Cw * R * R) ** 0.5).to(dev)
+    wb = w.bfloat16().float()
+    C = conv.pad8(Cw)
+    xn = torch.zeros(N, H, W, C, dtype=torch.bfloat16, device=dev)
+    xn[..., :Cw] = _nhwc(x).bfloat16()
+    return x, w, wb, xn
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+def test_conv_fwd_and_stats(gpu_device, shape):
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device)
+    wr = conv.pack_weight(w)
+    stats = torch.zeros(2, O, device=gpu_device)
+    y = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=stats)
+    ref = F.conv2d(x, wb, stride=st, padding=pad)
+    torch.cuda.synchronize()
+    assert _rel(y.float(), _nhwc(ref)) < 1e-2
+    yb = y.float()
+    assert torch.allclose(stats[0], yb.sum((0, 1, 2)), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(stats[1], (yb * yb).sum((0, 1, 2)), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+def test_conv_dgrad_wgrad(gpu_device, shape):
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device, seed=1)
+    xr = x.clone().requires_grad_(True)
+    wr_ = wb.clone().requires_grad_(True)
+    out = F.conv2d(xr, wr_, stride=st, padding=pad)
+    gy = torch.randn_like(out).bfloat16().float()
+    out.backward(gy)
+    dyn = _nhwc(gy).bfloat16()
+    wpk = conv.pack_weight(w)
+    dx = conv.conv2d_dgrad(dyn, wpk, xn.shape, st, pad, Cw=Cw)
+    dw = conv.conv2d_wgrad(xn, dyn, R, R, st, pad, Cw=Cw)
+    torch.cuda.synchronize()
+    assert _rel(dx[..., :Cw].float(), _nhwc(xr.grad)) < 1e-2
+    if Cw < dx.shape[-1]:   # padded input channels see zero weights
+        assert float(dx[..., Cw:].float().abs().max()) == 0.0
+    assert _rel(dw, wr_.grad) < 1e-2
+
+
+def test_conv_wgrad_split_invariance(gpu_device):
+    shape = (8, 16, 16, 64, 64, 3, 1, 1)
+    _, _, _, xn = _make(shape, gpu_device, seed=2)
+    dy = torch.randn(8, 16, 16, 64, device=gpu_device).bfloat16()
+    a = conv.conv2d_wgrad(xn, dy, 3, 3, 1, 1, splits=1)
+    b = conv.conv2d_wgrad(xn, dy, 3, 3, 1, 1, splits=7)
+    torch.cuda.synchronize()
+    assert _rel(a, b) < 1e-4
+
+
+def _bn_ref(z, gamma, beta, eps=1e-5):
+    mean = z.mean(0)
+    var = z.var(0, unbiased=False)
+    return (z - mean) / torch.sqrt(var + eps) * gamma + beta, mean, var
+
+
+def test_bn_forward_backward_with_projection_residual(gpu_device):
+    torch.manual_seed(3)
+    dev = gpu_device
+    M, C = 4 * 16 * 16, 128
+    za = (torch.randn(M, C, device=dev) * 2 + 0.5).bfloat16()
+    zb = (torch.randn(M, C, device=dev) - 0.3).bfloat16()
+    ga, ba = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+    gb, bb = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+    sa = torch.stack([za.float().sum(0), (za.float() ** 2).sum(0)])
+    sb = torch.stack([zb.float().sum(0), (zb.float() ** 2).sum(0)])
+    rma, rva, rmb, rvb = (torch.zeros(C, device=dev), torch.ones(C, device=dev),
+                          torch.zeros(C, device=dev), torch.ones(C, device=dev))
+    nbt = torch.zeros(1, dtype=torch.int64, device=dev)
+    sma, sia, smb, sib = (torch.empty(C, device=dev) for _ in range(4))
+    A = cnn.bn_desc(sa, ga, ba, rma, rva, nbt, sma, sia)
+    B = cnn.bn_desc(sb, gb, bb, rmb, rvb, None, smb, sib)
+    y = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    cnn.bn_apply(za, A, y, train=True, relu=True, z2=zb, b=B)
+    # reference
+    zar, zbr = za.float().requires_grad_(True), zb.float().requires_grad_(True)
+    gar, gbr = ga.clone().requires_grad_(True), gb.clone().requires_grad_(True)
+    bar, bbr = ba.clone().requires_grad_(True), bb.clone().requires_grad_(True)
+    ya, mean_a, var_a = _bn_ref(zar, gar, bar)
+    yb, _, _ = _bn_ref(zbr, gbr, bbr)
+    yref = F.relu(ya + yb)
+    torch.cuda.synchronize()
+    assert _rel(y.float(), yref) < 1e-2
+    assert torch.allclose(rma, 0.1 * mean_a.detach(), atol=1e-4)
+    assert torch.allclose(rva, 0.9 + 0.1 * var_a.detach() * M / (M - 1), rtol=1e-3)
+    assert int(nbt.item()) == 1
+    # backward with a residual fan-in (dya + dyb)
+    dya = torch.randn(M, C, device=dev).bfloat16()
+    dyb = torch.randn(M, C, device=dev).bfloat16()
+    yref.backward(dya.float() + dyb.float())
+    dza, dzb, gout = (torch.empty(M, C, dtype=torch.bfloat16, device=dev) for _ in range(3))
+    dga, dba, dgb, dbb = (torch.empty(C, device=dev) for _ in range(4))
+    red = torch.zeros(3, C, device=dev)
+    cnn.bn_bwd(dya, za, A, dga, dba, dza, red, dyb=dyb, y=y, zb=zb, b=B, dgamma_b=dgb, dbeta_b=dbb, dzb=dzb,
+               gout=gout)
+    torch.cuda.synchronize()
+    assert _rel(dza.float(), zar.grad) < 2e-2
+    assert _rel(dzb.float(), zbr.grad) < 2e-2
+    assert _rel(dga, gar.grad) < 1e-2 and _rel(dba, bar.grad) < 1e-2
+    assert _rel(dgb, gbr.grad) < 1e-2 and _rel(dbb, bbr.grad) < 1e-2
+    mask = (y.float() > 0).float()
+    assert _rel(gout.float(), (dya.float() + dyb.float()) * mask) < 1e-2
+
+
+def test_bn_eval_uses_running_stats(gpu_device):
+    dev = gpu_device
+    M, C = 64, 64
+    z = torch.randn(M, C, device=dev).bfloat16()
+    g, b = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    rm, rv = torch.randn(C, device=dev), torch.rand(C, device=dev) + 0.5
+    y = torch.empty_like(z)
+    res = torch.randn(M, C, device=dev).bfloat16()
+    cnn.bn_apply(z, cnn.bn_desc(None, g, b, rm, rv), y, train=False, relu=False, res=res)
+    ref = (z.float() - rm) / torch.sqrt(rv + 1e-5) * g + b + res.float()
+    torch.cuda.synchronize()
+    assert _rel(y.float(), ref) < 1e-2
+
+
+def test_head_ce_and_grads(gpu_device):
+    torch.manual_seed(4)
+    dev = gpu_device
+    N, HW, C, J = 16, 16, 512, 10
+    y = torch.randn(N, 4, 4, C, device=dev).bfloat16()
+    labels = torch.randint(0, J, (N,), device=dev, dtype=torch.int32)
+    W = torch.randn(J, C, device=dev) * 0.05
+    b = torch.randn(J, device=dev) * 0.1
+    stats = torch.zeros(4, device=dev)
+    pooled = torch.empty(N, C, device=dev)
+    dlog = torch.empty(N, J, device=dev)
+    dy = torch.empty_like(y)
+    dW = torch.empty(J, C, device=dev)
+    db = torch.empty(J, device=dev)
+    cnn.head(y, labels, 0, W, b, stats, True, pooled, dlog, dy, dW, db)
+    yr = y.float().requires_grad_(True)
+    Wr, br = W.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    logits = F.linear(yr.mean((1, 2)), Wr, br)
+    loss = F.cross_entropy(logits, labels.long())
+    loss.backward()
+    torch.cuda.synchronize()
+    s = stats.view(torch.int32)
+    assert abs(float(stats[0]) / N - float(loss)) < 1e-3
+    assert int(s[1]) == int((logits.argmax(1) == labels.long()).sum()) and int(s[2]) == N
+    assert _rel(dW, Wr.grad) < 1e-4 and _rel(db, br.grad) < 1e-4
+    assert _rel(dy.float(), yr.grad) < 1e-2
+
+
+def test_prep_input_matches_host_twin(gpu_device):
+    from fedmi.engine.data import augment_normalize
+    import numpy as np
+
+    dev = gpu_device
+    imgs = torch.randint(0, 256, (10, 3, 32, 32), dtype=torch.uint8, device=dev)
+    rc = torch.tensor([3, 0, 0, 0], dtype=torch.int32, device=dev)
+    out = cnn.prep_input(imgs, 2, 6, True, 1234, rc)
+    ref = augment_normalize(imgs[2:8], np.arange(2, 8), 1234, 3)
+    torch.cuda.synchronize()
+    assert torch.allclose(out[..., :3].float(), _nhwc(ref), atol=2e-2)
+    assert float(out[..., 3:].float().abs().max()) == 0.0
+
+
+DW_SHAPES = [(4, 32, 32, 32, 3, 1), (4, 32, 32, 64, 3, 2), (8, 4, 4, 1024, 3, 1), (2, 16, 16, 96, 5, 2),
+             (2, 8, 8, 16, 7, 1)]
+
+
+@pytest.mark.parametrize("shape", DW_SHAPES, ids=[str(s) for s in DW_SHAPES])
+def test_depthwise_fwd_dgrad_wgrad(gpu_device, shape):
+    N, H, W, C, R, st = shape
+    pad = R // 2
+    dev = gpu_device
+    torch.manual_seed(5)
+    x = torch.randn(N, C, H, W, device=dev).bfloat16().float().requires_grad_(True)
+    w = (torch.randn(C, 1, R, R, device=dev) * 0.2)
+    wb = w.bfloat16().float().requires_grad_(True)
+    ref = F.conv2d(x, w, stride=st, padding=pad, groups=C)
+    gy = torch.randn_like(ref).bfloat16().float()
+    ref.backward(gy)
+    wref = F.conv2d(x.detach(), wb, stride=st, padding=pad, groups=C)
+    wref.backward(gy)
+    xn = _nhwc(x.detach()).bfloat16()
+    stats = torch.zeros(2, C, device=dev)
+    y = conv.dwconv_fwd(xn, w, st, pad, stats=stats)
+    dx = conv.dwconv_dgrad(_nhwc(gy).bfloat16(), w, xn.shape, st, pad)
+    dw = conv.dwconv_wgrad(xn, _nhwc(gy).bfloat16(), R, st, pad)
+    torch.cuda.synchronize()
+    assert _rel(y.float(), _nhwc(ref.detach())) < 1e-2
+    yb = y.float()
+    assert torch.allclose(stats[0], yb.sum((0, 1, 2)), rtol=1e-3, atol=1e-2)
+    assert _rel(dx.float(), _nhwc(x.grad)) < 1e-2
+    assert _rel(dw, wb.grad) < 1e-2
