@@ -36,14 +36,21 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-# Reference (CPU-measured) rounds/s with LeNet at N clients.
-BASELINE_ROUNDS_PER_S = {1: 0.373, 2: 0.428, 4: 0.436, 8: 0.426}
+# Reference (CPU-measured, BASELINE.md / SURVEY.md §6) rounds/s at N clients.
+BASELINE_ROUNDS_PER_S = {
+    "lenet": {1: 0.373, 2: 0.428, 4: 0.436, 8: 0.426},
+    "mobilenet": {2: 0.0137},
+}
 N_TRAIN, N_TEST, BATCH = 50000, 10000, 128
 
 
-def _baseline_samples_per_s(n: int) -> float:
-    key = min(BASELINE_ROUNDS_PER_S, key=lambda k: abs(k - n))
-    return BASELINE_ROUNDS_PER_S[key] * N_TRAIN
+def _baseline_rounds(model: str, n: int):
+    table = BASELINE_ROUNDS_PER_S.get(model.lower().replace("_", ""))
+    if not table:
+        return None
+    if model.lower() == "lenet":
+        return table[min(table, key=lambda k: abs(k - n))]
+    return table.get(n)
 
 
 def main() -> int:
@@ -51,7 +58,10 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20, help="timed federated rounds")
     ap.add_argument("--warmup", type=int, default=3, help="untimed rounds")
-    ap.add_argument("--model", default="lenet")
+    ap.add_argument("--model", default="lenet",
+                    help="lenet (headline) | resnet18 | mobilenet | ... (native HIP engines on GPU)")
+    ap.add_argument("--noniid", type=int, default=0,
+                    help="non-IID label shards per client (BASELINE config 3: ResNet-18, 2 shards); 0 = strided IID")
     ap.add_argument("--compress", default="none", choices=["none", "topk", "int8"],
                     help="-c Y data-plane compression of the FedAvg update")
     ap.add_argument("--topk-ratio", type=float, default=0.01)
@@ -87,7 +97,14 @@ def main() -> int:
     cfg = TrainerConfig(seed=17, use_graph=not args.no_graph)
     trainer = build_trainer(args.model, data, device, cfg)
     broadcast_state_(trainer, 0)                     # one shared init (reference quirk A7 fixed)
-    trainer.set_schedule(*strided_schedule(N_TRAIN, BATCH, rank, world))
+    if args.noniid > 0:     # McMahan-style label shards: each client trains only its own shard
+        from fedmi.engine.data import contiguous_schedule, label_shard_indices
+
+        shards = label_shard_indices(data.train.y.cpu().numpy(), world, args.noniid, seed=0)
+        trainer.set_train_data(data.train.subset(shards[rank]))
+        trainer.set_schedule(*contiguous_schedule(len(shards[rank]), BATCH))
+    else:
+        trainer.set_schedule(*strided_schedule(N_TRAIN, BATCH, rank, world))
     agg = FedAvg(compressor=make_compressor(args.compress, args.topk_ratio, trainer))
 
     root = Path(args.ckpt_dir or tempfile.mkdtemp(prefix="fedmi_bench_"))
@@ -129,8 +146,10 @@ def main() -> int:
     ev_stats = trainer.eval_stats() if not args.no_eval else None
     rounds_per_s = args.steps / T
     value = rounds_per_s * N_TRAIN
+    base_r = _baseline_rounds(args.model, world)
     out = {
-        "metric": "rounds/sec + samples/sec/client, 2-conv CNN FedAvg at 1/2/4/8 MI355X clients",
+        "metric": "rounds/sec + samples/sec/client, 2-conv CNN FedAvg at 1/2/4/8 MI355X clients"
+        if args.model.lower() == "lenet" else f"rounds/sec + samples/sec/client, {args.model} FedAvg",
         "value": round(value, 3),
         "unit": "samples/s",
         "n_gpus": world,
@@ -139,17 +158,18 @@ def main() -> int:
         "ms_per_step": round(T / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "strong",
-        "vs_baseline": round(value / _baseline_samples_per_s(world), 3),
+        "vs_baseline": round(rounds_per_s / base_r, 3) if base_r else None,
         "dtype": "bf16",
         "data": "synthetic (CIFAR-shaped uint8 50k/10k, class-structured), random-init weights",
         "config": {"model": args.model, "global_batch": BATCH * world, "seq_len": None,
                    "parallelism": f"fedavg-dp{world}", "per_client_batch": BATCH,
                    "local_epochs_per_round": 1, "eval_per_round": not args.no_eval,
+                   "data_split": f"noniid-{args.noniid}-shards" if args.noniid else "strided-iid",
                    "aggregation": "rccl-allreduce" + ("" if args.compress == "none" else f"+{args.compress}"),
                    "hip_graph": not args.no_graph},
         "rounds_per_sec": round(rounds_per_s, 4),
         "samples_per_sec_per_client": round(value / world, 3),
-        "baseline_rounds_per_sec": BASELINE_ROUNDS_PER_S.get(world),
+        "baseline_rounds_per_sec": base_r,
         "last_round": {"train_loss": round(tr_stats.loss, 4), "train_acc": round(tr_stats.acc, 3),
                        **({"test_loss": round(ev_stats.loss, 4), "test_acc": round(ev_stats.acc, 3)}
                           if ev_stats else {})},

@@ -93,7 +93,9 @@ def contiguous_schedule(n: int, batch: int):
 
 
 def label_shard_indices(labels: np.ndarray, world: int, shards_per_client: int = 2, seed: int = 0):
-    """Non-IID split (McMahan et al.): sort by label, cut into world*spc shards, deal spc per client."""
+    """Non-IID split (McMahan et al.): sort by label, cut into world*spc shards, deal spc per client.
+
+    Each client's indices come back in ascending index order (a fixed shuffle of its labels)."""
     rng = np.random.default_rng(seed)
     order = np.argsort(labels, kind="stable")
     nshards = world * shards_per_client
@@ -135,7 +137,8 @@ class FedDataset:
         return FedDataset(self.name, self.train.to(device), self.test.to(device), self.mean, self.std, self.augment)
 
 
-def _synthetic_images(n: int, shape, n_classes: int, seed: int, device, split: int = 0) -> ImageSet:
+def _synthetic_images(n: int, shape, n_classes: int, seed: int, device, split: int = 0, contrast: float = 0.12,
+                      noise_std: float = 0.3) -> ImageSet:
     """Class-structured synthetic images (learnable), uint8, generated on ``device``.
 
     The class templates depend only on ``seed`` (shared by train and test);
@@ -155,18 +158,18 @@ def _synthetic_images(n: int, shape, n_classes: int, seed: int, device, split: i
     gd = torch.Generator(device=device).manual_seed(seed * 1000003 + split + 1)
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
-        noise = torch.randn(e - s, c, h, w, generator=gd, device=device) * 0.3
+        noise = torch.randn(e - s, c, h, w, generator=gd, device=device) * noise_std
         # contrast/noise chosen so the reference recipe (SGD lr 0.1, m 0.9, no BN) trains
         # LeNet stably for 24+ epochs (fp32 torch: ~50 % test acc, loss ~1.77); higher
         # contrast makes that recipe diverge to a dead network after ~12 epochs
-        img = templates[labels_d[s:e]] * 0.12 + 0.44 + noise
+        img = templates[labels_d[s:e]] * contrast + 0.5 - contrast / 2 + noise
         out[s:e] = (img.clamp_(0, 1) * 255.0).round_().to(torch.uint8)
     return ImageSet(out, labels_d.to(torch.int32))
 
 
-def synthetic_cifar10(n_train=50000, n_test=10000, seed=0, device="cpu") -> FedDataset:
-    tr = _synthetic_images(n_train, (3, 32, 32), 10, seed, device, split=0)
-    te = _synthetic_images(n_test, (3, 32, 32), 10, seed, device, split=1)
+def synthetic_cifar10(n_train=50000, n_test=10000, seed=0, device="cpu", contrast=0.12, noise_std=0.3) -> FedDataset:
+    tr = _synthetic_images(n_train, (3, 32, 32), 10, seed, device, split=0, contrast=contrast, noise_std=noise_std)
+    te = _synthetic_images(n_test, (3, 32, 32), 10, seed, device, split=1, contrast=contrast, noise_std=noise_std)
     return FedDataset("synthetic-cifar10", tr, te, CIFAR_MEAN, CIFAR_STD, True)
 
 
@@ -200,7 +203,10 @@ def cifar10_binary(root: str | Path) -> FedDataset:
 
 def make_dataset(spec: str, device="cpu", n_train: int | None = None, n_test: int | None = None,
                  seed: int = 0) -> FedDataset:
-    """``synthetic-cifar10`` | ``synthetic-mnist`` | ``cifar10-bin:<dir>``."""
+    """``synthetic-cifar10`` | ``synthetic-cifar10-easy`` | ``synthetic-mnist`` | ``cifar10-bin:<dir>``.
+
+    ``-easy``: high-contrast, low-noise templates (deep BN nets learn it in a few epochs; the
+    default low-contrast set is tuned so the reference LeNet recipe trains stably)."""
     if spec.startswith("cifar10-bin:"):
         ds = cifar10_binary(spec.split(":", 1)[1])
         if n_train:
@@ -210,6 +216,8 @@ def make_dataset(spec: str, device="cpu", n_train: int | None = None, n_test: in
         return ds.to(device)
     if spec in ("synthetic-cifar10", "synthetic", "cifar10-synthetic"):
         return synthetic_cifar10(n_train or 50000, n_test or 10000, seed, device)
+    if spec == "synthetic-cifar10-easy":
+        return synthetic_cifar10(n_train or 50000, n_test or 10000, seed, device, contrast=0.6, noise_std=0.1)
     if spec in ("synthetic-mnist", "mnist-synthetic"):
         return synthetic_mnist(n_train or 60000, n_test or 10000, seed, device)
     raise ValueError(f"unknown dataset spec {spec!r}")
