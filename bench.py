@@ -10,7 +10,11 @@ A *step* is one federated round with the reference's semantics
      training images at batch 128 with RandomCrop+HFlip augmentation, SGD
      (lr 0.1, momentum 0.9, wd 5e-4)   [fused HIP kernels, hipGraph replay]
   2. FedAvg of the full model across clients   [RCCL all-reduce over xGMI]
-  3. every client evaluates the global model on the full 10,000-image test set
+  3. the global model is evaluated on the full 10,000-image test set: split
+     over the N clients (they all hold the same averaged model), per-round
+     (loss, correct, count) kept on device and summed over clients in one
+     collective -- the same numbers as every client evaluating all of it
+     (``--eval-full`` runs that reference-literal redundant variant)
   4. the global model is persisted as Primary/optimizedModel.pth (rank 0) and
      every client checkpoint as checkpoint/<client>.pth ({'net','acc','epoch'}),
      flushed to disk inside the timed region.
@@ -66,6 +70,9 @@ def main() -> int:
                     help="-c Y data-plane compression of the FedAvg update")
     ap.add_argument("--topk-ratio", type=float, default=0.01)
     ap.add_argument("--no-eval", action="store_true", help="skip per-round eval (NOT the headline config)")
+    ap.add_argument("--eval-full", action="store_true",
+                    help="every client evaluates the whole test set (reference-literal, redundant); default: "
+                         "the 10k test set is split over the clients and the accumulators summed")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--ckpt-dir", default=None)
     ap.add_argument("--json-out", default=None)
@@ -90,7 +97,7 @@ def main() -> int:
     from fedmi.engine import build_trainer
     from fedmi.engine.base import TrainerConfig
     from fedmi.engine.data import make_dataset, strided_schedule
-    from fedmi.parallel.fedavg import FedAvg, broadcast_state_
+    from fedmi.parallel.fedavg import EvalHistory, FedAvg, broadcast_state_, eval_shard
     from fedmi.parallel.compress import make_compressor
 
     data = make_dataset("synthetic-cifar10", device=device, n_train=N_TRAIN, n_test=N_TEST, seed=0)
@@ -106,6 +113,9 @@ def main() -> int:
     else:
         trainer.set_schedule(*strided_schedule(N_TRAIN, BATCH, rank, world))
     agg = FedAvg(compressor=make_compressor(args.compress, args.topk_ratio, trainer))
+    if world > 1 and not args.eval_full:
+        trainer.set_test_data(eval_shard(data.test, rank, world))
+    hist = EvalHistory(trainer, args.warmup + args.steps)
 
     root = Path(args.ckpt_dir or tempfile.mkdtemp(prefix="fedmi_bench_"))
     prim = mount_dir(root, primary=True) if rank == 0 else None
@@ -117,10 +127,10 @@ def main() -> int:
         agg.average(trainer)
         if not args.no_eval:
             trainer.evaluate()
-        sd = trainer.state_dict()
-        if prim is not None:
-            writer.submit(prim / OPTIMIZED_MODEL, sd, acc=1, epoch=r + 1)
-        writer.submit(cpath, sd, acc=1, epoch=r + 1)
+            hist.record()
+        # global model -> Primary/optimizedModel.pth (rank 0) + this client's checkpoint, one snapshot
+        writer.submit([prim / OPTIMIZED_MODEL, cpath] if prim is not None else cpath, trainer.state_dict(),
+                      acc=1, epoch=r + 1)
 
     def barrier():
         if world > 1:
@@ -135,6 +145,7 @@ def main() -> int:
     for r in range(args.warmup, args.warmup + args.steps):
         one_round(r)
     writer.flush()
+    rounds_eval = hist.reduce() if not args.no_eval and not args.eval_full else None
     barrier()
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
@@ -143,7 +154,12 @@ def main() -> int:
     T = float(elapsed.item())
 
     tr_stats = trainer.train_stats()
-    ev_stats = trainer.eval_stats() if not args.no_eval else None
+    if args.no_eval:
+        ev_stats = None
+    elif rounds_eval is not None:
+        ev_stats = rounds_eval[-1]
+    else:
+        ev_stats = trainer.eval_stats()
     rounds_per_s = args.steps / T
     value = rounds_per_s * N_TRAIN
     base_r = _baseline_rounds(args.model, world)
@@ -164,6 +180,7 @@ def main() -> int:
         "config": {"model": args.model, "global_batch": BATCH * world, "seq_len": None,
                    "parallelism": f"fedavg-dp{world}", "per_client_batch": BATCH,
                    "local_epochs_per_round": 1, "eval_per_round": not args.no_eval,
+                   "eval_split": "full-per-client" if args.eval_full or world == 1 else f"1/{world}-per-client",
                    "data_split": f"noniid-{args.noniid}-shards" if args.noniid else "strided-iid",
                    "aggregation": "rccl-allreduce" + ("" if args.compress == "none" else f"+{args.compress}"),
                    "hip_graph": not args.no_graph},

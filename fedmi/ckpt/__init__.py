@@ -109,27 +109,48 @@ class AsyncCheckpointWriter:
         self.written = 0
 
     def _snapshot(self, state_dict):
+        """Device->pinned-host copy of a state dict: ONE copy per device storage.
+
+        State dicts of the fedmi engines are views into one flat fp32 buffer;
+        copying the covered span once replaces a copy (+ pinned alloc) per
+        tensor.  The writer thread later clones every view into its own storage
+        so the file layout is the reference's (one storage per tensor)."""
         out = OrderedDict()
         ev = None
+        groups: Dict[tuple, list] = {}
         for k, v in state_dict.items():
             v = v.detach()
-            if v.is_cuda:
+            if v.is_cuda and v.is_contiguous():
+                key = (v.untyped_storage().data_ptr(), v.dtype, v.device)
+                groups.setdefault(key, []).append((k, v))
+                out[k] = None
+            elif v.is_cuda:
                 host = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
                 host.copy_(v, non_blocking=True)
                 out[k] = host
-                if ev is None:
-                    ev = torch.cuda.Event()
             else:
                 out[k] = v.clone()
-        if ev is not None:
+        for (_, dt, dev), items in groups.items():
+            lo = min(v.storage_offset() for _, v in items)
+            hi = max(v.storage_offset() + v.numel() for _, v in items)
+            base = torch.empty(0, dtype=dt, device=dev).set_(items[0][1].untyped_storage())
+            host = torch.empty(hi - lo, dtype=dt, pin_memory=True)
+            host.copy_(base[lo:hi], non_blocking=True)
+            for k, v in items:
+                o = v.storage_offset() - lo
+                out[k] = host[o:o + v.numel()].view(v.shape)
+        if any(v.is_cuda for v in state_dict.values()):
+            ev = torch.cuda.Event()
             ev.record()
         return out, ev
 
-    def submit(self, path: Path | str, state_dict, acc=1, epoch: int = 0, on_done=None) -> None:
+    def submit(self, path, state_dict, acc=1, epoch: int = 0, on_done=None) -> None:
+        """Queue ``{'net','acc','epoch'}`` for ``path`` (a path or a list of paths sharing one snapshot)."""
         if self._err:
             raise RuntimeError("checkpoint writer failed") from self._err
         snap, ev = self._snapshot(state_dict)
-        self._q.put((Path(path), snap, ev, acc, epoch, on_done))
+        paths = [Path(p) for p in path] if isinstance(path, (list, tuple)) else [Path(path)]
+        self._q.put((paths, snap, ev, acc, epoch, on_done))
 
     def _run(self):
         while True:
@@ -137,15 +158,19 @@ class AsyncCheckpointWriter:
             if item is None:
                 self._q.task_done()
                 return
-            path, snap, ev, acc, epoch, on_done = item
+            paths, snap, ev, acc, epoch, on_done = item
             try:
                 if ev is not None:
                     ev.synchronize()
-                data = to_bytes({"net": snap, "acc": acc, "epoch": int(epoch)})
-                atomic_write(path, data)
-                self.written += 1
-                if on_done is not None:
-                    on_done(path, data)
+                # one storage per tensor, like a plain module.state_dict()
+                net = OrderedDict((k, v.clone() if v.untyped_storage().nbytes() != v.nbytes else v)
+                                  for k, v in snap.items())
+                data = to_bytes({"net": net, "acc": acc, "epoch": int(epoch)})
+                for path in paths:
+                    atomic_write(path, data)
+                    self.written += 1
+                    if on_done is not None:
+                        on_done(path, data)
             except BaseException as e:  # pragma: no cover
                 self._err = e
             finally:

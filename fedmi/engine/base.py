@@ -96,6 +96,21 @@ class LocalTrainer(abc.ABC):
     def eval_stats(self) -> EpochStats:
         ...
 
+    def set_test_data(self, data) -> None:
+        """Replace the evaluation set (e.g. this client's slice of a data-parallel eval)."""
+        t = data.to(self.device)
+        if self.device.type == "cuda" and t.y.dtype != torch.int32:
+            t.y = t.y.to(torch.int32)          # native engines read int32 labels
+        self.test_set = t
+
+    def eval_stats_raw(self) -> torch.Tensor:
+        """Device-resident eval accumulator of the last :meth:`evaluate` (engine-specific layout);
+        :meth:`decode_stats` turns a host copy of it into :class:`EpochStats`."""
+        raise NotImplementedError
+
+    def decode_stats(self, raw: torch.Tensor) -> EpochStats:
+        raise NotImplementedError
+
     @property
     @abc.abstractmethod
     def device(self) -> torch.device:

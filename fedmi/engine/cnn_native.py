@@ -470,9 +470,16 @@ class CNNNativeTrainer(LocalTrainer):
         return self._read_stats(0)
 
     def _read_stats(self, i: int) -> EpochStats:
-        row = self.stats[i].cpu()
-        iv = row.view(torch.int32)
-        return EpochStats(float(row[0]), int(iv[1]), int(iv[2]))
+        return self.decode_stats(self.stats[i].cpu())
+
+    def decode_stats(self, raw: torch.Tensor) -> EpochStats:
+        # head kernel row: {float loss_sum, int correct, int count, pad} in a float32[4] row
+        raw = raw.contiguous()
+        iv = raw.view(torch.int32)
+        return EpochStats(float(raw[0]), int(iv[1]), int(iv[2]))
+
+    def eval_stats_raw(self) -> torch.Tensor:
+        return self.stats[1]
 
     @torch.no_grad()
     def evaluate(self) -> None:

@@ -145,9 +145,15 @@ class LeNetNativeTrainer(LocalTrainer):
         self.engine.step(self._stream(), int(start), int(nb), bool(bump_round))
 
     def _read_stats(self, i: int) -> EpochStats:
-        row = self.stats[i].cpu()
-        loss = float(row[0:1].view(torch.float32).item())
-        return EpochStats(loss, int(row[1]), int(row[2]))
+        return self.decode_stats(self.stats[i].cpu())
+
+    def decode_stats(self, raw: torch.Tensor) -> EpochStats:
+        # lenet::Stats: {float loss_sum, int correct, int count, pad} in an int32[4] row
+        raw = raw.contiguous()
+        return EpochStats(float(raw[0:1].view(torch.float32).item()), int(raw[1]), int(raw[2]))
+
+    def eval_stats_raw(self) -> torch.Tensor:
+        return self.stats[1]
 
     def train_stats(self) -> EpochStats:
         return self._read_stats(0)

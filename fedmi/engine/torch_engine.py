@@ -172,7 +172,13 @@ class TorchTrainer(LocalTrainer):
             self._estats[2] += y.numel()
 
     def eval_stats(self) -> EpochStats:
-        v = self._estats.cpu().tolist()
+        return self.decode_stats(self._estats.cpu())
+
+    def eval_stats_raw(self) -> torch.Tensor:
+        return self._estats
+
+    def decode_stats(self, raw: torch.Tensor) -> EpochStats:
+        v = raw.tolist()
         return EpochStats(v[0], int(v[1]), int(v[2]))
 
     def set_lr(self, lr: float) -> None:

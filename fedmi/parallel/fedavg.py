@@ -101,3 +101,52 @@ class FedAvg:
         self.timer.last_ms = dt
         self.timer.total_ms += dt
         self.timer.calls += 1
+
+
+def eval_shard(test, rank: int, world: int):
+    """Contiguous 1/world slice of the test set for data-parallel evaluation.
+
+    After FedAvg every client holds the same global model, so the reference's
+    "every client evaluates the full test set" (src/client.py:30 ->
+    src/main.py:167-191) computes the same numbers ``world`` times; splitting
+    the set and summing the (loss, correct, count) accumulators over the clients
+    gives the identical global result with 1/world of the work per client.
+    """
+    n = len(test)
+    lo, hi = n * rank // world, n * (rank + 1) // world
+    return type(test)(test.x[lo:hi], test.y[lo:hi])
+
+
+class EvalHistory:
+    """Per-round eval accumulators kept on device; one collective when read.
+
+    ``record()`` after each :meth:`LocalTrainer.evaluate` is a 16-byte
+    device-to-device copy (no host sync, no collective on the round's critical
+    path); ``reduce()`` sums every round's (loss_sum, correct, count) over the
+    group in ONE all-reduce and returns the global per-round EpochStats.
+    """
+
+    def __init__(self, trainer: LocalTrainer, max_rounds: int):
+        raw = trainer.eval_stats_raw()
+        self.trainer = trainer
+        self.buf = torch.zeros((max_rounds,) + tuple(raw.shape), dtype=raw.dtype, device=raw.device)
+        self.n = 0
+
+    def record(self) -> None:
+        if self.n >= self.buf.shape[0]:
+            raise IndexError("EvalHistory full")
+        self.buf[self.n].copy_(self.trainer.eval_stats_raw(), non_blocking=True)
+        self.n += 1
+
+    def reduce(self, group=None):
+        from ..engine.base import EpochStats
+
+        rows = self.buf[: self.n].cpu()
+        vals = [self.trainer.decode_stats(rows[i]) for i in range(self.n)]
+        t = torch.tensor([[s.loss_sum, s.correct, s.count] for s in vals], dtype=torch.float64).reshape(-1, 3)
+        if _world(group) > 1:
+            if _supports_avg(group):           # RCCL reduces device tensors
+                t = t.to(self.buf.device)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+            t = t.cpu()
+        return [EpochStats(float(a), int(round(b)), int(round(c))) for a, b, c in t.tolist()]
