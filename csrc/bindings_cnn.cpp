@@ -9,6 +9,7 @@
 
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "kernels/common.h"
 
@@ -18,8 +19,15 @@ namespace fedmi {
 struct ConvShape {
   int N, H, W, C, Cw, O, P, Q, R, S, st, pad;
 };
-void launch_conv_fwd(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, const float*);
-void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*);
+void launch_conv_fwd(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, const float*, float*, long);
+void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, long);
+long conv_fd_ws_floats(const ConvShape&);
+struct PackItem {
+  const float* w;
+  bf16* wr;
+  int O, Cw, C, RS;
+};
+void launch_conv_pack_multi(hipStream_t, const PackItem*, int);
 void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int);
 long conv_wgrad_ws_floats(const ConvShape&);
 void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int);
@@ -46,7 +54,8 @@ void launch_prep_input(hipStream_t, const uint8_t*, int, const int*, int, int, u
 void launch_sched_next(hipStream_t, const int*, int*, int*);
 void launch_bn_apply(hipStream_t, const bf16*, const BNDesc&, const bf16*, const BNDesc*, const bf16*, bf16*, int, int,
                      float, float, int, int);
-void launch_bn_bwd(hipStream_t, const BNBwdDesc&, float*, int, int);
+void launch_bn_bwd(hipStream_t, const BNBwdDesc&, float*, int, int, float*, long);
+long bn_bwd_ws_floats(int, int);
 void launch_head(hipStream_t, const bf16*, const int*, int, const int*, int, int, int, int, const float*,
                  const float*, float*, float*, bf16*, float*, float*, float*, int);
 }  // namespace fedmi
@@ -92,14 +101,30 @@ BNDesc bn_from(const py::dict& d) {
 
 void fedmi_bind_cnn(py::module_& m) {
   m.def("conv_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
-                       uintptr_t shift) {
+                       uintptr_t shift, uintptr_t ws, long ws_floats) {
     launch_conv_fwd(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(w), P<bf16>(y), P<float>(stats),
-                    P<const float>(shift));
+                    P<const float>(shift), P<float>(ws), ws ? ws_floats : 0);
     check("conv_fwd");
-  });
-  m.def("conv_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx) {
-    launch_conv_dgrad(S(st), shape_from(shp), P<const bf16>(dy), P<const bf16>(w), P<bf16>(dx));
+  }, py::arg("st"), py::arg("shape"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("shift"),
+     py::arg("ws") = 0, py::arg("ws_floats") = 0);
+  m.def("conv_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
+                         long ws_floats) {
+    launch_conv_dgrad(S(st), shape_from(shp), P<const bf16>(dy), P<const bf16>(w), P<bf16>(dx), P<float>(ws),
+                      ws ? ws_floats : 0);
     check("conv_dgrad");
+  }, py::arg("st"), py::arg("shape"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("ws") = 0,
+     py::arg("ws_floats") = 0);
+  m.def("conv_fd_ws_floats", [](const py::tuple& shp) { return conv_fd_ws_floats(shape_from(shp)); });
+  m.def("conv_pack_multi", [](uintptr_t st, const py::list& items) {
+    std::vector<PackItem> v;
+    for (const auto& it : items) {
+      const py::tuple t = it.cast<py::tuple>();
+      if (t.size() != 6) throw std::invalid_argument("conv_pack_multi item: (w, wr, O, Cw, C, RS)");
+      v.push_back(PackItem{P<const float>(t[0].cast<uintptr_t>()), P<bf16>(t[1].cast<uintptr_t>()), t[2].cast<int>(),
+                           t[3].cast<int>(), t[4].cast<int>(), t[5].cast<int>()});
+    }
+    if (!v.empty()) launch_conv_pack_multi(S(st), v.data(), (int)v.size());
+    check("conv_pack_multi");
   });
   m.def("conv_wgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws,
                          long ws_floats, int splits, int accumulate) {
@@ -148,7 +173,8 @@ void fedmi_bind_cnn(py::module_& m) {
                     P<bf16>(y), M, C, eps, mom, train, relu);
     check("bn_apply");
   });
-  m.def("bn_bwd", [](uintptr_t st, const py::dict& d, uintptr_t red, int M, int C) {
+  m.def("bn_bwd_ws_floats", [](int M, int C) { return bn_bwd_ws_floats(M, C); });
+  m.def("bn_bwd", [](uintptr_t st, const py::dict& d, uintptr_t red, int M, int C, uintptr_t ws, long ws_floats) {
     BNBwdDesc b{P<const bf16>(dget(d, "dya")),     P<const bf16>(dget(d, "dyb")),     P<const bf16>(dget(d, "y")),
                 P<const bf16>(dget(d, "za")),      P<const float>(dget(d, "meanA")),  P<const float>(dget(d, "invA")),
                 P<const float>(dget(d, "gammaA")), P<float>(dget(d, "dgammaA")),      P<float>(dget(d, "dbetaA")),
@@ -157,9 +183,10 @@ void fedmi_bind_cnn(py::module_& m) {
                 P<float>(dget(d, "dbetaB")),       P<bf16>(dget(d, "dzb")),           P<bf16>(dget(d, "gout")),
                 P<float>(dget(d, "shiftA")),       P<float>(dget(d, "shiftB"))};
     if (!b.dya || !b.za || !b.meanA || !b.invA || !b.gammaA || !b.dza) throw std::invalid_argument("bn_bwd: missing A");
-    launch_bn_bwd(S(st), b, P<float>(red), M, C);
+    launch_bn_bwd(S(st), b, P<float>(red), M, C, P<float>(ws), ws ? ws_floats : 0);
     check("bn_bwd");
-  });
+  }, py::arg("st"), py::arg("desc"), py::arg("red"), py::arg("M"), py::arg("C"), py::arg("ws") = 0,
+     py::arg("ws_floats") = 0);
   m.def("head", [](uintptr_t st, uintptr_t y, uintptr_t labels, int base, uintptr_t dbase, int N, int HW, int C, int J,
                    uintptr_t W, uintptr_t b, uintptr_t pooled, uintptr_t dlog, uintptr_t dy, uintptr_t stats,
                    uintptr_t dW, uintptr_t db, int train) {

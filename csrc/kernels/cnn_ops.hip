@@ -158,6 +158,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
 // ---------------------------------------------------------------------------
 // BN backward. g = (dya [+ dyb]) * (y > 0 if relu).  Per channel:
 //   red[0] = sum g,  red[1] = sum g * xhatA,  red[2] = sum g * xhatB
+constexpr int BN_REP = 16;   // atomic replicas of the two-level BN-backward channel sums
+
 struct BwdIn {
   const bf16* dya;
   const bf16* dyb;        // optional second incoming grad (residual fan-in)
@@ -186,8 +188,12 @@ FEDMI_DEV void load_g(const BwdIn& in, long i, float* g) {
   }
 }
 
+// red: [3][C] accumulated with atomics (partials == nullptr), or two-level: the
+// block sums are added into one of BN_REP replicas partials[rep][3][C]
+// (rep = block % BN_REP: 1/BN_REP of the same-address atomic contention) and
+// bn_bwd_finalize sums the replicas into red and re-zeroes them.
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BwdIn in, float* __restrict__ red, int M, int C,
-                                                            int rows_per_block) {
+                                                            int rows_per_block, float* __restrict__ partials) {
   __shared__ float part[3][256][8];
   const int VR = C >> 3;                 // host: blockDim.x % VR == 0
   const int cg = threadIdx.x % VR, rstep = blockDim.x / VR, r0 = threadIdx.x / VR;
@@ -232,8 +238,26 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BwdIn in, float* __r
     const int g = c >> 3, j = c & 7;
     float s = 0.f;
     for (int t = g; t < (int)blockDim.x; t += VR) s += part[qn][t][j];
-    unsafeAtomicAdd(red + qn * C + c, s);
+    unsafeAtomicAdd((partials ? partials + (long)(blockIdx.x % BN_REP) * 3 * C : red) + qn * C + c, s);
   }
+}
+
+// red[q][c] = sum_r partials[r][q][c]; the replicas are left zero for the next BN
+// (launches of a step are stream-serial, so one scratch serves every BN layer).
+__global__ __launch_bounds__(256) void bn_bwd_finalize(float* __restrict__ partials, int C, float* __restrict__ red) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 3 * C) return;
+  const long stride = 3l * C;
+  float v[BN_REP];
+#pragma unroll
+  for (int r = 0; r < BN_REP; ++r) v[r] = partials[r * stride + e];
+#pragma unroll
+  for (int r = 0; r < BN_REP; ++r) partials[r * stride + e] = 0.f;
+#pragma unroll
+  for (int w = BN_REP / 2; w >= 1; w >>= 1)
+#pragma unroll
+    for (int r = 0; r < w; ++r) v[r] += v[r + w];
+  red[e] = v[0];
 }
 
 struct BwdOut {
@@ -356,24 +380,62 @@ __global__ __launch_bounds__(256) void head_fwd_bwd_kernel(const bf16* __restric
   }
   __syncthreads();
   bf16* dyn = dy + (size_t)n * HW * C;
-  for (int e = tid; e < HW * C; e += 256) dyn[e] = (bf16)pl[e % C];
+  const int VR = C >> 3;   // C % 8 == 0: 16-B stores of 8 channels
+  for (int e = tid; e < HW * VR; e += 256) {
+    const int c0 = (e % VR) * 8;
+    bf16x8v v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (bf16)pl[c0 + j];
+    *reinterpret_cast<bf16x8v*>(dyn + (size_t)e * 8) = v;
+  }
 }
 
+constexpr int HEAD_MAXN = 512;
 // dW[j][c] = sum_n dlog[n][j] * pooled[n][c];  db[j] = sum_n dlog[n][j]
+// Block = 64 channels x 4 sample groups (fixed-order LDS combine: deterministic);
+// block 0 also reduces db.
 __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict__ pooled, const float* __restrict__ dlog,
                                                          int N, int C, int J, float* __restrict__ dW,
                                                          float* __restrict__ db) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < J * C) {
-    const int j = e / C, c = e - j * C;
+  __shared__ float part[4][16][64];
+  __shared__ float dls[HEAD_MAXN * 16];   // dlog staged once per block, read as LDS broadcasts
+  const int cl = threadIdx.x & 63, ng = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int nn = min(N, HEAD_MAXN);
+  for (int i = threadIdx.x; i < nn * J; i += 256) dls[(i / J) * 16 + i % J] = dlog[i];
+  __syncthreads();
+  float acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  for (int n = ng; n < N; n += 4) {
+    const float pv = c < C ? pooled[(size_t)n * C + c] : 0.f;
+    const float* dl = n < HEAD_MAXN ? dls + n * 16 : nullptr;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < J) acc[j] += (dl ? dl[j] : dlog[(size_t)n * J + j]) * pv;
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) part[ng][j][cl] = acc[j];
+  __syncthreads();
+  for (int e = threadIdx.x; e < J * 64; e += 256) {
+    const int j = e >> 6, cc = e & 63;
+    if (blockIdx.x * 64 + cc < C)
+      dW[(size_t)j * C + blockIdx.x * 64 + cc] = (part[0][j][cc] + part[1][j][cc]) + (part[2][j][cc] + part[3][j][cc]);
+  }
+  if (blockIdx.x == 0) {   // db: 16 classes x 16 sample groups from the staged dlog, then a fixed-order combine
+    __syncthreads();
+    const int j = threadIdx.x & 15, g = threadIdx.x >> 4;
     float s = 0.f;
-    for (int n = 0; n < N; ++n) s += dlog[(size_t)n * J + j] * pooled[(size_t)n * C + c];
-    dW[e] = s;
-  } else if (e < J * C + J) {
-    const int j = e - J * C;
-    float s = 0.f;
-    for (int n = 0; n < N; ++n) s += dlog[(size_t)n * J + j];
-    db[j] = s;
+    if (j < J)
+      for (int n = g; n < N; n += 16) s += n < HEAD_MAXN ? dls[n * 16 + j] : dlog[(size_t)n * J + j];
+    float* red = &part[0][0][0];   // reuse: [16 groups][16 classes]
+    red[g * 16 + j] = s;
+    __syncthreads();
+    if (threadIdx.x < J) {
+      float t = 0.f;
+      for (int q = 0; q < 16; ++q) t += red[q * 16 + threadIdx.x];
+      db[threadIdx.x] = t;
+    }
   }
 }
 
@@ -428,18 +490,36 @@ struct BNBwdDesc {
   float* shiftA; float* shiftB;
 };
 
-// red: [3][C] fp32 accumulator, must be zero on entry (callers zero all BN
-// accumulators of a step with one fill, keeping memset nodes out of graphs)
-void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, float* red, int M, int C) {
+static void bn_bwd_grid(int M, int C, int* tb, int* rows_per_block, int* nblk) {
+  const int VR = C / 8;
+  *tb = (256 / VR) * VR;   // block size a multiple of C/8: fixed channel group per thread
+  const int rstep = *tb / VR;
+  // <= 1024 row-blocks (~4 per CU), each >= 2 row passes of the block
+  *rows_per_block = std::max(2 * rstep, (M + 1023) / 1024);
+  *nblk = (M + *rows_per_block - 1) / *rows_per_block;
+}
+
+// Scratch (floats) the two-level reduction of launch_bn_bwd needs (ZERO-initialised once
+// by the caller; every launch leaves it zero again).
+long bn_bwd_ws_floats(int M, int C) {
+  (void)M;
+  return (long)BN_REP * 3 * C;
+}
+
+// red: [3][C] fp32.  With ``ws`` (>= bn_bwd_ws_floats, zero): replica atomics + a
+// finalize launch (red needs no zeroing).  Without: atomics into red, which must
+// be zero on entry.
+void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, float* red, int M, int C, float* ws, long ws_floats) {
   const int VR = C / 8;
   if (C % 8 || VR > 256) throw std::invalid_argument("bn_bwd: need C % 8 == 0 and C <= 2048");
-  const int tb = (256 / VR) * VR;   // block size a multiple of C/8: fixed channel group per thread
   BwdIn in{d.dya, d.dyb, d.y, d.za, d.meanA, d.invA, d.zb, d.meanB, d.invB};
   BwdOut out{d.dza, d.dzb, d.gout, d.dgammaA, d.dbetaA, d.dgammaB, d.dbetaB, d.gammaA, d.gammaB, d.shiftA, d.shiftB};
-  // ~2 row-blocks per CU worth of work, >= 64 rows each
-  const int rows_per_block = std::max(64, (M + 511) / 512);
-  const int nblk = (M + rows_per_block - 1) / rows_per_block;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(tb), 0, st, in, red, M, C, rows_per_block);
+  int tb, rows_per_block, nblk;
+  bn_bwd_grid(M, C, &tb, &rows_per_block, &nblk);
+  const bool two = ws && ws_floats >= (long)BN_REP * 3 * C;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(tb), 0, st, in, red, M, C, rows_per_block,
+                     two ? ws : nullptr);
+  if (two) hipLaunchKernelGGL(bn_bwd_finalize, dim3((3 * C + 255) / 256), dim3(256), 0, st, ws, C, red);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for((long)M * VR)), dim3(256), 6 * C * sizeof(float), st, in, out,
                      red, M, C);
 }
@@ -448,11 +528,11 @@ void launch_head(hipStream_t st, const bf16* y, const int* labels, int base, con
                  const float* W, const float* b, float* pooled, float* dlog, bf16* dy, float* stats, float* dW,
                  float* db, int train) {
   if (J > 16) throw std::invalid_argument("head: at most 16 classes");
+  if (C % 8) throw std::invalid_argument("head: C % 8 != 0");
   hipLaunchKernelGGL(head_fwd_bwd_kernel, dim3(N), dim3(256), (C + 32) * sizeof(float), st, y, labels, base, dbase, HW, C,
                      J, W, b, pooled, dlog, dy, stats, N, train);
   if (train)
-    hipLaunchKernelGGL(head_wgrad_kernel, dim3((J * C + J + 255) / 256), dim3(256), 0, st, pooled, dlog, N, C, J, dW,
-                       db);
+    hipLaunchKernelGGL(head_wgrad_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pooled, dlog, N, C, J, dW, db);
 }
 
 }  // namespace fedmi

@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, co
                                                   const bf16* __restrict__ dy, bf16* __restrict__ out,
                                                   float* __restrict__ gout, float* __restrict__ stats,
                                                   const float* __restrict__ shift, ConvGeom g,
-                                                  int ksteps_per_split) {
+                                                  int ksteps_per_split, int partial) {
   constexpr int A_IMG = (MODE == WGRAD) ? BK * BM : BM * KC_LD;
   constexpr int B_IMG = (MODE == FWD) ? BN * KC_LD : BK * BN;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, co
   const int ksteps = (g.K + BK - 1) / BK;
   const int kb = blockIdx.z * ksteps_per_split;
   const int ke = min(ksteps, kb + ksteps_per_split);
-  if (MODE == WGRAD && kb >= ke) return;   // (never launched: every split owns >= 1 step)
+  if ((MODE == WGRAD || partial) && kb >= ke) return;   // (never launched: every split owns >= 1 step)
 
   Loader<MODE, BM, BN> L;
   L.init(g, m0, n0, tid);
@@ -312,10 +312,11 @@ __global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, co
 
   // ---- epilogue
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
-  if constexpr (MODE == WGRAD) {
-    // fp32 partial of this K split -> workspace [split][O][R*S*C] (natural GEMM
-    // layout, plain stores); conv_wgrad_reduce sums the splits and permutes
-    // into the PyTorch [O][Cw][R][S] gradient.
+  if (MODE == WGRAD || partial) {
+    // fp32 partial of this K split -> workspace [split][M][NC] (natural GEMM
+    // layout, plain stores).  WGRAD: conv_wgrad_reduce sums the splits and
+    // permutes into the PyTorch [O][Cw][R][S] gradient; split-K FWD / DGRAD:
+    // conv_splitk_reduce sums, rounds to bf16 (+ BN statistics for FWD).
     float* ws = gout + (long)blockIdx.z * g.M * g.NC;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -383,30 +384,138 @@ __global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, co
 }
 
 // dW[o][c][r][s] (+)= sum_z ws[z][o][(r*S + s)*C + c]     (c < Cw)
+// Block = 64 consecutive workspace columns x 4 split groups: every wave reads
+// 256 contiguous bytes per split (the workspace is read exactly once, fully
+// coalesced), the 4 groups are combined in LDS, and the 64 sums are written to
+// their permuted [O][Cw][R][S] positions.  Deterministic (fixed order).
 __global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict__ ws, int splits, int O, int C, int Cw,
                                                          int RS, float* __restrict__ dw, int accumulate) {
-  const long total = (long)O * Cw * RS;
+  __shared__ float part[4][64];
   const long plane = (long)O * RS * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int rs = i % RS;
-    const long t = i / RS;
-    const int c = t % Cw, o = t / Cw;
-    const long src = ((long)o * RS + rs) * C + c;
-    float v = accumulate ? dw[i] : 0.f;
-    for (int z = 0; z < splits; ++z) v += ws[z * plane + src];
-    dw[i] = v;
+  const long e = (long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int zg = threadIdx.x >> 6;
+  float v = 0.f;
+  if (e < plane) {
+    const float* p = ws + e;
+    int z = zg;
+    for (; z + 12 < splits; z += 16) {   // 4 independent loads in flight per lane
+      const float a = p[(long)z * plane], b = p[(long)(z + 4) * plane];
+      const float c = p[(long)(z + 8) * plane], d = p[(long)(z + 12) * plane];
+      v += (a + b) + (c + d);
+    }
+    for (; z < splits; z += 4) v += p[(long)z * plane];
+  }
+  part[zg][threadIdx.x & 63] = v;
+  __syncthreads();
+  if (threadIdx.x < 64 && e < plane) {
+    const float s = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+    const int c = (int)(e % C);
+    if (c < Cw) {
+      const long t = e / C;
+      const int rs = (int)(t % RS), o = (int)(t / RS);
+      const long i = ((long)o * Cw + c) * RS + rs;
+      dw[i] = accumulate ? dw[i] + s : s;
+    }
   }
 }
 
-// W fp32 [O][Cw][R][S] -> W_rsc bf16 [O][R][S][C]   (C = Cw padded to 8; pad = 0)
-__global__ __launch_bounds__(256) void conv_pack_kernel(const float* __restrict__ w, bf16* __restrict__ wr, int O, int Cw,
-                                                        int C, int RS) {
-  const long total = (long)O * RS * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = i % C;
-    const long t = i / C;
-    const int rs = t % RS, o = t / RS;
-    wr[i] = c < Cw ? (bf16)w[((long)o * Cw + c) * RS + rs] : (bf16)0.f;
+// Split-K FWD / DGRAD combine: out[row][c] = bf16(sum_z ws[z][m][c]); FWD also
+// accumulates the BatchNorm batch statistics (sum / sum of squares of
+// bf16(y) - shift[c]) like the single-pass epilogue.  Each thread owns one
+// 8-channel group (two 16-B loads per split) of rows r0, r0 + rstep, ...
+__global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restrict__ ws, int splits, ConvGeom g,
+                                                          bf16* __restrict__ out, float* __restrict__ stats,
+                                                          const float* __restrict__ shift, int remap,
+                                                          int rows_per_block) {
+  __shared__ float red[2][256][8];
+  const int VR = g.NC >> 3;                 // host: blockDim.x % VR == 0
+  const int cg = threadIdx.x % VR, rstep = blockDim.x / VR, r0 = threadIdx.x / VR;
+  const int c0 = cg * 8;
+  const long plane = (long)g.M * g.NC;
+  float sh[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[j] = (stats && shift) ? shift[c0 + j] : 0.f;
+    s1[j] = s2[j] = 0.f;
+  }
+  const int rb = blockIdx.x * rows_per_block, re = min(g.M, rb + rows_per_block);
+  for (int m = rb + r0; m < re; m += rstep) {
+    const float* p = ws + (long)m * g.NC + c0;
+    float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    for (int z = 1; z < splits; ++z) {
+      const float4 ua = *reinterpret_cast<const float4*>(p + z * plane);
+      const float4 ub = *reinterpret_cast<const float4*>(p + z * plane + 4);
+      a.x += ua.x; a.y += ua.y; a.z += ua.z; a.w += ua.w;
+      b.x += ub.x; b.y += ub.y; b.z += ub.z; b.w += ub.w;
+    }
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+    long orow = m;
+    if (remap) {   // DGRAD stride-2 phase row -> input pixel row
+      const uint32_t n = fdiv(m, g.dHWp), hw = m - n * g.Hp * g.Wp;
+      const uint32_t hh = fdiv(hw, g.dWp), ww = hw - hh * g.Wp;
+      orow = ((long)n * g.H + hh * g.st + g.ph) * g.W + ww * g.st + g.pw;
+    }
+    *reinterpret_cast<bf16x8*>(out + orow * g.NC + c0) = o;
+    if (stats) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (float)o[j] - sh[j];
+        s1[j] += d;
+        s2[j] += d * d;
+      }
+    }
+  }
+  if (!stats) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][threadIdx.x][j] = s1[j];
+    red[1][threadIdx.x][j] = s2[j];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 2 * g.NC; e += blockDim.x) {
+    const int q = e / g.NC, c = e - q * g.NC;
+    const int grp = c >> 3, j = c & 7;
+    float t = 0.f;
+    for (int th = grp; th < (int)blockDim.x; th += VR) t += red[q][th][j];
+    unsafeAtomicAdd(stats + q * g.NC + c, t);
+  }
+}
+
+// Multi-tensor weight pack: every dense conv of a network in one launch.
+// One workgroup per output-channel row: the fp32 [Cw][R*S] row is read
+// coalesced into LDS, then written as the bf16 [R*S][C] row (zero channel pad),
+// also coalesced (a direct element map reads with an R*S stride).
+struct PackEntry {
+  const float* w;
+  bf16* wr;
+  int O, Cw, C, RS;
+  int row0;          // first workgroup (row) of this entry in the launch
+};
+constexpr int MAX_PACK = 24;
+constexpr int PACK_ROW_MAX = 8192;   // Cw * R * S floats staged per row (32 KiB)
+struct PackTable {
+  PackEntry e[MAX_PACK];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void conv_pack_multi_kernel(PackTable t) {
+  __shared__ float row[PACK_ROW_MAX];
+  int k = 0;
+  while (k + 1 < t.n && (int)blockIdx.x >= t.e[k + 1].row0) ++k;
+  const PackEntry& p = t.e[k];
+  const int o = blockIdx.x - p.row0;
+  const int n_in = p.Cw * p.RS;
+  const float* src = p.w + (long)o * n_in;
+  for (int i = threadIdx.x; i < n_in; i += 256) row[i] = src[i];
+  __syncthreads();
+  bf16* dst = p.wr + (long)o * p.RS * p.C;
+  const int n_out = p.RS * p.C;
+  for (int i = threadIdx.x; i < n_out; i += 256) {
+    const int rs = i / p.C, c = i - rs * p.C;
+    dst[i] = c < p.Cw ? (bf16)row[c * p.RS + rs] : (bf16)0.f;
   }
 }
 
@@ -472,25 +581,65 @@ static TileCfg pick_tiles(int M, int NC) {
 
 template <int MODE, int BM, int BN>
 static void launch_tiled(hipStream_t st, dim3 grid, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy,
-                         bf16* out, float* gout, float* stats, const float* shift, int kps) {
-  hipLaunchKernelGGL((conv_igemm<MODE, BM, BN>), grid, dim3(256), 0, st, x, w, dy, out, gout, stats, shift, g, kps);
+                         bf16* out, float* gout, float* stats, const float* shift, int kps, int partial) {
+  hipLaunchKernelGGL((conv_igemm<MODE, BM, BN>), grid, dim3(256), 0, st, x, w, dy, out, gout, stats, shift, g, kps,
+                     partial);
+}
+
+// FWD / DGRAD split-K: GEMMs with fewer output tiles than CUs and a long K loop
+// (ResNet layer3/4 at batch 128: 128-256 tiles, 36-72 K steps) leave most of
+// the chip idle behind a serial K chain.  Split K so that ~3 workgroups per CU
+// run >= 8 K steps each, partials into ``ws``; 1 = no split.
+static int fd_splits(const ConvGeom& g, long ws_floats) {
+  if (ws_floats <= 0) return 1;
+  const TileCfg t = pick_tiles(g.M, g.NC);
+  const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
+  const int ksteps = (g.K + BK - 1) / BK;
+  if (tiles >= 2l * num_cus() || ksteps < 16) return 1;
+  long sp = std::min<long>((3l * num_cus() + tiles - 1) / tiles, ksteps / 8);
+  sp = std::min<long>(sp, ws_floats / ((long)g.M * g.NC));
+  if (sp < 2) return 1;
+  const int kps = (int)((ksteps + sp - 1) / sp);
+  return (ksteps + kps - 1) / kps;
 }
 
 template <int MODE>
 static void launch_mode(hipStream_t st, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy, bf16* out,
-                        float* gout, float* stats, int splits, const float* shift = nullptr) {
+                        float* gout, float* stats, int splits, const float* shift = nullptr, int partial = 0) {
   const TileCfg t = pick_tiles(g.M, g.NC);
   const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
   const int ksteps = (g.K + BK - 1) / BK;
-  if (MODE != WGRAD) splits = 1;
+  if (MODE != WGRAD && !partial) splits = 1;
   splits = std::max(1, std::min(splits, ksteps));
   const int kps = std::max(1, (ksteps + splits - 1) / splits);
   splits = std::max(1, (ksteps + kps - 1) / kps);
   dim3 grid((unsigned)tiles, 1, (unsigned)splits);
-  if (t.BM == 128 && t.BN == 128) launch_tiled<MODE, 128, 128>(st, grid, g, x, w, dy, out, gout, stats, shift, kps);
-  else if (t.BM == 128) launch_tiled<MODE, 128, 64>(st, grid, g, x, w, dy, out, gout, stats, shift, kps);
-  else if (t.BN == 128) launch_tiled<MODE, 64, 128>(st, grid, g, x, w, dy, out, gout, stats, shift, kps);
-  else launch_tiled<MODE, 64, 64>(st, grid, g, x, w, dy, out, gout, stats, shift, kps);
+  if (t.BM == 128 && t.BN == 128) launch_tiled<MODE, 128, 128>(st, grid, g, x, w, dy, out, gout, stats, shift, kps, partial);
+  else if (t.BM == 128) launch_tiled<MODE, 128, 64>(st, grid, g, x, w, dy, out, gout, stats, shift, kps, partial);
+  else if (t.BN == 128) launch_tiled<MODE, 64, 128>(st, grid, g, x, w, dy, out, gout, stats, shift, kps, partial);
+  else launch_tiled<MODE, 64, 64>(st, grid, g, x, w, dy, out, gout, stats, shift, kps, partial);
+}
+
+// FWD / DGRAD with automatic split-K through ``ws`` (null / 0 floats: never split).
+template <int MODE>
+static void launch_fd(hipStream_t st, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy, bf16* out,
+                      float* stats, const float* shift, float* ws, long ws_floats) {
+  const int sp = fd_splits(g, ws_floats);
+  if (sp <= 1) {
+    launch_mode<MODE>(st, g, x, w, dy, out, nullptr, stats, 1, shift, 0);
+    return;
+  }
+  launch_mode<MODE>(st, g, x, w, dy, nullptr, ws, nullptr, sp, nullptr, 1);
+  const int VR = g.NC / 8;
+  const int tb = (256 / VR) * VR;
+  const int rstep = tb / VR;
+  // plain combine: ~4 blocks per CU; with BN statistics fewer blocks (their
+  // per-channel atomics contend on 2 x NC addresses)
+  const int rows_per_block = stats ? std::max(2 * rstep, (g.M + 255) / 256) : std::max(rstep, (g.M + 1023) / 1024);
+  const int nblk = (g.M + rows_per_block - 1) / rows_per_block;
+  const int remap = (MODE == DGRAD && g.st != 1) ? 1 : 0;
+  hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, sp, g, out, stats, shift, remap,
+                     rows_per_block);
 }
 
 // K-split count for the weight gradient: about two workgroups per CU, at least
@@ -509,22 +658,23 @@ static int wgrad_splits(const ConvGeom& g, long ws_cap_floats) {
 
 // Y[N,P,Q,O] = conv(X[N,H,W,C], W_rsc); stats (optional) += [sum | sumsq] of (Y - shift) per output channel.
 void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf16* wrsc, bf16* y, float* stats,
-                     const float* shift) {
+                     const float* shift, float* ws, long ws_floats) {
   check_shape(s);
   ConvGeom g = make_geom(s);
   g.M = s.N * s.P * s.Q; g.NC = s.O; g.K = s.R * s.S * s.C;
-  launch_mode<FWD>(st, g, x, wrsc, nullptr, y, nullptr, stats, 1, shift);
+  launch_fd<FWD>(st, g, x, wrsc, nullptr, y, stats, shift, ws, ws_floats);
 }
 
 // dX[N,H,W,C] = conv_transpose(dY[N,P,Q,O], W_rsc)   (every element written).
 // Stride 2 runs as 4 sub-pixel phases so no MFMA multiplies a structural zero.
-void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const bf16* wrsc, bf16* dx) {
+void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const bf16* wrsc, bf16* dx, float* ws,
+                       long ws_floats) {
   check_shape(s);
   ConvGeom g = make_geom(s);
   g.NC = s.C;
   if (s.st == 1) {
     g.M = s.N * s.H * s.W; g.K = s.R * s.S * s.O;
-    launch_mode<DGRAD>(st, g, nullptr, wrsc, dy, dx, nullptr, nullptr, 1);
+    launch_fd<DGRAD>(st, g, nullptr, wrsc, dy, dx, nullptr, nullptr, ws, ws_floats);
     return;
   }
   for (int ph = 0; ph < 2; ++ph)
@@ -537,7 +687,11 @@ void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const
       if (q.Hp <= 0 || q.Wp <= 0) continue;
       q.dNS = make_div(std::max(q.ns, 1)); q.dWp = make_div(q.Wp); q.dHWp = make_div(q.Hp * q.Wp);
       q.M = s.N * q.Hp * q.Wp; q.K = q.nr * q.ns * s.O;
-      launch_mode<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, 1);
+      if (q.K == 0) {   // phase with no taps (1x1 stride 2, odd parity): the kernel writes zeros
+        launch_mode<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, 1);
+        continue;
+      }
+      launch_fd<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, ws, ws_floats);
     }
 }
 
@@ -546,6 +700,41 @@ static ConvGeom wgrad_geom(const ConvShape& s) {
   ConvGeom g = make_geom(s);
   g.M = s.O; g.NC = s.R * s.S * s.C; g.K = s.N * s.P * s.Q;
   return g;
+}
+
+// Workspace (floats) split-K FWD + DGRAD want for this shape (0: they never split).
+long conv_fd_ws_floats(const ConvShape& s) {
+  check_shape(s);
+  ConvGeom g = make_geom(s);
+  g.M = s.N * s.P * s.Q; g.NC = s.O; g.K = s.R * s.S * s.C;
+  long need = 0;
+  const long cap = 1l << 40;
+  int sp = fd_splits(g, cap);
+  if (sp > 1) need = std::max(need, (long)sp * g.M * g.NC);
+  ConvGeom d = make_geom(s);
+  d.NC = s.C;
+  if (s.st == 1) {
+    d.M = s.N * s.H * s.W; d.K = s.R * s.S * s.O;
+    sp = fd_splits(d, cap);
+    if (sp > 1) need = std::max(need, (long)sp * d.M * d.NC);
+  } else {
+    for (int ph = 0; ph < 2; ++ph) {
+      const int r0 = (ph + s.pad) & 1;
+      const int nr = std::max(0, (s.R - r0 + 1) / 2);
+      const int Hp = (s.H - ph + 1) / 2;
+      for (int pw = 0; pw < 2; ++pw) {
+        const int s0 = (pw + s.pad) & 1;
+        const int ns = std::max(0, (s.S - s0 + 1) / 2);
+        const int Wp = (s.W - pw + 1) / 2;
+        if (Hp <= 0 || Wp <= 0 || nr * ns == 0) continue;
+        ConvGeom q = d;
+        q.M = s.N * Hp * Wp; q.K = nr * ns * s.O;
+        sp = fd_splits(q, cap);
+        if (sp > 1) need = std::max(need, (long)sp * q.M * q.NC);
+      }
+    }
+  }
+  return need;
 }
 
 // Workspace (floats) launch_conv_wgrad needs for this shape with automatic splits.
@@ -568,16 +757,37 @@ void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const 
   splits = (ksteps + kps - 1) / kps;
   if ((long)splits * plane > ws_floats) throw std::invalid_argument("conv_wgrad: workspace too small for splits");
   launch_mode<WGRAD>(st, g, x, nullptr, dy, nullptr, ws, nullptr, splits);
-  const long total = (long)s.O * s.Cw * s.R * s.S;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(conv_wgrad_reduce, dim3(blocks), dim3(256), 0, st, ws, splits, s.O, s.C, s.Cw, s.R * s.S, dw,
-                     accumulate);
+  const long blocks = (plane + 63) / 64;
+  hipLaunchKernelGGL(conv_wgrad_reduce, dim3((unsigned)blocks), dim3(256), 0, st, ws, splits, s.O, s.C, s.Cw,
+                     s.R * s.S, dw, accumulate);
+}
+
+struct PackItem {
+  const float* w;
+  bf16* wr;
+  int O, Cw, C, RS;
+};
+
+// All dense-conv weight images of a network from their fp32 masters, <= MAX_PACK per launch.
+void launch_conv_pack_multi(hipStream_t st, const PackItem* items, int n) {
+  for (int b = 0; b < n; b += MAX_PACK) {
+    PackTable t{};
+    t.n = std::min(MAX_PACK, n - b);
+    int rows = 0;
+    for (int k = 0; k < t.n; ++k) {
+      const PackItem& it = items[b + k];
+      if (it.C % 8 || it.C < it.Cw) throw std::invalid_argument("conv_pack_multi: bad channel padding");
+      if ((long)it.Cw * it.RS > PACK_ROW_MAX) throw std::invalid_argument("conv_pack_multi: row too long");
+      t.e[k] = PackEntry{it.w, it.wr, it.O, it.Cw, it.C, it.RS, rows};
+      rows += it.O;
+    }
+    hipLaunchKernelGGL(conv_pack_multi_kernel, dim3(rows), dim3(256), 0, st, t);
+  }
 }
 
 void launch_conv_pack(hipStream_t st, const float* w, bf16* wrsc, int O, int Cw, int C, int RS) {
-  const long total = (long)O * RS * C;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(conv_pack_kernel, dim3(blocks), dim3(256), 0, st, w, wrsc, O, Cw, C, RS);
+  const PackItem it{w, wrsc, O, Cw, C, RS};
+  launch_conv_pack_multi(st, &it, 1);
 }
 
 }  // namespace fedmi

@@ -93,17 +93,18 @@ class _Unit:
     def ws_floats(self, nb: int) -> int:
         if self.depthwise:
             return conv.dwconv_ws_floats(self.in_shape(nb), self.R, self.stride, self.pad)
-        return conv.wgrad_ws_floats(self.in_shape(nb), self.O, self.R, self.S, self.stride, self.pad, self.Cw)
+        shp = (self.in_shape(nb), self.O, self.R, self.S, self.stride, self.pad, self.Cw)
+        return max(conv.wgrad_ws_floats(*shp), conv.fd_ws_floats(*shp))
 
-    # ---- launches
-    def fwd(self, x: torch.Tensor, nb: int, stats) -> None:
+    # ---- launches (``ws``: the engine's shared split-K workspace; launches are stream-serial)
+    def fwd(self, x: torch.Tensor, nb: int, stats, ws: Optional[torch.Tensor] = None) -> None:
         sh = self.shift if stats is not None else None
         if self.depthwise:
             conv.dwconv_fwd(x, self.conv.weight, self.stride, self.pad, stats=stats, out=self.view(self.z, nb),
                             shift=sh)
         else:
             conv.conv2d_fwd(x, self.wr, self.stride, self.pad, Cw=self.Cw, stats=stats, out=self.view(self.z, nb),
-                            shift=sh)
+                            shift=sh, ws=ws)
 
     def wgrad(self, x: torch.Tensor, nb: int, ws: torch.Tensor) -> None:
         dz = self.view(self.dz, nb)
@@ -113,15 +114,14 @@ class _Unit:
             conv.conv2d_wgrad(x, dz, self.R, self.S, self.stride, self.pad, Cw=self.Cw, out=self.conv.weight.grad,
                               ws=ws)
 
-    def dgrad(self, nb: int, out: torch.Tensor) -> torch.Tensor:
+    def dgrad(self, nb: int, out: torch.Tensor, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
         dz = self.view(self.dz, nb)
         if self.depthwise:
             return conv.dwconv_dgrad(dz, self.conv.weight, self.in_shape(nb), self.stride, self.pad, out=out)
-        return conv.conv2d_dgrad(dz, self.wr, self.in_shape(nb), self.stride, self.pad, Cw=self.Cw, out=out)
+        return conv.conv2d_dgrad(dz, self.wr, self.in_shape(nb), self.stride, self.pad, Cw=self.Cw, out=out, ws=ws)
 
-    def pack(self) -> None:
-        if not self.depthwise:
-            conv.pack_weight(self.conv.weight.data, self.C, out=self.wr)
+    def pack_item(self):
+        return None if self.depthwise else (self.conv.weight.data, self.wr)
 
 
 class _Block:
@@ -260,7 +260,11 @@ class CNNNativeTrainer(LocalTrainer):
             so += 2 * u.O
             ro += 3 * u.O
         B = cfg.batch_size
-        self.wgrad_ws = torch.empty(max(u.ws_floats(B) for u in self.units), device=device)
+        # one fp32 split-K workspace for every conv launch of a step (fwd / dgrad / wgrad)
+        self.wgrad_ws = torch.empty(max(max(u.ws_floats(nb) for u in self.units) for nb in {B, self.eval_bs}),
+                                    device=device)
+        # BN-backward two-level channel sums (replicated atomics + finalize; kept zero between uses)
+        self.bn_ws = torch.zeros(max(cnn.bn_bwd_ws_floats(B * u.P * u.P, u.O) for u in self.units), device=device)
         self.xin = torch.empty(R, 32, 32, 8, dtype=act_dtype, device=device)
         self.dhead = torch.empty(R * self.head_hw * self.head_hw * self.head_c, dtype=act_dtype, device=device)
         self.pooled = torch.empty(R, self.head_c, device=device)
@@ -309,8 +313,7 @@ class CNNNativeTrainer(LocalTrainer):
         self._graphs.clear()
 
     def pack(self) -> None:
-        for u in self.units:
-            u.pack()
+        conv.pack_weights([it for it in (u.pack_item() for u in self.units) if it is not None])
 
     # ---- data ----------------------------------------------------------------------------
     def set_schedule(self, starts, sizes) -> None:
@@ -340,16 +343,17 @@ class CNNNativeTrainer(LocalTrainer):
         a = x
         for b in self.blocks:
             h = a
+            ws = self.wgrad_ws
             for v in b.main[:-1]:
-                v.fwd(h, nb, v.stats if train else None)
+                v.fwd(h, nb, v.stats if train else None, ws)
                 h = self._bn(v, v.view(v.z, nb), v.view(v.y, nb), train, v.relu)
             last = b.main[-1]
-            last.fwd(h, nb, last.stats if train else None)
+            last.fwd(h, nb, last.stats if train else None, ws)
             out = b.out_view(nb)
             z = last.view(last.z, nb)
             if b.shortcut == "proj":
                 p = b.proj
-                p.fwd(a, nb, p.stats if train else None)
+                p.fwd(a, nb, p.stats if train else None, ws)
                 self._bn(last, z, out, train, b.out_relu, z2=p.view(p.z, nb), b=p.bn_args(p.stats))
             elif b.shortcut == "identity":
                 self._bn(last, z, out, train, b.out_relu, res=a)
@@ -363,14 +367,14 @@ class CNNNativeTrainer(LocalTrainer):
                  dbase=dbase)
         return x, hd
 
-    @staticmethod
-    def _bn_bwd(u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None) -> None:
+    def _bn_bwd(self, u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None) -> None:
+        bn_ws = self.bn_ws if self.bn_ws.numel() else None
         kw = {}
         if zb is not None:
             kw = dict(zb=zb.view(zb.z, nb), b=zb.bn_args(None), dgamma_b=zb.bn.weight.grad,
                       dbeta_b=zb.bn.bias.grad, dzb=zb.view(zb.dz, nb))
         cnn.bn_bwd(dya, u.view(u.z, nb), u.bn_args(None), u.bn.weight.grad, u.bn.bias.grad, u.view(u.dz, nb), u.red,
-                   dyb=dyb, y=y, gout=gout, **kw)
+                   dyb=dyb, y=y, gout=gout, ws=bn_ws, **kw)
 
     def _backward(self, nb: int, x: torch.Tensor, dhead: torch.Tensor) -> None:
         dya, dyb = dhead, None
@@ -388,13 +392,13 @@ class CNNNativeTrainer(LocalTrainer):
                 v.wgrad(xin, nb, ws)
                 if j > 0:
                     w = b.main[j - 1]
-                    v.dgrad(nb, w.view(w.dy, nb))
+                    v.dgrad(nb, w.view(w.dy, nb), ws)
                     self._bn_bwd(w, nb, w.view(w.dy, nb), None, w.view(w.y, nb) if w.relu else None)
                 elif not b.first:
-                    v.dgrad(nb, b.in_view(b.din_a, nb))
+                    v.dgrad(nb, b.in_view(b.din_a, nb), ws)
             if b.proj is not None:
                 b.proj.wgrad(a_in, nb, ws)
-                b.proj.dgrad(nb, din_b)
+                b.proj.dgrad(nb, din_b, ws)
             if not b.first:
                 dya = b.in_view(b.din_a, nb)
                 dyb = din_b
@@ -408,7 +412,8 @@ class CNNNativeTrainer(LocalTrainer):
     def _forward_backward(self, nb: int) -> None:
         # every gradient entry is overwritten (wgrad reduce, BN dgamma/dbeta, head): no grad zeroing
         self.stats_all.zero_()
-        self.red_all.zero_()
+        if not self.bn_ws.numel():     # atomic BN-backward sums (emulation) need zeroed accumulators
+            self.red_all.zero_()
         x, dh = self._forward(nb, True, self.train_set.x, self.train_set.y, self.cur, 0)
         self._backward(nb, x, dh)
 

@@ -76,10 +76,13 @@ def bn_apply(z: torch.Tensor, a: BNParams, y: torch.Tensor, train: bool, relu: b
 def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Tensor, dbeta_a: torch.Tensor,
            dza: torch.Tensor, red: torch.Tensor, dyb: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None,
            zb: Optional[torch.Tensor] = None, b: Optional[BNParams] = None, dgamma_b=None, dbeta_b=None, dzb=None,
-           gout: Optional[torch.Tensor] = None) -> None:
+           gout: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> None:
     """BatchNorm backward through an optional ReLU mask (``y``: forward output) for one or two BN
     branches sharing the incoming grad g = dya (+ dyb).  Writes dz for each branch, dgamma/dbeta,
-    and optionally g itself (``gout``, the identity-shortcut grad).  ``red``: [3, C] fp32, ZERO on entry."""
+    and optionally g itself (``gout``, the identity-shortcut grad).  ``red``: [3, C] fp32 channel
+    sums.  With ``ws`` (>= :func:`bn_bwd_ws_floats` fp32, ZERO before first use; every call leaves it
+    zero) the sums go through replicated atomics + a finalize and ``red`` needs no init; without,
+    they are atomics straight into ``red``, which must be ZERO."""
     C = za.shape[-1]
     M = za.numel() // C
     if red.numel() < 3 * C:
@@ -89,7 +92,12 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
     if zb is not None:
         d.update(zb=_p(zb), meanB=_p(b.smean), invB=_p(b.sinv), gammaB=_p(b.gamma), dgammaB=_p(dgamma_b),
                  dbetaB=_p(dbeta_b), dzb=_p(dzb), shiftB=_p(b.shift))
-    native.require().bn_bwd(native.stream_handle(red.device), d, red.data_ptr(), M, C)
+    native.require().bn_bwd(native.stream_handle(red.device), d, red.data_ptr(), M, C,
+                            ws.data_ptr() if ws is not None else 0, ws.numel() if ws is not None else 0)
+
+
+def bn_bwd_ws_floats(M: int, C: int) -> int:
+    return int(native.require().bn_bwd_ws_floats(int(M), int(C)))
 
 
 def head(y: torch.Tensor, labels: torch.Tensor, base: int, W: torch.Tensor, b: torch.Tensor, stats: torch.Tensor,

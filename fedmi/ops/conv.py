@@ -54,11 +54,37 @@ def pack_weight(w: torch.Tensor, c_pad: Optional[int] = None, out: Optional[torc
     return out
 
 
+def pack_weights(items) -> None:
+    """Pack many ``(w fp32 [O,Cw,R,S], out bf16 [O,R,S,C])`` pairs in one multi-tensor launch."""
+    items = list(items)
+    if not items:
+        return
+    for w, out in items:
+        _check(w, torch.float32, "pack_weights.w")
+        _check(out, torch.bfloat16, "pack_weights.out")
+        if out.shape[0] != w.shape[0] or tuple(out.shape[1:3]) != tuple(w.shape[2:]) or out.shape[3] < w.shape[1]:
+            raise ValueError(f"pack_weights: image {tuple(out.shape)} vs master {tuple(w.shape)}")
+    dev = items[0][0].device
+    native.require().conv_pack_multi(
+        native.stream_handle(dev),
+        [(w.data_ptr(), o.data_ptr(), w.shape[0], w.shape[1], o.shape[3], w.shape[2] * w.shape[3]) for w, o in items])
+
+
+def fd_ws_floats(x_shape, O: int, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None) -> int:
+    """Split-K workspace (fp32 elements) the forward + data-gradient launches of this conv can use."""
+    return int(native.require().conv_fd_ws_floats(shape_tuple(x_shape, O, R, S, stride, pad, Cw)))
+
+
+def _ws_args(ws: Optional[torch.Tensor]):
+    return (ws.data_ptr(), ws.numel()) if ws is not None else (0, 0)
+
+
 def conv2d_fwd(x: torch.Tensor, wrsc: torch.Tensor, stride: int, pad: int, Cw: Optional[int] = None,
                stats: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-               shift: Optional[torch.Tensor] = None) -> torch.Tensor:
+               shift: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y[N,P,Q,O] = conv(x[N,H,W,C]); ``stats`` ([2, O] fp32) += per-channel sum / sum of squares of
-    (y - shift) (``shift``: [O] fp32 or None = 0)."""
+    (y - shift) (``shift``: [O] fp32 or None = 0).  ``ws`` (fp32): optional split-K workspace for
+    deep-K / few-tile shapes (see :func:`fd_ws_floats`)."""
     _check(x, torch.bfloat16, "conv2d_fwd.x")
     _check(wrsc, torch.bfloat16, "conv2d_fwd.w")
     O, R, S, C = wrsc.shape
@@ -74,12 +100,12 @@ def conv2d_fwd(x: torch.Tensor, wrsc: torch.Tensor, stride: int, pad: int, Cw: O
         raise ValueError("conv2d_fwd: stats must be [2, O] fp32")
     native.require().conv_fwd(native.stream_handle(x.device), shp, x.data_ptr(), wrsc.data_ptr(), out.data_ptr(),
                               stats.data_ptr() if stats is not None else 0,
-                              shift.data_ptr() if shift is not None else 0)
+                              shift.data_ptr() if shift is not None else 0, *_ws_args(ws))
     return out
 
 
 def conv2d_dgrad(dy: torch.Tensor, wrsc: torch.Tensor, x_shape, stride: int, pad: int, Cw: Optional[int] = None,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dx[N,H,W,C] from dy[N,P,Q,O]."""
     _check(dy, torch.bfloat16, "conv2d_dgrad.dy")
     O, R, S, C = wrsc.shape
@@ -88,7 +114,8 @@ def conv2d_dgrad(dy: torch.Tensor, wrsc: torch.Tensor, x_shape, stride: int, pad
         raise ValueError(f"conv2d_dgrad: dy shape {tuple(dy.shape)} vs expected {(shp[0], shp[6], shp[7], O)}")
     if out is None:
         out = torch.empty(*x_shape, dtype=torch.bfloat16, device=dy.device)
-    native.require().conv_dgrad(native.stream_handle(dy.device), shp, dy.data_ptr(), wrsc.data_ptr(), out.data_ptr())
+    native.require().conv_dgrad(native.stream_handle(dy.device), shp, dy.data_ptr(), wrsc.data_ptr(), out.data_ptr(),
+                                *_ws_args(ws))
     return out
 
 

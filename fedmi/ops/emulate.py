@@ -50,6 +50,15 @@ def pack_weight(w, c_pad=None, out=None):
     return out
 
 
+def pack_weights(items):
+    for w, out in items:
+        pack_weight(w, out.shape[3], out=out)
+
+
+def fd_ws_floats(*a, **k):
+    return 0
+
+
 def _w_from_img(wr: torch.Tensor, Cw: Optional[int]) -> torch.Tensor:
     m = _MASTER.get(wr.data_ptr())
     w = m.float() if m is not None and m.shape[2:] == wr.shape[1:3] else wr.permute(0, 3, 1, 2).float()
@@ -66,7 +75,7 @@ def _stats_add(stats, y_bf16_nhwc, shift=None):
 
 
 @torch.no_grad()
-def conv2d_fwd(x, wrsc, stride, pad, Cw=None, stats=None, out=None, shift=None):
+def conv2d_fwd(x, wrsc, stride, pad, Cw=None, stats=None, out=None, shift=None, ws=None):
     Cw = Cw or x.shape[3]
     y = F.conv2d(_nchw(x)[:, :Cw], _w_from_img(wrsc, Cw), stride=stride, padding=pad)
     if out is None:
@@ -77,7 +86,7 @@ def conv2d_fwd(x, wrsc, stride, pad, Cw=None, stats=None, out=None, shift=None):
 
 
 @torch.no_grad()
-def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None):
+def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None, ws=None):
     N, H, W, C = x_shape
     Cw = Cw or C
     dx = torch.nn.grad.conv2d_input((N, Cw, H, W), _w_from_img(wrsc, Cw), _nchw(dy), stride=stride, padding=pad)
@@ -204,7 +213,7 @@ def bn_apply(z, a, y, train, relu, z2=None, b=None, res=None, eps=1e-5, momentum
 
 @torch.no_grad()
 def bn_bwd(dya, za, a, dgamma_a, dbeta_a, dza, red, dyb=None, y=None, zb=None, b=None, dgamma_b=None,
-           dbeta_b=None, dzb=None, gout=None):
+           dbeta_b=None, dzb=None, gout=None, ws=None):
     C = za.shape[-1]
     M = za.numel() // C
     g = dya.float().reshape(M, C)
@@ -226,6 +235,10 @@ def bn_bwd(dya, za, a, dgamma_a, dbeta_a, dza, red, dyb=None, y=None, zb=None, b
             p.shift.copy_(p.smean)
         d = p.gamma * p.sinv * (g - sg / M - xhat * sgx / M)
         dz.copy_(d.reshape(dz.shape).to(dz.dtype))
+
+
+def bn_bwd_ws_floats(M, C):
+    return 0
 
 
 @torch.no_grad()
@@ -270,10 +283,10 @@ def emulated():
         saved.append((mod, name, getattr(mod, name)))
         setattr(mod, name, fn)
 
-    for name in ("pack_weight", "conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
+    for name in ("pack_weight", "pack_weights", "fd_ws_floats", "conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
                  "dwconv_dgrad", "dwconv_wgrad", "dwconv_ws_floats"):
         swap(conv, name, globals()[name])
-    for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "head"):
+    for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "bn_bwd_ws_floats", "head"):
         swap(cnn, name, globals()[name])
     swap(native, "require", lambda: _NativeStub())
     swap(native, "stream_handle", lambda device=None: 0)

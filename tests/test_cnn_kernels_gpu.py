@@ -138,6 +138,19 @@ def test_bn_forward_backward_with_projection_residual(gpu_device):
     assert _rel(dgb, gbr.grad) < 1e-2 and _rel(dbb, bbr.grad) < 1e-2
     mask = (y.float() > 0).float()
     assert _rel(gout.float(), (dya.float() + dyb.float()) * mask) < 1e-2
+    # two-level reduction (replicated atomics + finalize): same result, red needs no init, ws left zero
+    ws = torch.zeros(cnn.bn_bwd_ws_floats(M, C), device=dev)
+    red2 = torch.full((3, C), float("nan"), device=dev)
+    dza2, dzb2 = torch.empty_like(dza), torch.empty_like(dzb)
+    dga2, dba2, dgb2, dbb2 = (torch.empty(C, device=dev) for _ in range(4))
+    for _ in range(2):   # the scratch is reusable without re-zeroing
+        cnn.bn_bwd(dya, za, A, dga2, dba2, dza2, red2, dyb=dyb, y=y, zb=zb, b=B, dgamma_b=dgb2, dbeta_b=dbb2,
+                   dzb=dzb2, ws=ws)
+        first = dga2.clone() if _ == 0 else first
+    torch.cuda.synchronize()
+    assert _rel(first, dga2) < 1e-5 and float(ws.abs().max()) == 0.0
+    assert _rel(dza2.float(), dza.float()) < 1e-2 and _rel(dzb2.float(), dzb.float()) < 1e-2
+    assert _rel(dga2, dga) < 1e-4 and _rel(dba2, dba) < 1e-4 and _rel(dgb2, dgb) < 1e-4
 
 
 def test_bn_eval_uses_running_stats(gpu_device):
@@ -225,3 +238,74 @@ def test_depthwise_fwd_dgrad_wgrad(gpu_device, shape):
     assert torch.allclose(stats[0], yb.sum((0, 1, 2)), rtol=1e-3, atol=1e-2)
     assert _rel(dx.float(), _nhwc(x.grad)) < 1e-2
     assert _rel(dw, wb.grad) < 1e-2
+
+
+# full-batch ResNet-18 layer3/4 shapes: few output tiles + long K -> split-K through a workspace
+SPLIT_SHAPES = [
+    (128, 8, 8, 256, 256, 3, 1, 1),     # layer3
+    (128, 4, 4, 512, 512, 3, 1, 1),     # layer4
+    (128, 8, 8, 256, 512, 3, 2, 1),     # layer4 downsample (stride-2 dgrad phases)
+]
+
+
+@pytest.mark.parametrize("shape", SPLIT_SHAPES, ids=[str(s) for s in SPLIT_SHAPES])
+def test_conv_splitk_fwd_dgrad(gpu_device, shape):
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device, seed=4)
+    wr = conv.pack_weight(w)
+    need = conv.fd_ws_floats(xn.shape, O, R, R, st, pad, Cw)
+    assert need > 0, "shape expected to take the split-K path"
+    ws = torch.full((need,), float("nan"), device=gpu_device)   # every partial must be written
+    shift = torch.randn(O, device=gpu_device) * 0.1
+    s_split = torch.zeros(2, O, device=gpu_device)
+    s_one = torch.zeros(2, O, device=gpu_device)
+    y = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=s_split, shift=shift, ws=ws)
+    y1 = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=s_one, shift=shift)
+    ref = F.conv2d(x, wb, stride=st, padding=pad)
+    torch.cuda.synchronize()
+    assert _rel(y.float(), _nhwc(ref)) < 1e-2
+    assert _rel(y.float(), y1.float()) < 1e-2
+    d = y.float() - shift
+    assert torch.allclose(s_split[0], d.sum((0, 1, 2)), rtol=1e-3, atol=1e-1)
+    assert torch.allclose(s_split[1], (d * d).sum((0, 1, 2)), rtol=1e-3, atol=1e-1)
+    # data gradient
+    xr = x.clone().requires_grad_(True)
+    out = F.conv2d(xr, wb, stride=st, padding=pad)
+    gy = torch.randn_like(out).bfloat16().float()
+    out.backward(gy)
+    dyn = _nhwc(gy).bfloat16()
+    ws.fill_(float("nan"))
+    dx = conv.conv2d_dgrad(dyn, wr, xn.shape, st, pad, Cw=Cw, ws=ws)
+    torch.cuda.synchronize()
+    assert _rel(dx.float(), _nhwc(xr.grad)) < 1e-2
+
+
+def test_conv_wgrad_many_splits_and_padded_channels(gpu_device):
+    # stem-like: 3 real channels padded to 8, deep K (many splits): the parallel reduce + permute
+    shape = (64, 32, 32, 3, 64, 3, 1, 1)
+    x, w, wb, xn = _make(shape, gpu_device, seed=5)
+    xr = x.clone()
+    wr_ = wb.clone().requires_grad_(True)
+    out = F.conv2d(xr, wr_, stride=1, padding=1)
+    gy = torch.randn_like(out).bfloat16().float()
+    out.backward(gy)
+    dyn = _nhwc(gy).bfloat16()
+    for sp in (0, 1, 37, 128):
+        dw = conv.conv2d_wgrad(xn, dyn, 3, 3, 1, 1, Cw=3, splits=sp)
+        torch.cuda.synchronize()
+        assert _rel(dw, wr_.grad) < 1e-2, sp
+    base = torch.randn(64, 3, 3, 3, device=gpu_device)
+    acc = conv.conv2d_wgrad(xn, dyn, 3, 3, 1, 1, Cw=3, out=base.clone(), accumulate=True)
+    torch.cuda.synchronize()
+    assert _rel(acc - base, wr_.grad) < 1e-2
+
+
+def test_pack_weights_multi(gpu_device):
+    torch.manual_seed(6)
+    ws = [torch.randn(o, c, r, r, device=gpu_device) for o, c, r in ((64, 3, 3), (128, 64, 1), (16, 24, 5))]
+    single = [conv.pack_weight(w) for w in ws]
+    multi = [torch.full_like(s, 7.0) for s in single]
+    conv.pack_weights(list(zip(ws, multi)))
+    torch.cuda.synchronize()
+    for a, b in zip(single, multi):
+        assert torch.equal(a, b)
