@@ -20,7 +20,13 @@ struct ConvShape {
   int N, H, W, C, Cw, O, P, Q, R, S, st, pad;
 };
 void launch_conv_fwd(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, const float*, float*, long);
-void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, long);
+void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, long, const bf16*);
+struct DPackItem {
+  const float* w;
+  bf16* wd;
+  int O, Cw, C, R, S, st, pad;
+};
+void launch_dgrad_pack_multi(hipStream_t, const DPackItem*, int);
 long conv_fd_ws_floats(const ConvShape&);
 struct PackItem {
   const float* w;
@@ -100,6 +106,7 @@ BNDesc bn_from(const py::dict& d) {
 }  // namespace
 
 void fedmi_bind_cnn(py::module_& m) {
+  m.attr("STAT_REP") = STAT_REP;
   m.def("conv_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                        uintptr_t shift, uintptr_t ws, long ws_floats) {
     launch_conv_fwd(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(w), P<bf16>(y), P<float>(stats),
@@ -108,12 +115,24 @@ void fedmi_bind_cnn(py::module_& m) {
   }, py::arg("st"), py::arg("shape"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("shift"),
      py::arg("ws") = 0, py::arg("ws_floats") = 0);
   m.def("conv_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
-                         long ws_floats) {
+                         long ws_floats, uintptr_t wd) {
     launch_conv_dgrad(S(st), shape_from(shp), P<const bf16>(dy), P<const bf16>(w), P<bf16>(dx), P<float>(ws),
-                      ws ? ws_floats : 0);
+                      ws ? ws_floats : 0, P<const bf16>(wd));
     check("conv_dgrad");
   }, py::arg("st"), py::arg("shape"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("ws") = 0,
-     py::arg("ws_floats") = 0);
+     py::arg("ws_floats") = 0, py::arg("wd") = 0);
+  m.def("dgrad_pack_multi", [](uintptr_t st, const py::list& items) {
+    std::vector<DPackItem> v;
+    for (const auto& it : items) {
+      const py::tuple t = it.cast<py::tuple>();
+      if (t.size() != 9) throw std::invalid_argument("dgrad_pack_multi item: (w, wd, O, Cw, C, R, S, stride, pad)");
+      v.push_back(DPackItem{P<const float>(t[0].cast<uintptr_t>()), P<bf16>(t[1].cast<uintptr_t>()), t[2].cast<int>(),
+                            t[3].cast<int>(), t[4].cast<int>(), t[5].cast<int>(), t[6].cast<int>(), t[7].cast<int>(),
+                            t[8].cast<int>()});
+    }
+    if (!v.empty()) launch_dgrad_pack_multi(S(st), v.data(), (int)v.size());
+    check("dgrad_pack_multi");
+  });
   m.def("conv_fd_ws_floats", [](const py::tuple& shp) { return conv_fd_ws_floats(shape_from(shp)); });
   m.def("conv_pack_multi", [](uintptr_t st, const py::list& items) {
     std::vector<PackItem> v;

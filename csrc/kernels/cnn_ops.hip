@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void prep_input_kernel(const uint8_t* __restri
 
 // ---------------------------------------------------------------------------
 struct BNArgs {
-  const float* stats;     // [2][C]: sum, sum of squares over M rows (train)
+  const float* stats;     // [STAT_REP][2][C]: sum, sum of squares over M rows (train)
   const float* gamma;
   const float* beta;
   float* rmean;           // running stats (updated in train mode, read in eval)
@@ -93,8 +93,14 @@ FEDMI_DEV void bn_coeffs(const BNArgs& a, int C, int M, float eps, float mom, in
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float mean, inv;
     if (train) {
-      const float ms = a.stats[c] / (float)M;   // mean of (z - shift)
-      const float var = fmaxf(a.stats[C + c] / (float)M - ms * ms, 0.f);
+      float s1 = 0.f, s2 = 0.f;   // sum the STAT_REP replicas of [sum | sum of squares]
+#pragma unroll 4
+      for (int r = 0; r < STAT_REP; ++r) {
+        s1 += a.stats[(2 * r) * C + c];
+        s2 += a.stats[(2 * r + 1) * C + c];
+      }
+      const float ms = s1 / (float)M;   // mean of (z - shift)
+      const float var = fmaxf(s2 / (float)M - ms * ms, 0.f);
       mean = ms + (a.shift ? a.shift[c] : 0.f);
       inv = rsqrtf(var + eps);
       if (blockIdx.x == 0) {

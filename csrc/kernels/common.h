@@ -15,6 +15,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define FEDMI_DEV __device__ __forceinline__
 
+// BatchNorm batch statistics are accumulated into STAT_REP replicas
+// [STAT_REP][2][C] (replica = producing workgroup % STAT_REP): the per-channel
+// atomics of hundreds of workgroups would otherwise serialise on 2*C addresses.
+// Consumers (bn_apply) sum the replicas.
+constexpr int STAT_REP = 16;
+
 FEDMI_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }

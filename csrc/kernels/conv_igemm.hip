@@ -31,6 +31,7 @@
 // Reference parity: these are the convolution / convolution_backward ops of
 // every zoo model (src/models/resnet.py:14-104 etc.).
 #include <algorithm>
+#include <vector>
 #include <stdexcept>
 
 #include "common.h"
@@ -54,6 +55,21 @@ struct ConvGeom {
   int ph, pw, r0, s0, nr, ns, Hp, Wp;
   FastDiv dC, dO, dS, dQ, dPQ, dW, dHW, dNS, dWp, dHWp;
 };
+
+// GEMM row m = (n, p, q) over an output grid P x Q -> row of the stored output:
+// identity, or the stride-`st` sub-pixel scatter of a DGRAD phase:
+// ((n * OH + p * st + ph) * OW + q * st + pw).
+struct RowMap {
+  int on;
+  int P, Q, OH, OW, st, ph, pw;
+  FastDiv dPQ, dQ;
+};
+FEDMI_DEV long map_row(const RowMap& r, int m) {
+  if (!r.on) return m;
+  const uint32_t n = fdiv(m, r.dPQ), pq = m - n * r.P * r.Q;
+  const uint32_t p = fdiv(pq, r.dQ), q = pq - p * r.Q;
+  return ((long)n * r.OH + p * r.st + r.ph) * r.OW + q * r.st + r.pw;
+}
 
 enum { FWD = 0, DGRAD = 1, WGRAD = 2 };
 constexpr int BK = 64;
@@ -377,9 +393,266 @@ __global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, co
         float t = 0.f;
 #pragma unroll
         for (int pp = 0; pp < PARTS; ++pp) t += red[(pp * 2 + q) * BN + cl];
-        if (n0 + cl < g.NC) unsafeAtomicAdd(stats + q * g.NC + n0 + cl, t);
+        if (n0 + cl < g.NC) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.NC + n0 + cl, t);
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Tap-major implicit GEMM with LDS-DMA staging (FWD, and DGRAD through
+// flipped/transposed "dgrad weight images"; input channels C % 64 == 0).
+//
+//   out[m = (n,p,q)][o] = sum_{r,s,c} in[n][p*st - pad_h + r][q*st - pad_w + s][c] * wt[o][r][s][c]
+//
+// With C % 64 == 0 every BK = 64 K step is ONE tap (r, s) and 64 consecutive
+// channels, so a row of the A tile is 128 contiguous bytes of one input pixel
+// (or zeros in the halo).  Both operand tiles are therefore K-contiguous
+// [rows][64] images filled by global_load_lds_dwordx4 (no VGPR staging, no
+// ds_write): each wave-instruction writes 8 rows x 128 B linearly, and the
+// per-lane GLOBAL address carries the XOR swizzle (16-B chunk kc of row r is
+// stored at chunk kc ^ (r & 7)), which ds_read_b128 fragment reads undo.  Halo
+// / tail lanes read a 16-B zero block instead of branching.
+//
+// Pipeline: three LDS stages, the DMA two K steps ahead, ONE raw s_barrier per
+// step behind a counted `s_waitcnt vmcnt` (never vmcnt(0) or __syncthreads()
+// while a DMA is in flight).  Tile 128 x BN (BN 128 | 64), 4 waves of 64 x BN/2.
+// ---------------------------------------------------------------------------
+struct TapGeom {
+  int N, H, W, C;          // input [N][H][W][C], C % 64 == 0
+  int O;                   // GEMM columns = weight rows [O][R][S][C]
+  int P, Q;                // output grid, GEMM rows M = N * P * Q
+  int R, S, st, pad_h, pad_w;
+  int M, K;                // K = R * S * C
+  FastDiv dPQ, dQ;
+};
+
+__device__ __attribute__((aligned(16))) const uint4 g_zero16[4] = {};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+FEDMI_DEV void glds16(const void* g, bf16* lds_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_base, 16, 0, 0);
+}
+
+// fragment of rows [i0, i0+16), k block kk (0/1) from a swizzled [rows][64] image
+FEDMI_DEV bf16x8 frag_sw(const bf16* img, int i0, int kk, int lane) {
+  const int row = i0 + (lane & 15);
+  const int kc = kk * 4 + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((kc ^ (row & 7)) << 3));
+}
+
+template <int BN>
+__global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+                                                bf16* __restrict__ out, float* __restrict__ part,
+                                                float* __restrict__ stats, const float* __restrict__ shift,
+                                                TapGeom g, RowMap rmap, int ksteps_per_split) {
+  constexpr int BM = 128;
+  constexpr int NA = BM / 32;            // A wave-instructions per stage per wave (8 rows each)
+  constexpr int NB = BN / 32;
+  constexpr int STAGE = (BM + BN) * 64;  // elements
+  constexpr int TM = 4, TN = BN / 32;    // 16x16 fragments per wave: 64 x BN/2
+  constexpr int NST = 3;                 // LDS stages: DMA runs two K steps ahead
+  __shared__ __attribute__((aligned(16))) bf16 smem[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = (g.O + BN - 1) / BN;
+  const int tile_n = blockIdx.x % ntn, tile_m = blockIdx.x / ntn;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * (BN / 2);
+
+  const int ksteps = g.K / 64;
+  const int kb = blockIdx.z * ksteps_per_split;
+  const int ke = min(ksteps, kb + ksteps_per_split);
+
+  // per-lane DMA sources: row (l >> 3) of each 8-row group, logical chunk kc
+  const int lrow = lane >> 3;
+  const int kc = (lane & 7) ^ lrow;
+  long a_off[NA];
+  int a_h[NA], a_w[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int m = m0 + (wave * NA + i) * 8 + lrow;
+    const bool ok = m < g.M;
+    const uint32_t mm = ok ? m : 0;
+    const uint32_t n = fdiv(mm, g.dPQ), pq = mm - n * g.P * g.Q;
+    const uint32_t p = fdiv(pq, g.dQ), q = pq - p * g.Q;
+    a_h[i] = ok ? (int)(p * g.st) - g.pad_h : -(1 << 20);   // invalid rows never pass the bounds test
+    a_w[i] = (int)(q * g.st) - g.pad_w;
+    a_off[i] = (((long)n * g.H + a_h[i]) * g.W + a_w[i]) * g.C + kc * 8;
+  }
+  long b_off[NB];
+  bool b_ok[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int o = n0 + (wave * NB + i) * 8 + lrow;
+    b_ok[i] = o < g.O;
+    b_off[i] = (long)o * g.K + kc * 8;
+  }
+
+  auto issue = [&](int t, int stage) {
+    const int k0 = t * 64;
+    const int rs = k0 / g.C, c0 = k0 - rs * g.C;
+    const int r = rs / g.S, sx = rs - r * g.S;
+    const long tap = ((long)r * g.W + sx) * g.C + c0;
+    bf16* As = smem + stage * STAGE;
+    bf16* Bs = As + BM * 64;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int h = a_h[i] + r, w = a_w[i] + sx;
+      const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const void* src = ok ? (const void*)(in + a_off[i] + tap) : (const void*)g_zero16;
+      glds16(src, As + (wave * NA + i) * 8 * 64);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const void* src = b_ok[i] ? (const void*)(wt + b_off[i] + k0) : (const void*)g_zero16;
+      glds16(src, Bs + (wave * NB + i) * 8 * 64);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+
+  // One barrier per K step: wait for this wave's DMA of step t (leaving step t+1's
+  // in flight), barrier (step t visible everywhere AND every wave is done reading
+  // step t-1's stage), refill that stage with step t+2, then MFMAs on step t.
+  if (kb < ke) issue(kb, 0);
+  if (kb + 1 < ke) issue(kb + 1, 1);
+  for (int t = kb; t < ke; ++t) {
+    const int stg = (t - kb) % NST;
+    if (t + 1 < ke) {
+      if constexpr (NA + NB == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < ke) issue(t + 2, (stg + 2) % NST);
+    const bf16* As = smem + stg * STAGE;
+    const bf16* Bs = As + BM * 64;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag_sw(As, wm0 + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = frag_sw(Bs, wn0 + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+  }
+  __syncthreads();   // every wave done with the stages (no DMA in flight) before LDS reuse
+
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  if (part != nullptr) {   // split-K partial -> [split][M][O] fp32
+    float* ws = part + (long)blockIdx.z * g.M * g.O;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn0 + 16 * j + col_l;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wm0 + 16 * i + row_l + e;
+          if (m < g.M && col < g.O) ws[(long)m * g.O + col] = acc[i][j][e];
+        }
+    }
+    return;
+  }
+  constexpr int CT_LD = BN + 8;
+  bf16* ct = smem;
+  float* red = reinterpret_cast<float*>(smem + BM * CT_LD);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        ct[(wm0 + 16 * i + row_l + e) * CT_LD + wn0 + 16 * j + col_l] = (bf16)acc[i][j][e];
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int c = tid; c < BM * CPR; c += 256) {
+    const int row = c / CPR, cc = c % CPR;
+    const int m = m0 + row, col = n0 + cc * 8;
+    if (m < g.M && col < g.O)
+      *reinterpret_cast<uint4*>(out + map_row(rmap, m) * g.O + col) = *reinterpret_cast<const uint4*>(ct + row * CT_LD + cc * 8);
+  }
+  if (stats != nullptr) {   // BN batch statistics of bf16(y) - shift, one atomic per column per WG
+    constexpr int PARTS = 256 / BN;
+    const int col = tid % BN, prt = tid / BN;
+    const int rows = min(BM, g.M - m0);
+    const float sh = (shift != nullptr && n0 + col < g.O) ? shift[n0 + col] : 0.f;
+    float s1 = 0.f, s2 = 0.f;
+    for (int r = prt; r < rows; r += PARTS) {
+      const float v = (float)ct[r * CT_LD + col] - sh;
+      s1 += v;
+      s2 += v * v;
+    }
+    red[(prt * 2) * BN + col] = s1;
+    red[(prt * 2 + 1) * BN + col] = s2;
+    __syncthreads();
+    if (tid < 2 * BN) {
+      const int q = tid / BN, cl = tid % BN;
+      float t = 0.f;
+#pragma unroll
+      for (int pp = 0; pp < PARTS; ++pp) t += red[(pp * 2 + q) * BN + cl];
+      if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, t);
+    }
+  }
+}
+
+// DGRAD weight images for conv_tap: for each sub-pixel phase (stride 1: the
+// single phase r0 = s0 = 0, nr = R, ns = S, step 1)
+//   wd[c][i][j][o] = W[o][c][r0 + step*(nr-1-i)][s0 + step*(ns-1-j)]   (c < Cw, else 0)
+// One workgroup per (64 output channels o, 4 input channels c): the fp32 rows
+// W[o][c0:c0+4][:][:] are read contiguously into LDS, the image rows
+// wd[c][i][j][o0:o0+64] written as 128-B runs.
+struct DPackEntry {
+  const float* w;    // fp32 master [O][Cw][R][S]
+  bf16* wd;          // image [Cpad][nr][ns][O]
+  int O, Cw, Cpad, R, S, r0, s0, nr, ns, step;
+  int blk0;          // first workgroup of this entry
+};
+constexpr int MAX_DPACK = 16;
+struct DPackTable {
+  DPackEntry e[MAX_DPACK];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void dgrad_pack_kernel(DPackTable t) {
+  __shared__ float tile[64][4 * 49 + 1];   // 64 o x (4 c x R*S <= 7x7)
+  int k = 0;
+  while (k + 1 < t.n && (int)blockIdx.x >= t.e[k + 1].blk0) ++k;
+  const DPackEntry& p = t.e[k];
+  const int b = blockIdx.x - p.blk0;
+  const int ncb = (p.Cpad + 3) / 4;
+  const int o0 = (b / ncb) * 64, c0 = (b % ncb) * 4;
+  const int RS = p.R * p.S;
+  const int span = 4 * RS;
+  for (int e = threadIdx.x; e < 64 * span; e += 256) {
+    const int oi = e / span, f = e - oi * span;   // f = (c - c0) * RS + rs
+    const int o = o0 + oi, c = c0 + f / RS;
+    tile[oi][f] = (o < p.O && c < p.Cw) ? p.w[((long)o * p.Cw + c) * RS + (f % RS)] : 0.f;
+  }
+  __syncthreads();
+  const int taps = p.nr * p.ns;
+  for (int e = threadIdx.x; e < 4 * taps * 64; e += 256) {
+    const int oi = e & 63, rest = e >> 6;
+    const int ci = rest / taps, ij = rest - ci * taps;
+    const int i = ij / p.ns, j = ij - i * p.ns;
+    const int c = c0 + ci, o = o0 + oi;
+    if (c >= p.Cpad || o >= p.O) continue;
+    const int r = p.r0 + p.step * (p.nr - 1 - i), sx = p.s0 + p.step * (p.ns - 1 - j);
+    p.wd[(((long)c * p.nr + i) * p.ns + j) * p.O + o] = (bf16)tile[oi][ci * RS + r * p.S + sx];
   }
 }
 
@@ -423,24 +696,24 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict
 // accumulates the BatchNorm batch statistics (sum / sum of squares of
 // bf16(y) - shift[c]) like the single-pass epilogue.  Each thread owns one
 // 8-channel group (two 16-B loads per split) of rows r0, r0 + rstep, ...
-__global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restrict__ ws, int splits, ConvGeom g,
-                                                          bf16* __restrict__ out, float* __restrict__ stats,
-                                                          const float* __restrict__ shift, int remap,
+__global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restrict__ ws, int splits, int M, int NC,
+                                                          RowMap rmap, bf16* __restrict__ out,
+                                                          float* __restrict__ stats, const float* __restrict__ shift,
                                                           int rows_per_block) {
   __shared__ float red[2][256][8];
-  const int VR = g.NC >> 3;                 // host: blockDim.x % VR == 0
+  const int VR = NC >> 3;                 // host: blockDim.x % VR == 0
   const int cg = threadIdx.x % VR, rstep = blockDim.x / VR, r0 = threadIdx.x / VR;
   const int c0 = cg * 8;
-  const long plane = (long)g.M * g.NC;
+  const long plane = (long)M * NC;
   float sh[8], s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sh[j] = (stats && shift) ? shift[c0 + j] : 0.f;
     s1[j] = s2[j] = 0.f;
   }
-  const int rb = blockIdx.x * rows_per_block, re = min(g.M, rb + rows_per_block);
+  const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
   for (int m = rb + r0; m < re; m += rstep) {
-    const float* p = ws + (long)m * g.NC + c0;
+    const float* p = ws + (long)m * NC + c0;
     float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
     for (int z = 1; z < splits; ++z) {
       const float4 ua = *reinterpret_cast<const float4*>(p + z * plane);
@@ -452,13 +725,8 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restric
     bf16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
-    long orow = m;
-    if (remap) {   // DGRAD stride-2 phase row -> input pixel row
-      const uint32_t n = fdiv(m, g.dHWp), hw = m - n * g.Hp * g.Wp;
-      const uint32_t hh = fdiv(hw, g.dWp), ww = hw - hh * g.Wp;
-      orow = ((long)n * g.H + hh * g.st + g.ph) * g.W + ww * g.st + g.pw;
-    }
-    *reinterpret_cast<bf16x8*>(out + orow * g.NC + c0) = o;
+    const long orow = map_row(rmap, m);
+    *reinterpret_cast<bf16x8*>(out + orow * NC + c0) = o;
     if (stats) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -475,12 +743,12 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restric
     red[1][threadIdx.x][j] = s2[j];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < 2 * g.NC; e += blockDim.x) {
-    const int q = e / g.NC, c = e - q * g.NC;
+  for (int e = threadIdx.x; e < 2 * NC; e += blockDim.x) {
+    const int q = e / NC, c = e - q * NC;
     const int grp = c >> 3, j = c & 7;
     float t = 0.f;
     for (int th = grp; th < (int)blockDim.x; th += VR) t += red[q][th][j];
-    unsafeAtomicAdd(stats + q * g.NC + c, t);
+    unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * NC + c, t);
   }
 }
 
@@ -536,6 +804,14 @@ namespace fedmi {
 struct ConvShape {
   int N, H, W, C, Cw, O, P, Q, R, S, st, pad;
 };
+
+static RowMap make_rowmap(int P, int Q, int OH, int OW, int st, int ph, int pw) {
+  RowMap r{};
+  r.on = 1;
+  r.P = P; r.Q = Q; r.OH = OH; r.OW = OW; r.st = st; r.ph = ph; r.pw = pw;
+  r.dPQ = make_div(P * Q); r.dQ = make_div(Q);
+  return r;
+}
 
 static ConvGeom make_geom(const ConvShape& s) {
   ConvGeom g{};
@@ -620,6 +896,99 @@ static void launch_mode(hipStream_t st, const ConvGeom& g, const bf16* x, const 
   else launch_tiled<MODE, 64, 64>(st, grid, g, x, w, dy, out, gout, stats, shift, kps, partial);
 }
 
+// ---- tap-major LDS-DMA path (conv_tap)
+static TapGeom make_tap(int N, int H, int W, int C, int O, int P, int Q, int R, int S, int st, int pad_h, int pad_w) {
+  TapGeom g{};
+  g.N = N; g.H = H; g.W = W; g.C = C; g.O = O; g.P = P; g.Q = Q;
+  g.R = R; g.S = S; g.st = st; g.pad_h = pad_h; g.pad_w = pad_w;
+  g.M = N * P * Q; g.K = R * S * C;
+  g.dPQ = make_div(P * Q); g.dQ = make_div(Q);
+  return g;
+}
+
+static int tap_bn(int O) { return O <= 64 ? 64 : 128; }
+
+// Split K only to fill one wave of workgroups: conv_tap keeps 1 (BN 128, 96 KiB
+// LDS) or 2 (BN 64) workgroups per CU, and a split costs an fp32 round trip.
+static int tap_splits(const TapGeom& g, long ws_floats) {
+  if (ws_floats <= 0) return 1;
+  const int bn = tap_bn(g.O);
+  const long tiles = (long)((g.M + 127) / 128) * ((g.O + bn - 1) / bn);
+  const long target = (bn == 128 ? 1l : 2l) * num_cus();
+  const int ksteps = g.K / 64;
+  if (4 * tiles >= 3 * target || ksteps < 16) return 1;
+  long sp = std::min<long>((target + tiles / 2) / tiles, ksteps / 8);
+  sp = std::min<long>(sp, ws_floats / ((long)g.M * g.O));
+  if (sp < 2) return 1;
+  const int kps = (int)((ksteps + sp - 1) / sp);
+  return (ksteps + kps - 1) / kps;
+}
+
+static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const bf16* wt, bf16* out, float* stats,
+                       const float* shift, const RowMap& rm, float* ws, long ws_floats) {
+  if (g.C % 64 || g.O % 8) throw std::invalid_argument("conv_tap: need C % 64 == 0 and O % 8 == 0");
+  const int BN = tap_bn(g.O);
+  const long tiles = (long)((g.M + 127) / 128) * ((g.O + BN - 1) / BN);
+  const int ksteps = g.K / 64;
+  const int sp = tap_splits(g, ws_floats);
+  const int kps = (ksteps + sp - 1) / sp;
+  const int splits = (ksteps + kps - 1) / kps;
+  dim3 grid((unsigned)tiles, 1, (unsigned)splits);
+  float* part = splits > 1 ? ws : nullptr;
+  if (BN == 128)
+    hipLaunchKernelGGL(conv_tap<128>, grid, dim3(256), 0, st, in, wt, out, part, part ? nullptr : stats, shift, g, rm, kps);
+  else
+    hipLaunchKernelGGL(conv_tap<64>, grid, dim3(256), 0, st, in, wt, out, part, part ? nullptr : stats, shift, g, rm, kps);
+  if (splits > 1) {
+    const int VR = g.O / 8;
+    const int tb = (256 / VR) * VR;
+    const int rstep = tb / VR;
+    const int rows_per_block = stats ? std::max(2 * rstep, (g.M + 255) / 256) : std::max(rstep, (g.M + 1023) / 1024);
+    const int nblk = (g.M + rows_per_block - 1) / rows_per_block;
+    hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, splits, g.M, g.O, rm, out, stats, shift,
+                       rows_per_block);
+  }
+}
+
+// DGRAD phases as conv_tap problems over dY: (geometry, row map, image offset) per phase.
+struct TapPhase {
+  TapGeom g;
+  RowMap rm;
+  long img_off;
+  int r0, s0, nr, ns;
+  bool empty;   // no taps land on this parity (1x1 stride 2): output rows must be zero
+  int ph, pw;
+};
+
+static int dgrad_tap_phases(const ConvShape& s, TapPhase* out) {
+  int n = 0;
+  if (s.st == 1) {
+    TapPhase& t = out[n++];
+    t = TapPhase{};
+    t.g = make_tap(s.N, s.P, s.Q, s.O, s.C, s.H, s.W, s.R, s.S, 1, s.R - 1 - s.pad, s.S - 1 - s.pad);
+    t.r0 = t.s0 = 0; t.nr = s.R; t.ns = s.S;
+    return n;
+  }
+  long off = 0;
+  for (int ph = 0; ph < 2; ++ph)
+    for (int pw = 0; pw < 2; ++pw) {
+      const int r0 = (ph + s.pad) & 1, s0 = (pw + s.pad) & 1;
+      const int nr = std::max(0, (s.R - r0 + 1) / 2), ns = std::max(0, (s.S - s0 + 1) / 2);
+      const int Hp = (s.H - ph + 1) / 2, Wp = (s.W - pw + 1) / 2;
+      if (Hp <= 0 || Wp <= 0) continue;
+      TapPhase& t = out[n++];
+      t = TapPhase{};
+      t.ph = ph; t.pw = pw; t.r0 = r0; t.s0 = s0; t.nr = nr; t.ns = ns;
+      t.empty = nr * ns == 0;
+      const int d0 = (ph + s.pad - r0) / 2, e0 = (pw + s.pad - s0) / 2;
+      t.g = make_tap(s.N, s.P, s.Q, s.O, s.C, Hp, Wp, std::max(nr, 1), std::max(ns, 1), 1, nr - 1 - d0, ns - 1 - e0);
+      t.rm = make_rowmap(Hp, Wp, s.H, s.W, 2, ph, pw);
+      t.img_off = off;
+      off += (long)s.C * nr * ns * s.O;
+    }
+  return n;
+}
+
 // FWD / DGRAD with automatic split-K through ``ws`` (null / 0 floats: never split).
 template <int MODE>
 static void launch_fd(hipStream_t st, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy, bf16* out,
@@ -637,11 +1006,14 @@ static void launch_fd(hipStream_t st, const ConvGeom& g, const bf16* x, const bf
   // per-channel atomics contend on 2 x NC addresses)
   const int rows_per_block = stats ? std::max(2 * rstep, (g.M + 255) / 256) : std::max(rstep, (g.M + 1023) / 1024);
   const int nblk = (g.M + rows_per_block - 1) / rows_per_block;
-  const int remap = (MODE == DGRAD && g.st != 1) ? 1 : 0;
-  hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, sp, g, out, stats, shift, remap,
+  RowMap rm{};
+  if (MODE == DGRAD && g.st != 1) rm = make_rowmap(g.Hp, g.Wp, g.H, g.W, g.st, g.ph, g.pw);
+  hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, sp, g.M, g.NC, rm, out, stats, shift,
                      rows_per_block);
 }
 
+// K-split count for the weight gradient: about two workgroups per CU, at least
+// 8 K steps per split, and a bounded workspace.
 // K-split count for the weight gradient: about two workgroups per CU, at least
 // 8 K steps per split, and a bounded workspace.
 static int wgrad_splits(const ConvGeom& g, long ws_cap_floats) {
@@ -662,14 +1034,36 @@ void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf
   check_shape(s);
   ConvGeom g = make_geom(s);
   g.M = s.N * s.P * s.Q; g.NC = s.O; g.K = s.R * s.S * s.C;
+  if (s.C % 64 == 0) {
+    const TapGeom t = make_tap(s.N, s.H, s.W, s.C, s.O, s.P, s.Q, s.R, s.S, s.st, s.pad, s.pad);
+    launch_tap(st, t, x, wrsc, y, stats, shift, RowMap{}, ws, ws_floats);
+    return;
+  }
   launch_fd<FWD>(st, g, x, wrsc, nullptr, y, stats, shift, ws, ws_floats);
 }
 
 // dX[N,H,W,C] = conv_transpose(dY[N,P,Q,O], W_rsc)   (every element written).
 // Stride 2 runs as 4 sub-pixel phases so no MFMA multiplies a structural zero.
 void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const bf16* wrsc, bf16* dx, float* ws,
-                       long ws_floats) {
+                       long ws_floats, const bf16* wd) {
   check_shape(s);
+  if (wd != nullptr && s.O % 64 == 0) {   // tap-major path on the dgrad weight image
+    TapPhase ph[4];
+    const int n = dgrad_tap_phases(s, ph);
+    for (int i = 0; i < n; ++i) {
+      if (ph[i].empty) {   // zero this parity's rows with the generic kernel (K = 0)
+        ConvGeom q = make_geom(s);
+        q.NC = s.C; q.ph = ph[i].ph; q.pw = ph[i].pw; q.r0 = ph[i].r0; q.s0 = ph[i].s0; q.nr = 0; q.ns = 0;
+        q.Hp = ph[i].g.P; q.Wp = ph[i].g.Q;
+        q.dNS = make_div(1); q.dWp = make_div(q.Wp); q.dHWp = make_div(q.Hp * q.Wp);
+        q.M = s.N * q.Hp * q.Wp; q.K = 0;
+        launch_mode<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, 1);
+        continue;
+      }
+      launch_tap(st, ph[i].g, dy, wd + ph[i].img_off, dx, nullptr, nullptr, ph[i].rm, ws, ws_floats);
+    }
+    return;
+  }
   ConvGeom g = make_geom(s);
   g.NC = s.C;
   if (s.st == 1) {
@@ -711,6 +1105,20 @@ long conv_fd_ws_floats(const ConvShape& s) {
   const long cap = 1l << 40;
   int sp = fd_splits(g, cap);
   if (sp > 1) need = std::max(need, (long)sp * g.M * g.NC);
+  if (s.C % 64 == 0) {
+    const TapGeom t = make_tap(s.N, s.H, s.W, s.C, s.O, s.P, s.Q, s.R, s.S, s.st, s.pad, s.pad);
+    const int tsp = tap_splits(t, cap);
+    if (tsp > 1) need = std::max(need, (long)tsp * t.M * t.O);
+  }
+  if (s.O % 64 == 0) {
+    TapPhase ph[4];
+    const int n = dgrad_tap_phases(s, ph);
+    for (int i = 0; i < n; ++i) {
+      if (ph[i].empty) continue;
+      const int tsp = tap_splits(ph[i].g, cap);
+      if (tsp > 1) need = std::max(need, (long)tsp * ph[i].g.M * ph[i].g.O);
+    }
+  }
   ConvGeom d = make_geom(s);
   d.NC = s.C;
   if (s.st == 1) {
@@ -782,6 +1190,45 @@ void launch_conv_pack_multi(hipStream_t st, const PackItem* items, int n) {
       rows += it.O;
     }
     hipLaunchKernelGGL(conv_pack_multi_kernel, dim3(rows), dim3(256), 0, st, t);
+  }
+}
+
+// DGRAD weight images (conv_tap layout, phases concatenated) for several convs, one launch per <= MAX_DPACK phases.
+struct DPackItem {
+  const float* w;
+  bf16* wd;
+  int O, Cw, C, R, S, st, pad;
+};
+
+void launch_dgrad_pack_multi(hipStream_t st, const DPackItem* items, int n) {
+  std::vector<DPackEntry> all;
+  for (int k = 0; k < n; ++k) {
+    const DPackItem& it = items[k];
+    if (it.R * it.S > 49 || it.C % 8 || it.C < it.Cw) throw std::invalid_argument("dgrad_pack: unsupported shape");
+    ConvShape s{};
+    s.N = 1; s.H = 8; s.W = 8; s.P = 4; s.Q = 4;   // spatial sizes only gate empty phases here
+    s.C = it.C; s.Cw = it.Cw; s.O = it.O; s.R = it.R; s.S = it.S; s.st = it.st; s.pad = it.pad;
+    TapPhase ph[4];
+    const int np = dgrad_tap_phases(s, ph);
+    for (int i = 0; i < np; ++i) {
+      if (ph[i].empty) continue;
+      DPackEntry e{};
+      e.w = it.w; e.wd = it.wd + ph[i].img_off;
+      e.O = it.O; e.Cw = it.Cw; e.Cpad = it.C; e.R = it.R; e.S = it.S;
+      e.r0 = ph[i].r0; e.s0 = ph[i].s0; e.nr = ph[i].nr; e.ns = ph[i].ns; e.step = it.st;
+      all.push_back(e);
+    }
+  }
+  for (size_t b = 0; b < all.size(); b += MAX_DPACK) {
+    DPackTable t{};
+    t.n = (int)std::min<size_t>(MAX_DPACK, all.size() - b);
+    int blk = 0;
+    for (int k = 0; k < t.n; ++k) {
+      t.e[k] = all[b + k];
+      t.e[k].blk0 = blk;
+      blk += ((t.e[k].O + 63) / 64) * ((t.e[k].Cpad + 3) / 4);
+    }
+    hipLaunchKernelGGL(dgrad_pack_kernel, dim3(blk), dim3(256), 0, st, t);
   }
 }
 

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x,
     const int grp = c >> 3, j = c & 7;
     float sum = 0.f;
     for (int t = grp; t < (int)blockDim.x; t += VC) sum += red[qn][t][j];
-    unsafeAtomicAdd(stats + qn * g.C + c, sum);
+    unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + qn) * g.C + c, sum);
   }
 }
 

@@ -71,6 +71,9 @@ class _Unit:
         bf = dict(dtype=act_dtype, device=dev)
         self.wr = None if self.depthwise else torch.empty(self.O, self.R, self.S, self.C, dtype=torch.bfloat16,
                                                           device=dev)
+        # flipped/transposed weight image for the tap-major DGRAD kernel (O % 64 == 0)
+        self.wd = (torch.empty(conv.dgrad_image_numel(c.weight.shape, self.C), dtype=torch.bfloat16, device=dev)
+                   if not self.depthwise and conv.dgrad_eligible(self.O) else None)
         self.z = torch.empty(n_out, **bf)                            # conv output (pre-BN)
         self.y = torch.empty(n_out, **bf) if need_y else None        # BN(+ReLU) output inside a block
         self.dz = torch.empty(n_out, **bf)                           # grad wrt z
@@ -118,10 +121,14 @@ class _Unit:
         dz = self.view(self.dz, nb)
         if self.depthwise:
             return conv.dwconv_dgrad(dz, self.conv.weight, self.in_shape(nb), self.stride, self.pad, out=out)
-        return conv.conv2d_dgrad(dz, self.wr, self.in_shape(nb), self.stride, self.pad, Cw=self.Cw, out=out, ws=ws)
+        return conv.conv2d_dgrad(dz, self.wr, self.in_shape(nb), self.stride, self.pad, Cw=self.Cw, out=out, ws=ws,
+                                 wd=self.wd)
 
     def pack_item(self):
         return None if self.depthwise else (self.conv.weight.data, self.wr)
+
+    def dgrad_pack_item(self):
+        return None if self.wd is None else (self.conv.weight.data, self.wd, self.stride, self.pad, self.C)
 
 
 class _Block:
@@ -251,13 +258,13 @@ class CNNNativeTrainer(LocalTrainer):
         self.head_hw, self.head_c = last.out_hw, last.cout
         self.units: List[_Unit] = [u for b in self.blocks for u in b.units()]
         # per-step accumulators: BN batch stats [2][O] and BN-backward sums [3][O], one fill each
-        self.stats_all = torch.zeros(sum(2 * u.O for u in self.units), device=device)
+        self.stats_all = torch.zeros(sum(conv.STAT_REP * 2 * u.O for u in self.units), device=device)
         self.red_all = torch.zeros(sum(3 * u.O for u in self.units), device=device)
         so = ro = 0
         for u in self.units:
-            u.stats = self.stats_all[so:so + 2 * u.O].view(2, u.O)
+            u.stats = self.stats_all[so:so + conv.STAT_REP * 2 * u.O].view(conv.STAT_REP, 2, u.O)
             u.red = self.red_all[ro:ro + 3 * u.O].view(3, u.O)
-            so += 2 * u.O
+            so += conv.STAT_REP * 2 * u.O
             ro += 3 * u.O
         B = cfg.batch_size
         # one fp32 split-K workspace for every conv launch of a step (fwd / dgrad / wgrad)
@@ -314,6 +321,10 @@ class CNNNativeTrainer(LocalTrainer):
 
     def pack(self) -> None:
         conv.pack_weights([it for it in (u.pack_item() for u in self.units) if it is not None])
+        # the network input block never needs a data gradient: skip its image
+        first = set(id(u) for u in self.blocks[0].units()) if self.blocks[0].first else set()
+        conv.dgrad_pack_weights([it for u in self.units if id(u) not in first
+                                 for it in [u.dgrad_pack_item()] if it is not None])
 
     # ---- data ----------------------------------------------------------------------------
     def set_schedule(self, starts, sizes) -> None:

@@ -26,7 +26,12 @@ def _load():
         variant = os.environ.get("FEDMI_NATIVE_VARIANT", "")
         name = "fedmi._fedmi_native" + (f"_{variant}" if variant else "")
         try:
-            _mod = importlib.import_module(name)
+            mod = importlib.import_module(name)
+            from .ops.conv import STAT_REP
+
+            if getattr(mod, "STAT_REP", STAT_REP) != STAT_REP:
+                raise ImportError(f"{name}: STAT_REP {mod.STAT_REP} != fedmi.ops.conv.STAT_REP {STAT_REP}")
+            _mod = mod
         except Exception as e:  # pragma: no cover - depends on build state
             _err = e
 

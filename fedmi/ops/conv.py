@@ -19,6 +19,26 @@ import torch
 from .. import native
 
 
+# BatchNorm statistics buffers are [STAT_REP, 2, C] fp32 replicas (csrc/kernels/common.h STAT_REP): the
+# conv / depthwise epilogues add into replica (workgroup % STAT_REP), bn_apply sums them.
+STAT_REP = 16
+
+
+def stats_buffer(C: int, device) -> torch.Tensor:
+    return torch.zeros(STAT_REP, 2, C, dtype=torch.float32, device=device)
+
+
+def stats_total(stats: torch.Tensor) -> torch.Tensor:
+    """[2, C] totals (sum, sum of squares) of a replicated statistics buffer."""
+    return stats.view(STAT_REP, 2, -1).sum(0)
+
+
+def _check_stats(stats: Optional[torch.Tensor], C: int, who: str) -> None:
+    if stats is not None and (stats.numel() != STAT_REP * 2 * C or stats.dtype != torch.float32
+                              or not stats.is_contiguous()):
+        raise ValueError(f"{who}: stats must be contiguous fp32 [STAT_REP={STAT_REP}, 2, {C}]")
+
+
 def pad8(c: int) -> int:
     return (c + 7) // 8 * 8
 
@@ -82,8 +102,8 @@ def _ws_args(ws: Optional[torch.Tensor]):
 def conv2d_fwd(x: torch.Tensor, wrsc: torch.Tensor, stride: int, pad: int, Cw: Optional[int] = None,
                stats: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
                shift: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y[N,P,Q,O] = conv(x[N,H,W,C]); ``stats`` ([2, O] fp32) += per-channel sum / sum of squares of
-    (y - shift) (``shift``: [O] fp32 or None = 0).  ``ws`` (fp32): optional split-K workspace for
+    """y[N,P,Q,O] = conv(x[N,H,W,C]); ``stats`` ([STAT_REP, 2, O] fp32, :func:`stats_buffer`) +=
+    per-channel sum / sum of squares of (y - shift) (``shift``: [O] fp32 or None = 0).  ``ws`` (fp32): optional split-K workspace for
     deep-K / few-tile shapes (see :func:`fd_ws_floats`)."""
     _check(x, torch.bfloat16, "conv2d_fwd.x")
     _check(wrsc, torch.bfloat16, "conv2d_fwd.w")
@@ -96,17 +116,45 @@ def conv2d_fwd(x: torch.Tensor, wrsc: torch.Tensor, stride: int, pad: int, Cw: O
         out = torch.empty(N, P, Q, O, dtype=torch.bfloat16, device=x.device)
     elif tuple(out.shape) != (N, P, Q, O):
         raise ValueError("conv2d_fwd: bad out shape")
-    if stats is not None and (stats.numel() != 2 * O or stats.dtype != torch.float32):
-        raise ValueError("conv2d_fwd: stats must be [2, O] fp32")
+    _check_stats(stats, O, "conv2d_fwd")
     native.require().conv_fwd(native.stream_handle(x.device), shp, x.data_ptr(), wrsc.data_ptr(), out.data_ptr(),
                               stats.data_ptr() if stats is not None else 0,
                               shift.data_ptr() if shift is not None else 0, *_ws_args(ws))
     return out
 
 
+def dgrad_image_numel(w_shape, c_pad: Optional[int] = None) -> int:
+    O, Cw, R, S = (int(v) for v in w_shape)
+    return O * R * S * (c_pad or pad8(Cw))
+
+
+def dgrad_eligible(O: int) -> bool:
+    """The tap-major DGRAD reads dY as its input operand: needs O % 64 == 0."""
+    return O % 64 == 0
+
+
+def dgrad_pack_weights(items) -> None:
+    """DGRAD weight images for the tap-major kernel: ``(w fp32 [O,Cw,R,S], img bf16, stride, pad, c_pad)``
+    per conv (the image is the flipped/transposed weight, one block per sub-pixel phase), one launch."""
+    items = list(items)
+    if not items:
+        return
+    rows = []
+    for w, img, stride, pad, c_pad in items:
+        _check(w, torch.float32, "dgrad_pack_weights.w")
+        _check(img, torch.bfloat16, "dgrad_pack_weights.img")
+        O, Cw, R, S = w.shape
+        if img.numel() < dgrad_image_numel(w.shape, c_pad) or not dgrad_eligible(O):
+            raise ValueError("dgrad_pack_weights: image too small or O % 64 != 0")
+        rows.append((w.data_ptr(), img.data_ptr(), O, Cw, c_pad, R, S, int(stride), int(pad)))
+    native.require().dgrad_pack_multi(native.stream_handle(items[0][0].device), rows)
+
+
 def conv2d_dgrad(dy: torch.Tensor, wrsc: torch.Tensor, x_shape, stride: int, pad: int, Cw: Optional[int] = None,
-                 out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dx[N,H,W,C] from dy[N,P,Q,O]."""
+                 out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
+                 wd: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx[N,H,W,C] from dy[N,P,Q,O].  ``wd``: the conv's DGRAD weight image (:func:`dgrad_pack_weights`)
+    selects the tap-major LDS-DMA kernel (O % 64 == 0); without it the generic implicit GEMM runs."""
     _check(dy, torch.bfloat16, "conv2d_dgrad.dy")
     O, R, S, C = wrsc.shape
     shp = shape_tuple(x_shape, O, R, S, stride, pad, Cw)
@@ -114,8 +162,12 @@ def conv2d_dgrad(dy: torch.Tensor, wrsc: torch.Tensor, x_shape, stride: int, pad
         raise ValueError(f"conv2d_dgrad: dy shape {tuple(dy.shape)} vs expected {(shp[0], shp[6], shp[7], O)}")
     if out is None:
         out = torch.empty(*x_shape, dtype=torch.bfloat16, device=dy.device)
+    if wd is not None:
+        _check(wd, torch.bfloat16, "conv2d_dgrad.wd")
+        if wd.numel() < O * R * S * C:
+            raise ValueError("conv2d_dgrad: dgrad image too small")
     native.require().conv_dgrad(native.stream_handle(dy.device), shp, dy.data_ptr(), wrsc.data_ptr(), out.data_ptr(),
-                                *_ws_args(ws))
+                                *_ws_args(ws), wd.data_ptr() if wd is not None else 0)
     return out
 
 
@@ -185,6 +237,7 @@ def dwconv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats: O
     if one != 1 or C != x.shape[3] or R != S:
         raise ValueError("dwconv_fwd: weight must be [C, 1, R, R]")
     shp = _dw_shape(x.shape, R, stride, pad)
+    _check_stats(stats, C, "dwconv_fwd")
     P, Q = out_hw(shp[1], shp[2], R, R, stride, pad)
     if out is None:
         out = torch.empty(shp[0], P, Q, C, dtype=torch.bfloat16, device=x.device)

@@ -59,6 +59,10 @@ def fd_ws_floats(*a, **k):
     return 0
 
 
+def dgrad_pack_weights(items):
+    pass
+
+
 def _w_from_img(wr: torch.Tensor, Cw: Optional[int]) -> torch.Tensor:
     m = _MASTER.get(wr.data_ptr())
     w = m.float() if m is not None and m.shape[2:] == wr.shape[1:3] else wr.permute(0, 3, 1, 2).float()
@@ -70,8 +74,9 @@ def _stats_add(stats, y_bf16_nhwc, shift=None):
         v = y_bf16_nhwc.float().reshape(-1, y_bf16_nhwc.shape[-1])
         if shift is not None:
             v = v - shift
-        stats.view(2, -1)[0] += v.sum(0)
-        stats.view(2, -1)[1] += (v * v).sum(0)
+        rep0 = stats.view(conv.STAT_REP, 2, -1)[0]     # replica 0 (the native kernels spread over all)
+        rep0[0] += v.sum(0)
+        rep0[1] += (v * v).sum(0)
 
 
 @torch.no_grad()
@@ -86,7 +91,7 @@ def conv2d_fwd(x, wrsc, stride, pad, Cw=None, stats=None, out=None, shift=None, 
 
 
 @torch.no_grad()
-def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None, ws=None):
+def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None, ws=None, wd=None):
     N, H, W, C = x_shape
     Cw = Cw or C
     dx = torch.nn.grad.conv2d_input((N, Cw, H, W), _w_from_img(wrsc, Cw), _nchw(dy), stride=stride, padding=pad)
@@ -177,8 +182,9 @@ def sched_next(sched, counter, cur):
 
 def _coeffs(p: "cnn.BNParams", M: int, train: bool, eps: float, mom: float):
     if train:
-        ms = p.stats.view(2, -1)[0] / M
-        var = torch.clamp(p.stats.view(2, -1)[1] / M - ms * ms, min=0.0)
+        tot = conv.stats_total(p.stats)
+        ms = tot[0] / M
+        var = torch.clamp(tot[1] / M - ms * ms, min=0.0)
         mean = ms + (p.shift if p.shift is not None else 0.0)
         inv = torch.rsqrt(var + eps)
         p.smean.copy_(mean)
@@ -283,7 +289,7 @@ def emulated():
         saved.append((mod, name, getattr(mod, name)))
         setattr(mod, name, fn)
 
-    for name in ("pack_weight", "pack_weights", "fd_ws_floats", "conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
+    for name in ("pack_weight", "pack_weights", "fd_ws_floats", "dgrad_pack_weights", "conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
                  "dwconv_dgrad", "dwconv_wgrad", "dwconv_ws_floats"):
         swap(conv, name, globals()[name])
     for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "bn_bwd_ws_floats", "head"):

@@ -46,8 +46,9 @@ def test_conv_fwd_and_stats(gpu_device, shape):
     N, H, W, Cw, O, R, st, pad = shape
     x, w, wb, xn = _make(shape, gpu_device)
     wr = conv.pack_weight(w)
-    stats = torch.zeros(2, O, device=gpu_device)
-    y = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=stats)
+    rep = conv.stats_buffer(O, gpu_device)
+    y = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=rep)
+    stats = conv.stats_total(rep)
     ref = F.conv2d(x, wb, stride=st, padding=pad)
     torch.cuda.synchronize()
     assert _rel(y.float(), _nhwc(ref)) < 1e-2
@@ -74,6 +75,38 @@ def test_conv_dgrad_wgrad(gpu_device, shape):
     if Cw < dx.shape[-1]:   # padded input channels see zero weights
         assert float(dx[..., Cw:].float().abs().max()) == 0.0
     assert _rel(dw, wr_.grad) < 1e-2
+    if conv.dgrad_eligible(O):   # tap-major DGRAD on the flipped weight image, every sub-pixel phase
+        wd = torch.full((conv.dgrad_image_numel(w.shape, xn.shape[-1]),), float("nan"), dtype=torch.bfloat16,
+                        device=gpu_device)
+        conv.dgrad_pack_weights([(w, wd, st, pad, xn.shape[-1])])
+        dx2 = torch.full_like(dx, float("nan"))
+        conv.conv2d_dgrad(dyn, wpk, xn.shape, st, pad, Cw=Cw, out=dx2, wd=wd)
+        torch.cuda.synchronize()
+        assert _rel(dx2[..., :Cw].float(), _nhwc(xr.grad)) < 1e-2
+        assert _rel(dx2.float(), dx.float()) < 1e-2
+
+
+def test_dgrad_tap_edge_shapes(gpu_device):
+    # partial M tiles, 1x1 stride-2 (empty parity phases), 5x5 stride 2, odd spatial
+    for shape in [(3, 7, 5, 24, 64, 3, 1, 1), (4, 9, 9, 64, 128, 1, 2, 0), (2, 9, 11, 16, 64, 5, 2, 2),
+                  (5, 6, 6, 128, 64, 3, 2, 1)]:
+        N, H, W, Cw, O, R, st, pad = shape
+        x, w, wb, xn = _make(shape, gpu_device, seed=9)
+        xr = x.clone().requires_grad_(True)
+        out = F.conv2d(xr, wb, stride=st, padding=pad)
+        gy = torch.randn_like(out).bfloat16().float()
+        out.backward(gy)
+        dyn = _nhwc(gy).bfloat16()
+        C = xn.shape[-1]
+        wd = torch.empty(conv.dgrad_image_numel(w.shape, C), dtype=torch.bfloat16, device=gpu_device)
+        conv.dgrad_pack_weights([(w, wd, st, pad, C)])
+        dx = torch.full_like(xn, float("nan"))
+        conv.conv2d_dgrad(dyn, conv.pack_weight(w), xn.shape, st, pad, Cw=Cw, out=dx, wd=wd)
+        torch.cuda.synchronize()
+        assert not torch.isnan(dx.float()).any(), shape
+        assert _rel(dx[..., :Cw].float(), _nhwc(xr.grad)) < 1e-2, shape
+        if Cw < C:
+            assert float(dx[..., Cw:].float().abs().max()) == 0.0
 
 
 def test_conv_wgrad_split_invariance(gpu_device):
@@ -100,8 +133,11 @@ def test_bn_forward_backward_with_projection_residual(gpu_device):
     zb = (torch.randn(M, C, device=dev) - 0.3).bfloat16()
     ga, ba = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
     gb, bb = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
-    sa = torch.stack([za.float().sum(0), (za.float() ** 2).sum(0)])
-    sb = torch.stack([zb.float().sum(0), (zb.float() ** 2).sum(0)])
+    # replicated statistics buffers: the totals spread unevenly over the STAT_REP replicas
+    wrep = torch.arange(1, conv.STAT_REP + 1, device=dev, dtype=torch.float32)
+    wrep = (wrep / wrep.sum()).view(-1, 1, 1)
+    sa = (torch.stack([za.float().sum(0), (za.float() ** 2).sum(0)]) * wrep).contiguous()
+    sb = (torch.stack([zb.float().sum(0), (zb.float() ** 2).sum(0)]) * wrep).contiguous()
     rma, rva, rmb, rvb = (torch.zeros(C, device=dev), torch.ones(C, device=dev),
                           torch.zeros(C, device=dev), torch.ones(C, device=dev))
     nbt = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -228,8 +264,9 @@ def test_depthwise_fwd_dgrad_wgrad(gpu_device, shape):
     wref = F.conv2d(x.detach(), wb, stride=st, padding=pad, groups=C)
     wref.backward(gy)
     xn = _nhwc(x.detach()).bfloat16()
-    stats = torch.zeros(2, C, device=dev)
-    y = conv.dwconv_fwd(xn, w, st, pad, stats=stats)
+    rep = conv.stats_buffer(C, dev)
+    y = conv.dwconv_fwd(xn, w, st, pad, stats=rep)
+    stats = conv.stats_total(rep)
     dx = conv.dwconv_dgrad(_nhwc(gy).bfloat16(), w, xn.shape, st, pad)
     dw = conv.dwconv_wgrad(xn, _nhwc(gy).bfloat16(), R, st, pad)
     torch.cuda.synchronize()
@@ -257,10 +294,10 @@ def test_conv_splitk_fwd_dgrad(gpu_device, shape):
     assert need > 0, "shape expected to take the split-K path"
     ws = torch.full((need,), float("nan"), device=gpu_device)   # every partial must be written
     shift = torch.randn(O, device=gpu_device) * 0.1
-    s_split = torch.zeros(2, O, device=gpu_device)
-    s_one = torch.zeros(2, O, device=gpu_device)
-    y = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=s_split, shift=shift, ws=ws)
-    y1 = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=s_one, shift=shift)
+    r_split, r_one = conv.stats_buffer(O, gpu_device), conv.stats_buffer(O, gpu_device)
+    y = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=r_split, shift=shift, ws=ws)
+    y1 = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=r_one, shift=shift)
+    s_split = conv.stats_total(r_split)
     ref = F.conv2d(x, wb, stride=st, padding=pad)
     torch.cuda.synchronize()
     assert _rel(y.float(), _nhwc(ref)) < 1e-2
@@ -278,6 +315,12 @@ def test_conv_splitk_fwd_dgrad(gpu_device, shape):
     dx = conv.conv2d_dgrad(dyn, wr, xn.shape, st, pad, Cw=Cw, ws=ws)
     torch.cuda.synchronize()
     assert _rel(dx.float(), _nhwc(xr.grad)) < 1e-2
+    wd = torch.empty(conv.dgrad_image_numel(w.shape, xn.shape[-1]), dtype=torch.bfloat16, device=gpu_device)
+    conv.dgrad_pack_weights([(w, wd, st, pad, xn.shape[-1])])
+    ws.fill_(float("nan"))
+    dx2 = conv.conv2d_dgrad(dyn, wr, xn.shape, st, pad, Cw=Cw, ws=ws, wd=wd)
+    torch.cuda.synchronize()
+    assert _rel(dx2.float(), _nhwc(xr.grad)) < 1e-2
 
 
 def test_conv_wgrad_many_splits_and_padded_channels(gpu_device):

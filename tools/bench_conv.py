@@ -54,7 +54,7 @@ def main():
         wr = conv.pack_weight(w)
         P = (H + 2 * pad - k) // st + 1
         dy = torch.randn(N, P, P, Co, device=dev).bfloat16()
-        stats = torch.zeros(2, Co, device=dev)
+        stats = conv.stats_buffer(Co, dev)
         y = torch.empty(N, P, P, Co, dtype=torch.bfloat16, device=dev)
         dx = torch.empty_like(x)
         dw = torch.zeros(Co, Ci, k, k, device=dev)

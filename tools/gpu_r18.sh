@@ -9,3 +9,4 @@ timeout -k 10 300 python bench.py --model resnet18 --steps 2 --warmup 1 > gpurun
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r18 -o run --output-format csv -- python bench.py --model resnet18 --steps 1 --warmup 1 > gpurun_out/prof_r18.log 2>&1 || exit $?
 echo done >> gpurun_out/r18_summary.txt
+timeout -k 10 120 python tools/bench_tap.py --iters 30 > gpurun_out/bench_tap.log 2>&1 || exit $?
