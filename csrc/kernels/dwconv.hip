@@ -60,25 +60,44 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x,
   float sh[8];   // statistics are of (y - shift): see conv_igemm's epilogue
 #pragma unroll
   for (int j = 0; j < 8; ++j) sh[j] = shift ? shift[c0 + j] : 0.f;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long pix = i / VC;
-    const int q = pix % g.Q;
-    const long t2 = pix / g.Q;
-    const int p = t2 % g.P, n = t2 / g.P;
+  // 32-bit index math (host guarantees < 2^31 elements): 64-bit div/mod are software loops
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)total; i += gridDim.x * blockDim.x) {
+    const uint32_t pix = i / (uint32_t)VC;
+    const uint32_t t2 = pix / (uint32_t)g.Q;
+    const int q = (int)(pix - t2 * g.Q);
+    const int n = (int)(t2 / (uint32_t)g.P), p = (int)(t2 - (uint32_t)n * g.P);
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    for (int r = 0; r < g.R; ++r) {
-      const int h = p * g.st - g.pad + r;
-      if ((unsigned)h >= (unsigned)g.H) continue;
-      for (int s = 0; s < g.S; ++s) {
-        const int ww = q * g.st - g.pad + s;
-        if ((unsigned)ww >= (unsigned)g.W) continue;
-        float v[8];
-        ld8f(x + (((long)n * g.H + h) * g.W + ww) * g.C + c0, v);
-        const float* wt = wl + (r * g.S + s) * g.C + c0;
+    const long nb = (long)n * g.H;
+    if (g.R == 3) {   // the MobileNet case: 9 independent 16-B loads in flight
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += v[j] * wt[j];
+      for (int r = 0; r < 3; ++r) {
+        const int h = p * g.st - g.pad + r;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const int ww = q * g.st - g.pad + s;
+          const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+          float v[8];
+          ld8f(x + (ok ? ((nb + h) * g.W + ww) * g.C + c0 : c0), v);
+          const float* wt = wl + (r * 3 + s) * g.C + c0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += ok ? v[j] * wt[j] : 0.f;
+        }
+      }
+    } else {
+      for (int r = 0; r < g.R; ++r) {
+        const int h = p * g.st - g.pad + r;
+        if ((unsigned)h >= (unsigned)g.H) continue;
+        for (int s = 0; s < g.S; ++s) {
+          const int ww = q * g.st - g.pad + s;
+          if ((unsigned)ww >= (unsigned)g.W) continue;
+          float v[8];
+          ld8f(x + ((nb + h) * g.W + ww) * g.C + c0, v);
+          const float* wt = wl + (r * g.S + s) * g.C + c0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += v[j] * wt[j];
+        }
       }
     }
     bf16x8v o;
@@ -89,7 +108,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x,
       s1[j] += vb;
       s2[j] += vb * vb;
     }
-    *reinterpret_cast<bf16x8v*>(y + pix * g.C + c0) = o;
+    *reinterpret_cast<bf16x8v*>(y + (long)pix * g.C + c0) = o;
   }
   if (stats == nullptr) return;
 #pragma unroll
@@ -112,36 +131,54 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16* __restrict__ 
   stage_taps(w, wl, g.C, g.R * g.S);
   __syncthreads();
   const long total = (long)g.N * g.H * g.W * VC;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % VC) * 8;
-    const long pix = i / VC;
-    const int wq = pix % g.W;
-    const long t2 = pix / g.W;
-    const int h = t2 % g.H, n = t2 / g.H;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)total; i += gridDim.x * blockDim.x) {
+    const uint32_t pix = i / (uint32_t)VC;
+    const int c0 = (int)(i - pix * VC) * 8;
+    const uint32_t t2 = pix / (uint32_t)g.W;
+    const int wq = (int)(pix - t2 * g.W);
+    const int n = (int)(t2 / (uint32_t)g.H), h = (int)(t2 - (uint32_t)n * g.H);
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    for (int r = 0; r < g.R; ++r) {
-      int y = h + g.pad - r;
-      if (y < 0 || y % g.st) continue;
-      y /= g.st;
-      if (y >= g.P) continue;
-      for (int s = 0; s < g.S; ++s) {
-        int xx = wq + g.pad - s;
-        if (xx < 0 || xx % g.st) continue;
-        xx /= g.st;
-        if (xx >= g.Q) continue;
-        float v[8];
-        ld8f(dy + (((long)n * g.P + y) * g.Q + xx) * g.C + c0, v);
-        const float* wt = wl + (r * g.S + s) * g.C + c0;
+    const long nb = (long)n * g.P;
+    if (g.R == 3 && g.st == 1) {   // unrolled: all taps in flight
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += v[j] * wt[j];
+      for (int r = 0; r < 3; ++r) {
+        const int y = h + g.pad - r;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const int xx = wq + g.pad - s;
+          const bool ok = (unsigned)y < (unsigned)g.P && (unsigned)xx < (unsigned)g.Q;
+          float v[8];
+          ld8f(dy + (ok ? ((nb + y) * g.Q + xx) * g.C + c0 : c0), v);
+          const float* wt = wl + (r * 3 + s) * g.C + c0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += ok ? v[j] * wt[j] : 0.f;
+        }
+      }
+    } else {
+      for (int r = 0; r < g.R; ++r) {
+        int y = h + g.pad - r;
+        if (y < 0 || y % g.st) continue;
+        y /= g.st;
+        if (y >= g.P) continue;
+        for (int s = 0; s < g.S; ++s) {
+          int xx = wq + g.pad - s;
+          if (xx < 0 || xx % g.st) continue;
+          xx /= g.st;
+          if (xx >= g.Q) continue;
+          float v[8];
+          ld8f(dy + ((nb + y) * g.Q + xx) * g.C + c0, v);
+          const float* wt = wl + (r * g.S + s) * g.C + c0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += v[j] * wt[j];
+        }
       }
     }
     bf16x8v o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = (bf16)acc[j];
-    *reinterpret_cast<bf16x8v*>(dx + pix * g.C + c0) = o;
+    *reinterpret_cast<bf16x8v*>(dx + (long)pix * g.C + c0) = o;
   }
 }
 
@@ -160,12 +197,12 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16* __restrict__ 
   for (int t = 0; t < RS; ++t)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[t][j] = 0.f;
-  for (long pix = pb + lane_pix; pix < pe; pix += pstep) {
-    const int q = pix % g.Q;
-    const long t2 = pix / g.Q;
-    const int p = t2 % g.P, n = t2 / g.P;
+  for (uint32_t pix = (uint32_t)(pb + lane_pix); pix < (uint32_t)pe; pix += pstep) {
+    const uint32_t t2 = pix / (uint32_t)g.Q;
+    const int q = (int)(pix - t2 * g.Q);
+    const int n = (int)(t2 / (uint32_t)g.P), p = (int)(t2 - (uint32_t)n * g.P);
     float d[8];
-    ld8f(dy + pix * g.C + c0, d);
+    ld8f(dy + (long)pix * g.C + c0, d);
 #pragma unroll
     for (int t = 0; t < RS; ++t) {
       const int r = t / g.S, s = t - r * g.S;
@@ -195,12 +232,31 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16* __restrict__ 
   }
 }
 
+// dw[i] (+)= sum_b ws[b][i]: block = 16 outputs x 16 partial groups (each thread
+// sums nblk/16 partials, 4 loads in flight), fixed-order LDS combine.
 __global__ __launch_bounds__(256) void dw_wgrad_reduce(const float* __restrict__ ws, int nblk, int n,
                                                        float* __restrict__ dw, int accumulate) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    float v = accumulate ? dw[i] : 0.f;
-    for (int b = 0; b < nblk; ++b) v += ws[(long)b * n + i];
-    dw[i] = v;
+  __shared__ float part[16][17];
+  const int col = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + col;
+  float a = 0.f, b = 0.f, c = 0.f, d = 0.f;
+  if (i < n) {
+    int k = grp;
+    for (; k + 48 < nblk; k += 64) {
+      a += ws[(long)k * n + i];
+      b += ws[(long)(k + 16) * n + i];
+      c += ws[(long)(k + 32) * n + i];
+      d += ws[(long)(k + 48) * n + i];
+    }
+    for (; k < nblk; k += 16) a += ws[(long)k * n + i];
+  }
+  part[grp][col] = (a + b) + (c + d);
+  __syncthreads();
+  if (threadIdx.x < 16 && i < n) {
+    float v = 0.f;
+#pragma unroll
+    for (int g2 = 0; g2 < 16; ++g2) v += part[g2][col];
+    dw[i] = accumulate ? dw[i] + v : v;
   }
 }
 
@@ -221,6 +277,7 @@ static DwGeom dw_geom(const DwShape& s) {
   if (s.C % 8 || s.C / 8 > 256) throw std::invalid_argument("dwconv: need C % 8 == 0 and C <= 2048");
   if (s.R != s.S || (s.R != 3 && s.R != 5 && s.R != 7)) throw std::invalid_argument("dwconv: square 3/5/7 kernels");
   if ((long)s.C * s.R * s.S * 4 > 128 * 1024) throw std::invalid_argument("dwconv: filter image exceeds LDS");
+  if ((long)s.N * s.H * s.W * s.C >= (1l << 31)) throw std::invalid_argument("dwconv: tensor too large for 32-bit indexing");
   DwGeom g{s.N, s.H, s.W, s.C, (s.H + 2 * s.pad - s.R) / s.st + 1, (s.W + 2 * s.pad - s.S) / s.st + 1,
            s.R, s.S, s.st, s.pad};
   return g;
@@ -265,7 +322,7 @@ void launch_dw_wgrad(hipStream_t st, const DwShape& s, const bf16* x, const bf16
   if (g.R == 3) hipLaunchKernelGGL(dw_wgrad_kernel<9>, dim3(nblk), dim3(tb), 0, st, x, dy, ws, g, ppb);
   else if (g.R == 5) hipLaunchKernelGGL(dw_wgrad_kernel<25>, dim3(nblk), dim3(tb), 0, st, x, dy, ws, g, ppb);
   else hipLaunchKernelGGL(dw_wgrad_kernel<49>, dim3(nblk), dim3(tb), 0, st, x, dy, ws, g, ppb);
-  hipLaunchKernelGGL(dw_wgrad_reduce, dim3(blocks_for(n)), dim3(256), 0, st, ws, nblk, n, dw, accumulate);
+  hipLaunchKernelGGL(dw_wgrad_reduce, dim3((n + 15) / 16), dim3(256), 0, st, ws, nblk, n, dw, accumulate);
 }
 
 }  // namespace fedmi
