@@ -88,10 +88,16 @@ def main() -> int:
     if not torch.cuda.is_available():
         print("[bench] no GPU visible", file=sys.stderr)
         return 2
-    device = torch.device("cuda", local_rank)
+    # FEDMI_BENCH_REHEARSE=1: rehearse the N-rank code path on ONE GPU (every rank on cuda:0,
+    # gloo collectives) -- the multi-GPU run itself uses one GPU per rank and RCCL over xGMI
+    rehearse = os.environ.get("FEDMI_BENCH_REHEARSE", "0") == "1"
+    device = torch.device("cuda", 0 if rehearse else local_rank)
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        if rehearse:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
 
     from fedmi.ckpt import AsyncCheckpointWriter, OPTIMIZED_MODEL, client_ckpt_path, mount_dir
     from fedmi.engine import build_trainer
@@ -134,7 +140,10 @@ def main() -> int:
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local_rank])
+            if rehearse:
+                dist.barrier()
+            else:
+                dist.barrier(device_ids=[local_rank])
         torch.cuda.synchronize(device)
 
     for r in range(args.warmup):
