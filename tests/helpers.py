@@ -29,11 +29,12 @@ def small_trainer(model="mlp", n_train=512, n_test=256, seed=0, lr=0.05):
     return build_trainer(model, data, torch.device("cpu"), TrainerConfig(lr=lr, seed=seed, eval_batch_size=256))
 
 
-def spawn_client(address: str, root: Path, *extra: str, log_path: Path | None = None) -> subprocess.Popen:
+def spawn_client(address: str, root: Path, *extra: str, log_path: Path | None = None,
+                 device: str = "cpu") -> subprocess.Popen:
     env = dict(os.environ)
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     env["OMP_NUM_THREADS"] = "1"
-    cmd = [sys.executable, "-m", "fedmi.cli.client", "-a", address, "--device", "cpu", "--root", str(root),
+    cmd = [sys.executable, "-m", "fedmi.cli.client", "-a", address, "--device", device, "--root", str(root),
            "--quiet", *extra]
     out = open(log_path, "w") if log_path else subprocess.DEVNULL
     return subprocess.Popen(cmd, env=env, cwd=str(root), stdout=out, stderr=subprocess.STDOUT,
