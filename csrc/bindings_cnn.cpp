@@ -40,8 +40,10 @@ void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int);
 
 struct BNDesc {
   const float* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
-  float* smean; float* sinv; const float* shift;
+  float* smean; float* sinv; const float* shift; const float* cbias;
 };
+void launch_maxpool2(hipStream_t, const bf16*, bf16*, int, int, int, int);
+void launch_maxpool2_bwd(hipStream_t, const bf16*, const bf16*, bf16*, int, int, int, int);
 struct BNBwdDesc {
   const bf16* dya; const bf16* dyb; const bf16* y;
   const bf16* za; const float* meanA; const float* invA; const float* gammaA; float* dgammaA; float* dbetaA; bf16* dza;
@@ -101,7 +103,8 @@ DwShape dw_from(const py::tuple& t) {
 BNDesc bn_from(const py::dict& d) {
   return BNDesc{P<const float>(dget(d, "stats")), P<const float>(dget(d, "gamma")), P<const float>(dget(d, "beta")),
                 P<float>(dget(d, "rmean")),       P<float>(dget(d, "rvar")),        P<long long>(dget(d, "nbt")),
-                P<float>(dget(d, "smean")),       P<float>(dget(d, "sinv")),        P<const float>(dget(d, "shift"))};
+                P<float>(dget(d, "smean")),       P<float>(dget(d, "sinv")),        P<const float>(dget(d, "shift")),
+                P<const float>(dget(d, "cbias"))};
 }
 }  // namespace
 
@@ -178,6 +181,14 @@ void fedmi_bind_cnn(py::module_& m) {
     launch_prep_input(S(st), P<const uint8_t>(images), base, P<const int>(dbase), nb, augment, seed,
                       P<const int>(round_ctr), P<bf16>(out));
     check("prep_input");
+  });
+  m.def("maxpool2", [](uintptr_t st, uintptr_t x, uintptr_t y, int N, int H, int W, int C) {
+    launch_maxpool2(S(st), P<const bf16>(x), P<bf16>(y), N, H, W, C);
+    check("maxpool2");
+  });
+  m.def("maxpool2_bwd", [](uintptr_t st, uintptr_t x, uintptr_t dy, uintptr_t dx, int N, int H, int W, int C) {
+    launch_maxpool2_bwd(S(st), P<const bf16>(x), P<const bf16>(dy), P<bf16>(dx), N, H, W, C);
+    check("maxpool2_bwd");
   });
   m.def("sched_next", [](uintptr_t st, uintptr_t sched, uintptr_t counter, uintptr_t cur) {
     launch_sched_next(S(st), P<const int>(sched), P<int>(counter), P<int>(cur));

@@ -86,6 +86,8 @@ struct BNArgs {
   float* smean;           // saved batch mean / invstd for the backward
   float* sinv;
   const float* shift;     // the sums in ``stats`` are of (z - shift[c]) (null: 0)
+  const float* cbias;     // bias of the producing conv, NOT included in z (null: none):
+                          // BN(z + b) in train mode == BN(z); running_mean tracks mean(z) + b
 };
 
 // per-channel scale/shift into LDS; block 0 also commits the running stats
@@ -107,12 +109,12 @@ FEDMI_DEV void bn_coeffs(const BNArgs& a, int C, int M, float eps, float mom, in
         a.smean[c] = mean;
         a.sinv[c] = inv;
         if (a.rmean) {
-          a.rmean[c] = (1.f - mom) * a.rmean[c] + mom * mean;
+          a.rmean[c] = (1.f - mom) * a.rmean[c] + mom * (mean + (a.cbias ? a.cbias[c] : 0.f));
           a.rvar[c] = (1.f - mom) * a.rvar[c] + mom * var * ((float)M / (float)max(M - 1, 1));
         }
       }
     } else {
-      mean = a.rmean[c];
+      mean = a.rmean[c] - (a.cbias ? a.cbias[c] : 0.f);
       inv = rsqrtf(a.rvar[c] + eps);
     }
     sc[c] = a.gamma[c] * inv;
@@ -445,6 +447,69 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// MaxPool2d(2, 2) on NHWC bf16 (VGG, src/models/vgg.py:24-25): one thread per
+// (output pixel, 8 channels).  The backward recomputes the window argmax from
+// the saved input (first maximum in window order, as max_pool2d_with_indices)
+// instead of storing indices, and writes every input element (0 off-argmax).
+__global__ __launch_bounds__(256) void maxpool2_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N,
+                                                           int H, int W, int C) {
+  const int P = H >> 1, Q = W >> 1, VC = C >> 3;
+  const uint32_t total = (uint32_t)N * P * Q * VC;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t pix = i / VC;
+    const int c0 = (int)(i - pix * VC) * 8;
+    const uint32_t t = pix / Q;
+    const int q = (int)(pix - t * Q);
+    const int n = (int)(t / P), p = (int)(t - (uint32_t)n * P);
+    const bf16* b = x + (((long)n * H + 2 * p) * W + 2 * q) * C + c0;
+    const bf16x8v v0 = *reinterpret_cast<const bf16x8v*>(b);
+    const bf16x8v v1 = *reinterpret_cast<const bf16x8v*>(b + C);
+    const bf16x8v v2 = *reinterpret_cast<const bf16x8v*>(b + (long)W * C);
+    const bf16x8v v3 = *reinterpret_cast<const bf16x8v*>(b + (long)W * C + C);
+    bf16x8v o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      o[j] = (bf16)fmaxf(fmaxf((float)v0[j], (float)v1[j]), fmaxf((float)v2[j], (float)v3[j]));
+    *reinterpret_cast<bf16x8v*>(y + (long)pix * C + c0) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                           bf16* __restrict__ dx, int N, int H, int W, int C) {
+  const int P = H >> 1, Q = W >> 1, VC = C >> 3;
+  const uint32_t total = (uint32_t)N * P * Q * VC;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t pix = i / VC;
+    const int c0 = (int)(i - pix * VC) * 8;
+    const uint32_t t = pix / Q;
+    const int q = (int)(pix - t * Q);
+    const int n = (int)(t / P), p = (int)(t - (uint32_t)n * P);
+    const long o00 = (((long)n * H + 2 * p) * W + 2 * q) * C + c0;
+    const long offs[4] = {o00, o00 + C, o00 + (long)W * C, o00 + (long)W * C + C};
+    bf16x8v v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const bf16x8v*>(x + offs[k]);
+    const bf16x8v g = *reinterpret_cast<const bf16x8v*>(dy + (long)pix * C + c0);
+    int am[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float best = (float)v[0][j];
+      am[j] = 0;
+#pragma unroll
+      for (int k = 1; k < 4; ++k)
+        if ((float)v[k][j] > best) { best = (float)v[k][j]; am[j] = k; }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bf16x8v o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = am[j] == k ? g[j] : (bf16)0.f;
+      *reinterpret_cast<bf16x8v*>(dx + offs[k]) = o;
+    }
+  }
+}
+
 // cur[0] = sched[counter[0]++]  (first node of a captured training step)
 __global__ void sched_next_kernel(const int* __restrict__ sched, int* __restrict__ counter, int* __restrict__ cur) {
   if (threadIdx.x == 0) {
@@ -462,11 +527,23 @@ namespace fedmi {
 
 struct BNDesc {
   const float* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
-  float* smean; float* sinv; const float* shift;
+  float* smean; float* sinv; const float* shift; const float* cbias;
 };
 
 static BNArgs to_args(const BNDesc& d) {
-  return BNArgs{d.stats, d.gamma, d.beta, d.rmean, d.rvar, d.nbt, d.smean, d.sinv, d.shift};
+  return BNArgs{d.stats, d.gamma, d.beta, d.rmean, d.rvar, d.nbt, d.smean, d.sinv, d.shift, d.cbias};
+}
+
+void launch_maxpool2(hipStream_t st, const bf16* x, bf16* y, int N, int H, int W, int C) {
+  if (C % 8 || H % 2 || W % 2) throw std::invalid_argument("maxpool2: need C % 8 == 0 and even H, W");
+  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for((long)N * (H / 2) * (W / 2) * (C / 8))), dim3(256), 0, st, x,
+                     y, N, H, W, C);
+}
+
+void launch_maxpool2_bwd(hipStream_t st, const bf16* x, const bf16* dy, bf16* dx, int N, int H, int W, int C) {
+  if (C % 8 || H % 2 || W % 2) throw std::invalid_argument("maxpool2_bwd: need C % 8 == 0 and even H, W");
+  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for((long)N * (H / 2) * (W / 2) * (C / 8))), dim3(256), 0, st, x,
+                     dy, dx, N, H, W, C);
 }
 
 void launch_prep_input(hipStream_t st, const uint8_t* images, int base, const int* dbase, int nb, int augment,

@@ -40,6 +40,7 @@ from torch import nn
 from .. import native
 from ..models import build_model
 from ..models.zoo.mobile import DWSeparable, InvertedResidual, MobileNet, MobileNetV2
+from ..models.zoo.multibranch import VGG
 from ..models.zoo.residual import BasicBlock, Bottleneck, ResNet
 from ..ops import cnn, conv
 from .base import EpochStats, LocalTrainer, TrainerConfig
@@ -55,7 +56,9 @@ class _Unit:
 
     def __init__(self, c: nn.Conv2d, bn: nn.BatchNorm2d, in_hw: int, relu: bool, rows: int, dev,
                  need_y: bool = True, c_in_pad: Optional[int] = None, act_dtype=torch.bfloat16):
-        assert c.bias is None and c.dilation == (1, 1)
+        assert c.dilation == (1, 1)
+        # a conv bias (VGG) stays out of z: train-mode BN cancels it exactly (its gradient is 0, the
+        # flat grad entry is never written), it only enters running_mean / eval via BNParams.cbias
         self.conv, self.bn, self.relu = c, bn, relu
         self.depthwise = c.groups > 1
         if self.depthwise and not (c.groups == c.in_channels == c.out_channels):
@@ -88,7 +91,7 @@ class _Unit:
     def bn_args(self, stats) -> dict:
         b = self.bn
         return cnn.bn_desc(stats, b.weight, b.bias, b.running_mean, b.running_var, b.num_batches_tracked,
-                           self.smean, self.sinv, self.shift)
+                           self.smean, self.sinv, self.shift, cbias=self.conv.bias)
 
     def in_shape(self, nb: int):
         return (nb, self.H, self.H, self.C)
@@ -132,10 +135,11 @@ class _Unit:
 
 
 class _Block:
-    """Chain of units; the last unit's BN is fused with the shortcut and the output ReLU."""
+    """Chain of units; the last unit's BN is fused with the shortcut and the output ReLU, optionally
+    followed by MaxPool2d(2, 2) (VGG)."""
 
     def __init__(self, pairs, relus, in_hw: int, cin: int, rows: int, dev, shortcut: str = "none",
-                 proj=None, out_relu: bool = True, first: bool = False, act_dtype=torch.bfloat16):
+                 proj=None, out_relu: bool = True, first: bool = False, act_dtype=torch.bfloat16, pool: bool = False):
         self.main: List[_Unit] = []
         hw = in_hw
         for i, ((c, bn), r) in enumerate(zip(pairs, relus)):
@@ -144,7 +148,12 @@ class _Block:
                       c_in_pad=8 if first and i == 0 else None, act_dtype=act_dtype)
             self.main.append(u)
             hw = u.P
-        self.in_hw, self.cin, self.out_hw = in_hw, cin, hw
+        self.in_hw, self.cin = in_hw, cin
+        self.pre_hw = hw                    # spatial size before the optional pool
+        self.pool = pool
+        if pool and (shortcut != "none" or hw % 2):
+            raise TypeError("maxpool blocks: no shortcut, even spatial size")
+        self.out_hw = hw // 2 if pool else hw
         self.cout = self.main[-1].O
         self.shortcut = shortcut            # "none" | "identity" | "proj"
         self.proj = (_Unit(proj[0], proj[1], in_hw, relu=False, rows=rows, dev=dev, need_y=False,
@@ -152,7 +161,9 @@ class _Block:
         self.out_relu = out_relu
         self.first = first                  # network input block: no input gradient
         bf = dict(dtype=act_dtype, device=dev)
-        self.out = torch.empty(rows * hw * hw * self.cout, **bf)
+        self.pre = torch.empty(rows * hw * hw * self.cout, **bf)
+        self.out = torch.empty(rows * self.out_hw * self.out_hw * self.cout, **bf) if pool else self.pre
+        self.dpre = torch.empty(rows * hw * hw * self.cout, **bf) if pool else None
         n_in = rows * in_hw * in_hw * cin
         self.din_a = None if first else torch.empty(n_in, **bf)
         self.din_b = torch.empty(n_in, **bf) if shortcut != "none" else None
@@ -162,6 +173,12 @@ class _Block:
 
     def out_view(self, nb: int) -> torch.Tensor:
         return self.out[: nb * self.out_hw * self.out_hw * self.cout].view(nb, self.out_hw, self.out_hw, self.cout)
+
+    def pre_view(self, nb: int) -> torch.Tensor:
+        return self.pre[: nb * self.pre_hw * self.pre_hw * self.cout].view(nb, self.pre_hw, self.pre_hw, self.cout)
+
+    def dpre_view(self, nb: int) -> torch.Tensor:
+        return self.dpre[: nb * self.pre_hw * self.pre_hw * self.cout].view(nb, self.pre_hw, self.pre_hw, self.cout)
 
     def in_view(self, t: torch.Tensor, nb: int) -> torch.Tensor:
         return t[: nb * self.in_hw * self.in_hw * self.cin].view(nb, self.in_hw, self.in_hw, self.cin)
@@ -220,7 +237,31 @@ def _plan_mobilenetv2(m: MobileNetV2, rows, dev, dt) -> List[_Block]:
     return blocks
 
 
-PLANS = {ResNet: _plan_resnet, MobileNet: _plan_mobilenet, MobileNetV2: _plan_mobilenetv2}
+def _plan_vgg(m: VGG, rows, dev, dt) -> List[_Block]:
+    """features = [Conv2d(bias), BN, ReLU | MaxPool2d(2)]..., AvgPool2d(1) (identity), classifier."""
+    mods = list(m.features)
+    blocks: List[_Block] = []
+    hw, c = 32, 8
+    i = 0
+    while i < len(mods):
+        mod = mods[i]
+        if isinstance(mod, nn.Conv2d):
+            bn = mods[i + 1]
+            assert isinstance(bn, nn.BatchNorm2d) and isinstance(mods[i + 2], nn.ReLU)
+            pool = i + 3 < len(mods) and isinstance(mods[i + 3], nn.MaxPool2d)
+            b = _Block([(mod, bn)], [True], hw, c, rows, dev, out_relu=True, first=not blocks, act_dtype=dt,
+                       pool=pool)
+            blocks.append(b)
+            hw, c = b.out_hw, b.cout
+            i += 4 if pool else 3
+        elif isinstance(mod, nn.AvgPool2d) and mod.kernel_size in (1, (1, 1)):
+            i += 1
+        else:
+            raise TypeError(f"VGG plan: unexpected {type(mod).__name__}")
+    return blocks
+
+
+PLANS = {ResNet: _plan_resnet, MobileNet: _plan_mobilenet, MobileNetV2: _plan_mobilenetv2, VGG: _plan_vgg}
 
 
 def supports(model: nn.Module) -> bool:
@@ -238,7 +279,7 @@ class CNNNativeTrainer(LocalTrainer):
         torch.manual_seed(cfg.seed)
         model = build_model(model_name)
         if type(model) not in PLANS:
-            raise TypeError(f"{model_name}: no native plan (ResNet, MobileNet, MobileNetV2 are supported)")
+            raise TypeError(f"{model_name}: no native plan (ResNet, MobileNet, MobileNetV2, VGG are supported)")
         if init_state is not None:
             model.load_state_dict(init_state)
         self.model = model.to(device)
@@ -275,7 +316,8 @@ class CNNNativeTrainer(LocalTrainer):
         self.xin = torch.empty(R, 32, 32, 8, dtype=act_dtype, device=device)
         self.dhead = torch.empty(R * self.head_hw * self.head_hw * self.head_c, dtype=act_dtype, device=device)
         self.pooled = torch.empty(R, self.head_c, device=device)
-        self.dlog = torch.empty(R, self.model.linear.out_features, device=device)
+        self.head_lin = getattr(self.model, "linear", None) or self.model.classifier
+        self.dlog = torch.empty(R, self.head_lin.out_features, device=device)
         self.stats = torch.zeros(2, 4, device=device)        # [train, eval] x {loss, correct, count, pad}
         self.round_ctr = torch.zeros(4, dtype=torch.int32, device=device)
         self.sched = torch.zeros(1, dtype=torch.int32, device=device)
@@ -360,7 +402,7 @@ class CNNNativeTrainer(LocalTrainer):
                 h = self._bn(v, v.view(v.z, nb), v.view(v.y, nb), train, v.relu)
             last = b.main[-1]
             last.fwd(h, nb, last.stats if train else None, ws)
-            out = b.out_view(nb)
+            out = b.pre_view(nb)
             z = last.view(last.z, nb)
             if b.shortcut == "proj":
                 p = b.proj
@@ -370,8 +412,10 @@ class CNNNativeTrainer(LocalTrainer):
                 self._bn(last, z, out, train, b.out_relu, res=a)
             else:
                 self._bn(last, z, out, train, b.out_relu)
-            a = out
-        lin = self.model.linear
+            if b.pool:
+                cnn.maxpool2(out, out=b.out_view(nb))
+            a = b.out_view(nb)
+        lin = self.head_lin
         hd = self.dhead[: a.numel()].view_as(a)
         cnn.head(a, labels, 0, lin.weight, lin.bias, self.stats[stats_row], train, self.pooled[:nb], self.dlog[:nb],
                  hd if train else None, lin.weight.grad if train else None, lin.bias.grad if train else None,
@@ -395,7 +439,9 @@ class CNNNativeTrainer(LocalTrainer):
             a_in = x if b.first else self.blocks[i - 1].out_view(nb)
             last = b.main[-1]
             din_b = b.in_view(b.din_b, nb) if b.din_b is not None else None
-            self._bn_bwd(last, nb, dya, dyb, b.out_view(nb) if b.out_relu else None, zb=b.proj,
+            if b.pool:   # grad wrt the pooled output -> grad wrt the pre-pool activation
+                dya = cnn.maxpool2_bwd(b.pre_view(nb), dya, out=b.dpre_view(nb))
+            self._bn_bwd(last, nb, dya, dyb, b.pre_view(nb) if b.out_relu else None, zb=b.proj,
                          gout=din_b if b.shortcut == "identity" else None)
             for j in range(len(b.main) - 1, -1, -1):
                 v = b.main[j]

@@ -42,23 +42,47 @@ def sched_next(sched: torch.Tensor, counter: torch.Tensor, cur: torch.Tensor) ->
 class BNParams:
     """One BatchNorm2d's device tensors (train-time batch stats + params + running/saved stats)."""
 
-    __slots__ = ("stats", "gamma", "beta", "rmean", "rvar", "nbt", "smean", "sinv", "shift")
+    __slots__ = ("stats", "gamma", "beta", "rmean", "rvar", "nbt", "smean", "sinv", "shift", "cbias")
 
     def __init__(self, stats=None, gamma=None, beta=None, rmean=None, rvar=None, nbt=None, smean=None, sinv=None,
-                 shift=None):
+                 shift=None, cbias=None):
         self.stats, self.gamma, self.beta = stats, gamma, beta
         self.rmean, self.rvar, self.nbt = rmean, rvar, nbt
         self.smean, self.sinv = smean, sinv
         # ``stats`` hold sums of (z - shift); bn_bwd stores this step's batch mean into ``shift``
         self.shift = shift
+        # bias of the producing conv (VGG / GoogLeNet convs have one), kept OUT of z: a train-mode BN
+        # is invariant to it (its gradient is exactly 0); it only enters running_mean and eval
+        self.cbias = cbias
 
     def ptrs(self) -> dict:
         return {k: _p(getattr(self, k)) for k in self.__slots__}
 
 
 def bn_desc(stats=None, gamma=None, beta=None, rmean=None, rvar=None, nbt=None, smean=None, sinv=None,
-            shift=None) -> BNParams:
-    return BNParams(stats, gamma, beta, rmean, rvar, nbt, smean, sinv, shift)
+            shift=None, cbias=None) -> BNParams:
+    return BNParams(stats, gamma, beta, rmean, rvar, nbt, smean, sinv, shift, cbias)
+
+
+def maxpool2(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """MaxPool2d(2, 2) of NHWC bf16 ``x`` [N, H, W, C] (H, W even, C % 8 == 0)."""
+    N, H, W, C = x.shape
+    if out is None:
+        out = torch.empty(N, H // 2, W // 2, C, dtype=x.dtype, device=x.device)
+    native.require().maxpool2(native.stream_handle(x.device), x.data_ptr(), out.data_ptr(), N, H, W, C)
+    return out
+
+
+def maxpool2_bwd(x: torch.Tensor, dy: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx of MaxPool2d(2, 2): dy routed to each window's first maximum of ``x``, 0 elsewhere."""
+    N, H, W, C = x.shape
+    if tuple(dy.shape) != (N, H // 2, W // 2, C):
+        raise ValueError("maxpool2_bwd: dy shape mismatch")
+    if out is None:
+        out = torch.empty_like(x)
+    native.require().maxpool2_bwd(native.stream_handle(x.device), x.data_ptr(), dy.data_ptr(), out.data_ptr(),
+                                  N, H, W, C)
+    return out
 
 
 def bn_apply(z: torch.Tensor, a: BNParams, y: torch.Tensor, train: bool, relu: bool,

@@ -190,12 +190,12 @@ def _coeffs(p: "cnn.BNParams", M: int, train: bool, eps: float, mom: float):
         p.smean.copy_(mean)
         p.sinv.copy_(inv)
         if p.rmean is not None:
-            p.rmean.mul_(1 - mom).add_(mom * mean)
+            p.rmean.mul_(1 - mom).add_(mom * (mean + (p.cbias if p.cbias is not None else 0.0)))
             p.rvar.mul_(1 - mom).add_(mom * var * M / max(M - 1, 1))
         if p.nbt is not None:
             p.nbt += 1
     else:
-        mean, inv = p.rmean, torch.rsqrt(p.rvar + eps)
+        mean, inv = p.rmean - (p.cbias if p.cbias is not None else 0.0), torch.rsqrt(p.rvar + eps)
     sc = p.gamma * inv
     return sc, p.beta - mean * sc
 
@@ -215,6 +215,23 @@ def bn_apply(z, a, y, train, relu, z2=None, b=None, res=None, eps=1e-5, momentum
         v = torch.relu(v)
     y.copy_(v.reshape(y.shape).to(y.dtype))
     return y
+
+
+@torch.no_grad()
+def maxpool2(x, out=None):
+    y = F.max_pool2d(_nchw(x), 2, 2)
+    if out is None:
+        out = torch.empty(y.shape[0], y.shape[2], y.shape[3], y.shape[1], dtype=x.dtype, device=x.device)
+    return _nhwc_into(out, y)
+
+
+def maxpool2_bwd(x, dy, out=None):
+    xr = _nchw(x).requires_grad_(True)
+    with torch.enable_grad():
+        F.max_pool2d(xr, 2, 2).backward(_nchw(dy))
+    if out is None:
+        out = torch.empty_like(x)
+    return _nhwc_into(out, xr.grad)
 
 
 @torch.no_grad()
@@ -292,7 +309,8 @@ def emulated():
     for name in ("pack_weight", "pack_weights", "fd_ws_floats", "dgrad_pack_weights", "conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
                  "dwconv_dgrad", "dwconv_wgrad", "dwconv_ws_floats"):
         swap(conv, name, globals()[name])
-    for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "bn_bwd_ws_floats", "head"):
+    for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "bn_bwd_ws_floats", "head", "maxpool2",
+                 "maxpool2_bwd"):
         swap(cnn, name, globals()[name])
     swap(native, "require", lambda: _NativeStub())
     swap(native, "stream_handle", lambda device=None: 0)

@@ -1,7 +1,7 @@
 """CPU check of the native CNN engine's schedule: with every kernel swapped for
 its PyTorch emulation (fedmi.ops.emulate) and fp32 activation buffers, one
 forward+backward through the engine must reproduce torch autograd's loss,
-parameter gradients and BN running statistics for ResNet (basic + bottleneck),
+parameter gradients and BN running statistics for ResNet (basic + bottleneck), VGG,
 MobileNet and MobileNetV2 to fp32 rounding.  (With bf16 activations even
 torch's own bf16 model differs from fp32 at init by up to cos 0.4 in the
 first layers of MobileNet, so precision is factored out here.)
@@ -21,7 +21,7 @@ def _cos(a, b):
     return float(F.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0))
 
 
-@pytest.mark.parametrize("name", ["ResNet18", "ResNet50", "MobileNet", "MobileNetV2"])
+@pytest.mark.parametrize("name", ["ResNet18", "ResNet50", "MobileNet", "MobileNetV2", "VGG11"])
 def test_engine_schedule_matches_autograd(name):
     from fedmi.engine.cnn_native import CNNNativeTrainer
 
@@ -66,7 +66,7 @@ def test_engine_schedule_matches_autograd(name):
             assert int(bufs[k]) == int(b), k
 
 
-@pytest.mark.parametrize("name", ["ResNet18", "MobileNetV2"])
+@pytest.mark.parametrize("name", ["ResNet18", "MobileNetV2", "VGG11"])
 def test_engine_eval_matches_torch_eval(name):
     """Eval mode (BN from running statistics) through the engine schedule == torch .eval()."""
     from fedmi.engine.cnn_native import CNNNativeTrainer

@@ -352,3 +352,45 @@ def test_pack_weights_multi(gpu_device):
     torch.cuda.synchronize()
     for a, b in zip(single, multi):
         assert torch.equal(a, b)
+
+
+def test_maxpool2_fwd_bwd(gpu_device):
+    torch.manual_seed(11)
+    x = torch.randn(6, 8, 10, 24, device=gpu_device).bfloat16()
+    y = cnn.maxpool2(x)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.max_pool2d(xr, 2, 2)
+    g = torch.randn_like(ref).bfloat16().float()
+    ref.backward(g)
+    dx = cnn.maxpool2_bwd(x, _nhwc(g).bfloat16().contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(y.float(), _nhwc(ref.detach()))
+    assert torch.equal(dx.float(), _nhwc(xr.grad))
+
+
+def test_bn_conv_bias_folding(gpu_device):
+    """BN(z + b) with b kept out of z: same train output, running_mean includes b, eval uses it."""
+    torch.manual_seed(12)
+    dev = gpu_device
+    M, C = 512, 64
+    z = torch.randn(M, C, device=dev).bfloat16()
+    b = torch.randn(C, device=dev)
+    g, be = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    rep = conv.stats_buffer(C, dev)
+    rep[0, 0] = z.float().sum(0)
+    rep[0, 1] = (z.float() ** 2).sum(0)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    sm, si = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    y = torch.empty_like(z)
+    cnn.bn_apply(z, cnn.bn_desc(rep, g, be, rm, rv, None, sm, si, cbias=b), y, train=True, relu=False)
+    zb = z.float() + b
+    mean, var = zb.mean(0), zb.var(0, unbiased=False)
+    ref = (zb - mean) / torch.sqrt(var + 1e-5) * g + be
+    torch.cuda.synchronize()
+    assert _rel(y.float(), ref) < 1e-2
+    assert torch.allclose(rm, 0.1 * mean, atol=1e-4)
+    ye = torch.empty_like(z)
+    cnn.bn_apply(z, cnn.bn_desc(None, g, be, rm, rv, cbias=b), ye, train=False, relu=False)
+    refe = (zb - rm) / torch.sqrt(rv + 1e-5) * g + be
+    torch.cuda.synchronize()
+    assert _rel(ye.float(), refe) < 1e-2
