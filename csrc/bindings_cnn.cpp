@@ -19,7 +19,8 @@ namespace fedmi {
 struct ConvShape {
   int N, H, W, C, Cw, O, P, Q, R, S, st, pad;
 };
-void launch_conv_fwd(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, const float*, float*, long);
+void launch_conv_fwd(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, const float*, float*, long,
+                     const bf16*);
 void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, long, const bf16*);
 struct DPackItem {
   const float* w;
@@ -50,6 +51,7 @@ struct BNBwdDesc {
   const bf16* zb; const float* meanB; const float* invB; const float* gammaB; float* dgammaB; float* dbetaB; bf16* dzb;
   bf16* gout;
   float* shiftA; float* shiftB;
+  const bf16* dadd;
 };
 struct DwShape {
   int N, H, W, C, R, S, st, pad;
@@ -111,12 +113,12 @@ BNDesc bn_from(const py::dict& d) {
 void fedmi_bind_cnn(py::module_& m) {
   m.attr("STAT_REP") = STAT_REP;
   m.def("conv_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
-                       uintptr_t shift, uintptr_t ws, long ws_floats) {
+                       uintptr_t shift, uintptr_t ws, long ws_floats, uintptr_t res) {
     launch_conv_fwd(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(w), P<bf16>(y), P<float>(stats),
-                    P<const float>(shift), P<float>(ws), ws ? ws_floats : 0);
+                    P<const float>(shift), P<float>(ws), ws ? ws_floats : 0, P<const bf16>(res));
     check("conv_fwd");
   }, py::arg("st"), py::arg("shape"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("shift"),
-     py::arg("ws") = 0, py::arg("ws_floats") = 0);
+     py::arg("ws") = 0, py::arg("ws_floats") = 0, py::arg("res") = 0);
   m.def("conv_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
                          long ws_floats, uintptr_t wd) {
     launch_conv_dgrad(S(st), shape_from(shp), P<const bf16>(dy), P<const bf16>(w), P<bf16>(dx), P<float>(ws),
@@ -211,7 +213,7 @@ void fedmi_bind_cnn(py::module_& m) {
                 P<bf16>(dget(d, "dza")),           P<const bf16>(dget(d, "zb")),      P<const float>(dget(d, "meanB")),
                 P<const float>(dget(d, "invB")),   P<const float>(dget(d, "gammaB")), P<float>(dget(d, "dgammaB")),
                 P<float>(dget(d, "dbetaB")),       P<bf16>(dget(d, "dzb")),           P<bf16>(dget(d, "gout")),
-                P<float>(dget(d, "shiftA")),       P<float>(dget(d, "shiftB"))};
+                P<float>(dget(d, "shiftA")),       P<float>(dget(d, "shiftB")),       P<const bf16>(dget(d, "dadd"))};
     if (!b.dya || !b.za || !b.meanA || !b.invA || !b.gammaA || !b.dza) throw std::invalid_argument("bn_bwd: missing A");
     launch_bn_bwd(S(st), b, P<float>(red), M, C, P<float>(ws), ws ? ws_floats : 0);
     check("bn_bwd");

@@ -280,6 +280,7 @@ struct BwdOut {
   const float* gammaB;
   float* shiftA;          // <- this step's batch mean: the next step's statistics shift
   float* shiftB;
+  const bf16* dadd;       // optional grad added to dza (a residual edge that bypasses this BN)
 };
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdIn in, BwdOut out, const float* __restrict__ red,
@@ -322,6 +323,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdIn in, BwdOut out,
     load8f(in.za + i * 8, z);
 #pragma unroll
     for (int j = 0; j < 8; ++j) d[j] = co[c0 + j] * g[j] + co[C + c0 + j] * z[j] + co[2 * C + c0 + j];
+    if (out.dadd) {
+      float t[8];
+      load8f(out.dadd + i * 8, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] += t[j];
+    }
     store8f(out.dza + i * 8, d);
     if (in.zb) {
       load8f(in.zb + i * 8, z);
@@ -571,6 +578,7 @@ struct BNBwdDesc {
   const bf16* zb; const float* meanB; const float* invB; const float* gammaB; float* dgammaB; float* dbetaB; bf16* dzb;
   bf16* gout;
   float* shiftA; float* shiftB;
+  const bf16* dadd;
 };
 
 static void bn_bwd_grid(int M, int C, int* tb, int* rows_per_block, int* nblk) {
@@ -596,7 +604,8 @@ void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, float* red, int M, int C,
   const int VR = C / 8;
   if (C % 8 || VR > 256) throw std::invalid_argument("bn_bwd: need C % 8 == 0 and C <= 2048");
   BwdIn in{d.dya, d.dyb, d.y, d.za, d.meanA, d.invA, d.zb, d.meanB, d.invB};
-  BwdOut out{d.dza, d.dzb, d.gout, d.dgammaA, d.dbetaA, d.dgammaB, d.dbetaB, d.gammaA, d.gammaB, d.shiftA, d.shiftB};
+  BwdOut out{d.dza, d.dzb, d.gout, d.dgammaA, d.dbetaA, d.dgammaB, d.dbetaB, d.gammaA, d.gammaB, d.shiftA, d.shiftB,
+             d.dadd};
   int tb, rows_per_block, nblk;
   bn_bwd_grid(M, C, &tb, &rows_per_block, &nblk);
   const bool two = ws && ws_floats >= (long)BN_REP * 3 * C;

@@ -447,7 +447,8 @@ template <int BN>
 __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                 bf16* __restrict__ out, float* __restrict__ part,
                                                 float* __restrict__ stats, const float* __restrict__ shift,
-                                                TapGeom g, RowMap rmap, int ksteps_per_split) {
+                                                TapGeom g, RowMap rmap, int ksteps_per_split,
+                                                const bf16* __restrict__ res) {
   constexpr int BM = 128;
   constexpr int NA = BM / 32;            // A wave-instructions per stage per wave (8 rows each)
   constexpr int NB = BN / 32;
@@ -583,9 +584,19 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
   for (int c = tid; c < BM * CPR; c += 256) {
     const int row = c / CPR, cc = c % CPR;
     const int m = m0 + row, col = n0 + cc * 8;
-    if (m < g.M && col < g.O)
-      *reinterpret_cast<uint4*>(out + map_row(rmap, m) * g.O + col) = *reinterpret_cast<const uint4*>(ct + row * CT_LD + cc * 8);
+    if (m < g.M && col < g.O) {
+      const long orow = map_row(rmap, m);
+      if (res != nullptr) {   // fused residual add (pre-activation blocks): y = conv + res, stats of y
+        bf16x8 t = *reinterpret_cast<const bf16x8*>(ct + row * CT_LD + cc * 8);
+        const bf16x8 r = *reinterpret_cast<const bf16x8*>(res + orow * g.O + col);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = (bf16)((float)t[j] + (float)r[j]);
+        *reinterpret_cast<bf16x8*>(ct + row * CT_LD + cc * 8) = t;
+      }
+      *reinterpret_cast<uint4*>(out + orow * g.O + col) = *reinterpret_cast<const uint4*>(ct + row * CT_LD + cc * 8);
+    }
   }
+  if (res != nullptr) __syncthreads();
   if (stats != nullptr) {   // BN batch statistics of bf16(y) - shift, one atomic per column per WG
     constexpr int PARTS = 256 / BN;
     const int col = tid % BN, prt = tid / BN;
@@ -699,7 +710,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict
 __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restrict__ ws, int splits, int M, int NC,
                                                           RowMap rmap, bf16* __restrict__ out,
                                                           float* __restrict__ stats, const float* __restrict__ shift,
-                                                          int rows_per_block) {
+                                                          int rows_per_block, const bf16* __restrict__ res) {
   __shared__ float red[2][256][8];
   const int VR = NC >> 3;                 // host: blockDim.x % VR == 0
   const int cg = threadIdx.x % VR, rstep = blockDim.x / VR, r0 = threadIdx.x / VR;
@@ -721,11 +732,16 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restric
       a.x += ua.x; a.y += ua.y; a.z += ua.z; a.w += ua.w;
       b.x += ub.x; b.y += ub.y; b.z += ub.z; b.w += ub.w;
     }
-    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const long orow = map_row(rmap, m);
+    if (res != nullptr) {
+      const bf16x8 r = *reinterpret_cast<const bf16x8*>(res + orow * NC + c0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += (float)r[j];
+    }
     bf16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
-    const long orow = map_row(rmap, m);
     *reinterpret_cast<bf16x8*>(out + orow * NC + c0) = o;
     if (stats) {
 #pragma unroll
@@ -925,7 +941,8 @@ static int tap_splits(const TapGeom& g, long ws_floats) {
 }
 
 static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const bf16* wt, bf16* out, float* stats,
-                       const float* shift, const RowMap& rm, float* ws, long ws_floats) {
+                       const float* shift, const RowMap& rm, float* ws, long ws_floats,
+                       const bf16* res = nullptr) {
   if (g.C % 64 || g.O % 8) throw std::invalid_argument("conv_tap: need C % 64 == 0 and O % 8 == 0");
   const int BN = tap_bn(g.O);
   const long tiles = (long)((g.M + 127) / 128) * ((g.O + BN - 1) / BN);
@@ -936,9 +953,11 @@ static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const b
   dim3 grid((unsigned)tiles, 1, (unsigned)splits);
   float* part = splits > 1 ? ws : nullptr;
   if (BN == 128)
-    hipLaunchKernelGGL(conv_tap<128>, grid, dim3(256), 0, st, in, wt, out, part, part ? nullptr : stats, shift, g, rm, kps);
+    hipLaunchKernelGGL(conv_tap<128>, grid, dim3(256), 0, st, in, wt, out, part, part ? nullptr : stats, shift, g, rm, kps,
+                       part ? nullptr : res);
   else
-    hipLaunchKernelGGL(conv_tap<64>, grid, dim3(256), 0, st, in, wt, out, part, part ? nullptr : stats, shift, g, rm, kps);
+    hipLaunchKernelGGL(conv_tap<64>, grid, dim3(256), 0, st, in, wt, out, part, part ? nullptr : stats, shift, g, rm, kps,
+                       part ? nullptr : res);
   if (splits > 1) {
     const int VR = g.O / 8;
     const int tb = (256 / VR) * VR;
@@ -946,7 +965,7 @@ static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const b
     const int rows_per_block = stats ? std::max(2 * rstep, (g.M + 255) / 256) : std::max(rstep, (g.M + 1023) / 1024);
     const int nblk = (g.M + rows_per_block - 1) / rows_per_block;
     hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, splits, g.M, g.O, rm, out, stats, shift,
-                       rows_per_block);
+                       rows_per_block, res);
   }
 }
 
@@ -1009,7 +1028,7 @@ static void launch_fd(hipStream_t st, const ConvGeom& g, const bf16* x, const bf
   RowMap rm{};
   if (MODE == DGRAD && g.st != 1) rm = make_rowmap(g.Hp, g.Wp, g.H, g.W, g.st, g.ph, g.pw);
   hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, sp, g.M, g.NC, rm, out, stats, shift,
-                     rows_per_block);
+                     rows_per_block, nullptr);
 }
 
 // K-split count for the weight gradient: about two workgroups per CU, at least
@@ -1030,15 +1049,16 @@ static int wgrad_splits(const ConvGeom& g, long ws_cap_floats) {
 
 // Y[N,P,Q,O] = conv(X[N,H,W,C], W_rsc); stats (optional) += [sum | sumsq] of (Y - shift) per output channel.
 void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf16* wrsc, bf16* y, float* stats,
-                     const float* shift, float* ws, long ws_floats) {
+                     const float* shift, float* ws, long ws_floats, const bf16* res) {
   check_shape(s);
   ConvGeom g = make_geom(s);
   g.M = s.N * s.P * s.Q; g.NC = s.O; g.K = s.R * s.S * s.C;
   if (s.C % 64 == 0) {
     const TapGeom t = make_tap(s.N, s.H, s.W, s.C, s.O, s.P, s.Q, s.R, s.S, s.st, s.pad, s.pad);
-    launch_tap(st, t, x, wrsc, y, stats, shift, RowMap{}, ws, ws_floats);
+    launch_tap(st, t, x, wrsc, y, stats, shift, RowMap{}, ws, ws_floats, res);
     return;
   }
+  if (res) throw std::invalid_argument("conv_fwd: a fused residual needs the tap path (C % 64 == 0)");
   launch_fd<FWD>(st, g, x, wrsc, nullptr, y, stats, shift, ws, ws_floats);
 }
 

@@ -41,7 +41,7 @@ from .. import native
 from ..models import build_model
 from ..models.zoo.mobile import DWSeparable, InvertedResidual, MobileNet, MobileNetV2
 from ..models.zoo.multibranch import VGG
-from ..models.zoo.residual import BasicBlock, Bottleneck, ResNet
+from ..models.zoo.residual import BasicBlock, Bottleneck, PreActBlock, PreActBottleneck, PreActResNet, ResNet
 from ..ops import cnn, conv
 from .base import EpochStats, LocalTrainer, TrainerConfig
 from .data import FedDataset, ImageSet
@@ -103,25 +103,28 @@ class _Unit:
         return max(conv.wgrad_ws_floats(*shp), conv.fd_ws_floats(*shp))
 
     # ---- launches (``ws``: the engine's shared split-K workspace; launches are stream-serial)
-    def fwd(self, x: torch.Tensor, nb: int, stats, ws: Optional[torch.Tensor] = None) -> None:
+    def fwd(self, x: torch.Tensor, nb: int, stats, ws: Optional[torch.Tensor] = None,
+            res: Optional[torch.Tensor] = None) -> None:
         sh = self.shift if stats is not None else None
         if self.depthwise:
+            assert res is None
             conv.dwconv_fwd(x, self.conv.weight, self.stride, self.pad, stats=stats, out=self.view(self.z, nb),
                             shift=sh)
         else:
             conv.conv2d_fwd(x, self.wr, self.stride, self.pad, Cw=self.Cw, stats=stats, out=self.view(self.z, nb),
-                            shift=sh, ws=ws)
+                            shift=sh, ws=ws, res=res)
 
-    def wgrad(self, x: torch.Tensor, nb: int, ws: torch.Tensor) -> None:
-        dz = self.view(self.dz, nb)
+    def wgrad(self, x: torch.Tensor, nb: int, ws: torch.Tensor, dz: Optional[torch.Tensor] = None) -> None:
+        dz = self.view(self.dz, nb) if dz is None else dz
         if self.depthwise:
             conv.dwconv_wgrad(x, dz, self.R, self.stride, self.pad, out=self.conv.weight.grad, ws=ws)
         else:
             conv.conv2d_wgrad(x, dz, self.R, self.S, self.stride, self.pad, Cw=self.Cw, out=self.conv.weight.grad,
                               ws=ws)
 
-    def dgrad(self, nb: int, out: torch.Tensor, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-        dz = self.view(self.dz, nb)
+    def dgrad(self, nb: int, out: torch.Tensor, ws: Optional[torch.Tensor] = None,
+              dz: Optional[torch.Tensor] = None) -> torch.Tensor:
+        dz = self.view(self.dz, nb) if dz is None else dz
         if self.depthwise:
             return conv.dwconv_dgrad(dz, self.conv.weight, self.in_shape(nb), self.stride, self.pad, out=out)
         return conv.conv2d_dgrad(dz, self.wr, self.in_shape(nb), self.stride, self.pad, Cw=self.Cw, out=out, ws=ws,
@@ -261,7 +264,65 @@ def _plan_vgg(m: VGG, rows, dev, dt) -> List[_Block]:
     return blocks
 
 
-PLANS = {ResNet: _plan_resnet, MobileNet: _plan_mobilenet, MobileNetV2: _plan_mobilenetv2, VGG: _plan_vgg}
+class _PABlock:
+    """Pre-activation residual block (src/models/preact_resnet.py:12-62) as units.
+
+    A unit is (conv, the BN that normalises its output).  Inside the block:
+    (conv1, bn2) [, (conv2, bn3)], and the last conv pairs with the NEXT block's
+    bn1 (None for the network's last block: its output goes to the head); its
+    epilogue also adds the shortcut (identity x, or the 1x1 shortcut conv of the
+    pre-activation, a BN-less unit) so the next bn1's statistics are of x + skip.
+    """
+
+    def __init__(self, blk, in_hw: int, cin: int, rows: int, dev, dt, next_bn):
+        if isinstance(blk, PreActBlock):
+            pairs = [(blk.conv1, blk.bn2), (blk.conv2, next_bn)]
+        elif isinstance(blk, PreActBottleneck):
+            pairs = [(blk.conv1, blk.bn2), (blk.conv2, blk.bn3), (blk.conv3, next_bn)]
+        else:
+            raise TypeError(type(blk).__name__)
+        self.units: List[_Unit] = []
+        hw = in_hw
+        for c, bn in pairs:
+            u = _Unit(c, bn, hw, relu=True, rows=rows, dev=dev, need_y=bn is not None, act_dtype=dt)
+            self.units.append(u)
+            hw = u.P
+        self.sc = (_Unit(blk.shortcut[0], None, in_hw, relu=False, rows=rows, dev=dev, need_y=False, act_dtype=dt)
+                   if hasattr(blk, "shortcut") else None)
+        self.in_hw, self.cin, self.out_hw, self.cout = in_hw, cin, hw, self.units[-1].O
+        self.da2 = torch.empty(rows * in_hw * in_hw * cin, dtype=dt, device=dev) if self.sc else None
+
+    def all_units(self) -> List[_Unit]:
+        return self.units + ([self.sc] if self.sc else [])
+
+    def in_view(self, t: torch.Tensor, nb: int) -> torch.Tensor:
+        return t[: nb * self.in_hw * self.in_hw * self.cin].view(nb, self.in_hw, self.in_hw, self.cin)
+
+
+class _PreActPlan:
+    def __init__(self, m: PreActResNet, rows, dev, dt):
+        blks = [b for layer in (m.layer1, m.layer2, m.layer3, m.layer4) for b in layer]
+        # stem conv (no BN of its own) pairs with the first block's bn1
+        self.stem = _Unit(m.conv1, blks[0].bn1, 32, relu=True, rows=rows, dev=dev, need_y=True, c_in_pad=8,
+                          act_dtype=dt)
+        self.blocks: List[_PABlock] = []
+        hw, c = self.stem.P, self.stem.O
+        for i, b in enumerate(blks):
+            nb = blks[i + 1].bn1 if i + 1 < len(blks) else None
+            pb = _PABlock(b, hw, c, rows, dev, dt, nb)
+            self.blocks.append(pb)
+            hw, c = pb.out_hw, pb.cout
+
+    def units(self) -> List[_Unit]:
+        return [self.stem] + [u for b in self.blocks for u in b.all_units()]
+
+
+def _plan_preact(m, rows, dev, dt):
+    return _PreActPlan(m, rows, dev, dt)
+
+
+PLANS = {ResNet: _plan_resnet, MobileNet: _plan_mobilenet, MobileNetV2: _plan_mobilenetv2, VGG: _plan_vgg,
+         PreActResNet: _plan_preact}
 
 
 def supports(model: nn.Module) -> bool:
@@ -279,7 +340,7 @@ class CNNNativeTrainer(LocalTrainer):
         torch.manual_seed(cfg.seed)
         model = build_model(model_name)
         if type(model) not in PLANS:
-            raise TypeError(f"{model_name}: no native plan (ResNet, MobileNet, MobileNetV2, VGG are supported)")
+            raise TypeError(f"{model_name}: no native plan (ResNet, PreActResNet, MobileNet, MobileNetV2, VGG)")
         if init_state is not None:
             model.load_state_dict(init_state)
         self.model = model.to(device)
@@ -294,10 +355,15 @@ class CNNNativeTrainer(LocalTrainer):
                 s.y = s.y.to(torch.int32)
         self.eval_bs = min(cfg.eval_batch_size, 500)
         self.rows = R = max(cfg.batch_size, self.eval_bs)
-        self.blocks = PLANS[type(model)](self.model, R, device, act_dtype)
+        plan = PLANS[type(model)](self.model, R, device, act_dtype)
+        self.preact = plan if isinstance(plan, _PreActPlan) else None
+        self.blocks = plan.blocks if self.preact else plan
         last = self.blocks[-1]
         self.head_hw, self.head_c = last.out_hw, last.cout
-        self.units: List[_Unit] = [u for b in self.blocks for u in b.units()]
+        self.units: List[_Unit] = plan.units() if self.preact else [u for b in self.blocks for u in b.units()]
+        # units whose data gradient is never needed (they read the network input)
+        self._no_dgrad = ({id(self.preact.stem)} if self.preact else
+                          {id(u) for u in self.blocks[0].units()} if self.blocks[0].first else set())
         # per-step accumulators: BN batch stats [2][O] and BN-backward sums [3][O], one fill each
         self.stats_all = torch.zeros(sum(conv.STAT_REP * 2 * u.O for u in self.units), device=device)
         self.red_all = torch.zeros(sum(3 * u.O for u in self.units), device=device)
@@ -363,9 +429,8 @@ class CNNNativeTrainer(LocalTrainer):
 
     def pack(self) -> None:
         conv.pack_weights([it for it in (u.pack_item() for u in self.units) if it is not None])
-        # the network input block never needs a data gradient: skip its image
-        first = set(id(u) for u in self.blocks[0].units()) if self.blocks[0].first else set()
-        conv.dgrad_pack_weights([it for u in self.units if id(u) not in first
+        # the network input units never need a data gradient: skip their images
+        conv.dgrad_pack_weights([it for u in self.units if id(u) not in self._no_dgrad
                                  for it in [u.dgrad_pack_item()] if it is not None])
 
     # ---- data ----------------------------------------------------------------------------
@@ -391,6 +456,8 @@ class CNNNativeTrainer(LocalTrainer):
         return cnn.bn_apply(z, u.bn_args(u.stats), y, train, relu, eps=BN_EPS, momentum=BN_MOM, **kw)
 
     def _forward(self, nb: int, train: bool, images: torch.Tensor, labels: torch.Tensor, dbase, stats_row: int):
+        if self.preact is not None:
+            return self._forward_preact(nb, train, images, labels, dbase, stats_row)
         x = cnn.prep_input(images, 0, nb, self.augment and train, self.cfg.seed, self.round_ctr,
                            out=self.xin[:nb], dbase=dbase)
         a = x
@@ -422,16 +489,18 @@ class CNNNativeTrainer(LocalTrainer):
                  dbase=dbase)
         return x, hd
 
-    def _bn_bwd(self, u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None) -> None:
+    def _bn_bwd(self, u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None, dadd=None) -> None:
         bn_ws = self.bn_ws if self.bn_ws.numel() else None
         kw = {}
         if zb is not None:
             kw = dict(zb=zb.view(zb.z, nb), b=zb.bn_args(None), dgamma_b=zb.bn.weight.grad,
                       dbeta_b=zb.bn.bias.grad, dzb=zb.view(zb.dz, nb))
         cnn.bn_bwd(dya, u.view(u.z, nb), u.bn_args(None), u.bn.weight.grad, u.bn.bias.grad, u.view(u.dz, nb), u.red,
-                   dyb=dyb, y=y, gout=gout, ws=bn_ws, **kw)
+                   dyb=dyb, y=y, gout=gout, ws=bn_ws, dadd=dadd, **kw)
 
     def _backward(self, nb: int, x: torch.Tensor, dhead: torch.Tensor) -> None:
+        if self.preact is not None:
+            return self._backward_preact(nb, x, dhead)
         dya, dyb = dhead, None
         ws = self.wgrad_ws
         for i in range(len(self.blocks) - 1, -1, -1):
@@ -459,6 +528,73 @@ class CNNNativeTrainer(LocalTrainer):
             if not b.first:
                 dya = b.in_view(b.din_a, nb)
                 dyb = din_b
+
+    # ---- pre-activation ResNets --------------------------------------------------------------
+    def _head(self, a, nb, train, labels, dbase, stats_row):
+        lin = self.head_lin
+        hd = self.dhead[: a.numel()].view_as(a)
+        cnn.head(a, labels, 0, lin.weight, lin.bias, self.stats[stats_row], train, self.pooled[:nb], self.dlog[:nb],
+                 hd if train else None, lin.weight.grad if train else None, lin.bias.grad if train else None,
+                 dbase=dbase)
+        return hd
+
+    def _forward_preact(self, nb: int, train: bool, images, labels, dbase, stats_row: int):
+        P, ws = self.preact, self.wgrad_ws
+        x = cnn.prep_input(images, 0, nb, self.augment and train, self.cfg.seed, self.round_ctr,
+                           out=self.xin[:nb], dbase=dbase)
+        st = P.stem
+        st.fwd(x, nb, st.stats if train else None, ws)
+        self._bn(st, st.view(st.z, nb), st.view(st.y, nb), train, True)
+        prev = st
+        for b in P.blocks:
+            a = prev.view(prev.y, nb)                      # relu(bn1(x_b))
+            h = a
+            for u in b.units[:-1]:
+                u.fwd(h, nb, u.stats if train else None, ws)
+                self._bn(u, u.view(u.z, nb), u.view(u.y, nb), train, True)
+                h = u.view(u.y, nb)
+            if b.sc is not None:
+                b.sc.fwd(a, nb, None, ws)
+                skip = b.sc.view(b.sc.z, nb)
+            else:
+                skip = prev.view(prev.z, nb)               # identity: x_b
+            L = b.units[-1]
+            L.fwd(h, nb, L.stats if (train and L.bn is not None) else None, ws, res=skip)
+            if L.bn is not None:
+                self._bn(L, L.view(L.z, nb), L.view(L.y, nb), train, True)
+            prev = L
+        return x, self._head(prev.view(prev.z, nb), nb, train, labels, dbase, stats_row)
+
+    def _backward_preact(self, nb: int, x: torch.Tensor, dhead: torch.Tensor) -> None:
+        P, ws = self.preact, self.wgrad_ws
+        g = dhead                                          # dL / d x_{b+1} (= dz of the block's last unit)
+        for bi in range(len(P.blocks) - 1, -1, -1):
+            b = P.blocks[bi]
+            prev = P.blocks[bi - 1].units[-1] if bi > 0 else P.stem
+            a = prev.view(prev.y, nb)
+            L = b.units[-1]
+            pen = b.units[-2]
+            L.wgrad(pen.view(pen.y, nb), nb, ws, dz=g)
+            L.dgrad(nb, pen.view(pen.dy, nb), ws, dz=g)
+            for j in range(len(b.units) - 2, -1, -1):
+                u = b.units[j]
+                self._bn_bwd(u, nb, u.view(u.dy, nb), None, u.view(u.y, nb))
+                if j > 0:
+                    w = b.units[j - 1]
+                    u.wgrad(w.view(w.y, nb), nb, ws)
+                    u.dgrad(nb, w.view(w.dy, nb), ws)
+                else:
+                    u.wgrad(a, nb, ws)
+                    u.dgrad(nb, prev.view(prev.dy, nb), ws)      # d a_b, conv1 branch
+            da2 = None
+            if b.sc is not None:                           # d a_b, shortcut-conv branch
+                b.sc.wgrad(a, nb, ws, dz=g)
+                da2 = b.in_view(b.da2, nb)
+                b.sc.dgrad(nb, da2, ws, dz=g)
+            # bn1 of this block (prev's BN): dx_b = BN_bwd(relu mask) + identity-shortcut grad
+            self._bn_bwd(prev, nb, prev.view(prev.dy, nb), da2, a, dadd=None if b.sc is not None else g)
+            g = prev.view(prev.dz, nb)
+        P.stem.wgrad(x, nb, ws)
 
     def _sgd(self) -> None:
         c, fs = self.cfg, self.fs

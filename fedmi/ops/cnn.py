@@ -100,7 +100,8 @@ def bn_apply(z: torch.Tensor, a: BNParams, y: torch.Tensor, train: bool, relu: b
 def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Tensor, dbeta_a: torch.Tensor,
            dza: torch.Tensor, red: torch.Tensor, dyb: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None,
            zb: Optional[torch.Tensor] = None, b: Optional[BNParams] = None, dgamma_b=None, dbeta_b=None, dzb=None,
-           gout: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> None:
+           gout: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
+           dadd: Optional[torch.Tensor] = None) -> None:
     """BatchNorm backward through an optional ReLU mask (``y``: forward output) for one or two BN
     branches sharing the incoming grad g = dya (+ dyb).  Writes dz for each branch, dgamma/dbeta,
     and optionally g itself (``gout``, the identity-shortcut grad).  ``red``: [3, C] fp32 channel
@@ -112,7 +113,8 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
     if red.numel() < 3 * C:
         raise ValueError("bn_bwd: scratch too small")
     d = dict(dya=_p(dya), dyb=_p(dyb), y=_p(y), za=_p(za), meanA=_p(a.smean), invA=_p(a.sinv), gammaA=_p(a.gamma),
-             dgammaA=_p(dgamma_a), dbetaA=_p(dbeta_a), dza=_p(dza), gout=_p(gout), shiftA=_p(a.shift))
+             dgammaA=_p(dgamma_a), dbetaA=_p(dbeta_a), dza=_p(dza), gout=_p(gout), shiftA=_p(a.shift),
+             dadd=_p(dadd))
     if zb is not None:
         d.update(zb=_p(zb), meanB=_p(b.smean), invB=_p(b.sinv), gammaB=_p(b.gamma), dgammaB=_p(dgamma_b),
                  dbetaB=_p(dbeta_b), dzb=_p(dzb), shiftB=_p(b.shift))

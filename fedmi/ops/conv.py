@@ -101,8 +101,10 @@ def _ws_args(ws: Optional[torch.Tensor]):
 
 def conv2d_fwd(x: torch.Tensor, wrsc: torch.Tensor, stride: int, pad: int, Cw: Optional[int] = None,
                stats: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-               shift: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y[N,P,Q,O] = conv(x[N,H,W,C]); ``stats`` ([STAT_REP, 2, O] fp32, :func:`stats_buffer`) +=
+               shift: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
+               res: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y[N,P,Q,O] = conv(x[N,H,W,C]) (+ ``res`` [N,P,Q,O] bf16, fused into the epilogue: pre-activation
+    residual blocks; needs C % 64 == 0); ``stats`` ([STAT_REP, 2, O] fp32, :func:`stats_buffer`) +=
     per-channel sum / sum of squares of (y - shift) (``shift``: [O] fp32 or None = 0).  ``ws`` (fp32): optional split-K workspace for
     deep-K / few-tile shapes (see :func:`fd_ws_floats`)."""
     _check(x, torch.bfloat16, "conv2d_fwd.x")
@@ -117,9 +119,14 @@ def conv2d_fwd(x: torch.Tensor, wrsc: torch.Tensor, stride: int, pad: int, Cw: O
     elif tuple(out.shape) != (N, P, Q, O):
         raise ValueError("conv2d_fwd: bad out shape")
     _check_stats(stats, O, "conv2d_fwd")
+    if res is not None:
+        _check(res, torch.bfloat16, "conv2d_fwd.res")
+        if tuple(res.shape) != (N, P, Q, O) or C % 64:
+            raise ValueError("conv2d_fwd: res must be [N,P,Q,O] and the input C % 64 == 0")
     native.require().conv_fwd(native.stream_handle(x.device), shp, x.data_ptr(), wrsc.data_ptr(), out.data_ptr(),
                               stats.data_ptr() if stats is not None else 0,
-                              shift.data_ptr() if shift is not None else 0, *_ws_args(ws))
+                              shift.data_ptr() if shift is not None else 0, *_ws_args(ws),
+                              res.data_ptr() if res is not None else 0)
     return out
 
 

@@ -80,9 +80,11 @@ def _stats_add(stats, y_bf16_nhwc, shift=None):
 
 
 @torch.no_grad()
-def conv2d_fwd(x, wrsc, stride, pad, Cw=None, stats=None, out=None, shift=None, ws=None):
+def conv2d_fwd(x, wrsc, stride, pad, Cw=None, stats=None, out=None, shift=None, ws=None, res=None):
     Cw = Cw or x.shape[3]
     y = F.conv2d(_nchw(x)[:, :Cw], _w_from_img(wrsc, Cw), stride=stride, padding=pad)
+    if res is not None:
+        y = y + _nchw(res)
     if out is None:
         out = torch.empty(y.shape[0], y.shape[2], y.shape[3], y.shape[1], dtype=_BF, device=x.device)
     _nhwc_into(out, y)
@@ -236,7 +238,7 @@ def maxpool2_bwd(x, dy, out=None):
 
 @torch.no_grad()
 def bn_bwd(dya, za, a, dgamma_a, dbeta_a, dza, red, dyb=None, y=None, zb=None, b=None, dgamma_b=None,
-           dbeta_b=None, dzb=None, gout=None, ws=None):
+           dbeta_b=None, dzb=None, gout=None, ws=None, dadd=None):
     C = za.shape[-1]
     M = za.numel() // C
     g = dya.float().reshape(M, C)
@@ -257,6 +259,8 @@ def bn_bwd(dya, za, a, dgamma_a, dbeta_a, dza, red, dyb=None, y=None, zb=None, b
         if p.shift is not None:
             p.shift.copy_(p.smean)
         d = p.gamma * p.sinv * (g - sg / M - xhat * sgx / M)
+        if dadd is not None and z is za:
+            d = d + dadd.float().reshape(M, C)
         dz.copy_(d.reshape(dz.shape).to(dz.dtype))
 
 

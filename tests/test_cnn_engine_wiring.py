@@ -21,7 +21,8 @@ def _cos(a, b):
     return float(F.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0))
 
 
-@pytest.mark.parametrize("name", ["ResNet18", "ResNet50", "MobileNet", "MobileNetV2", "VGG11"])
+@pytest.mark.parametrize("name", ["ResNet18", "ResNet50", "MobileNet", "MobileNetV2", "VGG11", "PreActResNet18",
+                                  "PreActResNet50"])
 def test_engine_schedule_matches_autograd(name):
     from fedmi.engine.cnn_native import CNNNativeTrainer
 
@@ -66,7 +67,7 @@ def test_engine_schedule_matches_autograd(name):
             assert int(bufs[k]) == int(b), k
 
 
-@pytest.mark.parametrize("name", ["ResNet18", "MobileNetV2", "VGG11"])
+@pytest.mark.parametrize("name", ["ResNet18", "MobileNetV2", "VGG11", "PreActResNet18"])
 def test_engine_eval_matches_torch_eval(name):
     """Eval mode (BN from running statistics) through the engine schedule == torch .eval()."""
     from fedmi.engine.cnn_native import CNNNativeTrainer

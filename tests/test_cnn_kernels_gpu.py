@@ -394,3 +394,47 @@ def test_bn_conv_bias_folding(gpu_device):
     refe = (zb - rm) / torch.sqrt(rv + 1e-5) * g + be
     torch.cuda.synchronize()
     assert _rel(ye.float(), refe) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(16, 16, 16, 64, 64, 3, 1, 1), (128, 4, 4, 512, 512, 3, 1, 1)],
+                         ids=["single", "splitk"])
+def test_conv_fwd_fused_residual(gpu_device, shape):
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device, seed=13)
+    wr = conv.pack_weight(w)
+    ref = _nhwc(F.conv2d(x, wb, stride=st, padding=pad))
+    res = torch.randn_like(ref).bfloat16()
+    shp = (xn.shape, O, R, R, st, pad, Cw)
+    ws = torch.empty(max(conv.fd_ws_floats(*shp), 1), device=gpu_device)
+    rep = conv.stats_buffer(O, gpu_device)
+    y = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=rep, ws=ws, res=res)
+    torch.cuda.synchronize()
+    want = ref + res.float()
+    assert _rel(y.float(), want) < 1e-2
+    tot = conv.stats_total(rep)
+    yb = y.float()
+    assert torch.allclose(tot[0], yb.sum((0, 1, 2)), rtol=1e-3, atol=1e-1)
+
+
+def test_bn_bwd_additive_residual_grad(gpu_device):
+    torch.manual_seed(14)
+    dev = gpu_device
+    M, C = 1024, 64
+    z = torch.randn(M, C, device=dev).bfloat16()
+    g, be = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+    rep = conv.stats_buffer(C, dev)
+    rep[0, 0], rep[0, 1] = z.float().sum(0), (z.float() ** 2).sum(0)
+    sm, si = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    A = cnn.bn_desc(rep, g, be, None, None, None, sm, si)
+    y = torch.empty_like(z)
+    cnn.bn_apply(z, A, y, train=True, relu=True)
+    dy = torch.randn(M, C, device=dev).bfloat16()
+    extra = torch.randn(M, C, device=dev).bfloat16()
+    d1, d2 = torch.empty_like(z), torch.empty_like(z)
+    dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    ws = torch.zeros(cnn.bn_bwd_ws_floats(M, C), device=dev)
+    red = torch.empty(3, C, device=dev)
+    cnn.bn_bwd(dy, z, A, dg, db, d1, red, y=y, ws=ws)
+    cnn.bn_bwd(dy, z, A, dg, db, d2, red, y=y, ws=ws, dadd=extra)
+    torch.cuda.synchronize()
+    assert _rel(d2.float() - extra.float(), d1.float()) < 2e-2
