@@ -130,6 +130,8 @@ static void fedmi_bind(py::module_& m) {
              e.eval(S(st), P<const uint8_t>(images), P<const int>(labels), n);
            }, py::call_guard<py::gil_scoped_release>())
       .def("pack", [](LeNetEngine& e, uintptr_t st) { e.pack(S(st)); }, py::call_guard<py::gil_scoped_release>())
+      .def("set_fuse_fc1", &LeNetEngine::set_fuse_fc1)
+      .def("fuse_fc1", &LeNetEngine::fuse_fc1)
       .def("set_sgd", [](LeNetEngine& e, float lr, float m, float wd) {
              SgdConfig c; c.lr = lr; c.momentum = m; c.weight_decay = wd; e.set_sgd(c);
            })
@@ -144,11 +146,12 @@ static void fedmi_bind(py::module_& m) {
                           P<uint8_t>(am1), P<uint8_t>(am2), P<lenet::Stats>(zero_stats));
     check_last("lenet_conv_fwd");
   });
-  // FC head = fc1 forward (tiled) + FC tail; kept as one entry point for the tests
+  // FC head = fc1 forward (tiled) + FC tail; kept as one entry point for the tests.
+  // h1 == 0: the fused variant (fc1 inside the tail, no K2a launch)
   m.def("lenet_fc_head", [](uintptr_t st, uintptr_t act2, uintptr_t labels, int nb, int train, uintptr_t pk,
                             uintptr_t params, uintptr_t h1, uintptr_t dact2, uintptr_t dZ1T, uintptr_t fc_slab,
                             uintptr_t stats) {
-    launch_lenet_fc1_fwd(S(st), P<const bf16>(act2), nb, P<const bf16>(pk), P<const float>(params), P<bf16>(h1));
+    if (h1) launch_lenet_fc1_fwd(S(st), P<const bf16>(act2), nb, P<const bf16>(pk), P<const float>(params), P<bf16>(h1));
     launch_lenet_fc_tail(S(st), P<const bf16>(h1), P<const bf16>(act2), P<const int>(labels), nb, train,
                          P<const bf16>(pk), P<const float>(params), P<float>(dact2), P<bf16>(dZ1T),
                          P<float>(fc_slab), P<lenet::Stats>(stats));

@@ -300,8 +300,12 @@ __global__ __launch_bounds__(256) void lenet_fc1_fwd(
 //        pool2 ReLU) -> d(pool2) for K3.
 // Every global operand is prefetched into registers at entry.
 // ---------------------------------------------------------------------------
+// FUSE_FC1: the tail computes H1 = relu(X W1^T + b1) for its 16 samples itself
+// (act2 tile -> LDS, this wave's 16 W1 rows -> 13 register fragments at entry)
+// instead of reading K2a's output: one launch and one H1 round trip fewer.
+template <bool FUSE_FC1>
 __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
-    const bf16* __restrict__ h1,     // [nb][128]  relu(fc1) from K2a
+    const bf16* __restrict__ h1,     // [nb][128]  relu(fc1) from K2a (unused with FUSE_FC1)
     const bf16* __restrict__ act2,   // [nb][F0P]  (for the dX mask)
     const int* __restrict__ labels,  // labels of this batch (already offset)
     int nb, int train,
@@ -318,6 +322,8 @@ __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
   __shared__ __attribute__((aligned(16))) bf16 sdZ1[16 * 128];
   __shared__ float sZ[16 * 16];
   __shared__ float sdb[128 + 96 + 16];
+  constexpr int SX_LD = F0P + 8;                   // act2 tile row stride (bank spread)
+  __shared__ __attribute__((aligned(16))) bf16 sX[FUSE_FC1 ? 16 * SX_LD : 8];
 
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
   const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
@@ -329,14 +335,32 @@ __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
   const bool lead = q == 0;                        // publishes stats, slabs and dZ1^T
   FEDMI_STAMP(1, 0);
 
-  // ---- prefetch: H1 tile, fc2/fc3 weights + biases, backward weights, dX tile + mask
+  // ---- prefetch: H1 tile (or act2 tile + W1 fragments), fc2/fc3 weights + biases,
+  //      backward weights, dX tile + mask
   uint4 h1v = make_uint4(0, 0, 0, 0);
-  if (tid < 16 * 128 / 8) {
+  constexpr int XCH = F0P / 8;                     // 52 16-B chunks per act2 row
+  uint4 xv[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+  bf16x8 w1f[FUSE_FC1 ? 13 : 1];
+  const int nf1 = wave * 16 + n16;
+  float b1 = 0.f;
+  if constexpr (FUSE_FC1) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * NT_FC;
+      if (e < 16 * XCH) {
+        const int r = e / XCH;
+        xv[u] = reinterpret_cast<const uint4*>(act2 + (size_t)(s0 + min(r, ns - 1)) * F0P)[e - r * XCH];
+        if (r >= ns) xv[u] = make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 13; ++ks) w1f[ks] = ld8(pk + PK_FC1 + nf1 * F0P + ks * 32 + kq);
+    b1 = params[P_F1B + min(nf1, F1 - 1)];
+  } else if (tid < 16 * 128 / 8) {
     const int r = tid >> 4;
     h1v = reinterpret_cast<const uint4*>(h1 + (size_t)(s0 + min(r, ns - 1)) * 128)[tid & 15];
     if (r >= ns) h1v = make_uint4(0, 0, 0, 0);
   }
-  const int nf1 = wave * 16 + n16;
   const int nf2 = (wave < 6 ? wave : 0) * 16 + n16;
   const float b2 = params[P_F2B + min(nf2, F2 - 1)];
   const float b3 = params[P_F3B + min(n16, NCLS - 1)];
@@ -368,7 +392,29 @@ __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
   zero_lds(sdZ3T, sizeof(sdZ3T));
   zero_lds(sdZ2T, sizeof(sdZ2T));
   for (int e = tid; e < 240; e += NT_FC) sdb[e] = 0.f;
-  if (tid < 16 * 128 / 8) reinterpret_cast<uint4*>(sH1)[tid] = h1v;
+  if constexpr (FUSE_FC1) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * NT_FC;
+      if (e < 16 * XCH) {
+        const int r = e / XCH;
+        *reinterpret_cast<uint4*>(sX + r * SX_LD + (e - r * XCH) * 8) = xv[u];
+      }
+    }
+    __syncthreads();
+    // fc1 fwd: wave -> 16 output columns, K = 416 (13 steps)
+    const bf16* xa = sX + n16 * SX_LD + kq;
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int ks = 0; ks < 13; ++ks) acc = mfma16(ld8(xa + ks * 32), w1f[ks], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int sr = rq + r;
+      sH1[sr * 128 + nf1] = (bf16)((nf1 < F1 && sr < ns) ? fmaxf(acc[r] + b1, 0.f) : 0.f);
+    }
+  } else {
+    if (tid < 16 * 128 / 8) reinterpret_cast<uint4*>(sH1)[tid] = h1v;
+  }
   __syncthreads();
   for (int e = tid; e < 16 * 128; e += NT_FC) {       // sample-contiguous copy for the dW2 GEMM
     const int r = e >> 7, c = e & 127;
@@ -932,13 +978,18 @@ void launch_lenet_fc1_fwd(hipStream_t st, const bf16* act2, int nb, const bf16* 
   hipLaunchKernelGGL(lenet_fc1_fwd, dim3(mtiles * 8), dim3(256), 0, st, act2, nb, pk, params, h1);
 }
 
+// h1 == nullptr: the tail computes fc1 itself (FUSE_FC1 variant, K2a not launched)
 void launch_lenet_fc_tail(hipStream_t st, const bf16* h1, const bf16* act2, const int* labels, int nb, int train,
                           const bf16* pk, const float* params, float* dact2, bf16* dZ1T, float* fc_slab,
                           Stats* stats) {
   if (nb <= 0) return;
   const int mtiles = (nb + FC_SPW - 1) / FC_SPW;
-  hipLaunchKernelGGL(lenet_fc_tail, dim3(mtiles * (train ? 4 : 1)), dim3(NT_FC), 0, st, h1, act2, labels, nb, train,
-                     pk, params, dact2, dZ1T, fc_slab, stats);
+  if (h1 == nullptr)
+    hipLaunchKernelGGL(lenet_fc_tail<true>, dim3(mtiles * (train ? 4 : 1)), dim3(NT_FC), 0, st, h1, act2, labels, nb,
+                       train, pk, params, dact2, dZ1T, fc_slab, stats);
+  else
+    hipLaunchKernelGGL(lenet_fc_tail<false>, dim3(mtiles * (train ? 4 : 1)), dim3(NT_FC), 0, st, h1, act2, labels, nb,
+                       train, pk, params, dact2, dZ1T, fc_slab, stats);
 }
 
 void launch_lenet_conv_bwd(hipStream_t st, const uint8_t* images, int sample_base, int nb,

@@ -56,6 +56,13 @@ void LeNetEngine::set_schedule(const std::vector<int>& starts, const std::vector
   drop_graph();
 }
 
+void LeNetEngine::set_fuse_fc1(bool on) {
+  if (on != fuse_fc1_) {
+    fuse_fc1_ = on;
+    drop_graph();
+  }
+}
+
 void LeNetEngine::set_sgd(SgdConfig sgd) {
   sgd_ = sgd;
   drop_graph();
@@ -68,9 +75,9 @@ void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round, bool 
   const int aug = augment_ ? 1 : 0;
   launch_lenet_conv_fwd(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug, b_.act2,
                         b_.act2T, MAX_TRAIN_BATCH, b_.pool1, b_.am1, b_.am2, reset_stats ? b_.train_stats : nullptr);
-  launch_lenet_fc1_fwd(st, b_.act2, nb, b_.pk, b_.params, b_.h1);
-  launch_lenet_fc_tail(st, b_.h1, b_.act2, b_.train_labels + start, nb, 1, b_.pk, b_.params, b_.dact2, b_.dZ1T,
-                       b_.fc_slab, b_.train_stats);
+  if (!fuse_fc1_) launch_lenet_fc1_fwd(st, b_.act2, nb, b_.pk, b_.params, b_.h1);
+  launch_lenet_fc_tail(st, fuse_fc1_ ? nullptr : b_.h1, b_.act2, b_.train_labels + start, nb, 1, b_.pk, b_.params,
+                       b_.dact2, b_.dZ1T, b_.fc_slab, b_.train_stats);
   launch_lenet_conv_bwd(st, b_.train_images, start, nb, seed_, b_.round_ctr, aug, b_.dact2, b_.act2T, b_.dZ1T,
                         b_.pool1, b_.am1, b_.am2, b_.pk, b_.conv_slab, b_.fc1w_grad);
   launch_lenet_sgd(st, b_.params, b_.mom, b_.pk, b_.conv_slab, nb, b_.fc1w_grad, b_.fc_slab,
@@ -114,8 +121,9 @@ void LeNetEngine::eval(hipStream_t st, const uint8_t* images, const int* labels,
   if (n <= 0 || n > b_.act2_rows) throw std::invalid_argument("LeNetEngine::eval: n exceeds act2 capacity");
   launch_lenet_conv_fwd(st, images, 0, n, b_.pk, b_.params, seed_, b_.round_ctr, 0, b_.act2, nullptr, 0,
                         nullptr, nullptr, nullptr, b_.eval_stats);
-  launch_lenet_fc1_fwd(st, b_.act2, n, b_.pk, b_.params, b_.h1);
-  launch_lenet_fc_tail(st, b_.h1, b_.act2, labels, n, 0, b_.pk, b_.params, nullptr, nullptr, nullptr, b_.eval_stats);
+  if (!fuse_fc1_) launch_lenet_fc1_fwd(st, b_.act2, n, b_.pk, b_.params, b_.h1);
+  launch_lenet_fc_tail(st, fuse_fc1_ ? nullptr : b_.h1, b_.act2, labels, n, 0, b_.pk, b_.params, nullptr, nullptr,
+                       nullptr, b_.eval_stats);
   check_hip(hipGetLastError(), "LeNetEngine::eval launch");
 }
 

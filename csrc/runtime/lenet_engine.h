@@ -62,6 +62,9 @@ class LeNetEngine {
   // Refresh the packed bf16 images from the fp32 master (after FedAvg/load).
   void pack(hipStream_t st);
   void set_sgd(SgdConfig sgd);
+  // fc1 computed inside the FC-tail kernel (4 launches per step) instead of its own kernel (5)
+  void set_fuse_fc1(bool on);
+  bool fuse_fc1() const { return fuse_fc1_; }
   bool graph_ready() const { return exec_ != nullptr; }
 
  private:
@@ -72,6 +75,7 @@ class LeNetEngine {
   SgdConfig sgd_;
   uint32_t seed_;
   bool augment_;
+  bool fuse_fc1_ = false;
   std::vector<int> starts_, sizes_;
   hipStream_t cap_stream_ = nullptr;
   hipGraph_t graph_ = nullptr;

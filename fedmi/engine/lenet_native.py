@@ -13,6 +13,8 @@ from collections import OrderedDict
 from typing import List, Optional
 
 import dataclasses
+import os
+
 import torch
 
 from .. import native
@@ -83,6 +85,8 @@ class LeNetNativeTrainer(LocalTrainer):
             round_ctr=_ptr(self.round_ctr))
         self.engine = nat.LeNetEngine(self._bufs, cfg.lr, cfg.momentum, cfg.weight_decay, cfg.seed & 0xFFFFFFFF,
                                       bool(data.augment and cfg.augment))
+        self.fuse_fc1 = os.environ.get("FEDMI_LENET_FUSE_FC1", "1") == "1"
+        self.engine.set_fuse_fc1(self.fuse_fc1)
         self._views = ordered_views(self.params, LENET_SPEC)
         if init_state is None:
             torch.manual_seed(cfg.seed)
@@ -133,6 +137,7 @@ class LeNetNativeTrainer(LocalTrainer):
                           n_train=len(self.train_set))
         self.engine = self._nat.LeNetEngine(self._bufs, self.cfg.lr, self.cfg.momentum, self.cfg.weight_decay,
                                             self.cfg.seed & 0xFFFFFFFF, bool(self.cfg.augment))
+        self.engine.set_fuse_fc1(self.fuse_fc1)
         self._starts, self._sizes = [], []
 
     # ---- compute ----------------------------------------------------------------
@@ -163,6 +168,11 @@ class LeNetNativeTrainer(LocalTrainer):
 
     def eval_stats(self) -> EpochStats:
         return self._read_stats(1)
+
+    def set_fuse_fc1(self, on: bool) -> None:
+        """fc1 inside the FC-tail kernel (default) or as its own kernel (the graph is re-captured)."""
+        self.fuse_fc1 = bool(on)
+        self.engine.set_fuse_fc1(self.fuse_fc1)
 
     def reset_momentum(self) -> None:
         self.mom.zero_()
