@@ -21,7 +21,7 @@ struct ConvShape {
 };
 void launch_conv_fwd(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, const float*, float*, long,
                      const bf16*);
-void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, long, const bf16*);
+void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, long, const bf16*, int);
 struct DPackItem {
   const float* w;
   bf16* wd;
@@ -44,6 +44,8 @@ struct BNDesc {
   float* smean; float* sinv; const float* shift; const float* cbias;
 };
 void launch_maxpool2(hipStream_t, const bf16*, bf16*, int, int, int, int);
+void launch_maxpool3(hipStream_t, const bf16*, bf16*, uint8_t*, int, int, int, int, int);
+void launch_maxpool3_bwd(hipStream_t, const bf16*, const uint8_t*, bf16*, int, int, int, int, int, int);
 void launch_maxpool2_bwd(hipStream_t, const bf16*, const bf16*, bf16*, int, int, int, int);
 struct BNBwdDesc {
   const bf16* dya; const bf16* dyb; const bf16* y;
@@ -63,8 +65,8 @@ void launch_dw_wgrad(hipStream_t, const DwShape&, const bf16*, const bf16*, floa
 void launch_prep_input(hipStream_t, const uint8_t*, int, const int*, int, int, uint32_t, const int*, bf16*);
 void launch_sched_next(hipStream_t, const int*, int*, int*);
 void launch_bn_apply(hipStream_t, const bf16*, const BNDesc&, const bf16*, const BNDesc*, const bf16*, bf16*, int, int,
-                     float, float, int, int);
-void launch_bn_bwd(hipStream_t, const BNBwdDesc&, float*, int, int, float*, long);
+                     float, float, int, int, int);
+void launch_bn_bwd(hipStream_t, const BNBwdDesc&, float*, int, int, float*, long, int, int);
 long bn_bwd_ws_floats(int, int);
 void launch_head(hipStream_t, const bf16*, const int*, int, const int*, int, int, int, int, const float*,
                  const float*, float*, float*, bf16*, float*, float*, float*, int);
@@ -120,12 +122,12 @@ void fedmi_bind_cnn(py::module_& m) {
   }, py::arg("st"), py::arg("shape"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("shift"),
      py::arg("ws") = 0, py::arg("ws_floats") = 0, py::arg("res") = 0);
   m.def("conv_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
-                         long ws_floats, uintptr_t wd) {
+                         long ws_floats, uintptr_t wd, int acc) {
     launch_conv_dgrad(S(st), shape_from(shp), P<const bf16>(dy), P<const bf16>(w), P<bf16>(dx), P<float>(ws),
-                      ws ? ws_floats : 0, P<const bf16>(wd));
+                      ws ? ws_floats : 0, P<const bf16>(wd), acc);
     check("conv_dgrad");
   }, py::arg("st"), py::arg("shape"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("ws") = 0,
-     py::arg("ws_floats") = 0, py::arg("wd") = 0);
+     py::arg("ws_floats") = 0, py::arg("wd") = 0, py::arg("acc") = 0);
   m.def("dgrad_pack_multi", [](uintptr_t st, const py::list& items) {
     std::vector<DPackItem> v;
     for (const auto& it : items) {
@@ -184,6 +186,15 @@ void fedmi_bind_cnn(py::module_& m) {
                       P<const int>(round_ctr), P<bf16>(out));
     check("prep_input");
   });
+  m.def("maxpool3", [](uintptr_t st, uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int stride) {
+    launch_maxpool3(S(st), P<const bf16>(x), P<bf16>(y), P<uint8_t>(idx), N, H, W, C, stride);
+    check("maxpool3");
+  });
+  m.def("maxpool3_bwd", [](uintptr_t st, uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int H, int W, int C,
+                           int stride, int acc) {
+    launch_maxpool3_bwd(S(st), P<const bf16>(dy), P<const uint8_t>(idx), P<bf16>(dx), N, H, W, C, stride, acc);
+    check("maxpool3_bwd");
+  });
   m.def("maxpool2", [](uintptr_t st, uintptr_t x, uintptr_t y, int N, int H, int W, int C) {
     launch_maxpool2(S(st), P<const bf16>(x), P<bf16>(y), N, H, W, C);
     check("maxpool2");
@@ -197,16 +208,18 @@ void fedmi_bind_cnn(py::module_& m) {
     check("sched_next");
   });
   m.def("bn_apply", [](uintptr_t st, uintptr_t z, const py::dict& a, uintptr_t z2, py::object b, uintptr_t res,
-                       uintptr_t y, int M, int C, float eps, float mom, int train, int relu) {
+                       uintptr_t y, int M, int C, float eps, float mom, int train, int relu, int ldy) {
     BNDesc bd{};
     const bool has_b = !b.is_none();
     if (has_b) bd = bn_from(b.cast<py::dict>());
     launch_bn_apply(S(st), P<const bf16>(z), bn_from(a), P<const bf16>(z2), has_b ? &bd : nullptr, P<const bf16>(res),
-                    P<bf16>(y), M, C, eps, mom, train, relu);
+                    P<bf16>(y), M, C, eps, mom, train, relu, ldy);
     check("bn_apply");
-  });
+  }, py::arg("st"), py::arg("z"), py::arg("a"), py::arg("z2"), py::arg("b"), py::arg("res"), py::arg("y"), py::arg("M"),
+     py::arg("C"), py::arg("eps"), py::arg("mom"), py::arg("train"), py::arg("relu"), py::arg("ldy") = 0);
   m.def("bn_bwd_ws_floats", [](int M, int C) { return bn_bwd_ws_floats(M, C); });
-  m.def("bn_bwd", [](uintptr_t st, const py::dict& d, uintptr_t red, int M, int C, uintptr_t ws, long ws_floats) {
+  m.def("bn_bwd", [](uintptr_t st, const py::dict& d, uintptr_t red, int M, int C, uintptr_t ws, long ws_floats,
+                     int ldd, int ldy) {
     BNBwdDesc b{P<const bf16>(dget(d, "dya")),     P<const bf16>(dget(d, "dyb")),     P<const bf16>(dget(d, "y")),
                 P<const bf16>(dget(d, "za")),      P<const float>(dget(d, "meanA")),  P<const float>(dget(d, "invA")),
                 P<const float>(dget(d, "gammaA")), P<float>(dget(d, "dgammaA")),      P<float>(dget(d, "dbetaA")),
@@ -215,10 +228,10 @@ void fedmi_bind_cnn(py::module_& m) {
                 P<float>(dget(d, "dbetaB")),       P<bf16>(dget(d, "dzb")),           P<bf16>(dget(d, "gout")),
                 P<float>(dget(d, "shiftA")),       P<float>(dget(d, "shiftB")),       P<const bf16>(dget(d, "dadd"))};
     if (!b.dya || !b.za || !b.meanA || !b.invA || !b.gammaA || !b.dza) throw std::invalid_argument("bn_bwd: missing A");
-    launch_bn_bwd(S(st), b, P<float>(red), M, C, P<float>(ws), ws ? ws_floats : 0);
+    launch_bn_bwd(S(st), b, P<float>(red), M, C, P<float>(ws), ws ? ws_floats : 0, ldd, ldy);
     check("bn_bwd");
   }, py::arg("st"), py::arg("desc"), py::arg("red"), py::arg("M"), py::arg("C"), py::arg("ws") = 0,
-     py::arg("ws_floats") = 0);
+     py::arg("ws_floats") = 0, py::arg("ldd") = 0, py::arg("ldy") = 0);
   m.def("head", [](uintptr_t st, uintptr_t y, uintptr_t labels, int base, uintptr_t dbase, int N, int HW, int C, int J,
                    uintptr_t W, uintptr_t b, uintptr_t pooled, uintptr_t dlog, uintptr_t dy, uintptr_t stats,
                    uintptr_t dW, uintptr_t db, int train) {

@@ -124,10 +124,11 @@ FEDMI_DEV void bn_coeffs(const BNArgs& a, int C, int M, float eps, float mom, in
 }
 
 // y = act(bnA(z) [+ res | + bnB(z2)])      res_mode: 0 none, 1 identity residual, 2 second BN branch
+// y rows have stride ldy (>= C): a channel slice of a concatenated output (GoogLeNet)
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ z, BNArgs A, const bf16* __restrict__ z2,
                                                        BNArgs B, const bf16* __restrict__ res, bf16* __restrict__ y,
                                                        int M, int C, float eps, float mom, int train, int relu,
-                                                       int res_mode) {
+                                                       int res_mode, int ldy) {
   extern __shared__ float co[];   // [4][C]
   float* sc = co;
   float* sh = co + C;
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
     }
-    store8f(y + i * 8, v);
+    store8f(y + (ldy == C ? i * 8 : (i / VR) * ldy + c0), v);
   }
 }
 
@@ -178,19 +179,23 @@ struct BwdIn {
   const bf16* zb;         // optional second BN branch (projection shortcut)
   const float* meanB;
   const float* invB;
+  int ldd;                // row stride of dya / dyb (elements; C = compact)
+  int ldy;                // row stride of y
 };
 
-FEDMI_DEV void load_g(const BwdIn& in, long i, float* g) {
-  load8f(in.dya + i * 8, g);
+// row r, channel group cg (8 channels)
+FEDMI_DEV void load_g(const BwdIn& in, long r, int cg, float* g) {
+  const long od = r * in.ldd + cg * 8;
+  load8f(in.dya + od, g);
   if (in.dyb) {
     float t[8];
-    load8f(in.dyb + i * 8, t);
+    load8f(in.dyb + od, t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] += t[j];
   }
   if (in.y) {
     float t[8];
-    load8f(in.y + i * 8, t);
+    load8f(in.y + r * in.ldy + cg * 8, t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = t[j] > 0.f ? g[j] : 0.f;
   }
@@ -219,7 +224,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BwdIn in, float* __r
   for (int r = rb + r0; r < re; r += rstep) {
     const long i = (long)r * VR + cg;
     float g[8], z[8];
-    load_g(in, i, g);
+    load_g(in, r, cg, g);
     load8f(in.za + i * 8, z);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -318,7 +323,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdIn in, BwdOut out,
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
     const int c0 = (int)(i % VR) * 8;
     float g[8], z[8], d[8];
-    load_g(in, i, g);
+    load_g(in, i / VR, c0 >> 3, g);
     if (out.gout) store8f(out.gout + i * 8, g);
     load8f(in.za + i * 8, z);
 #pragma unroll
@@ -517,6 +522,101 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const bf16* __restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// MaxPool2d(3, stride 1|2, padding 1) on NHWC bf16 (GoogLeNet branch 4 and its
+// stage pools, src/models/googlenet.py:27-30, 79): forward saves the window
+// argmax (tap 0..8, first maximum as max_pool2d_with_indices, padding never
+// wins) as one byte per output element; backward is a gather over the <= 9
+// windows covering each input pixel (no atomics), optionally accumulating into
+// dx (the branch's share of a fan-in gradient).
+__global__ __launch_bounds__(256) void maxpool3_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                           uint8_t* __restrict__ idx, int N, int H, int W, int C,
+                                                           int st, int P, int Q) {
+  const int VC = C >> 3;
+  const uint32_t total = (uint32_t)N * P * Q * VC;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t pix = i / VC;
+    const int c0 = (int)(i - pix * VC) * 8;
+    const uint32_t t = pix / Q;
+    const int q = (int)(pix - t * Q);
+    const int n = (int)(t / P), p = (int)(t - (uint32_t)n * P);
+    float best[8];
+    int am[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; am[j] = 0; }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int h = p * st - 1 + r;
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) {
+        const int w = q * st - 1 + s2;
+        if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) continue;
+        const bf16x8v v = *reinterpret_cast<const bf16x8v*>(x + (((long)n * H + h) * W + w) * C + c0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if ((float)v[j] > best[j]) { best[j] = (float)v[j]; am[j] = r * 3 + s2; }
+      }
+    }
+    bf16x8v o;
+    uint64_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = (bf16)best[j];
+      packed |= (uint64_t)am[j] << (8 * j);
+    }
+    *reinterpret_cast<bf16x8v*>(y + (long)pix * C + c0) = o;
+    *reinterpret_cast<uint64_t*>(idx + (long)pix * C + c0) = packed;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool3_bwd_kernel(const bf16* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                           bf16* __restrict__ dx, int N, int H, int W, int C, int st,
+                                                           int P, int Q, int acc) {
+  const int VC = C >> 3;
+  const uint32_t total = (uint32_t)N * H * W * VC;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t pix = i / VC;
+    const int c0 = (int)(i - pix * VC) * 8;
+    const uint32_t t = pix / W;
+    const int w = (int)(pix - t * W);
+    const int n = (int)(t / H), h = (int)(t - (uint32_t)n * H);
+    float g[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int ph = h + 1 - r;              // = p * st
+      if (ph < 0 || ph % st) continue;
+      const int p = ph / st;
+      if (p >= P) continue;
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) {
+        const int qw = w + 1 - s2;
+        if (qw < 0 || qw % st) continue;
+        const int q = qw / st;
+        if (q >= Q) continue;
+        const long o = (((long)n * P + p) * Q + q) * C + c0;
+        const uint64_t packed = *reinterpret_cast<const uint64_t*>(idx + o);
+        const bf16x8v d = *reinterpret_cast<const bf16x8v*>(dy + o);
+        const int tap = r * 3 + s2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if ((int)((packed >> (8 * j)) & 0xff) == tap) g[j] += (float)d[j];
+      }
+    }
+    bf16* dst = dx + (long)pix * C + c0;
+    if (acc) {
+      const bf16x8v e = *reinterpret_cast<const bf16x8v*>(dst);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] += (float)e[j];
+    }
+    bf16x8v o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)g[j];
+    *reinterpret_cast<bf16x8v*>(dst) = o;
+  }
+}
+
 // cur[0] = sched[counter[0]++]  (first node of a captured training step)
 __global__ void sched_next_kernel(const int* __restrict__ sched, int* __restrict__ counter, int* __restrict__ cur) {
   if (threadIdx.x == 0) {
@@ -539,6 +639,21 @@ struct BNDesc {
 
 static BNArgs to_args(const BNDesc& d) {
   return BNArgs{d.stats, d.gamma, d.beta, d.rmean, d.rvar, d.nbt, d.smean, d.sinv, d.shift, d.cbias};
+}
+
+void launch_maxpool3(hipStream_t st, const bf16* x, bf16* y, uint8_t* idx, int N, int H, int W, int C, int stride) {
+  if (C % 8 || (stride != 1 && stride != 2)) throw std::invalid_argument("maxpool3: need C % 8 == 0, stride 1|2");
+  const int P = (H + 2 - 3) / stride + 1, Q = (W + 2 - 3) / stride + 1;
+  hipLaunchKernelGGL(maxpool3_fwd_kernel, dim3(grid_for((long)N * P * Q * (C / 8))), dim3(256), 0, st, x, y, idx, N, H,
+                     W, C, stride, P, Q);
+}
+
+void launch_maxpool3_bwd(hipStream_t st, const bf16* dy, const uint8_t* idx, bf16* dx, int N, int H, int W, int C,
+                         int stride, int acc) {
+  if (C % 8 || (stride != 1 && stride != 2)) throw std::invalid_argument("maxpool3_bwd: need C % 8 == 0, stride 1|2");
+  const int P = (H + 2 - 3) / stride + 1, Q = (W + 2 - 3) / stride + 1;
+  hipLaunchKernelGGL(maxpool3_bwd_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(256), 0, st, dy, idx, dx, N,
+                     H, W, C, stride, P, Q, acc);
 }
 
 void launch_maxpool2(hipStream_t st, const bf16* x, bf16* y, int N, int H, int W, int C) {
@@ -564,12 +679,14 @@ void launch_sched_next(hipStream_t st, const int* sched, int* counter, int* cur)
 }
 
 void launch_bn_apply(hipStream_t st, const bf16* z, const BNDesc& a, const bf16* z2, const BNDesc* b, const bf16* res,
-                     bf16* y, int M, int C, float eps, float mom, int train, int relu) {
+                     bf16* y, int M, int C, float eps, float mom, int train, int relu, int ldy) {
   if (C % 8) throw std::invalid_argument("bn_apply: C % 8 != 0");
+  if (ldy <= 0) ldy = C;
+  if (ldy < C || ldy % 8) throw std::invalid_argument("bn_apply: bad output row stride");
   const int res_mode = b ? 2 : (res ? 1 : 0);
   const BNArgs bb = b ? to_args(*b) : BNArgs{};
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((long)M * (C / 8))), dim3(256), 4 * C * sizeof(float), st, z,
-                     to_args(a), z2, bb, res, y, M, C, eps, mom, train, relu, res_mode);
+                     to_args(a), z2, bb, res, y, M, C, eps, mom, train, relu, res_mode, ldy);
 }
 
 struct BNBwdDesc {
@@ -600,10 +717,14 @@ long bn_bwd_ws_floats(int M, int C) {
 // red: [3][C] fp32.  With ``ws`` (>= bn_bwd_ws_floats, zero): replica atomics + a
 // finalize launch (red needs no zeroing).  Without: atomics into red, which must
 // be zero on entry.
-void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, float* red, int M, int C, float* ws, long ws_floats) {
+void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, float* red, int M, int C, float* ws, long ws_floats, int ldd,
+                   int ldy) {
   const int VR = C / 8;
   if (C % 8 || VR > 256) throw std::invalid_argument("bn_bwd: need C % 8 == 0 and C <= 2048");
-  BwdIn in{d.dya, d.dyb, d.y, d.za, d.meanA, d.invA, d.zb, d.meanB, d.invB};
+  if (ldd <= 0) ldd = C;
+  if (ldy <= 0) ldy = C;
+  if (ldd < C || ldy < C || ldd % 8 || ldy % 8) throw std::invalid_argument("bn_bwd: bad row strides");
+  BwdIn in{d.dya, d.dyb, d.y, d.za, d.meanA, d.invA, d.zb, d.meanB, d.invB, ldd, ldy};
   BwdOut out{d.dza, d.dzb, d.gout, d.dgammaA, d.dbetaA, d.dgammaB, d.dbetaB, d.gammaA, d.gammaB, d.shiftA, d.shiftB,
              d.dadd};
   int tb, rows_per_block, nblk;

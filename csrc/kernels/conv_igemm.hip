@@ -267,6 +267,7 @@ __global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, co
                                                   float* __restrict__ gout, float* __restrict__ stats,
                                                   const float* __restrict__ shift, ConvGeom g,
                                                   int ksteps_per_split, int partial) {
+  // partial bit 0: fp32 split-K partial into gout; bit 1: out += result (bf16 outputs)
   constexpr int A_IMG = (MODE == WGRAD) ? BK * BM : BM * KC_LD;
   constexpr int B_IMG = (MODE == FWD) ? BN * KC_LD : BK * BN;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
@@ -281,7 +282,7 @@ __global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, co
   const int ksteps = (g.K + BK - 1) / BK;
   const int kb = blockIdx.z * ksteps_per_split;
   const int ke = min(ksteps, kb + ksteps_per_split);
-  if ((MODE == WGRAD || partial) && kb >= ke) return;   // (never launched: every split owns >= 1 step)
+  if ((MODE == WGRAD || (partial & 1)) && kb >= ke) return;   // (never launched: every split owns >= 1 step)
 
   Loader<MODE, BM, BN> L;
   L.init(g, m0, n0, tid);
@@ -328,7 +329,7 @@ __global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, co
 
   // ---- epilogue
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
-  if (MODE == WGRAD || partial) {
+  if (MODE == WGRAD || (partial & 1)) {
     // fp32 partial of this K split -> workspace [split][M][NC] (natural GEMM
     // layout, plain stores).  WGRAD: conv_wgrad_reduce sums the splits and
     // permutes into the PyTorch [O][Cw][R][S] gradient; split-K FWD / DGRAD:
@@ -369,8 +370,15 @@ __global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, co
         const uint32_t hh = fdiv(hw, g.dWp), ww = hw - hh * g.Wp;
         orow = ((long)n * g.H + hh * g.st + g.ph) * g.W + ww * g.st + g.pw;
       }
-      if (m < g.M && col < g.NC)
-        *reinterpret_cast<uint4*>(out + orow * g.NC + col) = *reinterpret_cast<const uint4*>(ct + row * CT_LD + cc * 8);
+      if (m < g.M && col < g.NC) {
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + row * CT_LD + cc * 8);
+        if (partial & 2) {   // accumulate (gradient fan-in of a multi-branch block)
+          const bf16x8 o = *reinterpret_cast<const bf16x8*>(out + orow * g.NC + col);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)o[j]);
+        }
+        *reinterpret_cast<bf16x8*>(out + orow * g.NC + col) = v;
+      }
     }
     if (MODE == FWD && stats != nullptr) {
       // sums of (y - shift[c]): shift = the previous step's batch mean of this
@@ -901,7 +909,7 @@ static void launch_mode(hipStream_t st, const ConvGeom& g, const bf16* x, const 
   const TileCfg t = pick_tiles(g.M, g.NC);
   const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
   const int ksteps = (g.K + BK - 1) / BK;
-  if (MODE != WGRAD && !partial) splits = 1;
+  if (MODE != WGRAD && !(partial & 1)) splits = 1;
   splits = std::max(1, std::min(splits, ksteps));
   const int kps = std::max(1, (ksteps + splits - 1) / splits);
   splits = std::max(1, (ksteps + kps - 1) / kps);
@@ -1011,10 +1019,10 @@ static int dgrad_tap_phases(const ConvShape& s, TapPhase* out) {
 // FWD / DGRAD with automatic split-K through ``ws`` (null / 0 floats: never split).
 template <int MODE>
 static void launch_fd(hipStream_t st, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy, bf16* out,
-                      float* stats, const float* shift, float* ws, long ws_floats) {
+                      float* stats, const float* shift, float* ws, long ws_floats, bool acc = false) {
   const int sp = fd_splits(g, ws_floats);
   if (sp <= 1) {
-    launch_mode<MODE>(st, g, x, w, dy, out, nullptr, stats, 1, shift, 0);
+    launch_mode<MODE>(st, g, x, w, dy, out, nullptr, stats, 1, shift, acc ? 2 : 0);
     return;
   }
   launch_mode<MODE>(st, g, x, w, dy, nullptr, ws, nullptr, sp, nullptr, 1);
@@ -1028,7 +1036,7 @@ static void launch_fd(hipStream_t st, const ConvGeom& g, const bf16* x, const bf
   RowMap rm{};
   if (MODE == DGRAD && g.st != 1) rm = make_rowmap(g.Hp, g.Wp, g.H, g.W, g.st, g.ph, g.pw);
   hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, sp, g.M, g.NC, rm, out, stats, shift,
-                     rows_per_block, nullptr);
+                     rows_per_block, acc ? out : nullptr);
 }
 
 // K-split count for the weight gradient: about two workgroups per CU, at least
@@ -1064,8 +1072,9 @@ void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf
 
 // dX[N,H,W,C] = conv_transpose(dY[N,P,Q,O], W_rsc)   (every element written).
 // Stride 2 runs as 4 sub-pixel phases so no MFMA multiplies a structural zero.
+// acc: dx += result (the data gradient of one branch of a multi-branch block)
 void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const bf16* wrsc, bf16* dx, float* ws,
-                       long ws_floats, const bf16* wd) {
+                       long ws_floats, const bf16* wd, int acc) {
   check_shape(s);
   if (wd != nullptr && s.O % 64 == 0) {   // tap-major path on the dgrad weight image
     TapPhase ph[4];
@@ -1077,10 +1086,11 @@ void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const
         q.Hp = ph[i].g.P; q.Wp = ph[i].g.Q;
         q.dNS = make_div(1); q.dWp = make_div(q.Wp); q.dHWp = make_div(q.Hp * q.Wp);
         q.M = s.N * q.Hp * q.Wp; q.K = 0;
-        launch_mode<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, 1);
+        launch_mode<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, 1, nullptr, acc ? 2 : 0);
         continue;
       }
-      launch_tap(st, ph[i].g, dy, wd + ph[i].img_off, dx, nullptr, nullptr, ph[i].rm, ws, ws_floats);
+      launch_tap(st, ph[i].g, dy, wd + ph[i].img_off, dx, nullptr, nullptr, ph[i].rm, ws, ws_floats,
+                 acc ? dx : nullptr);
     }
     return;
   }
@@ -1088,7 +1098,7 @@ void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const
   g.NC = s.C;
   if (s.st == 1) {
     g.M = s.N * s.H * s.W; g.K = s.R * s.S * s.O;
-    launch_fd<DGRAD>(st, g, nullptr, wrsc, dy, dx, nullptr, nullptr, ws, ws_floats);
+    launch_fd<DGRAD>(st, g, nullptr, wrsc, dy, dx, nullptr, nullptr, ws, ws_floats, acc != 0);
     return;
   }
   for (int ph = 0; ph < 2; ++ph)
@@ -1102,10 +1112,10 @@ void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const
       q.dNS = make_div(std::max(q.ns, 1)); q.dWp = make_div(q.Wp); q.dHWp = make_div(q.Hp * q.Wp);
       q.M = s.N * q.Hp * q.Wp; q.K = q.nr * q.ns * s.O;
       if (q.K == 0) {   // phase with no taps (1x1 stride 2, odd parity): the kernel writes zeros
-        launch_mode<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, 1);
+        launch_mode<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, 1, nullptr, acc ? 2 : 0);
         continue;
       }
-      launch_fd<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, ws, ws_floats);
+      launch_fd<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, ws, ws_floats, acc != 0);
     }
 }
 

@@ -11,7 +11,7 @@ from .data import FedDataset
 # zoo models with a native (hand-written HIP) training engine on the GPU
 NATIVE_CNNS = ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "mobilenet", "mobilenetv2", "vgg11",
                "vgg13", "vgg16", "vgg19", "preactresnet18", "preactresnet34", "preactresnet50", "preactresnet101",
-               "preactresnet152")
+               "preactresnet152", "googlenet")
 
 
 def build_trainer(model: str, data: FedDataset, device, cfg: TrainerConfig = TrainerConfig(),

@@ -40,7 +40,7 @@ from torch import nn
 from .. import native
 from ..models import build_model
 from ..models.zoo.mobile import DWSeparable, InvertedResidual, MobileNet, MobileNetV2
-from ..models.zoo.multibranch import VGG
+from ..models.zoo.multibranch import VGG, GoogLeNet, Inception
 from ..models.zoo.residual import BasicBlock, Bottleneck, PreActBlock, PreActBottleneck, PreActResNet, ResNet
 from ..ops import cnn, conv
 from .base import EpochStats, LocalTrainer, TrainerConfig
@@ -123,12 +123,13 @@ class _Unit:
                               ws=ws)
 
     def dgrad(self, nb: int, out: torch.Tensor, ws: Optional[torch.Tensor] = None,
-              dz: Optional[torch.Tensor] = None) -> torch.Tensor:
+              dz: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
         dz = self.view(self.dz, nb) if dz is None else dz
         if self.depthwise:
+            assert not accumulate
             return conv.dwconv_dgrad(dz, self.conv.weight, self.in_shape(nb), self.stride, self.pad, out=out)
         return conv.conv2d_dgrad(dz, self.wr, self.in_shape(nb), self.stride, self.pad, Cw=self.Cw, out=out, ws=ws,
-                                 wd=self.wd)
+                                 wd=self.wd, accumulate=accumulate)
 
     def pack_item(self):
         return None if self.depthwise else (self.conv.weight.data, self.wr)
@@ -321,8 +322,95 @@ def _plan_preact(m, rows, dev, dt):
     return _PreActPlan(m, rows, dev, dt)
 
 
+def _nhwc(t: torch.Tensor, nb: int, hw: int, c: int) -> torch.Tensor:
+    return t[: nb * hw * hw * c].view(nb, hw, hw, c)
+
+
+class _Incep:
+    """Inception module (src/models/googlenet.py:7-53) as four unit chains (1x1 | 1x1-3x3 |
+    1x1-3x3-3x3 | maxpool3x3/1 -> 1x1).  Each chain's last BN+ReLU writes its channel slice of
+    one concatenated NHWC output (strided ``bn_apply``), so ``torch.cat`` never runs; backward
+    reads the slices of the output grad in place and the four input grads are summed by the
+    first convs' DGRAD epilogues (accumulate) and the maxpool backward's gather."""
+
+    def __init__(self, m: Inception, hw: int, cin: int, rows: int, dev, dt, pool_after: bool):
+        self.branches: List[List[_Unit]] = []
+        for k, seq in enumerate((m.b1, m.b2, m.b3, m.b4)):
+            mods = list(seq)
+            if k == 3:
+                mp = mods.pop(0)
+                if not (isinstance(mp, nn.MaxPool2d) and mp.kernel_size == 3 and mp.stride == 1 and mp.padding == 1):
+                    raise TypeError("Inception pool branch: expected MaxPool2d(3, 1, 1)")
+            pairs = [(mods[i], mods[i + 1]) for i in range(0, len(mods), 3)]
+            us = []
+            for i, (c, bn) in enumerate(pairs):
+                assert isinstance(c, nn.Conv2d) and isinstance(bn, nn.BatchNorm2d)
+                us.append(_Unit(c, bn, hw, relu=True, rows=rows, dev=dev, need_y=i < len(pairs) - 1, act_dtype=dt))
+            self.branches.append(us)
+        self.widths = [br[-1].O for br in self.branches]
+        self.offs = [sum(self.widths[:k]) for k in range(4)]
+        self.hw, self.cin, self.cout = hw, cin, sum(self.widths)
+        bf = dict(dtype=dt, device=dev)
+        n_in, n_out = rows * hw * hw * cin, rows * hw * hw * self.cout
+        self.out = torch.empty(n_out, **bf)                  # concatenated branch outputs
+        self.dout = torch.empty(n_out, **bf)                 # grad wrt out
+        self.bp = torch.empty(n_in, **bf)                    # maxpool3/1 of the input (pool branch)
+        self.bidx = torch.empty(n_in, dtype=torch.uint8, device=dev)
+        self.dbp = torch.empty(n_in, **bf)
+        self.pool_after = pool_after                         # MaxPool2d(3, 2, 1) after the module
+        self.out_hw = (hw - 1) // 2 + 1 if pool_after else hw
+        n_sp = rows * self.out_hw * self.out_hw * self.cout
+        self.sp = torch.empty(n_sp, **bf) if pool_after else None
+        self.sidx = torch.empty(n_sp, dtype=torch.uint8, device=dev) if pool_after else None
+        self.dsp = torch.empty(n_sp, **bf) if pool_after else None
+        self._bidx = self._sidx = None                       # argmax records of the current step
+
+    def units(self) -> List[_Unit]:
+        return [u for br in self.branches for u in br]
+
+    def out_view(self, t, nb):
+        return _nhwc(t, nb, self.hw, self.cout)
+
+    def in_view(self, t, nb):
+        return _nhwc(t, nb, self.hw, self.cin)
+
+    def final_view(self, t, nb):                             # the module's result (after the stage pool)
+        return _nhwc(t, nb, self.out_hw, self.cout)
+
+    def slice(self, t4, k):
+        return t4[..., self.offs[k]:self.offs[k] + self.widths[k]]
+
+
+class _GoogPlan:
+    """pre_layers (conv3x3+BN+ReLU) -> a3 b3 | pool | a4..e4 | pool | a5 b5 -> avgpool(8) + linear
+    (src/models/googlenet.py:56-98)."""
+
+    def __init__(self, m: GoogLeNet, rows, dev, dt):
+        c0, bn0 = m.pre_layers[0], m.pre_layers[1]
+        self.pre = _Unit(c0, bn0, 32, relu=True, rows=rows, dev=dev, need_y=True, c_in_pad=8, act_dtype=dt)
+        hw, c = self.pre.P, self.pre.O
+        mp = m.maxpool
+        if not (mp.kernel_size == 3 and mp.stride == 2 and mp.padding == 1):
+            raise TypeError("GoogLeNet plan: expected MaxPool2d(3, 2, 1) between stages")
+        self.mods: List[_Incep] = []
+        for name, _ in m.STAGES:
+            I = _Incep(getattr(m, name), hw, c, rows, dev, dt, name in ("b3", "e4"))
+            self.mods.append(I)
+            hw, c = I.out_hw, I.cout
+        if m.avgpool.kernel_size not in (hw, (hw, hw)):
+            raise TypeError("GoogLeNet plan: the head must average the whole final map")
+        self.head_hw, self.head_c = hw, c
+
+    def units(self) -> List[_Unit]:
+        return [self.pre] + [u for I in self.mods for u in I.units()]
+
+
+def _plan_googlenet(m, rows, dev, dt):
+    return _GoogPlan(m, rows, dev, dt)
+
+
 PLANS = {ResNet: _plan_resnet, MobileNet: _plan_mobilenet, MobileNetV2: _plan_mobilenetv2, VGG: _plan_vgg,
-         PreActResNet: _plan_preact}
+         PreActResNet: _plan_preact, GoogLeNet: _plan_googlenet}
 
 
 def supports(model: nn.Module) -> bool:
@@ -357,13 +445,20 @@ class CNNNativeTrainer(LocalTrainer):
         self.rows = R = max(cfg.batch_size, self.eval_bs)
         plan = PLANS[type(model)](self.model, R, device, act_dtype)
         self.preact = plan if isinstance(plan, _PreActPlan) else None
-        self.blocks = plan.blocks if self.preact else plan
-        last = self.blocks[-1]
-        self.head_hw, self.head_c = last.out_hw, last.cout
-        self.units: List[_Unit] = plan.units() if self.preact else [u for b in self.blocks for u in b.units()]
-        # units whose data gradient is never needed (they read the network input)
-        self._no_dgrad = ({id(self.preact.stem)} if self.preact else
-                          {id(u) for u in self.blocks[0].units()} if self.blocks[0].first else set())
+        self.goog = plan if isinstance(plan, _GoogPlan) else None
+        if self.goog is not None:
+            self.blocks = []
+            self.head_hw, self.head_c = plan.head_hw, plan.head_c
+            self.units: List[_Unit] = plan.units()
+            self._no_dgrad = {id(plan.pre)}
+        else:
+            self.blocks = plan.blocks if self.preact else plan
+            last = self.blocks[-1]
+            self.head_hw, self.head_c = last.out_hw, last.cout
+            self.units = plan.units() if self.preact else [u for b in self.blocks for u in b.units()]
+            # units whose data gradient is never needed (they read the network input)
+            self._no_dgrad = ({id(self.preact.stem)} if self.preact else
+                              {id(u) for u in self.blocks[0].units()} if self.blocks[0].first else set())
         # per-step accumulators: BN batch stats [2][O] and BN-backward sums [3][O], one fill each
         self.stats_all = torch.zeros(sum(conv.STAT_REP * 2 * u.O for u in self.units), device=device)
         self.red_all = torch.zeros(sum(3 * u.O for u in self.units), device=device)
@@ -458,6 +553,8 @@ class CNNNativeTrainer(LocalTrainer):
     def _forward(self, nb: int, train: bool, images: torch.Tensor, labels: torch.Tensor, dbase, stats_row: int):
         if self.preact is not None:
             return self._forward_preact(nb, train, images, labels, dbase, stats_row)
+        if self.goog is not None:
+            return self._forward_goog(nb, train, images, labels, dbase, stats_row)
         x = cnn.prep_input(images, 0, nb, self.augment and train, self.cfg.seed, self.round_ctr,
                            out=self.xin[:nb], dbase=dbase)
         a = x
@@ -501,6 +598,8 @@ class CNNNativeTrainer(LocalTrainer):
     def _backward(self, nb: int, x: torch.Tensor, dhead: torch.Tensor) -> None:
         if self.preact is not None:
             return self._backward_preact(nb, x, dhead)
+        if self.goog is not None:
+            return self._backward_goog(nb, x, dhead)
         dya, dyb = dhead, None
         ws = self.wgrad_ws
         for i in range(len(self.blocks) - 1, -1, -1):
@@ -595,6 +694,66 @@ class CNNNativeTrainer(LocalTrainer):
             self._bn_bwd(prev, nb, prev.view(prev.dy, nb), da2, a, dadd=None if b.sc is not None else g)
             g = prev.view(prev.dz, nb)
         P.stem.wgrad(x, nb, ws)
+
+    # ---- GoogLeNet ----------------------------------------------------------------------------
+    def _forward_goog(self, nb: int, train: bool, images, labels, dbase, stats_row: int):
+        G, ws = self.goog, self.wgrad_ws
+        x = cnn.prep_input(images, 0, nb, self.augment and train, self.cfg.seed, self.round_ctr,
+                           out=self.xin[:nb], dbase=dbase)
+        p = G.pre
+        p.fwd(x, nb, p.stats if train else None, ws)
+        a = self._bn(p, p.view(p.z, nb), p.view(p.y, nb), train, True)
+        for I in G.mods:
+            out = I.out_view(I.out, nb)
+            for k, br in enumerate(I.branches):
+                h = a
+                if k == 3:
+                    h, I._bidx = cnn.maxpool3(a, 1, out=I.in_view(I.bp, nb), idx=I.in_view(I.bidx, nb))
+                for u in br[:-1]:
+                    u.fwd(h, nb, u.stats if train else None, ws)
+                    h = self._bn(u, u.view(u.z, nb), u.view(u.y, nb), train, True)
+                L = br[-1]
+                L.fwd(h, nb, L.stats if train else None, ws)
+                self._bn(L, L.view(L.z, nb), I.slice(out, k), train, True)    # its channel slice of the concat
+            a = out
+            if I.pool_after:
+                a, I._sidx = cnn.maxpool3(out, 2, out=I.final_view(I.sp, nb), idx=I.final_view(I.sidx, nb))
+        return x, self._head(a, nb, train, labels, dbase, stats_row)
+
+    def _backward_goog(self, nb: int, x: torch.Tensor, dhead: torch.Tensor) -> None:
+        G, ws = self.goog, self.wgrad_ws
+        p = G.pre
+        g = dhead                                          # grad wrt the current module's result
+        for i in range(len(G.mods) - 1, -1, -1):
+            I = G.mods[i]
+            if i > 0:                                      # the module input and where its grad goes
+                J = G.mods[i - 1]
+                a = J.final_view(J.sp if J.pool_after else J.out, nb)
+                dx = J.final_view(J.dsp if J.pool_after else J.dout, nb)
+            else:
+                a, dx = p.view(p.y, nb), p.view(p.dy, nb)
+            if I.pool_after:
+                g = cnn.maxpool3_bwd(g, I._sidx, (nb, I.hw, I.hw, I.cout), 2, out=I.out_view(I.dout, nb))
+            out = I.out_view(I.out, nb)
+            for k, br in enumerate(I.branches):
+                self._bn_bwd(br[-1], nb, I.slice(g, k), None, I.slice(out, k))
+                for j in range(len(br) - 1, -1, -1):
+                    v = br[j]
+                    if j > 0:
+                        w = br[j - 1]
+                        v.wgrad(w.view(w.y, nb), nb, ws)
+                        v.dgrad(nb, w.view(w.dy, nb), ws)
+                        self._bn_bwd(w, nb, w.view(w.dy, nb), None, w.view(w.y, nb))
+                    elif k < 3:                            # branch heads: the module input's grad fan-in
+                        v.wgrad(a, nb, ws)
+                        v.dgrad(nb, dx, ws, accumulate=k > 0)
+                    else:
+                        v.wgrad(I.in_view(I.bp, nb), nb, ws)
+                        dbp = v.dgrad(nb, I.in_view(I.dbp, nb), ws)
+                        cnn.maxpool3_bwd(dbp, I._bidx, (nb, I.hw, I.hw, I.cin), 1, out=dx, accumulate=True)
+            g = dx
+        self._bn_bwd(p, nb, p.view(p.dy, nb), None, p.view(p.y, nb))
+        p.wgrad(x, nb, ws)
 
     def _sgd(self) -> None:
         c, fs = self.cfg, self.fs

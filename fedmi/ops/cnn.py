@@ -59,9 +59,51 @@ class BNParams:
         return {k: _p(getattr(self, k)) for k in self.__slots__}
 
 
+def row_stride(t: torch.Tensor) -> int:
+    """Row stride (elements) of an NHWC / [M, C] tensor that may be a channel slice of a wider buffer
+    (a branch's output inside a concatenated tensor); rows must be evenly spaced, channels unit-stride."""
+    if t.is_contiguous():
+        return int(t.shape[-1])
+    st, sh = t.stride(), t.shape
+    if st[-1] != 1:
+        raise ValueError("channel dimension must be unit-stride")
+    ld = st[-2]
+    for d in range(t.dim() - 2):
+        if st[d] != st[d + 1] * sh[d + 1]:
+            raise ValueError("rows of a channel-slice view must be evenly spaced")
+    if ld % 8 or t.data_ptr() % 16:
+        raise ValueError("channel-slice views need 16-byte aligned rows (offset and stride % 8)")
+    return int(ld)
+
+
 def bn_desc(stats=None, gamma=None, beta=None, rmean=None, rvar=None, nbt=None, smean=None, sinv=None,
             shift=None, cbias=None) -> BNParams:
     return BNParams(stats, gamma, beta, rmean, rvar, nbt, smean, sinv, shift, cbias)
+
+
+def maxpool3(x: torch.Tensor, stride: int, out: Optional[torch.Tensor] = None,
+             idx: Optional[torch.Tensor] = None):
+    """MaxPool2d(3, stride, padding=1) of NHWC bf16 ``x``; returns (y, idx) with idx the uint8 window argmax."""
+    N, H, W, C = x.shape
+    P, Q = (H - 1) // stride + 1, (W - 1) // stride + 1
+    if out is None:
+        out = torch.empty(N, P, Q, C, dtype=x.dtype, device=x.device)
+    if idx is None:
+        idx = torch.empty(N, P, Q, C, dtype=torch.uint8, device=x.device)
+    native.require().maxpool3(native.stream_handle(x.device), x.data_ptr(), out.data_ptr(), idx.data_ptr(), N, H, W, C,
+                              int(stride))
+    return out, idx
+
+
+def maxpool3_bwd(dy: torch.Tensor, idx: torch.Tensor, x_shape, stride: int, out: Optional[torch.Tensor] = None,
+                 accumulate: bool = False) -> torch.Tensor:
+    """dx of :func:`maxpool3` (gather over the covering windows); ``accumulate``: dx += instead of =."""
+    N, H, W, C = (int(v) for v in x_shape)
+    if out is None:
+        out = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+    native.require().maxpool3_bwd(native.stream_handle(dy.device), dy.data_ptr(), idx.data_ptr(), out.data_ptr(), N, H,
+                                  W, C, int(stride), int(accumulate))
+    return out
 
 
 def maxpool2(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -93,7 +135,7 @@ def bn_apply(z: torch.Tensor, a: BNParams, y: torch.Tensor, train: bool, relu: b
     M = z.numel() // C
     native.require().bn_apply(native.stream_handle(z.device), z.data_ptr(), a.ptrs(), _p(z2),
                               b.ptrs() if b is not None else None, _p(res), y.data_ptr(), M, C, eps, momentum,
-                              int(train), int(relu))
+                              int(train), int(relu), row_stride(y))
     return y
 
 
@@ -118,8 +160,12 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
     if zb is not None:
         d.update(zb=_p(zb), meanB=_p(b.smean), invB=_p(b.sinv), gammaB=_p(b.gamma), dgammaB=_p(dgamma_b),
                  dbetaB=_p(dbeta_b), dzb=_p(dzb), shiftB=_p(b.shift))
+    ldd = row_stride(dya)
+    if dyb is not None and row_stride(dyb) != ldd:
+        raise ValueError("bn_bwd: dya and dyb must share a row stride")
     native.require().bn_bwd(native.stream_handle(red.device), d, red.data_ptr(), M, C,
-                            ws.data_ptr() if ws is not None else 0, ws.numel() if ws is not None else 0)
+                            ws.data_ptr() if ws is not None else 0, ws.numel() if ws is not None else 0,
+                            ldd, row_stride(y) if y is not None else C)
 
 
 def bn_bwd_ws_floats(M: int, C: int) -> int:

@@ -159,22 +159,25 @@ def dgrad_pack_weights(items) -> None:
 
 def conv2d_dgrad(dy: torch.Tensor, wrsc: torch.Tensor, x_shape, stride: int, pad: int, Cw: Optional[int] = None,
                  out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-                 wd: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 wd: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
     """dx[N,H,W,C] from dy[N,P,Q,O].  ``wd``: the conv's DGRAD weight image (:func:`dgrad_pack_weights`)
-    selects the tap-major LDS-DMA kernel (O % 64 == 0); without it the generic implicit GEMM runs."""
+    selects the tap-major LDS-DMA kernel (O % 64 == 0); without it the generic implicit GEMM runs.
+    ``accumulate``: out += dx (one branch's share of a multi-branch block's input gradient)."""
     _check(dy, torch.bfloat16, "conv2d_dgrad.dy")
     O, R, S, C = wrsc.shape
     shp = shape_tuple(x_shape, O, R, S, stride, pad, Cw)
     if tuple(dy.shape) != (shp[0], shp[6], shp[7], O):
         raise ValueError(f"conv2d_dgrad: dy shape {tuple(dy.shape)} vs expected {(shp[0], shp[6], shp[7], O)}")
     if out is None:
+        if accumulate:
+            raise ValueError("conv2d_dgrad: accumulate needs out")
         out = torch.empty(*x_shape, dtype=torch.bfloat16, device=dy.device)
     if wd is not None:
         _check(wd, torch.bfloat16, "conv2d_dgrad.wd")
         if wd.numel() < O * R * S * C:
             raise ValueError("conv2d_dgrad: dgrad image too small")
     native.require().conv_dgrad(native.stream_handle(dy.device), shp, dy.data_ptr(), wrsc.data_ptr(), out.data_ptr(),
-                                *_ws_args(ws), wd.data_ptr() if wd is not None else 0)
+                                *_ws_args(ws), wd.data_ptr() if wd is not None else 0, int(accumulate))
     return out
 
 

@@ -93,7 +93,7 @@ def conv2d_fwd(x, wrsc, stride, pad, Cw=None, stats=None, out=None, shift=None, 
 
 
 @torch.no_grad()
-def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None, ws=None, wd=None):
+def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None, ws=None, wd=None, accumulate=False):
     N, H, W, C = x_shape
     Cw = Cw or C
     dx = torch.nn.grad.conv2d_input((N, Cw, H, W), _w_from_img(wrsc, Cw), _nchw(dy), stride=stride, padding=pad)
@@ -101,6 +101,8 @@ def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None, ws=None, wd=
     full[:, :Cw] = dx
     if out is None:
         out = torch.empty(*x_shape, dtype=_BF, device=dy.device)
+    if accumulate:
+        full = full + _nchw(out)
     return _nhwc_into(out, full)
 
 
@@ -220,6 +222,28 @@ def bn_apply(z, a, y, train, relu, z2=None, b=None, res=None, eps=1e-5, momentum
 
 
 @torch.no_grad()
+def maxpool3(x, stride, out=None, idx=None):
+    y, ind = F.max_pool2d(_nchw(x), 3, stride, 1, return_indices=True)
+    if out is None:
+        out = torch.empty(y.shape[0], y.shape[2], y.shape[3], y.shape[1], dtype=x.dtype, device=x.device)
+    _nhwc_into(out, y)
+    # emulation keeps the input itself (not the kernel's tap bytes): overlapping windows need autograd's sum
+    return out, x
+
+
+def maxpool3_bwd(dy, idx, x_shape, stride, out=None, accumulate=False):
+    xr = _nchw(idx).requires_grad_(True)
+    with torch.enable_grad():
+        F.max_pool2d(xr, 3, stride, 1).backward(_nchw(dy))
+    g = xr.grad
+    if out is None:
+        out = torch.empty(*x_shape, dtype=dy.dtype, device=dy.device)
+    if accumulate:
+        g = g + _nchw(out)
+    return _nhwc_into(out, g)
+
+
+@torch.no_grad()
 def maxpool2(x, out=None):
     y = F.max_pool2d(_nchw(x), 2, 2)
     if out is None:
@@ -314,7 +338,7 @@ def emulated():
                  "dwconv_dgrad", "dwconv_wgrad", "dwconv_ws_floats"):
         swap(conv, name, globals()[name])
     for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "bn_bwd_ws_floats", "head", "maxpool2",
-                 "maxpool2_bwd"):
+                 "maxpool2_bwd", "maxpool3", "maxpool3_bwd"):
         swap(cnn, name, globals()[name])
     swap(native, "require", lambda: _NativeStub())
     swap(native, "stream_handle", lambda device=None: 0)

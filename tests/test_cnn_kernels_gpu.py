@@ -416,6 +416,82 @@ def test_conv_fwd_fused_residual(gpu_device, shape):
     assert torch.allclose(tot[0], yb.sum((0, 1, 2)), rtol=1e-3, atol=1e-1)
 
 
+@pytest.mark.parametrize("stride,shape", [(1, (4, 9, 7, 24)), (2, (3, 16, 16, 64)), (2, (2, 9, 11, 16))])
+def test_maxpool3_fwd_bwd_accumulate(gpu_device, stride, shape):
+    """MaxPool2d(3, stride, 1) (GoogLeNet) vs torch: forward, gather backward (overlapping windows sum), +=."""
+    torch.manual_seed(15)
+    x = torch.randn(*shape, device=gpu_device).bfloat16()
+    y, idx = cnn.maxpool3(x, stride)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.max_pool2d(xr, 3, stride, 1)
+    g = torch.randn_like(ref).bfloat16().float()
+    ref.backward(g)
+    base = torch.randn_like(x)
+    dx = cnn.maxpool3_bwd(_nhwc(g).bfloat16(), idx, x.shape, stride, out=base.clone(), accumulate=True)
+    dx0 = cnn.maxpool3_bwd(_nhwc(g).bfloat16(), idx, x.shape, stride)
+    torch.cuda.synchronize()
+    assert torch.equal(y.float(), _nhwc(ref.detach()))
+    assert _rel(dx0.float(), _nhwc(xr.grad)) < 1e-2
+    assert _rel(dx.float() - base.float(), _nhwc(xr.grad)) < 2e-2
+
+
+def test_bn_strided_channel_slices(gpu_device):
+    """bn_apply writing, and bn_bwd reading, a channel slice of a wider NHWC buffer (concat outputs)."""
+    torch.manual_seed(16)
+    dev = gpu_device
+    M, C, W, off = 768, 48, 160, 64
+    z = torch.randn(M, C, device=dev).bfloat16()
+    g, be = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+    rep = conv.stats_buffer(C, dev)
+    rep[0, 0], rep[0, 1] = z.float().sum(0), (z.float() ** 2).sum(0)
+    sm, si = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    A = cnn.bn_desc(rep, g, be, None, None, None, sm, si)
+    wide = torch.full((M, W), 7.0, device=dev).bfloat16()
+    ys = wide[:, off:off + C]
+    cnn.bn_apply(z, A, ys, train=True, relu=True)
+    yc = torch.empty_like(z)
+    cnn.bn_apply(z, A, yc, train=True, relu=True)
+    torch.cuda.synchronize()
+    assert torch.equal(ys.float(), yc.float())
+    assert float((wide[:, :off].float() - 7).abs().max()) == 0 and float((wide[:, off + C:].float() - 7).abs().max()) == 0
+    dwide = torch.randn(M, W, device=dev).bfloat16()
+    red = torch.empty(3, C, device=dev)
+    ws = torch.zeros(cnn.bn_bwd_ws_floats(M, C), device=dev)
+    d1, d2 = torch.empty_like(z), torch.empty_like(z)
+    dg1, db1, dg2, db2 = (torch.empty(C, device=dev) for _ in range(4))
+    cnn.bn_bwd(dwide[:, off:off + C], z, A, dg1, db1, d1, red, y=ys, ws=ws)
+    cnn.bn_bwd(dwide[:, off:off + C].contiguous(), z, A, dg2, db2, d2, red, y=yc, ws=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(d1, d2) and torch.allclose(dg1, dg2, rtol=1e-5, atol=1e-4) and torch.allclose(db1, db2)
+
+
+@pytest.mark.parametrize("shape", [(4, 16, 16, 64, 64, 3, 1, 1), (8, 8, 8, 128, 64, 1, 1, 0),
+                                   (4, 16, 16, 64, 128, 3, 2, 1), (3, 7, 5, 24, 40, 3, 1, 1)])
+def test_conv_dgrad_accumulate(gpu_device, shape):
+    """dx += DGRAD (fan-in of a multi-branch block), tap-major and generic paths, with split-K."""
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device, seed=17)
+    xr = x.clone().requires_grad_(True)
+    out = F.conv2d(xr, wb, stride=st, padding=pad)
+    gy = torch.randn_like(out).bfloat16().float()
+    out.backward(gy)
+    dyn = _nhwc(gy).bfloat16()
+    wpk = conv.pack_weight(w)
+    C = xn.shape[-1]
+    shp = (xn.shape, O, R, R, st, pad, Cw)
+    wsp = torch.empty(max(conv.fd_ws_floats(*shp), 1), device=gpu_device)
+    wds = [None]
+    if conv.dgrad_eligible(O):
+        wd = torch.empty(conv.dgrad_image_numel(w.shape, C), dtype=torch.bfloat16, device=gpu_device)
+        conv.dgrad_pack_weights([(w, wd, st, pad, C)])
+        wds.append(wd)
+    for wd in wds:
+        base = (torch.randn_like(xn.float()) * 0.05).bfloat16()
+        dx = conv.conv2d_dgrad(dyn, wpk, xn.shape, st, pad, Cw=Cw, out=base.clone(), ws=wsp, wd=wd, accumulate=True)
+        torch.cuda.synchronize()
+        assert _rel(dx[..., :Cw].float() - base[..., :Cw].float(), _nhwc(xr.grad)) < 2e-2, wd is not None
+
+
 def test_bn_bwd_additive_residual_grad(gpu_device):
     torch.manual_seed(14)
     dev = gpu_device

@@ -30,7 +30,8 @@ def _cos(a, b):
                                        ("MobileNetV2", ["linear.weight", "bn2.weight"]),
                                        ("VGG11", ["classifier.weight", "features.26.weight", "features.25.weight"]),
                                        ("PreActResNet18", ["linear.weight", "layer4.1.conv2.weight",
-                                                           "layer4.1.bn2.weight"])])
+                                                           "layer4.1.bn2.weight"]),
+                                       ("GoogLeNet", ["linear.weight", "b5.b1.1.weight", "b5.b4.2.weight"])])
 def test_loss_and_tail_grads_match_torch(gpu_device, name, tail):
     from fedmi.engine.cnn_native import CNNNativeTrainer
 
@@ -101,7 +102,7 @@ def test_native_matches_emulated_kernels_on_gpu(gpu_device, name, avg_cos):
     assert sum(_cos(gn[k], ge[k]) for k in names) / len(names) > avg_cos
 
 
-@pytest.mark.parametrize("name", ["ResNet18", "MobileNet", "VGG11", "PreActResNet18"])
+@pytest.mark.parametrize("name", ["ResNet18", "MobileNet", "VGG11", "PreActResNet18", "GoogLeNet"])
 def test_native_trains_like_torch_engine(gpu_device, name):
     from fedmi.engine.cnn_native import CNNNativeTrainer
     from fedmi.engine.torch_engine import TorchTrainer
