@@ -74,7 +74,8 @@ def _worker(rank, world, port, q):
     i8.flat.add_(delta)
     FedAvg(compressor=c3).average(i8)
     out["int8"] = i8.flat.clone()
-    q.put((rank, out))
+    # tensors travel by value (numpy pickles): torch's fd-sharing reducer races the worker's exit
+    q.put((rank, {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in out.items()}))
     dist.destroy_process_group()
 
 
@@ -86,6 +87,8 @@ def test_fedavg_gloo_two_ranks():
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
+    res = {r: {k: (torch.from_numpy(v) if hasattr(v, "dtype") and not torch.is_tensor(v) and not isinstance(v, (int, float)) else v)
+               for k, v in d.items()} for r, d in res.items()}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
