@@ -890,8 +890,12 @@ static void launch_tiled(hipStream_t st, dim3 grid, const ConvGeom& g, const bf1
 // (ResNet layer3/4 at batch 128: 128-256 tiles, 36-72 K steps) leave most of
 // the chip idle behind a serial K chain.  Split K so that ~3 workgroups per CU
 // run >= 8 K steps each, partials into ``ws``; 1 = no split.
+// The split-K combine (conv_splitk_reduce) gives each lane one 8-channel vector of a row and needs a
+// whole row in one 256-lane block: rows wider than 2048 channels never split.
+static constexpr int SPLITK_MAX_NC = 2048;
+
 static int fd_splits(const ConvGeom& g, long ws_floats) {
-  if (ws_floats <= 0) return 1;
+  if (ws_floats <= 0 || g.NC > SPLITK_MAX_NC) return 1;
   const TileCfg t = pick_tiles(g.M, g.NC);
   const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
   const int ksteps = (g.K + BK - 1) / BK;
@@ -935,7 +939,7 @@ static int tap_bn(int O) { return O <= 64 ? 64 : 128; }
 // Split K only to fill one wave of workgroups: conv_tap keeps 1 (BN 128, 96 KiB
 // LDS) or 2 (BN 64) workgroups per CU, and a split costs an fp32 round trip.
 static int tap_splits(const TapGeom& g, long ws_floats) {
-  if (ws_floats <= 0) return 1;
+  if (ws_floats <= 0 || g.O > SPLITK_MAX_NC) return 1;
   const int bn = tap_bn(g.O);
   const long tiles = (long)((g.M + 127) / 128) * ((g.O + bn - 1) / bn);
   const long target = (bn == 128 ? 1l : 2l) * num_cus();

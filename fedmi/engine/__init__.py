@@ -1,6 +1,8 @@
 """Local training engines (one per federated client)."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import native
@@ -17,8 +19,9 @@ NATIVE_CNNS = ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "mo
 def build_trainer(model: str, data: FedDataset, device, cfg: TrainerConfig = TrainerConfig(),
                   init_state=None) -> LocalTrainer:
     """On a GPU: LeNet -> fused HIP engine; ResNet / MobileNet / MobileNetV2 -> the implicit-GEMM +
-    BN-fused HIP engine (mandatory, no silent fallback).  Other zoo models and CPU runs -> the
-    generic PyTorch engine (flat buffers + native fused SGD on GPU)."""
+    BN-fused HIP engine (mandatory, no silent fallback).  Other zoo models -> the generic PyTorch
+    engine with the native MFMA convs installed under autograd (``FEDMI_HYBRID=0``: PyTorch convs, fp32);
+    CPU runs -> the generic PyTorch engine."""
     device = torch.device(device)
     from ..models import _canon
 
@@ -37,7 +40,10 @@ def build_trainer(model: str, data: FedDataset, device, cfg: TrainerConfig = Tra
     if _canon(model) in ("lenet", "mlp"):
         c, h, w = data.train.x.shape[1:]
         kw = {"in_channels": c} if _canon(model) == "lenet" else {"in_features": c * h * w}
-    return TorchTrainer(model, data, device, cfg, init_state=init_state, model_kwargs=kw)
+    # zoo models without a whole-network engine: native MFMA convs under PyTorch autograd (bf16 NHWC)
+    hybrid = (device.type == "cuda" and not native.force_torch_path() and os.environ.get("FEDMI_HYBRID", "1") != "0"
+              and _canon(model) not in ("lenet", "mlp"))
+    return TorchTrainer(model, data, device, cfg, init_state=init_state, model_kwargs=kw, hybrid=hybrid)
 
 
 __all__ = ["build_trainer", "EpochStats", "LocalTrainer", "TrainerConfig", "FedDataset"]

@@ -6,6 +6,11 @@ gradients in one flat grad buffer and all floating BN buffers in a second flat
 buffer, so FedAvg is a single collective over :meth:`float_state` and the SGD
 update is a single ``sgd_flat`` launch instead of 4 ops per tensor.
 On CPU the identical update is done with torch ops (reference semantics).
+
+``hybrid=True`` (GPU; what :func:`fedmi.engine.build_trainer` picks for zoo models without a
+whole-network native engine): every eligible conv runs on the MFMA implicit-GEMM kernels
+(:mod:`fedmi.ops.native_layers`), the network runs channels-last under bf16 autocast, so the
+remaining PyTorch ops (BN, pooling, concat, SE gates) work on the same NHWC bf16 activations.
 """
 from __future__ import annotations
 
@@ -61,7 +66,7 @@ class FlatState:
 
 class TorchTrainer(LocalTrainer):
     def __init__(self, model_name: str, data: FedDataset, device: torch.device,
-                 cfg: TrainerConfig = TrainerConfig(), init_state=None, model_kwargs=None):
+                 cfg: TrainerConfig = TrainerConfig(), init_state=None, model_kwargs=None, hybrid: bool = False):
         self.model_name = model_name
         self.cfg = dataclasses.replace(cfg)   # private copy: set_lr mutates it
         self._device = torch.device(device)
@@ -81,6 +86,17 @@ class TorchTrainer(LocalTrainer):
         self._tstats = torch.zeros(3, dtype=torch.float64, device=self._device)
         self._estats = torch.zeros(3, dtype=torch.float64, device=self._device)
         self._nat = native.require() if self._device.type == "cuda" and not native.force_torch_path() else None
+        self.hybrid = bool(hybrid and self._nat is not None)
+        self.native_convs: List[str] = []
+        if self.hybrid:
+            from ..ops import native_layers
+
+            self.native_convs = native_layers.install(self.model)
+        # hybrid mode replays each full-batch SGD step (forward + autograd backward + SGD + stats) from
+        # one captured HIP graph: the Python / launch overhead of ~10^3 small kernels per step goes away
+        self.use_graph = bool(self.hybrid and cfg.use_graph)
+        self._graph = None
+        self._gx = self._gy = None
 
     @property
     def device(self) -> torch.device:
@@ -117,7 +133,16 @@ class TorchTrainer(LocalTrainer):
         x = self.train_set.x[start:start + nb]
         gidx = np.arange(start, start + nb) if self.augment else None
         xin = augment_normalize(x, gidx, self.cfg.seed & 0xFFFFFFFF, self.round_idx, self.mean, self.std)
-        return xin, self.train_set.y[start:start + nb].long()
+        return self._layout(xin), self.train_set.y[start:start + nb].long()
+
+    def _layout(self, x: torch.Tensor) -> torch.Tensor:
+        return x.contiguous(memory_format=torch.channels_last) if self.hybrid and x.dim() == 4 else x
+
+    def _run(self, x: torch.Tensor) -> torch.Tensor:
+        if self.hybrid:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                return self.model(x).float()
+        return self.model(x)
 
     # ---- compute -------------------------------------------------------------------
     def _sgd(self) -> None:
@@ -134,8 +159,42 @@ class TorchTrainer(LocalTrainer):
 
     def train_step(self, start: int, nb: int) -> torch.Tensor:
         x, y = self._batch(start, nb)
+        if self.use_graph and nb == self.cfg.batch_size:
+            if self._graph is None:
+                self._capture(x, y)
+            self._gx.copy_(x)
+            self._gy.copy_(y)
+            self._graph.replay()
+            return self._gloss
+        return self._step_body(x, y)
+
+    def _capture(self, x: torch.Tensor, y: torch.Tensor) -> None:
+        """Capture one SGD step on static input buffers.  The warm-up step that precedes capture (it sizes
+        the native workspaces and lets MIOpen pick its kernels) runs on a state snapshot that is restored
+        afterwards, so capturing never changes the training trajectory."""
+        fs = self.fs
+        self._gx, self._gy = x.clone(), y.clone()
+        snap = (fs.flat.clone(), fs.mom.clone(), [b.clone() for b in self.int_state()], self._tstats.clone())
+        side = torch.cuda.Stream(self._device)
+        side.wait_stream(torch.cuda.current_stream(self._device))
+        with torch.cuda.stream(side):
+            self._step_body(self._gx, self._gy)
+        torch.cuda.current_stream(self._device).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._gloss = self._step_body(self._gx, self._gy)
+        with torch.no_grad():
+            fs.flat.copy_(snap[0])
+            fs.mom.copy_(snap[1])
+            for b, v in zip(self.int_state(), snap[2]):
+                b.copy_(v)
+            self._tstats.copy_(snap[3])
+        self._graph = g
+
+    def _step_body(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        nb = x.shape[0]
         self.fs.grad.zero_()
-        out = self.model(x)
+        out = self._run(x)
         loss = F.cross_entropy(out, y)
         loss.backward()
         self._sgd()
@@ -164,9 +223,9 @@ class TorchTrainer(LocalTrainer):
         n = len(self.test_set)
         bs = self.cfg.eval_batch_size
         for s in range(0, n, bs):
-            x = augment_normalize(self.test_set.x[s:s + bs], None, 0, 0, self.mean, self.std)
+            x = self._layout(augment_normalize(self.test_set.x[s:s + bs], None, 0, 0, self.mean, self.std))
             y = self.test_set.y[s:s + bs].long()
-            out = self.model(x)
+            out = self._run(x)
             self._estats[0] += F.cross_entropy(out, y, reduction="sum").double()
             self._estats[1] += (out.argmax(1) == y).sum()
             self._estats[2] += y.numel()
@@ -182,4 +241,6 @@ class TorchTrainer(LocalTrainer):
         return EpochStats(v[0], int(v[1]), int(v[2]))
 
     def set_lr(self, lr: float) -> None:
+        if float(lr) != self.cfg.lr:
+            self._graph = None           # the learning rate is a kernel argument baked into the graph
         self.cfg.lr = float(lr)

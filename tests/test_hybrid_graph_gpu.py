@@ -1,0 +1,36 @@
+"""Hybrid engine: a captured-graph SGD step reproduces the eager step (fedmi/engine/torch_engine.py)."""
+import pytest
+import torch
+
+from fedmi.engine.base import TrainerConfig
+from fedmi.engine.data import contiguous_schedule, make_dataset
+from fedmi.models import build_model
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["SimpleDLA", "EfficientNetB0"])
+def test_hybrid_graph_matches_eager(gpu_device, name):
+    from fedmi.engine.torch_engine import TorchTrainer
+
+    data = make_dataset("synthetic-cifar10-easy", device=gpu_device, n_train=512, n_test=200, seed=0)
+    init = build_model(name).state_dict()
+    runs = {}
+    for graph in (False, True):
+        tr = TorchTrainer(name, data, gpu_device, TrainerConfig(batch_size=128, lr=0.05, seed=3, use_graph=graph),
+                          init_state=init, hybrid=True)
+        assert tr.use_graph == graph
+        tr.set_schedule(*contiguous_schedule(len(data.train), 128))
+        tr.train_epoch()
+        torch.cuda.synchronize()
+        if graph:
+            assert tr._graph is not None
+        runs[graph] = (tr.float_state().clone(), tr.train_stats())
+    (fe, se), (fg, sg) = runs[False], runs[True]
+    assert se.count == sg.count == 512
+    init_flat = TorchTrainer(name, data, gpu_device, TrainerConfig(seed=3), init_state=init).float_state()
+    de, dg = fe - init_flat, fg - init_flat
+    cos = float(torch.nn.functional.cosine_similarity(de, dg, dim=0))
+    # EfficientNet's drop-connect draws different masks eager vs replayed: only the direction is compared
+    assert cos > (0.9 if name == "SimpleDLA" else 0.5), cos
+    assert abs(se.loss - sg.loss) < 0.05 * se.loss, (se.loss, sg.loss)

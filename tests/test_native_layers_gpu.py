@@ -1,0 +1,116 @@
+"""Native MFMA conv under autograd (fedmi/ops/native_layers.py) vs PyTorch fp32 conv, and the hybrid
+engine (zoo models without a whole-network engine) end to end."""
+import pytest
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from fedmi.engine.base import TrainerConfig
+from fedmi.engine.data import contiguous_schedule, make_dataset
+from fedmi.models import build_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6))
+
+
+# (N, H, C, O, k, stride, pad, bias): DenseNet 1x1 bottlenecks (C % 64 != 0), 3x3 growth convs,
+# strided 3x3 / 1x1 (DLA / SENet shortcuts), a 5x5 and 7x7 window
+SHAPES = [(8, 16, 24, 48, 1, 1, 0, False), (8, 16, 48, 16, 3, 1, 1, False), (4, 16, 64, 128, 3, 2, 1, False),
+          (4, 16, 64, 128, 1, 2, 0, True), (4, 8, 128, 64, 3, 1, 1, True), (2, 16, 32, 64, 5, 1, 2, False),
+          (2, 16, 16, 32, 7, 2, 3, False)]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+def test_native_conv_module_fwd_bwd(gpu_device, shape):
+    from fedmi.ops import native_layers
+
+    N, H, C, O, k, st, pad, bias = shape
+    torch.manual_seed(0)
+    ref = nn.Conv2d(C, O, k, st, pad, bias=bias).to(gpu_device)
+    nat = nn.Conv2d(C, O, k, st, pad, bias=bias).to(gpu_device)
+    nat.load_state_dict(ref.state_dict())
+    # bf16-representable operands so the comparison isolates accumulation error
+    with torch.no_grad():
+        for p in list(ref.parameters()) + list(nat.parameters()):
+            p.copy_(p.bfloat16().float())
+    assert native_layers.install(nat) == [""]
+    x = torch.randn(N, C, H, H, device=gpu_device).bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    xn = x.clone().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    yr = ref(xr)
+    yn = nat(xn)
+    assert yn.shape == yr.shape and yn.dtype == torch.bfloat16
+    gy = torch.randn_like(yr).bfloat16().float()
+    yr.backward(gy)
+    yn.backward(gy.to(torch.bfloat16))
+    torch.cuda.synchronize()
+    assert _rel(yn, yr) < 1e-2
+    assert _rel(xn.grad, xr.grad) < 1e-2
+    assert _rel(nat.weight.grad, ref.weight.grad) < 1e-2
+    if bias:
+        assert _rel(nat.bias.grad, ref.bias.grad) < 1e-2
+
+
+# (N, H, C, k, stride, groups): depthwise (native dwconv kernels) and grouped (fp32 fallback)
+DW = [(8, 16, 32, 3, 1, 32), (4, 16, 64, 5, 2, 64), (4, 8, 96, 7, 1, 96), (4, 16, 64, 3, 1, 2), (4, 16, 58, 1, 1, 1)]
+
+
+@pytest.mark.parametrize("shape", DW, ids=[str(s) for s in DW])
+def test_depthwise_and_fallback_convs(gpu_device, shape):
+    from fedmi.ops import native_layers
+
+    N, H, C, k, st, g = shape
+    torch.manual_seed(1)
+    ref = nn.Conv2d(C, C, k, st, k // 2, groups=g, bias=False).to(gpu_device)
+    nat = nn.Conv2d(C, C, k, st, k // 2, groups=g, bias=False).to(gpu_device)
+    with torch.no_grad():
+        ref.weight.copy_(ref.weight.bfloat16().float())
+        nat.weight.copy_(ref.weight)
+    native = native_layers.install(nat) == [""]
+    assert native == (g == C)
+    x = torch.randn(N, C, H, H, device=gpu_device).bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    xn = x.clone().contiguous(memory_format=torch.channels_last).bfloat16().requires_grad_(True)
+    yr, yn = ref(xr), nat(xn)
+    assert yn.dtype == torch.bfloat16 and yn.is_contiguous(memory_format=torch.channels_last)
+    gy = torch.randn_like(yr).bfloat16().float()
+    yr.backward(gy)
+    yn.backward(gy.to(torch.bfloat16))
+    torch.cuda.synchronize()
+    assert _rel(yn, yr) < 1e-2
+    assert _rel(xn.grad, xr.grad) < 1e-2
+    assert _rel(nat.weight.grad, ref.weight.grad) < 1e-2
+
+
+@pytest.mark.parametrize("name", ["densenet_cifar", "SENet18", "SimpleDLA", "ShuffleNetV2", "DPN26"])
+def test_hybrid_engine_trains_like_fp32(gpu_device, name):
+    from fedmi.engine import build_trainer
+    from fedmi.engine.torch_engine import TorchTrainer
+
+    data = make_dataset("synthetic-cifar10-easy", device=gpu_device, n_train=1280, n_test=500, seed=0)
+    cfg = TrainerConfig(batch_size=128, lr=0.02, seed=7)
+    init = build_model(name).state_dict()
+    res = {}
+    for kind in ("hybrid", "fp32"):
+        tr = (build_trainer(name, data, gpu_device, cfg, init_state=init) if kind == "hybrid"
+              else TorchTrainer(name, data, gpu_device, cfg, init_state=init))
+        if kind == "hybrid":
+            assert isinstance(tr, TorchTrainer) and tr.hybrid and len(tr.native_convs) > 0
+        tr.set_schedule(*contiguous_schedule(len(data.train), 128))
+        losses = []
+        for _ in range(3):
+            tr.train_epoch()
+            losses.append(tr.train_stats().loss)
+        tr.evaluate()
+        res[kind] = (losses, tr.eval_stats())
+    (lh, eh), (lf, ef) = res["hybrid"], res["fp32"]
+    assert abs(lh[0] - lf[0]) < 0.05 * lf[0], (lh, lf)
+    assert lh[-1] < lh[0], (lh, lf)
+    assert eh.count == ef.count == 500
+    # test accuracy after 3 short epochs swings 30-80 % run to run for the deep models (BN running
+    # statistics still lag the weights; tools/diag_hybrid.py): compare the training trajectories instead
+    assert lh[-1] < 1.5 * lf[-1] + 0.1, (lh, lf)
+    assert eh.loss == eh.loss and eh.acc > 0.0

@@ -1,0 +1,48 @@
+"""Per-step time of the generic engine on zoo models without a whole-network native engine:
+PyTorch fp32 (MIOpen) vs PyTorch bf16 channels-last autocast (MIOpen) vs hybrid (native MFMA convs).
+
+    python tools/bench_hybrid.py [model ...]      -> one JSON line per (model, mode)
+"""
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+import torch  # noqa: E402
+
+from fedmi.engine.base import TrainerConfig  # noqa: E402
+from fedmi.engine.data import make_dataset  # noqa: E402
+from fedmi.engine.torch_engine import TorchTrainer  # noqa: E402
+from fedmi.models import build_model  # noqa: E402
+
+MODELS = sys.argv[1:] or ["DenseNet121", "SENet18", "SimpleDLA", "DPN26", "RegNetX_200MF", "ResNeXt29_2x64d",
+                          "EfficientNetB0", "ShuffleNetV2"]
+dev = torch.device("cuda", 0)
+data = make_dataset("synthetic-cifar10", device=dev, n_train=128 * 12, n_test=1000, seed=0)
+for name in MODELS:
+    init = build_model(name).state_dict()
+    for mode in ("fp32", "bf16-miopen-graph", "hybrid-eager", "hybrid-graph"):
+        tr = TorchTrainer(name, data, dev, TrainerConfig(seed=1), init_state=init, hybrid=(mode != "fp32"))
+        tr.use_graph = mode.endswith("graph")
+        if mode.startswith("bf16-miopen"):
+            for m in tr.model.modules():
+                m.__dict__.pop("forward", None)      # drop the native override, keep autocast + channels-last
+            tr.native_convs = []
+        tr.model.train()
+        for i in range(3):
+            tr.train_step(128 * i, 128)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = 9
+        for i in range(n):
+            tr.train_step(128 * (3 + i), 128)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / n * 1e3
+        tr.evaluate()
+        print(json.dumps({"model": name, "mode": mode, "ms_per_step": round(ms, 3),
+                          "native_convs": len(tr.native_convs),
+                          "eval_acc": round(tr.eval_stats().acc, 2)}), flush=True)
+        del tr
+        torch.cuda.empty_cache()
