@@ -9,7 +9,8 @@ channels-last bf16 end to end (the network runs under bf16 autocast; BN / poolin
 PyTorch on the same NHWC tensors, so no layout change happens between layers).
 
 Eligible: ``groups == 1``, no dilation, stride 1 or 2 (square), symmetric zero padding, in/out channels
-multiples of 8.  Depthwise convs (``groups == C == O``, square 3/5/7 windows, C % 8 == 0, C <= 2048) run
+multiples of 8.  Grouped convs with at most 8 groups of width % 8 == 0 (ResNeXt) run one implicit
+GEMM per group on channel-sliced copies.  Depthwise convs (``groups == C == O``, square 3/5/7 windows, C % 8 == 0, C <= 2048) run
 on the depthwise kernels (``csrc/kernels/dwconv.hip``).  Every other conv (grouped, odd widths, the
 3-channel stems) runs PyTorch's fp32 NCHW kernel: MIOpen's bf16 channels-last grouped / odd-width
 convolutions measured up to 2x slower than its fp32 ones (profiles/hybrid_engine_r1.jsonl).
@@ -39,6 +40,21 @@ def conv_eligible(m: nn.Module) -> bool:
             and m.out_channels % 8 == 0 and k[0] <= 7 and k[1] <= 7)
 
 
+MAX_GROUPS = 8
+
+
+def grouped_eligible(m: nn.Module) -> bool:
+    """Grouped conv with few, wide groups (ResNeXt cardinality <= 8, group width % 8 == 0): one MFMA
+    implicit GEMM per group on channel-sliced copies of the operands."""
+    if type(m) is not nn.Conv2d or not (1 < m.groups <= MAX_GROUPS):
+        return False
+    k, s, p, d = m.kernel_size, m.stride, m.padding, m.dilation
+    G = m.groups
+    return (m.in_channels % (8 * G) == 0 and m.out_channels % (8 * G) == 0 and d == (1, 1) and s[0] == s[1]
+            and s[0] in (1, 2) and not isinstance(p, str) and p[0] == p[1] and m.padding_mode == "zeros"
+            and k[0] <= 7 and k[1] <= 7)
+
+
 def dw_eligible(m: nn.Module) -> bool:
     if type(m) is not nn.Conv2d:
         return False
@@ -50,7 +66,7 @@ def dw_eligible(m: nn.Module) -> bool:
 
 
 def fallback(m: nn.Module) -> bool:
-    return type(m) is nn.Conv2d and not conv_eligible(m) and not dw_eligible(m)
+    return type(m) is nn.Conv2d and not conv_eligible(m) and not dw_eligible(m) and not grouped_eligible(m)
 
 
 def _nhwc_bf16(t: torch.Tensor) -> torch.Tensor:
@@ -93,6 +109,49 @@ class _NativeConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = C.conv2d_wgrad(xh, gyh, R, S, stride, pad)
         return dx, dw, None, None
+
+
+class _NativeGroupedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride: int, pad: int, groups: int):
+        xh = _nhwc_bf16(x)
+        O, Cg, R, S = w.shape
+        Og = O // groups
+        xs, wps, ys = [], [], []
+        for g in range(groups):
+            xg = xh[..., g * Cg:(g + 1) * Cg].contiguous()
+            wp = C.pack_weight(w.detach()[g * Og:(g + 1) * Og])
+            ws = _ws(x.device, C.fd_ws_floats(xg.shape, Og, R, S, stride, pad))
+            ys.append(C.conv2d_fwd(xg, wp, stride, pad, ws=ws))
+            xs.append(xg)
+            wps.append(wp)
+        ctx.save_for_backward(w, *xs, *wps)
+        ctx.stride, ctx.pad, ctx.groups, ctx.x_dtype = stride, pad, groups, x.dtype
+        return torch.cat(ys, dim=3).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gy):
+        G, stride, pad = ctx.groups, ctx.stride, ctx.pad
+        w, xs, wps = ctx.saved_tensors[0], ctx.saved_tensors[1:1 + G], ctx.saved_tensors[1 + G:]
+        O, Cg, R, S = w.shape
+        Og = O // G
+        gyh = _nhwc_bf16(gy)
+        dxs, dws = [], []
+        for g in range(G):
+            dyg = gyh[..., g * Og:(g + 1) * Og].contiguous()
+            if ctx.needs_input_grad[0]:
+                ws = _ws(gy.device, C.fd_ws_floats(xs[g].shape, Og, R, S, stride, pad))
+                dxs.append(C.conv2d_dgrad(dyg, wps[g], xs[g].shape, stride, pad, ws=ws))
+            if ctx.needs_input_grad[1]:
+                dws.append(C.conv2d_wgrad(xs[g], dyg, R, S, stride, pad))
+        dx = dw = None
+        if dxs:
+            dx = torch.cat(dxs, dim=3).permute(0, 3, 1, 2)
+            if ctx.x_dtype != torch.bfloat16:
+                dx = dx.to(ctx.x_dtype)
+        if dws:
+            dw = torch.cat(dws, dim=0)
+        return dx, dw, None, None, None
 
 
 class _NativeDWFn(torch.autograd.Function):
@@ -144,6 +203,15 @@ def _dw_forward(self: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     return y
 
 
+def _grouped_forward(self: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    if self.weight.dtype != torch.float32 or not self.weight.is_contiguous():
+        raise ValueError("native grouped conv: weight must be the contiguous fp32 master")
+    y = _NativeGroupedFn.apply(x, self.weight, int(self.stride[0]), int(self.padding[0]), int(self.groups))
+    if self.bias is not None:
+        y = y + self.bias.to(y.dtype).view(1, -1, 1, 1)
+    return y
+
+
 def _fallback_forward(self: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     with torch.autocast("cuda", enabled=False):
         y = nn.Conv2d._conv_forward(self, x.float().contiguous(), self.weight, self.bias)
@@ -162,6 +230,9 @@ def install(model: nn.Module) -> List[str]:
         elif dw_eligible(m):
             m.forward = types.MethodType(_dw_forward, m)
             done.append(name)
+        elif grouped_eligible(m):
+            m.forward = types.MethodType(_grouped_forward, m)
+            done.append(name)
         elif fallback(m):
             m.forward = types.MethodType(_fallback_forward, m)
     return done
@@ -176,7 +247,7 @@ def coverage(model: nn.Module) -> dict:
         if isinstance(m, nn.Conv2d):
             k = m.weight.numel()
             wt += k
-            if conv_eligible(m) or dw_eligible(m):
+            if conv_eligible(m) or dw_eligible(m) or grouped_eligible(m):
                 nat += 1
                 wn += k
             else:
@@ -184,4 +255,4 @@ def coverage(model: nn.Module) -> dict:
     return {"native": nat, "fallback": fb, "native_weight_frac": (wn / wt) if wt else 0.0}
 
 
-__all__ = ["conv_eligible", "dw_eligible", "fallback", "native_conv2d", "install", "coverage"]
+__all__ = ["conv_eligible", "grouped_eligible", "dw_eligible", "fallback", "native_conv2d", "install", "coverage"]

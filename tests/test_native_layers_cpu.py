@@ -11,12 +11,14 @@ def test_eligibility_rules():
     ok = [nn.Conv2d(64, 128, 3, 1, 1), nn.Conv2d(24, 48, 1), nn.Conv2d(64, 64, 3, 2, 1, bias=False),
           nn.Conv2d(16, 32, 7, 2, 3)]
     bad = [nn.Conv2d(3, 64, 3, 1, 1),                 # stem: C % 8
-           nn.Conv2d(64, 64, 3, 1, 1, groups=2),      # grouped
+           nn.Conv2d(64, 64, 3, 1, 1, groups=16),     # grouped, many narrow groups (RegNet)
            nn.Conv2d(64, 64, 3, 1, 1, groups=64),     # depthwise
            nn.Conv2d(64, 64, 3, 1, 2, dilation=2),    # dilated
            nn.Conv2d(36, 48, 1),                      # DenseNet growth-12 widths
            nn.Conv2d(64, 64, 3, 3, 1)]                # stride 3
     assert all(native_layers.conv_eligible(m) for m in ok)
+    assert native_layers.grouped_eligible(nn.Conv2d(128, 128, 3, 1, 1, groups=2))
+    assert native_layers.dw_eligible(nn.Conv2d(64, 64, 3, 1, 1, groups=64))
     assert not any(native_layers.conv_eligible(m) for m in bad)
 
 
