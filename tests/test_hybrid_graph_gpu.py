@@ -10,9 +10,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("name", ["SimpleDLA", "EfficientNetB0"])
-def test_hybrid_graph_matches_eager(gpu_device, name):
+def test_hybrid_graph_matches_eager(gpu_device, name, monkeypatch):
     from fedmi.engine.torch_engine import TorchTrainer
 
+    monkeypatch.setenv("FEDMI_HYBRID_GRAPH", "1")
     data = make_dataset("synthetic-cifar10-easy", device=gpu_device, n_train=512, n_test=200, seed=0)
     init = build_model(name).state_dict()
     runs = {}
