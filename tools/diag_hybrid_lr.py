@@ -20,13 +20,25 @@ data = make_dataset("synthetic-cifar10", device=dev, n_train=n, n_test=500, seed
 init = build_model(name).state_dict()
 MODES = sys.argv[3].split(",") if len(sys.argv) > 3 else ["fp32", "hyb-eager", "hyb-graph"]
 for mode in MODES:
-    # hyb-graph-nomiopen: MIOpen off (PyTorch's own BN / conv kernels) ; bf16-graph: native convs removed
+    # *-nchw: NCHW input; hyb-graph-nomiopen: MIOpen off (PyTorch's own BN / conv kernels) ; bf16-graph: native convs removed
     torch.backends.cudnn.enabled = mode != "hyb-graph-nomiopen"
     tr = TorchTrainer(name, data, dev, TrainerConfig(lr=0.02 if mode.endswith("lr02") else 0.1, seed=1,
                                                      use_graph="graph" in mode),
                       init_state=init, hybrid=not mode.startswith("fp32"))
-    if mode == "fp32-graph":
-        tr.use_graph = True
+    tr.use_graph = "graph" in mode
+    torch.backends.cuda.preferred_blas_library("cublas" if "rocblas" in mode else "default")
+    if "fp32linear" in mode:                  # classifier GEMMs outside autocast
+        import types
+        from torch import nn
+
+        def _lin(self, x):
+            with torch.autocast("cuda", enabled=False):
+                return nn.functional.linear(x.float(), self.weight, self.bias)
+        for m in tr.model.modules():
+            if isinstance(m, nn.Linear):
+                m.forward = types.MethodType(_lin, m)
+    if "nchw" in mode:                       # keep the network input NCHW (no channels-last propagation)
+        tr._layout = lambda x: x
     if mode == "bf16-graph":
         for m in tr.model.modules():
             m.__dict__.pop("forward", None)
