@@ -95,10 +95,11 @@ class TorchTrainer(LocalTrainer):
             self.native_convs = native_layers.install(self.model)
         # hybrid mode replays each full-batch SGD step (forward + autograd backward + SGD + stats) from
         # one captured HIP graph: the Python / launch overhead of ~10^3 small kernels per step goes away
-        # Opt-in (FEDMI_HYBRID_GRAPH=1): SENet18 at lr 0.1 replayed from the graph goes NaN ~130 steps in
-        # while the identical eager step sequence trains for 2+ epochs (native convs off / MIOpen off /
-        # autocast cache off all still diverge; fp32 without autocast does not) — open issue, so the
-        # default hybrid step runs eagerly (tools/diag_hybrid_lr.py, profiles/hybrid_engine_r1.jsonl).
+        # Opt-in (FEDMI_HYBRID_GRAPH=1): SENet18 replayed from the graph goes NaN ~130 steps in (earlier
+        # when the host syncs every replay) while the identical eager sequence trains for 2+ epochs;
+        # ResNet18 / SimpleDLA replay cleanly, and native convs, MIOpen, BLAS backend, layout and the
+        # autocast cache are all excluded — the trigger sits in the bf16 squeeze-excite ops under replay
+        # (tools/diag_hybrid_lr.py, profiles/hybrid_graph_nan_diag_r1.txt).  Default: eager.
         self.use_graph = bool(self.hybrid and cfg.use_graph and os.environ.get("FEDMI_HYBRID_GRAPH", "0") == "1")
         self._graph = None
         self._gx = self._gy = None

@@ -188,6 +188,8 @@ def native_conv2d(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> to
 
 
 def _forward(self: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    if self.kernel_size == (1, 1) and x.shape[2] == 1 and x.shape[3] == 1:
+        return _fallback_forward(self, x)       # squeeze-excite FC on a 1x1 map: a tiny fp32 GEMM
     y = native_conv2d(x, self.weight, self.stride[0], self.padding[0])
     if self.bias is not None:
         y = y + self.bias.to(y.dtype).view(1, -1, 1, 1)
@@ -213,6 +215,12 @@ def _grouped_forward(self: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
 
 
 def _fallback_forward(self: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    if (self.kernel_size == (1, 1) and self.groups == 1 and self.padding in ((0, 0), 0) and x.shape[2] == 1
+            and x.shape[3] == 1):
+        # 1x1 conv on a 1x1 map (squeeze-excite FCs): a plain fp32 GEMM, no MIOpen solver search
+        with torch.autocast("cuda", enabled=False):
+            y = torch.nn.functional.linear(x.float().flatten(1), self.weight.flatten(1), self.bias)
+        return y.to(torch.bfloat16)[:, :, None, None]
     with torch.autocast("cuda", enabled=False):
         y = nn.Conv2d._conv_forward(self, x.float().contiguous(), self.weight, self.bias)
     return y.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)

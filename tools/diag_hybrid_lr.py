@@ -48,6 +48,8 @@ for mode in MODES:
     for j in range(2 * steps):
         i = j % steps
         loss = tr.train_step(128 * i, 128)
+        if "sync" in mode:                    # host waits for every replay (no launch run-ahead)
+            torch.cuda.synchronize()
         if j % 30 == 29:
             v = float(loss.detach())
             out.append(round(v, 3))
