@@ -97,9 +97,10 @@ class TorchTrainer(LocalTrainer):
         # one captured HIP graph: the Python / launch overhead of ~10^3 small kernels per step goes away
         # Opt-in (FEDMI_HYBRID_GRAPH=1): SENet18 replayed from the graph goes NaN ~130 steps in (earlier
         # when the host syncs every replay) while the identical eager sequence trains for 2+ epochs;
-        # ResNet18 / SimpleDLA replay cleanly, and native convs, MIOpen, BLAS backend, layout and the
-        # autocast cache are all excluded — the trigger sits in the bf16 squeeze-excite ops under replay
-        # (tools/diag_hybrid_lr.py, profiles/hybrid_graph_nan_diag_r1.txt).  Default: eager.
+        # ResNet18 / SimpleDLA replay cleanly; one trigger was PyTorch's bf16 adaptive_avg_pool2d (now an
+        # fp32 mean, models/zoo/pool.py: SENet18 replays cleanly), but EfficientNetB0 / RegNetY_400MF still
+        # diverge under replay only (tools/diag_hybrid_lr.py, profiles/hybrid_graph_nan_diag_r1.txt).
+        # Default: eager.
         self.use_graph = bool(self.hybrid and cfg.use_graph and os.environ.get("FEDMI_HYBRID_GRAPH", "0") == "1")
         self._graph = None
         self._gx = self._gy = None

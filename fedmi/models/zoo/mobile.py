@@ -19,6 +19,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .pool import global_avg_pool
+
 
 def _bn(c: int) -> nn.BatchNorm2d:
     return nn.BatchNorm2d(c)
@@ -240,7 +242,7 @@ class SqueezeExcite(nn.Module):
         self.act = act
 
     def forward(self, x):
-        s = self.act(self.se1(F.adaptive_avg_pool2d(x, 1)))
+        s = self.act(self.se1(global_avg_pool(x)))
         return x * torch.sigmoid(self.se2(s))
 
 
@@ -290,7 +292,7 @@ class EfficientNet(nn.Module):
 
     def forward(self, x):
         y = self.layers(swish(self.bn1(self.conv1(x))))
-        y = torch.flatten(F.adaptive_avg_pool2d(y, 1), 1)
+        y = torch.flatten(global_avg_pool(y), 1)
         if self.training and self.dropout > 0:
             y = F.dropout(y, p=self.dropout)
         return self.linear(y)
@@ -339,7 +341,7 @@ class RegNet(nn.Module):
     def forward(self, x):
         y = F.relu(self.bn1(self.conv1(x)))
         y = self.layer4(self.layer3(self.layer2(self.layer1(y))))
-        return self.linear(torch.flatten(F.adaptive_avg_pool2d(y, 1), 1))
+        return self.linear(torch.flatten(global_avg_pool(y), 1))
 
 
 # --------------------------------------------------------------------------- PNASNet

@@ -16,6 +16,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .pool import global_avg_pool
+
 
 def _conv3(cin: int, cout: int, stride: int = 1, groups: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, groups=groups, bias=False)
@@ -207,7 +209,7 @@ class SEPreActBlock(nn.Module):
         pre = F.relu(self.bn1(x))
         skip = self.shortcut(pre) if hasattr(self, "shortcut") else x
         y = self.conv2(F.relu(self.bn2(self.conv1(pre))))
-        gate = torch.sigmoid(self.fc2(F.relu(self.fc1(F.adaptive_avg_pool2d(y, 1)))))
+        gate = torch.sigmoid(self.fc2(F.relu(self.fc1(global_avg_pool(y)))))
         return y * gate + skip
 
 

@@ -26,6 +26,18 @@ for mode in MODES:
                                                      use_graph="graph" in mode),
                       init_state=init, hybrid=not mode.startswith("fp32"))
     tr.use_graph = "graph" in mode
+    if "meanpool" in mode:                    # SE global pool as an fp32 mean instead of adaptive_avg_pool2d
+        import torch.nn.functional as F
+        from fedmi.models.zoo import residual as _res
+
+        class _F:
+            def __getattr__(self, k):
+                return getattr(F, k)
+
+            @staticmethod
+            def adaptive_avg_pool2d(x, out):
+                return x.float().mean((2, 3), keepdim=True).to(x.dtype)
+        _res.F = _F()
     torch.backends.cuda.preferred_blas_library("cublas" if "rocblas" in mode else "default")
     if "fp32linear" in mode:                  # classifier GEMMs outside autocast
         import types
