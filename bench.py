@@ -191,7 +191,7 @@ def main() -> int:
                    "local_epochs_per_round": 1, "eval_per_round": not args.no_eval,
                    "eval_split": "full-per-client" if args.eval_full or world == 1 else f"1/{world}-per-client",
                    "data_split": f"noniid-{args.noniid}-shards" if args.noniid else "strided-iid",
-                   "aggregation": "rccl-allreduce" + ("" if args.compress == "none" else f"+{args.compress}"),
+                   "aggregation": ("gloo-rehearsal-allreduce" if rehearse and world > 1 else "rccl-allreduce") +("" if args.compress == "none" else f"+{args.compress}"),
                    "hip_graph": not args.no_graph},
         "rounds_per_sec": round(rounds_per_s, 4),
         "samples_per_sec_per_client": round(value / world, 3),
