@@ -1,0 +1,335 @@
+// fedmi — peer-to-peer collectives over hipIpc-mapped staging buffers (see peer_comm.h).
+//
+// Synchronisation (one barrier = one phase):
+//   every wave of the workgroup waits for its own stores (vmcnt 0), workgroup
+//   barrier, wave 0 issues a SYSTEM-scope release (L2 write-back: the peer may be
+//   another GPU across xGMI or another XCD of this one), then lane p stores the
+//   call's epoch into rank p's flag slot [phase][block][me] and polls its own slot
+//   [phase][block][p]; a SYSTEM-scope acquire (L1/L2 invalidate) follows, then a
+//   workgroup barrier releases the other waves to read peer data.
+//   Flags live in uncached memory; polls are bounded by a wall-clock timeout that
+//   sets PeerSignal::error instead of hanging when a peer died mid-collective.
+//
+// Buffer reuse: call k uses staging slot k & 1.  A rank rewrites slot k & 1 only
+// in call k + 2, after call k + 1's barrier, which every peer enters only once
+// its stream has finished call k — so one barrier per call suffices for oneshot.
+#include "peer_comm.h"
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace fedmi {
+void check_hip(hipError_t e, const char* what);
+}
+
+namespace {
+
+using fedmi::PeerArgs;
+using fedmi::PeerSignal;
+using fedmi::kPeerMaxRanks;
+
+#define PDEV __device__ __forceinline__
+
+PDEV uint32_t ld_sys(const uint32_t* p) { return __scoped_atomic_load_n(p, __ATOMIC_RELAXED, __MEMORY_SCOPE_SYSTEM); }
+PDEV void st_sys(uint32_t* p, uint32_t v) { __scoped_atomic_store_n(p, v, __ATOMIC_RELAXED, __MEMORY_SCOPE_SYSTEM); }
+
+PDEV char* region(const PeerArgs& a, int p, int slot, int which) {
+  return a.data[p] + (long long)(slot * 2 + which) * a.cap;
+}
+
+// Epoch of this call for workgroup b (device-side counter: replays from a graph stay in step).
+PDEV uint32_t begin_call(const PeerArgs& a, int b) {
+  __shared__ uint32_t s_ep;
+  if (threadIdx.x == 0) s_ep = ld_sys(&a.sig[a.rank]->epoch[b]) + 1u;
+  __syncthreads();
+  return s_ep;
+}
+
+PDEV void end_call(const PeerArgs& a, int b, uint32_t ep) {
+  if (threadIdx.x == 0) st_sys(&a.sig[a.rank]->epoch[b], ep);
+}
+
+PDEV void peer_barrier(const PeerArgs& a, int phase, int b, uint32_t ep) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int p = threadIdx.x;
+    if (p < a.world) {
+      st_sys(&a.sig[p]->flags[phase][b][a.rank], ep);
+      const uint32_t* mine = &a.sig[a.rank]->flags[phase][b][p];
+      const unsigned long long t0 = wall_clock64();
+      while (ld_sys(mine) < ep) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((long long)(wall_clock64() - t0) > a.timeout_ticks) {
+          st_sys(&a.sig[a.rank]->error, 1u);
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+PDEV float4 f4add(float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); }
+
+// Sum of element i (float4 granule) over all ranks, in rank order 0..W-1.
+PDEV float4 gather_sum4(const PeerArgs& a, int slot, long long i) {
+  float4 v[kPeerMaxRanks];
+#pragma unroll
+  for (int p = 0; p < kPeerMaxRanks; ++p)
+    if (p < a.world) v[p] = reinterpret_cast<const float4*>(region(a, p, slot, 0))[i];
+  float4 acc = v[0];
+#pragma unroll
+  for (int p = 1; p < kPeerMaxRanks; ++p)
+    if (p < a.world) acc = f4add(acc, v[p]);
+  return acc;
+}
+
+PDEV float gather_sum1(const PeerArgs& a, int slot, long long i) {
+  float acc = reinterpret_cast<const float*>(region(a, 0, slot, 0))[i];
+  for (int p = 1; p < a.world; ++p) acc += reinterpret_cast<const float*>(region(a, p, slot, 0))[i];
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void peer_oneshot_f32_kernel(PeerArgs a, const float* in, float* out, long long n,
+                                                               float scale) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const uint32_t ep = begin_call(a, b);
+  const int slot = ep & 1;
+  const long long n4 = n >> 2, stride = (long long)gridDim.x * 256;
+  const int tail = (int)(n & 3);
+  float* mine = reinterpret_cast<float*>(region(a, a.rank, slot, 0));
+  for (long long i = (long long)b * 256 + t; i < n4; i += stride)
+    reinterpret_cast<float4*>(mine)[i] = reinterpret_cast<const float4*>(in)[i];
+  if (b == 0 && t < tail) mine[n4 * 4 + t] = in[n4 * 4 + t];
+  peer_barrier(a, 0, b, ep);
+  for (long long i = (long long)b * 256 + t; i < n4; i += stride) {
+    float4 s = gather_sum4(a, slot, i);
+    s.x *= scale; s.y *= scale; s.z *= scale; s.w *= scale;
+    reinterpret_cast<float4*>(out)[i] = s;
+  }
+  if (b == 0 && t < tail) out[n4 * 4 + t] = scale * gather_sum1(a, slot, n4 * 4 + t);
+  end_call(a, b, ep);
+}
+
+// Two-shot: slices of L float4 granules; rank r owns slice r.
+__global__ __launch_bounds__(256) void peer_twoshot_f32_kernel(PeerArgs a, const float* in, float* out, long long n,
+                                                               float scale) {
+  const int b = blockIdx.x, t = threadIdx.x, W = a.world, r = a.rank;
+  const uint32_t ep = begin_call(a, b);
+  const int slot = ep & 1;
+  const long long n4 = n >> 2, stride = (long long)gridDim.x * 256;
+  const long long L = (n4 + W - 1) / W;
+  const int tail = (int)(n & 3);
+  float* mine_in = reinterpret_cast<float*>(region(a, r, slot, 0));
+  float* mine_out = reinterpret_cast<float*>(region(a, r, slot, 1));
+  // 1. stage the whole input (slice s, sub-range of workgroup b, for every s)
+  for (int s = 0; s < W; ++s) {
+    const long long lo = s * L, hi = (s + 1) * L < n4 ? (s + 1) * L : n4;
+    for (long long i = lo + (long long)b * 256 + t; i < hi; i += stride)
+      reinterpret_cast<float4*>(mine_in)[i] = reinterpret_cast<const float4*>(in)[i];
+  }
+  if (b == 0 && t < tail) mine_in[n4 * 4 + t] = in[n4 * 4 + t];
+  peer_barrier(a, 0, b, ep);
+  // 2. reduce my slice from every peer, push the result into every peer's result area
+  {
+    const long long lo = r * L, hi = (r + 1) * L < n4 ? (r + 1) * L : n4;
+    for (long long i = lo + (long long)b * 256 + t; i < hi; i += stride) {
+      float4 s = gather_sum4(a, slot, i);
+      s.x *= scale; s.y *= scale; s.z *= scale; s.w *= scale;
+      for (int p = 0; p < W; ++p) reinterpret_cast<float4*>(region(a, p, slot, 1))[i] = s;
+    }
+    if (r == 0 && b == 0 && t < tail) {
+      const float v = scale * gather_sum1(a, slot, n4 * 4 + t);
+      for (int p = 0; p < W; ++p) reinterpret_cast<float*>(region(a, p, slot, 1))[n4 * 4 + t] = v;
+    }
+  }
+  peer_barrier(a, 1, b, ep);
+  // 3. every slice of the result is now in my result area
+  for (int s = 0; s < W; ++s) {
+    const long long lo = s * L, hi = (s + 1) * L < n4 ? (s + 1) * L : n4;
+    for (long long i = lo + (long long)b * 256 + t; i < hi; i += stride)
+      reinterpret_cast<float4*>(out)[i] = reinterpret_cast<const float4*>(mine_out)[i];
+  }
+  if (b == 0 && t < tail) out[n4 * 4 + t] = mine_out[n4 * 4 + t];
+  end_call(a, b, ep);
+}
+
+// int64 counters (BN num_batches_tracked): floor(sum / W), one workgroup.
+__global__ __launch_bounds__(256) void peer_i64_mean_floor_kernel(PeerArgs a, const int64_t* in, int64_t* out,
+                                                                  long long n) {
+  const uint32_t ep = begin_call(a, 0);
+  const int slot = ep & 1;
+  int64_t* mine = reinterpret_cast<int64_t*>(region(a, a.rank, slot, 0));
+  for (long long i = threadIdx.x; i < n; i += 256) mine[i] = in[i];
+  peer_barrier(a, 0, 0, ep);
+  for (long long i = threadIdx.x; i < n; i += 256) {
+    int64_t s = 0;
+    for (int p = 0; p < a.world; ++p) s += reinterpret_cast<const int64_t*>(region(a, p, slot, 0))[i];
+    int64_t q = s / a.world;
+    if ((s % a.world) != 0 && s < 0) --q;          // floor, like torch.div(..., rounding_mode="floor")
+    out[i] = q;
+  }
+  end_call(a, 0, ep);
+}
+
+__global__ __launch_bounds__(256) void peer_allgather_kernel(PeerArgs a, const uint4* in, uint4* out, long long n16) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const uint32_t ep = begin_call(a, b);
+  const int slot = ep & 1;
+  const long long stride = (long long)gridDim.x * 256;
+  uint4* mine = reinterpret_cast<uint4*>(region(a, a.rank, slot, 0));
+  for (long long i = (long long)b * 256 + t; i < n16; i += stride) mine[i] = in[i];
+  peer_barrier(a, 0, b, ep);
+  for (int p = 0; p < a.world; ++p) {
+    const uint4* src = reinterpret_cast<const uint4*>(region(a, p, slot, 0));
+    for (long long i = (long long)b * 256 + t; i < n16; i += stride) out[(long long)p * n16 + i] = src[i];
+  }
+  end_call(a, b, ep);
+}
+
+}  // namespace
+
+namespace fedmi {
+
+PeerComm::PeerComm(int rank, int world, long long cap_bytes) {
+  if (world < 1 || world > kPeerMaxRanks) throw std::invalid_argument("PeerComm: world must be in [1, 16]");
+  if (rank < 0 || rank >= world) throw std::invalid_argument("PeerComm: bad rank");
+  if (cap_bytes <= 0) throw std::invalid_argument("PeerComm: capacity must be > 0");
+  cap_bytes = (cap_bytes + 255) & ~255LL;
+  check_hip(hipGetDevice(&device_), "hipGetDevice");
+  check_hip(hipExtMallocWithFlags(reinterpret_cast<void**>(&sig_), sizeof(PeerSignal), hipDeviceMallocUncached),
+            "PeerComm signal alloc");
+  check_hip(hipMemset(sig_, 0, sizeof(PeerSignal)), "PeerComm signal memset");
+  // Staging is uncached as well: the payload is read once per call by peers on other GPUs, and an
+  // uncached mapping needs no cache maintenance to be coherent across xGMI.
+  check_hip(hipExtMallocWithFlags(reinterpret_cast<void**>(&data_), 4 * cap_bytes, hipDeviceMallocUncached),
+            "PeerComm staging alloc");
+  check_hip(hipMemset(data_, 0, 4 * cap_bytes), "PeerComm staging memset");
+  check_hip(hipDeviceSynchronize(), "PeerComm init sync");
+  a_.rank = rank;
+  a_.world = world;
+  a_.cap = cap_bytes;
+  a_.sig[rank] = sig_;
+  a_.data[rank] = data_;
+  set_timeout_ms(30000.0);
+}
+
+PeerComm::~PeerComm() {
+  try {
+    disconnect();
+  } catch (...) {
+  }
+  (void)hipFree(data_);
+  (void)hipFree(sig_);
+}
+
+std::vector<uint8_t> PeerComm::handle() const {
+  hipIpcMemHandle_t hs, hd;
+  check_hip(hipIpcGetMemHandle(&hs, sig_), "hipIpcGetMemHandle(signal)");
+  check_hip(hipIpcGetMemHandle(&hd, data_), "hipIpcGetMemHandle(staging)");
+  std::vector<uint8_t> out(2 * sizeof(hipIpcMemHandle_t));
+  std::memcpy(out.data(), &hs, sizeof(hs));
+  std::memcpy(out.data() + sizeof(hs), &hd, sizeof(hd));
+  return out;
+}
+
+void PeerComm::connect(const std::vector<std::vector<uint8_t>>& handles) {
+  if ((int)handles.size() != a_.world) throw std::invalid_argument("PeerComm::connect: need one handle per rank");
+  if (connected_) return;
+  check_hip(hipSetDevice(device_), "hipSetDevice");
+  for (int p = 0; p < a_.world; ++p) {
+    if (p == a_.rank) continue;
+    if (handles[p].size() != 2 * sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("PeerComm: bad handle size");
+    hipIpcMemHandle_t hs, hd;
+    std::memcpy(&hs, handles[p].data(), sizeof(hs));
+    std::memcpy(&hd, handles[p].data() + sizeof(hs), sizeof(hd));
+    void* ps = nullptr;
+    void* pd = nullptr;
+    check_hip(hipIpcOpenMemHandle(&ps, hs, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(signal)");
+    check_hip(hipIpcOpenMemHandle(&pd, hd, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(staging)");
+    a_.sig[p] = reinterpret_cast<PeerSignal*>(ps);
+    a_.data[p] = reinterpret_cast<char*>(pd);
+  }
+  connected_ = true;
+}
+
+void PeerComm::disconnect() {
+  if (!connected_) return;
+  (void)hipDeviceSynchronize();
+  for (int p = 0; p < a_.world; ++p) {
+    if (p == a_.rank) continue;
+    if (a_.sig[p]) (void)hipIpcCloseMemHandle(a_.sig[p]);
+    if (a_.data[p]) (void)hipIpcCloseMemHandle(a_.data[p]);
+    a_.sig[p] = nullptr;
+    a_.data[p] = nullptr;
+  }
+  connected_ = false;
+}
+
+void PeerComm::set_timeout_ms(double ms) { a_.timeout_ticks = (long long)(ms * 1e5); }  // 100 MHz realtime clock
+
+uint32_t PeerComm::error() const {
+  uint32_t e = 0;
+  check_hip(hipMemcpy(&e, &sig_->error, sizeof(e), hipMemcpyDeviceToHost), "PeerComm::error");
+  return e;
+}
+
+void PeerComm::clear_error() { check_hip(hipMemset(&sig_->error, 0, sizeof(uint32_t)), "PeerComm::clear_error"); }
+
+int PeerComm::default_blocks(long long bytes, int algo, int world) {
+  long long g4 = bytes / 16;                         // float4 granules
+  if (algo == kPeerTwoShot) g4 = (g4 + world - 1) / world;
+  long long b = (g4 + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 128) b = 128;
+  return (int)b;
+}
+
+static void need(bool ok, const char* msg) {
+  if (!ok) throw std::invalid_argument(msg);
+}
+
+void PeerComm::allreduce_f32(hipStream_t st, const float* in, float* out, long long n, float scale, int algo,
+                             int blocks) {
+  need(connected_ || a_.world == 1, "PeerComm: not connected");
+  need(n >= 0 && n * 4 <= a_.cap, "PeerComm::allreduce_f32: payload exceeds capacity");
+  need((reinterpret_cast<uintptr_t>(in) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0,
+       "PeerComm::allreduce_f32: buffers must be 16-byte aligned");
+  if (n == 0) return;
+  if (blocks <= 0) blocks = default_blocks(n * 4, algo, a_.world);
+  need(blocks <= kPeerMaxBlocks, "PeerComm: too many blocks");
+  if (algo == kPeerTwoShot)
+    hipLaunchKernelGGL(peer_twoshot_f32_kernel, dim3(blocks), dim3(256), 0, st, a_, in, out, n, scale);
+  else
+    hipLaunchKernelGGL(peer_oneshot_f32_kernel, dim3(blocks), dim3(256), 0, st, a_, in, out, n, scale);
+  check_hip(hipGetLastError(), "peer allreduce_f32 launch");
+}
+
+void PeerComm::allreduce_i64_mean_floor(hipStream_t st, const int64_t* in, int64_t* out, long long n) {
+  need(connected_ || a_.world == 1, "PeerComm: not connected");
+  need(n >= 0 && n * 8 <= a_.cap, "PeerComm::allreduce_i64: payload exceeds capacity");
+  if (n == 0) return;
+  hipLaunchKernelGGL(peer_i64_mean_floor_kernel, dim3(1), dim3(256), 0, st, a_, in, out, n);
+  check_hip(hipGetLastError(), "peer allreduce_i64 launch");
+}
+
+void PeerComm::allgather(hipStream_t st, const void* in, void* out, long long nbytes, int blocks) {
+  need(connected_ || a_.world == 1, "PeerComm: not connected");
+  need(nbytes >= 0 && nbytes <= a_.cap && nbytes % 16 == 0, "PeerComm::allgather: bad size (<= cap, % 16)");
+  need((reinterpret_cast<uintptr_t>(in) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0,
+       "PeerComm::allgather: buffers must be 16-byte aligned");
+  if (nbytes == 0) return;
+  if (blocks <= 0) blocks = default_blocks(nbytes * a_.world, kPeerOneShot, a_.world);
+  need(blocks <= kPeerMaxBlocks, "PeerComm: too many blocks");
+  hipLaunchKernelGGL(peer_allgather_kernel, dim3(blocks), dim3(256), 0, st, a_, reinterpret_cast<const uint4*>(in),
+                     reinterpret_cast<uint4*>(out), nbytes / 16);
+  check_hip(hipGetLastError(), "peer allgather launch");
+}
+
+}  // namespace fedmi

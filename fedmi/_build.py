@@ -31,9 +31,11 @@ SOURCES = [
     CSRC / "kernels" / "conv_igemm.hip",
     CSRC / "kernels" / "cnn_ops.hip",
     CSRC / "kernels" / "dwconv.hip",
+    CSRC / "comm" / "peer_comm.hip",
     CSRC / "runtime" / "lenet_engine.cpp",
     CSRC / "bindings.cpp",
     CSRC / "bindings_cnn.cpp",
+    CSRC / "bindings_comm.cpp",
 ]
 HEADERS = sorted(CSRC.rglob("*.h"))
 

@@ -1,0 +1,147 @@
+"""Peer-to-peer (hipIpc) collectives: 2 and 4 client processes sharing cuda:0.
+
+RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so on a one-GPU
+box the hand-written peer kernels (csrc/comm/peer_comm.hip) are the only GPU
+data plane that can run multi-rank.  Every result is compared BIT-EXACTLY with
+the rank-ordered fp32 sum computed on the host, over many calls with fresh data
+(stale staging lines would show up), odd sizes (scalar tail), in-place use,
+alternating payload sizes (per-workgroup epochs stay in step), int64 floor-mean
+and all-gather.  A peer that never arrives must time out, not hang.
+"""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(240)]
+
+SIZES = [5, 62006, 1 << 20 | 3]
+
+
+def _data(rank: int, it: int, n: int) -> torch.Tensor:
+    g = torch.Generator().manual_seed(1000 * it + 17 * rank + n)
+    return torch.randn(n, generator=g)
+
+
+def _expected(world: int, it: int, n: int) -> torch.Tensor:
+    acc = _data(0, it, n).clone()
+    for r in range(1, world):
+        acc = acc + _data(r, it, n)
+    return acc * (1.0 / world)
+
+
+def _worker(rank, world, path, algo, q):
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    from fedmi.parallel.peer import PeerAllReduce
+
+    store = dist.FileStore(path, world)
+    dev = torch.device("cuda", 0)
+    res = {"ok": True, "msgs": []}
+    try:
+        pc = PeerAllReduce(rank, world, 4 * (max(SIZES) + 64), store, tag=f"t{algo}", algo=algo)
+        it = 0
+        for rep in range(3):
+            for n in SIZES:
+                x = _data(rank, it, n).to(dev)
+                pc.allreduce_mean_(x)                      # in place
+                got = x.cpu()
+                exp = _expected(world, it, n)
+                if not torch.equal(got, exp):
+                    res["ok"] = False
+                    res["msgs"].append(f"f32 n={n} it={it} maxdiff={(got - exp).abs().max().item():.3e}")
+                it += 1
+        # out-of-place with an explicit scale (sum)
+        src = _data(rank, 99, 4096).to(dev)
+        dst = torch.empty_like(src)
+        pc.allreduce_sum(src, dst, 1.0)
+        exp = _expected(world, 99, 4096) * world
+        if not torch.allclose(dst.cpu(), exp, rtol=1e-6, atol=1e-6):
+            res["ok"] = False
+            res["msgs"].append("sum mismatch")
+        # int64 floor mean (negatives floor like torch.div(rounding_mode='floor'))
+        iv = torch.tensor([10 + 3 * rank, -7 - rank, 5], dtype=torch.int64, device=dev)
+        pc.allreduce_mean_(iv)
+        tot = torch.tensor([sum(10 + 3 * r for r in range(world)), sum(-7 - r for r in range(world)), 5 * world])
+        if not torch.equal(iv.cpu(), torch.div(tot, world, rounding_mode="floor")):
+            res["ok"] = False
+            res["msgs"].append(f"i64 {iv.cpu().tolist()}")
+        # all-gather of a 10-element int32 tensor (40 B: padded to 48 internally)
+        gi = torch.arange(10, dtype=torch.int32, device=dev) + 100 * rank
+        rows = pc.all_gather(gi).cpu()
+        for r in range(world):
+            if not torch.equal(rows[r], torch.arange(10, dtype=torch.int32) + 100 * r):
+                res["ok"] = False
+                res["msgs"].append(f"allgather row {r}")
+        res["error"] = pc.error()
+        pc.close()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        res["ok"] = False
+        res["msgs"].append(repr(e))
+    q.put((rank, res))
+
+
+def _run(world: int, algo: str):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "store")
+        procs = [ctx.Process(target=_worker, args=(r, world, path, algo, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        out = dict(q.get(timeout=200) for _ in procs)
+        for p in procs:
+            p.join(timeout=60)
+    for r in range(world):
+        assert out[r]["ok"], (r, out[r]["msgs"])
+        assert out[r]["error"] == 0
+    for p in procs:
+        assert p.exitcode == 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_peer_oneshot_bit_exact(world):
+    _run(world, "oneshot")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_peer_twoshot_bit_exact(world):
+    _run(world, "twoshot")
+
+
+def _timeout_worker(rank, world, path, q):
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    from fedmi.parallel.peer import PeerAllReduce
+
+    store = dist.FileStore(path, world)
+    pc = PeerAllReduce(rank, world, 1 << 16, store, tag="to", timeout_ms=300.0)
+    x = torch.ones(1000, device="cuda")
+    err = 0
+    if rank == 0:                        # rank 1 never joins the collective
+        pc.allreduce_mean_(x)
+        torch.cuda.synchronize()
+        err = pc.error()
+    store.set(f"done{rank}", "1")
+    store.get("done0")
+    store.get("done1")
+    pc.close(barrier=False)
+    q.put((rank, err))
+
+
+def test_peer_timeout_sets_error_instead_of_hanging():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "store")
+        procs = [ctx.Process(target=_timeout_worker, args=(r, 2, path, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        out = dict(q.get(timeout=120) for _ in procs)
+        for p in procs:
+            p.join(timeout=60)
+    assert out[0] == 1 and out[1] == 0
