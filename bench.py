@@ -9,7 +9,9 @@ A *step* is one federated round with the reference's semantics
   1. local epoch: one pass over this client's strided 1/N shard of the 50,000
      training images at batch 128 with RandomCrop+HFlip augmentation, SGD
      (lr 0.1, momentum 0.9, wd 5e-4)   [fused HIP kernels, hipGraph replay]
-  2. FedAvg of the full model across clients   [RCCL all-reduce over xGMI]
+  2. FedAvg of the full model across clients   [hand-written hipIpc peer all-reduce
+     over xGMI (csrc/comm/peer_comm.hip) or RCCL -- ``--allreduce auto`` verifies
+     both against each other at start-up and keeps the faster]
   3. the global model is evaluated on the full 10,000-image test set: split
      over the N clients (they all hold the same averaged model), per-round
      (loss, correct, count) kept on device and summed over clients in one
@@ -57,6 +59,100 @@ def _baseline_rounds(model: str, n: int):
     return table.get(n)
 
 
+def _timed(fn, iters: int, device) -> float:
+    """ms per call (device time, cuda events), MAX over ranks."""
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize(device)
+    t = torch.tensor([e0.elapsed_time(e1) / iters], dtype=torch.float64)
+    if dist.get_backend() == "nccl":
+        t = t.to(device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_transport(args, trainer, rank: int, world: int, rehearse: bool, device):
+    """The FedAvg data plane at N>1.
+
+    ``oneshot``/``twoshot``: hipIpc peer kernels.  ``rccl``: torch.distributed (RCCL).
+    ``auto``: build the peer kernel, check it against the reference collective on random
+    data (all ranks must agree), time both on the model's flat state and keep the faster.
+    In the 1-GPU rehearsal RCCL cannot run (two ranks on one GPU), so the peer kernel
+    is the GPU data plane and gloo the fallback.
+    """
+    from fedmi.parallel.peer import PeerAllReduce
+
+    x = trainer.float_state()
+    want = args.allreduce
+    if want == "rccl":
+        return None, {"chosen": "rccl" if not rehearse else "gloo"}
+    algos = ["oneshot", "twoshot"] if want == "auto" else [want]
+    cap = max(4 * x.numel(), 16 * (int(x.numel() * args.topk_ratio) + 64), x.numel() + 4 * (x.numel() // 256 + 64))
+    store = dist.distributed_c10d._get_default_store()
+    ok = torch.ones(1, device=device if not rehearse else "cpu")
+    peer = None
+    try:
+        peer = PeerAllReduce(rank, world, cap, store, tag="bench", algo=algos[0], device=device)
+    except Exception as e:  # pragma: no cover - depends on the node's IPC/peer support
+        print(f"[bench] rank {rank}: peer transport unavailable: {e!r}", file=sys.stderr)
+        ok.zero_()
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if ok.item() < 1:
+        if peer is not None:
+            peer.close()
+        if want != "auto":
+            raise RuntimeError("--allreduce peer transport failed on some rank")
+        return None, {"chosen": "rccl", "reason": "peer transport unavailable"}
+    g = torch.Generator(device=device).manual_seed(1234 + rank)
+    probe = torch.randn(x.numel(), generator=g, device=device)
+    ref = probe.clone()
+    if rehearse:
+        ref_h = ref.cpu()
+        dist.all_reduce(ref_h)
+        ref = (ref_h / world).to(device)
+    else:
+        dist.all_reduce(ref, op=dist.ReduceOp.AVG)
+    info = {"verified_against": "gloo" if rehearse else "rccl"}
+    times = {}
+    for algo in algos:
+        peer.algo = algo
+        got = probe.clone()
+        peer.allreduce_mean_(got)
+        good = torch.allclose(got, ref, rtol=1e-5, atol=1e-6) and peer.error() == 0
+        okt = torch.tensor([1.0 if good else 0.0], device=device if not rehearse else "cpu")
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        if okt.item() < 1:
+            info[f"{algo}_verified"] = False
+            continue
+        info[f"{algo}_verified"] = True
+        buf = x.detach().clone()
+        times[algo] = _timed(lambda: peer.allreduce_mean_(buf), 20, device)
+    if not rehearse:
+        buf = x.detach().clone()
+        times["rccl"] = _timed(lambda: dist.all_reduce(buf, op=dist.ReduceOp.AVG), 20, device)
+    info["ms"] = {k: round(v, 5) for k, v in times.items()}
+    peer_times = {a: t for a, t in times.items() if a != "rccl"}
+    if not peer_times:
+        peer.close()
+        if want != "auto":
+            raise RuntimeError(f"peer all-reduce ({want}) failed verification")
+        info["chosen"] = "rccl"
+        return None, info
+    best = min(peer_times, key=peer_times.get)
+    if want == "auto" and "rccl" in times and times["rccl"] < peer_times[best]:
+        peer.close()
+        info["chosen"] = "rccl"
+        return None, info
+    peer.algo = best
+    info["chosen"] = best
+    return peer, info
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -69,6 +165,9 @@ def main() -> int:
     ap.add_argument("--compress", default="none", choices=["none", "topk", "int8"],
                     help="-c Y data-plane compression of the FedAvg update")
     ap.add_argument("--topk-ratio", type=float, default=0.01)
+    ap.add_argument("--allreduce", default="auto", choices=["auto", "rccl", "oneshot", "twoshot"],
+                    help="FedAvg transport at N>1: hipIpc peer kernels (oneshot/twoshot), RCCL, or auto = verify "
+                         "the peer kernel against RCCL and time both, keep the faster")
     ap.add_argument("--no-eval", action="store_true", help="skip per-round eval (NOT the headline config)")
     ap.add_argument("--eval-full", action="store_true",
                     help="every client evaluates the whole test set (reference-literal, redundant); default: "
@@ -118,7 +217,10 @@ def main() -> int:
         trainer.set_schedule(*contiguous_schedule(len(shards[rank]), BATCH))
     else:
         trainer.set_schedule(*strided_schedule(N_TRAIN, BATCH, rank, world))
-    agg = FedAvg(compressor=make_compressor(args.compress, args.topk_ratio, trainer))
+    transport, select = None, {}
+    if world > 1:
+        transport, select = make_transport(args, trainer, rank, world, rehearse, device)
+    agg = FedAvg(compressor=make_compressor(args.compress, args.topk_ratio, trainer), transport=transport)
     if world > 1 and not args.eval_full:
         trainer.set_test_data(eval_shard(data.test, rank, world))
     hist = EvalHistory(trainer, args.warmup + args.steps)
@@ -191,7 +293,7 @@ def main() -> int:
                    "local_epochs_per_round": 1, "eval_per_round": not args.no_eval,
                    "eval_split": "full-per-client" if args.eval_full or world == 1 else f"1/{world}-per-client",
                    "data_split": f"noniid-{args.noniid}-shards" if args.noniid else "strided-iid",
-                   "aggregation": ("gloo-rehearsal-allreduce" if rehearse and world > 1 else "rccl-allreduce") +("" if args.compress == "none" else f"+{args.compress}"),
+                   "aggregation": agg.label() + (" [1-GPU rehearsal]" if rehearse and world > 1 else ""),
                    "hip_graph": not args.no_graph},
         "rounds_per_sec": round(rounds_per_s, 4),
         "samples_per_sec_per_client": round(value / world, 3),
@@ -200,8 +302,15 @@ def main() -> int:
                        **({"test_loss": round(ev_stats.loss, 4), "test_acc": round(ev_stats.acc, 3)}
                           if ev_stats else {})},
         "allreduce_ms_last": round(agg.timer.last_ms, 4),
+        **({"transport_select": select} if select else {}),
+        **({"compression": {"kind": args.compress, "bytes_per_round_per_client":
+                            agg.compressor.bytes_sent // max(1, agg.compressor.rounds),
+                            "dense_bytes_per_round_per_client": agg.compressor.dense_bytes // max(1, agg.compressor.rounds)}}
+           if agg.compressor is not None and agg.compressor.rounds else {}),
     }
     writer.close()
+    if transport is not None:
+        transport.close()
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

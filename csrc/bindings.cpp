@@ -37,7 +37,7 @@ size_t select_state_bytes();
 int compact_chunk();
 void launch_ef_delta(hipStream_t, const float*, const float*, const float*, float*, long);
 void launch_topk(hipStream_t, const float*, long, int, void*, int*, int*, float*, float*);
-void launch_scatter_add_scaled(hipStream_t, float*, const int*, const float*, long, float, long);
+void launch_scatter_add_ranked(hipStream_t, float*, const int*, const float*, int, long, float, long);
 void launch_quant_int8(hipStream_t, const float*, long, signed char*, float*, float*);
 void launch_dequant_accum(hipStream_t, const signed char*, const float*, int, long, float*, float);
 }  // namespace fedmi
@@ -216,9 +216,11 @@ static void fedmi_bind(py::module_& m) {
                 P<float>(residual));
     check_last("topk");
   });
-  m.def("scatter_add_scaled", [](uintptr_t st, uintptr_t out, uintptr_t idx, uintptr_t val, long m_, float scale, long n) {
-    launch_scatter_add_scaled(S(st), P<float>(out), P<const int>(idx), P<const float>(val), m_, scale, n);
-    check_last("scatter_add_scaled");
+  m.def("scatter_add_ranked", [](uintptr_t st, uintptr_t out, uintptr_t idx, uintptr_t val, int R, long m_, float scale,
+                                 long n) {
+    if (R <= 0) throw std::invalid_argument("scatter_add_ranked: R must be > 0");
+    launch_scatter_add_ranked(S(st), P<float>(out), P<const int>(idx), P<const float>(val), R, m_, scale, n);
+    check_last("scatter_add_ranked");
   });
   m.def("quant_int8", [](uintptr_t st, uintptr_t d, long n, uintptr_t q, uintptr_t scales, uintptr_t residual) {
     launch_quant_int8(S(st), P<const float>(d), n, P<signed char>(q), P<float>(scales), P<float>(residual));

@@ -12,7 +12,7 @@
 //   int8:   per-256-element-chunk absmax scaling, residual <- d - deq(q(d))
 //
 // The compressed payloads are all-gathered over RCCL and folded back with
-// scatter_add_scaled / dequant_accum (one launch each).
+// scatter_add_ranked (rank-ordered, atomic-free) / dequant_accum.
 #include "common.h"
 
 namespace {
@@ -158,12 +158,16 @@ __global__ __launch_bounds__(256) void compact_write_kernel(const float* __restr
   }
 }
 
-__global__ __launch_bounds__(256) void scatter_add_scaled_kernel(float* __restrict__ out, const int* __restrict__ idx,
-                                                                 const float* __restrict__ val, long m, float scale, long n) {
+// out[idx[i]] += scale * val[i] for ONE rank's payload.  Indices are unique within a
+// rank (top-k), so no atomics: the launcher applies the ranks' payloads one launch
+// after another in rank order, and every client computes the same fp32 sums in the
+// same order -> bit-identical global models (atomics would add in arrival order).
+__global__ __launch_bounds__(256) void scatter_add_rank_kernel(float* __restrict__ out, const int* __restrict__ idx,
+                                                               const float* __restrict__ val, long m, float scale, long n) {
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
     const int j = idx[i];
-    if (j >= 0 && j < n) atomicAdd(&out[j], scale * val[i]);
+    if (j >= 0 && j < n) out[j] += scale * val[i];
   }
 }
 
@@ -234,9 +238,13 @@ void launch_topk(hipStream_t st, const float* d, long n, int k, void* state, int
   hipLaunchKernelGGL(compact_write_kernel, dim3(nb), dim3(256), 0, st, d, n, s, counts, idx, val, residual);
 }
 
-void launch_scatter_add_scaled(hipStream_t st, float* out, const int* idx, const float* val, long m, float scale, long n) {
+// idx/val: [R][m] gathered payloads, applied in rank order 0..R-1.
+void launch_scatter_add_ranked(hipStream_t st, float* out, const int* idx, const float* val, int R, long m, float scale,
+                               long n) {
   if (m <= 0) return;
-  hipLaunchKernelGGL(scatter_add_scaled_kernel, dim3(grid_for(m)), dim3(256), 0, st, out, idx, val, m, scale, n);
+  for (int r = 0; r < R; ++r)
+    hipLaunchKernelGGL(scatter_add_rank_kernel, dim3(grid_for(m)), dim3(256), 0, st, out, idx + (long)r * m,
+                       val + (long)r * m, m, scale, n);
 }
 
 void launch_quant_int8(hipStream_t st, const float* d, long n, signed char* q, float* scales, float* residual) {

@@ -96,17 +96,33 @@ class AsyncCheckpointWriter:
     ``submit`` snapshots the device tensors into pinned host memory with a
     non-blocking copy on the current stream and records an event; the writer
     thread waits for that event, then ``torch.save``s atomically.  The GPU
-    stream never blocks on file I/O.
+    stream never blocks on file I/O.  Pinned snapshot buffers are pooled per
+    (storage span, dtype) and recycled once the writer has serialised them, so a
+    per-round checkpoint allocates no pinned memory in steady state.
     """
 
     def __init__(self, max_pending: int = 4):
         self._q: "queue.Queue" = queue.Queue(maxsize=max_pending)
         self._err: Optional[BaseException] = None
-        self._pinned: Dict[str, torch.Tensor] = {}
+        self._pool: Dict[tuple, list] = {}
         self._pin_lock = threading.Lock()
         self._t = threading.Thread(target=self._run, name="fedmi-ckpt-writer", daemon=True)
         self._t.start()
         self.written = 0
+        self.pinned_allocs = 0
+
+    def _pinned(self, key: tuple, n: int, dtype) -> torch.Tensor:
+        with self._pin_lock:
+            free = self._pool.get(key)
+            if free:
+                return free.pop()
+        self.pinned_allocs += 1
+        return torch.empty(n, dtype=dtype, pin_memory=True)
+
+    def _recycle(self, bufs) -> None:
+        with self._pin_lock:
+            for key, b in bufs:
+                self._pool.setdefault(key, []).append(b)
 
     def _snapshot(self, state_dict):
         """Device->pinned-host copy of a state dict: ONE copy per device storage.
@@ -117,6 +133,7 @@ class AsyncCheckpointWriter:
         so the file layout is the reference's (one storage per tensor)."""
         out = OrderedDict()
         ev = None
+        pooled = []
         groups: Dict[tuple, list] = {}
         for k, v in state_dict.items():
             v = v.detach()
@@ -130,27 +147,36 @@ class AsyncCheckpointWriter:
                 out[k] = host
             else:
                 out[k] = v.clone()
-        for (_, dt, dev), items in groups.items():
+        for (ptr, dt, dev), items in groups.items():
             lo = min(v.storage_offset() for _, v in items)
             hi = max(v.storage_offset() + v.numel() for _, v in items)
             base = torch.empty(0, dtype=dt, device=dev).set_(items[0][1].untyped_storage())
-            host = torch.empty(hi - lo, dtype=dt, pin_memory=True)
+            pkey = (ptr, lo, hi, dt)
+            host = self._pinned(pkey, hi - lo, dt)
             host.copy_(base[lo:hi], non_blocking=True)
+            pooled.append((pkey, host))
             for k, v in items:
                 o = v.storage_offset() - lo
                 out[k] = host[o:o + v.numel()].view(v.shape)
         if any(v.is_cuda for v in state_dict.values()):
             ev = torch.cuda.Event()
             ev.record()
-        return out, ev
+        return out, ev, pooled
 
     def submit(self, path, state_dict, acc=1, epoch: int = 0, on_done=None) -> None:
-        """Queue ``{'net','acc','epoch'}`` for ``path`` (a path or a list of paths sharing one snapshot)."""
+        """Queue ``{'net','acc','epoch'}`` for ``path`` (a path, a list of paths sharing one snapshot,
+        or None: serialise only and hand the bytes to ``on_done(None, data)``)."""
         if self._err:
             raise RuntimeError("checkpoint writer failed") from self._err
-        snap, ev = self._snapshot(state_dict)
-        paths = [Path(p) for p in path] if isinstance(path, (list, tuple)) else [Path(path)]
-        self._q.put((paths, snap, ev, acc, epoch, on_done))
+        snap, ev, pooled = self._snapshot(state_dict)
+        paths = [] if path is None else [Path(p) for p in path] if isinstance(path, (list, tuple)) else [Path(path)]
+        self._q.put(("ckpt", paths, snap, ev, acc, epoch, on_done, pooled))
+
+    def submit_bytes(self, path, data: bytes) -> None:
+        """Queue an already-serialised checkpoint (e.g. a received model) for an atomic write."""
+        if self._err:
+            raise RuntimeError("checkpoint writer failed") from self._err
+        self._q.put(("bytes", [Path(path)], data, None, None, None, None, []))
 
     def _run(self):
         while True:
@@ -158,19 +184,25 @@ class AsyncCheckpointWriter:
             if item is None:
                 self._q.task_done()
                 return
-            paths, snap, ev, acc, epoch, on_done = item
+            kind, paths, snap, ev, acc, epoch, on_done, pooled = item
             try:
+                if kind == "bytes":
+                    for path in paths:
+                        atomic_write(path, snap)
+                        self.written += 1
+                    continue
                 if ev is not None:
                     ev.synchronize()
                 # one storage per tensor, like a plain module.state_dict()
                 net = OrderedDict((k, v.clone() if v.untyped_storage().nbytes() != v.nbytes else v)
                                   for k, v in snap.items())
                 data = to_bytes({"net": net, "acc": acc, "epoch": int(epoch)})
+                self._recycle(pooled)
                 for path in paths:
                     atomic_write(path, data)
                     self.written += 1
-                    if on_done is not None:
-                        on_done(path, data)
+                if on_done is not None:
+                    on_done(paths[0] if paths else None, data)
             except BaseException as e:  # pragma: no cover
                 self._err = e
             finally:

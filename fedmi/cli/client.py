@@ -34,7 +34,12 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--model", default="lenet")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--agg", default="collective", choices=["collective", "grpc"])
-    ap.add_argument("--backend", default="auto", help="data-plane backend: nccl (RCCL) | gloo | auto")
+    ap.add_argument("--backend", default="auto", help="dist data-plane backend: nccl (RCCL) | gloo | auto")
+    ap.add_argument("--transport", default="auto", choices=["auto", "peer", "dist"],
+                    help="FedAvg data plane: peer = hipIpc peer kernels among the node's GPU clients (also "
+                         "several clients on one GPU); dist = torch.distributed (--backend); auto = peer on GPU")
+    ap.add_argument("--collective-timeout", type=float, default=20.0,
+                    help="seconds before a collective with a lost peer fails (peer barrier / RCCL abort)")
     ap.add_argument("--data", default="synthetic-cifar10",
                     help="synthetic-cifar10 | synthetic-mnist | cifar10-bin:<dir>")
     ap.add_argument("--n-train", type=int, default=None)
@@ -69,7 +74,8 @@ def main(argv=None) -> int:
     dev = pick_device(a.device)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
-        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")   # surface peer loss as an error
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "3")   # surface peer loss as an error, no teardown
+        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")          # collectives honour the PG timeout
     log(f"client {a.address}", f"Client is running on {a.address} ({dev}); Compression {a.compressFlag} enabled")
     data = make_dataset(a.data, device=dev, n_train=a.n_train, n_test=a.n_test, seed=a.data_seed)
     cfg = TrainerConfig(lr=a.lr, batch_size=a.batch_size, seed=a.seed, use_graph=not a.no_graph)
@@ -78,9 +84,14 @@ def main(argv=None) -> int:
         shards = label_shard_indices(data.train.y.cpu().numpy(), a.num_clients, a.noniid, seed=a.data_seed)
         trainer.set_train_data(data.train.subset(shards[a.client_index]))
     backend = a.backend if a.backend != "auto" else ("nccl" if dev.type == "cuda" else "gloo")
+    transport = a.transport if a.transport != "auto" else ("peer" if dev.type == "cuda" else "dist")
     comp_kind = a.compress if a.compress is not None else ("topk" if gzip else "none")
     fedavg = FedAvg(compressor=make_compressor(comp_kind, a.topk_ratio, trainer))
-    agent = ClientAgent(trainer, a.address, root=a.root, agg=a.agg, group=GroupManager(backend, dev),
+    n = trainer.float_state().numel()
+    cap = max(4 * n, 16 * (int(n * a.topk_ratio) + 64), n + 4 * (n // 256 + 64))
+    group = GroupManager(backend, dev, timeout_s=a.collective_timeout, transport=transport, peer_capacity=cap,
+                         peer_timeout_ms=1000.0 * a.collective_timeout)
+    agent = ClientAgent(trainer, a.address, root=a.root, agg=a.agg, group=group,
                         fedavg=fedavg, batch_size=a.batch_size, local_shard=a.noniid > 0, resume=a.resume,
                         metrics=MetricsLog(a.metrics), verbose=not a.quiet)
     server, port = serve_client(agent, a.address, gzip=gzip)
@@ -90,6 +101,7 @@ def main(argv=None) -> int:
     while not stop.is_set():
         stop.wait(0.5)
     server.stop(grace=1.0)
+    agent.close()
     if agent.group is not None:
         agent.group.shutdown()
     return 0

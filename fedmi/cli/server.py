@@ -38,6 +38,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--store-port", type=int, default=0)
     ap.add_argument("--min-clients", type=int, default=1)
     ap.add_argument("--metrics", default=None, help="JSONL metrics file")
+    ap.add_argument("--ckpt-sync-every", type=int, default=0,
+                    help="rank 0 uploads THAT round's checkpoint every k rounds (0: pipelined by one round, "
+                         "synchronous on the final round)")
     return ap
 
 
@@ -48,7 +51,7 @@ def main(argv=None) -> int:
     cfg = CoordinatorConfig(clients=[c for c in a.clients.split(",") if c], rounds=a.rounds, agg=a.agg, gzip=gzip,
                             root=a.root, primary=(a.p == "y"), train_timeout_s=a.train_timeout,
                             rpc_timeout_s=a.rpc_timeout, heartbeat_s=a.heartbeat, store_host=a.store_host,
-                            store_port=a.store_port, min_clients=a.min_clients,
+                            store_port=a.store_port, min_clients=a.min_clients, ckpt_sync_every=a.ckpt_sync_every,
                             backup_address=f"{a.backupAddress}:{a.backupPort}")
     metrics = MetricsLog(a.metrics)
     stop = threading.Event()

@@ -10,6 +10,11 @@ Reference: src/client.py:15-35 (+ the import-time trainer in src/main.py).
         data-plane generation + rendezvous store from gRPC metadata); every
         client evaluates the global model; only rank 0 uploads the (already
         averaged) checkpoint so the coordinator can persist/replicate it.
+        Checkpoints are written by a background writer; rank 0's upload is
+        pipelined (the reply carries the newest checkpoint serialised so far,
+        usually the previous round's) unless the coordinator asks for this
+        round's (``x-fedmi-sync-ckpt: 1``, e.g. on the final round).
+        A new membership generation starts with a resync from rank 0.
   SendModel(b64 checkpoint) -> install it (resync / grpc-mode broadcast), persist,
       evaluate.
   HeartBeat() -> status 1.
@@ -40,6 +45,7 @@ META_TERM = "x-fedmi-term"
 META_ROUND = "x-fedmi-round"
 META_GEN = "x-fedmi-gen"
 META_STORE = "x-fedmi-store"
+META_SYNC = "x-fedmi-sync-ckpt"        # "1": the reply must carry THIS round's checkpoint
 
 
 def metadata_dict(context) -> dict:
@@ -53,7 +59,7 @@ class ClientAgent(P.TrainerServicer):
     def __init__(self, trainer: LocalTrainer, address: str, *, root: str | Path = ".", agg: str = "collective",
                  group: Optional[GroupManager] = None, fedavg: Optional[FedAvg] = None, batch_size: int = 128,
                  local_shard: bool = False, resume: bool = False, metrics: Optional[MetricsLog] = None,
-                 verbose: bool = True):
+                 verbose: bool = True, writer: Optional[ck.AsyncCheckpointWriter] = None):
         if agg not in ("collective", "grpc"):
             raise ValueError(f"agg must be 'collective' or 'grpc', not {agg!r}")
         self.trainer = trainer
@@ -65,9 +71,14 @@ class ClientAgent(P.TrainerServicer):
         self.local_shard = local_shard          # non-IID: the client owns its data, rank does not pick batches
         self.metrics = metrics or MetricsLog()
         self.verbose = verbose
+        self.writer = writer or ck.AsyncCheckpointWriter()
         self.lock = threading.RLock()
         self.max_term = 0
         self.round = 0
+        self._busy_gen: Optional[int] = None    # generation of the round holding the lock
+        self._ready_lock = threading.Lock()
+        self._ready: Optional[tuple] = None     # (epoch, bytes) newest serialised global checkpoint
+        self._sent_epoch = -1
         self.ckpt_path = ck.client_ckpt_path(root, address.replace("/", "_"))
         if resume and self.ckpt_path.exists():
             c = ck.load(self.ckpt_path)
@@ -96,58 +107,111 @@ class ClientAgent(P.TrainerServicer):
             return contiguous_schedule(n, self.batch)
         return strided_schedule(n, self.batch, rank, world)
 
-    def _persist(self, acc, epoch: int) -> bytes:
-        data = ck.to_bytes(ck.make_checkpoint(self.trainer.state_dict(), acc=acc, epoch=epoch))
-        ck.atomic_write(self.ckpt_path, data)
-        return data
+    def _persist_async(self, acc, epoch: int, keep: bool) -> None:
+        """Checkpoint off the RPC thread (pinned snapshot + writer thread); with ``keep`` the
+        serialised bytes are also kept for the coordinator's upload."""
+        def _keep(_path, data, _epoch=epoch):
+            with self._ready_lock:
+                if self._ready is None or _epoch >= self._ready[0]:
+                    self._ready = (_epoch, data)
+
+        self.writer.submit(self.ckpt_path, self.trainer.state_dict(), acc=acc, epoch=epoch,
+                           on_done=_keep if keep else None)
+
+    def _take_ready(self) -> tuple:
+        """(epoch, b64) of the newest serialised checkpoint not uploaded yet, or (-1, '')."""
+        with self._ready_lock:
+            if self._ready is None or self._ready[0] <= self._sent_epoch:
+                return -1, ""
+            self._sent_epoch = self._ready[0]
+            return self._ready[0], ck.to_b64(self._ready[1])
 
     # ---- RPCs ---------------------------------------------------------------------
     def StartTrain(self, request, context):
         meta = metadata_dict(context)
+        gen = int(meta.get(META_GEN, "0") or 0)
+        busy = self._busy_gen
+        if self.group is not None and busy is not None and gen > busy:
+            # a newer membership while an older round is still blocked in its collective
+            self._log(f"generation {gen} supersedes running generation {busy}: interrupting it")
+            self.group.interrupt()
         with self.lock:
-            self._fence(meta, context)
-            rank, world = int(request.rank), int(request.world)
-            if world <= 0 or not 0 <= rank < world:
-                context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"bad rank/world {rank}/{world}")
-            rnd = int(meta.get(META_ROUND, self.round + 1) or self.round + 1)
-            t = Timer()
-            self.trainer.set_schedule(*self._schedule(rank, world))
-            self.trainer.train_epoch()
-            tr = self.trainer.train_stats()
-            t_train = t.ms()
-            rec = {"role": "client", "address": self.address, "round": rnd, "rank": rank, "world": world,
-                   "agg": self.agg, **tr.as_dict("train"), "train_ms": t_train}
-            if self.agg == "collective":
-                gen = int(meta.get(META_GEN, "0") or 0)
-                host, _, port = (meta.get(META_STORE) or "127.0.0.1:0").rpartition(":")
-                if self.group is not None:
-                    self.group.ensure(Membership(gen, rank, world, host, int(port)))
-                elif world > 1:
-                    context.abort(grpc.StatusCode.FAILED_PRECONDITION, "collective aggregation needs a GroupManager")
-                t2 = Timer()
-                self.fedavg.average(self.trainer)
-                rec["allreduce_ms"] = t2.ms()
-                self.trainer.evaluate()
-                ev = self.trainer.eval_stats()
-                rec.update(ev.as_dict("test"))
-                self.round = rnd
-                data = self._persist(ev.acc, rnd)
-                message = ck.to_b64(data) if rank == 0 else ""
-            else:
-                self.round = rnd
-                data = self._persist(tr.acc, rnd)
-                message = ck.to_b64(data)
-            rec["round_ms"] = t.ms()
-            self.metrics.write(**rec)
-            self._log(f"round {rnd} rank {rank}/{world}: train loss {tr.loss:.4f} acc {tr.acc:.2f}%"
-                      + (f" | test acc {rec['test_acc']:.2f}%" if "test_acc" in rec else ""))
+            self._busy_gen = gen
             try:
-                context.set_trailing_metadata((("x-fedmi-client-round", str(self.round)),
-                                               ("x-fedmi-train-loss", f"{tr.loss:.6f}"),
-                                               ("x-fedmi-test-acc", f"{rec.get('test_acc', -1):.4f}")))
-            except Exception:
-                pass
-            return P.TrainReply(message=message)
+                return self._start_train(request, context, meta, gen)
+            finally:
+                self._busy_gen = None
+
+    def _start_train(self, request, context, meta: dict, gen: int):
+        self._fence(meta, context)
+        rank, world = int(request.rank), int(request.world)
+        if world <= 0 or not 0 <= rank < world:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"bad rank/world {rank}/{world}")
+        rnd = int(meta.get(META_ROUND, self.round + 1) or self.round + 1)
+        t = Timer()
+        rec = {"role": "client", "address": self.address, "round": rnd, "rank": rank, "world": world,
+               "agg": self.agg, "generation": gen}
+        if self.agg == "collective":
+            host, _, port = (meta.get(META_STORE) or "127.0.0.1:0").rpartition(":")
+            changed = False
+            if self.group is not None:
+                changed = self.group.ensure(Membership(gen, rank, world, host, int(port)))
+                self.fedavg.transport = self.group.transport
+            elif world > 1:
+                context.abort(grpc.StatusCode.FAILED_PRECONDITION, "collective aggregation needs a GroupManager")
+            if changed and world > 1:
+                # new member set: everyone starts this generation from rank 0's model (one anchor
+                # for the -c Y compressors; undoes any partially applied aborted round)
+                self.fedavg.resync(self.trainer, 0)
+                rec["resync"] = True
+            elif changed and self.fedavg.compressor is not None:
+                self.fedavg.compressor.reset(self.trainer)
+            rec["group_ms"] = t.ms()
+        t1 = Timer()
+        self.trainer.set_schedule(*self._schedule(rank, world))
+        self.trainer.train_epoch()
+        tr = self.trainer.train_stats()
+        rec.update(tr.as_dict("train"))
+        rec["train_ms"] = t1.ms()
+        if self.agg == "collective":
+            t2 = Timer()
+            self.fedavg.average(self.trainer)
+            tp = self.fedavg.transport
+            if tp is not None and tp.error():
+                context.abort(grpc.StatusCode.ABORTED, "peer collective timed out (a client was lost)")
+            rec["allreduce_ms"] = t2.ms()
+            t3 = Timer()
+            self.trainer.evaluate()
+            ev = self.trainer.eval_stats()
+            rec["eval_ms"] = t3.ms()
+            rec.update(ev.as_dict("test"))
+            self.round = rnd
+            t4 = Timer()
+            self._persist_async(ev.acc, rnd, keep=(rank == 0))
+            if rank == 0 and meta.get(META_SYNC) == "1":
+                self.writer.flush()
+            ck_epoch, message = self._take_ready() if rank == 0 else (-1, "")
+            rec["ckpt_ms"] = t4.ms()
+        else:
+            # reference parameter-server path: the reply IS this round's local model
+            self.round = rnd
+            t4 = Timer()
+            data = ck.to_bytes(ck.make_checkpoint(self.trainer.state_dict(), acc=tr.acc, epoch=rnd))
+            self.writer.submit_bytes(self.ckpt_path, data)
+            ck_epoch, message = rnd, ck.to_b64(data)
+            rec["ckpt_ms"] = t4.ms()
+        rec["round_ms"] = t.ms()
+        self.metrics.write(**rec)
+        self._log(f"round {rnd} rank {rank}/{world}: train loss {tr.loss:.4f} acc {tr.acc:.2f}%"
+                  + (f" | test acc {rec['test_acc']:.2f}%" if "test_acc" in rec else ""))
+        try:
+            context.set_trailing_metadata((("x-fedmi-client-round", str(self.round)),
+                                           ("x-fedmi-ckpt-epoch", str(ck_epoch)),
+                                           ("x-fedmi-train-loss", f"{tr.loss:.6f}"),
+                                           ("x-fedmi-test-acc", f"{rec.get('test_acc', -1):.4f}")))
+        except Exception:
+            pass
+        return P.TrainReply(message=message)
 
     def SendModel(self, request, context):
         meta = metadata_dict(context)
@@ -159,7 +223,7 @@ class ClientAgent(P.TrainerServicer):
             comp = getattr(self.fedavg, "compressor", None)
             if comp is not None:
                 comp.reset(self.trainer)
-            ck.atomic_write(self.ckpt_path, data)
+            self.writer.submit_bytes(self.ckpt_path, data)
             self.round = max(self.round, int(c.get("epoch", 0) or 0))
             self.trainer.evaluate()
             ev = self.trainer.eval_stats()
@@ -170,6 +234,9 @@ class ClientAgent(P.TrainerServicer):
 
     def HeartBeat(self, request, context):
         return P.HeartBeatResponse(status=1)
+
+    def close(self) -> None:
+        self.writer.close()
 
 
 def serve_client(agent: ClientAgent, address: str, gzip: bool = False, max_workers: int = 10):

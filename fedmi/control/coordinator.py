@@ -10,7 +10,11 @@ Per round (synchronous, one local epoch per client, like the reference):
   * ``agg="grpc"``: reference parameter-server path — replies are written to
     ``<mount>/test_<rank>.pth``, averaged (only the replies of THIS round), the
     result saved and SendModel'ed back.
-  ``<mount>/optimizedModel.pth`` is replicated to the backup asynchronously.
+  ``<mount>/optimizedModel.pth`` is written and replicated to the backup by a
+  background thread (in order), off the round's critical path.  In collective
+  mode rank 0's upload is pipelined by one round except on the final round.
+  A collective round that lost a client is aborted: the survivors are rolled
+  back to the last committed global model (SendModel) before regrouping.
 
 Fixes vs the reference: deadlines on every RPC (A3),
 world = live clients only and no stale-file averaging (A5/A6), the round is
@@ -36,7 +40,7 @@ from .. import ckpt as ck
 from ..parallel.group import StoreHost
 from ..utils.metrics import MetricsLog, Timer, log
 from ..wire import proto as P
-from .client_agent import META_GEN, META_ROUND, META_STORE, META_TERM
+from .client_agent import META_GEN, META_ROUND, META_STORE, META_SYNC, META_TERM
 
 
 @dataclass
@@ -55,6 +59,7 @@ class CoordinatorConfig:
     backup_address: Optional[str] = None
     min_clients: int = 1
     round_pause_s: float = 0.0
+    ckpt_sync_every: int = 0             # >0: rank 0 uploads THAT round's checkpoint every k rounds (always the last)
 
 
 def fedavg_state_dicts(sds: List[dict], weights: Optional[List[float]] = None) -> "OrderedDict[str, torch.Tensor]":
@@ -122,6 +127,8 @@ class Coordinator:
             self._backup = P.TrainerStub(P.make_channel(cfg.backup_address))
         self._tracker: Optional[threading.Thread] = None
         self.round_times: List[float] = []
+        self.installed_epoch = ck.read_epoch(self.model_path) or -1
+        self._pending: list = []
 
     # ---- logging / membership -------------------------------------------------
     def _log(self, msg: str) -> None:
@@ -144,23 +151,38 @@ class Coordinator:
 
     def _meta(self, round_no: int):
         md = [(META_TERM, str(self.term)), (META_ROUND, str(round_no)), (META_GEN, str(self.generation))]
+        k = self.cfg.ckpt_sync_every
+        if round_no >= self.cfg.rounds or (k > 0 and round_no % k == 0):
+            md.append((META_SYNC, "1"))
         if self.store is not None:
             md.append((META_STORE, f"{self.store.host}:{self.store.port}"))
         return md
 
     # ---- model persistence / replication --------------------------------------
-    def _install_global(self, data: bytes) -> None:
-        ck.atomic_write(self.model_path, data)
+    def _install_global(self, data: bytes, epoch: Optional[int] = None) -> None:
+        if epoch is not None and epoch <= self.installed_epoch:
+            return
         self.latest_model = data
-        if self._backup is not None:
-            self._replicator.submit(self._replicate, data)
+        if epoch is not None:
+            self.installed_epoch = epoch
+        self._pending.append(self._replicator.submit(self._persist_and_replicate, data))
+        self._pending = [f for f in self._pending if not f.done()]
 
-    def _replicate(self, data: bytes) -> None:
+    def _persist_and_replicate(self, data: bytes) -> None:
+        ck.atomic_write(self.model_path, data)
+        if self._backup is None:
+            return
         try:
             self._backup.SendModel(P.SendModelRequest(model=ck.to_b64(data)), timeout=self.cfg.rpc_timeout_s,
                                    metadata=[(META_TERM, str(self.term))])
         except grpc.RpcError as e:
             self._log(f"backup replication failed: {e.code().name}")
+
+    def flush(self) -> None:
+        """Wait until every installed model is on disk (and offered to the backup)."""
+        for f in list(self._pending):
+            f.result()
+        self._pending = []
 
     def _send_model(self, address: str, data_b64: str) -> bool:
         m = self.members[address]
@@ -192,13 +214,15 @@ class Coordinator:
             stub = self.members[addr].stub
             futs[addr] = (rank, stub.StartTrain.future(P.TrainRequest(rank=rank, world=world),
                                                        timeout=self.cfg.train_timeout_s, metadata=md))
-        replies, failed, client_rounds = {}, [], []
+        replies, failed, client_rounds, ckpt_epochs = {}, [], [], {}
         for addr, (rank, f) in futs.items():
             try:
                 replies[rank] = f.result().message
                 tm = dict(f.trailing_metadata() or ())
                 if "x-fedmi-client-round" in tm:
                     client_rounds.append(int(tm["x-fedmi-client-round"]))
+                if "x-fedmi-ckpt-epoch" in tm:
+                    ckpt_epochs[rank] = int(tm["x-fedmi-ckpt-epoch"])
             except grpc.RpcError as e:
                 self._log(f"StartTrain on {addr} failed: {e.code().name} {e.details() or ''}".strip())
                 failed.append(addr)
@@ -207,12 +231,18 @@ class Coordinator:
         ok = False
         if self.cfg.agg == "collective":
             if failed:
-                # the survivors' all-reduce for this round is not trustworthy: redo with a new group
-                self._log(f"round {rnd} aborted ({len(failed)} client(s) lost); regrouping")
+                # the survivors' all-reduce for this round is not trustworthy: roll them back to the
+                # last committed global model, then regroup (new generation) next round
+                self._log(f"round {rnd} aborted ({len(failed)} client(s) lost); rolling back survivors, regrouping")
+                if self.latest_model is not None:
+                    b64 = ck.to_b64(self.latest_model)
+                    sends = [self._pool.submit(self._send_model, a, b64) for a in live if a not in failed]
+                    for s_ in sends:
+                        s_.result()
             else:
-                msg = replies.get(0) or next((v for v in replies.values() if v), "")
+                msg = replies.get(0, "")
                 if msg:
-                    self._install_global(ck.from_b64(msg))
+                    self._install_global(ck.from_b64(msg), ckpt_epochs.get(0, rnd))
                 ok = True
         else:
             good = {r: ck.from_b64(m) for r, m in replies.items() if m}
@@ -222,11 +252,11 @@ class Coordinator:
                 sds = [ck.from_bytes(d)["net"] for d in good.values()]
                 avg = fedavg_state_dicts(sds)
                 data = ck.to_bytes(ck.make_checkpoint(avg, acc=1, epoch=rnd))
-                self._install_global(data)
+                self._install_global(data, rnd)
                 b64 = ck.to_b64(data)
                 sends = [self._pool.submit(self._send_model, a, b64) for a in live if a not in failed]
-                for s in sends:
-                    s.result()
+                for s_ in sends:
+                    s_.result()
                 ok = True
         if ok:
             self.round = max([rnd] + client_rounds)
@@ -274,6 +304,7 @@ class Coordinator:
 
     def close(self) -> None:
         self.stop()
+        self.flush()
         self._replicator.shutdown(wait=True)
         self._pool.shutdown(wait=False, cancel_futures=True)
         for m in self.members.values():

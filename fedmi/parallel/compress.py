@@ -8,13 +8,20 @@ channel) and compresses the *update* instead:
 * ``topk``  — each client sends the k largest-magnitude entries of
   d = (w_local - w_global) + e (error feedback e carries the rest to the next
   round); selection is an exact radix select on the GPU
-  (csrc/kernels/compress.hip); (idx, val) pairs are all-gathered over RCCL and
-  scatter-added into the global model.  Payload per client: 8k bytes.
+  (csrc/kernels/compress.hip); (idx, val) pairs are all-gathered (RCCL, or the
+  hipIpc peer kernels of :mod:`fedmi.parallel.peer`) and applied to the global
+  model in rank order without atomics, so every client holds a bit-identical
+  global model.  Payload per client: 8k bytes.
 * ``int8``  — per-256-element absmax int8 quantisation with error feedback;
   payload n + 4n/256 bytes (~3.9x smaller than fp32).
 
 After aggregation every client holds w_global' = w_global + mean(sparse d),
 exactly like dense FedAvg when k = n.
+
+Every client must hold the same anchor ``global_ref``.  It is re-anchored
+(:meth:`reset`) whenever the model is replaced from outside — a rank-0 init
+broadcast, a SendModel resync, a new membership generation — and a client
+that trains alone (world 1) simply adopts its local model.
 """
 from __future__ import annotations
 
@@ -30,10 +37,12 @@ def _world(group) -> int:
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
-def _all_gather_flat(t: torch.Tensor, group) -> torch.Tensor:
+def _all_gather_flat(t: torch.Tensor, group, transport=None) -> torch.Tensor:
+    if transport is not None:
+        return transport.all_gather(t)
     w = _world(group)
     if w == 1:
-        return t.clone()
+        return t.clone().unsqueeze(0)
     out = torch.empty((w,) + tuple(t.shape), dtype=t.dtype, device=t.device)
     if t.is_cuda:
         dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=group)
@@ -51,7 +60,9 @@ class _EFCompressor:
         self.residual = torch.zeros_like(self.global_ref)
         self.d = torch.empty_like(self.global_ref)
         self._nat = native.require() if x.is_cuda else None
-        self.bytes_sent = 0
+        self.bytes_sent = 0          # this client's compressed payload bytes, summed over rounds
+        self.dense_bytes = 0         # what dense fp32 FedAvg would have sent
+        self.rounds = 0
 
     def reset(self, trainer) -> None:
         """Re-anchor on the trainer's current model (after a resync/load)."""
@@ -91,18 +102,21 @@ class TopKCompressor(_EFCompressor):
             self.residual.copy_(self.d)
             self.residual[sel] = 0.0
 
-    def aggregate(self, trainer, group=None) -> None:
+    def aggregate(self, trainer, group=None, transport=None) -> None:
         x = trainer.float_state()
         self.compress(x)
-        w = _world(group)
-        idx_all = _all_gather_flat(self.idx, group).view(-1)
-        val_all = _all_gather_flat(self.val, group).view(-1)
+        w = transport.world if transport is not None else _world(group)
+        idx_all = _all_gather_flat(self.idx, group, transport)
+        val_all = _all_gather_flat(self.val, group, transport)
         self.bytes_sent += 8 * self.k
+        self.dense_bytes += 4 * self.n
+        self.rounds += 1
         if self._nat is not None:
-            self._nat.scatter_add_scaled(native.stream_handle(self.dev), self.global_ref.data_ptr(),
-                                         idx_all.data_ptr(), val_all.data_ptr(), idx_all.numel(), 1.0 / w, self.n)
+            self._nat.scatter_add_ranked(native.stream_handle(self.dev), self.global_ref.data_ptr(),
+                                         idx_all.data_ptr(), val_all.data_ptr(), w, self.k, 1.0 / w, self.n)
         else:
-            self.global_ref.index_add_(0, idx_all.long(), val_all / w)
+            for r in range(w):                 # rank order, like the GPU path
+                self.global_ref.index_add_(0, idx_all[r].long(), val_all[r] * (1.0 / w))
         x.copy_(self.global_ref)
 
 
@@ -131,13 +145,15 @@ class Int8Compressor(_EFCompressor):
             self.scales.copy_(s)
             self.residual.copy_(self.d - (q * s[:, None]).view(-1)[:self.n])
 
-    def aggregate(self, trainer, group=None) -> None:
+    def aggregate(self, trainer, group=None, transport=None) -> None:
         x = trainer.float_state()
         self.compress(x)
-        w = _world(group)
-        q_all = _all_gather_flat(self.q, group)
-        s_all = _all_gather_flat(self.scales, group)
+        w = transport.world if transport is not None else _world(group)
+        q_all = _all_gather_flat(self.q, group, transport)
+        s_all = _all_gather_flat(self.scales, group, transport)
         self.bytes_sent += self.n + 4 * self.nchunks
+        self.dense_bytes += 4 * self.n
+        self.rounds += 1
         if self._nat is not None:
             self._nat.dequant_accum(native.stream_handle(self.dev), q_all.data_ptr(), s_all.data_ptr(), w, self.n,
                                     self.global_ref.data_ptr(), 1.0 / w)

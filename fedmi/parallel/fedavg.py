@@ -78,29 +78,71 @@ class AggregationTimer:
 
 @dataclass
 class FedAvg:
-    """Dense or compressed FedAvg of a LocalTrainer's state across the group."""
+    """Dense or compressed FedAvg of a LocalTrainer's state across the group.
+
+    ``transport``: a :class:`fedmi.parallel.peer.PeerAllReduce` — the hand-written
+    hipIpc peer kernels carry the aggregation instead of ``torch.distributed``
+    collectives (RCCL on GPUs, gloo on CPU).
+    """
 
     group: Optional[object] = None
     compressor: Optional[object] = None      # fedmi.parallel.compress.Compressor
+    transport: Optional[object] = None       # fedmi.parallel.peer.PeerAllReduce
     timer: AggregationTimer = field(default_factory=AggregationTimer)
 
     def world(self) -> int:
+        if self.transport is not None:
+            return self.transport.world
         return _world(self.group)
+
+    def label(self) -> str:
+        """What actually carries the aggregation (reported by the benches)."""
+        if self.world() == 1:
+            base = "none (single client)"
+        elif self.transport is not None:
+            base = f"peer-{self.transport.algo}-hipipc"
+        else:
+            be = dist.get_backend(self.group)
+            base = "rccl-allreduce" if be == "nccl" else f"{be}-allreduce"
+        if self.compressor is not None and self.world() > 1:
+            base += "+" + type(self.compressor).__name__.replace("Compressor", "").lower()
+        return base
 
     def average(self, trainer: LocalTrainer) -> None:
         t0 = time.perf_counter()
         if self.world() > 1:
             if self.compressor is not None:
-                self.compressor.aggregate(trainer, self.group)
+                self.compressor.aggregate(trainer, self.group, transport=self.transport)
+            elif self.transport is not None:
+                self.transport.allreduce_mean_(trainer.float_state())
             else:
                 allreduce_mean_(trainer.float_state(), self.group)
             for b in trainer.int_state():
-                allreduce_int_mean_(b, self.group)
+                if self.transport is not None:
+                    self.transport.allreduce_mean_(b)
+                else:
+                    allreduce_int_mean_(b, self.group)
+        elif self.compressor is not None:
+            # a client training alone holds the global model: it becomes the new anchor
+            self.compressor.reset(trainer)
         trainer.after_aggregate()
         dt = (time.perf_counter() - t0) * 1e3
         self.timer.last_ms = dt
         self.timer.total_ms += dt
         self.timer.calls += 1
+
+    def resync(self, trainer: LocalTrainer, src: int = 0) -> None:
+        """Everyone adopts rank ``src``'s model (init, or after an aborted round) and re-anchors."""
+        if self.transport is not None:
+            if self.transport.world > 1:
+                self.transport.broadcast_(trainer.float_state(), src)
+                for b in trainer.int_state():
+                    self.transport.broadcast_(b, src)
+            trainer.after_aggregate()
+        else:
+            broadcast_state_(trainer, src, self.group)
+        if self.compressor is not None:
+            self.compressor.reset(trainer)
 
 
 def eval_shard(test, rank: int, world: int):

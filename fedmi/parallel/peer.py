@@ -94,6 +94,11 @@ class PeerAllReduce:
         rows = out.view(self.world, nbytes + pad)[:, :nbytes].contiguous()
         return rows.view(t.dtype).view((self.world,) + tuple(t.shape))
 
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        """In place: every rank gets rank ``src``'s ``t`` (an all-gather, row ``src`` kept)."""
+        t.copy_(self.all_gather(t)[src])
+        return t
+
     def error(self) -> int:
         """Nonzero if a barrier timed out (a peer died or never arrived); synchronous."""
         return int(self.comm.error())

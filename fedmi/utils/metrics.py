@@ -12,30 +12,43 @@ import json
 import sys
 import threading
 import time
+from collections import deque
 from pathlib import Path
 from typing import Optional
 
 
 class MetricsLog:
-    def __init__(self, path: Optional[str | Path] = None, echo: bool = False):
+    """JSONL sink.  ``records`` keeps only the newest ``keep`` records in memory (a
+    coordinator may run for millions of rounds); the file has all of them."""
+
+    def __init__(self, path: Optional[str | Path] = None, echo: bool = False, keep: int = 1024):
         self.path = Path(path) if path else None
         self.echo = echo
         self._lock = threading.Lock()
-        self.records = []
+        self.records: deque = deque(maxlen=keep)
+        self.count = 0
+        self._f = None
         if self.path:
             self.path.parent.mkdir(parents=True, exist_ok=True)
+            self._f = open(self.path, "a", buffering=1)      # line-buffered: readable while running
 
     def write(self, **rec) -> dict:
         rec.setdefault("ts", time.time())
         line = json.dumps(rec, default=float)
         with self._lock:
             self.records.append(rec)
-            if self.path:
-                with open(self.path, "a") as f:
-                    f.write(line + "\n")
+            self.count += 1
+            if self._f is not None:
+                self._f.write(line + "\n")
             if self.echo:
                 print(line, flush=True)
         return rec
+
+    def close(self) -> None:
+        with self._lock:
+            if self._f is not None:
+                self._f.close()
+                self._f = None
 
 
 def log(role: str, msg: str, stream=None) -> None:

@@ -4,7 +4,7 @@ themselves; the primary dies mid-run, the backup promotes itself, rebuilds the
 client process group under its own rendezvous store and continues from the
 replicated round; the clients' checkpoints keep advancing.  The CPU variant
 runs MLP clients on gloo; the GPU variant runs native-LeNet clients on the
-MI355X (sharing its one GPU, so their collective is gloo here too)."""
+MI355X (sharing its one GPU; their FedAvg runs through the hipIpc peer kernels)."""
 import threading
 import time
 
@@ -28,7 +28,8 @@ def _wait(pred, timeout=60.0, step=0.05):
 
 def _run(tmp_path, device: str, model_args):
     addrs = [f"127.0.0.1:{free_port()}" for _ in range(2)]
-    procs = [spawn_client(a, tmp_path, "--agg", "collective", "--backend", "gloo", *model_args,
+    transport = ("--transport", "peer") if device.startswith("cuda") else ("--backend", "gloo")
+    procs = [spawn_client(a, tmp_path, "--agg", "collective", *transport, *model_args,
                           log_path=tmp_path / f"client{i}.log", device=device) for i, a in enumerate(addrs)]
     try:
         for a in addrs:

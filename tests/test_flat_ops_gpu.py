@@ -70,16 +70,21 @@ def test_topk_exact(nat, gpu_device, n, k):
     assert res[~mask].abs().sum().item() == 0
 
 
-def test_scatter_add_scaled(nat, gpu_device):
-    n = 1000
-    out = torch.zeros(n, device=gpu_device)
-    idx = torch.tensor([1, 5, 5, 999], dtype=torch.int32, device=gpu_device)
-    val = torch.tensor([1.0, 2.0, 3.0, 4.0], device=gpu_device)
-    nat.scatter_add_scaled(S(), out.data_ptr(), idx.data_ptr(), val.data_ptr(), 4, 0.5, n)
+def test_scatter_add_ranked_is_rank_ordered(nat, gpu_device):
+    """Two ranks' top-k payloads (unique indices within a rank, overlapping across ranks) are
+    applied in rank order without atomics: the result equals the sequential fp32 sum."""
+    n, m = 1000, 4
+    base = torch.randn(n, device=gpu_device)
+    out = base.clone()
+    idx = torch.tensor([[1, 5, 7, 999], [5, 2, 999, 0]], dtype=torch.int32, device=gpu_device)
+    val = torch.randn(2, m, device=gpu_device)
+    nat.scatter_add_ranked(S(), out.data_ptr(), idx.data_ptr(), val.data_ptr(), 2, m, 0.5, n)
     torch.cuda.synchronize()
-    exp = torch.zeros(n, device=gpu_device)
-    exp[1], exp[5], exp[999] = 0.5, 2.5, 2.0
-    assert torch.equal(out, exp)
+    exp = base.clone().cpu()
+    for r in range(2):
+        for i in range(m):
+            exp[int(idx[r, i])] += 0.5 * float(val[r, i])
+    assert torch.equal(out.cpu(), exp)
 
 
 def test_int8_roundtrip(nat, gpu_device):

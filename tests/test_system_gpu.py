@@ -1,8 +1,10 @@
 """End-to-end system on the MI355X: the reference's process layout (coordinator +
 client processes speaking federated.proto over gRPC) with the native LeNet HIP
-engine on the GPU.  Both clients share the box's one GPU, so their collective
-FedAvg runs over gloo here; on a multi-GPU node each client owns a GPU and the
-same code path uses RCCL (``--backend nccl``)."""
+engine on the GPU.  Both clients share the box's one GPU; their FedAvg runs on
+the GPU through the hipIpc peer kernels (csrc/comm/peer_comm.hip) -- RCCL
+refuses two ranks on one GPU -- the transport a multi-GPU node uses over xGMI."""
+import time
+
 import pytest
 import torch
 
@@ -17,7 +19,7 @@ pytestmark = pytest.mark.gpu
 def _clients(tmp_path, n, extra=()):
     addrs = [f"127.0.0.1:{free_port()}" for _ in range(n)]
     procs = [spawn_client(a, tmp_path, "--agg", "collective", "--model", "lenet", "--n-train", "2560",
-                          "--n-test", "1000", "--backend", "gloo", *extra, log_path=tmp_path / f"client{i}.log",
+                          "--n-test", "1000", "--transport", "peer", *extra, log_path=tmp_path / f"client{i}.log",
                           device="cuda:0")
              for i, a in enumerate(addrs)]
     for a in addrs:
@@ -41,10 +43,13 @@ def test_grpc_coordinator_drives_gpu_clients(tmp_path, compress):
                                   "fc1.bias", "fc2.weight", "fc2.bias", "fc3.weight", "fc3.bias"]
         assert all(torch.isfinite(v).all() for v in g["net"].values())
         for a in addrs:
+            t0 = time.time()          # client checkpoints are written by a background writer
+            while (ck.read_epoch(tmp_path / "checkpoint" / f"{a}.pth") or 0) < 3 and time.time() - t0 < 30:
+                time.sleep(0.05)
             c = ck.load(tmp_path / "checkpoint" / f"{a}.pth")
             assert c["epoch"] == 3
             for k in g["net"]:
-                assert torch.allclose(c["net"][k], g["net"][k], atol=1e-6), k
+                assert torch.equal(c["net"][k], g["net"][k]), k     # rank-ordered peer sums: bit-identical
     finally:
         for p in procs:
             stop_proc(p)

@@ -1,0 +1,86 @@
+#!/usr/bin/env python
+"""-c Y kernel timings (csrc/kernels/compress.hip) at the LeNet and ResNet-18 state sizes.
+
+For n = 62,006 (LeNet) and 11,173,962 (ResNet-18): device time of the
+error-feedback delta + exact top-k radix select (k = 1 %), of the rank-ordered
+scatter of 4 ranks' payloads, of int8 quantisation and of a 4-rank dequant
+accumulate; plus payload bytes vs dense fp32.  One JSON line per size.
+"""
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def _time(fn, iters):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def main() -> int:
+    from fedmi import native
+
+    nat = native.require()
+    dev = torch.device("cuda", 0)
+    S = lambda: native.stream_handle(dev)   # noqa: E731
+    out = []
+    for name, n in (("lenet", 62006), ("resnet18", 11173962)):
+        iters = 200 if n < 1e6 else 20
+        k = max(1, int(round(n * 0.01)))
+        R = 4
+        local = torch.randn(n, device=dev)
+        glob = torch.randn(n, device=dev)
+        resid = torch.zeros(n, device=dev)
+        d = torch.empty(n, device=dev)
+        state = torch.zeros(nat.select_state_bytes(), dtype=torch.uint8, device=dev)
+        counts = torch.zeros(2 * ((n + nat.compact_chunk() - 1) // nat.compact_chunk()), dtype=torch.int32, device=dev)
+        idx = torch.empty(k, dtype=torch.int32, device=dev)
+        val = torch.empty(k, device=dev)
+
+        def topk():
+            nat.ef_delta(S(), local.data_ptr(), glob.data_ptr(), resid.data_ptr(), d.data_ptr(), n)
+            nat.topk(S(), d.data_ptr(), n, k, state.data_ptr(), counts.data_ptr(), idx.data_ptr(), val.data_ptr(),
+                     resid.data_ptr())
+
+        t_topk = _time(topk, iters)
+        idx_all = torch.stack([torch.randperm(n, device=dev)[:k].to(torch.int32) for _ in range(R)])
+        val_all = torch.randn(R, k, device=dev)
+        acc = torch.zeros(n, device=dev)
+        t_scatter = _time(lambda: nat.scatter_add_ranked(S(), acc.data_ptr(), idx_all.data_ptr(), val_all.data_ptr(),
+                                                          R, k, 1.0 / R, n), iters)
+        nch = (n + 255) // 256
+        q = torch.empty(n, dtype=torch.int8, device=dev)
+        sc = torch.empty(nch, device=dev)
+        t_q = _time(lambda: nat.quant_int8(S(), d.data_ptr(), n, q.data_ptr(), sc.data_ptr(), resid.data_ptr()), iters)
+        q_all = q.repeat(R)
+        s_all = sc.repeat(R)
+        t_dq = _time(lambda: nat.dequant_accum(S(), q_all.data_ptr(), s_all.data_ptr(), R, n, acc.data_ptr(), 1.0 / R),
+                     iters)
+        rec = {"bench": "compress_kernels", "payload": name, "n": n, "k": k,
+               "topk_us": round(t_topk, 2), "scatter_ranked_4rank_us": round(t_scatter, 2),
+               "quant_int8_us": round(t_q, 2), "dequant_accum_4rank_us": round(t_dq, 2),
+               "bytes_dense": 4 * n, "bytes_topk": 8 * k, "bytes_int8": n + 4 * nch,
+               "ratio_topk": round(4 * n / (8 * k), 2), "ratio_int8": round(4 * n / (n + 4 * nch), 2)}
+        print(json.dumps(rec), flush=True)
+        out.append(rec)
+    if len(sys.argv) > 1:
+        Path(sys.argv[1]).write_text("".join(json.dumps(r) + "\n" for r in out))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

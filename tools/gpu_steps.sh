@@ -1,0 +1,24 @@
+#!/bin/bash
+# Run named GPU steps, each under its own time limit, logging to gpurun_out/<tag>/.
+# A step that fails normally (rc 1/2: a failing test) does not stop the script;
+# a fault, abort, segfault or time limit (rc >= 124) ends it right there.
+#   usage: bash tools/gpu_steps.sh <tag> <name> <seconds> <command> [<name> <seconds> <command> ...]
+set -u
+tag=$1; shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+while [ $# -ge 3 ]; do
+  name=$1; secs=$2; cmd=$3; shift 3
+  echo "=== $name (limit ${secs}s): $cmd" | tee -a "$out/steps.txt"
+  start=$(date +%s)
+  timeout -k 10 "$secs" bash -c "$cmd" > "$out/$name.log" 2>&1
+  rc=$?
+  echo "=== $name rc=$rc wall=$(( $(date +%s) - start ))s" | tee -a "$out/steps.txt"
+  tail -5 "$out/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "=== stopping after $name (rc=$rc)" | tee -a "$out/steps.txt"
+    exit $rc
+  fi
+done
+exit 0
