@@ -204,6 +204,7 @@ def main() -> int:
     from fedmi.engine.data import make_dataset, strided_schedule
     from fedmi.parallel.fedavg import EvalHistory, FedAvg, broadcast_state_, eval_shard
     from fedmi.parallel.compress import make_compressor
+    from fedmi.utils.trace import phase
 
     data = make_dataset("synthetic-cifar10", device=device, n_train=N_TRAIN, n_test=N_TEST, seed=0)
     cfg = TrainerConfig(seed=17, use_graph=not args.no_graph)
@@ -231,14 +232,18 @@ def main() -> int:
     writer = AsyncCheckpointWriter()
 
     def one_round(r: int) -> None:
-        trainer.train_epoch()
-        agg.average(trainer)
+        with phase("local-train"):
+            trainer.train_epoch()
+        with phase("allreduce"):
+            agg.average(trainer)
         if not args.no_eval:
-            trainer.evaluate()
-            hist.record()
+            with phase("eval"):
+                trainer.evaluate()
+                hist.record()
         # global model -> Primary/optimizedModel.pth (rank 0) + this client's checkpoint, one snapshot
-        writer.submit([prim / OPTIMIZED_MODEL, cpath] if prim is not None else cpath, trainer.state_dict(),
-                      acc=1, epoch=r + 1)
+        with phase("checkpoint"):
+            writer.submit([prim / OPTIMIZED_MODEL, cpath] if prim is not None else cpath, trainer.state_dict(),
+                          acc=1, epoch=r + 1)
 
     def barrier():
         if world > 1:

@@ -50,13 +50,18 @@ PDEV void end_call(const PeerArgs& a, int b, uint32_t ep) {
   if (threadIdx.x == 0) st_sys(&a.sig[a.rank]->epoch[b], ep);
 }
 
-PDEV void peer_barrier(const PeerArgs& a, int phase, int b, uint32_t ep) {
+// Returns false (for the whole workgroup) when a peer never arrived: the caller then
+// skips every further access to peer memory -- a dead peer's buffers are not touched.
+PDEV bool peer_barrier(const PeerArgs& a, int phase, int b, uint32_t ep) {
+  __shared__ int s_ok;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) s_ok = 1;
   __syncthreads();
   if (threadIdx.x < 64) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int p = threadIdx.x;
+    bool ok = true;
     if (p < a.world) {
       st_sys(&a.sig[p]->flags[phase][b][a.rank], ep);
       const uint32_t* mine = &a.sig[a.rank]->flags[phase][b][p];
@@ -65,14 +70,17 @@ PDEV void peer_barrier(const PeerArgs& a, int phase, int b, uint32_t ep) {
         __builtin_amdgcn_s_sleep(1);
         if ((long long)(wall_clock64() - t0) > a.timeout_ticks) {
           st_sys(&a.sig[a.rank]->error, 1u);
+          ok = false;
           break;
         }
       }
     }
+    if (__ballot(!ok) != 0ull && threadIdx.x == 0) s_ok = 0;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  return s_ok != 0;
 }
 
 PDEV float4 f4add(float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); }
@@ -107,7 +115,7 @@ __global__ __launch_bounds__(256) void peer_oneshot_f32_kernel(PeerArgs a, const
   for (long long i = (long long)b * 256 + t; i < n4; i += stride)
     reinterpret_cast<float4*>(mine)[i] = reinterpret_cast<const float4*>(in)[i];
   if (b == 0 && t < tail) mine[n4 * 4 + t] = in[n4 * 4 + t];
-  peer_barrier(a, 0, b, ep);
+  if (!peer_barrier(a, 0, b, ep)) return;
   for (long long i = (long long)b * 256 + t; i < n4; i += stride) {
     float4 s = gather_sum4(a, slot, i);
     s.x *= scale; s.y *= scale; s.z *= scale; s.w *= scale;
@@ -135,7 +143,7 @@ __global__ __launch_bounds__(256) void peer_twoshot_f32_kernel(PeerArgs a, const
       reinterpret_cast<float4*>(mine_in)[i] = reinterpret_cast<const float4*>(in)[i];
   }
   if (b == 0 && t < tail) mine_in[n4 * 4 + t] = in[n4 * 4 + t];
-  peer_barrier(a, 0, b, ep);
+  if (!peer_barrier(a, 0, b, ep)) return;
   // 2. reduce my slice from every peer, push the result into every peer's result area
   {
     const long long lo = r * L, hi = (r + 1) * L < n4 ? (r + 1) * L : n4;
@@ -149,7 +157,7 @@ __global__ __launch_bounds__(256) void peer_twoshot_f32_kernel(PeerArgs a, const
       for (int p = 0; p < W; ++p) reinterpret_cast<float*>(region(a, p, slot, 1))[n4 * 4 + t] = v;
     }
   }
-  peer_barrier(a, 1, b, ep);
+  if (!peer_barrier(a, 1, b, ep)) return;
   // 3. every slice of the result is now in my result area
   for (int s = 0; s < W; ++s) {
     const long long lo = s * L, hi = (s + 1) * L < n4 ? (s + 1) * L : n4;
@@ -167,7 +175,7 @@ __global__ __launch_bounds__(256) void peer_i64_mean_floor_kernel(PeerArgs a, co
   const int slot = ep & 1;
   int64_t* mine = reinterpret_cast<int64_t*>(region(a, a.rank, slot, 0));
   for (long long i = threadIdx.x; i < n; i += 256) mine[i] = in[i];
-  peer_barrier(a, 0, 0, ep);
+  if (!peer_barrier(a, 0, 0, ep)) return;
   for (long long i = threadIdx.x; i < n; i += 256) {
     int64_t s = 0;
     for (int p = 0; p < a.world; ++p) s += reinterpret_cast<const int64_t*>(region(a, p, slot, 0))[i];
@@ -185,7 +193,7 @@ __global__ __launch_bounds__(256) void peer_allgather_kernel(PeerArgs a, const u
   const long long stride = (long long)gridDim.x * 256;
   uint4* mine = reinterpret_cast<uint4*>(region(a, a.rank, slot, 0));
   for (long long i = (long long)b * 256 + t; i < n16; i += stride) mine[i] = in[i];
-  peer_barrier(a, 0, b, ep);
+  if (!peer_barrier(a, 0, b, ep)) return;
   for (int p = 0; p < a.world; ++p) {
     const uint4* src = reinterpret_cast<const uint4*>(region(a, p, slot, 0));
     for (long long i = (long long)b * 256 + t; i < n16; i += stride) out[(long long)p * n16 + i] = src[i];

@@ -364,11 +364,17 @@ __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
   const int nf2 = (wave < 6 ? wave : 0) * 16 + n16;
   const float b2 = params[P_F2B + min(nf2, F2 - 1)];
   const float b3 = params[P_F3B + min(n16, NCLS - 1)];
+  // each wave loads only the fragments it uses (the prefetch is bandwidth-per-CU bound:
+  // 8 waves loading fc3's image for wave 0 alone cost ~0.4 us per step)
   bf16x8 w2f[4], w3f[3];
+  if (wave < 6) {
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) w2f[ks] = ld8(pk + PK_FC2 + nf2 * 128 + ks * 32 + kq);
+    for (int ks = 0; ks < 4; ++ks) w2f[ks] = ld8(pk + PK_FC2 + nf2 * 128 + ks * 32 + kq);
+  }
+  if (wave == 0) {
 #pragma unroll
-  for (int ks = 0; ks < 3; ++ks) w3f[ks] = ld8(pk + PK_FC3 + n16 * 96 + ks * 32 + kq);
+    for (int ks = 0; ks < 3; ++ks) w3f[ks] = ld8(pk + PK_FC3 + n16 * 96 + ks * 32 + kq);
+  }
   const int q5 = wave >= 6 ? wave : wave + 8;      // this wave's dH2 task (valid if < 12)
   // dX tiles of this quarter: 25 tiles split 7/6/6/6
   const int t0 = q == 0 ? 0 : 7 + 6 * (q - 1), t1 = q == 0 ? 7 : t0 + 6;
@@ -377,13 +383,15 @@ __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
   bf16x8 w3t, w2t[3], wxt[4];
   float xm[4];
   if (train) {
-    w3t = ld8(pk + PK_FC3T + ((min(q5, 11) - 6) * 16 + n16) * 32 + kq);
+    if (q5 < 12) w3t = ld8(pk + PK_FC3T + ((q5 - 6) * 16 + n16) * 32 + kq);
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks) w2t[ks] = ld8(pk + PK_FC2T + nf1 * 96 + ks * 32 + kq);
+    if (tx < t1) {
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) wxt[ks] = ld8(pk + PK_FC1T + fx * 128 + ks * 32 + kq);
+      for (int ks = 0; ks < 4; ++ks) wxt[ks] = ld8(pk + PK_FC1T + fx * 128 + ks * 32 + kq);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) xm[r] = (float)act2[(size_t)(s0 + min(rq + r, ns - 1)) * F0P + fx];
+      for (int r = 0; r < 4; ++r) xm[r] = (float)act2[(size_t)(s0 + min(rq + r, ns - 1)) * F0P + fx];
+    }
   }
 
   zero_lds(sH1T, sizeof(sH1T));

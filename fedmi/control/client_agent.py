@@ -26,6 +26,7 @@ checkpoints are never ``module.``-prefixed, the checkpoint dir is created.
 """
 from __future__ import annotations
 
+import os
 import threading
 import time
 from pathlib import Path
@@ -39,6 +40,7 @@ from ..engine.data import contiguous_schedule, strided_schedule
 from ..parallel.fedavg import FedAvg
 from ..parallel.group import GroupManager, Membership
 from ..utils.metrics import MetricsLog, Timer, log
+from ..utils.trace import phase
 from ..wire import proto as P
 
 META_TERM = "x-fedmi-term"
@@ -80,6 +82,9 @@ class ClientAgent(P.TrainerServicer):
         self._ready: Optional[tuple] = None     # (epoch, bytes) newest serialised global checkpoint
         self._sent_epoch = -1
         self.ckpt_path = ck.client_ckpt_path(root, address.replace("/", "_"))
+        # fault injection (tests / drills): stall this many seconds right before the FedAvg
+        # collective, so a kill lands while the other clients wait inside it
+        self.fault_stall_avg_s = float(os.environ.get("FEDMI_FAULT_STALL_AVG_S", "0") or 0)
         if resume and self.ckpt_path.exists():
             c = ck.load(self.ckpt_path)
             trainer.load_state_dict(c["net"])
@@ -155,7 +160,11 @@ class ClientAgent(P.TrainerServicer):
             host, _, port = (meta.get(META_STORE) or "127.0.0.1:0").rpartition(":")
             changed = False
             if self.group is not None:
-                changed = self.group.ensure(Membership(gen, rank, world, host, int(port)))
+                with phase("group"):
+                    try:
+                        changed = self.group.ensure(Membership(gen, rank, world, host, int(port)))
+                    except Exception as e:      # rendezvous failed (a member never showed up)
+                        context.abort(grpc.StatusCode.ABORTED, f"data-plane group failed: {e}"[:500])
                 self.fedavg.transport = self.group.transport
             elif world > 1:
                 context.abort(grpc.StatusCode.FAILED_PRECONDITION, "collective aggregation needs a GroupManager")
@@ -168,29 +177,41 @@ class ClientAgent(P.TrainerServicer):
                 self.fedavg.compressor.reset(self.trainer)
             rec["group_ms"] = t.ms()
         t1 = Timer()
-        self.trainer.set_schedule(*self._schedule(rank, world))
-        self.trainer.train_epoch()
-        tr = self.trainer.train_stats()
+        with phase("local-train"):
+            self.trainer.set_schedule(*self._schedule(rank, world))
+            self.trainer.train_epoch()
+            tr = self.trainer.train_stats()
         rec.update(tr.as_dict("train"))
         rec["train_ms"] = t1.ms()
         if self.agg == "collective":
+            if self.fault_stall_avg_s > 0 and world > 1:
+                self.trainer.synchronize()
+                time.sleep(self.fault_stall_avg_s)
             t2 = Timer()
-            self.fedavg.average(self.trainer)
-            tp = self.fedavg.transport
-            if tp is not None and tp.error():
-                context.abort(grpc.StatusCode.ABORTED, "peer collective timed out (a client was lost)")
+            with phase("allreduce"):
+                try:
+                    self.fedavg.average(self.trainer)
+                    tp = self.fedavg.transport
+                    err = "peer collective timed out (a client was lost)" if tp is not None and tp.error() else ""
+                except Exception as e:          # gloo / RCCL error: a peer was lost mid-collective
+                    err = f"collective failed: {e}"
+            if err:
+                # ABORTED (not UNAVAILABLE): this client is alive, only the round is void
+                context.abort(grpc.StatusCode.ABORTED, err[:500])
             rec["allreduce_ms"] = t2.ms()
             t3 = Timer()
-            self.trainer.evaluate()
-            ev = self.trainer.eval_stats()
+            with phase("eval"):
+                self.trainer.evaluate()
+                ev = self.trainer.eval_stats()
             rec["eval_ms"] = t3.ms()
             rec.update(ev.as_dict("test"))
             self.round = rnd
             t4 = Timer()
-            self._persist_async(ev.acc, rnd, keep=(rank == 0))
-            if rank == 0 and meta.get(META_SYNC) == "1":
-                self.writer.flush()
-            ck_epoch, message = self._take_ready() if rank == 0 else (-1, "")
+            with phase("checkpoint"):
+                self._persist_async(ev.acc, rnd, keep=(rank == 0))
+                if rank == 0 and meta.get(META_SYNC) == "1":
+                    self.writer.flush()
+                ck_epoch, message = self._take_ready() if rank == 0 else (-1, "")
             rec["ckpt_ms"] = t4.ms()
         else:
             # reference parameter-server path: the reply IS this round's local model

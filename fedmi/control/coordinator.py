@@ -39,6 +39,7 @@ import torch
 from .. import ckpt as ck
 from ..parallel.group import StoreHost
 from ..utils.metrics import MetricsLog, Timer, log
+from ..utils.trace import phase
 from ..wire import proto as P
 from .client_agent import META_GEN, META_ROUND, META_STORE, META_SYNC, META_TERM
 
@@ -197,6 +198,10 @@ class Coordinator:
 
     # ---- one round ------------------------------------------------------------------
     def run_round(self) -> bool:
+        with phase("coordinator-round"):
+            return self._run_round()
+
+    def _run_round(self) -> bool:
         live = self.live()
         if len(live) < max(1, self.cfg.min_clients):
             time.sleep(self.cfg.heartbeat_s)
@@ -226,7 +231,10 @@ class Coordinator:
             except grpc.RpcError as e:
                 self._log(f"StartTrain on {addr} failed: {e.code().name} {e.details() or ''}".strip())
                 failed.append(addr)
-                self._mark(addr, False)
+                # ABORTED / FAILED_PRECONDITION: the client answered (its collective lost a peer, or it
+                # fenced us); only an unreachable or silent client leaves the membership
+                if e.code() not in (grpc.StatusCode.ABORTED, grpc.StatusCode.FAILED_PRECONDITION):
+                    self._mark(addr, False)
         t_train = t.ms()
         ok = False
         if self.cfg.agg == "collective":

@@ -30,8 +30,9 @@ def small_trainer(model="mlp", n_train=512, n_test=256, seed=0, lr=0.05):
 
 
 def spawn_client(address: str, root: Path, *extra: str, log_path: Path | None = None,
-                 device: str = "cpu") -> subprocess.Popen:
+                 device: str = "cpu", env_extra: dict | None = None) -> subprocess.Popen:
     env = dict(os.environ)
+    env.update(env_extra or {})
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     env["OMP_NUM_THREADS"] = "1"
     cmd = [sys.executable, "-m", "fedmi.cli.client", "-a", address, "--device", device, "--root", str(root),
@@ -66,3 +67,48 @@ def stop_proc(p: subprocess.Popen) -> None:
         except subprocess.TimeoutExpired:
             os.killpg(p.pid, 9)
             p.wait(timeout=10)
+
+
+def spawn_server(root: Path, *args: str, log_path: Path | None = None) -> subprocess.Popen:
+    """``python server.py ...`` (the reference-compatible coordinator entry point) in its own session."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    env["OMP_NUM_THREADS"] = "1"
+    out = open(log_path, "w") if log_path else subprocess.DEVNULL
+    return subprocess.Popen([sys.executable, str(ROOT / "server.py"), *args], env=env, cwd=str(root), stdout=out,
+                            stderr=subprocess.STDOUT, start_new_session=True)
+
+
+def kill9(p: subprocess.Popen) -> float:
+    """SIGKILL the process group; returns the kill time (time.time())."""
+    t = time.time()
+    try:
+        os.killpg(p.pid, 9)
+    except ProcessLookupError:
+        pass
+    p.wait(timeout=10)
+    return t
+
+
+def read_jsonl(path: Path) -> list:
+    import json
+
+    if not Path(path).exists():
+        return []
+    out = []
+    for line in Path(path).read_text().splitlines():
+        try:
+            out.append(json.loads(line))
+        except ValueError:          # a line being written
+            pass
+    return out
+
+
+def wait_for(pred, timeout: float = 60.0, step: float = 0.05):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        v = pred()
+        if v:
+            return v
+        time.sleep(step)
+    raise TimeoutError("condition not reached")
