@@ -27,7 +27,10 @@ void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, cons
 bool stamps_enabled();
 void read_stamps(unsigned long long*, bool);
 void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, const float*, const float*, int, float,
-                      float, float, int*);
+                      float, float, int*, int*);
+void launch_lenet_fwd_head(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*, int,
+                           bf16*, bf16*, bf16*, uint8_t*, uint8_t*, const int*, float*, bf16*, float*, lenet::Stats*,
+                           int*, const int*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
 void launch_sgd_flat(hipStream_t, float*, const float*, float*, long, float, float, float, float, int, int);
 int fedavg_max_inputs();
@@ -77,6 +80,8 @@ static LeNetBuffers buffers_from(const py::dict& d) {
   b.train_stats = P<lenet::Stats>(get("train_stats"));
   b.eval_stats = P<lenet::Stats>(get("eval_stats"));
   b.round_ctr = P<int>(get("round_ctr"));
+  b.done_flags = P<int>(get("done_flags"));
+  b.step_gen = P<int>(get("step_gen"));
   return b;
 }
 
@@ -137,7 +142,9 @@ static void fedmi_bind(py::module_& m) {
       .def("set_sgd", [](LeNetEngine& e, float lr, float m, float wd) {
              SgdConfig c; c.lr = lr; c.momentum = m; c.weight_decay = wd; e.set_sgd(c);
            })
-      .def("graph_ready", &LeNetEngine::graph_ready);
+      .def("graph_ready", &LeNetEngine::graph_ready)
+      .def("set_fuse_head", &LeNetEngine::set_fuse_head)
+      .def("fuse_head", &LeNetEngine::fuse_head);
 
   // ---- raw LeNet kernels (numerics tests drive them one by one) -------------
   m.def("lenet_conv_fwd", [](uintptr_t st, uintptr_t images, int base, int nb, uintptr_t pk, uintptr_t params,
@@ -170,10 +177,24 @@ static void fedmi_bind(py::module_& m) {
   });
   m.def("lenet_sgd", [](uintptr_t st, uintptr_t params, uintptr_t mom, uintptr_t pk, uintptr_t conv_slab, int n_conv,
                         uintptr_t fc1w_grad, uintptr_t fc_slab, int n_fc, float lr, float mo, float wd,
-                        uintptr_t round_ctr) {
+                        uintptr_t round_ctr, uintptr_t step_gen) {
     launch_lenet_sgd(S(st), P<float>(params), P<float>(mom), P<bf16>(pk), P<const float>(conv_slab), n_conv,
-                     P<const float>(fc1w_grad), P<const float>(fc_slab), n_fc, lr, mo, wd, P<int>(round_ctr));
+                     P<const float>(fc1w_grad), P<const float>(fc_slab), n_fc, lr, mo, wd, P<int>(round_ctr),
+                     P<int>(step_gen));
     check_last("lenet_sgd");
+  }, py::arg("stream"), py::arg("params"), py::arg("mom"), py::arg("pk"), py::arg("conv_slab"), py::arg("n_conv"),
+     py::arg("fc1w_grad"), py::arg("fc_slab"), py::arg("n_fc"), py::arg("lr"), py::arg("mo"), py::arg("wd"),
+     py::arg("round_ctr"), py::arg("step_gen") = 0);
+  // K1 + K2b in one launch (training); flags: int[128] hand-off flags, step_gen: int generation (K4 bumps it)
+  m.def("lenet_fwd_head", [](uintptr_t st, uintptr_t images, int base, int nb, uintptr_t pk, uintptr_t params,
+                             uint32_t seed, uintptr_t round_ctr, int augment, uintptr_t act2, uintptr_t act2T,
+                             uintptr_t pool1, uintptr_t am1, uintptr_t am2, uintptr_t labels, uintptr_t dact2,
+                             uintptr_t dZ1T, uintptr_t fc_slab, uintptr_t stats, uintptr_t flags, uintptr_t step_gen) {
+    launch_lenet_fwd_head(S(st), P<const uint8_t>(images), base, nb, P<const bf16>(pk), P<const float>(params), seed,
+                          P<const int>(round_ctr), augment, P<bf16>(act2), P<bf16>(act2T), P<bf16>(pool1),
+                          P<uint8_t>(am1), P<uint8_t>(am2), P<const int>(labels), P<float>(dact2), P<bf16>(dZ1T),
+                          P<float>(fc_slab), P<lenet::Stats>(stats), P<int>(flags), P<const int>(step_gen));
+    check_last("lenet_fwd_head");
   });
   m.def("lenet_pack", [](uintptr_t st, uintptr_t params, uintptr_t pk) {
     launch_lenet_pack(S(st), P<const float>(params), P<bf16>(pk));

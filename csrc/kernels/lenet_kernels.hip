@@ -100,8 +100,10 @@ FEDMI_DEV void zero_lds(void* p, int bytes) {
 // ---------------------------------------------------------------------------
 // K1: conv stack forward, one 8-wave workgroup per sample.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
-    const uint8_t* __restrict__ images, int sample_base, int nb,
+// Body of one sample's workgroup; 'done_flag' (fused fwd+head launch): after act2/act2T
+// are stored, publish 'gen' there for the FC-head workgroups of the same launch.
+FEDMI_DEV void conv_fwd_body(
+    int s, const uint8_t* __restrict__ images, int sample_base, int nb,
     const bf16* __restrict__ pk, const float* __restrict__ params,
     uint32_t seed, const int* __restrict__ round_ctr, int augment,
     bf16* __restrict__ act2,        // [nb][F0P]
@@ -110,7 +112,8 @@ __global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
     bf16* __restrict__ pool1_out,   // [nb][NP1] CHW, or null
     uint8_t* __restrict__ am1_out,  // [nb][NP1] or null
     uint8_t* __restrict__ am2_out,  // [nb][F0]  or null
-    Stats* __restrict__ zero_stats) // stats block to reset before K2 accumulates (or null)
+    Stats* __restrict__ zero_stats, // stats block to reset before K2 accumulates (or null)
+    int* __restrict__ done_flag, int gen)
 {
   // LDS: raw u8 | x channels-last [36][40][4] bf16 | conv1 out f32 channels-last [784][8]
   //      | pool1 channels-last [14][14][8] bf16 | conv2 out f32 channels-last [100][16]
@@ -123,8 +126,8 @@ __global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
   bf16* p1cl = reinterpret_cast<bf16*>(smem + O_P1);
   float* c2 = reinterpret_cast<float*>(smem + O_C2);
 
-  const int s = blockIdx.x;
   if (s >= nb) return;
+  [[maybe_unused]] const int stamp_wg = s;
   const int gidx = sample_base + s;
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
   const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
@@ -239,6 +242,17 @@ __global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
     if (act2T) act2T[(size_t)e * tstride + s] = mb;
   }
   FEDMI_STAMP(0, 5);
+  if (done_flag != nullptr) publish_flag(done_flag + s, gen);
+}
+
+__global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
+    const uint8_t* __restrict__ images, int sample_base, int nb, const bf16* __restrict__ pk,
+    const float* __restrict__ params, uint32_t seed, const int* __restrict__ round_ctr, int augment,
+    bf16* __restrict__ act2, bf16* __restrict__ act2T, int tstride, bf16* __restrict__ pool1_out,
+    uint8_t* __restrict__ am1_out, uint8_t* __restrict__ am2_out, Stats* __restrict__ zero_stats)
+{
+  conv_fwd_body(blockIdx.x, images, sample_base, nb, pk, params, seed, round_ctr, augment, act2, act2T, tstride,
+                pool1_out, am1_out, am2_out, zero_stats, nullptr, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -303,8 +317,11 @@ __global__ __launch_bounds__(256) void lenet_fc1_fwd(
 // FUSE_FC1: the tail computes H1 = relu(X W1^T + b1) for its 16 samples itself
 // (act2 tile -> LDS, this wave's 16 W1 rows -> 13 register fragments at entry)
 // instead of reading K2a's output: one launch and one H1 round trip fewer.
-template <bool FUSE_FC1>
-__global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
+// WAIT (fused fwd+head launch): the weight prefetch runs while the same launch's conv
+// workgroups are still computing; act2 is read only after its 16 samples' flags show 'gen'.
+template <bool FUSE_FC1, bool WAIT>
+FEDMI_DEV void fc_tail_body(
+    int bid,
     const bf16* __restrict__ h1,     // [nb][128]  relu(fc1) from K2a (unused with FUSE_FC1)
     const bf16* __restrict__ act2,   // [nb][F0P]  (for the dX mask)
     const int* __restrict__ labels,  // labels of this batch (already offset)
@@ -313,7 +330,8 @@ __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
     float* __restrict__ dact2,       // [128][F0]       (train)
     bf16* __restrict__ dZ1T,         // [128][DZ1_LD]   (train)
     float* __restrict__ fc_slab,     // [row groups][FS] (train)
-    Stats* __restrict__ stats)
+    Stats* __restrict__ stats,
+    const int* __restrict__ done_flags, int gen)
 {
   __shared__ __attribute__((aligned(16))) bf16 sH1[16 * 128], sH1T[128 * 32];
   __shared__ __attribute__((aligned(16))) bf16 sH2[16 * 96], sH2T[96 * 32];
@@ -328,7 +346,8 @@ __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
   const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
   const int nq = train ? 4 : 1;
-  const int mt = blockIdx.x / nq, q = blockIdx.x - mt * nq;
+  const int mt = bid / nq, q = bid - mt * nq;
+  [[maybe_unused]] const int stamp_wg = bid;
   const int s0 = mt * FC_SPW;
   const int ns = min(FC_SPW, nb - s0);
   if (ns <= 0) return;
@@ -344,15 +363,6 @@ __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
   const int nf1 = wave * 16 + n16;
   float b1 = 0.f;
   if constexpr (FUSE_FC1) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + u * NT_FC;
-      if (e < 16 * XCH) {
-        const int r = e / XCH;
-        xv[u] = reinterpret_cast<const uint4*>(act2 + (size_t)(s0 + min(r, ns - 1)) * F0P)[e - r * XCH];
-        if (r >= ns) xv[u] = make_uint4(0, 0, 0, 0);
-      }
-    }
 #pragma unroll
     for (int ks = 0; ks < 13; ++ks) w1f[ks] = ld8(pk + PK_FC1 + nf1 * F0P + ks * 32 + kq);
     b1 = params[P_F1B + min(nf1, F1 - 1)];
@@ -389,8 +399,6 @@ __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
     if (tx < t1) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) wxt[ks] = ld8(pk + PK_FC1T + fx * 128 + ks * 32 + kq);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) xm[r] = (float)act2[(size_t)(s0 + min(rq + r, ns - 1)) * F0P + fx];
     }
   }
 
@@ -400,6 +408,26 @@ __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
   zero_lds(sdZ3T, sizeof(sdZ3T));
   zero_lds(sdZ2T, sizeof(sdZ2T));
   for (int e = tid; e < 240; e += NT_FC) sdb[e] = 0.f;
+  if constexpr (WAIT) {
+    wait_flags(done_flags + s0, ns, gen, &stats->pad);
+    FEDMI_STAMP(1, 7);
+  }
+  // ---- act2-dependent loads: the act2 tile (fc1 input) and the pool2-ReLU mask of dX
+  if constexpr (FUSE_FC1) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * NT_FC;
+      if (e < 16 * XCH) {
+        const int r = e / XCH;
+        xv[u] = reinterpret_cast<const uint4*>(act2 + (size_t)(s0 + min(r, ns - 1)) * F0P)[e - r * XCH];
+        if (r >= ns) xv[u] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+  if (train && tx < t1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xm[r] = (float)act2[(size_t)(s0 + min(rq + r, ns - 1)) * F0P + fx];
+  }
   if constexpr (FUSE_FC1) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -612,6 +640,45 @@ __global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
   }
   FEDMI_STAMP(1, 6);
 }
+
+template <bool FUSE_FC1>
+__global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
+    const bf16* __restrict__ h1, const bf16* __restrict__ act2, const int* __restrict__ labels, int nb, int train,
+    const bf16* __restrict__ pk, const float* __restrict__ params, float* __restrict__ dact2,
+    bf16* __restrict__ dZ1T, float* __restrict__ fc_slab, Stats* __restrict__ stats)
+{
+  fc_tail_body<FUSE_FC1, false>(blockIdx.x, h1, act2, labels, nb, train, pk, params, dact2, dZ1T, fc_slab, stats,
+                                nullptr, 0);
+}
+
+// ---------------------------------------------------------------------------
+// K12: K1 + K2b in ONE launch (training).  Workgroups [0, nb) run the conv stack
+// of one sample each and publish it; workgroups [nb, nb + 4*rowgroups) are the FC
+// head: they stream their weight fragments from HBM WHILE the conv workgroups
+// compute, then wait for their 16 samples' flags.  Removes a kernel boundary and
+// takes the FC head's ~5 us weight prefetch off the critical path.  The conv
+// workgroups are dispatched first, so the waiting FC workgroups can never block
+// them (and the wait is wall-clock bounded).  Flags hold a step generation read
+// from 'step_gen' (bumped by K4 every step): no reset between steps.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT_FWD) void lenet_fwd_head(
+    const uint8_t* __restrict__ images, int sample_base, int nb, const bf16* __restrict__ pk,
+    const float* __restrict__ params, uint32_t seed, const int* __restrict__ round_ctr, int augment,
+    bf16* __restrict__ act2, bf16* __restrict__ act2T, bf16* __restrict__ pool1_out,
+    uint8_t* __restrict__ am1_out, uint8_t* __restrict__ am2_out, const int* __restrict__ labels,
+    float* __restrict__ dact2, bf16* __restrict__ dZ1T, float* __restrict__ fc_slab, Stats* __restrict__ stats,
+    int* __restrict__ done_flags, const int* __restrict__ step_gen)
+{
+  static_assert(NT_FWD == NT_FC, "one launch hosts both roles");
+  const int gen = step_gen[0] + 1;
+  if ((int)blockIdx.x < nb) {
+    conv_fwd_body(blockIdx.x, images, sample_base, nb, pk, params, seed, round_ctr, augment, act2, act2T,
+                  MAX_TRAIN_BATCH, pool1_out, am1_out, am2_out, nullptr, done_flags, gen);
+    return;
+  }
+  fc_tail_body<true, true>(blockIdx.x - nb, nullptr, act2, labels, nb, 1, pk, params, dact2, dZ1T, fc_slab, stats,
+                           done_flags, gen);
+}
 // ---------------------------------------------------------------------------
 // K3: conv stack backward (one workgroup per sample) + fc1 wgrad workgroups.
 // All per-sample inputs and the conv2 dgrad weights are staged into LDS with
@@ -691,6 +758,7 @@ __global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
   float* w1part = reinterpret_cast<float*>(smem + O_DW1);   // conv1 wgrad K-split partials [3][6][80]
 
   const int s = blockIdx.x;
+  [[maybe_unused]] const int stamp_wg = s;
   const int gidx = sample_base + s;
   FEDMI_STAMP(2, 0);
 
@@ -925,10 +993,11 @@ __global__ __launch_bounds__(256) void lenet_sgd(
     const float* __restrict__ conv_slab, int n_conv,
     const float* __restrict__ fc1w_grad,
     const float* __restrict__ fc_slab, int n_fc,
-    float lr, float momentum, float wd, int* __restrict__ round_ctr)
+    float lr, float momentum, float wd, int* __restrict__ round_ctr, int* __restrict__ step_gen)
 {
   __shared__ float red[16][17];
   const int b = blockIdx.x, tid = threadIdx.x;
+  [[maybe_unused]] const int stamp_wg = b;
   FEDMI_STAMP(3, 0);
   if (b < SGD_NA) {
     const int pl = tid & 15, g = tid >> 4;
@@ -962,7 +1031,10 @@ __global__ __launch_bounds__(256) void lenet_sgd(
       sgd_apply(i, sum, p, m, params, mom, pk, lr, momentum, wd);
     }
   }
-  if (round_ctr && b == 0 && tid == 0) atomicAdd(round_ctr, 1);
+  if (b == 0 && tid == 0) {
+    if (round_ctr) atomicAdd(round_ctr, 1);
+    if (step_gen) step_gen[0] += 1;        // generation of K12's hand-off flags (one writer)
+  }
   FEDMI_STAMP(3, 1);
 }
 
@@ -1011,9 +1083,20 @@ void launch_lenet_conv_bwd(hipStream_t st, const uint8_t* images, int sample_bas
 
 void launch_lenet_sgd(hipStream_t st, float* params, float* mom, bf16* pk, const float* conv_slab,
                       int n_conv, const float* fc1w_grad, const float* fc_slab, int n_fc, float lr,
-                      float momentum, float wd, int* round_ctr) {
+                      float momentum, float wd, int* round_ctr, int* step_gen) {
   hipLaunchKernelGGL(lenet_sgd, dim3(SGD_NA + SGD_NB + SGD_NC), dim3(256), 0, st, params, mom, pk,
-                     conv_slab, n_conv, fc1w_grad, fc_slab, n_fc, lr, momentum, wd, round_ctr);
+                     conv_slab, n_conv, fc1w_grad, fc_slab, n_fc, lr, momentum, wd, round_ctr, step_gen);
+}
+
+void launch_lenet_fwd_head(hipStream_t st, const uint8_t* images, int sample_base, int nb, const bf16* pk,
+                           const float* params, uint32_t seed, const int* round_ctr, int augment, bf16* act2,
+                           bf16* act2T, bf16* pool1, uint8_t* am1, uint8_t* am2, const int* labels, float* dact2,
+                           bf16* dZ1T, float* fc_slab, Stats* stats, int* done_flags, const int* step_gen) {
+  if (nb <= 0 || nb > MAX_TRAIN_BATCH) return;
+  const int mtiles = (nb + FC_SPW - 1) / FC_SPW;
+  hipLaunchKernelGGL(lenet_fwd_head, dim3(nb + 4 * mtiles), dim3(NT_FWD), 0, st, images, sample_base, nb, pk, params,
+                     seed, round_ctr, augment, act2, act2T, pool1, am1, am2, labels, dact2, dZ1T, fc_slab, stats,
+                     done_flags, step_gen);
 }
 
 bool stamps_enabled() {

@@ -36,6 +36,8 @@ struct LeNetBuffers {
   lenet::Stats* train_stats = nullptr;
   lenet::Stats* eval_stats = nullptr;
   int* round_ctr = nullptr;      // augmentation epoch counter (device)
+  int* done_flags = nullptr;     // [MAX_TRAIN_BATCH] K12 hand-off flags (optional: enables fuse_head)
+  int* step_gen = nullptr;       // step generation, bumped by K4
 };
 
 struct SgdConfig {
@@ -66,6 +68,9 @@ class LeNetEngine {
   void set_fuse_fc1(bool on);
   bool fuse_fc1() const { return fuse_fc1_; }
   bool graph_ready() const { return exec_ != nullptr; }
+  // conv stack + FC head in one launch (K12) instead of K1 then K2 (needs done_flags/step_gen)
+  void set_fuse_head(bool on);
+  bool fuse_head() const { return fuse_head_; }
 
  private:
   void enqueue_epoch(hipStream_t st);
@@ -76,6 +81,7 @@ class LeNetEngine {
   uint32_t seed_;
   bool augment_;
   bool fuse_fc1_ = false;
+  bool fuse_head_ = false;
   std::vector<int> starts_, sizes_;
   hipStream_t cap_stream_ = nullptr;
   hipGraph_t graph_ = nullptr;

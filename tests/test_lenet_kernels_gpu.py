@@ -348,3 +348,31 @@ def test_training_converges(env):
     ev = tr.eval_stats()
     assert ev.count == len(ds.test.y)
     assert ev.acc > 12.0 and accs[-1] > accs[0] + 5.0, (ev, accs)
+
+
+@pytest.mark.parametrize("use_graph", [True, False], ids=["graph", "eager"])
+def test_fused_fwd_head_matches_separate_kernels(env, use_graph):
+    """K12 (conv stack + FC head in one launch, flag hand-off) trains exactly like K1 then K2b."""
+    nat, dev, ds, ref, tr = env
+    starts, sizes = [0, 128, 384, 896], [128, 128, 33, 80]      # full and partial batches
+    res = []
+    for fuse in (False, True):
+        tr.engine.set_fuse_head(fuse)
+        tr.load_state_dict(ref.state_dict())
+        tr.mom.zero_()
+        tr.round_ctr.zero_()
+        tr.round_idx = 0
+        tr.cfg.use_graph = use_graph
+        tr.set_schedule(starts, sizes)
+        tr.train_epoch()
+        torch.cuda.synchronize()
+        res.append((tr.params.clone(), tr.train_stats(), int(tr.stats[0][3])))
+    (p0, s0, e0), (p1, s1, e1) = res
+    assert e1 == 0, "K12 hand-off timed out"
+    assert s0.count == s1.count == sum(sizes) and s0.correct == s1.correct
+    assert abs(s0.loss_sum - s1.loss_sum) <= 1e-4 * abs(s0.loss_sum)
+    assert rel(p1, p0) < 1e-5          # only the LDS-atomic order of K3's bias sums differs
+    tr.engine.set_fuse_head(True)
+    tr.cfg.use_graph = True
+    tr.load_state_dict(ref.state_dict())
+    tr.mom.zero_()
