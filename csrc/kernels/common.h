@@ -50,42 +50,6 @@ FEDMI_DEV uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
   return h;
 }
 
-// ---- in-launch producer -> consumer hand-off (MI355X_MICROARCH.md, inter-workgroup
-// visibility): the producer's stores are drained by every storing wave, a workgroup
-// barrier, ONE agent-scope release (L2 write-back), an asm wait (the compiler may drop
-// the one after the release), then a relaxed agent-scope flag store.  The consumer polls
-// relaxed, then ONE agent-scope acquire (L1 invalidate) + wait, then a workgroup barrier.
-FEDMI_DEV void publish_flag(int* flag, int value) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// Wait until flags[0..n) >= value (n <= 64).  Bounded (1 s of wall clock): on timeout the
-// workgroup goes on and *err is set, so a broken hand-off can never hang the GPU.
-FEDMI_DEV void wait_flags(const int* flags, int n, int value, int* err) {
-  if (threadIdx.x < 64) {
-    const int l = threadIdx.x;
-    if (l < n) {
-      const unsigned long long t0 = wall_clock64();
-      while (__hip_atomic_load(flags + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < value) {
-        __builtin_amdgcn_s_sleep(1);
-        if (wall_clock64() - t0 > 100000000ull) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-}
-
 // Wave64 sum via DPP-free shuffles.
 FEDMI_DEV float wave_sum(float v) {
 #pragma unroll

@@ -238,11 +238,24 @@ FEDMI_DEV void conv_fwd_body(
       mb = (bf16)m;
       if (am2_out) am2_out[(size_t)s * F0 + e] = (uint8_t)am;
     }
-    act2[(size_t)s * F0P + e] = mb;
+    if (done_flag != nullptr) reinterpret_cast<bf16*>(raw)[e] = mb;   // staged: published write-through below
+    else act2[(size_t)s * F0P + e] = mb;
     if (act2T) act2T[(size_t)e * tstride + s] = mb;
   }
+  if (done_flag != nullptr) {
+    // Hand-off to the FC-head workgroups of this launch without cache maintenance
+    // (MI355X_MICROARCH.md hand-off table, row 1): the act2 row goes out as 8-byte
+    // write-through (sc1) stores, every wave drains them, a workgroup barrier, then ONE
+    // lane's sc1 flag store.  The consumers read the row only with sc1 loads.
+    __syncthreads();
+    if (tid < F0P / 4)
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(act2 + (size_t)s * F0P) + tid,
+                         reinterpret_cast<const uint64_t*>(raw)[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(done_flag + s, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   FEDMI_STAMP(0, 5);
-  if (done_flag != nullptr) publish_flag(done_flag + s, gen);
 }
 
 __global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
@@ -408,12 +421,34 @@ FEDMI_DEV void fc_tail_body(
   zero_lds(sdZ3T, sizeof(sdZ3T));
   zero_lds(sdZ2T, sizeof(sdZ2T));
   for (int e = tid; e < 240; e += NT_FC) sdb[e] = 0.f;
+  // ---- act2-dependent loads: the act2 tile (fc1 input; in LDS it also gives the dX mask)
   if constexpr (WAIT) {
-    wait_flags(done_flags + s0, ns, gen, &stats->pad);
+    // consumer side of K12's hand-off: sc1 poll, then ONLY sc1 loads of the act2 rows
+    if (tid < 64) {
+      if (tid < ns) {
+        const unsigned long long t0 = wall_clock64();
+        while (__hip_atomic_load(done_flags + s0 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen) {
+          __builtin_amdgcn_s_sleep(1);
+          if (wall_clock64() - t0 > 100000000ull) {      // 1 s: never hang the GPU on a broken hand-off
+            __hip_atomic_store(&stats->pad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+    }
+    __syncthreads();
     FEDMI_STAMP(1, 7);
-  }
-  // ---- act2-dependent loads: the act2 tile (fc1 input) and the pool2-ReLU mask of dX
-  if constexpr (FUSE_FC1) {
+    constexpr int XQ = F0P / 4;                  // 104 8-byte words per act2 row
+    for (int e = tid; e < 16 * XQ; e += NT_FC) {
+      const int r = e / XQ, c = e - r * XQ;
+      uint64_t v = 0;
+      if (r < ns)
+        v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(act2 + (size_t)(s0 + r) * F0P) + c, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+      *reinterpret_cast<uint64_t*>(sX + r * SX_LD + c * 4) = v;
+    }
+    __syncthreads();
+  } else if constexpr (FUSE_FC1) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int e = tid + u * NT_FC;
@@ -424,20 +459,26 @@ FEDMI_DEV void fc_tail_body(
       }
     }
   }
-  if (train && tx < t1) {
+  if (!FUSE_FC1 && train && tx < t1) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) xm[r] = (float)act2[(size_t)(s0 + min(rq + r, ns - 1)) * F0P + fx];
   }
   if constexpr (FUSE_FC1) {
+    if constexpr (!WAIT) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + u * NT_FC;
-      if (e < 16 * XCH) {
-        const int r = e / XCH;
-        *reinterpret_cast<uint4*>(sX + r * SX_LD + (e - r * XCH) * 8) = xv[u];
+      for (int u = 0; u < 2; ++u) {
+        const int e = tid + u * NT_FC;
+        if (e < 16 * XCH) {
+          const int r = e / XCH;
+          *reinterpret_cast<uint4*>(sX + r * SX_LD + (e - r * XCH) * 8) = xv[u];
+        }
       }
+      __syncthreads();
     }
-    __syncthreads();
+    if (train && tx < t1) {                      // pool2-ReLU mask of dX from the LDS tile
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xm[r] = (float)sX[(rq + r) * SX_LD + fx];
+    }
     // fc1 fwd: wave -> 16 output columns, K = 416 (13 steps)
     const bf16* xa = sX + n16 * SX_LD + kq;
     f32x4 acc = zero4();
@@ -1005,8 +1046,16 @@ __global__ __launch_bounds__(256) void lenet_sgd(
     float p = 0.f, m = 0.f;
     if (g == 0 && i < CS) { p = params[i]; m = mom[i]; }      // issued before the slab sweep
     float sum = 0.f;
-    if (i < CS)
-      for (int q = g; q < n_conv; q += 16) sum += conv_slab[(size_t)q * CS + i];
+    if (i < CS) {
+      float v[MAX_TRAIN_BATCH / 16];             // all 8 slab loads in flight before the first add
+#pragma unroll
+      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) {
+        const int q = g + 16 * u;
+        v[u] = q < n_conv ? conv_slab[(size_t)q * CS + i] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) sum += v[u];
+    }
     red[g][pl] = sum;
     __syncthreads();
     if (g == 0 && i < CS) {
@@ -1026,8 +1075,12 @@ __global__ __launch_bounds__(256) void lenet_sgd(
     if (j < FS) {
       const int i = P_F1B + j;
       const float p = params[i], m = mom[i];
+      float v[MAX_FC_WG];
+#pragma unroll
+      for (int q = 0; q < MAX_FC_WG; ++q) v[q] = q < n_fc ? fc_slab[(size_t)q * FS + j] : 0.f;
       float sum = 0.f;
-      for (int q = 0; q < n_fc; ++q) sum += fc_slab[(size_t)q * FS + j];
+#pragma unroll
+      for (int q = 0; q < MAX_FC_WG; ++q) sum += v[q];
       sgd_apply(i, sum, p, m, params, mom, pk, lr, momentum, wd);
     }
   }

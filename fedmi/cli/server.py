@@ -32,6 +32,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--root", default=".", help="directory holding Primary/ and Backup/")
     ap.add_argument("--heartbeat", type=float, default=1.0, help="ping / rejoin-probe period (s)")
     ap.add_argument("--watchdog", type=float, default=3.0, help="backup promotes after this much ping silence (s)")
+    ap.add_argument("--startup-grace", type=float, default=None,
+                    help="before the first primary ping: promote only after this much silence (default max(10, 5*watchdog))")
     ap.add_argument("--train-timeout", type=float, default=600.0)
     ap.add_argument("--rpc-timeout", type=float, default=30.0)
     ap.add_argument("--store-host", default="127.0.0.1")
@@ -77,7 +79,7 @@ def main(argv=None) -> int:
         pinger.stop()
         return 0
     log("server", "Backup triggered")
-    backup = BackupServer(cfg, watchdog_s=a.watchdog, metrics=metrics)
+    backup = BackupServer(cfg, watchdog_s=a.watchdog, metrics=metrics, startup_grace_s=a.startup_grace)
     server, port = serve_backup(backup, a.backupPort)
     log("server", f"backup serving on :{port}")
     while not stop.is_set():

@@ -122,14 +122,19 @@ class Coordinator:
         self.latest_model: Optional[bytes] = self.model_path.read_bytes() if self.model_path.exists() else None
         self.store = StoreHost(cfg.store_host, cfg.store_port) if cfg.agg == "collective" else None
         self._pool = cf.ThreadPoolExecutor(max_workers=max(4, 2 * len(self.members)), thread_name_prefix="fedmi-rpc")
-        self._replicator = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fedmi-replica")
         self._backup = None
         if cfg.backup_address:
             self._backup = P.TrainerStub(P.make_channel(cfg.backup_address))
         self._tracker: Optional[threading.Thread] = None
         self.round_times: List[float] = []
         self.installed_epoch = ck.read_epoch(self.model_path) or -1
-        self._pending: list = []
+        self._persist_cv = threading.Condition()
+        self._to_persist: Optional[bytes] = None
+        self._persist_seq = 0
+        self._persisted_seq = 0
+        self._persist_stop = False
+        self._persist_thread = threading.Thread(target=self._persister, name="fedmi-persist", daemon=True)
+        self._persist_thread.start()
 
     # ---- logging / membership -------------------------------------------------
     def _log(self, msg: str) -> None:
@@ -166,24 +171,41 @@ class Coordinator:
         self.latest_model = data
         if epoch is not None:
             self.installed_epoch = epoch
-        self._pending.append(self._replicator.submit(self._persist_and_replicate, data))
-        self._pending = [f for f in self._pending if not f.done()]
+        with self._persist_cv:
+            self._to_persist = data            # coalesced: only the newest model is written/replicated
+            self._persist_seq += 1
+            self._persist_cv.notify()
 
-    def _persist_and_replicate(self, data: bytes) -> None:
-        ck.atomic_write(self.model_path, data)
-        if self._backup is None:
-            return
-        try:
-            self._backup.SendModel(P.SendModelRequest(model=ck.to_b64(data)), timeout=self.cfg.rpc_timeout_s,
-                                   metadata=[(META_TERM, str(self.term))])
-        except grpc.RpcError as e:
-            self._log(f"backup replication failed: {e.code().name}")
+    def _persister(self) -> None:
+        """Writes ``<mount>/optimizedModel.pth`` and replicates it to the backup, newest model first.
+
+        Rounds can outpace a slow disk or backup link: intermediate models are skipped
+        (bounded memory, minimal lag) instead of queueing every round's checkpoint."""
+        while True:
+            with self._persist_cv:
+                while self._to_persist is None and not self._persist_stop:
+                    self._persist_cv.wait()
+                if self._to_persist is None:
+                    return
+                data, seq = self._to_persist, self._persist_seq
+                self._to_persist = None
+            ck.atomic_write(self.model_path, data)
+            if self._backup is not None:
+                try:
+                    self._backup.SendModel(P.SendModelRequest(model=ck.to_b64(data)),
+                                           timeout=self.cfg.rpc_timeout_s, metadata=[(META_TERM, str(self.term))])
+                except grpc.RpcError as e:
+                    self._log(f"backup replication failed: {e.code().name}")
+            with self._persist_cv:
+                self._persisted_seq = seq
+                self._persist_cv.notify_all()
 
     def flush(self) -> None:
-        """Wait until every installed model is on disk (and offered to the backup)."""
-        for f in list(self._pending):
-            f.result()
-        self._pending = []
+        """Wait until the newest installed model is on disk (and offered to the backup)."""
+        with self._persist_cv:
+            target = self._persist_seq
+            while self._persisted_seq < target and self._persist_thread.is_alive():
+                self._persist_cv.wait(timeout=1.0)
 
     def _send_model(self, address: str, data_b64: str) -> bool:
         m = self.members[address]
@@ -313,7 +335,10 @@ class Coordinator:
     def close(self) -> None:
         self.stop()
         self.flush()
-        self._replicator.shutdown(wait=True)
+        with self._persist_cv:
+            self._persist_stop = True
+            self._persist_cv.notify_all()
+        self._persist_thread.join(timeout=30)
         self._pool.shutdown(wait=False, cancel_futures=True)
         for m in self.members.values():
             try:

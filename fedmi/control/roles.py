@@ -33,9 +33,13 @@ from .coordinator import Coordinator, CoordinatorConfig
 class BackupServer(P.TrainerServicer):
     """Hot standby: replica store + primary watchdog + promotion/demotion."""
 
-    def __init__(self, cfg: CoordinatorConfig, watchdog_s: float = 3.0, metrics: Optional[MetricsLog] = None):
+    def __init__(self, cfg: CoordinatorConfig, watchdog_s: float = 3.0, metrics: Optional[MetricsLog] = None,
+                 startup_grace_s: Optional[float] = None):
         self.cfg = replace(cfg, primary=False, backup_address=None)
         self.watchdog_s = watchdog_s
+        # Until the first ping of a primary arrives, silence only means "not started yet" (a primary
+        # process can take seconds to come up): promote only after this longer grace period.
+        self.startup_grace_s = startup_grace_s if startup_grace_s is not None else max(10.0, 5 * watchdog_s)
         self.metrics = metrics or MetricsLog()
         self.mount = ck.mount_dir(cfg.root, primary=False)
         self._lock = threading.Lock()
@@ -84,7 +88,8 @@ class BackupServer(P.TrainerServicer):
         while not self._stop.wait(period):
             with self._lock:
                 silent = time.monotonic() - self.last_ping
-                should = self.coordinator is None and silent > self.watchdog_s
+                limit = self.watchdog_s if self.primary_seen else self.startup_grace_s
+                should = self.coordinator is None and silent > limit
             if should:
                 self._log(f"no ping from primary for {silent:.2f}s: promoting to primary")
                 self.promote()

@@ -32,6 +32,29 @@ CPU_MODEL = ("--model", "mlp", "--data", "synthetic-mnist", "--n-train", "512", 
 GPU_MODEL = ("--model", "lenet", "--n-train", "2560", "--n-test", "1000")
 
 
+def _report(**rec):
+    """FEDMI_FAILOVER_REPORT=<jsonl>: append the measured drill numbers (profiles/)."""
+    path = os.environ.get("FEDMI_FAILOVER_REPORT")
+    if path:
+        import json
+
+        with open(path, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+
+
+def _keep_logs(tmp_path, tag):
+    """On failure, copy the drill's logs next to FEDMI_FAILOVER_REPORT (read back from the GPU box)."""
+    path = os.environ.get("FEDMI_FAILOVER_REPORT")
+    if path:
+        import shutil
+        from pathlib import Path
+
+        dst = Path(path).parent / f"logs_{tag}"
+        dst.mkdir(parents=True, exist_ok=True)
+        for f in list(tmp_path.glob("*.log")) + list(tmp_path.glob("*.jsonl")):
+            shutil.copy(f, dst / f.name)
+
+
 def _rounds(path, ok_only=True):
     return [r for r in read_jsonl(path) if r.get("event") == "round" and (r.get("ok") or not ok_only)]
 
@@ -58,6 +81,8 @@ def _primary_sigkill_and_recover(tmp_path, device):
         primary = spawn_server(tmp_path, "--p", "y", *common, "--metrics", str(tmp_path / "primary.jsonl"),
                                log_path=tmp_path / "primary.log")
         wait_for(lambda: len(_rounds(tmp_path / "primary.jsonl")) >= 4, timeout=120)
+        # the backup saw the primary (its watchdog is armed) and never acted as primary before the kill
+        assert not [r for r in read_jsonl(tmp_path / "backup.jsonl") if r.get("event") == "promoted"]
         wait_for(lambda: (tmp_path / "srv" / "Backup" / ck.OPTIMIZED_MODEL).exists(), timeout=30)
         # ---- the primary process dies mid-run (the round loop runs back to back: mid-round)
         t_kill = kill9(primary)
@@ -67,8 +92,9 @@ def _primary_sigkill_and_recover(tmp_path, device):
         takeover = promoted[0]["ts"] - t_kill
         assert takeover < 5.0, takeover                       # watchdog 1 s (reference: 13.7 s)
         # the acting backup resumes from the replicated round (not round 0, quirk A8) and keeps going
-        first = wait_for(lambda: _rounds(tmp_path / "backup.jsonl"), timeout=120)[0]
-        assert r_dead - 2 <= first["round"] <= r_dead + 2, (first["round"], r_dead)
+        first = wait_for(lambda: [r for r in _rounds(tmp_path / "backup.jsonl") if r["ts"] > t_kill], timeout=120)[0]
+        # (replication is asynchronous and coalesced: the replica may trail by a few fast rounds)
+        assert max(1, r_dead - 10) <= first["round"] <= r_dead + 2, (first["round"], r_dead)
         wait_for(lambda: max([r["round"] for r in _rounds(tmp_path / "backup.jsonl")] + [0]) >= r_dead + 2,
                  timeout=120)
         # ---- the primary process is restarted: the backup demotes itself cleanly (quirk A2)
@@ -78,9 +104,13 @@ def _primary_sigkill_and_recover(tmp_path, device):
         wait_for(lambda: [r for r in read_jsonl(tmp_path / "backup.jsonl") if r.get("event") == "demoted"],
                  timeout=60)
         r2 = wait_for(lambda: _rounds(tmp_path / "primary2.jsonl"), timeout=120)
-        assert r2[0]["round"] >= r_dead - 2                  # resumed from Primary/optimizedModel.pth's epoch
+        assert r2[0]["round"] >= r_dead - 10                 # resumed from Primary/optimizedModel.pth's epoch
         assert backup.poll() is None                         # the demoted backup is alive and serving
         wait_heartbeat(f"127.0.0.1:{bport}", timeout=10)
+        demoted = [r for r in read_jsonl(tmp_path / "backup.jsonl") if r.get("event") == "demoted"][0]
+        _report(drill="primary_sigkill", device=device, takeover_s=round(takeover, 3), primary_last_round=r_dead,
+                backup_first_round=first["round"], restarted_primary_first_round=r2[0]["round"],
+                demote_after_restart_s=round(demoted["ts"] - promoted[0]["ts"], 3))
         stop_proc(primary2)
         stop_proc(backup)
         return takeover
@@ -133,25 +163,35 @@ def _client_killed_mid_collective(tmp_path, device):
 
         for k in m0:
             assert torch.allclose(m0[k], m1[k], atol=1e-6), k
+        _report(drill="client_sigkill_mid_collective", device=device, recovery_s=round(recovery, 3),
+                aborted_round=aborted[0]["round"], next_ok_round=ok2[0]["round"], collective_timeout_s=3)
         return recovery
     finally:
         for p in procs:
             stop_proc(p)
 
 
+def _drill(fn, tmp_path, device, tag):
+    try:
+        return fn(tmp_path, device)
+    except BaseException:
+        _keep_logs(tmp_path, tag)
+        raise
+
+
 def test_primary_sigkill_backup_promotes_then_demotes_cpu(tmp_path):
-    _primary_sigkill_and_recover(tmp_path, "cpu")
+    _drill(_primary_sigkill_and_recover, tmp_path, "cpu", "primary_cpu")
 
 
 def test_client_sigkill_mid_collective_cpu(tmp_path):
-    _client_killed_mid_collective(tmp_path, "cpu")
+    _drill(_client_killed_mid_collective, tmp_path, "cpu", "client_cpu")
 
 
 @pytest.mark.gpu
 def test_primary_sigkill_backup_promotes_then_demotes_gpu(tmp_path):
-    _primary_sigkill_and_recover(tmp_path, "cuda:0")
+    _drill(_primary_sigkill_and_recover, tmp_path, "cuda:0", "primary_gpu")
 
 
 @pytest.mark.gpu
 def test_client_sigkill_mid_collective_gpu(tmp_path):
-    _client_killed_mid_collective(tmp_path, "cuda:0")
+    _drill(_client_killed_mid_collective, tmp_path, "cuda:0", "client_gpu")

@@ -52,18 +52,12 @@ def main():
               f"start spread {starts.max():7d} cyc")
         for j, ph in enumerate(phases):
             print(f"    {ph:16s} med {np.median(d[:, j]):8.0f}  max {d[:, j].max():8.0f}")
-    # timeline of the step relative to its first stamp (shows K1/K2 overlap in the fused launch)
-    t0 = min(int(st[k, :NWG[k], 0][st[k, :NWG[k], 0] > 0].min()) for k in NAMES if (st[k, :NWG[k], 0] > 0).any())
-    print("timeline (cycles from the step's first stamp): role start-min / end-median / end-max")
-    for k, (name, phases) in NAMES.items():
-        a = st[k, :NWG[k], :len(phases) + 1]
-        a = a[a[:, 0] > 0]
-        if len(a):
-            print(f"    {name:9s} {a[:, 0].min() - t0:9d} {np.median(a[:, -1]) - t0:11.0f} {a[:, -1].max() - t0:9d}")
-    w = st[1, :NWG[1], 7]
-    w = w[w > 0]
-    if len(w):
-        print(f"    fc wait done: median {np.median(w) - t0:.0f} max {w.max() - t0}")
+    # fused K12: split the FC head's first phase at the hand-off (slot 7 = flags seen)
+    f = st[1, :NWG[1]]
+    f = f[(f[:, 0] > 0) & (f[:, 7] > 0)]
+    if len(f):
+        print(f"    fc: start->flags seen med {np.median(f[:, 7] - f[:, 0]):8.0f}  max {(f[:, 7] - f[:, 0]).max():8.0f}"
+              f" | flags seen->H1 med {np.median(f[:, 1] - f[:, 7]):8.0f}  max {(f[:, 1] - f[:, 7]).max():8.0f}")
 
 
 if __name__ == "__main__":
