@@ -49,6 +49,7 @@ using namespace fedmi;
 
 void fedmi_bind_cnn(py::module_& m);   // bindings_cnn.cpp
 void fedmi_bind_comm(py::module_& m);  // bindings_comm.cpp
+void fedmi_bind_zoo(py::module_& m);   // bindings_zoo.cpp
 
 template <typename T>
 static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
@@ -88,6 +89,7 @@ static LeNetBuffers buffers_from(const py::dict& d) {
 static void fedmi_bind(py::module_& m) {
   fedmi_bind_cnn(m);
   fedmi_bind_comm(m);
+  fedmi_bind_zoo(m);
   m.def("stamps_enabled", &stamps_enabled);
   m.def("read_stamps", [](bool clear) {
     const size_t n = (size_t)FEDMI_STAMP_KERNELS * FEDMI_STAMP_WGS * FEDMI_STAMP_SLOTS;

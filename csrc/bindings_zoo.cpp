@@ -1,0 +1,125 @@
+// fedmi — Python bindings for the generic zoo kernels (csrc/kernels/zoo_ops.hip).
+// A tensor crosses as (data_ptr, dtype code, sizes, strides); dtype codes: 0 fp32, 1 bf16, 2 int64.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace fedmi {
+constexpr int ZMAXD = 6;
+struct ZTensor {
+  void* p;
+  int dtype;
+  int ndim;
+  long long size[ZMAXD];
+  long long stride[ZMAXD];
+};
+void launch_ew(hipStream_t, const ZTensor&, const ZTensor*, int, int, float, float, uint32_t, const int*);
+void launch_ctr_bump(hipStream_t, int*);
+void launch_reduce(hipStream_t, const ZTensor&, const ZTensor&, const ZTensor&, const ZTensor&, const void*, int,
+                   const void*, int, const float*, float*, float*, int);
+void launch_bn_fwd_coeffs(hipStream_t, const float*, const float*, const float*, int, long long, const float*,
+                          const float*, float*, float*, float, float, int, float*, float*, float*, float*);
+void launch_bn_bwd_coeffs(hipStream_t, const float*, const float*, const float*, const float*, const float*, int,
+                          long long, float*, float*, float*, float*, float*);
+void launch_pool_fwd(hipStream_t, const ZTensor&, const ZTensor&, const ZTensor&, int, int, int, int, int, int, int, int,
+                     int);
+void launch_pool_bwd(hipStream_t, const ZTensor&, const ZTensor&, const ZTensor&, int, int, int, int, int, int, int, int,
+                     int);
+void launch_gemm(hipStream_t, const ZTensor&, const ZTensor&, const ZTensor&, const ZTensor&, float, float);
+void launch_log_softmax(hipStream_t, const ZTensor&, const ZTensor&, int, const ZTensor&);
+void launch_nll_fwd(hipStream_t, const ZTensor&, const long long*, long long, int, int, void*, int, void*, int);
+void launch_nll_bwd(hipStream_t, const ZTensor&, const void*, int, const void*, int, const long long*, long long, int,
+                    int);
+void launch_ce_stats(hipStream_t, const ZTensor&, const long long*, float*);
+void launch_gconv(hipStream_t, int, const ZTensor&, const ZTensor&, const ZTensor&, int, int, int, int, int);
+}  // namespace fedmi
+
+using fedmi::ZTensor;
+
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// (ptr, dtype, sizes, strides) or None
+static ZTensor zt(const py::object& o) {
+  ZTensor t{};
+  if (o.is_none()) return t;
+  py::tuple tp = o.cast<py::tuple>();
+  if (tp.size() != 4) throw std::invalid_argument("tensor descriptor: (ptr, dtype, sizes, strides)");
+  t.p = reinterpret_cast<void*>(tp[0].cast<uintptr_t>());
+  t.dtype = tp[1].cast<int>();
+  auto sz = tp[2].cast<std::vector<long long>>();
+  auto sd = tp[3].cast<std::vector<long long>>();
+  if (sz.size() != sd.size() || sz.size() > (size_t)fedmi::ZMAXD) throw std::invalid_argument("tensor descriptor: rank");
+  t.ndim = (int)sz.size();
+  for (int d = 0; d < t.ndim; ++d) {
+    t.size[d] = sz[d];
+    t.stride[d] = sd[d];
+  }
+  return t;
+}
+
+void fedmi_bind_zoo(py::module_& m) {
+  m.def("z_ew", [](uintptr_t st, py::object out, std::vector<py::object> ins, int op, float s0, float s1,
+                   uint32_t seed, uintptr_t ctr) {
+    std::vector<ZTensor> v;
+    for (auto& o : ins) v.push_back(zt(o));
+    fedmi::launch_ew(S(st), zt(out), v.data(), (int)v.size(), op, s0, s1, seed, reinterpret_cast<const int*>(ctr));
+  });
+  m.def("z_ctr_bump", [](uintptr_t st, uintptr_t ctr) { fedmi::launch_ctr_bump(S(st), reinterpret_cast<int*>(ctr)); });
+  m.def("z_reduce", [](uintptr_t st, py::object outer, py::object inner, py::object outer_b, py::object inner_b,
+                       uintptr_t a, int a_dt, uintptr_t b, int b_dt, uintptr_t shift, uintptr_t acc, uintptr_t acc2,
+                       int op) {
+    fedmi::launch_reduce(S(st), zt(outer), zt(inner), zt(outer_b), zt(inner_b), reinterpret_cast<const void*>(a), a_dt,
+                         reinterpret_cast<const void*>(b), b_dt, reinterpret_cast<const float*>(shift),
+                         reinterpret_cast<float*>(acc), reinterpret_cast<float*>(acc2), op);
+  });
+  m.def("z_bn_fwd_coeffs", [](uintptr_t st, uintptr_t s1, uintptr_t s2, uintptr_t shift, int C, long long M, uintptr_t w,
+                              uintptr_t b, uintptr_t rmean, uintptr_t rvar, float eps, float mom, int train,
+                              uintptr_t save_mean, uintptr_t save_invstd, uintptr_t scale, uintptr_t bias) {
+    auto f = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
+    fedmi::launch_bn_fwd_coeffs(S(st), f(s1), f(s2), f(shift), C, M, f(w), f(b), f(rmean), f(rvar), eps, mom, train,
+                                f(save_mean), f(save_invstd), f(scale), f(bias));
+  });
+  m.def("z_bn_bwd_coeffs", [](uintptr_t st, uintptr_t sg, uintptr_t sgx, uintptr_t mean, uintptr_t invstd, uintptr_t w,
+                              int C, long long M, uintptr_t k, uintptr_t bb, uintptr_t cc, uintptr_t dw, uintptr_t db) {
+    auto f = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
+    fedmi::launch_bn_bwd_coeffs(S(st), f(sg), f(sgx), f(mean), f(invstd), f(w), C, M, f(k), f(bb), f(cc), f(dw), f(db));
+  });
+  m.def("z_pool_fwd", [](uintptr_t st, py::object x, py::object y, py::object idx, int kh, int kw, int sh, int sw,
+                         int ph, int pw, int cip, int divisor, int is_max) {
+    fedmi::launch_pool_fwd(S(st), zt(x), zt(y), zt(idx), kh, kw, sh, sw, ph, pw, cip, divisor, is_max);
+  });
+  m.def("z_pool_bwd", [](uintptr_t st, py::object dx, py::object dy, py::object idx, int kh, int kw, int sh, int sw,
+                         int ph, int pw, int cip, int divisor, int is_max) {
+    fedmi::launch_pool_bwd(S(st), zt(dx), zt(dy), zt(idx), kh, kw, sh, sw, ph, pw, cip, divisor, is_max);
+  });
+  m.def("z_gemm", [](uintptr_t st, py::object a, py::object b, py::object c, py::object bias, float alpha, float beta) {
+    fedmi::launch_gemm(S(st), zt(a), zt(b), zt(c), zt(bias), alpha, beta);
+  });
+  m.def("z_log_softmax", [](uintptr_t st, py::object x, py::object y, int bwd, py::object gy) {
+    fedmi::launch_log_softmax(S(st), zt(x), zt(y), bwd, zt(gy));
+  });
+  m.def("z_nll_fwd", [](uintptr_t st, py::object lp, uintptr_t tgt, long long tstride, int ignore, int mean,
+                        uintptr_t out, int out_bf16, uintptr_t tw, int tw_bf16) {
+    fedmi::launch_nll_fwd(S(st), zt(lp), reinterpret_cast<const long long*>(tgt), tstride, ignore, mean,
+                          reinterpret_cast<void*>(out), out_bf16, reinterpret_cast<void*>(tw), tw_bf16);
+  });
+  m.def("z_nll_bwd", [](uintptr_t st, py::object gx, uintptr_t g, int g_bf16, uintptr_t tw, int tw_bf16, uintptr_t tgt,
+                        long long tstride, int ignore, int mean) {
+    fedmi::launch_nll_bwd(S(st), zt(gx), reinterpret_cast<const void*>(g), g_bf16, reinterpret_cast<const void*>(tw),
+                          tw_bf16, reinterpret_cast<const long long*>(tgt), tstride, ignore, mean);
+  });
+  m.def("z_ce_stats", [](uintptr_t st, py::object logits, uintptr_t y, uintptr_t stats) {
+    fedmi::launch_ce_stats(S(st), zt(logits), reinterpret_cast<const long long*>(y), reinterpret_cast<float*>(stats));
+  });
+  m.def("z_gconv", [](uintptr_t st, int mode, py::object x, py::object w, py::object y, int G, int sth, int stw,
+                      int padh, int padw) {
+    fedmi::launch_gconv(S(st), mode, zt(x), zt(w), zt(y), G, sth, stw, padh, padw);
+  });
+}

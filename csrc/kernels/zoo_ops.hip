@@ -1,0 +1,717 @@
+// fedmi — generic native kernels for the zoo families without a whole-network
+// engine (DenseNet, ResNeXt, DPN, ShuffleNet v1/v2, SENet, EfficientNet, RegNet,
+// PNASNet, DLA, SimpleDLA).  They back the aten ops of a
+// training step through fedmi.ops.native_mode (a TorchDispatchMode): every
+// elementwise / reduction / BatchNorm / pooling / GEMM / loss / grouped-conv op of
+// those models runs here or on the MFMA / depthwise conv kernels, none on ATen.
+//
+// Tensors are described by (ptr, dtype, sizes, strides) so one kernel serves any
+// layout (channels-last activations, broadcast operands, channel slices of a
+// concatenation); dtypes are fp32 / bf16 / int64.  Integer index math is 64-bit
+// only where a tensor can exceed 2^31 elements' byte range (never, in practice).
+#include <cstdint>
+#include <stdexcept>
+
+#include "common.h"
+
+namespace fedmi {
+void check_hip(hipError_t e, const char* what);
+
+constexpr int ZMAXD = 6;
+enum ZDtype : int { Z_F32 = 0, Z_BF16 = 1, Z_I64 = 2 };
+
+struct ZTensor {
+  void* p;
+  int dtype;
+  int ndim;
+  long long size[ZMAXD];
+  long long stride[ZMAXD];
+};
+}  // namespace fedmi
+
+namespace {
+using fedmi::ZTensor;
+using fedmi::ZMAXD;
+
+FEDMI_DEV float zload(const ZTensor& t, long long off) {
+  if (t.dtype == 0) return reinterpret_cast<const float*>(t.p)[off];
+  if (t.dtype == 1) return (float)reinterpret_cast<const bf16*>(t.p)[off];
+  return (float)reinterpret_cast<const long long*>(t.p)[off];
+}
+FEDMI_DEV void zstore(const ZTensor& t, long long off, float v) {
+  if (t.dtype == 0) reinterpret_cast<float*>(t.p)[off] = v;
+  else if (t.dtype == 1) reinterpret_cast<bf16*>(t.p)[off] = (bf16)v;
+  else reinterpret_cast<long long*>(t.p)[off] = (long long)v;
+}
+
+// ---- elementwise ------------------------------------------------------------------
+enum EwOp : int {
+  EW_COPY = 0,       // o = a
+  EW_ADD = 1,        // o = a + s0 * b
+  EW_MUL = 2,        // o = a * b
+  EW_MULS = 3,       // o = a * s0
+  EW_RELU = 4,       // o = max(a, 0)
+  EW_THR_BWD = 5,    // o = b > s0 ? a : 0          (threshold_backward(grad=a, self=b))
+  EW_SIGMOID = 6,    // o = 1 / (1 + exp(-a))
+  EW_SIG_BWD = 7,    // o = a * b * (1 - b)         (sigmoid_backward(grad=a, out=b))
+  EW_FILL = 8,       // o = s0
+  EW_FMA = 9,        // o = a * b + c
+  EW_BNB = 11,       // o = a * b + c * d + e      (BatchNorm backward apply: g*k + x*bb + cc)
+  EW_BERN = 12,      // o = hash(seed, ctr, i) < s0 ? 1 : 0   (bernoulli_(p = s0))
+  EW_SUB = 13,       // o = a - s0 * b
+  EW_DIV = 14,       // o = a / b
+  EW_ADDS = 15,      // o = a + s0
+};
+
+struct EwArgs {
+  ZTensor o;
+  ZTensor in[5];
+  float s0, s1;
+  int op;
+  uint32_t seed;
+  const int* ctr;    // EW_BERN: device step counter
+};
+
+// offset of linear element `i` of the output iteration space in tensor t
+// (32-bit index decode: the host guarantees every tensor has < 2^31 elements)
+FEDMI_DEV long long zoffset(const ZTensor& shape, const ZTensor& t, long long i64) {
+  uint32_t i = (uint32_t)i64;
+  long long off = 0;
+#pragma unroll
+  for (int d = ZMAXD - 1; d >= 0; --d) {
+    if (d < shape.ndim) {
+      const uint32_t sz = (uint32_t)shape.size[d];
+      const uint32_t q = i / sz;
+      off += (long long)(i - q * sz) * t.stride[d];
+      i = q;
+    }
+  }
+  return off;
+}
+
+__global__ __launch_bounds__(256) void ew_kernel(EwArgs a, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const uint32_t ctr = a.ctr ? (uint32_t)a.ctr[0] : 0u;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f, x4 = 0.f;
+    if (a.in[0].p) x0 = zload(a.in[0], zoffset(a.o, a.in[0], i));
+    if (a.in[1].p) x1 = zload(a.in[1], zoffset(a.o, a.in[1], i));
+    if (a.in[2].p) x2 = zload(a.in[2], zoffset(a.o, a.in[2], i));
+    if (a.in[3].p) x3 = zload(a.in[3], zoffset(a.o, a.in[3], i));
+    if (a.in[4].p) x4 = zload(a.in[4], zoffset(a.o, a.in[4], i));
+    float v;
+    switch (a.op) {
+      case EW_COPY: v = x0; break;
+      case EW_ADD: v = x0 + a.s0 * x1; break;
+      case EW_SUB: v = x0 - a.s0 * x1; break;
+      case EW_MUL: v = x0 * x1; break;
+      case EW_DIV: v = x0 / x1; break;
+      case EW_ADDS: v = x0 + a.s0; break;
+      case EW_MULS: v = x0 * a.s0; break;
+      case EW_RELU: v = fmaxf(x0, 0.f); break;
+      case EW_THR_BWD: v = x1 > a.s0 ? x0 : 0.f; break;
+      case EW_SIGMOID: v = 1.f / (1.f + __expf(-x0)); break;
+      case EW_SIG_BWD: v = x0 * x1 * (1.f - x1); break;
+      case EW_FILL: v = a.s0; break;
+      case EW_FMA: v = x0 * x1 + x2; break;
+      case EW_BNB: v = x0 * x1 + x2 * x3 + x4; break;
+      case EW_BERN: {
+        const uint32_t h = hash3(a.seed, ctr, (uint32_t)i ^ (uint32_t)(i >> 32));
+        v = ((float)(h >> 8) * (1.f / 16777216.f)) < a.s0 ? 1.f : 0.f;
+        break;
+      }
+      default: v = 0.f;
+    }
+    zstore(a.o, zoffset(a.o, a.o, i), v);
+  }
+}
+
+__global__ void ctr_bump_kernel(int* ctr) {
+  if (threadIdx.x == 0) ctr[0] += 1;
+}
+
+// ---- reduction: out[outer] (+)= sum over inner of f(in...) ----------------------------
+// outer / inner index spaces with their own sizes and per-tensor strides.
+enum RdOp : int { RD_SUM = 0, RD_SUMSQ_SHIFT = 1, RD_DOT_SHIFT = 2 };
+struct RdArgs {
+  ZTensor outer;     // sizes of the kept dims; strides of input a along them
+  ZTensor inner;     // sizes of the reduced dims; strides of input a along them
+  ZTensor outer_b;   // strides of input b along the kept dims (RD_DOT_SHIFT)
+  ZTensor inner_b;
+  const void* a;
+  int a_dtype;
+  const void* b;
+  int b_dtype;
+  const float* shift;   // per-outer shift (moments of (a - shift)), or null
+  float* acc;           // fp32 [n_outer] accumulator (atomics), zeroed by the host
+  float* acc2;          // second accumulator (RD_SUMSQ_SHIFT: sum of squares; RD_DOT_SHIFT: sum a*(b-shift))
+  int op;
+};
+
+FEDMI_DEV float rload(const void* p, int dt, long long off) {
+  if (dt == 0) return reinterpret_cast<const float*>(p)[off];
+  return (float)reinterpret_cast<const bf16*>(p)[off];
+}
+
+// block = 64 outer lanes x 4 inner lanes; grid = (outer tiles, inner splits)
+__global__ __launch_bounds__(256) void reduce_kernel(RdArgs r, long long n_outer, long long n_inner) {
+  __shared__ float red[2][4][64];
+  const int lo = threadIdx.x & 63, li = threadIdx.x >> 6;
+  const long long o = (long long)blockIdx.x * 64 + lo;
+  float s1 = 0.f, s2 = 0.f;
+  if (o < n_outer) {
+    const long long base_a = zoffset(r.outer, r.outer, o);
+    const long long base_b = r.b ? zoffset(r.outer, r.outer_b, o) : 0;
+    const float sh = r.shift ? r.shift[o] : 0.f;
+    const long long per = (n_inner + gridDim.y - 1) / gridDim.y;
+    const long long i0 = (long long)blockIdx.y * per, i1 = i0 + per < n_inner ? i0 + per : n_inner;
+    for (long long i = i0 + li; i < i1; i += 4) {
+      const float va = rload(r.a, r.a_dtype, base_a + zoffset(r.inner, r.inner, i));
+      if (r.op == RD_SUM) {
+        s1 += va;
+      } else if (r.op == RD_SUMSQ_SHIFT) {
+        const float d = va - sh;
+        s1 += d;
+        s2 += d * d;
+      } else {
+        const float vb = rload(r.b, r.b_dtype, base_b + zoffset(r.inner, r.inner_b, i));
+        s1 += va;
+        s2 += va * (vb - sh);
+      }
+    }
+  }
+  red[0][li][lo] = s1;
+  red[1][li][lo] = s2;
+  __syncthreads();
+  if (li == 0 && o < n_outer) {
+    const float t1 = red[0][0][lo] + red[0][1][lo] + red[0][2][lo] + red[0][3][lo];
+    atomicAdd(r.acc + o, t1);
+    if (r.op != RD_SUM) {
+      const float t2 = red[1][0][lo] + red[1][1][lo] + red[1][2][lo] + red[1][3][lo];
+      atomicAdd(r.acc2 + o, t2);
+    }
+  }
+}
+
+// ---- BatchNorm per-channel coefficients --------------------------------------------
+// forward (train): from sum(x - shift), sum((x - shift)^2) over M rows:
+//   mean, invstd -> save_mean / save_invstd; scale = w * invstd, bias = b - mean * scale;
+//   running stats (momentum, unbiased var) updated in place.
+// forward (eval): from running stats.
+__global__ void bn_fwd_coeffs_kernel(const float* s1, const float* s2, const float* shift, int C, long long M,
+                                     const float* w, const float* b, float* rmean, float* rvar, float eps,
+                                     float mom, int train, float* save_mean, float* save_invstd, float* scale,
+                                     float* bias) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float mean, inv;
+  if (train) {
+    const float ms = s1[c] / (float)M;
+    const float var = fmaxf(s2[c] / (float)M - ms * ms, 0.f);
+    mean = ms + (shift ? shift[c] : 0.f);
+    inv = rsqrtf(var + eps);
+    if (save_mean) save_mean[c] = mean;
+    if (save_invstd) save_invstd[c] = inv;
+    if (rmean) {
+      rmean[c] = (1.f - mom) * rmean[c] + mom * mean;
+      rvar[c] = (1.f - mom) * rvar[c] + mom * var * ((float)M / (float)(M > 1 ? M - 1 : 1));
+    }
+  } else {
+    mean = rmean[c];
+    inv = rsqrtf(rvar[c] + eps);
+  }
+  const float sc = (w ? w[c] : 1.f) * inv;
+  scale[c] = sc;
+  bias[c] = (b ? b[c] : 0.f) - mean * sc;
+}
+
+// backward: from sg = sum g, sgx = sum g * (x - mean):
+//   k = w * invstd, dx = g * k + x * bb + cc with bb = -k * invstd^2 * sgx / M, cc = -k * sg / M - bb * mean
+__global__ void bn_bwd_coeffs_kernel(const float* sg, const float* sgx, const float* mean, const float* invstd,
+                                     const float* w, int C, long long M, float* k, float* bb, float* cc,
+                                     float* dw, float* db) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = invstd[c];
+  const float kk = (w ? w[c] : 1.f) * inv;
+  const float b = -kk * inv * inv * sgx[c] / (float)M;
+  k[c] = kk;
+  bb[c] = b;
+  cc[c] = -kk * sg[c] / (float)M - b * mean[c];
+  if (dw) dw[c] = sgx[c] * inv;
+  if (db) db[c] = sg[c];
+}
+
+// ---- pooling (any layout via strides; 4-D [N, C, H, W] logical) ----------------------
+struct PoolArgs {
+  ZTensor x;    // [N, C, H, W]
+  ZTensor y;    // [N, C, P, Q]
+  ZTensor idx;  // int64 [N, C, P, Q] (max pool) or p == null
+  int kh, kw, sh, sw, ph, pw;
+  int count_include_pad;
+  int divisor;  // 0: default
+};
+
+__global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a, int is_max, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long P = a.y.size[2], Q = a.y.size[3], C = a.y.size[1], H = a.x.size[2], W = a.x.size[3];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    long long t = i;
+    const long long q = t % Q; t /= Q;
+    const long long p = t % P; t /= P;
+    const long long c = t % C; t /= C;
+    const long long nn = t;
+    const long long h0 = p * a.sh - a.ph, w0 = q * a.sw - a.pw;
+    const long long xb = nn * a.x.stride[0] + c * a.x.stride[1];
+    float acc = is_max ? -INFINITY : 0.f;
+    long long arg = -1;
+    int cnt = 0;
+    for (int r = 0; r < a.kh; ++r) {
+      const long long h = h0 + r;
+      for (int s = 0; s < a.kw; ++s) {
+        const long long w = w0 + s;
+        const bool in = h >= 0 && h < H && w >= 0 && w < W;
+        if (is_max) {
+          if (in) {
+            const float v = zload(a.x, xb + h * a.x.stride[2] + w * a.x.stride[3]);
+            if (v > acc || arg < 0 || v != v) { acc = v; arg = h * W + w; }
+          }
+        } else {
+          if (in) acc += zload(a.x, xb + h * a.x.stride[2] + w * a.x.stride[3]);
+          // count_include_pad counts the padded window clipped to the padded input
+          if (in || (a.count_include_pad && h < H + a.ph && w < W + a.pw)) ++cnt;
+        }
+      }
+    }
+    const long long yo = nn * a.y.stride[0] + c * a.y.stride[1] + p * a.y.stride[2] + q * a.y.stride[3];
+    if (is_max) {
+      zstore(a.y, yo, acc);
+      if (a.idx.p)
+        reinterpret_cast<long long*>(a.idx.p)[nn * a.idx.stride[0] + c * a.idx.stride[1] + p * a.idx.stride[2] +
+                                              q * a.idx.stride[3]] = arg;
+    } else {
+      const int div = a.divisor ? a.divisor : (cnt > 0 ? cnt : 1);
+      zstore(a.y, yo, acc / (float)div);
+    }
+  }
+}
+
+// dx gather: every input element sums the grads of the windows covering it
+__global__ __launch_bounds__(256) void pool_bwd_kernel(PoolArgs a, ZTensor dy, int is_max, long long n) {
+  // here a.x describes dx (output), dy the incoming grad [N, C, P, Q]
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long P = dy.size[2], Q = dy.size[3], C = a.x.size[1], H = a.x.size[2], W = a.x.size[3];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    long long t = i;
+    const long long w = t % W; t /= W;
+    const long long h = t % H; t /= H;
+    const long long c = t % C; t /= C;
+    const long long nn = t;
+    // windows p with p*sh - ph <= h < p*sh - ph + kh
+    const long long pl = (h + a.ph - a.kh) >= 0 ? (h + a.ph - a.kh) / a.sh + 1 : 0;
+    const long long ph_ = (h + a.ph) / a.sh;
+    const long long ql = (w + a.pw - a.kw) >= 0 ? (w + a.pw - a.kw) / a.sw + 1 : 0;
+    const long long qh = (w + a.pw) / a.sw;
+    float acc = 0.f;
+    for (long long p = pl; p <= ph_ && p < P; ++p) {
+      for (long long q = ql; q <= qh && q < Q; ++q) {
+        const long long o = nn * dy.stride[0] + c * dy.stride[1] + p * dy.stride[2] + q * dy.stride[3];
+        if (is_max) {
+          const long long arg = reinterpret_cast<const long long*>(a.idx.p)[nn * a.idx.stride[0] + c * a.idx.stride[1] +
+                                                                            p * a.idx.stride[2] + q * a.idx.stride[3]];
+          if (arg == h * W + w) acc += zload(dy, o);
+        } else {
+          int cnt;
+          if (a.divisor) {
+            cnt = a.divisor;
+          } else {
+            const long long hs = p * a.sh - a.ph, ws = q * a.sw - a.pw;
+            long long he = hs + a.kh, we = ws + a.kw;
+            if (a.count_include_pad) {
+              he = he < H + a.ph ? he : H + a.ph;
+              we = we < W + a.pw ? we : W + a.pw;
+              cnt = (int)((he - hs) * (we - ws));
+            } else {
+              const long long h0 = hs > 0 ? hs : 0, w0 = ws > 0 ? ws : 0;
+              he = he < H ? he : H;
+              we = we < W ? we : W;
+              cnt = (int)((he - h0) * (we - w0));
+            }
+          }
+          acc += zload(dy, o) / (float)(cnt > 0 ? cnt : 1);
+        }
+      }
+    }
+    zstore(a.x, nn * a.x.stride[0] + c * a.x.stride[1] + h * a.x.stride[2] + w * a.x.stride[3], acc);
+  }
+}
+
+// ---- small GEMM: C[M,N] = alpha * A[M,K] B[K,N] + beta * bias (broadcast over rows) ------
+// 16 x 16 output tile per 256-thread block, K in LDS chunks of 16; fp32 accumulate.
+__global__ __launch_bounds__(256) void gemm_kernel(ZTensor A, ZTensor B, ZTensor Cm, ZTensor bias, float alpha,
+                                                   float beta) {
+  __shared__ float as[16][17], bs[16][17];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const long long M = Cm.size[0], N = Cm.size[1], K = A.size[1];
+  const long long row = (long long)blockIdx.y * 16 + ty, col = (long long)blockIdx.x * 16 + tx;
+  float acc = 0.f;
+  for (long long k0 = 0; k0 < K; k0 += 16) {
+    const long long ka = k0 + tx, kb = k0 + ty;
+    const long long ar = (long long)blockIdx.y * 16 + ty, bc = (long long)blockIdx.x * 16 + tx;
+    as[ty][tx] = (ar < M && ka < K) ? zload(A, ar * A.stride[0] + ka * A.stride[1]) : 0.f;
+    bs[ty][tx] = (kb < K && bc < N) ? zload(B, kb * B.stride[0] + bc * B.stride[1]) : 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) acc += as[ty][kk] * bs[kk][tx];
+    __syncthreads();
+  }
+  if (row < M && col < N) {
+    float v = alpha * acc;
+    if (bias.p) v += beta * zload(bias, (bias.ndim == 2 ? row * bias.stride[0] : 0) + col * bias.stride[bias.ndim - 1]);
+    zstore(Cm, row * Cm.stride[0] + col * Cm.stride[1], v);
+  }
+}
+
+// ---- log_softmax over dim 1 of a 2-D tensor; NLL loss (mean, ignore_index) -------------
+__global__ void log_softmax_kernel(ZTensor x, ZTensor y, int bwd, ZTensor gy) {
+  // fwd: y = x - logsumexp(x); bwd (x = output of fwd): y = gy - exp(x) * sum(gy)
+  const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= x.size[0]) return;
+  const long long J = x.size[1];
+  if (!bwd) {
+    float mx = -INFINITY;
+    for (long long j = 0; j < J; ++j) mx = fmaxf(mx, zload(x, r * x.stride[0] + j * x.stride[1]));
+    float se = 0.f;
+    for (long long j = 0; j < J; ++j) se += __expf(zload(x, r * x.stride[0] + j * x.stride[1]) - mx);
+    const float lse = mx + __logf(se);
+    for (long long j = 0; j < J; ++j) zstore(y, r * y.stride[0] + j * y.stride[1], zload(x, r * x.stride[0] + j * x.stride[1]) - lse);
+  } else {
+    float sg = 0.f;
+    for (long long j = 0; j < J; ++j) sg += zload(gy, r * gy.stride[0] + j * gy.stride[1]);
+    for (long long j = 0; j < J; ++j)
+      zstore(y, r * y.stride[0] + j * y.stride[1],
+             zload(gy, r * gy.stride[0] + j * gy.stride[1]) - __expf(zload(x, r * x.stride[0] + j * x.stride[1])) * sg);
+  }
+}
+
+// nll fwd: out = -sum_r lp[r][t_r] / n_valid ; total_weight = n_valid.  One workgroup.
+__global__ __launch_bounds__(256) void nll_fwd_kernel(ZTensor lp, const long long* tgt, long long tstride,
+                                                      int ignore, int reduction_mean, float* out_f32, bf16* out_bf16,
+                                                      float* tw_f32, bf16* tw_bf16) {
+  __shared__ float sl[256], sc[256];
+  float l = 0.f, c = 0.f;
+  for (long long r = threadIdx.x; r < lp.size[0]; r += 256) {
+    const long long t = tgt[r * tstride];
+    if (t != ignore) { l -= zload(lp, r * lp.stride[0] + t * lp.stride[1]); c += 1.f; }
+  }
+  sl[threadIdx.x] = l; sc[threadIdx.x] = c;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) { sl[threadIdx.x] += sl[threadIdx.x + s]; sc[threadIdx.x] += sc[threadIdx.x + s]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float v = reduction_mean ? sl[0] / fmaxf(sc[0], 1.f) : sl[0];
+    if (out_f32) *out_f32 = v; else *out_bf16 = (bf16)v;
+    if (tw_f32) *tw_f32 = sc[0]; else if (tw_bf16) *tw_bf16 = (bf16)sc[0];
+  }
+}
+
+// nll bwd: gx[r][j] = (j == t_r) ? -g / total_weight : 0   (mean); -g (sum)
+__global__ void nll_bwd_kernel(ZTensor gx, const float* g, const float* tw, const long long* tgt, long long tstride,
+                               int ignore, int reduction_mean, int g_bf16, int tw_bf16) {
+  const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= gx.size[0]) return;
+  const float gv = g_bf16 ? (float)*reinterpret_cast<const bf16*>(g) : *g;
+  const float twv = tw_bf16 ? (float)*reinterpret_cast<const bf16*>(tw) : *tw;
+  const long long t = tgt[r * tstride];
+  const float v = reduction_mean ? -gv / fmaxf(twv, 1.f) : -gv;
+  for (long long j = 0; j < gx.size[1]; ++j) zstore(gx, r * gx.stride[0] + j * gx.stride[1], (t != ignore && j == t) ? v : 0.f);
+}
+
+// training statistics of a classifier output: loss_sum += CE, correct += argmax == y, count += n
+__global__ __launch_bounds__(256) void ce_stats_kernel(ZTensor logits, const long long* y, float* stats) {
+  __shared__ float sl[256], sc[256];
+  float l = 0.f, c = 0.f;
+  const long long J = logits.size[1];
+  for (long long r = threadIdx.x; r < logits.size[0]; r += 256) {
+    float mx = -INFINITY;
+    long long am = 0;
+    for (long long j = 0; j < J; ++j) {
+      const float v = zload(logits, r * logits.stride[0] + j * logits.stride[1]);
+      if (v > mx) { mx = v; am = j; }
+    }
+    float se = 0.f;
+    for (long long j = 0; j < J; ++j) se += __expf(zload(logits, r * logits.stride[0] + j * logits.stride[1]) - mx);
+    const long long t = y[r];
+    l += mx + __logf(se) - zload(logits, r * logits.stride[0] + t * logits.stride[1]);
+    c += (am == t) ? 1.f : 0.f;
+  }
+  sl[threadIdx.x] = l; sc[threadIdx.x] = c;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) { sl[threadIdx.x] += sl[threadIdx.x + s]; sc[threadIdx.x] += sc[threadIdx.x + s]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    stats[0] += sl[0];
+    stats[1] += sc[0];
+    stats[2] += (float)logits.size[0];
+  }
+}
+
+// ---- direct (VALU) grouped convolution, any channel counts ---------------------------
+// x [N, C, H, W], w [O, C/G, R, S], y [N, O, P, Q] -- logical NCHW, any strides.
+struct GConv {
+  ZTensor x, w, y;
+  int G, st_h, st_w, pad_h, pad_w, R, S;
+};
+
+__global__ __launch_bounds__(256) void gconv_fwd_kernel(GConv g, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long O = g.y.size[1], P = g.y.size[2], Q = g.y.size[3];
+  const long long H = g.x.size[2], W = g.x.size[3];
+  const long long Cg = g.w.size[1], Og = O / g.G;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    // o fastest: neighbouring lanes read the same input pixel, neighbouring weights
+    long long t = i;
+    const long long o = t % O; t /= O;
+    const long long q = t % Q; t /= Q;
+    const long long p = t % P; t /= P;
+    const long long nn = t;
+    const long long c0 = (o / Og) * Cg;
+    float acc = 0.f;
+    for (int r = 0; r < g.R; ++r) {
+      const long long h = p * g.st_h - g.pad_h + r;
+      if (h < 0 || h >= H) continue;
+      for (int s = 0; s < g.S; ++s) {
+        const long long w = q * g.st_w - g.pad_w + s;
+        if (w < 0 || w >= W) continue;
+        const long long xb = nn * g.x.stride[0] + h * g.x.stride[2] + w * g.x.stride[3];
+        const long long wb = o * g.w.stride[0] + r * g.w.stride[2] + s * g.w.stride[3];
+        for (long long c = 0; c < Cg; ++c)
+          acc += zload(g.x, xb + (c0 + c) * g.x.stride[1]) * zload(g.w, wb + c * g.w.stride[1]);
+      }
+    }
+    zstore(g.y, nn * g.y.stride[0] + o * g.y.stride[1] + p * g.y.stride[2] + q * g.y.stride[3], acc);
+  }
+}
+
+// dx[n][c][h][w] = sum_{o in group(c), r, s: (h + pad - r) % st == 0} dy[n][o][(h+pad-r)/st][(w+pad-s)/st] w[o][c - c0][r][s]
+__global__ __launch_bounds__(256) void gconv_dgrad_kernel(GConv g, long long n) {
+  // g.x = dx (output), g.y = dy (input)
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long C = g.x.size[1], H = g.x.size[2], W = g.x.size[3];
+  const long long O = g.y.size[1], P = g.y.size[2], Q = g.y.size[3];
+  const long long Cg = g.w.size[1], Og = O / g.G;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    long long t = i;
+    const long long c = t % C; t /= C;
+    const long long w = t % W; t /= W;
+    const long long h = t % H; t /= H;
+    const long long nn = t;
+    const long long grp = c / Cg, cc = c - grp * Cg;
+    float acc = 0.f;
+    for (int r = 0; r < g.R; ++r) {
+      const long long hp = h + g.pad_h - r;
+      if (hp < 0 || hp % g.st_h) continue;
+      const long long p = hp / g.st_h;
+      if (p >= P) continue;
+      for (int s = 0; s < g.S; ++s) {
+        const long long wp = w + g.pad_w - s;
+        if (wp < 0 || wp % g.st_w) continue;
+        const long long q = wp / g.st_w;
+        if (q >= Q) continue;
+        const long long yb = nn * g.y.stride[0] + p * g.y.stride[2] + q * g.y.stride[3];
+        for (long long oo = 0; oo < Og; ++oo) {
+          const long long o = grp * Og + oo;
+          acc += zload(g.y, yb + o * g.y.stride[1]) *
+                 zload(g.w, o * g.w.stride[0] + cc * g.w.stride[1] + r * g.w.stride[2] + s * g.w.stride[3]);
+        }
+      }
+    }
+    zstore(g.x, nn * g.x.stride[0] + c * g.x.stride[1] + h * g.x.stride[2] + w * g.x.stride[3], acc);
+  }
+}
+
+// dw[o][c][r][s] = sum_{n,p,q} dy[n][o][p][q] x[n][c0 + c][p*st - pad + r][q*st - pad + s]
+// one workgroup per weight element; 256 lanes split the (n, p, q) sum, LDS tree reduce.
+__global__ __launch_bounds__(256) void gconv_wgrad_kernel(GConv g, ZTensor dw) {
+  __shared__ float red[256];
+  const long long O = g.y.size[1], P = g.y.size[2], Q = g.y.size[3];
+  const long long H = g.x.size[2], W = g.x.size[3], N = g.x.size[0];
+  const long long Cg = g.w.size[1], Og = O / g.G;
+  long long e = blockIdx.x;
+  const int s = (int)(e % g.S); e /= g.S;
+  const int r = (int)(e % g.R); e /= g.R;
+  const long long c = e % Cg; e /= Cg;
+  const long long o = e;
+  const long long cx = (o / Og) * Cg + c;
+  float acc = 0.f;
+  const long long tot = N * P * Q;
+  for (long long i = threadIdx.x; i < tot; i += 256) {
+    long long t = i;
+    const long long q = t % Q; t /= Q;
+    const long long p = t % P; t /= P;
+    const long long nn = t;
+    const long long h = p * g.st_h - g.pad_h + r, w = q * g.st_w - g.pad_w + s;
+    if (h < 0 || h >= H || w < 0 || w >= W) continue;
+    acc += zload(g.y, nn * g.y.stride[0] + o * g.y.stride[1] + p * g.y.stride[2] + q * g.y.stride[3]) *
+           zload(g.x, nn * g.x.stride[0] + cx * g.x.stride[1] + h * g.x.stride[2] + w * g.x.stride[3]);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    zstore(dw, o * dw.stride[0] + c * dw.stride[1] + r * dw.stride[2] + s * dw.stride[3], red[0]);
+}
+
+int grid1(long long n) {
+  long long b = (n + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 4096) b = 4096;
+  return (int)b;
+}
+
+}  // namespace
+
+namespace fedmi {
+
+void launch_ew(hipStream_t st, const ZTensor& o, const ZTensor* ins, int nin, int op, float s0, float s1,
+               uint32_t seed, const int* ctr) {
+  if (nin > 5) throw std::invalid_argument("ew: at most 5 inputs");
+  EwArgs a{};
+  a.o = o;
+  for (int i = 0; i < nin; ++i) a.in[i] = ins[i];
+  a.op = op;
+  a.s0 = s0;
+  a.s1 = s1;
+  a.seed = seed;
+  a.ctr = ctr;
+  long long n = 1;
+  for (int d = 0; d < o.ndim; ++d) n *= o.size[d];
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ew_kernel, dim3(grid1(n)), dim3(256), 0, st, a, n);
+  check_hip(hipGetLastError(), "ew_kernel");
+}
+
+void launch_ctr_bump(hipStream_t st, int* ctr) {
+  hipLaunchKernelGGL(ctr_bump_kernel, dim3(1), dim3(64), 0, st, ctr);
+}
+
+void launch_reduce(hipStream_t st, const ZTensor& outer, const ZTensor& inner, const ZTensor& outer_b,
+                   const ZTensor& inner_b, const void* a, int a_dt, const void* b, int b_dt, const float* shift,
+                   float* acc, float* acc2, int op) {
+  long long no = 1, ni = 1;
+  for (int d = 0; d < outer.ndim; ++d) no *= outer.size[d];
+  for (int d = 0; d < inner.ndim; ++d) ni *= inner.size[d];
+  if (no <= 0) return;
+  RdArgs r{};
+  r.outer = outer; r.inner = inner; r.outer_b = outer_b; r.inner_b = inner_b;
+  r.a = a; r.a_dtype = a_dt; r.b = b; r.b_dtype = b_dt; r.shift = shift; r.acc = acc; r.acc2 = acc2; r.op = op;
+  const long long tiles = (no + 63) / 64;
+  long long splits = (1024 + tiles - 1) / tiles;             // ~1024 workgroups in flight
+  const long long max_split = (ni + 255) / 256;              // >= 64 inner elements per lane group
+  if (splits > max_split) splits = max_split;
+  if (splits < 1) splits = 1;
+  if (splits > 65535) splits = 65535;
+  hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)tiles, (unsigned)splits), dim3(256), 0, st, r, no, ni);
+  check_hip(hipGetLastError(), "reduce_kernel");
+}
+
+void launch_bn_fwd_coeffs(hipStream_t st, const float* s1, const float* s2, const float* shift, int C, long long M,
+                          const float* w, const float* b, float* rmean, float* rvar, float eps, float mom, int train,
+                          float* save_mean, float* save_invstd, float* scale, float* bias) {
+  hipLaunchKernelGGL(bn_fwd_coeffs_kernel, dim3((C + 255) / 256), dim3(256), 0, st, s1, s2, shift, C, M, w, b, rmean,
+                     rvar, eps, mom, train, save_mean, save_invstd, scale, bias);
+  check_hip(hipGetLastError(), "bn_fwd_coeffs");
+}
+
+void launch_bn_bwd_coeffs(hipStream_t st, const float* sg, const float* sgx, const float* mean, const float* invstd,
+                          const float* w, int C, long long M, float* k, float* bb, float* cc, float* dw, float* db) {
+  hipLaunchKernelGGL(bn_bwd_coeffs_kernel, dim3((C + 255) / 256), dim3(256), 0, st, sg, sgx, mean, invstd, w, C, M, k,
+                     bb, cc, dw, db);
+  check_hip(hipGetLastError(), "bn_bwd_coeffs");
+}
+
+void launch_pool_fwd(hipStream_t st, const ZTensor& x, const ZTensor& y, const ZTensor& idx, int kh, int kw, int sh,
+                     int sw, int ph, int pw, int count_include_pad, int divisor, int is_max) {
+  PoolArgs a{};
+  a.x = x; a.y = y; a.idx = idx; a.kh = kh; a.kw = kw; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw;
+  a.count_include_pad = count_include_pad; a.divisor = divisor;
+  long long n = y.size[0] * y.size[1] * y.size[2] * y.size[3];
+  if (n <= 0) return;
+  hipLaunchKernelGGL(pool_fwd_kernel, dim3(grid1(n)), dim3(256), 0, st, a, is_max, n);
+  check_hip(hipGetLastError(), "pool_fwd");
+}
+
+void launch_pool_bwd(hipStream_t st, const ZTensor& dx, const ZTensor& dy, const ZTensor& idx, int kh, int kw, int sh,
+                     int sw, int ph, int pw, int count_include_pad, int divisor, int is_max) {
+  PoolArgs a{};
+  a.x = dx; a.idx = idx; a.kh = kh; a.kw = kw; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw;
+  a.count_include_pad = count_include_pad; a.divisor = divisor;
+  long long n = dx.size[0] * dx.size[1] * dx.size[2] * dx.size[3];
+  if (n <= 0) return;
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3(grid1(n)), dim3(256), 0, st, a, dy, is_max, n);
+  check_hip(hipGetLastError(), "pool_bwd");
+}
+
+void launch_gemm(hipStream_t st, const ZTensor& A, const ZTensor& B, const ZTensor& Cm, const ZTensor& bias, float alpha,
+                 float beta) {
+  const long long M = Cm.size[0], N = Cm.size[1];
+  if (M <= 0 || N <= 0) return;
+  dim3 grid((unsigned)((N + 15) / 16), (unsigned)((M + 15) / 16));
+  hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, st, A, B, Cm, bias, alpha, beta);
+  check_hip(hipGetLastError(), "gemm");
+}
+
+void launch_log_softmax(hipStream_t st, const ZTensor& x, const ZTensor& y, int bwd, const ZTensor& gy) {
+  const long long R = x.size[0];
+  hipLaunchKernelGGL(log_softmax_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, st, x, y, bwd, gy);
+  check_hip(hipGetLastError(), "log_softmax");
+}
+
+void launch_nll_fwd(hipStream_t st, const ZTensor& lp, const long long* tgt, long long tstride, int ignore, int mean,
+                    void* out, int out_bf16, void* tw, int tw_bf16) {
+  hipLaunchKernelGGL(nll_fwd_kernel, dim3(1), dim3(256), 0, st, lp, tgt, tstride, ignore, mean,
+                     out_bf16 ? nullptr : reinterpret_cast<float*>(out), out_bf16 ? reinterpret_cast<bf16*>(out) : nullptr,
+                     tw_bf16 ? nullptr : reinterpret_cast<float*>(tw), tw_bf16 ? reinterpret_cast<bf16*>(tw) : nullptr);
+  check_hip(hipGetLastError(), "nll_fwd");
+}
+
+void launch_nll_bwd(hipStream_t st, const ZTensor& gx, const void* g, int g_bf16, const void* tw, int tw_bf16,
+                    const long long* tgt, long long tstride, int ignore, int mean) {
+  const long long R = gx.size[0];
+  hipLaunchKernelGGL(nll_bwd_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, st, gx,
+                     reinterpret_cast<const float*>(g), reinterpret_cast<const float*>(tw), tgt, tstride, ignore, mean,
+                     g_bf16, tw_bf16);
+  check_hip(hipGetLastError(), "nll_bwd");
+}
+
+void launch_ce_stats(hipStream_t st, const ZTensor& logits, const long long* y, float* stats) {
+  hipLaunchKernelGGL(ce_stats_kernel, dim3(1), dim3(256), 0, st, logits, y, stats);
+  check_hip(hipGetLastError(), "ce_stats");
+}
+
+void launch_gconv(hipStream_t st, int mode, const ZTensor& x, const ZTensor& w, const ZTensor& y, int G, int sth,
+                  int stw, int padh, int padw) {
+  GConv g{};
+  g.x = x; g.w = w; g.y = y; g.G = G; g.st_h = sth; g.st_w = stw; g.pad_h = padh; g.pad_w = padw;
+  g.R = (int)w.size[2]; g.S = (int)w.size[3];
+  if (mode == 0) {
+    const long long n = y.size[0] * y.size[1] * y.size[2] * y.size[3];
+    if (n > 0) hipLaunchKernelGGL(gconv_fwd_kernel, dim3(grid1(n)), dim3(256), 0, st, g, n);
+  } else if (mode == 1) {
+    const long long n = x.size[0] * x.size[1] * x.size[2] * x.size[3];
+    if (n > 0) hipLaunchKernelGGL(gconv_dgrad_kernel, dim3(grid1(n)), dim3(256), 0, st, g, n);
+  } else {
+    const long long n = w.size[0] * w.size[1] * w.size[2] * w.size[3];
+    if (n > 0) hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((unsigned)n), dim3(256), 0, st, g, w);
+  }
+  check_hip(hipGetLastError(), "gconv");
+}
+
+}  // namespace fedmi

@@ -31,11 +31,13 @@ SOURCES = [
     CSRC / "kernels" / "conv_igemm.hip",
     CSRC / "kernels" / "cnn_ops.hip",
     CSRC / "kernels" / "dwconv.hip",
+    CSRC / "kernels" / "zoo_ops.hip",
     CSRC / "comm" / "peer_comm.hip",
     CSRC / "runtime" / "lenet_engine.cpp",
     CSRC / "bindings.cpp",
     CSRC / "bindings_cnn.cpp",
     CSRC / "bindings_comm.cpp",
+    CSRC / "bindings_zoo.cpp",
 ]
 HEADERS = sorted(CSRC.rglob("*.h"))
 

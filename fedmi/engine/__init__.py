@@ -19,9 +19,10 @@ NATIVE_CNNS = ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "mo
 def build_trainer(model: str, data: FedDataset, device, cfg: TrainerConfig = TrainerConfig(),
                   init_state=None) -> LocalTrainer:
     """On a GPU: LeNet -> fused HIP engine; ResNet / MobileNet / MobileNetV2 -> the implicit-GEMM +
-    BN-fused HIP engine (mandatory, no silent fallback).  Other zoo models -> the generic PyTorch
-    engine with the native MFMA convs installed under autograd (``FEDMI_HYBRID=0``: PyTorch convs, fp32);
-    CPU runs -> the generic PyTorch engine."""
+    BN-fused HIP engine (mandatory, no silent fallback).  Other zoo models -> the generic engine with
+    every aten op of the step on fedmi's HIP kernels (:class:`fedmi.ops.native_mode.NativeMode`, bf16
+    channels-last activations, graph-replayed; ``FEDMI_HYBRID=0``: plain PyTorch fp32); CPU runs -> the
+    generic PyTorch engine."""
     device = torch.device(device)
     from ..models import _canon
 
@@ -40,9 +41,9 @@ def build_trainer(model: str, data: FedDataset, device, cfg: TrainerConfig = Tra
     if _canon(model) in ("lenet", "mlp"):
         c, h, w = data.train.x.shape[1:]
         kw = {"in_channels": c} if _canon(model) == "lenet" else {"in_features": c * h * w}
-    # zoo models without a whole-network engine: native MFMA convs under PyTorch autograd (bf16 NHWC)
+    # zoo models without a whole-network engine: PyTorch autograd over the native aten backend
     hybrid = (device.type == "cuda" and not native.force_torch_path() and os.environ.get("FEDMI_HYBRID", "1") != "0"
-              and _canon(model) not in ("lenet", "mlp"))
+              and _canon(model) != "lenet")
     return TorchTrainer(model, data, device, cfg, init_state=init_state, model_kwargs=kw, hybrid=hybrid)
 
 

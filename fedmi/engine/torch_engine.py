@@ -8,9 +8,11 @@ update is a single ``sgd_flat`` launch instead of 4 ops per tensor.
 On CPU the identical update is done with torch ops (reference semantics).
 
 ``hybrid=True`` (GPU; what :func:`fedmi.engine.build_trainer` picks for zoo models without a
-whole-network native engine): every eligible conv runs on the MFMA implicit-GEMM kernels
-(:mod:`fedmi.ops.native_layers`), the network runs channels-last under bf16 autocast, so the
-remaining PyTorch ops (BN, pooling, concat, SE gates) work on the same NHWC bf16 activations.
+whole-network native engine): the step runs under :class:`fedmi.ops.native_mode.NativeMode`, so
+every aten op of forward AND autograd backward executes on fedmi's HIP kernels (MFMA / depthwise /
+grouped convs, BatchNorm, pooling, concat, SE gates, GEMM, loss) on channels-last bf16 activations
+with fp32 master weights; the whole SGD step (zero-grad, forward, backward, fused SGD, loss /
+accuracy statistics) is captured once into a HIP graph and replayed.
 """
 from __future__ import annotations
 
@@ -84,24 +86,25 @@ class TorchTrainer(LocalTrainer):
         self.round_idx = 0
         self._starts: List[int] = []
         self._sizes: List[int] = []
-        self._tstats = torch.zeros(3, dtype=torch.float64, device=self._device)
-        self._estats = torch.zeros(3, dtype=torch.float64, device=self._device)
         self._nat = native.require() if self._device.type == "cuda" and not native.force_torch_path() else None
         self.hybrid = bool(hybrid and self._nat is not None)
-        self.native_convs: List[str] = []
+        # hybrid: the native ce_stats kernel accumulates fp32 (exact for counts < 2^24)
+        sdt = torch.float32 if self.hybrid else torch.float64
+        self._tstats = torch.zeros(3, dtype=sdt, device=self._device)
+        self._estats = torch.zeros(3, dtype=sdt, device=self._device)
+        self.mode = None
+        self._flat_input = model_name.lower() == "mlp"     # flattens NCHW: keep the fp32 input as is
         if self.hybrid:
-            from ..ops import native_layers
+            from ..ops.native_mode import NativeMode
 
-            self.native_convs = native_layers.install(self.model)
-        # hybrid mode replays each full-batch SGD step (forward + autograd backward + SGD + stats) from
-        # one captured HIP graph: the Python / launch overhead of ~10^3 small kernels per step goes away
-        # Opt-in (FEDMI_HYBRID_GRAPH=1): SENet18 replayed from the graph goes NaN ~130 steps in (earlier
-        # when the host syncs every replay) while the identical eager sequence trains for 2+ epochs;
-        # ResNet18 / SimpleDLA replay cleanly; one trigger was PyTorch's bf16 adaptive_avg_pool2d (now an
-        # fp32 mean, models/zoo/pool.py: SENet18 replays cleanly), but EfficientNetB0 / RegNetY_400MF still
-        # diverge under replay only (tools/diag_hybrid_lr.py, profiles/hybrid_graph_nan_diag_r1.txt).
-        # Default: eager.
-        self.use_graph = bool(self.hybrid and cfg.use_graph and os.environ.get("FEDMI_HYBRID_GRAPH", "0") == "1")
+            self.mode = NativeMode(strict=os.environ.get("FEDMI_NATIVE_STRICT", "0") == "1", seed=cfg.seed)
+            self.mode.rng_ctr(self._device)      # allocated here, never inside a captured step
+        # hybrid mode replays each full-batch SGD step (zero-grad + forward + autograd backward + SGD +
+        # stats) from one captured HIP graph: the Python / launch overhead of ~10^3 small kernels per step
+        # goes away.  Round 1's NaN-under-replay (autocast weight-cast cache, bf16 adaptive pooling, host
+        # RNG state baked into the graph) is gone with the native backend: no autocast, fp32-accumulated
+        # reductions, dropout masks keyed by a device counter the graph itself bumps.
+        self.use_graph = bool(self.hybrid and cfg.use_graph and os.environ.get("FEDMI_HYBRID_GRAPH", "1") == "1")
         self._graph = None
         self._gx = self._gy = None
 
@@ -143,14 +146,14 @@ class TorchTrainer(LocalTrainer):
         return self._layout(xin), self.train_set.y[start:start + nb].long()
 
     def _layout(self, x: torch.Tensor) -> torch.Tensor:
-        return x.contiguous(memory_format=torch.channels_last) if self.hybrid and x.dim() == 4 else x
+        if self.hybrid and x.dim() == 4 and not self._flat_input:
+            from ..ops.native_mode import EW_COPY, ew
+
+            out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+            return ew(out.contiguous(memory_format=torch.channels_last), [x], EW_COPY)
+        return x
 
     def _run(self, x: torch.Tensor) -> torch.Tensor:
-        if self.hybrid:
-            # no autocast weight-cast cache: a cached cast made while capturing goes stale in the replayed
-            # graph (training diverged to NaN ~130 steps in, eager was fine; tools/diag_hybrid_lr.py)
-            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
-                return self.model(x).float()
         return self.model(x)
 
     # ---- compute -------------------------------------------------------------------
@@ -207,6 +210,17 @@ class TorchTrainer(LocalTrainer):
 
     def _step_body(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         nb = x.shape[0]
+        if self.mode is not None:
+            from ..ops.native_mode import ce_stats_
+
+            with self.mode:
+                self.fs.grad.zero_()
+                out = self._run(x)
+                loss = F.cross_entropy(out, y)
+                loss.backward()
+            self._sgd()
+            ce_stats_(out.detach(), y, self._tstats)
+            return loss
         self.fs.grad.zero_()
         out = self._run(x)
         loss = F.cross_entropy(out, y)
@@ -239,6 +253,13 @@ class TorchTrainer(LocalTrainer):
         for s in range(0, n, bs):
             x = self._layout(augment_normalize(self.test_set.x[s:s + bs], None, 0, 0, self.mean, self.std))
             y = self.test_set.y[s:s + bs].long()
+            if self.mode is not None:
+                from ..ops.native_mode import ce_stats_
+
+                with self.mode:
+                    out = self._run(x)
+                ce_stats_(out, y, self._estats)
+                continue
             out = self._run(x)
             self._estats[0] += F.cross_entropy(out, y, reduction="sum").double()
             self._estats[1] += (out.argmax(1) == y).sum()

@@ -1,0 +1,781 @@
+"""A native aten backend for the zoo families without a whole-network engine.
+
+:class:`NativeMode` is a ``TorchDispatchMode``: while it is active, every aten op
+of a training step that launches device work -- forward AND the backward ops
+autograd generates -- is executed by fedmi's HIP kernels instead of ATen/MIOpen/
+rocBLAS:
+
+* convolutions: the MFMA implicit-GEMM kernels (``conv_igemm.hip``: forward,
+  data gradient, weight gradient) for dense convs with 8-aligned channels, the
+  depthwise kernels (``dwconv.hip``), one MFMA GEMM per group for few wide groups
+  (ResNeXt), and a direct VALU kernel (``zoo_ops.hip``) for every other grouped /
+  odd-width conv (DPN, ShuffleNet, RegNet, the 3-channel stems);
+* BatchNorm (train + eval, running statistics), elementwise / activation ops with
+  broadcasting, channel concat / slice gradients, spatial reductions (SE gates,
+  bias gradients), avg / max pooling, the classifier GEMMs, log-softmax + NLL,
+  dropout / drop-connect masks (a counter-based RNG keyed by a device step counter,
+  so a replayed HIP graph draws fresh masks) -- all in ``zoo_ops.hip``.
+
+Metadata ops (views, expand, transpose, detach, empty) pass through: they launch
+nothing.  Output shapes / strides / dtypes follow ATen's own meta functions where
+the operands share a dtype, so layouts (channels-last activations) are preserved.
+Ops without a native implementation are counted in :attr:`NativeMode.fallbacks`
+(and raise with ``strict=True``): the GPU tests assert that a training step of
+every hybrid family needs none.
+
+Reference ops: the union of SURVEY.md §2.4(d) (convolution(+backward), addmm/mm,
+native_batch_norm(+backward), relu / threshold_backward, avg_pool2d, cat,
+max_pool2d_with_indices, sigmoid, mul, mean, slice_backward, bernoulli_, ...).
+"""
+from __future__ import annotations
+
+import collections
+from typing import Optional
+
+import torch
+from torch.utils._python_dispatch import TorchDispatchMode
+
+from .. import native
+from . import conv as CV
+
+aten = torch.ops.aten
+
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.int64: 2}
+
+# elementwise op codes (zoo_ops.hip EwOp)
+EW_COPY, EW_ADD, EW_MUL, EW_MULS, EW_RELU, EW_THR_BWD, EW_SIGMOID, EW_SIG_BWD, EW_FILL, EW_FMA = range(10)
+EW_BNB, EW_BERN, EW_SUB, EW_DIV, EW_ADDS = 11, 12, 13, 14, 15
+# an impl returns ATEN when the op is legitimately ATen's (host copies, scalar reads): not a fallback
+ATEN = object()
+RD_SUM, RD_SUMSQ_SHIFT, RD_DOT_SHIFT = 0, 1, 2
+
+
+def _nat():
+    return native.require()
+
+
+def _st(dev) -> int:
+    return native.stream_handle(dev)
+
+
+def zd(t: Optional[torch.Tensor]):
+    """(ptr, dtype code, sizes, strides) descriptor of a CUDA tensor (None passes through)."""
+    if t is None:
+        return None
+    if t.dtype not in _DT:
+        raise TypeError(f"native_mode: unsupported dtype {t.dtype}")
+    if t.numel() >= (1 << 31):
+        raise ValueError("native_mode: tensors must have < 2^31 elements")
+    if t.dim() == 0:
+        return (t.data_ptr(), _DT[t.dtype], [1], [1])
+    return (t.data_ptr(), _DT[t.dtype], list(t.shape), list(t.stride()))
+
+
+def _bcast(t: torch.Tensor, shape) -> torch.Tensor:
+    if tuple(t.shape) == tuple(shape):
+        return t
+    return t.expand(shape) if t.dim() == len(shape) else t.reshape((1,) * (len(shape) - t.dim()) + tuple(t.shape)).expand(shape)
+
+
+def ew(out: torch.Tensor, ins, op: int, s0: float = 0.0, s1: float = 0.0, seed: int = 0, ctr=None) -> torch.Tensor:
+    """out[...] = op(ins...) with broadcasting of every input to out's shape."""
+    if out.numel() == 0:
+        return out
+    shape = out.shape if out.dim() else (1,)
+    o = out if out.dim() else out.view(1)
+    descs = [zd(_bcast(t if t.dim() else t.view(1), shape)) for t in ins]
+    _nat().z_ew(_st(out.device), zd(o), descs, op, float(s0), float(s1), int(seed) & 0xFFFFFFFF,
+                0 if ctr is None else ctr.data_ptr())
+    return out
+
+
+def fill_(t: torch.Tensor, v: float) -> torch.Tensor:
+    return ew(t, [], EW_FILL, v)
+
+
+def _scalar(x) -> Optional[float]:
+    """A Python number or a CPU 0-dim 'wrapped number' tensor -> float; a device tensor -> None."""
+    if isinstance(x, (int, float, bool)):
+        return float(x)
+    if isinstance(x, torch.Tensor) and x.dim() == 0 and not x.is_cuda:
+        return float(x.item())
+    return None
+
+
+def _meta(t):
+    if isinstance(t, torch.Tensor):
+        return torch.empty_strided(t.shape, t.stride(), dtype=t.dtype, device="meta")
+    if isinstance(t, (list, tuple)):
+        return type(t)(_meta(v) for v in t)
+    return t
+
+
+def _alloc_like_meta(func, args, kwargs, dev):
+    """Run ATen's meta function for the output metadata, allocate real (uninitialised) outputs."""
+    m = func(*_meta(args), **{k: _meta(v) for k, v in kwargs.items()})
+    if isinstance(m, torch.Tensor):
+        return torch.empty_strided(m.shape, m.stride(), dtype=m.dtype, device=dev)
+    return type(m)(torch.empty_strided(t.shape, t.stride(), dtype=t.dtype, device=dev) for t in m)
+
+
+def _dev(*ts):
+    for t in ts:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            return t.device
+        if isinstance(t, (list, tuple)):
+            d = _dev(*t)
+            if d is not None:
+                return d
+    return None
+
+
+def reduce_sum(a: torch.Tensor, dims, acc: torch.Tensor, op: int = RD_SUM, b: Optional[torch.Tensor] = None,
+               shift: Optional[torch.Tensor] = None, acc2: Optional[torch.Tensor] = None) -> None:
+    """acc (fp32, ZEROED, one entry per kept element in order) += sum over ``dims`` of f(a[, b])."""
+    dims = sorted(d % a.dim() for d in dims)
+    kept = [d for d in range(a.dim()) if d not in dims]
+    def desc(t, ds):
+        if not ds:
+            return (0, 0, [1], [0])
+        return (0, 0, [t.shape[d] for d in ds], [t.stride(d) for d in ds])
+    outer, inner = desc(a, kept), desc(a, dims)
+    outer_b = desc(b, kept) if b is not None else None
+    inner_b = desc(b, dims) if b is not None else None
+    _nat().z_reduce(_st(a.device), outer, inner, outer_b, inner_b, a.data_ptr(), _DT[a.dtype],
+                    b.data_ptr() if b is not None else 0, _DT[b.dtype] if b is not None else 0,
+                    shift.data_ptr() if shift is not None else 0, acc.data_ptr(),
+                    acc2.data_ptr() if acc2 is not None else 0, op)
+
+
+# ---------------------------------------------------------------------------- op impls
+_IMPL = {}
+
+
+def impl(*ops):
+    def deco(fn):
+        for o in ops:
+            _IMPL[o] = fn
+        return fn
+    return deco
+
+
+# ---- elementwise ---------------------------------------------------------------
+@impl(aten.add.Tensor, aten.sub.Tensor)
+def _add(func, self, other, alpha=1):
+    sign = -1.0 if func is aten.sub.Tensor else 1.0
+    s = _scalar(other)
+    if s is not None:
+        return ew(torch.empty_like(self), [self], EW_ADDS, sign * alpha * s)
+    out = _alloc_like_meta(func, (self, other), {"alpha": alpha}, self.device)
+    return ew(out, [self, other], EW_ADD, sign * alpha)
+
+
+@impl(aten.add_.Tensor, aten.sub_.Tensor)
+def _add_(func, self, other, alpha=1):
+    sign = -1.0 if func is aten.sub_.Tensor else 1.0
+    s = _scalar(other)
+    if s is not None:
+        return ew(self, [self], EW_ADDS, sign * alpha * s)
+    return ew(self, [self, other], EW_ADD, sign * alpha)
+
+
+@impl(aten.mul.Tensor)
+def _mul(func, self, other):
+    s = _scalar(other)
+    if s is not None:
+        return ew(torch.empty_like(self), [self], EW_MULS, s)
+    s = _scalar(self)
+    if s is not None:
+        return ew(torch.empty_like(other), [other], EW_MULS, s)
+    out = _alloc_like_meta(func, (self, other), {}, _dev(self, other))
+    return ew(out, [self, other], EW_MUL)
+
+
+@impl(aten.mul_.Tensor)
+def _mul_(func, self, other):
+    s = _scalar(other)
+    if s is not None:
+        return ew(self, [self], EW_MULS, s)
+    return ew(self, [self, other], EW_MUL)
+
+
+@impl(aten.mul.Scalar)
+def _mul_s(func, self, other):
+    return ew(torch.empty_like(self), [self], EW_MULS, float(other))
+
+
+@impl(aten.div.Scalar)
+def _div_s(func, self, other):
+    return ew(torch.empty_like(self), [self], EW_MULS, 1.0 / float(other))
+
+
+@impl(aten.div_.Scalar)
+def _div_s_(func, self, other):
+    return ew(self, [self], EW_MULS, 1.0 / float(other))
+
+
+@impl(aten.div.Tensor)
+def _div_t(func, self, other):
+    s = _scalar(other)
+    if s is not None:
+        return ew(torch.empty_like(self), [self], EW_MULS, 1.0 / s)
+    out = _alloc_like_meta(func, (self, other), {}, _dev(self, other))
+    return ew(out, [self, other], EW_DIV)
+
+
+@impl(aten.relu.default)
+def _relu(func, self):
+    return ew(torch.empty_like(self), [self], EW_RELU)
+
+
+@impl(aten.relu_.default)
+def _relu_(func, self):
+    return ew(self, [self], EW_RELU)
+
+
+@impl(aten.threshold_backward.default)
+def _thr_bwd(func, grad_output, self, threshold):
+    out = _alloc_like_meta(func, (grad_output, self, threshold), {}, grad_output.device)
+    return ew(out, [grad_output, self], EW_THR_BWD, float(threshold))
+
+
+@impl(aten.sigmoid.default)
+def _sigmoid(func, self):
+    return ew(torch.empty_like(self), [self], EW_SIGMOID)
+
+
+@impl(aten.sigmoid_backward.default)
+def _sigmoid_bwd(func, grad_output, output):
+    out = _alloc_like_meta(func, (grad_output, output), {}, grad_output.device)
+    return ew(out, [grad_output, output], EW_SIG_BWD)
+
+
+@impl(aten._to_copy.default)
+def _to_copy(func, self, **kw):
+    dev = kw.get("device")
+    if not self.is_cuda or (dev is not None and torch.device(dev).type != "cuda"):
+        return ATEN                                   # host copies stay ATen (not a device kernel)
+    mkw = {k: v for k, v in kw.items() if k not in ("device", "pin_memory", "non_blocking")}
+    out = _alloc_like_meta(func, (self,), mkw, self.device)
+    return ew(out, [self], EW_COPY)
+
+
+@impl(aten.clone.default)
+def _clone(func, self, memory_format=None):
+    out = _alloc_like_meta(func, (self,), {"memory_format": memory_format} if memory_format else {}, self.device)
+    return ew(out, [self], EW_COPY)
+
+
+@impl(aten.copy_.default)
+def _copy_(func, self, src, non_blocking=False):
+    if not (src.is_cuda and self.is_cuda):
+        return ATEN                                   # H2D / D2H transfer, not a compute kernel
+    return ew(self, [src], EW_COPY)
+
+
+@impl(aten.ones_like.default, aten.zeros_like.default)
+def _fill_like(func, self, **kw):
+    out = _alloc_like_meta(func, (self,), kw, self.device)
+    return fill_(out, 1.0 if func is aten.ones_like.default else 0.0)
+
+
+@impl(aten.fill_.Scalar)
+def _fill_s(func, self, value):
+    return fill_(self, float(value))
+
+
+@impl(aten.zero_.default)
+def _zero_(func, self):
+    return fill_(self, 0.0)
+
+
+# ---- concat / slicing -------------------------------------------------------------
+@impl(aten.cat.default)
+def _cat(func, tensors, dim=0):
+    tensors = [t for t in tensors if t.numel() > 0 or t.dim() > 1]
+    out = _alloc_like_meta(func, (tensors,), {"dim": dim}, _dev(tensors))
+    d = dim % out.dim()
+    off = 0
+    for t in tensors:
+        if t.numel():
+            ew(out.narrow(d, off, t.shape[d]), [t], EW_COPY)
+        off += t.shape[d] if t.dim() else 0
+    return out
+
+
+@impl(aten.slice_backward.default)
+def _slice_bwd(func, grad_output, input_sizes, dim, start, end, step):
+    out = _alloc_like_meta(func, (grad_output, input_sizes, dim, start, end, step), {}, grad_output.device)
+    fill_(out, 0.0)
+    ew(out.slice(dim, start, end, step), [grad_output], EW_COPY)
+    return out
+
+
+# ---- reductions ----------------------------------------------------------------
+def _sum_like(func, self, dim, keepdim, dtype, scale_by_count: bool):
+    dims = list(range(self.dim())) if dim is None or len(dim) == 0 else [d % self.dim() for d in dim]
+    kw = {"keepdim": keepdim}
+    if dtype is not None:
+        kw["dtype"] = dtype
+    out = _alloc_like_meta(func, (self, dim), kw, self.device)
+    acc = torch.empty(out.shape, dtype=torch.float32, device=self.device)
+    fill_(acc, 0.0)
+    reduce_sum(self, dims, acc)
+    cnt = 1
+    for d in dims:
+        cnt *= self.shape[d]
+    if scale_by_count:
+        return ew(out, [acc], EW_MULS, 1.0 / max(cnt, 1))
+    return ew(out, [acc], EW_COPY)
+
+
+@impl(aten.sum.dim_IntList)
+def _sum(func, self, dim, keepdim=False, dtype=None):
+    return _sum_like(func, self, dim, keepdim, dtype, False)
+
+
+@impl(aten.mean.dim)
+def _mean(func, self, dim, keepdim=False, dtype=None):
+    return _sum_like(func, self, dim, keepdim, dtype, True)
+
+
+@impl(aten.sum.default)
+def _sum_all(func, self, dtype=None):
+    out = torch.empty((), dtype=dtype or self.dtype, device=self.device)
+    acc = torch.empty((), dtype=torch.float32, device=self.device)
+    fill_(acc, 0.0)
+    reduce_sum(self, list(range(self.dim())), acc.view(1))
+    return ew(out, [acc], EW_COPY)
+
+
+# ---- BatchNorm -------------------------------------------------------------------
+@impl(aten.native_batch_norm.default)
+def _bn(func, input, weight, bias, running_mean, running_var, training, momentum, eps):
+    x = input
+    C = x.shape[1]
+    dev = x.device
+    M = x.numel() // C
+    f32 = dict(dtype=torch.float32, device=dev)
+    scale, shift_out = torch.empty(C, **f32), torch.empty(C, **f32)
+    nat = _nat()
+    if training:
+        acc = torch.empty(2 * C, **f32)
+        fill_(acc, 0.0)
+        dims = [0] + list(range(2, x.dim()))
+        # moments of (x - running_mean): no catastrophic cancellation in E[d^2] - E[d]^2
+        reduce_sum(x, dims, acc[:C], RD_SUMSQ_SHIFT, shift=running_mean, acc2=acc[C:])
+        save_mean, save_invstd = torch.empty(C, **f32), torch.empty(C, **f32)
+        p = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
+        nat.z_bn_fwd_coeffs(_st(dev), acc.data_ptr(), acc[C:].data_ptr(), p(running_mean), C, M, p(weight), p(bias),
+                            p(running_mean), p(running_var), float(eps), float(momentum if momentum is not None else 0.1),
+                            1, save_mean.data_ptr(), save_invstd.data_ptr(), scale.data_ptr(), shift_out.data_ptr())
+    else:
+        p = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
+        nat.z_bn_fwd_coeffs(_st(dev), 0, 0, 0, C, M, p(weight), p(bias), p(running_mean), p(running_var), float(eps),
+                            0.0, 0, 0, 0, scale.data_ptr(), shift_out.data_ptr())
+        save_mean = torch.empty(0, **f32)
+        save_invstd = torch.empty(0, **f32)
+    bshape = [1, C] + [1] * (x.dim() - 2)
+    out = torch.empty_like(x)
+    ew(out, [x, scale.view(bshape), shift_out.view(bshape)], EW_FMA)
+    return out, save_mean, save_invstd
+
+
+@impl(aten.native_batch_norm_backward.default)
+def _bn_bwd(func, grad_out, input, weight, running_mean, running_var, save_mean, save_invstd, train, eps,
+            output_mask):
+    if not train:
+        return None
+    x, g = input, grad_out
+    C = x.shape[1]
+    dev = x.device
+    M = x.numel() // C
+    f32 = dict(dtype=torch.float32, device=dev)
+    acc = torch.empty(2 * C, **f32)
+    fill_(acc, 0.0)
+    dims = [0] + list(range(2, x.dim()))
+    reduce_sum(g, dims, acc[:C], RD_DOT_SHIFT, b=x, shift=save_mean, acc2=acc[C:])
+    k, bb, cc = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(C, **f32)
+    gw = torch.empty(C, **f32) if output_mask[1] else None
+    gb = torch.empty(C, **f32) if output_mask[2] else None
+    p = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
+    _nat().z_bn_bwd_coeffs(_st(dev), acc.data_ptr(), acc[C:].data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(),
+                           p(weight), C, M, k.data_ptr(), bb.data_ptr(), cc.data_ptr(), p(gw), p(gb))
+    gi = None
+    if output_mask[0]:
+        bshape = [1, C] + [1] * (x.dim() - 2)
+        gi = torch.empty_like(x)
+        ew(gi, [g, k.view(bshape), x, bb.view(bshape), cc.view(bshape)], EW_BNB)
+    if gw is not None and weight is not None and gw.dtype != weight.dtype:
+        gw = ew(torch.empty_like(weight), [gw], EW_COPY)
+    return gi, gw, gb
+
+
+# ---- pooling ---------------------------------------------------------------------
+def _pair(v, default=None):
+    if v is None or (isinstance(v, (list, tuple)) and len(v) == 0):
+        return default
+    if isinstance(v, int):
+        return (v, v)
+    return (int(v[0]), int(v[1] if len(v) > 1 else v[0]))
+
+
+@impl(aten.avg_pool2d.default)
+def _avgpool(func, self, kernel_size, stride=(), padding=0, ceil_mode=False, count_include_pad=True,
+             divisor_override=None):
+    k = _pair(kernel_size)
+    s = _pair(stride, k)
+    p = _pair(padding)
+    out = _alloc_like_meta(func, (self, kernel_size, stride, padding, ceil_mode, count_include_pad, divisor_override),
+                           {}, self.device)
+    _nat().z_pool_fwd(_st(self.device), zd(self), zd(out), None, k[0], k[1], s[0], s[1], p[0], p[1],
+                      int(count_include_pad), int(divisor_override or 0), 0)
+    return out
+
+
+@impl(aten.avg_pool2d_backward.default)
+def _avgpool_bwd(func, grad_output, self, kernel_size, stride, padding, ceil_mode, count_include_pad,
+                 divisor_override):
+    k = _pair(kernel_size)
+    s = _pair(stride, k)
+    p = _pair(padding)
+    gi = torch.empty_like(self)
+    _nat().z_pool_bwd(_st(self.device), zd(gi), zd(grad_output), None, k[0], k[1], s[0], s[1], p[0], p[1],
+                      int(count_include_pad), int(divisor_override or 0), 0)
+    return gi
+
+
+@impl(aten.max_pool2d_with_indices.default)
+def _maxpool(func, self, kernel_size, stride=(), padding=0, dilation=1, ceil_mode=False):
+    if _pair(dilation) != (1, 1):
+        return None
+    k = _pair(kernel_size)
+    s = _pair(stride, k)
+    p = _pair(padding)
+    out, idx = _alloc_like_meta(func, (self, kernel_size, stride, padding, dilation, ceil_mode), {}, self.device)
+    _nat().z_pool_fwd(_st(self.device), zd(self), zd(out), zd(idx), k[0], k[1], s[0], s[1], p[0], p[1], 0, 0, 1)
+    return out, idx
+
+
+@impl(aten.max_pool2d_with_indices_backward.default)
+def _maxpool_bwd(func, grad_output, self, kernel_size, stride, padding, dilation, ceil_mode, indices):
+    k = _pair(kernel_size)
+    s = _pair(stride, k)
+    p = _pair(padding)
+    gi = torch.empty_like(self)
+    _nat().z_pool_bwd(_st(self.device), zd(gi), zd(grad_output), zd(indices), k[0], k[1], s[0], s[1], p[0], p[1], 0, 0,
+                      1)
+    return gi
+
+
+# ---- GEMM ---------------------------------------------------------------------------
+def _gemm_out_dtype(*ts):
+    return torch.float32 if any(t is not None and t.dtype == torch.float32 for t in ts) else ts[0].dtype
+
+
+@impl(aten.mm.default)
+def _mm(func, self, mat2):
+    out = torch.empty(self.shape[0], mat2.shape[1], dtype=_gemm_out_dtype(self, mat2), device=self.device)
+    _nat().z_gemm(_st(self.device), zd(self), zd(mat2), zd(out), None, 1.0, 0.0)
+    return out
+
+
+@impl(aten.addmm.default)
+def _addmm(func, bias, mat1, mat2, beta=1, alpha=1):
+    out = torch.empty(mat1.shape[0], mat2.shape[1], dtype=_gemm_out_dtype(mat1, mat2, bias), device=mat1.device)
+    _nat().z_gemm(_st(mat1.device), zd(mat1), zd(mat2), zd(out), zd(bias), float(alpha), float(beta))
+    return out
+
+
+# ---- log-softmax / NLL --------------------------------------------------------------
+@impl(aten._log_softmax.default)
+def _log_softmax(func, self, dim, half_to_float):
+    if self.dim() != 2 or dim % 2 != 1:
+        return None
+    out = _alloc_like_meta(func, (self, dim, half_to_float), {}, self.device)
+    _nat().z_log_softmax(_st(self.device), zd(self), zd(out), 0, None)
+    return out
+
+
+@impl(aten._log_softmax_backward_data.default)
+def _log_softmax_bwd(func, grad_output, output, dim, input_dtype):
+    if output.dim() != 2 or dim % 2 != 1:
+        return None
+    out = torch.empty(output.shape, dtype=input_dtype, device=output.device)
+    _nat().z_log_softmax(_st(output.device), zd(output), zd(out), 1, zd(grad_output))
+    return out
+
+
+@impl(aten.nll_loss_forward.default)
+def _nll_fwd(func, self, target, weight, reduction, ignore_index):
+    if weight is not None or self.dim() != 2 or reduction not in (1, 2):
+        return None
+    out = torch.empty((), dtype=self.dtype, device=self.device)
+    tw = torch.empty((), dtype=self.dtype, device=self.device)
+    _nat().z_nll_fwd(_st(self.device), zd(self), target.data_ptr(), target.stride(0), int(ignore_index),
+                     int(reduction == 1), out.data_ptr(), int(out.dtype == torch.bfloat16), tw.data_ptr(),
+                     int(tw.dtype == torch.bfloat16))
+    return out, tw
+
+
+@impl(aten.nll_loss_backward.default)
+def _nll_bwd(func, grad_output, self, target, weight, reduction, ignore_index, total_weight):
+    if weight is not None or self.dim() != 2 or reduction not in (1, 2):
+        return None
+    gx = torch.empty_like(self)
+    _nat().z_nll_bwd(_st(self.device), zd(gx), grad_output.data_ptr(), int(grad_output.dtype == torch.bfloat16),
+                     total_weight.data_ptr(), int(total_weight.dtype == torch.bfloat16), target.data_ptr(),
+                     target.stride(0), int(ignore_index), int(reduction == 1))
+    return gx
+
+
+# ---- RNG (dropout / drop-connect) -----------------------------------------------------
+@impl(aten.bernoulli_.float)
+def _bernoulli_(func, self, p=0.5, generator=None):
+    mode = NativeMode.current
+    ew(self, [], EW_BERN, float(p), seed=mode.seed, ctr=mode.rng_ctr(self.device))
+    _nat().z_ctr_bump(_st(self.device), mode.rng_ctr(self.device).data_ptr())
+    return self
+
+
+@impl(aten.native_dropout.default)
+def _native_dropout(func, input, p, train):
+    mask = torch.empty_like(input)
+    if not train or p == 0:
+        fill_(mask, 1.0)
+        return ew(torch.empty_like(input), [input], EW_COPY), mask
+    # the mask is kept in the input's dtype (0 / 1): only native_dropout_backward below reads it
+    _bernoulli_(None, mask, 1.0 - float(p))
+    out = ew(torch.empty_like(input), [input, mask], EW_MUL)
+    return ew(out, [out], EW_MULS, 1.0 / (1.0 - float(p))), mask
+
+
+@impl(aten.native_dropout_backward.default)
+def _native_dropout_bwd(func, grad_output, mask, scale):
+    out = ew(torch.empty_like(grad_output), [grad_output, mask], EW_MUL)
+    return ew(out, [out], EW_MULS, float(scale))
+
+
+# ---- convolution ----------------------------------------------------------------------
+def _cl_bf16(x: torch.Tensor) -> torch.Tensor:
+    """channels-last contiguous bf16 (NCHW-shaped) -- a no-op for the engine's activations."""
+    if x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last):
+        return x
+    out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device).contiguous(memory_format=torch.channels_last)
+    return ew(out, [x], EW_COPY)
+
+
+def _conv_kind(C, O, groups, k, stride, pad, dil):
+    square = k[0] == k[1] and stride[0] == stride[1] and pad[0] == pad[1]
+    if dil != (1, 1) or not square or stride[0] not in (1, 2) or k[0] > 7:
+        return "gconv"
+    if groups == 1 and C % 8 == 0 and O % 8 == 0:
+        return "mfma"
+    if groups == C == O and C % 8 == 0 and C <= 2048 and k[0] in (3, 5, 7) and C * k[0] * k[0] * 4 <= 128 * 1024:
+        return "dw"
+    if 1 < groups <= 8 and C % (8 * groups) == 0 and O % (8 * groups) == 0:
+        return "grouped_mfma"
+    return "gconv"
+
+
+def _nchw(t_nhwc: torch.Tensor) -> torch.Tensor:
+    return t_nhwc.permute(0, 3, 1, 2)
+
+
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    return t.permute(0, 2, 3, 1)
+
+
+def _ws(dev, floats):
+    return CV.wgrad_workspace(dev, floats) if floats > 0 else None
+
+
+@impl(aten.convolution.default)
+def _conv(func, input, weight, bias, stride, padding, dilation, transposed, output_padding, groups):
+    if transposed or input.dim() != 4:
+        return None
+    k = tuple(weight.shape[2:])
+    st, pd, dl = _pair(stride), _pair(padding), _pair(dilation)
+    N, C, H, W = input.shape
+    O = weight.shape[0]
+    kind = _conv_kind(C, O, groups, k, st, pd, dl)
+    dev = input.device
+    w32 = weight if weight.dtype == torch.float32 else ew(torch.empty(weight.shape, device=dev), [weight], EW_COPY)
+    if kind in ("mfma", "dw", "grouped_mfma"):
+        xh = _nhwc(_cl_bf16(input))
+        if kind == "mfma":
+            wp = CV.pack_weight(w32.contiguous())
+            y = CV.conv2d_fwd(xh, wp, st[0], pd[0], ws=_ws(dev, CV.fd_ws_floats(xh.shape, O, k[0], k[1], st[0], pd[0])))
+        elif kind == "dw":
+            y = CV.dwconv_fwd(xh, w32.contiguous(), st[0], pd[0])
+        else:
+            P = (H + 2 * pd[0] - k[0]) // st[0] + 1
+            Q = (W + 2 * pd[1] - k[1]) // st[1] + 1
+            y = torch.empty(N, P, Q, O, dtype=torch.bfloat16, device=dev)
+            Cg, Og = C // groups, O // groups
+            for g in range(groups):
+                xg = ew(torch.empty(N, H, W, Cg, dtype=torch.bfloat16, device=dev), [xh[..., g * Cg:(g + 1) * Cg]],
+                        EW_COPY)
+                wp = CV.pack_weight(w32[g * Og:(g + 1) * Og].contiguous())
+                yg = CV.conv2d_fwd(xg, wp, st[0], pd[0], ws=_ws(dev, CV.fd_ws_floats(xg.shape, Og, k[0], k[1], st[0],
+                                                                                     pd[0])))
+                ew(y[..., g * Og:(g + 1) * Og], [yg], EW_COPY)
+        out = _nchw(y)
+    else:
+        P = (H + 2 * pd[0] - dl[0] * (k[0] - 1) - 1) // st[0] + 1
+        Q = (W + 2 * pd[1] - dl[1] * (k[1] - 1) - 1) // st[1] + 1
+        if dl != (1, 1):
+            return None
+        out = torch.empty(N, O, P, Q, dtype=torch.bfloat16, device=dev).contiguous(memory_format=torch.channels_last)
+        _nat().z_gconv(_st(dev), 0, zd(input), zd(w32), zd(out), int(groups), st[0], st[1], pd[0], pd[1])
+    if bias is not None:
+        ew(out, [out, bias.view(1, O, 1, 1)], EW_ADD, 1.0)
+    return out
+
+
+@impl(aten.convolution_backward.default)
+def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dilation, transposed, output_padding,
+              groups, output_mask):
+    if transposed or input.dim() != 4:
+        return None
+    k = tuple(weight.shape[2:])
+    st, pd, dl = _pair(stride), _pair(padding), _pair(dilation)
+    N, C, H, W = input.shape
+    O = weight.shape[0]
+    kind = _conv_kind(C, O, groups, k, st, pd, dl)
+    dev = input.device
+    w32 = weight if weight.dtype == torch.float32 else ew(torch.empty(weight.shape, device=dev), [weight], EW_COPY)
+    gi = gw = gb = None
+    if kind in ("mfma", "dw", "grouped_mfma"):
+        xh = _nhwc(_cl_bf16(input))
+        gy = _nhwc(_cl_bf16(grad_output))
+        if kind == "mfma":
+            if output_mask[0]:
+                wp = CV.pack_weight(w32.contiguous())
+                wd = None
+                if CV.dgrad_eligible(O):
+                    wd = torch.empty(CV.dgrad_image_numel(w32.shape, C), dtype=torch.bfloat16, device=dev)
+                    CV.dgrad_pack_weights([(w32.contiguous(), wd, st[0], pd[0], C)])
+                gi = _nchw(CV.conv2d_dgrad(gy, wp, xh.shape, st[0], pd[0], wd=wd,
+                                           ws=_ws(dev, CV.fd_ws_floats(xh.shape, O, k[0], k[1], st[0], pd[0]))))
+            if output_mask[1]:
+                gw = CV.conv2d_wgrad(xh, gy, k[0], k[1], st[0], pd[0])
+        elif kind == "dw":
+            if output_mask[0]:
+                gi = _nchw(CV.dwconv_dgrad(gy, w32.contiguous(), xh.shape, st[0], pd[0]))
+            if output_mask[1]:
+                gw = CV.dwconv_wgrad(xh, gy, k[0], st[0], pd[0])
+        else:
+            Cg, Og = C // groups, O // groups
+            gih = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dev) if output_mask[0] else None
+            gw = torch.empty(O, Cg, k[0], k[1], dtype=torch.float32, device=dev) if output_mask[1] else None
+            for g in range(groups):
+                xg = ew(torch.empty(N, H, W, Cg, dtype=torch.bfloat16, device=dev), [xh[..., g * Cg:(g + 1) * Cg]],
+                        EW_COPY)
+                gyg = ew(torch.empty(gy.shape[:3] + (Og,), dtype=torch.bfloat16, device=dev),
+                         [gy[..., g * Og:(g + 1) * Og]], EW_COPY)
+                if gih is not None:
+                    wp = CV.pack_weight(w32[g * Og:(g + 1) * Og].contiguous())
+                    dxg = CV.conv2d_dgrad(gyg, wp, xg.shape, st[0], pd[0],
+                                          ws=_ws(dev, CV.fd_ws_floats(xg.shape, Og, k[0], k[1], st[0], pd[0])))
+                    ew(gih[..., g * Cg:(g + 1) * Cg], [dxg], EW_COPY)
+                if gw is not None:
+                    CV.conv2d_wgrad(xg, gyg, k[0], k[1], st[0], pd[0], out=gw[g * Og:(g + 1) * Og])
+            gi = _nchw(gih) if gih is not None else None
+        if gi is not None and input.dtype != torch.bfloat16:
+            gi = ew(torch.empty_like(input), [gi], EW_COPY)
+    else:
+        if dl != (1, 1):
+            return None
+        if output_mask[0]:
+            gi = torch.empty_like(input)
+            _nat().z_gconv(_st(dev), 1, zd(gi), zd(w32), zd(grad_output), int(groups), st[0], st[1], pd[0], pd[1])
+        if output_mask[1]:
+            gw = torch.empty(w32.shape, dtype=torch.float32, device=dev)
+            _nat().z_gconv(_st(dev), 2, zd(input), zd(gw), zd(grad_output), int(groups), st[0], st[1], pd[0], pd[1])
+    if gw is not None and gw.dtype != weight.dtype:
+        gw = ew(torch.empty_like(weight), [gw], EW_COPY)
+    if output_mask[2]:
+        gb = torch.empty(O, dtype=weight.dtype, device=dev)
+        acc = torch.empty(O, dtype=torch.float32, device=dev)
+        fill_(acc, 0.0)
+        reduce_sum(grad_output, [0, 2, 3], acc)
+        ew(gb, [acc], EW_COPY)
+    return gi, gw, gb
+
+
+# ---------------------------------------------------------------------------- the mode
+def _ops(*names):
+    out = set()
+    for n in names:
+        pkt, _, ov = n.partition(".")
+        op = getattr(getattr(aten, pkt, None), ov or "default", None)
+        if op is not None:
+            out.add(op)
+    return out
+
+
+_PASSTHROUGH = _ops(
+    "view", "_unsafe_view", "expand", "t", "transpose.int", "permute", "slice.Tensor", "select.int", "detach",
+    "alias", "unsqueeze", "squeeze.dim", "squeeze", "squeeze.dims", "as_strided", "split.Tensor",
+    "split_with_sizes", "chunk", "unbind.int", "empty.memory_format", "empty_like", "empty_strided", "new_empty",
+    "new_empty_strided", "reshape", "flatten.using_ints", "_reshape_alias", "lift_fresh", "narrow", "unflatten.int",
+    "_local_scalar_dense", "is_same_size", "view.dtype", "set_.source_Storage_storage_offset",
+)
+
+
+class NativeMode(TorchDispatchMode):
+    """Route a training step's aten ops to fedmi's HIP kernels (see module docstring)."""
+
+    current: "NativeMode" = None
+
+    def __init__(self, strict: bool = False, seed: int = 0):
+        super().__init__()
+        self.strict = strict
+        self.seed = seed
+        self.fallbacks = collections.Counter()
+        self.native_ops = collections.Counter()
+        self._ctr = {}
+
+    def rng_ctr(self, dev) -> torch.Tensor:
+        dev = torch.device(dev)
+        if dev not in self._ctr:
+            self._ctr[dev] = torch.zeros(4, dtype=torch.int32, device=dev)
+        return self._ctr[dev]
+
+    def __enter__(self):
+        self._prev = NativeMode.current
+        NativeMode.current = self
+        return super().__enter__()
+
+    def __exit__(self, *exc):
+        NativeMode.current = self._prev
+        return super().__exit__(*exc)
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func in _PASSTHROUGH:
+            return func(*args, **kwargs)
+        fn = _IMPL.get(func)
+        on_gpu = _dev(args, tuple(kwargs.values())) is not None
+        if fn is not None and on_gpu:
+            out = fn(func, *args, **kwargs)
+            if out is ATEN:
+                return func(*args, **kwargs)
+            if out is not None:
+                self.native_ops[str(func)] += 1
+                return out
+        if on_gpu:
+            self.fallbacks[str(func)] += 1
+            if self.strict:
+                raise RuntimeError(f"native_mode: no native kernel for {func}")
+        return func(*args, **kwargs)
+
+
+def ce_stats_(logits: torch.Tensor, labels: torch.Tensor, stats: torch.Tensor) -> None:
+    """stats (fp32 [3]) += (cross-entropy sum, correct, count) of a classifier batch (one native launch)."""
+    y = labels if labels.dtype == torch.int64 else labels.long()
+    _nat().z_ce_stats(_st(logits.device), zd(logits), y.data_ptr(), stats.data_ptr())
+
+
+__all__ = ["NativeMode", "ce_stats_", "ew", "fill_", "reduce_sum", "zd"]

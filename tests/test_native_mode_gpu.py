@@ -1,0 +1,288 @@
+"""The native aten backend (fedmi/ops/native_mode.py, csrc/kernels/zoo_ops.hip) vs PyTorch fp32.
+
+Per op: forward outputs and autograd gradients of each native implementation against the same
+op in fp32 PyTorch (operands rounded to bf16 first, so the comparison isolates accumulation
+error).  Per family: a training step of every zoo family without a whole-network engine runs
+under the mode in strict mode (any aten op without a native kernel raises) and tracks the fp32
+engine's loss; the HIP-graph replay of the step matches eager execution.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from fedmi.engine.base import TrainerConfig
+from fedmi.engine.data import contiguous_schedule, make_dataset
+from fedmi.models import build_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6))
+
+
+def _mode(**kw):
+    from fedmi.ops.native_mode import NativeMode
+
+    return NativeMode(strict=True, **kw)
+
+
+def _bf(t):
+    return t.bfloat16().float()
+
+
+def _run_pair(gpu_device, make, x_shape, seed=0, cl=True, tol=1e-2, gy_dtype=torch.bfloat16):
+    """ref: fp32 module on fp32 input; nat: same weights, bf16 channels-last input, under the mode."""
+    torch.manual_seed(seed)
+    ref = make().to(gpu_device)
+    nat = make().to(gpu_device)
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_(_bf(p))
+    nat.load_state_dict(ref.state_dict())
+    x = _bf(torch.randn(*x_shape, device=gpu_device))
+    xr = x.clone().requires_grad_(True)
+    xn = x.clone()
+    if cl and xn.dim() == 4:
+        xn = xn.contiguous(memory_format=torch.channels_last)
+    xn = xn.to(torch.bfloat16).requires_grad_(True)
+    yr = ref(xr)
+    mode = _mode()
+    with mode:
+        yn = nat(xn)
+    gy = _bf(torch.randn_like(yr))
+    yr.backward(gy)
+    with mode:
+        yn.backward(gy.to(yn.dtype))
+    torch.cuda.synchronize()
+    assert not mode.fallbacks, dict(mode.fallbacks)
+    assert yn.shape == yr.shape
+    assert _rel(yn, yr) < tol, ("y", _rel(yn, yr))
+    assert _rel(xn.grad, xr.grad) < tol, ("dx", _rel(xn.grad, xr.grad))
+    for (n, pr), pn in zip(ref.named_parameters(), nat.parameters()):
+        assert pn.grad is not None, n
+        assert _rel(pn.grad, pr.grad) < tol, (n, _rel(pn.grad, pr.grad))
+    for (n, br), bn in zip(ref.named_buffers(), nat.buffers()):
+        if br.is_floating_point():
+            assert _rel(bn, br) < 1e-3, (n, _rel(bn, br))
+    return mode
+
+
+# (N, H, C, O, k, stride, pad, groups, bias): MFMA dense (DenseNet 1x1 C % 64 != 0, strided 3x3 / 1x1
+# shortcuts, 5x5 / 7x7), depthwise, grouped MFMA (ResNeXt 2x64d), VALU grouped (ResNeXt 32x4d, DPN,
+# RegNet, ShuffleNet g3 widths), the 3-channel stem, a biased conv
+CONVS = [(8, 16, 24, 48, 1, 1, 0, 1, False), (8, 16, 48, 16, 3, 1, 1, 1, False), (4, 16, 64, 128, 3, 2, 1, 1, False),
+         (4, 16, 64, 128, 1, 2, 0, 1, True), (2, 16, 32, 64, 5, 1, 2, 1, False), (2, 16, 16, 32, 7, 2, 3, 1, False),
+         (8, 16, 32, 32, 3, 1, 1, 32, False), (4, 16, 64, 64, 5, 2, 2, 64, False), (4, 16, 128, 128, 3, 1, 1, 2, False),
+         (4, 8, 128, 128, 3, 2, 1, 32, False), (4, 8, 96, 96, 3, 1, 1, 3, False), (4, 8, 60, 60, 1, 1, 0, 3, False),
+         (4, 16, 3, 64, 3, 1, 1, 1, False), (4, 16, 58, 58, 1, 1, 0, 1, True)]
+
+
+@pytest.mark.parametrize("shape", CONVS, ids=[str(s) for s in CONVS])
+def test_conv_fwd_bwd(gpu_device, shape):
+    N, H, C, O, k, st, pad, g, bias = shape
+    _run_pair(gpu_device, lambda: nn.Conv2d(C, O, k, st, pad, groups=g, bias=bias), (N, C, H, H))
+
+
+def test_batchnorm_train_eval(gpu_device):
+    def make():
+        return nn.Sequential(nn.BatchNorm2d(48), nn.ReLU())
+    mode = _run_pair(gpu_device, make, (16, 48, 8, 8))
+    assert mode.native_ops["aten.native_batch_norm.default"] == 1
+    # eval: running statistics path
+    torch.manual_seed(3)
+    ref = nn.BatchNorm2d(16).to(gpu_device)
+    with torch.no_grad():
+        ref.running_mean.uniform_(-1, 1)
+        ref.running_var.uniform_(0.5, 2)
+        ref.weight.uniform_(0.5, 1.5)
+    ref.eval()
+    x = _bf(torch.randn(8, 16, 6, 6, device=gpu_device))
+    with _mode():
+        yn = ref(x.contiguous(memory_format=torch.channels_last).bfloat16())
+    assert _rel(yn, ref(x)) < 1e-2
+
+
+def test_batchnorm_large_mean(gpu_device):
+    """Moments are taken about the running mean: a channel whose mean dwarfs its spread keeps its
+    variance (E[x^2] - E[x]^2 in fp32 would cancel)."""
+    bn = nn.BatchNorm2d(8).to(gpu_device)
+    with torch.no_grad():
+        bn.running_mean.fill_(100.0)
+    x = 100.0 + torch.randn(32, 8, 8, 8, device=gpu_device)
+    ref = nn.BatchNorm2d(8).to(gpu_device)
+    with torch.no_grad():
+        ref.running_mean.fill_(100.0)
+    yr = ref(x)
+    with _mode():
+        yn = bn(x)
+    assert _rel(yn, yr) < 1e-3
+    assert _rel(bn.running_var, ref.running_var) < 1e-3
+
+
+class _SE(nn.Module):
+    """SE gate + residual add + concat + slice: the mul / sigmoid / mean / cat / slice_backward ops."""
+
+    def __init__(self, c=32):
+        super().__init__()
+        self.fc1 = nn.Conv2d(c, c // 4, 1)
+        self.fc2 = nn.Conv2d(c // 4, c, 1)
+
+    def forward(self, x):
+        w = F.adaptive_avg_pool2d(x.float(), 1).to(x.dtype)
+        w = torch.sigmoid(self.fc2(F.relu(self.fc1(w))))
+        y = x * w + x
+        z = torch.cat([y, x[:, : x.shape[1] // 2]], 1)
+        return z[:, 8:] * 0.5
+
+
+def test_se_concat_slice(gpu_device):
+    _run_pair(gpu_device, _SE, (8, 32, 8, 8))
+
+
+@pytest.mark.parametrize("pool", ["max3s2p1", "max2", "avg2", "avg3s1p1", "avg3s2p1_ceil_nopad", "avg4"])
+def test_pools(gpu_device, pool):
+    mk = {"max3s2p1": lambda: nn.MaxPool2d(3, 2, 1), "max2": lambda: nn.MaxPool2d(2),
+          "avg2": lambda: nn.AvgPool2d(2), "avg3s1p1": lambda: nn.AvgPool2d(3, 1, 1),
+          "avg3s2p1_ceil_nopad": lambda: nn.AvgPool2d(3, 2, 1, ceil_mode=True, count_include_pad=False),
+          "avg4": lambda: nn.AvgPool2d(4)}[pool]
+    _run_pair(gpu_device, mk, (4, 16, 9, 9) if "ceil" in pool else (4, 16, 8, 8))
+
+
+def test_linear_cross_entropy(gpu_device):
+    torch.manual_seed(0)
+    lin = nn.Linear(64, 10).to(gpu_device)
+    ref = nn.Linear(64, 10).to(gpu_device)
+    ref.load_state_dict(lin.state_dict())
+    x = _bf(torch.randn(32, 64, device=gpu_device))
+    y = torch.randint(0, 10, (32,), device=gpu_device)
+    xr = x.clone().requires_grad_(True)
+    lr_ = F.cross_entropy(ref(xr), y)
+    lr_.backward()
+    xn = x.bfloat16().requires_grad_(True)
+    mode = _mode()
+    with mode:
+        ln = F.cross_entropy(lin(xn), y)
+        ln.backward()
+    assert not mode.fallbacks
+    assert abs(float(ln) - float(lr_)) < 1e-3 * max(1.0, abs(float(lr_)))
+    assert _rel(xn.grad, xr.grad) < 1e-2
+    assert _rel(lin.weight.grad, ref.weight.grad) < 1e-3
+    assert _rel(lin.bias.grad, ref.bias.grad) < 1e-3
+
+
+def test_ce_stats(gpu_device):
+    from fedmi.ops.native_mode import ce_stats_
+
+    torch.manual_seed(0)
+    logits = torch.randn(300, 10, device=gpu_device)
+    y = torch.randint(0, 10, (300,), device=gpu_device)
+    st = torch.zeros(3, device=gpu_device)
+    ce_stats_(logits, y, st)
+    ce_stats_(logits.bfloat16(), y, st)
+    ref_l = F.cross_entropy(logits, y, reduction="sum") + F.cross_entropy(logits.bfloat16().float(), y, reduction="sum")
+    ref_c = (logits.argmax(1) == y).sum() + (logits.bfloat16().float().argmax(1) == y).sum()
+    assert abs(float(st[0]) - float(ref_l)) < 1e-3 * float(ref_l)
+    assert int(st[1]) == int(ref_c) and int(st[2]) == 600
+
+
+def test_dropout_and_drop_connect(gpu_device):
+    x = torch.ones(64, 256, device=gpu_device, requires_grad=True)
+    mode = _mode(seed=5)
+    with mode:
+        y = F.dropout(x, p=0.25, training=True)
+        y.sum().backward()
+        m = torch.empty(4096, 1, 1, 1, device=gpu_device).bernoulli_(0.8)
+        m2 = torch.empty(4096, 1, 1, 1, device=gpu_device).bernoulli_(0.8)
+    torch.cuda.synchronize()
+    kept = (y != 0).float().mean().item()
+    assert abs(kept - 0.75) < 0.02
+    assert torch.allclose(y[y != 0], torch.full_like(y[y != 0], 1 / 0.75))
+    assert torch.equal(x.grad, (y != 0).float() / 0.75)      # backward reuses the forward mask
+    assert abs(m.mean().item() - 0.8) < 0.03
+    assert not torch.equal(m, m2)                             # the device counter advanced
+    assert not mode.fallbacks
+
+
+HYBRID = ["densenet_cifar", "ResNeXt29_2x64d", "ResNeXt29_32x4d", "DPN26", "ShuffleNetG2", "ShuffleNetG3",
+          "ShuffleNetV2", "SENet18", "EfficientNetB0", "RegNetX_200MF", "RegNetY_400MF", "PNASNetA", "PNASNetB",
+          "DLA", "SimpleDLA", "MLP"]
+
+
+@pytest.mark.parametrize("name", HYBRID)
+def test_family_step_native_only(gpu_device, name):
+    """One SGD step of each family under the strict mode: no ATen compute op, loss matches fp32."""
+    from fedmi.engine import build_trainer
+    from fedmi.engine.torch_engine import TorchTrainer
+
+    data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=256, n_test=64, seed=0)
+    cfg = TrainerConfig(batch_size=64, lr=0.02, seed=7, augment=False)
+    init = build_model(name).state_dict()
+    tr = build_trainer(name, data, gpu_device, cfg, init_state=init)
+    assert isinstance(tr, TorchTrainer) and tr.hybrid and tr.mode is not None
+    tr.mode.strict = True
+    ref = TorchTrainer(name, data, gpu_device, cfg, init_state=init)
+    losses = {}
+    for kind, t in (("native", tr), ("fp32", ref)):
+        t.set_schedule([0, 64], [64, 64])
+        t.train_epoch()
+        losses[kind] = t.train_stats().loss
+        t.evaluate()
+        assert t.eval_stats().count == 64
+    assert not tr.mode.fallbacks, dict(tr.mode.fallbacks)
+    assert math.isfinite(losses["native"])
+    assert abs(losses["native"] - losses["fp32"]) < 0.05 * losses["fp32"] + 0.02, losses
+
+
+@pytest.mark.parametrize("name", ["densenet_cifar", "SENet18", "DPN26", "EfficientNetB0", "RegNetY_400MF"])
+def test_family_trains_like_fp32(gpu_device, name):
+    """Three short epochs, graph-replayed: the trajectory tracks the fp32 engine (round 1's hybrid
+    EfficientNet / RegNetY went NaN under replay)."""
+    from fedmi.engine import build_trainer
+    from fedmi.engine.torch_engine import TorchTrainer
+
+    data = make_dataset("synthetic-cifar10-easy", device=gpu_device, n_train=1280, n_test=500, seed=0)
+    cfg = TrainerConfig(batch_size=128, lr=0.02, seed=7)
+    init = build_model(name).state_dict()
+    res = {}
+    for kind in ("native", "fp32"):
+        tr = (build_trainer(name, data, gpu_device, cfg, init_state=init) if kind == "native"
+              else TorchTrainer(name, data, gpu_device, cfg, init_state=init))
+        if kind == "native":
+            assert tr.use_graph
+        tr.set_schedule(*contiguous_schedule(len(data.train), 128))
+        losses = []
+        for _ in range(3):
+            tr.train_epoch()
+            losses.append(tr.train_stats().loss)
+        tr.evaluate()
+        res[kind] = (losses, tr.eval_stats())
+        if kind == "native":
+            assert tr._graph is not None and not tr.mode.fallbacks
+    (lh, eh), (lf, ef) = res["native"], res["fp32"]
+    assert all(math.isfinite(v) for v in lh), lh
+    assert abs(lh[0] - lf[0]) < 0.1 * lf[0], (lh, lf)
+    assert lh[-1] < lh[0], (lh, lf)
+    assert lh[-1] < 1.5 * lf[-1] + 0.1, (lh, lf)
+    assert eh.count == ef.count == 500 and eh.loss == eh.loss
+
+
+def test_graph_replay_matches_eager(gpu_device):
+    from fedmi.engine import build_trainer
+
+    data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=640, n_test=64, seed=0)
+    cfg = TrainerConfig(batch_size=128, lr=0.02, seed=7, augment=False)
+    init = build_model("SimpleDLA").state_dict()
+    out = {}
+    for graph in (False, True):
+        tr = build_trainer("SimpleDLA", data, gpu_device, cfg, init_state=init)
+        tr.use_graph = graph
+        tr.set_schedule(*contiguous_schedule(640, 128))
+        tr.train_epoch()
+        tr.train_epoch()
+        out[graph] = (tr.train_stats().loss, tr.float_state().clone())
+    assert abs(out[True][0] - out[False][0]) < 1e-3 * out[False][0]
+    assert _rel(out[True][1], out[False][1]) < 1e-3

@@ -10,7 +10,7 @@ import torch  # noqa: E402
 
 from fedmi.models import build_model  # noqa: E402
 from fedmi.ops import conv as C  # noqa: E402
-from fedmi.ops import native_layers as nl  # noqa: E402
+from fedmi.ops import native_mode as nm  # noqa: E402
 
 dev = torch.device("cuda", 0)
 for name in sys.argv[1:]:
@@ -18,7 +18,10 @@ for name in sys.argv[1:]:
     shapes = set()
     hooks = [mm.register_forward_hook(lambda mod, i, o: shapes.add(
         (tuple(i[0].shape[1:]), mod.out_channels, mod.kernel_size[0], mod.stride[0], mod.padding[0]))
-        if nl.conv_eligible(mod) else None) for mm in m.modules()]
+        if isinstance(mod, torch.nn.Conv2d) and nm._conv_kind(mod.in_channels, mod.out_channels, mod.groups,
+                                                                mod.kernel_size, mod.stride, mod.padding,
+                                                                mod.dilation) == "mfma" else None)
+        for mm in m.modules()]
     m(torch.randn(2, 3, 32, 32))
     for (c, h, w), O, k, st, pad in sorted(shapes):
         x = torch.randn(128, h, w, c, device=dev).bfloat16()
