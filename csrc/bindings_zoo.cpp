@@ -20,8 +20,11 @@ struct ZTensor {
   long long size[ZMAXD];
   long long stride[ZMAXD];
 };
-void launch_ew(hipStream_t, const ZTensor&, const ZTensor*, int, int, float, float, uint32_t, const int*);
+void launch_ew(hipStream_t, const ZTensor&, const ZTensor*, int, int, float, float, uint32_t, const int*, int);
 void launch_ctr_bump(hipStream_t, int*);
+long long reduce_rows_ws_floats(long long, int);
+void launch_reduce_rows(hipStream_t, const void*, int, long long, const void*, int, long long, const float*, int,
+                        long long, int, float*, long long, float*, float*);
 void launch_reduce(hipStream_t, const ZTensor&, const ZTensor&, const ZTensor&, const ZTensor&, const void*, int,
                    const void*, int, const float*, float*, float*, int);
 void launch_bn_fwd_coeffs(hipStream_t, const float*, const float*, const float*, int, long long, const float*,
@@ -38,7 +41,9 @@ void launch_nll_fwd(hipStream_t, const ZTensor&, const long long*, long long, in
 void launch_nll_bwd(hipStream_t, const ZTensor&, const void*, int, const void*, int, const long long*, long long, int,
                     int);
 void launch_ce_stats(hipStream_t, const ZTensor&, const long long*, float*);
-void launch_gconv(hipStream_t, int, const ZTensor&, const ZTensor&, const ZTensor&, int, int, int, int, int);
+void launch_gconv(hipStream_t, int, const ZTensor&, const ZTensor&, const ZTensor&, int, int, int, int, int, float*,
+                  long long);
+long long gconv_wgrad_ws_floats(long long, long long, long long, long long);
 }  // namespace fedmi
 
 using fedmi::ZTensor;
@@ -65,12 +70,15 @@ static ZTensor zt(const py::object& o) {
 }
 
 void fedmi_bind_zoo(py::module_& m) {
+  // vmask < 0: scalar launch; otherwise the 8-wide vector launch (descriptors pre-divided by the caller)
   m.def("z_ew", [](uintptr_t st, py::object out, std::vector<py::object> ins, int op, float s0, float s1,
-                   uint32_t seed, uintptr_t ctr) {
+                   uint32_t seed, uintptr_t ctr, int vmask) {
     std::vector<ZTensor> v;
     for (auto& o : ins) v.push_back(zt(o));
-    fedmi::launch_ew(S(st), zt(out), v.data(), (int)v.size(), op, s0, s1, seed, reinterpret_cast<const int*>(ctr));
-  });
+    fedmi::launch_ew(S(st), zt(out), v.data(), (int)v.size(), op, s0, s1, seed, reinterpret_cast<const int*>(ctr),
+                     vmask);
+  }, py::arg("st"), py::arg("out"), py::arg("ins"), py::arg("op"), py::arg("s0"), py::arg("s1"), py::arg("seed"),
+        py::arg("ctr"), py::arg("vmask") = -1);
   m.def("z_ctr_bump", [](uintptr_t st, uintptr_t ctr) { fedmi::launch_ctr_bump(S(st), reinterpret_cast<int*>(ctr)); });
   m.def("z_reduce", [](uintptr_t st, py::object outer, py::object inner, py::object outer_b, py::object inner_b,
                        uintptr_t a, int a_dt, uintptr_t b, int b_dt, uintptr_t shift, uintptr_t acc, uintptr_t acc2,
@@ -78,6 +86,14 @@ void fedmi_bind_zoo(py::module_& m) {
     fedmi::launch_reduce(S(st), zt(outer), zt(inner), zt(outer_b), zt(inner_b), reinterpret_cast<const void*>(a), a_dt,
                          reinterpret_cast<const void*>(b), b_dt, reinterpret_cast<const float*>(shift),
                          reinterpret_cast<float*>(acc), reinterpret_cast<float*>(acc2), op);
+  });
+  m.def("z_reduce_rows_ws_floats", &fedmi::reduce_rows_ws_floats);
+  m.def("z_reduce_rows", [](uintptr_t st, uintptr_t a, int a_dt, long long lda, uintptr_t b, int b_dt, long long ldb,
+                            uintptr_t shift, int C, long long M, int op, uintptr_t part, long long part_floats,
+                            uintptr_t acc, uintptr_t acc2) {
+    fedmi::launch_reduce_rows(S(st), reinterpret_cast<const void*>(a), a_dt, lda, reinterpret_cast<const void*>(b), b_dt,
+                              ldb, reinterpret_cast<const float*>(shift), C, M, op, reinterpret_cast<float*>(part),
+                              part_floats, reinterpret_cast<float*>(acc), reinterpret_cast<float*>(acc2));
   });
   m.def("z_bn_fwd_coeffs", [](uintptr_t st, uintptr_t s1, uintptr_t s2, uintptr_t shift, int C, long long M, uintptr_t w,
                               uintptr_t b, uintptr_t rmean, uintptr_t rvar, float eps, float mom, int train,
@@ -119,7 +135,10 @@ void fedmi_bind_zoo(py::module_& m) {
     fedmi::launch_ce_stats(S(st), zt(logits), reinterpret_cast<const long long*>(y), reinterpret_cast<float*>(stats));
   });
   m.def("z_gconv", [](uintptr_t st, int mode, py::object x, py::object w, py::object y, int G, int sth, int stw,
-                      int padh, int padw) {
-    fedmi::launch_gconv(S(st), mode, zt(x), zt(w), zt(y), G, sth, stw, padh, padw);
-  });
+                      int padh, int padw, uintptr_t ws, long long ws_floats) {
+    fedmi::launch_gconv(S(st), mode, zt(x), zt(w), zt(y), G, sth, stw, padh, padw, reinterpret_cast<float*>(ws),
+                        ws_floats);
+  }, py::arg("st"), py::arg("mode"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("G"), py::arg("sth"),
+        py::arg("stw"), py::arg("padh"), py::arg("padw"), py::arg("ws") = 0, py::arg("ws_floats") = 0);
+  m.def("z_gconv_wgrad_ws_floats", &fedmi::gconv_wgrad_ws_floats);
 }

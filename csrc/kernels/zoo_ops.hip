@@ -70,15 +70,17 @@ struct EwArgs {
   int op;
   uint32_t seed;
   const int* ctr;    // EW_BERN: device step counter
+  int vmask;         // vector launch: bit k set = input k is contiguous over the 8-element group
 };
 
 // offset of linear element `i` of the output iteration space in tensor t
-// (32-bit index decode: the host guarantees every tensor has < 2^31 elements)
+// (32-bit index decode: the host guarantees every tensor has < 2^31 elements; the host also
+// coalesces dims, so activations + per-channel operands arrive as 1-2 dims: 0-1 divisions)
 FEDMI_DEV long long zoffset(const ZTensor& shape, const ZTensor& t, long long i64) {
   uint32_t i = (uint32_t)i64;
   long long off = 0;
 #pragma unroll
-  for (int d = ZMAXD - 1; d >= 0; --d) {
+  for (int d = ZMAXD - 1; d >= 1; --d) {
     if (d < shape.ndim) {
       const uint32_t sz = (uint32_t)shape.size[d];
       const uint32_t q = i / sz;
@@ -86,7 +88,78 @@ FEDMI_DEV long long zoffset(const ZTensor& shape, const ZTensor& t, long long i6
       i = q;
     }
   }
-  return off;
+  return off + (long long)i * t.stride[0];
+}
+
+FEDMI_DEV float ew_apply(const EwArgs& a, float x0, float x1, float x2, float x3, float x4) {
+  switch (a.op) {
+    case EW_COPY: return x0;
+    case EW_ADD: return x0 + a.s0 * x1;
+    case EW_SUB: return x0 - a.s0 * x1;
+    case EW_MUL: return x0 * x1;
+    case EW_DIV: return x0 / x1;
+    case EW_ADDS: return x0 + a.s0;
+    case EW_MULS: return x0 * a.s0;
+    case EW_RELU: return fmaxf(x0, 0.f);
+    case EW_THR_BWD: return x1 > a.s0 ? x0 : 0.f;
+    case EW_SIGMOID: return 1.f / (1.f + __expf(-x0));
+    case EW_SIG_BWD: return x0 * x1 * (1.f - x1);
+    case EW_FILL: return a.s0;
+    case EW_FMA: return x0 * x1 + x2;
+    case EW_BNB: return x0 * x1 + x2 * x3 + x4;
+    default: return 0.f;
+  }
+}
+
+FEDMI_DEV void ew_load8(const ZTensor& t, long long off, bool contiguous, float v[8]) {
+  if (!contiguous) {
+    const float s = zload(t, off);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = s;
+  } else if (t.dtype == 1) {
+    const bf16x8 q = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(t.p) + off);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (float)q[u];
+  } else {
+    const f32x4 q0 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(t.p) + off);
+    const f32x4 q1 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(t.p) + off + 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { v[u] = q0[u]; v[u + 4] = q1[u]; }
+  }
+}
+
+// 8 consecutive innermost elements per thread: 16-byte loads / stores (host-checked alignment);
+// the descriptors' innermost size is already divided by 8 and unit strides scaled by 8
+__global__ __launch_bounds__(256) void ew_vec_kernel(EwArgs a, long long n8) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float x[5][8];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      if (a.in[k].p) {
+        ew_load8(a.in[k], zoffset(a.o, a.in[k], i), (a.vmask >> k) & 1, x[k]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[k][u] = 0.f;
+      }
+    }
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ew_apply(a, x[0][u], x[1][u], x[2][u], x[3][u], x[4][u]);
+    const long long oo = zoffset(a.o, a.o, i);
+    if (a.o.dtype == 1) {
+      bf16x8 q;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] = (bf16)v[u];
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.o.p) + oo) = q;
+    } else {
+      f32x4 q0, q1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { q0[u] = v[u]; q1[u] = v[u + 4]; }
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.o.p) + oo) = q0;
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.o.p) + oo + 4) = q1;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void ew_kernel(EwArgs a, long long n) {
@@ -100,27 +173,11 @@ __global__ __launch_bounds__(256) void ew_kernel(EwArgs a, long long n) {
     if (a.in[3].p) x3 = zload(a.in[3], zoffset(a.o, a.in[3], i));
     if (a.in[4].p) x4 = zload(a.in[4], zoffset(a.o, a.in[4], i));
     float v;
-    switch (a.op) {
-      case EW_COPY: v = x0; break;
-      case EW_ADD: v = x0 + a.s0 * x1; break;
-      case EW_SUB: v = x0 - a.s0 * x1; break;
-      case EW_MUL: v = x0 * x1; break;
-      case EW_DIV: v = x0 / x1; break;
-      case EW_ADDS: v = x0 + a.s0; break;
-      case EW_MULS: v = x0 * a.s0; break;
-      case EW_RELU: v = fmaxf(x0, 0.f); break;
-      case EW_THR_BWD: v = x1 > a.s0 ? x0 : 0.f; break;
-      case EW_SIGMOID: v = 1.f / (1.f + __expf(-x0)); break;
-      case EW_SIG_BWD: v = x0 * x1 * (1.f - x1); break;
-      case EW_FILL: v = a.s0; break;
-      case EW_FMA: v = x0 * x1 + x2; break;
-      case EW_BNB: v = x0 * x1 + x2 * x3 + x4; break;
-      case EW_BERN: {
-        const uint32_t h = hash3(a.seed, ctr, (uint32_t)i ^ (uint32_t)(i >> 32));
-        v = ((float)(h >> 8) * (1.f / 16777216.f)) < a.s0 ? 1.f : 0.f;
-        break;
-      }
-      default: v = 0.f;
+    if (a.op == EW_BERN) {
+      const uint32_t h = hash3(a.seed, ctr, (uint32_t)i ^ (uint32_t)(i >> 32));
+      v = ((float)(h >> 8) * (1.f / 16777216.f)) < a.s0 ? 1.f : 0.f;
+    } else {
+      v = ew_apply(a, x0, x1, x2, x3, x4);
     }
     zstore(a.o, zoffset(a.o, a.o, i), v);
   }
@@ -191,6 +248,101 @@ __global__ __launch_bounds__(256) void reduce_kernel(RdArgs r, long long n_outer
       atomicAdd(r.acc2 + o, t2);
     }
   }
+}
+
+// ---- row reduction of a [M, C] row-major matrix (ld = row stride), C % 8 == 0 ------------------
+// The channels-last case of the BN moments / bias gradients: a thread owns 8 channels (one 16-byte
+// load per row), RL = 256 / (C/8) row lanes per block, grid.y row slabs; per-slab partials go to
+// `part` [slabs][2][C] and a finalize pass adds them in slab order (deterministic).
+FEDMI_DEV void rows_load8(const void* p, int dt, long long off, float v[8]) {
+  if (dt == 1) {
+    const bf16x8 q = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(p) + off);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (float)q[u];
+  } else {
+    const f32x4 q0 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + off);
+    const f32x4 q1 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + off + 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { v[u] = q0[u]; v[u + 4] = q1[u]; }
+  }
+}
+
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_dt, long long lda, const void* b,
+                                                          int b_dt, long long ldb, const float* shift, int C,
+                                                          long long M, int op, float* part) {
+  __shared__ float red[2][256 * 8];
+  const int VL = C / 8;
+  const int vt = min(VL, 256);
+  const int RL = 256 / vt;
+  const int v = blockIdx.x * vt + (threadIdx.x % vt);
+  const int rl = threadIdx.x / vt;
+  const bool act = rl < RL && v < VL;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) { s1[u] = 0.f; s2[u] = 0.f; }
+  if (act) {
+    float sh[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) sh[u] = shift ? shift[v * 8 + u] : 0.f;
+    const long long per = (M + gridDim.y - 1) / gridDim.y;
+    const long long r0 = (long long)blockIdx.y * per, r1 = min(M, r0 + per);
+    for (long long r = r0 + rl; r < r1; r += RL) {
+      float x[8];
+      rows_load8(a, a_dt, r * lda + v * 8, x);
+      if (op == RD_SUM) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s1[u] += x[u];
+      } else if (op == RD_SUMSQ_SHIFT) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { const float d = x[u] - sh[u]; s1[u] += d; s2[u] += d * d; }
+      } else {
+        float y[8];
+        rows_load8(b, b_dt, r * ldb + v * 8, y);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { s1[u] += x[u]; s2[u] += x[u] * (y[u] - sh[u]); }
+      }
+    }
+  }
+  // tree over the row lanes of each channel vector
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    red[0][threadIdx.x * 8 + u] = s1[u];
+    red[1][threadIdx.x * 8 + u] = s2[u];
+  }
+  __syncthreads();
+  if (rl == 0 && v < VL) {
+    for (int k = 1; k < RL; ++k) {
+      const int t = k * vt + (threadIdx.x % vt);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { s1[u] += red[0][t * 8 + u]; s2[u] += red[1][t * 8 + u]; }
+    }
+    float* dst = part + (long long)blockIdx.y * 2 * C;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { dst[v * 8 + u] = s1[u]; dst[C + v * 8 + u] = s2[u]; }
+  }
+}
+
+__global__ __launch_bounds__(256) void reduce_rows_finalize(const float* part, int slabs, int C, int two, float* acc,
+                                                            float* acc2) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float t1 = 0.f, t2 = 0.f;
+  for (int b = 0; b < slabs; ++b) {
+    t1 += part[(long long)b * 2 * C + c];
+    if (two) t2 += part[(long long)b * 2 * C + C + c];
+  }
+  acc[c] += t1;
+  if (two) acc2[c] += t2;
+}
+
+int rows_slabs(long long M, int C) {
+  const int VL = C / 8, vt = VL < 256 ? VL : 256, RL = 256 / vt;
+  const long long tiles = (VL + vt - 1) / vt;
+  long long sl = M / ((long long)RL * 32);          // >= 32 rows per row lane
+  const long long cap = (2048 + tiles - 1) / tiles;  // ~2048 blocks in flight at most
+  if (sl > cap) sl = cap;
+  if (sl < 1) sl = 1;
+  return (int)sl;
 }
 
 // ---- BatchNorm per-channel coefficients --------------------------------------------
@@ -461,57 +613,130 @@ __global__ __launch_bounds__(256) void ce_stats_kernel(ZTensor logits, const lon
 }
 
 // ---- direct (VALU) grouped convolution, any channel counts ---------------------------
-// x [N, C, H, W], w [O, C/G, R, S], y [N, O, P, Q] -- logical NCHW, any strides.
+// x [N, C, H, W], w [O, C/G, R, S], y [N, O, P, Q] -- logical NCHW, any strides (channels-last in
+// practice).  Grouped convs with narrow groups (RegNet group width 8, DPN / ResNeXt cardinality 32,
+// ShuffleNet g2/g3 widths) and odd channel counts have no MFMA-shaped tile; they run here.
+// FWD: a thread owns one output pixel x GT output channels of one group; the (group, channel
+// chunk)'s weights sit in LDS as [r*S+s][c][GT] and are read as wave-wide broadcasts, the input
+// channels of a tap are contiguous (channels-last), so each tap costs one cached load per channel
+// and GT FMAs.  DGRAD: the same with the roles of x and y swapped (one input pixel x GT input
+// channels).  WGRAD: a thread owns weights (o, r, s, c) with c fastest -- neighbouring lanes read
+// neighbouring channels of the same pixel (coalesced) and share the dy value (broadcast) -- and
+// sums over the pixels of an image slab; per-slab partials go to a workspace and a second pass
+// adds them in slab order (deterministic, no atomics).
+constexpr int GT = 8;          // output (FWD) / input (DGRAD) channels per thread
+constexpr int GC_LDS = 8192;   // floats of LDS for a weight chunk (32 KiB)
+
 struct GConv {
   ZTensor x, w, y;
   int G, st_h, st_w, pad_h, pad_w, R, S;
+  int vec_x, vec_y;    // channels of x (resp. y) load as aligned bf16x8 vectors (host-checked)
 };
 
-__global__ __launch_bounds__(256) void gconv_fwd_kernel(GConv g, long long n) {
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  const long long O = g.y.size[1], P = g.y.size[2], Q = g.y.size[3];
+FEDMI_DEV void load8(const ZTensor& t, long long off, long long cstride, bool vec, float v[8]) {
+  if (vec) {
+    const bf16x8 q = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(t.p) + off);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (float)q[u];
+  } else {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = zload(t, off + u * cstride);
+  }
+}
+
+__global__ __launch_bounds__(256) void gconv_fwd_kernel(GConv g) {
+  __shared__ float wl[GC_LDS];
+  const long long N = g.y.size[0], O = g.y.size[1], P = g.y.size[2], Q = g.y.size[3];
   const long long H = g.x.size[2], W = g.x.size[3];
-  const long long Cg = g.w.size[1], Og = O / g.G;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    // o fastest: neighbouring lanes read the same input pixel, neighbouring weights
-    long long t = i;
-    const long long o = t % O; t /= O;
-    const long long q = t % Q; t /= Q;
-    const long long p = t % P; t /= P;
-    const long long nn = t;
-    const long long c0 = (o / Og) * Cg;
-    float acc = 0.f;
+  const int Cg = (int)g.w.size[1], Og = (int)(O / g.G), RS = g.R * g.S;
+  const int grp = blockIdx.y, o0 = blockIdx.z * GT;
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = pix < N * P * Q;
+  long long t = valid ? pix : 0;
+  const long long q = t % Q; t /= Q;
+  const long long p = t % P;
+  const long long n = t / P;
+  float acc[GT];
+#pragma unroll
+  for (int j = 0; j < GT; ++j) acc[j] = 0.f;
+  const int cch = max(8, GC_LDS / (RS * GT) / 8 * 8);
+  const long long xb = n * g.x.stride[0] + (long long)grp * Cg * g.x.stride[1];
+  for (int c0 = 0; c0 < Cg; c0 += cch) {
+    const int cn = min(cch, Cg - c0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < RS * cn * GT; e += 256) {
+      const int j = e % GT, c = (e / GT) % cn, rs = e / (GT * cn);
+      const int o = o0 + j;
+      wl[e] = o < Og ? zload(g.w, (long long)(grp * Og + o) * g.w.stride[0] + (long long)(c0 + c) * g.w.stride[1] +
+                                      (rs / g.S) * g.w.stride[2] + (rs % g.S) * g.w.stride[3])
+                     : 0.f;
+    }
+    __syncthreads();
+    if (!valid) continue;
     for (int r = 0; r < g.R; ++r) {
       const long long h = p * g.st_h - g.pad_h + r;
       if (h < 0 || h >= H) continue;
       for (int s = 0; s < g.S; ++s) {
         const long long w = q * g.st_w - g.pad_w + s;
         if (w < 0 || w >= W) continue;
-        const long long xb = nn * g.x.stride[0] + h * g.x.stride[2] + w * g.x.stride[3];
-        const long long wb = o * g.w.stride[0] + r * g.w.stride[2] + s * g.w.stride[3];
-        for (long long c = 0; c < Cg; ++c)
-          acc += zload(g.x, xb + (c0 + c) * g.x.stride[1]) * zload(g.w, wb + c * g.w.stride[1]);
+        const long long base = xb + h * g.x.stride[2] + w * g.x.stride[3] + (long long)c0 * g.x.stride[1];
+        const float* wr = wl + (r * g.S + s) * cn * GT;
+        int c = 0;
+        if (g.vec_x) {
+          for (; c + 8 <= cn; c += 8) {
+            float xv[8];
+            load8(g.x, base + c, 1, true, xv);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+              for (int j = 0; j < GT; ++j) acc[j] += xv[u] * wr[(c + u) * GT + j];
+          }
+        }
+        for (; c < cn; ++c) {
+          const float xv = zload(g.x, base + (long long)c * g.x.stride[1]);
+#pragma unroll
+          for (int j = 0; j < GT; ++j) acc[j] += xv * wr[c * GT + j];
+        }
       }
     }
-    zstore(g.y, nn * g.y.stride[0] + o * g.y.stride[1] + p * g.y.stride[2] + q * g.y.stride[3], acc);
   }
+  if (!valid) return;
+  const long long yb = n * g.y.stride[0] + p * g.y.stride[2] + q * g.y.stride[3];
+#pragma unroll
+  for (int j = 0; j < GT; ++j)
+    if (o0 + j < Og) zstore(g.y, yb + (long long)(grp * Og + o0 + j) * g.y.stride[1], acc[j]);
 }
 
-// dx[n][c][h][w] = sum_{o in group(c), r, s: (h + pad - r) % st == 0} dy[n][o][(h+pad-r)/st][(w+pad-s)/st] w[o][c - c0][r][s]
-__global__ __launch_bounds__(256) void gconv_dgrad_kernel(GConv g, long long n) {
-  // g.x = dx (output), g.y = dy (input)
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  const long long C = g.x.size[1], H = g.x.size[2], W = g.x.size[3];
+// g.x = dx (output), g.y = dy (input)
+__global__ __launch_bounds__(256) void gconv_dgrad_kernel(GConv g) {
+  __shared__ float wl[GC_LDS];
+  const long long N = g.x.size[0], H = g.x.size[2], W = g.x.size[3];
   const long long O = g.y.size[1], P = g.y.size[2], Q = g.y.size[3];
-  const long long Cg = g.w.size[1], Og = O / g.G;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    long long t = i;
-    const long long c = t % C; t /= C;
-    const long long w = t % W; t /= W;
-    const long long h = t % H; t /= H;
-    const long long nn = t;
-    const long long grp = c / Cg, cc = c - grp * Cg;
-    float acc = 0.f;
+  const int Cg = (int)g.w.size[1], Og = (int)(O / g.G), RS = g.R * g.S;
+  const int grp = blockIdx.y, c0 = blockIdx.z * GT;
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = pix < N * H * W;
+  long long t = valid ? pix : 0;
+  const long long w = t % W; t /= W;
+  const long long h = t % H;
+  const long long n = t / H;
+  float acc[GT];
+#pragma unroll
+  for (int j = 0; j < GT; ++j) acc[j] = 0.f;
+  const int och = max(8, GC_LDS / (RS * GT) / 8 * 8);
+  const long long yb = n * g.y.stride[0] + (long long)grp * Og * g.y.stride[1];
+  for (int o0 = 0; o0 < Og; o0 += och) {
+    const int on = min(och, Og - o0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < RS * on * GT; e += 256) {
+      const int j = e % GT, o = (e / GT) % on, rs = e / (GT * on);
+      const int c = c0 + j;
+      wl[e] = c < Cg ? zload(g.w, (long long)(grp * Og + o0 + o) * g.w.stride[0] + (long long)c * g.w.stride[1] +
+                                      (rs / g.S) * g.w.stride[2] + (rs % g.S) * g.w.stride[3])
+                     : 0.f;
+    }
+    __syncthreads();
+    if (!valid) continue;
     for (int r = 0; r < g.R; ++r) {
       const long long hp = h + g.pad_h - r;
       if (hp < 0 || hp % g.st_h) continue;
@@ -522,51 +747,105 @@ __global__ __launch_bounds__(256) void gconv_dgrad_kernel(GConv g, long long n) 
         if (wp < 0 || wp % g.st_w) continue;
         const long long q = wp / g.st_w;
         if (q >= Q) continue;
-        const long long yb = nn * g.y.stride[0] + p * g.y.stride[2] + q * g.y.stride[3];
-        for (long long oo = 0; oo < Og; ++oo) {
-          const long long o = grp * Og + oo;
-          acc += zload(g.y, yb + o * g.y.stride[1]) *
-                 zload(g.w, o * g.w.stride[0] + cc * g.w.stride[1] + r * g.w.stride[2] + s * g.w.stride[3]);
+        const long long base = yb + p * g.y.stride[2] + q * g.y.stride[3] + (long long)o0 * g.y.stride[1];
+        const float* wr = wl + (r * g.S + s) * on * GT;
+        int o = 0;
+        if (g.vec_y) {
+          for (; o + 8 <= on; o += 8) {
+            float dv[8];
+            load8(g.y, base + o, 1, true, dv);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+              for (int j = 0; j < GT; ++j) acc[j] += dv[u] * wr[(o + u) * GT + j];
+          }
+        }
+        for (; o < on; ++o) {
+          const float dv = zload(g.y, base + (long long)o * g.y.stride[1]);
+#pragma unroll
+          for (int j = 0; j < GT; ++j) acc[j] += dv * wr[o * GT + j];
         }
       }
     }
-    zstore(g.x, nn * g.x.stride[0] + c * g.x.stride[1] + h * g.x.stride[2] + w * g.x.stride[3], acc);
   }
+  if (!valid) return;
+  const long long xo = n * g.x.stride[0] + h * g.x.stride[2] + w * g.x.stride[3];
+#pragma unroll
+  for (int j = 0; j < GT; ++j)
+    if (c0 + j < Cg) zstore(g.x, xo + (long long)(grp * Cg + c0 + j) * g.x.stride[1], acc[j]);
 }
 
-// dw[o][c][r][s] = sum_{n,p,q} dy[n][o][p][q] x[n][c0 + c][p*st - pad + r][q*st - pad + s]
-// one workgroup per weight element; 256 lanes split the (n, p, q) sum, LDS tree reduce.
-__global__ __launch_bounds__(256) void gconv_wgrad_kernel(GConv g, ZTensor dw) {
-  __shared__ float red[256];
+// partial[slab][o][c][r][s] = sum over images [slab*nb, +nb) and all (p, q).  A thread owns one
+// (o, r, s) and 8 consecutive input channels (one bf16x8 load per pixel when x is channels-last);
+// grid (thread blocks over (o, rs, channel block), groups, slabs)
+__global__ __launch_bounds__(256) void gconv_wgrad_kernel(GConv g, float* part, int nb) {
+  const long long N = g.x.size[0], H = g.x.size[2], W = g.x.size[3];
   const long long O = g.y.size[1], P = g.y.size[2], Q = g.y.size[3];
-  const long long H = g.x.size[2], W = g.x.size[3], N = g.x.size[0];
-  const long long Cg = g.w.size[1], Og = O / g.G;
-  long long e = blockIdx.x;
-  const int s = (int)(e % g.S); e /= g.S;
-  const int r = (int)(e % g.R); e /= g.R;
-  const long long c = e % Cg; e /= Cg;
-  const long long o = e;
-  const long long cx = (o / Og) * Cg + c;
-  float acc = 0.f;
-  const long long tot = N * P * Q;
-  for (long long i = threadIdx.x; i < tot; i += 256) {
-    long long t = i;
-    const long long q = t % Q; t /= Q;
-    const long long p = t % P; t /= P;
-    const long long nn = t;
-    const long long h = p * g.st_h - g.pad_h + r, w = q * g.st_w - g.pad_w + s;
-    if (h < 0 || h >= H || w < 0 || w >= W) continue;
-    acc += zload(g.y, nn * g.y.stride[0] + o * g.y.stride[1] + p * g.y.stride[2] + q * g.y.stride[3]) *
-           zload(g.x, nn * g.x.stride[0] + cx * g.x.stride[1] + h * g.x.stride[2] + w * g.x.stride[3]);
+  const int Cg = (int)g.w.size[1], Og = (int)(O / g.G), RS = g.R * g.S;
+  const int CB = (Cg + 7) / 8;
+  const int grp = blockIdx.y;
+  const long long Wg = (long long)Og * RS * Cg;
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)Og * RS * CB) return;
+  // e = (o * RS + rs) * CB + cb
+  const int cb = (int)(e % CB);
+  const int rs = (int)((e / CB) % RS);
+  const int o = (int)(e / ((long long)CB * RS));
+  const int r = rs / g.S, s = rs % g.S;
+  const int c0 = cb * 8, cn = min(8, Cg - c0);
+  const bool vec = g.vec_x && cn == 8;
+  const long long n0 = (long long)blockIdx.z * nb, n1 = min(N, n0 + nb);
+  const long long xc = (long long)(grp * Cg + c0) * g.x.stride[1];
+  const long long yc = (long long)(grp * Og + o) * g.y.stride[1];
+  float acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = 0.f;
+  for (long long n = n0; n < n1; ++n) {
+    for (long long p = 0; p < P; ++p) {
+      const long long h = p * g.st_h - g.pad_h + r;
+      if (h < 0 || h >= H) continue;
+      const long long xr = n * g.x.stride[0] + h * g.x.stride[2] + xc;
+      const long long yr = n * g.y.stride[0] + p * g.y.stride[2] + yc;
+      for (long long q = 0; q < Q; ++q) {
+        const long long w = q * g.st_w - g.pad_w + s;
+        if (w < 0 || w >= W) continue;
+        const float dv = zload(g.y, yr + q * g.y.stride[3]);
+        float xv[8];
+        if (vec) {
+          load8(g.x, xr + w * g.x.stride[3], 1, true, xv);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) xv[u] = u < cn ? zload(g.x, xr + w * g.x.stride[3] + u * g.x.stride[1]) : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] += dv * xv[u];
+      }
+    }
   }
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int k = 128; k > 0; k >>= 1) {
-    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0)
-    zstore(dw, o * dw.stride[0] + c * dw.stride[1] + r * dw.stride[2] + s * dw.stride[3], red[0]);
+  // partial layout: [slab][grp][o][c][r][s] = the PyTorch weight layout per slab
+  float* dst = part + (long long)blockIdx.z * g.G * Wg + (long long)grp * Wg;
+  for (int u = 0; u < cn; ++u) dst[((long long)o * Cg + c0 + u) * RS + rs] = acc[u];
+}
+
+// dw[i] = sum_slab part[slab][i] in slab order (dw: any strides over the contiguous [O, Cg, R, S] order)
+__global__ __launch_bounds__(256) void gconv_wgrad_sum_kernel(const float* part, int slabs, long long total,
+                                                              ZTensor dw) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  float v = 0.f;
+  for (int b = 0; b < slabs; ++b) v += part[(long long)b * total + i];
+  const long long RS = dw.size[2] * dw.size[3], Cg = dw.size[1];
+  const long long rs = i % RS, c = (i / RS) % Cg, o = i / (RS * Cg);
+  zstore(dw, o * dw.stride[0] + c * dw.stride[1] + (rs / dw.size[3]) * dw.stride[2] + (rs % dw.size[3]) * dw.stride[3], v);
+}
+
+// images per wgrad slab: >= ~2048 pixels of work per thread block
+int gconv_slab_images(long long N, long long P, long long Q) {
+  long long pq = P * Q > 0 ? P * Q : 1;
+  long long nb = (2048 + pq - 1) / pq;
+  if (nb < 1) nb = 1;
+  if (nb > N) nb = N;
+  return (int)nb;
 }
 
 int grid1(long long n) {
@@ -581,7 +860,7 @@ int grid1(long long n) {
 namespace fedmi {
 
 void launch_ew(hipStream_t st, const ZTensor& o, const ZTensor* ins, int nin, int op, float s0, float s1,
-               uint32_t seed, const int* ctr) {
+               uint32_t seed, const int* ctr, int vmask) {
   if (nin > 5) throw std::invalid_argument("ew: at most 5 inputs");
   EwArgs a{};
   a.o = o;
@@ -591,10 +870,16 @@ void launch_ew(hipStream_t st, const ZTensor& o, const ZTensor* ins, int nin, in
   a.s1 = s1;
   a.seed = seed;
   a.ctr = ctr;
+  a.vmask = vmask < 0 ? 0 : vmask;
   long long n = 1;
   for (int d = 0; d < o.ndim; ++d) n *= o.size[d];
   if (n <= 0) return;
-  hipLaunchKernelGGL(ew_kernel, dim3(grid1(n)), dim3(256), 0, st, a, n);
+  if (vmask >= 0) {
+    if (op == EW_BERN) throw std::invalid_argument("ew: no vector launch for bernoulli");
+    hipLaunchKernelGGL(ew_vec_kernel, dim3(grid1(n)), dim3(256), 0, st, a, n);
+  } else {
+    hipLaunchKernelGGL(ew_kernel, dim3(grid1(n)), dim3(256), 0, st, a, n);
+  }
   check_hip(hipGetLastError(), "ew_kernel");
 }
 
@@ -620,6 +905,22 @@ void launch_reduce(hipStream_t st, const ZTensor& outer, const ZTensor& inner, c
   if (splits > 65535) splits = 65535;
   hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)tiles, (unsigned)splits), dim3(256), 0, st, r, no, ni);
   check_hip(hipGetLastError(), "reduce_kernel");
+}
+
+long long reduce_rows_ws_floats(long long M, int C) { return (long long)rows_slabs(M, C) * 2 * C; }
+
+void launch_reduce_rows(hipStream_t st, const void* a, int a_dt, long long lda, const void* b, int b_dt,
+                        long long ldb, const float* shift, int C, long long M, int op, float* part, long long part_floats,
+                        float* acc, float* acc2) {
+  if (C % 8 || C <= 0 || M <= 0) throw std::invalid_argument("reduce_rows: C % 8 == 0 and M > 0 required");
+  const int slabs = rows_slabs(M, C);
+  if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("reduce_rows: workspace too small");
+  const int VL = C / 8, vt = VL < 256 ? VL : 256;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((VL + vt - 1) / vt), (unsigned)slabs), dim3(256), 0, st, a,
+                     a_dt, lda, b, b_dt, ldb, shift, C, M, op, part);
+  hipLaunchKernelGGL(reduce_rows_finalize, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, part, slabs, C,
+                     op != RD_SUM ? 1 : 0, acc, acc2);
+  check_hip(hipGetLastError(), "reduce_rows");
 }
 
 void launch_bn_fwd_coeffs(hipStream_t st, const float* s1, const float* s2, const float* shift, int C, long long M,
@@ -696,20 +997,51 @@ void launch_ce_stats(hipStream_t st, const ZTensor& logits, const long long* y, 
   check_hip(hipGetLastError(), "ce_stats");
 }
 
+long long gconv_wgrad_ws_floats(long long N, long long P, long long Q, long long w_numel) {
+  const int nb = gconv_slab_images(N, P, Q);
+  return ((N + nb - 1) / nb) * w_numel;
+}
+
 void launch_gconv(hipStream_t st, int mode, const ZTensor& x, const ZTensor& w, const ZTensor& y, int G, int sth,
-                  int stw, int padh, int padw) {
+                  int stw, int padh, int padw, float* ws, long long ws_floats) {
   GConv g{};
   g.x = x; g.w = w; g.y = y; g.G = G; g.st_h = sth; g.st_w = stw; g.pad_h = padh; g.pad_w = padw;
   g.R = (int)w.size[2]; g.S = (int)w.size[3];
+  const long long O = y.size[1], Cg = w.size[1], Og = O / G;
+  // bf16x8 channel vectors: bf16, unit channel stride, every other stride and the group offset a
+  // multiple of 8 elements, 16-byte aligned base
+  auto vec_ok = [](const ZTensor& t, long long per_group) {
+    if (t.dtype != 1 || t.ndim != 4 || t.stride[1] != 1 || per_group % 8) return 0;
+    if (reinterpret_cast<uintptr_t>(t.p) % 16) return 0;
+    for (int d : {0, 2, 3})
+      if (t.stride[d] % 8) return 0;
+    return 1;
+  };
+  g.vec_x = vec_ok(x, Cg);
+  g.vec_y = vec_ok(y, Og);
+  if (G <= 0 || O % G || x.size[1] != Cg * G || w.size[0] != O || g.R * g.S * GT > GC_LDS)
+    throw std::invalid_argument("gconv: inconsistent shapes");
   if (mode == 0) {
-    const long long n = y.size[0] * y.size[1] * y.size[2] * y.size[3];
-    if (n > 0) hipLaunchKernelGGL(gconv_fwd_kernel, dim3(grid1(n)), dim3(256), 0, st, g, n);
+    const long long n = y.size[0] * y.size[2] * y.size[3];
+    if (n <= 0) return;
+    hipLaunchKernelGGL(gconv_fwd_kernel, dim3((unsigned)((n + 255) / 256), G, (unsigned)((Og + GT - 1) / GT)), dim3(256),
+                       0, st, g);
   } else if (mode == 1) {
-    const long long n = x.size[0] * x.size[1] * x.size[2] * x.size[3];
-    if (n > 0) hipLaunchKernelGGL(gconv_dgrad_kernel, dim3(grid1(n)), dim3(256), 0, st, g, n);
+    const long long n = x.size[0] * x.size[2] * x.size[3];
+    if (n <= 0) return;
+    hipLaunchKernelGGL(gconv_dgrad_kernel, dim3((unsigned)((n + 255) / 256), G, (unsigned)((Cg + GT - 1) / GT)),
+                       dim3(256), 0, st, g);
   } else {
-    const long long n = w.size[0] * w.size[1] * w.size[2] * w.size[3];
-    if (n > 0) hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((unsigned)n), dim3(256), 0, st, g, w);
+    const long long N = x.size[0], P = y.size[2], Q = y.size[3];
+    const long long total = w.size[0] * w.size[1] * w.size[2] * w.size[3];
+    const int nb = gconv_slab_images(N, P, Q);
+    const long long slabs = (N + nb - 1) / nb;
+    if (!ws || ws_floats < slabs * total) throw std::invalid_argument("gconv wgrad: workspace too small");
+    const long long threads = Og * g.R * g.S * ((Cg + 7) / 8);
+    hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((unsigned)((threads + 255) / 256), G, (unsigned)slabs), dim3(256), 0, st,
+                       g, ws, nb);
+    hipLaunchKernelGGL(gconv_wgrad_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, ws, (int)slabs,
+                       total, w);
   }
   check_hip(hipGetLastError(), "gconv");
 }

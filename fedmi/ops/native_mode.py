@@ -33,6 +33,8 @@ import collections
 from typing import Optional
 
 import torch
+import torch.nn.functional as F
+from torch.overrides import TorchFunctionMode
 from torch.utils._python_dispatch import TorchDispatchMode
 
 from .. import native
@@ -77,16 +79,73 @@ def _bcast(t: torch.Tensor, shape) -> torch.Tensor:
     return t.expand(shape) if t.dim() == len(shape) else t.reshape((1,) * (len(shape) - t.dim()) + tuple(t.shape)).expand(shape)
 
 
+def coalesce(shape, strides):
+    """Merge the dims of an iteration space shared by several operands (``strides``: one stride list per
+    operand, operand 0 decides the order): size-1 dims drop, dims are ordered by operand 0's strides and
+    neighbours that are contiguous in EVERY operand merge -- a channels-last activation with a
+    per-channel operand becomes [N*H*W, C], a pure elementwise op one flat dim."""
+    dims = [d for d in range(len(shape)) if shape[d] != 1]
+    if not dims:
+        return [1], [[0] for _ in strides]
+    dims.sort(key=lambda d: -abs(strides[0][d]))
+    nshape = [shape[dims[0]]]
+    nstr = [[s[dims[0]]] for s in strides]
+    for d in dims[1:]:
+        if all(ns[-1] == s[d] * shape[d] for ns, s in zip(nstr, strides)):
+            nshape[-1] *= shape[d]
+            for ns, s in zip(nstr, strides):
+                ns[-1] = s[d]
+        else:
+            nshape.append(shape[d])
+            for ns, s in zip(nstr, strides):
+                ns.append(s[d])
+    return nshape, nstr
+
+
 def ew(out: torch.Tensor, ins, op: int, s0: float = 0.0, s1: float = 0.0, seed: int = 0, ctr=None) -> torch.Tensor:
     """out[...] = op(ins...) with broadcasting of every input to out's shape."""
     if out.numel() == 0:
         return out
-    shape = out.shape if out.dim() else (1,)
+    if out.numel() >= (1 << 31):
+        raise ValueError("native_mode: tensors must have < 2^31 elements")
+    shape = list(out.shape) if out.dim() else [1]
     o = out if out.dim() else out.view(1)
-    descs = [zd(_bcast(t if t.dim() else t.view(1), shape)) for t in ins]
-    _nat().z_ew(_st(out.device), zd(o), descs, op, float(s0), float(s1), int(seed) & 0xFFFFFFFF,
-                0 if ctr is None else ctr.data_ptr())
+    ts = [_bcast(t if t.dim() else t.view(1), shape) for t in ins]
+    for t in ts:
+        if t.dtype not in _DT:
+            raise TypeError(f"native_mode: unsupported dtype {t.dtype}")
+    if op == EW_BERN:
+        # the counter-based mask is a function of the logical element index: keep the logical order
+        nshape, nstr = shape, [list(o.stride())] + [list(t.stride()) for t in ts]
+    else:
+        nshape, nstr = coalesce(shape, [list(o.stride())] + [list(t.stride()) for t in ts])
+    allt = [o] + ts
+    vmask = _vec_mask(nshape, nstr, allt) if op != EW_BERN else -1
+    if vmask >= 0:
+        nshape = nshape[:-1] + [nshape[-1] // 8]
+        nstr = [st[:-1] + [st[-1] * 8] for st in nstr]
+    descs = [(t.data_ptr(), _DT[t.dtype], nshape, st) for t, st in zip(allt, nstr)]
+    _nat().z_ew(_st(out.device), descs[0], descs[1:], op, float(s0), float(s1), int(seed) & 0xFFFFFFFF,
+                0 if ctr is None else ctr.data_ptr(), vmask)
     return out
+
+
+def _vec_mask(shape, strides, ts) -> int:
+    """Bit k (input k) set if that operand is contiguous over groups of 8 innermost elements, 0 bit = a
+    broadcast operand; -1 = the 8-wide vector launch does not apply (odd sizes, misalignment, int64, an
+    output that is not unit-stride innermost)."""
+    if shape[-1] % 8:
+        return -1
+    mask = 0
+    for k, (t, st) in enumerate(zip(ts, strides)):
+        inner = st[-1]
+        if inner == 0 and k > 0:
+            continue
+        if inner != 1 or t.dtype == torch.int64 or t.data_ptr() % 16 or any(v % 8 for v in st[:-1]):
+            return -1
+        if k > 0:
+            mask |= 1 << (k - 1)
+    return mask
 
 
 def fill_(t: torch.Tensor, v: float) -> torch.Tensor:
@@ -134,17 +193,51 @@ def reduce_sum(a: torch.Tensor, dims, acc: torch.Tensor, op: int = RD_SUM, b: Op
     """acc (fp32, ZEROED, one entry per kept element in order) += sum over ``dims`` of f(a[, b])."""
     dims = sorted(d % a.dim() for d in dims)
     kept = [d for d in range(a.dim()) if d not in dims]
-    def desc(t, ds):
+    ops = [a] if b is None else [a, b]
+
+    def space(ds, order_by_acc):
         if not ds:
-            return (0, 0, [1], [0])
-        return (0, 0, [t.shape[d] for d in ds], [t.stride(d) for d in ds])
-    outer, inner = desc(a, kept), desc(a, dims)
-    outer_b = desc(b, kept) if b is not None else None
-    inner_b = desc(b, dims) if b is not None else None
+            return [1], [[0] for _ in ops]
+        shp = [a.shape[d] for d in ds]
+        strs = [[t.stride(d) for d in ds] for t in ops]
+        if order_by_acc:
+            # kept dims: the accumulator index is row-major over them -- merge only, never reorder
+            acc_str = [1] * len(ds)
+            for j in range(len(ds) - 2, -1, -1):
+                acc_str[j] = acc_str[j + 1] * shp[j + 1]
+            ns, nst = coalesce(shp, [acc_str] + strs)
+            return ns, nst[1:]
+        return coalesce(shp, strs)
+
+    oshape, ostr = space(kept, True)
+    ishape, istr = space(dims, False)
+    if _rows_ok(oshape, ostr, ishape, istr, ops):
+        # channels-last moments / bias gradients: [M, C] rows, 16-byte channel vectors, deterministic
+        C, M = oshape[0], ishape[0]
+        nat = _nat()
+        part = torch.empty(int(nat.z_reduce_rows_ws_floats(M, C)), dtype=torch.float32, device=a.device)
+        nat.z_reduce_rows(_st(a.device), a.data_ptr(), _DT[a.dtype], istr[0][0],
+                          b.data_ptr() if b is not None else 0, _DT[b.dtype] if b is not None else 0,
+                          istr[1][0] if b is not None else 0, shift.data_ptr() if shift is not None else 0, C, M, op,
+                          part.data_ptr(), part.numel(), acc.data_ptr(), acc2.data_ptr() if acc2 is not None else 0)
+        return
+    outer = (0, 0, oshape, ostr[0])
+    inner = (0, 0, ishape, istr[0])
+    outer_b = (0, 0, oshape, ostr[1]) if b is not None else None
+    inner_b = (0, 0, ishape, istr[1]) if b is not None else None
     _nat().z_reduce(_st(a.device), outer, inner, outer_b, inner_b, a.data_ptr(), _DT[a.dtype],
                     b.data_ptr() if b is not None else 0, _DT[b.dtype] if b is not None else 0,
                     shift.data_ptr() if shift is not None else 0, acc.data_ptr(),
                     acc2.data_ptr() if acc2 is not None else 0, op)
+
+
+def _rows_ok(oshape, ostr, ishape, istr, ops) -> bool:
+    if len(oshape) != 1 or len(ishape) != 1 or oshape[0] % 8 or ishape[0] < 1:
+        return False
+    for t, os_, is_ in zip(ops, ostr, istr):
+        if os_[0] != 1 or is_[0] % 8 or t.dtype not in (torch.float32, torch.bfloat16) or t.data_ptr() % 16:
+            return False
+    return True
 
 
 # ---------------------------------------------------------------------------- op impls
@@ -279,6 +372,12 @@ def _fill_like(func, self, **kw):
     return fill_(out, 1.0 if func is aten.ones_like.default else 0.0)
 
 
+@impl(aten.new_zeros.default, aten.new_ones.default)
+def _new_fill(func, self, size, **kw):
+    out = _alloc_like_meta(func, (self, size), kw, self.device)
+    return fill_(out, 1.0 if func is aten.new_ones.default else 0.0)
+
+
 @impl(aten.fill_.Scalar)
 def _fill_s(func, self, value):
     return fill_(self, float(value))
@@ -307,7 +406,7 @@ def _cat(func, tensors, dim=0):
 def _slice_bwd(func, grad_output, input_sizes, dim, start, end, step):
     out = _alloc_like_meta(func, (grad_output, input_sizes, dim, start, end, step), {}, grad_output.device)
     fill_(out, 0.0)
-    ew(out.slice(dim, start, end, step), [grad_output], EW_COPY)
+    ew(aten.slice.Tensor(out, dim, start, end, step), [grad_output], EW_COPY)
     return out
 
 
@@ -379,6 +478,19 @@ def _bn(func, input, weight, bias, running_mean, running_var, training, momentum
     out = torch.empty_like(x)
     ew(out, [x, scale.view(bshape), shift_out.view(bshape)], EW_FMA)
     return out, save_mean, save_invstd
+
+
+@impl(aten.miopen_batch_norm.default)
+def _bn_miopen(func, input, weight, bias, running_mean, running_var, training, exponential_average_factor, epsilon):
+    # ATen's batch_norm picks the MIOpen variant for CUDA inputs before dispatch; same op, same saved
+    # tensors (mean, invstd) as the native_batch_norm path -- only our backward reads them
+    return _bn(None, input, weight, bias, running_mean, running_var, training, exponential_average_factor, epsilon)
+
+
+@impl(aten.miopen_batch_norm_backward.default)
+def _bn_miopen_bwd(func, input, grad_output, weight, running_mean, running_var, save_mean, save_var, epsilon):
+    return _bn_bwd(None, grad_output, input, weight, running_mean, running_var, save_mean, save_var, True, epsilon,
+                   [True, weight is not None, weight is not None])
 
 
 @impl(aten.native_batch_norm_backward.default)
@@ -569,13 +681,82 @@ def _conv_kind(C, O, groups, k, stride, pad, dil):
     square = k[0] == k[1] and stride[0] == stride[1] and pad[0] == pad[1]
     if dil != (1, 1) or not square or stride[0] not in (1, 2) or k[0] > 7:
         return "gconv"
-    if groups == 1 and C % 8 == 0 and O % 8 == 0:
-        return "mfma"
     if groups == C == O and C % 8 == 0 and C <= 2048 and k[0] in (3, 5, 7) and C * k[0] * k[0] * 4 <= 128 * 1024:
         return "dw"
-    if 1 < groups <= 8 and C % (8 * groups) == 0 and O % (8 * groups) == 0:
-        return "grouped_mfma"
+    if groups <= 8:
+        # one MFMA implicit GEMM per group; channel counts off the 8-grid (stems, DenseNet growth widths,
+        # ShuffleNet g2/g3 widths) are zero-padded
+        return "mfma"
     return "gconv"
+
+
+def _pad_c(t: torch.Tensor, c8: int) -> torch.Tensor:
+    """NHWC bf16 [.., C] (possibly a channel slice) -> contiguous [.., c8], zero channels C..c8."""
+    C = t.shape[-1]
+    if C == c8 and t.is_contiguous():
+        return t
+    out = torch.empty(*t.shape[:-1], c8, dtype=torch.bfloat16, device=t.device)
+    if c8 > C:
+        fill_(out[..., C:], 0.0)
+    ew(out[..., :C], [t], EW_COPY)
+    return out
+
+
+def _unpad_c(t: torch.Tensor, c: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if out is None:
+        if t.shape[-1] == c:
+            return t
+        out = torch.empty(*t.shape[:-1], c, dtype=t.dtype, device=t.device)
+    return ew(out, [t[..., :c]], EW_COPY)
+
+
+def _pad_o(w32: torch.Tensor, o8: int) -> torch.Tensor:
+    """fp32 [O, C, R, S] -> contiguous [o8, C, R, S] with zero filters O..o8."""
+    O = w32.shape[0]
+    if O == o8 and w32.is_contiguous():
+        return w32
+    out = torch.empty(o8, *w32.shape[1:], dtype=torch.float32, device=w32.device)
+    if o8 > O:
+        fill_(out[O:], 0.0)
+    ew(out[:O], [w32], EW_COPY)
+    return out
+
+
+def _dense_fwd(xh, w32, st, pd, out=None):
+    """One group: y [N,P,Q,Og] = conv(xh [N,H,W,Cg] NHWC bf16 (a view is fine), w32 [Og,Cg,R,S])."""
+    Og, Cg, R, S = w32.shape
+    C8, O8 = CV.pad8(Cg), CV.pad8(Og)
+    xp = _pad_c(xh, C8)
+    wp = CV.pack_weight(_pad_o(w32, O8), c_pad=C8)
+    y = CV.conv2d_fwd(xp, wp, st, pd, ws=_ws(xh.device, CV.fd_ws_floats(xp.shape, O8, R, S, st, pd)))
+    return _unpad_c(y, Og, out)
+
+
+def _dense_bwd(xh, gy, w32, st, pd, need_dx, need_dw, dx_out=None, dw_out=None):
+    """One group's data / weight gradients; dx written into ``dx_out`` (NHWC view) when given."""
+    Og, Cg, R, S = w32.shape
+    N, H, W = xh.shape[:3]
+    C8, O8 = CV.pad8(Cg), CV.pad8(Og)
+    gyp = _pad_c(gy, O8)
+    dx = dw = None
+    if need_dx:
+        w8 = _pad_o(w32, O8)
+        wp = CV.pack_weight(w8, c_pad=C8)
+        wd = None
+        if CV.dgrad_eligible(O8):
+            wd = torch.empty(CV.dgrad_image_numel(w8.shape, C8), dtype=torch.bfloat16, device=xh.device)
+            CV.dgrad_pack_weights([(w8, wd, st, pd, C8)])
+        xs = (N, H, W, C8)
+        d = CV.conv2d_dgrad(gyp, wp, xs, st, pd, wd=wd, ws=_ws(xh.device, CV.fd_ws_floats(xs, O8, R, S, st, pd)))
+        dx = _unpad_c(d, Cg, dx_out)
+    if need_dw:
+        if dw_out is not None and O8 == Og:
+            dw = CV.conv2d_wgrad(_pad_c(xh, C8), gyp, R, S, st, pd, Cw=Cg, out=dw_out)
+        else:
+            dw = CV.conv2d_wgrad(_pad_c(xh, C8), gyp, R, S, st, pd, Cw=Cg)[:Og]
+            if dw_out is not None:
+                dw = ew(dw_out, [dw], EW_COPY)
+    return dx, dw
 
 
 def _nchw(t_nhwc: torch.Tensor) -> torch.Tensor:
@@ -601,25 +782,20 @@ def _conv(func, input, weight, bias, stride, padding, dilation, transposed, outp
     kind = _conv_kind(C, O, groups, k, st, pd, dl)
     dev = input.device
     w32 = weight if weight.dtype == torch.float32 else ew(torch.empty(weight.shape, device=dev), [weight], EW_COPY)
-    if kind in ("mfma", "dw", "grouped_mfma"):
+    if kind in ("mfma", "dw"):
         xh = _nhwc(_cl_bf16(input))
-        if kind == "mfma":
-            wp = CV.pack_weight(w32.contiguous())
-            y = CV.conv2d_fwd(xh, wp, st[0], pd[0], ws=_ws(dev, CV.fd_ws_floats(xh.shape, O, k[0], k[1], st[0], pd[0])))
-        elif kind == "dw":
+        if kind == "dw":
             y = CV.dwconv_fwd(xh, w32.contiguous(), st[0], pd[0])
+        elif groups == 1:
+            y = _dense_fwd(xh, w32, st[0], pd[0])
         else:
             P = (H + 2 * pd[0] - k[0]) // st[0] + 1
             Q = (W + 2 * pd[1] - k[1]) // st[1] + 1
             y = torch.empty(N, P, Q, O, dtype=torch.bfloat16, device=dev)
             Cg, Og = C // groups, O // groups
             for g in range(groups):
-                xg = ew(torch.empty(N, H, W, Cg, dtype=torch.bfloat16, device=dev), [xh[..., g * Cg:(g + 1) * Cg]],
-                        EW_COPY)
-                wp = CV.pack_weight(w32[g * Og:(g + 1) * Og].contiguous())
-                yg = CV.conv2d_fwd(xg, wp, st[0], pd[0], ws=_ws(dev, CV.fd_ws_floats(xg.shape, Og, k[0], k[1], st[0],
-                                                                                     pd[0])))
-                ew(y[..., g * Og:(g + 1) * Og], [yg], EW_COPY)
+                _dense_fwd(xh[..., g * Cg:(g + 1) * Cg], w32[g * Og:(g + 1) * Og], st[0], pd[0],
+                           out=y[..., g * Og:(g + 1) * Og])
         out = _nchw(y)
     else:
         P = (H + 2 * pd[0] - dl[0] * (k[0] - 1) - 1) // st[0] + 1
@@ -646,41 +822,26 @@ def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dil
     dev = input.device
     w32 = weight if weight.dtype == torch.float32 else ew(torch.empty(weight.shape, device=dev), [weight], EW_COPY)
     gi = gw = gb = None
-    if kind in ("mfma", "dw", "grouped_mfma"):
+    if kind in ("mfma", "dw"):
         xh = _nhwc(_cl_bf16(input))
         gy = _nhwc(_cl_bf16(grad_output))
-        if kind == "mfma":
-            if output_mask[0]:
-                wp = CV.pack_weight(w32.contiguous())
-                wd = None
-                if CV.dgrad_eligible(O):
-                    wd = torch.empty(CV.dgrad_image_numel(w32.shape, C), dtype=torch.bfloat16, device=dev)
-                    CV.dgrad_pack_weights([(w32.contiguous(), wd, st[0], pd[0], C)])
-                gi = _nchw(CV.conv2d_dgrad(gy, wp, xh.shape, st[0], pd[0], wd=wd,
-                                           ws=_ws(dev, CV.fd_ws_floats(xh.shape, O, k[0], k[1], st[0], pd[0]))))
-            if output_mask[1]:
-                gw = CV.conv2d_wgrad(xh, gy, k[0], k[1], st[0], pd[0])
-        elif kind == "dw":
+        if kind == "dw":
             if output_mask[0]:
                 gi = _nchw(CV.dwconv_dgrad(gy, w32.contiguous(), xh.shape, st[0], pd[0]))
             if output_mask[1]:
                 gw = CV.dwconv_wgrad(xh, gy, k[0], st[0], pd[0])
+        elif groups == 1:
+            dx, gw = _dense_bwd(xh, gy, w32, st[0], pd[0], output_mask[0], output_mask[1])
+            gi = _nchw(dx) if dx is not None else None
         else:
             Cg, Og = C // groups, O // groups
             gih = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dev) if output_mask[0] else None
             gw = torch.empty(O, Cg, k[0], k[1], dtype=torch.float32, device=dev) if output_mask[1] else None
             for g in range(groups):
-                xg = ew(torch.empty(N, H, W, Cg, dtype=torch.bfloat16, device=dev), [xh[..., g * Cg:(g + 1) * Cg]],
-                        EW_COPY)
-                gyg = ew(torch.empty(gy.shape[:3] + (Og,), dtype=torch.bfloat16, device=dev),
-                         [gy[..., g * Og:(g + 1) * Og]], EW_COPY)
-                if gih is not None:
-                    wp = CV.pack_weight(w32[g * Og:(g + 1) * Og].contiguous())
-                    dxg = CV.conv2d_dgrad(gyg, wp, xg.shape, st[0], pd[0],
-                                          ws=_ws(dev, CV.fd_ws_floats(xg.shape, Og, k[0], k[1], st[0], pd[0])))
-                    ew(gih[..., g * Cg:(g + 1) * Cg], [dxg], EW_COPY)
-                if gw is not None:
-                    CV.conv2d_wgrad(xg, gyg, k[0], k[1], st[0], pd[0], out=gw[g * Og:(g + 1) * Og])
+                _dense_bwd(xh[..., g * Cg:(g + 1) * Cg], gy[..., g * Og:(g + 1) * Og], w32[g * Og:(g + 1) * Og],
+                           st[0], pd[0], output_mask[0], output_mask[1],
+                           dx_out=gih[..., g * Cg:(g + 1) * Cg] if gih is not None else None,
+                           dw_out=gw[g * Og:(g + 1) * Og] if gw is not None else None)
             gi = _nchw(gih) if gih is not None else None
         if gi is not None and input.dtype != torch.bfloat16:
             gi = ew(torch.empty_like(input), [gi], EW_COPY)
@@ -692,7 +853,11 @@ def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dil
             _nat().z_gconv(_st(dev), 1, zd(gi), zd(w32), zd(grad_output), int(groups), st[0], st[1], pd[0], pd[1])
         if output_mask[1]:
             gw = torch.empty(w32.shape, dtype=torch.float32, device=dev)
-            _nat().z_gconv(_st(dev), 2, zd(input), zd(gw), zd(grad_output), int(groups), st[0], st[1], pd[0], pd[1])
+            P, Q = grad_output.shape[2], grad_output.shape[3]
+            wsf = int(_nat().z_gconv_wgrad_ws_floats(N, P, Q, gw.numel()))
+            ws = CV.wgrad_workspace(dev, wsf)
+            _nat().z_gconv(_st(dev), 2, zd(input), zd(gw), zd(grad_output), int(groups), st[0], st[1], pd[0], pd[1],
+                           ws.data_ptr(), ws.numel())
     if gw is not None and gw.dtype != weight.dtype:
         gw = ew(torch.empty_like(weight), [gw], EW_COPY)
     if output_mask[2]:
@@ -720,8 +885,29 @@ _PASSTHROUGH = _ops(
     "alias", "unsqueeze", "squeeze.dim", "squeeze", "squeeze.dims", "as_strided", "split.Tensor",
     "split_with_sizes", "chunk", "unbind.int", "empty.memory_format", "empty_like", "empty_strided", "new_empty",
     "new_empty_strided", "reshape", "flatten.using_ints", "_reshape_alias", "lift_fresh", "narrow", "unflatten.int",
-    "_local_scalar_dense", "is_same_size", "view.dtype", "set_.source_Storage_storage_offset",
+    "_local_scalar_dense", "is_same_size", "as_strided_", "view.dtype", "set_.source_Storage_storage_offset",
 )
+
+
+class _MixedDtypeConv(TorchFunctionMode):
+    """``F.conv2d`` refuses a bf16 input with an fp32 bias before dispatch (the fp32 master bias of SE
+    gates / classifier convs): route such calls straight to ``aten.convolution``, whose native impl
+    reads each operand in its own dtype."""
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func is F.conv2d or func is torch.conv2d:
+            a = list(args) + [None] * (7 - len(args))
+            x, w, b = a[0], a[1], a[2] if len(args) > 2 else kwargs.get("bias")
+            if (isinstance(x, torch.Tensor) and x.is_cuda and b is not None and b.dtype != x.dtype
+                    and not isinstance(kwargs.get("padding", a[4]), str)):
+                stride = kwargs.get("stride", a[3] if a[3] is not None else 1)
+                padding = kwargs.get("padding", a[4] if a[4] is not None else 0)
+                dilation = kwargs.get("dilation", a[5] if a[5] is not None else 1)
+                groups = kwargs.get("groups", a[6] if a[6] is not None else 1)
+                return aten.convolution.default(x, w, b, list(_pair(stride)), list(_pair(padding)),
+                                                list(_pair(dilation)), False, [0, 0], int(groups))
+        return func(*args, **kwargs)
 
 
 class NativeMode(TorchDispatchMode):
@@ -746,11 +932,16 @@ class NativeMode(TorchDispatchMode):
     def __enter__(self):
         self._prev = NativeMode.current
         NativeMode.current = self
+        self._fn_mode = _MixedDtypeConv()
+        self._fn_mode.__enter__()
         return super().__enter__()
 
     def __exit__(self, *exc):
         NativeMode.current = self._prev
-        return super().__exit__(*exc)
+        try:
+            return super().__exit__(*exc)
+        finally:
+            self._fn_mode.__exit__(*exc)
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}

@@ -72,10 +72,12 @@ def test_conv_kind_routing():
     k3, s1, s2, p1, d1 = (3, 3), (1, 1), (2, 2), (1, 1), (1, 1)
     assert nm._conv_kind(64, 128, 1, k3, s1, p1, d1) == "mfma"
     assert nm._conv_kind(64, 64, 64, k3, s2, p1, d1) == "dw"
-    assert nm._conv_kind(128, 128, 2, k3, s1, p1, d1) == "grouped_mfma"
-    assert nm._conv_kind(3, 64, 1, k3, s1, p1, d1) == "gconv"           # stem: C % 8
+    assert nm._conv_kind(128, 128, 2, k3, s1, p1, d1) == "mfma"         # one MFMA GEMM per group
+    assert nm._conv_kind(3, 64, 1, k3, s1, p1, d1) == "mfma"            # stem: C zero-padded to 8
+    assert nm._conv_kind(36, 12, 1, (1, 1), s1, (0, 0), d1) == "mfma"   # DenseNet growth widths
     assert nm._conv_kind(128, 128, 32, k3, s1, p1, d1) == "gconv"       # many narrow groups
-    assert nm._conv_kind(60, 60, 3, (1, 1), s1, (0, 0), d1) == "gconv"  # ShuffleNet g3 widths
+    assert nm._conv_kind(60, 60, 3, (1, 1), s1, (0, 0), d1) == "mfma"   # ShuffleNet g3 widths, padded
+    assert nm._conv_kind(96, 96, 32, k3, s1, p1, d1) == "gconv"         # DPN cardinality 32
     assert nm._conv_kind(64, 64, 1, k3, (3, 3), p1, d1) == "gconv"      # stride 3
 
 

@@ -1,5 +1,6 @@
 """Per-step time of the generic engine on zoo models without a whole-network native engine:
-PyTorch fp32 (MIOpen) vs PyTorch bf16 channels-last autocast (MIOpen) vs hybrid (native MFMA convs).
+PyTorch fp32 (MIOpen / rocBLAS / ATen) vs the native aten backend (fedmi.ops.native_mode: every op on
+fedmi's HIP kernels), eager and HIP-graph replayed.
 
     python tools/bench_hybrid.py [model ...]      -> one JSON line per (model, mode)
 """
@@ -23,13 +24,9 @@ dev = torch.device("cuda", 0)
 data = make_dataset("synthetic-cifar10", device=dev, n_train=128 * 12, n_test=1000, seed=0)
 for name in MODELS:
     init = build_model(name).state_dict()
-    for mode in ("fp32", "bf16-miopen-graph", "hybrid-eager", "hybrid-graph"):
+    for mode in ("fp32", "native-eager", "native-graph"):
         tr = TorchTrainer(name, data, dev, TrainerConfig(seed=1), init_state=init, hybrid=(mode != "fp32"))
         tr.use_graph = mode.endswith("graph")
-        if mode.startswith("bf16-miopen"):
-            for m in tr.model.modules():
-                m.__dict__.pop("forward", None)      # drop the native override, keep autocast + channels-last
-            tr.native_convs = []
         tr.model.train()
         for i in range(3):
             tr.train_step(128 * i, 128)
@@ -42,7 +39,7 @@ for name in MODELS:
         ms = (time.perf_counter() - t0) / n * 1e3
         tr.evaluate()
         print(json.dumps({"model": name, "mode": mode, "ms_per_step": round(ms, 3),
-                          "native_convs": len(tr.native_convs),
+                          "fallbacks": dict(tr.mode.fallbacks) if tr.mode is not None else None,
                           "eval_acc": round(tr.eval_stats().acc, 2)}), flush=True)
         del tr
         torch.cuda.empty_cache()
