@@ -20,7 +20,7 @@ struct ZTensor {
   long long size[ZMAXD];
   long long stride[ZMAXD];
 };
-void launch_ew(hipStream_t, const ZTensor&, const ZTensor*, int, int, float, float, uint32_t, const int*, int);
+void launch_ew(hipStream_t, const ZTensor&, const ZTensor*, int, int, float, float, uint32_t, const int*, int, int);
 void launch_ctr_bump(hipStream_t, int*);
 long long reduce_rows_ws_floats(long long, int);
 void launch_reduce_rows(hipStream_t, const void*, int, long long, const void*, int, long long, const float*, int,
@@ -72,13 +72,13 @@ static ZTensor zt(const py::object& o) {
 void fedmi_bind_zoo(py::module_& m) {
   // vmask < 0: scalar launch; otherwise the 8-wide vector launch (descriptors pre-divided by the caller)
   m.def("z_ew", [](uintptr_t st, py::object out, std::vector<py::object> ins, int op, float s0, float s1,
-                   uint32_t seed, uintptr_t ctr, int vmask) {
+                   uint32_t seed, uintptr_t ctr, int vmask, int vw) {
     std::vector<ZTensor> v;
     for (auto& o : ins) v.push_back(zt(o));
     fedmi::launch_ew(S(st), zt(out), v.data(), (int)v.size(), op, s0, s1, seed, reinterpret_cast<const int*>(ctr),
-                     vmask);
+                     vmask, vw);
   }, py::arg("st"), py::arg("out"), py::arg("ins"), py::arg("op"), py::arg("s0"), py::arg("s1"), py::arg("seed"),
-        py::arg("ctr"), py::arg("vmask") = -1);
+        py::arg("ctr"), py::arg("vmask") = -1, py::arg("vw") = 8);
   m.def("z_ctr_bump", [](uintptr_t st, uintptr_t ctr) { fedmi::launch_ctr_bump(S(st), reinterpret_cast<int*>(ctr)); });
   m.def("z_reduce", [](uintptr_t st, py::object outer, py::object inner, py::object outer_b, py::object inner_b,
                        uintptr_t a, int a_dt, uintptr_t b, int b_dt, uintptr_t shift, uintptr_t acc, uintptr_t acc2,

@@ -111,54 +111,78 @@ FEDMI_DEV float ew_apply(const EwArgs& a, float x0, float x1, float x2, float x3
   }
 }
 
-FEDMI_DEV void ew_load8(const ZTensor& t, long long off, bool contiguous, float v[8]) {
-  if (!contiguous) {
-    const float s = zload(t, off);
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// VW consecutive elements (VW = 8 or 4) as 16- / 8-byte bf16 or 16-byte fp32 vector accesses
+template <int VW>
+FEDMI_DEV void vload(const void* p, int dt, long long off, float* v) {
+  if (dt == 1) {
+    if constexpr (VW == 8) {
+      const bf16x8 q = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(p) + off);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = s;
-  } else if (t.dtype == 1) {
-    const bf16x8 q = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(t.p) + off);
+      for (int u = 0; u < 8; ++u) v[u] = (float)q[u];
+    } else {
+      const bf16x4 q = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const bf16*>(p) + off);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = (float)q[u];
+      for (int u = 0; u < 4; ++u) v[u] = (float)q[u];
+    }
   } else {
-    const f32x4 q0 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(t.p) + off);
-    const f32x4 q1 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(t.p) + off + 4);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) { v[u] = q0[u]; v[u + 4] = q1[u]; }
+    for (int h = 0; h < VW / 4; ++h) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + off + 4 * h);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[4 * h + u] = q[u];
+    }
   }
 }
 
-// 8 consecutive innermost elements per thread: 16-byte loads / stores (host-checked alignment);
-// the descriptors' innermost size is already divided by 8 and unit strides scaled by 8
-__global__ __launch_bounds__(256) void ew_vec_kernel(EwArgs a, long long n8) {
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
-    float x[5][8];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      if (a.in[k].p) {
-        ew_load8(a.in[k], zoffset(a.o, a.in[k], i), (a.vmask >> k) & 1, x[k]);
-      } else {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) x[k][u] = 0.f;
-      }
-    }
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = ew_apply(a, x[0][u], x[1][u], x[2][u], x[3][u], x[4][u]);
-    const long long oo = zoffset(a.o, a.o, i);
-    if (a.o.dtype == 1) {
+template <int VW>
+FEDMI_DEV void vstore(void* p, int dt, long long off, const float* v) {
+  if (dt == 1) {
+    if constexpr (VW == 8) {
       bf16x8 q;
 #pragma unroll
       for (int u = 0; u < 8; ++u) q[u] = (bf16)v[u];
-      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.o.p) + oo) = q;
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(p) + off) = q;
     } else {
-      f32x4 q0, q1;
+      bf16x4 q;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) { q0[u] = v[u]; q1[u] = v[u + 4]; }
-      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.o.p) + oo) = q0;
-      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.o.p) + oo + 4) = q1;
+      for (int u = 0; u < 4; ++u) q[u] = (bf16)v[u];
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p) + off) = q;
     }
+  } else {
+#pragma unroll
+    for (int h = 0; h < VW / 4; ++h) {
+      f32x4 q;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = v[4 * h + u];
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p) + off + 4 * h) = q;
+    }
+  }
+}
+
+// VW consecutive innermost elements per thread (host-checked alignment); the descriptors' innermost
+// size is already divided by VW and unit strides scaled by VW; a broadcast input (vmask bit clear)
+// is one scalar load
+template <int VW>
+__global__ __launch_bounds__(256) void ew_vec_kernel(EwArgs a, long long nv) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    float x[5][VW];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      if (a.in[k].p && ((a.vmask >> k) & 1)) {
+        vload<VW>(a.in[k].p, a.in[k].dtype, zoffset(a.o, a.in[k], i), x[k]);
+      } else {
+        const float sv = a.in[k].p ? zload(a.in[k], zoffset(a.o, a.in[k], i)) : 0.f;
+#pragma unroll
+        for (int u = 0; u < VW; ++u) x[k][u] = sv;
+      }
+    }
+    float v[VW];
+#pragma unroll
+    for (int u = 0; u < VW; ++u) v[u] = ew_apply(a, x[0][u], x[1][u], x[2][u], x[3][u], x[4][u]);
+    vstore<VW>(a.o.p, a.o.dtype, zoffset(a.o, a.o, i), v);
   }
 }
 
@@ -250,95 +274,99 @@ __global__ __launch_bounds__(256) void reduce_kernel(RdArgs r, long long n_outer
   }
 }
 
+// sum over slabs of part[slab * pitch + i], 64 elements x 4 slab lanes per block, lanes combined in
+// a fixed order (deterministic); returns the total on lane 0 (others: 0)
+FEDMI_DEV float ordered_slab_sum(const float* part, int slabs, long long pitch, long long i, bool valid) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x >> 6, el = threadIdx.x & 63;
+  float v = 0.f;
+  if (valid) {
+#pragma unroll 8
+    for (int b = lane; b < slabs; b += 4) v += part[(long long)b * pitch + i];
+  }
+  red[lane][el] = v;
+  __syncthreads();
+  return lane == 0 ? red[0][el] + red[1][el] + red[2][el] + red[3][el] : 0.f;
+}
+
 // ---- row reduction of a [M, C] row-major matrix (ld = row stride), C % 8 == 0 ------------------
 // The channels-last case of the BN moments / bias gradients: a thread owns 8 channels (one 16-byte
 // load per row), RL = 256 / (C/8) row lanes per block, grid.y row slabs; per-slab partials go to
 // `part` [slabs][2][C] and a finalize pass adds them in slab order (deterministic).
-FEDMI_DEV void rows_load8(const void* p, int dt, long long off, float v[8]) {
-  if (dt == 1) {
-    const bf16x8 q = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(p) + off);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = (float)q[u];
-  } else {
-    const f32x4 q0 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + off);
-    const f32x4 q1 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + off + 4);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) { v[u] = q0[u]; v[u + 4] = q1[u]; }
-  }
-}
-
+template <int VW>
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_dt, long long lda, const void* b,
                                                           int b_dt, long long ldb, const float* shift, int C,
                                                           long long M, int op, float* part) {
-  __shared__ float red[2][256 * 8];
-  const int VL = C / 8;
+  __shared__ float red[2][256 * VW];
+  const int VL = C / VW;
   const int vt = min(VL, 256);
   const int RL = 256 / vt;
   const int v = blockIdx.x * vt + (threadIdx.x % vt);
   const int rl = threadIdx.x / vt;
   const bool act = rl < RL && v < VL;
-  float s1[8], s2[8];
+  float s1[VW], s2[VW];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) { s1[u] = 0.f; s2[u] = 0.f; }
+  for (int u = 0; u < VW; ++u) { s1[u] = 0.f; s2[u] = 0.f; }
   if (act) {
-    float sh[8];
+    float sh[VW];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) sh[u] = shift ? shift[v * 8 + u] : 0.f;
+    for (int u = 0; u < VW; ++u) sh[u] = shift ? shift[v * VW + u] : 0.f;
     const long long per = (M + gridDim.y - 1) / gridDim.y;
     const long long r0 = (long long)blockIdx.y * per, r1 = min(M, r0 + per);
     for (long long r = r0 + rl; r < r1; r += RL) {
-      float x[8];
-      rows_load8(a, a_dt, r * lda + v * 8, x);
+      float x[VW];
+      vload<VW>(a, a_dt, r * lda + v * VW, x);
       if (op == RD_SUM) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s1[u] += x[u];
+        for (int u = 0; u < VW; ++u) s1[u] += x[u];
       } else if (op == RD_SUMSQ_SHIFT) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) { const float d = x[u] - sh[u]; s1[u] += d; s2[u] += d * d; }
+        for (int u = 0; u < VW; ++u) { const float d = x[u] - sh[u]; s1[u] += d; s2[u] += d * d; }
       } else {
-        float y[8];
-        rows_load8(b, b_dt, r * ldb + v * 8, y);
+        float y[VW];
+        vload<VW>(b, b_dt, r * ldb + v * VW, y);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) { s1[u] += x[u]; s2[u] += x[u] * (y[u] - sh[u]); }
+        for (int u = 0; u < VW; ++u) { s1[u] += x[u]; s2[u] += x[u] * (y[u] - sh[u]); }
       }
     }
   }
   // tree over the row lanes of each channel vector
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    red[0][threadIdx.x * 8 + u] = s1[u];
-    red[1][threadIdx.x * 8 + u] = s2[u];
+  for (int u = 0; u < VW; ++u) {
+    red[0][threadIdx.x * VW + u] = s1[u];
+    red[1][threadIdx.x * VW + u] = s2[u];
   }
   __syncthreads();
   if (rl == 0 && v < VL) {
     for (int k = 1; k < RL; ++k) {
       const int t = k * vt + (threadIdx.x % vt);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) { s1[u] += red[0][t * 8 + u]; s2[u] += red[1][t * 8 + u]; }
+      for (int u = 0; u < VW; ++u) { s1[u] += red[0][t * VW + u]; s2[u] += red[1][t * VW + u]; }
     }
     float* dst = part + (long long)blockIdx.y * 2 * C;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) { dst[v * 8 + u] = s1[u]; dst[C + v * 8 + u] = s2[u]; }
+    for (int u = 0; u < VW; ++u) { dst[v * VW + u] = s1[u]; dst[C + v * VW + u] = s2[u]; }
   }
 }
 
+// acc[c] += sum_slab part[slab][0][c] (and acc2 from part[slab][1][c]), slab order
 __global__ __launch_bounds__(256) void reduce_rows_finalize(const float* part, int slabs, int C, int two, float* acc,
                                                             float* acc2) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float t1 = 0.f, t2 = 0.f;
-  for (int b = 0; b < slabs; ++b) {
-    t1 += part[(long long)b * 2 * C + c];
-    if (two) t2 += part[(long long)b * 2 * C + C + c];
-  }
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float t1 = ordered_slab_sum(part, slabs, 2LL * C, c, c < C);
+  __syncthreads();
+  const float t2 = two ? ordered_slab_sum(part + C, slabs, 2LL * C, c, c < C) : 0.f;
+  if ((threadIdx.x >> 6) || c >= C) return;
   acc[c] += t1;
   if (two) acc2[c] += t2;
 }
 
+int rows_vw(int C) { return C % 8 == 0 ? 8 : 4; }
+
 int rows_slabs(long long M, int C) {
-  const int VL = C / 8, vt = VL < 256 ? VL : 256, RL = 256 / vt;
+  const int VL = C / rows_vw(C), vt = VL < 256 ? VL : 256, RL = 256 / vt;
   const long long tiles = (VL + vt - 1) / vt;
-  long long sl = M / ((long long)RL * 32);          // >= 32 rows per row lane
+  long long sl = M / ((long long)RL * 16);          // >= 16 rows per row lane
   const long long cap = (2048 + tiles - 1) / tiles;  // ~2048 blocks in flight at most
   if (sl > cap) sl = cap;
   if (sl < 1) sl = 1;
@@ -775,77 +803,80 @@ __global__ __launch_bounds__(256) void gconv_dgrad_kernel(GConv g) {
     if (c0 + j < Cg) zstore(g.x, xo + (long long)(grp * Cg + c0 + j) * g.x.stride[1], acc[j]);
 }
 
-// partial[slab][o][c][r][s] = sum over images [slab*nb, +nb) and all (p, q).  A thread owns one
-// (o, r, s) and 8 consecutive input channels (one bf16x8 load per pixel when x is channels-last);
-// grid (thread blocks over (o, rs, channel block), groups, slabs)
-__global__ __launch_bounds__(256) void gconv_wgrad_kernel(GConv g, float* part, int nb) {
+// partial[slab][O][Cg][R][S] = sum over the output rows [slab*rps, +rps) of the flattened (n, p)
+// space.  A thread owns one (o, r, s) and 8 consecutive input channels of o's group (one bf16x8 load
+// per pixel when x is channels-last); blocks tile the flattened (o, rs, channel block) space of ALL
+// groups, grid.y = row slabs -- enough lanes in flight even for 8-wide groups.
+__global__ __launch_bounds__(256) void gconv_wgrad_kernel(GConv g, float* part, int rps) {
   const long long N = g.x.size[0], H = g.x.size[2], W = g.x.size[3];
   const long long O = g.y.size[1], P = g.y.size[2], Q = g.y.size[3];
   const int Cg = (int)g.w.size[1], Og = (int)(O / g.G), RS = g.R * g.S;
   const int CB = (Cg + 7) / 8;
-  const int grp = blockIdx.y;
-  const long long Wg = (long long)Og * RS * Cg;
   const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (long long)Og * RS * CB) return;
-  // e = (o * RS + rs) * CB + cb
+  if (e >= O * RS * CB) return;
+  // e = (og * RS + rs) * CB + cb, og = the global output channel
   const int cb = (int)(e % CB);
   const int rs = (int)((e / CB) % RS);
-  const int o = (int)(e / ((long long)CB * RS));
+  const int og = (int)(e / ((long long)CB * RS));
+  const int grp = og / Og;
   const int r = rs / g.S, s = rs % g.S;
   const int c0 = cb * 8, cn = min(8, Cg - c0);
   const bool vec = g.vec_x && cn == 8;
-  const long long n0 = (long long)blockIdx.z * nb, n1 = min(N, n0 + nb);
   const long long xc = (long long)(grp * Cg + c0) * g.x.stride[1];
-  const long long yc = (long long)(grp * Og + o) * g.y.stride[1];
+  const long long yc = (long long)og * g.y.stride[1];
+  const long long row0 = (long long)blockIdx.y * rps, row1 = min(N * P, row0 + rps);
   float acc[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) acc[u] = 0.f;
-  for (long long n = n0; n < n1; ++n) {
-    for (long long p = 0; p < P; ++p) {
-      const long long h = p * g.st_h - g.pad_h + r;
-      if (h < 0 || h >= H) continue;
-      const long long xr = n * g.x.stride[0] + h * g.x.stride[2] + xc;
-      const long long yr = n * g.y.stride[0] + p * g.y.stride[2] + yc;
-      for (long long q = 0; q < Q; ++q) {
-        const long long w = q * g.st_w - g.pad_w + s;
-        if (w < 0 || w >= W) continue;
-        const float dv = zload(g.y, yr + q * g.y.stride[3]);
-        float xv[8];
-        if (vec) {
-          load8(g.x, xr + w * g.x.stride[3], 1, true, xv);
-        } else {
+  for (long long row = row0; row < row1; ++row) {
+    const long long n = row / P, p = row - n * P;
+    const long long h = p * g.st_h - g.pad_h + r;
+    if (h < 0 || h >= H) continue;
+    const long long xr = n * g.x.stride[0] + h * g.x.stride[2] + xc;
+    const long long yr = n * g.y.stride[0] + p * g.y.stride[2] + yc;
+    for (long long q = 0; q < Q; ++q) {
+      const long long w = q * g.st_w - g.pad_w + s;
+      if (w < 0 || w >= W) continue;
+      const float dv = zload(g.y, yr + q * g.y.stride[3]);
+      float xv[8];
+      if (vec) {
+        load8(g.x, xr + w * g.x.stride[3], 1, true, xv);
+      } else {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) xv[u] = u < cn ? zload(g.x, xr + w * g.x.stride[3] + u * g.x.stride[1]) : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc[u] += dv * xv[u];
+        for (int u = 0; u < 8; ++u) xv[u] = u < cn ? zload(g.x, xr + w * g.x.stride[3] + u * g.x.stride[1]) : 0.f;
       }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += dv * xv[u];
     }
   }
-  // partial layout: [slab][grp][o][c][r][s] = the PyTorch weight layout per slab
-  float* dst = part + (long long)blockIdx.z * g.G * Wg + (long long)grp * Wg;
-  for (int u = 0; u < cn; ++u) dst[((long long)o * Cg + c0 + u) * RS + rs] = acc[u];
+  float* dst = part + (long long)blockIdx.y * O * Cg * RS;
+  for (int u = 0; u < cn; ++u) dst[((long long)og * Cg + c0 + u) * RS + rs] = acc[u];
 }
 
-// dw[i] = sum_slab part[slab][i] in slab order (dw: any strides over the contiguous [O, Cg, R, S] order)
+// dw[i] = sum_slab part[slab][i] (dw: any strides over the contiguous [O, Cg, R, S] order)
 __global__ __launch_bounds__(256) void gconv_wgrad_sum_kernel(const float* part, int slabs, long long total,
                                                               ZTensor dw) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  float v = 0.f;
-  for (int b = 0; b < slabs; ++b) v += part[(long long)b * total + i];
+  const long long i = (long long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const float v = ordered_slab_sum(part, slabs, total, i, i < total);
+  if ((threadIdx.x >> 6) || i >= total) return;
   const long long RS = dw.size[2] * dw.size[3], Cg = dw.size[1];
   const long long rs = i % RS, c = (i / RS) % Cg, o = i / (RS * Cg);
   zstore(dw, o * dw.stride[0] + c * dw.stride[1] + (rs / dw.size[3]) * dw.stride[2] + (rs % dw.size[3]) * dw.stride[3], v);
 }
 
-// images per wgrad slab: >= ~2048 pixels of work per thread block
-int gconv_slab_images(long long N, long long P, long long Q) {
-  long long pq = P * Q > 0 ? P * Q : 1;
-  long long nb = (2048 + pq - 1) / pq;
-  if (nb < 1) nb = 1;
-  if (nb > N) nb = N;
-  return (int)nb;
+// output rows per wgrad slab (>= ~256 pixels per thread) and the slab count, with the partials
+// capped at 8M floats
+void gconv_slabs(long long N, long long P, long long Q, long long total, long long* rps, long long* slabs) {
+  const long long rows = N * P > 0 ? N * P : 1;
+  long long r = (256 + Q - 1) / (Q > 0 ? Q : 1);
+  if (r < 1) r = 1;
+  long long sl = (rows + r - 1) / r;
+  const long long cap = total > 0 ? (8LL << 20) / total : 1;
+  if (sl > cap) sl = cap > 0 ? cap : 1;
+  if (sl > 65535) sl = 65535;
+  r = (rows + sl - 1) / sl;
+  *rps = r;
+  *slabs = (rows + r - 1) / r;
 }
 
 int grid1(long long n) {
@@ -860,7 +891,7 @@ int grid1(long long n) {
 namespace fedmi {
 
 void launch_ew(hipStream_t st, const ZTensor& o, const ZTensor* ins, int nin, int op, float s0, float s1,
-               uint32_t seed, const int* ctr, int vmask) {
+               uint32_t seed, const int* ctr, int vmask, int vw) {
   if (nin > 5) throw std::invalid_argument("ew: at most 5 inputs");
   EwArgs a{};
   a.o = o;
@@ -876,7 +907,12 @@ void launch_ew(hipStream_t st, const ZTensor& o, const ZTensor* ins, int nin, in
   if (n <= 0) return;
   if (vmask >= 0) {
     if (op == EW_BERN) throw std::invalid_argument("ew: no vector launch for bernoulli");
-    hipLaunchKernelGGL(ew_vec_kernel, dim3(grid1(n)), dim3(256), 0, st, a, n);
+    if (vw == 8)
+      hipLaunchKernelGGL(ew_vec_kernel<8>, dim3(grid1(n)), dim3(256), 0, st, a, n);
+    else if (vw == 4)
+      hipLaunchKernelGGL(ew_vec_kernel<4>, dim3(grid1(n)), dim3(256), 0, st, a, n);
+    else
+      throw std::invalid_argument("ew: vector width 8 or 4");
   } else {
     hipLaunchKernelGGL(ew_kernel, dim3(grid1(n)), dim3(256), 0, st, a, n);
   }
@@ -912,13 +948,16 @@ long long reduce_rows_ws_floats(long long M, int C) { return (long long)rows_sla
 void launch_reduce_rows(hipStream_t st, const void* a, int a_dt, long long lda, const void* b, int b_dt,
                         long long ldb, const float* shift, int C, long long M, int op, float* part, long long part_floats,
                         float* acc, float* acc2) {
-  if (C % 8 || C <= 0 || M <= 0) throw std::invalid_argument("reduce_rows: C % 8 == 0 and M > 0 required");
+  if (C % 4 || C <= 0 || M <= 0) throw std::invalid_argument("reduce_rows: C % 4 == 0 and M > 0 required");
   const int slabs = rows_slabs(M, C);
   if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("reduce_rows: workspace too small");
-  const int VL = C / 8, vt = VL < 256 ? VL : 256;
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((VL + vt - 1) / vt), (unsigned)slabs), dim3(256), 0, st, a,
-                     a_dt, lda, b, b_dt, ldb, shift, C, M, op, part);
-  hipLaunchKernelGGL(reduce_rows_finalize, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, part, slabs, C,
+  const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
+  const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
+  if (vw == 8)
+    hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part);
+  else
+    hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part);
+  hipLaunchKernelGGL(reduce_rows_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C,
                      op != RD_SUM ? 1 : 0, acc, acc2);
   check_hip(hipGetLastError(), "reduce_rows");
 }
@@ -998,8 +1037,9 @@ void launch_ce_stats(hipStream_t st, const ZTensor& logits, const long long* y, 
 }
 
 long long gconv_wgrad_ws_floats(long long N, long long P, long long Q, long long w_numel) {
-  const int nb = gconv_slab_images(N, P, Q);
-  return ((N + nb - 1) / nb) * w_numel;
+  long long rps, slabs;
+  gconv_slabs(N, P, Q, w_numel, &rps, &slabs);
+  return slabs * w_numel;
 }
 
 void launch_gconv(hipStream_t st, int mode, const ZTensor& x, const ZTensor& w, const ZTensor& y, int G, int sth,
@@ -1034,13 +1074,13 @@ void launch_gconv(hipStream_t st, int mode, const ZTensor& x, const ZTensor& w, 
   } else {
     const long long N = x.size[0], P = y.size[2], Q = y.size[3];
     const long long total = w.size[0] * w.size[1] * w.size[2] * w.size[3];
-    const int nb = gconv_slab_images(N, P, Q);
-    const long long slabs = (N + nb - 1) / nb;
+    long long rps, slabs;
+    gconv_slabs(N, P, Q, total, &rps, &slabs);
     if (!ws || ws_floats < slabs * total) throw std::invalid_argument("gconv wgrad: workspace too small");
-    const long long threads = Og * g.R * g.S * ((Cg + 7) / 8);
-    hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((unsigned)((threads + 255) / 256), G, (unsigned)slabs), dim3(256), 0, st,
-                       g, ws, nb);
-    hipLaunchKernelGGL(gconv_wgrad_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, ws, (int)slabs,
+    const long long threads = O * g.R * g.S * ((Cg + 7) / 8);
+    hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((unsigned)((threads + 255) / 256), (unsigned)slabs), dim3(256), 0, st,
+                       g, ws, (int)rps);
+    hipLaunchKernelGGL(gconv_wgrad_sum_kernel, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, st, ws, (int)slabs,
                        total, w);
   }
   check_hip(hipGetLastError(), "gconv");

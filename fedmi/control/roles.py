@@ -72,8 +72,11 @@ class BackupServer(P.TrainerServicer):
     def CheckIfPrimaryUp(self, request, context):
         with self._lock:
             self.last_ping = time.monotonic()
+            first = not self.primary_seen
             self.primary_seen = True
             demote = request.req == "1" and self.coordinator is not None
+        if first:
+            self.metrics.write(role="backup", event="primary_seen")
         if demote:
             self._log("primary is back (recovering=1): stepping down")
             threading.Thread(target=self.demote, name="fedmi-demote", daemon=True).start()

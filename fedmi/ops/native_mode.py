@@ -120,28 +120,34 @@ def ew(out: torch.Tensor, ins, op: int, s0: float = 0.0, s1: float = 0.0, seed: 
     else:
         nshape, nstr = coalesce(shape, [list(o.stride())] + [list(t.stride()) for t in ts])
     allt = [o] + ts
-    vmask = _vec_mask(nshape, nstr, allt) if op != EW_BERN else -1
+    vw, vmask = 8, -1
+    if op != EW_BERN:
+        for vw in (8, 4):
+            vmask = _vec_mask(nshape, nstr, allt, vw)
+            if vmask >= 0:
+                break
     if vmask >= 0:
-        nshape = nshape[:-1] + [nshape[-1] // 8]
-        nstr = [st[:-1] + [st[-1] * 8] for st in nstr]
+        nshape = nshape[:-1] + [nshape[-1] // vw]
+        nstr = [st[:-1] + [st[-1] * vw] for st in nstr]
     descs = [(t.data_ptr(), _DT[t.dtype], nshape, st) for t, st in zip(allt, nstr)]
     _nat().z_ew(_st(out.device), descs[0], descs[1:], op, float(s0), float(s1), int(seed) & 0xFFFFFFFF,
-                0 if ctr is None else ctr.data_ptr(), vmask)
+                0 if ctr is None else ctr.data_ptr(), vmask, vw)
     return out
 
 
-def _vec_mask(shape, strides, ts) -> int:
-    """Bit k (input k) set if that operand is contiguous over groups of 8 innermost elements, 0 bit = a
-    broadcast operand; -1 = the 8-wide vector launch does not apply (odd sizes, misalignment, int64, an
-    output that is not unit-stride innermost)."""
-    if shape[-1] % 8:
+def _vec_mask(shape, strides, ts, vw: int = 8) -> int:
+    """Bit k (input k) set if that operand is contiguous over groups of ``vw`` innermost elements, bit
+    clear = a broadcast operand; -1 = the vector launch does not apply (odd sizes, misalignment,
+    int64, an output that is not unit-stride innermost, fp32 with vw 4 below 16-byte alignment)."""
+    if shape[-1] % vw:
         return -1
     mask = 0
     for k, (t, st) in enumerate(zip(ts, strides)):
         inner = st[-1]
         if inner == 0 and k > 0:
             continue
-        if inner != 1 or t.dtype == torch.int64 or t.data_ptr() % 16 or any(v % 8 for v in st[:-1]):
+        align = 16 if (t.dtype == torch.float32 or vw == 8) else 8
+        if inner != 1 or t.dtype == torch.int64 or t.data_ptr() % align or any(v % vw for v in st[:-1]):
             return -1
         if k > 0:
             mask |= 1 << (k - 1)
@@ -232,10 +238,12 @@ def reduce_sum(a: torch.Tensor, dims, acc: torch.Tensor, op: int = RD_SUM, b: Op
 
 
 def _rows_ok(oshape, ostr, ishape, istr, ops) -> bool:
-    if len(oshape) != 1 or len(ishape) != 1 or oshape[0] % 8 or ishape[0] < 1:
+    if len(oshape) != 1 or len(ishape) != 1 or oshape[0] % 4 or ishape[0] < 1:
         return False
+    vw = 8 if oshape[0] % 8 == 0 else 4
     for t, os_, is_ in zip(ops, ostr, istr):
-        if os_[0] != 1 or is_[0] % 8 or t.dtype not in (torch.float32, torch.bfloat16) or t.data_ptr() % 16:
+        align = 16 if (t.dtype == torch.float32 or vw == 8) else 8
+        if os_[0] != 1 or is_[0] % vw or t.dtype not in (torch.float32, torch.bfloat16) or t.data_ptr() % align:
             return False
     return True
 

@@ -128,9 +128,19 @@ CHANNEL_OPTIONS = [
 ]
 
 
+# A peer that is not up yet (a backup still importing, a restarting client) must not push the
+# channel into gRPC's default exponential reconnect backoff (up to 120 s): liveness pings and
+# rejoin probes would then miss the peer for minutes.  Reconnect at most every second.
+RECONNECT_OPTIONS = [
+    ("grpc.initial_reconnect_backoff_ms", 100),
+    ("grpc.min_reconnect_backoff_ms", 100),
+    ("grpc.max_reconnect_backoff_ms", 1000),
+]
+
+
 def make_channel(address: str, gzip: bool = False) -> grpc.Channel:
     comp = grpc.Compression.Gzip if gzip else None
-    return grpc.insecure_channel(address, options=CHANNEL_OPTIONS, compression=comp)
+    return grpc.insecure_channel(address, options=CHANNEL_OPTIONS + RECONNECT_OPTIONS, compression=comp)
 
 
 def make_server(max_workers: int = 10, gzip: bool = False) -> grpc.Server:

@@ -81,6 +81,9 @@ def _primary_sigkill_and_recover(tmp_path, device):
         primary = spawn_server(tmp_path, "--p", "y", *common, "--metrics", str(tmp_path / "primary.jsonl"),
                                log_path=tmp_path / "primary.log")
         wait_for(lambda: len(_rounds(tmp_path / "primary.jsonl")) >= 4, timeout=120)
+        # the backup's watchdog is armed (it has had a ping) before the kill
+        wait_for(lambda: [r for r in read_jsonl(tmp_path / "backup.jsonl") if r.get("event") == "primary_seen"],
+                 timeout=15)
         # the backup saw the primary (its watchdog is armed) and never acted as primary before the kill
         assert not [r for r in read_jsonl(tmp_path / "backup.jsonl") if r.get("event") == "promoted"]
         wait_for(lambda: (tmp_path / "srv" / "Backup" / ck.OPTIMIZED_MODEL).exists(), timeout=30)

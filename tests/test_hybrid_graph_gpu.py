@@ -37,20 +37,23 @@ def test_hybrid_graph_matches_eager(gpu_device, name, monkeypatch):
     assert abs(se.loss - sg.loss) < 0.05 * se.loss, (se.loss, sg.loss)
 
 
-def test_hybrid_default_is_eager_and_stable_at_reference_lr(gpu_device, monkeypatch):
-    """The default hybrid engine (eager; graph replay is opt-in after the NaN recorded in
-    profiles/hybrid_graph_nan_diag_r1.txt) trains SENet18 past step 150 at lr 0.1 with finite state."""
+@pytest.mark.parametrize("name", ["SENet18", "EfficientNetB0", "RegNetY_400MF"])
+def test_hybrid_default_graph_is_stable_at_reference_lr(gpu_device, name, monkeypatch):
+    """The default hybrid engine replays a captured graph of the native step; the three models whose
+    round-1 replay went NaN (autocast / ATen backend, profiles/hybrid_graph_nan_diag_r1.txt) train
+    160 SGD steps at lr 0.1 with finite state."""
     from fedmi.engine import build_trainer
 
     monkeypatch.delenv("FEDMI_HYBRID_GRAPH", raising=False)
     data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=128 * 40, n_test=200, seed=0)
-    tr = build_trainer("SENet18", data, gpu_device, TrainerConfig(lr=0.1, seed=1))
-    assert tr.hybrid and not tr.use_graph
+    tr = build_trainer(name, data, gpu_device, TrainerConfig(lr=0.1, seed=1))
+    assert tr.hybrid and tr.use_graph
     tr.set_schedule(*contiguous_schedule(len(data.train), 128))
     losses = []
     for _ in range(4):                      # 160 SGD steps
         tr.train_epoch()
         losses.append(tr.train_stats().loss)
     torch.cuda.synchronize()
+    assert tr._graph is not None and not tr.mode.fallbacks
     assert all(v == v for v in losses) and torch.isfinite(tr.float_state()).all(), losses
     assert losses[-1] < losses[0], losses

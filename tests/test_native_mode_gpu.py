@@ -143,6 +143,33 @@ def test_se_concat_slice(gpu_device):
     _run_pair(gpu_device, _SE, (8, 32, 8, 8))
 
 
+@pytest.mark.parametrize("C", [8, 12, 36, 7, 64])
+def test_elementwise_and_reductions_layouts(gpu_device, C):
+    """Vector (8 / 4 wide) and scalar launches: channel slices at odd offsets, broadcast operands,
+    fp32 / bf16 mixes, channels-last row reductions and generic reductions, against fp32 torch."""
+    torch.manual_seed(C)
+    big = _bf(torch.randn(4, C + 5, 6, 7, device=gpu_device)).contiguous(memory_format=torch.channels_last)
+    xs = big[:, 3:3 + C]                                   # channel slice: unaligned base
+    xb = big.bfloat16()[:, 3:3 + C]
+    b = torch.randn(C, device=gpu_device)
+    mode = _mode()
+    with mode:
+        y = xb * b.view(1, C, 1, 1) + xb
+        z = torch.relu(y)
+        s = z.sum((0, 2, 3))
+        m = z.float().mean((2, 3), keepdim=True)
+        cl = z.contiguous(memory_format=torch.channels_last)
+        sc = cl.sum((0, 2, 3))
+        w = xs * 0.5 + 1.0
+    ref_y = xs * b.view(1, C, 1, 1) + xs
+    ref_z = torch.relu(ref_y)
+    assert not mode.fallbacks
+    assert _rel(y, ref_y) < 1e-2 and _rel(z, ref_z) < 1e-2
+    assert _rel(s, ref_z.sum((0, 2, 3))) < 1e-2 and _rel(sc, ref_z.sum((0, 2, 3))) < 1e-2
+    assert _rel(m, ref_z.mean((2, 3), keepdim=True)) < 1e-2
+    assert torch.allclose(w, xs * 0.5 + 1.0)
+
+
 @pytest.mark.parametrize("pool", ["max3s2p1", "max2", "avg2", "avg3s1p1", "avg3s2p1_ceil_nopad", "avg4"])
 def test_pools(gpu_device, pool):
     mk = {"max3s2p1": lambda: nn.MaxPool2d(3, 2, 1), "max2": lambda: nn.MaxPool2d(2),
