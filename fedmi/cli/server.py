@@ -40,6 +40,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--store-port", type=int, default=0)
     ap.add_argument("--min-clients", type=int, default=1)
     ap.add_argument("--metrics", default=None, help="JSONL metrics file")
+    ap.add_argument("--ckpt-fetch-interval", type=float, default=0.05,
+                    help="collective mode: pull rank 0's newest checkpoint in the background at most this often "
+                         "(s) instead of inside every StartTrain reply; <= 0: upload in every reply")
     ap.add_argument("--ckpt-sync-every", type=int, default=0,
                     help="rank 0 uploads THAT round's checkpoint every k rounds (0: pipelined by one round, "
                          "synchronous on the final round)")
@@ -54,6 +57,7 @@ def main(argv=None) -> int:
                             root=a.root, primary=(a.p == "y"), train_timeout_s=a.train_timeout,
                             rpc_timeout_s=a.rpc_timeout, heartbeat_s=a.heartbeat, store_host=a.store_host,
                             store_port=a.store_port, min_clients=a.min_clients, ckpt_sync_every=a.ckpt_sync_every,
+                            ckpt_fetch_interval_s=a.ckpt_fetch_interval,
                             backup_address=f"{a.backupAddress}:{a.backupPort}")
     metrics = MetricsLog(a.metrics)
     stop = threading.Event()

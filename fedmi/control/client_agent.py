@@ -48,6 +48,8 @@ META_ROUND = "x-fedmi-round"
 META_GEN = "x-fedmi-gen"
 META_STORE = "x-fedmi-store"
 META_SYNC = "x-fedmi-sync-ckpt"        # "1": the reply must carry THIS round's checkpoint
+META_UPLOAD = "x-fedmi-upload"         # "0": leave the checkpoint out of the StartTrain reply (fetched later)
+META_FETCH = "x-fedmi-fetch"           # on SendModel: "1" = return the newest checkpoint instead of installing
 
 
 def metadata_dict(context) -> dict:
@@ -209,9 +211,11 @@ class ClientAgent(P.TrainerServicer):
             t4 = Timer()
             with phase("checkpoint"):
                 self._persist_async(ev.acc, rnd, keep=(rank == 0))
-                if rank == 0 and meta.get(META_SYNC) == "1":
+                sync = meta.get(META_SYNC) == "1"
+                if rank == 0 and sync:
                     self.writer.flush()
-                ck_epoch, message = self._take_ready() if rank == 0 else (-1, "")
+                upload = rank == 0 and (sync or meta.get(META_UPLOAD) != "0")
+                ck_epoch, message = self._take_ready() if upload else (-1, "")
             rec["ckpt_ms"] = t4.ms()
         else:
             # reference parameter-server path: the reply IS this round's local model
@@ -236,6 +240,8 @@ class ClientAgent(P.TrainerServicer):
 
     def SendModel(self, request, context):
         meta = metadata_dict(context)
+        if meta.get(META_FETCH) == "1":
+            return self._fetch(meta, context)
         with self.lock:
             self._fence(meta, context)
             data = ck.from_b64(request.model)
@@ -252,6 +258,25 @@ class ClientAgent(P.TrainerServicer):
                                **ev.as_dict("test"))
             self._log(f"installed model (epoch {self.round}): test loss {ev.loss:.4f} acc {ev.acc:.2f}%")
             return P.SendModelReply(reply="success")
+
+    def _fetch(self, meta: dict, context):
+        """The coordinator pulls the newest serialised global checkpoint off the round's critical path
+        (fedmi extension over the reference's SendModel: the reply string carries the base64 model).
+        Takes only the ready-buffer lock, so it never waits for a running StartTrain."""
+        term = int(meta.get(META_TERM, "0") or 0)
+        if term and term < self.max_term:
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION, f"stale coordinator term {term} < {self.max_term}")
+        with self._ready_lock:
+            ready = self._ready
+        if ready is None:
+            epoch, b64 = -1, ""
+        else:
+            epoch, b64 = ready[0], ck.to_b64(ready[1])
+        try:
+            context.set_trailing_metadata((("x-fedmi-ckpt-epoch", str(epoch)),))
+        except Exception:
+            pass
+        return P.SendModelReply(reply=b64)
 
     def HeartBeat(self, request, context):
         return P.HeartBeatResponse(status=1)

@@ -41,7 +41,7 @@ from ..parallel.group import StoreHost
 from ..utils.metrics import MetricsLog, Timer, log
 from ..utils.trace import phase
 from ..wire import proto as P
-from .client_agent import META_GEN, META_ROUND, META_STORE, META_SYNC, META_TERM
+from .client_agent import META_FETCH, META_GEN, META_ROUND, META_STORE, META_SYNC, META_TERM, META_UPLOAD
 
 
 @dataclass
@@ -61,6 +61,9 @@ class CoordinatorConfig:
     min_clients: int = 1
     round_pause_s: float = 0.0
     ckpt_sync_every: int = 0             # >0: rank 0 uploads THAT round's checkpoint every k rounds (always the last)
+    # collective mode with fedmi clients: the per-round model upload leaves the StartTrain reply and a
+    # background fetcher pulls rank 0's newest checkpoint at most this often (<= 0: upload every reply)
+    ckpt_fetch_interval_s: float = 0.05
 
 
 def fedavg_state_dicts(sds: List[dict], weights: Optional[List[float]] = None) -> "OrderedDict[str, torch.Tensor]":
@@ -87,11 +90,12 @@ def fedavg_state_dicts(sds: List[dict], weights: Optional[List[float]] = None) -
 
 
 class _Member:
-    __slots__ = ("address", "active", "channel", "stub")
+    __slots__ = ("address", "active", "channel", "stub", "fedmi")
 
     def __init__(self, address: str, gzip: bool):
         self.address = address
         self.active = True
+        self.fedmi = False          # answered with fedmi trailing metadata: understands upload/fetch
         self.channel = P.make_channel(address, gzip=gzip)
         self.stub = P.TrainerStub(self.channel)
 
@@ -135,6 +139,11 @@ class Coordinator:
         self._persist_stop = False
         self._persist_thread = threading.Thread(target=self._persister, name="fedmi-persist", daemon=True)
         self._persist_thread.start()
+        self._fetch_thread: Optional[threading.Thread] = None
+        self._fetches = 0
+        if cfg.agg == "collective" and cfg.ckpt_fetch_interval_s > 0:
+            self._fetch_thread = threading.Thread(target=self._fetcher, name="fedmi-fetch", daemon=True)
+            self._fetch_thread.start()
 
     # ---- logging / membership -------------------------------------------------
     def _log(self, msg: str) -> None:
@@ -155,11 +164,14 @@ class Coordinator:
         with self._lock:
             return {a: m.active for a, m in self.members.items()}
 
-    def _meta(self, round_no: int):
+    def _meta(self, round_no: int, live: List[str]):
         md = [(META_TERM, str(self.term)), (META_ROUND, str(round_no)), (META_GEN, str(self.generation))]
         k = self.cfg.ckpt_sync_every
-        if round_no >= self.cfg.rounds or (k > 0 and round_no % k == 0):
+        sync = round_no >= self.cfg.rounds or (k > 0 and round_no % k == 0)
+        if sync:
             md.append((META_SYNC, "1"))
+        elif (self._fetch_thread is not None and live and self.members[live[0]].fedmi):
+            md.append((META_UPLOAD, "0"))           # rank 0's model is fetched off the critical path
         if self.store is not None:
             md.append((META_STORE, f"{self.store.host}:{self.store.port}"))
         return md
@@ -200,6 +212,26 @@ class Coordinator:
                 self._persisted_seq = seq
                 self._persist_cv.notify_all()
 
+    def _fetcher(self) -> None:
+        """Pull rank 0's newest checkpoint (SendModel + x-fedmi-fetch) whenever rounds moved past the
+        installed model, at most every ``ckpt_fetch_interval_s``: persistence and backup replication
+        without a model upload inside each StartTrain reply."""
+        while not self.stop_event.wait(self.cfg.ckpt_fetch_interval_s):
+            live = self.live()
+            if not live or self.round <= self.installed_epoch or not self.members[live[0]].fedmi:
+                continue
+            m = self.members[live[0]]
+            try:
+                call = m.stub.SendModel.with_call(P.SendModelRequest(model=""), timeout=self.cfg.rpc_timeout_s,
+                                                  metadata=[(META_TERM, str(self.term)), (META_FETCH, "1")])
+            except grpc.RpcError:
+                continue                     # membership changes are the round loop's business
+            reply, call = call
+            epoch = int(dict(call.trailing_metadata() or ()).get("x-fedmi-ckpt-epoch", "-1"))
+            if reply.reply and epoch > self.installed_epoch:
+                self._fetches += 1
+                self._install_global(ck.from_b64(reply.reply), epoch)
+
     def flush(self) -> None:
         """Wait until the newest installed model is on disk (and offered to the backup)."""
         with self._persist_cv:
@@ -235,7 +267,7 @@ class Coordinator:
         rnd = self.round + 1
         self._log(f"Starting round {rnd} with {world} client(s) (gen {self.generation})")
         t = Timer()
-        md = self._meta(rnd)
+        md = self._meta(rnd, live)
         futs = {}
         for rank, addr in enumerate(live):
             stub = self.members[addr].stub
@@ -248,6 +280,7 @@ class Coordinator:
                 tm = dict(f.trailing_metadata() or ())
                 if "x-fedmi-client-round" in tm:
                     client_rounds.append(int(tm["x-fedmi-client-round"]))
+                    self.members[addr].fedmi = True
                 if "x-fedmi-ckpt-epoch" in tm:
                     ckpt_epochs[rank] = int(tm["x-fedmi-ckpt-epoch"])
             except grpc.RpcError as e:
@@ -334,6 +367,8 @@ class Coordinator:
 
     def close(self) -> None:
         self.stop()
+        if self._fetch_thread is not None:
+            self._fetch_thread.join(timeout=self.cfg.rpc_timeout_s)
         self.flush()
         with self._persist_cv:
             self._persist_stop = True

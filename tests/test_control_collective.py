@@ -70,3 +70,35 @@ def test_collective_client_loss_regroups(tmp_path):
     finally:
         for p in procs:
             stop_proc(p)
+
+
+def test_checkpoint_fetched_off_the_round_path(tmp_path):
+    """Collective mode with fedmi clients: StartTrain replies stop carrying the model after the first
+    round (x-fedmi-upload: 0); the coordinator's fetcher pulls rank 0's newest checkpoint through
+    SendModel + x-fedmi-fetch, persists and keeps up, and the final round is still synchronous."""
+    addrs, procs = _start_clients(tmp_path, 1)
+    try:
+        cfg = CoordinatorConfig(clients=addrs, rounds=12, agg="collective", root=str(tmp_path / "srv"),
+                                train_timeout_s=120, rpc_timeout_s=10, heartbeat_s=0.2, ckpt_fetch_interval_s=0.01)
+        coord = Coordinator(cfg)
+        seen = []
+        orig = coord._install_global
+
+        def spy(data, epoch=None):
+            seen.append(epoch)
+            orig(data, epoch)
+
+        coord._install_global = spy
+        for _ in range(11):
+            assert coord.run_round()
+            time.sleep(0.05)                     # give the fetcher a window between rounds
+        assert coord.members[addrs[0]].fedmi
+        assert coord._fetches > 0                # models arrived through the fetch path
+        assert coord.installed_epoch >= 9
+        assert coord.run_round()                 # final round: synchronous upload in the reply
+        coord.close()
+        assert coord.installed_epoch == 12 and seen[-1] == 12
+        assert ck.load(tmp_path / "srv" / "Primary" / "optimizedModel.pth")["epoch"] == 12
+    finally:
+        for p in procs:
+            stop_proc(p)
