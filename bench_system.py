@@ -169,6 +169,26 @@ def main() -> int:
     phases["coordinator_round_ms"] = coord_round
     if coord_round is not None and phases.get("client_round_ms") is not None:
         phases["rpc_and_coordinator_overhead_ms"] = round(coord_round - phases["client_round_ms"], 4)
+    # the overhead split (one host clock): request latency (coordinator send -> client handler entry),
+    # client handler work outside its timed round, reply latency (handler exit -> coordinator has the
+    # reply), coordinator bookkeeping after the replies, and the gap to the next round's send
+    by_round = {r["round"]: r for r in rounds}
+    c0 = {r["round"]: r for r in _jsonl(run / "client0.jsonl") if r.get("round") in timed and "t_enter" in r}
+    req, rep, post, gap, hnd = [], [], [], [], []
+    for rnd_, cr in c0.items():
+        pr = by_round.get(rnd_)
+        if pr is None or "t_send" not in pr:
+            continue
+        req.append((cr["t_enter"] - pr["t_send"]) * 1e3)
+        rep.append((pr["t_recv"] - cr["t_exit"]) * 1e3)
+        hnd.append((cr["t_exit"] - cr["t_enter"]) * 1e3 - cr["round_ms"])
+        post.append((pr["t_done"] - pr["t_recv"]) * 1e3)
+        nxt = by_round.get(rnd_ + 1)
+        if nxt is not None and "t_send" in nxt:
+            gap.append((nxt["t_send"] - pr["t_done"]) * 1e3)
+    if req:
+        phases.update(request_latency_ms=mean(req), client_handler_untimed_ms=mean(hnd), reply_latency_ms=mean(rep),
+                      coordinator_post_ms=mean(post), coordinator_loop_gap_ms=mean(gap))
     last_rec = [r for r in _jsonl(run / "client0.jsonl") if r.get("round") == total]
     out = {
         "metric": f"system rounds/sec (primary+backup+{a.clients} client processes over gRPC), {a.model} FedAvg",

@@ -676,11 +676,54 @@ __global__ __launch_bounds__(256) void dgrad_pack_kernel(DPackTable t) {
 }
 
 // dW[o][c][r][s] (+)= sum_z ws[z][o][(r*S + s)*C + c]     (c < Cw)
+// Block = one output channel o x 64 input channels, all R*S taps, 4 split groups:
+// each wave reads 256 contiguous bytes per (tap, split), the groups combine in
+// LDS in a fixed order (deterministic), and the block writes its 64 x RS results
+// as ONE contiguous run of dW[o][c0:c0+64][:][:] (the former one-lane-per-column
+// layout scattered every 4-byte store RS floats apart).
+constexpr int WRED_MAX_RS = 49;
+__global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict__ ws, int splits, int O, int C, int Cw,
+                                                         int RS, float* __restrict__ dw, int accumulate) {
+  extern __shared__ float part_[];                 // [4][RS][65], sized by the launch
+  auto part = [&](int zg, int rs, int ci) -> float& { return part_[(zg * RS + rs) * 65 + ci]; };
+  const long plane = (long)O * RS * C;
+  const int ncb = (C + 63) / 64;
+  const int o = blockIdx.x / ncb, c0 = (blockIdx.x % ncb) * 64;
+  const int cl = threadIdx.x & 63, zg = threadIdx.x >> 6;
+  const int c = c0 + cl;
+  for (int rs = 0; rs < RS; ++rs) {
+    float v = 0.f;
+    if (c < C) {
+      const float* p = ws + ((long)o * RS + rs) * C + c;
+      int z = zg;
+      for (; z + 12 < splits; z += 16) {   // 4 independent loads in flight per lane
+        const float a = p[(long)z * plane], b = p[(long)(z + 4) * plane];
+        const float cc = p[(long)(z + 8) * plane], d = p[(long)(z + 12) * plane];
+        v += (a + b) + (cc + d);
+      }
+      for (; z < splits; z += 4) v += p[(long)z * plane];
+    }
+    part(zg, rs, cl) = v;
+  }
+  __syncthreads();
+  const int cn = min(64, Cw - c0);
+  if (cn <= 0) return;
+  float* out = dw + ((long)o * Cw + c0) * RS;
+  for (int e = threadIdx.x; e < cn * RS; e += 256) {
+    const int ci = e / RS, rs = e - ci * RS;
+    const float s = (part(0, rs, ci) + part(1, rs, ci)) + (part(2, rs, ci) + part(3, rs, ci));
+    out[e] = accumulate ? out[e] + s : s;
+  }
+}
+
+// Column-mapped variant (one lane per workspace column, scattered stores): more workgroups, so
+// it wins when the plane is small and the split count large (ResNet-18's 64-channel layers).
+// dW[o][c][r][s] (+)= sum_z ws[z][o][(r*S + s)*C + c]     (c < Cw)
 // Block = 64 consecutive workspace columns x 4 split groups: every wave reads
 // 256 contiguous bytes per split (the workspace is read exactly once, fully
 // coalesced), the 4 groups are combined in LDS, and the 64 sums are written to
 // their permuted [O][Cw][R][S] positions.  Deterministic (fixed order).
-__global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict__ ws, int splits, int O, int C, int Cw,
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_cols(const float* __restrict__ ws, int splits, int O, int C, int Cw,
                                                          int RS, float* __restrict__ dw, int accumulate) {
   __shared__ float part[4][64];
   const long plane = (long)O * RS * C;
@@ -1199,9 +1242,15 @@ void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const 
   splits = (ksteps + kps - 1) / kps;
   if ((long)splits * plane > ws_floats) throw std::invalid_argument("conv_wgrad: workspace too small for splits");
   launch_mode<WGRAD>(st, g, x, nullptr, dy, nullptr, ws, nullptr, splits);
-  const long blocks = (plane + 63) / 64;
-  hipLaunchKernelGGL(conv_wgrad_reduce, dim3((unsigned)blocks), dim3(256), 0, st, ws, splits, s.O, s.C, s.Cw,
-                     s.R * s.S, dw, accumulate);
+  if (s.R * s.S > WRED_MAX_RS) throw std::invalid_argument("conv_wgrad: window larger than 7x7");
+  const long blocks = (long)s.O * ((s.C + 63) / 64);
+  if (blocks >= 1024) {      // enough (o, channel-block) tiles: coalesced tile writes
+    hipLaunchKernelGGL(conv_wgrad_reduce, dim3((unsigned)blocks), dim3(256), 4 * s.R * s.S * 65 * sizeof(float), st,
+                       ws, splits, s.O, s.C, s.Cw, s.R * s.S, dw, accumulate);
+  } else {
+    hipLaunchKernelGGL(conv_wgrad_reduce_cols, dim3((unsigned)((plane + 63) / 64)), dim3(256), 0, st, ws, splits, s.O,
+                       s.C, s.Cw, s.R * s.S, dw, accumulate);
+  }
 }
 
 struct PackItem {

@@ -135,6 +135,7 @@ class ClientAgent(P.TrainerServicer):
 
     # ---- RPCs ---------------------------------------------------------------------
     def StartTrain(self, request, context):
+        t_enter = time.time()
         meta = metadata_dict(context)
         gen = int(meta.get(META_GEN, "0") or 0)
         busy = self._busy_gen
@@ -145,11 +146,11 @@ class ClientAgent(P.TrainerServicer):
         with self.lock:
             self._busy_gen = gen
             try:
-                return self._start_train(request, context, meta, gen)
+                return self._start_train(request, context, meta, gen, t_enter)
             finally:
                 self._busy_gen = None
 
-    def _start_train(self, request, context, meta: dict, gen: int):
+    def _start_train(self, request, context, meta: dict, gen: int, t_enter: float = 0.0):
         self._fence(meta, context)
         rank, world = int(request.rank), int(request.world)
         if world <= 0 or not 0 <= rank < world:
@@ -226,6 +227,7 @@ class ClientAgent(P.TrainerServicer):
             ck_epoch, message = rnd, ck.to_b64(data)
             rec["ckpt_ms"] = t4.ms()
         rec["round_ms"] = t.ms()
+        rec["t_enter"], rec["t_exit"] = t_enter, time.time()
         self.metrics.write(**rec)
         self._log(f"round {rnd} rank {rank}/{world}: train loss {tr.loss:.4f} acc {tr.acc:.2f}%"
                   + (f" | test acc {rec['test_acc']:.2f}%" if "test_acc" in rec else ""))

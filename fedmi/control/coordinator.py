@@ -268,6 +268,7 @@ class Coordinator:
         self._log(f"Starting round {rnd} with {world} client(s) (gen {self.generation})")
         t = Timer()
         md = self._meta(rnd, live)
+        t_send = time.time()
         futs = {}
         for rank, addr in enumerate(live):
             stub = self.members[addr].stub
@@ -291,6 +292,7 @@ class Coordinator:
                 if e.code() not in (grpc.StatusCode.ABORTED, grpc.StatusCode.FAILED_PRECONDITION):
                     self._mark(addr, False)
         t_train = t.ms()
+        t_recv = time.time()
         ok = False
         if self.cfg.agg == "collective":
             if failed:
@@ -326,7 +328,8 @@ class Coordinator:
         dt = t.ms()
         self.round_times.append(dt)
         self.metrics.write(role=self.role, event="round", round=rnd, ok=ok, world=world, generation=self.generation,
-                           failed=failed, train_ms=t_train, round_ms=dt, term=self.term)
+                           failed=failed, train_ms=t_train, round_ms=dt, term=self.term, t_send=t_send, t_recv=t_recv,
+                           t_done=time.time())
         if self.cfg.round_pause_s:
             time.sleep(self.cfg.round_pause_s)
         return ok
