@@ -30,7 +30,7 @@ void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, con
                       float, float, int*, int*);
 void launch_lenet_fwd_head(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*, int,
                            bf16*, bf16*, bf16*, uint8_t*, uint8_t*, const int*, float*, bf16*, float*, lenet::Stats*,
-                           int*, const int*);
+                           int*, const int*, int*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
 void launch_sgd_flat(hipStream_t, float*, const float*, float*, long, float, float, float, float, int, int);
 int fedavg_max_inputs();
@@ -83,6 +83,8 @@ static LeNetBuffers buffers_from(const py::dict& d) {
   b.round_ctr = P<int>(get("round_ctr"));
   b.done_flags = P<int>(get("done_flags"));
   b.step_gen = P<int>(get("step_gen"));
+  b.bwd_flags = P<int>(get("bwd_flags"));
+  b.bwd_gen = P<int>(get("bwd_gen"));
   return b;
 }
 
@@ -146,7 +148,9 @@ static void fedmi_bind(py::module_& m) {
            })
       .def("graph_ready", &LeNetEngine::graph_ready)
       .def("set_fuse_head", &LeNetEngine::set_fuse_head)
-      .def("fuse_head", &LeNetEngine::fuse_head);
+      .def("fuse_head", &LeNetEngine::fuse_head)
+      .def("set_fuse_sgd", &LeNetEngine::set_fuse_sgd)
+      .def("fuse_sgd", &LeNetEngine::fuse_sgd);
 
   // ---- raw LeNet kernels (numerics tests drive them one by one) -------------
   m.def("lenet_conv_fwd", [](uintptr_t st, uintptr_t images, int base, int nb, uintptr_t pk, uintptr_t params,
@@ -195,7 +199,8 @@ static void fedmi_bind(py::module_& m) {
     launch_lenet_fwd_head(S(st), P<const uint8_t>(images), base, nb, P<const bf16>(pk), P<const float>(params), seed,
                           P<const int>(round_ctr), augment, P<bf16>(act2), P<bf16>(act2T), P<bf16>(pool1),
                           P<uint8_t>(am1), P<uint8_t>(am2), P<const int>(labels), P<float>(dact2), P<bf16>(dZ1T),
-                          P<float>(fc_slab), P<lenet::Stats>(stats), P<int>(flags), P<const int>(step_gen));
+                          P<float>(fc_slab), P<lenet::Stats>(stats), P<int>(flags), P<const int>(step_gen),
+                          nullptr);
     check_last("lenet_fwd_head");
   });
   m.def("lenet_pack", [](uintptr_t st, uintptr_t params, uintptr_t pk) {

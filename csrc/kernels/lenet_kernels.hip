@@ -708,10 +708,11 @@ __global__ __launch_bounds__(NT_FWD) void lenet_fwd_head(
     bf16* __restrict__ act2, bf16* __restrict__ act2T, bf16* __restrict__ pool1_out,
     uint8_t* __restrict__ am1_out, uint8_t* __restrict__ am2_out, const int* __restrict__ labels,
     float* __restrict__ dact2, bf16* __restrict__ dZ1T, float* __restrict__ fc_slab, Stats* __restrict__ stats,
-    int* __restrict__ done_flags, const int* __restrict__ step_gen)
+    int* __restrict__ done_flags, const int* __restrict__ step_gen, int* __restrict__ bwd_gen)
 {
   static_assert(NT_FWD == NT_FC, "one launch hosts both roles");
   const int gen = step_gen[0] + 1;
+  if (bwd_gen && blockIdx.x == 0 && threadIdx.x == 0) bwd_gen[0] += 1;   // K34's flag generation (read only by K34)
   if ((int)blockIdx.x < nb) {
     conv_fwd_body(blockIdx.x, images, sample_base, nb, pk, params, seed, round_ctr, augment, act2, act2T,
                   MAX_TRAIN_BATCH, pool1_out, am1_out, am2_out, nullptr, done_flags, gen);
@@ -725,8 +726,27 @@ __global__ __launch_bounds__(NT_FWD) void lenet_fwd_head(
 // All per-sample inputs and the conv2 dgrad weights are staged into LDS with
 // 16-byte loads at entry; every MFMA operand afterwards is an LDS read.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
-    const uint8_t* __restrict__ images, int sample_base, int nb,
+// PUB (K34, the fused backward + SGD launch): gradient stores go out write-through
+// (sc1) and each producer workgroup then raises its flag -- the SGD workgroups of
+// the same launch consume them with sc1 loads (the K12 hand-off recipe).
+template <bool PUB>
+FEDMI_DEV void put_grad(float* p, float v) {
+  if constexpr (PUB) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+template <bool PUB>
+FEDMI_DEV void publish_flag(int* flags, int idx, int gen) {
+  if constexpr (PUB) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flags + idx, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <bool PUB>
+FEDMI_DEV void conv_bwd_body(
+    int blk, const uint8_t* __restrict__ images, int sample_base, int nb,
     uint32_t seed, const int* __restrict__ round_ctr, int augment,
     const float* __restrict__ dact2,       // [nb][F0]   d(pool2), ReLU-masked
     const bf16* __restrict__ act2T,        // [F0P][128]
@@ -736,7 +756,8 @@ __global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
     const uint8_t* __restrict__ am2,       // [nb][F0]
     const bf16* __restrict__ pk,
     float* __restrict__ conv_slab,         // [nb][CS]
-    float* __restrict__ fc1w_grad)         // [F1W_N]
+    float* __restrict__ fc1w_grad,         // [F1W_N]
+    int* __restrict__ flags, int gen)      // PUB: producer flags [nb + N_DW1_WG]
 {
   // Operand images are padded so the 16 lanes of an MFMA fragment read land on
   // distinct 16-byte bank groups (strides in 16-B units: coprime with 16 or
@@ -759,10 +780,11 @@ __global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
   const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
 
-  if ((int)blockIdx.x >= nb) {
+  if (blk >= nb) {
     // ---- fc1.weight grad: dW1[n][f] = sum_s dZ1[s][n] X[s][f], f in [16e, 16e+16)
-    const int e = blockIdx.x - nb;
-    if (e >= N_DW1_WG || wave >= 8) return;     // 8 row tiles of 16 outputs
+    const int e = blk - nb;
+    if (e >= N_DW1_WG) return;
+    if (wave < 8) {                              // 8 row tiles of 16 outputs
     const int nks = (nb + 31) >> 5;
     const bf16* ap = dZ1T + (wave * 16 + n16) * DZ1_LD + kq;
     const bf16* bp = act2T + (size_t)(e * 16 + n16) * MAX_TRAIN_BATCH + kq;
@@ -779,8 +801,10 @@ __global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = wave * 16 + rq + r;
-      if (n < F1) fc1w_grad[n * F0 + e * 16 + n16] = acc[r];
+      if (n < F1) put_grad<PUB>(fc1w_grad + n * F0 + e * 16 + n16, acc[r]);
     }
+    }
+    publish_flag<PUB>(flags, blk, gen);
     return;
   }
 
@@ -798,7 +822,7 @@ __global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
   float* db = reinterpret_cast<float*>(smem + O_DB);
   float* w1part = reinterpret_cast<float*>(smem + O_DW1);   // conv1 wgrad K-split partials [3][6][80]
 
-  const int s = blockIdx.x;
+  const int s = blk;
   [[maybe_unused]] const int stamp_wg = s;
   const int gidx = sample_base + s;
   FEDMI_STAMP(2, 0);
@@ -885,7 +909,7 @@ __global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
     }
     if (kk < 150) {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) slab[P_C2W + (rq + rr) * 150 + kk] = acc[rr];
+      for (int rr = 0; rr < 4; ++rr) put_grad<PUB>(slab + P_C2W + (rq + rr) * 150 + kk, acc[rr]);
     }
   }
 
@@ -965,11 +989,22 @@ __global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
   FEDMI_STAMP(2, 4);
   for (int e = tid; e < C1 * 75; e += NT_CONV) {
     const int o = e / 75, kk = e - o * 75;
-    slab[P_C1W + e] = w1part[o * 80 + kk] + w1part[(6 + o) * 80 + kk] + w1part[(12 + o) * 80 + kk];
+    put_grad<PUB>(slab + P_C1W + e, w1part[o * 80 + kk] + w1part[(6 + o) * 80 + kk] + w1part[(12 + o) * 80 + kk]);
   }
-  if (tid < C1) slab[P_C1B + tid] = db[16 + tid];
-  if (tid < C2) slab[P_C2B + tid] = db[tid];
+  if (tid < C1) put_grad<PUB>(slab + P_C1B + tid, db[16 + tid]);
+  if (tid < C2) put_grad<PUB>(slab + P_C2B + tid, db[tid]);
+  publish_flag<PUB>(flags, s, gen);
   FEDMI_STAMP(2, 5);
+}
+
+__global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
+    const uint8_t* __restrict__ images, int sample_base, int nb, uint32_t seed, const int* __restrict__ round_ctr,
+    int augment, const float* __restrict__ dact2, const bf16* __restrict__ act2T, const bf16* __restrict__ dZ1T,
+    const bf16* __restrict__ pool1, const uint8_t* __restrict__ am1, const uint8_t* __restrict__ am2,
+    const bf16* __restrict__ pk, float* __restrict__ conv_slab, float* __restrict__ fc1w_grad)
+{
+  conv_bwd_body<false>(blockIdx.x, images, sample_base, nb, seed, round_ctr, augment, dact2, act2T, dZ1T, pool1, am1,
+                       am2, pk, conv_slab, fc1w_grad, nullptr, 0);
 }
 // ---------------------------------------------------------------------------
 // Packing: fp32 master -> bf16 MFMA operand images.
@@ -1092,6 +1127,118 @@ __global__ __launch_bounds__(256) void lenet_sgd(
 }
 
 // ---------------------------------------------------------------------------
+// K34: conv backward (K3's producers) + SGD in ONE launch.  The producer
+// workgroups (nb per-sample conv workgroups, N_DW1_WG fc1-wgrad workgroups) come
+// first in the grid; the SGD workgroups after them either start at once (FC-tail
+// params: their grads come from K12) or wait on the producers' flags (fc1.weight
+// after the fc1-wgrad workgroups, conv params after every sample) and read the
+// published grads with sc1 loads.  The slab combine has K4's order (bit-identical
+// results).  Flags carry 'bwd_gen' (bumped by K12 every step); K34 bumps K12's
+// 'step_gen' and, on a round's last step, the augmentation counter -- each counter
+// is read only by the OTHER kernel.  Waits are wall-clock bounded (stats->pad = 2).
+// ---------------------------------------------------------------------------
+constexpr int K34_NA = (CS + 63) / 64;                    // 45: 64 conv params x 16 slab lanes
+constexpr int K34_NB = (F1W_N + NT_CONV - 1) / NT_CONV;   // 47: fc1.weight
+constexpr int K34_NC = (FS + NT_CONV - 1) / NT_CONV;      // 11: FC tail
+constexpr int K34_SGD_WG = K34_NA + K34_NB + K34_NC;
+
+FEDMI_DEV void wait_flags(const int* flags, int n, int gen, Stats* stats) {
+  if ((int)threadIdx.x < n) {
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(flags + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > 100000000ull) {      // 1 s: never hang the GPU on a broken hand-off
+        __hip_atomic_store(&stats->pad, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+FEDMI_DEV void sgd_fused_body(int r, int nb, float* __restrict__ params, float* __restrict__ mom,
+                              bf16* __restrict__ pk, const float* __restrict__ conv_slab,
+                              const float* __restrict__ fc1w_grad, const float* __restrict__ fc_slab, int n_fc,
+                              float lr, float momentum, float wd, const int* __restrict__ flags, int gen,
+                              int* __restrict__ round_bump, int* __restrict__ step_gen, Stats* __restrict__ stats) {
+  __shared__ float red[16][65];
+  const int tid = threadIdx.x;
+  if (r < K34_NA) {
+    wait_flags(flags, nb, gen, stats);
+    if (r == 0 && tid == 0) {             // every producer has read both counters by now
+      if (round_bump) atomicAdd(round_bump, 1);
+      step_gen[0] += 1;
+    }
+    const int pl = tid & 63, g = tid >> 6;
+    const int i = r * 64 + pl;
+    float p = 0.f, m = 0.f;
+    if (g == 0 && i < CS) { p = params[i]; m = mom[i]; }
+    float sum = 0.f;
+    if (i < CS) {
+      float v[MAX_TRAIN_BATCH / 16];
+#pragma unroll
+      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) {
+        const int q = g + 16 * u;
+        v[u] = q < nb ? __hip_atomic_load(conv_slab + (size_t)q * CS + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) sum += v[u];
+    }
+    red[g][pl] = sum;
+    __syncthreads();
+    if (g == 0 && i < CS) {
+      float tot = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) tot += red[q][pl];
+      sgd_apply(i, tot, p, m, params, mom, pk, lr, momentum, wd);
+    }
+  } else if (r < K34_NA + K34_NB) {
+    const int j = (r - K34_NA) * NT_CONV + tid;
+    const bool ok = j < F1W_N;
+    const int i = P_F1W + (ok ? j : 0);
+    const float p = ok ? params[i] : 0.f, m = ok ? mom[i] : 0.f;    // loaded while the fc1 wgrad runs
+    wait_flags(flags + nb, N_DW1_WG, gen, stats);
+    if (ok)
+      sgd_apply(i, __hip_atomic_load(fc1w_grad + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), p, m, params, mom,
+                pk, lr, momentum, wd);
+  } else {
+    const int j = (r - K34_NA - K34_NB) * NT_CONV + tid;
+    if (j < FS) {                          // grads from K12 (previous launch): plain loads
+      const int i = P_F1B + j;
+      const float p = params[i], m = mom[i];
+      float v[MAX_FC_WG];
+#pragma unroll
+      for (int q = 0; q < MAX_FC_WG; ++q) v[q] = q < n_fc ? fc_slab[(size_t)q * FS + j] : 0.f;
+      float sum = 0.f;
+#pragma unroll
+      for (int q = 0; q < MAX_FC_WG; ++q) sum += v[q];
+      sgd_apply(i, sum, p, m, params, mom, pk, lr, momentum, wd);
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT_CONV) void lenet_bwd_sgd(
+    const uint8_t* __restrict__ images, int sample_base, int nb, uint32_t seed, const int* __restrict__ round_ctr,
+    int augment, const float* __restrict__ dact2, const bf16* __restrict__ act2T, const bf16* __restrict__ dZ1T,
+    const bf16* __restrict__ pool1, const uint8_t* __restrict__ am1, const uint8_t* __restrict__ am2,
+    const bf16* pk_in, float* conv_slab, float* fc1w_grad,   // (pk_in == pk, conv_slab / fc1w_grad: both roles)
+    float* __restrict__ params, float* __restrict__ mom, bf16* pk, const float* __restrict__ fc_slab,
+    int n_fc, float lr, float momentum, float wd, int* __restrict__ flags, const int* __restrict__ bwd_gen,
+    int* __restrict__ round_bump, int* __restrict__ step_gen, Stats* __restrict__ stats)
+{
+  const int gen = bwd_gen[0];
+  const int nprod = nb + N_DW1_WG;
+  if ((int)blockIdx.x < nprod) {
+    conv_bwd_body<true>(blockIdx.x, images, sample_base, nb, seed, round_ctr, augment, dact2, act2T, dZ1T, pool1, am1,
+                        am2, pk_in, conv_slab, fc1w_grad, flags, gen);
+    return;
+  }
+  sgd_fused_body(blockIdx.x - nprod, nb, params, mom, pk, conv_slab, fc1w_grad, fc_slab, n_fc, lr, momentum, wd, flags,
+                 gen, round_bump, step_gen, stats);
+}
+
+// ---------------------------------------------------------------------------
 // Host launchers (called by the native executor, csrc/runtime/lenet_engine.cpp)
 // ---------------------------------------------------------------------------
 namespace fedmi {
@@ -1144,12 +1291,25 @@ void launch_lenet_sgd(hipStream_t st, float* params, float* mom, bf16* pk, const
 void launch_lenet_fwd_head(hipStream_t st, const uint8_t* images, int sample_base, int nb, const bf16* pk,
                            const float* params, uint32_t seed, const int* round_ctr, int augment, bf16* act2,
                            bf16* act2T, bf16* pool1, uint8_t* am1, uint8_t* am2, const int* labels, float* dact2,
-                           bf16* dZ1T, float* fc_slab, Stats* stats, int* done_flags, const int* step_gen) {
+                           bf16* dZ1T, float* fc_slab, Stats* stats, int* done_flags, const int* step_gen,
+                           int* bwd_gen) {
   if (nb <= 0 || nb > MAX_TRAIN_BATCH) return;
   const int mtiles = (nb + FC_SPW - 1) / FC_SPW;
   hipLaunchKernelGGL(lenet_fwd_head, dim3(nb + 4 * mtiles), dim3(NT_FWD), 0, st, images, sample_base, nb, pk, params,
                      seed, round_ctr, augment, act2, act2T, pool1, am1, am2, labels, dact2, dZ1T, fc_slab, stats,
-                     done_flags, step_gen);
+                     done_flags, step_gen, bwd_gen);
+}
+
+void launch_lenet_bwd_sgd(hipStream_t st, const uint8_t* images, int sample_base, int nb, uint32_t seed,
+                          const int* round_ctr, int augment, const float* dact2, const bf16* act2T, const bf16* dZ1T,
+                          const bf16* pool1, const uint8_t* am1, const uint8_t* am2, float* conv_slab,
+                          float* fc1w_grad, float* params, float* mom, bf16* pk, const float* fc_slab, int n_fc, float lr,
+                          float momentum, float wd, int* flags, const int* bwd_gen, int* round_bump, int* step_gen,
+                          Stats* stats) {
+  if (nb <= 0 || nb > MAX_TRAIN_BATCH) return;
+  hipLaunchKernelGGL(lenet_bwd_sgd, dim3(nb + N_DW1_WG + K34_SGD_WG), dim3(NT_CONV), 0, st, images, sample_base, nb,
+                     seed, round_ctr, augment, dact2, act2T, dZ1T, pool1, am1, am2, pk, conv_slab, fc1w_grad, params,
+                     mom, pk, fc_slab, n_fc, lr, momentum, wd, flags, bwd_gen, round_bump, step_gen, stats);
 }
 
 bool stamps_enabled() {

@@ -20,7 +20,10 @@ void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, con
                       float, float, int*, int*);
 void launch_lenet_fwd_head(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*, int,
                            bf16*, bf16*, bf16*, uint8_t*, uint8_t*, const int*, float*, bf16*, float*, Stats*, int*,
-                           const int*);
+                           const int*, int*);
+void launch_lenet_bwd_sgd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const float*, const bf16*,
+                          const bf16*, const bf16*, const uint8_t*, const uint8_t*, float*, float*, float*, float*, bf16*,
+                          const float*, int, float, float, float, int*, const int*, int*, int*, Stats*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
 
 void check_hip(hipError_t e, const char* what) {
@@ -80,7 +83,7 @@ void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round, bool 
     if (reset_stats) check_hip(hipMemsetAsync(b_.train_stats, 0, sizeof(Stats), st), "memset stats");
     launch_lenet_fwd_head(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug, b_.act2,
                           b_.act2T, b_.pool1, b_.am1, b_.am2, b_.train_labels + start, b_.dact2, b_.dZ1T, b_.fc_slab,
-                          b_.train_stats, b_.done_flags, b_.step_gen);
+                          b_.train_stats, b_.done_flags, b_.step_gen, b_.bwd_gen);
   } else {
     launch_lenet_conv_fwd(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug, b_.act2,
                           b_.act2T, MAX_TRAIN_BATCH, b_.pool1, b_.am1, b_.am2, reset_stats ? b_.train_stats : nullptr);
@@ -88,11 +91,18 @@ void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round, bool 
     launch_lenet_fc_tail(st, fuse_fc1_ ? nullptr : b_.h1, b_.act2, b_.train_labels + start, nb, 1, b_.pk, b_.params,
                          b_.dact2, b_.dZ1T, b_.fc_slab, b_.train_stats);
   }
-  launch_lenet_conv_bwd(st, b_.train_images, start, nb, seed_, b_.round_ctr, aug, b_.dact2, b_.act2T, b_.dZ1T,
-                        b_.pool1, b_.am1, b_.am2, b_.pk, b_.conv_slab, b_.fc1w_grad);
-  launch_lenet_sgd(st, b_.params, b_.mom, b_.pk, b_.conv_slab, nb, b_.fc1w_grad, b_.fc_slab,
-                   (nb + FC_SPW - 1) / FC_SPW, sgd_.lr, sgd_.momentum, sgd_.weight_decay,
-                   bump_round ? b_.round_ctr : nullptr, b_.step_gen);
+  if (fuse_sgd_ && fuse_head_) {
+    launch_lenet_bwd_sgd(st, b_.train_images, start, nb, seed_, b_.round_ctr, aug, b_.dact2, b_.act2T, b_.dZ1T,
+                         b_.pool1, b_.am1, b_.am2, b_.conv_slab, b_.fc1w_grad, b_.params, b_.mom, b_.pk, b_.fc_slab,
+                         (nb + FC_SPW - 1) / FC_SPW, sgd_.lr, sgd_.momentum, sgd_.weight_decay, b_.bwd_flags, b_.bwd_gen,
+                         bump_round ? b_.round_ctr : nullptr, b_.step_gen, b_.train_stats);
+  } else {
+    launch_lenet_conv_bwd(st, b_.train_images, start, nb, seed_, b_.round_ctr, aug, b_.dact2, b_.act2T, b_.dZ1T,
+                          b_.pool1, b_.am1, b_.am2, b_.pk, b_.conv_slab, b_.fc1w_grad);
+    launch_lenet_sgd(st, b_.params, b_.mom, b_.pk, b_.conv_slab, nb, b_.fc1w_grad, b_.fc_slab,
+                     (nb + FC_SPW - 1) / FC_SPW, sgd_.lr, sgd_.momentum, sgd_.weight_decay,
+                     bump_round ? b_.round_ctr : nullptr, b_.step_gen);
+  }
   check_hip(hipGetLastError(), "LeNetEngine::step launch");
 }
 
@@ -100,6 +110,14 @@ void LeNetEngine::set_fuse_head(bool on) {
   if (on && (!b_.done_flags || !b_.step_gen)) throw std::invalid_argument("fuse_head needs done_flags and step_gen");
   if (on != fuse_head_) {
     fuse_head_ = on;
+    drop_graph();
+  }
+}
+
+void LeNetEngine::set_fuse_sgd(bool on) {
+  if (on && (!b_.bwd_flags || !b_.bwd_gen)) throw std::invalid_argument("fuse_sgd needs bwd_flags and bwd_gen");
+  if (on != fuse_sgd_) {
+    fuse_sgd_ = on;
     drop_graph();
   }
 }

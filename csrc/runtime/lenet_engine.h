@@ -37,7 +37,9 @@ struct LeNetBuffers {
   lenet::Stats* eval_stats = nullptr;
   int* round_ctr = nullptr;      // augmentation epoch counter (device)
   int* done_flags = nullptr;     // [MAX_TRAIN_BATCH] K12 hand-off flags (optional: enables fuse_head)
-  int* step_gen = nullptr;       // step generation, bumped by K4
+  int* step_gen = nullptr;       // step generation, bumped by K4 / K34
+  int* bwd_flags = nullptr;      // [MAX_TRAIN_BATCH + N_DW1_WG] K34 producer flags (optional: enables fuse_sgd)
+  int* bwd_gen = nullptr;        // K34's flag generation, bumped by K12
 };
 
 struct SgdConfig {
@@ -71,6 +73,9 @@ class LeNetEngine {
   // conv stack + FC head in one launch (K12) instead of K1 then K2 (needs done_flags/step_gen)
   void set_fuse_head(bool on);
   bool fuse_head() const { return fuse_head_; }
+  // conv backward + SGD in one launch (K34) instead of K3 then K4 (needs fuse_head, bwd_flags/bwd_gen)
+  void set_fuse_sgd(bool on);
+  bool fuse_sgd() const { return fuse_sgd_; }
 
  private:
   void enqueue_epoch(hipStream_t st);
@@ -82,6 +87,7 @@ class LeNetEngine {
   bool augment_;
   bool fuse_fc1_ = false;
   bool fuse_head_ = false;
+  bool fuse_sgd_ = false;
   std::vector<int> starts_, sizes_;
   hipStream_t cap_stream_ = nullptr;
   hipGraph_t graph_ = nullptr;

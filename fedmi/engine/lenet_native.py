@@ -78,19 +78,24 @@ class LeNetNativeTrainer(LocalTrainer):
             self.round_ctr = z(4, dt=torch.int32)
             self.done_flags = z(B, dt=torch.int32)       # K12 conv -> FC-head hand-off flags (step generations)
             self.step_gen = z(4, dt=torch.int32)
+            self.bwd_flags = z(B + L["N_DW1_WG"], dt=torch.int32)   # K34 producer -> SGD hand-off flags
+            self.bwd_gen = z(4, dt=torch.int32)
         self._bufs = dict(
             train_images=_ptr(self.train_set.x), train_labels=_ptr(self.train_set.y), n_train=len(self.train_set),
             params=_ptr(self.params), mom=_ptr(self.mom), pk=_ptr(self.pk), act2=_ptr(self.act2),
             act2_rows=self.act2_rows, act2T=_ptr(self.act2T), h1=_ptr(self.h1), pool1=_ptr(self.pool1), am1=_ptr(self.am1),
             am2=_ptr(self.am2), dact2=_ptr(self.dact2), dZ1T=_ptr(self.dZ1T), conv_slab=_ptr(self.conv_slab),
             fc1w_grad=_ptr(self.fc1w_grad), fc_slab=_ptr(self.fc_slab), train_stats=_ptr(self.stats[0]), eval_stats=_ptr(self.stats[1]),
-            round_ctr=_ptr(self.round_ctr), done_flags=_ptr(self.done_flags), step_gen=_ptr(self.step_gen))
+            round_ctr=_ptr(self.round_ctr), done_flags=_ptr(self.done_flags), step_gen=_ptr(self.step_gen),
+            bwd_flags=_ptr(self.bwd_flags), bwd_gen=_ptr(self.bwd_gen))
         self.engine = nat.LeNetEngine(self._bufs, cfg.lr, cfg.momentum, cfg.weight_decay, cfg.seed & 0xFFFFFFFF,
                                       bool(data.augment and cfg.augment))
         self.fuse_fc1 = os.environ.get("FEDMI_LENET_FUSE_FC1", "1") == "1"
         self.engine.set_fuse_fc1(self.fuse_fc1)
         # K1 + K2 in one launch (FC-head weight prefetch overlapped with the conv stack)
         self.engine.set_fuse_head(os.environ.get("FEDMI_LENET_FUSE_HEAD", "1") == "1")
+        # K3 + K4 in one launch: the SGD workgroups consume the backward's grads through flags
+        self.engine.set_fuse_sgd(os.environ.get("FEDMI_LENET_FUSE_SGD", "1") == "1")
         self._views = ordered_views(self.params, LENET_SPEC)
         if init_state is None:
             torch.manual_seed(cfg.seed)

@@ -351,6 +351,37 @@ def test_training_converges(env):
 
 
 @pytest.mark.parametrize("use_graph", [True, False], ids=["graph", "eager"])
+def test_fused_bwd_sgd_matches_separate_kernels(env, use_graph):
+    """K34 (conv backward + SGD in one launch, producer flags -> SGD workgroups) trains like K3 then K4,
+    across steps (flag generations) and rounds (augmentation counter bumped once per round)."""
+    nat, dev, ds, ref, tr = env
+    starts, sizes = [0, 128, 384, 896], [128, 128, 33, 80]
+    res = []
+    for fuse in (False, True):
+        tr.engine.set_fuse_head(True)
+        tr.engine.set_fuse_sgd(fuse)
+        assert tr.engine.fuse_sgd() == fuse
+        tr.load_state_dict(ref.state_dict())
+        tr.mom.zero_()
+        tr.round_ctr.zero_()
+        tr.stats.zero_()
+        tr.round_idx = 0
+        tr.cfg.use_graph = use_graph
+        tr.set_schedule(starts, sizes)
+        for _ in range(2):
+            tr.train_epoch()
+        torch.cuda.synchronize()
+        res.append((tr.params.clone(), tr.mom.clone(), tr.train_stats(), int(tr.stats[0][3]),
+                    int(tr.round_ctr[0])))
+    (p0, m0, s0, e0, r0), (p1, m1, s1, e1, r1) = res
+    assert e0 == 0 and e1 == 0, "hand-off timed out"
+    assert r0 == r1 == 2
+    assert s0.count == s1.count == sum(sizes) and s0.correct == s1.correct
+    assert abs(s0.loss_sum - s1.loss_sum) <= 1e-4 * abs(s0.loss_sum)
+    assert rel(p1, p0) < 1e-5 and rel(m1, m0) < 1e-5   # only the LDS-atomic order of K3's bias sums differs
+
+
+@pytest.mark.parametrize("use_graph", [True, False], ids=["graph", "eager"])
 def test_fused_fwd_head_matches_separate_kernels(env, use_graph):
     """K12 (conv stack + FC head in one launch, flag hand-off) trains exactly like K1 then K2b."""
     nat, dev, ds, ref, tr = env
