@@ -94,8 +94,9 @@ class LeNetNativeTrainer(LocalTrainer):
         self.engine.set_fuse_fc1(self.fuse_fc1)
         # K1 + K2 in one launch (FC-head weight prefetch overlapped with the conv stack)
         self.engine.set_fuse_head(os.environ.get("FEDMI_LENET_FUSE_HEAD", "1") == "1")
-        # K3 + K4 in one launch: the SGD workgroups consume the backward's grads through flags
-        self.engine.set_fuse_sgd(os.environ.get("FEDMI_LENET_FUSE_SGD", "1") == "1")
+        # K3 + K4 in one launch (flag hand-off to SGD workgroups): opt-in -- measured 15.0 us vs 10.4 + 4.9,
+        # the conv-param slab combine then trails the slowest sample (profiles/r2_lenet/experiments.md)
+        self.engine.set_fuse_sgd(os.environ.get("FEDMI_LENET_FUSE_SGD", "0") == "1")
         self._views = ordered_views(self.params, LENET_SPEC)
         if init_state is None:
             torch.manual_seed(cfg.seed)
