@@ -514,3 +514,53 @@ def test_bn_bwd_additive_residual_grad(gpu_device):
     cnn.bn_bwd(dy, z, A, dg, db, d2, red, y=y, ws=ws, dadd=extra)
     torch.cuda.synchronize()
     assert _rel(d2.float() - extra.float(), d1.float()) < 2e-2
+
+
+# The exact batch-128 ResNet-18 (CIFAR) conv shapes of SURVEY.md §2.4(b), run the way the engine runs
+# them: forward with the split-K workspace and fused BN statistics, tap-major DGRAD on the weight
+# image (+ workspace), auto-split WGRAD.
+R18_B128 = [
+    (128, 32, 32, 3, 64, 3, 1, 1),      # stem (input padded 3 -> 8 channels)
+    (128, 32, 32, 64, 64, 3, 1, 1),     # layer1 (x4)
+    (128, 32, 32, 64, 128, 3, 2, 1),    # layer2.0.conv1
+    (128, 16, 16, 128, 128, 3, 1, 1),   # layer2
+    (128, 32, 32, 64, 128, 1, 2, 0),    # layer2.0 shortcut
+    (128, 16, 16, 128, 256, 3, 2, 1),   # layer3.0.conv1
+    (128, 8, 8, 256, 256, 3, 1, 1),     # layer3
+    (128, 16, 16, 128, 256, 1, 2, 0),   # layer3.0 shortcut
+    (128, 8, 8, 256, 512, 3, 2, 1),     # layer4.0.conv1
+    (128, 4, 4, 512, 512, 3, 1, 1),     # layer4
+    (128, 8, 8, 256, 512, 1, 2, 0),     # layer4.0 shortcut
+]
+
+
+@pytest.mark.parametrize("shape", R18_B128, ids=[str(s) for s in R18_B128])
+def test_resnet18_batch128_conv_shapes(gpu_device, shape):
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device, seed=3)
+    xr = x.clone().requires_grad_(True)
+    wr_ = wb.clone().requires_grad_(True)
+    ref = F.conv2d(xr, wr_, stride=st, padding=pad)
+    gy = torch.randn_like(ref).bfloat16().float()
+    ref.backward(gy)
+    C = xn.shape[-1]
+    shp = (xn.shape, O, R, R, st, pad, Cw)
+    ws = conv.wgrad_workspace(gpu_device, max(conv.fd_ws_floats(*shp), conv.wgrad_ws_floats(*shp), 1))
+    wpk = conv.pack_weight(w)
+    rep = conv.stats_buffer(O, gpu_device)
+    y = conv.conv2d_fwd(xn, wpk, st, pad, Cw=Cw, stats=rep, ws=ws)
+    dyn = _nhwc(gy).bfloat16()
+    wd = None
+    if conv.dgrad_eligible(O):
+        wd = torch.empty(conv.dgrad_image_numel(w.shape, C), dtype=torch.bfloat16, device=gpu_device)
+        conv.dgrad_pack_weights([(w, wd, st, pad, C)])
+    dx = conv.conv2d_dgrad(dyn, wpk, xn.shape, st, pad, Cw=Cw, ws=ws, wd=wd)
+    dw = conv.conv2d_wgrad(xn, dyn, R, R, st, pad, Cw=Cw, ws=ws)
+    torch.cuda.synchronize()
+    assert _rel(y.float(), _nhwc(ref.detach())) < 1e-2
+    stats = conv.stats_total(rep)
+    yb = y.float()
+    assert _rel(stats[0], yb.sum((0, 1, 2))) < 1e-3
+    assert _rel(stats[1], (yb * yb).sum((0, 1, 2))) < 1e-3
+    assert _rel(dx[..., :Cw].float(), _nhwc(xr.grad)) < 1e-2
+    assert _rel(dw, wr_.grad) < 1e-2
