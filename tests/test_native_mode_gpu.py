@@ -78,7 +78,9 @@ CONVS = [(8, 16, 24, 48, 1, 1, 0, 1, False), (8, 16, 48, 16, 3, 1, 1, 1, False),
          (4, 16, 64, 128, 1, 2, 0, 1, True), (2, 16, 32, 64, 5, 1, 2, 1, False), (2, 16, 16, 32, 7, 2, 3, 1, False),
          (8, 16, 32, 32, 3, 1, 1, 32, False), (4, 16, 64, 64, 5, 2, 2, 64, False), (4, 16, 128, 128, 3, 1, 1, 2, False),
          (4, 8, 128, 128, 3, 2, 1, 32, False), (4, 8, 96, 96, 3, 1, 1, 3, False), (4, 8, 60, 60, 1, 1, 0, 3, False),
-         (4, 16, 3, 64, 3, 1, 1, 1, False), (4, 16, 58, 58, 1, 1, 0, 1, True)]
+         (4, 16, 3, 64, 3, 1, 1, 1, False), (4, 16, 58, 58, 1, 1, 0, 1, True),
+         (4, 8, 160, 160, 3, 2, 1, 10, False), (4, 4, 384, 384, 3, 1, 1, 24, False),   # RegNetY group width 16
+         (4, 16, 64, 64, 3, 1, 1, 4, False), (4, 16, 200, 200, 1, 1, 0, 2, False)]     # 4 x 16 groups, ShuffleNet
 
 
 @pytest.mark.parametrize("shape", CONVS, ids=[str(s) for s in CONVS])
@@ -265,7 +267,8 @@ def test_family_step_native_only(gpu_device, name):
     assert abs(losses["native"] - losses["fp32"]) < 0.05 * losses["fp32"] + 0.02, losses
 
 
-@pytest.mark.parametrize("name", ["densenet_cifar", "SENet18", "DPN26", "EfficientNetB0", "RegNetY_400MF"])
+@pytest.mark.parametrize("name", ["densenet_cifar", "SENet18", "DPN26", "ResNeXt29_2x64d", "EfficientNetB0",
+                                  "RegNetY_400MF"])
 def test_family_trains_like_fp32(gpu_device, name):
     """Three short epochs, graph-replayed: the trajectory tracks the fp32 engine (round 1's hybrid
     EfficientNet / RegNetY went NaN under replay)."""
