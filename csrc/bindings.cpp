@@ -33,9 +33,6 @@ void launch_lenet_fwd_head(hipStream_t, const uint8_t*, int, int, const bf16*, c
                            int*, const int*, int*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
 void launch_sgd_flat(hipStream_t, float*, const float*, float*, long, float, float, float, float, int, int);
-int fedavg_max_inputs();
-void launch_fedavg_reduce(hipStream_t, const float* const*, const float*, int, float*, long);
-void launch_scale(hipStream_t, float*, long, float);
 size_t select_state_bytes();
 int compact_chunk();
 void launch_ef_delta(hipStream_t, const float*, const float*, const float*, float*, long);
@@ -214,20 +211,6 @@ static void fedmi_bind(py::module_& m) {
     launch_sgd_flat(S(st), P<float>(p), P<const float>(g), P<float>(buf), n, lr, mo, wd, damp, nesterov ? 1 : 0,
                     first ? 1 : 0);
     check_last("sgd_flat");
-  });
-  m.def("fedavg_max_inputs", &fedavg_max_inputs);
-  m.def("fedavg_reduce", [](uintptr_t st, const std::vector<uintptr_t>& ins, const std::vector<float>& w, uintptr_t out,
-                            long n) {
-    if (ins.size() != w.size() || ins.empty() || (int)ins.size() > fedavg_max_inputs())
-      throw std::invalid_argument("fedavg_reduce: bad inputs");
-    std::vector<const float*> ptrs;
-    for (auto p : ins) ptrs.push_back(P<const float>(p));
-    launch_fedavg_reduce(S(st), ptrs.data(), w.data(), (int)ins.size(), P<float>(out), n);
-    check_last("fedavg_reduce");
-  });
-  m.def("scale", [](uintptr_t st, uintptr_t x, long n, float a) {
-    launch_scale(S(st), P<float>(x), n, a);
-    check_last("scale");
   });
 
   // ---- compression ---------------------------------------------------------------

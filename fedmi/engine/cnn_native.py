@@ -420,7 +420,7 @@ def supports(model: nn.Module) -> bool:
 class CNNNativeTrainer(LocalTrainer):
     def __init__(self, model_name: str, data: FedDataset, device: torch.device, cfg: TrainerConfig = TrainerConfig(),
                  init_state=None, act_dtype=torch.bfloat16):
-        """``act_dtype`` other than bf16 only works under fedmi.ops.emulate (wiring tests)."""
+        """``act_dtype`` other than bf16 only works under the tests' kernel emulation (tests/emulate.py)."""
         self._nat = native.require()
         self._device = device = torch.device(device)
         self.cfg = dataclasses.replace(cfg)

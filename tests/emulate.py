@@ -17,7 +17,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
-from . import cnn, conv
+from fedmi.ops import cnn, conv
 
 _BF = torch.bfloat16
 
@@ -165,7 +165,7 @@ def dwconv_ws_floats(*a, **k):
 def prep_input(images_u8, base, nb, augment, seed, round_ctr, out=None, dbase=None):
     import numpy as np
 
-    from ..engine.data import augment_normalize
+    from fedmi.engine.data import augment_normalize
 
     b = base + (int(dbase.view(-1)[0]) if dbase is not None else 0)
     gidx = np.arange(b, b + nb) if augment else None
@@ -326,7 +326,7 @@ class _NativeStub:
 @contextlib.contextmanager
 def emulated():
     """Swap fedmi.ops kernels (and native.require) for their torch emulations."""
-    from .. import native
+    from fedmi import native
 
     saved = []
 

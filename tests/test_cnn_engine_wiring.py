@@ -1,5 +1,5 @@
 """CPU check of the native CNN engine's schedule: with every kernel swapped for
-its PyTorch emulation (fedmi.ops.emulate) and fp32 activation buffers, one
+its PyTorch emulation (tests/emulate.py) and fp32 activation buffers, one
 forward+backward through the engine must reproduce torch autograd's loss,
 parameter gradients and BN running statistics for ResNet (basic + bottleneck), VGG,
 MobileNet and MobileNetV2 to fp32 rounding.  (With bf16 activations even
@@ -14,7 +14,7 @@ import torch.nn.functional as F
 from fedmi.engine.base import TrainerConfig
 from fedmi.engine.data import augment_normalize, make_dataset
 from fedmi.models import build_model
-from fedmi.ops.emulate import emulated
+from emulate import emulated
 
 
 def _cos(a, b):

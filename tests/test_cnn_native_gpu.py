@@ -72,9 +72,9 @@ def test_loss_and_tail_grads_match_torch(gpu_device, name, tail):
 
 @pytest.mark.parametrize("name,avg_cos", [("ResNet18", 0.75), ("MobileNetV2", 0.35)])
 def test_native_matches_emulated_kernels_on_gpu(gpu_device, name, avg_cos):
-    """Same engine schedule, same bf16 buffers, kernels vs their PyTorch twins (fedmi.ops.emulate)."""
+    """Same engine schedule, same bf16 buffers, kernels vs their PyTorch twins (tests/emulate.py)."""
     from fedmi.engine.cnn_native import CNNNativeTrainer
-    from fedmi.ops.emulate import emulated
+    from emulate import emulated
 
     nb = 64
     data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=128, n_test=64, seed=0)

@@ -33,16 +33,6 @@ def test_sgd_flat(nat, gpu_device, n):
     assert torch.allclose(p, pr, rtol=1e-6, atol=1e-6)
 
 
-def test_fedavg_reduce(nat, gpu_device):
-    n = 62006
-    xs = [torch.randn(n, device=gpu_device) for _ in range(5)]
-    w = [0.2] * 5
-    out = torch.empty(n, device=gpu_device)
-    nat.fedavg_reduce(S(), [x.data_ptr() for x in xs], w, out.data_ptr(), n)
-    torch.cuda.synchronize()
-    assert torch.allclose(out, torch.stack(xs).mean(0), atol=1e-6)
-
-
 @pytest.mark.parametrize("n,k", [(62006, 620), (5000, 1), (5000, 5000), (1 << 20, 10000)])
 def test_topk_exact(nat, gpu_device, n, k):
     torch.manual_seed(k)
