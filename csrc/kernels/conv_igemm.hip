@@ -34,6 +34,8 @@
 #include <vector>
 #include <stdexcept>
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -922,6 +924,19 @@ static TileCfg pick_tiles(int M, int NC) {
   return TileCfg{(M > 64 && t128 >= cus) ? 128 : 64, BN};
 }
 
+// WGRAD always splits K, so the tile count never has to fill the chip: take the 128 x 128 tile
+// (twice the MFMA work per loaded byte) for O >= 256 -- measured 44 -> 38 us (256x256 3x3) and
+// 51 -> 47 us (512x512) at batch 128, but slower at O = 128.  FEDMI_WGRAD_TILE=64 restores 64 x 128.
+static TileCfg pick_tiles_wgrad(int M, int NC) {
+  static const int forced = [] {
+    const char* e = std::getenv("FEDMI_WGRAD_TILE");
+    return e ? std::atoi(e) : 0;
+  }();
+  TileCfg t = pick_tiles(M, NC);
+  if (forced != 64 && M >= 256 && NC > 64) t.BM = 128;
+  return t;
+}
+
 template <int MODE, int BM, int BN>
 static void launch_tiled(hipStream_t st, dim3 grid, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy,
                          bf16* out, float* gout, float* stats, const float* shift, int kps, int partial) {
@@ -953,7 +968,7 @@ static int fd_splits(const ConvGeom& g, long ws_floats) {
 template <int MODE>
 static void launch_mode(hipStream_t st, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy, bf16* out,
                         float* gout, float* stats, int splits, const float* shift = nullptr, int partial = 0) {
-  const TileCfg t = pick_tiles(g.M, g.NC);
+  const TileCfg t = MODE == WGRAD ? pick_tiles_wgrad(g.M, g.NC) : pick_tiles(g.M, g.NC);
   const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
   const int ksteps = (g.K + BK - 1) / BK;
   if (MODE != WGRAD && !(partial & 1)) splits = 1;
@@ -1091,7 +1106,7 @@ static void launch_fd(hipStream_t st, const ConvGeom& g, const bf16* x, const bf
 // K-split count for the weight gradient: about two workgroups per CU, at least
 // 8 K steps per split, and a bounded workspace.
 static int wgrad_splits(const ConvGeom& g, long ws_cap_floats) {
-  const TileCfg t = pick_tiles(g.M, g.NC);
+  const TileCfg t = pick_tiles_wgrad(g.M, g.NC);
   const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
   const int ksteps = (g.K + BK - 1) / BK;
   long sp = (2l * num_cus() + tiles - 1) / tiles;
