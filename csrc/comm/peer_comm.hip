@@ -237,13 +237,18 @@ PeerComm::~PeerComm() {
   (void)hipFree(sig_);
 }
 
+// Handle blob: [signal IPC handle][staging IPC handle][PCI bus id of the owner's GPU, 64 bytes].
+constexpr int kBusIdLen = 64;
+
 std::vector<uint8_t> PeerComm::handle() const {
   hipIpcMemHandle_t hs, hd;
   check_hip(hipIpcGetMemHandle(&hs, sig_), "hipIpcGetMemHandle(signal)");
   check_hip(hipIpcGetMemHandle(&hd, data_), "hipIpcGetMemHandle(staging)");
-  std::vector<uint8_t> out(2 * sizeof(hipIpcMemHandle_t));
+  std::vector<uint8_t> out(2 * sizeof(hipIpcMemHandle_t) + kBusIdLen, 0);
   std::memcpy(out.data(), &hs, sizeof(hs));
   std::memcpy(out.data() + sizeof(hs), &hd, sizeof(hd));
+  check_hip(hipDeviceGetPCIBusId(reinterpret_cast<char*>(out.data() + 2 * sizeof(hs)), kBusIdLen - 1, device_),
+            "hipDeviceGetPCIBusId");
   return out;
 }
 
@@ -251,9 +256,26 @@ void PeerComm::connect(const std::vector<std::vector<uint8_t>>& handles) {
   if ((int)handles.size() != a_.world) throw std::invalid_argument("PeerComm::connect: need one handle per rank");
   if (connected_) return;
   check_hip(hipSetDevice(device_), "hipSetDevice");
+  const size_t want = 2 * sizeof(hipIpcMemHandle_t) + kBusIdLen;
+  // refuse BEFORE mapping anything when a peer's GPU is not directly addressable from ours: the
+  // kernels dereference peer memory, and a missing xGMI / P2P path would fault instead of failing
   for (int p = 0; p < a_.world; ++p) {
     if (p == a_.rank) continue;
-    if (handles[p].size() != 2 * sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("PeerComm: bad handle size");
+    if (handles[p].size() != want) throw std::invalid_argument("PeerComm: bad handle size");
+    char bus[kBusIdLen];
+    std::memcpy(bus, handles[p].data() + 2 * sizeof(hipIpcMemHandle_t), kBusIdLen);
+    bus[kBusIdLen - 1] = 0;
+    int dev = -1;
+    check_hip(hipDeviceGetByPCIBusId(&dev, bus), "hipDeviceGetByPCIBusId");
+    if (dev != device_) {
+      int can = 0;
+      check_hip(hipDeviceCanAccessPeer(&can, device_, dev), "hipDeviceCanAccessPeer");
+      if (!can) throw std::runtime_error("PeerComm: GPU " + std::to_string(device_) + " cannot access peer GPU " +
+                                         std::to_string(dev));
+    }
+  }
+  for (int p = 0; p < a_.world; ++p) {
+    if (p == a_.rank) continue;
     hipIpcMemHandle_t hs, hd;
     std::memcpy(&hs, handles[p].data(), sizeof(hs));
     std::memcpy(&hd, handles[p].data() + sizeof(hs), sizeof(hd));
