@@ -631,6 +631,242 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
   }
 }
 
+// ---------------------------------------------------------------------------
+// Halo-patch implicit GEMM for 3x3 / stride 1 / pad 1 (FWD, and the stride-1
+// DGRAD through its flipped weight image -- also a 3x3 pad-1 convolution).
+//
+// conv_tap re-reads every input pixel once per tap: nine 128-B rows per output
+// pixel per 64-channel chunk go through L2 -> LDS, and at BN 128 that is 32 KiB
+// of LDS-DMA per 512 MFMA cycles -- more than a CU's L2 share delivers.  Here a
+// 128-pixel tile is IMGS images x TH rows x W columns, and its input window
+// (TH + 2 rows x W + 2 columns per image, zero halo) is DMA'd into LDS ONCE per
+// 64-channel chunk; the nine taps of that chunk read shifted rows of the same
+// patch.  Per K step only the weight tile streams (plus 1/7 of the next
+// chunk's patch), 16 + ~3.5 KiB instead of 32.
+//
+// Pipeline: weight tiles in three stages two steps ahead (as conv_tap); the
+// next chunk's patch goes to the other of two patch buffers, one piece per
+// step on taps 2..8 of the current chunk (the buffer's last reader, chunk c-1,
+// finished before the barrier of tap 0).  Each step's DMA count is fixed by
+// (BN, whether it carries a patch piece), so every wait is a counted vmcnt.
+// ---------------------------------------------------------------------------
+struct HaloGeom {
+  int N, H, W, C, O;
+  int M, K;                // M = N * H * W output pixels, K = 9 * C (weight row length)
+  int TH, IMGS;            // tile = IMGS images x TH rows x W columns = 128 pixels
+  int PW, NPR;             // patch row width W + 2, patch rows IMGS * (TH + 2) * (W + 2)
+  int nchunks;             // C / 64
+};
+
+template <int BN, int PP>
+__global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+                                                 bf16* __restrict__ out, float* __restrict__ part,
+                                                 float* __restrict__ stats, const float* __restrict__ shift,
+                                                 HaloGeom g, int chunks_per_split, const bf16* __restrict__ res) {
+  constexpr int BM = 128;
+  constexpr int NB = BN / 32;              // weight wave-instructions per step per wave
+  constexpr int TM = 4, TN = BN / 32;
+  constexpr int PCAP = PP == 1 ? 208 : 288;   // patch rows per buffer
+  constexpr int NPIECE = 7;                   // patch pieces per chunk (taps 2..8)
+  constexpr int WST = BN * 64;
+  constexpr int NST = 3;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * PCAP * 64 + NST * WST + 512];
+  bf16* const wbuf = smem + 2 * PCAP * 64;
+  bf16* const dummy = wbuf + NST * WST;       // landing row block for patch slots past PCAP
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = (g.O + BN - 1) / BN;
+  const int tile_n = blockIdx.x % ntn, tile_m = blockIdx.x / ntn;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * (BN / 2);
+  const int HW = g.H * g.W;
+  const int img0 = m0 / HW, h0 = (m0 - img0 * HW) / g.W;   // tile origin (IMGS > 1: h0 = 0)
+
+  const int c_begin = blockIdx.z * chunks_per_split;
+  const int c_end = min(g.nchunks, c_begin + chunks_per_split);
+  const int T0 = 9 * c_begin, T1 = 9 * c_end;
+
+  const int lrow = lane >> 3;
+  const int kc = (lane & 7) ^ lrow;          // logical 16-B chunk this lane's DMA carries
+  // patch slots: slot (piece p, wave, u) covers patch rows ((p * 4 + wave) * PP + u) * 8 + [0, 8)
+  int poff[NPIECE * PP];                     // input element offset of this lane's row (chunk 0), -1 = zero
+#pragma unroll
+  for (int s = 0; s < NPIECE * PP; ++s) {
+    const int p = s / PP, u = s - p * PP;
+    const int pr = ((p * 4 + wave) * PP + u) * 8 + lrow;
+    const int per_img = (g.TH + 2) * g.PW;
+    const int i = pr / per_img, rem = pr - i * per_img;
+    const int hh = rem / g.PW, ww = rem - hh * g.PW;
+    const int n = img0 + i, h = h0 - 1 + hh, w = ww - 1;
+    const bool ok = pr < g.NPR && n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+    poff[s] = ok ? ((n * g.H + h) * g.W + w) * g.C + kc * 8 : -1;
+  }
+  long b_off[NB];
+  bool b_ok[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int o = n0 + (wave * NB + i) * 8 + lrow;
+    b_ok[i] = o < g.O;
+    b_off[i] = (long)o * g.K + kc * 8;
+  }
+  // A fragment rows: tile pixel -> patch row at tap (0, 0)
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ml = wm0 + 16 * i + (lane & 15);
+    const int thw = g.TH * g.W;
+    const int im = ml / thw, rem = ml - im * thw;
+    const int p = rem / g.W, q = rem - p * g.W;
+    abase[i] = (im * (g.TH + 2) + p) * g.PW + q;
+  }
+
+  auto issue_piece = [&](int c, int p) {   // piece p of chunk c's patch -> buffer c & 1
+    bf16* pb = smem + (c & 1) * PCAP * 64;
+#pragma unroll
+    for (int u = 0; u < PP; ++u) {
+      const int slot = p * PP + u;
+      const int base = ((p * 4 + wave) * PP + u) * 8;
+      const int off = poff[slot];
+      const void* src = off >= 0 ? (const void*)(in + off + c * 64) : (const void*)g_zero16;
+      glds16(src, base < PCAP ? pb + base * 64 : dummy);
+    }
+  };
+  auto has_piece = [&](int t) { return t % 9 >= 2 && t / 9 + 1 < c_end; };
+  auto issue = [&](int t) {
+    const int c = t / 9, j = t - 9 * c;
+    bf16* Bs = wbuf + ((t - T0) % NST) * WST;
+    const long koff = (long)j * g.C + c * 64;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const void* src = b_ok[i] ? (const void*)(wt + b_off[i] + koff) : (const void*)g_zero16;
+      glds16(src, Bs + (wave * NB + i) * 8 * 64);
+    }
+    if (has_piece(t)) {
+#pragma unroll
+      for (int p = 0; p < NPIECE; ++p)   // constant piece index: poff stays in registers
+        if (p == j - 2) issue_piece(c + 1, p);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+
+  if (T0 < T1) {
+#pragma unroll
+    for (int p = 0; p < NPIECE; ++p) issue_piece(c_begin, p);
+    issue(T0);
+    if (T0 + 1 < T1) issue(T0 + 1);
+  }
+  for (int t = T0; t < T1; ++t) {
+    // wait for everything but issue(t + 1) (the youngest group in flight)
+    if (t + 1 < T1) {
+      const int younger = NB + (has_piece(t + 1) ? PP : 0);
+      if (younger == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if (younger == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if (younger == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (younger == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < T1) issue(t + 2);
+    const int c = t / 9, j = t - 9 * c;
+    const int r = j / 3, s = j - 3 * r;
+    const int tap = r * g.PW + s;
+    const bf16* Ps = smem + (c & 1) * PCAP * 64;
+    const bf16* Bs = wbuf + ((t - T0) % NST) * WST;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+      const int kq = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int pr = abase[i] + tap;
+        af[i] = *reinterpret_cast<const bf16x8*>(Ps + pr * 64 + ((kq ^ (pr & 7)) << 3));
+      }
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj) bfr[jj] = frag_sw(Bs, wn0 + 16 * jj, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj) acc[i][jj] = mfma16(af[i], bfr[jj], acc[i][jj]);
+    }
+  }
+  __syncthreads();   // no DMA in flight (vmcnt(0) on the last step), every wave done reading
+
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  if (part != nullptr) {   // split-K partial -> [split][M][O] fp32
+    float* ws = part + (long)blockIdx.z * g.M * g.O;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn0 + 16 * j + col_l;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wm0 + 16 * i + row_l + e;
+          if (m < g.M && col < g.O) ws[(long)m * g.O + col] = acc[i][j][e];
+        }
+    }
+    return;
+  }
+  constexpr int CT_LD = BN + 8;
+  bf16* ct = smem;
+  float* red = reinterpret_cast<float*>(smem + BM * CT_LD);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        ct[(wm0 + 16 * i + row_l + e) * CT_LD + wn0 + 16 * j + col_l] = (bf16)acc[i][j][e];
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int cidx = tid; cidx < BM * CPR; cidx += 256) {
+    const int row = cidx / CPR, cc = cidx % CPR;
+    const int m = m0 + row, col = n0 + cc * 8;
+    if (m < g.M && col < g.O) {
+      if (res != nullptr) {
+        bf16x8 tv = *reinterpret_cast<const bf16x8*>(ct + row * CT_LD + cc * 8);
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + (long)m * g.O + col);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) tv[q] = (bf16)((float)tv[q] + (float)rv[q]);
+        *reinterpret_cast<bf16x8*>(ct + row * CT_LD + cc * 8) = tv;
+      }
+      *reinterpret_cast<uint4*>(out + (long)m * g.O + col) = *reinterpret_cast<const uint4*>(ct + row * CT_LD + cc * 8);
+    }
+  }
+  if (res != nullptr) __syncthreads();
+  if (stats != nullptr) {
+    constexpr int PARTS = 256 / BN;
+    const int col = tid % BN, prt = tid / BN;
+    const int rows = min(BM, g.M - m0);
+    const float sh = (shift != nullptr && n0 + col < g.O) ? shift[n0 + col] : 0.f;
+    float s1 = 0.f, s2 = 0.f;
+    for (int rr = prt; rr < rows; rr += PARTS) {
+      const float v = (float)ct[rr * CT_LD + col] - sh;
+      s1 += v;
+      s2 += v * v;
+    }
+    red[(prt * 2) * BN + col] = s1;
+    red[(prt * 2 + 1) * BN + col] = s2;
+    __syncthreads();
+    if (tid < 2 * BN) {
+      const int q = tid / BN, cl = tid % BN;
+      float tsum = 0.f;
+#pragma unroll
+      for (int pp = 0; pp < PARTS; ++pp) tsum += red[(pp * 2 + q) * BN + cl];
+      if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, tsum);
+    }
+  }
+}
+
 // DGRAD weight images for conv_tap: for each sub-pixel phase (stride 1: the
 // single phase r0 = s0 = 0, nr = R, ns = S, step 1)
 //   wd[c][i][j][o] = W[o][c][r0 + step*(nr-1-i)][s0 + step*(ns-1-j)]   (c < Cw, else 0)
@@ -1010,10 +1246,85 @@ static int tap_splits(const TapGeom& g, long ws_floats) {
   return (ksteps + kps - 1) / kps;
 }
 
+// conv_halo geometry for a 3x3 / stride-1 / pad-1 problem, or false (then conv_tap runs it).
+// Opt-in (FEDMI_CONV_HALO=1, read per launch so a test can flip it) until it measures faster
+// than conv_tap end to end.
+static bool halo_geom(const TapGeom& g, const RowMap& rm, HaloGeom* h) {
+  const char* e = std::getenv("FEDMI_CONV_HALO");
+  const bool enabled = e && e[0] == '1';
+  if (!enabled || rm.on || g.R != 3 || g.S != 3 || g.st != 1 || g.pad_h != 1 || g.pad_w != 1 || g.P != g.H ||
+      g.Q != g.W || g.C % 64 || g.O % 8 || g.M % 128)
+    return false;
+  const int HW = g.H * g.W;
+  HaloGeom x{};
+  x.N = g.N; x.H = g.H; x.W = g.W; x.C = g.C; x.O = g.O; x.M = g.M; x.K = 9 * g.C;
+  if (HW <= 128) {
+    if (128 % HW) return false;
+    x.IMGS = 128 / HW; x.TH = g.H;
+  } else {
+    if (128 % g.W || g.H % (128 / g.W)) return false;
+    x.IMGS = 1; x.TH = 128 / g.W;
+  }
+  x.PW = g.W + 2;
+  x.NPR = x.IMGS * (x.TH + 2) * x.PW;
+  x.nchunks = g.C / 64;
+  if (x.NPR > 288) return false;
+  *h = x;
+  return true;
+}
+
+static int halo_splits(const HaloGeom& h, long ws_floats) {
+  if (ws_floats <= 0 || h.O > SPLITK_MAX_NC || h.nchunks < 2) return 1;
+  const int bn = tap_bn(h.O);
+  const long tiles = (long)(h.M / 128) * ((h.O + bn - 1) / bn);
+  const long target = (bn == 128 || h.NPR > 208 ? 1l : 2l) * num_cus();
+  if (4 * tiles >= 3 * target) return 1;
+  long sp = std::min<long>((target + tiles / 2) / tiles, h.nchunks);
+  sp = std::min<long>(sp, ws_floats / ((long)h.M * h.O));
+  if (sp < 2) return 1;
+  const int cps = (int)((h.nchunks + sp - 1) / sp);
+  return (h.nchunks + cps - 1) / cps;
+}
+
+static void launch_halo(hipStream_t st, const HaloGeom& h, const bf16* in, const bf16* wt, bf16* out, float* stats,
+                        const float* shift, float* ws, long ws_floats, const bf16* res) {
+  const int BN = tap_bn(h.O);
+  const long tiles = (long)(h.M / 128) * ((h.O + BN - 1) / BN);
+  const int sp = halo_splits(h, ws_floats);
+  const int cps = (h.nchunks + sp - 1) / sp;
+  const int splits = (h.nchunks + cps - 1) / cps;
+  dim3 grid((unsigned)tiles, 1, (unsigned)splits);
+  float* part = splits > 1 ? ws : nullptr;
+  float* stt = part ? nullptr : stats;
+  const bf16* rs = part ? nullptr : res;
+  const bool pp2 = h.NPR > 208;
+  if (BN == 128) {
+    if (pp2) hipLaunchKernelGGL((conv_halo<128, 2>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs);
+    else hipLaunchKernelGGL((conv_halo<128, 1>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs);
+  } else {
+    if (pp2) hipLaunchKernelGGL((conv_halo<64, 2>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs);
+    else hipLaunchKernelGGL((conv_halo<64, 1>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs);
+  }
+  if (splits > 1) {
+    const int VR = h.O / 8;
+    const int tb = (256 / VR) * VR;
+    const int rstep = tb / VR;
+    const int rows_per_block = stats ? std::max(2 * rstep, (h.M + 255) / 256) : std::max(rstep, (h.M + 1023) / 1024);
+    const int nblk = (h.M + rows_per_block - 1) / rows_per_block;
+    hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, splits, h.M, h.O, RowMap{}, out, stats,
+                       shift, rows_per_block, res);
+  }
+}
+
 static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const bf16* wt, bf16* out, float* stats,
                        const float* shift, const RowMap& rm, float* ws, long ws_floats,
                        const bf16* res = nullptr) {
   if (g.C % 64 || g.O % 8) throw std::invalid_argument("conv_tap: need C % 64 == 0 and O % 8 == 0");
+  HaloGeom hg;
+  if (halo_geom(g, rm, &hg)) {
+    launch_halo(st, hg, in, wt, out, stats, shift, ws, ws_floats, res);
+    return;
+  }
   const int BN = tap_bn(g.O);
   const long tiles = (long)((g.M + 127) / 128) * ((g.O + BN - 1) / BN);
   const int ksteps = g.K / 64;
@@ -1201,6 +1512,11 @@ long conv_fd_ws_floats(const ConvShape& s) {
     const TapGeom t = make_tap(s.N, s.H, s.W, s.C, s.O, s.P, s.Q, s.R, s.S, s.st, s.pad, s.pad);
     const int tsp = tap_splits(t, cap);
     if (tsp > 1) need = std::max(need, (long)tsp * t.M * t.O);
+    HaloGeom h;
+    if (halo_geom(t, RowMap{}, &h)) {
+      const int hsp = halo_splits(h, cap);
+      if (hsp > 1) need = std::max(need, (long)hsp * h.M * h.O);
+    }
   }
   if (s.O % 64 == 0) {
     TapPhase ph[4];
@@ -1209,6 +1525,11 @@ long conv_fd_ws_floats(const ConvShape& s) {
       if (ph[i].empty) continue;
       const int tsp = tap_splits(ph[i].g, cap);
       if (tsp > 1) need = std::max(need, (long)tsp * ph[i].g.M * ph[i].g.O);
+      HaloGeom h;
+      if (halo_geom(ph[i].g, ph[i].rm, &h)) {
+        const int hsp = halo_splits(h, cap);
+        if (hsp > 1) need = std::max(need, (long)hsp * h.M * h.O);
+      }
     }
   }
   ConvGeom d = make_geom(s);

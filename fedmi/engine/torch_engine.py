@@ -149,8 +149,8 @@ class TorchTrainer(LocalTrainer):
         if self.hybrid and x.dim() == 4 and not self._flat_input:
             from ..ops.native_mode import EW_COPY, ew
 
-            out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
-            return ew(out.contiguous(memory_format=torch.channels_last), [x], EW_COPY)
+            out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+            return ew(out, [x], EW_COPY)
         return x
 
     def _run(self, x: torch.Tensor) -> torch.Tensor:

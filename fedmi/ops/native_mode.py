@@ -681,7 +681,7 @@ def _cl_bf16(x: torch.Tensor) -> torch.Tensor:
     """channels-last contiguous bf16 (NCHW-shaped) -- a no-op for the engine's activations."""
     if x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last):
         return x
-    out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device).contiguous(memory_format=torch.channels_last)
+    out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
     return ew(out, [x], EW_COPY)
 
 
@@ -810,7 +810,7 @@ def _conv(func, input, weight, bias, stride, padding, dilation, transposed, outp
         Q = (W + 2 * pd[1] - dl[1] * (k[1] - 1) - 1) // st[1] + 1
         if dl != (1, 1):
             return None
-        out = torch.empty(N, O, P, Q, dtype=torch.bfloat16, device=dev).contiguous(memory_format=torch.channels_last)
+        out = torch.empty(N, O, P, Q, dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
         _nat().z_gconv(_st(dev), 0, zd(input), zd(w32), zd(out), int(groups), st[0], st[1], pd[0], pd[1])
     if bias is not None:
         ew(out, [out, bias.view(1, O, 1, 1)], EW_ADD, 1.0)

@@ -564,3 +564,76 @@ def test_resnet18_batch128_conv_shapes(gpu_device, shape):
     assert _rel(stats[1], (yb * yb).sum((0, 1, 2))) < 1e-3
     assert _rel(dx[..., :Cw].float(), _nhwc(xr.grad)) < 1e-2
     assert _rel(dw, wr_.grad) < 1e-2
+
+
+# conv_halo (3x3 / stride 1 / pad 1, input window DMA'd once per 64-channel chunk): every tile
+# geometry -- TH rows of one image (W 64 / 32 / 16), whole images per tile (8x8 -> 2, 4x4 -> 8 with the
+# 288-row patch), 3 chunks, O not a multiple of the 128-column tile; forward (+ BN statistics) and the
+# stride-1 DGRAD on the flipped weight image, outputs pre-filled with NaN.
+HALO_SHAPES = [
+    (2, 64, 64, 64, 64, 3, 1, 1),
+    (2, 32, 32, 128, 64, 3, 1, 1),
+    (4, 16, 16, 192, 96, 3, 1, 1),
+    (4, 8, 8, 64, 128, 3, 1, 1),
+    (8, 4, 4, 64, 136, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("shape", HALO_SHAPES, ids=[str(s) for s in HALO_SHAPES])
+def test_conv_halo_geometries(gpu_device, shape, monkeypatch):
+    monkeypatch.setenv("FEDMI_CONV_HALO", "1")
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device, seed=21)
+    xr = x.clone().requires_grad_(True)
+    ref = F.conv2d(xr, wb, stride=1, padding=1)
+    gy = torch.randn_like(ref).bfloat16().float()
+    ref.backward(gy)
+    wpk = conv.pack_weight(w)
+    rep = conv.stats_buffer(O, gpu_device)
+    y = torch.full((N, H, W, O), float("nan"), dtype=torch.bfloat16, device=gpu_device)
+    conv.conv2d_fwd(xn, wpk, 1, 1, Cw=Cw, stats=rep, out=y)
+    dyn = _nhwc(gy).bfloat16()
+    dx = None
+    if conv.dgrad_eligible(O):
+        wd = torch.empty(conv.dgrad_image_numel(w.shape, Cw), dtype=torch.bfloat16, device=gpu_device)
+        conv.dgrad_pack_weights([(w, wd, 1, 1, Cw)])
+        dx = torch.full_like(xn, float("nan"))
+        conv.conv2d_dgrad(dyn, wpk, xn.shape, 1, 1, Cw=Cw, out=dx, wd=wd)
+    torch.cuda.synchronize()
+    assert _rel(y.float(), _nhwc(ref.detach())) < 1e-2
+    st_ = conv.stats_total(rep)
+    assert _rel(st_[0], y.float().sum((0, 1, 2))) < 1e-3
+    if dx is not None:
+        assert not torch.isnan(dx.float()).any()
+        assert _rel(dx.float(), _nhwc(xr.grad)) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(128, 8, 8, 256, 256, 3, 1, 1), (128, 4, 4, 512, 512, 3, 1, 1)],
+                         ids=["layer3", "layer4"])
+def test_conv_halo_splitk_residual(gpu_device, shape, monkeypatch):
+    """conv_halo split over 64-channel chunks (fp32 partials + combine) with fused residual and BN
+    statistics, and the split stride-1 DGRAD."""
+    monkeypatch.setenv("FEDMI_CONV_HALO", "1")
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device, seed=22)
+    xr = x.clone().requires_grad_(True)
+    ref = F.conv2d(xr, wb, stride=1, padding=1)
+    gy = torch.randn_like(ref).bfloat16().float()
+    ref.backward(gy)
+    wpk = conv.pack_weight(w)
+    shp = (xn.shape, O, R, R, st, pad, Cw)
+    need = conv.fd_ws_floats(*shp)
+    assert need > 0
+    ws = torch.full((need,), float("nan"), device=gpu_device)
+    res = torch.randn(N, H, W, O, device=gpu_device).bfloat16()
+    rep = conv.stats_buffer(O, gpu_device)
+    y = conv.conv2d_fwd(xn, wpk, 1, 1, Cw=Cw, stats=rep, ws=ws, res=res)
+    torch.cuda.synchronize()
+    assert _rel(y.float(), _nhwc(ref.detach()) + res.float()) < 1e-2
+    assert _rel(conv.stats_total(rep)[0], y.float().sum((0, 1, 2))) < 1e-3
+    wd = torch.empty(conv.dgrad_image_numel(w.shape, Cw), dtype=torch.bfloat16, device=gpu_device)
+    conv.dgrad_pack_weights([(w, wd, 1, 1, Cw)])
+    ws.fill_(float("nan"))
+    dx = conv.conv2d_dgrad(_nhwc(gy).bfloat16(), wpk, xn.shape, 1, 1, Cw=Cw, ws=ws, wd=wd)
+    torch.cuda.synchronize()
+    assert _rel(dx.float(), _nhwc(xr.grad)) < 1e-2

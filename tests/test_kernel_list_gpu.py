@@ -1,0 +1,52 @@
+"""The kernels a training step launches are fedmi's own ("assert a kernel list").
+
+torch.profiler records every GPU kernel of an eager step; the step of the flagship LeNet engine and
+of a native-mode zoo model (the aten backend) must launch no ATen, MIOpen or rocBLAS/hipBLASLt kernel.
+"""
+import pytest
+import torch
+from torch.profiler import ProfilerActivity, profile
+
+from fedmi.engine import build_trainer
+from fedmi.engine.base import TrainerConfig
+from fedmi.engine.data import contiguous_schedule, make_dataset
+
+pytestmark = pytest.mark.gpu
+
+FOREIGN = ("at::native", "miopen", "MIOpen", "Cijk_", "rocblas", "hipblaslt", "igemm_", "naive_conv")
+
+
+def _kernels(fn):
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+    return [n for n in names if "memcpy" not in n.lower() and "memset" not in n.lower()
+            and "copyBuffer" not in n and "fillBuffer" not in n]
+
+
+def test_lenet_step_launches_only_fedmi_kernels(gpu_device):
+    data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=256, n_test=128, seed=0)
+    tr = build_trainer("lenet", data, gpu_device, TrainerConfig(seed=1, use_graph=False))
+    tr.set_schedule(*contiguous_schedule(256, 128))
+    tr.train_epoch()                                   # warm-up (packing, first-touch)
+    names = _kernels(tr.train_epoch)
+    assert names, "profiler saw no kernels"
+    bad = [n for n in names if any(f in n for f in FOREIGN)]
+    assert not bad, bad[:10]
+    assert any("lenet_fwd_head" in n for n in names) and any("lenet_conv_bwd" in n for n in names), set(names)
+
+
+@pytest.mark.parametrize("name", ["SimpleDLA", "RegNetX_200MF"])
+def test_native_mode_step_launches_only_fedmi_kernels(gpu_device, name):
+    data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=256, n_test=64, seed=0)
+    tr = build_trainer(name, data, gpu_device, TrainerConfig(batch_size=128, seed=1, augment=False))
+    tr.use_graph = False
+    x, y = tr._batch(0, 128)                           # input prep (augment / layout) outside the step
+    tr.model.train()
+    tr._step_body(x, y)                                # warm-up
+    names = _kernels(lambda: tr._step_body(x, y))
+    bad = [n for n in names if any(f in n for f in FOREIGN)]
+    assert not bad, sorted(set(bad))[:10]
+    assert not tr.mode.fallbacks
+    assert any("conv_igemm" in n or "conv_tap" in n for n in names)
