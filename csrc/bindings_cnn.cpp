@@ -38,6 +38,7 @@ void launch_conv_pack_multi(hipStream_t, const PackItem*, int);
 void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int);
 long conv_wgrad_ws_floats(const ConvShape&);
 void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int);
+void set_conv_halo_stamps(long long*);
 
 struct BNDesc {
   const float* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
@@ -114,6 +115,8 @@ BNDesc bn_from(const py::dict& d) {
 
 void fedmi_bind_cnn(py::module_& m) {
   m.attr("STAT_REP") = STAT_REP;
+  // diagnostic: conv_halo writes 8 int64 per workgroup (see the kernel) into this device buffer; 0 = off
+  m.def("conv_halo_stamps", [](uintptr_t p) { set_conv_halo_stamps(reinterpret_cast<long long*>(p)); });
   m.def("conv_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                        uintptr_t shift, uintptr_t ws, long ws_floats, uintptr_t res) {
     launch_conv_fwd(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(w), P<bf16>(y), P<float>(stats),

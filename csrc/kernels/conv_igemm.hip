@@ -31,6 +31,7 @@
 // Reference parity: these are the convolution / convolution_backward ops of
 // every zoo model (src/models/resnet.py:14-104 etc.).
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 #include <stdexcept>
 
@@ -589,7 +590,38 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         ct[(wm0 + 16 * i + row_l + e) * CT_LD + wn0 + 16 * j + col_l] = (bf16)acc[i][j][e];
+  if (stats != nullptr && res == nullptr) {
+    // BN statistics of bf16(y) - shift straight from the accumulators (rows past M masked), the wave's
+    // 4 row groups combined by cross-lane adds, the two row halves of the tile through LDS
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn0 + 16 * j + col_l;
+      const float sh = (shift != nullptr && col < g.O) ? shift[col] : 0.f;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = (m0 + wm0 + 16 * i + row_l + e < g.M) ? (float)(bf16)acc[i][j][e] - sh : 0.f;
+          s1 += v;
+          s2 += v * v;
+        }
+      s1 += __shfl_xor(s1, 16);
+      s2 += __shfl_xor(s2, 16);
+      s1 += __shfl_xor(s1, 32);
+      s2 += __shfl_xor(s2, 32);
+      if (lane < 16) {
+        red[((wave >> 1) * 2) * BN + wn0 + 16 * j + lane] = s1;
+        red[((wave >> 1) * 2 + 1) * BN + wn0 + 16 * j + lane] = s2;
+      }
+    }
+  }
   __syncthreads();
+  if (stats != nullptr && res == nullptr && tid < 2 * BN) {
+    const int q = tid / BN, cl = tid % BN;
+    const float tsum = red[q * BN + cl] + red[(2 + q) * BN + cl];
+    if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, tsum);
+  }
   constexpr int CPR = BN / 8;
   for (int c = tid; c < BM * CPR; c += 256) {
     const int row = c / CPR, cc = c % CPR;
@@ -606,8 +638,8 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
       *reinterpret_cast<uint4*>(out + orow * g.O + col) = *reinterpret_cast<const uint4*>(ct + row * CT_LD + cc * 8);
     }
   }
-  if (res != nullptr) __syncthreads();
-  if (stats != nullptr) {   // BN batch statistics of bf16(y) - shift, one atomic per column per WG
+  if (stats != nullptr && res != nullptr) {   // statistics of y = conv + res, from the summed tile
+    __syncthreads();
     constexpr int PARTS = 256 / BN;
     const int col = tid % BN, prt = tid / BN;
     const int rows = min(BM, g.M - m0);
@@ -644,11 +676,12 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
 // patch.  Per K step only the weight tile streams (plus 1/7 of the next
 // chunk's patch), 16 + ~3.5 KiB instead of 32.
 //
-// Pipeline: weight tiles in three stages two steps ahead (as conv_tap); the
-// next chunk's patch goes to the other of two patch buffers, one piece per
-// step on taps 2..8 of the current chunk (the buffer's last reader, chunk c-1,
-// finished before the barrier of tap 0).  Each step's DMA count is fixed by
-// (BN, whether it carries a patch piece), so every wait is a counted vmcnt.
+// Pipeline: weight tiles in NST stages, NST - 1 steps ahead; chunk c + 1's
+// whole patch is issued at tap 0 of chunk c into the other of two patch
+// buffers (its last reader, chunk c - 1, finished before that barrier), so it
+// has nine steps to land.  Every wait is a counted vmcnt over the groups still
+// allowed in flight.  BatchNorm statistics come straight from the accumulators
+// (bf16-rounded, cross-lane reduced), not from a serial pass over the tile.
 // ---------------------------------------------------------------------------
 struct HaloGeom {
   int N, H, W, C, O;
@@ -656,20 +689,37 @@ struct HaloGeom {
   int TH, IMGS;            // tile = IMGS images x TH rows x W columns = 128 pixels
   int PW, NPR;             // patch row width W + 2, patch rows IMGS * (TH + 2) * (W + 2)
   int nchunks;             // C / 64
+  FastDiv dPI, dPW, dTHW, dW, dHW;   // by (TH + 2) * PW, PW, TH * W, W, H * W
 };
 
-template <int BN, int PP>
+// s_waitcnt vmcnt(n) for a run-time n <= N (expcnt / lgkmcnt left at their maxima)
+template <int N>
+FEDMI_DEV void vm_wait_le(int n) {
+  if constexpr (N <= 0) {
+    __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
+  } else {
+    if (n >= N) __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+    else vm_wait_le<N - 1>(n);
+  }
+}
+
+template <int BN, int PP, int NST>
 __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                  bf16* __restrict__ out, float* __restrict__ part,
                                                  float* __restrict__ stats, const float* __restrict__ shift,
-                                                 HaloGeom g, int chunks_per_split, const bf16* __restrict__ res) {
+                                                 HaloGeom g, int chunks_per_split, const bf16* __restrict__ res,
+                                                 long long* __restrict__ stamps) {
+  // stamps (diagnostic, null in production): per workgroup [realtime at start, memtime at start, after
+  // the prologue's data landed, after the main loop, at the end]
+  long long st0 = 0, st1 = 0, st2 = 0;
+  const long long rt0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  if (stamps) st0 = __builtin_amdgcn_s_memtime();
   constexpr int BM = 128;
   constexpr int NB = BN / 32;              // weight wave-instructions per step per wave
   constexpr int TM = 4, TN = BN / 32;
   constexpr int PCAP = PP == 1 ? 208 : 288;   // patch rows per buffer
-  constexpr int NPIECE = 7;                   // patch pieces per chunk (taps 2..8)
+  constexpr int NPS = 7 * PP;                 // patch wave-instructions per chunk per wave (<= 224 * PP rows)
   constexpr int WST = BN * 64;
-  constexpr int NST = 3;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * PCAP * 64 + NST * WST + 512];
   bf16* const wbuf = smem + 2 * PCAP * 64;
   bf16* const dummy = wbuf + NST * WST;       // landing row block for patch slots past PCAP
@@ -680,7 +730,7 @@ __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, co
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * (BN / 2);
   const int HW = g.H * g.W;
-  const int img0 = m0 / HW, h0 = (m0 - img0 * HW) / g.W;   // tile origin (IMGS > 1: h0 = 0)
+  const int img0 = fdiv(m0, g.dHW), h0 = fdiv(m0 - img0 * HW, g.dW);   // tile origin (IMGS > 1: h0 = 0)
 
   const int c_begin = blockIdx.z * chunks_per_split;
   const int c_end = min(g.nchunks, c_begin + chunks_per_split);
@@ -688,18 +738,17 @@ __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, co
 
   const int lrow = lane >> 3;
   const int kc = (lane & 7) ^ lrow;          // logical 16-B chunk this lane's DMA carries
-  // patch slots: slot (piece p, wave, u) covers patch rows ((p * 4 + wave) * PP + u) * 8 + [0, 8)
-  int poff[NPIECE * PP];                     // input element offset of this lane's row (chunk 0), -1 = zero
+  // patch slot s of this wave covers patch rows (s * 4 + wave) * 8 + [0, 8)
+  int poff[NPS];                             // input element offset of this lane's row (chunk 0), -1 = zero
+  const int per_img = (g.TH + 2) * g.PW;
 #pragma unroll
-  for (int s = 0; s < NPIECE * PP; ++s) {
-    const int p = s / PP, u = s - p * PP;
-    const int pr = ((p * 4 + wave) * PP + u) * 8 + lrow;
-    const int per_img = (g.TH + 2) * g.PW;
-    const int i = pr / per_img, rem = pr - i * per_img;
-    const int hh = rem / g.PW, ww = rem - hh * g.PW;
+  for (int sl = 0; sl < NPS; ++sl) {
+    const int pr = (sl * 4 + wave) * 8 + lrow;
+    const int i = fdiv(pr, g.dPI), rem = pr - i * per_img;
+    const int hh = fdiv(rem, g.dPW), ww = rem - hh * g.PW;
     const int n = img0 + i, h = h0 - 1 + hh, w = ww - 1;
     const bool ok = pr < g.NPR && n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-    poff[s] = ok ? ((n * g.H + h) * g.W + w) * g.C + kc * 8 : -1;
+    poff[sl] = ok ? ((n * g.H + h) * g.W + w) * g.C + kc * 8 : -1;
   }
   long b_off[NB];
   bool b_ok[NB];
@@ -715,36 +764,27 @@ __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, co
   for (int i = 0; i < TM; ++i) {
     const int ml = wm0 + 16 * i + (lane & 15);
     const int thw = g.TH * g.W;
-    const int im = ml / thw, rem = ml - im * thw;
-    const int p = rem / g.W, q = rem - p * g.W;
+    const int im = fdiv(ml, g.dTHW), rem = ml - im * thw;
+    const int p = fdiv(rem, g.dW), q = rem - p * g.W;
     abase[i] = (im * (g.TH + 2) + p) * g.PW + q;
   }
 
-  auto issue_piece = [&](int c, int p) {   // piece p of chunk c's patch -> buffer c & 1
+  auto issue_patch = [&](int c) {   // chunk c's whole patch -> buffer c & 1
     bf16* pb = smem + (c & 1) * PCAP * 64;
 #pragma unroll
-    for (int u = 0; u < PP; ++u) {
-      const int slot = p * PP + u;
-      const int base = ((p * 4 + wave) * PP + u) * 8;
-      const int off = poff[slot];
-      const void* src = off >= 0 ? (const void*)(in + off + c * 64) : (const void*)g_zero16;
+    for (int sl = 0; sl < NPS; ++sl) {
+      const int base = (sl * 4 + wave) * 8;
+      const void* src = poff[sl] >= 0 ? (const void*)(in + poff[sl] + c * 64) : (const void*)g_zero16;
       glds16(src, base < PCAP ? pb + base * 64 : dummy);
     }
   };
-  auto has_piece = [&](int t) { return t % 9 >= 2 && t / 9 + 1 < c_end; };
-  auto issue = [&](int t) {
-    const int c = t / 9, j = t - 9 * c;
-    bf16* Bs = wbuf + ((t - T0) % NST) * WST;
+  auto issue_w = [&](int c, int j, int stage) {   // weight tile of step (c, j) -> stage
+    bf16* Bs = wbuf + stage * WST;
     const long koff = (long)j * g.C + c * 64;
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const void* src = b_ok[i] ? (const void*)(wt + b_off[i] + koff) : (const void*)g_zero16;
       glds16(src, Bs + (wave * NB + i) * 8 * 64);
-    }
-    if (has_piece(t)) {
-#pragma unroll
-      for (int p = 0; p < NPIECE; ++p)   // constant piece index: poff stays in registers
-        if (p == j - 2) issue_piece(c + 1, p);
     }
   };
 
@@ -754,33 +794,40 @@ __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, co
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
 
+  // DMA groups (per wave): the prologue issues chunk c_begin's patch and the weights of the first
+  // NST - 1 steps; iteration t issues the weights of step t + NST - 1 and, at a chunk's tap 0, the
+  // next chunk's whole patch.  At iteration t the groups of iterations t - NST + 2 .. t - 1 may stay
+  // in flight: NB each while they carried weights (all but the last NST - 1 iterations), plus NPS
+  // when tap 0 of this chunk is among them and a next chunk exists.
+  constexpr int STEADY = (NST - 2) * NB;
   if (T0 < T1) {
+    issue_patch(c_begin);
 #pragma unroll
-    for (int p = 0; p < NPIECE; ++p) issue_piece(c_begin, p);
-    issue(T0);
-    if (T0 + 1 < T1) issue(T0 + 1);
+    for (int k = 0; k < NST - 1; ++k)
+      if (T0 + k < T1) issue_w((T0 + k) / 9, (T0 + k) % 9, k);
   }
+  int c = c_begin, j = 0;                  // step t = 9 c + j
+  int stg = 0;                             // stage holding step t
+  int wc = (T0 + NST - 1) / 9, wj = (T0 + NST - 1) % 9;   // step t + NST - 1
   for (int t = T0; t < T1; ++t) {
-    // wait for everything but issue(t + 1) (the youngest group in flight)
-    if (t + 1 < T1) {
-      const int younger = NB + (has_piece(t + 1) ? PP : 0);
-      if (younger == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else if (younger == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else if (younger == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if (younger == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    const bool pin = j >= 1 && j <= NST - 2 && c + 1 < c_end;   // next chunk's patch in the window
+    const int tail = T1 - 1 - t;
+    if (tail >= NST - 2 && !pin) {
+      vm_wait_le<STEADY>(STEADY);
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int younger = NB * min(NST - 2, tail) + (pin ? NPS : 0);
+      vm_wait_le<STEADY + NPS>(younger);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 2 < T1) issue(t + 2);
-    const int c = t / 9, j = t - 9 * c;
+    if (stamps && t == T0) st1 = __builtin_amdgcn_s_memtime();
+    if (t + NST - 1 < T1) issue_w(wc, wj, stg == 0 ? NST - 1 : stg - 1);
+    if (j == 0 && c + 1 < c_end) issue_patch(c + 1);
     const int r = j / 3, s = j - 3 * r;
     const int tap = r * g.PW + s;
     const bf16* Ps = smem + (c & 1) * PCAP * 64;
-    const bf16* Bs = wbuf + ((t - T0) % NST) * WST;
+    const bf16* Bs = wbuf + stg * WST;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[TM], bfr[TN];
@@ -797,8 +844,19 @@ __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, co
 #pragma unroll
         for (int jj = 0; jj < TN; ++jj) acc[i][jj] = mfma16(af[i], bfr[jj], acc[i][jj]);
     }
+    if (++j == 9) { j = 0; ++c; }
+    if (++wj == 9) { wj = 0; ++wc; }
+    if (++stg == NST) stg = 0;
   }
-  __syncthreads();   // no DMA in flight (vmcnt(0) on the last step), every wave done reading
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();   // no DMA in flight, every wave done reading
+  if (stamps) st2 = __builtin_amdgcn_s_memtime();
+  auto put_stamps = [&]() {
+    if (stamps && tid == 0) {
+      long long* d = stamps + 8l * (blockIdx.x + (long)gridDim.x * blockIdx.z);
+      d[0] = rt0; d[1] = st0; d[2] = st1; d[3] = st2; d[4] = __builtin_amdgcn_s_memtime();
+    }
+  };
 
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
   if (part != nullptr) {   // split-K partial -> [split][M][O] fp32
@@ -811,14 +869,15 @@ __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, co
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int m = m0 + wm0 + 16 * i + row_l + e;
-          if (m < g.M && col < g.O) ws[(long)m * g.O + col] = acc[i][j][e];
+          if (col < g.O) ws[(long)m * g.O + col] = acc[i][j][e];
         }
     }
+    put_stamps();
     return;
   }
   constexpr int CT_LD = BN + 8;
   bf16* ct = smem;
-  float* red = reinterpret_cast<float*>(smem + BM * CT_LD);
+  float* red = reinterpret_cast<float*>(smem + BM * CT_LD);   // [2 row halves][2][BN]
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -826,12 +885,43 @@ __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, co
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         ct[(wm0 + 16 * i + row_l + e) * CT_LD + wn0 + 16 * j + col_l] = (bf16)acc[i][j][e];
+  if (stats != nullptr && res == nullptr) {
+    // sums of bf16(y) - shift over this wave's 64 rows, per column: registers, then the 4 row groups
+    // of the wave (lanes l, l^16, l^32, l^48) by cross-lane adds
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn0 + 16 * j + col_l;
+      const float sh = (shift != nullptr && col < g.O) ? shift[col] : 0.f;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = (float)(bf16)acc[i][j][e] - sh;
+          s1 += v;
+          s2 += v * v;
+        }
+      s1 += __shfl_xor(s1, 16);
+      s2 += __shfl_xor(s2, 16);
+      s1 += __shfl_xor(s1, 32);
+      s2 += __shfl_xor(s2, 32);
+      if (lane < 16) {
+        red[((wave >> 1) * 2) * BN + wn0 + 16 * j + lane] = s1;
+        red[((wave >> 1) * 2 + 1) * BN + wn0 + 16 * j + lane] = s2;
+      }
+    }
+  }
   __syncthreads();
+  if (stats != nullptr && res == nullptr && tid < 2 * BN) {
+    const int q = tid / BN, cl = tid % BN;
+    const float tsum = red[q * BN + cl] + red[(2 + q) * BN + cl];
+    if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, tsum);
+  }
   constexpr int CPR = BN / 8;
   for (int cidx = tid; cidx < BM * CPR; cidx += 256) {
     const int row = cidx / CPR, cc = cidx % CPR;
     const int m = m0 + row, col = n0 + cc * 8;
-    if (m < g.M && col < g.O) {
+    if (col < g.O) {
       if (res != nullptr) {
         bf16x8 tv = *reinterpret_cast<const bf16x8*>(ct + row * CT_LD + cc * 8);
         const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + (long)m * g.O + col);
@@ -842,14 +932,13 @@ __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, co
       *reinterpret_cast<uint4*>(out + (long)m * g.O + col) = *reinterpret_cast<const uint4*>(ct + row * CT_LD + cc * 8);
     }
   }
-  if (res != nullptr) __syncthreads();
-  if (stats != nullptr) {
+  if (stats != nullptr && res != nullptr) {   // statistics of y = conv + res: from the summed tile
+    __syncthreads();
     constexpr int PARTS = 256 / BN;
     const int col = tid % BN, prt = tid / BN;
-    const int rows = min(BM, g.M - m0);
     const float sh = (shift != nullptr && n0 + col < g.O) ? shift[n0 + col] : 0.f;
     float s1 = 0.f, s2 = 0.f;
-    for (int rr = prt; rr < rows; rr += PARTS) {
+    for (int rr = prt; rr < BM; rr += PARTS) {
       const float v = (float)ct[rr * CT_LD + col] - sh;
       s1 += v;
       s2 += v * v;
@@ -864,6 +953,194 @@ __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, co
       for (int pp = 0; pp < PARTS; ++pp) tsum += red[(pp * 2 + q) * BN + cl];
       if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, tsum);
     }
+  }
+  put_stamps();
+}
+
+// ---------------------------------------------------------------------------
+// Halo-patch WGRAD for 3x3 / stride 1 / pad 1:
+//   dW[o][(r, s, c)] = sum_{pixels m} dY[m][o] * X[m shifted by (r - 1, s - 1)][c]
+// One workgroup owns 64 output channels x (9 taps x 64 input channels) = 64 x 576
+// fp32 accumulators and walks 128-pixel blocks of its K split.  Per block the
+// dY tile [128 px][64 o] and the block's input window [rows][64 c] (the fwd
+// halo geometry) are DMA'd once; all nine taps read shifted rows of the same
+// window, so each barrier amortises 144 MFMAs per wave (the generic WGRAD: 16)
+// and no im2col row is ever re-fetched.  Both LDS images use the MNC swizzle
+// (mnc_off<64>), written by the DMA through per-lane source columns, and are
+// read with ds_read_b64_tr_b16 at precomputed per-lane offsets (kk, tap).
+// Waves split the 64 input channels (16 each); the fp32 partial of a split goes
+// to ws[split][o][(r, s, c)] -- the generic WGRAD's layout, so its reduce kernels
+// sum the splits and permute into [O][Cw][3][3].
+// ---------------------------------------------------------------------------
+template <int PP>
+__global__ __launch_bounds__(256) void conv_wgrad_halo(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                       float* __restrict__ ws, HaloGeom g, int blocks_per_split) {
+  constexpr int PCAP = PP == 1 ? 208 : 288;
+  constexpr int NPS = 7 * PP;             // patch wave-instructions per block per wave
+  constexpr int DYE = 128 * 64;           // dY stage elements
+  constexpr int PTE = PCAP * 64;          // patch stage elements
+  constexpr int NST = 3;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NST * (DYE + PTE) + 512];
+  bf16* const dummy = smem + NST * (DYE + PTE);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nct = g.nchunks;                       // c-chunk tiles
+  const int o0 = (blockIdx.x / nct) * 64, c0 = (blockIdx.x % nct) * 64;
+  const int nblk = g.M / 128;
+  const int b_begin = blockIdx.z * blocks_per_split;
+  const int b_end = min(nblk, b_begin + blocks_per_split);
+  const int HW = g.H * g.W;
+  const int per_img = (g.TH + 2) * g.PW;
+
+  // ---- DMA lanes: row R = base + (lane >> 3), physical 16-B slot sl = lane & 7 holds logical
+  // columns ((sl >> 1) ^ f(R)) * 16 + (sl & 1) * 8  (mnc_off<64> inverse)
+  const int lr = lane >> 3, sl = lane & 7;
+  auto lcol = [&](int R) {
+    const int f = ((R >> 1) & 1) | (((R >> 3) & 1) << 1);
+    return (((sl >> 1) ^ f) << 4) + ((sl & 1) << 3);
+  };
+  // dY rows: 128 per block -> 16 instructions, 4 per wave: rows (u * 4 + wave) * 8 + lr
+  int dyo[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int R = (u * 4 + wave) * 8 + lr;
+    dyo[u] = R * g.O + o0 + lcol(R);             // + block * 128 * O
+  }
+  // patch rows (q * 4 + wave) * 8 + lr: (image, row, column) of the window packed as i << 16 | hh << 8 | ww
+  // (-1 past the window's rows)
+  int pk[NPS];
+#pragma unroll
+  for (int q = 0; q < NPS; ++q) {
+    const int pr = (q * 4 + wave) * 8 + lr;
+    const int i = fdiv(pr, g.dPI), rem = pr - i * per_img;
+    const int hh = fdiv(rem, g.dPW), ww = rem - hh * g.PW;
+    pk[q] = pr < g.NPR ? (i << 16) | (hh << 8) | ww : -1;
+  }
+  auto issue = [&](int b, int stage) {
+    bf16* Ds = smem + stage * (DYE + PTE);
+    bf16* Ps = Ds + DYE;
+    const long mb = (long)b * 128;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) glds16(dy + mb * g.O + dyo[u], Ds + (u * 4 + wave) * 512);
+    const int m0 = b * 128;
+    const int img0 = fdiv(m0, g.dHW), h0 = fdiv(m0 - img0 * HW, g.dW);
+#pragma unroll
+    for (int q = 0; q < NPS; ++q) {
+      const int base = (q * 4 + wave) * 8;
+      const int n = img0 + (pk[q] >> 16), h = h0 + ((pk[q] >> 8) & 255) - 1, w = (pk[q] & 255) - 1;
+      const bool ok = pk[q] >= 0 && n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const void* src = ok ? (const void*)(x + (((long)n * g.H + h) * g.W + w) * g.C + c0 + lcol(base + lr))
+                           : (const void*)g_zero16;
+      glds16(src, base < PCAP ? Ps + base * 64 : dummy);
+    }
+  };
+
+  const int nb = b_end - b_begin;
+  if (nb > 0) issue(b_begin, 0);         // the first two blocks load while the offset tables are built
+  if (nb > 1) issue(b_begin + 1, 1);
+
+  // ---- fragment offsets (elements, stage-relative).  frag_mnc's lane map: g4 = lane >> 4,
+  // q4 = (lane & 15) >> 2, p4 = lane & 3; rows kk * 32 + 8 g4 + q4 and + 4; columns col0 + 4 p4.
+  const int g4 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  int aoff[4][4][2];        // [kk][o block][row half] in the dY image
+  int boff[4][9][2];        // [kk][tap][row half] in the patch image
+  const int thw = g.TH * g.W;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int k = kk * 32 + 8 * g4 + q4 + 4 * h2;        // pixel of the block
+#pragma unroll
+      for (int i = 0; i < 4; ++i) aoff[kk][i][h2] = mnc_off<64>(k, 16 * i + 4 * p4);
+      const int im = fdiv(k, g.dTHW), rem = k - im * thw;
+      const int pp = fdiv(rem, g.dW), qq = rem - pp * g.W;
+      const int prow = (im * (g.TH + 2) + pp) * g.PW + qq;  // patch row at tap (0, 0)
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+        boff[kk][t][h2] = mnc_off<64>(prow + (t / 3) * g.PW + (t % 3), wave * 16 + 4 * p4);
+    }
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  auto tr = [&](const bf16* base, int o0_, int o1_) {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + o0_));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + o1_));
+    const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo);
+    const bf16x4 h4 = __builtin_bit_cast(bf16x4, hi);
+    return (bf16x8)__builtin_shufflevector(l4, h4, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = zero4();
+
+  constexpr int GRP = 4 + NPS;            // DMA instructions per block per wave
+  auto step = [&](int it, auto stg) {
+    constexpr int S = decltype(stg)::value;
+    if (it + 1 < nb) vm_wait_le<GRP>(GRP);
+    else vm_wait_le<0>(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + 2 < nb) issue(b_begin + it + 2, (S + 2) % NST);
+    const bf16* Ds = smem + S * (DYE + PTE);
+    const bf16* Ps = Ds + DYE;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = tr(Ds, aoff[kk][i][0], aoff[kk][i][1]);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const bf16x8 bfr = tr(Ps, boff[kk][t][0], boff[kk][t][1]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][t] = mfma16(af[i], bfr, acc[i][t]);
+      }
+    }
+  };
+  for (int it = 0; it < nb; it += NST) {
+    step(it, std::integral_constant<int, 0>{});
+    if (it + 1 < nb) step(it + 1, std::integral_constant<int, 1>{});
+    if (it + 2 < nb) step(it + 2, std::integral_constant<int, 2>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- partial -> ws[split][o][tap * C + c], staged through LDS (free after the loop) so that every
+  // global store is 16 bytes: two passes of 32 output channels; each lane drops its 4 consecutive-o
+  // values of a column as one 16-B LDS write into a [576 col][32 o (+1 pad)] tile, then each thread
+  // gathers 4 consecutive columns of one o and stores them as a float4.
+  constexpr int TLD = 33;
+  float* tile = reinterpret_cast<float*>(smem);    // 576 x 33 floats = 76 KB
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  const long NC = 9l * g.C;
+  float* wsp = ws + (long)blockIdx.z * g.O * NC;
+  __syncthreads();
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int i = 2 * half + ii;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int col = t * 64 + wave * 16 + col_l;     // column within the tile (tap, c)
+        float* d = tile + col * TLD + 16 * ii + row_l;
+        d[0] = acc[i][t][0]; d[1] = acc[i][t][1]; d[2] = acc[i][t][2]; d[3] = acc[i][t][3];
+      }
+    }
+    __syncthreads();
+    // 32 o x 144 column quads
+    for (int idx = tid; idx < 32 * 144; idx += 256) {
+      const int ol = idx / 144, cq = idx - ol * 144;
+      const int col = cq * 4;
+      float4 v;
+      v.x = tile[(col + 0) * TLD + ol];
+      v.y = tile[(col + 1) * TLD + ol];
+      v.z = tile[(col + 2) * TLD + ol];
+      v.w = tile[(col + 3) * TLD + ol];
+      const int t = col >> 6, c = col & 63;
+      *reinterpret_cast<float4*>(wsp + (long)(o0 + 32 * half + ol) * NC + t * g.C + c0 + c) = v;
+    }
+    __syncthreads();
   }
 }
 
@@ -1249,9 +1526,9 @@ static int tap_splits(const TapGeom& g, long ws_floats) {
 // conv_halo geometry for a 3x3 / stride-1 / pad-1 problem, or false (then conv_tap runs it).
 // Opt-in (FEDMI_CONV_HALO=1, read per launch so a test can flip it) until it measures faster
 // than conv_tap end to end.
-static bool halo_geom(const TapGeom& g, const RowMap& rm, HaloGeom* h) {
+static bool halo_geom(const TapGeom& g, const RowMap& rm, HaloGeom* h, bool gate = true) {
   const char* e = std::getenv("FEDMI_CONV_HALO");
-  const bool enabled = e && e[0] == '1';
+  const bool enabled = !gate || (e && e[0] == '1');
   if (!enabled || rm.on || g.R != 3 || g.S != 3 || g.st != 1 || g.pad_h != 1 || g.pad_w != 1 || g.P != g.H ||
       g.Q != g.W || g.C % 64 || g.O % 8 || g.M % 128)
     return false;
@@ -1269,6 +1546,8 @@ static bool halo_geom(const TapGeom& g, const RowMap& rm, HaloGeom* h) {
   x.NPR = x.IMGS * (x.TH + 2) * x.PW;
   x.nchunks = g.C / 64;
   if (x.NPR > 288) return false;
+  x.dPI = make_div((x.TH + 2) * x.PW); x.dPW = make_div(x.PW); x.dTHW = make_div(x.TH * g.W);
+  x.dW = make_div(g.W); x.dHW = make_div(HW);
   *h = x;
   return true;
 }
@@ -1286,6 +1565,8 @@ static int halo_splits(const HaloGeom& h, long ws_floats) {
   return (h.nchunks + cps - 1) / cps;
 }
 
+static long long* g_halo_stamps = nullptr;   // diagnostic (conv_halo_stamps binding)
+
 static void launch_halo(hipStream_t st, const HaloGeom& h, const bf16* in, const bf16* wt, bf16* out, float* stats,
                         const float* shift, float* ws, long ws_floats, const bf16* res) {
   const int BN = tap_bn(h.O);
@@ -1298,12 +1579,21 @@ static void launch_halo(hipStream_t st, const HaloGeom& h, const bf16* in, const
   float* stt = part ? nullptr : stats;
   const bf16* rs = part ? nullptr : res;
   const bool pp2 = h.NPR > 208;
+  // BN 64 / PP 1: 3 stages keep two workgroups per CU (79 KB LDS); FEDMI_HALO_DEEP64=1 takes 6 (one per CU)
+  const char* d64 = std::getenv("FEDMI_HALO_DEEP64");
+  const bool deep64 = d64 && d64[0] == '1';
   if (BN == 128) {
-    if (pp2) hipLaunchKernelGGL((conv_halo<128, 2>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs);
-    else hipLaunchKernelGGL((conv_halo<128, 1>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs);
+    if (pp2) hipLaunchKernelGGL((conv_halo<128, 2, 5>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs,
+                                g_halo_stamps);
+    else hipLaunchKernelGGL((conv_halo<128, 1, 6>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs,
+                            g_halo_stamps);
   } else {
-    if (pp2) hipLaunchKernelGGL((conv_halo<64, 2>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs);
-    else hipLaunchKernelGGL((conv_halo<64, 1>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs);
+    if (pp2) hipLaunchKernelGGL((conv_halo<64, 2, 6>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs,
+                                g_halo_stamps);
+    else if (deep64) hipLaunchKernelGGL((conv_halo<64, 1, 6>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h,
+                                        cps, rs, g_halo_stamps);
+    else hipLaunchKernelGGL((conv_halo<64, 1, 3>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs,
+                            g_halo_stamps);
   }
   if (splits > 1) {
     const int VR = h.O / 8;
@@ -1559,9 +1849,37 @@ long conv_fd_ws_floats(const ConvShape& s) {
 }
 
 // Workspace (floats) launch_conv_wgrad needs for this shape with automatic splits.
+// conv_wgrad_halo applies (3x3 / stride 1 / pad 1, C and O % 64, 128-pixel blocks); FEDMI_WGRAD_HALO=0
+// keeps the generic WGRAD (A/B switch, read per launch).
+static bool wgrad_halo_geom(const ConvShape& s, HaloGeom* h) {
+  const char* e = std::getenv("FEDMI_WGRAD_HALO");
+  if ((e && e[0] == '0') || s.R != 3 || s.S != 3 || s.st != 1 || s.pad != 1 || s.C % 64 || s.O % 64) return false;
+  const TapGeom t = make_tap(s.N, s.H, s.W, s.C, s.O, s.P, s.Q, 3, 3, 1, 1, 1);
+  // the 288-row window (4x4 images) would spill the per-lane fragment offset tables: generic path
+  return halo_geom(t, RowMap{}, h, false) && h->NPR <= 208;
+}
+
+// K splits of the halo WGRAD: about FEDMI_WGRAD_HALO_WGS (default: one per CU) workgroups over the
+// (O / 64) x (C / 64) tiles -- fewer splits mean fewer fp32 partial bytes to write and reduce.
+static int wgrad_halo_splits(const HaloGeom& h, long ws_cap_floats) {
+  const char* e = std::getenv("FEDMI_WGRAD_HALO_WGS");
+  const long want = (e && std::atoi(e) > 0) ? std::atoi(e) : num_cus();
+  const long tiles = (long)(h.O / 64) * h.nchunks;
+  const int nblk = h.M / 128;
+  long sp = std::max<long>(1, (want + tiles / 2) / tiles);
+  sp = std::min<long>(sp, nblk);
+  if (ws_cap_floats > 0) sp = std::min<long>(sp, ws_cap_floats / ((long)h.O * 9 * h.C));
+  sp = std::max<long>(1, sp);
+  const int bps = (int)((nblk + sp - 1) / sp);
+  return (nblk + bps - 1) / bps;
+}
+
 long conv_wgrad_ws_floats(const ConvShape& s) {
   const ConvGeom g = wgrad_geom(s);
-  return (long)wgrad_splits(g, 0) * g.M * g.NC;
+  long need = (long)wgrad_splits(g, 0) * g.M * g.NC;
+  HaloGeom h;
+  if (wgrad_halo_geom(s, &h)) need = std::max(need, (long)wgrad_halo_splits(h, 0) * g.M * g.NC);
+  return need;
 }
 
 // dW[O][Cw][R][S] (fp32, PyTorch layout) = (or +=) X^T dY.  ``ws`` holds
@@ -1571,13 +1889,22 @@ void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const 
   const ConvGeom g = wgrad_geom(s);
   const long plane = (long)g.M * g.NC;
   if (ws_floats < plane) throw std::invalid_argument("conv_wgrad: workspace smaller than one O x RSC plane");
-  if (splits <= 0) splits = wgrad_splits(g, ws_floats);
-  const int ksteps = (g.K + BK - 1) / BK;
-  splits = std::max(1, std::min<int>(splits, ksteps));
-  const int kps = (ksteps + splits - 1) / splits;
-  splits = (ksteps + kps - 1) / kps;
-  if ((long)splits * plane > ws_floats) throw std::invalid_argument("conv_wgrad: workspace too small for splits");
-  launch_mode<WGRAD>(st, g, x, nullptr, dy, nullptr, ws, nullptr, splits);
+  HaloGeom h;
+  if (splits <= 0 && wgrad_halo_geom(s, &h)) {
+    splits = wgrad_halo_splits(h, ws_floats);
+    const int nblk = h.M / 128;
+    const int bps = (nblk + splits - 1) / splits;
+    dim3 grid((unsigned)((h.O / 64) * h.nchunks), 1, (unsigned)splits);
+    hipLaunchKernelGGL(conv_wgrad_halo<1>, grid, dim3(256), 0, st, x, dy, ws, h, bps);
+  } else {
+    if (splits <= 0) splits = wgrad_splits(g, ws_floats);
+    const int ksteps = (g.K + BK - 1) / BK;
+    splits = std::max(1, std::min<int>(splits, ksteps));
+    const int kps = (ksteps + splits - 1) / splits;
+    splits = (ksteps + kps - 1) / kps;
+    if ((long)splits * plane > ws_floats) throw std::invalid_argument("conv_wgrad: workspace too small for splits");
+    launch_mode<WGRAD>(st, g, x, nullptr, dy, nullptr, ws, nullptr, splits);
+  }
   if (s.R * s.S > WRED_MAX_RS) throw std::invalid_argument("conv_wgrad: window larger than 7x7");
   const long blocks = (long)s.O * ((s.C + 63) / 64);
   if (blocks >= 1024) {      // enough (o, channel-block) tiles: coalesced tile writes
@@ -1650,6 +1977,8 @@ void launch_dgrad_pack_multi(hipStream_t st, const DPackItem* items, int n) {
     hipLaunchKernelGGL(dgrad_pack_kernel, dim3(blk), dim3(256), 0, st, t);
   }
 }
+
+void set_conv_halo_stamps(long long* p) { g_halo_stamps = p; }
 
 void launch_conv_pack(hipStream_t st, const float* w, bf16* wrsc, int O, int Cw, int C, int RS) {
   const PackItem it{w, wrsc, O, Cw, C, RS};

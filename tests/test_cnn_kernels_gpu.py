@@ -637,3 +637,29 @@ def test_conv_halo_splitk_residual(gpu_device, shape, monkeypatch):
     dx = conv.conv2d_dgrad(_nhwc(gy).bfloat16(), wpk, xn.shape, 1, 1, Cw=Cw, ws=ws, wd=wd)
     torch.cuda.synchronize()
     assert _rel(dx.float(), _nhwc(xr.grad)) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(4, 32, 32, 64, 64, 3, 1, 1), (8, 16, 16, 128, 64, 3, 1, 1),
+                                   (16, 8, 8, 64, 192, 3, 1, 1), (128, 32, 32, 64, 64, 3, 1, 1),
+                                   (128, 8, 8, 256, 256, 3, 1, 1)],
+                         ids=["w32", "w16", "w8_o192", "l1_b128", "l3_b128"])
+def test_conv_wgrad_halo(gpu_device, shape, monkeypatch):
+    """Halo-patch WGRAD (3x3 / stride 1, one input window per 128-pixel block for all nine taps) vs torch,
+    and vs the generic WGRAD (FEDMI_WGRAD_HALO=0) on the same inputs."""
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device, seed=23)
+    wr_ = wb.clone().requires_grad_(True)
+    ref = F.conv2d(x, wr_, stride=1, padding=1)
+    gy = torch.randn_like(ref).bfloat16().float()
+    ref.backward(gy)
+    dyn = _nhwc(gy).bfloat16()
+    shp = (xn.shape, O, R, R, st, pad, Cw)
+    ws = torch.full((conv.wgrad_ws_floats(*shp),), float("nan"), device=gpu_device)
+    monkeypatch.setenv("FEDMI_WGRAD_HALO", "1")
+    dw = conv.conv2d_wgrad(xn, dyn, 3, 3, 1, 1, Cw=Cw, ws=ws)
+    monkeypatch.setenv("FEDMI_WGRAD_HALO", "0")
+    dw0 = conv.conv2d_wgrad(xn, dyn, 3, 3, 1, 1, Cw=Cw, ws=ws)
+    torch.cuda.synchronize()
+    assert not torch.isnan(dw).any()
+    assert _rel(dw, wr_.grad) < 1e-2
+    assert _rel(dw, dw0) < 1e-3

@@ -21,14 +21,29 @@ SHAPES = {"l1": (32, 64, 64, 3, 1), "l2": (16, 128, 128, 3, 1), "l3": (8, 256, 2
           "d2": (32, 64, 128, 3, 2), "d4": (8, 256, 512, 3, 2)}
 
 
+GRAPH = False
+
+
 def timeit(fn, iters):
+    """us per call; with --graph the calls are captured once and replayed (no host launch cost)."""
     for _ in range(3):
         fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
+    if GRAPH:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(iters):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        run = g.replay
+    else:
+        def run():
+            for _ in range(iters):
+                fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(iters):
-        fn()
+    run()
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / iters * 1e3
@@ -39,7 +54,11 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--shapes", default="l1,l2,l3,l4,d2,d4")
     ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--graph", action="store_true", help="time graph replays (kernel time, no launch cost)")
+    ap.add_argument("--passes", default="", help="comma list of passes to run (default: all)")
     a = ap.parse_args()
+    global GRAPH
+    GRAPH = a.graph
     dev = torch.device("cuda", 0)
     N = a.batch
     for key in a.shapes.split(","):
@@ -68,6 +87,8 @@ def main():
             "wgrad": lambda: conv.conv2d_wgrad(x, dy, k, k, st, pad, Cw=Ci, out=dw, ws=ws),
         }
         for name, fn in runs.items():
+            if a.passes and name not in a.passes.split(","):
+                continue
             us = timeit(fn, a.iters)
             print(json.dumps({"shape": key, "pass": name, "us": round(us, 2), "tflops": round(flops / us / 1e6, 1)}),
                   flush=True)
