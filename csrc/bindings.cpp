@@ -26,6 +26,7 @@ void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, cons
                            const bf16*, const bf16*, const uint8_t*, const uint8_t*, const bf16*, float*, float*);
 bool stamps_enabled();
 void read_stamps(unsigned long long*, bool);
+void set_ks1_diag(int);
 void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, const float*, const float*, int, float,
                       float, float, int*, int*);
 void launch_lenet_fwd_head(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*, int,
@@ -90,6 +91,7 @@ static void fedmi_bind(py::module_& m) {
   fedmi_bind_comm(m);
   fedmi_bind_zoo(m);
   m.def("stamps_enabled", &stamps_enabled);
+  m.def("set_ks1_diag", &set_ks1_diag);
   m.def("read_stamps", [](bool clear) {
     const size_t n = (size_t)FEDMI_STAMP_KERNELS * FEDMI_STAMP_WGS * FEDMI_STAMP_SLOTS;
     std::vector<unsigned long long> buf(n, 0ull);
@@ -147,7 +149,9 @@ static void fedmi_bind(py::module_& m) {
       .def("set_fuse_head", &LeNetEngine::set_fuse_head)
       .def("fuse_head", &LeNetEngine::fuse_head)
       .def("set_fuse_sgd", &LeNetEngine::set_fuse_sgd)
-      .def("fuse_sgd", &LeNetEngine::fuse_sgd);
+      .def("fuse_sgd", &LeNetEngine::fuse_sgd)
+      .def("set_sample_path", &LeNetEngine::set_sample_path)
+      .def("sample_path", &LeNetEngine::sample_path);
 
   // ---- raw LeNet kernels (numerics tests drive them one by one) -------------
   m.def("lenet_conv_fwd", [](uintptr_t st, uintptr_t images, int base, int nb, uintptr_t pk, uintptr_t params,

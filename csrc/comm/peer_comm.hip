@@ -211,12 +211,19 @@ PeerComm::PeerComm(int rank, int world, long long cap_bytes) {
   if (cap_bytes <= 0) throw std::invalid_argument("PeerComm: capacity must be > 0");
   cap_bytes = (cap_bytes + 255) & ~255LL;
   check_hip(hipGetDevice(&device_), "hipGetDevice");
-  check_hip(hipExtMallocWithFlags(reinterpret_cast<void**>(&sig_), sizeof(PeerSignal), hipDeviceMallocUncached),
+  // Both buffers are rounded up to whole 2 MiB fragments: the runtime may carve small uncached
+  // allocations out of one shared block, and a later generation's buffer exported from a block
+  // that an earlier (retired, still mapped) generation already exported failed with
+  // hipIpcGetMemHandle: invalid argument (failover drill, third data-plane group of a client).
+  constexpr size_t kFrag = 2u << 20;
+  const size_t sig_bytes = (sizeof(PeerSignal) + kFrag - 1) / kFrag * kFrag;
+  check_hip(hipExtMallocWithFlags(reinterpret_cast<void**>(&sig_), sig_bytes, hipDeviceMallocUncached),
             "PeerComm signal alloc");
   check_hip(hipMemset(sig_, 0, sizeof(PeerSignal)), "PeerComm signal memset");
   // Staging is uncached as well: the payload is read once per call by peers on other GPUs, and an
   // uncached mapping needs no cache maintenance to be coherent across xGMI.
-  check_hip(hipExtMallocWithFlags(reinterpret_cast<void**>(&data_), 4 * cap_bytes, hipDeviceMallocUncached),
+  const size_t data_bytes = (4 * (size_t)cap_bytes + kFrag - 1) / kFrag * kFrag;
+  check_hip(hipExtMallocWithFlags(reinterpret_cast<void**>(&data_), data_bytes, hipDeviceMallocUncached),
             "PeerComm staging alloc");
   check_hip(hipMemset(data_, 0, 4 * cap_bytes), "PeerComm staging memset");
   check_hip(hipDeviceSynchronize(), "PeerComm init sync");

@@ -352,23 +352,60 @@ __global__ __launch_bounds__(256) void head_fwd_bwd_kernel(const bf16* __restric
                                                            const float* __restrict__ b, float* __restrict__ pooled,
                                                            float* __restrict__ dlog, bf16* __restrict__ dy,
                                                            float* __restrict__ stats, int N, int train) {
-  extern __shared__ float sm[];   // pooled[C], logits[16], dl[16]
+  // Every phase issues ALL of a thread's global loads before consuming any of them: with
+  // one workgroup per sample the kernel is latency-bound, and a load-use loop paid one
+  // memory round trip per position / weight (round 1: 25 us for ResNet-18's 4x4x512 head).
+  extern __shared__ float sm[];   // pooled[C], logits[16], dl[16], partial sums [pg][C]
   float* pl = sm;
   float* lg = sm + C;
   float* dl = lg + 16;
+  float* ps = dl + 16;
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bf16* yn = y + (size_t)n * HW * C;
   const float invHW = 1.f / (float)HW;
-  for (int c = tid; c < C; c += 256) {
-    float s = 0.f;
-    for (int p = 0; p < HW; ++p) s += (float)yn[(size_t)p * C + c];
-    pl[c] = s * invHW;
-    if (train) pooled[(size_t)n * C + c] = s * invHW;
+  {
+    // thread = (position group pg, 8-channel group cg); 8 positions' 16-B loads in flight
+    const int VC = C >> 3, npg = max(1, 256 / VC), cg = tid % VC, pg = tid / VC;
+    if (pg < npg && cg < VC) {
+      float s[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] = 0.f;
+      for (int p0 = pg; p0 < HW; p0 += 8 * npg) {
+        bf16x8v v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int p = p0 + u * npg;
+          if (p < HW) v[u] = *reinterpret_cast<const bf16x8v*>(yn + (size_t)p * C + cg * 8);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (p0 + u * npg < HW) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s[j] += (float)v[u][j];
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ps[pg * C + cg * 8 + j] = s[j];
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+      float s = 0.f;
+      for (int g = 0; g < npg; ++g) s += ps[g * C + c];   // fixed order: deterministic
+      pl[c] = s * invHW;
+      if (train) pooled[(size_t)n * C + c] = s * invHW;
+    }
   }
   __syncthreads();
   for (int j = wave; j < J; j += 4) {
     float s = 0.f;
-    for (int c = lane; c < C; c += 64) s += W[(size_t)j * C + c] * pl[c];
+    for (int c0 = lane; c0 < C; c0 += 64 * 8) {
+      float w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[u] = c0 + 64 * u < C ? W[(size_t)j * C + c0 + 64 * u] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (c0 + 64 * u < C) s += w[u] * pl[c0 + 64 * u];
+    }
     s = wave_sum(s);
     if (lane == 0) lg[j] = s + b[j];
   }
@@ -394,8 +431,13 @@ __global__ __launch_bounds__(256) void head_fwd_bwd_kernel(const bf16* __restric
   if (!train) return;
   __syncthreads();
   for (int c = tid; c < C; c += 256) {
+    float w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = j < J ? W[(size_t)j * C + c] : 0.f;
     float s = 0.f;
-    for (int j = 0; j < J; ++j) s += W[(size_t)j * C + c] * dl[j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < J) s += w[j] * dl[j];
     pl[c] = s * invHW;   // reuse: d pooled / HW
   }
   __syncthreads();
@@ -411,9 +453,10 @@ __global__ __launch_bounds__(256) void head_fwd_bwd_kernel(const bf16* __restric
 }
 
 constexpr int HEAD_MAXN = 512;
-// dW[j][c] = sum_n dlog[n][j] * pooled[n][c];  db[j] = sum_n dlog[n][j]
+// dW[j][c] = sum_n dlog[n][j] * pooled[n][c];  db[j] = sum_n dlog[n][j]   (N <= HEAD_MAXN)
 // Block = 64 channels x 4 sample groups (fixed-order LDS combine: deterministic);
-// block 0 also reduces db.
+// block 0 also reduces db.  Loads are issued 8 at a time before use (the kernel has
+// C/64 workgroups, so a load-use loop was one memory round trip per sample: 30 us).
 __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict__ pooled, const float* __restrict__ dlog,
                                                          int N, int C, int J, float* __restrict__ dW,
                                                          float* __restrict__ db) {
@@ -421,18 +464,37 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict
   __shared__ float dls[HEAD_MAXN * 16];   // dlog staged once per block, read as LDS broadcasts
   const int cl = threadIdx.x & 63, ng = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  const int nn = min(N, HEAD_MAXN);
-  for (int i = threadIdx.x; i < nn * J; i += 256) dls[(i / J) * 16 + i % J] = dlog[i];
+  for (int i0 = threadIdx.x; i0 < N * J; i0 += 256 * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = i0 + 256 * u < N * J ? dlog[i0 + 256 * u] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + 256 * u;
+      if (i < N * J) dls[(i / J) * 16 + i % J] = v[u];
+    }
+  }
   __syncthreads();
   float acc[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-  for (int n = ng; n < N; n += 4) {
-    const float pv = c < C ? pooled[(size_t)n * C + c] : 0.f;
-    const float* dl = n < HEAD_MAXN ? dls + n * 16 : nullptr;
+  for (int n0 = ng; n0 < N; n0 += 32) {
+    float pv[8];
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (j < J) acc[j] += (dl ? dl[j] : dlog[(size_t)n * J + j]) * pv;
+    for (int u = 0; u < 8; ++u) {
+      const int n = n0 + 4 * u;
+      pv[u] = (c < C && n < N) ? pooled[(size_t)n * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int n = n0 + 4 * u;
+      if (n < N) {
+        const float* dl = dls + n * 16;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (j < J) acc[j] += dl[j] * pv[u];
+      }
+    }
   }
 #pragma unroll
   for (int j = 0; j < 16; ++j) part[ng][j][cl] = acc[j];
@@ -447,7 +509,7 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict
     const int j = threadIdx.x & 15, g = threadIdx.x >> 4;
     float s = 0.f;
     if (j < J)
-      for (int n = g; n < N; n += 16) s += n < HEAD_MAXN ? dls[n * 16 + j] : dlog[(size_t)n * J + j];
+      for (int n = g; n < N; n += 16) s += dls[n * 16 + j];
     float* red = &part[0][0][0];   // reuse: [16 groups][16 classes]
     red[g * 16 + j] = s;
     __syncthreads();
@@ -741,9 +803,11 @@ void launch_head(hipStream_t st, const bf16* y, const int* labels, int base, con
                  const float* W, const float* b, float* pooled, float* dlog, bf16* dy, float* stats, float* dW,
                  float* db, int train) {
   if (J > 16) throw std::invalid_argument("head: at most 16 classes");
-  if (C % 8) throw std::invalid_argument("head: C % 8 != 0");
-  hipLaunchKernelGGL(head_fwd_bwd_kernel, dim3(N), dim3(256), (C + 32) * sizeof(float), st, y, labels, base, dbase, HW, C,
+  if (C % 8 || C > 2048) throw std::invalid_argument("head: need C % 8 == 0 and C <= 2048");
+  const int npg = std::max(1, 256 / (C / 8));
+  hipLaunchKernelGGL(head_fwd_bwd_kernel, dim3(N), dim3(256), (C + 32 + npg * C) * sizeof(float), st, y, labels, base, dbase, HW, C,
                      J, W, b, pooled, dlog, dy, stats, N, train);
+  if (train && N > HEAD_MAXN) throw std::invalid_argument("head: training batch > 512");
   if (train)
     hipLaunchKernelGGL(head_wgrad_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pooled, dlog, N, C, J, dW, db);
 }

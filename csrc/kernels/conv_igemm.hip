@@ -1163,7 +1163,10 @@ struct DPackTable {
 };
 
 __global__ __launch_bounds__(256) void dgrad_pack_kernel(DPackTable t) {
-  __shared__ float tile[64][4 * 49 + 1];   // 64 o x (4 c x R*S <= 7x7)
+  // 64 o x (4 c x R*S) tile, LDS sized by the launch for the table's largest R*S (a fixed
+  // 7x7-sized tile held occupancy at 3 blocks per CU for the 3x3 convs); 8 loads in flight
+  // per thread before the LDS stores.
+  extern __shared__ float tile_[];
   int k = 0;
   while (k + 1 < t.n && (int)blockIdx.x >= t.e[k + 1].blk0) ++k;
   const DPackEntry& p = t.e[k];
@@ -1171,11 +1174,21 @@ __global__ __launch_bounds__(256) void dgrad_pack_kernel(DPackTable t) {
   const int ncb = (p.Cpad + 3) / 4;
   const int o0 = (b / ncb) * 64, c0 = (b % ncb) * 4;
   const int RS = p.R * p.S;
-  const int span = 4 * RS;
-  for (int e = threadIdx.x; e < 64 * span; e += 256) {
-    const int oi = e / span, f = e - oi * span;   // f = (c - c0) * RS + rs
-    const int o = o0 + oi, c = c0 + f / RS;
-    tile[oi][f] = (o < p.O && c < p.Cw) ? p.w[((long)o * p.Cw + c) * RS + (f % RS)] : 0.f;
+  const int span = 4 * RS, ld = span + 1;
+  for (int e0 = threadIdx.x; e0 < 64 * span; e0 += 256 * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + 256 * u;
+      const int oi = e / span, f = e - oi * span;   // f = (c - c0) * RS + rs
+      const int o = o0 + oi, c = c0 + f / RS;
+      v[u] = (e < 64 * span && o < p.O && c < p.Cw) ? p.w[((long)o * p.Cw + c) * RS + (f % RS)] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + 256 * u;
+      if (e < 64 * span) tile_[(e / span) * ld + e % span] = v[u];
+    }
   }
   __syncthreads();
   const int taps = p.nr * p.ns;
@@ -1186,7 +1199,7 @@ __global__ __launch_bounds__(256) void dgrad_pack_kernel(DPackTable t) {
     const int c = c0 + ci, o = o0 + oi;
     if (c >= p.Cpad || o >= p.O) continue;
     const int r = p.r0 + p.step * (p.nr - 1 - i), sx = p.s0 + p.step * (p.ns - 1 - j);
-    p.wd[(((long)c * p.nr + i) * p.ns + j) * p.O + o] = (bf16)tile[oi][ci * RS + r * p.S + sx];
+    p.wd[(((long)c * p.nr + i) * p.ns + j) * p.O + o] = (bf16)tile_[oi * ld + ci * RS + r * p.S + sx];
   }
 }
 
@@ -1352,14 +1365,21 @@ struct PackTable {
 };
 
 __global__ __launch_bounds__(256) void conv_pack_multi_kernel(PackTable t) {
-  __shared__ float row[PACK_ROW_MAX];
+  extern __shared__ float row[];   // sized by the launch: the table's longest Cw * R * S
   int k = 0;
   while (k + 1 < t.n && (int)blockIdx.x >= t.e[k + 1].row0) ++k;
   const PackEntry& p = t.e[k];
   const int o = blockIdx.x - p.row0;
   const int n_in = p.Cw * p.RS;
   const float* src = p.w + (long)o * n_in;
-  for (int i = threadIdx.x; i < n_in; i += 256) row[i] = src[i];
+  for (int i0 = threadIdx.x; i0 < n_in; i0 += 256 * 8) {   // 8 loads in flight per thread
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = i0 + 256 * u < n_in ? src[i0 + 256 * u] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + 256 * u < n_in) row[i0 + 256 * u] = v[u];
+  }
   __syncthreads();
   bf16* dst = p.wr + (long)o * p.RS * p.C;
   const int n_out = p.RS * p.C;
@@ -1927,15 +1947,16 @@ void launch_conv_pack_multi(hipStream_t st, const PackItem* items, int n) {
   for (int b = 0; b < n; b += MAX_PACK) {
     PackTable t{};
     t.n = std::min(MAX_PACK, n - b);
-    int rows = 0;
+    int rows = 0, max_row = 1;
     for (int k = 0; k < t.n; ++k) {
       const PackItem& it = items[b + k];
       if (it.C % 8 || it.C < it.Cw) throw std::invalid_argument("conv_pack_multi: bad channel padding");
       if ((long)it.Cw * it.RS > PACK_ROW_MAX) throw std::invalid_argument("conv_pack_multi: row too long");
       t.e[k] = PackEntry{it.w, it.wr, it.O, it.Cw, it.C, it.RS, rows};
       rows += it.O;
+      max_row = std::max(max_row, it.Cw * it.RS);
     }
-    hipLaunchKernelGGL(conv_pack_multi_kernel, dim3(rows), dim3(256), 0, st, t);
+    hipLaunchKernelGGL(conv_pack_multi_kernel, dim3(rows), dim3(256), max_row * sizeof(float), st, t);
   }
 }
 
@@ -1974,7 +1995,9 @@ void launch_dgrad_pack_multi(hipStream_t st, const DPackItem* items, int n) {
       t.e[k].blk0 = blk;
       blk += ((t.e[k].O + 63) / 64) * ((t.e[k].Cpad + 3) / 4);
     }
-    hipLaunchKernelGGL(dgrad_pack_kernel, dim3(blk), dim3(256), 0, st, t);
+    int max_rs = 1;
+    for (int k = 0; k < t.n; ++k) max_rs = std::max(max_rs, t.e[k].R * t.e[k].S);
+    hipLaunchKernelGGL(dgrad_pack_kernel, dim3(blk), dim3(256), 64 * (4 * max_rs + 1) * sizeof(float), st, t);
   }
 }
 

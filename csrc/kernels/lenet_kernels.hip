@@ -28,6 +28,8 @@
 //
 // The whole local epoch is replayed from a hipGraph built by the native
 // executor (csrc/runtime/lenet_engine.cpp).
+#include <stdexcept>
+
 #include "common.h"
 #include "lenet_layout.h"
 
@@ -35,6 +37,9 @@ using namespace lenet;
 
 #ifdef FEDMI_STAMPS
 __device__ unsigned long long fedmi_stamps[FEDMI_STAMP_KERNELS][FEDMI_STAMP_WGS][FEDMI_STAMP_SLOTS];
+// diagnostic build only: KS1 staging experiments (bit 0: skip the packed-weight loads, bit 1: every
+// workgroup reads sample 0's image).  Timing probes -- the numerics of such a step are meaningless.
+__device__ int fedmi_ks1_diag;
 #endif
 
 namespace {
@@ -138,15 +143,25 @@ FEDMI_DEV void conv_fwd_body(
 
   load_raw(images + (size_t)gidx * IMG_BYTES, raw);
   zero_lds(xcl, XCL * 2);   // channel 3 and the right/bottom pad stay zero
-  // conv1 weights (B fragments) + per-lane group offsets, while the image lands
-  bf16x8 wb1[4];
-  int go1[4];
+  // conv1 AND conv2 weights (B fragments), biases and per-lane group offsets, all issued
+  // while the image lands: every later __syncthreads drains vmcnt, so a global load
+  // issued after conv1 (round 1) put its full latency on the conv1 -> pool1 barrier.
+  bf16x8 wb1[4], wb2[7];
+  int go1[4], go2[7];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     wb1[ks] = ld8(pk + PK_W1C + n16 * K1C + ks * 32 + kq);
     const int g = ks * 4 + (lane >> 4);
     go1[ks] = g < 15 ? ((g / 3) * 40 + 2 * (g % 3)) * 4 : 0;
   }
+#pragma unroll
+  for (int ks = 0; ks < 7; ++ks) {
+    wb2[ks] = ld8(pk + PK_W2C + n16 * K2C + ks * 32 + kq);
+    const int g = ks * 4 + (lane >> 4);
+    go2[ks] = g < 25 ? ((g / 5) * P1 + (g % 5)) * 8 : 0;
+  }
+  const float bias1 = n16 < C1 ? params[P_C1B + n16] : 0.f;
+  const float bias2 = params[P_C2B + n16];
   const Aug a = aug_params(augment, seed, round_ctr, gidx);
   __syncthreads();
   for (int e = tid; e < IMG_BYTES; e += NT_FWD) {   // lanes walk x: raw reads broadcast within a dword
@@ -158,27 +173,37 @@ FEDMI_DEV void conv_fwd_body(
 
   // ---- conv1: M = 784 positions (49 tiles), N = 6 (pad 16), K = 128 (4 steps)
   {
-    const float bias = n16 < C1 ? params[P_C1B + n16] : 0.f;
-    for (int t = wave; t < NPOS1 / 16; t += NW_FWD) {
-      const int pos = t * 16 + n16;
-      const int py = pos / O1, px = pos - py * O1;
-      const bf16* xb = xcl + (py * 40 + px) * 4;
-      f32x4 acc = zero4();
+    const float bias = bias1;
+    // two tiles per pass (t, t + NW_FWD): both tiles' 8 operand reads are in flight
+    // together and the two accumulation chains interleave on the matrix core, so a
+    // wave pays the LDS round trip once per two tiles.
+    for (int t = wave; t < NPOS1 / 16; t += 2 * NW_FWD) {
+      const int tb = t + NW_FWD;
+      const bool two = tb < NPOS1 / 16;
+      const int pa = t * 16 + n16, pb = (two ? tb : t) * 16 + n16;
+      const bf16* xa = xcl + ((pa / O1) * 40 + pa % O1) * 4;
+      const bf16* xbb = xcl + ((pb / O1) * 40 + pb % O1) * 4;
+      bf16x8 fa[4], fb[4];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) acc = mfma16(ld8_b64x2(xb + go1[ks]), wb1[ks], acc);
+      for (int ks = 0; ks < 4; ++ks) {
+        fa[ks] = ld8_b64x2(xa + go1[ks]);
+        fb[ks] = ld8_b64x2(xbb + go1[ks]);
+      }
+      f32x4 acc = zero4(), accb = zero4();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        acc = mfma16(fa[ks], wb1[ks], acc);
+        accb = mfma16(fb[ks], wb1[ks], accb);
+      }
       if (n16 < C1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) c1[(t * 16 + rq + r) * 8 + n16] = fmaxf(acc[r] + bias, 0.f);
+        if (two) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) c1[(tb * 16 + rq + r) * 8 + n16] = fmaxf(accb[r] + bias, 0.f);
+        }
       }
     }
-  }
-  bf16x8 wb2[7];
-  int go2[7];
-#pragma unroll
-  for (int ks = 0; ks < 7; ++ks) {
-    wb2[ks] = ld8(pk + PK_W2C + n16 * K2C + ks * 32 + kq);
-    const int g = ks * 4 + (lane >> 4);
-    go2[ks] = g < 25 ? ((g / 5) * P1 + (g % 5)) * 8 : 0;
   }
   __syncthreads();
   FEDMI_STAMP(0, 2);
@@ -208,7 +233,7 @@ FEDMI_DEV void conv_fwd_body(
   // ---- conv2: M = 100 positions (7 tiles), N = 16, K = 224 (7 steps)
   if (wave < 7) {
     const int t = wave;
-    const float bias = params[P_C2B + n16];
+    const float bias = bias2;
     int pos = t * 16 + n16;
     if (pos >= NPOS2) pos = 0;
     const int py = pos / O2, px = pos - py * O2;
@@ -744,6 +769,206 @@ FEDMI_DEV void publish_flag(int* flags, int idx, int gen) {
   }
 }
 
+// Operand images are padded so the 16 lanes of an MFMA fragment read land on
+// distinct 16-byte bank groups (strides in 16-B units: coprime with 16 or
+// chosen so the (c, r, s) im2col column index maps to distinct groups).
+constexpr int BW_XROW = 40, BW_XS_C = 32 * BW_XROW + 72, BW_XS_S = 3 * BW_XS_C + 48;  // xsh[s][c][y][x']: 5/169/513
+constexpr int BW_XSH = 5 * BW_XS_S;
+constexpr int BW_P1SH = 5 * 6 * 14 * 16;       // pool1 shifted copies [s][c][y][x']
+constexpr int BW_DY2W = 16 * 160;              // conv2 out-grad [o][i*16+j]
+constexpr int BW_DY2S = 24;                    // conv2 out-grad channels-last position stride (3 units)
+constexpr int BW_DY2C = 18 * 18 * BW_DY2S;     // 4-px zero border
+constexpr int BW_DY1S = 904;                   // conv1 out-grad row stride [o][i*32+j] (113 units)
+constexpr int BW_DY1 = 6 * BW_DY1S;
+constexpr int BW_WDGS = KDGP + 8;              // conv2 dgrad weight row stride (53 units)
+// bytes of the backward's scratch region (shifted copies, out-grads, wgrad partials, bias sums)
+constexpr int BW_O_XSH = 0, BW_O_P1SH = BW_O_XSH + BW_XSH * 2, BW_O_DY2W = BW_O_P1SH + BW_P1SH * 2,
+              BW_O_DY2C = BW_O_DY2W + BW_DY2W * 2, BW_O_DY1 = BW_O_DY2C + BW_DY2C * 2,
+              BW_O_DW1 = BW_O_DY1 + BW_DY1 * 2, BW_O_DB = BW_O_DW1 + 3 * 6 * 80 * 4, BW_SCRATCH = BW_O_DB + 32 * 4;
+
+// LDS operands of one sample's conv backward (K3 stages them from global memory; the
+// per-sample step kernel KS1 still holds them from its own forward).
+struct BwdLds {
+  const uint8_t* raw;     // uint8 CHW image
+  const bf16* p1r;        // pool1 output, CHW [NP1]
+  const uint8_t* am1s;    // pool1 argmax codes [NP1]
+  const uint8_t* am2s;    // pool2 argmax codes [F0]
+  const float* dxs;       // d(pool2) [F0], ReLU-masked
+  const bf16* wdg;        // conv2 dgrad weight image, rows of BW_WDGS
+  bf16* xsh; bf16* p1sh; bf16* dY2w; bf16* dY2c; bf16* dY1; float* db; float* w1part;
+};
+
+FEDMI_DEV BwdLds bwd_lds(unsigned char* scratch, const uint8_t* raw, const bf16* p1r, const uint8_t* am1s,
+                         const uint8_t* am2s, const float* dxs, const bf16* wdg) {
+  BwdLds L;
+  L.raw = raw; L.p1r = p1r; L.am1s = am1s; L.am2s = am2s; L.dxs = dxs; L.wdg = wdg;
+  L.xsh = reinterpret_cast<bf16*>(scratch + BW_O_XSH);
+  L.p1sh = reinterpret_cast<bf16*>(scratch + BW_O_P1SH);
+  L.dY2w = reinterpret_cast<bf16*>(scratch + BW_O_DY2W);
+  L.dY2c = reinterpret_cast<bf16*>(scratch + BW_O_DY2C);
+  L.dY1 = reinterpret_cast<bf16*>(scratch + BW_O_DY1);
+  L.w1part = reinterpret_cast<float*>(scratch + BW_O_DW1);   // conv1 wgrad K-split partials [3][6][80]
+  L.db = reinterpret_cast<float*>(scratch + BW_O_DB);
+  return L;
+}
+
+// zero the out-grad images, the shifted copies' tails (x' + s beyond the row) and the bias sums
+FEDMI_DEV void bwd_zero(const BwdLds& L) {
+  zero_lds(L.dY2w, BW_DY2W * 2);
+  zero_lds(L.dY2c, BW_DY2C * 2);
+  zero_lds(L.dY1, BW_DY1 * 2);
+  zero_lds(L.xsh, BW_XSH * 2);
+  zero_lds(L.p1sh, BW_P1SH * 2);
+  if (threadIdx.x < 32) L.db[threadIdx.x] = 0.f;
+}
+
+// each augmented pixel / pooled value is computed once and stored into its 5
+// column-shifted copies: copy s holds element x at column x - s
+FEDMI_DEV void bwd_build_shifted(const BwdLds& L, const Aug& a, int tid = threadIdx.x, int nthr = NT_CONV) {
+  for (int e = tid; e < IMG_BYTES; e += nthr) {
+    const int c = e >> 10, y = (e >> 5) & 31, x = e & 31;
+    const bf16 v = (bf16)aug_pixel(L.raw, a, c, y, x);
+    bf16* row = L.xsh + c * BW_XS_C + y * BW_XROW + x;
+#pragma unroll
+    for (int sh = 0; sh < 5; ++sh)
+      if (x >= sh) row[sh * BW_XS_S - sh] = v;
+  }
+  for (int e = tid; e < NP1; e += nthr) {
+    const int c = e / 196, rem = e - c * 196, y = rem / P1, x = rem - y * P1;
+    const bf16 v = L.p1r[e];
+    bf16* row = L.p1sh + (c * 14 + y) * 16 + x;
+#pragma unroll
+    for (int sh = 0; sh < 5; ++sh)
+      if (x >= sh) row[sh * (6 * 14 * 16) - sh] = v;
+  }
+}
+
+// d(pool2) -> conv2 out-grad images + conv2 bias sums, then conv2 wgrad + dgrad, conv1 wgrad,
+// and the sample's gradient slab.  Stamps slots 2..5 of kernel 'sk'.
+template <bool PUB>
+FEDMI_DEV void bwd_main(const BwdLds& L, float* __restrict__ slab, int* __restrict__ flags, int s, int gen,
+                        int sk, int stamp_wg) {
+  (void)sk; (void)stamp_wg;
+  const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
+  const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
+  float* db = L.db;
+  for (int f = tid; f < F0; f += NT_CONV) {
+    const int o = f / 25, rem = f - o * 25, py = rem / P2, px = rem - py * P2;
+    const int am = L.am2s[f];
+    const int y = 2 * py + (am >> 1), x = 2 * px + (am & 1);
+    const float g = L.dxs[f];
+    const bf16 gb = (bf16)g;
+    L.dY2w[o * 160 + y * 16 + x] = gb;
+    L.dY2c[((y + 4) * 18 + (x + 4)) * BW_DY2S + o] = gb;
+    atomicAdd(&db[o], g);
+  }
+  __syncthreads();
+  FEDMI_STAMP(sk, 2);
+
+  // ---- conv2 wgrad: dW2[o][k'] = sum_p dY2[o][p] * im2col(pool1)[p][k']
+  //      M = 16 (o), N = 150 (10 tiles), K = 160 (p' = i*16 + j, 5 steps)
+  // task map over 16 waves: dgrad tile t -> wave t (t < 13), wgrad tile t -> wave (13 + t) % 16
+  for (int t = (wave + 3) & 15; t < 10; t += NW_CONV) {
+    const int kk = t * 16 + n16;
+    const int kc = kk < 150 ? kk : 0;
+    const int c = kc / 25, rs = kc - c * 25, r = rs / 5, sc = rs - r * 5;
+    const bf16* bb = L.p1sh + ((sc * 6 + c) * 14 + r) * 16 + (kq & 15);
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int ks = 0; ks < 5; ++ks) {
+      const int i = 2 * ks + (kq >> 4);
+      acc = mfma16(ld8(L.dY2w + n16 * 160 + ks * 32 + kq), ld8(bb + i * 16), acc);
+    }
+    if (kk < 150) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) put_grad<PUB>(slab + P_C2W + (rq + rr) * 150 + kk, acc[rr]);
+    }
+  }
+
+  // ---- conv2 dgrad: dP1[c][pos] = sum_(r,s,o) dY2[o][y-r][x-s] W2[o][c][r][s]
+  //      M = 196 positions (13 tiles), N = 6 (pad 16), K = 416 (13 steps)
+  int koff[13];   // per-lane K-group offsets into dY2c relative to the output position
+#pragma unroll
+  for (int ks = 0; ks < 13; ++ks) {
+    const int G = ks * 4 + (lane >> 4), g = G >> 1;
+    const int r = g / 5, sc = g - r * 5;
+    koff[ks] = g < 25 ? (-r * 18 - sc) * BW_DY2S + (G & 1) * 8 : 0;   // pad group: weight 0, any in-bounds read
+  }
+  for (int t = wave; t < 13; t += NW_CONV) {
+    int pos = t * 16 + n16;
+    if (pos >= 196) pos = 0;
+    const int y = pos / P1, x = pos - y * P1;
+    const bf16* gb = L.dY2c + ((y + 4) * 18 + (x + 4)) * BW_DY2S;
+    const bf16* wb = L.wdg + min(n16, C1) * BW_WDGS + kq;     // rows >= 6 are zero: share row 6 (broadcast)
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int ks = 0; ks < 13; ++ks) acc = mfma16(ld8(gb + koff[ks]), ld8(wb + ks * 32), acc);
+    if (n16 < C1) {
+      const int c = n16;
+      float csum = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int p = t * 16 + rq + rr;
+        if (p < 196) {
+          const int py = p / P1, px = p - py * P1;
+          const float pooled = (float)L.p1r[c * 196 + p];
+          const float g = pooled > 0.f ? acc[rr] : 0.f;
+          const int am = L.am1s[c * 196 + p];
+          const int yy = 2 * py + (am >> 1), xx = 2 * px + (am & 1);
+          L.dY1[c * BW_DY1S + yy * 32 + xx] = (bf16)g;
+          csum += g;
+        }
+      }
+      atomicAdd(&db[16 + c], csum);
+    }
+  }
+  __syncthreads();
+  FEDMI_STAMP(sk, 3);
+
+  // ---- conv1 wgrad: dW1[o][k'] = sum_p dY1[o][p] * im2col(x)[p][k']
+  //      M = 16 (o < 6), N = 75 (5 tiles), K = 896 (p' = i*32 + j, 28 steps = conv1
+  //      output rows) split in 3 parts: 15 waves = 5 tiles x 3 K-parts, then a
+  //      deterministic 3-way combine through LDS.
+  if (wave < 15) {
+    const int nt = wave % 5, part = wave / 5;
+    const int ks0 = part * 10, ks1 = min(ks0 + 10, O1);
+    const int kk = nt * 16 + n16;
+    const int kc = kk < 75 ? kk : kk - 64;                 // pad columns: distinct bank groups, result dropped
+    const int c = kc / 25, rs = kc - c * 25, r = rs / 5, sc = rs - r * 5;
+    const bf16* bb = L.xsh + sc * BW_XS_S + c * BW_XS_C + r * BW_XROW + kq;
+    const bf16* ab = L.dY1 + min(n16, C1 - 1) * BW_DY1S + kq;
+    const bool arow = n16 < C1;
+    f32x4 acc0 = zero4(), acc1 = zero4();
+    int ks = ks0;
+    for (; ks + 1 < ks1; ks += 2) {
+      bf16x8 a0 = ld8(ab + ks * 32), a1 = ld8(ab + ks * 32 + 32);
+      if (!arow) { a0 = zero8(); a1 = zero8(); }
+      acc0 = mfma16(a0, ld8(bb + ks * BW_XROW), acc0);
+      acc1 = mfma16(a1, ld8(bb + (ks + 1) * BW_XROW), acc1);
+    }
+    if (ks < ks1) {
+      bf16x8 a0 = ld8(ab + ks * 32);
+      if (!arow) a0 = zero8();
+      acc0 = mfma16(a0, ld8(bb + ks * BW_XROW), acc0);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int o = rq + rr;
+      if (o < C1 && kk < 75) L.w1part[(part * 6 + o) * 80 + kk] = acc0[rr] + acc1[rr];
+    }
+  }
+  __syncthreads();
+  FEDMI_STAMP(sk, 4);
+  for (int e = tid; e < C1 * 75; e += NT_CONV) {
+    const int o = e / 75, kk = e - o * 75;
+    put_grad<PUB>(slab + P_C1W + e, L.w1part[o * 80 + kk] + L.w1part[(6 + o) * 80 + kk] + L.w1part[(12 + o) * 80 + kk]);
+  }
+  if (tid < C1) put_grad<PUB>(slab + P_C1B + tid, db[16 + tid]);
+  if (tid < C2) put_grad<PUB>(slab + P_C2B + tid, db[tid]);
+  publish_flag<PUB>(flags, s, gen);
+  FEDMI_STAMP(sk, 5);
+}
+
 template <bool PUB>
 FEDMI_DEV void conv_bwd_body(
     int blk, const uint8_t* __restrict__ images, int sample_base, int nb,
@@ -759,22 +984,8 @@ FEDMI_DEV void conv_bwd_body(
     float* __restrict__ fc1w_grad,         // [F1W_N]
     int* __restrict__ flags, int gen)      // PUB: producer flags [nb + N_DW1_WG]
 {
-  // Operand images are padded so the 16 lanes of an MFMA fragment read land on
-  // distinct 16-byte bank groups (strides in 16-B units: coprime with 16 or
-  // chosen so the (c, r, s) im2col column index maps to distinct groups).
-  constexpr int XROW = 40, XS_C = 32 * XROW + 72, XS_S = 3 * XS_C + 48;   // xsh[s][c][y][x']: units 5 / 169 / 513
-  constexpr int XSH = 5 * XS_S;
-  constexpr int P1SH = 5 * 6 * 14 * 16;       // pool1 shifted copies [s][c][y][x']
-  constexpr int DY2W = 16 * 160;              // conv2 out-grad [o][i*16+j]
-  constexpr int DY2S = 24;                    // conv2 out-grad channels-last position stride (3 units)
-  constexpr int DY2C = 18 * 18 * DY2S;        // 4-px zero border
-  constexpr int DY1S = 904;                   // conv1 out-grad row stride [o][i*32+j] (113 units)
-  constexpr int DY1 = 6 * DY1S;
-  constexpr int WDGS = KDGP + 8;              // conv2 dgrad weight row stride (53 units)
   constexpr int O_RAW = 0, O_P1R = 3072, O_AM1 = O_P1R + 2368, O_AM2 = O_AM1 + 1184, O_DX = O_AM2 + 416,
-                O_WDG = O_DX + F0 * 4, O_XSH = O_WDG + 16 * WDGS * 2, O_P1SH = O_XSH + XSH * 2,
-                O_DY2W = O_P1SH + P1SH * 2, O_DY2C = O_DY2W + DY2W * 2, O_DY1 = O_DY2C + DY2C * 2,
-                O_DW1 = O_DY1 + DY1 * 2, O_DB = O_DW1 + 3 * 6 * 80 * 4, O_END = O_DB + 32 * 4;
+                O_WDG = O_DX + F0 * 4, O_SCR = O_WDG + 16 * BW_WDGS * 2, O_END = O_SCR + BW_SCRATCH;
   __shared__ __attribute__((aligned(16))) unsigned char smem[O_END];
 
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
@@ -785,7 +996,6 @@ FEDMI_DEV void conv_bwd_body(
     const int e = blk - nb;
     if (e >= N_DW1_WG) return;
     if (wave < 8) {                              // 8 row tiles of 16 outputs
-    const int nks = (nb + 31) >> 5;
     const bf16* ap = dZ1T + (wave * 16 + n16) * DZ1_LD + kq;
     const bf16* bp = act2T + (size_t)(e * 16 + n16) * MAX_TRAIN_BATCH + kq;
     bf16x8 a[4], b[4];
@@ -794,7 +1004,6 @@ FEDMI_DEV void conv_bwd_body(
       a[ks] = ld8(ap + ks * 32);
       b[ks] = ld8(bp + ks * 32);
     }
-    (void)nks;
     f32x4 acc = zero4();
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) acc = mfma16(a[ks], b[ks], acc);
@@ -814,13 +1023,7 @@ FEDMI_DEV void conv_bwd_body(
   uint8_t* am2s = smem + O_AM2;
   float* dxs = reinterpret_cast<float*>(smem + O_DX);
   bf16* wdg = reinterpret_cast<bf16*>(smem + O_WDG);
-  bf16* xsh = reinterpret_cast<bf16*>(smem + O_XSH);
-  bf16* p1sh = reinterpret_cast<bf16*>(smem + O_P1SH);
-  bf16* dY2w = reinterpret_cast<bf16*>(smem + O_DY2W);
-  bf16* dY2c = reinterpret_cast<bf16*>(smem + O_DY2C);
-  bf16* dY1 = reinterpret_cast<bf16*>(smem + O_DY1);
-  float* db = reinterpret_cast<float*>(smem + O_DB);
-  float* w1part = reinterpret_cast<float*>(smem + O_DW1);   // conv1 wgrad K-split partials [3][6][80]
+  const BwdLds L = bwd_lds(smem + O_SCR, raw, p1r, am1s, am2s, dxs, wdg);
 
   const int s = blk;
   [[maybe_unused]] const int stamp_wg = s;
@@ -846,155 +1049,16 @@ FEDMI_DEV void conv_bwd_body(
       else if (e < E5) reinterpret_cast<uint4*>(dxs)[e - E4] = dx4[e - E4];
       else {   // padded rows: 52 x 16 B per weight row
         const int w = e - E5, row = w / (KDGP / 8), col = w - row * (KDGP / 8);
-        reinterpret_cast<uint4*>(wdg + row * WDGS)[col] = wdg4[w];
+        reinterpret_cast<uint4*>(wdg + row * BW_WDGS)[col] = wdg4[w];
       }
     }
   }
-  zero_lds(dY2w, DY2W * 2);
-  zero_lds(dY2c, DY2C * 2);
-  zero_lds(dY1, DY1 * 2);
-  zero_lds(xsh, XSH * 2);      // tails of the shifted copies (x' + s beyond the row) stay zero
-  zero_lds(p1sh, P1SH * 2);
-  if (tid < 32) db[tid] = 0.f;
+  bwd_zero(L);
   const Aug a = aug_params(augment, seed, round_ctr, gidx);
   __syncthreads();
   FEDMI_STAMP(2, 1);
-
-  // each augmented pixel / pooled value is computed once and stored into its 5
-  // column-shifted copies: copy s holds element x at column x - s
-  for (int e = tid; e < IMG_BYTES; e += NT_CONV) {
-    const int c = e >> 10, y = (e >> 5) & 31, x = e & 31;
-    const bf16 v = (bf16)aug_pixel(raw, a, c, y, x);
-    bf16* row = xsh + c * XS_C + y * XROW + x;
-#pragma unroll
-    for (int sh = 0; sh < 5; ++sh)
-      if (x >= sh) row[sh * XS_S - sh] = v;
-  }
-  for (int e = tid; e < NP1; e += NT_CONV) {
-    const int c = e / 196, rem = e - c * 196, y = rem / P1, x = rem - y * P1;
-    const bf16 v = p1r[e];
-    bf16* row = p1sh + (c * 14 + y) * 16 + x;
-#pragma unroll
-    for (int sh = 0; sh < 5; ++sh)
-      if (x >= sh) row[sh * (6 * 14 * 16) - sh] = v;
-  }
-  for (int f = tid; f < F0; f += NT_CONV) {
-    const int o = f / 25, rem = f - o * 25, py = rem / P2, px = rem - py * P2;
-    const int am = am2s[f];
-    const int y = 2 * py + (am >> 1), x = 2 * px + (am & 1);
-    const float g = dxs[f];
-    const bf16 gb = (bf16)g;
-    dY2w[o * 160 + y * 16 + x] = gb;
-    dY2c[((y + 4) * 18 + (x + 4)) * DY2S + o] = gb;
-    atomicAdd(&db[o], g);
-  }
-  __syncthreads();
-  FEDMI_STAMP(2, 2);
-
-  float* slab = conv_slab + (size_t)s * CS;
-
-  // ---- conv2 wgrad: dW2[o][k'] = sum_p dY2[o][p] * im2col(pool1)[p][k']
-  //      M = 16 (o), N = 150 (10 tiles), K = 160 (p' = i*16 + j, 5 steps)
-  // task map over 16 waves: dgrad tile t -> wave t (t < 13), wgrad tile t -> wave (13 + t) % 16
-  for (int t = (wave + 3) & 15; t < 10; t += NW_CONV) {
-    const int kk = t * 16 + n16;
-    const int kc = kk < 150 ? kk : 0;
-    const int c = kc / 25, rs = kc - c * 25, r = rs / 5, sc = rs - r * 5;
-    const bf16* bb = p1sh + ((sc * 6 + c) * 14 + r) * 16 + (kq & 15);
-    f32x4 acc = zero4();
-#pragma unroll
-    for (int ks = 0; ks < 5; ++ks) {
-      const int i = 2 * ks + (kq >> 4);
-      acc = mfma16(ld8(dY2w + n16 * 160 + ks * 32 + kq), ld8(bb + i * 16), acc);
-    }
-    if (kk < 150) {
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) put_grad<PUB>(slab + P_C2W + (rq + rr) * 150 + kk, acc[rr]);
-    }
-  }
-
-  // ---- conv2 dgrad: dP1[c][pos] = sum_(r,s,o) dY2[o][y-r][x-s] W2[o][c][r][s]
-  //      M = 196 positions (13 tiles), N = 6 (pad 16), K = 416 (13 steps)
-  int koff[13];   // per-lane K-group offsets into dY2c relative to the output position
-#pragma unroll
-  for (int ks = 0; ks < 13; ++ks) {
-    const int G = ks * 4 + (lane >> 4), g = G >> 1;
-    const int r = g / 5, sc = g - r * 5;
-    koff[ks] = g < 25 ? (-r * 18 - sc) * DY2S + (G & 1) * 8 : 0;   // pad group: weight 0, any in-bounds read
-  }
-  for (int t = wave; t < 13; t += NW_CONV) {
-    int pos = t * 16 + n16;
-    if (pos >= 196) pos = 0;
-    const int y = pos / P1, x = pos - y * P1;
-    const bf16* gb = dY2c + ((y + 4) * 18 + (x + 4)) * DY2S;
-    const bf16* wb = wdg + min(n16, C1) * WDGS + kq;     // rows >= 6 are zero: share row 6 (broadcast)
-    f32x4 acc = zero4();
-#pragma unroll
-    for (int ks = 0; ks < 13; ++ks) acc = mfma16(ld8(gb + koff[ks]), ld8(wb + ks * 32), acc);
-    if (n16 < C1) {
-      const int c = n16;
-      float csum = 0.f;
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int p = t * 16 + rq + rr;
-        if (p < 196) {
-          const int py = p / P1, px = p - py * P1;
-          const float pooled = (float)p1r[c * 196 + p];
-          const float g = pooled > 0.f ? acc[rr] : 0.f;
-          const int am = am1s[c * 196 + p];
-          const int yy = 2 * py + (am >> 1), xx = 2 * px + (am & 1);
-          dY1[c * DY1S + yy * 32 + xx] = (bf16)g;
-          csum += g;
-        }
-      }
-      atomicAdd(&db[16 + c], csum);
-    }
-  }
-  __syncthreads();
-  FEDMI_STAMP(2, 3);
-
-  // ---- conv1 wgrad: dW1[o][k'] = sum_p dY1[o][p] * im2col(x)[p][k']
-  //      M = 16 (o < 6), N = 75 (5 tiles), K = 896 (p' = i*32 + j, 28 steps = conv1
-  //      output rows) split in 3 parts: 15 waves = 5 tiles x 3 K-parts, then a
-  //      deterministic 3-way combine through LDS.
-  if (wave < 15) {
-    const int nt = wave % 5, part = wave / 5;
-    const int ks0 = part * 10, ks1 = min(ks0 + 10, O1);
-    const int kk = nt * 16 + n16;
-    const int kc = kk < 75 ? kk : kk - 64;                 // pad columns: distinct bank groups, result dropped
-    const int c = kc / 25, rs = kc - c * 25, r = rs / 5, sc = rs - r * 5;
-    const bf16* bb = xsh + sc * XS_S + c * XS_C + r * XROW + kq;
-    const bf16* ab = dY1 + min(n16, C1 - 1) * DY1S + kq;
-    const bool arow = n16 < C1;
-    f32x4 acc0 = zero4(), acc1 = zero4();
-    int ks = ks0;
-    for (; ks + 1 < ks1; ks += 2) {
-      bf16x8 a0 = ld8(ab + ks * 32), a1 = ld8(ab + ks * 32 + 32);
-      if (!arow) { a0 = zero8(); a1 = zero8(); }
-      acc0 = mfma16(a0, ld8(bb + ks * XROW), acc0);
-      acc1 = mfma16(a1, ld8(bb + (ks + 1) * XROW), acc1);
-    }
-    if (ks < ks1) {
-      bf16x8 a0 = ld8(ab + ks * 32);
-      if (!arow) a0 = zero8();
-      acc0 = mfma16(a0, ld8(bb + ks * XROW), acc0);
-    }
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int o = rq + rr;
-      if (o < C1 && kk < 75) w1part[(part * 6 + o) * 80 + kk] = acc0[rr] + acc1[rr];
-    }
-  }
-  __syncthreads();
-  FEDMI_STAMP(2, 4);
-  for (int e = tid; e < C1 * 75; e += NT_CONV) {
-    const int o = e / 75, kk = e - o * 75;
-    put_grad<PUB>(slab + P_C1W + e, w1part[o * 80 + kk] + w1part[(6 + o) * 80 + kk] + w1part[(12 + o) * 80 + kk]);
-  }
-  if (tid < C1) put_grad<PUB>(slab + P_C1B + tid, db[16 + tid]);
-  if (tid < C2) put_grad<PUB>(slab + P_C2B + tid, db[tid]);
-  publish_flag<PUB>(flags, s, gen);
-  FEDMI_STAMP(2, 5);
+  bwd_build_shifted(L, a);
+  bwd_main<PUB>(L, conv_slab + (size_t)s * CS, flags, s, gen, 2, stamp_wg);
 }
 
 __global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
@@ -1006,6 +1070,421 @@ __global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
   conv_bwd_body<false>(blockIdx.x, images, sample_base, nb, seed, round_ctr, augment, dact2, act2T, dZ1T, pool1, am1,
                        am2, pk, conv_slab, fc1w_grad, nullptr, 0);
 }
+// ---------------------------------------------------------------------------
+// KS1 + KS2: the per-sample training step (the default training path).
+//
+// KS1 lenet_sample_step: ONE 16-wave workgroup per sample runs the WHOLE chain that
+// has no cross-sample dependency: augment -> conv stack forward -> fc1/fc2/fc3 ->
+// cross-entropy -> FC backward down to d(pool2) -> conv stack backward -> the
+// sample's conv gradient slab.  Every forward operand the backward needs (image,
+// pool1, argmax codes, act2) stays in LDS: no flag hand-off between workgroups
+// (nothing waits on another workgroup, so a shared GPU can never deadlock it), no
+// restaging from global memory, one kernel boundary less than K12 -> K3.  The FC
+// layers of ONE sample are GEMVs: VALU dot products over 16-B weight chunks of the
+// packed images (L2-resident, read by all 128 workgroups) with 8-lane shuffle
+// reductions -- a 16-row MFMA tile would be 15/16 padding.
+// KS1 writes the per-sample FC operands of the weight gradients (act2T, h1T, h2T,
+// dZ1T, dZ2T, dZ3T: sample-contiguous rows), the FC bias gradients and its loss.
+//
+// KS2 lenet_sgd2: fc1/fc2/fc3 weight gradients as MFMA GEMMs over the batch
+// (K = 128 samples), each workgroup applying SGD to the tile it just computed; the
+// conv slab combine (K4's), the bias sums and the loss/accuracy counters in fixed
+// order (deterministic, no atomics).
+// ---------------------------------------------------------------------------
+// Per-step FC side buffers, carved out of the [128][F0] fp32 'dact2' buffer (bytes).
+constexpr int AUX_H2T = 0;                              // bf16 [96][128]
+constexpr int AUX_DZ2T = AUX_H2T + 96 * 128 * 2;        // bf16 [96][128]
+constexpr int AUX_DZ3T = AUX_DZ2T + 96 * 128 * 2;       // bf16 [16][128]
+constexpr int FCB_N = 224;                              // fc1.bias 120 | fc2.bias 84 | fc3.bias 10 | pad
+constexpr int AUX_FCB = AUX_DZ3T + 16 * 128 * 2;        // f32 [128][FCB_N] per-sample bias grads
+constexpr int AUX_LOSS = AUX_FCB + MAX_TRAIN_BATCH * FCB_N * 4;   // f32 [128]
+constexpr int AUX_CORR = AUX_LOSS + MAX_TRAIN_BATCH * 4;          // f32 [128]
+constexpr int AUX_BYTES = AUX_CORR + MAX_TRAIN_BATCH * 4;
+static_assert(AUX_BYTES <= MAX_TRAIN_BATCH * F0 * 4, "FC side buffers must fit in dact2");
+
+// KS1 LDS (bytes): persistent operands, then one scratch region shared by the forward
+// (x image, conv1 out, pool1 channels-last, conv2 out) and the backward (BwdLds scratch).
+constexpr int S_O_RAW = 0, S_O_P1R = 3072, S_O_AM1 = S_O_P1R + 2368, S_O_AM2 = S_O_AM1 + 1184,
+              S_O_X = S_O_AM2 + 416, S_O_DX = S_O_X + F0P * 2, S_O_WDG = S_O_DX + F0 * 4,
+              S_O_FC = S_O_WDG + 16 * BW_WDGS * 2, S_O_W1C = S_O_FC + 2048, S_O_W2C = S_O_W1C + 16 * 136 * 2,
+              S_O_SCR = S_O_W2C + 16 * 232 * 2;
+// conv1 / conv2 B images in LDS, rows padded to 136 / 232 bf16 (17 / 29 16-B units: the 16 rows of a
+// fragment read land on distinct bank groups).  Staged ONCE per workgroup: per-wave register loads of
+// the same fragments cost 16 waves x 11 KB of L2 traffic per sample.
+constexpr int S_W1C_LD = 136, S_W2C_LD = 232;
+constexpr int S_F_XCL = 0, S_F_C1 = S_F_XCL + 36 * 40 * 4 * 2, S_F_P1 = S_F_C1 + NPOS1 * 8 * 4,
+              S_F_C2 = S_F_P1 + 14 * 14 * 8 * 2, S_F_END = S_F_C2 + C2 * NPOS2 * 4;
+constexpr int S_END = S_O_SCR + (S_F_END > BW_SCRATCH ? S_F_END : BW_SCRATCH);
+// FC scratch (floats, bf16-rounded values where the old MFMA path used bf16 operands)
+constexpr int SF_H1 = 0, SF_H2 = 128, SF_Z = 224, SF_DZ3 = 240, SF_DZ2 = 256, SF_DZ1 = 352, SF_END = 480;
+static_assert(SF_END * 4 <= 2048, "FC scratch");
+
+FEDMI_DEV float dot8(const bf16x8& a, const bf16x8& b, float acc) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc += (float)a[j] * (float)b[j];
+  return acc;
+}
+FEDMI_DEV float dot8f(const float* a, const bf16x8& b, float acc) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc += a[j] * (float)b[j];
+  return acc;
+}
+FEDMI_DEV float sum8lanes(float v) {   // over the 8 consecutive lanes of a group
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  return v;
+}
+FEDMI_DEV float bfr(float v) { return (float)(bf16)v; }
+
+__global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
+    const uint8_t* __restrict__ images, int sample_base, int nb,
+    const bf16* __restrict__ pk, const float* __restrict__ params,
+    uint32_t seed, const int* __restrict__ round_ctr, int augment,
+    const int* __restrict__ labels,      // labels of this batch (already offset)
+    bf16* __restrict__ act2T,            // [F0P][128]
+    bf16* __restrict__ h1T,              // [128][128]
+    unsigned char* __restrict__ aux,     // AUX_* side buffers
+    bf16* __restrict__ dZ1T,             // [128][128]
+    float* __restrict__ conv_slab)       // [nb][CS]
+{
+  __shared__ __attribute__((aligned(16))) unsigned char smem[S_END];
+  const int s = blockIdx.x;
+  if (s >= nb) return;
+  [[maybe_unused]] const int stamp_wg = s;
+  const int gidx = sample_base + s;
+  const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
+  const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
+  uint8_t* raw = smem + S_O_RAW;
+  bf16* p1r = reinterpret_cast<bf16*>(smem + S_O_P1R);
+  uint8_t* am1s = smem + S_O_AM1;
+  uint8_t* am2s = smem + S_O_AM2;
+  bf16* xrow = reinterpret_cast<bf16*>(smem + S_O_X);
+  float* dxs = reinterpret_cast<float*>(smem + S_O_DX);
+  bf16* wdg = reinterpret_cast<bf16*>(smem + S_O_WDG);
+  float* fcs = reinterpret_cast<float*>(smem + S_O_FC);
+  unsigned char* scr = smem + S_O_SCR;
+  bf16* xcl = reinterpret_cast<bf16*>(scr + S_F_XCL);
+  float* c1 = reinterpret_cast<float*>(scr + S_F_C1);
+  bf16* p1cl = reinterpret_cast<bf16*>(scr + S_F_P1);
+  float* c2 = reinterpret_cast<float*>(scr + S_F_C2);
+  FEDMI_STAMP(0, 0);
+
+  // ---- stage: image (192 x 16 B) and the conv2 dgrad weight image (832 x 16 B) -- one
+  //      16-B load per thread; both land while the x image is zeroed and the augmentation drawn
+  bf16* w1c = reinterpret_cast<bf16*>(smem + S_O_W1C);
+  bf16* w2c = reinterpret_cast<bf16*>(smem + S_O_W2C);
+  float bias1, bias2;
+  Aug a;
+  {
+    // 192 image + 832 dgrad-weight + 256 conv1-weight + 448 conv2-weight 16-B chunks (<= 2 per thread)
+    constexpr int NI = IMG_BYTES / 16, NWD = 16 * KDGP / 8, NW1 = 16 * K1C / 8, NW2 = 16 * K2C / 8;
+    constexpr int E1 = NI, E2 = E1 + NWD, E3 = E2 + NW1, E4 = E3 + NW2;
+    uint4 v[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+#ifdef FEDMI_STAMPS
+    const int dg = fedmi_ks1_diag;
+    const size_t img_sample = (dg & 2) ? 0 : (size_t)gidx;
+    const int lim = (dg & 1) ? E1 : E4;
+#else
+    const size_t img_sample = (size_t)gidx;
+    constexpr int lim = E4;
+#endif
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * NT_CONV;
+      if (e < E1) v[u] = reinterpret_cast<const uint4*>(images + img_sample * IMG_BYTES)[e];
+      else if (e >= lim) {}
+      else if (e < E2) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2DG)[e - E1];
+      else if (e < E3) v[u] = reinterpret_cast<const uint4*>(pk + PK_W1C)[e - E2];
+      else if (e < E4) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2C)[e - E3];
+    }
+    // the other global reads of the kernel's start go out in the same wave of requests (one
+    // memory latency for the whole stage instead of one per dependent group)
+    bias1 = n16 < C1 ? params[P_C1B + n16] : 0.f;
+    bias2 = params[P_C2B + n16];
+    a = aug_params(augment, seed, round_ctr, gidx);
+    zero_lds(xcl, 36 * 40 * 4 * 2);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * NT_CONV;
+      if (e < E1) {
+        reinterpret_cast<uint4*>(raw)[e] = v[u];
+      } else if (e < E2) {
+        const int w = e - E1, row = w / (KDGP / 8), col = w - row * (KDGP / 8);
+        reinterpret_cast<uint4*>(wdg + row * BW_WDGS)[col] = v[u];
+      } else if (e < E3) {
+        const int w = e - E2, row = w / (K1C / 8), col = w - row * (K1C / 8);
+        reinterpret_cast<uint4*>(w1c + row * S_W1C_LD)[col] = v[u];
+      } else if (e < E4) {
+        const int w = e - E3, row = w / (K2C / 8), col = w - row * (K2C / 8);
+        reinterpret_cast<uint4*>(w2c + row * S_W2C_LD)[col] = v[u];
+      }
+    }
+  }
+  int go1[4], go2[7];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int g = ks * 4 + (lane >> 4);
+    go1[ks] = g < 15 ? ((g / 3) * 40 + 2 * (g % 3)) * 4 : 0;
+  }
+#pragma unroll
+  for (int ks = 0; ks < 7; ++ks) {
+    const int g = ks * 4 + (lane >> 4);
+    go2[ks] = g < 25 ? ((g / 5) * P1 + (g % 5)) * 8 : 0;
+  }
+  __syncthreads();
+  FEDMI_STAMP(1, 7);
+  bf16x8 wb1[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) wb1[ks] = ld8(w1c + n16 * S_W1C_LD + ks * 32 + kq);
+  for (int e = tid; e < IMG_BYTES; e += NT_CONV) {
+    const int c = e >> 10, y = (e >> 5) & 31, x = e & 31;
+    xcl[(y * 40 + x) * 4 + c] = (bf16)aug_pixel(raw, a, c, y, x);
+  }
+  __syncthreads();
+  FEDMI_STAMP(0, 1);
+
+  // ---- conv1 (+bias+ReLU): 49 tiles over 16 waves, two tiles per pass
+  for (int t = wave; t < NPOS1 / 16; t += 2 * NW_CONV) {
+    const int tb = t + NW_CONV;
+    const bool two = tb < NPOS1 / 16;
+    const int pa = t * 16 + n16, pb = (two ? tb : t) * 16 + n16;
+    const bf16* xa = xcl + ((pa / O1) * 40 + pa % O1) * 4;
+    const bf16* xbb = xcl + ((pb / O1) * 40 + pb % O1) * 4;
+    bf16x8 fa[4], fb[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      fa[ks] = ld8_b64x2(xa + go1[ks]);
+      fb[ks] = ld8_b64x2(xbb + go1[ks]);
+    }
+    f32x4 acc = zero4(), accb = zero4();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      acc = mfma16(fa[ks], wb1[ks], acc);
+      accb = mfma16(fb[ks], wb1[ks], accb);
+    }
+    if (n16 < C1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c1[(t * 16 + rq + r) * 8 + n16] = fmaxf(acc[r] + bias1, 0.f);
+      if (two) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c1[(tb * 16 + rq + r) * 8 + n16] = fmaxf(accb[r] + bias1, 0.f);
+      }
+    }
+  }
+  // fc1 weight chunks of this thread (row n = tid/8, k = q*8 + 64 i): in flight through pool1..pool2
+  const int fn = tid >> 3, fq = tid & 7;
+  bf16x8 w1v[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int k = fq * 8 + 64 * i;
+    w1v[i] = k < F0P ? ld8(pk + PK_FC1 + fn * F0P + k) : zero8();
+  }
+  __syncthreads();
+  FEDMI_STAMP(0, 2);
+
+  // ---- maxpool2 #1 (+ argmax code: 0=(0,0) 1=(0,1) 2=(1,0) 3=(1,1), first max wins)
+  for (int e = tid; e < 14 * 14 * 8; e += NT_CONV) {
+    const int pos = e >> 3, c = e & 7;
+    bf16 mb = (bf16)0.f;
+    if (c < C1) {
+      const int py = pos / P1, px = pos - py * P1;
+      const float* w = c1 + ((2 * py) * O1 + 2 * px) * 8 + c;
+      float m = w[0]; int am = 0;
+      if (w[8] > m) { m = w[8]; am = 1; }
+      if (w[O1 * 8] > m) { m = w[O1 * 8]; am = 2; }
+      if (w[O1 * 8 + 8] > m) { m = w[O1 * 8 + 8]; am = 3; }
+      mb = (bf16)m;
+      p1r[c * 196 + pos] = mb;
+      am1s[c * 196 + pos] = (uint8_t)am;
+    }
+    p1cl[e] = mb;
+  }
+  __syncthreads();
+  FEDMI_STAMP(0, 3);
+
+  // ---- conv2 (+bias+ReLU): M = 100 positions (7 tiles), N = 16, K = 224
+  if (wave < 7) {
+    const int t = wave;
+    int pos = t * 16 + n16;
+    if (pos >= NPOS2) pos = 0;
+    const int py = pos / O2, px = pos - py * O2;
+    const bf16* pb = p1cl + (py * P1 + px) * 8;
+    const bf16* wb = w2c + n16 * S_W2C_LD + kq;
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int ks = 0; ks < 7; ++ks) acc = mfma16(ld8(pb + go2[ks]), ld8(wb + ks * 32), acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int p = t * 16 + rq + r;
+      if (p < NPOS2) c2[p * 16 + n16] = fmaxf(acc[r] + bias2, 0.f);
+    }
+  }
+  __syncthreads();
+  FEDMI_STAMP(0, 4);
+
+  // ---- maxpool2 #2 -> act2 row (torch .view order o*25 + py*5 + px) in LDS + act2T column
+  for (int e = tid; e < F0P; e += NT_CONV) {
+    bf16 mb = (bf16)0.f;
+    if (e < F0) {
+      const int o = e / 25, rem = e - o * 25, py = rem / P2, px = rem - py * P2;
+      const float* w = c2 + ((2 * py) * O2 + 2 * px) * 16 + o;
+      float m = w[0]; int am = 0;
+      if (w[16] > m) { m = w[16]; am = 1; }
+      if (w[O2 * 16] > m) { m = w[O2 * 16]; am = 2; }
+      if (w[O2 * 16 + 16] > m) { m = w[O2 * 16 + 16]; am = 3; }
+      mb = (bf16)m;
+      am2s[e] = (uint8_t)am;
+    }
+    xrow[e] = mb;
+    act2T[(size_t)e * MAX_TRAIN_BATCH + s] = mb;
+  }
+  // fc2 / fc3 weight chunks and the FC biases
+  const int n2 = fn < 96 ? fn : 95, n3 = fn < 16 ? fn : 15;
+  bf16x8 w2v[2], w3v[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    w2v[i] = ld8(pk + PK_FC2 + n2 * 128 + fq * 8 + 64 * i);
+    w3v[i] = (fq * 8 + 64 * i < 96) ? ld8(pk + PK_FC3 + n3 * 96 + fq * 8 + 64 * i) : zero8();
+  }
+  const float fb1 = params[P_F1B + min(fn, F1 - 1)];
+  const float fb2 = params[P_F2B + min(fn, F2 - 1)];
+  const float fb3 = params[P_F3B + min(fn, NCLS - 1)];
+  __syncthreads();
+  const BwdLds L = bwd_lds(scr, raw, p1r, am1s, am2s, dxs, wdg);
+  bwd_zero(L);                 // the forward scratch is dead: the backward's images take its place
+  FEDMI_STAMP(0, 5);
+
+  // ---- fc1: h1[n] = relu(x . W1[n] + b1)  (thread = (n, 8-lane k slice))
+  unsigned char* auxp = aux;
+  float* fcb = reinterpret_cast<float*>(auxp + AUX_FCB) + (size_t)s * FCB_N;
+  {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int k = fq * 8 + 64 * i;
+      if (k < F0P) acc = dot8(ld8(xrow + k), w1v[i], acc);
+    }
+    acc = sum8lanes(acc);
+    if (fq == 0) {
+      const float h = bfr(fn < F1 ? fmaxf(acc + fb1, 0.f) : 0.f);
+      fcs[SF_H1 + fn] = h;
+      h1T[(size_t)fn * MAX_TRAIN_BATCH + s] = (bf16)h;
+    }
+  }
+  // backward weight chunks: fc1^T rows (dX), fc2^T rows (dH1), fc3^T rows (dH2)
+  const int kx = tid >> 1, hx = tid & 1;
+  bf16x8 w1t[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w1t[i] = kx < F0 ? ld8(pk + PK_FC1T + kx * 128 + hx * 8 + 16 * i) : zero8();
+  bf16x8 w2t[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) w2t[i] = (fq * 8 + 64 * i < 96) ? ld8(pk + PK_FC2T + fn * 96 + fq * 8 + 64 * i) : zero8();
+  bf16x8 w3t[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) w3t[i] = tid < 96 ? ld8(pk + PK_FC3T + tid * 32 + 8 * i) : zero8();
+  __syncthreads();
+
+  FEDMI_STAMP(1, 0);
+  // ---- fc2: h2[n] = relu(h1 . W2[n] + b2)
+  if (fn < 96) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc = dot8f(fcs + SF_H1 + fq * 8 + 64 * i, w2v[i], acc);
+    acc = sum8lanes(acc);
+    if (fq == 0) {
+      const float h = bfr(fn < F2 ? fmaxf(acc + fb2, 0.f) : 0.f);
+      fcs[SF_H2 + fn] = h;
+      reinterpret_cast<bf16*>(auxp + AUX_H2T)[(size_t)fn * MAX_TRAIN_BATCH + s] = (bf16)h;
+    }
+  }
+  __syncthreads();
+  FEDMI_STAMP(1, 1);
+  // ---- fc3: logits (waves 0..1); waves 2..15 meanwhile build the conv backward's column-shifted
+  //      copies (zeroed after pool2): the FC chain's idle waves absorb that LDS work
+  if (fn < 16) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (fq * 8 + 64 * i < 96) acc = dot8f(fcs + SF_H2 + fq * 8 + 64 * i, w3v[i], acc);
+    acc = sum8lanes(acc);
+    if (fq == 0) fcs[SF_Z + fn] = fn < NCLS ? acc + fb3 : 0.f;
+  } else {
+    bwd_build_shifted(L, a, tid - 128, NT_CONV - 128);
+  }
+  __syncthreads();
+  FEDMI_STAMP(1, 2);
+  // ---- cross-entropy (mean over the batch nb), accuracy, dZ3 (one lane: ten classes)
+  if (tid == 0) {
+    float z[NCLS];
+#pragma unroll
+    for (int n = 0; n < NCLS; ++n) z[n] = fcs[SF_Z + n];
+    float mx = z[0]; int am = 0;
+#pragma unroll
+    for (int n = 1; n < NCLS; ++n) if (z[n] > mx) { mx = z[n]; am = n; }
+    float se = 0.f;
+#pragma unroll
+    for (int n = 0; n < NCLS; ++n) se += __expf(z[n] - mx);
+    const float lse = mx + __logf(se);
+    const int y = labels[s];
+    float zy = 0.f;
+#pragma unroll
+    for (int n = 0; n < NCLS; ++n) zy = (n == y) ? z[n] : zy;
+    reinterpret_cast<float*>(auxp + AUX_LOSS)[s] = lse - zy;
+    reinterpret_cast<float*>(auxp + AUX_CORR)[s] = (am == y) ? 1.f : 0.f;
+    const float inv = 1.f / (float)nb;
+    bf16* dz3t = reinterpret_cast<bf16*>(auxp + AUX_DZ3T);
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      const float d = n < NCLS ? (__expf(z[n] - lse) - (n == y ? 1.f : 0.f)) * inv : 0.f;
+      fcs[SF_DZ3 + n] = bfr(d);
+      dz3t[(size_t)n * MAX_TRAIN_BATCH + s] = (bf16)d;
+      if (n < NCLS) fcb[204 + n] = d;
+    }
+  }
+  __syncthreads();
+  FEDMI_STAMP(1, 3);
+  // ---- dH2 = dZ3 . W3 -> dZ2 (pool of fc2's ReLU)
+  if (tid < 96) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc = dot8f(fcs + SF_DZ3 + 8 * i, w3t[i], acc);
+    const float g = (tid < F2 && fcs[SF_H2 + tid] > 0.f) ? acc : 0.f;
+    fcs[SF_DZ2 + tid] = bfr(g);
+    reinterpret_cast<bf16*>(auxp + AUX_DZ2T)[(size_t)tid * MAX_TRAIN_BATCH + s] = (bf16)g;
+    if (tid < F2) fcb[120 + tid] = g;
+  }
+  __syncthreads();
+  FEDMI_STAMP(1, 4);
+  // ---- dH1 = dZ2 . W2 -> dZ1
+  {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (fq * 8 + 64 * i < 96) acc = dot8f(fcs + SF_DZ2 + fq * 8 + 64 * i, w2t[i], acc);
+    acc = sum8lanes(acc);
+    if (fq == 0) {
+      const float g = (fn < F1 && fcs[SF_H1 + fn] > 0.f) ? acc : 0.f;
+      fcs[SF_DZ1 + fn] = bfr(g);
+      dZ1T[(size_t)fn * DZ1_LD + s] = (bf16)g;
+      if (fn < F1) fcb[fn] = g;
+    }
+  }
+  __syncthreads();
+  FEDMI_STAMP(1, 5);
+  // ---- dX = dZ1 . W1, masked by the pool2 ReLU -> d(pool2) in LDS
+  {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc = dot8f(fcs + SF_DZ1 + hx * 8 + 16 * i, w1t[i], acc);
+    acc += __shfl_xor(acc, 1, 64);
+    if (hx == 0 && kx < F0) dxs[kx] = (float)xrow[kx] > 0.f ? acc : 0.f;
+  }
+  __syncthreads();             // d(pool2) from every wave before the conv backward scatters it
+  FEDMI_STAMP(0, 6);
+  bwd_main<false>(L, conv_slab + (size_t)s * CS, nullptr, s, 0, 2, stamp_wg);
+}
+
 // ---------------------------------------------------------------------------
 // Packing: fp32 master -> bf16 MFMA operand images.
 // ---------------------------------------------------------------------------
@@ -1122,6 +1601,187 @@ __global__ __launch_bounds__(256) void lenet_sgd(
   if (b == 0 && tid == 0) {
     if (round_ctr) atomicAdd(round_ctr, 1);
     if (step_gen) step_gen[0] += 1;        // generation of K12's hand-off flags (one writer)
+  }
+  FEDMI_STAMP(3, 1);
+}
+
+// Masks the sample columns >= nb of an operand fragment (8 consecutive samples from s0).
+FEDMI_DEV bf16x8 mask_cols(bf16x8 v, int s0, int nb) {
+  if (s0 + 8 <= nb) return v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (s0 + j >= nb) v[j] = (bf16)0.f;
+  return v;
+}
+
+// One 16x16 tile of dW = dZ^T X over the batch: A rows = dZ^T (sample-contiguous, masked
+// beyond nb), B rows = X^T (sample-contiguous), K = 128 samples (4 MFMA steps).
+// Both operands are masked: columns >= nb may hold anything (the buffers are shared scratch).
+// The tile's SGD operands (params / momentum of the <= 4 elements of this lane, indices idx[r],
+// -1 = none) are loaded in the same wave of requests as the GEMM operands.
+FEDMI_DEV f32x4 batch_tile(const bf16* __restrict__ a, const bf16* __restrict__ b, int nb,
+                           const float* __restrict__ params, const float* __restrict__ mom, const int* idx,
+                           float* p, float* m) {
+  const int lane = lane_id(), kq = (lane >> 4) * 8, n16 = lane & 15;
+  bf16x8 av[4], bv[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    av[ks] = ld8(a + n16 * MAX_TRAIN_BATCH + ks * 32 + kq);
+    bv[ks] = ld8(b + n16 * MAX_TRAIN_BATCH + ks * 32 + kq);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    p[r] = idx[r] >= 0 ? params[idx[r]] : 0.f;
+    m[r] = idx[r] >= 0 ? mom[idx[r]] : 0.f;
+  }
+  f32x4 acc = zero4();
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+    acc = mfma16(mask_cols(av[ks], ks * 32 + kq, nb), mask_cols(bv[ks], ks * 32 + kq, nb), acc);
+  return acc;
+}
+
+constexpr int SGD2_NB = (8 * 25 + 3) / 4;    // fc1.weight: 200 tiles, one per wave
+constexpr int SGD2_NC = (6 * 8 + 3) / 4;     // fc2.weight: 48 tiles
+constexpr int SGD2_ND = (6 + 3) / 4;         // fc3.weight: 6 tiles
+constexpr int SGD2_NE = 4;                   // FC biases: 64 per block x 4 sample groups
+constexpr int SGD2_GRID = SGD_NA + SGD2_NB + SGD2_NC + SGD2_ND + SGD2_NE + 1;   // + loss/accuracy block
+
+__global__ __launch_bounds__(256) void lenet_sgd2(
+    float* __restrict__ params, float* __restrict__ mom, bf16* __restrict__ pk,
+    const float* __restrict__ conv_slab, int nb,
+    const bf16* __restrict__ act2T, const bf16* __restrict__ h1T, const unsigned char* __restrict__ aux,
+    const bf16* __restrict__ dZ1T, float lr, float momentum, float wd,
+    int* __restrict__ round_ctr, int* __restrict__ step_gen, Stats* __restrict__ stats)
+{
+  __shared__ float red[16][17];
+  const int b = blockIdx.x, tid = threadIdx.x, wave = wave_id(), lane = lane_id();
+  const int n16 = lane & 15, rq = (lane >> 4) * 4;
+  [[maybe_unused]] const int stamp_wg = b;
+  FEDMI_STAMP(3, 0);
+  if (b < SGD_NA) {                                   // conv params: K4's slab combine
+    const int pl = tid & 15, g = tid >> 4;
+    const int i = b * 16 + pl;
+    float p = 0.f, m = 0.f;
+    if (g == 0 && i < CS) { p = params[i]; m = mom[i]; }
+    float sum = 0.f;
+    if (i < CS) {
+      float v[MAX_TRAIN_BATCH / 16];
+#pragma unroll
+      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) {
+        const int q = g + 16 * u;
+        v[u] = q < nb ? conv_slab[(size_t)q * CS + i] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) sum += v[u];
+    }
+    red[g][pl] = sum;
+    __syncthreads();
+    if (g == 0 && i < CS) {
+      float tot = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) tot += red[q][pl];
+      sgd_apply(i, tot, p, m, params, mom, pk, lr, momentum, wd);
+    }
+  } else if (b < SGD_NA + SGD2_NB) {                  // fc1.weight [120][400]: 8 x 25 tiles
+    const int t = (b - SGD_NA) * 4 + wave;
+    if (t < 200) {
+      const int nt = t / 25, ft = t - nt * 25;
+      int idx[4];
+      float p[4], m[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = nt * 16 + rq + r, f = ft * 16 + n16;
+        idx[r] = n < F1 ? P_F1W + n * F0 + f : -1;
+      }
+      const f32x4 acc = batch_tile(dZ1T + (size_t)nt * 16 * DZ1_LD, act2T + (size_t)ft * 16 * MAX_TRAIN_BATCH, nb,
+                                   params, mom, idx, p, m);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (idx[r] >= 0) sgd_apply(idx[r], acc[r], p[r], m[r], params, mom, pk, lr, momentum, wd);
+    }
+  } else if (b < SGD_NA + SGD2_NB + SGD2_NC) {        // fc2.weight [84][120]: 6 x 8 tiles
+    const int t = (b - SGD_NA - SGD2_NB) * 4 + wave;
+    if (t < 48) {
+      const int nt = t >> 3, ft = t & 7;
+      const bf16* dz2t = reinterpret_cast<const bf16*>(aux + AUX_DZ2T);
+      int idx[4];
+      float p[4], m[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = nt * 16 + rq + r, f = ft * 16 + n16;
+        idx[r] = (n < F2 && f < F1) ? P_F2W + n * F1 + f : -1;
+      }
+      const f32x4 acc = batch_tile(dz2t + (size_t)nt * 16 * MAX_TRAIN_BATCH, h1T + (size_t)ft * 16 * MAX_TRAIN_BATCH, nb,
+                                   params, mom, idx, p, m);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (idx[r] >= 0) sgd_apply(idx[r], acc[r], p[r], m[r], params, mom, pk, lr, momentum, wd);
+    }
+  } else if (b < SGD_NA + SGD2_NB + SGD2_NC + SGD2_ND) {   // fc3.weight [10][84]: 1 x 6 tiles
+    const int t = (b - SGD_NA - SGD2_NB - SGD2_NC) * 4 + wave;
+    if (t < 6) {
+      const bf16* dz3t = reinterpret_cast<const bf16*>(aux + AUX_DZ3T);
+      const bf16* h2t = reinterpret_cast<const bf16*>(aux + AUX_H2T);
+      int idx[4];
+      float p[4], m[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = rq + r, f = t * 16 + n16;
+        idx[r] = (n < NCLS && f < F2) ? P_F3W + n * F2 + f : -1;
+      }
+      const f32x4 acc = batch_tile(dz3t, h2t + (size_t)t * 16 * MAX_TRAIN_BATCH, nb, params, mom, idx, p, m);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (idx[r] >= 0) sgd_apply(idx[r], acc[r], p[r], m[r], params, mom, pk, lr, momentum, wd);
+    }
+  } else {                                            // FC biases + loss / accuracy counters
+    // block e < 4: biases [64e, 64e + 64) x 4 sample groups of 32 (all 32 loads in flight),
+    // fixed-order combine; block 4: the per-sample losses / hits (fixed tree order)
+    const int e = b - (SGD_NA + SGD2_NB + SGD2_NC + SGD2_ND);
+    const float* fcb = reinterpret_cast<const float*>(aux + AUX_FCB);
+    const int j = e * 64 + (tid & 63), g = tid >> 6;
+    __shared__ float bsum[4][64];
+    float bp = 0.f, bm = 0.f;
+    const int bi = j < 120 ? P_F1B + j : (j < 204 ? P_F2B + j - 120 : P_F3B + j - 204);
+    if (e < SGD2_NE && g == 0 && j < 214) { bp = params[bi]; bm = mom[bi]; }
+    if (e < SGD2_NE && j < 214) {
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int sm = g * 32 + u;
+        v[u] = sm < nb ? fcb[(size_t)sm * FCB_N + j] : 0.f;
+      }
+      float sum = 0.f;
+#pragma unroll
+      for (int u = 0; u < 32; ++u) sum += v[u];
+      bsum[g][tid & 63] = sum;
+    } else if (e == SGD2_NE && g == 0 && stats != nullptr) {
+      const float* lv = reinterpret_cast<const float*>(aux + AUX_LOSS);
+      const float* cv = reinterpret_cast<const float*>(aux + AUX_CORR);
+      float ls = 0.f, cs = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int sm = lane + 64 * u;
+        if (sm < nb) { ls += lv[sm]; cs += cv[sm]; }
+      }
+      ls = wave_sum(ls);
+      cs = wave_sum(cs);
+      if (lane == 0) {
+        stats->loss_sum += ls;
+        stats->correct += (int)(cs + 0.5f);
+        stats->count += nb;
+      }
+    }
+    __syncthreads();
+    if (e < SGD2_NE && g == 0 && j < 214) {
+      const float sum = (bsum[0][tid] + bsum[1][tid]) + (bsum[2][tid] + bsum[3][tid]);
+      sgd_apply(bi, sum, bp, bm, params, mom, pk, lr, momentum, wd);
+    }
+  }
+  if (b == 0 && tid == 0) {
+    if (round_ctr) atomicAdd(round_ctr, 1);
+    if (step_gen) step_gen[0] += 1;
   }
   FEDMI_STAMP(3, 1);
 }
@@ -1320,6 +1980,14 @@ bool stamps_enabled() {
 #endif
 }
 
+void set_ks1_diag(int v) {
+#ifdef FEDMI_STAMPS
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(fedmi_ks1_diag), &v, sizeof(v), 0, hipMemcpyHostToDevice);
+#else
+  (void)v;
+#endif
+}
+
 // Copy (and optionally clear) the per-phase s_memtime stamps of the diagnostic build.
 void read_stamps(unsigned long long* host, bool clear) {
 #ifdef FEDMI_STAMPS
@@ -1336,6 +2004,23 @@ void read_stamps(unsigned long long* host, bool clear) {
 
 void launch_lenet_pack(hipStream_t st, const float* params, bf16* pk) {
   hipLaunchKernelGGL(lenet_pack, dim3((P_TOTAL + 255) / 256), dim3(256), 0, st, params, pk);
+}
+
+
+void launch_lenet_sample_step(hipStream_t st, const uint8_t* images, int sample_base, int nb, const bf16* pk,
+                              const float* params, uint32_t seed, const int* round_ctr, int augment,
+                              const int* labels, bf16* act2T, bf16* h1T, float* aux, bf16* dZ1T, float* conv_slab) {
+  if (nb <= 0 || nb > MAX_TRAIN_BATCH) throw std::invalid_argument("lenet_sample_step: batch must be in [1, 128]");
+  hipLaunchKernelGGL(lenet_sample_step, dim3(nb), dim3(NT_CONV), 0, st, images, sample_base, nb, pk, params, seed,
+                     round_ctr, augment, labels, act2T, h1T, reinterpret_cast<unsigned char*>(aux), dZ1T, conv_slab);
+}
+
+void launch_lenet_sgd2(hipStream_t st, float* params, float* mom, bf16* pk, const float* conv_slab, int nb,
+                       const bf16* act2T, const bf16* h1T, const float* aux, const bf16* dZ1T, float lr,
+                       float momentum, float wd, int* round_ctr, int* step_gen, Stats* stats) {
+  if (nb <= 0 || nb > MAX_TRAIN_BATCH) throw std::invalid_argument("lenet_sgd2: batch must be in [1, 128]");
+  hipLaunchKernelGGL(lenet_sgd2, dim3(SGD2_GRID), dim3(256), 0, st, params, mom, pk, conv_slab, nb, act2T, h1T,
+                     reinterpret_cast<const unsigned char*>(aux), dZ1T, lr, momentum, wd, round_ctr, step_gen, stats);
 }
 
 }  // namespace fedmi

@@ -25,6 +25,10 @@ void launch_lenet_bwd_sgd(hipStream_t, const uint8_t*, int, int, uint32_t, const
                           const bf16*, const bf16*, const uint8_t*, const uint8_t*, float*, float*, float*, float*, bf16*,
                           const float*, int, float, float, float, int*, const int*, int*, int*, Stats*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
+void launch_lenet_sample_step(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*,
+                              int, const int*, bf16*, bf16*, float*, bf16*, float*);
+void launch_lenet_sgd2(hipStream_t, float*, float*, bf16*, const float*, int, const bf16*, const bf16*, const float*,
+                       const bf16*, float, float, float, int*, int*, lenet::Stats*);
 
 void check_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("fedmi HIP error in ") + what + ": " + hipGetErrorString(e));
@@ -79,6 +83,17 @@ void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round, bool 
   if (nb <= 0 || nb > MAX_TRAIN_BATCH || start < 0 || start + nb > b_.n_train)
     throw std::invalid_argument("LeNetEngine::step: batch out of range");
   const int aug = augment_ ? 1 : 0;
+  if (sample_path_) {
+    if (reset_stats) check_hip(hipMemsetAsync(b_.train_stats, 0, sizeof(Stats), st), "memset stats");
+    // the FC side buffers (h2T, dZ2T, dZ3T, bias grads, losses) live in the dact2 buffer, h1T in h1
+    launch_lenet_sample_step(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug,
+                             b_.train_labels + start, b_.act2T, b_.h1, b_.dact2, b_.dZ1T, b_.conv_slab);
+    launch_lenet_sgd2(st, b_.params, b_.mom, b_.pk, b_.conv_slab, nb, b_.act2T, b_.h1, b_.dact2, b_.dZ1T, sgd_.lr,
+                      sgd_.momentum, sgd_.weight_decay, bump_round ? b_.round_ctr : nullptr, b_.step_gen,
+                      b_.train_stats);
+    check_hip(hipGetLastError(), "LeNetEngine::step launch");
+    return;
+  }
   if (fuse_head_) {
     if (reset_stats) check_hip(hipMemsetAsync(b_.train_stats, 0, sizeof(Stats), st), "memset stats");
     launch_lenet_fwd_head(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug, b_.act2,
@@ -104,6 +119,15 @@ void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round, bool 
                      bump_round ? b_.round_ctr : nullptr, b_.step_gen);
   }
   check_hip(hipGetLastError(), "LeNetEngine::step launch");
+}
+
+void LeNetEngine::set_sample_path(bool on) {
+  if (on && (!b_.h1 || !b_.dact2 || !b_.dZ1T || !b_.act2T))
+    throw std::invalid_argument("sample path needs h1, dact2, dZ1T and act2T buffers");
+  if (on != sample_path_) {
+    sample_path_ = on;
+    drop_graph();
+  }
 }
 
 void LeNetEngine::set_fuse_head(bool on) {

@@ -76,6 +76,10 @@ class LeNetEngine {
   // conv backward + SGD in one launch (K34) instead of K3 then K4 (needs fuse_head, bwd_flags/bwd_gen)
   void set_fuse_sgd(bool on);
   bool fuse_sgd() const { return fuse_sgd_; }
+  // per-sample step (KS1: one workgroup runs a sample's whole forward + backward) + GEMM/SGD (KS2):
+  // 2 launches per step, no inter-workgroup hand-off; takes precedence over fuse_head / fuse_sgd
+  void set_sample_path(bool on);
+  bool sample_path() const { return sample_path_; }
 
  private:
   void enqueue_epoch(hipStream_t st);
@@ -88,6 +92,7 @@ class LeNetEngine {
   bool fuse_fc1_ = false;
   bool fuse_head_ = false;
   bool fuse_sgd_ = false;
+  bool sample_path_ = false;
   std::vector<int> starts_, sizes_;
   hipStream_t cap_stream_ = nullptr;
   hipGraph_t graph_ = nullptr;

@@ -299,6 +299,7 @@ class Coordinator:
                 # the survivors' all-reduce for this round is not trustworthy: roll them back to the
                 # last committed global model, then regroup (new generation) next round
                 self._log(f"round {rnd} aborted ({len(failed)} client(s) lost); rolling back survivors, regrouping")
+                self._last_live = None           # force a new generation even if every member answered ABORTED
                 if self.latest_model is not None:
                     b64 = ck.to_b64(self.latest_model)
                     sends = [self._pool.submit(self._send_model, a, b64) for a in live if a not in failed]

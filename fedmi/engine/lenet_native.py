@@ -91,12 +91,7 @@ class LeNetNativeTrainer(LocalTrainer):
         self.engine = nat.LeNetEngine(self._bufs, cfg.lr, cfg.momentum, cfg.weight_decay, cfg.seed & 0xFFFFFFFF,
                                       bool(data.augment and cfg.augment))
         self.fuse_fc1 = os.environ.get("FEDMI_LENET_FUSE_FC1", "1") == "1"
-        self.engine.set_fuse_fc1(self.fuse_fc1)
-        # K1 + K2 in one launch (FC-head weight prefetch overlapped with the conv stack)
-        self.engine.set_fuse_head(os.environ.get("FEDMI_LENET_FUSE_HEAD", "1") == "1")
-        # K3 + K4 in one launch (flag hand-off to SGD workgroups): opt-in -- measured 15.0 us vs 10.4 + 4.9,
-        # the conv-param slab combine then trails the slowest sample (profiles/r2_lenet/experiments.md)
-        self.engine.set_fuse_sgd(os.environ.get("FEDMI_LENET_FUSE_SGD", "0") == "1")
+        self._configure_engine()
         self._views = ordered_views(self.params, LENET_SPEC)
         if init_state is None:
             torch.manual_seed(cfg.seed)
@@ -147,8 +142,20 @@ class LeNetNativeTrainer(LocalTrainer):
                           n_train=len(self.train_set))
         self.engine = self._nat.LeNetEngine(self._bufs, self.cfg.lr, self.cfg.momentum, self.cfg.weight_decay,
                                             self.cfg.seed & 0xFFFFFFFF, bool(self.cfg.augment))
-        self.engine.set_fuse_fc1(self.fuse_fc1)
+        self._configure_engine()
         self._starts, self._sizes = [], []
+
+    def _configure_engine(self) -> None:
+        """Launch-schedule switches of a (re)built engine binding (env overrides for A/B runs)."""
+        self.engine.set_fuse_fc1(self.fuse_fc1)
+        # K1 + K2 in one launch (FC-head weight prefetch overlapped with the conv stack)
+        self.engine.set_fuse_head(os.environ.get("FEDMI_LENET_FUSE_HEAD", "1") == "1")
+        # K3 + K4 in one launch (flag hand-off to SGD workgroups): opt-in -- measured 15.0 us vs 10.4 + 4.9,
+        # the conv-param slab combine then trails the slowest sample (profiles/r2_lenet/experiments.md)
+        self.engine.set_fuse_sgd(os.environ.get("FEDMI_LENET_FUSE_SGD", "0") == "1")
+        # FEDMI_LENET_PATH=sample: per-sample step kernel + batched FC-gradient GEMM/SGD kernel (2 launches)
+        # instead of K12 -> K3 -> K4 (profiles/r2_lenet/experiments.md: not yet faster, so opt-in)
+        self.engine.set_sample_path(os.environ.get("FEDMI_LENET_PATH", "head") == "sample")
 
     # ---- compute ----------------------------------------------------------------
     def train_epoch(self) -> None:

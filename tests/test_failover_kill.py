@@ -37,7 +37,9 @@ def _report(**rec):
     path = os.environ.get("FEDMI_FAILOVER_REPORT")
     if path:
         import json
+        from pathlib import Path
 
+        Path(path).parent.mkdir(parents=True, exist_ok=True)
         with open(path, "a") as f:
             f.write(json.dumps(rec) + "\n")
 
@@ -96,8 +98,12 @@ def _primary_sigkill_and_recover(tmp_path, device):
         assert takeover < 5.0, takeover                       # watchdog 1 s (reference: 13.7 s)
         # the acting backup resumes from the replicated round (not round 0, quirk A8) and keeps going
         first = wait_for(lambda: [r for r in _rounds(tmp_path / "backup.jsonl") if r["ts"] > t_kill], timeout=120)[0]
-        # (replication is asynchronous and coalesced: the replica may trail by a few fast rounds)
-        assert max(1, r_dead - 10) <= first["round"] <= r_dead + 2, (first["round"], r_dead)
+        # Replication is asynchronous and coalesced (fetch every 50 ms), so the replica trails the dead
+        # primary by a bounded TIME, not a bounded round count: GPU rounds of this drill take a few ms.
+        # It must hold at least what the primary had finished 1 s before the kill.
+        prim = _rounds(tmp_path / "primary.jsonl")
+        r_floor = max([r["round"] for r in prim if r["ts"] <= t_kill - 1.0] + [1])
+        assert r_floor <= first["round"] <= r_dead + 2, (first["round"], r_floor, r_dead)
         wait_for(lambda: max([r["round"] for r in _rounds(tmp_path / "backup.jsonl")] + [0]) >= r_dead + 2,
                  timeout=120)
         # ---- the primary process is restarted: the backup demotes itself cleanly (quirk A2)
@@ -107,7 +113,7 @@ def _primary_sigkill_and_recover(tmp_path, device):
         wait_for(lambda: [r for r in read_jsonl(tmp_path / "backup.jsonl") if r.get("event") == "demoted"],
                  timeout=60)
         r2 = wait_for(lambda: _rounds(tmp_path / "primary2.jsonl"), timeout=120)
-        assert r2[0]["round"] >= r_dead - 10                 # resumed from Primary/optimizedModel.pth's epoch
+        assert r2[0]["round"] >= r_floor                     # resumed from Primary/optimizedModel.pth's epoch
         assert backup.poll() is None                         # the demoted backup is alive and serving
         wait_heartbeat(f"127.0.0.1:{bport}", timeout=10)
         demoted = [r for r in read_jsonl(tmp_path / "backup.jsonl") if r.get("event") == "demoted"][0]

@@ -357,6 +357,7 @@ def test_fused_bwd_sgd_matches_separate_kernels(env, use_graph):
     nat, dev, ds, ref, tr = env
     starts, sizes = [0, 128, 384, 896], [128, 128, 33, 80]
     res = []
+    tr.engine.set_sample_path(False)
     for fuse in (False, True):
         tr.engine.set_fuse_head(True)
         tr.engine.set_fuse_sgd(fuse)
@@ -379,6 +380,7 @@ def test_fused_bwd_sgd_matches_separate_kernels(env, use_graph):
     assert s0.count == s1.count == sum(sizes) and s0.correct == s1.correct
     assert abs(s0.loss_sum - s1.loss_sum) <= 1e-4 * abs(s0.loss_sum)
     assert rel(p1, p0) < 1e-5 and rel(m1, m0) < 1e-5   # only the LDS-atomic order of K3's bias sums differs
+    tr.engine.set_fuse_sgd(False)
 
 
 @pytest.mark.parametrize("use_graph", [True, False], ids=["graph", "eager"])
@@ -387,6 +389,7 @@ def test_fused_fwd_head_matches_separate_kernels(env, use_graph):
     nat, dev, ds, ref, tr = env
     starts, sizes = [0, 128, 384, 896], [128, 128, 33, 80]      # full and partial batches
     res = []
+    tr.engine.set_sample_path(False)
     for fuse in (False, True):
         tr.engine.set_fuse_head(fuse)
         tr.load_state_dict(ref.state_dict())
@@ -404,6 +407,72 @@ def test_fused_fwd_head_matches_separate_kernels(env, use_graph):
     assert abs(s0.loss_sum - s1.loss_sum) <= 1e-4 * abs(s0.loss_sum)
     assert rel(p1, p0) < 1e-5          # only the LDS-atomic order of K3's bias sums differs
     tr.engine.set_fuse_head(True)
+    tr.cfg.use_graph = True
+    tr.load_state_dict(ref.state_dict())
+    tr.mom.zero_()
+
+
+@pytest.mark.parametrize("start,nb", [(0, 128), (896, 80), (128, 33)])
+def test_sample_step_gradients_match_head_kernels(env, start, nb):
+    """KS1 + KS2 (one workgroup per sample, batched FC-gradient GEMMs) compute the same gradients as
+    K1 + K2 + K3 (per-tensor rel. L2 at the bf16 level: the FC GEMVs sum in a different order and a
+    bf16 rounding of an intermediate may land one ulp apart), the same loss and accuracy."""
+    nat, dev, ds, ref, tr = env
+    tr.load_state_dict(ref.state_dict())
+    tr.round_ctr.zero_()
+    g_head, st_head = _run_grad(nat, tr, start, nb, True, fused=True)
+    lr, wd = tr.cfg.lr, tr.cfg.weight_decay
+    tr.engine.set_sample_path(True)
+    tr.load_state_dict(ref.state_dict())
+    tr.mom.zero_()
+    tr.stats.zero_()
+    p0 = tr.params.clone()
+    tr.train_step(start, nb)                    # momentum buffer 0: p = p0 - lr * (g + wd * p0)
+    torch.cuda.synchronize()
+    g = (p0.double() - tr.params.double()) / lr - wd * p0.double()
+    off = 0
+    for name, shape in LENET_SPEC:
+        k = int(np.prod(shape))
+        e = rel(g[off:off + k], g_head[off:off + k])
+        assert e < 1e-2, f"{name}: rel err {e:.3e}"
+        off += k
+    st, sh = tr.stats[0].cpu(), st_head.cpu()
+    assert int(st[2]) == nb
+    assert abs(int(st[1]) - int(sh[1])) <= 1
+    ls, lh = float(st[0:1].view(torch.float32)), float(sh[0:1].view(torch.float32))
+    assert abs(ls - lh) < 1e-3 * max(1.0, abs(lh))
+    assert rel(tr.mom.double(), g + wd * p0.double()) < 1e-4   # g is recovered from fp32 params
+    tr.engine.set_sample_path(False)
+    tr.load_state_dict(ref.state_dict())
+    tr.mom.zero_()
+
+
+@pytest.mark.parametrize("use_graph", [True, False], ids=["graph", "eager"])
+def test_sample_path_trains_like_head_path(env, use_graph):
+    """Two epochs of full and partial batches: the per-sample path and K12 -> K3 -> K4 stay together."""
+    nat, dev, ds, ref, tr = env
+    starts, sizes = [0, 128, 384, 896], [128, 128, 33, 80]
+    res = []
+    for sample in (False, True):
+        tr.engine.set_sample_path(sample)
+        tr.load_state_dict(ref.state_dict())
+        tr.mom.zero_()
+        tr.round_ctr.zero_()
+        tr.stats.zero_()
+        tr.round_idx = 0
+        tr.cfg.use_graph = use_graph
+        tr.set_schedule(starts, sizes)
+        for _ in range(2):
+            tr.train_epoch()
+        torch.cuda.synchronize()
+        res.append((tr.params.clone(), tr.train_stats(), int(tr.round_ctr[0])))
+    (p0, s0, r0), (p1, s1, r1) = res
+    init = torch.cat([v.detach().reshape(-1).float() for v in ref.state_dict().values()])
+    assert r0 == r1 == 2
+    assert s0.count == s1.count == sum(sizes) and abs(s0.correct - s1.correct) <= 2
+    assert abs(s0.loss_sum - s1.loss_sum) <= 2e-3 * abs(s0.loss_sum)
+    assert rel(p1 - init, p0 - init) < 5e-2      # 8 SGD steps of bf16-level differences
+    tr.engine.set_sample_path(False)
     tr.cfg.use_graph = True
     tr.load_state_dict(ref.state_dict())
     tr.mom.zero_()

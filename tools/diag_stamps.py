@@ -35,6 +35,7 @@ def main():
     dev = torch.device("cuda", 0)
     ds = make_dataset("synthetic-cifar10", device=dev, n_train=4096, n_test=1024)
     tr = LeNetNativeTrainer(ds, dev, TrainerConfig(seed=1))
+    nat.set_ks1_diag(int(os.environ.get("FEDMI_KS1_DIAG", "0")))   # staging probes (sample path)
     for i in range(8):
         tr.train_step(128 * i, 128)
     torch.cuda.synchronize()
@@ -42,8 +43,35 @@ def main():
     tr.train_step(0, 128)
     torch.cuda.synchronize()
     st = np.frombuffer(nat.read_stamps(True), dtype=np.uint64).reshape(nat.STAMP_SHAPE).astype(np.int64)
-    for k, (name, phases) in NAMES.items():
-        a = st[k, :NWG[k], :len(phases) + 1]
+    if tr.engine.sample_path():
+        # KS1: forward slots 0..6 under kernel 0, its backward slots 2..5 under kernel 2; KS2 under kernel 3
+        ks1 = np.concatenate([st[0, :128, :7], st[2, :128, 2:6]], axis=1)
+        phases = ["stage+aug", "conv1", "pool1", "conv2", "pool2+zero+shift", "fc fwd+bwd", "dY2 scatter",
+                  "c2 wgrad+dgrad", "c1 wgrad", "slab store"]
+        a = ks1[ks1[:, 0] > 0]
+        d = np.diff(a, axis=1)
+        tot = a[:, -1] - a[:, 0]
+        print(f"sample    wgs={len(a):4d} total med {np.median(tot):8.0f} max {tot.max():8.0f} cyc")
+        for j, ph in enumerate(phases):
+            print(f"    {ph:16s} med {np.median(d[:, j]):8.0f}  max {d[:, j].max():8.0f}")
+        f = st[1, :128]
+        f = f[(f[:, 0] > 0)]
+        k0 = st[0, :128]
+        k0 = k0[k0[:, 0] > 0]
+        if len(f) and len(k0):
+            print(f"    stage loads landed med {np.median(k0[:len(f), 0] * 0 + f[:, 7] - k0[:len(f), 0]):8.0f}")
+            fcn = ["fc1+h1T", "fc2", "fc3|shift build", "CE", "dH2", "dH1"]
+            prev = k0[:len(f), 5]
+            for j, nm in enumerate(fcn):
+                print(f"    fc.{nm:14s} med {np.median(f[:, j] - prev):8.0f}")
+                prev = f[:, j]
+            print(f"    fc.dX          med {np.median(k0[:len(f), 6] - prev):8.0f}")
+        names = {3: ("sgd2", ["all"])}
+        nwg = {3: 249}
+    else:
+        names, nwg = NAMES, NWG
+    for k, (name, phases) in names.items():
+        a = st[k, :nwg[k], :len(phases) + 1]
         a = a[a[:, 0] > 0]
         d = np.diff(a, axis=1)
         tot = a[:, -1] - a[:, 0]
@@ -52,6 +80,8 @@ def main():
               f"start spread {starts.max():7d} cyc")
         for j, ph in enumerate(phases):
             print(f"    {ph:16s} med {np.median(d[:, j]):8.0f}  max {d[:, j].max():8.0f}")
+    if tr.engine.sample_path():
+        return
     # fused K12: split the FC head's first phase at the hand-off (slot 7 = flags seen)
     f = st[1, :NWG[1]]
     f = f[(f[:, 0] > 0) & (f[:, 7] > 0)]
