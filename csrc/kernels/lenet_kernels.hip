@@ -824,7 +824,7 @@ FEDMI_DEV void bwd_zero(const BwdLds& L) {
 
 // each augmented pixel / pooled value is computed once and stored into its 5
 // column-shifted copies: copy s holds element x at column x - s
-FEDMI_DEV void bwd_build_shifted(const BwdLds& L, const Aug& a, int tid = threadIdx.x, int nthr = NT_CONV) {
+FEDMI_DEV void bwd_build_shifted_img(const BwdLds& L, const Aug& a, int tid, int nthr) {
   for (int e = tid; e < IMG_BYTES; e += nthr) {
     const int c = e >> 10, y = (e >> 5) & 31, x = e & 31;
     const bf16 v = (bf16)aug_pixel(L.raw, a, c, y, x);
@@ -833,6 +833,8 @@ FEDMI_DEV void bwd_build_shifted(const BwdLds& L, const Aug& a, int tid = thread
     for (int sh = 0; sh < 5; ++sh)
       if (x >= sh) row[sh * BW_XS_S - sh] = v;
   }
+}
+FEDMI_DEV void bwd_build_shifted_p1(const BwdLds& L, int tid, int nthr) {
   for (int e = tid; e < NP1; e += nthr) {
     const int c = e / 196, rem = e - c * 196, y = rem / P1, x = rem - y * P1;
     const bf16 v = L.p1r[e];
@@ -841,6 +843,10 @@ FEDMI_DEV void bwd_build_shifted(const BwdLds& L, const Aug& a, int tid = thread
     for (int sh = 0; sh < 5; ++sh)
       if (x >= sh) row[sh * (6 * 14 * 16) - sh] = v;
   }
+}
+FEDMI_DEV void bwd_build_shifted(const BwdLds& L, const Aug& a) {
+  bwd_build_shifted_img(L, a, threadIdx.x, NT_CONV);
+  bwd_build_shifted_p1(L, threadIdx.x, NT_CONV);
 }
 
 // d(pool2) -> conv2 out-grad images + conv2 bias sums, then conv2 wgrad + dgrad, conv1 wgrad,
@@ -1410,37 +1416,40 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
     acc = sum8lanes(acc);
     if (fq == 0) fcs[SF_Z + fn] = fn < NCLS ? acc + fb3 : 0.f;
   } else {
-    bwd_build_shifted(L, a, tid - 128, NT_CONV - 128);
+    bwd_build_shifted_img(L, a, tid - 128, NT_CONV - 128);
   }
   __syncthreads();
   FEDMI_STAMP(1, 2);
-  // ---- cross-entropy (mean over the batch nb), accuracy, dZ3 (one lane: ten classes)
-  if (tid == 0) {
-    float z[NCLS];
+  // ---- cross-entropy (mean over the batch nb), accuracy, dZ3: lanes 0..15 of wave 0 hold one
+  //      class each (max / sum by xor shuffles); waves 1..15 build the pool1 shifted copies
+  if (wave == 0) {
+    const int n = lane & 15;
+    const float zn = n < NCLS ? fcs[SF_Z + n] : -INFINITY;
+    float mx = zn;
 #pragma unroll
-    for (int n = 0; n < NCLS; ++n) z[n] = fcs[SF_Z + n];
-    float mx = z[0]; int am = 0;
+    for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    // first index reaching the max (torch argmax semantics)
+    float cand = (zn == mx) ? (float)n : 16.f;
 #pragma unroll
-    for (int n = 1; n < NCLS; ++n) if (z[n] > mx) { mx = z[n]; am = n; }
-    float se = 0.f;
+    for (int o = 1; o < 16; o <<= 1) cand = fminf(cand, __shfl_xor(cand, o, 64));
+    float se = n < NCLS ? __expf(zn - mx) : 0.f;
 #pragma unroll
-    for (int n = 0; n < NCLS; ++n) se += __expf(z[n] - mx);
+    for (int o = 1; o < 16; o <<= 1) se += __shfl_xor(se, o, 64);
     const float lse = mx + __logf(se);
     const int y = labels[s];
-    float zy = 0.f;
-#pragma unroll
-    for (int n = 0; n < NCLS; ++n) zy = (n == y) ? z[n] : zy;
-    reinterpret_cast<float*>(auxp + AUX_LOSS)[s] = lse - zy;
-    reinterpret_cast<float*>(auxp + AUX_CORR)[s] = (am == y) ? 1.f : 0.f;
-    const float inv = 1.f / (float)nb;
-    bf16* dz3t = reinterpret_cast<bf16*>(auxp + AUX_DZ3T);
-#pragma unroll
-    for (int n = 0; n < 16; ++n) {
-      const float d = n < NCLS ? (__expf(z[n] - lse) - (n == y ? 1.f : 0.f)) * inv : 0.f;
+    const float zy = __shfl(zn, y, 64);
+    const float d = n < NCLS ? (__expf(zn - lse) - (n == y ? 1.f : 0.f)) * (1.f / (float)nb) : 0.f;
+    if (lane < 16) {
       fcs[SF_DZ3 + n] = bfr(d);
-      dz3t[(size_t)n * MAX_TRAIN_BATCH + s] = (bf16)d;
+      reinterpret_cast<bf16*>(auxp + AUX_DZ3T)[(size_t)n * MAX_TRAIN_BATCH + s] = (bf16)d;
       if (n < NCLS) fcb[204 + n] = d;
     }
+    if (lane == 0) {
+      reinterpret_cast<float*>(auxp + AUX_LOSS)[s] = lse - zy;
+      reinterpret_cast<float*>(auxp + AUX_CORR)[s] = ((int)cand == y) ? 1.f : 0.f;
+    }
+  } else {
+    bwd_build_shifted_p1(L, tid - 64, NT_CONV - 64);
   }
   __syncthreads();
   FEDMI_STAMP(1, 3);

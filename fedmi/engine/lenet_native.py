@@ -153,9 +153,9 @@ class LeNetNativeTrainer(LocalTrainer):
         # K3 + K4 in one launch (flag hand-off to SGD workgroups): opt-in -- measured 15.0 us vs 10.4 + 4.9,
         # the conv-param slab combine then trails the slowest sample (profiles/r2_lenet/experiments.md)
         self.engine.set_fuse_sgd(os.environ.get("FEDMI_LENET_FUSE_SGD", "0") == "1")
-        # FEDMI_LENET_PATH=sample: per-sample step kernel + batched FC-gradient GEMM/SGD kernel (2 launches)
-        # instead of K12 -> K3 -> K4 (profiles/r2_lenet/experiments.md: not yet faster, so opt-in)
-        self.engine.set_sample_path(os.environ.get("FEDMI_LENET_PATH", "head") == "sample")
+        # default: per-sample step kernel + batched FC-gradient GEMM/SGD kernel (2 launches, 10.45 vs
+        # 12.95 ms per round, profiles/r2_lenet/experiments.md); FEDMI_LENET_PATH=head: K12 -> K3 -> K4
+        self.engine.set_sample_path(os.environ.get("FEDMI_LENET_PATH", "sample") == "sample")
 
     # ---- compute ----------------------------------------------------------------
     def train_epoch(self) -> None:

@@ -381,6 +381,7 @@ def test_fused_bwd_sgd_matches_separate_kernels(env, use_graph):
     assert abs(s0.loss_sum - s1.loss_sum) <= 1e-4 * abs(s0.loss_sum)
     assert rel(p1, p0) < 1e-5 and rel(m1, m0) < 1e-5   # only the LDS-atomic order of K3's bias sums differs
     tr.engine.set_fuse_sgd(False)
+    tr.engine.set_sample_path(True)
 
 
 @pytest.mark.parametrize("use_graph", [True, False], ids=["graph", "eager"])
@@ -407,6 +408,7 @@ def test_fused_fwd_head_matches_separate_kernels(env, use_graph):
     assert abs(s0.loss_sum - s1.loss_sum) <= 1e-4 * abs(s0.loss_sum)
     assert rel(p1, p0) < 1e-5          # only the LDS-atomic order of K3's bias sums differs
     tr.engine.set_fuse_head(True)
+    tr.engine.set_sample_path(True)
     tr.cfg.use_graph = True
     tr.load_state_dict(ref.state_dict())
     tr.mom.zero_()
@@ -442,7 +444,6 @@ def test_sample_step_gradients_match_head_kernels(env, start, nb):
     ls, lh = float(st[0:1].view(torch.float32)), float(sh[0:1].view(torch.float32))
     assert abs(ls - lh) < 1e-3 * max(1.0, abs(lh))
     assert rel(tr.mom.double(), g + wd * p0.double()) < 1e-4   # g is recovered from fp32 params
-    tr.engine.set_sample_path(False)
     tr.load_state_dict(ref.state_dict())
     tr.mom.zero_()
 
@@ -472,7 +473,7 @@ def test_sample_path_trains_like_head_path(env, use_graph):
     assert s0.count == s1.count == sum(sizes) and abs(s0.correct - s1.correct) <= 2
     assert abs(s0.loss_sum - s1.loss_sum) <= 2e-3 * abs(s0.loss_sum)
     assert rel(p1 - init, p0 - init) < 5e-2      # 8 SGD steps of bf16-level differences
-    tr.engine.set_sample_path(False)
+    tr.engine.set_sample_path(True)
     tr.cfg.use_graph = True
     tr.load_state_dict(ref.state_dict())
     tr.mom.zero_()
