@@ -858,23 +858,32 @@ FEDMI_DEV void bwd_main(const BwdLds& L, float* __restrict__ slab, int* __restri
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
   const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
   float* db = L.db;
-  for (int f = tid; f < F0; f += NT_CONV) {
-    const int o = f / 25, rem = f - o * 25, py = rem / P2, px = rem - py * P2;
-    const int am = L.am2s[f];
-    const int y = 2 * py + (am >> 1), x = 2 * px + (am & 1);
-    const float g = L.dxs[f];
-    const bf16 gb = (bf16)g;
-    L.dY2w[o * 160 + y * 16 + x] = gb;
-    L.dY2c[((y + 4) * 18 + (x + 4)) * BW_DY2S + o] = gb;
-    atomicAdd(&db[o], g);
+  // thread = (channel o, slot r < 32): the 25 positions of a channel sit in 32 consecutive lanes, so
+  // the conv2 bias grad is a shuffle reduction (400 LDS atomics onto 16 addresses took ~2k cycles)
+  if (tid < C2 * 32) {
+    const int o = tid >> 5, rem = tid & 31;
+    float g = 0.f;
+    if (rem < 25) {
+      const int f = o * 25 + rem, py = rem / P2, px = rem - py * P2;
+      const int am = L.am2s[f];
+      const int y = 2 * py + (am >> 1), x = 2 * px + (am & 1);
+      g = L.dxs[f];
+      const bf16 gb = (bf16)g;
+      L.dY2w[o * 160 + y * 16 + x] = gb;
+      L.dY2c[((y + 4) * 18 + (x + 4)) * BW_DY2S + o] = gb;
+    }
+#pragma unroll
+    for (int w = 1; w < 32; w <<= 1) g += __shfl_xor(g, w, 64);
+    if (rem == 0) db[o] = g;
   }
   __syncthreads();
   FEDMI_STAMP(sk, 2);
 
   // ---- conv2 wgrad: dW2[o][k'] = sum_p dY2[o][p] * im2col(pool1)[p][k']
   //      M = 16 (o), N = 150 (10 tiles), K = 160 (p' = i*16 + j, 5 steps)
-  // task map over 16 waves: dgrad tile t -> wave t (t < 13), wgrad tile t -> wave (13 + t) % 16
-  for (int t = (wave + 3) & 15; t < 10; t += NW_CONV) {
+  // task map over 16 waves: dgrad tiles (2w, 2w+1) -> wave w < 7 (one read of each weight fragment
+  // feeds two tiles), wgrad tiles -> waves 7..15 (wave 7 takes tiles 0 and 9)
+  for (int t = wave - 7; t >= 0 && t < 10; t += 9) {
     const int kk = t * 16 + n16;
     const int kc = kk < 150 ? kk : 0;
     const int c = kc / 25, rs = kc - c * 25, r = rs / 5, sc = rs - r * 5;
@@ -900,29 +909,39 @@ FEDMI_DEV void bwd_main(const BwdLds& L, float* __restrict__ slab, int* __restri
     const int r = g / 5, sc = g - r * 5;
     koff[ks] = g < 25 ? (-r * 18 - sc) * BW_DY2S + (G & 1) * 8 : 0;   // pad group: weight 0, any in-bounds read
   }
-  for (int t = wave; t < 13; t += NW_CONV) {
-    int pos = t * 16 + n16;
-    if (pos >= 196) pos = 0;
-    const int y = pos / P1, x = pos - y * P1;
-    const bf16* gb = L.dY2c + ((y + 4) * 18 + (x + 4)) * BW_DY2S;
+  if (wave < 7) {
+    const int ta = 2 * wave, tb = 2 * wave + 1;          // tb == 13 (wave 6) is a duplicate, not stored
+    int pa = ta * 16 + n16, pb = tb * 16 + n16;
+    if (pa >= 196) pa = 0;
+    if (pb >= 196) pb = 0;
+    const bf16* ga = L.dY2c + (((pa / P1) + 4) * 18 + (pa % P1 + 4)) * BW_DY2S;
+    const bf16* gbb = L.dY2c + (((pb / P1) + 4) * 18 + (pb % P1 + 4)) * BW_DY2S;
     const bf16* wb = L.wdg + min(n16, C1) * BW_WDGS + kq;     // rows >= 6 are zero: share row 6 (broadcast)
-    f32x4 acc = zero4();
+    f32x4 acc[2] = {zero4(), zero4()};
 #pragma unroll
-    for (int ks = 0; ks < 13; ++ks) acc = mfma16(ld8(gb + koff[ks]), ld8(wb + ks * 32), acc);
+    for (int ks = 0; ks < 13; ++ks) {
+      const bf16x8 w = ld8(wb + ks * 32);
+      acc[0] = mfma16(ld8(ga + koff[ks]), w, acc[0]);
+      acc[1] = mfma16(ld8(gbb + koff[ks]), w, acc[1]);
+    }
     if (n16 < C1) {
       const int c = n16;
       float csum = 0.f;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int p = t * 16 + rq + rr;
-        if (p < 196) {
-          const int py = p / P1, px = p - py * P1;
-          const float pooled = (float)L.p1r[c * 196 + p];
-          const float g = pooled > 0.f ? acc[rr] : 0.f;
-          const int am = L.am1s[c * 196 + p];
-          const int yy = 2 * py + (am >> 1), xx = 2 * px + (am & 1);
-          L.dY1[c * BW_DY1S + yy * 32 + xx] = (bf16)g;
-          csum += g;
+      for (int h = 0; h < 2; ++h) {
+        const int t = h ? tb : ta;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int p = t * 16 + rq + rr;
+          if (p < 196) {
+            const int py = p / P1, px = p - py * P1;
+            const float pooled = (float)L.p1r[c * 196 + p];
+            const float g = pooled > 0.f ? acc[h][rr] : 0.f;
+            const int am = L.am1s[c * 196 + p];
+            const int yy = 2 * py + (am >> 1), xx = 2 * px + (am & 1);
+            L.dY1[c * BW_DY1S + yy * 32 + xx] = (bf16)g;
+            csum += g;
+          }
         }
       }
       atomicAdd(&db[16 + c], csum);
@@ -1280,12 +1299,11 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
   }
   // fc1 weight chunks of this thread (row n = tid/8, k = q*8 + 64 i): in flight through pool1..pool2
   const int fn = tid >> 3, fq = tid & 7;
+  // (every weight load below is unconditional from a clamped address and only its USE is guarded:
+  //  a select between a loaded value and zero made the compiler wait for the load on the spot)
   bf16x8 w1v[7];
 #pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const int k = fq * 8 + 64 * i;
-    w1v[i] = k < F0P ? ld8(pk + PK_FC1 + fn * F0P + k) : zero8();
-  }
+  for (int i = 0; i < 7; ++i) w1v[i] = ld8(pk + PK_FC1 + fn * F0P + min(fq * 8 + 64 * i, F0P - 8));
   __syncthreads();
   FEDMI_STAMP(0, 2);
 
@@ -1351,8 +1369,9 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     w2v[i] = ld8(pk + PK_FC2 + n2 * 128 + fq * 8 + 64 * i);
-    w3v[i] = (fq * 8 + 64 * i < 96) ? ld8(pk + PK_FC3 + n3 * 96 + fq * 8 + 64 * i) : zero8();
+    w3v[i] = ld8(pk + PK_FC3 + n3 * 96 + min(fq * 8 + 64 * i, 88));
   }
+  const int label = labels[s];
   const float fb1 = params[P_F1B + min(fn, F1 - 1)];
   const float fb2 = params[P_F2B + min(fn, F2 - 1)];
   const float fb3 = params[P_F3B + min(fn, NCLS - 1)];
@@ -1382,13 +1401,13 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
   const int kx = tid >> 1, hx = tid & 1;
   bf16x8 w1t[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) w1t[i] = kx < F0 ? ld8(pk + PK_FC1T + kx * 128 + hx * 8 + 16 * i) : zero8();
+  for (int i = 0; i < 8; ++i) w1t[i] = ld8(pk + PK_FC1T + min(kx, F0 - 1) * 128 + hx * 8 + 16 * i);
   bf16x8 w2t[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) w2t[i] = (fq * 8 + 64 * i < 96) ? ld8(pk + PK_FC2T + fn * 96 + fq * 8 + 64 * i) : zero8();
+  for (int i = 0; i < 2; ++i) w2t[i] = ld8(pk + PK_FC2T + fn * 96 + min(fq * 8 + 64 * i, 88));
   bf16x8 w3t[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) w3t[i] = tid < 96 ? ld8(pk + PK_FC3T + tid * 32 + 8 * i) : zero8();
+  for (int i = 0; i < 2; ++i) w3t[i] = ld8(pk + PK_FC3T + min(tid, 95) * 32 + 8 * i);
   __syncthreads();
 
   FEDMI_STAMP(1, 0);
@@ -1436,7 +1455,7 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) se += __shfl_xor(se, o, 64);
     const float lse = mx + __logf(se);
-    const int y = labels[s];
+    const int y = label;
     const float zy = __shfl(zn, y, 64);
     const float d = n < NCLS ? (__expf(zn - lse) - (n == y ? 1.f : 0.f)) * (1.f / (float)nb) : 0.f;
     if (lane < 16) {
