@@ -182,14 +182,16 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16* __restrict__ 
   }
 }
 
-// Partial weight gradients: block b sums a contiguous range of output pixels
-// for ALL channel groups (thread -> fixed group), writes ws[b][C][RS].
+// Partial weight gradients: block (b, chunk) sums a contiguous range of output pixels for
+// the VCB channel groups of its chunk (thread -> fixed group), writes ws[b][C][RS] for those
+// channels.  Wide layers are split into channel chunks so that small-spatial / many-channel
+// layers still launch ~100+ workgroups (round 1: 8 workgroups for MobileNet's 2x2x1024 layer).
 template <int RS>
 __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
-                                                       float* __restrict__ ws, DwGeom g, int pix_per_block) {
-  const int VC = g.C >> 3;   // host: blockDim.x % VC == 0
+                                                       float* __restrict__ ws, DwGeom g, int pix_per_block, int VCB) {
+  const int VC = VCB;        // channel groups of this block's chunk; host: blockDim.x % VCB == 0
   const int cg = threadIdx.x % VC, lane_pix = threadIdx.x / VC, pstep = blockDim.x / VC;
-  const int c0 = cg * 8;
+  const int c0 = blockIdx.y * VCB * 8 + cg * 8;
   const long npix = (long)g.N * g.P * g.Q;
   const long pb = (long)blockIdx.x * pix_per_block, pe = std::min<long>(npix, pb + pix_per_block);
   float acc[RS][8];
@@ -222,11 +224,11 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = acc[t][j];
     __syncthreads();
-    for (int c = threadIdx.x; c < g.C; c += blockDim.x) {
+    for (int c = threadIdx.x; c < VCB * 8; c += blockDim.x) {
       const int grp = c >> 3, j = c & 7;
       float sum = 0.f;
       for (int tt = grp; tt < (int)blockDim.x; tt += VC) sum += red[tt][j];
-      out[(long)c * RS + t] = sum;
+      out[(long)(blockIdx.y * VCB * 8 + c) * RS + t] = sum;
     }
     __syncthreads();
   }
@@ -300,9 +302,17 @@ void launch_dw_dgrad(hipStream_t st, const DwShape& s, const bf16* dy, const flo
                      dx, g);
 }
 
+// channel groups per wgrad workgroup (<= 32: >= 8 pixel lanes) and pixel blocks (>= 2 pixels per lane)
+static int dw_wgrad_vcb(const DwGeom& g) {   // largest divisor of C/8 that is <= 32
+  const int vc = g.C / 8;
+  for (int d = std::min(vc, 32); d > 1; --d)
+    if (vc % d == 0) return d;
+  return 1;
+}
 static int dw_wgrad_blocks(const DwGeom& g) {
   const long npix = (long)g.N * g.P * g.Q;
-  return (int)std::max<long>(1, std::min<long>(512, (npix + 63) / 64));
+  const int pstep = block_threads(dw_wgrad_vcb(g) * 8) / dw_wgrad_vcb(g);
+  return (int)std::max<long>(1, std::min<long>(512, (npix + 2 * pstep - 1) / (2 * pstep)));
 }
 
 long dw_wgrad_ws_floats(const DwShape& s) {
@@ -318,10 +328,12 @@ void launch_dw_wgrad(hipStream_t st, const DwShape& s, const bf16* x, const bf16
   if ((long)nblk * n > ws_floats) throw std::invalid_argument("dw_wgrad: workspace too small");
   const long npix = (long)g.N * g.P * g.Q;
   const int ppb = (int)((npix + nblk - 1) / nblk);
-  const int tb = block_threads(g.C);
-  if (g.R == 3) hipLaunchKernelGGL(dw_wgrad_kernel<9>, dim3(nblk), dim3(tb), 0, st, x, dy, ws, g, ppb);
-  else if (g.R == 5) hipLaunchKernelGGL(dw_wgrad_kernel<25>, dim3(nblk), dim3(tb), 0, st, x, dy, ws, g, ppb);
-  else hipLaunchKernelGGL(dw_wgrad_kernel<49>, dim3(nblk), dim3(tb), 0, st, x, dy, ws, g, ppb);
+  const int vcb = dw_wgrad_vcb(g);
+  const int tb = block_threads(vcb * 8);
+  const dim3 grid(nblk, (g.C / 8) / vcb);
+  if (g.R == 3) hipLaunchKernelGGL(dw_wgrad_kernel<9>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb);
+  else if (g.R == 5) hipLaunchKernelGGL(dw_wgrad_kernel<25>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb);
+  else hipLaunchKernelGGL(dw_wgrad_kernel<49>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb);
   hipLaunchKernelGGL(dw_wgrad_reduce, dim3((n + 15) / 16), dim3(256), 0, st, ws, nblk, n, dw, accumulate);
 }
 

@@ -246,7 +246,10 @@ def test_prep_input_matches_host_twin(gpu_device):
 
 
 DW_SHAPES = [(4, 32, 32, 32, 3, 1), (4, 32, 32, 64, 3, 2), (8, 4, 4, 1024, 3, 1), (2, 16, 16, 96, 5, 2),
-             (2, 8, 8, 16, 7, 1)]
+             (2, 8, 8, 16, 7, 1),
+             # batch-128 MobileNet / MobileNetV2 layers where the wgrad splits channels into chunks
+             # (C/8 = 128, 64, 120 -> chunks of 32, 32, 30; 48 -> 24)
+             (128, 2, 2, 1024, 3, 1), (128, 4, 4, 512, 3, 1), (128, 4, 4, 960, 3, 1), (128, 8, 8, 384, 3, 1)]
 
 
 @pytest.mark.parametrize("shape", DW_SHAPES, ids=[str(s) for s in DW_SHAPES])
