@@ -1147,9 +1147,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo(const bf16* __restrict__ 
 // DGRAD weight images for conv_tap: for each sub-pixel phase (stride 1: the
 // single phase r0 = s0 = 0, nr = R, ns = S, step 1)
 //   wd[c][i][j][o] = W[o][c][r0 + step*(nr-1-i)][s0 + step*(ns-1-j)]   (c < Cw, else 0)
-// One workgroup per (64 output channels o, 4 input channels c): the fp32 rows
-// W[o][c0:c0+4][:][:] are read contiguously into LDS, the image rows
-// wd[c][i][j][o0:o0+64] written as 128-B runs.
+// One workgroup per (64 output channels o, DP_CB input channels c): the fp32 rows
+// W[o][c0:c0+DP_CB][:][:] are read contiguously into LDS (one wave walks 16 rows, its
+// lanes stride the row: no per-element division), the image rows wd[c][i][j][o0:o0+64]
+// written as 128-B runs (lane = o).  Round 1's 4-channel blocks with per-element index
+// divisions took 45 us for ResNet-18's layer-3/4 weights.
+constexpr int DP_CB = 16;      // input channels per workgroup for R*S <= 9 (4 for larger filters: LDS)
 struct DPackEntry {
   const float* w;    // fp32 master [O][Cw][R][S]
   bf16* wd;          // image [Cpad][nr][ns][O]
@@ -1160,46 +1163,53 @@ constexpr int MAX_DPACK = 16;
 struct DPackTable {
   DPackEntry e[MAX_DPACK];
   int n;
+  int cb;            // input channels per workgroup (DP_CB or 4)
 };
 
 __global__ __launch_bounds__(256) void dgrad_pack_kernel(DPackTable t) {
-  // 64 o x (4 c x R*S) tile, LDS sized by the launch for the table's largest R*S (a fixed
-  // 7x7-sized tile held occupancy at 3 blocks per CU for the 3x3 convs); 8 loads in flight
-  // per thread before the LDS stores.
-  extern __shared__ float tile_[];
+  extern __shared__ float tile_[];   // [64][cb * R*S + 1], sized by the launch for the largest R*S
+  const int CB = t.cb;
   int k = 0;
   while (k + 1 < t.n && (int)blockIdx.x >= t.e[k + 1].blk0) ++k;
   const DPackEntry& p = t.e[k];
   const int b = blockIdx.x - p.blk0;
-  const int ncb = (p.Cpad + 3) / 4;
-  const int o0 = (b / ncb) * 64, c0 = (b % ncb) * 4;
+  const int ncb = (p.Cpad + CB - 1) / CB;
+  const int o0 = (b / ncb) * 64, c0 = (b % ncb) * CB;
   const int RS = p.R * p.S;
-  const int span = 4 * RS, ld = span + 1;
-  for (int e0 = threadIdx.x; e0 < 64 * span; e0 += 256 * 8) {
-    float v[8];
+  const int cw = max(0, min(CB, p.Cw - c0));               // real input channels of this block
+  const int span = CB * RS, ld = span + 1, live = cw * RS;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave w owns rows w, w+4, ..., w+60; 4 rows x 3 row chunks = 12 loads in flight per lane
+  for (int k0 = 0; k0 < 16; k0 += 4) {
+    for (int f0 = lane; f0 < span; f0 += 64 * 3) {
+      float v[4][3];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = e0 + 256 * u;
-      const int oi = e / span, f = e - oi * span;   // f = (c - c0) * RS + rs
-      const int o = o0 + oi, c = c0 + f / RS;
-      v[u] = (e < 64 * span && o < p.O && c < p.Cw) ? p.w[((long)o * p.Cw + c) * RS + (f % RS)] : 0.f;
-    }
+      for (int u = 0; u < 4; ++u) {
+        const int o = o0 + wave + 4 * (k0 + u);
+        const float* src = p.w + ((long)o * p.Cw + c0) * RS;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = e0 + 256 * u;
-      if (e < 64 * span) tile_[(e / span) * ld + e % span] = v[u];
+        for (int q = 0; q < 3; ++q) {
+          const int f = f0 + 64 * q;
+          v[u][q] = (o < p.O && f < live) ? src[f] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          if (f0 + 64 * q < span) tile_[(wave + 4 * (k0 + u)) * ld + f0 + 64 * q] = v[u][q];
     }
   }
   __syncthreads();
   const int taps = p.nr * p.ns;
-  for (int e = threadIdx.x; e < 4 * taps * 64; e += 256) {
-    const int oi = e & 63, rest = e >> 6;
-    const int ci = rest / taps, ij = rest - ci * taps;
+  const int o = o0 + lane;
+  for (int idx = wave; idx < CB * taps; idx += 4) {      // (ci, tap) per wave: scalar index math
+    const int ci = idx / taps, ij = idx - ci * taps;
     const int i = ij / p.ns, j = ij - i * p.ns;
-    const int c = c0 + ci, o = o0 + oi;
+    const int c = c0 + ci;
     if (c >= p.Cpad || o >= p.O) continue;
     const int r = p.r0 + p.step * (p.nr - 1 - i), sx = p.s0 + p.step * (p.ns - 1 - j);
-    p.wd[(((long)c * p.nr + i) * p.ns + j) * p.O + o] = (bf16)tile_[oi * ld + ci * RS + r * p.S + sx];
+    p.wd[(((long)c * p.nr + i) * p.ns + j) * p.O + o] = (bf16)tile_[lane * ld + ci * RS + r * p.S + sx];
   }
 }
 
@@ -1989,15 +1999,16 @@ void launch_dgrad_pack_multi(hipStream_t st, const DPackItem* items, int n) {
   for (size_t b = 0; b < all.size(); b += MAX_DPACK) {
     DPackTable t{};
     t.n = (int)std::min<size_t>(MAX_DPACK, all.size() - b);
+    int max_rs = 1;
+    for (int k = 0; k < t.n; ++k) max_rs = std::max(max_rs, all[b + k].R * all[b + k].S);
+    t.cb = max_rs <= 9 ? DP_CB : 4;
     int blk = 0;
     for (int k = 0; k < t.n; ++k) {
       t.e[k] = all[b + k];
       t.e[k].blk0 = blk;
-      blk += ((t.e[k].O + 63) / 64) * ((t.e[k].Cpad + 3) / 4);
+      blk += ((t.e[k].O + 63) / 64) * ((t.e[k].Cpad + t.cb - 1) / t.cb);
     }
-    int max_rs = 1;
-    for (int k = 0; k < t.n; ++k) max_rs = std::max(max_rs, t.e[k].R * t.e[k].S);
-    hipLaunchKernelGGL(dgrad_pack_kernel, dim3(blk), dim3(256), 64 * (4 * max_rs + 1) * sizeof(float), st, t);
+    hipLaunchKernelGGL(dgrad_pack_kernel, dim3(blk), dim3(256), 64 * (t.cb * max_rs + 1) * sizeof(float), st, t);
   }
 }
 

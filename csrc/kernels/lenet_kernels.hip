@@ -107,6 +107,7 @@ FEDMI_DEV void zero_lds(void* p, int bytes) {
 // ---------------------------------------------------------------------------
 // Body of one sample's workgroup; 'done_flag' (fused fwd+head launch): after act2/act2T
 // are stored, publish 'gen' there for the FC-head workgroups of the same launch.
+template <bool LDSW>
 FEDMI_DEV void conv_fwd_body(
     int s, const uint8_t* __restrict__ images, int sample_base, int nb,
     const bf16* __restrict__ pk, const float* __restrict__ params,
@@ -122,9 +123,17 @@ FEDMI_DEV void conv_fwd_body(
 {
   // LDS: raw u8 | x channels-last [36][40][4] bf16 | conv1 out f32 channels-last [784][8]
   //      | pool1 channels-last [14][14][8] bf16 | conv2 out f32 channels-last [100][16]
+  //      | conv1 / conv2 B images (rows padded to 136 / 232 bf16, staged once per workgroup: the
+  //        per-wave register loads of round 1 moved 8 waves x 11 KB of L2 traffic per sample)
+  //        (LDSW: the fused K12 launch, where the fewer workgroups make the LDS cost free; the
+  //        10 000-workgroup eval launch keeps register fragments: its occupancy is worth more)
   constexpr int XCL = 36 * 40 * 4, P1CL = 14 * 14 * 8;
-  constexpr int O_X = 3072, O_C1 = O_X + XCL * 2, O_P1 = O_C1 + NPOS1 * 8 * 4, O_C2 = O_P1 + P1CL * 2;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[O_C2 + C2 * NPOS2 * 4];
+  constexpr int O_X = 3072, O_C1 = O_X + XCL * 2, O_P1 = O_C1 + NPOS1 * 8 * 4, O_C2 = O_P1 + P1CL * 2,
+                O_W1 = O_C2 + C2 * NPOS2 * 4, O_W2 = O_W1 + 16 * 136 * 2,
+                O_END = LDSW ? O_W2 + 16 * 232 * 2 : O_W1;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[O_END];
+  bf16* w1c = reinterpret_cast<bf16*>(smem + O_W1);
+  bf16* w2c = reinterpret_cast<bf16*>(smem + O_W2);
   uint8_t* raw = smem;
   bf16* xcl = reinterpret_cast<bf16*>(smem + O_X);
   float* c1 = reinterpret_cast<float*>(smem + O_C1);
@@ -141,22 +150,49 @@ FEDMI_DEV void conv_fwd_body(
   if (zero_stats != nullptr && s == 0 && tid == 0) *zero_stats = Stats{0.f, 0, 0, 0};
   FEDMI_STAMP(0, 0);
 
-  load_raw(images + (size_t)gidx * IMG_BYTES, raw);
-  zero_lds(xcl, XCL * 2);   // channel 3 and the right/bottom pad stay zero
-  // conv1 AND conv2 weights (B fragments), biases and per-lane group offsets, all issued
-  // while the image lands: every later __syncthreads drains vmcnt, so a global load
-  // issued after conv1 (round 1) put its full latency on the conv1 -> pool1 barrier.
-  bf16x8 wb1[4], wb2[7];
+  // image (192) + conv1 (256) + conv2 (448) weight chunks of 16 B, <= 2 per thread, and every other
+  // global read of the kernel start, issued together while the x image is zeroed
+  bf16x8 wr1[4], wr2[7];
+  if constexpr (!LDSW) {
+    load_raw(images + (size_t)gidx * IMG_BYTES, raw);
+    zero_lds(xcl, XCL * 2);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) wr1[ks] = ld8(pk + PK_W1C + n16 * K1C + ks * 32 + kq);
+#pragma unroll
+    for (int ks = 0; ks < 7; ++ks) wr2[ks] = ld8(pk + PK_W2C + n16 * K2C + ks * 32 + kq);
+  } else {
+    constexpr int NI = IMG_BYTES / 16, NW1 = 16 * K1C / 8, NW2 = 16 * K2C / 8;
+    uint4 v[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * NT_FWD;
+      if (e < NI) v[u] = reinterpret_cast<const uint4*>(images + (size_t)gidx * IMG_BYTES)[e];
+      else if (e < NI + NW1) v[u] = reinterpret_cast<const uint4*>(pk + PK_W1C)[e - NI];
+      else if (e < NI + NW1 + NW2) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2C)[e - NI - NW1];
+    }
+    zero_lds(xcl, XCL * 2);   // channel 3 and the right/bottom pad stay zero
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * NT_FWD;
+      if (e < NI) {
+        reinterpret_cast<uint4*>(raw)[e] = v[u];
+      } else if (e < NI + NW1) {
+        const int w = e - NI;
+        reinterpret_cast<uint4*>(w1c + (w / (K1C / 8)) * 136)[w % (K1C / 8)] = v[u];
+      } else if (e < NI + NW1 + NW2) {
+        const int w = e - NI - NW1;
+        reinterpret_cast<uint4*>(w2c + (w / (K2C / 8)) * 232)[w % (K2C / 8)] = v[u];
+      }
+    }
+  }
   int go1[4], go2[7];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    wb1[ks] = ld8(pk + PK_W1C + n16 * K1C + ks * 32 + kq);
     const int g = ks * 4 + (lane >> 4);
     go1[ks] = g < 15 ? ((g / 3) * 40 + 2 * (g % 3)) * 4 : 0;
   }
 #pragma unroll
   for (int ks = 0; ks < 7; ++ks) {
-    wb2[ks] = ld8(pk + PK_W2C + n16 * K2C + ks * 32 + kq);
     const int g = ks * 4 + (lane >> 4);
     go2[ks] = g < 25 ? ((g / 5) * P1 + (g % 5)) * 8 : 0;
   }
@@ -164,6 +200,9 @@ FEDMI_DEV void conv_fwd_body(
   const float bias2 = params[P_C2B + n16];
   const Aug a = aug_params(augment, seed, round_ctr, gidx);
   __syncthreads();
+  bf16x8 wb1[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) wb1[ks] = LDSW ? ld8(w1c + n16 * 136 + ks * 32 + kq) : wr1[ks];
   for (int e = tid; e < IMG_BYTES; e += NT_FWD) {   // lanes walk x: raw reads broadcast within a dword
     const int c = e >> 10, y = (e >> 5) & 31, x = e & 31;
     xcl[(y * 40 + x) * 4 + c] = (bf16)aug_pixel(raw, a, c, y, x);
@@ -238,9 +277,10 @@ FEDMI_DEV void conv_fwd_body(
     if (pos >= NPOS2) pos = 0;
     const int py = pos / O2, px = pos - py * O2;
     const bf16* pb = p1cl + (py * P1 + px) * 8;
+    const bf16* wb = w2c + n16 * 232 + kq;
     f32x4 acc = zero4();
 #pragma unroll
-    for (int ks = 0; ks < 7; ++ks) acc = mfma16(ld8(pb + go2[ks]), wb2[ks], acc);
+    for (int ks = 0; ks < 7; ++ks) acc = mfma16(ld8(pb + go2[ks]), LDSW ? ld8(wb + ks * 32) : wr2[ks], acc);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int p = t * 16 + rq + r;
@@ -289,7 +329,7 @@ __global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
     bf16* __restrict__ act2, bf16* __restrict__ act2T, int tstride, bf16* __restrict__ pool1_out,
     uint8_t* __restrict__ am1_out, uint8_t* __restrict__ am2_out, Stats* __restrict__ zero_stats)
 {
-  conv_fwd_body(blockIdx.x, images, sample_base, nb, pk, params, seed, round_ctr, augment, act2, act2T, tstride,
+  conv_fwd_body<false>(blockIdx.x, images, sample_base, nb, pk, params, seed, round_ctr, augment, act2, act2T, tstride,
                 pool1_out, am1_out, am2_out, zero_stats, nullptr, 0);
 }
 
@@ -739,7 +779,7 @@ __global__ __launch_bounds__(NT_FWD) void lenet_fwd_head(
   const int gen = step_gen[0] + 1;
   if (bwd_gen && blockIdx.x == 0 && threadIdx.x == 0) bwd_gen[0] += 1;   // K34's flag generation (read only by K34)
   if ((int)blockIdx.x < nb) {
-    conv_fwd_body(blockIdx.x, images, sample_base, nb, pk, params, seed, round_ctr, augment, act2, act2T,
+    conv_fwd_body<true>(blockIdx.x, images, sample_base, nb, pk, params, seed, round_ctr, augment, act2, act2T,
                   MAX_TRAIN_BATCH, pool1_out, am1_out, am2_out, nullptr, done_flags, gen);
     return;
   }
