@@ -67,10 +67,11 @@ void launch_prep_input(hipStream_t, const uint8_t*, int, const int*, int, int, u
 void launch_sched_next(hipStream_t, const int*, int*, int*);
 void launch_bn_apply(hipStream_t, const bf16*, const BNDesc&, const bf16*, const BNDesc*, const bf16*, bf16*, int, int,
                      float, float, int, int, int);
-void launch_bn_bwd(hipStream_t, const BNBwdDesc&, float*, int, int, float*, long, int, int);
+void launch_bn_bwd(hipStream_t, const BNBwdDesc&, float*, int, int, float*, long, int, int, int);
 long bn_bwd_ws_floats(int, int);
+int bn_bwd_chain_reps(int);
 void launch_head(hipStream_t, const bf16*, const int*, int, const int*, int, int, int, int, const float*,
-                 const float*, float*, float*, bf16*, float*, float*, float*, int);
+                 const float*, float*, float*, bf16*, float*, float*, float*, int, float*, long);
 }  // namespace fedmi
 
 using namespace fedmi;
@@ -222,7 +223,7 @@ void fedmi_bind_cnn(py::module_& m) {
      py::arg("C"), py::arg("eps"), py::arg("mom"), py::arg("train"), py::arg("relu"), py::arg("ldy") = 0);
   m.def("bn_bwd_ws_floats", [](int M, int C) { return bn_bwd_ws_floats(M, C); });
   m.def("bn_bwd", [](uintptr_t st, const py::dict& d, uintptr_t red, int M, int C, uintptr_t ws, long ws_floats,
-                     int ldd, int ldy) {
+                     int ldd, int ldy, int chained) {
     BNBwdDesc b{P<const bf16>(dget(d, "dya")),     P<const bf16>(dget(d, "dyb")),     P<const bf16>(dget(d, "y")),
                 P<const bf16>(dget(d, "za")),      P<const float>(dget(d, "meanA")),  P<const float>(dget(d, "invA")),
                 P<const float>(dget(d, "gammaA")), P<float>(dget(d, "dgammaA")),      P<float>(dget(d, "dbetaA")),
@@ -231,16 +232,19 @@ void fedmi_bind_cnn(py::module_& m) {
                 P<float>(dget(d, "dbetaB")),       P<bf16>(dget(d, "dzb")),           P<bf16>(dget(d, "gout")),
                 P<float>(dget(d, "shiftA")),       P<float>(dget(d, "shiftB")),       P<const bf16>(dget(d, "dadd"))};
     if (!b.dya || !b.za || !b.meanA || !b.invA || !b.gammaA || !b.dza) throw std::invalid_argument("bn_bwd: missing A");
-    launch_bn_bwd(S(st), b, P<float>(red), M, C, P<float>(ws), ws ? ws_floats : 0, ldd, ldy);
+    launch_bn_bwd(S(st), b, P<float>(red), M, C, P<float>(ws), ws ? ws_floats : 0, ldd, ldy, chained);
     check("bn_bwd");
   }, py::arg("st"), py::arg("desc"), py::arg("red"), py::arg("M"), py::arg("C"), py::arg("ws") = 0,
-     py::arg("ws_floats") = 0, py::arg("ldd") = 0, py::arg("ldy") = 0);
+     py::arg("ws_floats") = 0, py::arg("ldd") = 0, py::arg("ldy") = 0, py::arg("chained") = 0);
+  m.def("bn_bwd_chain_reps", [](int C) { return bn_bwd_chain_reps(C); });
   m.def("head", [](uintptr_t st, uintptr_t y, uintptr_t labels, int base, uintptr_t dbase, int N, int HW, int C, int J,
                    uintptr_t W, uintptr_t b, uintptr_t pooled, uintptr_t dlog, uintptr_t dy, uintptr_t stats,
-                   uintptr_t dW, uintptr_t db, int train) {
+                   uintptr_t dW, uintptr_t db, int train, uintptr_t zero_buf, long zero_n) {
     launch_head(S(st), P<const bf16>(y), P<const int>(labels), base, P<const int>(dbase), N, HW, C, J, P<const float>(W),
                 P<const float>(b), P<float>(pooled), P<float>(dlog), P<bf16>(dy), P<float>(stats), P<float>(dW),
-                P<float>(db), train);
+                P<float>(db), train, P<float>(zero_buf), zero_n);
     check("head");
-  });
+  }, py::arg("st"), py::arg("y"), py::arg("labels"), py::arg("base"), py::arg("dbase"), py::arg("N"), py::arg("HW"),
+     py::arg("C"), py::arg("J"), py::arg("W"), py::arg("b"), py::arg("pooled"), py::arg("dlog"), py::arg("dy"),
+     py::arg("stats"), py::arg("dW"), py::arg("db"), py::arg("train"), py::arg("zero_buf") = 0, py::arg("zero_n") = 0);
 }

@@ -206,7 +206,8 @@ FEDMI_DEV void load_g(const BwdIn& in, long r, int cg, float* g) {
 // (rep = block % BN_REP: 1/BN_REP of the same-address atomic contention) and
 // bn_bwd_finalize sums the replicas into red and re-zeroes them.
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BwdIn in, float* __restrict__ red, int M, int C,
-                                                            int rows_per_block, float* __restrict__ partials) {
+                                                            int rows_per_block, float* __restrict__ partials,
+                                                            int reps) {
   __shared__ float part[3][256][8];
   const int VR = C >> 3;                 // host: blockDim.x % VR == 0
   const int cg = threadIdx.x % VR, rstep = blockDim.x / VR, r0 = threadIdx.x / VR;
@@ -251,7 +252,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BwdIn in, float* __r
     const int g = c >> 3, j = c & 7;
     float s = 0.f;
     for (int t = g; t < (int)blockDim.x; t += VR) s += part[qn][t][j];
-    unsafeAtomicAdd((partials ? partials + (long)(blockIdx.x % BN_REP) * 3 * C : red) + qn * C + c, s);
+    unsafeAtomicAdd((partials ? partials + (long)(blockIdx.x % reps) * 3 * C : red) + qn * C + c, s);
   }
 }
 
@@ -288,12 +289,28 @@ struct BwdOut {
   const bf16* dadd;       // optional grad added to dza (a residual edge that bypasses this BN)
 };
 
+// partials != null (chained mode): the channel sums are read straight from the reduce kernel's
+// 'reps' atomic replicas (no finalize launch); the caller zeroes them before the next step.
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdIn in, BwdOut out, const float* __restrict__ red,
-                                                           int M, int C) {
+                                                           int M, int C, const float* __restrict__ partials,
+                                                           int reps) {
   extern __shared__ float co[];   // [6][C]: kA, bA, cA, kB, bB, cB  (dz = k*g + b*xhat + c)
   const float invM = 1.f / (float)M;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float sg = red[c], sgx = red[C + c];
+    float sg, sgx, sgx2 = 0.f;
+    if (partials) {
+      sg = sgx = 0.f;
+      for (int r = 0; r < reps; ++r) {           // fixed order: every block derives identical coefficients
+        const float* pr = partials + (long)r * 3 * C;
+        sg += pr[c];
+        sgx += pr[C + c];
+        if (in.zb) sgx2 += pr[2 * C + c];
+      }
+    } else {
+      sg = red[c];
+      sgx = red[C + c];
+      if (in.zb) sgx2 = red[2 * C + c];
+    }
     const float scA = out.gammaA[c] * in.invA[c];
     // dz = scA * (g - sg/M - xhat * sgx/M),  xhat = (z - mean) * inv
     co[c] = scA;
@@ -305,7 +322,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdIn in, BwdOut out,
       if (out.shiftA) out.shiftA[c] = in.meanA[c];
     }
     if (in.zb) {
-      const float sgx2 = red[2 * C + c];
       const float scB = out.gammaB[c] * in.invB[c];
       co[3 * C + c] = scB;
       co[4 * C + c] = -scB * sgx2 * invM * in.invB[c];
@@ -351,7 +367,12 @@ __global__ __launch_bounds__(256) void head_fwd_bwd_kernel(const bf16* __restric
                                                            int base, const int* __restrict__ dbase, int HW, int C, int J, const float* __restrict__ W,
                                                            const float* __restrict__ b, float* __restrict__ pooled,
                                                            float* __restrict__ dlog, bf16* __restrict__ dy,
-                                                           float* __restrict__ stats, int N, int train) {
+                                                           float* __restrict__ stats, int N, int train,
+                                                           float4* __restrict__ zero_buf, long zero_n4) {
+  // the step's BN-backward replica arena (chained mode) is cleared here: the head runs after every
+  // BN backward of the previous step and before any of this step
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < zero_n4; i += (long)gridDim.x * 256)
+    zero_buf[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   // Every phase issues ALL of a thread's global loads before consuming any of them: with
   // one workgroup per sample the kernel is latency-bound, and a load-use loop paid one
   // memory round trip per position / weight (round 1: 25 us for ResNet-18's 4x4x512 head).
@@ -779,8 +800,12 @@ long bn_bwd_ws_floats(int M, int C) {
 // red: [3][C] fp32.  With ``ws`` (>= bn_bwd_ws_floats, zero): replica atomics + a
 // finalize launch (red needs no zeroing).  Without: atomics into red, which must
 // be zero on entry.
+// Replicas per channel sum in chained mode: <= 2048 floats per quantity, 4..16 (a replica spreads
+// the reduce workgroups' same-address atomics; the apply prologue reads them all).
+int bn_bwd_chain_reps(int C) { return std::max(4, std::min(16, 2048 / std::max(C, 1))); }
+
 void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, float* red, int M, int C, float* ws, long ws_floats, int ldd,
-                   int ldy) {
+                   int ldy, int chained) {
   const int VR = C / 8;
   if (C % 8 || VR > 256) throw std::invalid_argument("bn_bwd: need C % 8 == 0 and C <= 2048");
   if (ldd <= 0) ldd = C;
@@ -791,22 +816,34 @@ void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, float* red, int M, int C,
              d.dadd};
   int tb, rows_per_block, nblk;
   bn_bwd_grid(M, C, &tb, &rows_per_block, &nblk);
+  if (chained) {
+    // ws: this BN's own replica buffer, ZERO on entry (the head kernel clears the arena every step)
+    const int reps = bn_bwd_chain_reps(C);
+    if (!ws || ws_floats < (long)reps * 3 * C) throw std::invalid_argument("bn_bwd: chained replicas too small");
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(tb), 0, st, in, red, M, C, rows_per_block, ws, reps);
+    const int gblk = (int)std::min<long>(((long)M * VR + 255) / 256, 1024);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(gblk), dim3(256), 6 * C * sizeof(float), st, in, out, red, M, C,
+                       ws, reps);
+    return;
+  }
   const bool two = ws && ws_floats >= (long)BN_REP * 3 * C;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(tb), 0, st, in, red, M, C, rows_per_block,
-                     two ? ws : nullptr);
+                     two ? ws : nullptr, BN_REP);
   if (two) hipLaunchKernelGGL(bn_bwd_finalize, dim3((3 * C + 255) / 256), dim3(256), 0, st, ws, C, red);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for((long)M * VR)), dim3(256), 6 * C * sizeof(float), st, in, out,
-                     red, M, C);
+                     red, M, C, nullptr, 0);
 }
 
 void launch_head(hipStream_t st, const bf16* y, const int* labels, int base, const int* dbase, int N, int HW, int C, int J,
                  const float* W, const float* b, float* pooled, float* dlog, bf16* dy, float* stats, float* dW,
-                 float* db, int train) {
+                 float* db, int train, float* zero_buf, long zero_n) {
+  if (zero_n % 4 || (reinterpret_cast<uintptr_t>(zero_buf) & 15)) throw std::invalid_argument("head: zero arena alignment");
   if (J > 16) throw std::invalid_argument("head: at most 16 classes");
   if (C % 8 || C > 2048) throw std::invalid_argument("head: need C % 8 == 0 and C <= 2048");
   const int npg = std::max(1, 256 / (C / 8));
   hipLaunchKernelGGL(head_fwd_bwd_kernel, dim3(N), dim3(256), (C + 32 + npg * C) * sizeof(float), st, y, labels, base, dbase, HW, C,
-                     J, W, b, pooled, dlog, dy, stats, N, train);
+                     J, W, b, pooled, dlog, dy, stats, N, train,
+                     reinterpret_cast<float4*>(zero_buf), zero_n / 4);
   if (train && N > HEAD_MAXN) throw std::invalid_argument("head: training batch > 512");
   if (train)
     hipLaunchKernelGGL(head_wgrad_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pooled, dlog, N, C, J, dW, db);

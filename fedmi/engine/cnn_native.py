@@ -474,6 +474,15 @@ class CNNNativeTrainer(LocalTrainer):
                                     device=device)
         # BN-backward two-level channel sums (replicated atomics + finalize; kept zero between uses)
         self.bn_ws = torch.zeros(max(cnn.bn_bwd_ws_floats(B * u.P * u.P, u.O) for u in self.units), device=device)
+        # chained BN backward: every BN gets its own replica slice of one arena, the head launch clears the
+        # arena each step and the apply kernels read the replicas directly (no finalize launch per BN)
+        self.bn_chain = torch.zeros(sum((cnn.bn_bwd_chain_floats(u.O) + 3) // 4 * 4 for u in self.units) + 4,
+                                    device=device)
+        co = 0
+        for u in self.units:
+            n = (cnn.bn_bwd_chain_floats(u.O) + 3) // 4 * 4
+            u.bn_rep = self.bn_chain[co:co + n] if n else None
+            co += n
         self.xin = torch.empty(R, 32, 32, 8, dtype=act_dtype, device=device)
         self.dhead = torch.empty(R * self.head_hw * self.head_hw * self.head_c, dtype=act_dtype, device=device)
         self.pooled = torch.empty(R, self.head_c, device=device)
@@ -583,17 +592,20 @@ class CNNNativeTrainer(LocalTrainer):
         hd = self.dhead[: a.numel()].view_as(a)
         cnn.head(a, labels, 0, lin.weight, lin.bias, self.stats[stats_row], train, self.pooled[:nb], self.dlog[:nb],
                  hd if train else None, lin.weight.grad if train else None, lin.bias.grad if train else None,
-                 dbase=dbase)
+                 dbase=dbase, zero=self.bn_chain if train else None)
         return x, hd
 
     def _bn_bwd(self, u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None, dadd=None) -> None:
         bn_ws = self.bn_ws if self.bn_ws.numel() else None
+        chained = u.bn_rep is not None
+        if chained:
+            bn_ws = u.bn_rep
         kw = {}
         if zb is not None:
             kw = dict(zb=zb.view(zb.z, nb), b=zb.bn_args(None), dgamma_b=zb.bn.weight.grad,
                       dbeta_b=zb.bn.bias.grad, dzb=zb.view(zb.dz, nb))
         cnn.bn_bwd(dya, u.view(u.z, nb), u.bn_args(None), u.bn.weight.grad, u.bn.bias.grad, u.view(u.dz, nb), u.red,
-                   dyb=dyb, y=y, gout=gout, ws=bn_ws, dadd=dadd, **kw)
+                   dyb=dyb, y=y, gout=gout, ws=bn_ws, dadd=dadd, chained=chained, **kw)
 
     def _backward(self, nb: int, x: torch.Tensor, dhead: torch.Tensor) -> None:
         if self.preact is not None:
@@ -634,7 +646,7 @@ class CNNNativeTrainer(LocalTrainer):
         hd = self.dhead[: a.numel()].view_as(a)
         cnn.head(a, labels, 0, lin.weight, lin.bias, self.stats[stats_row], train, self.pooled[:nb], self.dlog[:nb],
                  hd if train else None, lin.weight.grad if train else None, lin.bias.grad if train else None,
-                 dbase=dbase)
+                 dbase=dbase, zero=self.bn_chain if train else None)
         return hd
 
     def _forward_preact(self, nb: int, train: bool, images, labels, dbase, stats_row: int):

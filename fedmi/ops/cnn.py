@@ -143,13 +143,15 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
            dza: torch.Tensor, red: torch.Tensor, dyb: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None,
            zb: Optional[torch.Tensor] = None, b: Optional[BNParams] = None, dgamma_b=None, dbeta_b=None, dzb=None,
            gout: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-           dadd: Optional[torch.Tensor] = None) -> None:
+           dadd: Optional[torch.Tensor] = None, chained: bool = False) -> None:
     """BatchNorm backward through an optional ReLU mask (``y``: forward output) for one or two BN
     branches sharing the incoming grad g = dya (+ dyb).  Writes dz for each branch, dgamma/dbeta,
     and optionally g itself (``gout``, the identity-shortcut grad).  ``red``: [3, C] fp32 channel
     sums.  With ``ws`` (>= :func:`bn_bwd_ws_floats` fp32, ZERO before first use; every call leaves it
     zero) the sums go through replicated atomics + a finalize and ``red`` needs no init; without,
-    they are atomics straight into ``red``, which must be ZERO."""
+    they are atomics straight into ``red``, which must be ZERO.  ``chained``: ``ws`` is this BN's own
+    replica buffer (>= :func:`bn_bwd_chain_floats`, ZERO on entry -- the engine's head launch clears
+    the arena every step); no finalize launch, the apply kernel reads the replicas."""
     C = za.shape[-1]
     M = za.numel() // C
     if red.numel() < 3 * C:
@@ -165,7 +167,12 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
         raise ValueError("bn_bwd: dya and dyb must share a row stride")
     native.require().bn_bwd(native.stream_handle(red.device), d, red.data_ptr(), M, C,
                             ws.data_ptr() if ws is not None else 0, ws.numel() if ws is not None else 0,
-                            ldd, row_stride(y) if y is not None else C)
+                            ldd, row_stride(y) if y is not None else C, int(chained))
+
+
+def bn_bwd_chain_floats(C: int) -> int:
+    """fp32 replica floats one BN needs in chained mode."""
+    return 3 * int(C) * int(native.require().bn_bwd_chain_reps(int(C)))
 
 
 def bn_bwd_ws_floats(M: int, C: int) -> int:
@@ -173,10 +180,11 @@ def bn_bwd_ws_floats(M: int, C: int) -> int:
 
 
 def head(y: torch.Tensor, labels: torch.Tensor, base: int, W: torch.Tensor, b: torch.Tensor, stats: torch.Tensor,
-         train: bool, pooled=None, dlog=None, dy=None, dW=None, db=None, dbase=None) -> None:
+         train: bool, pooled=None, dlog=None, dy=None, dW=None, db=None, dbase=None,
+         zero: Optional[torch.Tensor] = None) -> None:
     N, H, Wd, C = y.shape
     J = W.shape[0]
     native.require().head(native.stream_handle(y.device), y.data_ptr(), labels.data_ptr(), base, _p(dbase), N,
                           H * Wd, C, J,
                           W.data_ptr(), b.data_ptr(), _p(pooled), _p(dlog), _p(dy), stats.data_ptr(), _p(dW), _p(db),
-                          int(train))
+                          int(train), _p(zero), zero.numel() if zero is not None else 0)

@@ -262,7 +262,7 @@ def maxpool2_bwd(x, dy, out=None):
 
 @torch.no_grad()
 def bn_bwd(dya, za, a, dgamma_a, dbeta_a, dza, red, dyb=None, y=None, zb=None, b=None, dgamma_b=None,
-           dbeta_b=None, dzb=None, gout=None, ws=None, dadd=None):
+           dbeta_b=None, dzb=None, gout=None, ws=None, dadd=None, chained=False):
     C = za.shape[-1]
     M = za.numel() // C
     g = dya.float().reshape(M, C)
@@ -292,8 +292,15 @@ def bn_bwd_ws_floats(M, C):
     return 0
 
 
+def bn_bwd_chain_floats(C):
+    return 0
+
+
 @torch.no_grad()
-def head(y, labels, base, W, b, stats, train, pooled=None, dlog=None, dy=None, dW=None, db=None, dbase=None):
+def head(y, labels, base, W, b, stats, train, pooled=None, dlog=None, dy=None, dW=None, db=None, dbase=None,
+         zero=None):
+    if zero is not None:
+        zero.zero_()
     N, H, Wd, C = y.shape
     base = base + (int(dbase.view(-1)[0]) if dbase is not None else 0)
     lab = labels[base:base + N].long()
@@ -337,7 +344,7 @@ def emulated():
     for name in ("pack_weight", "pack_weights", "fd_ws_floats", "dgrad_pack_weights", "conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
                  "dwconv_dgrad", "dwconv_wgrad", "dwconv_ws_floats"):
         swap(conv, name, globals()[name])
-    for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "bn_bwd_ws_floats", "head", "maxpool2",
+    for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "bn_bwd_ws_floats", "bn_bwd_chain_floats", "head", "maxpool2",
                  "maxpool2_bwd", "maxpool3", "maxpool3_bwd"):
         swap(cnn, name, globals()[name])
     swap(native, "require", lambda: _NativeStub())

@@ -187,6 +187,25 @@ def test_bn_forward_backward_with_projection_residual(gpu_device):
     assert _rel(first, dga2) < 1e-5 and float(ws.abs().max()) == 0.0
     assert _rel(dza2.float(), dza.float()) < 1e-2 and _rel(dzb2.float(), dzb.float()) < 1e-2
     assert _rel(dga2, dga) < 1e-4 and _rel(dba2, dba) < 1e-4 and _rel(dgb2, dgb) < 1e-4
+    # chained mode (the engine's default): per-BN replicas read by the apply kernel, no finalize launch,
+    # no 'red' use at all; the replicas must be zero on entry (the head launch clears them per step)
+    rep = torch.zeros(cnn.bn_bwd_chain_floats(C), device=dev)
+    red3 = torch.full((3, C), float("nan"), device=dev)
+    dza3, dzb3 = torch.empty_like(dza), torch.empty_like(dzb)
+    dga3, dba3, dgb3, dbb3 = (torch.empty(C, device=dev) for _ in range(4))
+    cnn.bn_bwd(dya, za, A, dga3, dba3, dza3, red3, dyb=dyb, y=y, zb=zb, b=B, dgamma_b=dgb3, dbeta_b=dbb3,
+               dzb=dzb3, ws=rep, chained=True)
+    torch.cuda.synchronize()
+    assert _rel(dza3.float(), dza.float()) < 1e-2 and _rel(dzb3.float(), dzb.float()) < 1e-2
+    assert _rel(dga3, dga) < 1e-4 and _rel(dba3, dba) < 1e-4 and _rel(dgb3, dgb) < 1e-4 and _rel(dbb3, dbb) < 1e-4
+    # the head launch clears a replica arena
+    rep2 = torch.ones(64, device=dev)
+    Nh, Ch = 4, 64
+    cnn.head(torch.randn(Nh, 2, 2, Ch, device=dev).bfloat16(), torch.zeros(Nh, dtype=torch.int32, device=dev), 0,
+             torch.randn(10, Ch, device=dev), torch.zeros(10, device=dev), torch.zeros(4, device=dev), False,
+             zero=rep2)
+    torch.cuda.synchronize()
+    assert float(rep2.abs().max()) == 0.0
 
 
 def test_bn_eval_uses_running_stats(gpu_device):
