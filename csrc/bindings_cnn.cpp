@@ -55,19 +55,21 @@ struct BNBwdDesc {
   bf16* gout;
   float* shiftA; float* shiftB;
   const bf16* dadd;
+  const float* msc;
 };
 struct DwShape {
   int N, H, W, C, R, S, st, pad;
 };
-void launch_dw_fwd(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, float*, const float*);
+void launch_dw_fwd(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, float*, const float*, const float*);
 void launch_dw_dgrad(hipStream_t, const DwShape&, const bf16*, const float*, bf16*);
 long dw_wgrad_ws_floats(const DwShape&);
-void launch_dw_wgrad(hipStream_t, const DwShape&, const bf16*, const bf16*, float*, float*, long, int);
+void launch_dw_wgrad(hipStream_t, const DwShape&, const bf16*, const bf16*, float*, float*, long, int, const float*);
 void launch_prep_input(hipStream_t, const uint8_t*, int, const int*, int, int, uint32_t, const int*, bf16*);
 void launch_sched_next(hipStream_t, const int*, int*, int*);
 void launch_bn_apply(hipStream_t, const bf16*, const BNDesc&, const bf16*, const BNDesc*, const bf16*, bf16*, int, int,
                      float, float, int, int, int);
 void launch_bn_bwd(hipStream_t, const BNBwdDesc&, float*, int, int, float*, long, int, int, int);
+void launch_bn_coeff(hipStream_t, const BNDesc&, int, int, float, float, int, float*);
 long bn_bwd_ws_floats(int, int);
 int bn_bwd_chain_reps(int);
 void launch_head(hipStream_t, const bf16*, const int*, int, const int*, int, int, int, int, const float*,
@@ -168,22 +170,24 @@ void fedmi_bind_cnn(py::module_& m) {
     check("conv_pack");
   });
   m.def("dw_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
-                     uintptr_t shift) {
+                     uintptr_t shift, uintptr_t isc) {
     launch_dw_fwd(S(st), dw_from(shp), P<const bf16>(x), P<const float>(w), P<bf16>(y), P<float>(stats),
-                  P<const float>(shift));
+                  P<const float>(shift), P<const float>(isc));
     check("dw_fwd");
-  });
+  }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("shift"),
+     py::arg("isc") = 0);
   m.def("dw_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx) {
     launch_dw_dgrad(S(st), dw_from(shp), P<const bf16>(dy), P<const float>(w), P<bf16>(dx));
     check("dw_dgrad");
   });
   m.def("dw_wgrad_ws_floats", [](const py::tuple& shp) { return dw_wgrad_ws_floats(dw_from(shp)); });
   m.def("dw_wgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws,
-                       long ws_floats, int accumulate) {
+                       long ws_floats, int accumulate, uintptr_t isc) {
     launch_dw_wgrad(S(st), dw_from(shp), P<const bf16>(x), P<const bf16>(dy), P<float>(dw), P<float>(ws), ws_floats,
-                    accumulate);
+                    accumulate, P<const float>(isc));
     check("dw_wgrad");
-  });
+  }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ws"), py::arg("ws_floats"),
+     py::arg("accumulate"), py::arg("isc") = 0);
   m.def("prep_input", [](uintptr_t st, uintptr_t images, int base, uintptr_t dbase, int nb, int augment,
                          uint32_t seed, uintptr_t round_ctr, uintptr_t out) {
     launch_prep_input(S(st), P<const uint8_t>(images), base, P<const int>(dbase), nb, augment, seed,
@@ -221,6 +225,10 @@ void fedmi_bind_cnn(py::module_& m) {
     check("bn_apply");
   }, py::arg("st"), py::arg("z"), py::arg("a"), py::arg("z2"), py::arg("b"), py::arg("res"), py::arg("y"), py::arg("M"),
      py::arg("C"), py::arg("eps"), py::arg("mom"), py::arg("train"), py::arg("relu"), py::arg("ldy") = 0);
+  m.def("bn_coeff", [](uintptr_t st, const py::dict& a, int M, int C, float eps, float mom, int train, uintptr_t co) {
+    launch_bn_coeff(S(st), bn_from(a), M, C, eps, mom, train, P<float>(co));
+    check("bn_coeff");
+  });
   m.def("bn_bwd_ws_floats", [](int M, int C) { return bn_bwd_ws_floats(M, C); });
   m.def("bn_bwd", [](uintptr_t st, const py::dict& d, uintptr_t red, int M, int C, uintptr_t ws, long ws_floats,
                      int ldd, int ldy, int chained) {
@@ -230,7 +238,8 @@ void fedmi_bind_cnn(py::module_& m) {
                 P<bf16>(dget(d, "dza")),           P<const bf16>(dget(d, "zb")),      P<const float>(dget(d, "meanB")),
                 P<const float>(dget(d, "invB")),   P<const float>(dget(d, "gammaB")), P<float>(dget(d, "dgammaB")),
                 P<float>(dget(d, "dbetaB")),       P<bf16>(dget(d, "dzb")),           P<bf16>(dget(d, "gout")),
-                P<float>(dget(d, "shiftA")),       P<float>(dget(d, "shiftB")),       P<const bf16>(dget(d, "dadd"))};
+                P<float>(dget(d, "shiftA")),       P<float>(dget(d, "shiftB")),       P<const bf16>(dget(d, "dadd")),
+                P<const float>(dget(d, "msc"))};
     if (!b.dya || !b.za || !b.meanA || !b.invA || !b.gammaA || !b.dza) throw std::invalid_argument("bn_bwd: missing A");
     launch_bn_bwd(S(st), b, P<float>(red), M, C, P<float>(ws), ws ? ws_floats : 0, ldd, ldy, chained);
     check("bn_bwd");

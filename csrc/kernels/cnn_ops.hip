@@ -123,6 +123,13 @@ FEDMI_DEV void bn_coeffs(const BNArgs& a, int C, int M, float eps, float mom, in
   if (train && blockIdx.x == 0 && threadIdx.x == 0 && a.nbt) a.nbt[0] += 1;
 }
 
+// BN scale / shift only ([2][C] fp32), with bn_apply's running-stat / saved-stat commit: for a BN whose
+// consumer applies it on load (bn_apply's output is never written).  One workgroup.
+__global__ __launch_bounds__(256) void bn_coeff_kernel(BNArgs A, int M, int C, float eps, float mom, int train,
+                                                       float* __restrict__ co) {
+  bn_coeffs(A, C, M, eps, mom, train, co, co + C);
+}
+
 // y = act(bnA(z) [+ res | + bnB(z2)])      res_mode: 0 none, 1 identity residual, 2 second BN branch
 // y rows have stride ldy (>= C): a channel slice of a concatenated output (GoogLeNet)
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ z, BNArgs A, const bf16* __restrict__ z2,
@@ -181,10 +188,12 @@ struct BwdIn {
   const float* invB;
   int ldd;                // row stride of dya / dyb (elements; C = compact)
   int ldy;                // row stride of y
+  const float* msc;       // [2][C] (optional, y == null): ReLU mask from za, relu(za * sc + sh) > 0 -- the
+                          // forward never materialised y (its consumer applied this BN on load)
 };
 
-// row r, channel group cg (8 channels)
-FEDMI_DEV void load_g(const BwdIn& in, long r, int cg, float* g) {
+// row r, channel group cg (8 channels); z: the 8 za values of the row (for the msc mask)
+FEDMI_DEV void load_g(const BwdIn& in, long r, int cg, float* g, const float* z) {
   const long od = r * in.ldd + cg * 8;
   load8f(in.dya + od, g);
   if (in.dyb) {
@@ -198,6 +207,10 @@ FEDMI_DEV void load_g(const BwdIn& in, long r, int cg, float* g) {
     load8f(in.y + r * in.ldy + cg * 8, t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = t[j] > 0.f ? g[j] : 0.f;
+  } else if (in.msc) {
+    const int C = in.ldd;   // msc mode: compact rows (host checks ldd == C)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = z[j] * in.msc[cg * 8 + j] + in.msc[C + cg * 8 + j] > 0.f ? g[j] : 0.f;
   }
 }
 
@@ -225,8 +238,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BwdIn in, float* __r
   for (int r = rb + r0; r < re; r += rstep) {
     const long i = (long)r * VR + cg;
     float g[8], z[8];
-    load_g(in, r, cg, g);
     load8f(in.za + i * 8, z);
+    load_g(in, r, cg, g, z);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       s0[j] += g[j];
@@ -339,9 +352,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdIn in, BwdOut out,
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
     const int c0 = (int)(i % VR) * 8;
     float g[8], z[8], d[8];
-    load_g(in, i / VR, c0 >> 3, g);
-    if (out.gout) store8f(out.gout + i * 8, g);
     load8f(in.za + i * 8, z);
+    load_g(in, i / VR, c0 >> 3, g, z);
+    if (out.gout) store8f(out.gout + i * 8, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) d[j] = co[c0 + j] * g[j] + co[C + c0 + j] * z[j] + co[2 * C + c0 + j];
     if (out.dadd) {
@@ -772,6 +785,10 @@ void launch_bn_apply(hipStream_t st, const bf16* z, const BNDesc& a, const bf16*
                      to_args(a), z2, bb, res, y, M, C, eps, mom, train, relu, res_mode, ldy);
 }
 
+void launch_bn_coeff(hipStream_t st, const BNDesc& a, int M, int C, float eps, float mom, int train, float* co) {
+  hipLaunchKernelGGL(bn_coeff_kernel, dim3(1), dim3(256), 0, st, to_args(a), M, C, eps, mom, train, co);
+}
+
 struct BNBwdDesc {
   const bf16* dya; const bf16* dyb; const bf16* y;
   const bf16* za; const float* meanA; const float* invA; const float* gammaA; float* dgammaA; float* dbetaA; bf16* dza;
@@ -779,6 +796,7 @@ struct BNBwdDesc {
   bf16* gout;
   float* shiftA; float* shiftB;
   const bf16* dadd;
+  const float* msc;
 };
 
 static void bn_bwd_grid(int M, int C, int* tb, int* rows_per_block, int* nblk) {
@@ -811,7 +829,8 @@ void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, float* red, int M, int C,
   if (ldd <= 0) ldd = C;
   if (ldy <= 0) ldy = C;
   if (ldd < C || ldy < C || ldd % 8 || ldy % 8) throw std::invalid_argument("bn_bwd: bad row strides");
-  BwdIn in{d.dya, d.dyb, d.y, d.za, d.meanA, d.invA, d.zb, d.meanB, d.invB, ldd, ldy};
+  if (d.msc && (d.y || ldd != C)) throw std::invalid_argument("bn_bwd: the z-derived ReLU mask needs y == null, compact rows");
+  BwdIn in{d.dya, d.dyb, d.y, d.za, d.meanA, d.invA, d.zb, d.meanB, d.invB, ldd, ldy, d.msc};
   BwdOut out{d.dza, d.dzb, d.gout, d.dgammaA, d.dbetaA, d.dgammaB, d.dbetaB, d.gammaA, d.gammaB, d.shiftA, d.shiftB,
              d.dadd};
   int tb, rows_per_block, nblk;

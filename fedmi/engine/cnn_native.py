@@ -51,6 +51,14 @@ BN_EPS = 1e-5
 BN_MOM = 0.1
 
 
+class _Lazy:
+    """An activation that was never materialised: relu(BN(z)) with the BN's [2, C] scale / shift
+    ``co``; only a depthwise consumer can take it (it applies the BN on load)."""
+
+    def __init__(self, z: torch.Tensor, co: torch.Tensor):
+        self.z, self.co = z, co
+
+
 class _Unit:
     """conv (dense or depthwise, no bias) + BatchNorm2d (+ ReLU), with its device buffers."""
 
@@ -106,18 +114,26 @@ class _Unit:
     def fwd(self, x: torch.Tensor, nb: int, stats, ws: Optional[torch.Tensor] = None,
             res: Optional[torch.Tensor] = None) -> None:
         sh = self.shift if stats is not None else None
+        in_bn = None
+        if isinstance(x, _Lazy):
+            assert self.depthwise, "only a depthwise conv applies its producer's BN on load"
+            x, in_bn = x.z, x.co
         if self.depthwise:
             assert res is None
             conv.dwconv_fwd(x, self.conv.weight, self.stride, self.pad, stats=stats, out=self.view(self.z, nb),
-                            shift=sh)
+                            shift=sh, in_bn=in_bn)
         else:
             conv.conv2d_fwd(x, self.wr, self.stride, self.pad, Cw=self.Cw, stats=stats, out=self.view(self.z, nb),
                             shift=sh, ws=ws, res=res)
 
     def wgrad(self, x: torch.Tensor, nb: int, ws: torch.Tensor, dz: Optional[torch.Tensor] = None) -> None:
         dz = self.view(self.dz, nb) if dz is None else dz
+        in_bn = None
+        if isinstance(x, _Lazy):
+            assert self.depthwise, "only a depthwise conv applies its producer's BN on load"
+            x, in_bn = x.z, x.co
         if self.depthwise:
-            conv.dwconv_wgrad(x, dz, self.R, self.stride, self.pad, out=self.conv.weight.grad, ws=ws)
+            conv.dwconv_wgrad(x, dz, self.R, self.stride, self.pad, out=self.conv.weight.grad, ws=ws, in_bn=in_bn)
         else:
             conv.conv2d_wgrad(x, dz, self.R, self.S, self.stride, self.pad, Cw=self.Cw, out=self.conv.weight.grad,
                               ws=ws)
@@ -456,6 +472,8 @@ class CNNNativeTrainer(LocalTrainer):
             last = self.blocks[-1]
             self.head_hw, self.head_c = last.out_hw, last.cout
             self.units = plan.units() if self.preact else [u for b in self.blocks for u in b.units()]
+            if not self.preact:
+                self._mark_deferred_bn(device)
             # units whose data gradient is never needed (they read the network input)
             self._no_dgrad = ({id(self.preact.stem)} if self.preact else
                               {id(u) for u in self.blocks[0].units()} if self.blocks[0].first else set())
@@ -555,6 +573,28 @@ class CNNNativeTrainer(LocalTrainer):
         self._starts, self._sizes = [], []
         self._graphs.clear()
 
+    def _mark_deferred_bn(self, device) -> None:
+        """A block whose output feeds ONLY the next block's depthwise conv (no shortcut, no pool, not the
+        network output: MobileNet's pointwise -> depthwise chain) skips its BN-apply pass: the BN's
+        scale / shift are computed by one small launch, the depthwise forward and weight-gradient
+        kernels apply it on load, and its BN backward derives the ReLU mask from z
+        (FEDMI_CNN_DEFER_BN=0 restores the materialised activation)."""
+        import os
+
+        on = os.environ.get("FEDMI_CNN_DEFER_BN", "1") == "1"
+        for b, nxt in zip(self.blocks[:-1], self.blocks[1:]):
+            b.defer = bool(on and b.shortcut == "none" and not b.pool and b.out_relu and nxt.main[0].depthwise
+                           and nxt.shortcut == "none" and nxt.proj is None)
+            b.co = torch.empty(2, b.cout, device=device) if b.defer else None
+        self.blocks[-1].defer, self.blocks[-1].co = False, None
+
+    def _act(self, b: "_Block", nb: int):
+        """A block's output as its consumer sees it (materialised or lazy)."""
+        if getattr(b, "defer", False):
+            last = b.main[-1]
+            return _Lazy(last.view(last.z, nb), b.co)
+        return b.out_view(nb)
+
     # ---- kernel schedule ---------------------------------------------------------------------
     def _bn(self, u: _Unit, z: torch.Tensor, y: torch.Tensor, train: bool, relu: bool, **kw) -> torch.Tensor:
         return cnn.bn_apply(z, u.bn_args(u.stats), y, train, relu, eps=BN_EPS, momentum=BN_MOM, **kw)
@@ -583,11 +623,14 @@ class CNNNativeTrainer(LocalTrainer):
                 self._bn(last, z, out, train, b.out_relu, z2=p.view(p.z, nb), b=p.bn_args(p.stats))
             elif b.shortcut == "identity":
                 self._bn(last, z, out, train, b.out_relu, res=a)
+            elif getattr(b, "defer", False):
+                cnn.bn_coeff(z.numel() // last.O, last.O, last.bn_args(last.stats if train else None), b.co, train,
+                             eps=BN_EPS, momentum=BN_MOM)
             else:
                 self._bn(last, z, out, train, b.out_relu)
             if b.pool:
                 cnn.maxpool2(out, out=b.out_view(nb))
-            a = b.out_view(nb)
+            a = self._act(b, nb)
         lin = self.head_lin
         hd = self.dhead[: a.numel()].view_as(a)
         cnn.head(a, labels, 0, lin.weight, lin.bias, self.stats[stats_row], train, self.pooled[:nb], self.dlog[:nb],
@@ -595,7 +638,8 @@ class CNNNativeTrainer(LocalTrainer):
                  dbase=dbase, zero=self.bn_chain if train else None)
         return x, hd
 
-    def _bn_bwd(self, u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None, dadd=None) -> None:
+    def _bn_bwd(self, u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None, dadd=None,
+                mask_bn=None) -> None:
         bn_ws = self.bn_ws if self.bn_ws.numel() else None
         chained = u.bn_rep is not None
         if chained:
@@ -605,7 +649,7 @@ class CNNNativeTrainer(LocalTrainer):
             kw = dict(zb=zb.view(zb.z, nb), b=zb.bn_args(None), dgamma_b=zb.bn.weight.grad,
                       dbeta_b=zb.bn.bias.grad, dzb=zb.view(zb.dz, nb))
         cnn.bn_bwd(dya, u.view(u.z, nb), u.bn_args(None), u.bn.weight.grad, u.bn.bias.grad, u.view(u.dz, nb), u.red,
-                   dyb=dyb, y=y, gout=gout, ws=bn_ws, dadd=dadd, chained=chained, **kw)
+                   dyb=dyb, y=y, gout=gout, ws=bn_ws, dadd=dadd, chained=chained, mask_bn=mask_bn, **kw)
 
     def _backward(self, nb: int, x: torch.Tensor, dhead: torch.Tensor) -> None:
         if self.preact is not None:
@@ -616,13 +660,16 @@ class CNNNativeTrainer(LocalTrainer):
         ws = self.wgrad_ws
         for i in range(len(self.blocks) - 1, -1, -1):
             b = self.blocks[i]
-            a_in = x if b.first else self.blocks[i - 1].out_view(nb)
+            a_in = x if b.first else self._act(self.blocks[i - 1], nb)
             last = b.main[-1]
             din_b = b.in_view(b.din_b, nb) if b.din_b is not None else None
             if b.pool:   # grad wrt the pooled output -> grad wrt the pre-pool activation
                 dya = cnn.maxpool2_bwd(b.pre_view(nb), dya, out=b.dpre_view(nb))
-            self._bn_bwd(last, nb, dya, dyb, b.pre_view(nb) if b.out_relu else None, zb=b.proj,
-                         gout=din_b if b.shortcut == "identity" else None)
+            if getattr(b, "defer", False):
+                self._bn_bwd(last, nb, dya, dyb, None, mask_bn=b.co)
+            else:
+                self._bn_bwd(last, nb, dya, dyb, b.pre_view(nb) if b.out_relu else None, zb=b.proj,
+                             gout=din_b if b.shortcut == "identity" else None)
             for j in range(len(b.main) - 1, -1, -1):
                 v = b.main[j]
                 xin = b.main[j - 1].view(b.main[j - 1].y, nb) if j > 0 else a_in

@@ -139,11 +139,22 @@ def bn_apply(z: torch.Tensor, a: BNParams, y: torch.Tensor, train: bool, relu: b
     return y
 
 
+def bn_coeff(z_rows: int, C: int, a: BNParams, co: torch.Tensor, train: bool, eps: float = 1e-5,
+             momentum: float = 0.1) -> torch.Tensor:
+    """BN scale / shift ([2, C] fp32 into ``co``) with bn_apply's running / saved statistics commit, for
+    a BN whose consumer applies it on load (the depthwise conv's ``in_bn``): bn_apply's output pass and
+    its activation buffer are skipped."""
+    native.require().bn_coeff(native.stream_handle(co.device), a.ptrs(), int(z_rows), int(C), eps, momentum,
+                              int(train), co.data_ptr())
+    return co
+
+
 def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Tensor, dbeta_a: torch.Tensor,
            dza: torch.Tensor, red: torch.Tensor, dyb: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None,
            zb: Optional[torch.Tensor] = None, b: Optional[BNParams] = None, dgamma_b=None, dbeta_b=None, dzb=None,
            gout: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-           dadd: Optional[torch.Tensor] = None, chained: bool = False) -> None:
+           dadd: Optional[torch.Tensor] = None, chained: bool = False,
+           mask_bn: Optional[torch.Tensor] = None) -> None:
     """BatchNorm backward through an optional ReLU mask (``y``: forward output) for one or two BN
     branches sharing the incoming grad g = dya (+ dyb).  Writes dz for each branch, dgamma/dbeta,
     and optionally g itself (``gout``, the identity-shortcut grad).  ``red``: [3, C] fp32 channel
@@ -151,14 +162,16 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
     zero) the sums go through replicated atomics + a finalize and ``red`` needs no init; without,
     they are atomics straight into ``red``, which must be ZERO.  ``chained``: ``ws`` is this BN's own
     replica buffer (>= :func:`bn_bwd_chain_floats`, ZERO on entry -- the engine's head launch clears
-    the arena every step); no finalize launch, the apply kernel reads the replicas."""
+    the arena every step); no finalize launch, the apply kernel reads the replicas.  ``mask_bn``
+    ([2, C] scale / shift, with ``y`` None): the ReLU mask is relu(za * scale + shift) > 0 -- for a BN
+    whose output was never materialised (its consumer applied it on load)."""
     C = za.shape[-1]
     M = za.numel() // C
     if red.numel() < 3 * C:
         raise ValueError("bn_bwd: scratch too small")
     d = dict(dya=_p(dya), dyb=_p(dyb), y=_p(y), za=_p(za), meanA=_p(a.smean), invA=_p(a.sinv), gammaA=_p(a.gamma),
              dgammaA=_p(dgamma_a), dbetaA=_p(dbeta_a), dza=_p(dza), gout=_p(gout), shiftA=_p(a.shift),
-             dadd=_p(dadd))
+             dadd=_p(dadd), msc=_p(mask_bn))
     if zb is not None:
         d.update(zb=_p(zb), meanB=_p(b.smean), invB=_p(b.sinv), gammaB=_p(b.gamma), dgammaB=_p(dgamma_b),
                  dbetaB=_p(dbeta_b), dzb=_p(dzb), shiftB=_p(b.shift))

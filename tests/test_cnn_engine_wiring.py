@@ -67,7 +67,7 @@ def test_engine_schedule_matches_autograd(name):
             assert int(bufs[k]) == int(b), k
 
 
-@pytest.mark.parametrize("name", ["ResNet18", "MobileNetV2", "VGG11", "PreActResNet18", "GoogLeNet"])
+@pytest.mark.parametrize("name", ["ResNet18", "MobileNet", "MobileNetV2", "VGG11", "PreActResNet18", "GoogLeNet"])
 def test_engine_eval_matches_torch_eval(name):
     """Eval mode (BN from running statistics) through the engine schedule == torch .eval()."""
     from fedmi.engine.cnn_native import CNNNativeTrainer

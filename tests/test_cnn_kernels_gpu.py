@@ -299,6 +299,58 @@ def test_depthwise_fwd_dgrad_wgrad(gpu_device, shape):
     assert _rel(dw, wb.grad) < 1e-2
 
 
+def test_depthwise_input_bn_and_z_mask(gpu_device):
+    """Deferred BN (MobileNet pointwise -> depthwise): the depthwise fwd / wgrad read the producer's z and
+    apply relu(z * scale + shift) on load; the producer's BN backward derives its ReLU mask from z."""
+    dev = gpu_device
+    torch.manual_seed(9)
+    N, H, W, C, R, st = 8, 8, 8, 256, 3, 1
+    z = torch.randn(N, H, W, C, device=dev).bfloat16()
+    co = torch.stack([torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.3]).contiguous()
+    y = torch.relu(z.float() * co[0] + co[1])                       # the activation that is never written
+    w = torch.randn(C, 1, R, R, device=dev) * 0.2
+    out = conv.dwconv_fwd(z, w, st, 1, in_bn=co)
+    ref = F.conv2d(y.permute(0, 3, 1, 2), w, stride=st, padding=1, groups=C)
+    gy = torch.randn(N, H, W, C, device=dev).bfloat16()
+    dw = conv.dwconv_wgrad(z, gy, R, st, 1, in_bn=co)
+    dwr = torch.nn.grad.conv2d_weight(y.permute(0, 3, 1, 2), (C, 1, R, R), gy.float().permute(0, 3, 1, 2),
+                                      stride=st, padding=1, groups=C)
+    torch.cuda.synchronize()
+    assert _rel(out.float(), _nhwc(ref)) < 1e-2
+    assert _rel(dw, dwr) < 1e-2
+    # BN backward: mask from z == mask from the materialised y
+    M = N * H * W
+    zr = z.reshape(M, C)
+    stats = conv.stats_buffer(C, dev)
+    stats.zero_()
+    stats[0, 0].copy_(zr.float().sum(0))
+    stats[0, 1].copy_((zr.float() ** 2).sum(0))
+    g, b = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+    sm, si = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    A = cnn.bn_desc(stats, g, b, None, None, None, sm, si)
+    co2 = torch.empty(2, C, device=dev)
+    cnn.bn_coeff(M, C, A, co2, True)
+    yb = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    cnn.bn_apply(zr, A, yb, train=True, relu=True)
+    torch.cuda.synchronize()
+    assert _rel(torch.relu(zr.float() * co2[0] + co2[1]), yb.float()) < 1e-2
+    dya = torch.randn(M, C, device=dev).bfloat16()
+    outs = []
+    for use_mask in (False, True):
+        dz = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+        dg, db_ = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        red = torch.zeros(3, C, device=dev)
+        if use_mask:
+            cnn.bn_bwd(dya, zr, A, dg, db_, dz, red, mask_bn=co2)
+        else:
+            cnn.bn_bwd(dya, zr, A, dg, db_, dz, red, y=yb)
+        outs.append((dz.float(), dg.clone(), db_.clone()))
+    torch.cuda.synchronize()
+    (dz0, dg0, db0), (dz1, dg1, db1) = outs
+    # y is bf16-rounded: a value at the ReLU edge may flip; everything else is identical math
+    assert _rel(dz1, dz0) < 1e-2 and _rel(dg1, dg0) < 1e-2 and _rel(db1, db0) < 1e-2
+
+
 # full-batch ResNet-18 layer3/4 shapes: few output tiles + long K -> split-K through a workspace
 SPLIT_SHAPES = [
     (128, 8, 8, 256, 256, 3, 1, 1),     # layer3
