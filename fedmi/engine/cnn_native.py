@@ -577,11 +577,13 @@ class CNNNativeTrainer(LocalTrainer):
         """A block whose output feeds ONLY the next block's depthwise conv (no shortcut, no pool, not the
         network output: MobileNet's pointwise -> depthwise chain) skips its BN-apply pass: the BN's
         scale / shift are computed by one small launch, the depthwise forward and weight-gradient
-        kernels apply it on load, and its BN backward derives the ReLU mask from z
-        (FEDMI_CNN_DEFER_BN=0 restores the materialised activation)."""
+        kernels apply it on load, and its BN backward derives the ReLU mask from z.  Opt-in
+        (FEDMI_CNN_DEFER_BN=1): measured slower on MobileNet (profiles/r2_lenet/experiments.md) -- the
+        per-tap transform made the 9-tap depthwise kernels VALU-bound (+86 / +85 us) and the coefficient
+        launches cost 6.9 us each, more than the 112 us of BN-apply passes they removed."""
         import os
 
-        on = os.environ.get("FEDMI_CNN_DEFER_BN", "1") == "1"
+        on = os.environ.get("FEDMI_CNN_DEFER_BN", "0") == "1"
         for b, nxt in zip(self.blocks[:-1], self.blocks[1:]):
             b.defer = bool(on and b.shortcut == "none" and not b.pool and b.out_relu and nxt.main[0].depthwise
                            and nxt.shortcut == "none" and nxt.proj is None)
