@@ -34,11 +34,23 @@ FEDMI_DEV void ld8f(const bf16* p, float* v) {
 
 constexpr int MAXRS = 49;   // up to 7x7 (PNASNet)
 
-// Filter taps staged in LDS as [tap][C] fp32 (8 consecutive channels = 32 B).
+// Filter taps staged in LDS as [tap][C] fp32 (8 consecutive channels = 32 B).  8 loads in flight per
+// thread: a load-use loop paid one memory round trip per C*RS/blockDim taps (18 for a 512-channel 3x3
+// filter, ~half of those layers' 16 us).
 FEDMI_DEV void stage_taps(const float* __restrict__ w, float* wl, int C, int RS) {
-  for (int i = threadIdx.x; i < C * RS; i += blockDim.x) {
-    const int c = i / RS, t = i - c * RS;
-    wl[t * C + c] = w[i];
+  const int n = C * RS, step = blockDim.x;
+  for (int i0 = threadIdx.x; i0 < n; i0 += 8 * step) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = i0 + u * step < n ? w[i0 + u * step] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * step;
+      if (i < n) {
+        const int c = i / RS, t = i - c * RS;
+        wl[t * C + c] = v[u];
+      }
+    }
   }
 }
 
