@@ -268,7 +268,9 @@ DW_SHAPES = [(4, 32, 32, 32, 3, 1), (4, 32, 32, 64, 3, 2), (8, 4, 4, 1024, 3, 1)
              (2, 8, 8, 16, 7, 1),
              # batch-128 MobileNet / MobileNetV2 layers where the wgrad splits channels into chunks
              # (C/8 = 128, 64, 120 -> chunks of 32, 32, 30; 48 -> 24)
-             (128, 2, 2, 1024, 3, 1), (128, 4, 4, 512, 3, 1), (128, 4, 4, 960, 3, 1), (128, 8, 8, 384, 3, 1)]
+             (128, 2, 2, 1024, 3, 1), (128, 4, 4, 512, 3, 1), (128, 4, 4, 960, 3, 1), (128, 8, 8, 384, 3, 1),
+             # odd output widths: the row-pair 3x3 forward's unpaired last column
+             (3, 7, 7, 64, 3, 1), (2, 9, 9, 32, 3, 2)]
 
 
 @pytest.mark.parametrize("shape", DW_SHAPES, ids=[str(s) for s in DW_SHAPES])
