@@ -307,6 +307,28 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16* __restrict__ 
   }
 }
 
+// Sum acc over the pstep threads of the block that share a channel group (LDS, one tap at a
+// time) and write this block's partial ws[blockIdx.x][C][RS] for the chunk's channels.
+template <int RS>
+__device__ __forceinline__ void wgrad_block_reduce(const float (&acc)[RS][8], float* __restrict__ ws, const DwGeom& g,
+                                                   int VCB) {
+  __shared__ float red[256][8];
+  float* out = ws + (long)blockIdx.x * g.C * RS;
+#pragma unroll
+  for (int t = 0; t < RS; ++t) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = acc[t][j];
+    __syncthreads();
+    for (int c = threadIdx.x; c < VCB * 8; c += blockDim.x) {
+      const int grp = c >> 3, j = c & 7;
+      float sum = 0.f;
+      for (int tt = grp; tt < (int)blockDim.x; tt += VCB) sum += red[tt][j];
+      out[(long)(blockIdx.y * VCB * 8 + c) * RS + t] = sum;
+    }
+    __syncthreads();
+  }
+}
+
 // Partial weight gradients: block (b, chunk) sums a contiguous range of output pixels for
 // the VCB channel groups of its chunk (thread -> fixed group), writes ws[b][C][RS] for those
 // channels.  Wide layers are split into channel chunks so that small-spatial / many-channel
@@ -349,22 +371,69 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16* __restrict__ 
       for (int j = 0; j < 8; ++j) acc[t][j] += ok ? v[j] * d[j] : 0.f;
     }
   }
-  // reduce the pstep threads sharing a channel group through LDS, one tap at a time
-  __shared__ float red[256][8];
-  float* out = ws + (long)blockIdx.x * g.C * RS;
+  wgrad_block_reduce<RS>(acc, ws, g, VCB);
+}
+
+// Row-pair 3x3 wgrad (pad 1, stride ST): a thread takes two horizontally adjacent output
+// pixels per step, so the 3 x (ST==1 ? 4 : 5) input columns they share are loaded once:
+// 2 + 12 (15) loads for 18 tap updates instead of 2 x 10.  Pixel blocks range over pairs.
+// The launcher uses it for stride 1 only (see dw_wgrad_pair).
+template <int ST>
+__global__ __launch_bounds__(256) void dw_wgrad3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                        float* __restrict__ ws, DwGeom g, int pairs_per_block,
+                                                        int VCB, const float* __restrict__ isc) {
+  constexpr int NCOL = ST == 1 ? 4 : 5;
+  const int VC = VCB;
+  const int cg = threadIdx.x % VC, lane_pix = threadIdx.x / VC, pstep = blockDim.x / VC;
+  const int c0 = blockIdx.y * VCB * 8 + cg * 8;
+  const int Q2 = (g.Q + 1) >> 1;
+  const long npair = (long)g.N * g.P * Q2;
+  const long pb = (long)blockIdx.x * pairs_per_block, pe = std::min<long>(npair, pb + pairs_per_block);
+  float acc[9][8];
 #pragma unroll
-  for (int t = 0; t < RS; ++t) {
+  for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = acc[t][j];
-    __syncthreads();
-    for (int c = threadIdx.x; c < VCB * 8; c += blockDim.x) {
-      const int grp = c >> 3, j = c & 7;
-      float sum = 0.f;
-      for (int tt = grp; tt < (int)blockDim.x; tt += VC) sum += red[tt][j];
-      out[(long)(blockIdx.y * VCB * 8 + c) * RS + t] = sum;
-    }
-    __syncthreads();
+    for (int j = 0; j < 8; ++j) acc[t][j] = 0.f;
+  float bsc[8], bsh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bsc[j] = isc ? isc[c0 + j] : 1.f;
+    bsh[j] = isc ? isc[g.C + c0 + j] : 0.f;
   }
+  for (uint32_t pr = (uint32_t)(pb + lane_pix); pr < (uint32_t)pe; pr += pstep) {
+    const uint32_t t2 = pr / (uint32_t)Q2;
+    const int q0 = (int)(pr - t2 * Q2) * 2;
+    const int n = (int)(t2 / (uint32_t)g.P), p = (int)(t2 - (uint32_t)n * g.P);
+    const long pix0 = ((long)n * g.P + p) * g.Q + q0;
+    const bool q1ok = q0 + 1 < g.Q;
+    float d0[8], d1[8];
+    ld8f(dy + pix0 * g.C + c0, d0);
+    ld8f(dy + (q1ok ? pix0 + 1 : pix0) * g.C + c0, d1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d1[j] = q1ok ? d1[j] : 0.f;
+    const long nb = (long)n * g.H;
+    const int w0 = q0 * ST - 1;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int h = p * ST - 1 + r;
+      const bool hok = (unsigned)h < (unsigned)g.H;
+      float v[NCOL][8];
+#pragma unroll
+      for (int k = 0; k < NCOL; ++k) {
+        const int ww = w0 + k;
+        const bool ok = hok && (unsigned)ww < (unsigned)g.W;
+        ld8f(x + (ok ? ((nb + h) * g.W + ww) * g.C + c0 : c0), v[k]);
+        if (isc) in_bn8(bsc, bsh, v[k]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = ok ? v[k][j] : 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[r * 3 + s][j] += v[s][j] * d0[j] + v[ST + s][j] * d1[j];
+    }
+  }
+  wgrad_block_reduce<9>(acc, ws, g, VCB);
 }
 
 // dw[i] (+)= sum_b ws[b][i]: block = 16 outputs x 16 partial groups (each thread
@@ -451,10 +520,16 @@ static int dw_wgrad_vcb(const DwGeom& g) {   // largest divisor of C/8 that is <
     if (vc % d == 0) return d;
   return 1;
 }
+// stride 1 only: at stride 2 the pair shares 3 of 5 columns, and measured slower (MobileNet 37 -> 64 us)
+static bool dw_wgrad_pair(const DwGeom& g) { return g.R == 3 && g.st == 1 && g.pad == 1; }
+static long dw_wgrad_items(const DwGeom& g) {   // output pixels, or pixel pairs for the row-pair kernel
+  return dw_wgrad_pair(g) ? (long)g.N * g.P * ((g.Q + 1) / 2) : (long)g.N * g.P * g.Q;
+}
 static int dw_wgrad_blocks(const DwGeom& g) {
-  const long npix = (long)g.N * g.P * g.Q;
+  const long npix = dw_wgrad_items(g);
   const int pstep = block_threads(dw_wgrad_vcb(g) * 8) / dw_wgrad_vcb(g);
-  return (int)std::max<long>(1, std::min<long>(512, (npix + 2 * pstep - 1) / (2 * pstep)));
+  const int per_lane = dw_wgrad_pair(g) ? 1 : 2;   // a pair is already two pixels
+  return (int)std::max<long>(1, std::min<long>(512, (npix + per_lane * pstep - 1) / (per_lane * pstep)));
 }
 
 long dw_wgrad_ws_floats(const DwShape& s) {
@@ -468,12 +543,14 @@ void launch_dw_wgrad(hipStream_t st, const DwShape& s, const bf16* x, const bf16
   const int nblk = dw_wgrad_blocks(g);
   const int n = g.C * g.R * g.S;
   if ((long)nblk * n > ws_floats) throw std::invalid_argument("dw_wgrad: workspace too small");
-  const long npix = (long)g.N * g.P * g.Q;
+  const long npix = dw_wgrad_items(g);
   const int ppb = (int)((npix + nblk - 1) / nblk);
   const int vcb = dw_wgrad_vcb(g);
   const int tb = block_threads(vcb * 8);
   const dim3 grid(nblk, (g.C / 8) / vcb);
-  if (g.R == 3) hipLaunchKernelGGL(dw_wgrad_kernel<9>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb, isc);
+  if (dw_wgrad_pair(g))
+    hipLaunchKernelGGL(dw_wgrad3_kernel<1>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb, isc);
+  else if (g.R == 3) hipLaunchKernelGGL(dw_wgrad_kernel<9>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb, isc);
   else if (g.R == 5) hipLaunchKernelGGL(dw_wgrad_kernel<25>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb, isc);
   else hipLaunchKernelGGL(dw_wgrad_kernel<49>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb, isc);
   hipLaunchKernelGGL(dw_wgrad_reduce, dim3((n + 15) / 16), dim3(256), 0, st, ws, nblk, n, dw, accumulate);
