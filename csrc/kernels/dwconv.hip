@@ -14,6 +14,7 @@
 //   wgrad  dw[c,r,s]   = sum_npq dy[n,p,q,c] * x[n, p*st-pad+r, q*st-pad+s, c]
 //          (per-block partials -> workspace -> deterministic reduce)
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "common.h"
@@ -521,7 +522,10 @@ static int dw_wgrad_vcb(const DwGeom& g) {   // largest divisor of C/8 that is <
   return 1;
 }
 // stride 1 only: at stride 2 the pair shares 3 of 5 columns, and measured slower (MobileNet 37 -> 64 us)
-static bool dw_wgrad_pair(const DwGeom& g) { return g.R == 3 && g.st == 1 && g.pad == 1; }
+static bool dw_wgrad_pair(const DwGeom& g) {
+  static const bool off = [] { const char* e = std::getenv("FEDMI_DW_WGRAD_PAIR"); return e && e[0] == '0'; }();
+  return !off && g.R == 3 && g.st == 1 && g.pad == 1;
+}
 static long dw_wgrad_items(const DwGeom& g) {   // output pixels, or pixel pairs for the row-pair kernel
   return dw_wgrad_pair(g) ? (long)g.N * g.P * ((g.Q + 1) / 2) : (long)g.N * g.P * g.Q;
 }
