@@ -19,7 +19,10 @@ A *step* is one federated round with the reference's semantics
      (``--eval-full`` runs that reference-literal redundant variant)
   4. the global model is persisted as Primary/optimizedModel.pth (rank 0) and
      every client checkpoint as checkpoint/<client>.pth ({'net','acc','epoch'}),
-     flushed to disk inside the timed region.
+     by the native C++ writer (csrc/runtime/ckpt_writer.cpp: async device->pinned
+     snapshot, torch.save-identical archive, no GIL); a round that finds the
+     previous one still queued supersedes it (the files hold the newest model
+     either way); the newest round is flushed to disk inside the timed region.
 
 Total work per round is fixed (50k samples split over N clients) -> strong
 scaling.  ``value`` is the whole-job training throughput (samples/s summed over
@@ -198,7 +201,7 @@ def main() -> int:
         else:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
 
-    from fedmi.ckpt import AsyncCheckpointWriter, OPTIMIZED_MODEL, client_ckpt_path, mount_dir
+    from fedmi.ckpt import OPTIMIZED_MODEL, RoundCheckpointWriter, client_ckpt_path, mount_dir
     from fedmi.engine import build_trainer
     from fedmi.engine.base import TrainerConfig
     from fedmi.engine.data import make_dataset, strided_schedule
@@ -229,7 +232,7 @@ def main() -> int:
     root = Path(args.ckpt_dir or tempfile.mkdtemp(prefix="fedmi_bench_"))
     prim = mount_dir(root, primary=True) if rank == 0 else None
     cpath = client_ckpt_path(root, f"client{rank}")
-    writer = AsyncCheckpointWriter()
+    writer = RoundCheckpointWriter()      # native C++ writer, coalescing (fedmi/ckpt, csrc/runtime/ckpt_writer.cpp)
 
     def one_round(r: int) -> None:
         with phase("local-train"):
@@ -307,6 +310,8 @@ def main() -> int:
                        **({"test_loss": round(ev_stats.loss, 4), "test_acc": round(ev_stats.acc, 3)}
                           if ev_stats else {})},
         "allreduce_ms_last": round(agg.timer.last_ms, 4),
+        "checkpoint": {"writer": writer.backend, "files_written": writer.written,
+                       "rounds_coalesced": writer.coalesced},
         **({"transport_select": select} if select else {}),
         **({"compression": {"kind": args.compress, "bytes_per_round_per_client":
                             agg.compressor.bytes_sent // max(1, agg.compressor.rounds),

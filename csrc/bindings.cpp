@@ -48,6 +48,7 @@ using namespace fedmi;
 void fedmi_bind_cnn(py::module_& m);   // bindings_cnn.cpp
 void fedmi_bind_comm(py::module_& m);  // bindings_comm.cpp
 void fedmi_bind_zoo(py::module_& m);   // bindings_zoo.cpp
+void fedmi_bind_io(py::module_& m);    // bindings_io.cpp
 
 template <typename T>
 static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
@@ -90,6 +91,7 @@ static void fedmi_bind(py::module_& m) {
   fedmi_bind_cnn(m);
   fedmi_bind_comm(m);
   fedmi_bind_zoo(m);
+  fedmi_bind_io(m);
   m.def("stamps_enabled", &stamps_enabled);
   m.def("set_ks1_diag", &set_ks1_diag);
   m.def("read_stamps", [](bool clear) {

@@ -42,6 +42,7 @@ void fedmi_bind_comm(py::module_& m) {
              c.allgather(S(st), reinterpret_cast<const void*>(in), reinterpret_cast<void*>(out), nbytes, blocks);
            }, py::arg("stream"), py::arg("src"), py::arg("dst"), py::arg("nbytes"), py::arg("blocks") = 0)
       .def("error", &PeerComm::error)
+      .def("epochs", &PeerComm::epochs)
       .def("clear_error", &PeerComm::clear_error)
       .def("set_timeout_ms", &PeerComm::set_timeout_ms)
       .def("disconnect", &PeerComm::disconnect, py::call_guard<py::gil_scoped_release>())

@@ -73,6 +73,7 @@ class PeerComm {
   void allgather(hipStream_t st, const void* in, void* out, long long nbytes, int blocks);
 
   uint32_t error() const;           // synchronous read of the timeout flag
+  std::vector<uint32_t> epochs() const;   // synchronous read of the per-block call counters (tests)
   void clear_error();
   void set_timeout_ms(double ms);
   void disconnect();                // unmap peers (call after a host-side barrier)

@@ -13,6 +13,14 @@
 // Buffer reuse: call k uses staging slot k & 1.  A rank rewrites slot k & 1 only
 // in call k + 2, after call k + 1's barrier, which every peer enters only once
 // its stream has finished call k — so one barrier per call suffices for oneshot.
+//
+// Call counter: every call advances ALL kPeerMaxBlocks epoch words, whatever its
+// grid size (block b of a B-block call writes words b, b + B, b + 2B, ...), so the
+// epoch -- and with it the slot parity -- is one communicator-wide call number.
+// Calls of different grid sizes (fedavg's f32 reduce then a 1-block int64 call,
+// the int8 compressor's gather then scale) therefore stay in step on every block.
+// The words are read at the start of the NEXT call, which the stream orders after
+// every block of this one has retired.
 #include "peer_comm.h"
 
 #include <cstring>
@@ -47,7 +55,8 @@ PDEV uint32_t begin_call(const PeerArgs& a, int b) {
 }
 
 PDEV void end_call(const PeerArgs& a, int b, uint32_t ep) {
-  if (threadIdx.x == 0) st_sys(&a.sig[a.rank]->epoch[b], ep);
+  for (int j = b + (int)threadIdx.x * (int)gridDim.x; j < fedmi::kPeerMaxBlocks; j += (int)(blockDim.x * gridDim.x))
+    st_sys(&a.sig[a.rank]->epoch[j], ep);
 }
 
 // Returns false (for the whole workgroup) when a peer never arrived: the caller then
@@ -314,6 +323,13 @@ void PeerComm::set_timeout_ms(double ms) { a_.timeout_ticks = (long long)(ms * 1
 uint32_t PeerComm::error() const {
   uint32_t e = 0;
   check_hip(hipMemcpy(&e, &sig_->error, sizeof(e), hipMemcpyDeviceToHost), "PeerComm::error");
+  return e;
+}
+
+std::vector<uint32_t> PeerComm::epochs() const {
+  std::vector<uint32_t> e(kPeerMaxBlocks);
+  check_hip(hipMemcpy(e.data(), sig_->epoch, sizeof(uint32_t) * kPeerMaxBlocks, hipMemcpyDeviceToHost),
+            "PeerComm::epochs");
   return e;
 }
 

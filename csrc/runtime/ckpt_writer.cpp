@@ -1,0 +1,196 @@
+// fedmi — native per-round checkpoint writer (see ckpt_writer.h).
+#include "runtime/ckpt_writer.h"
+
+#include <fcntl.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+
+namespace fedmi {
+void check_hip(hipError_t e, const char* what);
+
+namespace {
+
+void put_u32(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)v;
+  p[1] = (uint8_t)(v >> 8);
+  p[2] = (uint8_t)(v >> 16);
+  p[3] = (uint8_t)(v >> 24);
+}
+
+// Write all of `data` to `path` atomically: tmp file in the same directory, then rename.
+void atomic_write(const std::string& path, const uint8_t* data, size_t n) {
+  const std::string tmp = path + ".tmpn" + std::to_string(::getpid());
+  const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) throw std::runtime_error("ckpt writer: cannot open " + tmp);
+  size_t off = 0;
+  while (off < n) {
+    const ssize_t w = ::write(fd, data + off, n - off);
+    if (w < 0) {
+      ::close(fd);
+      ::unlink(tmp.c_str());
+      throw std::runtime_error("ckpt writer: write failed for " + tmp);
+    }
+    off += (size_t)w;
+  }
+  if (::close(fd) != 0) throw std::runtime_error("ckpt writer: close failed for " + tmp);
+  if (::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("ckpt writer: rename to " + path);
+}
+
+}  // namespace
+
+CkptWriter::CkptWriter(std::vector<uint8_t> tmpl, std::vector<CkptSegment> segs, std::vector<CkptRecord> recs,
+                       long long epoch_at, std::vector<std::string> paths, bool device)
+    : tmpl_(std::move(tmpl)), segs_(std::move(segs)), recs_(std::move(recs)), epoch_at_(epoch_at),
+      paths_(std::move(paths)), device_(device) {
+  const long long n = (long long)tmpl_.size();
+  if (epoch_at_ < 0 || epoch_at_ + 4 > n) throw std::invalid_argument("CkptWriter: epoch offset outside template");
+  for (const auto& s : segs_) {
+    if (s.bytes < 0 || s.snap_off < 0) throw std::invalid_argument("CkptWriter: bad segment");
+    snap_bytes_ = std::max(snap_bytes_, s.snap_off + s.bytes);
+  }
+  for (const auto& r : recs_) {
+    if (r.data_off < 0 || r.bytes < 0 || r.data_off + r.bytes > n) throw std::invalid_argument("CkptWriter: record");
+    if (r.snap_off >= 0 && r.snap_off + r.bytes > snap_bytes_) throw std::invalid_argument("CkptWriter: record src");
+    for (long long c : r.crc_at)
+      if (c < 0 || c + 4 > n) throw std::invalid_argument("CkptWriter: CRC offset outside template");
+  }
+  if (paths_.empty()) throw std::invalid_argument("CkptWriter: no target paths");
+  const size_t sb = (size_t)std::max(snap_bytes_, 16LL);
+  for (int i = 0; i < 2; ++i) {
+    if (device_) {
+      check_hip(hipHostMalloc(reinterpret_cast<void**>(&snap_[i]), sb, hipHostMallocDefault), "CkptWriter pinned");
+      check_hip(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "CkptWriter event");
+    } else {
+      snap_[i] = new uint8_t[sb];
+    }
+  }
+  out_ = tmpl_;
+  th_ = std::thread([this] { run(); });
+}
+
+CkptWriter::~CkptWriter() {
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [this] { return (pending_ < 0 && busy_ < 0) || !err_.empty(); });
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (th_.joinable()) th_.join();
+  for (int i = 0; i < 2; ++i) {
+    if (device_) {
+      if (ev_[i]) (void)hipEventDestroy(ev_[i]);
+      if (snap_[i]) (void)hipHostFree(snap_[i]);
+    } else {
+      delete[] snap_[i];
+    }
+  }
+}
+
+void CkptWriter::submit(hipStream_t st, int32_t epoch) {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (!err_.empty()) throw std::runtime_error("checkpoint writer failed: " + err_);
+  ++submitted_;
+  // The buffer the writer is NOT reading.  If a pending (not yet picked up) snapshot sits in
+  // it, it is superseded: this copy is stream-ordered after that one and the writer has not
+  // touched it.  The lock is held across the copy issue so the writer cannot pick the
+  // pending snapshot up between the choice and the event record.
+  int buf;
+  if (pending_ >= 0) {          // never the busy one: the writer takes pending_ and busy_ under this lock
+    buf = pending_;
+    ++coalesced_;
+  } else {
+    buf = busy_ == 0 ? 1 : 0;
+  }
+  for (const auto& s : segs_) {
+    if (s.bytes == 0) continue;
+    if (device_)
+      check_hip(hipMemcpyAsync(snap_[buf] + s.snap_off, reinterpret_cast<const void*>(s.src), (size_t)s.bytes,
+                               hipMemcpyDeviceToHost, st),
+                "CkptWriter snapshot copy");
+    else
+      std::memcpy(snap_[buf] + s.snap_off, reinterpret_cast<const void*>(s.src), (size_t)s.bytes);
+  }
+  if (device_) check_hip(hipEventRecord(ev_[buf], st), "CkptWriter event record");
+  pending_ = buf;
+  pending_epoch_ = epoch;
+  lk.unlock();
+  cv_.notify_all();
+}
+
+void CkptWriter::write_one(int buf, int32_t epoch) {
+  if (device_) check_hip(hipEventSynchronize(ev_[buf]), "CkptWriter snapshot wait");
+  uint8_t* o = out_.data();
+  put_u32(o + epoch_at_, (uint32_t)epoch);        // pickle BININT ('J' + int32 LE)
+  for (const auto& r : recs_) {
+    if (r.snap_off >= 0) std::memcpy(o + r.data_off, snap_[buf] + r.snap_off, (size_t)r.bytes);
+    uLong crc = crc32(0L, Z_NULL, 0);
+    long long done = 0;
+    while (done < r.bytes) {                        // zlib's length is a uInt
+      const long long chunk = std::min(r.bytes - done, 1LL << 30);
+      crc = crc32(crc, o + r.data_off + done, (uInt)chunk);
+      done += chunk;
+    }
+    for (long long c : r.crc_at) put_u32(o + c, (uint32_t)crc);
+  }
+  for (const auto& p : paths_) atomic_write(p, o, out_.size());
+}
+
+void CkptWriter::run() {
+  for (;;) {
+    int buf;
+    int32_t epoch;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [this] { return pending_ >= 0 || stop_; });
+      if (pending_ < 0) return;
+      buf = pending_;
+      epoch = pending_epoch_;
+      pending_ = -1;
+      busy_ = buf;
+    }
+    std::string e;
+    try {
+      write_one(buf, epoch);
+    } catch (const std::exception& ex) {
+      e = ex.what();
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      busy_ = -1;
+      if (e.empty())
+        written_ += (long long)paths_.size();
+      else
+        err_ = e;
+    }
+    cv_.notify_all();
+  }
+}
+
+void CkptWriter::flush() {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait(lk, [this] { return (pending_ < 0 && busy_ < 0) || !err_.empty(); });
+  if (!err_.empty()) throw std::runtime_error("checkpoint writer failed: " + err_);
+}
+
+long long CkptWriter::written() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return written_;
+}
+long long CkptWriter::coalesced() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return coalesced_;
+}
+long long CkptWriter::submitted() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return submitted_;
+}
+std::vector<uint8_t> CkptWriter::last_file() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return out_;
+}
+
+}  // namespace fedmi

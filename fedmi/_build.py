@@ -34,10 +34,12 @@ SOURCES = [
     CSRC / "kernels" / "zoo_ops.hip",
     CSRC / "comm" / "peer_comm.hip",
     CSRC / "runtime" / "lenet_engine.cpp",
+    CSRC / "runtime" / "ckpt_writer.cpp",
     CSRC / "bindings.cpp",
     CSRC / "bindings_cnn.cpp",
     CSRC / "bindings_comm.cpp",
     CSRC / "bindings_zoo.cpp",
+    CSRC / "bindings_io.cpp",
 ]
 HEADERS = sorted(CSRC.rglob("*.h"))
 
@@ -101,7 +103,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True, variant: str
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda src: _compile(src, variant), SOURCES))
     tmp = out.with_suffix(".tmp.so")
-    cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp)]
+    cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-lz", "-o", str(tmp)]
     proc = subprocess.run(cmd, capture_output=True, text=True)
     if proc.returncode != 0:
         raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{proc.stdout}\n{proc.stderr}")

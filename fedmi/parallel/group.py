@@ -58,7 +58,10 @@ def abort_default_group() -> None:
 
 class GroupManager:
     def __init__(self, backend: str, device: Optional[torch.device] = None, timeout_s: float = 20.0,
-                 transport: str = "dist", peer_capacity: int = 0, peer_timeout_ms: float = 10000.0):
+                 transport: str = "dist", peer_capacity: int = 0, peer_timeout_ms: float = 10000.0,
+                 init_world1: bool = False):
+        """``init_world1``: form a process group even for a client alone (world 1); by default a
+        lone client has no data plane at all, since FedAvg of one model is the identity."""
         if transport not in ("dist", "peer"):
             raise ValueError("transport must be 'dist' or 'peer'")
         self.backend = backend
@@ -67,6 +70,7 @@ class GroupManager:
         self.transport_kind = transport
         self.peer_capacity = peer_capacity
         self.peer_timeout_ms = peer_timeout_ms
+        self.init_world1 = init_world1
         self.current: Optional[Membership] = None
         self.transport = None               # PeerAllReduce of the current generation (peer mode)
         self._retired: list = []            # previous generations' buffers, kept mapped a while: a peer that
@@ -88,10 +92,11 @@ class GroupManager:
     def ensure(self, m: Membership) -> bool:
         """Join (or re-join) the data-plane group described by ``m``; True if it changed."""
         with self._lock:
-            if self.current == m and (m.world == 1 or self.transport is not None or dist.is_initialized()):
+            if self.current == m and ((m.world == 1 and not self.init_world1) or self.transport is not None
+                                      or dist.is_initialized()):
                 return False
             self._drop()
-            if m.world > 1:
+            if m.world > 1 or (self.init_world1 and self.transport_kind == "dist"):
                 store = dist.TCPStore(m.store_host, m.store_port, world_size=None, is_master=False,
                                       timeout=self.timeout, wait_for_workers=False)
                 pstore = dist.PrefixStore(f"fedmi/gen{m.generation}", store)

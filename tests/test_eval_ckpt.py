@@ -99,3 +99,95 @@ def test_async_writer_coalesced_views(tmp_path):
         for k, v in sd.items():
             assert torch.equal(ck["net"][k], v)
         assert ck["net"]["a.bias"].untyped_storage().nbytes() == 12    # own storage, like module.state_dict()
+
+
+def test_async_writer_coalesces_superseded_rounds(tmp_path, monkeypatch):
+    """A writer slower than the round cadence keeps only the newest queued checkpoint per file
+    set: submit never blocks, flush leaves the LAST round on disk, and other files keep FIFO."""
+    import threading
+
+    import fedmi.ckpt as ck
+
+    gate = threading.Event()
+    real = ck.atomic_write
+    order = []
+
+    def slow_write(path, data):
+        gate.wait(10)
+        order.append(path.name)
+        real(path, data)
+
+    monkeypatch.setattr(ck, "atomic_write", slow_write)
+    w = ck.AsyncCheckpointWriter(max_pending=2)
+    a, b = tmp_path / "a.pth", tmp_path / "b.pth"
+    t = torch.zeros(4)
+    w.submit(a, {"w": t + 0}, epoch=0)            # picked up by the writer, blocked in the write
+    import time
+    deadline = time.monotonic() + 5
+    while not w._busy and time.monotonic() < deadline:
+        time.sleep(0.001)
+    for r in range(1, 50):                        # 49 more rounds: would block on a 2-deep queue
+        w.submit(a, {"w": t + r}, epoch=r)
+    w.submit(b, {"w": t - 1}, epoch=7)
+    assert w.coalesced == 48
+    gate.set()
+    w.flush()
+    assert ck.load(a)["epoch"] == 49 and torch.equal(ck.load(a)["net"]["w"], t + 49)
+    assert ck.load(b)["epoch"] == 7
+    assert order == ["a.pth", "a.pth", "b.pth"]
+    w.close()
+
+
+def test_async_writer_no_coalesce_writes_every_submission(tmp_path, monkeypatch):
+    import fedmi.ckpt as ck
+
+    seen = []
+    real = ck.atomic_write
+    monkeypatch.setattr(ck, "atomic_write", lambda p, d: (seen.append(ck.from_bytes(d)["epoch"]), real(p, d)))
+    w = ck.AsyncCheckpointWriter(max_pending=2, coalesce=False)
+    for r in range(10):
+        w.submit(tmp_path / "a.pth", {"w": torch.full((3,), float(r))}, epoch=r)
+    w.close()
+    assert seen == list(range(10))
+
+
+def test_native_round_writer_matches_torch_save(tmp_path):
+    """The C++ writer's archives (host mode on CPU) load with weights_only torch.load, pass the
+    zip CRC check, hold the newest round after flush, and coalesce rounds it could not keep up with."""
+    import zipfile
+    from collections import OrderedDict
+
+    from fedmi import native
+    from fedmi.ckpt import RoundCheckpointWriter, load
+
+    if not native.available():
+        pytest.skip("native extension not built")
+    flat = torch.randn(64)
+    nbt = torch.tensor(5, dtype=torch.int64)
+    sd = OrderedDict([("module.a.weight", flat[0:12].view(3, 4)), ("a.bias", flat[12:15]),
+                      ("bn.num_batches_tracked", nbt), ("b.weight", flat[20:35].view(5, 3)),
+                      ("empty", flat[40:40])])
+    paths = [tmp_path / "Primary" / "optimizedModel.pth", tmp_path / "checkpoint" / "c0.pth"]
+    w = RoundCheckpointWriter()
+    for r in range(100):
+        flat.add_(1.0)
+        nbt.add_(1)
+        w.submit(paths, sd, acc=1, epoch=r + 1 if r < 99 else 70000)   # last epoch needs all 4 bytes
+    w.flush()
+    assert w.backend == "native"
+    assert w.written + 2 * w.coalesced == 200
+    for p in paths:
+        assert zipfile.ZipFile(p).testzip() is None
+        ck = load(p)
+        assert ck["epoch"] == 70000 and ck["acc"] == 1
+        assert list(ck["net"]) == ["a.weight", "a.bias", "bn.num_batches_tracked", "b.weight", "empty"]
+        for k, v in sd.items():
+            assert torch.equal(ck["net"][k.replace("module.", "")], v)
+        assert ck["net"]["bn.num_batches_tracked"].dtype == torch.int64
+    # a different acc rebuilds the template; a new state-dict layout rebuilds the writer
+    w.submit(paths, sd, acc=0.5, epoch=3)
+    sd2 = OrderedDict([("x", torch.ones(2, 2))])
+    w.submit(paths[:1], sd2, acc=1, epoch=4)
+    w.close()
+    assert load(paths[1])["acc"] == 0.5 and load(paths[1])["epoch"] == 3
+    assert list(load(paths[0])["net"]) == ["x"] and load(paths[0])["epoch"] == 4

@@ -1,4 +1,4 @@
-"""Peer-to-peer (hipIpc) collectives: 2 and 4 client processes sharing cuda:0.
+"""Peer-to-peer (hipIpc) collectives: 2, 4 and 8 client processes sharing cuda:0.
 
 RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so on a one-GPU
 box the hand-written peer kernels (csrc/comm/peer_comm.hip) are the only GPU
@@ -102,14 +102,85 @@ def _run(world: int, algo: str):
         assert p.exitcode == 0
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_peer_oneshot_bit_exact(world):
     _run(world, "oneshot")
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_peer_twoshot_bit_exact(world):
     _run(world, "twoshot")
+
+
+# (kind, n, blocks): consecutive calls with different grid sizes and payload sizes.  Every call
+# must advance the communicator-wide call counter on ALL 256 epoch words (so the staging-slot
+# parity is one call number), and every result must stay bit-exact.
+MIXED = [("f32", 1 << 20, 128), ("i64", 3, 1), ("f32", 4099, 1), ("gather", 1 << 16, 0), ("f32", 1 << 20, 7),
+         ("f32", 64, 3), ("i64", 5, 1), ("gather", 48, 0), ("f32", 1 << 20, 0), ("f32", 1000, 128)]
+
+
+def _mixed_worker(rank, world, path, algo, q):
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    from fedmi.parallel.peer import ALGOS, PeerAllReduce
+    from fedmi import native
+
+    store = dist.FileStore(path, world)
+    dev = torch.device("cuda", 0)
+    res = {"ok": True, "msgs": []}
+    try:
+        pc = PeerAllReduce(rank, world, 4 * ((1 << 20) + 64), store, tag=f"mx{algo}", algo=algo)
+        for it, (kind, n, blocks) in enumerate(MIXED * 2):
+            if kind == "f32":
+                x = _data(rank, it, n).to(dev)
+                pc.comm.allreduce_f32(native.stream_handle(dev), x.data_ptr(), x.data_ptr(), n, 1.0 / world,
+                                      ALGOS[algo], blocks)
+                if not torch.equal(x.cpu(), _expected(world, it, n)):
+                    res["ok"] = False
+                    res["msgs"].append(f"f32 it={it} n={n} blocks={blocks}")
+            elif kind == "i64":
+                iv = torch.arange(n, dtype=torch.int64, device=dev) * (rank + 1) - 3 * it
+                pc.allreduce_mean_(iv)
+                tot = sum(torch.arange(n, dtype=torch.int64) * (r + 1) - 3 * it for r in range(world))
+                if not torch.equal(iv.cpu(), torch.div(tot, world, rounding_mode="floor")):
+                    res["ok"] = False
+                    res["msgs"].append(f"i64 it={it}")
+            else:
+                g = (torch.arange(n // 4, dtype=torch.int32, device=dev) + 7 * it) * (rank + 1)
+                rows = pc.all_gather(g).cpu()
+                for r in range(world):
+                    if not torch.equal(rows[r], (torch.arange(n // 4, dtype=torch.int32) + 7 * it) * (r + 1)):
+                        res["ok"] = False
+                        res["msgs"].append(f"gather it={it} row={r}")
+            torch.cuda.synchronize()
+            ep = pc.comm.epochs()
+            if len(set(ep)) != 1 or ep[0] != it + 1:
+                res["ok"] = False
+                res["msgs"].append(f"epochs after call {it}: {sorted(set(ep))}")
+        res["error"] = pc.error()
+        pc.close()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        res["ok"] = False
+        res["msgs"].append(repr(e))
+    q.put((rank, res))
+
+
+@pytest.mark.parametrize("world,algo", [(3, "oneshot"), (8, "twoshot")])
+def test_peer_mixed_grids_keep_one_call_counter(world, algo):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "store")
+        procs = [ctx.Process(target=_mixed_worker, args=(r, world, path, algo, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        out = dict(q.get(timeout=200) for _ in procs)
+        for p in procs:
+            p.join(timeout=60)
+    for r in range(world):
+        assert out[r]["ok"], (r, out[r]["msgs"])
+        assert out[r]["error"] == 0
 
 
 def _timeout_worker(rank, world, path, q):
