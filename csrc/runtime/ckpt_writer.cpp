@@ -43,10 +43,11 @@ void atomic_write(const std::string& path, const uint8_t* data, size_t n) {
 }  // namespace
 
 CkptWriter::CkptWriter(std::vector<uint8_t> tmpl, std::vector<CkptSegment> segs, std::vector<CkptRecord> recs,
-                       long long epoch_at, std::vector<std::string> paths, bool device)
+                       long long epoch_at, std::vector<std::string> paths, bool device, int slots, bool coalesce)
     : tmpl_(std::move(tmpl)), segs_(std::move(segs)), recs_(std::move(recs)), epoch_at_(epoch_at),
-      paths_(std::move(paths)), device_(device) {
+      paths_(std::move(paths)), device_(device), coalesce_(coalesce) {
   const long long n = (long long)tmpl_.size();
+  if (slots < 1 || slots > 64) throw std::invalid_argument("CkptWriter: slots must be in [1, 64]");
   if (epoch_at_ < 0 || epoch_at_ + 4 > n) throw std::invalid_argument("CkptWriter: epoch offset outside template");
   for (const auto& s : segs_) {
     if (s.bytes < 0 || s.snap_off < 0) throw std::invalid_argument("CkptWriter: bad segment");
@@ -60,13 +61,17 @@ CkptWriter::CkptWriter(std::vector<uint8_t> tmpl, std::vector<CkptSegment> segs,
   }
   if (paths_.empty()) throw std::invalid_argument("CkptWriter: no target paths");
   const size_t sb = (size_t)std::max(snap_bytes_, 16LL);
-  for (int i = 0; i < 2; ++i) {
+  snap_.assign(slots, nullptr);
+  ev_.assign(slots, nullptr);
+  epoch_.assign(slots, 0);
+  for (int i = 0; i < slots; ++i) {
     if (device_) {
       check_hip(hipHostMalloc(reinterpret_cast<void**>(&snap_[i]), sb, hipHostMallocDefault), "CkptWriter pinned");
       check_hip(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "CkptWriter event");
     } else {
       snap_[i] = new uint8_t[sb];
     }
+    free_.push_back(slots - 1 - i);
   }
   out_ = tmpl_;
   th_ = std::thread([this] { run(); });
@@ -75,12 +80,12 @@ CkptWriter::CkptWriter(std::vector<uint8_t> tmpl, std::vector<CkptSegment> segs,
 CkptWriter::~CkptWriter() {
   {
     std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait(lk, [this] { return (pending_ < 0 && busy_ < 0) || !err_.empty(); });
+    cv_.wait(lk, [this] { return (queue_.empty() && busy_ < 0) || !err_.empty(); });
     stop_ = true;
   }
   cv_.notify_all();
   if (th_.joinable()) th_.join();
-  for (int i = 0; i < 2; ++i) {
+  for (size_t i = 0; i < snap_.size(); ++i) {
     if (device_) {
       if (ev_[i]) (void)hipEventDestroy(ev_[i]);
       if (snap_[i]) (void)hipHostFree(snap_[i]);
@@ -94,39 +99,41 @@ void CkptWriter::submit(hipStream_t st, int32_t epoch) {
   std::unique_lock<std::mutex> lk(mu_);
   if (!err_.empty()) throw std::runtime_error("checkpoint writer failed: " + err_);
   ++submitted_;
-  // The buffer the writer is NOT reading.  If a pending (not yet picked up) snapshot sits in
-  // it, it is superseded: this copy is stream-ordered after that one and the writer has not
-  // touched it.  The lock is held across the copy issue so the writer cannot pick the
-  // pending snapshot up between the choice and the event record.
-  int buf;
-  if (pending_ >= 0) {          // never the busy one: the writer takes pending_ and busy_ under this lock
-    buf = pending_;
+  int slot;
+  if (free_.empty() && coalesce_ && !queue_.empty()) {
+    // every slot taken: supersede the newest queued snapshot (the writer has not touched it; this
+    // copy is stream-ordered after the one it replaces)
+    slot = queue_.back();
     ++coalesced_;
   } else {
-    buf = busy_ == 0 ? 1 : 0;
+    cv_.wait(lk, [this] { return !free_.empty() || !err_.empty(); });
+    if (!err_.empty()) throw std::runtime_error("checkpoint writer failed: " + err_);
+    slot = free_.back();
+    free_.pop_back();
+    queue_.push_back(slot);
   }
+  // the copy is issued under the lock: the writer cannot pick the slot up before its event is recorded
   for (const auto& s : segs_) {
     if (s.bytes == 0) continue;
     if (device_)
-      check_hip(hipMemcpyAsync(snap_[buf] + s.snap_off, reinterpret_cast<const void*>(s.src), (size_t)s.bytes,
+      check_hip(hipMemcpyAsync(snap_[slot] + s.snap_off, reinterpret_cast<const void*>(s.src), (size_t)s.bytes,
                                hipMemcpyDeviceToHost, st),
                 "CkptWriter snapshot copy");
     else
-      std::memcpy(snap_[buf] + s.snap_off, reinterpret_cast<const void*>(s.src), (size_t)s.bytes);
+      std::memcpy(snap_[slot] + s.snap_off, reinterpret_cast<const void*>(s.src), (size_t)s.bytes);
   }
-  if (device_) check_hip(hipEventRecord(ev_[buf], st), "CkptWriter event record");
-  pending_ = buf;
-  pending_epoch_ = epoch;
+  if (device_) check_hip(hipEventRecord(ev_[slot], st), "CkptWriter event record");
+  epoch_[slot] = epoch;
   lk.unlock();
   cv_.notify_all();
 }
 
-void CkptWriter::write_one(int buf, int32_t epoch) {
-  if (device_) check_hip(hipEventSynchronize(ev_[buf]), "CkptWriter snapshot wait");
+void CkptWriter::write_one(int slot, int32_t epoch) {
+  if (device_) check_hip(hipEventSynchronize(ev_[slot]), "CkptWriter snapshot wait");
   uint8_t* o = out_.data();
   put_u32(o + epoch_at_, (uint32_t)epoch);        // pickle BININT ('J' + int32 LE)
   for (const auto& r : recs_) {
-    if (r.snap_off >= 0) std::memcpy(o + r.data_off, snap_[buf] + r.snap_off, (size_t)r.bytes);
+    if (r.snap_off >= 0) std::memcpy(o + r.data_off, snap_[slot] + r.snap_off, (size_t)r.bytes);
     uLong crc = crc32(0L, Z_NULL, 0);
     long long done = 0;
     while (done < r.bytes) {                        // zlib's length is a uInt
@@ -141,26 +148,27 @@ void CkptWriter::write_one(int buf, int32_t epoch) {
 
 void CkptWriter::run() {
   for (;;) {
-    int buf;
+    int slot;
     int32_t epoch;
     {
       std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [this] { return pending_ >= 0 || stop_; });
-      if (pending_ < 0) return;
-      buf = pending_;
-      epoch = pending_epoch_;
-      pending_ = -1;
-      busy_ = buf;
+      cv_.wait(lk, [this] { return !queue_.empty() || stop_; });
+      if (queue_.empty()) return;
+      slot = queue_.front();
+      queue_.pop_front();
+      epoch = epoch_[slot];
+      busy_ = slot;
     }
     std::string e;
     try {
-      write_one(buf, epoch);
+      write_one(slot, epoch);
     } catch (const std::exception& ex) {
       e = ex.what();
     }
     {
       std::lock_guard<std::mutex> lk(mu_);
       busy_ = -1;
+      free_.push_back(slot);
       if (e.empty())
         written_ += (long long)paths_.size();
       else
@@ -172,7 +180,7 @@ void CkptWriter::run() {
 
 void CkptWriter::flush() {
   std::unique_lock<std::mutex> lk(mu_);
-  cv_.wait(lk, [this] { return (pending_ < 0 && busy_ < 0) || !err_.empty(); });
+  cv_.wait(lk, [this] { return (queue_.empty() && busy_ < 0) || !err_.empty(); });
   if (!err_.empty()) throw std::runtime_error("checkpoint writer failed: " + err_);
 }
 

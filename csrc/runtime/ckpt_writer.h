@@ -14,10 +14,14 @@
 //     and the CRC-32s of the changed records rewritten (data descriptor + central
 //     directory) -- byte-for-byte what torch.save would have written.
 //   * submit(): ONE async device->pinned-host copy per source storage on the
-//     caller's stream + an event, into whichever of two snapshot buffers the writer
-//     is not reading.  Never waits for the GPU or for I/O.
-//   * coalescing: a submission that finds the previous one still queued (the writer
-//     is busy) replaces it -- the files hold the newest model either way.
+//     caller's stream + an event, into a free slot of a ring of `slots` pinned
+//     snapshot buffers.  It never waits for the GPU or for I/O while a slot is free.
+//   * every submission is written, in order (the reference writes every round).  A
+//     host running more than `slots` rounds ahead of the writer waits for a slot --
+//     the GPU queue then already holds that many rounds of work.  Optional
+//     coalescing (`coalesce`): with every slot taken, a submission replaces the
+//     newest queued one instead of waiting (the files hold the newest model either
+//     way); the coordinator-side persister works like that.
 //   * the writer thread waits for the event, assembles the archive, CRCs it and
 //     writes every target path atomically (tmp file + rename).
 #pragma once
@@ -25,6 +29,7 @@
 #include <stdint.h>
 
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -50,7 +55,7 @@ class CkptWriter {
   // device: true = segments are device pointers copied on a stream (pinned snapshots);
   //         false = host pointers copied synchronously (CPU hosts / tests).
   CkptWriter(std::vector<uint8_t> tmpl, std::vector<CkptSegment> segs, std::vector<CkptRecord> recs,
-             long long epoch_at, std::vector<std::string> paths, bool device);
+             long long epoch_at, std::vector<std::string> paths, bool device, int slots = 4, bool coalesce = false);
   ~CkptWriter();
   CkptWriter(const CkptWriter&) = delete;
   CkptWriter& operator=(const CkptWriter&) = delete;
@@ -72,14 +77,17 @@ class CkptWriter {
   long long epoch_at_;
   std::vector<std::string> paths_;
   bool device_;
+  bool coalesce_;
   long long snap_bytes_ = 0;
-  uint8_t* snap_[2] = {nullptr, nullptr};
-  hipEvent_t ev_[2] = {nullptr, nullptr};
+  std::vector<uint8_t*> snap_;
+  std::vector<hipEvent_t> ev_;
+  std::vector<int32_t> epoch_;           // epoch of the snapshot in each slot
 
   mutable std::mutex mu_;
   std::condition_variable cv_;
-  int pending_ = -1, busy_ = -1;
-  int32_t pending_epoch_ = 0;
+  std::vector<int> free_;                // free slots
+  std::deque<int> queue_;                // submitted, not yet picked up (FIFO)
+  int busy_ = -1;                        // slot the writer is reading
   bool stop_ = false;
   std::string err_;
   long long written_ = 0, coalesced_ = 0, submitted_ = 0;

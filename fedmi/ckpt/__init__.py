@@ -83,6 +83,19 @@ def load(path: Path | str) -> dict:
         return from_bytes(f.read())
 
 
+def state_digest(net) -> str:
+    """Hash of the bytes of every floating-point entry of a state dict (key order): an exact identity
+    check that two processes hold the same model, independent of reduction order or thread count."""
+    import hashlib
+
+    h = hashlib.blake2b(digest_size=16)
+    for k, v in net.items():
+        if v.is_floating_point():
+            h.update(k.encode())
+            h.update(v.detach().to("cpu").contiguous().view(-1).view(torch.uint8).numpy().tobytes())
+    return h.hexdigest()
+
+
 def read_epoch(path: Path | str) -> Optional[int]:
     try:
         return int(load(path).get("epoch", 0))
@@ -321,11 +334,14 @@ class NativeCheckpointWriter:
     once and parsed into record offsets; every later ``submit`` is one async
     device->pinned copy per source storage + an event, and the C++ writer patches
     storages, epoch and CRC-32s into the template -- the same bytes torch.save
-    writes.  Rounds submitted while the writer is busy are coalesced (newest wins).
-    Raises ``ValueError`` for state dicts it cannot map (mixed devices,
-    non-contiguous tensors); :class:`RoundCheckpointWriter` then uses Python."""
+    writes.  Every submission is written in order; ``slots`` snapshot buffers
+    bound how far the host may run ahead (``submit`` waits for a free one), or,
+    with ``coalesce``, a submission that finds every slot taken supersedes the
+    newest queued one.  Raises ``ValueError`` for state dicts it cannot map
+    (mixed devices, non-contiguous tensors); :class:`RoundCheckpointWriter` then
+    uses Python."""
 
-    def __init__(self, paths, state_dict, acc=1):
+    def __init__(self, paths, state_dict, acc=1, slots: int = 4, coalesce: bool = False):
         from .. import native
 
         nat = native.require()
@@ -384,7 +400,7 @@ class NativeCheckpointWriter:
         self.paths = [str(Path(p)) for p in paths]
         for p in self.paths:
             Path(p).parent.mkdir(parents=True, exist_ok=True)
-        self.w = nat.CkptWriter(blob, segs, recs, at + 1, self.paths, self.device)
+        self.w = nat.CkptWriter(blob, segs, recs, at + 1, self.paths, self.device, int(slots), bool(coalesce))
         self._stream = native.stream_handle if self.device else None
 
     @staticmethod
@@ -413,10 +429,12 @@ class NativeCheckpointWriter:
 
 class RoundCheckpointWriter:
     """Per-round checkpoints (same files every round): the native writer where the state dict
-    maps onto it, else :class:`AsyncCheckpointWriter` (coalescing).  FEDMI_NATIVE_CKPT=0 forces
-    the Python writer."""
+    maps onto it, else :class:`AsyncCheckpointWriter`.  Every round is written unless
+    ``coalesce`` (then a host that outruns the writer by ``slots`` rounds supersedes queued
+    rounds instead of waiting).  FEDMI_NATIVE_CKPT=0 forces the Python writer."""
 
-    def __init__(self):
+    def __init__(self, slots: int = 4, coalesce: bool = False):
+        self.slots, self.coalesce = slots, coalesce
         self._native: Dict[tuple, NativeCheckpointWriter] = {}
         self._py: Optional[AsyncCheckpointWriter] = None
         self.backend = None
@@ -429,7 +447,7 @@ class RoundCheckpointWriter:
 
     def _python(self) -> AsyncCheckpointWriter:
         if self._py is None:
-            self._py = AsyncCheckpointWriter()
+            self._py = AsyncCheckpointWriter(max_pending=self.slots, coalesce=self.coalesce)
         return self._py
 
     def submit(self, path, state_dict, acc=1, epoch: int = 0) -> None:
@@ -441,7 +459,7 @@ class RoundCheckpointWriter:
                 w = None
             if w is None:
                 try:
-                    w = NativeCheckpointWriter(paths, state_dict, acc)
+                    w = NativeCheckpointWriter(paths, state_dict, acc, self.slots, self.coalesce)
                     self._native[paths] = w
                 except (ValueError, RuntimeError):
                     w = None

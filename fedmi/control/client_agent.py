@@ -33,6 +33,7 @@ from pathlib import Path
 from typing import Optional
 
 import grpc
+import torch
 
 from .. import ckpt as ck
 from ..engine.base import LocalTrainer
@@ -87,6 +88,8 @@ class ClientAgent(P.TrainerServicer):
         # fault injection (tests / drills): stall this many seconds right before the FedAvg
         # collective, so a kill lands while the other clients wait inside it
         self.fault_stall_avg_s = float(os.environ.get("FEDMI_FAULT_STALL_AVG_S", "0") or 0)
+        self.fault_stall_from = int(os.environ.get("FEDMI_FAULT_STALL_FROM_ROUND", "0") or 0)
+        self._round_start = None                # (float, [int]) device copies of the round's starting global model
         if resume and self.ckpt_path.exists():
             c = ck.load(self.ckpt_path)
             trainer.load_state_dict(c["net"])
@@ -124,6 +127,28 @@ class ClientAgent(P.TrainerServicer):
 
         self.writer.submit(self.ckpt_path, self.trainer.state_dict(), acc=acc, epoch=epoch,
                            on_done=_keep if keep else None)
+
+    def _snapshot_round_start(self) -> None:
+        """Device copy of the model this round starts from (the last committed global model): one
+        D2D copy of the flat state, the rollback target if the round's collective fails."""
+        fs, ints = self.trainer.float_state(), self.trainer.int_state()
+        if self._round_start is None or self._round_start[0].shape != fs.shape or len(self._round_start[1]) != len(ints):
+            self._round_start = (torch.empty_like(fs), [torch.empty_like(b) for b in ints])
+        self._round_start[0].copy_(fs, non_blocking=True)
+        for d, b in zip(self._round_start[1], ints):
+            d.copy_(b, non_blocking=True)
+
+    def _restore_round_start(self) -> Optional[float]:
+        if self._round_start is None:
+            return None
+        self.trainer.float_state().copy_(self._round_start[0])
+        for b, src in zip(self.trainer.int_state(), self._round_start[1]):
+            b.copy_(src)
+        self.trainer.after_aggregate()
+        comp = getattr(self.fedavg, "compressor", None)
+        if comp is not None:
+            comp.reset(self.trainer)
+        return ck.state_digest(self.trainer.state_dict())
 
     def _take_ready(self) -> tuple:
         """(epoch, b64) of the newest serialised checkpoint not uploaded yet, or (-1, '')."""
@@ -179,6 +204,8 @@ class ClientAgent(P.TrainerServicer):
             elif changed and self.fedavg.compressor is not None:
                 self.fedavg.compressor.reset(self.trainer)
             rec["group_ms"] = t.ms()
+        if self.agg == "collective" and world > 1:
+            self._snapshot_round_start()
         t1 = Timer()
         with phase("local-train"):
             self.trainer.set_schedule(*self._schedule(rank, world))
@@ -187,7 +214,7 @@ class ClientAgent(P.TrainerServicer):
         rec.update(tr.as_dict("train"))
         rec["train_ms"] = t1.ms()
         if self.agg == "collective":
-            if self.fault_stall_avg_s > 0 and world > 1:
+            if self.fault_stall_avg_s > 0 and world > 1 and rnd >= self.fault_stall_from:
                 self.trainer.synchronize()
                 time.sleep(self.fault_stall_avg_s)
             t2 = Timer()
@@ -199,6 +226,11 @@ class ClientAgent(P.TrainerServicer):
                 except Exception as e:          # gloo / RCCL error: a peer was lost mid-collective
                     err = f"collective failed: {e}"
             if err:
+                # the round is void: back to the global model it started from (identical on every survivor;
+                # a peer collective may have written the mean into part of the model before failing)
+                digest = self._restore_round_start()
+                self.metrics.write(role="client", address=self.address, event="round_aborted", round=rnd,
+                                   generation=gen, error=err[:200], restored_sum=digest)
                 # ABORTED (not UNAVAILABLE): this client is alive, only the round is void
                 context.abort(grpc.StatusCode.ABORTED, err[:500])
             rec["allreduce_ms"] = t2.ms()
@@ -257,6 +289,7 @@ class ClientAgent(P.TrainerServicer):
             self.trainer.evaluate()
             ev = self.trainer.eval_stats()
             self.metrics.write(role="client", address=self.address, event="send_model", round=self.round,
+                               epoch=int(c.get("epoch", 0) or 0), state_sum=ck.state_digest(c["net"]),
                                **ev.as_dict("test"))
             self._log(f"installed model (epoch {self.round}): test loss {ev.loss:.4f} acc {ev.acc:.2f}%")
             return P.SendModelReply(reply="success")

@@ -232,6 +232,28 @@ class Coordinator:
                 self._fetches += 1
                 self._install_global(ck.from_b64(reply.reply), epoch)
 
+    def _catch_up_committed(self, addr: str, wait_s: float = 2.0) -> None:
+        """Synchronously pull the newest COMMITTED global model from ``addr`` (the aborted round's rank 0,
+        which keeps the checkpoint of its last successful round) until it covers ``self.round``: the
+        background fetcher may be several rounds behind.  Best effort -- an unreachable rank 0 leaves
+        ``latest_model`` as it is."""
+        m = self.members.get(addr)
+        if m is None or not m.fedmi or self.cfg.agg != "collective":
+            return
+        deadline = time.monotonic() + wait_s
+        while self.installed_epoch < self.round and time.monotonic() < deadline:
+            try:
+                reply, call = m.stub.SendModel.with_call(
+                    P.SendModelRequest(model=""), timeout=self.cfg.rpc_timeout_s,
+                    metadata=[(META_TERM, str(self.term)), (META_FETCH, "1")])
+            except grpc.RpcError:
+                return
+            epoch = int(dict(call.trailing_metadata() or ()).get("x-fedmi-ckpt-epoch", "-1"))
+            if reply.reply and epoch > self.installed_epoch:
+                self._install_global(ck.from_b64(reply.reply), epoch)
+            elif epoch < self.round:
+                time.sleep(0.02)             # its writer is still serialising the committed round
+
     def flush(self) -> None:
         """Wait until the newest installed model is on disk (and offered to the backup)."""
         with self._persist_cv:
@@ -300,9 +322,21 @@ class Coordinator:
                 # last committed global model, then regroup (new generation) next round
                 self._log(f"round {rnd} aborted ({len(failed)} client(s) lost); rolling back survivors, regrouping")
                 self._last_live = None           # force a new generation even if every member answered ABORTED
+                self._catch_up_committed(live[0])
                 if self.latest_model is not None:
+                    if self.installed_epoch >= 0 and self.installed_epoch < self.round:
+                        # rank 0's newest committed round was not reachable: the round counter follows
+                        # the model the survivors are rolled back to
+                        self._log(f"rewinding round {self.round} -> {self.installed_epoch} (newest committed model)")
+                        self.round = self.installed_epoch
                     b64 = ck.to_b64(self.latest_model)
-                    sends = [self._pool.submit(self._send_model, a, b64) for a in live if a not in failed]
+                    # EVERY member still active -- the ones that answered ABORTED too: their model may be
+                    # partially averaged (peer blocks past the barrier wrote the mean in place)
+                    with self._lock:
+                        targets = [a for a in live if self.members[a].active]
+                    self.metrics.write(role=self.role, event="rollback", round=rnd, epoch=self.installed_epoch,
+                                       targets=targets, state_sum=ck.state_digest(ck.from_bytes(self.latest_model)["net"]))
+                    sends = [self._pool.submit(self._send_model, a, b64) for a in targets]
                     for s_ in sends:
                         s_.result()
             else:

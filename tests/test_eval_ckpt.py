@@ -168,7 +168,7 @@ def test_native_round_writer_matches_torch_save(tmp_path):
                       ("bn.num_batches_tracked", nbt), ("b.weight", flat[20:35].view(5, 3)),
                       ("empty", flat[40:40])])
     paths = [tmp_path / "Primary" / "optimizedModel.pth", tmp_path / "checkpoint" / "c0.pth"]
-    w = RoundCheckpointWriter()
+    w = RoundCheckpointWriter(coalesce=True, slots=2)
     for r in range(100):
         flat.add_(1.0)
         nbt.add_(1)
@@ -191,3 +191,27 @@ def test_native_round_writer_matches_torch_save(tmp_path):
     w.close()
     assert load(paths[1])["acc"] == 0.5 and load(paths[1])["epoch"] == 3
     assert list(load(paths[0])["net"]) == ["x"] and load(paths[0])["epoch"] == 4
+
+
+def test_native_round_writer_writes_every_round_in_order(tmp_path, monkeypatch):
+    """Default (no coalescing): every submitted round reaches the disk, in order."""
+    from fedmi import native
+    from fedmi.ckpt import RoundCheckpointWriter, load
+
+    if not native.available():
+        pytest.skip("native extension not built")
+    flat = torch.zeros(1000)
+    sd = {"w": flat[:600].view(20, 30), "b": flat[600:]}
+    w = RoundCheckpointWriter(slots=2)
+    seen = []
+    for r in range(60):
+        flat.fill_(float(r))
+        w.submit(tmp_path / "m.pth", sd, epoch=r)
+        if r % 7 == 0:
+            w.flush()
+            seen.append(load(tmp_path / "m.pth")["epoch"])
+    w.close()
+    assert w.coalesced == 0 and w.written == 60
+    assert seen == [r for r in range(60) if r % 7 == 0]
+    ck = load(tmp_path / "m.pth")
+    assert ck["epoch"] == 59 and torch.equal(ck["net"]["w"], torch.full((20, 30), 59.0))

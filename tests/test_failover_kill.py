@@ -134,8 +134,10 @@ def _client_killed_mid_collective(tmp_path, device):
     addrs = [f"127.0.0.1:{free_port()}" for _ in range(3)]
     victim = 2
     procs = [spawn_client(a, tmp_path, "--agg", "collective", *_client_args(device),
+                          "--metrics", str(tmp_path / f"client{i}.jsonl"),
                           log_path=tmp_path / f"client{i}.log", device=device,
-                          env_extra={"FEDMI_FAULT_STALL_AVG_S": "4"} if i == victim else None)
+                          env_extra={"FEDMI_FAULT_STALL_AVG_S": "4", "FEDMI_FAULT_STALL_FROM_ROUND": "3"}
+                          if i == victim else None)
              for i, a in enumerate(addrs)]
     import threading
 
@@ -149,16 +151,30 @@ def _client_killed_mid_collective(tmp_path, device):
         coord = Coordinator(cfg, metrics=MetricsLog(tmp_path / "coord.jsonl"))
         t = threading.Thread(target=coord.run, daemon=True)
         t.start()
-        # the victim stalls 4 s before every collective: the survivors are inside it by then
-        wait_for(lambda: (tmp_path / "client0.log").exists(), timeout=5)
+        # rounds 1-2 commit; from round 3 on the victim stalls 4 s before the collective: the survivors
+        # are inside it when it dies
+        wait_for(lambda: len(_rounds(tmp_path / "coord.jsonl")) >= 2, timeout=60)
         time.sleep(2.0)
         t_kill = kill9(procs[victim])
+        committed = max(r["round"] for r in _rounds(tmp_path / "coord.jsonl") if r["ts"] < t_kill)
         # survivors fail fast, the round is aborted; the next round runs with world 2
         ok2 = wait_for(lambda: [r for r in _rounds(tmp_path / "coord.jsonl") if r["world"] == 2], timeout=90)
         recovery = ok2[0]["ts"] - t_kill
         aborted = [r for r in _rounds(tmp_path / "coord.jsonl", ok_only=False) if not r.get("ok")]
         assert aborted and addrs[victim] in aborted[0]["failed"]
         assert recovery < 30.0, recovery
+        # every survivor -- each answered ABORTED -- was rolled back to the committed global model
+        rb = wait_for(lambda: [r for r in read_jsonl(tmp_path / "coord.jsonl") if r.get("event") == "rollback"],
+                      timeout=10)[0]
+        assert sorted(rb["targets"]) == sorted(addrs[:2]), rb
+        assert rb["epoch"] == committed, (rb, committed)          # not a stale fetch: the newest committed round
+        for i in range(2):
+            got = [r for r in read_jsonl(tmp_path / f"client{i}.jsonl")
+                   if r.get("event") == "send_model" and r["ts"] > t_kill]
+            assert got and got[0]["epoch"] == rb["epoch"] and got[0]["state_sum"] == rb["state_sum"], (i, got[:1], rb)
+            # the client restored the round's starting (= committed) model itself, before the coordinator did
+            ab = [r for r in read_jsonl(tmp_path / f"client{i}.jsonl") if r.get("event") == "round_aborted"]
+            assert ab and ab[0]["restored_sum"] == rb["state_sum"], (i, ab[:1], rb)
         wait_for(lambda: len([r for r in _rounds(tmp_path / "coord.jsonl") if r["world"] == 2]) >= 2, timeout=60)
         coord.stop()
         t.join(timeout=60)

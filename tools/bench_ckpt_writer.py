@@ -46,7 +46,8 @@ def run(coalesce, rounds: int, cadence_ms: float, device) -> dict:
     paths = [root / "Primary" / "optimizedModel.pth", root / "checkpoint" / "client0.pth"]
     for p in paths:
         p.parent.mkdir(parents=True, exist_ok=True)
-    w = RoundCheckpointWriter() if coalesce == "native" else AsyncCheckpointWriter(coalesce=coalesce)
+    native = isinstance(coalesce, str)
+    w = RoundCheckpointWriter(coalesce=coalesce == "native-coalesce") if native else AsyncCheckpointWriter(coalesce=coalesce)
     lat = []
     t0 = time.perf_counter()
     nxt = t0
@@ -65,7 +66,8 @@ def run(coalesce, rounds: int, cadence_ms: float, device) -> dict:
     last = load(paths[0])["epoch"]
     w.close()
     lat.sort()
-    return {"writer": "native-cxx" if coalesce == "native" else "python-thread", "coalesce": bool(coalesce), "rounds": rounds, "target_cadence_ms": cadence_ms,
+    return {"writer": "native-cxx" if native else "python-thread",
+            "coalesce": coalesce == "native-coalesce" if native else coalesce, "rounds": rounds, "target_cadence_ms": cadence_ms,
             "achieved_cadence_ms": round(t_loop / rounds * 1e3, 4), "flush_ms": round((t_all - t_loop) * 1e3, 3),
             "submit_ms_p50": round(lat[len(lat) // 2], 4), "submit_ms_p99": round(lat[int(len(lat) * 0.99)], 4),
             "submit_ms_max": round(lat[-1], 4), "files_written": w.written, "rounds_coalesced": w.coalesced,
@@ -79,7 +81,8 @@ def main() -> int:
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
-    rows = [run("native", a.rounds, a.cadence_ms, dev), run(True, a.rounds, a.cadence_ms, dev),
+    rows = [run("native", a.rounds, a.cadence_ms, dev), run("native-coalesce", a.rounds, a.cadence_ms, dev),
+            run(True, a.rounds, a.cadence_ms, dev),
             run(False, a.rounds, a.cadence_ms, dev)]
     for r in rows:
         print(json.dumps(r), flush=True)
