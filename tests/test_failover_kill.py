@@ -67,8 +67,8 @@ def _client_args(device):
     return ("--backend", "gloo", "--collective-timeout", "3") + CPU_MODEL
 
 
-def _primary_sigkill_and_recover(tmp_path, device):
-    addrs = [f"127.0.0.1:{free_port()}" for _ in range(2)]
+def _primary_sigkill_and_recover(tmp_path, device, n_clients=2):
+    addrs = [f"127.0.0.1:{free_port()}" for _ in range(n_clients)]
     procs = [spawn_client(a, tmp_path, "--agg", "collective", *_client_args(device),
                           log_path=tmp_path / f"client{i}.log", device=device) for i, a in enumerate(addrs)]
     bport = free_port()
@@ -117,7 +117,8 @@ def _primary_sigkill_and_recover(tmp_path, device):
         assert backup.poll() is None                         # the demoted backup is alive and serving
         wait_heartbeat(f"127.0.0.1:{bport}", timeout=10)
         demoted = [r for r in read_jsonl(tmp_path / "backup.jsonl") if r.get("event") == "demoted"][0]
-        _report(drill="primary_sigkill", device=device, takeover_s=round(takeover, 3), primary_last_round=r_dead,
+        _report(drill="primary_sigkill", device=device, clients=n_clients, takeover_s=round(takeover, 3),
+                primary_last_round=r_dead,
                 backup_first_round=first["round"], restarted_primary_first_round=r2[0]["round"],
                 demote_after_restart_s=round(demoted["ts"] - promoted[0]["ts"], 3))
         stop_proc(primary2)
@@ -128,11 +129,12 @@ def _primary_sigkill_and_recover(tmp_path, device):
             stop_proc(p)
 
 
-def _client_killed_mid_collective(tmp_path, device):
+def _client_killed_mid_collective(tmp_path, device, n_clients=3):
     from fedmi.control.coordinator import Coordinator, CoordinatorConfig
 
-    addrs = [f"127.0.0.1:{free_port()}" for _ in range(3)]
-    victim = 2
+    addrs = [f"127.0.0.1:{free_port()}" for _ in range(n_clients)]
+    victim = n_clients - 1
+    surv = n_clients - 1
     procs = [spawn_client(a, tmp_path, "--agg", "collective", *_client_args(device),
                           "--metrics", str(tmp_path / f"client{i}.jsonl"),
                           log_path=tmp_path / f"client{i}.log", device=device,
@@ -157,8 +159,8 @@ def _client_killed_mid_collective(tmp_path, device):
         time.sleep(2.0)
         t_kill = kill9(procs[victim])
         committed = max(r["round"] for r in _rounds(tmp_path / "coord.jsonl") if r["ts"] < t_kill)
-        # survivors fail fast, the round is aborted; the next round runs with world 2
-        ok2 = wait_for(lambda: [r for r in _rounds(tmp_path / "coord.jsonl") if r["world"] == 2], timeout=90)
+        # survivors fail fast, the round is aborted; the next round runs with the survivors only
+        ok2 = wait_for(lambda: [r for r in _rounds(tmp_path / "coord.jsonl") if r["world"] == surv], timeout=90)
         recovery = ok2[0]["ts"] - t_kill
         aborted = [r for r in _rounds(tmp_path / "coord.jsonl", ok_only=False) if not r.get("ok")]
         assert aborted and addrs[victim] in aborted[0]["failed"]
@@ -166,29 +168,30 @@ def _client_killed_mid_collective(tmp_path, device):
         # every survivor -- each answered ABORTED -- was rolled back to the committed global model
         rb = wait_for(lambda: [r for r in read_jsonl(tmp_path / "coord.jsonl") if r.get("event") == "rollback"],
                       timeout=10)[0]
-        assert sorted(rb["targets"]) == sorted(addrs[:2]), rb
+        assert sorted(rb["targets"]) == sorted(addrs[:surv]), rb
         assert rb["epoch"] == committed, (rb, committed)          # not a stale fetch: the newest committed round
-        for i in range(2):
+        for i in range(surv):
             got = [r for r in read_jsonl(tmp_path / f"client{i}.jsonl")
                    if r.get("event") == "send_model" and r["ts"] > t_kill]
             assert got and got[0]["epoch"] == rb["epoch"] and got[0]["state_sum"] == rb["state_sum"], (i, got[:1], rb)
             # the client restored the round's starting (= committed) model itself, before the coordinator did
             ab = [r for r in read_jsonl(tmp_path / f"client{i}.jsonl") if r.get("event") == "round_aborted"]
             assert ab and ab[0]["restored_sum"] == rb["state_sum"], (i, ab[:1], rb)
-        wait_for(lambda: len([r for r in _rounds(tmp_path / "coord.jsonl") if r["world"] == 2]) >= 2, timeout=60)
+        wait_for(lambda: len([r for r in _rounds(tmp_path / "coord.jsonl") if r["world"] == surv]) >= 2, timeout=60)
         coord.stop()
         t.join(timeout=60)
         coord.close()
-        # the two survivors hold the same global model
-        for a in addrs[:2]:
+        # the survivors hold the same global model
+        for a in addrs[:surv]:
             wait_for(lambda a=a: (ck.read_epoch(tmp_path / "checkpoint" / f"{a}.pth") or 0) >= coord.round, timeout=30)
         m0 = ck.load(tmp_path / "checkpoint" / f"{addrs[0]}.pth")["net"]
-        m1 = ck.load(tmp_path / "checkpoint" / f"{addrs[1]}.pth")["net"]
         import torch
 
-        for k in m0:
-            assert torch.allclose(m0[k], m1[k], atol=1e-6), k
-        _report(drill="client_sigkill_mid_collective", device=device, recovery_s=round(recovery, 3),
+        for a in addrs[1:surv]:
+            m1 = ck.load(tmp_path / "checkpoint" / f"{a}.pth")["net"]
+            for k in m0:
+                assert torch.allclose(m0[k], m1[k], atol=1e-6), (a, k)
+        _report(drill="client_sigkill_mid_collective", device=device, clients=n_clients, recovery_s=round(recovery, 3),
                 aborted_round=aborted[0]["round"], next_ok_round=ok2[0]["round"], collective_timeout_s=3)
         return recovery
     finally:
@@ -220,3 +223,21 @@ def test_primary_sigkill_backup_promotes_then_demotes_gpu(tmp_path):
 @pytest.mark.gpu
 def test_client_sigkill_mid_collective_gpu(tmp_path):
     _drill(_client_killed_mid_collective, tmp_path, "cuda:0", "client_gpu")
+
+
+# BASELINE config 5 at its stated scale: 8 client processes (all on the one GPU of the test box, peer
+# transport over same-device hipIpc), primary + backup coordinators.
+@pytest.mark.gpu
+@pytest.mark.timeout(420)
+def test_primary_sigkill_8_clients_gpu(tmp_path):
+    _drill(lambda t, d: _primary_sigkill_and_recover(t, d, n_clients=8), tmp_path, "cuda:0", "primary_gpu8")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(420)
+def test_client_sigkill_mid_collective_8_clients_gpu(tmp_path):
+    _drill(lambda t, d: _client_killed_mid_collective(t, d, n_clients=8), tmp_path, "cuda:0", "client_gpu8")
+
+
+def test_client_sigkill_mid_collective_8_clients_cpu(tmp_path):
+    _drill(lambda t, d: _client_killed_mid_collective(t, d, n_clients=8), tmp_path, "cpu", "client_cpu8")
