@@ -19,7 +19,7 @@ namespace fedmi {
 struct ConvShape {
   int N, H, W, C, Cw, O, P, Q, R, S, st, pad;
 };
-void launch_conv_fwd(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, const float*, float*, long,
+void launch_conv_fwd(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, double*, const float*, float*, long,
                      const bf16*);
 void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, long, const bf16*, int);
 struct DPackItem {
@@ -41,7 +41,7 @@ void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int);
 void set_conv_halo_stamps(long long*);
 
 struct BNDesc {
-  const float* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
+  const double* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
   float* smean; float* sinv; const float* shift; const float* cbias;
 };
 void launch_maxpool2(hipStream_t, const bf16*, bf16*, int, int, int, int);
@@ -60,7 +60,7 @@ struct BNBwdDesc {
 struct DwShape {
   int N, H, W, C, R, S, st, pad;
 };
-void launch_dw_fwd(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, float*, const float*, const float*);
+void launch_dw_fwd(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, double*, const float*, const float*);
 void launch_dw_dgrad(hipStream_t, const DwShape&, const bf16*, const float*, bf16*);
 long dw_wgrad_ws_floats(const DwShape&);
 void launch_dw_wgrad(hipStream_t, const DwShape&, const bf16*, const bf16*, float*, float*, long, int, const float*);
@@ -68,7 +68,7 @@ void launch_prep_input(hipStream_t, const uint8_t*, int, const int*, int, int, u
 void launch_sched_next(hipStream_t, const int*, int*, int*);
 void launch_bn_apply(hipStream_t, const bf16*, const BNDesc&, const bf16*, const BNDesc*, const bf16*, bf16*, int, int,
                      float, float, int, int, int);
-void launch_bn_bwd(hipStream_t, const BNBwdDesc&, float*, int, int, float*, long, int, int, int);
+void launch_bn_bwd(hipStream_t, const BNBwdDesc&, double*, int, int, double*, long, int, int, int);
 void launch_bn_coeff(hipStream_t, const BNDesc&, int, int, float, float, int, float*);
 long bn_bwd_ws_floats(int, int);
 int bn_bwd_chain_reps(int);
@@ -109,7 +109,7 @@ DwShape dw_from(const py::tuple& t) {
 }
 
 BNDesc bn_from(const py::dict& d) {
-  return BNDesc{P<const float>(dget(d, "stats")), P<const float>(dget(d, "gamma")), P<const float>(dget(d, "beta")),
+  return BNDesc{P<const double>(dget(d, "stats")), P<const float>(dget(d, "gamma")), P<const float>(dget(d, "beta")),
                 P<float>(dget(d, "rmean")),       P<float>(dget(d, "rvar")),        P<long long>(dget(d, "nbt")),
                 P<float>(dget(d, "smean")),       P<float>(dget(d, "sinv")),        P<const float>(dget(d, "shift")),
                 P<const float>(dget(d, "cbias"))};
@@ -122,7 +122,7 @@ void fedmi_bind_cnn(py::module_& m) {
   m.def("conv_halo_stamps", [](uintptr_t p) { set_conv_halo_stamps(reinterpret_cast<long long*>(p)); });
   m.def("conv_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                        uintptr_t shift, uintptr_t ws, long ws_floats, uintptr_t res) {
-    launch_conv_fwd(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(w), P<bf16>(y), P<float>(stats),
+    launch_conv_fwd(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(w), P<bf16>(y), P<double>(stats),
                     P<const float>(shift), P<float>(ws), ws ? ws_floats : 0, P<const bf16>(res));
     check("conv_fwd");
   }, py::arg("st"), py::arg("shape"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("shift"),
@@ -171,7 +171,7 @@ void fedmi_bind_cnn(py::module_& m) {
   });
   m.def("dw_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                      uintptr_t shift, uintptr_t isc) {
-    launch_dw_fwd(S(st), dw_from(shp), P<const bf16>(x), P<const float>(w), P<bf16>(y), P<float>(stats),
+    launch_dw_fwd(S(st), dw_from(shp), P<const bf16>(x), P<const float>(w), P<bf16>(y), P<double>(stats),
                   P<const float>(shift), P<const float>(isc));
     check("dw_fwd");
   }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("shift"),
@@ -241,7 +241,7 @@ void fedmi_bind_cnn(py::module_& m) {
                 P<float>(dget(d, "shiftA")),       P<float>(dget(d, "shiftB")),       P<const bf16>(dget(d, "dadd")),
                 P<const float>(dget(d, "msc"))};
     if (!b.dya || !b.za || !b.meanA || !b.invA || !b.gammaA || !b.dza) throw std::invalid_argument("bn_bwd: missing A");
-    launch_bn_bwd(S(st), b, P<float>(red), M, C, P<float>(ws), ws ? ws_floats : 0, ldd, ldy, chained);
+    launch_bn_bwd(S(st), b, P<double>(red), M, C, P<double>(ws), ws ? ws_floats : 0, ldd, ldy, chained);
     check("bn_bwd");
   }, py::arg("st"), py::arg("desc"), py::arg("red"), py::arg("M"), py::arg("C"), py::arg("ws") = 0,
      py::arg("ws_floats") = 0, py::arg("ldd") = 0, py::arg("ldy") = 0, py::arg("chained") = 0);

@@ -47,6 +47,7 @@ void fedmi_bind_comm(py::module_& m) {
       .def("set_timeout_ms", &PeerComm::set_timeout_ms)
       .def("disconnect", &PeerComm::disconnect, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("connected", &PeerComm::connected)
+      .def_property_readonly("colocated", &PeerComm::colocated)
       .def_property_readonly("rank", &PeerComm::rank)
       .def_property_readonly("world", &PeerComm::world)
       .def_property_readonly("capacity", &PeerComm::capacity)

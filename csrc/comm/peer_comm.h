@@ -64,6 +64,10 @@ class PeerComm {
   // handles[p] from every rank (own entry ignored); maps the peers.
   void connect(const std::vector<std::vector<uint8_t>>& handles);
   bool connected() const { return connected_; }
+  // some peer runs on THIS GPU (one-GPU rehearsals): its kernels share our hardware queues, so a
+  // barrier kernel spinning here can starve a peer that has not launched yet (callers then gate
+  // each collective with a host-side barrier)
+  bool colocated() const { return colocated_; }
 
   // out = scale * sum_p in_p  (fp32; in == out allowed)
   void allreduce_f32(hipStream_t st, const float* in, float* out, long long n, float scale, int algo, int blocks);
@@ -88,6 +92,7 @@ class PeerComm {
   PeerSignal* sig_ = nullptr;       // own (uncached)
   char* data_ = nullptr;            // own staging
   bool connected_ = false;
+  bool colocated_ = false;
   int device_ = 0;
 };
 

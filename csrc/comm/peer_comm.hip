@@ -283,6 +283,7 @@ void PeerComm::connect(const std::vector<std::vector<uint8_t>>& handles) {
     bus[kBusIdLen - 1] = 0;
     int dev = -1;
     check_hip(hipDeviceGetByPCIBusId(&dev, bus), "hipDeviceGetByPCIBusId");
+    if (dev == device_) colocated_ = true;
     if (dev != device_) {
       int can = 0;
       check_hip(hipDeviceCanAccessPeer(&can, device_, dev), "hipDeviceCanAccessPeer");

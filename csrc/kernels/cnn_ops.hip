@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void prep_input_kernel(const uint8_t* __restri
 
 // ---------------------------------------------------------------------------
 struct BNArgs {
-  const float* stats;     // [STAT_REP][2][C]: sum, sum of squares over M rows (train)
+  const double* stats;    // [STAT_REP][2][C] fp64: sum, sum of squares over M rows (train)
   const float* gamma;
   const float* beta;
   float* rmean;           // running stats (updated in train mode, read in eval)
@@ -95,14 +95,17 @@ FEDMI_DEV void bn_coeffs(const BNArgs& a, int C, int M, float eps, float mom, in
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float mean, inv;
     if (train) {
-      float s1 = 0.f, s2 = 0.f;   // sum the STAT_REP replicas of [sum | sum of squares]
+      // fp64 replicas (the epilogues add float block partials with fp64 atomics: the totals do not
+      // depend on the order the workgroups arrive in, up to fp64 rounding far below the fp32 result)
+      double s1 = 0.0, s2 = 0.0;
 #pragma unroll 4
       for (int r = 0; r < STAT_REP; ++r) {
         s1 += a.stats[(2 * r) * C + c];
         s2 += a.stats[(2 * r + 1) * C + c];
       }
-      const float ms = s1 / (float)M;   // mean of (z - shift)
-      const float var = fmaxf(s2 / (float)M - ms * ms, 0.f);
+      const double msd = s1 / (double)M;   // mean of (z - shift)
+      const float ms = (float)msd;
+      const float var = (float)fmax(s2 / (double)M - msd * msd, 0.0);
       mean = ms + (a.shift ? a.shift[c] : 0.f);
       inv = rsqrtf(var + eps);
       if (blockIdx.x == 0) {
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
 // ---------------------------------------------------------------------------
 // BN backward. g = (dya [+ dyb]) * (y > 0 if relu).  Per channel:
 //   red[0] = sum g,  red[1] = sum g * xhatA,  red[2] = sum g * xhatB
-constexpr int BN_REP = 16;   // atomic replicas of the two-level BN-backward channel sums
+constexpr int BN_REP = 16;   // atomic replicas of the two-level BN-backward channel sums (fp64)
 
 struct BwdIn {
   const bf16* dya;
@@ -214,12 +217,14 @@ FEDMI_DEV void load_g(const BwdIn& in, long r, int cg, float* g, const float* z)
   }
 }
 
-// red: [3][C] accumulated with atomics (partials == nullptr), or two-level: the
+// red: [3][C] fp64 accumulated with atomics (partials == nullptr), or two-level: the
 // block sums are added into one of BN_REP replicas partials[rep][3][C]
 // (rep = block % BN_REP: 1/BN_REP of the same-address atomic contention) and
-// bn_bwd_finalize sums the replicas into red and re-zeroes them.
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BwdIn in, float* __restrict__ red, int M, int C,
-                                                            int rows_per_block, float* __restrict__ partials,
+// bn_bwd_finalize sums the replicas into red and re-zeroes them.  fp64 atomics of the
+// float block sums: the channel sums do not depend on the workgroups' arrival order
+// (up to fp64 rounding, far below the fp32 coefficients derived from them).
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BwdIn in, double* __restrict__ red, int M, int C,
+                                                            int rows_per_block, double* __restrict__ partials,
                                                             int reps) {
   __shared__ float part[3][256][8];
   const int VR = C >> 3;                 // host: blockDim.x % VR == 0
@@ -265,21 +270,21 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BwdIn in, float* __r
     const int g = c >> 3, j = c & 7;
     float s = 0.f;
     for (int t = g; t < (int)blockDim.x; t += VR) s += part[qn][t][j];
-    unsafeAtomicAdd((partials ? partials + (long)(blockIdx.x % reps) * 3 * C : red) + qn * C + c, s);
+    unsafeAtomicAdd((partials ? partials + (long)(blockIdx.x % reps) * 3 * C : red) + qn * C + c, (double)s);
   }
 }
 
 // red[q][c] = sum_r partials[r][q][c]; the replicas are left zero for the next BN
 // (launches of a step are stream-serial, so one scratch serves every BN layer).
-__global__ __launch_bounds__(256) void bn_bwd_finalize(float* __restrict__ partials, int C, float* __restrict__ red) {
+__global__ __launch_bounds__(256) void bn_bwd_finalize(double* __restrict__ partials, int C, double* __restrict__ red) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= 3 * C) return;
   const long stride = 3l * C;
-  float v[BN_REP];
+  double v[BN_REP];
 #pragma unroll
   for (int r = 0; r < BN_REP; ++r) v[r] = partials[r * stride + e];
 #pragma unroll
-  for (int r = 0; r < BN_REP; ++r) partials[r * stride + e] = 0.f;
+  for (int r = 0; r < BN_REP; ++r) partials[r * stride + e] = 0.0;
 #pragma unroll
   for (int w = BN_REP / 2; w >= 1; w >>= 1)
 #pragma unroll
@@ -304,26 +309,26 @@ struct BwdOut {
 
 // partials != null (chained mode): the channel sums are read straight from the reduce kernel's
 // 'reps' atomic replicas (no finalize launch); the caller zeroes them before the next step.
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdIn in, BwdOut out, const float* __restrict__ red,
-                                                           int M, int C, const float* __restrict__ partials,
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdIn in, BwdOut out, const double* __restrict__ red,
+                                                           int M, int C, const double* __restrict__ partials,
                                                            int reps) {
   extern __shared__ float co[];   // [6][C]: kA, bA, cA, kB, bB, cB  (dz = k*g + b*xhat + c)
   const float invM = 1.f / (float)M;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float sg, sgx, sgx2 = 0.f;
+    double dg = 0.0, dgx = 0.0, dgx2 = 0.0;
     if (partials) {
-      sg = sgx = 0.f;
       for (int r = 0; r < reps; ++r) {           // fixed order: every block derives identical coefficients
-        const float* pr = partials + (long)r * 3 * C;
-        sg += pr[c];
-        sgx += pr[C + c];
-        if (in.zb) sgx2 += pr[2 * C + c];
+        const double* pr = partials + (long)r * 3 * C;
+        dg += pr[c];
+        dgx += pr[C + c];
+        if (in.zb) dgx2 += pr[2 * C + c];
       }
     } else {
-      sg = red[c];
-      sgx = red[C + c];
-      if (in.zb) sgx2 = red[2 * C + c];
+      dg = red[c];
+      dgx = red[C + c];
+      if (in.zb) dgx2 = red[2 * C + c];
     }
+    const float sg = (float)dg, sgx = (float)dgx, sgx2 = (float)dgx2;
     const float scA = out.gammaA[c] * in.invA[c];
     // dz = scA * (g - sg/M - xhat * sgx/M),  xhat = (z - mean) * inv
     co[c] = scA;
@@ -735,7 +740,7 @@ int grid_for(long nv) { return (int)std::min<long>((nv + 255) / 256, 2048); }
 namespace fedmi {
 
 struct BNDesc {
-  const float* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
+  const double* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
   float* smean; float* sinv; const float* shift; const float* cbias;
 };
 
@@ -822,21 +827,21 @@ static void bn_bwd_grid(int M, int C, int* tb, int* rows_per_block, int* nblk) {
   *nblk = (M + *rows_per_block - 1) / *rows_per_block;
 }
 
-// Scratch (floats) the two-level reduction of launch_bn_bwd needs (ZERO-initialised once
-// by the caller; every launch leaves it zero again).
+// Scratch (fp64 elements) the two-level reduction of launch_bn_bwd needs (ZERO-initialised
+// once by the caller; every launch leaves it zero again).
 long bn_bwd_ws_floats(int M, int C) {
   (void)M;
   return (long)BN_REP * 3 * C;
 }
 
-// red: [3][C] fp32.  With ``ws`` (>= bn_bwd_ws_floats, zero): replica atomics + a
+// red: [3][C] fp64.  With ``ws`` (fp64, >= bn_bwd_ws_floats elements, zero): replica atomics + a
 // finalize launch (red needs no zeroing).  Without: atomics into red, which must
 // be zero on entry.
-// Replicas per channel sum in chained mode: <= 2048 floats per quantity, 4..16 (a replica spreads
+// Replicas per channel sum in chained mode: <= 2048 values per quantity, 4..16 (a replica spreads
 // the reduce workgroups' same-address atomics; the apply prologue reads them all).
 int bn_bwd_chain_reps(int C) { return std::max(4, std::min(16, 2048 / std::max(C, 1))); }
 
-void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, float* red, int M, int C, float* ws, long ws_floats, int ldd,
+void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, double* red, int M, int C, double* ws, long ws_floats, int ldd,
                    int ldy, int chained) {
   const int VR = C / 8;
   if (C % 8 || VR > 256) throw std::invalid_argument("bn_bwd: need C % 8 == 0 and C <= 2048");

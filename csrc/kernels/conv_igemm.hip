@@ -267,7 +267,7 @@ struct Loader {
 template <int MODE, int BM, int BN>
 __global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                   const bf16* __restrict__ dy, bf16* __restrict__ out,
-                                                  float* __restrict__ gout, float* __restrict__ stats,
+                                                  float* __restrict__ gout, double* __restrict__ stats,
                                                   const float* __restrict__ shift, ConvGeom g,
                                                   int ksteps_per_split, int partial) {
   // partial bit 0: fp32 split-K partial into gout; bit 1: out += result (bf16 outputs)
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(256) void conv_igemm(const bf16* __restrict__ x, co
         float t = 0.f;
 #pragma unroll
         for (int pp = 0; pp < PARTS; ++pp) t += red[(pp * 2 + q) * BN + cl];
-        if (n0 + cl < g.NC) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.NC + n0 + cl, t);
+        if (n0 + cl < g.NC) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.NC + n0 + cl, (double)t);
       }
     }
   }
@@ -457,7 +457,7 @@ FEDMI_DEV bf16x8 frag_sw(const bf16* img, int i0, int kk, int lane) {
 template <int BN>
 __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                 bf16* __restrict__ out, float* __restrict__ part,
-                                                float* __restrict__ stats, const float* __restrict__ shift,
+                                                double* __restrict__ stats, const float* __restrict__ shift,
                                                 TapGeom g, RowMap rmap, int ksteps_per_split,
                                                 const bf16* __restrict__ res) {
   constexpr int BM = 128;
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
   if (stats != nullptr && res == nullptr && tid < 2 * BN) {
     const int q = tid / BN, cl = tid % BN;
     const float tsum = red[q * BN + cl] + red[(2 + q) * BN + cl];
-    if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, tsum);
+    if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, (double)tsum);
   }
   constexpr int CPR = BN / 8;
   for (int c = tid; c < BM * CPR; c += 256) {
@@ -658,7 +658,7 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
       float t = 0.f;
 #pragma unroll
       for (int pp = 0; pp < PARTS; ++pp) t += red[(pp * 2 + q) * BN + cl];
-      if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, t);
+      if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, (double)t);
     }
   }
 }
@@ -706,7 +706,7 @@ FEDMI_DEV void vm_wait_le(int n) {
 template <int BN, int PP, int NST>
 __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                  bf16* __restrict__ out, float* __restrict__ part,
-                                                 float* __restrict__ stats, const float* __restrict__ shift,
+                                                 double* __restrict__ stats, const float* __restrict__ shift,
                                                  HaloGeom g, int chunks_per_split, const bf16* __restrict__ res,
                                                  long long* __restrict__ stamps) {
   // stamps (diagnostic, null in production): per workgroup [realtime at start, memtime at start, after
@@ -915,7 +915,7 @@ __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, co
   if (stats != nullptr && res == nullptr && tid < 2 * BN) {
     const int q = tid / BN, cl = tid % BN;
     const float tsum = red[q * BN + cl] + red[(2 + q) * BN + cl];
-    if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, tsum);
+    if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, (double)tsum);
   }
   constexpr int CPR = BN / 8;
   for (int cidx = tid; cidx < BM * CPR; cidx += 256) {
@@ -951,7 +951,7 @@ __global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, co
       float tsum = 0.f;
 #pragma unroll
       for (int pp = 0; pp < PARTS; ++pp) tsum += red[(pp * 2 + q) * BN + cl];
-      if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, tsum);
+      if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, (double)tsum);
     }
   }
   put_stamps();
@@ -1298,7 +1298,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_cols(const float* __res
 // 8-channel group (two 16-B loads per split) of rows r0, r0 + rstep, ...
 __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restrict__ ws, int splits, int M, int NC,
                                                           RowMap rmap, bf16* __restrict__ out,
-                                                          float* __restrict__ stats, const float* __restrict__ shift,
+                                                          double* __restrict__ stats, const float* __restrict__ shift,
                                                           int rows_per_block, const bf16* __restrict__ res) {
   __shared__ float red[2][256][8];
   const int VR = NC >> 3;                 // host: blockDim.x % VR == 0
@@ -1353,7 +1353,7 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restric
     const int grp = c >> 3, j = c & 7;
     float t = 0.f;
     for (int th = grp; th < (int)blockDim.x; th += VR) t += red[q][th][j];
-    unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * NC + c, t);
+    unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * NC + c, (double)t);
   }
 }
 
@@ -1482,7 +1482,7 @@ static TileCfg pick_tiles_wgrad(int M, int NC) {
 
 template <int MODE, int BM, int BN>
 static void launch_tiled(hipStream_t st, dim3 grid, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy,
-                         bf16* out, float* gout, float* stats, const float* shift, int kps, int partial) {
+                         bf16* out, float* gout, double* stats, const float* shift, int kps, int partial) {
   hipLaunchKernelGGL((conv_igemm<MODE, BM, BN>), grid, dim3(256), 0, st, x, w, dy, out, gout, stats, shift, g, kps,
                      partial);
 }
@@ -1510,7 +1510,7 @@ static int fd_splits(const ConvGeom& g, long ws_floats) {
 
 template <int MODE>
 static void launch_mode(hipStream_t st, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy, bf16* out,
-                        float* gout, float* stats, int splits, const float* shift = nullptr, int partial = 0) {
+                        float* gout, double* stats, int splits, const float* shift = nullptr, int partial = 0) {
   const TileCfg t = MODE == WGRAD ? pick_tiles_wgrad(g.M, g.NC) : pick_tiles(g.M, g.NC);
   const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
   const int ksteps = (g.K + BK - 1) / BK;
@@ -1597,7 +1597,7 @@ static int halo_splits(const HaloGeom& h, long ws_floats) {
 
 static long long* g_halo_stamps = nullptr;   // diagnostic (conv_halo_stamps binding)
 
-static void launch_halo(hipStream_t st, const HaloGeom& h, const bf16* in, const bf16* wt, bf16* out, float* stats,
+static void launch_halo(hipStream_t st, const HaloGeom& h, const bf16* in, const bf16* wt, bf16* out, double* stats,
                         const float* shift, float* ws, long ws_floats, const bf16* res) {
   const int BN = tap_bn(h.O);
   const long tiles = (long)(h.M / 128) * ((h.O + BN - 1) / BN);
@@ -1606,7 +1606,7 @@ static void launch_halo(hipStream_t st, const HaloGeom& h, const bf16* in, const
   const int splits = (h.nchunks + cps - 1) / cps;
   dim3 grid((unsigned)tiles, 1, (unsigned)splits);
   float* part = splits > 1 ? ws : nullptr;
-  float* stt = part ? nullptr : stats;
+  double* stt = part ? nullptr : stats;
   const bf16* rs = part ? nullptr : res;
   const bool pp2 = h.NPR > 208;
   // BN 64 / PP 1: 3 stages keep two workgroups per CU (79 KB LDS); FEDMI_HALO_DEEP64=1 takes 6 (one per CU)
@@ -1636,7 +1636,7 @@ static void launch_halo(hipStream_t st, const HaloGeom& h, const bf16* in, const
   }
 }
 
-static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const bf16* wt, bf16* out, float* stats,
+static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const bf16* wt, bf16* out, double* stats,
                        const float* shift, const RowMap& rm, float* ws, long ws_floats,
                        const bf16* res = nullptr) {
   if (g.C % 64 || g.O % 8) throw std::invalid_argument("conv_tap: need C % 64 == 0 and O % 8 == 0");
@@ -1712,7 +1712,7 @@ static int dgrad_tap_phases(const ConvShape& s, TapPhase* out) {
 // FWD / DGRAD with automatic split-K through ``ws`` (null / 0 floats: never split).
 template <int MODE>
 static void launch_fd(hipStream_t st, const ConvGeom& g, const bf16* x, const bf16* w, const bf16* dy, bf16* out,
-                      float* stats, const float* shift, float* ws, long ws_floats, bool acc = false) {
+                      double* stats, const float* shift, float* ws, long ws_floats, bool acc = false) {
   const int sp = fd_splits(g, ws_floats);
   if (sp <= 1) {
     launch_mode<MODE>(st, g, x, w, dy, out, nullptr, stats, 1, shift, acc ? 2 : 0);
@@ -1749,7 +1749,7 @@ static int wgrad_splits(const ConvGeom& g, long ws_cap_floats) {
 }
 
 // Y[N,P,Q,O] = conv(X[N,H,W,C], W_rsc); stats (optional) += [sum | sumsq] of (Y - shift) per output channel.
-void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf16* wrsc, bf16* y, float* stats,
+void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf16* wrsc, bf16* y, double* stats,
                      const float* shift, float* ws, long ws_floats, const bf16* res) {
   check_shape(s);
   ConvGeom g = make_geom(s);

@@ -66,7 +66,7 @@ FEDMI_DEV void in_bn8(const float* isc, const float* ish, float* v) {
 }
 
 __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
-                                                     bf16* __restrict__ y, float* __restrict__ stats,
+                                                     bf16* __restrict__ y, double* __restrict__ stats,
                                                      const float* __restrict__ shift, DwGeom g,
                                                      const float* __restrict__ isc) {
   extern __shared__ float wl[];   // [RS][C]
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x,
     const int grp = c >> 3, j = c & 7;
     float sum = 0.f;
     for (int t = grp; t < (int)blockDim.x; t += VC) sum += red[qn][t][j];
-    unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + qn) * g.C + c, sum);
+    unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + qn) * g.C + c, (double)sum);
   }
 }
 
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x,
 // LDS feed two outputs; same fused BN statistics and input-BN option as dw_fwd_kernel.
 template <int ST>
 __global__ __launch_bounds__(256) void dw_fwd3_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
-                                                      bf16* __restrict__ y, float* __restrict__ stats,
+                                                      bf16* __restrict__ y, double* __restrict__ stats,
                                                       const float* __restrict__ shift, DwGeom g,
                                                       const float* __restrict__ isc) {
   constexpr int NCOL = ST == 1 ? 4 : 5;
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(const bf16* __restrict__ x
     const int grp = c >> 3, j = c & 7;
     float sum = 0.f;
     for (int t = grp; t < (int)blockDim.x; t += VC) sum += red[qn][t][j];
-    unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + qn) * g.C + c, sum);
+    unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + qn) * g.C + c, (double)sum);
   }
 }
 
@@ -489,7 +489,7 @@ static DwGeom dw_geom(const DwShape& s) {
 }
 
 // w: fp32 [C][1][R][S] (PyTorch depthwise layout, used directly)
-void launch_dw_fwd(hipStream_t st, const DwShape& s, const bf16* x, const float* w, bf16* y, float* stats,
+void launch_dw_fwd(hipStream_t st, const DwShape& s, const bf16* x, const float* w, bf16* y, double* stats,
                    const float* shift, const float* isc) {
   const DwGeom g = dw_geom(s);
   const int tb = block_threads(g.C);

@@ -478,8 +478,10 @@ class CNNNativeTrainer(LocalTrainer):
             self._no_dgrad = ({id(self.preact.stem)} if self.preact else
                               {id(u) for u in self.blocks[0].units()} if self.blocks[0].first else set())
         # per-step accumulators: BN batch stats [2][O] and BN-backward sums [3][O], one fill each
-        self.stats_all = torch.zeros(sum(conv.STAT_REP * 2 * u.O for u in self.units), device=device)
-        self.red_all = torch.zeros(sum(3 * u.O for u in self.units), device=device)
+        # fp64 accumulators: the kernels add fp32 workgroup partials with fp64 atomics (order-independent sums)
+        self.stats_all = torch.zeros(sum(conv.STAT_REP * 2 * u.O for u in self.units), dtype=torch.float64,
+                                     device=device)
+        self.red_all = torch.zeros(sum(3 * u.O for u in self.units), dtype=torch.float64, device=device)
         so = ro = 0
         for u in self.units:
             u.stats = self.stats_all[so:so + conv.STAT_REP * 2 * u.O].view(conv.STAT_REP, 2, u.O)
@@ -491,11 +493,12 @@ class CNNNativeTrainer(LocalTrainer):
         self.wgrad_ws = torch.empty(max(max(u.ws_floats(nb) for u in self.units) for nb in {B, self.eval_bs}),
                                     device=device)
         # BN-backward two-level channel sums (replicated atomics + finalize; kept zero between uses)
-        self.bn_ws = torch.zeros(max(cnn.bn_bwd_ws_floats(B * u.P * u.P, u.O) for u in self.units), device=device)
+        self.bn_ws = torch.zeros(max(cnn.bn_bwd_ws_floats(B * u.P * u.P, u.O) for u in self.units),
+                                 dtype=torch.float64, device=device)
         # chained BN backward: every BN gets its own replica slice of one arena, the head launch clears the
         # arena each step and the apply kernels read the replicas directly (no finalize launch per BN)
         self.bn_chain = torch.zeros(sum((cnn.bn_bwd_chain_floats(u.O) + 3) // 4 * 4 for u in self.units) + 4,
-                                    device=device)
+                                    dtype=torch.float64, device=device)
         co = 0
         for u in self.units:
             n = (cnn.bn_bwd_chain_floats(u.O) + 3) // 4 * 4

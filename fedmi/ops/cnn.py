@@ -157,8 +157,8 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
            mask_bn: Optional[torch.Tensor] = None) -> None:
     """BatchNorm backward through an optional ReLU mask (``y``: forward output) for one or two BN
     branches sharing the incoming grad g = dya (+ dyb).  Writes dz for each branch, dgamma/dbeta,
-    and optionally g itself (``gout``, the identity-shortcut grad).  ``red``: [3, C] fp32 channel
-    sums.  With ``ws`` (>= :func:`bn_bwd_ws_floats` fp32, ZERO before first use; every call leaves it
+    and optionally g itself (``gout``, the identity-shortcut grad).  ``red``: [3, C] fp64 channel
+    sums.  With ``ws`` (>= :func:`bn_bwd_ws_floats` fp64, ZERO before first use; every call leaves it
     zero) the sums go through replicated atomics + a finalize and ``red`` needs no init; without,
     they are atomics straight into ``red``, which must be ZERO.  ``chained``: ``ws`` is this BN's own
     replica buffer (>= :func:`bn_bwd_chain_floats`, ZERO on entry -- the engine's head launch clears
@@ -167,8 +167,10 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
     whose output was never materialised (its consumer applied it on load)."""
     C = za.shape[-1]
     M = za.numel() // C
-    if red.numel() < 3 * C:
-        raise ValueError("bn_bwd: scratch too small")
+    if red.numel() < 3 * C or red.dtype != torch.float64:
+        raise ValueError("bn_bwd: red must be fp64 with >= 3*C elements")
+    if ws is not None and ws.dtype != torch.float64:
+        raise ValueError("bn_bwd: ws must be fp64")
     d = dict(dya=_p(dya), dyb=_p(dyb), y=_p(y), za=_p(za), meanA=_p(a.smean), invA=_p(a.sinv), gammaA=_p(a.gamma),
              dgammaA=_p(dgamma_a), dbetaA=_p(dbeta_a), dza=_p(dza), gout=_p(gout), shiftA=_p(a.shift),
              dadd=_p(dadd), msc=_p(mask_bn))
@@ -184,7 +186,7 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
 
 
 def bn_bwd_chain_floats(C: int) -> int:
-    """fp32 replica floats one BN needs in chained mode."""
+    """fp64 replica elements one BN needs in chained mode."""
     return 3 * int(C) * int(native.require().bn_bwd_chain_reps(int(C)))
 
 
@@ -200,4 +202,4 @@ def head(y: torch.Tensor, labels: torch.Tensor, base: int, W: torch.Tensor, b: t
     native.require().head(native.stream_handle(y.device), y.data_ptr(), labels.data_ptr(), base, _p(dbase), N,
                           H * Wd, C, J,
                           W.data_ptr(), b.data_ptr(), _p(pooled), _p(dlog), _p(dy), stats.data_ptr(), _p(dW), _p(db),
-                          int(train), _p(zero), zero.numel() if zero is not None else 0)
+                          int(train), _p(zero), zero.numel() * zero.element_size() // 4 if zero is not None else 0)

@@ -19,13 +19,15 @@ import torch
 from .. import native
 
 
-# BatchNorm statistics buffers are [STAT_REP, 2, C] fp32 replicas (csrc/kernels/common.h STAT_REP): the
-# conv / depthwise epilogues add into replica (workgroup % STAT_REP), bn_apply sums them.
+# BatchNorm statistics buffers are [STAT_REP, 2, C] fp64 replicas (csrc/kernels/common.h STAT_REP): the
+# conv / depthwise epilogues add their fp32 workgroup partials into replica (workgroup % STAT_REP) with fp64
+# atomics -- the totals do not depend on the order the workgroups arrive in (up to fp64 rounding, far
+# below the fp32 mean / variance derived from them) -- and bn_apply sums the replicas in fixed order.
 STAT_REP = 16
 
 
 def stats_buffer(C: int, device) -> torch.Tensor:
-    return torch.zeros(STAT_REP, 2, C, dtype=torch.float32, device=device)
+    return torch.zeros(STAT_REP, 2, C, dtype=torch.float64, device=device)
 
 
 def stats_total(stats: torch.Tensor) -> torch.Tensor:
@@ -34,9 +36,9 @@ def stats_total(stats: torch.Tensor) -> torch.Tensor:
 
 
 def _check_stats(stats: Optional[torch.Tensor], C: int, who: str) -> None:
-    if stats is not None and (stats.numel() != STAT_REP * 2 * C or stats.dtype != torch.float32
+    if stats is not None and (stats.numel() != STAT_REP * 2 * C or stats.dtype != torch.float64
                               or not stats.is_contiguous()):
-        raise ValueError(f"{who}: stats must be contiguous fp32 [STAT_REP={STAT_REP}, 2, {C}]")
+        raise ValueError(f"{who}: stats must be contiguous fp64 [STAT_REP={STAT_REP}, 2, {C}]")
 
 
 def pad8(c: int) -> int:
@@ -104,7 +106,7 @@ def conv2d_fwd(x: torch.Tensor, wrsc: torch.Tensor, stride: int, pad: int, Cw: O
                shift: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
                res: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y[N,P,Q,O] = conv(x[N,H,W,C]) (+ ``res`` [N,P,Q,O] bf16, fused into the epilogue: pre-activation
-    residual blocks; needs C % 64 == 0); ``stats`` ([STAT_REP, 2, O] fp32, :func:`stats_buffer`) +=
+    residual blocks; needs C % 64 == 0); ``stats`` ([STAT_REP, 2, O] fp64, :func:`stats_buffer`) +=
     per-channel sum / sum of squares of (y - shift) (``shift``: [O] fp32 or None = 0).  ``ws`` (fp32): optional split-K workspace for
     deep-K / few-tile shapes (see :func:`fd_ws_floats`)."""
     _check(x, torch.bfloat16, "conv2d_fwd.x")

@@ -49,6 +49,32 @@ class PeerAllReduce:
             self.comm.connect(handles)
         self._closed = False
         self.calls = 0
+        self.timeout_ms = float(timeout_ms)
+        # ranks sharing this GPU (one-GPU rehearsals / drills): a collective kernel spinning in its barrier
+        # can keep a co-located peer's queued kernels from being scheduled until the barrier times out, so
+        # each collective is gated by a host barrier once this rank's stream has drained.  Never taken with
+        # one rank per GPU (the production layout).
+        self.colocated = bool(self.comm.colocated) and world > 1
+        self._gate_n = 0
+        self._gate_failed = False
+
+    def _gate(self) -> bool:
+        """False: a peer never reached this collective (its kernel must not be launched; ``error()`` is set)."""
+        if not self.colocated:
+            return True
+        if self._gate_failed:
+            return False
+        torch.cuda.current_stream(self.device).synchronize()
+        self._gate_n += 1
+        key = f"fedmi/peer/{self.tag}/gate{self._gate_n}"
+        self.store.add(key, 1)
+        deadline = time.monotonic() + self.timeout_ms / 1e3
+        while int(self.store.add(key, 0)) < self.world:
+            if time.monotonic() > deadline:
+                self._gate_failed = True
+                return False
+            time.sleep(0.0002)
+        return True
 
     @property
     def capacity(self) -> int:
@@ -59,6 +85,8 @@ class PeerAllReduce:
 
     def allreduce_mean_(self, t: torch.Tensor) -> torch.Tensor:
         """In place: t <- mean over ranks (fp32, rank-ordered sum: bit-identical on every rank)."""
+        if not self._gate():
+            return t
         if t.dtype == torch.float32:
             if not t.is_contiguous() or t.data_ptr() % 16:
                 raise ValueError("peer all-reduce needs a contiguous, 16-byte aligned fp32 tensor")
@@ -72,6 +100,8 @@ class PeerAllReduce:
         return t
 
     def allreduce_sum(self, src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+        if not self._gate():
+            return dst
         self.comm.allreduce_f32(self._stream(), src.data_ptr(), dst.data_ptr(), src.numel(), float(scale),
                                 ALGOS[self.algo], 0)
         self.calls += 1
@@ -89,6 +119,8 @@ class PeerAllReduce:
         else:
             src = t.view(-1).view(torch.uint8)
         out = torch.empty(self.world * (nbytes + pad), dtype=torch.uint8, device=t.device)
+        if not self._gate():
+            return out.view(self.world, nbytes + pad)[:, :nbytes].contiguous().view(t.dtype).view((self.world,) + tuple(t.shape))
         self.comm.allgather(self._stream(), src.data_ptr(), out.data_ptr(), nbytes + pad, 0)
         self.calls += 1
         rows = out.view(self.world, nbytes + pad)[:, :nbytes].contiguous()
@@ -101,7 +133,7 @@ class PeerAllReduce:
 
     def error(self) -> int:
         """Nonzero if a barrier timed out (a peer died or never arrived); synchronous."""
-        return int(self.comm.error())
+        return int(self.comm.error()) or int(self._gate_failed)
 
     def close(self, barrier: bool = True) -> None:
         """Unmap peers.  With ``barrier`` every rank first drains its stream and waits for the

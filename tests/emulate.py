@@ -194,7 +194,7 @@ def sched_next(sched, counter, cur):
 
 def _coeffs(p: "cnn.BNParams", M: int, train: bool, eps: float, mom: float):
     if train:
-        tot = conv.stats_total(p.stats)
+        tot = conv.stats_total(p.stats).float()
         ms = tot[0] / M
         var = torch.clamp(tot[1] / M - ms * ms, min=0.0)
         mean = ms + (p.shift if p.shift is not None else 0.0)

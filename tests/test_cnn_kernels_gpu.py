@@ -134,10 +134,10 @@ def test_bn_forward_backward_with_projection_residual(gpu_device):
     ga, ba = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
     gb, bb = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
     # replicated statistics buffers: the totals spread unevenly over the STAT_REP replicas
-    wrep = torch.arange(1, conv.STAT_REP + 1, device=dev, dtype=torch.float32)
+    wrep = torch.arange(1, conv.STAT_REP + 1, device=dev, dtype=torch.float64)
     wrep = (wrep / wrep.sum()).view(-1, 1, 1)
-    sa = (torch.stack([za.float().sum(0), (za.float() ** 2).sum(0)]) * wrep).contiguous()
-    sb = (torch.stack([zb.float().sum(0), (zb.float() ** 2).sum(0)]) * wrep).contiguous()
+    sa = (torch.stack([za.double().sum(0), (za.double() ** 2).sum(0)]) * wrep).contiguous()
+    sb = (torch.stack([zb.double().sum(0), (zb.double() ** 2).sum(0)]) * wrep).contiguous()
     rma, rva, rmb, rvb = (torch.zeros(C, device=dev), torch.ones(C, device=dev),
                           torch.zeros(C, device=dev), torch.ones(C, device=dev))
     nbt = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -164,7 +164,7 @@ def test_bn_forward_backward_with_projection_residual(gpu_device):
     yref.backward(dya.float() + dyb.float())
     dza, dzb, gout = (torch.empty(M, C, dtype=torch.bfloat16, device=dev) for _ in range(3))
     dga, dba, dgb, dbb = (torch.empty(C, device=dev) for _ in range(4))
-    red = torch.zeros(3, C, device=dev)
+    red = torch.zeros(3, C, dtype=torch.float64, device=dev)
     cnn.bn_bwd(dya, za, A, dga, dba, dza, red, dyb=dyb, y=y, zb=zb, b=B, dgamma_b=dgb, dbeta_b=dbb, dzb=dzb,
                gout=gout)
     torch.cuda.synchronize()
@@ -175,8 +175,8 @@ def test_bn_forward_backward_with_projection_residual(gpu_device):
     mask = (y.float() > 0).float()
     assert _rel(gout.float(), (dya.float() + dyb.float()) * mask) < 1e-2
     # two-level reduction (replicated atomics + finalize): same result, red needs no init, ws left zero
-    ws = torch.zeros(cnn.bn_bwd_ws_floats(M, C), device=dev)
-    red2 = torch.full((3, C), float("nan"), device=dev)
+    ws = torch.zeros(cnn.bn_bwd_ws_floats(M, C), dtype=torch.float64, device=dev)
+    red2 = torch.full((3, C), float("nan"), dtype=torch.float64, device=dev)
     dza2, dzb2 = torch.empty_like(dza), torch.empty_like(dzb)
     dga2, dba2, dgb2, dbb2 = (torch.empty(C, device=dev) for _ in range(4))
     for _ in range(2):   # the scratch is reusable without re-zeroing
@@ -189,8 +189,8 @@ def test_bn_forward_backward_with_projection_residual(gpu_device):
     assert _rel(dga2, dga) < 1e-4 and _rel(dba2, dba) < 1e-4 and _rel(dgb2, dgb) < 1e-4
     # chained mode (the engine's default): per-BN replicas read by the apply kernel, no finalize launch,
     # no 'red' use at all; the replicas must be zero on entry (the head launch clears them per step)
-    rep = torch.zeros(cnn.bn_bwd_chain_floats(C), device=dev)
-    red3 = torch.full((3, C), float("nan"), device=dev)
+    rep = torch.zeros(cnn.bn_bwd_chain_floats(C), dtype=torch.float64, device=dev)
+    red3 = torch.full((3, C), float("nan"), dtype=torch.float64, device=dev)
     dza3, dzb3 = torch.empty_like(dza), torch.empty_like(dzb)
     dga3, dba3, dgb3, dbb3 = (torch.empty(C, device=dev) for _ in range(4))
     cnn.bn_bwd(dya, za, A, dga3, dba3, dza3, red3, dyb=dyb, y=y, zb=zb, b=B, dgamma_b=dgb3, dbeta_b=dbb3,
@@ -341,7 +341,7 @@ def test_depthwise_input_bn_and_z_mask(gpu_device):
     for use_mask in (False, True):
         dz = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
         dg, db_ = torch.empty(C, device=dev), torch.empty(C, device=dev)
-        red = torch.zeros(3, C, device=dev)
+        red = torch.zeros(3, C, dtype=torch.float64, device=dev)
         if use_mask:
             cnn.bn_bwd(dya, zr, A, dg, db_, dz, red, mask_bn=co2)
         else:
@@ -532,7 +532,7 @@ def test_bn_strided_channel_slices(gpu_device):
     assert float((wide[:, :off].float() - 7).abs().max()) == 0 and float((wide[:, off + C:].float() - 7).abs().max()) == 0
     dwide = torch.randn(M, W, device=dev).bfloat16()
     red = torch.empty(3, C, device=dev)
-    ws = torch.zeros(cnn.bn_bwd_ws_floats(M, C), device=dev)
+    ws = torch.zeros(cnn.bn_bwd_ws_floats(M, C), dtype=torch.float64, device=dev)
     d1, d2 = torch.empty_like(z), torch.empty_like(z)
     dg1, db1, dg2, db2 = (torch.empty(C, device=dev) for _ in range(4))
     cnn.bn_bwd(dwide[:, off:off + C], z, A, dg1, db1, d1, red, y=ys, ws=ws)
@@ -584,7 +584,7 @@ def test_bn_bwd_additive_residual_grad(gpu_device):
     extra = torch.randn(M, C, device=dev).bfloat16()
     d1, d2 = torch.empty_like(z), torch.empty_like(z)
     dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
-    ws = torch.zeros(cnn.bn_bwd_ws_floats(M, C), device=dev)
+    ws = torch.zeros(cnn.bn_bwd_ws_floats(M, C), dtype=torch.float64, device=dev)
     red = torch.empty(3, C, device=dev)
     cnn.bn_bwd(dy, z, A, dg, db, d1, red, y=y, ws=ws)
     cnn.bn_bwd(dy, z, A, dg, db, d2, red, y=y, ws=ws, dadd=extra)

@@ -70,6 +70,33 @@ def test_loss_and_tail_grads_match_torch(gpu_device, name, tail):
             assert int(rs[k]) == int(b), k
 
 
+@pytest.mark.parametrize("name", ["ResNet18", "MobileNet", "MobileNetV2", "VGG11", "PreActResNet18", "GoogLeNet"])
+def test_engine_is_deterministic(gpu_device, name):
+    """Two engines from the same init on the same batch produce bit-identical gradients, batch statistics and
+    running stats: BatchNorm sums go through fp64 atomics (order-independent), every split-K / weight-gradient
+    / head reduction is fixed-order."""
+    from fedmi.engine.cnn_native import CNNNativeTrainer
+
+    nb = 64
+    data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=128, n_test=64, seed=0)
+    init = build_model(name).state_dict()
+    runs = []
+    for _ in range(2):
+        tr = CNNNativeTrainer(name, data, gpu_device, TrainerConfig(batch_size=nb, augment=False, use_graph=False),
+                              init_state=init)
+        for _ in range(2):          # second pass: statistics shifted by the first pass's batch mean
+            tr.grads_for_batch(0, nb)
+        torch.cuda.synchronize()
+        runs.append(({k: p.grad.clone() for k, p in tr.model.named_parameters()},
+                     {k: b.clone() for k, b in tr.model.named_buffers()}, tr.train_stats()))
+    (ga, ba, sa), (gb, bb, sb) = runs
+    bad = [k for k in ga if not torch.equal(ga[k], gb[k])]
+    assert not bad, f"{len(bad)} / {len(ga)} gradients differ between identical runs: {bad[:5]}"
+    badb = [k for k in ba if not torch.equal(ba[k], bb[k])]
+    assert not badb, badb[:5]
+    assert sa.correct == sb.correct and sa.count == sb.count
+
+
 @pytest.mark.parametrize("name,avg_cos", [("ResNet18", 0.75), ("MobileNetV2", 0.35)])
 def test_native_matches_emulated_kernels_on_gpu(gpu_device, name, avg_cos):
     """Same engine schedule, same bf16 buffers, kernels vs their PyTorch twins (tests/emulate.py)."""

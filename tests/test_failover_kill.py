@@ -163,7 +163,7 @@ def _client_killed_mid_collective(tmp_path, device, n_clients=3):
         ok2 = wait_for(lambda: [r for r in _rounds(tmp_path / "coord.jsonl") if r["world"] == surv], timeout=90)
         recovery = ok2[0]["ts"] - t_kill
         aborted = [r for r in _rounds(tmp_path / "coord.jsonl", ok_only=False) if not r.get("ok")]
-        assert aborted and addrs[victim] in aborted[0]["failed"]
+        assert aborted and addrs[victim] in aborted[0]["failed"], aborted   # no spurious abort before the kill
         assert recovery < 30.0, recovery
         # every survivor -- each answered ABORTED -- was rolled back to the committed global model
         rb = wait_for(lambda: [r for r in read_jsonl(tmp_path / "coord.jsonl") if r.get("event") == "rollback"],
