@@ -178,6 +178,8 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--ckpt-dir", default=None)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--trace", action="store_true",
+                    help="print every rank's per-round train/test stats to stderr (synchronising: not for timing)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -247,6 +249,12 @@ def main() -> int:
         with phase("checkpoint"):
             writer.submit([prim / OPTIMIZED_MODEL, cpath] if prim is not None else cpath, trainer.state_dict(),
                           acc=1, epoch=r + 1)
+        if args.trace:
+            ts, fs = trainer.train_stats(), trainer.float_state()
+            ev = trainer.eval_stats() if not args.no_eval else None
+            print(f"[trace] rank {rank} round {r + 1}: train loss {ts.loss:.4f} acc {ts.acc:.2f} ({ts.count})"
+                  + (f" | eval acc {ev.acc:.2f} ({ev.count})" if ev else "")
+                  + f" | finite {bool(torch.isfinite(fs).all())} |w| {float(fs.norm()):.4f}", file=sys.stderr, flush=True)
 
     def barrier():
         if world > 1:

@@ -38,6 +38,8 @@ size_t select_state_bytes();
 int compact_chunk();
 void launch_ef_delta(hipStream_t, const float*, const float*, const float*, float*, long);
 void launch_topk(hipStream_t, const float*, long, int, void*, int*, int*, float*, float*);
+size_t topk_state_bytes();
+void launch_topk_ef(hipStream_t, const float*, const float*, float*, long, int, void*, int*, unsigned*, int*, float*);
 void launch_scatter_add_ranked(hipStream_t, float*, const int*, const float*, int, long, float, long);
 void launch_quant_int8(hipStream_t, const float*, long, signed char*, float*, float*);
 void launch_dequant_accum(hipStream_t, const signed char*, const float*, int, long, float*, float);
@@ -221,6 +223,16 @@ static void fedmi_bind(py::module_& m) {
 
   // ---- compression ---------------------------------------------------------------
   m.def("select_state_bytes", &select_state_bytes);
+  m.def("topk_state_bytes", &topk_state_bytes);
+  m.def("topk_ef", [](uintptr_t st, uintptr_t x, uintptr_t g, uintptr_t residual, long n, int k, uintptr_t state,
+                      uintptr_t cidx, uintptr_t ckey, uintptr_t idx, uintptr_t val) {
+    if (k <= 0 || k > n) throw std::invalid_argument("topk_ef: need 0 < k <= n");
+    if (n >= (1L << 31)) throw std::invalid_argument("topk_ef: n must fit int32 indices");
+    launch_topk_ef(S(st), P<const float>(x), P<const float>(g), P<float>(residual), n, k, P<void>(state), P<int>(cidx),
+                   P<unsigned>(ckey), P<int>(idx), P<float>(val));
+    check_last("topk_ef");
+  }, py::arg("stream"), py::arg("x"), py::arg("g"), py::arg("residual"), py::arg("n"), py::arg("k"), py::arg("state"),
+     py::arg("cidx"), py::arg("ckey"), py::arg("idx"), py::arg("val"));
   m.def("compact_chunk", &compact_chunk);
   m.def("ef_delta", [](uintptr_t st, uintptr_t local, uintptr_t global, uintptr_t residual, uintptr_t d, long n) {
     launch_ef_delta(S(st), P<const float>(local), P<const float>(global), P<const float>(residual), P<float>(d), n);

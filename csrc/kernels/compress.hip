@@ -13,6 +13,8 @@
 //
 // The compressed payloads are all-gathered over RCCL and folded back with
 // scatter_add_ranked (rank-ordered, atomic-free) / dequant_accum.
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -203,6 +205,230 @@ __global__ __launch_bounds__(256) void dequant_accum_kernel(const signed char* _
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused error-feedback top-k (the default path): 4 launches, 2 full passes over the state.
+//
+//   K1 tk_delta_hist   r <- x - g + r (the residual buffer holds d from here on), and a
+//                      histogram of the top 11 bits of |d| (key bits 30..20: exponent + 3
+//                      mantissa bits, each bin ~9 % of magnitude), LDS-privatised per
+//                      workgroup, nonzero bins added to the global histogram.
+//   K2 tk_pick1        one workgroup: the bin b1 holding the k-th largest key (block scan);
+//                      re-zeroes the histogram and the append counters for the next call.
+//   K3 tk_compact1     keys in bins > b1 are selected outright (idx/val appended, r <- 0);
+//                      keys in bin b1 become candidates (index + key appended).  Appends are
+//                      wave-aggregated (ballot + popcount, one global atomic per wave).
+//   K4 tk_select2      one workgroup: exact selection of the remaining `need` among the
+//                      candidates (2 LDS radix passes over the low 20 key bits; exact ties
+//                      resolved by the smallest indices, 3 more passes only when needed).
+//
+// The selected SET is exact and deterministic (ties: smallest indices); the order of the
+// (idx, val) list depends on arrival order, which no consumer sees: a rank's indices are
+// unique and scatter_add_ranked applies the ranks one after another.
+constexpr int kTkBins1 = 2048;
+struct TopKState {
+  unsigned hist[kTkBins1];
+  int b1, n_above, need, out_cnt, cand_cnt, pad[3];
+};
+
+FEDMI_DEV void tk_hist_add(unsigned* h, float v) { atomicAdd(&h[key_of(v) >> 20], 1u); }
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void tk_delta_hist_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                            float* __restrict__ r, long n, TopKState* __restrict__ st) {
+  __shared__ unsigned h[kTkBins1];
+  for (int i = threadIdx.x; i < kTkBins1; i += 256) h[i] = 0u;
+  __syncthreads();
+  const long stride = (long)gridDim.x * 256;
+  if (VEC) {
+    const long n4 = n >> 2;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    float4* r4 = reinterpret_cast<float4*>(r);
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+      const float4 a = x4[i], b = g4[i], c = r4[i];
+      const float4 d = make_float4(a.x - b.x + c.x, a.y - b.y + c.y, a.z - b.z + c.z, a.w - b.w + c.w);
+      r4[i] = d;
+      tk_hist_add(h, d.x);
+      tk_hist_add(h, d.y);
+      tk_hist_add(h, d.z);
+      tk_hist_add(h, d.w);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (int)(n & 3)) {
+      const long i = (n4 << 2) + threadIdx.x;
+      const float d = x[i] - g[i] + r[i];
+      r[i] = d;
+      tk_hist_add(h, d);
+    }
+  } else {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+      const float d = x[i] - g[i] + r[i];
+      r[i] = d;
+      tk_hist_add(h, d);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kTkBins1; i += 256)
+    if (h[i]) atomicAdd(&st->hist[i], h[i]);
+}
+
+// 1024 threads: bin b of h[0..nb) (nb = 1024 or 2048) such that above(b) < k <= above(b) + h[b],
+// scanning from the TOP bin down; above(b) = sum of the bins > b.  Result in res[0..1].
+FEDMI_DEV void tk_find_top(const unsigned* h, int nb, unsigned k, unsigned* scratch, unsigned* res) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, per = nb >> 10;
+  unsigned s = 0u;
+  for (int j = 0; j < per; ++j) s += h[nb - 1 - (t * per + j)];
+  unsigned inc = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned v = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += v;
+  }
+  if (lane == 63) scratch[w] = inc;
+  __syncthreads();
+  if (t == 0) {
+    unsigned a = 0u;
+    for (int q = 0; q < 16; ++q) { const unsigned v = scratch[q]; scratch[16 + q] = a; a += v; }
+  }
+  __syncthreads();
+  const unsigned excl = scratch[16 + w] + inc - s;
+  if (excl < k && k <= excl + s) {
+    unsigned above = excl;
+    for (int j = 0; j < per; ++j) {
+      const int b = nb - 1 - (t * per + j);
+      if (above + h[b] >= k) { res[0] = (unsigned)b; res[1] = above; break; }
+      above += h[b];
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void tk_pick1_kernel(TopKState* __restrict__ st, int k) {
+  __shared__ unsigned h[kTkBins1];
+  __shared__ unsigned scratch[32], res[2];
+  for (int i = threadIdx.x; i < kTkBins1; i += 1024) {
+    h[i] = st->hist[i];
+    st->hist[i] = 0u;                        // zero for the next call (graph-safe: no memset node)
+  }
+  __syncthreads();
+  tk_find_top(h, kTkBins1, (unsigned)k, scratch, res);
+  if (threadIdx.x == 0) {
+    st->b1 = (int)res[0];
+    st->n_above = (int)res[1];
+    st->need = k - (int)res[1];
+    st->out_cnt = 0;
+    st->cand_cnt = 0;
+  }
+}
+
+// wave-aggregated append: one global atomic per wave; returns this lane's slot (valid if flag)
+FEDMI_DEV int tk_append(int* counter, bool flag) {
+  const unsigned long long m = __ballot(flag);
+  if (m == 0ull) return 0;
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0) base = atomicAdd(counter, (int)__popcll(m));
+  base = __shfl(base, 0, 64);
+  const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  return base + (int)__popcll(m & lt);
+}
+
+__global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r, long n, TopKState* __restrict__ st,
+                                                          int* __restrict__ idx, float* __restrict__ val,
+                                                          int* __restrict__ cidx, unsigned* __restrict__ ckey) {
+  const unsigned b1 = (unsigned)st->b1;
+  const long stride = (long)gridDim.x * 256;
+  // uniform trip count per wave: every lane takes part in every ballot
+  for (long i0 = (long)blockIdx.x * 256; i0 < n; i0 += stride) {
+    const long i = i0 + threadIdx.x;
+    const bool in = i < n;
+    const float d = in ? r[i] : 0.f;
+    const unsigned key = key_of(d), bin = key >> 20;
+    const bool sel = in && bin > b1, cand = in && bin == b1;
+    const int ps = tk_append(&st->out_cnt, sel);
+    const int pc = tk_append(&st->cand_cnt, cand);
+    if (sel) { idx[ps] = (int)i; val[ps] = d; r[i] = 0.f; }
+    if (cand) { cidx[pc] = (int)i; ckey[pc] = key; }
+  }
+}
+
+__global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r, TopKState* __restrict__ st,
+                                                          const int* __restrict__ cidx, const unsigned* __restrict__ ckey,
+                                                          int* __restrict__ idx, float* __restrict__ val) {
+  __shared__ unsigned h[kTkBins1];
+  __shared__ unsigned scratch[32], res[2];
+  __shared__ int wcount;
+  const int t = threadIdx.x;
+  const int c = st->cand_cnt, nab = st->n_above;
+  const unsigned m = (unsigned)st->need;
+  // pass A: key bits 19..10
+  for (int i = t; i < 1024; i += 1024) h[i] = 0u;
+  __syncthreads();
+  for (int j = t; j < c; j += 1024) atomicAdd(&h[(ckey[j] >> 10) & 1023u], 1u);
+  __syncthreads();
+  tk_find_top(h, 1024, m, scratch, res);
+  const unsigned bA = res[0], mA = m - res[1];
+  // pass B: key bits 9..0 of the keys in bin bA
+  h[t] = 0u;
+  __syncthreads();
+  for (int j = t; j < c; j += 1024) {
+    const unsigned kk = ckey[j];
+    if (((kk >> 10) & 1023u) == bA) atomicAdd(&h[kk & 1023u], 1u);
+  }
+  __syncthreads();
+  tk_find_top(h, 1024, mA, scratch, res);
+  const unsigned bB = res[0];
+  const unsigned T = (bA << 10) | bB;        // low 20 bits of the k-th largest key
+  const unsigned ties_take = mA - res[1], ties = h[bB];
+  __syncthreads();
+  // exact ties beyond what is needed: keep the smallest indices (radix on the index, smallest first:
+  // digit' = nb-1-digit makes "top" the smallest)
+  unsigned ilim = 0xffffffffu;
+  if (ties > ties_take) {
+    unsigned pre = 0u, pmask = 0u, kk = ties_take;
+    const int shifts[3] = {20, 10, 0};
+    const int widths[3] = {11, 10, 10};
+    for (int ps = 0; ps < 3; ++ps) {
+      const int nb = 1 << widths[ps], sh = shifts[ps];
+      for (int i = t; i < kTkBins1; i += 1024) h[i] = 0u;
+      __syncthreads();
+      for (int j = t; j < c; j += 1024) {
+        const unsigned ix = (unsigned)cidx[j];
+        if ((ckey[j] & 0xfffffu) == T && (ix & pmask) == pre) atomicAdd(&h[nb - 1 - ((ix >> sh) & (nb - 1))], 1u);
+      }
+      __syncthreads();
+      tk_find_top(h, nb < 1024 ? 1024 : nb, kk, scratch, res);
+      pre |= (unsigned)(nb - 1 - (int)res[0]) << sh;
+      pmask |= (unsigned)(nb - 1) << sh;
+      kk -= res[1];
+      __syncthreads();
+    }
+    ilim = pre;                               // the ties_take-th smallest tied index
+  }
+  if (t == 0) wcount = 0;
+  __syncthreads();
+  for (int j0 = 0; j0 < c; j0 += 1024) {
+    const int j = j0 + t;
+    bool sel = false;
+    int ci = 0;
+    if (j < c) {
+      const unsigned low = ckey[j] & 0xfffffu;
+      ci = cidx[j];
+      sel = low > T || (low == T && (unsigned)ci <= ilim);
+    }
+    const unsigned long long msk = __ballot(sel);
+    int base = 0;
+    if ((t & 63) == 0 && msk) base = atomicAdd(&wcount, (int)__popcll(msk));
+    base = __shfl(base, 0, 64);
+    if (sel) {
+      const int lane = t & 63;
+      const int pos = nab + base + (int)__popcll(msk & (lane ? (~0ull >> (64 - lane)) : 0ull));
+      idx[pos] = ci;
+      val[pos] = r[ci];
+      r[ci] = 0.f;
+    }
+  }
+}
+
 int grid_for(long n) {
   long b = (n + 255) / 256;
   if (b < 1) b = 1;
@@ -236,6 +462,28 @@ void launch_topk(hipStream_t st, const float* d, long n, int k, void* state, int
   hipLaunchKernelGGL(compact_count_kernel, dim3(nb), dim3(256), 0, st, d, n, s, counts);
   hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(64), 0, st, counts, nb);
   hipLaunchKernelGGL(compact_write_kernel, dim3(nb), dim3(256), 0, st, d, n, s, counts, idx, val, residual);
+}
+
+size_t topk_state_bytes() { return sizeof(TopKState); }
+
+// Fused error-feedback exact top-k (see tk_* kernels).  residual: d is built IN it and the
+// selected entries are zeroed (= the new residual); state: topk_state_bytes(), zero on first
+// use (left zero by every call); cidx/ckey: candidate scratch of n entries each.
+void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* residual, long n, int k, void* state,
+                    int* cidx, unsigned* ckey, int* idx, float* val) {
+  TopKState* s = reinterpret_cast<TopKState*>(state);
+  const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g) |
+                     reinterpret_cast<uintptr_t>(residual)) & 15) == 0;
+  // ~16 float4 per thread (fewer global histogram atomics), at most 1024 workgroups
+  const int blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 16 * 1024 - 1) / (16 * 1024)));
+  if (vec)
+    hipLaunchKernelGGL(tk_delta_hist_kernel<true>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s);
+  else
+    hipLaunchKernelGGL(tk_delta_hist_kernel<false>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s);
+  hipLaunchKernelGGL(tk_pick1_kernel, dim3(1), dim3(1024), 0, st, s, k);
+  const int cblocks = (int)std::min<long>(2048, std::max<long>(1, (n + 8 * 256 - 1) / (8 * 256)));
+  hipLaunchKernelGGL(tk_compact1_kernel, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx, ckey);
+  hipLaunchKernelGGL(tk_select2_kernel, dim3(1), dim3(1024), 0, st, residual, s, cidx, ckey, idx, val);
 }
 
 // idx/val: [R][m] gathered payloads, applied in rank order 0..R-1.

@@ -867,7 +867,7 @@ class CNNNativeTrainer(LocalTrainer):
     def _capture(self, nb: int) -> torch.cuda.CUDAGraph:
         # a warm-up eager step precedes capture; snapshot and restore everything it touches
         saved = (self.fs.flat.clone(), self.fs.mom.clone(), [b.clone() for b in self.int_state()],
-                 self.counter.clone(), self.stats.clone())
+                 self.counter.clone(), self.stats.clone(), [u.shift.clone() for u in self.units])
         s = torch.cuda.Stream(self._device)
         s.wait_stream(torch.cuda.current_stream(self._device))
         with torch.cuda.stream(s):
@@ -883,6 +883,8 @@ class CNNNativeTrainer(LocalTrainer):
                 b.copy_(v)
             self.counter.copy_(saved[3])
             self.stats.copy_(saved[4])
+            for u, v in zip(self.units, saved[5]):      # BN statistics shifts: the replay starts bit-identical
+                u.shift.copy_(v)
         self.pack()
         self._graphs[("train", nb)] = g
         return g

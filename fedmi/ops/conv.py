@@ -31,8 +31,8 @@ def stats_buffer(C: int, device) -> torch.Tensor:
 
 
 def stats_total(stats: torch.Tensor) -> torch.Tensor:
-    """[2, C] totals (sum, sum of squares) of a replicated statistics buffer."""
-    return stats.view(STAT_REP, 2, -1).sum(0)
+    """[2, C] fp32 totals (sum, sum of squares) of a replicated fp64 statistics buffer."""
+    return stats.view(STAT_REP, 2, -1).sum(0).float()
 
 
 def _check_stats(stats: Optional[torch.Tensor], C: int, who: str) -> None:

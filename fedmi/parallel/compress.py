@@ -7,8 +7,10 @@ channel) and compresses the *update* instead:
 
 * ``topk``  — each client sends the k largest-magnitude entries of
   d = (w_local - w_global) + e (error feedback e carries the rest to the next
-  round); selection is an exact radix select on the GPU
-  (csrc/kernels/compress.hip); (idx, val) pairs are all-gathered (RCCL, or the
+  round); selection is exact, on the GPU in 4 launches and 2 passes over the
+  state (csrc/kernels/compress.hip ``launch_topk_ef``: fused delta + 11-bit
+  histogram, bin pick, wave-aggregated compaction of the certain winners and the
+  boundary-bin candidates, exact candidate select); (idx, val) pairs are all-gathered (RCCL, or the
   hipIpc peer kernels of :mod:`fedmi.parallel.peer`) and applied to the global
   model in rank order without atomics, so every client holds a bit-identical
   global model.  Payload per client: 8k bytes.
@@ -85,22 +87,24 @@ class TopKCompressor(_EFCompressor):
         self.idx = torch.empty(self.k, dtype=torch.int32, device=self.dev)
         self.val = torch.empty(self.k, dtype=torch.float32, device=self.dev)
         if self._nat is not None:
-            self.state = torch.zeros(self._nat.select_state_bytes(), dtype=torch.uint8, device=self.dev)
-            nblk = (self.n + self._nat.compact_chunk() - 1) // self._nat.compact_chunk()
-            self.counts = torch.zeros(2 * nblk, dtype=torch.int32, device=self.dev)
+            self.state = torch.zeros(self._nat.topk_state_bytes(), dtype=torch.uint8, device=self.dev)
+            # boundary-bin candidates (index, key): sized for the worst case (every entry in one bin)
+            self.cidx = torch.empty(self.n, dtype=torch.int32, device=self.dev)
+            self.ckey = torch.empty(self.n, dtype=torch.int32, device=self.dev)
 
     def compress(self, x: torch.Tensor) -> None:
-        self._delta(x)
         if self._nat is not None:
-            self._nat.topk(native.stream_handle(self.dev), self.d.data_ptr(), self.n, self.k, self.state.data_ptr(),
-                           self.counts.data_ptr(), self.idx.data_ptr(), self.val.data_ptr(),
-                           self.residual.data_ptr())
-        else:
-            sel = self.d.abs().topk(self.k, sorted=False).indices
-            self.idx.copy_(sel.to(torch.int32))
-            self.val.copy_(self.d[sel])
-            self.residual.copy_(self.d)
-            self.residual[sel] = 0.0
+            # d = x - global + residual is built IN the residual buffer; the winners are zeroed there
+            self._nat.topk_ef(native.stream_handle(self.dev), x.data_ptr(), self.global_ref.data_ptr(),
+                              self.residual.data_ptr(), self.n, self.k, self.state.data_ptr(), self.cidx.data_ptr(),
+                              self.ckey.data_ptr(), self.idx.data_ptr(), self.val.data_ptr())
+            return
+        self._delta(x)
+        sel = self.d.abs().topk(self.k, sorted=False).indices
+        self.idx.copy_(sel.to(torch.int32))
+        self.val.copy_(self.d[sel])
+        self.residual.copy_(self.d)
+        self.residual[sel] = 0.0
 
     def aggregate(self, trainer, group=None, transport=None) -> None:
         x = trainer.float_state()

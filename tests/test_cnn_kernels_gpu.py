@@ -531,7 +531,7 @@ def test_bn_strided_channel_slices(gpu_device):
     assert torch.equal(ys.float(), yc.float())
     assert float((wide[:, :off].float() - 7).abs().max()) == 0 and float((wide[:, off + C:].float() - 7).abs().max()) == 0
     dwide = torch.randn(M, W, device=dev).bfloat16()
-    red = torch.empty(3, C, device=dev)
+    red = torch.empty(3, C, dtype=torch.float64, device=dev)
     ws = torch.zeros(cnn.bn_bwd_ws_floats(M, C), dtype=torch.float64, device=dev)
     d1, d2 = torch.empty_like(z), torch.empty_like(z)
     dg1, db1, dg2, db2 = (torch.empty(C, device=dev) for _ in range(4))
@@ -585,7 +585,7 @@ def test_bn_bwd_additive_residual_grad(gpu_device):
     d1, d2 = torch.empty_like(z), torch.empty_like(z)
     dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
     ws = torch.zeros(cnn.bn_bwd_ws_floats(M, C), dtype=torch.float64, device=dev)
-    red = torch.empty(3, C, device=dev)
+    red = torch.empty(3, C, dtype=torch.float64, device=dev)
     cnn.bn_bwd(dy, z, A, dg, db, d1, red, y=y, ws=ws)
     cnn.bn_bwd(dy, z, A, dg, db, d2, red, y=y, ws=ws, dadd=extra)
     torch.cuda.synchronize()

@@ -60,6 +60,53 @@ def test_topk_exact(nat, gpu_device, n, k):
     assert res[~mask].abs().sum().item() == 0
 
 
+@pytest.mark.parametrize("n,k,ties", [(62006, 620, False), (5000, 1, False), (5000, 5000, False),
+                                       (1 << 20, 10000, False), (11173962, 111740, False), (70001, 700, True),
+                                       (4099, 17, True)])
+def test_topk_ef_exact(nat, gpu_device, n, k, ties):
+    """Fused error-feedback top-k: d = x - g + r built in r, exactly the k largest |d| selected (ties:
+    smallest indices), r keeps the rest; called twice on the same state (it must leave it reusable)."""
+    torch.manual_seed(k)
+    for rep in range(2):
+        x = torch.randn(n, device=gpu_device)
+        g = torch.randn(n, device=gpu_device) * 0.5
+        r = torch.randn(n, device=gpu_device) * 0.1
+        if ties:                              # many exact ties at the threshold magnitude
+            x[::3] = 0.75
+            g[::3] = 0.0
+            r[::3] = 0.0
+            x[1::7] = -0.75
+            g[1::7] = 0.0
+            r[1::7] = 0.0
+        x[::97] = 0.0
+        g[::97] = 0.0
+        r[::97] = 0.0
+        d = x - g + r
+        if rep == 0:
+            state = torch.zeros(nat.topk_state_bytes(), dtype=torch.uint8, device=gpu_device)
+            cidx = torch.empty(n, dtype=torch.int32, device=gpu_device)
+            ckey = torch.empty(n, dtype=torch.int32, device=gpu_device)
+        idx = torch.full((k,), -1, dtype=torch.int32, device=gpu_device)
+        val = torch.zeros(k, device=gpu_device)
+        nat.topk_ef(S(), x.data_ptr(), g.data_ptr(), r.data_ptr(), n, k, state.data_ptr(), cidx.data_ptr(),
+                    ckey.data_ptr(), idx.data_ptr(), val.data_ptr())
+        torch.cuda.synchronize()
+        assert int(idx.min()) >= 0
+        sel = idx.long()
+        assert len(set(sel.tolist())) == k
+        assert torch.equal(d[sel], val)
+        ref = d.abs().topk(k).values
+        assert torch.equal(val.abs().sort(descending=True).values, ref)
+        thr = ref[-1]
+        tied = (d.abs() == thr).nonzero().flatten()
+        chosen_tied = sel[d[sel].abs() == thr].sort().values
+        assert torch.equal(chosen_tied, tied[: chosen_tied.numel()])     # smallest indices win ties
+        mask = torch.ones(n, dtype=torch.bool, device=gpu_device)
+        mask[sel] = False
+        assert torch.equal(r[mask], d[mask])
+        assert r[~mask].abs().sum().item() == 0
+
+
 def test_scatter_add_ranked_is_rank_ordered(nat, gpu_device):
     """Two ranks' top-k payloads (unique indices within a rank, overlapping across ranks) are
     applied in rank order without atomics: the result equals the sequential fp32 sum."""

@@ -2,7 +2,9 @@
 """-c Y kernel timings (csrc/kernels/compress.hip) at the LeNet and ResNet-18 state sizes.
 
 For n = 62,006 (LeNet) and 11,173,962 (ResNet-18): device time of the
-error-feedback delta + exact top-k radix select (k = 1 %), of the rank-ordered
+error-feedback delta + exact top-k (k = 1 %: the fused 4-launch path ``topk_us``, round 2's
+ef_delta + 4-pass radix ``topk_r2_radix_us``, and one read+write pass over the state for
+scale ``rw_pass_us``), of the rank-ordered
 scatter of 4 ranks' payloads, of int8 quantisation and of a 4-rank dequant
 accumulate; plus payload bytes vs dense fp32.  One JSON line per size.
 """
@@ -56,7 +58,18 @@ def main() -> int:
             nat.topk(S(), d.data_ptr(), n, k, state.data_ptr(), counts.data_ptr(), idx.data_ptr(), val.data_ptr(),
                      resid.data_ptr())
 
-        t_topk = _time(topk, iters)
+        t_topk_old = _time(topk, iters)
+        tstate = torch.zeros(nat.topk_state_bytes(), dtype=torch.uint8, device=dev)
+        cidx = torch.empty(n, dtype=torch.int32, device=dev)
+        ckey = torch.empty(n, dtype=torch.int32, device=dev)
+
+        def topk_ef():
+            nat.topk_ef(S(), local.data_ptr(), glob.data_ptr(), resid.data_ptr(), n, k, tstate.data_ptr(),
+                        cidx.data_ptr(), ckey.data_ptr(), idx.data_ptr(), val.data_ptr())
+
+        t_topk = _time(topk_ef, iters)
+        dense = torch.randn(n, device=dev)
+        t_copy = _time(lambda: dense.mul_(1.0), iters)     # one read + write pass over the state
         idx_all = torch.stack([torch.randperm(n, device=dev)[:k].to(torch.int32) for _ in range(R)])
         val_all = torch.randn(R, k, device=dev)
         acc = torch.zeros(n, device=dev)
@@ -71,7 +84,8 @@ def main() -> int:
         t_dq = _time(lambda: nat.dequant_accum(S(), q_all.data_ptr(), s_all.data_ptr(), R, n, acc.data_ptr(), 1.0 / R),
                      iters)
         rec = {"bench": "compress_kernels", "payload": name, "n": n, "k": k,
-               "topk_us": round(t_topk, 2), "scatter_ranked_4rank_us": round(t_scatter, 2),
+               "topk_us": round(t_topk, 2), "topk_r2_radix_us": round(t_topk_old, 2),
+               "rw_pass_us": round(t_copy, 2), "scatter_ranked_4rank_us": round(t_scatter, 2),
                "quant_int8_us": round(t_q, 2), "dequant_accum_4rank_us": round(t_dq, 2),
                "bytes_dense": 4 * n, "bytes_topk": 8 * k, "bytes_int8": n + 4 * nch,
                "ratio_topk": round(4 * n / (8 * k), 2), "ratio_int8": round(4 * n / (n + 4 * nch), 2)}
