@@ -230,6 +230,11 @@ def main() -> int:
     if world > 1 and not args.eval_full:
         trainer.set_test_data(eval_shard(data.test, rank, world))
     hist = EvalHistory(trainer, args.warmup + args.steps)
+    if args.trace:
+        ys = trainer.train_set.y.long().cpu()
+        print(f"[trace] rank {rank} start: {len(ys)} train samples, labels {torch.bincount(ys, minlength=10).tolist()}, "
+              f"|w| {float(trainer.float_state().norm()):.4f}, sched {len(getattr(trainer, '_starts', []))} batches",
+              file=sys.stderr, flush=True)
 
     root = Path(args.ckpt_dir or tempfile.mkdtemp(prefix="fedmi_bench_"))
     prim = mount_dir(root, primary=True) if rank == 0 else None

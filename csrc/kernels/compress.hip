@@ -267,8 +267,11 @@ __global__ __launch_bounds__(256) void tk_delta_hist_kernel(const float* __restr
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kTkBins1; i += 256)
+  // rotated bin order per workgroup: concurrent workgroups hit different global bins at a time
+  for (int j = threadIdx.x; j < kTkBins1; j += 256) {
+    const int i = (j + (int)blockIdx.x * 64) & (kTkBins1 - 1);
     if (h[i]) atomicAdd(&st->hist[i], h[i]);
+  }
 }
 
 // 1024 threads: bin b of h[0..nb) (nb = 1024 or 2048) such that above(b) < k <= above(b) + h[b],
@@ -320,8 +323,8 @@ __global__ __launch_bounds__(1024) void tk_pick1_kernel(TopKState* __restrict__ 
   }
 }
 
-// wave-aggregated append: one global atomic per wave; returns this lane's slot (valid if flag)
-FEDMI_DEV int tk_append(int* counter, bool flag) {
+// wave-aggregated append into a block-local (LDS) counter; returns this lane's slot (valid if flag)
+FEDMI_DEV int tk_append_lds(int* counter, bool flag) {
   const unsigned long long m = __ballot(flag);
   if (m == 0ull) return 0;
   const int lane = threadIdx.x & 63;
@@ -332,22 +335,46 @@ FEDMI_DEV int tk_append(int* counter, bool flag) {
   return base + (int)__popcll(m & lt);
 }
 
+// Winners and candidates are staged in LDS and appended to the global lists once per workgroup (two
+// global atomics per flush): per-wave global atomics on the two list counters serialise at one L2
+// address each (2.4 ms at 11 M entries, measured).
+constexpr int kTkStage = 1024;
 __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r, long n, TopKState* __restrict__ st,
                                                           int* __restrict__ idx, float* __restrict__ val,
                                                           int* __restrict__ cidx, unsigned* __restrict__ ckey) {
+  __shared__ int s_si[kTkStage], s_ci[kTkStage];
+  __shared__ float s_sv[kTkStage];
+  __shared__ unsigned s_ck[kTkStage];
+  __shared__ int n_s, n_c, b_s, b_c;
   const unsigned b1 = (unsigned)st->b1;
   const long stride = (long)gridDim.x * 256;
-  // uniform trip count per wave: every lane takes part in every ballot
+  if (threadIdx.x == 0) { n_s = 0; n_c = 0; }
+  __syncthreads();
+  // uniform trip count per workgroup: every lane takes part in every ballot and barrier
   for (long i0 = (long)blockIdx.x * 256; i0 < n; i0 += stride) {
     const long i = i0 + threadIdx.x;
     const bool in = i < n;
     const float d = in ? r[i] : 0.f;
     const unsigned key = key_of(d), bin = key >> 20;
     const bool sel = in && bin > b1, cand = in && bin == b1;
-    const int ps = tk_append(&st->out_cnt, sel);
-    const int pc = tk_append(&st->cand_cnt, cand);
-    if (sel) { idx[ps] = (int)i; val[ps] = d; r[i] = 0.f; }
-    if (cand) { cidx[pc] = (int)i; ckey[pc] = key; }
+    const int ps = tk_append_lds(&n_s, sel);
+    const int pc = tk_append_lds(&n_c, cand);
+    if (sel) { s_si[ps] = (int)i; s_sv[ps] = d; r[i] = 0.f; }
+    if (cand) { s_ci[pc] = (int)i; s_ck[pc] = key; }
+    __syncthreads();
+    const bool last = i0 + stride >= n;
+    if (last || n_s > kTkStage - 256 || n_c > kTkStage - 256) {
+      if (threadIdx.x == 0) {
+        b_s = n_s ? atomicAdd(&st->out_cnt, n_s) : 0;
+        b_c = n_c ? atomicAdd(&st->cand_cnt, n_c) : 0;
+      }
+      __syncthreads();
+      for (int j = threadIdx.x; j < n_s; j += 256) { idx[b_s + j] = s_si[j]; val[b_s + j] = s_sv[j]; }
+      for (int j = threadIdx.x; j < n_c; j += 256) { cidx[b_c + j] = s_ci[j]; ckey[b_c + j] = s_ck[j]; }
+      __syncthreads();
+      if (threadIdx.x == 0) { n_s = 0; n_c = 0; }
+      __syncthreads();
+    }
   }
 }
 

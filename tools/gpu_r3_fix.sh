@@ -9,7 +9,7 @@ STAGES="${STAGES:-tests compress noniid}"
 for st in $STAGES; do
   case $st in
     tests)
-      timeout -k 10 900 python -u -m pytest tests/test_cnn_kernels_gpu.py tests/test_cnn_native_gpu.py \
+      timeout -k 10 900 python -u -m pytest ${TESTS:-tests/test_cnn_kernels_gpu.py tests/test_cnn_native_gpu.py} \
         tests/test_flat_ops_gpu.py -v --timeout 240 --timeout-method thread > $O/tests.log 2>&1; rc=$?
       echo "tests rc=$rc" >> $S; grep -E "FAILED|passed|failed" $O/tests.log | tail -12 >> $S; stop $rc ;;
     compress)
