@@ -244,14 +244,27 @@ __global__ __launch_bounds__(256) void tk_delta_hist_kernel(const float* __restr
     const float4* x4 = reinterpret_cast<const float4*>(x);
     const float4* g4 = reinterpret_cast<const float4*>(g);
     float4* r4 = reinterpret_cast<float4*>(r);
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
-      const float4 a = x4[i], b = g4[i], c = r4[i];
-      const float4 d = make_float4(a.x - b.x + c.x, a.y - b.y + c.y, a.z - b.z + c.z, a.w - b.w + c.w);
-      r4[i] = d;
-      tk_hist_add(h, d.x);
-      tk_hist_add(h, d.y);
-      tk_hist_add(h, d.z);
-      tk_hist_add(h, d.w);
+    // 4 float4 per thread per iteration, all 12 loads issued before the first use
+    for (long i0 = (long)blockIdx.x * 1024 + threadIdx.x; i0 < n4; i0 += stride * 4) {
+      float4 a[4], b[4], c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long i = i0 + u * 256;
+        if (i < n4) { a[u] = x4[i]; b[u] = g4[i]; c[u] = r4[i]; }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long i = i0 + u * 256;
+        if (i < n4) {
+          const float4 d = make_float4(a[u].x - b[u].x + c[u].x, a[u].y - b[u].y + c[u].y, a[u].z - b[u].z + c[u].z,
+                                       a[u].w - b[u].w + c[u].w);
+          r4[i] = d;
+          tk_hist_add(h, d.x);
+          tk_hist_add(h, d.y);
+          tk_hist_add(h, d.z);
+          tk_hist_add(h, d.w);
+        }
+      }
     }
     if (blockIdx.x == 0 && threadIdx.x < (int)(n & 3)) {
       const long i = (n4 << 2) + threadIdx.x;
@@ -338,11 +351,11 @@ FEDMI_DEV int tk_append_lds(int* counter, bool flag) {
 // Winners and candidates are staged in LDS and appended to the global lists once per workgroup (two
 // global atomics per flush): per-wave global atomics on the two list counters serialise at one L2
 // address each (2.4 ms at 11 M entries, measured).
-constexpr int kTkStage = 1024;
+constexpr int kTkStage = 4096;   // >= 2 iterations' worth (8 x 256 per iteration)
 __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r, long n, TopKState* __restrict__ st,
                                                           int* __restrict__ idx, float* __restrict__ val,
                                                           int* __restrict__ cidx, unsigned* __restrict__ ckey) {
-  __shared__ int s_si[kTkStage], s_ci[kTkStage];
+  __shared__ int s_si[kTkStage], s_ci[kTkStage];   // 4 x 16 KB of LDS
   __shared__ float s_sv[kTkStage];
   __shared__ unsigned s_ck[kTkStage];
   __shared__ int n_s, n_c, b_s, b_c;
@@ -350,20 +363,29 @@ __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r,
   const long stride = (long)gridDim.x * 256;
   if (threadIdx.x == 0) { n_s = 0; n_c = 0; }
   __syncthreads();
-  // uniform trip count per workgroup: every lane takes part in every ballot and barrier
-  for (long i0 = (long)blockIdx.x * 256; i0 < n; i0 += stride) {
-    const long i = i0 + threadIdx.x;
-    const bool in = i < n;
-    const float d = in ? r[i] : 0.f;
-    const unsigned key = key_of(d), bin = key >> 20;
-    const bool sel = in && bin > b1, cand = in && bin == b1;
-    const int ps = tk_append_lds(&n_s, sel);
-    const int pc = tk_append_lds(&n_c, cand);
-    if (sel) { s_si[ps] = (int)i; s_sv[ps] = d; r[i] = 0.f; }
-    if (cand) { s_ci[pc] = (int)i; s_ck[pc] = key; }
+  // uniform trip count per workgroup: every lane takes part in every ballot and barrier; 8 elements per
+  // thread per iteration, loaded before any is used
+  for (long i0 = (long)blockIdx.x * 2048; i0 < n; i0 += stride * 8) {
+    float dv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long i = i0 + u * 256 + threadIdx.x;
+      dv[u] = i < n ? r[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long i = i0 + u * 256 + threadIdx.x;
+      const bool in = i < n;
+      const unsigned key = key_of(dv[u]), bin = key >> 20;
+      const bool sel = in && bin > b1, cand = in && bin == b1;
+      const int ps = tk_append_lds(&n_s, sel);
+      const int pc = tk_append_lds(&n_c, cand);
+      if (sel) { s_si[ps] = (int)i; s_sv[ps] = dv[u]; r[i] = 0.f; }
+      if (cand) { s_ci[pc] = (int)i; s_ck[pc] = key; }
+    }
     __syncthreads();
-    const bool last = i0 + stride >= n;
-    if (last || n_s > kTkStage - 256 || n_c > kTkStage - 256) {
+    const bool last = i0 + stride * 8 >= n;
+    if (last || n_s > kTkStage - 8 * 256 || n_c > kTkStage - 8 * 256) {
       if (threadIdx.x == 0) {
         b_s = n_s ? atomicAdd(&st->out_cnt, n_s) : 0;
         b_c = n_c ? atomicAdd(&st->cand_cnt, n_c) : 0;
@@ -390,16 +412,27 @@ __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r,
   // pass A: key bits 19..10
   for (int i = t; i < 1024; i += 1024) h[i] = 0u;
   __syncthreads();
-  for (int j = t; j < c; j += 1024) atomicAdd(&h[(ckey[j] >> 10) & 1023u], 1u);
+  for (int j0 = t; j0 < c; j0 += 8 * 1024) {       // 8 loads in flight per thread
+    unsigned kk[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) kk[u] = j0 + u * 1024 < c ? ckey[j0 + u * 1024] : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (j0 + u * 1024 < c) atomicAdd(&h[(kk[u] >> 10) & 1023u], 1u);
+  }
   __syncthreads();
   tk_find_top(h, 1024, m, scratch, res);
   const unsigned bA = res[0], mA = m - res[1];
   // pass B: key bits 9..0 of the keys in bin bA
   h[t] = 0u;
   __syncthreads();
-  for (int j = t; j < c; j += 1024) {
-    const unsigned kk = ckey[j];
-    if (((kk >> 10) & 1023u) == bA) atomicAdd(&h[kk & 1023u], 1u);
+  for (int j0 = t; j0 < c; j0 += 8 * 1024) {
+    unsigned kk[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) kk[u] = j0 + u * 1024 < c ? ckey[j0 + u * 1024] : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (j0 + u * 1024 < c && ((kk[u] >> 10) & 1023u) == bA) atomicAdd(&h[kk[u] & 1023u], 1u);
   }
   __syncthreads();
   tk_find_top(h, 1024, mA, scratch, res);
@@ -433,25 +466,33 @@ __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r,
   }
   if (t == 0) wcount = 0;
   __syncthreads();
-  for (int j0 = 0; j0 < c; j0 += 1024) {
-    const int j = j0 + t;
-    bool sel = false;
-    int ci = 0;
-    if (j < c) {
-      const unsigned low = ckey[j] & 0xfffffu;
-      ci = cidx[j];
-      sel = low > T || (low == T && (unsigned)ci <= ilim);
+  for (int j0 = 0; j0 < c; j0 += 4 * 1024) {      // uniform trip count: every lane takes part in the ballots
+    unsigned kk[4];
+    int ci[4];
+    float dv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u * 1024 + t;
+      kk[u] = j < c ? ckey[j] : 0u;
+      ci[u] = j < c ? cidx[j] : 0;
     }
-    const unsigned long long msk = __ballot(sel);
-    int base = 0;
-    if ((t & 63) == 0 && msk) base = atomicAdd(&wcount, (int)__popcll(msk));
-    base = __shfl(base, 0, 64);
-    if (sel) {
-      const int lane = t & 63;
-      const int pos = nab + base + (int)__popcll(msk & (lane ? (~0ull >> (64 - lane)) : 0ull));
-      idx[pos] = ci;
-      val[pos] = r[ci];
-      r[ci] = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dv[u] = j0 + u * 1024 + t < c ? r[ci[u]] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned low = kk[u] & 0xfffffu;
+      const bool sel = j0 + u * 1024 + t < c && (low > T || (low == T && (unsigned)ci[u] <= ilim));
+      const unsigned long long msk = __ballot(sel);
+      int base = 0;
+      if ((t & 63) == 0 && msk) base = atomicAdd(&wcount, (int)__popcll(msk));
+      base = __shfl(base, 0, 64);
+      if (sel) {
+        const int lane = t & 63;
+        const int pos = nab + base + (int)__popcll(msk & (lane ? (~0ull >> (64 - lane)) : 0ull));
+        idx[pos] = ci[u];
+        val[pos] = dv[u];
+        r[ci[u]] = 0.f;
+      }
     }
   }
 }
@@ -501,14 +542,14 @@ void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* resid
   TopKState* s = reinterpret_cast<TopKState*>(state);
   const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g) |
                      reinterpret_cast<uintptr_t>(residual)) & 15) == 0;
-  // ~16 float4 per thread (fewer global histogram atomics), at most 1024 workgroups
-  const int blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 16 * 1024 - 1) / (16 * 1024)));
+  // ~8 float4 per thread, at most 2048 workgroups (their nonzero bins go to the global histogram)
+  const int blocks = (int)std::min<long>(2048, std::max<long>(1, (n + 8 * 1024 - 1) / (8 * 1024)));
   if (vec)
     hipLaunchKernelGGL(tk_delta_hist_kernel<true>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s);
   else
     hipLaunchKernelGGL(tk_delta_hist_kernel<false>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s);
   hipLaunchKernelGGL(tk_pick1_kernel, dim3(1), dim3(1024), 0, st, s, k);
-  const int cblocks = (int)std::min<long>(2048, std::max<long>(1, (n + 8 * 256 - 1) / (8 * 256)));
+  const int cblocks = (int)std::min<long>(2048, std::max<long>(1, (n + 2 * 2048 - 1) / (2 * 2048)));
   hipLaunchKernelGGL(tk_compact1_kernel, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx, ckey);
   hipLaunchKernelGGL(tk_select2_kernel, dim3(1), dim3(1024), 0, st, residual, s, cidx, ckey, idx, val);
 }
