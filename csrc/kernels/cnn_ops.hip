@@ -90,9 +90,13 @@ struct BNArgs {
                           // BN(z + b) in train mode == BN(z); running_mean tracks mean(z) + b
 };
 
-// per-channel scale/shift into LDS; block 0 also commits the running stats
-FEDMI_DEV void bn_coeffs(const BNArgs& a, int C, int M, float eps, float mom, int train, float* sc, float* sh) {
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+// per-channel scale/shift of channels [c_lo, c_lo + CC) into LDS sc[0..CC), sh[0..CC); the
+// commit block (its row chunk 0) also commits the running stats of those channels
+FEDMI_DEV void bn_coeffs(const BNArgs& a, int C, int M, float eps, float mom, int train, float* sc, float* sh,
+                         int c_lo = 0, int CC = -1, bool commit = true, bool count = true) {
+  if (CC < 0) CC = C;
+  for (int cc = threadIdx.x; cc < CC; cc += blockDim.x) {
+    const int c = c_lo + cc;
     float mean, inv;
     if (train) {
       // fp64 replicas (the epilogues add float block partials with fp64 atomics: the totals do not
@@ -108,7 +112,7 @@ FEDMI_DEV void bn_coeffs(const BNArgs& a, int C, int M, float eps, float mom, in
       const float var = (float)fmax(s2 / (double)M - msd * msd, 0.0);
       mean = ms + (a.shift ? a.shift[c] : 0.f);
       inv = rsqrtf(var + eps);
-      if (blockIdx.x == 0) {
+      if (commit) {
         a.smean[c] = mean;
         a.sinv[c] = inv;
         if (a.rmean) {
@@ -120,10 +124,10 @@ FEDMI_DEV void bn_coeffs(const BNArgs& a, int C, int M, float eps, float mom, in
       mean = a.rmean[c] - (a.cbias ? a.cbias[c] : 0.f);
       inv = rsqrtf(a.rvar[c] + eps);
     }
-    sc[c] = a.gamma[c] * inv;
-    sh[c] = a.beta[c] - mean * sc[c];
+    sc[cc] = a.gamma[c] * inv;
+    sh[cc] = a.beta[c] - mean * sc[cc];
   }
-  if (train && blockIdx.x == 0 && threadIdx.x == 0 && a.nbt) a.nbt[0] += 1;
+  if (train && commit && count && threadIdx.x == 0 && a.nbt) a.nbt[0] += 1;
 }
 
 // BN scale / shift only ([2][C] fp32), with bn_apply's running-stat / saved-stat commit: for a BN whose
@@ -133,6 +137,13 @@ __global__ __launch_bounds__(256) void bn_coeff_kernel(BNArgs A, int M, int C, f
   bn_coeffs(A, C, M, eps, mom, train, co, co + C);
 }
 
+// Channel-chunked grid of the apply kernels: blockIdx.y = chunk of CC <= 64 channels, blockIdx.x = chunk
+// of rows.  A block derives the BN coefficients of ITS channels only (16 fp64 replica reads x 2 per
+// channel): with the whole channel range per block, every block re-read all C channels' replicas --
+// 256 KB per block at C = 1024, which made the late small layers' applies latency-bound.
+constexpr int kBnChunk = 64;
+
+// Flat grid (C < 256 or C % 64 != 0: the coefficient prologue is cheap, every row load coalesced)
 // y = act(bnA(z) [+ res | + bnB(z2)])      res_mode: 0 none, 1 identity residual, 2 second BN branch
 // y rows have stride ldy (>= C): a channel slice of a concatenated output (GoogLeNet)
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ z, BNArgs A, const bf16* __restrict__ z2,
@@ -144,8 +155,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
   float* sh = co + C;
   float* sc2 = co + 2 * C;
   float* sh2 = co + 3 * C;
-  bn_coeffs(A, C, M, eps, mom, train, sc, sh);
-  if (res_mode == 2) bn_coeffs(B, C, M, eps, mom, train, sc2, sh2);
+  bn_coeffs(A, C, M, eps, mom, train, sc, sh, 0, C, blockIdx.x == 0);
+  if (res_mode == 2) bn_coeffs(B, C, M, eps, mom, train, sc2, sh2, 0, C, blockIdx.x == 0);
   __syncthreads();
   const int VR = C >> 3;
   const long nv = (long)M * VR;
@@ -171,6 +182,54 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
       for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
     }
     store8f(y + (ldy == C ? i * 8 : (i / VR) * ldy + c0), v);
+  }
+}
+
+// y = act(bnA(z) [+ res | + bnB(z2)])      res_mode: 0 none, 1 identity residual, 2 second BN branch
+// y rows have stride ldy (>= C): a channel slice of a concatenated output (GoogLeNet)
+__global__ __launch_bounds__(256) void bn_apply_chunk_kernel(const bf16* __restrict__ z, BNArgs A,
+                                                             const bf16* __restrict__ z2, BNArgs B,
+                                                             const bf16* __restrict__ res, bf16* __restrict__ y, int M,
+                                                             int C, float eps, float mom, int train, int relu,
+                                                             int res_mode, int ldy, int rows_per_block) {
+  __shared__ float co[4][kBnChunk];
+  const int CC = min(kBnChunk, C), c_lo = blockIdx.y * CC;
+  const bool commit = blockIdx.x == 0;
+  bn_coeffs(A, C, M, eps, mom, train, co[0], co[1], c_lo, CC, commit, blockIdx.y == 0);
+  if (res_mode == 2) bn_coeffs(B, C, M, eps, mom, train, co[2], co[3], c_lo, CC, commit, blockIdx.y == 0);
+  __syncthreads();
+  const int VC = CC >> 3, rstep = 256 / VC;
+  const int cv = threadIdx.x % VC, c0 = cv * 8, cg = c_lo + c0;
+  const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
+  if ((int)threadIdx.x >= rstep * VC) return;
+  float sa[8], ha[8], sb[8], hb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sa[j] = co[0][c0 + j]; ha[j] = co[1][c0 + j];
+    sb[j] = res_mode == 2 ? co[2][c0 + j] : 0.f; hb[j] = res_mode == 2 ? co[3][c0 + j] : 0.f;
+  }
+  for (int r = rb + (int)threadIdx.x / VC; r < re; r += rstep) {
+    const long i = (long)r * C + cg;
+    float v[8];
+    load8f(z + i, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * sa[j] + ha[j];
+    if (res_mode == 1) {
+      float t[8];
+      load8f(res + i, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += t[j];
+    } else if (res_mode == 2) {
+      float t[8];
+      load8f(z2 + i, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += t[j] * sb[j] + hb[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+    }
+    store8f(y + (long)r * ldy + cg, v);
   }
 }
 
@@ -307,9 +366,10 @@ struct BwdOut {
   const bf16* dadd;       // optional grad added to dza (a residual edge that bypasses this BN)
 };
 
+// Flat grid variant (see bn_apply_kernel).
 // partials != null (chained mode): the channel sums are read straight from the reduce kernel's
 // 'reps' atomic replicas (no finalize launch); the caller zeroes them before the next step.
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdIn in, BwdOut out, const double* __restrict__ red,
+__global__ __launch_bounds__(256) void bn_bwd_apply_flat_kernel(BwdIn in, BwdOut out, const double* __restrict__ red,
                                                            int M, int C, const double* __restrict__ partials,
                                                            int reps) {
   extern __shared__ float co[];   // [6][C]: kA, bA, cA, kB, bB, cB  (dz = k*g + b*xhat + c)
@@ -374,6 +434,82 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdIn in, BwdOut out,
 #pragma unroll
       for (int j = 0; j < 8; ++j) d[j] = co[3 * C + c0 + j] * g[j] + co[4 * C + c0 + j] * z[j] + co[5 * C + c0 + j];
       store8f(out.dzb + i * 8, d);
+    }
+  }
+}
+
+// partials != null (chained mode): the channel sums are read straight from the reduce kernel's
+// 'reps' atomic replicas (no finalize launch); the caller zeroes them before the next step.
+// Channel-chunked grid like bn_apply_kernel: a block derives the coefficients of its CC channels only.
+__global__ __launch_bounds__(256) void bn_bwd_apply_chunk_kernel(BwdIn in, BwdOut out, const double* __restrict__ red,
+                                                                 int M, int C, const double* __restrict__ partials,
+                                                                 int reps, int rows_per_block) {
+  __shared__ float co[6][kBnChunk];   // kA, bA, cA, kB, bB, cB  (dz = k*g + b*z + c)
+  const int CC = min(kBnChunk, C), c_lo = blockIdx.y * CC;
+  const float invM = 1.f / (float)M;
+  for (int cc = threadIdx.x; cc < CC; cc += blockDim.x) {
+    const int c = c_lo + cc;
+    double dg = 0.0, dgx = 0.0, dgx2 = 0.0;
+    if (partials) {
+      for (int r = 0; r < reps; ++r) {           // fixed order: every block derives identical coefficients
+        const double* pr = partials + (long)r * 3 * C;
+        dg += pr[c];
+        dgx += pr[C + c];
+        if (in.zb) dgx2 += pr[2 * C + c];
+      }
+    } else {
+      dg = red[c];
+      dgx = red[C + c];
+      if (in.zb) dgx2 = red[2 * C + c];
+    }
+    const float sg = (float)dg, sgx = (float)dgx, sgx2 = (float)dgx2;
+    const float scA = out.gammaA[c] * in.invA[c];
+    // dz = scA * (g - sg/M - xhat * sgx/M),  xhat = (z - mean) * inv
+    co[0][cc] = scA;
+    co[1][cc] = -scA * sgx * invM * in.invA[c];
+    co[2][cc] = -scA * sg * invM + scA * sgx * invM * in.invA[c] * in.meanA[c];
+    if (blockIdx.x == 0) {
+      out.dgammaA[c] = sgx;
+      out.dbetaA[c] = sg;
+      if (out.shiftA) out.shiftA[c] = in.meanA[c];
+    }
+    if (in.zb) {
+      const float scB = out.gammaB[c] * in.invB[c];
+      co[3][cc] = scB;
+      co[4][cc] = -scB * sgx2 * invM * in.invB[c];
+      co[5][cc] = -scB * sg * invM + scB * sgx2 * invM * in.invB[c] * in.meanB[c];
+      if (blockIdx.x == 0) {
+        out.dgammaB[c] = sgx2;
+        out.dbetaB[c] = sg;
+        if (out.shiftB) out.shiftB[c] = in.meanB[c];
+      }
+    }
+  }
+  __syncthreads();
+  const int VC = CC >> 3, rstep = 256 / VC;
+  const int cv = threadIdx.x % VC, c0 = cv * 8, cg = c_lo + c0;
+  const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
+  if ((int)threadIdx.x >= rstep * VC) return;
+  for (int r = rb + (int)threadIdx.x / VC; r < re; r += rstep) {
+    const long i = (long)r * C + cg;
+    float g[8], z[8], d[8];
+    load8f(in.za + i, z);
+    load_g(in, r, cg >> 3, g, z);
+    if (out.gout) store8f(out.gout + i, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = co[0][c0 + j] * g[j] + co[1][c0 + j] * z[j] + co[2][c0 + j];
+    if (out.dadd) {
+      float t[8];
+      load8f(out.dadd + i, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] += t[j];
+    }
+    store8f(out.dza + i, d);
+    if (in.zb) {
+      load8f(in.zb + i, z);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = co[3][c0 + j] * g[j] + co[4][c0 + j] * z[j] + co[5][c0 + j];
+      store8f(out.dzb + i, d);
     }
   }
 }
@@ -735,6 +871,17 @@ __global__ void sched_next_kernel(const int* __restrict__ sched, int* __restrict
 
 int grid_for(long nv) { return (int)std::min<long>((nv + 255) / 256, 2048); }
 
+// bn_apply / bn_bwd_apply grid: y = channel chunks of kBnChunk, x = row chunks of ~8 rows per thread-row
+// slot (C % 8 == 0; chunks of 64 channels need C % 64 == 0 when C > 64)
+bool use_chunked(int C) { return C >= 256 && C % kBnChunk == 0; }
+
+dim3 apply_grid(int M, int C) {
+  const int CC = std::min(kBnChunk, C), nch = C / CC, rstep = 256 / (CC / 8);
+  const long want = ((long)M + 8L * rstep - 1) / (8L * rstep);
+  const int bx = (int)std::max<long>(1, std::min<long>(want, std::max(1, 2048 / nch)));
+  return dim3(bx, nch);
+}
+
 }  // namespace
 
 namespace fedmi {
@@ -800,8 +947,14 @@ void launch_bn_apply(hipStream_t st, const bf16* z, const BNDesc& a, const bf16*
   if (ldy < C || ldy % 8) throw std::invalid_argument("bn_apply: bad output row stride");
   const int res_mode = b ? 2 : (res ? 1 : 0);
   const BNArgs bb = b ? to_args(*b) : BNArgs{};
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((long)M * (C / 8))), dim3(256), 4 * C * sizeof(float), st, z,
-                     to_args(a), z2, bb, res, y, M, C, eps, mom, train, relu, res_mode, ldy);
+  if (use_chunked(C)) {
+    const dim3 grid = apply_grid(M, C);
+    hipLaunchKernelGGL(bn_apply_chunk_kernel, grid, dim3(256), 0, st, z, to_args(a), z2, bb, res, y, M, C, eps, mom,
+                       train, relu, res_mode, ldy, (M + (int)grid.x - 1) / (int)grid.x);
+  } else {
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((long)M * (C / 8))), dim3(256), 4 * C * sizeof(float), st, z,
+                       to_args(a), z2, bb, res, y, M, C, eps, mom, train, relu, res_mode, ldy);
+  }
 }
 
 void launch_bn_coeff(hipStream_t st, const BNDesc& a, int M, int C, float eps, float mom, int train, float* co) {
@@ -859,17 +1012,29 @@ void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, double* red, int M, int C
     const int reps = bn_bwd_chain_reps(C);
     if (!ws || ws_floats < (long)reps * 3 * C) throw std::invalid_argument("bn_bwd: chained replicas too small");
     hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(tb), 0, st, in, red, M, C, rows_per_block, ws, reps);
-    const int gblk = (int)std::min<long>(((long)M * VR + 255) / 256, 1024);
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(gblk), dim3(256), 6 * C * sizeof(float), st, in, out, red, M, C,
-                       ws, reps);
+    if (use_chunked(C)) {
+      const dim3 ag = apply_grid(M, C);
+      hipLaunchKernelGGL(bn_bwd_apply_chunk_kernel, ag, dim3(256), 0, st, in, out, red, M, C, ws, reps,
+                         (M + (int)ag.x - 1) / (int)ag.x);
+    } else {
+      const int gblk = (int)std::min<long>(((long)M * VR + 255) / 256, 1024);
+      hipLaunchKernelGGL(bn_bwd_apply_flat_kernel, dim3(gblk), dim3(256), 6 * C * sizeof(float), st, in, out, red, M,
+                         C, ws, reps);
+    }
     return;
   }
   const bool two = ws && ws_floats >= (long)BN_REP * 3 * C;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(tb), 0, st, in, red, M, C, rows_per_block,
                      two ? ws : nullptr, BN_REP);
   if (two) hipLaunchKernelGGL(bn_bwd_finalize, dim3((3 * C + 255) / 256), dim3(256), 0, st, ws, C, red);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for((long)M * VR)), dim3(256), 6 * C * sizeof(float), st, in, out,
-                     red, M, C, nullptr, 0);
+  if (use_chunked(C)) {
+    const dim3 ag = apply_grid(M, C);
+    hipLaunchKernelGGL(bn_bwd_apply_chunk_kernel, ag, dim3(256), 0, st, in, out, red, M, C, nullptr, 0,
+                       (M + (int)ag.x - 1) / (int)ag.x);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_apply_flat_kernel, dim3(grid_for((long)M * VR)), dim3(256), 6 * C * sizeof(float), st,
+                       in, out, red, M, C, nullptr, 0);
+  }
 }
 
 void launch_head(hipStream_t st, const bf16* y, const int* labels, int base, const int* dbase, int N, int HW, int C, int J,

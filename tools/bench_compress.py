@@ -68,6 +68,19 @@ def main() -> int:
                         cidx.data_ptr(), ckey.data_ptr(), idx.data_ptr(), val.data_ptr())
 
         t_topk = _time(topk_ef, iters)
+        # realistic rounds: a fresh update every call (the residual carries the unsent part forward)
+        ups = [torch.randn(n, device=dev) * 0.01 for _ in range(4)]
+        calls = [0]
+
+        def topk_ef_fresh():
+            local.copy_(glob).add_(ups[calls[0] % 4])
+            calls[0] += 1
+            topk_ef()
+
+        resid.zero_()
+        t_topk_fresh = _time(topk_ef_fresh, iters) - _time(lambda: local.copy_(glob).add_(ups[0]), iters)
+        st_words = tstate.view(torch.int32).cpu()
+        cand = int(st_words[2048 + 4])
         dense = torch.randn(n, device=dev)
         t_copy = _time(lambda: dense.mul_(1.0), iters)     # one read + write pass over the state
         idx_all = torch.stack([torch.randperm(n, device=dev)[:k].to(torch.int32) for _ in range(R)])
@@ -84,7 +97,8 @@ def main() -> int:
         t_dq = _time(lambda: nat.dequant_accum(S(), q_all.data_ptr(), s_all.data_ptr(), R, n, acc.data_ptr(), 1.0 / R),
                      iters)
         rec = {"bench": "compress_kernels", "payload": name, "n": n, "k": k,
-               "topk_us": round(t_topk, 2), "topk_r2_radix_us": round(t_topk_old, 2),
+               "topk_us": round(t_topk, 2), "topk_fresh_update_us": round(t_topk_fresh, 2), "candidates_last": cand,
+               "topk_r2_radix_us": round(t_topk_old, 2),
                "rw_pass_us": round(t_copy, 2), "scatter_ranked_4rank_us": round(t_scatter, 2),
                "quant_int8_us": round(t_q, 2), "dequant_accum_4rank_us": round(t_dq, 2),
                "bytes_dense": 4 * n, "bytes_topk": 8 * k, "bytes_int8": n + 4 * nch,
