@@ -227,7 +227,7 @@ static void fedmi_bind(py::module_& m) {
   m.def("topk_ef", [](uintptr_t st, uintptr_t x, uintptr_t g, uintptr_t residual, long n, int k, uintptr_t state,
                       uintptr_t cidx, uintptr_t ckey, uintptr_t idx, uintptr_t val) {
     if (k <= 0 || k > n) throw std::invalid_argument("topk_ef: need 0 < k <= n");
-    if (n >= (1L << 31)) throw std::invalid_argument("topk_ef: n must fit int32 indices");
+    if (n >= (1L << 30)) throw std::invalid_argument("topk_ef: n must be < 2^30 (int32 indices, 2n scratch)");
     launch_topk_ef(S(st), P<const float>(x), P<const float>(g), P<float>(residual), n, k, P<void>(state), P<int>(cidx),
                    P<unsigned>(ckey), P<int>(idx), P<float>(val));
     check_last("topk_ef");

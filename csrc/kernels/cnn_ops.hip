@@ -208,28 +208,33 @@ __global__ __launch_bounds__(256) void bn_apply_chunk_kernel(const bf16* __restr
     sa[j] = co[0][c0 + j]; ha[j] = co[1][c0 + j];
     sb[j] = res_mode == 2 ? co[2][c0 + j] : 0.f; hb[j] = res_mode == 2 ? co[3][c0 + j] : 0.f;
   }
-  for (int r = rb + (int)threadIdx.x / VC; r < re; r += rstep) {
-    const long i = (long)r * C + cg;
-    float v[8];
-    load8f(z + i, v);
+  // two rows per thread-slot, every load issued before the first use (the kernel is latency-bound on
+  // the small late layers)
+  for (int r0 = rb + (int)threadIdx.x / VC; r0 < re; r0 += 2 * rstep) {
+    float v[2][8], t[2][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = v[j] * sa[j] + ha[j];
-    if (res_mode == 1) {
-      float t[8];
-      load8f(res + i, t);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += t[j];
-    } else if (res_mode == 2) {
-      float t[8];
-      load8f(z2 + i, t);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += t[j] * sb[j] + hb[j];
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + u * rstep;
+      if (r < re) {
+        const long i = (long)r * C + cg;
+        load8f(z + i, v[u]);
+        if (res_mode == 1) load8f(res + i, t[u]);
+        else if (res_mode == 2) load8f(z2 + i, t[u]);
+      }
     }
-    if (relu) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + u * rstep;
+      if (r >= re) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = v[u][j] * sa[j] + ha[j];
+        if (res_mode == 1) x += t[u][j];
+        else if (res_mode == 2) x += t[u][j] * sb[j] + hb[j];
+        v[u][j] = relu ? fmaxf(x, 0.f) : x;
+      }
+      store8f(y + (long)r * ldy + cg, v[u]);
     }
-    store8f(y + (long)r * ldy + cg, v);
   }
 }
 
@@ -490,26 +495,42 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_chunk_kernel(BwdIn in, BwdOu
   const int cv = threadIdx.x % VC, c0 = cv * 8, cg = c_lo + c0;
   const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
   if ((int)threadIdx.x >= rstep * VC) return;
-  for (int r = rb + (int)threadIdx.x / VC; r < re; r += rstep) {
-    const long i = (long)r * C + cg;
-    float g[8], z[8], d[8];
-    load8f(in.za + i, z);
-    load_g(in, r, cg >> 3, g, z);
-    if (out.gout) store8f(out.gout + i, g);
+  // two rows per thread-slot, every load issued before the first use
+  for (int r0 = rb + (int)threadIdx.x / VC; r0 < re; r0 += 2 * rstep) {
+    float z[2][8], g[2][8], zb[2][8], da[2][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = co[0][c0 + j] * g[j] + co[1][c0 + j] * z[j] + co[2][c0 + j];
-    if (out.dadd) {
-      float t[8];
-      load8f(out.dadd + i, t);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] += t[j];
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + u * rstep;
+      if (r < re) {
+        const long i = (long)r * C + cg;
+        load8f(in.za + i, z[u]);
+        if (in.zb) load8f(in.zb + i, zb[u]);
+        if (out.dadd) load8f(out.dadd + i, da[u]);
+      }
     }
-    store8f(out.dza + i, d);
-    if (in.zb) {
-      load8f(in.zb + i, z);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = co[3][c0 + j] * g[j] + co[4][c0 + j] * z[j] + co[5][c0 + j];
-      store8f(out.dzb + i, d);
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + u * rstep;
+      if (r < re) load_g(in, r, cg >> 3, g[u], z[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + u * rstep;
+      if (r >= re) continue;
+      const long i = (long)r * C + cg;
+      if (out.gout) store8f(out.gout + i, g[u]);
+      float d[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        d[j] = co[0][c0 + j] * g[u][j] + co[1][c0 + j] * z[u][j] + co[2][c0 + j];
+        if (out.dadd) d[j] += da[u][j];
+      }
+      store8f(out.dza + i, d);
+      if (in.zb) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = co[3][c0 + j] * g[u][j] + co[4][c0 + j] * zb[u][j] + co[5][c0 + j];
+        store8f(out.dzb + i, d);
+      }
     }
   }
 }
@@ -877,7 +898,7 @@ bool use_chunked(int C) { return C >= 256 && C % kBnChunk == 0; }
 
 dim3 apply_grid(int M, int C) {
   const int CC = std::min(kBnChunk, C), nch = C / CC, rstep = 256 / (CC / 8);
-  const long want = ((long)M + 8L * rstep - 1) / (8L * rstep);
+  const long want = ((long)M + 2L * rstep - 1) / (2L * rstep);   // ~2 rows per thread-slot
   const int bx = (int)std::max<long>(1, std::min<long>(want, std::max(1, 2048 / nch)));
   return dim3(bx, nch);
 }

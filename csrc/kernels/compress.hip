@@ -225,9 +225,13 @@ __global__ __launch_bounds__(256) void dequant_accum_kernel(const signed char* _
 // (idx, val) list depends on arrival order, which no consumer sees: a rank's indices are
 // unique and scatter_add_ranked applies the ranks one after another.
 constexpr int kTkBins1 = 2048;
+constexpr long kTkThreeLevel = 1 << 20;   // n at which the 3-level path takes over
 struct TopKState {
   unsigned hist[kTkBins1];
   int b1, n_above, need, out_cnt, cand_cnt, pad[3];
+  // 3-level path (large n): level-2 histogram of the candidates' key bits 19..9
+  unsigned hist2[kTkBins1];
+  int b2, n_above2, need2, out2_cnt, cand2_cnt, pad2[3];
 };
 
 FEDMI_DEV void tk_hist_add(unsigned* h, float v) { atomicAdd(&h[key_of(v) >> 20], 1u); }
@@ -336,6 +340,26 @@ __global__ __launch_bounds__(1024) void tk_pick1_kernel(TopKState* __restrict__ 
   }
 }
 
+// level 2 (large n): the bin b2 of key bits 19..9 holding the need-th largest candidate
+__global__ __launch_bounds__(1024) void tk_pick2_kernel(TopKState* __restrict__ st) {
+  __shared__ unsigned h[kTkBins1];
+  __shared__ unsigned scratch[32], res[2];
+  for (int i = threadIdx.x; i < kTkBins1; i += 1024) {
+    h[i] = st->hist2[i];
+    st->hist2[i] = 0u;
+  }
+  __syncthreads();
+  const int need = st->need;
+  tk_find_top(h, kTkBins1, (unsigned)need, scratch, res);
+  if (threadIdx.x == 0) {
+    st->b2 = (int)res[0];
+    st->n_above2 = (int)res[1];
+    st->need2 = need - (int)res[1];
+    st->out2_cnt = 0;
+    st->cand2_cnt = 0;
+  }
+}
+
 // wave-aggregated append into a block-local (LDS) counter; returns this lane's slot (valid if flag)
 FEDMI_DEV int tk_append_lds(int* counter, bool flag) {
   const unsigned long long m = __ballot(flag);
@@ -352,16 +376,20 @@ FEDMI_DEV int tk_append_lds(int* counter, bool flag) {
 // global atomics per flush): per-wave global atomics on the two list counters serialise at one L2
 // address each (2.4 ms at 11 M entries, measured).
 constexpr int kTkStage = 4096;   // >= 2 iterations' worth (8 x 256 per iteration)
+template <bool H2>
 __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r, long n, TopKState* __restrict__ st,
                                                           int* __restrict__ idx, float* __restrict__ val,
                                                           int* __restrict__ cidx, unsigned* __restrict__ ckey) {
   __shared__ int s_si[kTkStage], s_ci[kTkStage];   // 4 x 16 KB of LDS
   __shared__ float s_sv[kTkStage];
   __shared__ unsigned s_ck[kTkStage];
+  __shared__ unsigned h2[H2 ? kTkBins1 : 1];
   __shared__ int n_s, n_c, b_s, b_c;
   const unsigned b1 = (unsigned)st->b1;
   const long stride = (long)gridDim.x * 256;
   if (threadIdx.x == 0) { n_s = 0; n_c = 0; }
+  if (H2)
+    for (int i = threadIdx.x; i < kTkBins1; i += 256) h2[i] = 0u;
   __syncthreads();
   // uniform trip count per workgroup: every lane takes part in every ballot and barrier; 8 elements per
   // thread per iteration, loaded before any is used
@@ -381,7 +409,11 @@ __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r,
       const int ps = tk_append_lds(&n_s, sel);
       const int pc = tk_append_lds(&n_c, cand);
       if (sel) { s_si[ps] = (int)i; s_sv[ps] = dv[u]; r[i] = 0.f; }
-      if (cand) { s_ci[pc] = (int)i; s_ck[pc] = key; }
+      if (cand) {
+        s_ci[pc] = (int)i;
+        s_ck[pc] = key;
+        if (H2) atomicAdd(&h2[(key >> 9) & (kTkBins1 - 1)], 1u);
+      }
     }
     __syncthreads();
     const bool last = i0 + stride * 8 >= n;
@@ -398,8 +430,75 @@ __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r,
       __syncthreads();
     }
   }
+  if (H2) {
+    __syncthreads();
+    for (int j = threadIdx.x; j < kTkBins1; j += 256) {
+      const int i = (j + (int)blockIdx.x * 64) & (kTkBins1 - 1);
+      if (h2[i]) atomicAdd(&st->hist2[i], h2[i]);
+    }
+  }
 }
 
+// level 2 (large n): candidates with key bits 19..9 above b2 are winners (positions n_above + [0, n_above2)),
+// those in b2 go to the level-3 list; workgroup-staged appends like tk_compact1
+__global__ __launch_bounds__(256) void tk_compact2_kernel(float* __restrict__ r, TopKState* __restrict__ st,
+                                                          const int* __restrict__ cidx, const unsigned* __restrict__ ckey,
+                                                          int* __restrict__ idx, float* __restrict__ val,
+                                                          int* __restrict__ cidx2, unsigned* __restrict__ ckey2) {
+  __shared__ int s_si[kTkStage], s_ci[kTkStage];
+  __shared__ float s_sv[kTkStage];
+  __shared__ unsigned s_ck[kTkStage];
+  __shared__ int n_s, n_c, b_s, b_c;
+  const int c = st->cand_cnt, nab = st->n_above;
+  const unsigned b2 = (unsigned)st->b2;
+  const long stride = (long)gridDim.x * 256;
+  if (threadIdx.x == 0) { n_s = 0; n_c = 0; }
+  __syncthreads();
+  for (long j0 = (long)blockIdx.x * 2048; j0 < c; j0 += stride * 8) {
+    int ci[8];
+    unsigned kk[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long j = j0 + u * 256 + threadIdx.x;
+      ci[u] = j < c ? cidx[j] : 0;
+      kk[u] = j < c ? ckey[j] : 0u;
+    }
+    float dv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long j = j0 + u * 256 + threadIdx.x;
+      dv[u] = (j < c && ((kk[u] >> 9) & (kTkBins1 - 1)) > b2) ? r[ci[u]] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long j = j0 + u * 256 + threadIdx.x;
+      const unsigned bin = (kk[u] >> 9) & (kTkBins1 - 1);
+      const bool sel = j < c && bin > b2, cand = j < c && bin == b2;
+      const int ps = tk_append_lds(&n_s, sel);
+      const int pc = tk_append_lds(&n_c, cand);
+      if (sel) { s_si[ps] = ci[u]; s_sv[ps] = dv[u]; r[ci[u]] = 0.f; }
+      if (cand) { s_ci[pc] = ci[u]; s_ck[pc] = kk[u]; }
+    }
+    __syncthreads();
+    const bool last = j0 + stride * 8 >= c;
+    if (last || n_s > kTkStage - 8 * 256 || n_c > kTkStage - 8 * 256) {
+      if (threadIdx.x == 0) {
+        b_s = n_s ? atomicAdd(&st->out2_cnt, n_s) : 0;
+        b_c = n_c ? atomicAdd(&st->cand2_cnt, n_c) : 0;
+      }
+      __syncthreads();
+      for (int q = threadIdx.x; q < n_s; q += 256) { idx[nab + b_s + q] = s_si[q]; val[nab + b_s + q] = s_sv[q]; }
+      for (int q = threadIdx.x; q < n_c; q += 256) { cidx2[b_c + q] = s_ci[q]; ckey2[b_c + q] = s_ck[q]; }
+      __syncthreads();
+      if (threadIdx.x == 0) { n_s = 0; n_c = 0; }
+      __syncthreads();
+    }
+  }
+}
+
+// LEVELS == 2: the level-1 candidates (key bits 19..0 undecided, 2 radix passes); LEVELS == 1: the level-3
+// list of the 3-level path (bits 19..9 decided; one pass over bits 9..0, bit 9 common to all)
+template <int LEVELS>
 __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r, TopKState* __restrict__ st,
                                                           const int* __restrict__ cidx, const unsigned* __restrict__ ckey,
                                                           int* __restrict__ idx, float* __restrict__ val) {
@@ -407,22 +506,28 @@ __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r,
   __shared__ unsigned scratch[32], res[2];
   __shared__ int wcount;
   const int t = threadIdx.x;
-  const int c = st->cand_cnt, nab = st->n_above;
-  const unsigned m = (unsigned)st->need;
+  const int c = LEVELS == 2 ? st->cand_cnt : st->cand2_cnt;
+  const int nab = LEVELS == 2 ? st->n_above : st->n_above + st->n_above2;
+  const unsigned m = (unsigned)(LEVELS == 2 ? st->need : st->need2);
+  constexpr unsigned LOWMASK = LEVELS == 2 ? 0xfffffu : 0x3ffu;
   // pass A: key bits 19..10
-  for (int i = t; i < 1024; i += 1024) h[i] = 0u;
-  __syncthreads();
-  for (int j0 = t; j0 < c; j0 += 8 * 1024) {       // 8 loads in flight per thread
-    unsigned kk[8];
+  unsigned bA = 0u, mA = m;
+  if (LEVELS == 2) {
+    for (int i = t; i < 1024; i += 1024) h[i] = 0u;
+    __syncthreads();
+    for (int j0 = t; j0 < c; j0 += 8 * 1024) {       // 8 loads in flight per thread
+      unsigned kk[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) kk[u] = j0 + u * 1024 < c ? ckey[j0 + u * 1024] : 0u;
+      for (int u = 0; u < 8; ++u) kk[u] = j0 + u * 1024 < c ? ckey[j0 + u * 1024] : 0u;
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (j0 + u * 1024 < c) atomicAdd(&h[(kk[u] >> 10) & 1023u], 1u);
+      for (int u = 0; u < 8; ++u)
+        if (j0 + u * 1024 < c) atomicAdd(&h[(kk[u] >> 10) & 1023u], 1u);
+    }
+    __syncthreads();
+    tk_find_top(h, 1024, m, scratch, res);
+    bA = res[0];
+    mA = m - res[1];
   }
-  __syncthreads();
-  tk_find_top(h, 1024, m, scratch, res);
-  const unsigned bA = res[0], mA = m - res[1];
   // pass B: key bits 9..0 of the keys in bin bA
   h[t] = 0u;
   __syncthreads();
@@ -432,12 +537,12 @@ __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r,
     for (int u = 0; u < 8; ++u) kk[u] = j0 + u * 1024 < c ? ckey[j0 + u * 1024] : 0u;
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (j0 + u * 1024 < c && ((kk[u] >> 10) & 1023u) == bA) atomicAdd(&h[kk[u] & 1023u], 1u);
+      if (j0 + u * 1024 < c && (LEVELS == 1 || ((kk[u] >> 10) & 1023u) == bA)) atomicAdd(&h[kk[u] & 1023u], 1u);
   }
   __syncthreads();
   tk_find_top(h, 1024, mA, scratch, res);
   const unsigned bB = res[0];
-  const unsigned T = (bA << 10) | bB;        // low 20 bits of the k-th largest key
+  const unsigned T = LEVELS == 2 ? ((bA << 10) | bB) : bB;   // undecided low bits of the k-th largest key
   const unsigned ties_take = mA - res[1], ties = h[bB];
   __syncthreads();
   // exact ties beyond what is needed: keep the smallest indices (radix on the index, smallest first:
@@ -453,7 +558,7 @@ __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r,
       __syncthreads();
       for (int j = t; j < c; j += 1024) {
         const unsigned ix = (unsigned)cidx[j];
-        if ((ckey[j] & 0xfffffu) == T && (ix & pmask) == pre) atomicAdd(&h[nb - 1 - ((ix >> sh) & (nb - 1))], 1u);
+        if ((ckey[j] & LOWMASK) == T && (ix & pmask) == pre) atomicAdd(&h[nb - 1 - ((ix >> sh) & (nb - 1))], 1u);
       }
       __syncthreads();
       tk_find_top(h, nb < 1024 ? 1024 : nb, kk, scratch, res);
@@ -480,7 +585,7 @@ __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r,
     for (int u = 0; u < 4; ++u) dv[u] = j0 + u * 1024 + t < c ? r[ci[u]] : 0.f;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const unsigned low = kk[u] & 0xfffffu;
+      const unsigned low = kk[u] & LOWMASK;
       const bool sel = j0 + u * 1024 + t < c && (low > T || (low == T && (unsigned)ci[u] <= ilim));
       const unsigned long long msk = __ballot(sel);
       int base = 0;
@@ -536,7 +641,7 @@ size_t topk_state_bytes() { return sizeof(TopKState); }
 
 // Fused error-feedback exact top-k (see tk_* kernels).  residual: d is built IN it and the
 // selected entries are zeroed (= the new residual); state: topk_state_bytes(), zero on first
-// use (left zero by every call); cidx/ckey: candidate scratch of n entries each.
+// use (left zero by every call); cidx/ckey: candidate scratch of 2n entries each.
 void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* residual, long n, int k, void* state,
                     int* cidx, unsigned* ckey, int* idx, float* val) {
   TopKState* s = reinterpret_cast<TopKState*>(state);
@@ -550,8 +655,23 @@ void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* resid
     hipLaunchKernelGGL(tk_delta_hist_kernel<false>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s);
   hipLaunchKernelGGL(tk_pick1_kernel, dim3(1), dim3(1024), 0, st, s, k);
   const int cblocks = (int)std::min<long>(2048, std::max<long>(1, (n + 2 * 2048 - 1) / (2 * 2048)));
-  hipLaunchKernelGGL(tk_compact1_kernel, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx, ckey);
-  hipLaunchKernelGGL(tk_select2_kernel, dim3(1), dim3(1024), 0, st, residual, s, cidx, ckey, idx, val);
+  if (n < kTkThreeLevel) {
+    hipLaunchKernelGGL(tk_compact1_kernel<false>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx,
+                       ckey);
+    hipLaunchKernelGGL(tk_select2_kernel<2>, dim3(1), dim3(1024), 0, st, residual, s, cidx, ckey, idx, val);
+    return;
+  }
+  // large n: the boundary bin holds ~1-3 % of the entries -- too many for one workgroup; a second histogram
+  // level over the candidates (built by compact1) and a multi-workgroup compaction of them leave a
+  // level-3 list of a few hundred for the single-workgroup exact select
+  int* cidx2 = cidx + n;                     // second half of the 2n-entry candidate scratch
+  unsigned* ckey2 = ckey + n;
+  hipLaunchKernelGGL(tk_compact1_kernel<true>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx, ckey);
+  hipLaunchKernelGGL(tk_pick2_kernel, dim3(1), dim3(1024), 0, st, s);
+  const int c2blocks = (int)std::min<long>(1024, std::max<long>(1, (n / 50 + 2047) / 2048));
+  hipLaunchKernelGGL(tk_compact2_kernel, dim3(c2blocks), dim3(256), 0, st, residual, s, cidx, ckey, idx, val, cidx2,
+                     ckey2);
+  hipLaunchKernelGGL(tk_select2_kernel<1>, dim3(1), dim3(1024), 0, st, residual, s, cidx2, ckey2, idx, val);
 }
 
 // idx/val: [R][m] gathered payloads, applied in rank order 0..R-1.

@@ -88,9 +88,10 @@ class TopKCompressor(_EFCompressor):
         self.val = torch.empty(self.k, dtype=torch.float32, device=self.dev)
         if self._nat is not None:
             self.state = torch.zeros(self._nat.topk_state_bytes(), dtype=torch.uint8, device=self.dev)
-            # boundary-bin candidates (index, key): sized for the worst case (every entry in one bin)
-            self.cidx = torch.empty(self.n, dtype=torch.int32, device=self.dev)
-            self.ckey = torch.empty(self.n, dtype=torch.int32, device=self.dev)
+            # boundary-bin candidates (index, key) + the level-3 list: sized for the worst case (every
+            # entry in one bin)
+            self.cidx = torch.empty(2 * self.n, dtype=torch.int32, device=self.dev)
+            self.ckey = torch.empty(2 * self.n, dtype=torch.int32, device=self.dev)
 
     def compress(self, x: torch.Tensor) -> None:
         if self._nat is not None:

@@ -62,7 +62,7 @@ def test_topk_exact(nat, gpu_device, n, k):
 
 @pytest.mark.parametrize("n,k,ties", [(62006, 620, False), (5000, 1, False), (5000, 5000, False),
                                        (1 << 20, 10000, False), (11173962, 111740, False), (70001, 700, True),
-                                       (4099, 17, True)])
+                                       (4099, 17, True), (1 << 21, 5000, "sparse")])
 def test_topk_ef_exact(nat, gpu_device, n, k, ties):
     """Fused error-feedback top-k: d = x - g + r built in r, exactly the k largest |d| selected (ties:
     smallest indices), r keeps the rest; called twice on the same state (it must leave it reusable)."""
@@ -71,7 +71,10 @@ def test_topk_ef_exact(nat, gpu_device, n, k, ties):
         x = torch.randn(n, device=gpu_device)
         g = torch.randn(n, device=gpu_device) * 0.5
         r = torch.randn(n, device=gpu_device) * 0.1
-        if ties:                              # many exact ties at the threshold magnitude
+        if ties == "sparse":                  # 100 nonzeros, k = 5000: the rest are ties at 0 (huge candidate lists)
+            x.zero_(); g.zero_(); r.zero_()
+            x[torch.randperm(n, device=gpu_device)[:100]] = torch.randn(100, device=gpu_device)
+        elif ties:                            # many exact ties at the threshold magnitude
             x[::3] = 0.75
             g[::3] = 0.0
             r[::3] = 0.0
@@ -84,8 +87,8 @@ def test_topk_ef_exact(nat, gpu_device, n, k, ties):
         d = x - g + r
         if rep == 0:
             state = torch.zeros(nat.topk_state_bytes(), dtype=torch.uint8, device=gpu_device)
-            cidx = torch.empty(n, dtype=torch.int32, device=gpu_device)
-            ckey = torch.empty(n, dtype=torch.int32, device=gpu_device)
+            cidx = torch.empty(2 * n, dtype=torch.int32, device=gpu_device)
+            ckey = torch.empty(2 * n, dtype=torch.int32, device=gpu_device)
         idx = torch.full((k,), -1, dtype=torch.int32, device=gpu_device)
         val = torch.zeros(k, device=gpu_device)
         nat.topk_ef(S(), x.data_ptr(), g.data_ptr(), r.data_ptr(), n, k, state.data_ptr(), cidx.data_ptr(),

@@ -1,0 +1,60 @@
+"""BASELINE config 3 parity: FedAvg of ResNet-18 over 2 non-IID clients (2 label shards each), the
+native HIP engine vs plain PyTorch fp32, same split / init / recipe (lr 0.02, where the recipe is
+stable; profiles/r3_noniid/README.md has the lr 0.1 sweep).  Both clients run in this process
+(tools/fedavg_sim.py semantics: one local epoch each, uniform mean of the float state, floor mean of
+num_batches_tracked, global model evaluated on the full test set)."""
+import pytest
+import torch
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow, pytest.mark.timeout(420)]
+
+
+def _run(engine: str, rounds: int, monkeypatch):
+    if engine == "fp32":
+        monkeypatch.setenv("FEDMI_TORCH_PATH", "1")
+    else:
+        monkeypatch.delenv("FEDMI_TORCH_PATH", raising=False)
+    from fedmi.engine import build_trainer
+    from fedmi.engine.base import TrainerConfig
+    from fedmi.engine.data import contiguous_schedule, label_shard_indices, make_dataset
+
+    dev = torch.device("cuda", 0)
+    data = make_dataset("synthetic-cifar10", device=dev, n_train=50000, n_test=10000, seed=0)
+    cfg = TrainerConfig(seed=17, lr=0.02)
+    shards = label_shard_indices(data.train.y.cpu().numpy(), 2, 2, seed=0)
+    clients, init = [], None
+    for r in range(2):
+        tr = build_trainer("resnet18", data, dev, cfg, init_state=init)
+        if init is None:
+            init = {k: v.detach().cpu().clone() for k, v in tr.state_dict().items()}
+        tr.set_train_data(data.train.subset(shards[r]))
+        tr.set_schedule(*contiguous_schedule(len(shards[r]), 128))
+        clients.append(tr)
+    accs, train_accs = [], []
+    for _ in range(rounds):
+        for tr in clients:
+            tr.train_epoch()
+        train_accs.append([tr.train_stats().acc for tr in clients])
+        with torch.no_grad():
+            mean = torch.stack([tr.float_state() for tr in clients]).mean(0)
+            ints = [torch.div(a + b, 2, rounding_mode="floor")
+                    for a, b in zip(clients[0].int_state(), clients[1].int_state())]
+            for tr in clients:
+                tr.float_state().copy_(mean)
+                for b, v in zip(tr.int_state(), ints):
+                    b.copy_(v)
+                tr.after_aggregate()
+        clients[0].evaluate()
+        accs.append(clients[0].eval_stats().acc)
+    return accs, train_accs
+
+
+def test_native_tracks_fp32_on_noniid_label_shards(monkeypatch):
+    rounds = 5
+    nat, nat_tr = _run("native", rounds, monkeypatch)
+    ref, ref_tr = _run("fp32", rounds, monkeypatch)
+    # both learn on the skewed split (chance is 10 %), and the native engine stays close to fp32
+    assert ref[-1] > 30.0 and nat[-1] > 30.0, (nat, ref)
+    assert abs(nat[-1] - ref[-1]) < 10.0, (nat, ref)
+    for a, b in zip(nat_tr[-1], ref_tr[-1]):
+        assert abs(a - b) < 5.0, (nat_tr, ref_tr)

@@ -60,8 +60,8 @@ def main() -> int:
 
         t_topk_old = _time(topk, iters)
         tstate = torch.zeros(nat.topk_state_bytes(), dtype=torch.uint8, device=dev)
-        cidx = torch.empty(n, dtype=torch.int32, device=dev)
-        ckey = torch.empty(n, dtype=torch.int32, device=dev)
+        cidx = torch.empty(2 * n, dtype=torch.int32, device=dev)
+        ckey = torch.empty(2 * n, dtype=torch.int32, device=dev)
 
         def topk_ef():
             nat.topk_ef(S(), local.data_ptr(), glob.data_ptr(), resid.data_ptr(), n, k, tstate.data_ptr(),
