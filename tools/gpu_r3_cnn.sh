@@ -10,7 +10,7 @@ STAGES="${STAGES:-tests bench prof compress}"
 for st in $STAGES; do
   case $st in
     tests)
-      timeout -k 10 900 python -u -m pytest tests/test_cnn_kernels_gpu.py tests/test_cnn_native_gpu.py -q -x \
+      timeout -k 10 900 python -u -m pytest ${TESTS:-tests/test_cnn_kernels_gpu.py tests/test_cnn_native_gpu.py tests/test_flat_ops_gpu.py} -q -x \
         --timeout 240 --timeout-method thread > $O/tests.log 2>&1; rc=$?
       echo "tests rc=$rc" >> $S; tail -3 $O/tests.log >> $S; stop $rc ;;
     bench)
