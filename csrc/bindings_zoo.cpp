@@ -27,6 +27,11 @@ void launch_reduce_rows(hipStream_t, const void*, int, long long, const void*, i
                         long long, int, float*, long long, float*, float*);
 void launch_reduce(hipStream_t, const ZTensor&, const ZTensor&, const ZTensor&, const ZTensor&, const void*, int,
                    const void*, int, const float*, float*, float*, int);
+void launch_bn_rows_fwd(hipStream_t, const void*, int, long long, const float*, int, long long, float*, long long,
+                        const float*, const float*, float*, float*, float, float, float*, float*, float*, float*);
+void launch_bn_rows_bwd(hipStream_t, const void*, int, long long, const void*, int, long long, const void*, int,
+                        long long, float, const float*, const float*, const float*, int, long long, float*, long long,
+                        float*, float*, float*, float*, float*);
 void launch_bn_fwd_coeffs(hipStream_t, const float*, const float*, const float*, int, long long, const float*,
                           const float*, float*, float*, float, float, int, float*, float*, float*, float*);
 void launch_bn_bwd_coeffs(hipStream_t, const float*, const float*, const float*, const float*, const float*, int,
@@ -101,6 +106,23 @@ void fedmi_bind_zoo(py::module_& m) {
     auto f = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
     fedmi::launch_bn_fwd_coeffs(S(st), f(s1), f(s2), f(shift), C, M, f(w), f(b), f(rmean), f(rvar), eps, mom, train,
                                 f(save_mean), f(save_invstd), f(scale), f(bias));
+  });
+  m.def("z_bn_rows_fwd", [](uintptr_t st, uintptr_t x, int x_dt, long long ldx, uintptr_t shift, int C, long long M,
+                            uintptr_t part, long long part_floats, uintptr_t w, uintptr_t b, uintptr_t rmean,
+                            uintptr_t rvar, float eps, float mom, uintptr_t save_mean, uintptr_t save_invstd,
+                            uintptr_t scale, uintptr_t bias) {
+    auto f = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
+    fedmi::launch_bn_rows_fwd(S(st), reinterpret_cast<const void*>(x), x_dt, ldx, f(shift), C, M, f(part), part_floats,
+                              f(w), f(b), f(rmean), f(rvar), eps, mom, f(save_mean), f(save_invstd), f(scale), f(bias));
+  });
+  m.def("z_bn_rows_bwd", [](uintptr_t st, uintptr_t g, int g_dt, long long ldg, uintptr_t x, int x_dt, long long ldx,
+                            uintptr_t fm, int f_dt, long long ldf, float thr, uintptr_t mean, uintptr_t invstd,
+                            uintptr_t w, int C, long long M, uintptr_t part, long long part_floats, uintptr_t k,
+                            uintptr_t bb, uintptr_t cc, uintptr_t dw, uintptr_t db) {
+    auto f = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
+    fedmi::launch_bn_rows_bwd(S(st), reinterpret_cast<const void*>(g), g_dt, ldg, reinterpret_cast<const void*>(x), x_dt,
+                              ldx, reinterpret_cast<const void*>(fm), f_dt, ldf, thr, f(mean), f(invstd), f(w), C, M,
+                              f(part), part_floats, f(k), f(bb), f(cc), f(dw), f(db));
   });
   m.def("z_bn_bwd_coeffs", [](uintptr_t st, uintptr_t sg, uintptr_t sgx, uintptr_t mean, uintptr_t invstd, uintptr_t w,
                               int C, long long M, uintptr_t k, uintptr_t bb, uintptr_t cc, uintptr_t dw, uintptr_t db) {

@@ -61,11 +61,13 @@ enum EwOp : int {
   EW_SUB = 13,       // o = a - s0 * b
   EW_DIV = 14,       // o = a / b
   EW_ADDS = 15,      // o = a + s0
+  EW_FMA_RELU = 16,  // o = max(a * b + c, 0)      (BatchNorm apply + ReLU in one pass)
+  EW_BNB_THR = 17,   // o = (f > s0 ? a : 0) * b + c * d + e   (threshold_backward fused into BN backward)
 };
 
 struct EwArgs {
   ZTensor o;
-  ZTensor in[5];
+  ZTensor in[6];
   float s0, s1;
   int op;
   uint32_t seed;
@@ -91,7 +93,7 @@ FEDMI_DEV long long zoffset(const ZTensor& shape, const ZTensor& t, long long i6
   return off + (long long)i * t.stride[0];
 }
 
-FEDMI_DEV float ew_apply(const EwArgs& a, float x0, float x1, float x2, float x3, float x4) {
+FEDMI_DEV float ew_apply(const EwArgs& a, float x0, float x1, float x2, float x3, float x4, float x5 = 0.f) {
   switch (a.op) {
     case EW_COPY: return x0;
     case EW_ADD: return x0 + a.s0 * x1;
@@ -107,6 +109,8 @@ FEDMI_DEV float ew_apply(const EwArgs& a, float x0, float x1, float x2, float x3
     case EW_FILL: return a.s0;
     case EW_FMA: return x0 * x1 + x2;
     case EW_BNB: return x0 * x1 + x2 * x3 + x4;
+    case EW_FMA_RELU: return fmaxf(x0 * x1 + x2, 0.f);
+    case EW_BNB_THR: return (x5 > a.s0 ? x0 : 0.f) * x1 + x2 * x3 + x4;
     default: return 0.f;
   }
 }
@@ -168,9 +172,9 @@ template <int VW>
 __global__ __launch_bounds__(256) void ew_vec_kernel(EwArgs a, long long nv) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
-    float x[5][VW];
+    float x[6][VW];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < 6; ++k) {
       if (a.in[k].p && ((a.vmask >> k) & 1)) {
         vload<VW>(a.in[k].p, a.in[k].dtype, zoffset(a.o, a.in[k], i), x[k]);
       } else {
@@ -181,7 +185,7 @@ __global__ __launch_bounds__(256) void ew_vec_kernel(EwArgs a, long long nv) {
     }
     float v[VW];
 #pragma unroll
-    for (int u = 0; u < VW; ++u) v[u] = ew_apply(a, x[0][u], x[1][u], x[2][u], x[3][u], x[4][u]);
+    for (int u = 0; u < VW; ++u) v[u] = ew_apply(a, x[0][u], x[1][u], x[2][u], x[3][u], x[4][u], x[5][u]);
     vstore<VW>(a.o.p, a.o.dtype, zoffset(a.o, a.o, i), v);
   }
 }
@@ -190,18 +194,19 @@ __global__ __launch_bounds__(256) void ew_kernel(EwArgs a, long long n) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   const uint32_t ctr = a.ctr ? (uint32_t)a.ctr[0] : 0u;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f, x4 = 0.f;
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f, x4 = 0.f, x5 = 0.f;
     if (a.in[0].p) x0 = zload(a.in[0], zoffset(a.o, a.in[0], i));
     if (a.in[1].p) x1 = zload(a.in[1], zoffset(a.o, a.in[1], i));
     if (a.in[2].p) x2 = zload(a.in[2], zoffset(a.o, a.in[2], i));
     if (a.in[3].p) x3 = zload(a.in[3], zoffset(a.o, a.in[3], i));
     if (a.in[4].p) x4 = zload(a.in[4], zoffset(a.o, a.in[4], i));
+    if (a.in[5].p) x5 = zload(a.in[5], zoffset(a.o, a.in[5], i));
     float v;
     if (a.op == EW_BERN) {
       const uint32_t h = hash3(a.seed, ctr, (uint32_t)i ^ (uint32_t)(i >> 32));
       v = ((float)(h >> 8) * (1.f / 16777216.f)) < a.s0 ? 1.f : 0.f;
     } else {
-      v = ew_apply(a, x0, x1, x2, x3, x4);
+      v = ew_apply(a, x0, x1, x2, x3, x4, x5);
     }
     zstore(a.o, zoffset(a.o, a.o, i), v);
   }
@@ -296,7 +301,8 @@ FEDMI_DEV float ordered_slab_sum(const float* part, int slabs, long long pitch, 
 template <int VW>
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_dt, long long lda, const void* b,
                                                           int b_dt, long long ldb, const float* shift, int C,
-                                                          long long M, int op, float* part) {
+                                                          long long M, int op, float* part, const void* f = nullptr,
+                                                          int f_dt = 0, long long ldf = 0, float thr = 0.f) {
   __shared__ float red[2][256 * VW];
   const int VL = C / VW;
   const int vt = min(VL, 256);
@@ -316,6 +322,12 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_d
     for (long long r = r0 + rl; r < r1; r += RL) {
       float x[VW];
       vload<VW>(a, a_dt, r * lda + v * VW, x);
+      if (f) {                                   // a := threshold_backward(a, f) = f > thr ? a : 0
+        float m[VW];
+        vload<VW>(f, f_dt, r * ldf + v * VW, m);
+#pragma unroll
+        for (int u = 0; u < VW; ++u) x[u] = m[u] > thr ? x[u] : 0.f;
+      }
       if (op == RD_SUM) {
 #pragma unroll
         for (int u = 0; u < VW; ++u) s1[u] += x[u];
@@ -359,6 +371,52 @@ __global__ __launch_bounds__(256) void reduce_rows_finalize(const float* part, i
   if ((threadIdx.x >> 6) || c >= C) return;
   acc[c] += t1;
   if (two) acc2[c] += t2;
+}
+
+// BatchNorm forward from the reduce_rows slab partials of (x - shift): slab sums in order, then
+// the bn_fwd_coeffs math (one launch instead of finalize + coefficients)
+__global__ __launch_bounds__(256) void bn_rows_fwd_finalize(const float* part, int slabs, int C, long long M,
+                                                            const float* shift, const float* w, const float* b,
+                                                            float* rmean, float* rvar, float eps, float mom,
+                                                            float* save_mean, float* save_invstd, float* scale,
+                                                            float* bias) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float s1 = ordered_slab_sum(part, slabs, 2LL * C, c, c < C);
+  __syncthreads();
+  const float s2 = ordered_slab_sum(part + C, slabs, 2LL * C, c, c < C);
+  if ((threadIdx.x >> 6) || c >= C) return;
+  const float ms = s1 / (float)M;
+  const float var = fmaxf(s2 / (float)M - ms * ms, 0.f);
+  const float mean = ms + (shift ? shift[c] : 0.f);
+  const float inv = rsqrtf(var + eps);
+  if (save_mean) save_mean[c] = mean;
+  if (save_invstd) save_invstd[c] = inv;
+  if (rmean) {
+    rmean[c] = (1.f - mom) * rmean[c] + mom * mean;
+    rvar[c] = (1.f - mom) * rvar[c] + mom * var * ((float)M / (float)(M > 1 ? M - 1 : 1));
+  }
+  const float sc = (w ? w[c] : 1.f) * inv;
+  scale[c] = sc;
+  bias[c] = (b ? b[c] : 0.f) - mean * sc;
+}
+
+// BatchNorm backward from the slab partials of (sum g, sum g * (x - mean)): bn_bwd_coeffs math
+__global__ __launch_bounds__(256) void bn_rows_bwd_finalize(const float* part, int slabs, int C, long long M,
+                                                            const float* mean, const float* invstd, const float* w,
+                                                            float* k, float* bb, float* cc, float* dw, float* db) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float sg = ordered_slab_sum(part, slabs, 2LL * C, c, c < C);
+  __syncthreads();
+  const float sgx = ordered_slab_sum(part + C, slabs, 2LL * C, c, c < C);
+  if ((threadIdx.x >> 6) || c >= C) return;
+  const float inv = invstd[c];
+  const float kk = (w ? w[c] : 1.f) * inv;
+  const float b = -kk * inv * inv * sgx / (float)M;
+  k[c] = kk;
+  bb[c] = b;
+  cc[c] = -kk * sg / (float)M - b * mean[c];
+  if (dw) dw[c] = sgx * inv;
+  if (db) db[c] = sg;
 }
 
 int rows_vw(int C) { return C % 8 == 0 ? 8 : 4; }
@@ -892,7 +950,7 @@ namespace fedmi {
 
 void launch_ew(hipStream_t st, const ZTensor& o, const ZTensor* ins, int nin, int op, float s0, float s1,
                uint32_t seed, const int* ctr, int vmask, int vw) {
-  if (nin > 5) throw std::invalid_argument("ew: at most 5 inputs");
+  if (nin > 6) throw std::invalid_argument("ew: at most 6 inputs");
   EwArgs a{};
   a.o = o;
   for (int i = 0; i < nin; ++i) a.in[i] = ins[i];
@@ -954,12 +1012,55 @@ void launch_reduce_rows(hipStream_t st, const void* a, int a_dt, long long lda, 
   const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
   const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
   if (vw == 8)
-    hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part);
+    hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
+                       nullptr, 0, 0LL, 0.f);
   else
-    hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part);
+    hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
+                       nullptr, 0, 0LL, 0.f);
   hipLaunchKernelGGL(reduce_rows_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C,
                      op != RD_SUM ? 1 : 0, acc, acc2);
   check_hip(hipGetLastError(), "reduce_rows");
+}
+
+// BN forward statistics + coefficients of a channels-last [M, C] activation: reduce_rows + one finalize
+void launch_bn_rows_fwd(hipStream_t st, const void* x, int x_dt, long long ldx, const float* shift, int C, long long M,
+                        float* part, long long part_floats, const float* w, const float* b, float* rmean, float* rvar,
+                        float eps, float mom, float* save_mean, float* save_invstd, float* scale, float* bias) {
+  if (C % 4 || C <= 0 || M <= 0) throw std::invalid_argument("bn_rows_fwd: C % 4 == 0 and M > 0 required");
+  const int slabs = rows_slabs(M, C);
+  if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("bn_rows_fwd: workspace too small");
+  const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
+  const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
+  if (vw == 8)
+    hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, x, x_dt, ldx, nullptr, 0, 0LL, shift, C, M,
+                       (int)RD_SUMSQ_SHIFT, part, nullptr, 0, 0LL, 0.f);
+  else
+    hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, x, x_dt, ldx, nullptr, 0, 0LL, shift, C, M,
+                       (int)RD_SUMSQ_SHIFT, part, nullptr, 0, 0LL, 0.f);
+  hipLaunchKernelGGL(bn_rows_fwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C, M, shift,
+                     w, b, rmean, rvar, eps, mom, save_mean, save_invstd, scale, bias);
+  check_hip(hipGetLastError(), "bn_rows_fwd");
+}
+
+// BN backward sums + coefficients; f (optional): the ReLU output whose threshold_backward is fused in
+void launch_bn_rows_bwd(hipStream_t st, const void* g, int g_dt, long long ldg, const void* x, int x_dt, long long ldx,
+                        const void* f, int f_dt, long long ldf, float thr, const float* mean, const float* invstd,
+                        const float* w, int C, long long M, float* part, long long part_floats, float* k, float* bb,
+                        float* cc, float* dw, float* db) {
+  if (C % 4 || C <= 0 || M <= 0) throw std::invalid_argument("bn_rows_bwd: C % 4 == 0 and M > 0 required");
+  const int slabs = rows_slabs(M, C);
+  if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("bn_rows_bwd: workspace too small");
+  const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
+  const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
+  if (vw == 8)
+    hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, g, g_dt, ldg, x, x_dt, ldx, mean, C, M,
+                       (int)RD_DOT_SHIFT, part, f, f_dt, ldf, thr);
+  else
+    hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, g, g_dt, ldg, x, x_dt, ldx, mean, C, M,
+                       (int)RD_DOT_SHIFT, part, f, f_dt, ldf, thr);
+  hipLaunchKernelGGL(bn_rows_bwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C, M, mean,
+                     invstd, w, k, bb, cc, dw, db);
+  check_hip(hipGetLastError(), "bn_rows_bwd");
 }
 
 void launch_bn_fwd_coeffs(hipStream_t st, const float* s1, const float* s2, const float* shift, int C, long long M,

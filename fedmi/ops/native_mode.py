@@ -46,7 +46,7 @@ _DT = {torch.float32: 0, torch.bfloat16: 1, torch.int64: 2}
 
 # elementwise op codes (zoo_ops.hip EwOp)
 EW_COPY, EW_ADD, EW_MUL, EW_MULS, EW_RELU, EW_THR_BWD, EW_SIGMOID, EW_SIG_BWD, EW_FILL, EW_FMA = range(10)
-EW_BNB, EW_BERN, EW_SUB, EW_DIV, EW_ADDS = 11, 12, 13, 14, 15
+EW_BNB, EW_BERN, EW_SUB, EW_DIV, EW_ADDS, EW_FMA_RELU, EW_BNB_THR = 11, 12, 13, 14, 15, 16, 17
 # an impl returns ATEN when the op is legitimately ATen's (host copies, scalar reads): not a fallback
 ATEN = object()
 RD_SUM, RD_SUMSQ_SHIFT, RD_DOT_SHIFT = 0, 1, 2
@@ -326,17 +326,44 @@ def _div_t(func, self, other):
 
 @impl(aten.relu.default)
 def _relu(func, self):
+    pend = _mode_pending_bn(self)
+    if pend is not None:            # relu(BN(x)) in ONE pass; the BN output itself stays deferred (dead)
+        out = torch.empty_like(self)
+        ew(out, [pend.x, pend.scale, pend.shift], EW_FMA_RELU)
+        NativeMode.current._defer(self, lambda p=pend: ew(p.out, [p.x, p.scale, p.shift], EW_FMA))
+        NativeMode.current.fused["bn+relu"] += 1
+        return out
     return ew(torch.empty_like(self), [self], EW_RELU)
 
 
 @impl(aten.relu_.default)
 def _relu_(func, self):
+    pend = _mode_pending_bn(self)
+    if pend is not None:            # the BN output is overwritten by its ReLU: one pass, nothing deferred
+        NativeMode.current.fused["bn+relu_"] += 1
+        return ew(self, [pend.x, pend.scale, pend.shift], EW_FMA_RELU)
     return ew(self, [self], EW_RELU)
+
+
+class _PendingThr:
+    """threshold_backward(grad, relu_out) not yet computed: its consumer (BN backward) masks on the fly."""
+    __slots__ = ("out", "grad", "relu_out", "thr")
+
+    def __init__(self, out, grad, relu_out, thr):
+        self.out, self.grad, self.relu_out, self.thr = out, grad, relu_out, thr
+
+    def materialize(self):
+        ew(self.out, [self.grad, self.relu_out], EW_THR_BWD, self.thr)
 
 
 @impl(aten.threshold_backward.default)
 def _thr_bwd(func, grad_output, self, threshold):
     out = _alloc_like_meta(func, (grad_output, self, threshold), {}, grad_output.device)
+    mode = NativeMode.current
+    if (mode is not None and mode.fuse and _cl_rows(grad_output) and _cl_rows(self) and _cl_rows(out)
+            and _same_geom(grad_output, self) and _same_geom(out, self)):
+        mode._pend_thr = _PendingThr(out, grad_output, self, float(threshold))
+        return out
     return ew(out, [grad_output, self], EW_THR_BWD, float(threshold))
 
 
@@ -456,6 +483,48 @@ def _sum_all(func, self, dtype=None):
 
 
 # ---- BatchNorm -------------------------------------------------------------------
+def _cl_rows(t: torch.Tensor) -> bool:
+    """t is a [M, C] row matrix in memory (channels-last 4-D or contiguous 2-D), 16-B channel vectors."""
+    if t.dim() == 4:
+        if not t.is_contiguous(memory_format=torch.channels_last):
+            return False
+    elif t.dim() != 2 or not t.is_contiguous():
+        return False
+    C = t.shape[1]
+    if C % 4 or t.dtype not in (torch.float32, torch.bfloat16) or t.numel() == 0:
+        return False
+    align = 16 if (t.dtype == torch.float32 or C % 8 == 0) else 8
+    return t.data_ptr() % align == 0
+
+
+def _same_geom(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return a.shape == b.shape and a.stride() == b.stride()
+
+
+def _same(a, b) -> bool:
+    return isinstance(a, torch.Tensor) and a.data_ptr() == b.data_ptr() and _same_geom(a, b) and a.dtype == b.dtype
+
+
+class _PendingBN:
+    """A BatchNorm output whose apply pass (x * scale + shift) has not run yet: if the next op is its
+    ReLU, both become one pass (EW_FMA_RELU); any other op materialises it first."""
+    __slots__ = ("out", "x", "scale", "shift")
+
+    def __init__(self, out, x, scale, shift):
+        self.out, self.x, self.scale, self.shift = out, x, scale, shift
+
+    def materialize(self):
+        ew(self.out, [self.x, self.scale, self.shift], EW_FMA)
+
+
+def _mode_pending_bn(t):
+    mode = NativeMode.current
+    if mode is None or mode._pend_bn is None or not _same(t, mode._pend_bn.out):
+        return None
+    pend, mode._pend_bn = mode._pend_bn, None
+    return pend
+
+
 @impl(aten.native_batch_norm.default)
 def _bn(func, input, weight, bias, running_mean, running_var, training, momentum, eps):
     x = input
@@ -465,7 +534,19 @@ def _bn(func, input, weight, bias, running_mean, running_var, training, momentum
     f32 = dict(dtype=torch.float32, device=dev)
     scale, shift_out = torch.empty(C, **f32), torch.empty(C, **f32)
     nat = _nat()
-    if training:
+    mode = NativeMode.current
+    rows = _cl_rows(x)
+    if training and rows:
+        # channels-last rows: moments (slab partials) + ONE finalize that also derives the coefficients and
+        # the running stats (2 launches; the generic path below takes 4)
+        save_mean, save_invstd = torch.empty(C, **f32), torch.empty(C, **f32)
+        p = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
+        part = torch.empty(int(nat.z_reduce_rows_ws_floats(M, C)), **f32)
+        nat.z_bn_rows_fwd(_st(dev), x.data_ptr(), _DT[x.dtype], C, p(running_mean), C, M, part.data_ptr(), part.numel(),
+                          p(weight), p(bias), p(running_mean), p(running_var), float(eps),
+                          float(momentum if momentum is not None else 0.1), save_mean.data_ptr(), save_invstd.data_ptr(),
+                          scale.data_ptr(), shift_out.data_ptr())
+    elif training:
         acc = torch.empty(2 * C, **f32)
         fill_(acc, 0.0)
         dims = [0] + list(range(2, x.dim()))
@@ -484,7 +565,10 @@ def _bn(func, input, weight, bias, running_mean, running_var, training, momentum
         save_invstd = torch.empty(0, **f32)
     bshape = [1, C] + [1] * (x.dim() - 2)
     out = torch.empty_like(x)
-    ew(out, [x, scale.view(bshape), shift_out.view(bshape)], EW_FMA)
+    if mode is not None and mode.fuse and rows and _same_geom(out, x):
+        mode._pend_bn = _PendingBN(out, x, scale.view(bshape), shift_out.view(bshape))
+    else:
+        ew(out, [x, scale.view(bshape), shift_out.view(bshape)], EW_FMA)
     return out, save_mean, save_invstd
 
 
@@ -511,21 +595,43 @@ def _bn_bwd(func, grad_out, input, weight, running_mean, running_var, save_mean,
     dev = x.device
     M = x.numel() // C
     f32 = dict(dtype=torch.float32, device=dev)
-    acc = torch.empty(2 * C, **f32)
-    fill_(acc, 0.0)
-    dims = [0] + list(range(2, x.dim()))
-    reduce_sum(g, dims, acc[:C], RD_DOT_SHIFT, b=x, shift=save_mean, acc2=acc[C:])
     k, bb, cc = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(C, **f32)
     gw = torch.empty(C, **f32) if output_mask[1] else None
     gb = torch.empty(C, **f32) if output_mask[2] else None
     p = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
-    _nat().z_bn_bwd_coeffs(_st(dev), acc.data_ptr(), acc[C:].data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(),
-                           p(weight), C, M, k.data_ptr(), bb.data_ptr(), cc.data_ptr(), p(gw), p(gb))
+    mode = NativeMode.current
+    thr = None
+    if mode is not None and mode._pend_thr is not None and _same(g, mode._pend_thr.out):
+        thr, mode._pend_thr = mode._pend_thr, None   # this BN's ReLU backward, fused into its sums and apply
+        mode._defer(thr.out, thr.materialize)
+        mode.fused["relu_bwd+bn_bwd"] += 1
+        g = thr.grad
+    if _cl_rows(g) and _cl_rows(x) and _same_geom(g, x):
+        nat = _nat()
+        part = torch.empty(int(nat.z_reduce_rows_ws_floats(M, C)), **f32)
+        nat.z_bn_rows_bwd(_st(dev), g.data_ptr(), _DT[g.dtype], C, x.data_ptr(), _DT[x.dtype], C,
+                          thr.relu_out.data_ptr() if thr else 0, _DT[thr.relu_out.dtype] if thr else 0, C,
+                          thr.thr if thr else 0.0, save_mean.data_ptr(), save_invstd.data_ptr(), p(weight), C, M,
+                          part.data_ptr(), part.numel(), k.data_ptr(), bb.data_ptr(), cc.data_ptr(), p(gw), p(gb))
+    else:
+        if thr is not None:
+            thr.materialize()
+            g, thr = thr.out, None
+        acc = torch.empty(2 * C, **f32)
+        fill_(acc, 0.0)
+        dims = [0] + list(range(2, x.dim()))
+        reduce_sum(g, dims, acc[:C], RD_DOT_SHIFT, b=x, shift=save_mean, acc2=acc[C:])
+        _nat().z_bn_bwd_coeffs(_st(dev), acc.data_ptr(), acc[C:].data_ptr(), save_mean.data_ptr(),
+                               save_invstd.data_ptr(), p(weight), C, M, k.data_ptr(), bb.data_ptr(), cc.data_ptr(),
+                               p(gw), p(gb))
     gi = None
     if output_mask[0]:
         bshape = [1, C] + [1] * (x.dim() - 2)
         gi = torch.empty_like(x)
-        ew(gi, [g, k.view(bshape), x, bb.view(bshape), cc.view(bshape)], EW_BNB)
+        if thr is not None:
+            ew(gi, [g, k.view(bshape), x, bb.view(bshape), cc.view(bshape), thr.relu_out], EW_BNB_THR, thr.thr)
+        else:
+            ew(gi, [g, k.view(bshape), x, bb.view(bshape), cc.view(bshape)], EW_BNB)
     if gw is not None and weight is not None and gw.dtype != weight.dtype:
         gw = ew(torch.empty_like(weight), [gw], EW_COPY)
     return gi, gw, gb
@@ -923,19 +1029,62 @@ class NativeMode(TorchDispatchMode):
 
     current: "NativeMode" = None
 
-    def __init__(self, strict: bool = False, seed: int = 0):
+    def __init__(self, strict: bool = False, seed: int = 0, fuse: Optional[bool] = None):
         super().__init__()
         self.strict = strict
         self.seed = seed
         self.fallbacks = collections.Counter()
         self.native_ops = collections.Counter()
         self._ctr = {}
+        # BN -> ReLU (forward) and ReLU-backward -> BN-backward fusion (FEDMI_NATIVE_FUSE=0: off)
+        import os
 
-    def rng_ctr(self, dev) -> torch.Tensor:
-        dev = torch.device(dev)
-        if dev not in self._ctr:
-            self._ctr[dev] = torch.zeros(4, dtype=torch.int32, device=dev)
-        return self._ctr[dev]
+        self.fuse = (os.environ.get("FEDMI_NATIVE_FUSE", "1") != "0") if fuse is None else bool(fuse)
+        self._pend_bn: Optional[_PendingBN] = None
+        self._pend_thr: Optional[_PendingThr] = None
+        self._dead = {}                 # storage ptr -> materialiser of a tensor a fused op never wrote
+        self.fused = collections.Counter()
+
+    def _defer(self, t: torch.Tensor, materialize) -> None:
+        self._dead[t.untyped_storage().data_ptr()] = materialize
+
+    def _flush(self) -> None:
+        if self._pend_bn is not None:
+            pend, self._pend_bn = self._pend_bn, None
+            pend.materialize()
+        if self._pend_thr is not None:
+            pend, self._pend_thr = self._pend_thr, None
+            pend.materialize()
+
+    def _touch(self, args, kwargs) -> None:
+        """Before an op runs: materialise a pending result it does not fuse with, and any deferred tensor
+        it reads (a fused op left it unwritten)."""
+        if self._pend_bn is not None and not self._fuses_bn(args):
+            pend, self._pend_bn = self._pend_bn, None
+            pend.materialize()
+        if self._pend_thr is not None and not self._fuses_thr(args):
+            pend, self._pend_thr = self._pend_thr, None
+            pend.materialize()
+        if self._dead:
+            for t in _iter_tensors(args, kwargs):
+                fn = self._dead.pop(t.untyped_storage().data_ptr(), None) if t.is_cuda else None
+                if fn is not None:
+                    fn()
+
+    _func = None
+
+    def _fuses_bn(self, args) -> bool:
+        return (self._func in (aten.relu.default, aten.relu_.default) and len(args) > 0
+                and _same(args[0], self._pend_bn.out))
+
+    def _fuses_thr(self, args) -> bool:
+        if self._func is aten.native_batch_norm_backward.default:
+            g = args[0] if args else None
+        elif self._func is aten.miopen_batch_norm_backward.default:
+            g = args[1] if len(args) > 1 else None
+        else:
+            return False
+        return _same(g, self._pend_thr.out)
 
     def __enter__(self):
         self._prev = NativeMode.current
@@ -945,6 +1094,10 @@ class NativeMode(TorchDispatchMode):
         return super().__enter__()
 
     def __exit__(self, *exc):
+        try:
+            self._flush()
+        finally:
+            self._dead.clear()
         NativeMode.current = self._prev
         try:
             return super().__exit__(*exc)
@@ -954,7 +1107,12 @@ class NativeMode(TorchDispatchMode):
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
         if func in _PASSTHROUGH:
+            if func is aten._local_scalar_dense.default:     # reads device data: everything must be written
+                self._flush()
+                self._touch(args, kwargs)
             return func(*args, **kwargs)
+        self._func = func
+        self._touch(args, kwargs)
         fn = _IMPL.get(func)
         on_gpu = _dev(args, tuple(kwargs.values())) is not None
         if fn is not None and on_gpu:
@@ -969,6 +1127,16 @@ class NativeMode(TorchDispatchMode):
             if self.strict:
                 raise RuntimeError(f"native_mode: no native kernel for {func}")
         return func(*args, **kwargs)
+
+
+def _iter_tensors(args, kwargs):
+    for a in list(args) + list(kwargs.values()):
+        if isinstance(a, torch.Tensor):
+            yield a
+        elif isinstance(a, (list, tuple)):
+            for b in a:
+                if isinstance(b, torch.Tensor):
+                    yield b
 
 
 def ce_stats_(logits: torch.Tensor, labels: torch.Tensor, stats: torch.Tensor) -> None:

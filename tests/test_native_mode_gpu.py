@@ -329,3 +329,28 @@ def test_graph_replay_matches_eager(gpu_device):
     assert lg[-1] < lg[0] and le[-1] < le[0], out
     assert abs(lg[0] - le[0]) < 0.05 * le[0], out
     assert abs(lg[-1] - le[-1]) < 0.25 * le[-1] + 0.05, out
+
+
+@pytest.mark.parametrize("name", ["densenet_cifar", "ResNeXt29_2x64d", "DLA"])
+def test_bn_relu_fusion_is_exact(gpu_device, name):
+    """BN -> ReLU (one FMA+ReLU pass) and ReLU-backward -> BN-backward (masked sums and apply) fusion:
+    relu(bf16(BN(x))) == bf16(relu(BN(x))) and the mask is exact, so a training step with the fusion
+    gives BIT-IDENTICAL weights to the unfused step (eager, same init and batch)."""
+    from fedmi.engine import build_trainer
+
+    data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=128, n_test=64, seed=0)
+    cfg = TrainerConfig(batch_size=64, lr=0.02, seed=7, augment=False, use_graph=False)
+    init = build_model(name).state_dict()
+    res = {}
+    for fuse in (False, True):
+        tr = build_trainer(name, data, gpu_device, cfg, init_state=init)
+        tr.use_graph = False
+        tr.mode.fuse = fuse
+        tr.set_schedule([0, 64], [64, 64])
+        tr.train_epoch()
+        torch.cuda.synchronize()
+        res[fuse] = (tr.float_state().clone(), tr.train_stats(), dict(tr.mode.fused))
+    (w0, s0, f0), (w1, s1, f1) = res[False], res[True]
+    assert not f0 and f1.get("bn+relu", 0) + f1.get("bn+relu_", 0) > 0 and f1.get("relu_bwd+bn_bwd", 0) > 0, f1
+    assert torch.equal(w0, w1)
+    assert s0.correct == s1.correct and s0.count == s1.count

@@ -24,9 +24,11 @@ dev = torch.device("cuda", 0)
 data = make_dataset("synthetic-cifar10", device=dev, n_train=128 * 12, n_test=1000, seed=0)
 for name in MODELS:
     init = build_model(name).state_dict()
-    for mode in ("fp32", "native-eager", "native-graph"):
+    for mode in ("fp32", "native-eager", "native-graph-nofuse", "native-graph"):
         tr = TorchTrainer(name, data, dev, TrainerConfig(seed=1), init_state=init, hybrid=(mode != "fp32"))
-        tr.use_graph = mode.endswith("graph")
+        tr.use_graph = "graph" in mode
+        if tr.mode is not None:
+            tr.mode.fuse = not mode.endswith("nofuse")     # BN -> ReLU / ReLU-bwd -> BN-bwd fusion
         tr.model.train()
         for i in range(3):
             tr.train_step(128 * i, 128)
