@@ -26,7 +26,8 @@ long long reduce_rows_ws_floats(long long, int);
 void launch_reduce_rows(hipStream_t, const void*, int, long long, const void*, int, long long, const float*, int,
                         long long, int, float*, long long, float*, float*);
 void launch_reduce(hipStream_t, const ZTensor&, const ZTensor&, const ZTensor&, const ZTensor&, const void*, int,
-                   const void*, int, const float*, float*, float*, int);
+                   const void*, int, const float*, float*, float*, int, float*, long long);
+long long reduce_ws_floats(long long, long long);
 void launch_bn_rows_fwd(hipStream_t, const void*, int, long long, const float*, int, long long, float*, long long,
                         const float*, const float*, float*, float*, float, float, float*, float*, float*, float*);
 void launch_bn_rows_bwd(hipStream_t, const void*, int, long long, const void*, int, long long, const void*, int,
@@ -87,11 +88,13 @@ void fedmi_bind_zoo(py::module_& m) {
   m.def("z_ctr_bump", [](uintptr_t st, uintptr_t ctr) { fedmi::launch_ctr_bump(S(st), reinterpret_cast<int*>(ctr)); });
   m.def("z_reduce", [](uintptr_t st, py::object outer, py::object inner, py::object outer_b, py::object inner_b,
                        uintptr_t a, int a_dt, uintptr_t b, int b_dt, uintptr_t shift, uintptr_t acc, uintptr_t acc2,
-                       int op) {
+                       int op, uintptr_t part, long long part_floats) {
     fedmi::launch_reduce(S(st), zt(outer), zt(inner), zt(outer_b), zt(inner_b), reinterpret_cast<const void*>(a), a_dt,
                          reinterpret_cast<const void*>(b), b_dt, reinterpret_cast<const float*>(shift),
-                         reinterpret_cast<float*>(acc), reinterpret_cast<float*>(acc2), op);
+                         reinterpret_cast<float*>(acc), reinterpret_cast<float*>(acc2), op,
+                         reinterpret_cast<float*>(part), part_floats);
   });
+  m.def("z_reduce_ws_floats", &fedmi::reduce_ws_floats);
   m.def("z_reduce_rows_ws_floats", &fedmi::reduce_rows_ws_floats);
   m.def("z_reduce_rows", [](uintptr_t st, uintptr_t a, int a_dt, long long lda, uintptr_t b, int b_dt, long long ldb,
                             uintptr_t shift, int C, long long M, int op, uintptr_t part, long long part_floats,

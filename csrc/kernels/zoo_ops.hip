@@ -229,8 +229,9 @@ struct RdArgs {
   const void* b;
   int b_dtype;
   const float* shift;   // per-outer shift (moments of (a - shift)), or null
-  float* acc;           // fp32 [n_outer] accumulator (atomics), zeroed by the host
+  float* acc;           // fp32 [n_outer] accumulator, zeroed by the host
   float* acc2;          // second accumulator (RD_SUMSQ_SHIFT: sum of squares; RD_DOT_SHIFT: sum a*(b-shift))
+  float* part;          // [2][splits][n_outer] per-split partials (splits > 1), summed in split order afterwards
   int op;
 };
 
@@ -270,13 +271,30 @@ __global__ __launch_bounds__(256) void reduce_kernel(RdArgs r, long long n_outer
   red[1][li][lo] = s2;
   __syncthreads();
   if (li == 0 && o < n_outer) {
+    // no atomics: one writer per (split, outer), so the result does not depend on workgroup order
     const float t1 = red[0][0][lo] + red[0][1][lo] + red[0][2][lo] + red[0][3][lo];
-    atomicAdd(r.acc + o, t1);
-    if (r.op != RD_SUM) {
-      const float t2 = red[1][0][lo] + red[1][1][lo] + red[1][2][lo] + red[1][3][lo];
-      atomicAdd(r.acc2 + o, t2);
+    const float t2 = red[1][0][lo] + red[1][1][lo] + red[1][2][lo] + red[1][3][lo];
+    if (gridDim.y == 1) {
+      r.acc[o] += t1;
+      if (r.op != RD_SUM) r.acc2[o] += t2;
+    } else {
+      r.part[(long long)blockIdx.y * n_outer + o] = t1;
+      if (r.op != RD_SUM) r.part[((long long)gridDim.y + blockIdx.y) * n_outer + o] = t2;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void reduce_splits_kernel(const float* part, int splits, long long n_outer,
+                                                            float* acc, float* acc2) {
+  const long long o = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (o >= n_outer) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int y = 0; y < splits; ++y) {
+    s1 += part[(long long)y * n_outer + o];
+    if (acc2) s2 += part[((long long)splits + y) * n_outer + o];
+  }
+  acc[o] += s1;
+  if (acc2) acc2[o] += s2;
 }
 
 // sum over slabs of part[slab * pitch + i], 64 elements x 4 slab lanes per block, lanes combined in
@@ -608,6 +626,70 @@ __global__ __launch_bounds__(256) void gemm_kernel(ZTensor A, ZTensor B, ZTensor
     if (bias.p) v += beta * zload(bias, (bias.ndim == 2 ? row * bias.stride[0] : 0) + col * bias.stride[bias.ndim - 1]);
     zstore(Cm, row * Cm.stride[0] + col * Cm.stride[1], v);
   }
+}
+
+// ---- bf16 GEMM on MFMA: C[M,N] = alpha * A[M,K] B[K,N] + beta * bias --------------------
+// 64 x 64 output tile per 256-thread workgroup, each wave a 32 x 32 quadrant of 2 x 2
+// v_mfma_f32_16x16x32_bf16 tiles; K in steps of 32 staged through LDS with any operand strides
+// (the aten mm operands are often transposed views), both tiles stored k-contiguous so every
+// fragment is one 16-byte ds_read.  Used when both operands are bf16 (autocast linear layers and
+// their backward); fp32 operands keep the exact-fp32 gemm_kernel above.
+constexpr int kGmPitch = 40;   // bf16 per LDS row: 32 + 8 pad (80 B rows: 16-B aligned, bank-spread)
+
+__global__ __launch_bounds__(256) void gemm_mfma_kernel(ZTensor A, ZTensor B, ZTensor Cm, ZTensor bias, float alpha,
+                                                        float beta) {
+  __shared__ __attribute__((aligned(16))) bf16 as[64 * kGmPitch];
+  __shared__ __attribute__((aligned(16))) bf16 bs[64 * kGmPitch];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const long long M = Cm.size[0], N = Cm.size[1], K = A.size[1];
+  const long long m0 = (long long)blockIdx.y * 64, n0 = (long long)blockIdx.x * 64;
+  const bf16* Ap = reinterpret_cast<const bf16*>(A.p);
+  const bf16* Bp = reinterpret_cast<const bf16*>(B.p);
+  const int lr = t >> 2, lk = (t & 3) * 8;      // loader: tile row / column lr, 8 consecutive k
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = zero4();
+  for (long long k0 = 0; k0 < K; k0 += 32) {
+    bf16x8 va, vb;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const long long k = k0 + lk + e, m = m0 + lr, n = n0 + lr;
+      va[e] = (m < M && k < K) ? Ap[m * A.stride[0] + k * A.stride[1]] : (bf16)0.f;
+      vb[e] = (n < N && k < K) ? Bp[k * B.stride[0] + n * B.stride[1]] : (bf16)0.f;
+    }
+    *reinterpret_cast<bf16x8*>(as + lr * kGmPitch + lk) = va;
+    *reinterpret_cast<bf16x8*>(bs + lr * kGmPitch + lk) = vb;
+    __syncthreads();
+    const int fr = lane & 15, fk = (lane >> 4) * 8;
+    bf16x8 fa[2], fb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(as + (wm + i * 16 + fr) * kGmPitch + fk);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(bs + (wn + j * 16 + fr) * kGmPitch + fk);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
+    __syncthreads();
+  }
+  // 16x16x32 result layout: lane holds rows 4 * (lane / 16) + r of column lane % 16
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long long row = m0 + wm + i * 16 + (lane >> 4) * 4 + r, col = n0 + wn + j * 16 + (lane & 15);
+        if (row < M && col < N) {
+          float v = alpha * acc[i][j][r];
+          if (bias.p)
+            v += beta * zload(bias, (bias.ndim == 2 ? row * bias.stride[0] : 0) + col * bias.stride[bias.ndim - 1]);
+          zstore(Cm, row * Cm.stride[0] + col * Cm.stride[1], v);
+        }
+      }
 }
 
 // ---- log_softmax over dim 1 of a 2-D tensor; NLL loss (mean, ignore_index) -------------
@@ -981,9 +1063,24 @@ void launch_ctr_bump(hipStream_t st, int* ctr) {
   hipLaunchKernelGGL(ctr_bump_kernel, dim3(1), dim3(64), 0, st, ctr);
 }
 
+static long long reduce_splits(long long no, long long ni) {
+  const long long tiles = (no + 63) / 64;
+  long long splits = (1024 + tiles - 1) / tiles;             // ~1024 workgroups in flight
+  const long long max_split = (ni + 255) / 256;              // >= 64 inner elements per lane group
+  if (splits > max_split) splits = max_split;
+  if (splits > 256) splits = 256;                            // bounds the partials workspace
+  if (splits < 1) splits = 1;
+  return splits;
+}
+
+long long reduce_ws_floats(long long no, long long ni) {
+  const long long sp = reduce_splits(no, ni);
+  return sp > 1 ? 2 * sp * no : 0;
+}
+
 void launch_reduce(hipStream_t st, const ZTensor& outer, const ZTensor& inner, const ZTensor& outer_b,
                    const ZTensor& inner_b, const void* a, int a_dt, const void* b, int b_dt, const float* shift,
-                   float* acc, float* acc2, int op) {
+                   float* acc, float* acc2, int op, float* part, long long part_floats) {
   long long no = 1, ni = 1;
   for (int d = 0; d < outer.ndim; ++d) no *= outer.size[d];
   for (int d = 0; d < inner.ndim; ++d) ni *= inner.size[d];
@@ -991,14 +1088,18 @@ void launch_reduce(hipStream_t st, const ZTensor& outer, const ZTensor& inner, c
   RdArgs r{};
   r.outer = outer; r.inner = inner; r.outer_b = outer_b; r.inner_b = inner_b;
   r.a = a; r.a_dtype = a_dt; r.b = b; r.b_dtype = b_dt; r.shift = shift; r.acc = acc; r.acc2 = acc2; r.op = op;
+  r.part = part;
   const long long tiles = (no + 63) / 64;
-  long long splits = (1024 + tiles - 1) / tiles;             // ~1024 workgroups in flight
-  const long long max_split = (ni + 255) / 256;              // >= 64 inner elements per lane group
-  if (splits > max_split) splits = max_split;
-  if (splits < 1) splits = 1;
-  if (splits > 65535) splits = 65535;
+  const long long splits = reduce_splits(no, ni);
+  if (splits > 1 && (part == nullptr || part_floats < 2 * splits * no))
+    throw std::invalid_argument("launch_reduce: partials workspace too small");
   hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)tiles, (unsigned)splits), dim3(256), 0, st, r, no, ni);
   check_hip(hipGetLastError(), "reduce_kernel");
+  if (splits > 1) {
+    hipLaunchKernelGGL(reduce_splits_kernel, dim3((unsigned)((no + 255) / 256)), dim3(256), 0, st, part, (int)splits,
+                       no, acc, op != RD_SUM ? acc2 : nullptr);
+    check_hip(hipGetLastError(), "reduce_splits_kernel");
+  }
 }
 
 long long reduce_rows_ws_floats(long long M, int C) { return (long long)rows_slabs(M, C) * 2 * C; }
@@ -1104,6 +1205,12 @@ void launch_gemm(hipStream_t st, const ZTensor& A, const ZTensor& B, const ZTens
                  float beta) {
   const long long M = Cm.size[0], N = Cm.size[1];
   if (M <= 0 || N <= 0) return;
+  if (A.dtype == 1 && B.dtype == 1) {
+    dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64));
+    hipLaunchKernelGGL(gemm_mfma_kernel, grid, dim3(256), 0, st, A, B, Cm, bias, alpha, beta);
+    check_hip(hipGetLastError(), "gemm_mfma");
+    return;
+  }
   dim3 grid((unsigned)((N + 15) / 16), (unsigned)((M + 15) / 16));
   hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, st, A, B, Cm, bias, alpha, beta);
   check_hip(hipGetLastError(), "gemm");

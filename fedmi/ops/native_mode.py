@@ -30,6 +30,7 @@ max_pool2d_with_indices, sigmoid, mul, mean, slice_backward, bernoulli_, ...).
 from __future__ import annotations
 
 import collections
+import math
 from typing import Optional
 
 import torch
@@ -231,10 +232,14 @@ def reduce_sum(a: torch.Tensor, dims, acc: torch.Tensor, op: int = RD_SUM, b: Op
     inner = (0, 0, ishape, istr[0])
     outer_b = (0, 0, oshape, ostr[1]) if b is not None else None
     inner_b = (0, 0, ishape, istr[1]) if b is not None else None
-    _nat().z_reduce(_st(a.device), outer, inner, outer_b, inner_b, a.data_ptr(), _DT[a.dtype],
-                    b.data_ptr() if b is not None else 0, _DT[b.dtype] if b is not None else 0,
-                    shift.data_ptr() if shift is not None else 0, acc.data_ptr(),
-                    acc2.data_ptr() if acc2 is not None else 0, op)
+    nat = _nat()
+    # split partials summed in a fixed order afterwards (no float atomics: bitwise-reproducible steps)
+    nws = int(nat.z_reduce_ws_floats(math.prod(oshape), math.prod(ishape)))
+    part = torch.empty(max(nws, 1), dtype=torch.float32, device=a.device)
+    nat.z_reduce(_st(a.device), outer, inner, outer_b, inner_b, a.data_ptr(), _DT[a.dtype],
+                 b.data_ptr() if b is not None else 0, _DT[b.dtype] if b is not None else 0,
+                 shift.data_ptr() if shift is not None else 0, acc.data_ptr(),
+                 acc2.data_ptr() if acc2 is not None else 0, op, part.data_ptr(), nws)
 
 
 def _rows_ok(oshape, ostr, ishape, istr, ops) -> bool:
@@ -1085,6 +1090,12 @@ class NativeMode(TorchDispatchMode):
         else:
             return False
         return _same(g, self._pend_thr.out)
+
+    def rng_ctr(self, dev) -> torch.Tensor:
+        dev = torch.device(dev)
+        if dev not in self._ctr:
+            self._ctr[dev] = torch.zeros(4, dtype=torch.int32, device=dev)
+        return self._ctr[dev]
 
     def __enter__(self):
         self._prev = NativeMode.current

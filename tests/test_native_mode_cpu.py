@@ -101,3 +101,11 @@ def test_hybrid_is_gpu_only():
     data = make_dataset("synthetic-cifar10", device="cpu", n_train=64, n_test=32, seed=0)
     tr = build_trainer("SimpleDLA", data, "cpu")
     assert not tr.hybrid and tr.mode is None
+
+
+def test_native_mode_api_used_by_the_trainer():
+    """TorchTrainer allocates the dropout RNG counter before capture and reads the fusion counters."""
+    mode = nm.NativeMode(fuse=True)
+    ctr = mode.rng_ctr("cpu")
+    assert ctr.dtype == torch.int32 and ctr.numel() == 4 and mode.rng_ctr("cpu") is ctr
+    assert mode.fuse and not mode.fused and not mode.fallbacks

@@ -203,6 +203,29 @@ def test_linear_cross_entropy(gpu_device):
     assert _rel(lin.bias.grad, ref.bias.grad) < 1e-3
 
 
+@pytest.mark.parametrize("M,K,N", [(128, 1024, 10), (10, 128, 1024), (128, 10, 1024), (77, 300, 65), (1, 33, 1)])
+def test_bf16_gemm_mfma(gpu_device, M, K, N):
+    """bf16 mm / addmm (the MFMA kernel) on contiguous and transposed operands vs fp32 matmul of the same
+    bf16 values: the shapes of a classifier's forward, weight gradient and input gradient plus ragged ones."""
+    torch.manual_seed(M * 7 + K + N)
+    a = torch.randn(M, K, device=gpu_device).bfloat16()
+    b = torch.randn(K, N, device=gpu_device).bfloat16()
+    bias = torch.randn(N, device=gpu_device).bfloat16()
+    mode = _mode()
+    ref = a.float() @ b.float()
+    with mode:
+        y0 = torch.mm(a, b)
+        y1 = torch.mm(a.t().contiguous().t(), b.t().contiguous().t())
+        y2 = torch.addmm(bias, a, b, beta=0.5, alpha=2.0)
+    torch.cuda.synchronize()
+    assert not mode.fallbacks and y0.dtype == torch.bfloat16
+    scale = float(ref.abs().max()) + 1e-6
+    assert float((y0.float() - ref).abs().max()) / scale < 1e-2
+    assert torch.equal(y0, y1)
+    ref2 = 2.0 * ref + 0.5 * bias.float()
+    assert float((y2.float() - ref2).abs().max()) / (float(ref2.abs().max()) + 1e-6) < 1e-2
+
+
 def test_ce_stats(gpu_device):
     from fedmi.ops.native_mode import ce_stats_
 

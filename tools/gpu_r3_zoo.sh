@@ -9,11 +9,11 @@ STAGES="${STAGES:-tests bench}"
 for st in $STAGES; do
   case $st in
     tests)
-      timeout -k 10 1100 python -u -m pytest tests/test_native_mode_gpu.py -q -x --timeout 300 --timeout-method thread \
+      timeout -k 10 560 python -u -m pytest tests/test_native_mode_gpu.py -q -x --timeout 300 --timeout-method thread \
         > $O/tests.log 2>&1; rc=$?
       echo "tests rc=$rc" >> $S; tail -4 $O/tests.log >> $S; stop $rc ;;
     bench)
-      timeout -k 10 900 python tools/bench_hybrid.py ${ZOO:-densenet_cifar DenseNet121 RegNetY_400MF SENet18 DPN26 DLA ResNeXt29_2x64d EfficientNetB0 ShuffleNetG2} \
+      timeout -k 10 560 python tools/bench_hybrid.py ${ZOO:-densenet_cifar DenseNet121 RegNetY_400MF SENet18 DPN26 DLA ResNeXt29_2x64d EfficientNetB0 ShuffleNetG2} \
         > $O/bench_hybrid.jsonl 2> $O/bench_hybrid.err; rc=$?
       echo "bench rc=$rc" >> $S; cat $O/bench_hybrid.jsonl >> $S; stop $rc ;;
   esac
