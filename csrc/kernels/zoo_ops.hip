@@ -63,6 +63,8 @@ enum EwOp : int {
   EW_ADDS = 15,      // o = a + s0
   EW_FMA_RELU = 16,  // o = max(a * b + c, 0)      (BatchNorm apply + ReLU in one pass)
   EW_BNB_THR = 17,   // o = (f > s0 ? a : 0) * b + c * d + e   (threshold_backward fused into BN backward)
+  EW_FMA_ADD = 18,   // o = r(a * b + c) + d       (BatchNorm apply + residual add; r = bf16 rounding if s1)
+  EW_FMA_ADD_RELU = 19,  // o = max(r(a * b + c) + d, 0)  (BatchNorm apply + residual add + ReLU)
 };
 
 struct EwArgs {
@@ -111,6 +113,9 @@ FEDMI_DEV float ew_apply(const EwArgs& a, float x0, float x1, float x2, float x3
     case EW_BNB: return x0 * x1 + x2 * x3 + x4;
     case EW_FMA_RELU: return fmaxf(x0 * x1 + x2, 0.f);
     case EW_BNB_THR: return (x5 > a.s0 ? x0 : 0.f) * x1 + x2 * x3 + x4;
+    // s1 != 0: the BN output is rounded to bf16 before the add, exactly as the unfused pair stores it
+    case EW_FMA_ADD: return (a.s1 != 0.f ? (float)(bf16)(x0 * x1 + x2) : x0 * x1 + x2) + x3;
+    case EW_FMA_ADD_RELU: return fmaxf((a.s1 != 0.f ? (float)(bf16)(x0 * x1 + x2) : x0 * x1 + x2) + x3, 0.f);
     default: return 0.f;
   }
 }

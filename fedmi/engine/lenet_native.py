@@ -170,8 +170,15 @@ class LeNetNativeTrainer(LocalTrainer):
         return self.decode_stats(self.stats[i].cpu())
 
     def decode_stats(self, raw: torch.Tensor) -> EpochStats:
-        # lenet::Stats: {float loss_sum, int correct, int count, pad} in an int32[4] row
+        # lenet::Stats: {float loss_sum, int correct, int count, flag} in an int32[4] row.  The flag word is
+        # set by the cross-workgroup hand-off waits of the head path (K12 act2 wait: 1, K34 wait: 2) when
+        # they time out and the kernel went on with stale rows -- never train on that silently.
         raw = raw.contiguous()
+        flag = int(raw[3])
+        if flag:
+            what = {1: "conv -> FC-head act2 hand-off (K12)", 2: "K3 -> K4 gradient hand-off (K34)"}.get(flag, "?")
+            raise RuntimeError(f"LeNet kernel hand-off timed out: {what} (stats flag {flag}); the step ran on "
+                               "stale rows -- another process is starving this GPU, or a workgroup never ran")
         return EpochStats(float(raw[0:1].view(torch.float32).item()), int(raw[1]), int(raw[2]))
 
     def eval_stats_raw(self) -> torch.Tensor:

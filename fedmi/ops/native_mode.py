@@ -48,6 +48,7 @@ _DT = {torch.float32: 0, torch.bfloat16: 1, torch.int64: 2}
 # elementwise op codes (zoo_ops.hip EwOp)
 EW_COPY, EW_ADD, EW_MUL, EW_MULS, EW_RELU, EW_THR_BWD, EW_SIGMOID, EW_SIG_BWD, EW_FILL, EW_FMA = range(10)
 EW_BNB, EW_BERN, EW_SUB, EW_DIV, EW_ADDS, EW_FMA_RELU, EW_BNB_THR = 11, 12, 13, 14, 15, 16, 17
+EW_FMA_ADD, EW_FMA_ADD_RELU = 18, 19
 # an impl returns ATEN when the op is legitimately ATen's (host copies, scalar reads): not a fallback
 ATEN = object()
 RD_SUM, RD_SUMSQ_SHIFT, RD_DOT_SHIFT = 0, 1, 2
@@ -268,6 +269,16 @@ def impl(*ops):
 # ---- elementwise ---------------------------------------------------------------
 @impl(aten.add.Tensor, aten.sub.Tensor)
 def _add(func, self, other, alpha=1):
+    mode = NativeMode.current
+    if func is aten.add.Tensor and alpha == 1 and mode is not None and mode._pend_bn is not None:
+        pend = mode._pend_bn
+        res = _bn_add_partner(pend, (self, other))
+        if res is not None:         # BN(x) + shortcut joins the pending apply pass; the BN output stays deferred
+            out = torch.empty_like(pend.out)
+            mode._pend_bn = _PendingBN(out, pend.x, pend.scale, pend.shift, res)
+            mode._defer(pend.out, pend.materialize)
+            mode.fused["bn+add"] += 1
+            return out
     sign = -1.0 if func is aten.sub.Tensor else 1.0
     s = _scalar(other)
     if s is not None:
@@ -332,11 +343,11 @@ def _div_t(func, self, other):
 @impl(aten.relu.default)
 def _relu(func, self):
     pend = _mode_pending_bn(self)
-    if pend is not None:            # relu(BN(x)) in ONE pass; the BN output itself stays deferred (dead)
+    if pend is not None:            # relu(BN(x) [+ res]) in ONE pass; the pre-ReLU tensor stays deferred (dead)
         out = torch.empty_like(self)
-        ew(out, [pend.x, pend.scale, pend.shift], EW_FMA_RELU)
-        NativeMode.current._defer(self, lambda p=pend: ew(p.out, [p.x, p.scale, p.shift], EW_FMA))
-        NativeMode.current.fused["bn+relu"] += 1
+        pend.relu(out)
+        NativeMode.current._defer(self, pend.materialize)
+        NativeMode.current.fused["bn+relu" if pend.res is None else "bn+add+relu"] += 1
         return out
     return ew(torch.empty_like(self), [self], EW_RELU)
 
@@ -344,9 +355,9 @@ def _relu(func, self):
 @impl(aten.relu_.default)
 def _relu_(func, self):
     pend = _mode_pending_bn(self)
-    if pend is not None:            # the BN output is overwritten by its ReLU: one pass, nothing deferred
-        NativeMode.current.fused["bn+relu_"] += 1
-        return ew(self, [pend.x, pend.scale, pend.shift], EW_FMA_RELU)
+    if pend is not None:            # the pending output is overwritten by its ReLU: one pass, nothing deferred
+        NativeMode.current.fused["bn+relu_" if pend.res is None else "bn+add+relu_"] += 1
+        return pend.relu(self)
     return ew(self, [self], EW_RELU)
 
 
@@ -511,15 +522,41 @@ def _same(a, b) -> bool:
 
 
 class _PendingBN:
-    """A BatchNorm output whose apply pass (x * scale + shift) has not run yet: if the next op is its
-    ReLU, both become one pass (EW_FMA_RELU); any other op materialises it first."""
-    __slots__ = ("out", "x", "scale", "shift")
+    """A BatchNorm output whose apply pass (x * scale + shift [+ res]) has not run yet: if the next op is
+    a residual add of it (identity or projection shortcut), the add joins the pending pass; if the next
+    op is its ReLU, everything becomes one pass (EW_FMA_RELU / EW_FMA_ADD_RELU); any other op
+    materialises it first."""
+    __slots__ = ("out", "x", "scale", "shift", "res")
 
-    def __init__(self, out, x, scale, shift):
-        self.out, self.x, self.scale, self.shift = out, x, scale, shift
+    def __init__(self, out, x, scale, shift, res=None):
+        self.out, self.x, self.scale, self.shift, self.res = out, x, scale, shift, res
+
+    def inputs(self):
+        return [self.x, self.scale, self.shift] + ([] if self.res is None else [self.res])
+
+    def rounding(self) -> float:
+        # the unfused BN stores its output before the add reads it: round there too (bit-identical results)
+        return 1.0 if self.res is not None and self.out.dtype == torch.bfloat16 else 0.0
 
     def materialize(self):
-        ew(self.out, [self.x, self.scale, self.shift], EW_FMA)
+        ew(self.out, self.inputs(), EW_FMA if self.res is None else EW_FMA_ADD, 0.0, self.rounding())
+
+    def relu(self, out):
+        return ew(out, self.inputs(), EW_FMA_RELU if self.res is None else EW_FMA_ADD_RELU, 0.0, self.rounding())
+
+
+def _bn_add_partner(pend, args, kwargs=None):
+    """The other operand of ``add.Tensor(a, b)`` when one operand is the pending BN output and the pair can
+    join the pending pass (no alpha, same geometry and dtype, no residual taken yet); else None."""
+    if pend is None or pend.res is not None or len(args) < 2 or len(args) > 2 or (kwargs and kwargs.get("alpha", 1) != 1):
+        return None
+    a, b = args[0], args[1]
+    if not (isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor)):
+        return None
+    o = b if _same(a, pend.out) else a if _same(b, pend.out) else None
+    if o is None or o is pend.out or o.dtype != pend.out.dtype or not _same_geom(o, pend.out):
+        return None
+    return o
 
 
 def _mode_pending_bn(t):
@@ -1064,7 +1101,7 @@ class NativeMode(TorchDispatchMode):
     def _touch(self, args, kwargs) -> None:
         """Before an op runs: materialise a pending result it does not fuse with, and any deferred tensor
         it reads (a fused op left it unwritten)."""
-        if self._pend_bn is not None and not self._fuses_bn(args):
+        if self._pend_bn is not None and not self._fuses_bn(args, kwargs):
             pend, self._pend_bn = self._pend_bn, None
             pend.materialize()
         if self._pend_thr is not None and not self._fuses_thr(args):
@@ -1078,7 +1115,9 @@ class NativeMode(TorchDispatchMode):
 
     _func = None
 
-    def _fuses_bn(self, args) -> bool:
+    def _fuses_bn(self, args, kwargs=None) -> bool:
+        if self._func is aten.add.Tensor:
+            return _bn_add_partner(self._pend_bn, args, kwargs) is not None
         return (self._func in (aten.relu.default, aten.relu_.default) and len(args) > 0
                 and _same(args[0], self._pend_bn.out))
 

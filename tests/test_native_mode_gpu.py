@@ -356,9 +356,10 @@ def test_graph_replay_matches_eager(gpu_device):
 
 @pytest.mark.parametrize("name", ["densenet_cifar", "ResNeXt29_2x64d", "DLA"])
 def test_bn_relu_fusion_is_exact(gpu_device, name):
-    """BN -> ReLU (one FMA+ReLU pass) and ReLU-backward -> BN-backward (masked sums and apply) fusion:
-    relu(bf16(BN(x))) == bf16(relu(BN(x))) and the mask is exact, so a training step with the fusion
-    gives BIT-IDENTICAL weights to the unfused step (eager, same init and batch)."""
+    """BN -> [residual add ->] ReLU (one pass) and ReLU-backward -> BN-backward (masked sums and apply)
+    fusion: relu(bf16(BN(x))) == bf16(relu(BN(x))), the fused add rounds the BN output to bf16 where the
+    unfused pair stores it, and the mask is exact, so a training step with the fusion gives BIT-IDENTICAL
+    weights to the unfused step (eager, same init and batch)."""
     from fedmi.engine import build_trainer
 
     data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=128, n_test=64, seed=0)
@@ -375,5 +376,7 @@ def test_bn_relu_fusion_is_exact(gpu_device, name):
         res[fuse] = (tr.float_state().clone(), tr.train_stats(), dict(tr.mode.fused))
     (w0, s0, f0), (w1, s1, f1) = res[False], res[True]
     assert not f0 and f1.get("bn+relu", 0) + f1.get("bn+relu_", 0) > 0 and f1.get("relu_bwd+bn_bwd", 0) > 0, f1
+    if name == "ResNeXt29_2x64d":      # identity and projection shortcuts: BN + add + ReLU in one pass
+        assert f1.get("bn+add", 0) > 0 and f1.get("bn+add+relu", 0) > 0, f1
     assert torch.equal(w0, w1)
     assert s0.correct == s1.correct and s0.count == s1.count
