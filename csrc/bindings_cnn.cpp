@@ -21,7 +21,13 @@ struct ConvShape {
 };
 void launch_conv_fwd(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, double*, const float*, float*, long,
                      const bf16*);
-void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, long, const bf16*, int);
+struct BnSums {
+  double* rep; const bf16* z; const bf16* y; const float* mean; const float* inv; int reps;
+  const bf16* zb; const float* meanb; const float* invb;
+};
+void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, long, const bf16*, int,
+                       const bf16*, const BnSums*);
+int conv_dgrad_fusable(const ConvShape&, int);
 struct DPackItem {
   const float* w;
   bf16* wd;
@@ -68,7 +74,7 @@ void launch_prep_input(hipStream_t, const uint8_t*, int, const int*, int, int, u
 void launch_sched_next(hipStream_t, const int*, int*, int*);
 void launch_bn_apply(hipStream_t, const bf16*, const BNDesc&, const bf16*, const BNDesc*, const bf16*, bf16*, int, int,
                      float, float, int, int, int);
-void launch_bn_bwd(hipStream_t, const BNBwdDesc&, double*, int, int, double*, long, int, int, int);
+void launch_bn_bwd(hipStream_t, const BNBwdDesc&, double*, int, int, double*, long, int, int, int, int);
 void launch_bn_coeff(hipStream_t, const BNDesc&, int, int, float, float, int, float*);
 long bn_bwd_ws_floats(int, int);
 int bn_bwd_chain_reps(int);
@@ -127,13 +133,23 @@ void fedmi_bind_cnn(py::module_& m) {
     check("conv_fwd");
   }, py::arg("st"), py::arg("shape"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("shift"),
      py::arg("ws") = 0, py::arg("ws_floats") = 0, py::arg("res") = 0);
+  // add: dx = dgrad + add;  bsum (dict rep/reps/z/y/mean/inv): the producer BN's backward sums in the epilogue
   m.def("conv_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t ws,
-                         long ws_floats, uintptr_t wd, int acc) {
+                         long ws_floats, uintptr_t wd, int acc, uintptr_t add, py::object bsum) {
+    BnSums bs{};
+    const bool has_bs = !bsum.is_none();
+    if (has_bs) {
+      const py::dict d = bsum.cast<py::dict>();
+      bs = BnSums{P<double>(dget(d, "rep")), P<const bf16>(dget(d, "z")), P<const bf16>(dget(d, "y")),
+                  P<const float>(dget(d, "mean")), P<const float>(dget(d, "inv")), d["reps"].cast<int>(),
+                  P<const bf16>(dget(d, "zb")), P<const float>(dget(d, "meanb")), P<const float>(dget(d, "invb"))};
+    }
     launch_conv_dgrad(S(st), shape_from(shp), P<const bf16>(dy), P<const bf16>(w), P<bf16>(dx), P<float>(ws),
-                      ws ? ws_floats : 0, P<const bf16>(wd), acc);
+                      ws ? ws_floats : 0, P<const bf16>(wd), acc, P<const bf16>(add), has_bs ? &bs : nullptr);
     check("conv_dgrad");
   }, py::arg("st"), py::arg("shape"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("ws") = 0,
-     py::arg("ws_floats") = 0, py::arg("wd") = 0, py::arg("acc") = 0);
+     py::arg("ws_floats") = 0, py::arg("wd") = 0, py::arg("acc") = 0, py::arg("add") = 0, py::arg("bsum") = py::none());
+  m.def("conv_dgrad_fusable", [](const py::tuple& shp, int has_wd) { return conv_dgrad_fusable(shape_from(shp), has_wd); });
   m.def("dgrad_pack_multi", [](uintptr_t st, const py::list& items) {
     std::vector<DPackItem> v;
     for (const auto& it : items) {
@@ -231,7 +247,7 @@ void fedmi_bind_cnn(py::module_& m) {
   });
   m.def("bn_bwd_ws_floats", [](int M, int C) { return bn_bwd_ws_floats(M, C); });
   m.def("bn_bwd", [](uintptr_t st, const py::dict& d, uintptr_t red, int M, int C, uintptr_t ws, long ws_floats,
-                     int ldd, int ldy, int chained) {
+                     int ldd, int ldy, int chained, int presummed) {
     BNBwdDesc b{P<const bf16>(dget(d, "dya")),     P<const bf16>(dget(d, "dyb")),     P<const bf16>(dget(d, "y")),
                 P<const bf16>(dget(d, "za")),      P<const float>(dget(d, "meanA")),  P<const float>(dget(d, "invA")),
                 P<const float>(dget(d, "gammaA")), P<float>(dget(d, "dgammaA")),      P<float>(dget(d, "dbetaA")),
@@ -241,10 +257,11 @@ void fedmi_bind_cnn(py::module_& m) {
                 P<float>(dget(d, "shiftA")),       P<float>(dget(d, "shiftB")),       P<const bf16>(dget(d, "dadd")),
                 P<const float>(dget(d, "msc"))};
     if (!b.dya || !b.za || !b.meanA || !b.invA || !b.gammaA || !b.dza) throw std::invalid_argument("bn_bwd: missing A");
-    launch_bn_bwd(S(st), b, P<double>(red), M, C, P<double>(ws), ws ? ws_floats : 0, ldd, ldy, chained);
+    launch_bn_bwd(S(st), b, P<double>(red), M, C, P<double>(ws), ws ? ws_floats : 0, ldd, ldy, chained, presummed);
     check("bn_bwd");
   }, py::arg("st"), py::arg("desc"), py::arg("red"), py::arg("M"), py::arg("C"), py::arg("ws") = 0,
-     py::arg("ws_floats") = 0, py::arg("ldd") = 0, py::arg("ldy") = 0, py::arg("chained") = 0);
+     py::arg("ws_floats") = 0, py::arg("ldd") = 0, py::arg("ldy") = 0, py::arg("chained") = 0,
+     py::arg("presummed") = 0);
   m.def("bn_bwd_chain_reps", [](int C) { return bn_bwd_chain_reps(C); });
   m.def("head", [](uintptr_t st, uintptr_t y, uintptr_t labels, int base, uintptr_t dbase, int N, int HW, int C, int J,
                    uintptr_t W, uintptr_t b, uintptr_t pooled, uintptr_t dlog, uintptr_t dy, uintptr_t stats,

@@ -1015,8 +1015,10 @@ long bn_bwd_ws_floats(int M, int C) {
 // the reduce workgroups' same-address atomics; the apply prologue reads them all).
 int bn_bwd_chain_reps(int C) { return std::max(4, std::min(16, 2048 / std::max(C, 1))); }
 
+// presummed (chained mode only): the channel sums are already in ``ws`` -- the DGRAD that produced dya
+// took them in its epilogue (conv_igemm.hip BnSums) -- so only the apply pass runs.
 void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, double* red, int M, int C, double* ws, long ws_floats, int ldd,
-                   int ldy, int chained) {
+                   int ldy, int chained, int presummed) {
   const int VR = C / 8;
   if (C % 8 || VR > 256) throw std::invalid_argument("bn_bwd: need C % 8 == 0 and C <= 2048");
   if (ldd <= 0) ldd = C;
@@ -1032,7 +1034,10 @@ void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, double* red, int M, int C
     // ws: this BN's own replica buffer, ZERO on entry (the head kernel clears the arena every step)
     const int reps = bn_bwd_chain_reps(C);
     if (!ws || ws_floats < (long)reps * 3 * C) throw std::invalid_argument("bn_bwd: chained replicas too small");
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(tb), 0, st, in, red, M, C, rows_per_block, ws, reps);
+    if (presummed && (d.dyb || d.msc))
+      throw std::invalid_argument("bn_bwd: presummed sums cover one incoming grad and a y mask");
+    if (!presummed)
+      hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(tb), 0, st, in, red, M, C, rows_per_block, ws, reps);
     if (use_chunked(C)) {
       const dim3 ag = apply_grid(M, C);
       hipLaunchKernelGGL(bn_bwd_apply_chunk_kernel, ag, dim3(256), 0, st, in, out, red, M, C, ws, reps,
@@ -1044,6 +1049,7 @@ void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, double* red, int M, int C
     }
     return;
   }
+  if (presummed) throw std::invalid_argument("bn_bwd: presummed needs chained replicas");
   const bool two = ws && ws_floats >= (long)BN_REP * 3 * C;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(tb), 0, st, in, red, M, C, rows_per_block,
                      two ? ws : nullptr, BN_REP);

@@ -74,6 +74,61 @@ FEDMI_DEV long map_row(const RowMap& r, int m) {
   return ((long)n * r.OH + p * r.st + r.ph) * r.OW + q * r.st + r.pw;
 }
 
+}  // namespace
+
+namespace fedmi {
+// BatchNorm-backward channel sums of the BN that PRODUCED a DGRAD's output, taken in the DGRAD
+// epilogue (tap kernel or split-K combine) instead of a separate pass over (dy, z, y):
+//   g = bf16(dX)[row][c] * (y[row][c] > 0, or 1 without a ReLU)
+//   rep[blk % reps][0][c] += sum g,   rep[blk % reps][1][c] += sum g * (z[row][c] - mean[c]) * inv[c]
+//   (rep[..][2][c] += sum g * (zb - meanb) * invb: a projection-shortcut BN sharing g)
+// -- the chained replica layout bn_bwd's apply kernel reads (cnn_ops.hip, launch_bn_bwd presummed).
+struct BnSums {
+  double* rep;          // [reps][3][C] fp64, zero at the step start (null: off)
+  const bf16* z;        // the BN's input (its conv's output), compact [rows][C]
+  const bf16* y;        // the BN's ReLU output (mask) or null
+  const float* mean;    // saved batch mean / inverse std of the BN
+  const float* inv;
+  int reps;
+  const bf16* zb;       // second BN branch (projection shortcut) or null
+  const float* meanb;
+  const float* invb;
+};
+}  // namespace fedmi
+
+namespace {
+using fedmi::BnSums;
+
+// one 8-channel group of a DGRAD output row into the BN-backward sums (bm/bi: [2][8] mean / inv of
+// the two branches; q: [3][8])
+FEDMI_DEV void bnsum_acc(const BnSums& bs, long idx, const bf16x8& t, const float (*bm)[8], const float (*bi)[8],
+                         float (*q)[8]) {
+  const bf16x8 z = *reinterpret_cast<const bf16x8*>(bs.z + idx);
+  bf16x8 y{}, zb{};
+  if (bs.y) y = *reinterpret_cast<const bf16x8*>(bs.y + idx);
+  if (bs.zb) zb = *reinterpret_cast<const bf16x8*>(bs.zb + idx);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float g = (float)t[j];
+    if (bs.y && !((float)y[j] > 0.f)) g = 0.f;
+    q[0][j] += g;
+    q[1][j] += g * ((float)z[j] - bm[0][j]) * bi[0][j];
+    if (bs.zb) q[2][j] += g * ((float)zb[j] - bm[1][j]) * bi[1][j];
+  }
+}
+
+// mean / inv of an 8-channel group (both branches), zero past the last channel
+FEDMI_DEV void bnsum_coeffs(const BnSums& bs, int c0, bool ok, float (*bm)[8], float (*bi)[8], float (*q)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    q[0][j] = q[1][j] = q[2][j] = 0.f;
+    bm[0][j] = ok ? bs.mean[c0 + j] : 0.f;
+    bi[0][j] = ok ? bs.inv[c0 + j] : 0.f;
+    bm[1][j] = ok && bs.zb ? bs.meanb[c0 + j] : 0.f;
+    bi[1][j] = ok && bs.zb ? bs.invb[c0 + j] : 0.f;
+  }
+}
+
 enum { FWD = 0, DGRAD = 1, WGRAD = 2 };
 constexpr int BK = 64;
 constexpr int KC_LD = BK + 8;   // KC image row stride (elements): 144 B = 9 x 16 B
@@ -459,7 +514,7 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
                                                 bf16* __restrict__ out, float* __restrict__ part,
                                                 double* __restrict__ stats, const float* __restrict__ shift,
                                                 TapGeom g, RowMap rmap, int ksteps_per_split,
-                                                const bf16* __restrict__ res) {
+                                                const bf16* __restrict__ res, BnSums bs) {
   constexpr int BM = 128;
   constexpr int NA = BM / 32;            // A wave-instructions per stage per wave (8 rows each)
   constexpr int NB = BN / 32;
@@ -623,19 +678,40 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
     if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, (double)tsum);
   }
   constexpr int CPR = BN / 8;
+  // DGRAD: BN-backward sums of the producer BN (each thread keeps one 8-channel group: 256 % CPR == 0)
+  const bool bsum = bs.rep != nullptr;
+  float bq[3][8], bm[2][8], bi[2][8];
+  if (bsum) bnsum_coeffs(bs, n0 + (tid % CPR) * 8, n0 + (tid % CPR) * 8 < g.O, bm, bi, bq);
   for (int c = tid; c < BM * CPR; c += 256) {
     const int row = c / CPR, cc = c % CPR;
     const int m = m0 + row, col = n0 + cc * 8;
     if (m < g.M && col < g.O) {
       const long orow = map_row(rmap, m);
-      if (res != nullptr) {   // fused residual add (pre-activation blocks): y = conv + res, stats of y
-        bf16x8 t = *reinterpret_cast<const bf16x8*>(ct + row * CT_LD + cc * 8);
+      bf16x8 t = *reinterpret_cast<const bf16x8*>(ct + row * CT_LD + cc * 8);
+      if (res != nullptr) {   // fused residual add (pre-activation fwd) / second incoming grad (DGRAD)
         const bf16x8 r = *reinterpret_cast<const bf16x8*>(res + orow * g.O + col);
 #pragma unroll
         for (int j = 0; j < 8; ++j) t[j] = (bf16)((float)t[j] + (float)r[j]);
-        *reinterpret_cast<bf16x8*>(ct + row * CT_LD + cc * 8) = t;
+        if (stats != nullptr) *reinterpret_cast<bf16x8*>(ct + row * CT_LD + cc * 8) = t;
       }
-      *reinterpret_cast<uint4*>(out + orow * g.O + col) = *reinterpret_cast<const uint4*>(ct + row * CT_LD + cc * 8);
+      *reinterpret_cast<bf16x8*>(out + orow * g.O + col) = t;
+      if (bsum) bnsum_acc(bs, orow * g.O + col, t, bm, bi, bq);
+    }
+  }
+  if (bsum) {
+    // [3][256][8] partials behind the ct tile, then one (quantity, channel) per thread -> fp64 replica atomics
+    float* rs = red;
+    const int nq = bs.zb ? 3 : 2;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rs[(q * 256 + tid) * 8 + j] = bq[q][j];
+    __syncthreads();
+    for (int e = tid; e < nq * BN; e += 256) {
+      const int q = e / BN, cl = e % BN, grp = cl >> 3, j = cl & 7;
+      float s = 0.f;
+      for (int th = grp; th < 256; th += CPR) s += rs[(q * 256 + th) * 8 + j];
+      if (n0 + cl < g.O) unsafeAtomicAdd(bs.rep + ((long)(blockIdx.x % bs.reps) * 3 + q) * g.O + n0 + cl, (double)s);
     }
   }
   if (stats != nullptr && res != nullptr) {   // statistics of y = conv + res, from the summed tile
@@ -1299,18 +1375,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_cols(const float* __res
 __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restrict__ ws, int splits, int M, int NC,
                                                           RowMap rmap, bf16* __restrict__ out,
                                                           double* __restrict__ stats, const float* __restrict__ shift,
-                                                          int rows_per_block, const bf16* __restrict__ res) {
-  __shared__ float red[2][256][8];
+                                                          int rows_per_block, const bf16* __restrict__ res,
+                                                          BnSums bs) {
+  __shared__ float red[3][256][8];
   const int VR = NC >> 3;                 // host: blockDim.x % VR == 0
   const int cg = threadIdx.x % VR, rstep = blockDim.x / VR, r0 = threadIdx.x / VR;
   const int c0 = cg * 8;
   const long plane = (long)M * NC;
-  float sh[8], s1[8], s2[8];
+  const bool bsum = bs.rep != nullptr;    // DGRAD: BN-backward sums of the producer BN (conv_tap's epilogue)
+  float sh[8], bq[3][8], bm[2][8], bi[2][8];
+  bnsum_coeffs(bs, c0, bsum, bm, bi, bq);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sh[j] = (stats && shift) ? shift[c0 + j] : 0.f;
-    s1[j] = s2[j] = 0.f;
-  }
+  for (int j = 0; j < 8; ++j) sh[j] = (stats && shift) ? shift[c0 + j] : 0.f;
   const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
   for (int m = rb + r0; m < re; m += rstep) {
     const float* p = ws + (long)m * NC + c0;
@@ -1336,24 +1412,27 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restric
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = (float)o[j] - sh[j];
-        s1[j] += d;
-        s2[j] += d * d;
+        bq[0][j] += d;
+        bq[1][j] += d * d;
       }
+    } else if (bsum) {
+      bnsum_acc(bs, orow * NC + c0, o, bm, bi, bq);
     }
   }
-  if (!stats) return;
+  if (!stats && !bsum) return;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    red[0][threadIdx.x][j] = s1[j];
-    red[1][threadIdx.x][j] = s2[j];
-  }
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[q][threadIdx.x][j] = bq[q][j];
   __syncthreads();
-  for (int e = threadIdx.x; e < 2 * NC; e += blockDim.x) {
+  const int nq = (bsum && bs.zb) ? 3 : 2;
+  for (int e = threadIdx.x; e < nq * NC; e += blockDim.x) {
     const int q = e / NC, c = e - q * NC;
     const int grp = c >> 3, j = c & 7;
     float t = 0.f;
     for (int th = grp; th < (int)blockDim.x; th += VR) t += red[q][th][j];
-    unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * NC + c, (double)t);
+    if (stats) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * NC + c, (double)t);
+    else unsafeAtomicAdd(bs.rep + ((long)(blockIdx.x % bs.reps) * 3 + q) * NC + c, (double)t);
   }
 }
 
@@ -1632,16 +1711,16 @@ static void launch_halo(hipStream_t st, const HaloGeom& h, const bf16* in, const
     const int rows_per_block = stats ? std::max(2 * rstep, (h.M + 255) / 256) : std::max(rstep, (h.M + 1023) / 1024);
     const int nblk = (h.M + rows_per_block - 1) / rows_per_block;
     hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, splits, h.M, h.O, RowMap{}, out, stats,
-                       shift, rows_per_block, res);
+                       shift, rows_per_block, res, BnSums{});
   }
 }
 
 static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const bf16* wt, bf16* out, double* stats,
                        const float* shift, const RowMap& rm, float* ws, long ws_floats,
-                       const bf16* res = nullptr) {
+                       const bf16* res = nullptr, const BnSums& bs = BnSums{}) {
   if (g.C % 64 || g.O % 8) throw std::invalid_argument("conv_tap: need C % 64 == 0 and O % 8 == 0");
   HaloGeom hg;
-  if (halo_geom(g, rm, &hg)) {
+  if (!bs.rep && halo_geom(g, rm, &hg)) {
     launch_halo(st, hg, in, wt, out, stats, shift, ws, ws_floats, res);
     return;
   }
@@ -1653,20 +1732,23 @@ static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const b
   const int splits = (ksteps + kps - 1) / kps;
   dim3 grid((unsigned)tiles, 1, (unsigned)splits);
   float* part = splits > 1 ? ws : nullptr;
+  const BnSums tbs = part ? BnSums{} : bs;
   if (BN == 128)
     hipLaunchKernelGGL(conv_tap<128>, grid, dim3(256), 0, st, in, wt, out, part, part ? nullptr : stats, shift, g, rm, kps,
-                       part ? nullptr : res);
+                       part ? nullptr : res, tbs);
   else
     hipLaunchKernelGGL(conv_tap<64>, grid, dim3(256), 0, st, in, wt, out, part, part ? nullptr : stats, shift, g, rm, kps,
-                       part ? nullptr : res);
+                       part ? nullptr : res, tbs);
   if (splits > 1) {
     const int VR = g.O / 8;
     const int tb = (256 / VR) * VR;
     const int rstep = tb / VR;
-    const int rows_per_block = stats ? std::max(2 * rstep, (g.M + 255) / 256) : std::max(rstep, (g.M + 1023) / 1024);
+    // with BN statistics / BN-backward sums fewer blocks (their per-channel atomics contend on 2 x O addresses)
+    const int rows_per_block = (stats || bs.rep) ? std::max(2 * rstep, (g.M + 255) / 256)
+                                                 : std::max(rstep, (g.M + 1023) / 1024);
     const int nblk = (g.M + rows_per_block - 1) / rows_per_block;
     hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, splits, g.M, g.O, rm, out, stats, shift,
-                       rows_per_block, res);
+                       rows_per_block, res, bs);
   }
 }
 
@@ -1729,7 +1811,7 @@ static void launch_fd(hipStream_t st, const ConvGeom& g, const bf16* x, const bf
   RowMap rm{};
   if (MODE == DGRAD && g.st != 1) rm = make_rowmap(g.Hp, g.Wp, g.H, g.W, g.st, g.ph, g.pw);
   hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, sp, g.M, g.NC, rm, out, stats, shift,
-                     rows_per_block, acc ? out : nullptr);
+                     rows_per_block, acc ? out : nullptr, BnSums{});
 }
 
 // K-split count for the weight gradient: about two workgroups per CU, at least
@@ -1766,9 +1848,28 @@ void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf
 // dX[N,H,W,C] = conv_transpose(dY[N,P,Q,O], W_rsc)   (every element written).
 // Stride 2 runs as 4 sub-pixel phases so no MFMA multiplies a structural zero.
 // acc: dx += result (the data gradient of one branch of a multi-branch block)
-void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const bf16* wrsc, bf16* dx, float* ws,
-                       long ws_floats, const bf16* wd, int acc) {
+//
+// add: dx = result + add (a second incoming grad, e.g. the shortcut branch's; != dx) and bs: the
+// producer BN's backward sums taken in the epilogue -- both only on the tap path without empty
+// phases (conv_dgrad_fusable).
+int conv_dgrad_fusable(const ConvShape& s, int has_wd) {
   check_shape(s);
+  if (!has_wd || s.O % 64) return 0;
+  TapPhase ph[4];
+  const int n = dgrad_tap_phases(s, ph);
+  for (int i = 0; i < n; ++i)
+    if (ph[i].empty) return 0;
+  return 1;
+}
+
+void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const bf16* wrsc, bf16* dx, float* ws,
+                       long ws_floats, const bf16* wd, int acc, const bf16* add, const BnSums* bs) {
+  check_shape(s);
+  if ((add || bs) && !conv_dgrad_fusable(s, wd != nullptr))
+    throw std::invalid_argument("conv_dgrad: add / BN sums need the tap path (conv_dgrad_fusable)");
+  if (add && acc) throw std::invalid_argument("conv_dgrad: add and accumulate are exclusive");
+  if (bs && (!bs->rep || !bs->z || !bs->mean || !bs->inv || bs->reps < 1 || (bs->zb && (!bs->meanb || !bs->invb))))
+    throw std::invalid_argument("conv_dgrad: incomplete BN sums descriptor");
   if (wd != nullptr && s.O % 64 == 0) {   // tap-major path on the dgrad weight image
     TapPhase ph[4];
     const int n = dgrad_tap_phases(s, ph);
@@ -1783,7 +1884,7 @@ void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const
         continue;
       }
       launch_tap(st, ph[i].g, dy, wd + ph[i].img_off, dx, nullptr, nullptr, ph[i].rm, ws, ws_floats,
-                 acc ? dx : nullptr);
+                 acc ? dx : add, bs ? *bs : BnSums{});
     }
     return;
   }

@@ -92,6 +92,7 @@ class _Unit:
         self.smean = torch.empty(self.O, device=dev)
         self.sinv = torch.empty(self.O, device=dev)
         self.shift = torch.zeros(self.O, device=dev)   # previous batch mean: stats are sums of (z - shift)
+        self._fusable: Optional[bool] = None
 
     def view(self, t: torch.Tensor, nb: int) -> torch.Tensor:
         return t[: nb * self.P * self.P * self.O].view(nb, self.P, self.P, self.O)
@@ -139,13 +140,23 @@ class _Unit:
                               ws=ws)
 
     def dgrad(self, nb: int, out: torch.Tensor, ws: Optional[torch.Tensor] = None,
-              dz: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+              dz: Optional[torch.Tensor] = None, accumulate: bool = False, add: Optional[torch.Tensor] = None,
+              bn_sums: Optional[dict] = None) -> torch.Tensor:
         dz = self.view(self.dz, nb) if dz is None else dz
         if self.depthwise:
-            assert not accumulate
+            assert not accumulate and add is None and bn_sums is None
             return conv.dwconv_dgrad(dz, self.conv.weight, self.in_shape(nb), self.stride, self.pad, out=out)
         return conv.conv2d_dgrad(dz, self.wr, self.in_shape(nb), self.stride, self.pad, Cw=self.Cw, out=out, ws=ws,
-                                 wd=self.wd, accumulate=accumulate)
+                                 wd=self.wd, accumulate=accumulate, add=add, bn_sums=bn_sums)
+
+    def dgrad_fusable(self) -> bool:
+        """Whether this conv's DGRAD can take a second incoming grad and its producer BN's backward sums
+        in the epilogue (dense tap path)."""
+        if self._fusable is None:
+            self._fusable = (not self.depthwise and self.wd is not None and
+                             conv.dgrad_fusable(self.in_shape(1), self.O, self.R, self.S, self.stride, self.pad,
+                                                self.Cw, True))
+        return self._fusable
 
     def pack_item(self):
         return None if self.depthwise else (self.conv.weight.data, self.wr)
@@ -501,9 +512,16 @@ class CNNNativeTrainer(LocalTrainer):
                                     dtype=torch.float64, device=device)
         co = 0
         for u in self.units:
-            n = (cnn.bn_bwd_chain_floats(u.O) + 3) // 4 * 4
+            nf = cnn.bn_bwd_chain_floats(u.O)
+            n = (nf + 3) // 4 * 4
             u.bn_rep = self.bn_chain[co:co + n] if n else None
+            u.bn_reps = nf // (3 * u.O)
             co += n
+        # BN-backward channel sums taken in the epilogue of the DGRAD that writes the BN's output grad
+        # (conv_igemm.hip BnSums): no separate reduce pass over (dy, z, y).  FEDMI_CNN_FUSE_BN_BWD=0: off.
+        import os
+
+        self._fuse_bn_bwd = os.environ.get("FEDMI_CNN_FUSE_BN_BWD", "1") != "0"
         self.xin = torch.empty(R, 32, 32, 8, dtype=act_dtype, device=device)
         self.dhead = torch.empty(R * self.head_hw * self.head_hw * self.head_c, dtype=act_dtype, device=device)
         self.pooled = torch.empty(R, self.head_c, device=device)
@@ -643,8 +661,17 @@ class CNNNativeTrainer(LocalTrainer):
                  dbase=dbase, zero=self.bn_chain if train else None)
         return x, hd
 
+    def _sums(self, conv_u: _Unit, u: _Unit, nb: int, y, zb: Optional[_Unit] = None) -> Optional[dict]:
+        """BN-sums descriptor for ``u``'s BN, taken by ``conv_u``'s DGRAD epilogue (None: not fusable)."""
+        if not (self._fuse_bn_bwd and u.bn_rep is not None and u.bn_reps > 0 and conv_u.dgrad_fusable()):
+            return None
+        d = dict(rep=u.bn_rep, reps=u.bn_reps, z=u.view(u.z, nb), y=y, mean=u.smean, inv=u.sinv)
+        if zb is not None:
+            d.update(zb=zb.view(zb.z, nb), meanb=zb.smean, invb=zb.sinv)
+        return d
+
     def _bn_bwd(self, u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None, dadd=None,
-                mask_bn=None) -> None:
+                mask_bn=None, presummed: bool = False) -> None:
         bn_ws = self.bn_ws if self.bn_ws.numel() else None
         chained = u.bn_rep is not None
         if chained:
@@ -654,18 +681,20 @@ class CNNNativeTrainer(LocalTrainer):
             kw = dict(zb=zb.view(zb.z, nb), b=zb.bn_args(None), dgamma_b=zb.bn.weight.grad,
                       dbeta_b=zb.bn.bias.grad, dzb=zb.view(zb.dz, nb))
         cnn.bn_bwd(dya, u.view(u.z, nb), u.bn_args(None), u.bn.weight.grad, u.bn.bias.grad, u.view(u.dz, nb), u.red,
-                   dyb=dyb, y=y, gout=gout, ws=bn_ws, dadd=dadd, chained=chained, mask_bn=mask_bn, **kw)
+                   dyb=dyb, y=y, gout=gout, ws=bn_ws, dadd=dadd, chained=chained, mask_bn=mask_bn,
+                   presummed=presummed, **kw)
 
     def _backward(self, nb: int, x: torch.Tensor, dhead: torch.Tensor) -> None:
         if self.preact is not None:
             return self._backward_preact(nb, x, dhead)
         if self.goog is not None:
             return self._backward_goog(nb, x, dhead)
-        dya, dyb = dhead, None
+        dya, dyb, pres = dhead, None, False
         ws = self.wgrad_ws
         for i in range(len(self.blocks) - 1, -1, -1):
             b = self.blocks[i]
-            a_in = x if b.first else self._act(self.blocks[i - 1], nb)
+            prev = None if b.first else self.blocks[i - 1]
+            a_in = x if b.first else self._act(prev, nb)
             last = b.main[-1]
             din_b = b.in_view(b.din_b, nb) if b.din_b is not None else None
             if b.pool:   # grad wrt the pooled output -> grad wrt the pre-pool activation
@@ -673,24 +702,41 @@ class CNNNativeTrainer(LocalTrainer):
             if getattr(b, "defer", False):
                 self._bn_bwd(last, nb, dya, dyb, None, mask_bn=b.co)
             else:
+                # pres: the next block's first DGRAD wrote dya = (its grad + the shortcut grad) and this BN's sums
                 self._bn_bwd(last, nb, dya, dyb, b.pre_view(nb) if b.out_relu else None, zb=b.proj,
-                             gout=din_b if b.shortcut == "identity" else None)
+                             gout=din_b if b.shortcut == "identity" else None, presummed=pres)
+            proj_done = False
             for j in range(len(b.main) - 1, -1, -1):
                 v = b.main[j]
                 xin = b.main[j - 1].view(b.main[j - 1].y, nb) if j > 0 else a_in
                 v.wgrad(xin, nb, ws)
                 if j > 0:
                     w = b.main[j - 1]
-                    v.dgrad(nb, w.view(w.dy, nb), ws)
-                    self._bn_bwd(w, nb, w.view(w.dy, nb), None, w.view(w.y, nb) if w.relu else None)
+                    wy = w.view(w.y, nb) if w.relu else None
+                    bs = self._sums(v, w, nb, wy)
+                    v.dgrad(nb, w.view(w.dy, nb), ws, bn_sums=bs)
+                    self._bn_bwd(w, nb, w.view(w.dy, nb), None, wy, presummed=bs is not None)
                 elif not b.first:
-                    v.dgrad(nb, b.in_view(b.din_a, nb), ws)
-            if b.proj is not None:
+                    din_a = b.in_view(b.din_a, nb)
+                    bs = None
+                    if not (prev.pool or getattr(prev, "defer", False)):
+                        pl = prev.main[-1]
+                        bs = self._sums(v, pl, nb, prev.pre_view(nb) if prev.out_relu else None, zb=prev.proj)
+                    if bs is not None:
+                        # the shortcut's grad first, then conv1's DGRAD adds it and takes the previous
+                        # block's BN-backward sums from the complete grad
+                        if b.proj is not None:
+                            b.proj.wgrad(a_in, nb, ws)
+                            b.proj.dgrad(nb, din_b, ws)
+                            proj_done = True
+                        v.dgrad(nb, din_a, ws, add=din_b, bn_sums=bs)
+                        dya, dyb, pres = din_a, None, True
+                    else:
+                        v.dgrad(nb, din_a, ws)
+                        dya, dyb, pres = din_a, din_b, False
+            if b.proj is not None and not proj_done:
                 b.proj.wgrad(a_in, nb, ws)
                 b.proj.dgrad(nb, din_b, ws)
-            if not b.first:
-                dya = b.in_view(b.din_a, nb)
-                dyb = din_b
 
     # ---- pre-activation ResNets --------------------------------------------------------------
     def _head(self, a, nb, train, labels, dbase, stats_row):

@@ -154,7 +154,7 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
            zb: Optional[torch.Tensor] = None, b: Optional[BNParams] = None, dgamma_b=None, dbeta_b=None, dzb=None,
            gout: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
            dadd: Optional[torch.Tensor] = None, chained: bool = False,
-           mask_bn: Optional[torch.Tensor] = None) -> None:
+           mask_bn: Optional[torch.Tensor] = None, presummed: bool = False) -> None:
     """BatchNorm backward through an optional ReLU mask (``y``: forward output) for one or two BN
     branches sharing the incoming grad g = dya (+ dyb).  Writes dz for each branch, dgamma/dbeta,
     and optionally g itself (``gout``, the identity-shortcut grad).  ``red``: [3, C] fp64 channel
@@ -164,7 +164,9 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
     replica buffer (>= :func:`bn_bwd_chain_floats`, ZERO on entry -- the engine's head launch clears
     the arena every step); no finalize launch, the apply kernel reads the replicas.  ``mask_bn``
     ([2, C] scale / shift, with ``y`` None): the ReLU mask is relu(za * scale + shift) > 0 -- for a BN
-    whose output was never materialised (its consumer applied it on load)."""
+    whose output was never materialised (its consumer applied it on load).  ``presummed`` (chained): the
+    DGRAD that wrote ``dya`` already added the channel sums into ``ws`` (:func:`conv.conv2d_dgrad`
+    ``bn_sums``): only the apply pass runs."""
     C = za.shape[-1]
     M = za.numel() // C
     if red.numel() < 3 * C or red.dtype != torch.float64:
@@ -182,7 +184,7 @@ def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Ten
         raise ValueError("bn_bwd: dya and dyb must share a row stride")
     native.require().bn_bwd(native.stream_handle(red.device), d, red.data_ptr(), M, C,
                             ws.data_ptr() if ws is not None else 0, ws.numel() if ws is not None else 0,
-                            ldd, row_stride(y) if y is not None else C, int(chained))
+                            ldd, row_stride(y) if y is not None else C, int(chained), int(presummed))
 
 
 def bn_bwd_chain_floats(C: int) -> int:

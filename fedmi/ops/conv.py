@@ -161,10 +161,16 @@ def dgrad_pack_weights(items) -> None:
 
 def conv2d_dgrad(dy: torch.Tensor, wrsc: torch.Tensor, x_shape, stride: int, pad: int, Cw: Optional[int] = None,
                  out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-                 wd: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+                 wd: Optional[torch.Tensor] = None, accumulate: bool = False, add: Optional[torch.Tensor] = None,
+                 bn_sums: Optional[dict] = None) -> torch.Tensor:
     """dx[N,H,W,C] from dy[N,P,Q,O].  ``wd``: the conv's DGRAD weight image (:func:`dgrad_pack_weights`)
     selects the tap-major LDS-DMA kernel (O % 64 == 0); without it the generic implicit GEMM runs.
-    ``accumulate``: out += dx (one branch's share of a multi-branch block's input gradient)."""
+    ``accumulate``: out += dx (one branch's share of a multi-branch block's input gradient).
+    ``add``: out = dx + add (another incoming grad of the same tensor, e.g. the shortcut's).
+    ``bn_sums`` (dict rep, reps, z, y, mean, inv [, zb, meanb, invb: a projection-shortcut BN that shares
+    the incoming grad]): the BatchNorm that produced this conv's input gets
+    its backward channel sums from the epilogue (chained replica layout, :func:`cnn.bn_bwd` presummed)
+    -- ``add`` / ``bn_sums`` need :func:`dgrad_fusable`."""
     _check(dy, torch.bfloat16, "conv2d_dgrad.dy")
     O, R, S, C = wrsc.shape
     shp = shape_tuple(x_shape, O, R, S, stride, pad, Cw)
@@ -178,9 +184,31 @@ def conv2d_dgrad(dy: torch.Tensor, wrsc: torch.Tensor, x_shape, stride: int, pad
         _check(wd, torch.bfloat16, "conv2d_dgrad.wd")
         if wd.numel() < O * R * S * C:
             raise ValueError("conv2d_dgrad: dgrad image too small")
+    bs = None
+    if bn_sums is not None:
+        z, y = bn_sums["z"], bn_sums.get("y")
+        if z.shape != out.shape or (y is not None and y.shape != out.shape) or not z.is_contiguous():
+            raise ValueError("conv2d_dgrad: BN sums need compact z / y of the output's shape")
+        zb = bn_sums.get("zb")
+        if zb is not None and zb.shape != out.shape:
+            raise ValueError("conv2d_dgrad: BN sums zb must have the output's shape")
+        bs = dict(rep=bn_sums["rep"].data_ptr(), reps=int(bn_sums["reps"]), z=z.data_ptr(),
+                  y=y.data_ptr() if y is not None else 0, mean=bn_sums["mean"].data_ptr(),
+                  inv=bn_sums["inv"].data_ptr())
+        if zb is not None:
+            bs.update(zb=zb.data_ptr(), meanb=bn_sums["meanb"].data_ptr(), invb=bn_sums["invb"].data_ptr())
+    if add is not None and add.shape != out.shape:
+        raise ValueError("conv2d_dgrad: add must have the output's shape")
     native.require().conv_dgrad(native.stream_handle(dy.device), shp, dy.data_ptr(), wrsc.data_ptr(), out.data_ptr(),
-                                *_ws_args(ws), wd.data_ptr() if wd is not None else 0, int(accumulate))
+                                *_ws_args(ws), wd.data_ptr() if wd is not None else 0, int(accumulate),
+                                add.data_ptr() if add is not None else 0, bs)
     return out
+
+
+def dgrad_fusable(x_shape, O: int, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None,
+                  has_wd: bool = True) -> bool:
+    """Whether :func:`conv2d_dgrad` of this shape takes ``add`` / ``bn_sums`` (tap path, no empty phase)."""
+    return bool(native.require().conv_dgrad_fusable(shape_tuple(x_shape, O, R, S, stride, pad, Cw), int(has_wd)))
 
 
 _WS: dict = {}

@@ -93,9 +93,16 @@ def conv2d_fwd(x, wrsc, stride, pad, Cw=None, stats=None, out=None, shift=None, 
 
 
 @torch.no_grad()
-def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None, ws=None, wd=None, accumulate=False):
+def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None, ws=None, wd=None, accumulate=False, add=None,
+                 bn_sums=None):
+    """``bn_sums``: the kernel adds the producer BN's backward sums into its replicas; the emulated
+    bn_bwd recomputes them from dya either way, so only the schedule (``add``) matters here."""
     N, H, W, C = x_shape
     Cw = Cw or C
+    O, R, S = wrsc.shape[0], wrsc.shape[1], wrsc.shape[2]
+    if (add is not None or bn_sums is not None) and not dgrad_fusable(x_shape, O, R, S, stride, pad, Cw,
+                                                                     wd is not None):
+        raise ValueError("conv2d_dgrad: add / bn_sums need a fusable shape")
     dx = torch.nn.grad.conv2d_input((N, Cw, H, W), _w_from_img(wrsc, Cw), _nchw(dy), stride=stride, padding=pad)
     full = torch.zeros(N, C, H, W, device=dy.device)
     full[:, :Cw] = dx
@@ -103,7 +110,25 @@ def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None, ws=None, wd=
         out = torch.empty(*x_shape, dtype=_BF, device=dy.device)
     if accumulate:
         full = full + _nchw(out)
+    if add is not None:
+        full = _nchw(_nhwc_into(torch.empty_like(out), full)).float() + _nchw(add).float()
     return _nhwc_into(out, full)
+
+
+def dgrad_fusable(x_shape, O, R, S, stride, pad, Cw=None, has_wd=True):
+    """Mirror of conv_igemm.hip conv_dgrad_fusable: tap path (a DGRAD image, O % 64), no empty phase."""
+    if not has_wd or O % 64:
+        return False
+    if stride == 1:
+        return True
+    H, W = x_shape[1], x_shape[2]
+    for ph in range(2):
+        for pw in range(2):
+            r0, s0 = (ph + pad) & 1, (pw + pad) & 1
+            nr, ns = max(0, (R - r0 + 1) // 2), max(0, (S - s0 + 1) // 2)
+            if (H - ph + 1) // 2 > 0 and (W - pw + 1) // 2 > 0 and nr * ns == 0:
+                return False
+    return True
 
 
 @torch.no_grad()
@@ -278,7 +303,9 @@ def maxpool2_bwd(x, dy, out=None):
 
 @torch.no_grad()
 def bn_bwd(dya, za, a, dgamma_a, dbeta_a, dza, red, dyb=None, y=None, zb=None, b=None, dgamma_b=None,
-           dbeta_b=None, dzb=None, gout=None, ws=None, dadd=None, chained=False, mask_bn=None):
+           dbeta_b=None, dzb=None, gout=None, ws=None, dadd=None, chained=False, mask_bn=None, presummed=False):
+    if presummed and (dyb is not None or mask_bn is not None or not chained):
+        raise ValueError("bn_bwd: presummed covers one incoming grad and a y mask, chained replicas")
     C = za.shape[-1]
     M = za.numel() // C
     g = dya.float().reshape(M, C)
@@ -311,7 +338,7 @@ def bn_bwd_ws_floats(M, C):
 
 
 def bn_bwd_chain_floats(C):
-    return 0
+    return 12 * C    # a replica slice exists (the engine then takes the chained / presummed schedule)
 
 
 @torch.no_grad()
@@ -359,7 +386,7 @@ def emulated():
         saved.append((mod, name, getattr(mod, name)))
         setattr(mod, name, fn)
 
-    for name in ("pack_weight", "pack_weights", "fd_ws_floats", "dgrad_pack_weights", "conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
+    for name in ("pack_weight", "pack_weights", "fd_ws_floats", "dgrad_pack_weights", "conv2d_fwd", "conv2d_dgrad", "dgrad_fusable", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
                  "dwconv_dgrad", "dwconv_wgrad", "dwconv_ws_floats"):
         swap(conv, name, globals()[name])
     for name in ("prep_input", "sched_next", "bn_apply", "bn_coeff", "bn_bwd", "bn_bwd_ws_floats", "bn_bwd_chain_floats", "head", "maxpool2",

@@ -739,3 +739,88 @@ def test_conv_wgrad_halo(gpu_device, shape, monkeypatch):
     assert not torch.isnan(dw).any()
     assert _rel(dw, wr_.grad) < 1e-2
     assert _rel(dw, dw0) < 1e-3
+
+
+# DGRAD epilogue with a second incoming grad and the producer BN's backward sums (conv_igemm.hip BnSums):
+# single-pass tap kernel, split-K combine, and the four stride-2 sub-pixel phases
+FUSE_SHAPES = [(8, 16, 16, 64, 64, 3, 1, 1), (128, 32, 32, 64, 64, 3, 1, 1), (128, 8, 8, 256, 256, 3, 1, 1),
+               (128, 4, 4, 512, 512, 3, 1, 1), (16, 16, 16, 64, 128, 3, 2, 1), (16, 8, 8, 128, 256, 1, 1, 0)]
+
+
+@pytest.mark.parametrize("shape", FUSE_SHAPES, ids=[str(s) for s in FUSE_SHAPES])
+@pytest.mark.parametrize("relu,proj", [(True, False), (False, True)])
+def test_conv_dgrad_fused_bn_sums(gpu_device, shape, relu, proj):
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device, seed=31)
+    C = xn.shape[-1]
+    P = (H + 2 * pad - R) // st + 1
+    g = torch.Generator(device="cpu").manual_seed(5)
+    dyn = torch.randn(N, P, P, O, generator=g).to(gpu_device).bfloat16()
+    add = torch.randn(N, H, W, C, generator=g).to(gpu_device).bfloat16()
+    z = torch.randn(N, H, W, C, generator=g).to(gpu_device).bfloat16()
+    y = torch.relu(torch.randn(N, H, W, C, generator=g)).to(gpu_device).bfloat16() if relu else None
+    zb = torch.randn(N, H, W, C, generator=g).to(gpu_device).bfloat16() if proj else None
+    mean, inv = torch.randn(C, device=gpu_device) * 0.1, torch.rand(C, device=gpu_device) + 0.5
+    meanb, invb = torch.randn(C, device=gpu_device) * 0.1, torch.rand(C, device=gpu_device) + 0.5
+    wpk = conv.pack_weight(w)
+    wd = torch.empty(conv.dgrad_image_numel(w.shape, C), dtype=torch.bfloat16, device=gpu_device)
+    conv.dgrad_pack_weights([(w, wd, st, pad, C)])
+    shp = (xn.shape, O, R, R, st, pad, Cw)
+    assert conv.dgrad_fusable(*shp)
+    wsp = torch.empty(max(conv.fd_ws_floats(*shp), 1), device=gpu_device)
+    reps = 4
+    rep = torch.zeros(reps, 3, C, dtype=torch.float64, device=gpu_device)
+    bs = dict(rep=rep, reps=reps, z=z, y=y, mean=mean, inv=inv)
+    if proj:
+        bs.update(zb=zb, meanb=meanb, invb=invb)
+    plain = conv.conv2d_dgrad(dyn, wpk, xn.shape, st, pad, Cw=Cw, ws=wsp, wd=wd)
+    out = torch.full_like(plain, float("nan"))
+    conv.conv2d_dgrad(dyn, wpk, xn.shape, st, pad, Cw=Cw, out=out, ws=wsp, wd=wd, add=add, bn_sums=bs)
+    torch.cuda.synchronize()
+    # out = bf16(dgrad + add): one or two bf16 roundings of the same sum
+    ref = plain.float() + add.float()
+    assert float((out.float() - ref).abs().max()) <= 2 * float(ref.abs().max()) * 2 ** -8
+    # the sums are of the stored bf16 output (what bn_bwd's apply pass re-reads)
+    gm = out.double().reshape(-1, C)
+    if relu:
+        gm = torch.where(y.double().reshape(-1, C) > 0, gm, torch.zeros_like(gm))
+    s0 = gm.sum(0)
+    s1 = (gm * ((z.double().reshape(-1, C) - mean.double()) * inv.double())).sum(0)
+    got = rep.sum(0)
+    scale = gm.abs().sum(0) + 1.0
+    assert float(((got[0] - s0).abs() / scale).max()) < 1e-5
+    assert float(((got[1] - s1).abs() / (scale * 4)).max()) < 1e-5
+    if proj:
+        s2 = (gm * ((zb.double().reshape(-1, C) - meanb.double()) * invb.double())).sum(0)
+        assert float(((got[2] - s2).abs() / (scale * 4)).max()) < 1e-5
+    else:
+        assert float(got[2].abs().max()) == 0.0
+
+
+def test_bn_bwd_presummed_matches_reduce(gpu_device):
+    """bn_bwd's apply pass on epilogue-summed replicas == the reduce + apply pair (chained mode)."""
+    M, C = 4096, 128
+    g = torch.Generator(device="cpu").manual_seed(9)
+    dy = torch.randn(M, C, generator=g).to(gpu_device).bfloat16()
+    z = torch.randn(M, C, generator=g).to(gpu_device).bfloat16()
+    y = torch.relu(torch.randn(M, C, generator=g)).to(gpu_device).bfloat16()
+    gamma = torch.rand(C, device=gpu_device) + 0.5
+    mean, inv = torch.randn(C, device=gpu_device) * 0.1, torch.rand(C, device=gpu_device) + 0.5
+    reps = cnn.bn_bwd_chain_floats(C) // (3 * C)
+    outs = []
+    for pres in (False, True):
+        rep = torch.zeros(reps, 3, C, dtype=torch.float64, device=gpu_device)
+        if pres:   # what the DGRAD epilogue adds: the sums of masked dy over the rows, split over replicas
+            gm = torch.where(y.float() > 0, dy.float(), torch.zeros_like(dy.float())).double()
+            rep[0, 0] = gm.sum(0)
+            rep[0, 1] = (gm * ((z.double() - mean.double()) * inv.double())).sum(0)
+        a = cnn.bn_desc(gamma=gamma, smean=mean, sinv=inv)
+        dg, db = torch.empty(C, device=gpu_device), torch.empty(C, device=gpu_device)
+        dz = torch.empty(M, C, dtype=torch.bfloat16, device=gpu_device)
+        red = torch.zeros(3, C, dtype=torch.float64, device=gpu_device)
+        cnn.bn_bwd(dy, z, a, dg, db, dz, red, y=y, ws=rep.view(-1), chained=True, presummed=pres)
+        torch.cuda.synchronize()
+        outs.append((dz.float(), dg, db))
+    (dz0, dg0, db0), (dz1, dg1, db1) = outs
+    assert _rel(dg1, dg0) < 1e-5 and _rel(db1, db0) < 1e-5
+    assert _rel(dz1, dz0) < 1e-2
