@@ -21,10 +21,6 @@ struct ConvShape {
 };
 void launch_conv_fwd(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, double*, const float*, float*, long,
                      const bf16*);
-struct BnSums {
-  double* rep; const bf16* z; const bf16* y; const float* mean; const float* inv; int reps;
-  const bf16* zb; const float* meanb; const float* invb;
-};
 void launch_conv_dgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, bf16*, float*, long, const bf16*, int,
                        const bf16*, const BnSums*);
 int conv_dgrad_fusable(const ConvShape&, int);
@@ -67,13 +63,13 @@ struct DwShape {
   int N, H, W, C, R, S, st, pad;
 };
 void launch_dw_fwd(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, double*, const float*, const float*);
-void launch_dw_dgrad(hipStream_t, const DwShape&, const bf16*, const float*, bf16*);
+void launch_dw_dgrad(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, const BnSums*);
 long dw_wgrad_ws_floats(const DwShape&);
 void launch_dw_wgrad(hipStream_t, const DwShape&, const bf16*, const bf16*, float*, float*, long, int, const float*);
 void launch_prep_input(hipStream_t, const uint8_t*, int, const int*, int, int, uint32_t, const int*, bf16*);
 void launch_sched_next(hipStream_t, const int*, int*, int*);
 void launch_bn_apply(hipStream_t, const bf16*, const BNDesc&, const bf16*, const BNDesc*, const bf16*, bf16*, int, int,
-                     float, float, int, int, int);
+                     float, float, int, int, int, float*);
 void launch_bn_bwd(hipStream_t, const BNBwdDesc&, double*, int, int, double*, long, int, int, int, int);
 void launch_bn_coeff(hipStream_t, const BNDesc&, int, int, float, float, int, float*);
 long bn_bwd_ws_floats(int, int);
@@ -114,6 +110,13 @@ DwShape dw_from(const py::tuple& t) {
   return s;
 }
 
+BnSums bnsums_from(const py::dict& d) {
+  return BnSums{P<double>(dget(d, "rep")), P<const bf16>(dget(d, "z")), P<const bf16>(dget(d, "y")),
+                P<const float>(dget(d, "mean")), P<const float>(dget(d, "inv")), d["reps"].cast<int>(),
+                P<const bf16>(dget(d, "zb")), P<const float>(dget(d, "meanb")), P<const float>(dget(d, "invb")),
+                P<const float>(dget(d, "msc")), d.contains("msc_ld") ? d["msc_ld"].cast<int>() : 0};
+}
+
 BNDesc bn_from(const py::dict& d) {
   return BNDesc{P<const double>(dget(d, "stats")), P<const float>(dget(d, "gamma")), P<const float>(dget(d, "beta")),
                 P<float>(dget(d, "rmean")),       P<float>(dget(d, "rvar")),        P<long long>(dget(d, "nbt")),
@@ -138,12 +141,7 @@ void fedmi_bind_cnn(py::module_& m) {
                          long ws_floats, uintptr_t wd, int acc, uintptr_t add, py::object bsum) {
     BnSums bs{};
     const bool has_bs = !bsum.is_none();
-    if (has_bs) {
-      const py::dict d = bsum.cast<py::dict>();
-      bs = BnSums{P<double>(dget(d, "rep")), P<const bf16>(dget(d, "z")), P<const bf16>(dget(d, "y")),
-                  P<const float>(dget(d, "mean")), P<const float>(dget(d, "inv")), d["reps"].cast<int>(),
-                  P<const bf16>(dget(d, "zb")), P<const float>(dget(d, "meanb")), P<const float>(dget(d, "invb"))};
-    }
+    if (has_bs) bs = bnsums_from(bsum.cast<py::dict>());
     launch_conv_dgrad(S(st), shape_from(shp), P<const bf16>(dy), P<const bf16>(w), P<bf16>(dx), P<float>(ws),
                       ws ? ws_floats : 0, P<const bf16>(wd), acc, P<const bf16>(add), has_bs ? &bs : nullptr);
     check("conv_dgrad");
@@ -192,10 +190,14 @@ void fedmi_bind_cnn(py::module_& m) {
     check("dw_fwd");
   }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("shift"),
      py::arg("isc") = 0);
-  m.def("dw_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx) {
-    launch_dw_dgrad(S(st), dw_from(shp), P<const bf16>(dy), P<const float>(w), P<bf16>(dx));
+  m.def("dw_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx,
+                       py::object bsum) {
+    BnSums bs{};
+    const bool has_bs = !bsum.is_none();
+    if (has_bs) bs = bnsums_from(bsum.cast<py::dict>());
+    launch_dw_dgrad(S(st), dw_from(shp), P<const bf16>(dy), P<const float>(w), P<bf16>(dx), has_bs ? &bs : nullptr);
     check("dw_dgrad");
-  });
+  }, py::arg("st"), py::arg("shp"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("bsum") = py::none());
   m.def("dw_wgrad_ws_floats", [](const py::tuple& shp) { return dw_wgrad_ws_floats(dw_from(shp)); });
   m.def("dw_wgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws,
                        long ws_floats, int accumulate, uintptr_t isc) {
@@ -232,15 +234,17 @@ void fedmi_bind_cnn(py::module_& m) {
     check("sched_next");
   });
   m.def("bn_apply", [](uintptr_t st, uintptr_t z, const py::dict& a, uintptr_t z2, py::object b, uintptr_t res,
-                       uintptr_t y, int M, int C, float eps, float mom, int train, int relu, int ldy) {
+                       uintptr_t y, int M, int C, float eps, float mom, int train, int relu, int ldy,
+                       uintptr_t co_out) {
     BNDesc bd{};
     const bool has_b = !b.is_none();
     if (has_b) bd = bn_from(b.cast<py::dict>());
     launch_bn_apply(S(st), P<const bf16>(z), bn_from(a), P<const bf16>(z2), has_b ? &bd : nullptr, P<const bf16>(res),
-                    P<bf16>(y), M, C, eps, mom, train, relu, ldy);
+                    P<bf16>(y), M, C, eps, mom, train, relu, ldy, P<float>(co_out));
     check("bn_apply");
   }, py::arg("st"), py::arg("z"), py::arg("a"), py::arg("z2"), py::arg("b"), py::arg("res"), py::arg("y"), py::arg("M"),
-     py::arg("C"), py::arg("eps"), py::arg("mom"), py::arg("train"), py::arg("relu"), py::arg("ldy") = 0);
+     py::arg("C"), py::arg("eps"), py::arg("mom"), py::arg("train"), py::arg("relu"), py::arg("ldy") = 0,
+     py::arg("co_out") = 0);
   m.def("bn_coeff", [](uintptr_t st, const py::dict& a, int M, int C, float eps, float mom, int train, uintptr_t co) {
     launch_bn_coeff(S(st), bn_from(a), M, C, eps, mom, train, P<float>(co));
     check("bn_coeff");

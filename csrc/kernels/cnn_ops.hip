@@ -149,7 +149,7 @@ constexpr int kBnChunk = 64;
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ z, BNArgs A, const bf16* __restrict__ z2,
                                                        BNArgs B, const bf16* __restrict__ res, bf16* __restrict__ y,
                                                        int M, int C, float eps, float mom, int train, int relu,
-                                                       int res_mode, int ldy) {
+                                                       int res_mode, int ldy, float* __restrict__ co_out) {
   extern __shared__ float co[];   // [4][C]
   float* sc = co;
   float* sh = co + C;
@@ -157,6 +157,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
   float* sh2 = co + 3 * C;
   bn_coeffs(A, C, M, eps, mom, train, sc, sh, 0, C, blockIdx.x == 0);
   if (res_mode == 2) bn_coeffs(B, C, M, eps, mom, train, sc2, sh2, 0, C, blockIdx.x == 0);
+  if (co_out != nullptr && blockIdx.x == 0)   // the coefficients, for a backward that derives the ReLU mask from z
+    for (int c = threadIdx.x; c < C; c += blockDim.x) { co_out[c] = sc[c]; co_out[C + c] = sh[c]; }
   __syncthreads();
   const int VR = C >> 3;
   const long nv = (long)M * VR;
@@ -191,12 +193,15 @@ __global__ __launch_bounds__(256) void bn_apply_chunk_kernel(const bf16* __restr
                                                              const bf16* __restrict__ z2, BNArgs B,
                                                              const bf16* __restrict__ res, bf16* __restrict__ y, int M,
                                                              int C, float eps, float mom, int train, int relu,
-                                                             int res_mode, int ldy, int rows_per_block) {
+                                                             int res_mode, int ldy, int rows_per_block,
+                                                             float* __restrict__ co_out) {
   __shared__ float co[4][kBnChunk];
   const int CC = min(kBnChunk, C), c_lo = blockIdx.y * CC;
   const bool commit = blockIdx.x == 0;
   bn_coeffs(A, C, M, eps, mom, train, co[0], co[1], c_lo, CC, commit, blockIdx.y == 0);
   if (res_mode == 2) bn_coeffs(B, C, M, eps, mom, train, co[2], co[3], c_lo, CC, commit, blockIdx.y == 0);
+  if (co_out != nullptr && commit)
+    for (int cc = threadIdx.x; cc < CC; cc += blockDim.x) { co_out[c_lo + cc] = co[0][cc]; co_out[C + c_lo + cc] = co[1][cc]; }
   __syncthreads();
   const int VC = CC >> 3, rstep = 256 / VC;
   const int cv = threadIdx.x % VC, c0 = cv * 8, cg = c_lo + c0;
@@ -961,8 +966,9 @@ void launch_sched_next(hipStream_t st, const int* sched, int* counter, int* cur)
   hipLaunchKernelGGL(sched_next_kernel, dim3(1), dim3(64), 0, st, sched, counter, cur);
 }
 
+// co_out (optional): BN-A's scale / shift [2][C] as applied (a backward that derives the ReLU mask from z)
 void launch_bn_apply(hipStream_t st, const bf16* z, const BNDesc& a, const bf16* z2, const BNDesc* b, const bf16* res,
-                     bf16* y, int M, int C, float eps, float mom, int train, int relu, int ldy) {
+                     bf16* y, int M, int C, float eps, float mom, int train, int relu, int ldy, float* co_out) {
   if (C % 8) throw std::invalid_argument("bn_apply: C % 8 != 0");
   if (ldy <= 0) ldy = C;
   if (ldy < C || ldy % 8) throw std::invalid_argument("bn_apply: bad output row stride");
@@ -971,10 +977,10 @@ void launch_bn_apply(hipStream_t st, const bf16* z, const BNDesc& a, const bf16*
   if (use_chunked(C)) {
     const dim3 grid = apply_grid(M, C);
     hipLaunchKernelGGL(bn_apply_chunk_kernel, grid, dim3(256), 0, st, z, to_args(a), z2, bb, res, y, M, C, eps, mom,
-                       train, relu, res_mode, ldy, (M + (int)grid.x - 1) / (int)grid.x);
+                       train, relu, res_mode, ldy, (M + (int)grid.x - 1) / (int)grid.x, co_out);
   } else {
     hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((long)M * (C / 8))), dim3(256), 4 * C * sizeof(float), st, z,
-                       to_args(a), z2, bb, res, y, M, C, eps, mom, train, relu, res_mode, ldy);
+                       to_args(a), z2, bb, res, y, M, C, eps, mom, train, relu, res_mode, ldy, co_out);
   }
 }
 
@@ -1034,8 +1040,8 @@ void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, double* red, int M, int C
     // ws: this BN's own replica buffer, ZERO on entry (the head kernel clears the arena every step)
     const int reps = bn_bwd_chain_reps(C);
     if (!ws || ws_floats < (long)reps * 3 * C) throw std::invalid_argument("bn_bwd: chained replicas too small");
-    if (presummed && (d.dyb || d.msc))
-      throw std::invalid_argument("bn_bwd: presummed sums cover one incoming grad and a y mask");
+    if (presummed && d.dyb)
+      throw std::invalid_argument("bn_bwd: presummed sums cover one incoming grad");
     if (!presummed)
       hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(tb), 0, st, in, red, M, C, rows_per_block, ws, reps);
     if (use_chunked(C)) {

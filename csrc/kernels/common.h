@@ -75,3 +75,59 @@ extern __device__ unsigned long long fedmi_stamps[FEDMI_STAMP_KERNELS][FEDMI_STA
 #else
 #define FEDMI_STAMP(k, i) do {} while (0)
 #endif
+
+namespace fedmi {
+// BatchNorm-backward channel sums of the BN that PRODUCED a DGRAD's output, taken in the DGRAD
+// epilogue (tap kernel or split-K combine) instead of a separate pass over (dy, z, y):
+//   g = bf16(dX)[row][c] * (y[row][c] > 0, or 1 without a ReLU)
+//   rep[blk % reps][0][c] += sum g,   rep[blk % reps][1][c] += sum g * (z[row][c] - mean[c]) * inv[c]
+//   (rep[..][2][c] += sum g * (zb - meanb) * invb: a projection-shortcut BN sharing g)
+// -- the chained replica layout bn_bwd's apply kernel reads (cnn_ops.hip, launch_bn_bwd presummed).
+struct BnSums {
+  double* rep;          // [reps][3][C] fp64, zero at the step start (null: off)
+  const bf16* z;        // the BN's input (its conv's output), compact [rows][C]
+  const bf16* y;        // the BN's ReLU output (mask) or null
+  const float* mean;    // saved batch mean / inverse std of the BN
+  const float* inv;
+  int reps;
+  const bf16* zb;       // second BN branch (projection shortcut) or null
+  const float* meanb;
+  const float* invb;
+  const float* msc;     // y == null: [2][C] scale / shift the forward applied; ReLU mask = z * sc + sh > 0
+  int msc_ld;           // C (row stride of msc)
+};
+
+// one 8-channel group of a DGRAD output row into the BN-backward sums (bm/bi: [2][8] mean / inv of
+// the two branches; q: [3][8])
+FEDMI_DEV void bnsum_acc(const BnSums& bs, long idx, const bf16x8& t, const float (*bm)[8], const float (*bi)[8],
+                         float (*q)[8]) {   // bm / bi: [3][8] (see bnsum_coeffs)
+  const bf16x8 z = *reinterpret_cast<const bf16x8*>(bs.z + idx);
+  bf16x8 y{}, zb{};
+  if (bs.y) y = *reinterpret_cast<const bf16x8*>(bs.y + idx);
+  if (bs.zb) zb = *reinterpret_cast<const bf16x8*>(bs.zb + idx);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float g = (float)t[j];
+    if (bs.y && !((float)y[j] > 0.f)) g = 0.f;
+    else if (!bs.y && bs.msc && !((float)z[j] * bm[2][j] + bi[2][j] > 0.f)) g = 0.f;
+    q[0][j] += g;
+    q[1][j] += g * ((float)z[j] - bm[0][j]) * bi[0][j];
+    if (bs.zb) q[2][j] += g * ((float)zb[j] - bm[1][j]) * bi[1][j];
+  }
+}
+
+// mean / inv of an 8-channel group (both branches; [2]: the z-mask scale / shift), zero past the last channel
+FEDMI_DEV void bnsum_coeffs(const BnSums& bs, int c0, bool ok, float (*bm)[8], float (*bi)[8], float (*q)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    q[0][j] = q[1][j] = q[2][j] = 0.f;
+    bm[0][j] = ok ? bs.mean[c0 + j] : 0.f;
+    bi[0][j] = ok ? bs.inv[c0 + j] : 0.f;
+    bm[1][j] = ok && bs.zb ? bs.meanb[c0 + j] : 0.f;
+    bi[1][j] = ok && bs.zb ? bs.invb[c0 + j] : 0.f;
+    bm[2][j] = ok && bs.msc ? bs.msc[c0 + j] : 0.f;
+    bi[2][j] = ok && bs.msc ? bs.msc[bs.msc_ld + c0 + j] : 0.f;
+  }
+}
+
+}  // namespace fedmi

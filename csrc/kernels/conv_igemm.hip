@@ -74,60 +74,7 @@ FEDMI_DEV long map_row(const RowMap& r, int m) {
   return ((long)n * r.OH + p * r.st + r.ph) * r.OW + q * r.st + r.pw;
 }
 
-}  // namespace
-
-namespace fedmi {
-// BatchNorm-backward channel sums of the BN that PRODUCED a DGRAD's output, taken in the DGRAD
-// epilogue (tap kernel or split-K combine) instead of a separate pass over (dy, z, y):
-//   g = bf16(dX)[row][c] * (y[row][c] > 0, or 1 without a ReLU)
-//   rep[blk % reps][0][c] += sum g,   rep[blk % reps][1][c] += sum g * (z[row][c] - mean[c]) * inv[c]
-//   (rep[..][2][c] += sum g * (zb - meanb) * invb: a projection-shortcut BN sharing g)
-// -- the chained replica layout bn_bwd's apply kernel reads (cnn_ops.hip, launch_bn_bwd presummed).
-struct BnSums {
-  double* rep;          // [reps][3][C] fp64, zero at the step start (null: off)
-  const bf16* z;        // the BN's input (its conv's output), compact [rows][C]
-  const bf16* y;        // the BN's ReLU output (mask) or null
-  const float* mean;    // saved batch mean / inverse std of the BN
-  const float* inv;
-  int reps;
-  const bf16* zb;       // second BN branch (projection shortcut) or null
-  const float* meanb;
-  const float* invb;
-};
-}  // namespace fedmi
-
-namespace {
 using fedmi::BnSums;
-
-// one 8-channel group of a DGRAD output row into the BN-backward sums (bm/bi: [2][8] mean / inv of
-// the two branches; q: [3][8])
-FEDMI_DEV void bnsum_acc(const BnSums& bs, long idx, const bf16x8& t, const float (*bm)[8], const float (*bi)[8],
-                         float (*q)[8]) {
-  const bf16x8 z = *reinterpret_cast<const bf16x8*>(bs.z + idx);
-  bf16x8 y{}, zb{};
-  if (bs.y) y = *reinterpret_cast<const bf16x8*>(bs.y + idx);
-  if (bs.zb) zb = *reinterpret_cast<const bf16x8*>(bs.zb + idx);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float g = (float)t[j];
-    if (bs.y && !((float)y[j] > 0.f)) g = 0.f;
-    q[0][j] += g;
-    q[1][j] += g * ((float)z[j] - bm[0][j]) * bi[0][j];
-    if (bs.zb) q[2][j] += g * ((float)zb[j] - bm[1][j]) * bi[1][j];
-  }
-}
-
-// mean / inv of an 8-channel group (both branches), zero past the last channel
-FEDMI_DEV void bnsum_coeffs(const BnSums& bs, int c0, bool ok, float (*bm)[8], float (*bi)[8], float (*q)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    q[0][j] = q[1][j] = q[2][j] = 0.f;
-    bm[0][j] = ok ? bs.mean[c0 + j] : 0.f;
-    bi[0][j] = ok ? bs.inv[c0 + j] : 0.f;
-    bm[1][j] = ok && bs.zb ? bs.meanb[c0 + j] : 0.f;
-    bi[1][j] = ok && bs.zb ? bs.invb[c0 + j] : 0.f;
-  }
-}
 
 enum { FWD = 0, DGRAD = 1, WGRAD = 2 };
 constexpr int BK = 64;
@@ -680,7 +627,7 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
   constexpr int CPR = BN / 8;
   // DGRAD: BN-backward sums of the producer BN (each thread keeps one 8-channel group: 256 % CPR == 0)
   const bool bsum = bs.rep != nullptr;
-  float bq[3][8], bm[2][8], bi[2][8];
+  float bq[3][8], bm[3][8], bi[3][8];
   if (bsum) bnsum_coeffs(bs, n0 + (tid % CPR) * 8, n0 + (tid % CPR) * 8 < g.O, bm, bi, bq);
   for (int c = tid; c < BM * CPR; c += 256) {
     const int row = c / CPR, cc = c % CPR;
@@ -1383,7 +1330,7 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restric
   const int c0 = cg * 8;
   const long plane = (long)M * NC;
   const bool bsum = bs.rep != nullptr;    // DGRAD: BN-backward sums of the producer BN (conv_tap's epilogue)
-  float sh[8], bq[3][8], bm[2][8], bi[2][8];
+  float sh[8], bq[3][8], bm[3][8], bi[3][8];
   bnsum_coeffs(bs, c0, bsum, bm, bi, bq);
 #pragma unroll
   for (int j = 0; j < 8; ++j) sh[j] = (stats && shift) ? shift[c0 + j] : 0.f;
@@ -1868,7 +1815,8 @@ void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const
   if ((add || bs) && !conv_dgrad_fusable(s, wd != nullptr))
     throw std::invalid_argument("conv_dgrad: add / BN sums need the tap path (conv_dgrad_fusable)");
   if (add && acc) throw std::invalid_argument("conv_dgrad: add and accumulate are exclusive");
-  if (bs && (!bs->rep || !bs->z || !bs->mean || !bs->inv || bs->reps < 1 || (bs->zb && (!bs->meanb || !bs->invb))))
+  if (bs && (!bs->rep || !bs->z || !bs->mean || !bs->inv || bs->reps < 1 || (bs->zb && (!bs->meanb || !bs->invb)) ||
+             (bs->msc && (bs->y || bs->msc_ld <= 0))))
     throw std::invalid_argument("conv_dgrad: incomplete BN sums descriptor");
   if (wd != nullptr && s.O % 64 == 0) {   // tap-major path on the dgrad weight image
     TapPhase ph[4];

@@ -249,13 +249,19 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(const bf16* __restrict__ x
   }
 }
 
-// one thread per (input pixel, 8-channel group): gather form, no atomics
+// one thread per (input pixel, 8-channel group): gather form, no atomics.
+// bs (optional): the BatchNorm-backward channel sums of dx's producer BN (fedmi::BnSums, the dense
+// DGRAD epilogue's contract), from the stored bf16 dx; blockDim is a multiple of C/8, so a thread's
+// channel group is fixed and its sums reduce through LDS behind the filter image.
 __global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16* __restrict__ dy, const float* __restrict__ w,
-                                                       bf16* __restrict__ dx, DwGeom g) {
+                                                       bf16* __restrict__ dx, DwGeom g, fedmi::BnSums bs) {
   extern __shared__ float wl[];
   const int VC = g.C >> 3;
   stage_taps(w, wl, g.C, g.R * g.S);
   __syncthreads();
+  const bool bsum = bs.rep != nullptr;
+  float bq[3][8], bm[3][8], bi[3][8];
+  fedmi::bnsum_coeffs(bs, (int)(threadIdx.x % VC) * 8, bsum, bm, bi, bq);
   const long total = (long)g.N * g.H * g.W * VC;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)total; i += gridDim.x * blockDim.x) {
     const uint32_t pix = i / (uint32_t)VC;
@@ -305,6 +311,22 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = (bf16)acc[j];
     *reinterpret_cast<bf16x8v*>(dx + (long)pix * g.C + c0) = o;
+    if (bsum) fedmi::bnsum_acc(bs, (long)pix * g.C + c0, o, bm, bi, bq);
+  }
+  if (!bsum) return;
+  float* red = wl + g.C * g.R * g.S;   // [3][blockDim][8]
+  const int tb = blockDim.x;
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[(q * tb + threadIdx.x) * 8 + j] = bq[q][j];
+  __syncthreads();
+  const int nq = bs.zb ? 3 : 2;
+  for (int e = threadIdx.x; e < nq * g.C; e += tb) {
+    const int q = e / g.C, c = e - q * g.C, grp = c >> 3, j = c & 7;
+    float sum = 0.f;
+    for (int t = grp; t < tb; t += VC) sum += red[(q * tb + t) * 8 + j];
+    unsafeAtomicAdd(bs.rep + ((long)(blockIdx.x % bs.reps) * 3 + q) * g.C + c, (double)sum);
   }
 }
 
@@ -507,11 +529,19 @@ void launch_dw_fwd(hipStream_t st, const DwShape& s, const bf16* x, const float*
                      y, stats, shift, g, isc);
 }
 
-void launch_dw_dgrad(hipStream_t st, const DwShape& s, const bf16* dy, const float* w, bf16* dx) {
+// bs: optional BN-backward sums of dx's producer (see dw_dgrad_kernel); fewer, longer workgroups then
+// (their per-channel fp64 atomics land on 2-3 x C x reps addresses)
+void launch_dw_dgrad(hipStream_t st, const DwShape& s, const bf16* dy, const float* w, bf16* dx,
+                     const BnSums* bs) {
   const DwGeom g = dw_geom(s);
+  if (bs && (!bs->rep || !bs->z || !bs->mean || !bs->inv || bs->reps < 1 || (bs->zb && (!bs->meanb || !bs->invb)) ||
+             (bs->msc && (bs->y || bs->msc_ld <= 0))))
+    throw std::invalid_argument("dw_dgrad: incomplete BN sums descriptor");
   const long items = (long)g.N * g.H * g.W * (g.C / 8);
-  hipLaunchKernelGGL(dw_dgrad_kernel, dim3(blocks_for(items)), dim3(256), g.C * g.R * g.S * sizeof(float), st, dy, w,
-                     dx, g);
+  const int tb = block_threads(g.C);
+  const int nblk = bs ? std::min(blocks_for(items, tb), 1024) : blocks_for(items, tb);
+  const size_t lds = g.C * g.R * g.S * sizeof(float) + (bs ? 3 * tb * 8 * sizeof(float) : 0);
+  hipLaunchKernelGGL(dw_dgrad_kernel, dim3(nblk), dim3(tb), lds, st, dy, w, dx, g, bs ? *bs : BnSums{});
 }
 
 // channel groups per wgrad workgroup (<= 32: >= 8 pixel lanes) and pixel blocks (>= 2 pixels per lane)

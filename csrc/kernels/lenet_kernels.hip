@@ -30,6 +30,8 @@
 // executor (csrc/runtime/lenet_engine.cpp).
 #include <stdexcept>
 
+#include <type_traits>
+
 #include "common.h"
 #include "lenet_layout.h"
 
@@ -1206,25 +1208,33 @@ FEDMI_DEV float bfr(float v) { return (float)(bf16)v; }
 // loads are in flight and the LDS image is cleared -- for the SGD workgroups of step i-1 in the same
 // launch.  Wall-clock bounded like every hand-off (stats->pad = 3, raised by the host).
 FEDMI_DEV void wait_sgd_done(const int* ctr, int need, Stats* stats) {
+  // poll RELAXED and fence once: an acquire load per spin is a cache invalidation per spin (128
+  // workgroups spinning that way invalidated the caches the SGD workgroups were streaming through)
   if (threadIdx.x == 0) {
     const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need) {
-      __builtin_amdgcn_s_sleep(1);
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+      __builtin_amdgcn_s_sleep(2);
       if (wall_clock64() - t0 > 100000000ull) {      // 1 s: never hang the GPU on a broken hand-off
         __hip_atomic_store(&stats->pad, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the SGD workgroups' pk / params stores
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the SGD workgroups' pk / params stores, every wave
 }
+
+// PIPED: the SGD workgroups of the same launch write pk / params (before the hand-off), so they are
+// not restrict there (a restrict read-only argument lets the compiler treat the weights as invariant
+// for the whole kernel and read them ahead of the hand-off)
+template <bool PIPED, typename T>
+using WeightPtr = std::conditional_t<PIPED, const T*, const T* __restrict__>;
 
 template <bool PIPED>
 FEDMI_DEV void sample_step_body(
     unsigned char* smem, int s,
     const uint8_t* __restrict__ images, int sample_base, int nb,
-    const bf16* __restrict__ pk, const float* __restrict__ params,
+    WeightPtr<PIPED, bf16> pk, WeightPtr<PIPED, float> params,
     uint32_t seed, const int* __restrict__ round_ctr, int augment,
     const int* __restrict__ labels,      // labels of this batch (already offset)
     bf16* __restrict__ act2T,            // [F0P][128]
@@ -1996,9 +2006,15 @@ __global__ __launch_bounds__(NT_CONV) void lenet_step_piped(
     __syncthreads();
     if (b < SGD2_GRID) sgd2_block<1>(b, t, wave_id() & 3, lane_id(), red, bsum, c, A);
     if (w == 0 && threadIdx.x == 0 && step_gen) step_gen[0] += 1;
-    __threadfence();
+    // publish (cdna_hip_programming.md Guideline 16): every wave's stores retired, ONE agent release
+    // by lane 0, its own wait, then a relaxed ticket -- not a release fence per wave
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(sgd_done + par, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(sgd_done + par, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     FEDMI_STAMP(3, 1);
     return;
   }

@@ -144,14 +144,17 @@ class _Unit:
               bn_sums: Optional[dict] = None) -> torch.Tensor:
         dz = self.view(self.dz, nb) if dz is None else dz
         if self.depthwise:
-            assert not accumulate and add is None and bn_sums is None
-            return conv.dwconv_dgrad(dz, self.conv.weight, self.in_shape(nb), self.stride, self.pad, out=out)
+            assert not accumulate and add is None
+            return conv.dwconv_dgrad(dz, self.conv.weight, self.in_shape(nb), self.stride, self.pad, out=out,
+                                     bn_sums=bn_sums)
         return conv.conv2d_dgrad(dz, self.wr, self.in_shape(nb), self.stride, self.pad, Cw=self.Cw, out=out, ws=ws,
                                  wd=self.wd, accumulate=accumulate, add=add, bn_sums=bn_sums)
 
-    def dgrad_fusable(self) -> bool:
-        """Whether this conv's DGRAD can take a second incoming grad and its producer BN's backward sums
-        in the epilogue (dense tap path)."""
+    def dgrad_fusable(self, add: bool = False) -> bool:
+        """Whether this conv's DGRAD can take its producer BN's backward sums in the epilogue (dense tap
+        path, or the depthwise kernel) and, ``add``, a second incoming grad (dense tap path only)."""
+        if self.depthwise:
+            return not add
         if self._fusable is None:
             self._fusable = (not self.depthwise and self.wd is not None and
                              conv.dgrad_fusable(self.in_shape(1), self.O, self.R, self.S, self.stride, self.pad,
@@ -522,6 +525,15 @@ class CNNNativeTrainer(LocalTrainer):
         import os
 
         self._fuse_bn_bwd = os.environ.get("FEDMI_CNN_FUSE_BN_BWD", "1") != "0"
+        # a ReLU'd BN inside a block (no residual): the forward stores its scale / shift, and the backward
+        # derives the ReLU mask from z (z * sc + sh > 0) instead of re-reading the materialised y
+        for u in self.units:
+            u.zco = None
+        if self._fuse_bn_bwd and self.preact is None and self.goog is None:
+            for b in self.blocks:
+                for v in b.main[:-1]:
+                    if v.relu and v.bn_rep is not None:
+                        v.zco = torch.empty(2, v.O, device=device)
         self.xin = torch.empty(R, 32, 32, 8, dtype=act_dtype, device=device)
         self.dhead = torch.empty(R * self.head_hw * self.head_hw * self.head_c, dtype=act_dtype, device=device)
         self.pooled = torch.empty(R, self.head_c, device=device)
@@ -635,7 +647,8 @@ class CNNNativeTrainer(LocalTrainer):
             ws = self.wgrad_ws
             for v in b.main[:-1]:
                 v.fwd(h, nb, v.stats if train else None, ws)
-                h = self._bn(v, v.view(v.z, nb), v.view(v.y, nb), train, v.relu)
+                h = self._bn(v, v.view(v.z, nb), v.view(v.y, nb), train, v.relu,
+                             co_out=v.zco if train else None)
             last = b.main[-1]
             last.fwd(h, nb, last.stats if train else None, ws)
             out = b.pre_view(nb)
@@ -661,9 +674,11 @@ class CNNNativeTrainer(LocalTrainer):
                  dbase=dbase, zero=self.bn_chain if train else None)
         return x, hd
 
-    def _sums(self, conv_u: _Unit, u: _Unit, nb: int, y, zb: Optional[_Unit] = None) -> Optional[dict]:
-        """BN-sums descriptor for ``u``'s BN, taken by ``conv_u``'s DGRAD epilogue (None: not fusable)."""
-        if not (self._fuse_bn_bwd and u.bn_rep is not None and u.bn_reps > 0 and conv_u.dgrad_fusable()):
+    def _sums(self, conv_u: _Unit, u: _Unit, nb: int, y, zb: Optional[_Unit] = None,
+              add: bool = False) -> Optional[dict]:
+        """BN-sums descriptor for ``u``'s BN, taken by ``conv_u``'s DGRAD epilogue (None: not fusable).
+        ``add``: the DGRAD must also add a second incoming grad (a shortcut's)."""
+        if not (self._fuse_bn_bwd and u.bn_rep is not None and u.bn_reps > 0 and conv_u.dgrad_fusable(add)):
             return None
         d = dict(rep=u.bn_rep, reps=u.bn_reps, z=u.view(u.z, nb), y=y, mean=u.smean, inv=u.sinv)
         if zb is not None:
@@ -714,14 +729,19 @@ class CNNNativeTrainer(LocalTrainer):
                     w = b.main[j - 1]
                     wy = w.view(w.y, nb) if w.relu else None
                     bs = self._sums(v, w, nb, wy)
+                    msc = None
+                    if bs is not None and w.zco is not None:   # ReLU mask from z: y is not re-read
+                        bs.update(y=None, msc=w.zco)
+                        wy, msc = None, w.zco
                     v.dgrad(nb, w.view(w.dy, nb), ws, bn_sums=bs)
-                    self._bn_bwd(w, nb, w.view(w.dy, nb), None, wy, presummed=bs is not None)
+                    self._bn_bwd(w, nb, w.view(w.dy, nb), None, wy, presummed=bs is not None, mask_bn=msc)
                 elif not b.first:
                     din_a = b.in_view(b.din_a, nb)
                     bs = None
                     if not (prev.pool or getattr(prev, "defer", False)):
                         pl = prev.main[-1]
-                        bs = self._sums(v, pl, nb, prev.pre_view(nb) if prev.out_relu else None, zb=prev.proj)
+                        bs = self._sums(v, pl, nb, prev.pre_view(nb) if prev.out_relu else None, zb=prev.proj,
+                                        add=din_b is not None)
                     if bs is not None:
                         # the shortcut's grad first, then conv1's DGRAD adds it and takes the previous
                         # block's BN-backward sums from the complete grad
@@ -729,7 +749,7 @@ class CNNNativeTrainer(LocalTrainer):
                             b.proj.wgrad(a_in, nb, ws)
                             b.proj.dgrad(nb, din_b, ws)
                             proj_done = True
-                        v.dgrad(nb, din_a, ws, add=din_b, bn_sums=bs)
+                        v.dgrad(nb, din_a, ws, add=din_b, bn_sums=bs)   # add=None: no shortcut
                         dya, dyb, pres = din_a, None, True
                     else:
                         v.dgrad(nb, din_a, ws)

@@ -129,13 +129,17 @@ def maxpool2_bwd(x: torch.Tensor, dy: torch.Tensor, out: Optional[torch.Tensor] 
 
 def bn_apply(z: torch.Tensor, a: BNParams, y: torch.Tensor, train: bool, relu: bool,
              z2: Optional[torch.Tensor] = None, b: Optional[BNParams] = None, res: Optional[torch.Tensor] = None,
-             eps: float = 1e-5, momentum: float = 0.1) -> torch.Tensor:
-    """y = act(BN_a(z) [+ res | + BN_b(z2)]) over [M, C] rows; train mode commits running stats."""
+             eps: float = 1e-5, momentum: float = 0.1, co_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = act(BN_a(z) [+ res | + BN_b(z2)]) over [M, C] rows; train mode commits running stats.
+    ``co_out``: float32 [2, C] <- BN_a's scale / shift as applied (a backward that derives the ReLU mask
+    from z instead of re-reading y)."""
     C = z.shape[-1]
     M = z.numel() // C
+    if co_out is not None and (co_out.dtype != torch.float32 or co_out.numel() < 2 * C):
+        raise ValueError("bn_apply: co_out must be float32 [2, C]")
     native.require().bn_apply(native.stream_handle(z.device), z.data_ptr(), a.ptrs(), _p(z2),
                               b.ptrs() if b is not None else None, _p(res), y.data_ptr(), M, C, eps, momentum,
-                              int(train), int(relu), row_stride(y))
+                              int(train), int(relu), row_stride(y), _p(co_out))
     return y
 
 

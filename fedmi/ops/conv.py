@@ -168,7 +168,8 @@ def conv2d_dgrad(dy: torch.Tensor, wrsc: torch.Tensor, x_shape, stride: int, pad
     ``accumulate``: out += dx (one branch's share of a multi-branch block's input gradient).
     ``add``: out = dx + add (another incoming grad of the same tensor, e.g. the shortcut's).
     ``bn_sums`` (dict rep, reps, z, y, mean, inv [, zb, meanb, invb: a projection-shortcut BN that shares
-    the incoming grad]): the BatchNorm that produced this conv's input gets
+    the incoming grad] [, msc with y=None: the ReLU mask is z * msc[0] + msc[1] > 0]): the BatchNorm that
+    produced this conv's input gets
     its backward channel sums from the epilogue (chained replica layout, :func:`cnn.bn_bwd` presummed)
     -- ``add`` / ``bn_sums`` need :func:`dgrad_fusable`."""
     _check(dy, torch.bfloat16, "conv2d_dgrad.dy")
@@ -184,25 +185,38 @@ def conv2d_dgrad(dy: torch.Tensor, wrsc: torch.Tensor, x_shape, stride: int, pad
         _check(wd, torch.bfloat16, "conv2d_dgrad.wd")
         if wd.numel() < O * R * S * C:
             raise ValueError("conv2d_dgrad: dgrad image too small")
-    bs = None
-    if bn_sums is not None:
-        z, y = bn_sums["z"], bn_sums.get("y")
-        if z.shape != out.shape or (y is not None and y.shape != out.shape) or not z.is_contiguous():
-            raise ValueError("conv2d_dgrad: BN sums need compact z / y of the output's shape")
-        zb = bn_sums.get("zb")
-        if zb is not None and zb.shape != out.shape:
-            raise ValueError("conv2d_dgrad: BN sums zb must have the output's shape")
-        bs = dict(rep=bn_sums["rep"].data_ptr(), reps=int(bn_sums["reps"]), z=z.data_ptr(),
-                  y=y.data_ptr() if y is not None else 0, mean=bn_sums["mean"].data_ptr(),
-                  inv=bn_sums["inv"].data_ptr())
-        if zb is not None:
-            bs.update(zb=zb.data_ptr(), meanb=bn_sums["meanb"].data_ptr(), invb=bn_sums["invb"].data_ptr())
+    bs = _bn_sums_desc(bn_sums, out)
     if add is not None and add.shape != out.shape:
         raise ValueError("conv2d_dgrad: add must have the output's shape")
     native.require().conv_dgrad(native.stream_handle(dy.device), shp, dy.data_ptr(), wrsc.data_ptr(), out.data_ptr(),
                                 *_ws_args(ws), wd.data_ptr() if wd is not None else 0, int(accumulate),
                                 add.data_ptr() if add is not None else 0, bs)
     return out
+
+
+def _bn_sums_desc(bn_sums: Optional[dict], out: torch.Tensor) -> Optional[dict]:
+    """Device-pointer dict of a BN-sums descriptor (rep, reps, z, y[, zb, meanb, invb], mean, inv) whose
+    tensors are compact and shaped like the DGRAD output ``out``."""
+    if bn_sums is None:
+        return None
+    z, y, zb = bn_sums["z"], bn_sums.get("y"), bn_sums.get("zb")
+    for t in (z, y, zb):
+        if t is not None and (t.shape != out.shape or not t.is_contiguous() or t.dtype != torch.bfloat16):
+            raise ValueError("dgrad: BN sums need compact bf16 z / y / zb of the output's shape")
+    C = out.shape[-1]
+    rep = bn_sums["rep"]
+    if rep.dtype != torch.float64 or rep.numel() < 3 * C * int(bn_sums["reps"]):
+        raise ValueError("dgrad: BN sums replicas must be fp64 [reps][3][C]")
+    bs = dict(rep=rep.data_ptr(), reps=int(bn_sums["reps"]), z=z.data_ptr(), y=y.data_ptr() if y is not None else 0,
+              mean=bn_sums["mean"].data_ptr(), inv=bn_sums["inv"].data_ptr())
+    if zb is not None:
+        bs.update(zb=zb.data_ptr(), meanb=bn_sums["meanb"].data_ptr(), invb=bn_sums["invb"].data_ptr())
+    msc = bn_sums.get("msc")
+    if msc is not None:   # ReLU mask from z: [2][C] scale / shift as the forward applied them (bn_apply co_out)
+        if y is not None or msc.dtype != torch.float32 or msc.numel() < 2 * C:
+            raise ValueError("dgrad: BN sums msc needs y=None and a float32 [2][C] buffer")
+        bs.update(msc=msc.data_ptr(), msc_ld=C)
+    return bs
 
 
 def dgrad_fusable(x_shape, O: int, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None,
@@ -292,12 +306,14 @@ def dwconv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats: O
 
 
 def dwconv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, bn_sums: Optional[dict] = None) -> torch.Tensor:
+    """``bn_sums``: as :func:`conv2d_dgrad` (the producer BN's backward sums from the stored dx)."""
     _check(dy, torch.bfloat16, "dwconv_dgrad.dy")
     shp = _dw_shape(x_shape, w.shape[2], stride, pad)
     if out is None:
         out = torch.empty(*x_shape, dtype=torch.bfloat16, device=dy.device)
-    native.require().dw_dgrad(native.stream_handle(dy.device), shp, dy.data_ptr(), w.data_ptr(), out.data_ptr())
+    native.require().dw_dgrad(native.stream_handle(dy.device), shp, dy.data_ptr(), w.data_ptr(), out.data_ptr(),
+                              _bn_sums_desc(bn_sums, out))
     return out
 
 

@@ -168,7 +168,7 @@ def dwconv_fwd(x, w, stride, pad, stats=None, out=None, shift=None, in_bn=None):
 
 
 @torch.no_grad()
-def dwconv_dgrad(dy, w, x_shape, stride, pad, out=None):
+def dwconv_dgrad(dy, w, x_shape, stride, pad, out=None, bn_sums=None):
     N, H, W, C = x_shape
     dx = torch.nn.grad.conv2d_input((N, C, H, W), w.float(), _nchw(dy), stride=stride, padding=pad, groups=C)
     if out is None:
@@ -246,10 +246,13 @@ def bn_coeff(z_rows, C, a, co, train, eps=1e-5, momentum=0.1):
 
 
 @torch.no_grad()
-def bn_apply(z, a, y, train, relu, z2=None, b=None, res=None, eps=1e-5, momentum=0.1):
+def bn_apply(z, a, y, train, relu, z2=None, b=None, res=None, eps=1e-5, momentum=0.1, co_out=None):
     C = z.shape[-1]
     M = z.numel() // C
     sc, sh = _coeffs(a, M, train, eps, momentum)
+    if co_out is not None:
+        co_out[0].copy_(sc)
+        co_out[1].copy_(sh)
     v = z.float().reshape(M, C) * sc + sh
     if b is not None:
         sc2, sh2 = _coeffs(b, M, train, eps, momentum)
@@ -304,8 +307,8 @@ def maxpool2_bwd(x, dy, out=None):
 @torch.no_grad()
 def bn_bwd(dya, za, a, dgamma_a, dbeta_a, dza, red, dyb=None, y=None, zb=None, b=None, dgamma_b=None,
            dbeta_b=None, dzb=None, gout=None, ws=None, dadd=None, chained=False, mask_bn=None, presummed=False):
-    if presummed and (dyb is not None or mask_bn is not None or not chained):
-        raise ValueError("bn_bwd: presummed covers one incoming grad and a y mask, chained replicas")
+    if presummed and (dyb is not None or not chained):
+        raise ValueError("bn_bwd: presummed covers one incoming grad, chained replicas")
     C = za.shape[-1]
     M = za.numel() // C
     g = dya.float().reshape(M, C)

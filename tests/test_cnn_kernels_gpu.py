@@ -748,8 +748,9 @@ FUSE_SHAPES = [(8, 16, 16, 64, 64, 3, 1, 1), (128, 32, 32, 64, 64, 3, 1, 1), (12
 
 
 @pytest.mark.parametrize("shape", FUSE_SHAPES, ids=[str(s) for s in FUSE_SHAPES])
-@pytest.mark.parametrize("relu,proj", [(True, False), (False, True)])
-def test_conv_dgrad_fused_bn_sums(gpu_device, shape, relu, proj):
+@pytest.mark.parametrize("relu,proj,zmask", [(True, False, False), (False, True, False), (False, False, True)],
+                         ids=["ymask", "proj", "zmask"])
+def test_conv_dgrad_fused_bn_sums(gpu_device, shape, relu, proj, zmask):
     N, H, W, Cw, O, R, st, pad = shape
     x, w, wb, xn = _make(shape, gpu_device, seed=31)
     C = xn.shape[-1]
@@ -773,6 +774,9 @@ def test_conv_dgrad_fused_bn_sums(gpu_device, shape, relu, proj):
     bs = dict(rep=rep, reps=reps, z=z, y=y, mean=mean, inv=inv)
     if proj:
         bs.update(zb=zb, meanb=meanb, invb=invb)
+    msc = torch.stack([torch.rand(C, device=gpu_device) + 0.5, torch.randn(C, device=gpu_device) * 0.5])
+    if zmask:   # ReLU mask derived from z with the forward's scale / shift (y never re-read)
+        bs.update(msc=msc)
     plain = conv.conv2d_dgrad(dyn, wpk, xn.shape, st, pad, Cw=Cw, ws=wsp, wd=wd)
     out = torch.full_like(plain, float("nan"))
     conv.conv2d_dgrad(dyn, wpk, xn.shape, st, pad, Cw=Cw, out=out, ws=wsp, wd=wd, add=add, bn_sums=bs)
@@ -784,6 +788,9 @@ def test_conv_dgrad_fused_bn_sums(gpu_device, shape, relu, proj):
     gm = out.double().reshape(-1, C)
     if relu:
         gm = torch.where(y.double().reshape(-1, C) > 0, gm, torch.zeros_like(gm))
+    if zmask:
+        m = torch.addcmul(msc[1], z.float().reshape(-1, C), msc[0]) > 0
+        gm = torch.where(m, gm, torch.zeros_like(gm))
     s0 = gm.sum(0)
     s1 = (gm * ((z.double().reshape(-1, C) - mean.double()) * inv.double())).sum(0)
     got = rep.sum(0)
@@ -824,3 +831,30 @@ def test_bn_bwd_presummed_matches_reduce(gpu_device):
     (dz0, dg0, db0), (dz1, dg1, db1) = outs
     assert _rel(dg1, dg0) < 1e-5 and _rel(db1, db0) < 1e-5
     assert _rel(dz1, dz0) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(16, 16, 16, 64, 1), (128, 32, 32, 64, 1), (32, 8, 8, 96, 2), (8, 4, 4, 1024, 1)],
+                         ids=["c64", "c64_b128", "c96_s2", "c1024"])
+def test_dwconv_dgrad_fused_bn_sums(gpu_device, shape):
+    """Depthwise DGRAD with the producer BN's backward sums (MobileNet block boundaries)."""
+    N, H, W, C, st = shape
+    g = torch.Generator(device="cpu").manual_seed(13)
+    P = (H + 2 - 3) // st + 1
+    dy = torch.randn(N, P, P, C, generator=g).to(gpu_device).bfloat16()
+    w = (torch.randn(C, 1, 3, 3, generator=g) / 3).to(gpu_device)
+    z = torch.randn(N, H, W, C, generator=g).to(gpu_device).bfloat16()
+    y = torch.relu(torch.randn(N, H, W, C, generator=g)).to(gpu_device).bfloat16()
+    mean, inv = torch.randn(C, device=gpu_device) * 0.1, torch.rand(C, device=gpu_device) + 0.5
+    plain = conv.dwconv_dgrad(dy, w, (N, H, W, C), st, 1)
+    rep = torch.zeros(4, 3, C, dtype=torch.float64, device=gpu_device)
+    out = conv.dwconv_dgrad(dy, w, (N, H, W, C), st, 1, bn_sums=dict(rep=rep, reps=4, z=z, y=y, mean=mean, inv=inv))
+    torch.cuda.synchronize()
+    assert torch.equal(out, plain)
+    gm = out.double().reshape(-1, C)
+    gm = torch.where(y.double().reshape(-1, C) > 0, gm, torch.zeros_like(gm))
+    s0 = gm.sum(0)
+    s1 = (gm * ((z.double().reshape(-1, C) - mean.double()) * inv.double())).sum(0)
+    got = rep.sum(0)
+    scale = gm.abs().sum(0) + 1.0
+    assert float(((got[0] - s0).abs() / scale).max()) < 1e-5
+    assert float(((got[1] - s1).abs() / (scale * 4)).max()) < 1e-5
