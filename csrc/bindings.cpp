@@ -86,12 +86,6 @@ static LeNetBuffers buffers_from(const py::dict& d) {
   b.step_gen = P<int>(get("step_gen"));
   b.bwd_flags = P<int>(get("bwd_flags"));
   b.bwd_gen = P<int>(get("bwd_gen"));
-  b.act2T_b = P<bf16>(get("act2T_b"));
-  b.h1_b = P<bf16>(get("h1_b"));
-  b.dact2_b = P<float>(get("dact2_b"));
-  b.dZ1T_b = P<bf16>(get("dZ1T_b"));
-  b.conv_slab_b = P<float>(get("conv_slab_b"));
-  b.sgd_done = P<int>(get("sgd_done"));
   return b;
 }
 
@@ -161,8 +155,6 @@ static void fedmi_bind(py::module_& m) {
       .def("set_fuse_sgd", &LeNetEngine::set_fuse_sgd)
       .def("fuse_sgd", &LeNetEngine::fuse_sgd)
       .def("set_sample_path", &LeNetEngine::set_sample_path)
-      .def("set_pipeline", &LeNetEngine::set_pipeline)
-      .def_property_readonly("pipeline", &LeNetEngine::pipeline)
       .def("sample_path", &LeNetEngine::sample_path);
 
   // ---- raw LeNet kernels (numerics tests drive them one by one) -------------

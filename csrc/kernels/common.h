@@ -99,6 +99,20 @@ struct BnSums {
 
 // one 8-channel group of a DGRAD output row into the BN-backward sums (bm/bi: [2][8] mean / inv of
 // the two branches; q: [3][8])
+// the same on operands already in registers (an epilogue that prefetched its rows' z / y / zb)
+FEDMI_DEV void bnsum_acc_v(const BnSums& bs, const bf16x8& t, const bf16x8& z, const bf16x8& y, const bf16x8& zb,
+                           const float (*bm)[8], const float (*bi)[8], float (*q)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float g = (float)t[j];
+    if (bs.y && !((float)y[j] > 0.f)) g = 0.f;
+    else if (!bs.y && bs.msc && !((float)z[j] * bm[2][j] + bi[2][j] > 0.f)) g = 0.f;
+    q[0][j] += g;
+    q[1][j] += g * ((float)z[j] - bm[0][j]) * bi[0][j];
+    if (bs.zb) q[2][j] += g * ((float)zb[j] - bm[1][j]) * bi[1][j];
+  }
+}
+
 FEDMI_DEV void bnsum_acc(const BnSums& bs, long idx, const bf16x8& t, const float (*bm)[8], const float (*bi)[8],
                          float (*q)[8]) {   // bm / bi: [3][8] (see bnsum_coeffs)
   const bf16x8 z = *reinterpret_cast<const bf16x8*>(bs.z + idx);

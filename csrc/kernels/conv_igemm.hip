@@ -625,24 +625,52 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
     if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, (double)tsum);
   }
   constexpr int CPR = BN / 8;
+  constexpr int RPT = BM * CPR / 256;      // output rows (8-channel vectors) per thread
   // DGRAD: BN-backward sums of the producer BN (each thread keeps one 8-channel group: 256 % CPR == 0)
   const bool bsum = bs.rep != nullptr;
   float bq[3][8], bm[3][8], bi[3][8];
   if (bsum) bnsum_coeffs(bs, n0 + (tid % CPR) * 8, n0 + (tid % CPR) * 8 < g.O, bm, bi, bq);
-  for (int c = tid; c < BM * CPR; c += 256) {
-    const int row = c / CPR, cc = c % CPR;
+  // every global operand of the epilogue (residual / second grad, z / y / zb of the BN sums) in flight
+  // at once: one memory latency per tile instead of one per row (conditions hoisted out of the loads;
+  // invalid rows read row 0)
+  long pidx[RPT];
+  bool pok[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int c = tid + k * 256, row = c / CPR, cc = c % CPR;
     const int m = m0 + row, col = n0 + cc * 8;
-    if (m < g.M && col < g.O) {
-      const long orow = map_row(rmap, m);
+    pok[k] = m < g.M && col < g.O;
+    pidx[k] = pok[k] ? map_row(rmap, m) * g.O + col : 0;
+  }
+  bf16x8 pr[RPT], pz[RPT], py[RPT], pzb[RPT];
+  if (res != nullptr) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) pr[k] = *reinterpret_cast<const bf16x8*>(res + pidx[k]);
+  }
+  if (bsum) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) pz[k] = *reinterpret_cast<const bf16x8*>(bs.z + pidx[k]);
+    if (bs.y) {
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) py[k] = *reinterpret_cast<const bf16x8*>(bs.y + pidx[k]);
+    }
+    if (bs.zb) {
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) pzb[k] = *reinterpret_cast<const bf16x8*>(bs.zb + pidx[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int c = tid + k * 256, row = c / CPR, cc = c % CPR;
+    if (pok[k]) {
       bf16x8 t = *reinterpret_cast<const bf16x8*>(ct + row * CT_LD + cc * 8);
       if (res != nullptr) {   // fused residual add (pre-activation fwd) / second incoming grad (DGRAD)
-        const bf16x8 r = *reinterpret_cast<const bf16x8*>(res + orow * g.O + col);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) t[j] = (bf16)((float)t[j] + (float)r[j]);
+        for (int j = 0; j < 8; ++j) t[j] = (bf16)((float)t[j] + (float)pr[k][j]);
         if (stats != nullptr) *reinterpret_cast<bf16x8*>(ct + row * CT_LD + cc * 8) = t;
       }
-      *reinterpret_cast<bf16x8*>(out + orow * g.O + col) = t;
-      if (bsum) bnsum_acc(bs, orow * g.O + col, t, bm, bi, bq);
+      *reinterpret_cast<bf16x8*>(out + pidx[k]) = t;
+      if (bsum) bnsum_acc_v(bs, t, pz[k], py[k], pzb[k], bm, bi, bq);
     }
   }
   if (bsum) {
@@ -1335,35 +1363,77 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restric
 #pragma unroll
   for (int j = 0; j < 8; ++j) sh[j] = (stats && shift) ? shift[c0 + j] : 0.f;
   const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
-  for (int m = rb + r0; m < re; m += rstep) {
-    const float* p = ws + (long)m * NC + c0;
-    float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  // U rows per thread per pass, every load of the pass issued before the first use (the partials of all
+  // splits, the residual / second grad, the BN-sums operands): one memory latency per U rows
+  constexpr int U = 4;
+  for (int m0 = rb + r0; m0 < re; m0 += U * rstep) {
+    float v[U][8];
+    bf16x8 rr[U], pz[U], py[U], pzb[U];
+    long orow[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int m = m0 + u * rstep;
+      ok[u] = m < re;
+      const int mm = ok[u] ? m : rb + r0;
+      orow[u] = map_row(rmap, mm);
+      const float* p = ws + (long)mm * NC + c0;
+      const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+      v[u][0] = a.x; v[u][1] = a.y; v[u][2] = a.z; v[u][3] = a.w;
+      v[u][4] = b.x; v[u][5] = b.y; v[u][6] = b.z; v[u][7] = b.w;
+    }
     for (int z = 1; z < splits; ++z) {
-      const float4 ua = *reinterpret_cast<const float4*>(p + z * plane);
-      const float4 ub = *reinterpret_cast<const float4*>(p + z * plane + 4);
-      a.x += ua.x; a.y += ua.y; a.z += ua.z; a.w += ua.w;
-      b.x += ub.x; b.y += ub.y; b.z += ub.z; b.w += ub.w;
-    }
-    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    const long orow = map_row(rmap, m);
-    if (res != nullptr) {
-      const bf16x8 r = *reinterpret_cast<const bf16x8*>(res + orow * NC + c0);
+      float4 ua[U], ub[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += (float)r[j];
-    }
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
-    *reinterpret_cast<bf16x8*>(out + orow * NC + c0) = o;
-    if (stats) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = (float)o[j] - sh[j];
-        bq[0][j] += d;
-        bq[1][j] += d * d;
+      for (int u = 0; u < U; ++u) {
+        const int mm = ok[u] ? m0 + u * rstep : rb + r0;
+        const float* p = ws + (long)mm * NC + c0 + z * plane;
+        ua[u] = *reinterpret_cast<const float4*>(p);
+        ub[u] = *reinterpret_cast<const float4*>(p + 4);
       }
-    } else if (bsum) {
-      bnsum_acc(bs, orow * NC + c0, o, bm, bi, bq);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u][0] += ua[u].x; v[u][1] += ua[u].y; v[u][2] += ua[u].z; v[u][3] += ua[u].w;
+        v[u][4] += ub[u].x; v[u][5] += ub[u].y; v[u][6] += ub[u].z; v[u][7] += ub[u].w;
+      }
+    }
+    if (res != nullptr) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) rr[u] = *reinterpret_cast<const bf16x8*>(res + orow[u] * NC + c0);
+    }
+    if (bsum) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) pz[u] = *reinterpret_cast<const bf16x8*>(bs.z + orow[u] * NC + c0);
+      if (bs.y) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) py[u] = *reinterpret_cast<const bf16x8*>(bs.y + orow[u] * NC + c0);
+      }
+      if (bs.zb) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) pzb[u] = *reinterpret_cast<const bf16x8*>(bs.zb + orow[u] * NC + c0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      if (res != nullptr) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[u][j] += (float)rr[u][j];
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)v[u][j];
+      *reinterpret_cast<bf16x8*>(out + orow[u] * NC + c0) = o;
+      if (stats) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = (float)o[j] - sh[j];
+          bq[0][j] += d;
+          bq[1][j] += d * d;
+        }
+      } else if (bsum) {
+        bnsum_acc_v(bs, o, pz[u], py[u], pzb[u], bm, bi, bq);
+      }
     }
   }
   if (!stats && !bsum) return;

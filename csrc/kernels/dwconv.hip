@@ -539,7 +539,7 @@ void launch_dw_dgrad(hipStream_t st, const DwShape& s, const bf16* dy, const flo
     throw std::invalid_argument("dw_dgrad: incomplete BN sums descriptor");
   const long items = (long)g.N * g.H * g.W * (g.C / 8);
   const int tb = block_threads(g.C);
-  const int nblk = bs ? std::min(blocks_for(items, tb), 1024) : blocks_for(items, tb);
+  const int nblk = bs ? std::min(blocks_for(items, tb), 2048) : blocks_for(items, tb);
   const size_t lds = g.C * g.R * g.S * sizeof(float) + (bs ? 3 * tb * 8 * sizeof(float) : 0);
   hipLaunchKernelGGL(dw_dgrad_kernel, dim3(nblk), dim3(tb), lds, st, dy, w, dx, g, bs ? *bs : BnSums{});
 }

@@ -30,8 +30,6 @@
 // executor (csrc/runtime/lenet_engine.cpp).
 #include <stdexcept>
 
-#include <type_traits>
-
 #include "common.h"
 #include "lenet_layout.h"
 
@@ -1204,46 +1202,19 @@ FEDMI_DEV float sum8lanes(float v) {   // over the 8 consecutive lanes of a grou
 }
 FEDMI_DEV float bfr(float v) { return (float)(bf16)v; }
 
-// Pipelined epochs (lenet_step_piped): the sample workgroups of step i wait here -- after their image
-// loads are in flight and the LDS image is cleared -- for the SGD workgroups of step i-1 in the same
-// launch.  Wall-clock bounded like every hand-off (stats->pad = 3, raised by the host).
-FEDMI_DEV void wait_sgd_done(const int* ctr, int need, Stats* stats) {
-  // poll RELAXED and fence once: an acquire load per spin is a cache invalidation per spin (128
-  // workgroups spinning that way invalidated the caches the SGD workgroups were streaming through)
-  if (threadIdx.x == 0) {
-    const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-      __builtin_amdgcn_s_sleep(2);
-      if (wall_clock64() - t0 > 100000000ull) {      // 1 s: never hang the GPU on a broken hand-off
-        __hip_atomic_store(&stats->pad, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the SGD workgroups' pk / params stores
-  }
-  __syncthreads();
-}
-
-// PIPED: the SGD workgroups of the same launch write pk / params (before the hand-off), so they are
-// not restrict there (a restrict read-only argument lets the compiler treat the weights as invariant
-// for the whole kernel and read them ahead of the hand-off)
-template <bool PIPED, typename T>
-using WeightPtr = std::conditional_t<PIPED, const T*, const T* __restrict__>;
-
-template <bool PIPED>
-FEDMI_DEV void sample_step_body(
-    unsigned char* smem, int s,
+__global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
     const uint8_t* __restrict__ images, int sample_base, int nb,
-    WeightPtr<PIPED, bf16> pk, WeightPtr<PIPED, float> params,
+    const bf16* __restrict__ pk, const float* __restrict__ params,
     uint32_t seed, const int* __restrict__ round_ctr, int augment,
     const int* __restrict__ labels,      // labels of this batch (already offset)
     bf16* __restrict__ act2T,            // [F0P][128]
     bf16* __restrict__ h1T,              // [128][128]
     unsigned char* __restrict__ aux,     // AUX_* side buffers
     bf16* __restrict__ dZ1T,             // [128][128]
-    float* __restrict__ conv_slab,       // [nb][CS]
-    const int* sgd_done, int sgd_need, Stats* stats)   // PIPED: the previous step's SGD hand-off
+    float* __restrict__ conv_slab)       // [nb][CS]
 {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[S_END];
+  const int s = blockIdx.x;
   if (s >= nb) return;
   [[maybe_unused]] const int stamp_wg = s;
   const int gidx = sample_base + s;
@@ -1283,44 +1254,21 @@ FEDMI_DEV void sample_step_body(
     const size_t img_sample = (size_t)gidx;
     constexpr int lim = E4;
 #endif
-    if constexpr (PIPED) {
-      // the image and the augmentation draw do not depend on the weights: in flight while the
-      // previous step's SGD finishes; the weight chunks are read after the hand-off
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int e = tid + u * NT_CONV;
-        if (e < E1) v[u] = reinterpret_cast<const uint4*>(images + img_sample * IMG_BYTES)[e];
-      }
-      a = aug_params(augment, seed, round_ctr, gidx);
-      zero_lds(xcl, 36 * 40 * 4 * 2);
-      wait_sgd_done(sgd_done, sgd_need, stats);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int e = tid + u * NT_CONV;
-        if (e < E1 || e >= lim) {}
-        else if (e < E2) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2DG)[e - E1];
-        else if (e < E3) v[u] = reinterpret_cast<const uint4*>(pk + PK_W1C)[e - E2];
-        else if (e < E4) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2C)[e - E3];
-      }
-      bias1 = n16 < C1 ? params[P_C1B + n16] : 0.f;
-      bias2 = params[P_C2B + n16];
-    } else {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int e = tid + u * NT_CONV;
-        if (e < E1) v[u] = reinterpret_cast<const uint4*>(images + img_sample * IMG_BYTES)[e];
-        else if (e >= lim) {}
-        else if (e < E2) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2DG)[e - E1];
-        else if (e < E3) v[u] = reinterpret_cast<const uint4*>(pk + PK_W1C)[e - E2];
-        else if (e < E4) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2C)[e - E3];
-      }
-      // the other global reads of the kernel's start go out in the same wave of requests (one
-      // memory latency for the whole stage instead of one per dependent group)
-      bias1 = n16 < C1 ? params[P_C1B + n16] : 0.f;
-      bias2 = params[P_C2B + n16];
-      a = aug_params(augment, seed, round_ctr, gidx);
-      zero_lds(xcl, 36 * 40 * 4 * 2);
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * NT_CONV;
+      if (e < E1) v[u] = reinterpret_cast<const uint4*>(images + img_sample * IMG_BYTES)[e];
+      else if (e >= lim) {}
+      else if (e < E2) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2DG)[e - E1];
+      else if (e < E3) v[u] = reinterpret_cast<const uint4*>(pk + PK_W1C)[e - E2];
+      else if (e < E4) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2C)[e - E3];
     }
+    // the other global reads of the kernel's start go out in the same wave of requests (one
+    // memory latency for the whole stage instead of one per dependent group)
+    bias1 = n16 < C1 ? params[P_C1B + n16] : 0.f;
+    bias2 = params[P_C2B + n16];
+    a = aug_params(augment, seed, round_ctr, gidx);
+    zero_lds(xcl, 36 * 40 * 4 * 2);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int e = tid + u * NT_CONV;
@@ -1605,23 +1553,6 @@ FEDMI_DEV void sample_step_body(
   bwd_main<false>(L, conv_slab + (size_t)s * CS, nullptr, s, 0, 2, stamp_wg);
 }
 
-__global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
-    const uint8_t* __restrict__ images, int sample_base, int nb,
-    const bf16* __restrict__ pk, const float* __restrict__ params,
-    uint32_t seed, const int* __restrict__ round_ctr, int augment, const int* __restrict__ labels,
-    bf16* __restrict__ act2T, bf16* __restrict__ h1T, unsigned char* __restrict__ aux, bf16* __restrict__ dZ1T,
-    float* __restrict__ conv_slab, int* __restrict__ sgd_done)
-{
-  __shared__ __attribute__((aligned(16))) unsigned char smem[S_END];
-  // first step of a pipelined epoch: arm both hand-off counters for the launches that follow
-  if (sgd_done != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
-    sgd_done[0] = 0;
-    sgd_done[1] = 0;
-  }
-  sample_step_body<false>(smem, blockIdx.x, images, sample_base, nb, pk, params, seed, round_ctr, augment, labels,
-                          act2T, h1T, aux, dZ1T, conv_slab, nullptr, 0, nullptr);
-}
-
 // ---------------------------------------------------------------------------
 // Packing: fp32 master -> bf16 MFMA operand images.
 // ---------------------------------------------------------------------------
@@ -1784,166 +1715,6 @@ constexpr int SGD2_ND = (6 + 3) / 4;         // fc3.weight: 6 tiles
 constexpr int SGD2_NE = 4;                   // FC biases: 64 per block x 4 sample groups
 constexpr int SGD2_GRID = SGD_NA + SGD2_NB + SGD2_NC + SGD2_ND + SGD2_NE + 1;   // + loss/accuracy block
 
-// One 256-thread sgd2 block 'b' (4 waves), in two phases around ONE workgroup barrier, so that the
-// stand-alone kernel (one block per workgroup) and the pipelined step kernel (four blocks per
-// 1024-thread workgroup, lenet_step_piped) run the same code in the same summation order.
-struct Sgd2Args {
-  float* params;
-  float* mom;
-  bf16* pk;
-  const float* conv_slab;
-  int nb;
-  const bf16* act2T;
-  const bf16* h1T;
-  const unsigned char* aux;
-  const bf16* dZ1T;
-  float lr, momentum, wd;
-  Stats* stats;
-};
-
-template <int PH>
-FEDMI_DEV float2 sgd2_block(int b, int tid, int wave, int lane, float (*red)[17], float (*bsum)[64], float2 carry,
-                            const Sgd2Args& A) {
-  float* __restrict__ params = A.params;
-  float* __restrict__ mom = A.mom;
-  bf16* __restrict__ pk = A.pk;
-  const int nb = A.nb;
-  const float lr = A.lr, momentum = A.momentum, wd = A.wd;
-  const int n16 = lane & 15, rq = (lane >> 4) * 4;
-  if (b < SGD_NA) {                                   // conv params: K4's slab combine
-    const int pl = tid & 15, g = tid >> 4;
-    const int i = b * 16 + pl;
-    if constexpr (PH == 0) {
-      float p = 0.f, m = 0.f;
-      if (g == 0 && i < CS) { p = params[i]; m = mom[i]; }
-      float sum = 0.f;
-      if (i < CS) {
-        float v[MAX_TRAIN_BATCH / 16];
-#pragma unroll
-        for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) {
-          const int q = g + 16 * u;
-          v[u] = q < nb ? A.conv_slab[(size_t)q * CS + i] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) sum += v[u];
-      }
-      red[g][pl] = sum;
-      return make_float2(p, m);
-    } else {
-      if (g == 0 && i < CS) {
-        float tot = 0.f;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) tot += red[q][pl];
-        sgd_apply(i, tot, carry.x, carry.y, params, mom, pk, lr, momentum, wd);
-      }
-      return carry;
-    }
-  } else if (b < SGD_NA + SGD2_NB + SGD2_NC + SGD2_ND) {   // FC weight tiles: all in phase 0
-    if constexpr (PH == 0) {
-      if (b < SGD_NA + SGD2_NB) {                     // fc1.weight [120][400]: 8 x 25 tiles
-        const int t = (b - SGD_NA) * 4 + wave;
-        if (t < 200) {
-          const int nt = t / 25, ft = t - nt * 25;
-          int idx[4];
-          float p[4], m[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = nt * 16 + rq + r, f = ft * 16 + n16;
-            idx[r] = n < F1 ? P_F1W + n * F0 + f : -1;
-          }
-          const f32x4 acc = batch_tile(A.dZ1T + (size_t)nt * 16 * DZ1_LD, A.act2T + (size_t)ft * 16 * MAX_TRAIN_BATCH,
-                                       nb, params, mom, idx, p, m);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (idx[r] >= 0) sgd_apply(idx[r], acc[r], p[r], m[r], params, mom, pk, lr, momentum, wd);
-        }
-      } else if (b < SGD_NA + SGD2_NB + SGD2_NC) {    // fc2.weight [84][120]: 6 x 8 tiles
-        const int t = (b - SGD_NA - SGD2_NB) * 4 + wave;
-        if (t < 48) {
-          const int nt = t >> 3, ft = t & 7;
-          const bf16* dz2t = reinterpret_cast<const bf16*>(A.aux + AUX_DZ2T);
-          int idx[4];
-          float p[4], m[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = nt * 16 + rq + r, f = ft * 16 + n16;
-            idx[r] = (n < F2 && f < F1) ? P_F2W + n * F1 + f : -1;
-          }
-          const f32x4 acc = batch_tile(dz2t + (size_t)nt * 16 * MAX_TRAIN_BATCH,
-                                       A.h1T + (size_t)ft * 16 * MAX_TRAIN_BATCH, nb, params, mom, idx, p, m);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (idx[r] >= 0) sgd_apply(idx[r], acc[r], p[r], m[r], params, mom, pk, lr, momentum, wd);
-        }
-      } else {                                        // fc3.weight [10][84]: 1 x 6 tiles
-        const int t = (b - SGD_NA - SGD2_NB - SGD2_NC) * 4 + wave;
-        if (t < 6) {
-          const bf16* dz3t = reinterpret_cast<const bf16*>(A.aux + AUX_DZ3T);
-          const bf16* h2t = reinterpret_cast<const bf16*>(A.aux + AUX_H2T);
-          int idx[4];
-          float p[4], m[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = rq + r, f = t * 16 + n16;
-            idx[r] = (n < NCLS && f < F2) ? P_F3W + n * F2 + f : -1;
-          }
-          const f32x4 acc = batch_tile(dz3t, h2t + (size_t)t * 16 * MAX_TRAIN_BATCH, nb, params, mom, idx, p, m);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (idx[r] >= 0) sgd_apply(idx[r], acc[r], p[r], m[r], params, mom, pk, lr, momentum, wd);
-        }
-      }
-    }
-    return carry;
-  } else {                                            // FC biases + loss / accuracy counters
-    // block e < 4: biases [64e, 64e + 64) x 4 sample groups of 32 (all 32 loads in flight),
-    // fixed-order combine; block 4: the per-sample losses / hits (fixed tree order)
-    const int e = b - (SGD_NA + SGD2_NB + SGD2_NC + SGD2_ND);
-    const int j = e * 64 + (tid & 63), g = tid >> 6;
-    const int bi = j < 120 ? P_F1B + j : (j < 204 ? P_F2B + j - 120 : P_F3B + j - 204);
-    if constexpr (PH == 0) {
-      const float* fcb = reinterpret_cast<const float*>(A.aux + AUX_FCB);
-      float bp = 0.f, bm = 0.f;
-      if (e < SGD2_NE && g == 0 && j < 214) { bp = params[bi]; bm = mom[bi]; }
-      if (e < SGD2_NE && j < 214) {
-        float v[32];
-#pragma unroll
-        for (int u = 0; u < 32; ++u) {
-          const int sm = g * 32 + u;
-          v[u] = sm < nb ? fcb[(size_t)sm * FCB_N + j] : 0.f;
-        }
-        float sum = 0.f;
-#pragma unroll
-        for (int u = 0; u < 32; ++u) sum += v[u];
-        bsum[g][tid & 63] = sum;
-      } else if (e == SGD2_NE && g == 0 && A.stats != nullptr) {
-        const float* lv = reinterpret_cast<const float*>(A.aux + AUX_LOSS);
-        const float* cv = reinterpret_cast<const float*>(A.aux + AUX_CORR);
-        float ls = 0.f, cs = 0.f;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int sm = lane + 64 * u;
-          if (sm < nb) { ls += lv[sm]; cs += cv[sm]; }
-        }
-        ls = wave_sum(ls);
-        cs = wave_sum(cs);
-        if (lane == 0) {
-          A.stats->loss_sum += ls;
-          A.stats->correct += (int)(cs + 0.5f);
-          A.stats->count += nb;
-        }
-      }
-      return make_float2(bp, bm);
-    } else {
-      if (e < SGD2_NE && g == 0 && j < 214) {
-        const float sum = (bsum[0][tid] + bsum[1][tid]) + (bsum[2][tid] + bsum[3][tid]);
-        sgd_apply(bi, sum, carry.x, carry.y, params, mom, pk, lr, momentum, wd);
-      }
-      return carry;
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void lenet_sgd2(
     float* __restrict__ params, float* __restrict__ mom, bf16* __restrict__ pk,
     const float* __restrict__ conv_slab, int nb,
@@ -1952,74 +1723,135 @@ __global__ __launch_bounds__(256) void lenet_sgd2(
     int* __restrict__ round_ctr, int* __restrict__ step_gen, Stats* __restrict__ stats)
 {
   __shared__ float red[16][17];
-  __shared__ float bsum[4][64];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = blockIdx.x, tid = threadIdx.x, wave = wave_id(), lane = lane_id();
+  const int n16 = lane & 15, rq = (lane >> 4) * 4;
   [[maybe_unused]] const int stamp_wg = b;
   FEDMI_STAMP(3, 0);
-  const Sgd2Args A{params, mom, pk, conv_slab, nb, act2T, h1T, aux, dZ1T, lr, momentum, wd, stats};
-  const float2 c = sgd2_block<0>(b, tid, wave_id(), lane_id(), red, bsum, make_float2(0.f, 0.f), A);
-  __syncthreads();
-  sgd2_block<1>(b, tid, wave_id(), lane_id(), red, bsum, c, A);
+  if (b < SGD_NA) {                                   // conv params: K4's slab combine
+    const int pl = tid & 15, g = tid >> 4;
+    const int i = b * 16 + pl;
+    float p = 0.f, m = 0.f;
+    if (g == 0 && i < CS) { p = params[i]; m = mom[i]; }
+    float sum = 0.f;
+    if (i < CS) {
+      float v[MAX_TRAIN_BATCH / 16];
+#pragma unroll
+      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) {
+        const int q = g + 16 * u;
+        v[u] = q < nb ? conv_slab[(size_t)q * CS + i] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) sum += v[u];
+    }
+    red[g][pl] = sum;
+    __syncthreads();
+    if (g == 0 && i < CS) {
+      float tot = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) tot += red[q][pl];
+      sgd_apply(i, tot, p, m, params, mom, pk, lr, momentum, wd);
+    }
+  } else if (b < SGD_NA + SGD2_NB) {                  // fc1.weight [120][400]: 8 x 25 tiles
+    const int t = (b - SGD_NA) * 4 + wave;
+    if (t < 200) {
+      const int nt = t / 25, ft = t - nt * 25;
+      int idx[4];
+      float p[4], m[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = nt * 16 + rq + r, f = ft * 16 + n16;
+        idx[r] = n < F1 ? P_F1W + n * F0 + f : -1;
+      }
+      const f32x4 acc = batch_tile(dZ1T + (size_t)nt * 16 * DZ1_LD, act2T + (size_t)ft * 16 * MAX_TRAIN_BATCH, nb,
+                                   params, mom, idx, p, m);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (idx[r] >= 0) sgd_apply(idx[r], acc[r], p[r], m[r], params, mom, pk, lr, momentum, wd);
+    }
+  } else if (b < SGD_NA + SGD2_NB + SGD2_NC) {        // fc2.weight [84][120]: 6 x 8 tiles
+    const int t = (b - SGD_NA - SGD2_NB) * 4 + wave;
+    if (t < 48) {
+      const int nt = t >> 3, ft = t & 7;
+      const bf16* dz2t = reinterpret_cast<const bf16*>(aux + AUX_DZ2T);
+      int idx[4];
+      float p[4], m[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = nt * 16 + rq + r, f = ft * 16 + n16;
+        idx[r] = (n < F2 && f < F1) ? P_F2W + n * F1 + f : -1;
+      }
+      const f32x4 acc = batch_tile(dz2t + (size_t)nt * 16 * MAX_TRAIN_BATCH, h1T + (size_t)ft * 16 * MAX_TRAIN_BATCH, nb,
+                                   params, mom, idx, p, m);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (idx[r] >= 0) sgd_apply(idx[r], acc[r], p[r], m[r], params, mom, pk, lr, momentum, wd);
+    }
+  } else if (b < SGD_NA + SGD2_NB + SGD2_NC + SGD2_ND) {   // fc3.weight [10][84]: 1 x 6 tiles
+    const int t = (b - SGD_NA - SGD2_NB - SGD2_NC) * 4 + wave;
+    if (t < 6) {
+      const bf16* dz3t = reinterpret_cast<const bf16*>(aux + AUX_DZ3T);
+      const bf16* h2t = reinterpret_cast<const bf16*>(aux + AUX_H2T);
+      int idx[4];
+      float p[4], m[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = rq + r, f = t * 16 + n16;
+        idx[r] = (n < NCLS && f < F2) ? P_F3W + n * F2 + f : -1;
+      }
+      const f32x4 acc = batch_tile(dz3t, h2t + (size_t)t * 16 * MAX_TRAIN_BATCH, nb, params, mom, idx, p, m);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (idx[r] >= 0) sgd_apply(idx[r], acc[r], p[r], m[r], params, mom, pk, lr, momentum, wd);
+    }
+  } else {                                            // FC biases + loss / accuracy counters
+    // block e < 4: biases [64e, 64e + 64) x 4 sample groups of 32 (all 32 loads in flight),
+    // fixed-order combine; block 4: the per-sample losses / hits (fixed tree order)
+    const int e = b - (SGD_NA + SGD2_NB + SGD2_NC + SGD2_ND);
+    const float* fcb = reinterpret_cast<const float*>(aux + AUX_FCB);
+    const int j = e * 64 + (tid & 63), g = tid >> 6;
+    __shared__ float bsum[4][64];
+    float bp = 0.f, bm = 0.f;
+    const int bi = j < 120 ? P_F1B + j : (j < 204 ? P_F2B + j - 120 : P_F3B + j - 204);
+    if (e < SGD2_NE && g == 0 && j < 214) { bp = params[bi]; bm = mom[bi]; }
+    if (e < SGD2_NE && j < 214) {
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int sm = g * 32 + u;
+        v[u] = sm < nb ? fcb[(size_t)sm * FCB_N + j] : 0.f;
+      }
+      float sum = 0.f;
+#pragma unroll
+      for (int u = 0; u < 32; ++u) sum += v[u];
+      bsum[g][tid & 63] = sum;
+    } else if (e == SGD2_NE && g == 0 && stats != nullptr) {
+      const float* lv = reinterpret_cast<const float*>(aux + AUX_LOSS);
+      const float* cv = reinterpret_cast<const float*>(aux + AUX_CORR);
+      float ls = 0.f, cs = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int sm = lane + 64 * u;
+        if (sm < nb) { ls += lv[sm]; cs += cv[sm]; }
+      }
+      ls = wave_sum(ls);
+      cs = wave_sum(cs);
+      if (lane == 0) {
+        stats->loss_sum += ls;
+        stats->correct += (int)(cs + 0.5f);
+        stats->count += nb;
+      }
+    }
+    __syncthreads();
+    if (e < SGD2_NE && g == 0 && j < 214) {
+      const float sum = (bsum[0][tid] + bsum[1][tid]) + (bsum[2][tid] + bsum[3][tid]);
+      sgd_apply(bi, sum, bp, bm, params, mom, pk, lr, momentum, wd);
+    }
+  }
   if (b == 0 && tid == 0) {
     if (round_ctr) atomicAdd(round_ctr, 1);
     if (step_gen) step_gen[0] += 1;
   }
   FEDMI_STAMP(3, 1);
-}
-
-// ---------------------------------------------------------------------------
-// Pipelined step: SGD of step i-1 and the samples of step i in ONE launch.
-// The first PIPE_SGD_WG workgroups run the 249 sgd2 blocks (four per workgroup) on the previous
-// step's buffers, then publish (release) a counter; the sample workgroups after them -- the
-// dispatcher places workgroups in index order, so the SGD workgroups are resident first and never
-// wait on anything -- stage their image and draw the augmentation, wait for the counter (acquire),
-// and only then read the updated weights.  Removes one kernel boundary per step and overlaps the
-// SGD with the image stage; same arithmetic and order as lenet_sample_step + lenet_sgd2
-// (bit-identical epochs).  The per-step buffers alternate between two sets by step parity.
-// ---------------------------------------------------------------------------
-constexpr int PIPE_SGD_WG = (SGD2_GRID + 3) / 4;    // 63
-
-__global__ __launch_bounds__(NT_CONV) void lenet_step_piped(
-    const uint8_t* __restrict__ images, int sample_base, int nb, bf16* pk, float* params, float* mom,
-    uint32_t seed, const int* __restrict__ round_ctr, int augment, const int* __restrict__ labels,
-    bf16* __restrict__ act2T, bf16* __restrict__ h1T, unsigned char* __restrict__ aux, bf16* __restrict__ dZ1T,
-    float* __restrict__ conv_slab,
-    int nb_prev, const bf16* __restrict__ act2T_prev, const bf16* __restrict__ h1T_prev,
-    const unsigned char* __restrict__ aux_prev, const bf16* __restrict__ dZ1T_prev,
-    const float* __restrict__ conv_slab_prev, float lr, float momentum, float wd,
-    int* __restrict__ step_gen, Stats* __restrict__ stats, int* __restrict__ sgd_done, int par)
-{
-  __shared__ __attribute__((aligned(16))) unsigned char smem[S_END];
-  const int w = blockIdx.x;
-  if (w < PIPE_SGD_WG) {
-    const int q = wave_id() >> 2, t = threadIdx.x & 255, b = w * 4 + q;
-    [[maybe_unused]] const int stamp_wg = w;
-    FEDMI_STAMP(3, 0);
-    float (*red)[17] = reinterpret_cast<float (*)[17]>(smem + q * 2048);
-    float (*bsum)[64] = reinterpret_cast<float (*)[64]>(smem + 8192 + q * 1024);
-    // the other parity's counter was last used by the previous launch (complete): re-arm it
-    if (w == 0 && threadIdx.x == 0) __hip_atomic_store(sgd_done + (par ^ 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const Sgd2Args A{params, mom, pk, conv_slab_prev, nb_prev, act2T_prev, h1T_prev, aux_prev, dZ1T_prev,
-                     lr, momentum, wd, stats};
-    float2 c = make_float2(0.f, 0.f);
-    if (b < SGD2_GRID) c = sgd2_block<0>(b, t, wave_id() & 3, lane_id(), red, bsum, c, A);
-    __syncthreads();
-    if (b < SGD2_GRID) sgd2_block<1>(b, t, wave_id() & 3, lane_id(), red, bsum, c, A);
-    if (w == 0 && threadIdx.x == 0 && step_gen) step_gen[0] += 1;
-    // publish (cdna_hip_programming.md Guideline 16): every wave's stores retired, ONE agent release
-    // by lane 0, its own wait, then a relaxed ticket -- not a release fence per wave
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(sgd_done + par, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    FEDMI_STAMP(3, 1);
-    return;
-  }
-  sample_step_body<true>(smem, w - PIPE_SGD_WG, images, sample_base, nb, pk, params, seed, round_ctr, augment, labels,
-                         act2T, h1T, aux, dZ1T, conv_slab, sgd_done + par, PIPE_SGD_WG, stats);
 }
 
 // ---------------------------------------------------------------------------
@@ -2245,29 +2077,10 @@ void launch_lenet_pack(hipStream_t st, const float* params, bf16* pk) {
 
 void launch_lenet_sample_step(hipStream_t st, const uint8_t* images, int sample_base, int nb, const bf16* pk,
                               const float* params, uint32_t seed, const int* round_ctr, int augment,
-                              const int* labels, bf16* act2T, bf16* h1T, float* aux, bf16* dZ1T, float* conv_slab,
-                              int* sgd_done) {
+                              const int* labels, bf16* act2T, bf16* h1T, float* aux, bf16* dZ1T, float* conv_slab) {
   if (nb <= 0 || nb > MAX_TRAIN_BATCH) throw std::invalid_argument("lenet_sample_step: batch must be in [1, 128]");
   hipLaunchKernelGGL(lenet_sample_step, dim3(nb), dim3(NT_CONV), 0, st, images, sample_base, nb, pk, params, seed,
-                     round_ctr, augment, labels, act2T, h1T, reinterpret_cast<unsigned char*>(aux), dZ1T, conv_slab,
-                     sgd_done);
-}
-
-void launch_lenet_step_piped(hipStream_t st, const uint8_t* images, int sample_base, int nb, bf16* pk, float* params,
-                             float* mom, uint32_t seed, const int* round_ctr, int augment, const int* labels,
-                             bf16* act2T, bf16* h1T, float* aux, bf16* dZ1T, float* conv_slab, int nb_prev,
-                             const bf16* act2T_prev, const bf16* h1T_prev, const float* aux_prev,
-                             const bf16* dZ1T_prev, const float* conv_slab_prev, float lr, float momentum, float wd,
-                             int* step_gen, Stats* stats, int* sgd_done, int par) {
-  if (nb <= 0 || nb > MAX_TRAIN_BATCH || nb_prev <= 0 || nb_prev > MAX_TRAIN_BATCH)
-    throw std::invalid_argument("lenet_step_piped: batches must be in [1, 128]");
-  if (!sgd_done || !stats || (par != 0 && par != 1)) throw std::invalid_argument("lenet_step_piped: hand-off state");
-  if (act2T == act2T_prev || conv_slab == conv_slab_prev || aux == aux_prev)
-    throw std::invalid_argument("lenet_step_piped: the two steps need distinct buffer sets");
-  hipLaunchKernelGGL(lenet_step_piped, dim3(PIPE_SGD_WG + nb), dim3(NT_CONV), 0, st, images, sample_base, nb, pk,
-                     params, mom, seed, round_ctr, augment, labels, act2T, h1T, reinterpret_cast<unsigned char*>(aux),
-                     dZ1T, conv_slab, nb_prev, act2T_prev, h1T_prev, reinterpret_cast<const unsigned char*>(aux_prev),
-                     dZ1T_prev, conv_slab_prev, lr, momentum, wd, step_gen, stats, sgd_done, par);
+                     round_ctr, augment, labels, act2T, h1T, reinterpret_cast<unsigned char*>(aux), dZ1T, conv_slab);
 }
 
 void launch_lenet_sgd2(hipStream_t st, float* params, float* mom, bf16* pk, const float* conv_slab, int nb,

@@ -26,11 +26,7 @@ void launch_lenet_bwd_sgd(hipStream_t, const uint8_t*, int, int, uint32_t, const
                           const float*, int, float, float, float, int*, const int*, int*, int*, Stats*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
 void launch_lenet_sample_step(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*,
-                              int, const int*, bf16*, bf16*, float*, bf16*, float*, int*);
-void launch_lenet_step_piped(hipStream_t, const uint8_t*, int, int, bf16*, float*, float*, uint32_t, const int*, int,
-                             const int*, bf16*, bf16*, float*, bf16*, float*, int, const bf16*, const bf16*,
-                             const float*, const bf16*, const float*, float, float, float, int*, lenet::Stats*, int*,
-                             int);
+                              int, const int*, bf16*, bf16*, float*, bf16*, float*);
 void launch_lenet_sgd2(hipStream_t, float*, float*, bf16*, const float*, int, const bf16*, const bf16*, const float*,
                        const bf16*, float, float, float, int*, int*, lenet::Stats*);
 
@@ -91,7 +87,7 @@ void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round, bool 
     if (reset_stats) check_hip(hipMemsetAsync(b_.train_stats, 0, sizeof(Stats), st), "memset stats");
     // the FC side buffers (h2T, dZ2T, dZ3T, bias grads, losses) live in the dact2 buffer, h1T in h1
     launch_lenet_sample_step(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug,
-                             b_.train_labels + start, b_.act2T, b_.h1, b_.dact2, b_.dZ1T, b_.conv_slab, nullptr);
+                             b_.train_labels + start, b_.act2T, b_.h1, b_.dact2, b_.dZ1T, b_.conv_slab);
     launch_lenet_sgd2(st, b_.params, b_.mom, b_.pk, b_.conv_slab, nb, b_.act2T, b_.h1, b_.dact2, b_.dZ1T, sgd_.lr,
                       sgd_.momentum, sgd_.weight_decay, bump_round ? b_.round_ctr : nullptr, b_.step_gen,
                       b_.train_stats);
@@ -150,47 +146,9 @@ void LeNetEngine::set_fuse_sgd(bool on) {
   }
 }
 
-void LeNetEngine::set_pipeline(bool on) {
-  if (on && (!b_.act2T_b || !b_.h1_b || !b_.dact2_b || !b_.dZ1T_b || !b_.conv_slab_b || !b_.sgd_done))
-    throw std::invalid_argument("pipeline needs the second per-step buffer set and sgd_done");
-  if (on != pipeline_) {
-    pipeline_ = on;
-    drop_graph();
-  }
-}
-
 void LeNetEngine::enqueue_epoch(hipStream_t st) {
-  using namespace lenet;
   const size_t n = starts_.size();
-  if (!(sample_path_ && pipeline_ && n >= 2)) {
-    for (size_t i = 0; i < n; ++i) step(st, starts_[i], sizes_[i], i + 1 == n, i == 0);
-    return;
-  }
-  // pipelined: step 0 alone (arms the hand-off counters), then SGD(i-1) + samples(i) per launch, then
-  // SGD(n-1) with the round bump.  Step i's buffers: set (i & 1).
-  struct Set { bf16* act2T; bf16* h1; float* aux; bf16* dZ1T; float* slab; };
-  const Set sets[2] = {{b_.act2T, b_.h1, b_.dact2, b_.dZ1T, b_.conv_slab},
-                       {b_.act2T_b, b_.h1_b, b_.dact2_b, b_.dZ1T_b, b_.conv_slab_b}};
-  const int aug = augment_ ? 1 : 0;
-  for (size_t i = 0; i < n; ++i)
-    if (sizes_[i] <= 0 || sizes_[i] > MAX_TRAIN_BATCH || starts_[i] < 0 || starts_[i] + sizes_[i] > b_.n_train)
-      throw std::invalid_argument("LeNetEngine: batch out of range");
-  check_hip(hipMemsetAsync(b_.train_stats, 0, sizeof(Stats), st), "memset stats");
-  launch_lenet_sample_step(st, b_.train_images, starts_[0], sizes_[0], b_.pk, b_.params, seed_, b_.round_ctr, aug,
-                           b_.train_labels + starts_[0], sets[0].act2T, sets[0].h1, sets[0].aux, sets[0].dZ1T,
-                           sets[0].slab, b_.sgd_done);
-  for (size_t i = 1; i < n; ++i) {
-    const Set& c = sets[i & 1];
-    const Set& p = sets[(i - 1) & 1];
-    launch_lenet_step_piped(st, b_.train_images, starts_[i], sizes_[i], b_.pk, b_.params, b_.mom, seed_, b_.round_ctr,
-                            aug, b_.train_labels + starts_[i], c.act2T, c.h1, c.aux, c.dZ1T, c.slab, sizes_[i - 1],
-                            p.act2T, p.h1, p.aux, p.dZ1T, p.slab, sgd_.lr, sgd_.momentum, sgd_.weight_decay,
-                            b_.step_gen, b_.train_stats, b_.sgd_done, (int)(i & 1));
-  }
-  const Set& l = sets[(n - 1) & 1];
-  launch_lenet_sgd2(st, b_.params, b_.mom, b_.pk, l.slab, sizes_[n - 1], l.act2T, l.h1, l.aux, l.dZ1T, sgd_.lr,
-                    sgd_.momentum, sgd_.weight_decay, b_.round_ctr, b_.step_gen, b_.train_stats);
-  check_hip(hipGetLastError(), "LeNetEngine::enqueue_epoch (pipelined) launch");
+  for (size_t i = 0; i < n; ++i) step(st, starts_[i], sizes_[i], i + 1 == n, i == 0);
 }
 
 void LeNetEngine::run_epoch(hipStream_t st, bool use_graph) {

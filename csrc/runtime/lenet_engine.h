@@ -40,14 +40,6 @@ struct LeNetBuffers {
   int* step_gen = nullptr;       // step generation, bumped by K4 / K34
   int* bwd_flags = nullptr;      // [MAX_TRAIN_BATCH + N_DW1_WG] K34 producer flags (optional: enables fuse_sgd)
   int* bwd_gen = nullptr;        // K34's flag generation, bumped by K12
-  // second set of the sample path's per-step buffers + hand-off counters (optional: enables the
-  // pipelined epoch, where step i's samples run in the same launch as step i-1's SGD)
-  bf16* act2T_b = nullptr;
-  bf16* h1_b = nullptr;          // [128][128]
-  float* dact2_b = nullptr;
-  bf16* dZ1T_b = nullptr;
-  float* conv_slab_b = nullptr;
-  int* sgd_done = nullptr;       // [2] per-parity SGD-workgroup counters
 };
 
 struct SgdConfig {
@@ -88,9 +80,6 @@ class LeNetEngine {
   // 2 launches per step, no inter-workgroup hand-off; takes precedence over fuse_head / fuse_sgd
   void set_sample_path(bool on);
   bool sample_path() const { return sample_path_; }
-  // sample path only: an epoch as n+1 launches (step 0; SGD(i-1) + samples(i); SGD(n-1)) instead of 2n
-  void set_pipeline(bool on);
-  bool pipeline() const { return pipeline_; }
 
  private:
   void enqueue_epoch(hipStream_t st);
@@ -104,7 +93,6 @@ class LeNetEngine {
   bool fuse_head_ = false;
   bool fuse_sgd_ = false;
   bool sample_path_ = false;
-  bool pipeline_ = false;
   std::vector<int> starts_, sizes_;
   hipStream_t cap_stream_ = nullptr;
   hipGraph_t graph_ = nullptr;

@@ -506,6 +506,14 @@ class CNNNativeTrainer(LocalTrainer):
         # one fp32 split-K workspace for every conv launch of a step (fwd / dgrad / wgrad)
         self.wgrad_ws = torch.empty(max(max(u.ws_floats(nb) for u in self.units) for nb in {B, self.eval_bs}),
                                     device=device)
+        # weight gradients on a side stream (FEDMI_CNN_WGRAD_STREAM=0: one stream), with their own workspace
+        import os
+
+        self._side = None
+        self.wgrad_ws2 = None
+        if device.type == "cuda" and os.environ.get("FEDMI_CNN_WGRAD_STREAM", "1") != "0":
+            self._side = torch.cuda.Stream(device)
+            self.wgrad_ws2 = torch.empty_like(self.wgrad_ws)
         # BN-backward two-level channel sums (replicated atomics + finalize; kept zero between uses)
         self.bn_ws = torch.zeros(max(cnn.bn_bwd_ws_floats(B * u.P * u.P, u.O) for u in self.units),
                                  dtype=torch.float64, device=device)
@@ -685,6 +693,21 @@ class CNNNativeTrainer(LocalTrainer):
             d.update(zb=zb.view(zb.z, nb), meanb=zb.smean, invb=zb.sinv)
         return d
 
+    def _wgrad(self, u: _Unit, x, nb: int, dz=None) -> None:
+        """``u``'s weight gradient: nothing else in the backward reads it before the SGD, so with a side
+        stream it runs there (own split-K workspace), overlapping the dgrad / BN chain of the main stream;
+        ``_backward`` joins the streams at its end."""
+        if self._side is None:
+            u.wgrad(x, nb, self.wgrad_ws, dz=dz)
+            return
+        self._side.wait_stream(torch.cuda.current_stream(self._device))
+        with torch.cuda.stream(self._side):
+            u.wgrad(x, nb, self.wgrad_ws2, dz=dz)
+
+    def _join_side(self) -> None:
+        if self._side is not None:
+            torch.cuda.current_stream(self._device).wait_stream(self._side)
+
     def _bn_bwd(self, u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None, dadd=None,
                 mask_bn=None, presummed: bool = False) -> None:
         bn_ws = self.bn_ws if self.bn_ws.numel() else None
@@ -724,7 +747,7 @@ class CNNNativeTrainer(LocalTrainer):
             for j in range(len(b.main) - 1, -1, -1):
                 v = b.main[j]
                 xin = b.main[j - 1].view(b.main[j - 1].y, nb) if j > 0 else a_in
-                v.wgrad(xin, nb, ws)
+                self._wgrad(v, xin, nb)
                 if j > 0:
                     w = b.main[j - 1]
                     wy = w.view(w.y, nb) if w.relu else None
@@ -746,7 +769,7 @@ class CNNNativeTrainer(LocalTrainer):
                         # the shortcut's grad first, then conv1's DGRAD adds it and takes the previous
                         # block's BN-backward sums from the complete grad
                         if b.proj is not None:
-                            b.proj.wgrad(a_in, nb, ws)
+                            self._wgrad(b.proj, a_in, nb)
                             b.proj.dgrad(nb, din_b, ws)
                             proj_done = True
                         v.dgrad(nb, din_a, ws, add=din_b, bn_sums=bs)   # add=None: no shortcut
@@ -755,7 +778,7 @@ class CNNNativeTrainer(LocalTrainer):
                         v.dgrad(nb, din_a, ws)
                         dya, dyb, pres = din_a, din_b, False
             if b.proj is not None and not proj_done:
-                b.proj.wgrad(a_in, nb, ws)
+                self._wgrad(b.proj, a_in, nb)
                 b.proj.dgrad(nb, din_b, ws)
 
     # ---- pre-activation ResNets --------------------------------------------------------------
@@ -803,27 +826,27 @@ class CNNNativeTrainer(LocalTrainer):
             a = prev.view(prev.y, nb)
             L = b.units[-1]
             pen = b.units[-2]
-            L.wgrad(pen.view(pen.y, nb), nb, ws, dz=g)
+            self._wgrad(L, pen.view(pen.y, nb), nb, dz=g)
             L.dgrad(nb, pen.view(pen.dy, nb), ws, dz=g)
             for j in range(len(b.units) - 2, -1, -1):
                 u = b.units[j]
                 self._bn_bwd(u, nb, u.view(u.dy, nb), None, u.view(u.y, nb))
                 if j > 0:
                     w = b.units[j - 1]
-                    u.wgrad(w.view(w.y, nb), nb, ws)
+                    self._wgrad(u, w.view(w.y, nb), nb)
                     u.dgrad(nb, w.view(w.dy, nb), ws)
                 else:
-                    u.wgrad(a, nb, ws)
+                    self._wgrad(u, a, nb)
                     u.dgrad(nb, prev.view(prev.dy, nb), ws)      # d a_b, conv1 branch
             da2 = None
             if b.sc is not None:                           # d a_b, shortcut-conv branch
-                b.sc.wgrad(a, nb, ws, dz=g)
+                self._wgrad(b.sc, a, nb, dz=g)
                 da2 = b.in_view(b.da2, nb)
                 b.sc.dgrad(nb, da2, ws, dz=g)
             # bn1 of this block (prev's BN): dx_b = BN_bwd(relu mask) + identity-shortcut grad
             self._bn_bwd(prev, nb, prev.view(prev.dy, nb), da2, a, dadd=None if b.sc is not None else g)
             g = prev.view(prev.dz, nb)
-        P.stem.wgrad(x, nb, ws)
+        self._wgrad(P.stem, x, nb)
 
     # ---- GoogLeNet ----------------------------------------------------------------------------
     def _forward_goog(self, nb: int, train: bool, images, labels, dbase, stats_row: int):
@@ -871,19 +894,19 @@ class CNNNativeTrainer(LocalTrainer):
                     v = br[j]
                     if j > 0:
                         w = br[j - 1]
-                        v.wgrad(w.view(w.y, nb), nb, ws)
+                        self._wgrad(v, w.view(w.y, nb), nb)
                         v.dgrad(nb, w.view(w.dy, nb), ws)
                         self._bn_bwd(w, nb, w.view(w.dy, nb), None, w.view(w.y, nb))
                     elif k < 3:                            # branch heads: the module input's grad fan-in
-                        v.wgrad(a, nb, ws)
+                        self._wgrad(v, a, nb)
                         v.dgrad(nb, dx, ws, accumulate=k > 0)
                     else:
-                        v.wgrad(I.in_view(I.bp, nb), nb, ws)
+                        self._wgrad(v, I.in_view(I.bp, nb), nb)
                         dbp = v.dgrad(nb, I.in_view(I.dbp, nb), ws)
                         cnn.maxpool3_bwd(dbp, I._bidx, (nb, I.hw, I.hw, I.cin), 1, out=dx, accumulate=True)
             g = dx
         self._bn_bwd(p, nb, p.view(p.dy, nb), None, p.view(p.y, nb))
-        p.wgrad(x, nb, ws)
+        self._wgrad(p, x, nb)
 
     def _sgd(self) -> None:
         c, fs = self.cfg, self.fs
@@ -898,6 +921,7 @@ class CNNNativeTrainer(LocalTrainer):
             self.red_all.zero_()
         x, dh = self._forward(nb, True, self.train_set.x, self.train_set.y, self.cur, 0)
         self._backward(nb, x, dh)
+        self._join_side()          # the side stream's weight gradients before the SGD reads them
 
     def _train_step(self, nb: int) -> None:
         """One SGD step on the batch at sched[counter] (device-side)."""

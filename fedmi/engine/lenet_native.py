@@ -80,13 +80,6 @@ class LeNetNativeTrainer(LocalTrainer):
             self.step_gen = z(4, dt=torch.int32)
             self.bwd_flags = z(B + L["N_DW1_WG"], dt=torch.int32)   # K34 producer -> SGD hand-off flags
             self.bwd_gen = z(4, dt=torch.int32)
-            # second per-step buffer set + hand-off counters of the pipelined epoch
-            self.act2T_b = z(L["F0P"], B, dt=torch.bfloat16)
-            self.h1_b = z(B + 16, 128, dt=torch.bfloat16)
-            self.dact2_b = z(B, L["F0"])
-            self.dZ1T_b = z(L["DZ1_LD"], B, dt=torch.bfloat16)
-            self.conv_slab_b = z(B, L["CS"])
-            self.sgd_done = z(4, dt=torch.int32)
         self._bufs = dict(
             train_images=_ptr(self.train_set.x), train_labels=_ptr(self.train_set.y), n_train=len(self.train_set),
             params=_ptr(self.params), mom=_ptr(self.mom), pk=_ptr(self.pk), act2=_ptr(self.act2),
@@ -94,9 +87,7 @@ class LeNetNativeTrainer(LocalTrainer):
             am2=_ptr(self.am2), dact2=_ptr(self.dact2), dZ1T=_ptr(self.dZ1T), conv_slab=_ptr(self.conv_slab),
             fc1w_grad=_ptr(self.fc1w_grad), fc_slab=_ptr(self.fc_slab), train_stats=_ptr(self.stats[0]), eval_stats=_ptr(self.stats[1]),
             round_ctr=_ptr(self.round_ctr), done_flags=_ptr(self.done_flags), step_gen=_ptr(self.step_gen),
-            bwd_flags=_ptr(self.bwd_flags), bwd_gen=_ptr(self.bwd_gen), act2T_b=_ptr(self.act2T_b),
-            h1_b=_ptr(self.h1_b), dact2_b=_ptr(self.dact2_b), dZ1T_b=_ptr(self.dZ1T_b),
-            conv_slab_b=_ptr(self.conv_slab_b), sgd_done=_ptr(self.sgd_done))
+            bwd_flags=_ptr(self.bwd_flags), bwd_gen=_ptr(self.bwd_gen))
         self.engine = nat.LeNetEngine(self._bufs, cfg.lr, cfg.momentum, cfg.weight_decay, cfg.seed & 0xFFFFFFFF,
                                       bool(data.augment and cfg.augment))
         self.fuse_fc1 = os.environ.get("FEDMI_LENET_FUSE_FC1", "1") == "1"
@@ -165,8 +156,6 @@ class LeNetNativeTrainer(LocalTrainer):
         # default: per-sample step kernel + batched FC-gradient GEMM/SGD kernel (2 launches, 10.45 vs
         # 12.95 ms per round, profiles/r2_lenet/experiments.md); FEDMI_LENET_PATH=head: K12 -> K3 -> K4
         self.engine.set_sample_path(os.environ.get("FEDMI_LENET_PATH", "sample") == "sample")
-        # sample path: SGD of step i-1 and the samples of step i in one launch (n+1 launches per epoch)
-        self.engine.set_pipeline(os.environ.get("FEDMI_LENET_PIPE", "0") == "1")
 
     # ---- compute ----------------------------------------------------------------
     def train_epoch(self) -> None:
@@ -187,8 +176,7 @@ class LeNetNativeTrainer(LocalTrainer):
         raw = raw.contiguous()
         flag = int(raw[3])
         if flag:
-            what = {1: "conv -> FC-head act2 hand-off (K12)", 2: "K3 -> K4 gradient hand-off (K34)",
-                    3: "pipelined step: previous step's SGD -> samples"}.get(flag, "?")
+            what = {1: "conv -> FC-head act2 hand-off (K12)", 2: "K3 -> K4 gradient hand-off (K34)"}.get(flag, "?")
             raise RuntimeError(f"LeNet kernel hand-off timed out: {what} (stats flag {flag}); the step ran on "
                                "stale rows -- another process is starving this GPU, or a workgroup never ran")
         return EpochStats(float(raw[0:1].view(torch.float32).item()), int(raw[1]), int(raw[2]))

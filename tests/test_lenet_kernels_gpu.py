@@ -477,38 +477,3 @@ def test_sample_path_trains_like_head_path(env, use_graph):
     tr.cfg.use_graph = True
     tr.load_state_dict(ref.state_dict())
     tr.mom.zero_()
-
-
-@pytest.mark.parametrize("use_graph", [True, False], ids=["graph", "eager"])
-def test_pipelined_epoch_is_bit_identical(env, use_graph):
-    """lenet_step_piped (SGD of step i-1 + samples of step i in one launch, two buffer sets, counter
-    hand-off) trains BIT-IDENTICALLY to lenet_sample_step + lenet_sgd2 per step: same arithmetic, same
-    order; over two epochs of full and partial batches (parity of both buffer sets, odd and even step
-    counts, the round bump in the trailing SGD launch)."""
-    nat, dev, ds, ref, tr = env
-    tr.engine.set_sample_path(True)
-    res = []
-    for starts, sizes in (([0, 128, 384, 896], [128, 128, 33, 80]), ([0, 128, 256], [128, 100, 128])):
-        for pipe in (False, True):
-            tr.engine.set_pipeline(pipe)
-            assert tr.engine.pipeline == pipe
-            tr.load_state_dict(ref.state_dict())
-            tr.mom.zero_()
-            tr.round_ctr.zero_()
-            tr.stats.zero_()
-            tr.round_idx = 0
-            tr.cfg.use_graph = use_graph
-            tr.set_schedule(starts, sizes)
-            for _ in range(2):
-                tr.train_epoch()
-            torch.cuda.synchronize()
-            st = tr.train_stats()          # raises if a hand-off timed out
-            res.append((tr.params.clone(), tr.mom.clone(), tr.pk.clone(), st, int(tr.round_ctr[0])))
-        (p0, m0, k0, s0, r0), (p1, m1, k1, s1, r1) = res[-2:]
-        assert r0 == r1 == 2
-        assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(k0, k1)
-        assert (s0.loss_sum, s0.correct, s0.count) == (s1.loss_sum, s1.correct, s1.count) and s1.count == sum(sizes)
-    tr.engine.set_pipeline(False)
-    tr.cfg.use_graph = True
-    tr.load_state_dict(ref.state_dict())
-    tr.mom.zero_()
