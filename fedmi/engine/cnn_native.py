@@ -152,9 +152,12 @@ class _Unit:
 
     def dgrad_fusable(self, add: bool = False) -> bool:
         """Whether this conv's DGRAD can take its producer BN's backward sums in the epilogue (dense tap
-        path, or the depthwise kernel) and, ``add``, a second incoming grad (dense tap path only)."""
+        path; the depthwise kernel with FEDMI_CNN_FUSE_DW_BN_BWD=1 -- measured 846 vs 832 ms per MobileNet
+        round with it on) and, ``add``, a second incoming grad (dense tap path only)."""
         if self.depthwise:
-            return not add
+            import os
+
+            return not add and os.environ.get("FEDMI_CNN_FUSE_DW_BN_BWD", "0") == "1"
         if self._fusable is None:
             self._fusable = (not self.depthwise and self.wd is not None and
                              conv.dgrad_fusable(self.in_shape(1), self.O, self.R, self.S, self.stride, self.pad,
@@ -511,7 +514,9 @@ class CNNNativeTrainer(LocalTrainer):
 
         self._side = None
         self.wgrad_ws2 = None
-        if device.type == "cuda" and os.environ.get("FEDMI_CNN_WGRAD_STREAM", "1") != "0":
+        # opt-in: measured slower (ResNet-18 1036 vs 983 ms per round, MobileNet 886 vs 832): the concurrent
+        # kernels compete for CUs / LDS and the split-K sizing assumes the whole chip (profiles/r3_cnn)
+        if device.type == "cuda" and os.environ.get("FEDMI_CNN_WGRAD_STREAM", "0") == "1":
             self._side = torch.cuda.Stream(device)
             self.wgrad_ws2 = torch.empty_like(self.wgrad_ws)
         # BN-backward two-level channel sums (replicated atomics + finalize; kept zero between uses)
