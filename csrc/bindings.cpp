@@ -140,9 +140,11 @@ static void fedmi_bind(py::module_& m) {
            py::call_guard<py::gil_scoped_release>())
       .def("run_epoch", [](LeNetEngine& e, uintptr_t st, bool use_graph) { e.run_epoch(S(st), use_graph); },
            py::call_guard<py::gil_scoped_release>())
-      .def("eval", [](LeNetEngine& e, uintptr_t st, uintptr_t images, uintptr_t labels, int n) {
-             e.eval(S(st), P<const uint8_t>(images), P<const int>(labels), n);
-           }, py::call_guard<py::gil_scoped_release>())
+      .def("eval", [](LeNetEngine& e, uintptr_t st, uintptr_t images, uintptr_t labels, int n, uintptr_t pk,
+                      uintptr_t params) {
+             e.eval(S(st), P<const uint8_t>(images), P<const int>(labels), n, P<const bf16>(pk), P<const float>(params));
+           }, py::arg("st"), py::arg("images"), py::arg("labels"), py::arg("n"), py::arg("pk") = 0,
+           py::arg("params") = 0, py::call_guard<py::gil_scoped_release>())
       .def("pack", [](LeNetEngine& e, uintptr_t st) { e.pack(S(st)); }, py::call_guard<py::gil_scoped_release>())
       .def("set_fuse_fc1", &LeNetEngine::set_fuse_fc1)
       .def("fuse_fc1", &LeNetEngine::fuse_fc1)

@@ -176,13 +176,16 @@ void LeNetEngine::run_epoch(hipStream_t st, bool use_graph) {
   check_hip(hipGraphLaunch(exec_, st), "GraphLaunch");
 }
 
-void LeNetEngine::eval(hipStream_t st, const uint8_t* images, const int* labels, int n) {
+void LeNetEngine::eval(hipStream_t st, const uint8_t* images, const int* labels, int n, const bf16* pk,
+                       const float* params) {
   using namespace lenet;
   if (n <= 0 || n > b_.act2_rows) throw std::invalid_argument("LeNetEngine::eval: n exceeds act2 capacity");
-  launch_lenet_conv_fwd(st, images, 0, n, b_.pk, b_.params, seed_, b_.round_ctr, 0, b_.act2, nullptr, 0,
+  if (!pk) pk = b_.pk;
+  if (!params) params = b_.params;
+  launch_lenet_conv_fwd(st, images, 0, n, pk, params, seed_, b_.round_ctr, 0, b_.act2, nullptr, 0,
                         nullptr, nullptr, nullptr, b_.eval_stats);
-  if (!fuse_fc1_) launch_lenet_fc1_fwd(st, b_.act2, n, b_.pk, b_.params, b_.h1);
-  launch_lenet_fc_tail(st, fuse_fc1_ ? nullptr : b_.h1, b_.act2, labels, n, 0, b_.pk, b_.params, nullptr, nullptr,
+  if (!fuse_fc1_) launch_lenet_fc1_fwd(st, b_.act2, n, pk, params, b_.h1);
+  launch_lenet_fc_tail(st, fuse_fc1_ ? nullptr : b_.h1, b_.act2, labels, n, 0, pk, params, nullptr, nullptr,
                        nullptr, b_.eval_stats);
   check_hip(hipGetLastError(), "LeNetEngine::eval launch");
 }

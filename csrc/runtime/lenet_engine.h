@@ -61,8 +61,10 @@ class LeNetEngine {
   void step(hipStream_t st, int start, int nb, bool bump_round, bool reset_stats = false);
   // One local epoch over the schedule; graph replay when use_graph.
   void run_epoch(hipStream_t st, bool use_graph);
-  // Forward + CE/accuracy over n samples of an image set (eval mode).
-  void eval(hipStream_t st, const uint8_t* images, const int* labels, int n);
+  // Forward + CE/accuracy over n samples of an image set (eval mode).  pk / params (optional): read the
+  // model from these copies instead of the live buffers (an eval that overlaps the next round's training).
+  void eval(hipStream_t st, const uint8_t* images, const int* labels, int n, const bf16* pk = nullptr,
+            const float* params = nullptr);
   // Refresh the packed bf16 images from the fp32 master (after FedAvg/load).
   void pack(hipStream_t st);
   void set_sgd(SgdConfig sgd);

@@ -98,6 +98,9 @@ class LocalTrainer(abc.ABC):
 
     def set_test_data(self, data) -> None:
         """Replace the evaluation set (e.g. this client's slice of a data-parallel eval)."""
+        es = self.eval_stream()
+        if es is not None:
+            es.synchronize()                   # an overlapped eval may still read the old set
         t = data.to(self.device)
         if self.device.type == "cuda" and t.y.dtype != torch.int32:
             t.y = t.y.to(torch.int32)          # native engines read int32 labels
@@ -105,8 +108,13 @@ class LocalTrainer(abc.ABC):
 
     def eval_stats_raw(self) -> torch.Tensor:
         """Device-resident eval accumulator of the last :meth:`evaluate` (engine-specific layout);
-        :meth:`decode_stats` turns a host copy of it into :class:`EpochStats`."""
+        :meth:`decode_stats` turns a host copy of it into :class:`EpochStats`.  Valid on
+        :meth:`eval_stream` (device consumers order themselves after it)."""
         raise NotImplementedError
+
+    def eval_stream(self):
+        """The stream :meth:`evaluate` runs on when it overlaps later work (None: the current stream)."""
+        return None
 
     def decode_stats(self, raw: torch.Tensor) -> EpochStats:
         raise NotImplementedError

@@ -99,6 +99,8 @@ class LeNetNativeTrainer(LocalTrainer):
         self.load_state_dict(init_state)
         self._starts: List[int] = []
         self._sizes: List[int] = []
+        self._eval_overlap = os.environ.get("FEDMI_LENET_EVAL_OVERLAP", "1") == "1"
+        self._ev_stream = self._ev_params = self._ev_pk = None
 
     # ---- state -------------------------------------------------------------------
     @property
@@ -188,9 +190,32 @@ class LeNetNativeTrainer(LocalTrainer):
         return self._read_stats(0)
 
     def evaluate(self) -> None:
-        self.engine.eval(self._stream(), _ptr(self.test_set.x), _ptr(self.test_set.y), len(self.test_set))
+        """Eval of the current model.  Overlapped (default; FEDMI_LENET_EVAL_OVERLAP=0: in order): the weights
+        are snapshotted on the current stream and the eval kernels run on a side stream, so they fill the
+        CUs the next round's 128-workgroup training steps leave idle; the next round trains on the live
+        buffers meanwhile.  Readers: :meth:`eval_stats` waits for it, device consumers use
+        :meth:`eval_stream` (EvalHistory)."""
+        if not self._eval_overlap:
+            self.engine.eval(self._stream(), _ptr(self.test_set.x), _ptr(self.test_set.y), len(self.test_set))
+            return
+        main = torch.cuda.current_stream(self._device)
+        if self._ev_stream is None:
+            self._ev_stream = torch.cuda.Stream(self._device)
+            self._ev_params = torch.empty_like(self.params)
+            self._ev_pk = torch.empty_like(self.pk)
+        main.wait_stream(self._ev_stream)          # the previous eval is done with the snapshot
+        self._ev_params.copy_(self.params)
+        self._ev_pk.copy_(self.pk)
+        self._ev_stream.wait_stream(main)
+        self.engine.eval(native.stream_handle_of(self._ev_stream), _ptr(self.test_set.x), _ptr(self.test_set.y),
+                         len(self.test_set), _ptr(self._ev_pk), _ptr(self._ev_params))
+
+    def eval_stream(self):
+        return self._ev_stream if self._eval_overlap else None
 
     def eval_stats(self) -> EpochStats:
+        if self._eval_overlap and self._ev_stream is not None:
+            self._ev_stream.synchronize()
         return self._read_stats(1)
 
     def set_fuse_fc1(self, on: bool) -> None:

@@ -56,6 +56,11 @@ def stream_handle(device: torch.device | None = None) -> int:
     return int(torch.cuda.current_stream(device).cuda_stream)
 
 
+def stream_handle_of(stream: "torch.cuda.Stream") -> int:
+    """Raw hipStream_t of a given torch stream."""
+    return int(stream.cuda_stream)
+
+
 def on_gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 

@@ -177,12 +177,20 @@ class EvalHistory:
     def record(self) -> None:
         if self.n >= self.buf.shape[0]:
             raise IndexError("EvalHistory full")
-        self.buf[self.n].copy_(self.trainer.eval_stats_raw(), non_blocking=True)
+        es = self.trainer.eval_stream()
+        if es is None:
+            self.buf[self.n].copy_(self.trainer.eval_stats_raw(), non_blocking=True)
+        else:                                  # the eval runs overlapped on its own stream: copy there
+            with torch.cuda.stream(es):
+                self.buf[self.n].copy_(self.trainer.eval_stats_raw(), non_blocking=True)
         self.n += 1
 
     def reduce(self, group=None):
         from ..engine.base import EpochStats
 
+        es = self.trainer.eval_stream()
+        if es is not None:
+            torch.cuda.current_stream(self.buf.device).wait_stream(es)
         rows = self.buf[: self.n].cpu()
         vals = [self.trainer.decode_stats(rows[i]) for i in range(self.n)]
         t = torch.tensor([[s.loss_sum, s.correct, s.count] for s in vals], dtype=torch.float64).reshape(-1, 3)

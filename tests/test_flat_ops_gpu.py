@@ -148,3 +148,23 @@ def test_int8_roundtrip(nat, gpu_device):
     deq = (torch.round(pad.view(nch, 256) / s_ref[:, None]).clamp(-127, 127) * s_ref[:, None]).view(-1)[:n]
     assert torch.allclose(out, deq, atol=1e-6)
     assert torch.allclose(res, d - deq, atol=1e-6)
+
+
+def test_topk_ef_state_alternates_paths(nat, gpu_device):
+    """One state reused across calls that alternate between the 2-level (< 1 M entries) and 3-level paths
+    and between histogram parities: every call still selects exactly the top k."""
+    torch.manual_seed(3)
+    state = torch.zeros(nat.topk_state_bytes(), dtype=torch.uint8, device=gpu_device)
+    for n, k in ((1 << 21, 20000), (70001, 700), (300000, 3000), (1 << 21, 9000), (62006, 620)):
+        x = torch.randn(n, device=gpu_device)
+        g = torch.zeros(n, device=gpu_device)
+        r = torch.zeros(n, device=gpu_device)
+        cidx = torch.empty(2 * n, dtype=torch.int32, device=gpu_device)
+        ckey = torch.empty(2 * n, dtype=torch.int32, device=gpu_device)
+        idx = torch.full((k,), -1, dtype=torch.int32, device=gpu_device)
+        val = torch.zeros(k, device=gpu_device)
+        nat.topk_ef(S(), x.data_ptr(), g.data_ptr(), r.data_ptr(), n, k, state.data_ptr(), cidx.data_ptr(),
+                    ckey.data_ptr(), idx.data_ptr(), val.data_ptr())
+        torch.cuda.synchronize()
+        assert int(idx.min()) >= 0 and len(set(idx.tolist())) == k, n
+        assert torch.equal(val.abs().sort(descending=True).values, x.abs().topk(k).values), n
