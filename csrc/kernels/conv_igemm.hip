@@ -456,7 +456,9 @@ FEDMI_DEV bf16x8 frag_sw(const bf16* img, int i0, int kk, int lane) {
   return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((kc ^ (row & 7)) << 3));
 }
 
-template <int BN>
+// NST = 3: the DMA runs two K steps ahead (1 workgroup per CU at BN 128, 2 at BN 64); NST = 2: classic
+// double buffer, one step ahead, half the LDS so one more workgroup fits per CU (FEDMI_TAP_STAGES=2).
+template <int BN, int NST = 3>
 __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                 bf16* __restrict__ out, float* __restrict__ part,
                                                 double* __restrict__ stats, const float* __restrict__ shift,
@@ -467,8 +469,10 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
   constexpr int NB = BN / 32;
   constexpr int STAGE = (BM + BN) * 64;  // elements
   constexpr int TM = 4, TN = BN / 32;    // 16x16 fragments per wave: 64 x BN/2
-  constexpr int NST = 3;                 // LDS stages: DMA runs two K steps ahead
-  __shared__ __attribute__((aligned(16))) bf16 smem[NST * STAGE];
+  static_assert(NST == 2 || NST == 3, "conv_tap: 2 or 3 LDS stages");
+  // the epilogue reuses the stages for the bf16 tile and its partial sums
+  constexpr int EPI = BM * (BN + 8) + 2 * 3 * 256 * 8;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NST * STAGE > EPI ? NST * STAGE : EPI];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (g.O + BN - 1) / BN;
@@ -536,10 +540,10 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
   // in flight), barrier (step t visible everywhere AND every wave is done reading
   // step t-1's stage), refill that stage with step t+2, then MFMAs on step t.
   if (kb < ke) issue(kb, 0);
-  if (kb + 1 < ke) issue(kb + 1, 1);
+  if (NST == 3 && kb + 1 < ke) issue(kb + 1, 1);
   for (int t = kb; t < ke; ++t) {
     const int stg = (t - kb) % NST;
-    if (t + 1 < ke) {
+    if (NST == 3 && t + 1 < ke) {
       if constexpr (NA + NB == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
@@ -548,7 +552,10 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 2 < ke) issue(t + 2, (stg + 2) % NST);
+    // NST 3: refill the stage step t-1 used with step t+2; NST 2: the same stage with step t+1 (every
+    // wave is past step t-1's reads once it passed this barrier)
+    if (NST == 3 && t + 2 < ke) issue(t + 2, (stg + 2) % NST);
+    if (NST == 2 && t + 1 < ke) issue(t + 1, stg ^ 1);
     const bf16* As = smem + stg * STAGE;
     const bf16* Bs = As + BM * 64;
 #pragma unroll
@@ -1750,12 +1757,16 @@ static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const b
   dim3 grid((unsigned)tiles, 1, (unsigned)splits);
   float* part = splits > 1 ? ws : nullptr;
   const BnSums tbs = part ? BnSums{} : bs;
-  if (BN == 128)
-    hipLaunchKernelGGL(conv_tap<128>, grid, dim3(256), 0, st, in, wt, out, part, part ? nullptr : stats, shift, g, rm, kps,
-                       part ? nullptr : res, tbs);
-  else
-    hipLaunchKernelGGL(conv_tap<64>, grid, dim3(256), 0, st, in, wt, out, part, part ? nullptr : stats, shift, g, rm, kps,
-                       part ? nullptr : res, tbs);
+  static const bool two = [] { const char* e = std::getenv("FEDMI_TAP_STAGES"); return e && e[0] == '2'; }();
+  double* tst = part ? nullptr : stats;
+  const bf16* trs = part ? nullptr : res;
+  if (BN == 128) {
+    if (two) hipLaunchKernelGGL((conv_tap<128, 2>), grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
+    else hipLaunchKernelGGL((conv_tap<128, 3>), grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
+  } else {
+    if (two) hipLaunchKernelGGL((conv_tap<64, 2>), grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
+    else hipLaunchKernelGGL((conv_tap<64, 3>), grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
+  }
   if (splits > 1) {
     const int VR = g.O / 8;
     const int tb = (256 / VR) * VR;
