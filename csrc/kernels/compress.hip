@@ -206,20 +206,18 @@ __global__ __launch_bounds__(256) void dequant_accum_kernel(const signed char* _
 }
 
 // ---------------------------------------------------------------------------
-// Fused error-feedback top-k (the default path): 3 launches (4 from 1 M entries), 2 full passes over
-// the state.
+// Fused error-feedback top-k (the default path): 4 launches, 2 full passes over the state.
 //
 //   K1 tk_delta_hist   r <- x - g + r (the residual buffer holds d from here on), and a
 //                      histogram of the top 11 bits of |d| (key bits 30..20: exponent + 3
 //                      mantissa bits, each bin ~9 % of magnitude), LDS-privatised per
-//                      workgroup, nonzero bins added to the global histogram of this call's parity.
-//   K2 tk_compact1     every workgroup scans the 2048-bin histogram for the bin b1 holding the k-th
-//                      largest key (no single-workgroup pick launch in between); keys in bins > b1
-//                      are selected outright (idx/val appended, r <- 0); keys in bin b1 become
-//                      candidates (index + key appended).  Appends are wave-aggregated, staged per
-//                      workgroup.  Clears the other parity's histograms for the next call.
-//   (large n: K3 tk_compact2 -- level-2 bin from the candidates' histogram the same way)
-//   K3 tk_select2      one workgroup: exact selection of the remaining `need` among the
+//                      workgroup, nonzero bins added to the global histogram.
+//   K2 tk_pick1        one workgroup: the bin b1 holding the k-th largest key (block scan);
+//                      re-zeroes the histogram and the append counters for the next call.
+//   K3 tk_compact1     keys in bins > b1 are selected outright (idx/val appended, r <- 0);
+//                      keys in bin b1 become candidates (index + key appended).  Appends are
+//                      wave-aggregated (ballot + popcount, one global atomic per wave).
+//   K4 tk_select2      one workgroup: exact selection of the remaining `need` among the
 //                      candidates (2 LDS radix passes over the low 20 key bits; exact ties
 //                      resolved by the smallest indices, 3 more passes only when needed).
 //
@@ -228,15 +226,11 @@ __global__ __launch_bounds__(256) void dequant_accum_kernel(const signed char* _
 // unique and scatter_add_ranked applies the ranks one after another.
 constexpr int kTkBins1 = 2048;
 constexpr long kTkThreeLevel = 1 << 20;   // n at which the 3-level path takes over
-// The histograms are double-buffered by call parity: the compaction kernels derive the boundary bin
-// themselves (every workgroup scans the 8 KB histogram) and clear the OTHER parity's buffer for the next
-// call, so no single-workgroup pick launch sits between the passes.  The last kernel of a call resets
-// the append counters and bumps the call counter.
 struct TopKState {
-  unsigned hist[2][kTkBins1];
-  int b1, n_above, need, out_cnt, cand_cnt, call, pad[2];
+  unsigned hist[kTkBins1];
+  int b1, n_above, need, out_cnt, cand_cnt, pad[3];
   // 3-level path (large n): level-2 histogram of the candidates' key bits 19..9
-  unsigned hist2[2][kTkBins1];
+  unsigned hist2[kTkBins1];
   int b2, n_above2, need2, out2_cnt, cand2_cnt, pad2[3];
 };
 
@@ -291,18 +285,16 @@ __global__ __launch_bounds__(256) void tk_delta_hist_kernel(const float* __restr
   }
   __syncthreads();
   // rotated bin order per workgroup: concurrent workgroups hit different global bins at a time
-  unsigned* gh = st->hist[st->call & 1];
   for (int j = threadIdx.x; j < kTkBins1; j += 256) {
     const int i = (j + (int)blockIdx.x * 64) & (kTkBins1 - 1);
-    if (h[i]) atomicAdd(&gh[i], h[i]);
+    if (h[i]) atomicAdd(&st->hist[i], h[i]);
   }
 }
 
-// bin b of h[0..nb) (nb a multiple of blockDim.x) such that above(b) < k <= above(b) + h[b], scanning
-// from the TOP bin down; above(b) = sum of the bins > b.  Result in res[0..1].
+// 1024 threads: bin b of h[0..nb) (nb = 1024 or 2048) such that above(b) < k <= above(b) + h[b],
+// scanning from the TOP bin down; above(b) = sum of the bins > b.  Result in res[0..1].
 FEDMI_DEV void tk_find_top(const unsigned* h, int nb, unsigned k, unsigned* scratch, unsigned* res) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, per = nb / (int)blockDim.x;
-  const int nw = (int)blockDim.x >> 6;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, per = nb >> 10;
   unsigned s = 0u;
   for (int j = 0; j < per; ++j) s += h[nb - 1 - (t * per + j)];
   unsigned inc = s;
@@ -315,7 +307,7 @@ FEDMI_DEV void tk_find_top(const unsigned* h, int nb, unsigned k, unsigned* scra
   __syncthreads();
   if (t == 0) {
     unsigned a = 0u;
-    for (int q = 0; q < nw; ++q) { const unsigned v = scratch[q]; scratch[16 + q] = a; a += v; }
+    for (int q = 0; q < 16; ++q) { const unsigned v = scratch[q]; scratch[16 + q] = a; a += v; }
   }
   __syncthreads();
   const unsigned excl = scratch[16 + w] + inc - s;
@@ -328,6 +320,44 @@ FEDMI_DEV void tk_find_top(const unsigned* h, int nb, unsigned k, unsigned* scra
     }
   }
   __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void tk_pick1_kernel(TopKState* __restrict__ st, int k) {
+  __shared__ unsigned h[kTkBins1];
+  __shared__ unsigned scratch[32], res[2];
+  for (int i = threadIdx.x; i < kTkBins1; i += 1024) {
+    h[i] = st->hist[i];
+    st->hist[i] = 0u;                        // zero for the next call (graph-safe: no memset node)
+  }
+  __syncthreads();
+  tk_find_top(h, kTkBins1, (unsigned)k, scratch, res);
+  if (threadIdx.x == 0) {
+    st->b1 = (int)res[0];
+    st->n_above = (int)res[1];
+    st->need = k - (int)res[1];
+    st->out_cnt = 0;
+    st->cand_cnt = 0;
+  }
+}
+
+// level 2 (large n): the bin b2 of key bits 19..9 holding the need-th largest candidate
+__global__ __launch_bounds__(1024) void tk_pick2_kernel(TopKState* __restrict__ st) {
+  __shared__ unsigned h[kTkBins1];
+  __shared__ unsigned scratch[32], res[2];
+  for (int i = threadIdx.x; i < kTkBins1; i += 1024) {
+    h[i] = st->hist2[i];
+    st->hist2[i] = 0u;
+  }
+  __syncthreads();
+  const int need = st->need;
+  tk_find_top(h, kTkBins1, (unsigned)need, scratch, res);
+  if (threadIdx.x == 0) {
+    st->b2 = (int)res[0];
+    st->n_above2 = (int)res[1];
+    st->need2 = need - (int)res[1];
+    st->out2_cnt = 0;
+    st->cand2_cnt = 0;
+  }
 }
 
 // wave-aggregated append into a block-local (LDS) counter; returns this lane's slot (valid if flag)
@@ -347,32 +377,15 @@ FEDMI_DEV int tk_append_lds(int* counter, bool flag) {
 // address each (2.4 ms at 11 M entries, measured).
 constexpr int kTkStage = 4096;   // >= 2 iterations' worth (8 x 256 per iteration)
 template <bool H2>
-__global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r, long n, int k, TopKState* __restrict__ st,
+__global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r, long n, TopKState* __restrict__ st,
                                                           int* __restrict__ idx, float* __restrict__ val,
                                                           int* __restrict__ cidx, unsigned* __restrict__ ckey) {
   __shared__ int s_si[kTkStage], s_ci[kTkStage];   // 4 x 16 KB of LDS
   __shared__ float s_sv[kTkStage];
   __shared__ unsigned s_ck[kTkStage];
   __shared__ unsigned h2[H2 ? kTkBins1 : 1];
-  __shared__ unsigned hh[kTkBins1];
-  __shared__ unsigned scratch[32], res[2];
   __shared__ int n_s, n_c, b_s, b_c;
-  // every workgroup: the level-1 boundary bin from this call's histogram (8 KB), the other parity's
-  // histograms cleared for the next call
-  const int par = st->call & 1;
-  for (int i = threadIdx.x; i < kTkBins1; i += 256) hh[i] = st->hist[par][i];
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < kTkBins1; i += (long)gridDim.x * 256) {
-    st->hist[par ^ 1][i] = 0u;
-    st->hist2[par ^ 1][i] = 0u;     // (every call: a state may alternate between the 2- and 3-level paths)
-  }
-  __syncthreads();
-  tk_find_top(hh, kTkBins1, (unsigned)k, scratch, res);
-  const unsigned b1 = res[0];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->b1 = (int)res[0];
-    st->n_above = (int)res[1];
-    st->need = k - (int)res[1];
-  }
+  const unsigned b1 = (unsigned)st->b1;
   const long stride = (long)gridDim.x * 256;
   if (threadIdx.x == 0) { n_s = 0; n_c = 0; }
   if (H2)
@@ -421,7 +434,7 @@ __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r,
     __syncthreads();
     for (int j = threadIdx.x; j < kTkBins1; j += 256) {
       const int i = (j + (int)blockIdx.x * 64) & (kTkBins1 - 1);
-      if (h2[i]) atomicAdd(&st->hist2[par][i], h2[i]);
+      if (h2[i]) atomicAdd(&st->hist2[i], h2[i]);
     }
   }
 }
@@ -435,21 +448,9 @@ __global__ __launch_bounds__(256) void tk_compact2_kernel(float* __restrict__ r,
   __shared__ int s_si[kTkStage], s_ci[kTkStage];
   __shared__ float s_sv[kTkStage];
   __shared__ unsigned s_ck[kTkStage];
-  __shared__ unsigned hh[kTkBins1];
-  __shared__ unsigned scratch[32], res[2];
   __shared__ int n_s, n_c, b_s, b_c;
-  const int c = st->cand_cnt, nab = st->n_above, need = st->need;
-  // every workgroup: the level-2 boundary bin (key bits 19..9) of the need-th largest candidate
-  const int par = st->call & 1;
-  for (int i = threadIdx.x; i < kTkBins1; i += 256) hh[i] = st->hist2[par][i];
-  __syncthreads();
-  tk_find_top(hh, kTkBins1, (unsigned)need, scratch, res);
-  const unsigned b2 = res[0];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->b2 = (int)res[0];
-    st->n_above2 = (int)res[1];
-    st->need2 = need - (int)res[1];
-  }
+  const int c = st->cand_cnt, nab = st->n_above;
+  const unsigned b2 = (unsigned)st->b2;
   const long stride = (long)gridDim.x * 256;
   if (threadIdx.x == 0) { n_s = 0; n_c = 0; }
   __syncthreads();
@@ -599,15 +600,6 @@ __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r,
       }
     }
   }
-  // the call's last kernel: append counters back to zero, next call on the other histogram parity
-  __syncthreads();
-  if (t == 0) {
-    st->out_cnt = 0;
-    st->cand_cnt = 0;
-    st->out2_cnt = 0;
-    st->cand2_cnt = 0;
-    st->call += 1;
-  }
 }
 
 int grid_for(long n) {
@@ -649,7 +641,7 @@ size_t topk_state_bytes() { return sizeof(TopKState); }
 
 // Fused error-feedback exact top-k (see tk_* kernels).  residual: d is built IN it and the
 // selected entries are zeroed (= the new residual); state: topk_state_bytes(), zero on first
-// use (every call leaves it ready for the next); cidx/ckey: candidate scratch of 2n entries each.
+// use (left zero by every call); cidx/ckey: candidate scratch of 2n entries each.
 void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* residual, long n, int k, void* state,
                     int* cidx, unsigned* ckey, int* idx, float* val) {
   TopKState* s = reinterpret_cast<TopKState*>(state);
@@ -661,9 +653,10 @@ void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* resid
     hipLaunchKernelGGL(tk_delta_hist_kernel<true>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s);
   else
     hipLaunchKernelGGL(tk_delta_hist_kernel<false>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s);
+  hipLaunchKernelGGL(tk_pick1_kernel, dim3(1), dim3(1024), 0, st, s, k);
   const int cblocks = (int)std::min<long>(2048, std::max<long>(1, (n + 2 * 2048 - 1) / (2 * 2048)));
   if (n < kTkThreeLevel) {
-    hipLaunchKernelGGL(tk_compact1_kernel<false>, dim3(cblocks), dim3(256), 0, st, residual, n, k, s, idx, val, cidx,
+    hipLaunchKernelGGL(tk_compact1_kernel<false>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx,
                        ckey);
     hipLaunchKernelGGL(tk_select2_kernel<2>, dim3(1), dim3(1024), 0, st, residual, s, cidx, ckey, idx, val);
     return;
@@ -673,8 +666,8 @@ void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* resid
   // level-3 list of a few hundred for the single-workgroup exact select
   int* cidx2 = cidx + n;                     // second half of the 2n-entry candidate scratch
   unsigned* ckey2 = ckey + n;
-  hipLaunchKernelGGL(tk_compact1_kernel<true>, dim3(cblocks), dim3(256), 0, st, residual, n, k, s, idx, val, cidx,
-                     ckey);
+  hipLaunchKernelGGL(tk_compact1_kernel<true>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx, ckey);
+  hipLaunchKernelGGL(tk_pick2_kernel, dim3(1), dim3(1024), 0, st, s);
   const int c2blocks = (int)std::min<long>(1024, std::max<long>(1, (n / 50 + 2047) / 2048));
   hipLaunchKernelGGL(tk_compact2_kernel, dim3(c2blocks), dim3(256), 0, st, residual, s, cidx, ckey, idx, val, cidx2,
                      ckey2);

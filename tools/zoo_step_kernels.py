@@ -21,8 +21,8 @@ fam_t, fam_n = defaultdict(float), defaultdict(int)
 busy = 0.0
 for r in rows[a:b]:
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-    k = r["Kernel_Name"]
-    k = k.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")[:70]
+    k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+    k = k.split("(")[0][:70] or r["Kernel_Name"][:70]
     fam_t[k] += d
     fam_n[k] += 1
     busy += d
