@@ -846,15 +846,23 @@ def _conv_kind(C, O, groups, k, stride, pad, dil):
     return "gconv"
 
 
-def _pad_c(t: torch.Tensor, c8: int) -> torch.Tensor:
-    """NHWC bf16 [.., C] (possibly a channel slice) -> contiguous [.., c8], zero channels C..c8."""
+def _pad_c(t: torch.Tensor, c8: int, cache: bool = False) -> torch.Tensor:
+    """NHWC bf16 [.., C] (possibly a channel slice) -> contiguous [.., c8], zero channels C..c8.  ``cache``:
+    reuse / keep the padded copy for the rest of the NativeMode block (a conv's input is padded by its
+    forward and again by its weight gradient)."""
     C = t.shape[-1]
     if C == c8 and t.is_contiguous():
         return t
+    mode = NativeMode.current
+    key = ("pad", t.data_ptr(), tuple(t.shape), tuple(t.stride()), c8)
+    if cache and mode is not None and key in mode._wcache:
+        return mode._wcache[key][1]
     out = torch.empty(*t.shape[:-1], c8, dtype=torch.bfloat16, device=t.device)
     if c8 > C:
         fill_(out[..., C:], 0.0)
     ew(out[..., :C], [t], EW_COPY)
+    if cache and mode is not None:
+        mode._wcache[key] = (t, out)
     return out
 
 
@@ -878,12 +886,43 @@ def _pad_o(w32: torch.Tensor, o8: int) -> torch.Tensor:
     return out
 
 
+def _packed(w32, O8: int, C8: int, st: int, pd: int, need_wd: bool = False):
+    """bf16 [O8, R, S, C8] conv image of fp32 ``w32`` (and with ``need_wd`` its DGRAD image), packed once per
+    NativeMode block: the forward packs, the backward of the same step reuses (the weights only change at
+    the SGD, outside the block) -- per conv one pack launch, and the O-padding copies, fewer per step."""
+    mode = NativeMode.current
+    cache = mode._wcache if mode is not None else None
+    key = (w32.data_ptr(), tuple(w32.shape), tuple(w32.stride()), O8, C8, st, pd)
+    ent = cache.get(key) if cache is not None else None
+    if ent is None:
+        ent = {}
+        if cache is not None:
+            cache[key] = (w32, ent)          # holds w32: the pointer key stays valid for the block
+    else:
+        ent = ent[1]
+    O, Cw, R, S = w32.shape
+    if "wp" not in ent:
+        if O8 == O and w32.is_contiguous():
+            ent["wp"] = CV.pack_weight(w32, c_pad=C8)
+        else:
+            wp = torch.empty(O8, R, S, C8, dtype=torch.bfloat16, device=w32.device)
+            fill_(wp[O:], 0.0)
+            CV.pack_weight(w32.contiguous(), c_pad=C8, out=wp[:O])
+            ent["wp"] = wp
+    if need_wd and "wd" not in ent:
+        w8 = _pad_o(w32, O8)
+        wd = torch.empty(CV.dgrad_image_numel(w8.shape, C8), dtype=torch.bfloat16, device=w32.device)
+        CV.dgrad_pack_weights([(w8, wd, st, pd, C8)])
+        ent["wd"] = wd
+    return ent["wp"], ent.get("wd")
+
+
 def _dense_fwd(xh, w32, st, pd, out=None):
     """One group: y [N,P,Q,Og] = conv(xh [N,H,W,Cg] NHWC bf16 (a view is fine), w32 [Og,Cg,R,S])."""
     Og, Cg, R, S = w32.shape
     C8, O8 = CV.pad8(Cg), CV.pad8(Og)
-    xp = _pad_c(xh, C8)
-    wp = CV.pack_weight(_pad_o(w32, O8), c_pad=C8)
+    xp = _pad_c(xh, C8, cache=True)
+    wp, _ = _packed(w32, O8, C8, st, pd)
     y = CV.conv2d_fwd(xp, wp, st, pd, ws=_ws(xh.device, CV.fd_ws_floats(xp.shape, O8, R, S, st, pd)))
     return _unpad_c(y, Og, out)
 
@@ -896,20 +935,15 @@ def _dense_bwd(xh, gy, w32, st, pd, need_dx, need_dw, dx_out=None, dw_out=None):
     gyp = _pad_c(gy, O8)
     dx = dw = None
     if need_dx:
-        w8 = _pad_o(w32, O8)
-        wp = CV.pack_weight(w8, c_pad=C8)
-        wd = None
-        if CV.dgrad_eligible(O8):
-            wd = torch.empty(CV.dgrad_image_numel(w8.shape, C8), dtype=torch.bfloat16, device=xh.device)
-            CV.dgrad_pack_weights([(w8, wd, st, pd, C8)])
+        wp, wd = _packed(w32, O8, C8, st, pd, need_wd=CV.dgrad_eligible(O8))
         xs = (N, H, W, C8)
         d = CV.conv2d_dgrad(gyp, wp, xs, st, pd, wd=wd, ws=_ws(xh.device, CV.fd_ws_floats(xs, O8, R, S, st, pd)))
         dx = _unpad_c(d, Cg, dx_out)
     if need_dw:
         if dw_out is not None and O8 == Og:
-            dw = CV.conv2d_wgrad(_pad_c(xh, C8), gyp, R, S, st, pd, Cw=Cg, out=dw_out)
+            dw = CV.conv2d_wgrad(_pad_c(xh, C8, cache=True), gyp, R, S, st, pd, Cw=Cg, out=dw_out)
         else:
-            dw = CV.conv2d_wgrad(_pad_c(xh, C8), gyp, R, S, st, pd, Cw=Cg)[:Og]
+            dw = CV.conv2d_wgrad(_pad_c(xh, C8, cache=True), gyp, R, S, st, pd, Cw=Cg)[:Og]
             if dw_out is not None:
                 dw = ew(dw_out, [dw], EW_COPY)
     return dx, dw
@@ -1086,6 +1120,7 @@ class NativeMode(TorchDispatchMode):
         self._pend_thr: Optional[_PendingThr] = None
         self._dead = {}                 # storage ptr -> materialiser of a tensor a fused op never wrote
         self.fused = collections.Counter()
+        self._wcache = {}               # packed conv weights of the current block (see _packed)
 
     def _defer(self, t: torch.Tensor, materialize) -> None:
         self._dead[t.untyped_storage().data_ptr()] = materialize
@@ -1139,6 +1174,7 @@ class NativeMode(TorchDispatchMode):
     def __enter__(self):
         self._prev = NativeMode.current
         NativeMode.current = self
+        self._wcache = {}
         self._fn_mode = _MixedDtypeConv()
         self._fn_mode.__enter__()
         return super().__enter__()
@@ -1148,6 +1184,7 @@ class NativeMode(TorchDispatchMode):
             self._flush()
         finally:
             self._dead.clear()
+            self._wcache = {}
         NativeMode.current = self._prev
         try:
             return super().__exit__(*exc)

@@ -20,6 +20,10 @@ for st in $STAGES; do
         head -40 $O/kernels_$m.txt >> $S
         rm -f $tr
       done ;;
+    bench)
+      timeout -k 10 560 python tools/bench_hybrid.py ${ZOO:-densenet_cifar RegNetY_400MF} \
+        > $O/bench_hybrid.jsonl 2> $O/bench_hybrid.err; rc=$?
+      echo "bench rc=$rc" >> $S; cat $O/bench_hybrid.jsonl >> $S; stop $rc ;;
     gap)
       for lr in 0.02 0.005; do
         timeout -k 10 500 python tools/zoo_learning.py DPN26 RegNetY_400MF ShuffleNetG2 --seeds 0 1 2 --epochs 8 --lr $lr \
