@@ -11,6 +11,8 @@
 
 namespace py = pybind11;
 
+#include "kernels/common.h"
+
 namespace fedmi {
 constexpr int ZMAXD = 6;
 struct ZTensor {
@@ -23,6 +25,7 @@ struct ZTensor {
 void launch_ew(hipStream_t, const ZTensor&, const ZTensor*, int, int, float, float, uint32_t, const int*, int, int);
 void launch_ctr_bump(hipStream_t, int*);
 long long reduce_rows_ws_floats(long long, int);
+void launch_pad_rows(hipStream_t, const bf16*, long long, int, bf16*, int, long long);
 void launch_reduce_rows(hipStream_t, const void*, int, long long, const void*, int, long long, const float*, int,
                         long long, int, float*, long long, float*, float*);
 void launch_reduce(hipStream_t, const ZTensor&, const ZTensor&, const ZTensor&, const ZTensor&, const void*, int,
@@ -96,6 +99,9 @@ void fedmi_bind_zoo(py::module_& m) {
   });
   m.def("z_reduce_ws_floats", &fedmi::reduce_ws_floats);
   m.def("z_reduce_rows_ws_floats", &fedmi::reduce_rows_ws_floats);
+  m.def("z_pad_rows", [](uintptr_t st, uintptr_t src, long long lds, int C, uintptr_t dst, int C8, long long rows) {
+    fedmi::launch_pad_rows(S(st), reinterpret_cast<const bf16*>(src), lds, C, reinterpret_cast<bf16*>(dst), C8, rows);
+  });
   m.def("z_reduce_rows", [](uintptr_t st, uintptr_t a, int a_dt, long long lda, uintptr_t b, int b_dt, long long ldb,
                             uintptr_t shift, int C, long long M, int op, uintptr_t part, long long part_floats,
                             uintptr_t acc, uintptr_t acc2) {

@@ -594,9 +594,15 @@ __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r,
       if (sel) {
         const int lane = t & 63;
         const int pos = nab + base + (int)__popcll(msk & (lane ? (~0ull >> (64 - lane)) : 0ull));
-        idx[pos] = ci[u];
-        val[pos] = dv[u];
-        r[ci[u]] = 0.f;
+        // never past the k-entry payload (a selection larger than need would otherwise write beyond idx /
+        // val into whatever the allocator placed after them); an overflow is flagged in the state
+        if (pos < nab + (int)m) {
+          idx[pos] = ci[u];
+          val[pos] = dv[u];
+          r[ci[u]] = 0.f;
+        } else {
+          st->pad[0] = 1;
+        }
       }
     }
   }

@@ -317,6 +317,84 @@ FEDMI_DEV float ordered_slab_sum(const float* part, int slabs, long long pitch, 
   return lane == 0 ? red[0][el] + red[1][el] + red[2][el] + red[3][el] : 0.f;
 }
 
+// bf16 load of VW channels, no dtype branch (fast path of the row reduction)
+template <int VW>
+FEDMI_DEV void vload_bf(const void* p, long long off, float* v) {
+  if constexpr (VW == 8) {
+    const bf16x8 q = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(p) + off);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (float)q[u];
+  } else {
+    const bf16x4 q = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const bf16*>(p) + off);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (float)q[u];
+  }
+}
+
+// rows [r0 + rl, r1) step RL of one channel vector, U rows per pass with every load issued first (OPK 0: sum
+// of a, 1: sum / sum of squares of a - shift, 2: sum a / sum a * (b - shift); HF: a masked by f > thr)
+template <int VW, bool BF, bool HF, int OPK>
+FEDMI_DEV void rows_pass(const void* a, long long lda, const void* b, long long ldb, const void* f, long long ldf,
+                         float thr, const float* sh, int v, int rl, int RL, long long r0, long long r1, float* s1,
+                         float* s2) {
+  static_assert(BF, "bf16 operands only");
+  constexpr int U = 4;
+  for (long long rb = r0 + rl; rb < r1; rb += (long long)U * RL) {
+    float x[U][VW], m[U][VW], y[U][VW];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const long long rr = rb + (long long)k * RL;
+      const long long r = rr < r1 ? rr : rb;
+      vload_bf<VW>(a, r * lda + v * VW, x[k]);
+      if constexpr (HF) vload_bf<VW>(f, r * ldf + v * VW, m[k]);
+      if constexpr (OPK == 2) vload_bf<VW>(b, r * ldb + v * VW, y[k]);
+    }
+    // dead rows (past r1) contribute exact zeros through selects, never through an extra multiply: the
+    // accumulation expressions (and their FMA contraction) stay those of the one-row loop
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const bool live = rb + (long long)k * RL < r1;
+#pragma unroll
+      for (int u = 0; u < VW; ++u) {
+        float xv = live ? x[k][u] : 0.f;
+        if constexpr (HF) xv = m[k][u] > thr ? xv : 0.f;
+        if constexpr (OPK == 0) {
+          s1[u] += xv;
+        } else if constexpr (OPK == 1) {
+          const float d = live ? xv - sh[u] : 0.f;
+          s1[u] += d;
+          s2[u] += d * d;
+        } else {
+          const float yv = live ? y[k][u] - sh[u] : 0.f;
+          s1[u] += xv;
+          s2[u] += xv * yv;
+        }
+      }
+    }
+  }
+}
+
+// ---- channel pad: dst [rows][C8] (compact) = src [rows][C] (row stride lds, any 2-byte alignment), zero
+// channels C..C8; one launch for the fill + copy pair.  One thread per 8-channel destination vector.
+__global__ __launch_bounds__(256) void pad_rows_kernel(const bf16* __restrict__ src, long long lds, int C,
+                                                       bf16* __restrict__ dst, int C8, long long rows, int vec) {
+  const int VD = C8 >> 3;
+  const long long n = rows * VD;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long r = i / VD;
+    const int c0 = (int)(i - r * VD) * 8;
+    bf16x8 o;
+    const bf16* sp = src + r * lds + c0;
+    if (vec && c0 + 8 <= C) {
+      o = *reinterpret_cast<const bf16x8*>(sp);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) o[u] = c0 + u < C ? sp[u] : (bf16)0.f;
+    }
+    *reinterpret_cast<bf16x8*>(dst + r * C8 + c0) = o;
+  }
+}
+
 // ---- row reduction of a [M, C] row-major matrix (ld = row stride), C % 8 == 0 ------------------
 // The channels-last case of the BN moments / bias gradients: a thread owns 8 channels (one 16-byte
 // load per row), RL = 256 / (C/8) row lanes per block, grid.y row slabs; per-slab partials go to
@@ -342,28 +420,40 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_d
     for (int u = 0; u < VW; ++u) sh[u] = shift ? shift[v * VW + u] : 0.f;
     const long long per = (M + gridDim.y - 1) / gridDim.y;
     const long long r0 = (long long)blockIdx.y * per, r1 = min(M, r0 + per);
-    for (long long r = r0 + rl; r < r1; r += RL) {
-      float x[VW];
-      vload<VW>(a, a_dt, r * lda + v * VW, x);
-      if (f) {                                   // a := threshold_backward(a, f) = f > thr ? a : 0
-        float m[VW];
-        vload<VW>(f, f_dt, r * ldf + v * VW, m);
+    // U rows per pass, every load of the pass issued before the first use (clamped rows, masked): one
+    // memory latency per U rows instead of per row; dtypes / operands are compile-time in the pass
+    const bool dot = op != RD_SUM && op != RD_SUMSQ_SHIFT;
+    const bool bf = a_dt == 1 && (!f || f_dt == 1) && (!dot || b_dt == 1);
+    const int opk = op == RD_SUM ? 0 : op == RD_SUMSQ_SHIFT ? 1 : 2;
+#define FEDMI_ROWS(BF, HF, OPK) rows_pass<VW, BF, HF, OPK>(a, lda, b, ldb, f, ldf, thr, sh, v, rl, RL, r0, r1, s1, s2)
+    if (bf) {
+      if (f) { if (opk == 0) FEDMI_ROWS(true, true, 0); else if (opk == 1) FEDMI_ROWS(true, true, 1); else FEDMI_ROWS(true, true, 2); }
+      else { if (opk == 0) FEDMI_ROWS(true, false, 0); else if (opk == 1) FEDMI_ROWS(true, false, 1); else FEDMI_ROWS(true, false, 2); }
+    } else {
+      for (long long r = r0 + rl; r < r1; r += RL) {   // generic dtypes (fp32 operands): one row at a time
+        float x[VW];
+        vload<VW>(a, a_dt, r * lda + v * VW, x);
+        if (f) {
+          float m[VW];
+          vload<VW>(f, f_dt, r * ldf + v * VW, m);
 #pragma unroll
-        for (int u = 0; u < VW; ++u) x[u] = m[u] > thr ? x[u] : 0.f;
-      }
-      if (op == RD_SUM) {
+          for (int u = 0; u < VW; ++u) x[u] = m[u] > thr ? x[u] : 0.f;
+        }
+        if (opk == 0) {
 #pragma unroll
-        for (int u = 0; u < VW; ++u) s1[u] += x[u];
-      } else if (op == RD_SUMSQ_SHIFT) {
+          for (int u = 0; u < VW; ++u) s1[u] += x[u];
+        } else if (opk == 1) {
 #pragma unroll
-        for (int u = 0; u < VW; ++u) { const float d = x[u] - sh[u]; s1[u] += d; s2[u] += d * d; }
-      } else {
-        float y[VW];
-        vload<VW>(b, b_dt, r * ldb + v * VW, y);
+          for (int u = 0; u < VW; ++u) { const float d = x[u] - sh[u]; s1[u] += d; s2[u] += d * d; }
+        } else {
+          float y[VW];
+          vload<VW>(b, b_dt, r * ldb + v * VW, y);
 #pragma unroll
-        for (int u = 0; u < VW; ++u) { s1[u] += x[u]; s2[u] += x[u] * (y[u] - sh[u]); }
+          for (int u = 0; u < VW; ++u) { s1[u] += x[u]; s2[u] += x[u] * (y[u] - sh[u]); }
+        }
       }
     }
+#undef FEDMI_ROWS
   }
   // tree over the row lanes of each channel vector
 #pragma unroll
@@ -973,6 +1063,40 @@ __global__ __launch_bounds__(256) void gconv_wgrad_kernel(GConv g, float* part, 
   float acc[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) acc[u] = 0.f;
+  if (vec && g.y.dtype == 1) {
+    // bf16 channels-last fast path: 8 output columns per pass, all 16 loads (8 dy scalars, 8 x vectors)
+    // issued before the first use -- clamped addresses and a 0/1 mask instead of per-load branches, so the
+    // pass costs one memory latency (the scalar loop paid one per pixel: ~300 us per RegNetY launch)
+    const bf16* yp = reinterpret_cast<const bf16*>(g.y.p);
+    const bf16* xp = reinterpret_cast<const bf16*>(g.x.p);
+    const long long ys3 = g.y.stride[3], xs3 = g.x.stride[3];
+    for (long long row = row0; row < row1; ++row) {
+      const long long n = row / P, p = row - n * P;
+      const long long h = p * g.st_h - g.pad_h + r;
+      if (h < 0 || h >= H) continue;
+      const long long xr = n * g.x.stride[0] + h * g.x.stride[2] + xc;
+      const long long yr = n * g.y.stride[0] + p * g.y.stride[2] + yc;
+      for (long long q0 = 0; q0 < Q; q0 += 8) {
+        bf16 dq[8];
+        bf16x8 xq[8];
+        float okm[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const long long q = q0 + k, w = q * g.st_w - g.pad_w + s;
+          const bool ok = q < Q && w >= 0 && w < W;
+          okm[k] = ok ? 1.f : 0.f;
+          dq[k] = yp[yr + (ok ? q : 0) * ys3];
+          xq[k] = *reinterpret_cast<const bf16x8*>(xp + xr + (ok ? w : 0) * xs3);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float dv = okm[k] * (float)dq[k];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc[u] += dv * (float)xq[k][u];
+        }
+      }
+    }
+  } else
   for (long long row = row0; row < row1; ++row) {
     const long long n = row / P, p = row - n * P;
     const long long h = p * g.st_h - g.pad_h + r;
@@ -1105,6 +1229,15 @@ void launch_reduce(hipStream_t st, const ZTensor& outer, const ZTensor& inner, c
                        no, acc, op != RD_SUM ? acc2 : nullptr);
     check_hip(hipGetLastError(), "reduce_splits_kernel");
   }
+}
+
+void launch_pad_rows(hipStream_t st, const bf16* src, long long lds, int C, bf16* dst, int C8, long long rows) {
+  if (C8 % 8 || C > C8 || C <= 0 || lds < C || rows <= 0) throw std::invalid_argument("pad_rows: bad shape");
+  const int vec = (reinterpret_cast<uintptr_t>(src) % 16 == 0 && lds % 8 == 0) ? 1 : 0;
+  const long long n = rows * (C8 / 8);
+  const int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(pad_rows_kernel, dim3(blocks), dim3(256), 0, st, src, lds, C, dst, C8, rows, vec);
+  check_hip(hipGetLastError(), "pad_rows");
 }
 
 long long reduce_rows_ws_floats(long long M, int C) { return (long long)rows_slabs(M, C) * 2 * C; }

@@ -846,6 +846,24 @@ def _conv_kind(C, O, groups, k, stride, pad, dil):
     return "gconv"
 
 
+def _row_stride(t: torch.Tensor) -> Optional[int]:
+    """Row stride (elements) when ``t`` [..., C] is evenly spaced rows of unit-stride channels (a compact tensor
+    or a channel slice of one), else None."""
+    if t.dim() < 2 or t.stride(-1) != 1:
+        return None
+    ld = expect = None
+    for d in range(t.dim() - 2, -1, -1):
+        if t.shape[d] == 1:
+            continue
+        if ld is None:
+            ld, expect = t.stride(d), t.stride(d) * t.shape[d]
+        elif t.stride(d) != expect:
+            return None
+        else:
+            expect *= t.shape[d]
+    return int(ld) if ld is not None else int(t.shape[-1])
+
+
 def _pad_c(t: torch.Tensor, c8: int, cache: bool = False) -> torch.Tensor:
     """NHWC bf16 [.., C] (possibly a channel slice) -> contiguous [.., c8], zero channels C..c8.  ``cache``:
     reuse / keep the padded copy for the rest of the NativeMode block (a conv's input is padded by its
@@ -858,9 +876,13 @@ def _pad_c(t: torch.Tensor, c8: int, cache: bool = False) -> torch.Tensor:
     if cache and mode is not None and key in mode._wcache:
         return mode._wcache[key][1]
     out = torch.empty(*t.shape[:-1], c8, dtype=torch.bfloat16, device=t.device)
-    if c8 > C:
-        fill_(out[..., C:], 0.0)
-    ew(out[..., :C], [t], EW_COPY)
+    rows = t.numel() // C if C else 0
+    if t.dtype == torch.bfloat16 and rows and _row_stride(t) is not None:
+        _nat().z_pad_rows(_st(t.device), t.data_ptr(), _row_stride(t), C, out.data_ptr(), c8, rows)   # one launch
+    else:
+        if c8 > C:
+            fill_(out[..., C:], 0.0)
+        ew(out[..., :C], [t], EW_COPY)
     if cache and mode is not None:
         mode._wcache[key] = (t, out)
     return out
