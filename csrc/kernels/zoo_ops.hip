@@ -10,6 +10,7 @@
 // concatenation); dtypes are fp32 / bf16 / int64.  Integer index math is 64-bit
 // only where a tensor can exceed 2^31 elements' byte range (never, in practice).
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "common.h"
@@ -395,6 +396,48 @@ __global__ __launch_bounds__(256) void pad_rows_kernel(const bf16* __restrict__ 
   }
 }
 
+// Finalize arguments of a BatchNorm row pass folded into the reduction's last-arriving workgroup
+// (mode 1: forward statistics -> coefficients / running stats, 2: backward sums -> coefficients, 0: none)
+struct BnFin {
+  int mode;
+  int fast;               // 1: the prefetching bf16 row pass (FEDMI_ZOO_FAST=0: the one-row loop)
+  long long M;
+  const float* shift; const float* w; const float* b; float* rmean; float* rvar; float eps, mom;
+  float* save_mean; float* save_invstd; float* scale; float* bias;
+  const float* mean; const float* invstd; float* k; float* bb; float* cc; float* dw; float* db;
+};
+
+FEDMI_DEV void bn_fwd_fin(const BnFin& f, int c, float s1, float s2) {
+  const long long M = f.M;
+  const float ms = s1 / (float)M;
+  const float var = fmaxf(s2 / (float)M - ms * ms, 0.f);
+  const float mean = ms + (f.shift ? f.shift[c] : 0.f);
+  const float inv = rsqrtf(var + f.eps);
+  if (f.save_mean) f.save_mean[c] = mean;
+  if (f.save_invstd) f.save_invstd[c] = inv;
+  if (f.rmean) {
+    f.rmean[c] = (1.f - f.mom) * f.rmean[c] + f.mom * mean;
+    f.rvar[c] = (1.f - f.mom) * f.rvar[c] + f.mom * var * ((float)M / (float)(M > 1 ? M - 1 : 1));
+  }
+  const float sc = (f.w ? f.w[c] : 1.f) * inv;
+  f.scale[c] = sc;
+  f.bias[c] = (f.b ? f.b[c] : 0.f) - mean * sc;
+}
+
+FEDMI_DEV void bn_bwd_fin(const BnFin& f, int c, float sg, float sgx) {
+  const long long M = f.M;
+  const float inv = f.invstd[c];
+  const float kk = (f.w ? f.w[c] : 1.f) * inv;
+  const float b = -kk * inv * inv * sgx / (float)M;
+  f.k[c] = kk;
+  f.bb[c] = b;
+  f.cc[c] = -kk * sg / (float)M - b * f.mean[c];
+  if (f.dw) f.dw[c] = sgx * inv;
+  if (f.db) f.db[c] = sg;
+}
+
+__device__ unsigned int g_rows_ticket = 0u;   // arrivals of the current fused BN row pass (reset by the last)
+
 // ---- row reduction of a [M, C] row-major matrix (ld = row stride), C % 8 == 0 ------------------
 // The channels-last case of the BN moments / bias gradients: a thread owns 8 channels (one 16-byte
 // load per row), RL = 256 / (C/8) row lanes per block, grid.y row slabs; per-slab partials go to
@@ -403,7 +446,8 @@ template <int VW>
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_dt, long long lda, const void* b,
                                                           int b_dt, long long ldb, const float* shift, int C,
                                                           long long M, int op, float* part, const void* f = nullptr,
-                                                          int f_dt = 0, long long ldf = 0, float thr = 0.f) {
+                                                          int f_dt = 0, long long ldf = 0, float thr = 0.f,
+                                                          BnFin fin = BnFin{}) {
   __shared__ float red[2][256 * VW];
   const int VL = C / VW;
   const int vt = min(VL, 256);
@@ -423,7 +467,7 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_d
     // U rows per pass, every load of the pass issued before the first use (clamped rows, masked): one
     // memory latency per U rows instead of per row; dtypes / operands are compile-time in the pass
     const bool dot = op != RD_SUM && op != RD_SUMSQ_SHIFT;
-    const bool bf = a_dt == 1 && (!f || f_dt == 1) && (!dot || b_dt == 1);
+    const bool bf = fin.fast && a_dt == 1 && (!f || f_dt == 1) && (!dot || b_dt == 1);
     const int opk = op == RD_SUM ? 0 : op == RD_SUMSQ_SHIFT ? 1 : 2;
 #define FEDMI_ROWS(BF, HF, OPK) rows_pass<VW, BF, HF, OPK>(a, lda, b, ldb, f, ldf, thr, sh, v, rl, RL, r0, r1, s1, s2)
     if (bf) {
@@ -472,6 +516,38 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_d
 #pragma unroll
     for (int u = 0; u < VW; ++u) { dst[v * VW + u] = s1[u]; dst[C + v * VW + u] = s2[u]; }
   }
+  if (!fin.mode) return;
+  // BatchNorm finalize in the LAST workgroup to arrive (cdna_hip_programming.md Guideline 16: stores retired,
+  // one agent release, relaxed ticket; the last arriver acquires and reads every slab in slab order) -- one
+  // launch per BN pass instead of reduce + finalize
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned total = gridDim.x * gridDim.y;
+    const unsigned prev = __hip_atomic_fetch_add(&g_rows_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev + 1 == total;
+    if (last) {
+      __hip_atomic_store(&g_rows_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  const int slabs = (int)gridDim.y;
+  for (int cb = 0; cb < C; cb += 64) {
+    const int c = cb + (threadIdx.x & 63);
+    const float a1 = ordered_slab_sum(part, slabs, 2LL * C, c, c < C);
+    __syncthreads();
+    const float a2 = ordered_slab_sum(part + C, slabs, 2LL * C, c, c < C);
+    __syncthreads();
+    if (!(threadIdx.x >> 6) && c < C) {
+      if (fin.mode == 1) bn_fwd_fin(fin, c, a1, a2);
+      else bn_bwd_fin(fin, c, a1, a2);
+    }
+  }
 }
 
 // acc[c] += sum_slab part[slab][0][c] (and acc2 from part[slab][1][c]), slab order
@@ -498,19 +574,10 @@ __global__ __launch_bounds__(256) void bn_rows_fwd_finalize(const float* part, i
   __syncthreads();
   const float s2 = ordered_slab_sum(part + C, slabs, 2LL * C, c, c < C);
   if ((threadIdx.x >> 6) || c >= C) return;
-  const float ms = s1 / (float)M;
-  const float var = fmaxf(s2 / (float)M - ms * ms, 0.f);
-  const float mean = ms + (shift ? shift[c] : 0.f);
-  const float inv = rsqrtf(var + eps);
-  if (save_mean) save_mean[c] = mean;
-  if (save_invstd) save_invstd[c] = inv;
-  if (rmean) {
-    rmean[c] = (1.f - mom) * rmean[c] + mom * mean;
-    rvar[c] = (1.f - mom) * rvar[c] + mom * var * ((float)M / (float)(M > 1 ? M - 1 : 1));
-  }
-  const float sc = (w ? w[c] : 1.f) * inv;
-  scale[c] = sc;
-  bias[c] = (b ? b[c] : 0.f) - mean * sc;
+  BnFin f{};
+  f.M = M; f.shift = shift; f.w = w; f.b = b; f.rmean = rmean; f.rvar = rvar; f.eps = eps; f.mom = mom;
+  f.save_mean = save_mean; f.save_invstd = save_invstd; f.scale = scale; f.bias = bias;
+  bn_fwd_fin(f, c, s1, s2);
 }
 
 // BatchNorm backward from the slab partials of (sum g, sum g * (x - mean)): bn_bwd_coeffs math
@@ -522,17 +589,24 @@ __global__ __launch_bounds__(256) void bn_rows_bwd_finalize(const float* part, i
   __syncthreads();
   const float sgx = ordered_slab_sum(part + C, slabs, 2LL * C, c, c < C);
   if ((threadIdx.x >> 6) || c >= C) return;
-  const float inv = invstd[c];
-  const float kk = (w ? w[c] : 1.f) * inv;
-  const float b = -kk * inv * inv * sgx / (float)M;
-  k[c] = kk;
-  bb[c] = b;
-  cc[c] = -kk * sg / (float)M - b * mean[c];
-  if (dw) dw[c] = sgx * inv;
-  if (db) db[c] = sg;
+  BnFin f{};
+  f.M = M; f.mean = mean; f.invstd = invstd; f.w = w; f.k = k; f.bb = bb; f.cc = cc; f.dw = dw; f.db = db;
+  bn_bwd_fin(f, c, sg, sgx);
 }
 
 int rows_vw(int C) { return C % 8 == 0 ? 8 : 4; }
+
+// prefetching fast paths of the row pass and the grouped convs (FEDMI_ZOO_FAST=0: the original loops, A/B)
+bool zoo_fast() {
+  static const bool on = [] { const char* e = std::getenv("FEDMI_ZOO_FAST"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
+// BN row passes with the finalize in the last-arriving workgroup (FEDMI_BN_ROWS_FUSED=0: separate launch)
+bool bn_rows_fused() {
+  static const bool on = [] { const char* e = std::getenv("FEDMI_BN_ROWS_FUSED"); return !(e && e[0] == '0'); }();
+  return on;
+}
 
 int rows_slabs(long long M, int C) {
   const int VL = C / rows_vw(C), vt = VL < 256 ? VL : 256, RL = 256 / vt;
@@ -894,6 +968,7 @@ struct GConv {
   ZTensor x, w, y;
   int G, st_h, st_w, pad_h, pad_w, R, S;
   int vec_x, vec_y;    // channels of x (resp. y) load as aligned bf16x8 vectors (host-checked)
+  int fast;            // prefetching 3x3 / wgrad fast paths (FEDMI_ZOO_FAST)
 };
 
 FEDMI_DEV void load8(const ZTensor& t, long long off, long long cstride, bool vec, float v[8]) {
@@ -936,6 +1011,36 @@ __global__ __launch_bounds__(256) void gconv_fwd_kernel(GConv g) {
     }
     __syncthreads();
     if (!valid) continue;
+    if (g.fast && g.R == 3 && g.S == 3 && g.vec_x && g.x.dtype == 1 && cn % 8 == 0) {
+      // 3x3, bf16 channels-last: per 8-channel group the nine tap vectors are loaded together (clamped
+      // addresses, 0/1 masks), then the FMAs -- one memory latency per group instead of one per tap
+      const bf16* xp = reinterpret_cast<const bf16*>(g.x.p);
+      long long toff[9];
+      float tok[9];
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) {
+        const long long h = p * g.st_h - g.pad_h + tp / 3, w = q * g.st_w - g.pad_w + tp % 3;
+        const bool ok = h >= 0 && h < H && w >= 0 && w < W;
+        tok[tp] = ok ? 1.f : 0.f;
+        toff[tp] = xb + (ok ? h * g.x.stride[2] + w * g.x.stride[3] : 0) + (long long)c0;
+      }
+      for (int c = 0; c < cn; c += 8) {
+        bf16x8 xq[9];
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) xq[tp] = *reinterpret_cast<const bf16x8*>(xp + toff[tp] + c);
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+          const float* wr = wl + tp * cn * GT;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float xv = tok[tp] * (float)xq[tp][u];
+#pragma unroll
+            for (int j = 0; j < GT; ++j) acc[j] += xv * wr[(c + u) * GT + j];
+          }
+        }
+      }
+      continue;
+    }
     for (int r = 0; r < g.R; ++r) {
       const long long h = p * g.st_h - g.pad_h + r;
       if (h < 0 || h >= H) continue;
@@ -1000,6 +1105,37 @@ __global__ __launch_bounds__(256) void gconv_dgrad_kernel(GConv g) {
     }
     __syncthreads();
     if (!valid) continue;
+    if (g.fast && g.R == 3 && g.S == 3 && g.vec_y && g.y.dtype == 1 && on % 8 == 0) {
+      // 3x3, bf16 channels-last dy: the nine tap vectors of an 8-channel group loaded together (see fwd)
+      const bf16* yp = reinterpret_cast<const bf16*>(g.y.p);
+      long long toff[9];
+      float tok[9];
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) {
+        const long long hp = h + g.pad_h - tp / 3, wp = w + g.pad_w - tp % 3;
+        const bool okd = hp >= 0 && wp >= 0 && hp % g.st_h == 0 && wp % g.st_w == 0;
+        const long long p = okd ? hp / g.st_h : 0, q = okd ? wp / g.st_w : 0;
+        const bool ok = okd && p < P && q < Q;
+        tok[tp] = ok ? 1.f : 0.f;
+        toff[tp] = yb + (ok ? p * g.y.stride[2] + q * g.y.stride[3] : 0) + (long long)o0;
+      }
+      for (int o = 0; o < on; o += 8) {
+        bf16x8 yq[9];
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) yq[tp] = *reinterpret_cast<const bf16x8*>(yp + toff[tp] + o);
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+          const float* wr = wl + tp * on * GT;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float dv = tok[tp] * (float)yq[tp][u];
+#pragma unroll
+            for (int j = 0; j < GT; ++j) acc[j] += dv * wr[(o + u) * GT + j];
+          }
+        }
+      }
+      continue;
+    }
     for (int r = 0; r < g.R; ++r) {
       const long long hp = h + g.pad_h - r;
       if (hp < 0 || hp % g.st_h) continue;
@@ -1063,7 +1199,7 @@ __global__ __launch_bounds__(256) void gconv_wgrad_kernel(GConv g, float* part, 
   float acc[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) acc[u] = 0.f;
-  if (vec && g.y.dtype == 1) {
+  if (g.fast && vec && g.y.dtype == 1) {
     // bf16 channels-last fast path: 8 output columns per pass, all 16 loads (8 dy scalars, 8 x vectors)
     // issued before the first use -- clamped addresses and a 0/1 mask instead of per-load branches, so the
     // pass costs one memory latency (the scalar loop paid one per pixel: ~300 us per RegNetY launch)
@@ -1250,12 +1386,14 @@ void launch_reduce_rows(hipStream_t st, const void* a, int a_dt, long long lda, 
   if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("reduce_rows: workspace too small");
   const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
   const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
+  BnFin fin{};
+  fin.fast = zoo_fast();
   if (vw == 8)
     hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
-                       nullptr, 0, 0LL, 0.f);
+                       nullptr, 0, 0LL, 0.f, fin);
   else
     hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
-                       nullptr, 0, 0LL, 0.f);
+                       nullptr, 0, 0LL, 0.f, fin);
   hipLaunchKernelGGL(reduce_rows_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C,
                      op != RD_SUM ? 1 : 0, acc, acc2);
   check_hip(hipGetLastError(), "reduce_rows");
@@ -1270,14 +1408,22 @@ void launch_bn_rows_fwd(hipStream_t st, const void* x, int x_dt, long long ldx, 
   if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("bn_rows_fwd: workspace too small");
   const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
   const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
+  BnFin fin{};
+  fin.fast = zoo_fast();
+  if (bn_rows_fused()) {
+    fin.mode = 1; fin.M = M; fin.shift = shift; fin.w = w; fin.b = b; fin.rmean = rmean; fin.rvar = rvar;
+    fin.eps = eps; fin.mom = mom; fin.save_mean = save_mean; fin.save_invstd = save_invstd; fin.scale = scale;
+    fin.bias = bias;
+  }
   if (vw == 8)
     hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, x, x_dt, ldx, nullptr, 0, 0LL, shift, C, M,
-                       (int)RD_SUMSQ_SHIFT, part, nullptr, 0, 0LL, 0.f);
+                       (int)RD_SUMSQ_SHIFT, part, nullptr, 0, 0LL, 0.f, fin);
   else
     hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, x, x_dt, ldx, nullptr, 0, 0LL, shift, C, M,
-                       (int)RD_SUMSQ_SHIFT, part, nullptr, 0, 0LL, 0.f);
-  hipLaunchKernelGGL(bn_rows_fwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C, M, shift,
-                     w, b, rmean, rvar, eps, mom, save_mean, save_invstd, scale, bias);
+                       (int)RD_SUMSQ_SHIFT, part, nullptr, 0, 0LL, 0.f, fin);
+  if (!fin.mode)
+    hipLaunchKernelGGL(bn_rows_fwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C, M,
+                       shift, w, b, rmean, rvar, eps, mom, save_mean, save_invstd, scale, bias);
   check_hip(hipGetLastError(), "bn_rows_fwd");
 }
 
@@ -1291,14 +1437,21 @@ void launch_bn_rows_bwd(hipStream_t st, const void* g, int g_dt, long long ldg, 
   if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("bn_rows_bwd: workspace too small");
   const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
   const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
+  BnFin fin{};
+  fin.fast = zoo_fast();
+  if (bn_rows_fused()) {
+    fin.mode = 2; fin.M = M; fin.mean = mean; fin.invstd = invstd; fin.w = w; fin.k = k; fin.bb = bb; fin.cc = cc;
+    fin.dw = dw; fin.db = db;
+  }
   if (vw == 8)
     hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, g, g_dt, ldg, x, x_dt, ldx, mean, C, M,
-                       (int)RD_DOT_SHIFT, part, f, f_dt, ldf, thr);
+                       (int)RD_DOT_SHIFT, part, f, f_dt, ldf, thr, fin);
   else
     hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, g, g_dt, ldg, x, x_dt, ldx, mean, C, M,
-                       (int)RD_DOT_SHIFT, part, f, f_dt, ldf, thr);
-  hipLaunchKernelGGL(bn_rows_bwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C, M, mean,
-                     invstd, w, k, bb, cc, dw, db);
+                       (int)RD_DOT_SHIFT, part, f, f_dt, ldf, thr, fin);
+  if (!fin.mode)
+    hipLaunchKernelGGL(bn_rows_bwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C, M,
+                       mean, invstd, w, k, bb, cc, dw, db);
   check_hip(hipGetLastError(), "bn_rows_bwd");
 }
 
@@ -1405,6 +1558,7 @@ void launch_gconv(hipStream_t st, int mode, const ZTensor& x, const ZTensor& w, 
   };
   g.vec_x = vec_ok(x, Cg);
   g.vec_y = vec_ok(y, Og);
+  g.fast = zoo_fast() ? 1 : 0;
   if (G <= 0 || O % G || x.size[1] != Cg * G || w.size[0] != O || g.R * g.S * GT > GC_LDS)
     throw std::invalid_argument("gconv: inconsistent shapes");
   if (mode == 0) {

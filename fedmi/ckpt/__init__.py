@@ -464,6 +464,11 @@ class RoundCheckpointWriter:
                 except (ValueError, RuntimeError):
                     w = None
             if w is not None:
+                # another writer covering one of these files must land first, or its older round could
+                # overwrite this one (the writers run independently)
+                for k, o in self._native.items():
+                    if k != paths and set(k) & set(paths):
+                        o.flush()
                 self.backend = "native"
                 w.submit(epoch)
                 return

@@ -90,6 +90,10 @@ class ClientAgent(P.TrainerServicer):
         self.fault_stall_avg_s = float(os.environ.get("FEDMI_FAULT_STALL_AVG_S", "0") or 0)
         self.fault_stall_from = int(os.environ.get("FEDMI_FAULT_STALL_FROM_ROUND", "0") or 0)
         self._round_start = None                # (float, [int]) device copies of the round's starting global model
+        self._debug_stats = os.environ.get("FEDMI_DEBUG_STATS", "0") == "1"
+        if self._debug_stats:
+            from ..parallel import compress as _comp
+            _comp.PROBE = self._probe
         if resume and self.ckpt_path.exists():
             c = ck.load(self.ckpt_path)
             trainer.load_state_dict(c["net"])
@@ -102,6 +106,15 @@ class ClientAgent(P.TrainerServicer):
     def _log(self, msg: str) -> None:
         if self.verbose:
             log(f"client {self.address}", msg)
+
+    def _probe(self, tag: str) -> None:
+        """FEDMI_DEBUG_STATS=1: synchronise and log the trainer's stats rows after each phase (diagnostics
+        for a stats word that changed outside the training kernels)."""
+        st = getattr(self.trainer, "stats", None)
+        if not self._debug_stats or st is None:
+            return
+        torch.cuda.synchronize(st.device)
+        self._log(f"probe {tag}: stats {st.cpu().view(-1).tolist()}")
 
     # ---- helpers ------------------------------------------------------------------
     def _fence(self, meta: dict, context) -> None:
@@ -194,6 +207,7 @@ class ClientAgent(P.TrainerServicer):
                     except Exception as e:      # rendezvous failed (a member never showed up)
                         context.abort(grpc.StatusCode.ABORTED, f"data-plane group failed: {e}"[:500])
                 self.fedavg.transport = self.group.transport
+                self._probe("group")
             elif world > 1:
                 context.abort(grpc.StatusCode.FAILED_PRECONDITION, "collective aggregation needs a GroupManager")
             if changed and world > 1:
@@ -201,6 +215,7 @@ class ClientAgent(P.TrainerServicer):
                 # for the -c Y compressors; undoes any partially applied aborted round)
                 self.fedavg.resync(self.trainer, 0)
                 rec["resync"] = True
+                self._probe("resync")
             elif changed and self.fedavg.compressor is not None:
                 self.fedavg.compressor.reset(self.trainer)
             rec["group_ms"] = t.ms()
@@ -209,7 +224,9 @@ class ClientAgent(P.TrainerServicer):
         t1 = Timer()
         with phase("local-train"):
             self.trainer.set_schedule(*self._schedule(rank, world))
+            self._probe("pre-train")
             self.trainer.train_epoch()
+            self._probe("train")
             tr = self.trainer.train_stats()
         rec.update(tr.as_dict("train"))
         rec["train_ms"] = t1.ms()
@@ -221,6 +238,7 @@ class ClientAgent(P.TrainerServicer):
             with phase("allreduce"):
                 try:
                     self.fedavg.average(self.trainer)
+                    self._probe("average")
                     tp = self.fedavg.transport
                     err = "peer collective timed out (a client was lost)" if tp is not None and tp.error() else ""
                 except Exception as e:          # gloo / RCCL error: a peer was lost mid-collective
@@ -238,6 +256,7 @@ class ClientAgent(P.TrainerServicer):
             with phase("eval"):
                 self.trainer.evaluate()
                 ev = self.trainer.eval_stats()
+            self._probe("eval")
             rec["eval_ms"] = t3.ms()
             rec.update(ev.as_dict("test"))
             self.round = rnd
@@ -250,6 +269,7 @@ class ClientAgent(P.TrainerServicer):
                 upload = rank == 0 and (sync or meta.get(META_UPLOAD) != "0")
                 ck_epoch, message = self._take_ready() if upload else (-1, "")
             rec["ckpt_ms"] = t4.ms()
+            self._probe("ckpt")
         else:
             # reference parameter-server path: the reply IS this round's local model
             self.round = rnd

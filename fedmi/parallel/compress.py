@@ -39,6 +39,14 @@ def _world(group) -> int:
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
+PROBE = None          # diagnostics hook (client agent, FEDMI_DEBUG_STATS=1): called with a phase tag
+
+
+def _probe(tag: str) -> None:
+    if PROBE is not None:
+        PROBE(tag)
+
+
 def _all_gather_flat(t: torch.Tensor, group, transport=None) -> torch.Tensor:
     if transport is not None:
         return transport.all_gather(t)
@@ -110,9 +118,12 @@ class TopKCompressor(_EFCompressor):
     def aggregate(self, trainer, group=None, transport=None) -> None:
         x = trainer.float_state()
         self.compress(x)
+        _probe("topk")
         w = transport.world if transport is not None else _world(group)
         idx_all = _all_gather_flat(self.idx, group, transport)
+        _probe("gather-idx")
         val_all = _all_gather_flat(self.val, group, transport)
+        _probe("gather-val")
         self.bytes_sent += 8 * self.k
         self.dense_bytes += 4 * self.n
         self.rounds += 1
@@ -123,6 +134,7 @@ class TopKCompressor(_EFCompressor):
             for r in range(w):                 # rank order, like the GPU path
                 self.global_ref.index_add_(0, idx_all[r].long(), val_all[r] * (1.0 / w))
         x.copy_(self.global_ref)
+        _probe("scatter")
 
 
 class Int8Compressor(_EFCompressor):
