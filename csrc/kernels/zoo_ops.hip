@@ -350,8 +350,9 @@ FEDMI_DEV void rows_pass(const void* a, long long lda, const void* b, long long 
       if constexpr (HF) vload_bf<VW>(f, r * ldf + v * VW, m[k]);
       if constexpr (OPK == 2) vload_bf<VW>(b, r * ldb + v * VW, y[k]);
     }
-    // dead rows (past r1) contribute exact zeros through selects, never through an extra multiply: the
-    // accumulation expressions (and their FMA contraction) stay those of the one-row loop
+    // dead rows (past r1) contribute exact zeros through selects, never through an extra multiply; the
+    // products are explicit fmas, so the rounding cannot depend on how the compiler contracts each
+    // instantiation (a masked and a pre-masked gradient give bit-identical sums)
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const bool live = rb + (long long)k * RL < r1;
@@ -364,11 +365,11 @@ FEDMI_DEV void rows_pass(const void* a, long long lda, const void* b, long long 
         } else if constexpr (OPK == 1) {
           const float d = live ? xv - sh[u] : 0.f;
           s1[u] += d;
-          s2[u] += d * d;
+          s2[u] = __builtin_fmaf(d, d, s2[u]);
         } else {
           const float yv = live ? y[k][u] - sh[u] : 0.f;
           s1[u] += xv;
-          s2[u] += xv * yv;
+          s2[u] = __builtin_fmaf(xv, yv, s2[u]);
         }
       }
     }
@@ -488,12 +489,12 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_d
           for (int u = 0; u < VW; ++u) s1[u] += x[u];
         } else if (opk == 1) {
 #pragma unroll
-          for (int u = 0; u < VW; ++u) { const float d = x[u] - sh[u]; s1[u] += d; s2[u] += d * d; }
+          for (int u = 0; u < VW; ++u) { const float d = x[u] - sh[u]; s1[u] += d; s2[u] = __builtin_fmaf(d, d, s2[u]); }
         } else {
           float y[VW];
           vload<VW>(b, b_dt, r * ldb + v * VW, y);
 #pragma unroll
-          for (int u = 0; u < VW; ++u) { s1[u] += x[u]; s2[u] += x[u] * (y[u] - sh[u]); }
+          for (int u = 0; u < VW; ++u) { s1[u] += x[u]; s2[u] = __builtin_fmaf(x[u], y[u] - sh[u], s2[u]); }
         }
       }
     }
@@ -1041,29 +1042,28 @@ __global__ __launch_bounds__(256) void gconv_fwd_kernel(GConv g) {
       }
       continue;
     }
-    for (int r = 0; r < g.R; ++r) {
-      const long long h = p * g.st_h - g.pad_h + r;
-      if (h < 0 || h >= H) continue;
-      for (int s = 0; s < g.S; ++s) {
-        const long long w = q * g.st_w - g.pad_w + s;
-        if (w < 0 || w >= W) continue;
-        const long long base = xb + h * g.x.stride[2] + w * g.x.stride[3] + (long long)c0 * g.x.stride[1];
-        const float* wr = wl + (r * g.S + s) * cn * GT;
-        int c = 0;
-        if (g.vec_x) {
-          for (; c + 8 <= cn; c += 8) {
-            float xv[8];
-            load8(g.x, base + c, 1, true, xv);
+    // general path, in the fast path's accumulation order (8-channel group, then tap, then channel): the sums
+    // do not depend on which path a layout takes
+    for (int c = 0; c < cn; c += 8) {
+      const int cw = min(8, cn - c);
+      for (int r = 0; r < g.R; ++r) {
+        const long long h = p * g.st_h - g.pad_h + r;
+        if (h < 0 || h >= H) continue;
+        for (int s = 0; s < g.S; ++s) {
+          const long long w = q * g.st_w - g.pad_w + s;
+          if (w < 0 || w >= W) continue;
+          const long long base = xb + h * g.x.stride[2] + w * g.x.stride[3] + (long long)(c0 + c) * g.x.stride[1];
+          const float* wr = wl + (r * g.S + s) * cn * GT;
+          float xv[8];
+          if (g.vec_x && cw == 8) {
+            load8(g.x, base, 1, true, xv);
+          } else {
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-#pragma unroll
-              for (int j = 0; j < GT; ++j) acc[j] += xv[u] * wr[(c + u) * GT + j];
+            for (int u = 0; u < 8; ++u) xv[u] = u < cw ? zload(g.x, base + (long long)u * g.x.stride[1]) : 0.f;
           }
-        }
-        for (; c < cn; ++c) {
-          const float xv = zload(g.x, base + (long long)c * g.x.stride[1]);
+          for (int u = 0; u < cw; ++u)
 #pragma unroll
-          for (int j = 0; j < GT; ++j) acc[j] += xv * wr[c * GT + j];
+            for (int j = 0; j < GT; ++j) acc[j] += xv[u] * wr[(c + u) * GT + j];
         }
       }
     }
@@ -1136,33 +1136,31 @@ __global__ __launch_bounds__(256) void gconv_dgrad_kernel(GConv g) {
       }
       continue;
     }
-    for (int r = 0; r < g.R; ++r) {
-      const long long hp = h + g.pad_h - r;
-      if (hp < 0 || hp % g.st_h) continue;
-      const long long p = hp / g.st_h;
-      if (p >= P) continue;
-      for (int s = 0; s < g.S; ++s) {
-        const long long wp = w + g.pad_w - s;
-        if (wp < 0 || wp % g.st_w) continue;
-        const long long q = wp / g.st_w;
-        if (q >= Q) continue;
-        const long long base = yb + p * g.y.stride[2] + q * g.y.stride[3] + (long long)o0 * g.y.stride[1];
-        const float* wr = wl + (r * g.S + s) * on * GT;
-        int o = 0;
-        if (g.vec_y) {
-          for (; o + 8 <= on; o += 8) {
-            float dv[8];
-            load8(g.y, base + o, 1, true, dv);
+    // general path in the fast path's order (8-channel group, tap, channel), as in gconv_fwd_kernel
+    for (int o = 0; o < on; o += 8) {
+      const int ow = min(8, on - o);
+      for (int r = 0; r < g.R; ++r) {
+        const long long hp = h + g.pad_h - r;
+        if (hp < 0 || hp % g.st_h) continue;
+        const long long p = hp / g.st_h;
+        if (p >= P) continue;
+        for (int s = 0; s < g.S; ++s) {
+          const long long wp = w + g.pad_w - s;
+          if (wp < 0 || wp % g.st_w) continue;
+          const long long q = wp / g.st_w;
+          if (q >= Q) continue;
+          const long long base = yb + p * g.y.stride[2] + q * g.y.stride[3] + (long long)(o0 + o) * g.y.stride[1];
+          const float* wr = wl + (r * g.S + s) * on * GT;
+          float dv[8];
+          if (g.vec_y && ow == 8) {
+            load8(g.y, base, 1, true, dv);
+          } else {
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-#pragma unroll
-              for (int j = 0; j < GT; ++j) acc[j] += dv[u] * wr[(o + u) * GT + j];
+            for (int u = 0; u < 8; ++u) dv[u] = u < ow ? zload(g.y, base + (long long)u * g.y.stride[1]) : 0.f;
           }
-        }
-        for (; o < on; ++o) {
-          const float dv = zload(g.y, base + (long long)o * g.y.stride[1]);
+          for (int u = 0; u < ow; ++u)
 #pragma unroll
-          for (int j = 0; j < GT; ++j) acc[j] += dv * wr[o * GT + j];
+            for (int j = 0; j < GT; ++j) acc[j] += dv[u] * wr[(o + u) * GT + j];
         }
       }
     }

@@ -114,7 +114,7 @@ class ClientAgent(P.TrainerServicer):
         if not self._debug_stats or st is None:
             return
         torch.cuda.synchronize(st.device)
-        self._log(f"probe {tag}: stats {st.cpu().view(-1).tolist()}")
+        log(f"client {self.address}", f"probe {tag}: stats {st.cpu().view(-1).tolist()}")   # even with --quiet
 
     # ---- helpers ------------------------------------------------------------------
     def _fence(self, meta: dict, context) -> None:

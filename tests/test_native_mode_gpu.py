@@ -401,3 +401,36 @@ def test_native_backend_is_deterministic(gpu_device, name):
         outs.append((tr.float_state().clone(), tr.train_stats().loss))
     assert torch.equal(outs[0][0], outs[1][0]), float((outs[0][0] - outs[1][0]).abs().max())
     assert outs[0][1] == outs[1][1]
+
+
+@pytest.mark.parametrize("C", [24, 36, 48, 252])
+@pytest.mark.parametrize("M", [1000, 4096])
+def test_bn_rows_bwd_fused_mask_matches_premasked(gpu_device, C, M):
+    """The BN-backward row pass with the ReLU mask fused (f = ReLU output) gives BIT-IDENTICAL sums /
+    coefficients to the same pass over the pre-masked gradient (what the unfused threshold_backward
+    writes) -- the kernel-level half of test_bn_relu_fusion_is_exact."""
+    from fedmi import native
+    from fedmi.ops.native_mode import _DT
+
+    nat = native.require()
+    st = native.stream_handle(gpu_device)
+    g = torch.Generator(device="cpu").manual_seed(C * 7 + M)
+    mk = lambda *s: torch.randn(*s, generator=g).to(gpu_device)   # noqa: E731
+    gy, x = mk(M, C).bfloat16(), mk(M, C).bfloat16()
+    f = torch.relu(mk(M, C)).bfloat16()
+    gm = torch.where(f > 0, gy, torch.zeros_like(gy))
+    mean, invstd, w = mk(C), mk(C).abs() + 0.5, mk(C)
+    outs = []
+    for a, ff in ((gy, f), (gm, None)):
+        part = torch.empty(int(nat.z_reduce_rows_ws_floats(M, C)), dtype=torch.float32, device=gpu_device)
+        o = [torch.full((C,), float("nan"), device=gpu_device) for _ in range(5)]
+        nat.z_bn_rows_bwd(st, a.data_ptr(), _DT[a.dtype], C, x.data_ptr(), _DT[x.dtype], C,
+                          ff.data_ptr() if ff is not None else 0, _DT[f.dtype] if ff is not None else 0, C, 0.0,
+                          mean.data_ptr(), invstd.data_ptr(), w.data_ptr(), C, M, part.data_ptr(), part.numel(),
+                          *[t.data_ptr() for t in o])
+        outs.append(o)
+    torch.cuda.synchronize()
+    for name, p, q in zip(("k", "b", "c", "dw", "db"), *outs):
+        assert torch.equal(p, q), (name, (p - q).abs().max().item())
+    ref_db = gm.float().sum(0)
+    assert torch.allclose(outs[0][4], ref_db, rtol=1e-4, atol=1e-3)
