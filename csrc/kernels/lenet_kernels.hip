@@ -2070,6 +2070,17 @@ void read_stamps(unsigned long long* host, bool clear) {
 #endif
 }
 
+// Zeroes a Stats row in a kernel: an epoch captured into a hipGraph must not reset it with hipMemsetAsync --
+// a replayed memset node was measured writing stale bytes (host data such as "PDF1") into the row in a
+// gRPC client process whose host heap is reused between rounds (tests/test_system_gpu.py, -c Y).
+__global__ void lenet_zero_stats(Stats* __restrict__ s) {
+  if (threadIdx.x == 0) *s = Stats{0.f, 0, 0, 0};
+}
+
+void launch_lenet_zero_stats(hipStream_t st, Stats* s) {
+  hipLaunchKernelGGL(lenet_zero_stats, dim3(1), dim3(64), 0, st, s);
+}
+
 void launch_lenet_pack(hipStream_t st, const float* params, bf16* pk) {
   hipLaunchKernelGGL(lenet_pack, dim3((P_TOTAL + 255) / 256), dim3(256), 0, st, params, pk);
 }

@@ -25,6 +25,7 @@ void launch_lenet_bwd_sgd(hipStream_t, const uint8_t*, int, int, uint32_t, const
                           const bf16*, const bf16*, const uint8_t*, const uint8_t*, float*, float*, float*, float*, bf16*,
                           const float*, int, float, float, float, int*, const int*, int*, int*, Stats*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
+void launch_lenet_zero_stats(hipStream_t, lenet::Stats*);
 void launch_lenet_sample_step(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*,
                               int, const int*, bf16*, bf16*, float*, bf16*, float*);
 void launch_lenet_sgd2(hipStream_t, float*, float*, bf16*, const float*, int, const bf16*, const bf16*, const float*,
@@ -84,7 +85,7 @@ void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round, bool 
     throw std::invalid_argument("LeNetEngine::step: batch out of range");
   const int aug = augment_ ? 1 : 0;
   if (sample_path_) {
-    if (reset_stats) check_hip(hipMemsetAsync(b_.train_stats, 0, sizeof(Stats), st), "memset stats");
+    if (reset_stats) launch_lenet_zero_stats(st, b_.train_stats);   // a kernel node, not a memset (graph replay)
     // the FC side buffers (h2T, dZ2T, dZ3T, bias grads, losses) live in the dact2 buffer, h1T in h1
     launch_lenet_sample_step(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug,
                              b_.train_labels + start, b_.act2T, b_.h1, b_.dact2, b_.dZ1T, b_.conv_slab);
@@ -95,7 +96,7 @@ void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round, bool 
     return;
   }
   if (fuse_head_) {
-    if (reset_stats) check_hip(hipMemsetAsync(b_.train_stats, 0, sizeof(Stats), st), "memset stats");
+    if (reset_stats) launch_lenet_zero_stats(st, b_.train_stats);   // a kernel node, not a memset (graph replay)
     launch_lenet_fwd_head(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug, b_.act2,
                           b_.act2T, b_.pool1, b_.am1, b_.am2, b_.train_labels + start, b_.dact2, b_.dZ1T, b_.fc_slab,
                           b_.train_stats, b_.done_flags, b_.step_gen, b_.bwd_gen);

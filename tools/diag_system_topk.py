@@ -15,7 +15,7 @@ from fedmi.control.coordinator import Coordinator, CoordinatorConfig  # noqa: E4
 transport, compress = sys.argv[1], sys.argv[2] == "Y"
 extra = tuple(sys.argv[3:])
 tmp = Path(tempfile.mkdtemp(prefix="diag_sys_"))
-addrs = [f"127.0.0.1:{free_port()}" for _ in range(2)]
+addrs = [f"127.0.0.1:{free_port()}" for _ in range(int(__import__("os").environ.get("DIAG_CLIENTS", "2")))]
 args = ("--agg", "collective", "--model", "lenet", "--n-train", "2560", "--n-test", "1000", "--transport", transport)
 args += (("-c", "Y") if compress else ()) + extra
 procs = [spawn_client(a, tmp, *args, log_path=tmp / f"client{i}.log", device="cuda:0") for i, a in enumerate(addrs)]
@@ -31,7 +31,7 @@ try:
 finally:
     for p in procs:
         stop_proc(p)
-for i in range(2):
+for i in range(len(addrs)):
     lines = (tmp / f"client{i}.log").read_text().splitlines()
     print(f"--- client{i} log tail ---")
     print("\n".join(lines[-int(__import__("os").environ.get("DIAG_TAIL", "25")):]))
