@@ -1,7 +1,9 @@
-"""The -c Y system path (coordinator + 2 GPU client processes) under variants, to localise the
-train-stats corruption seen in tests/test_system_gpu.py::test_grpc_coordinator_drives_gpu_clients[topk]:
-  python tools/diag_system_topk.py <transport peer|dist> <compress Y|N> [extra client args...]
-Prints the coordinator's round log and the tail of each client log."""
+"""The product path on one GPU (coordinator + N GPU client processes over gRPC, peer or dist data plane):
+  [DIAG_CLIENTS=n] [FEDMI_DEBUG_STATS=1] python tools/diag_system_topk.py <transport peer|dist> <compress Y|N>
+      [extra client args...]
+Prints the coordinator's round log and the tail of each client log; FEDMI_DEBUG_STATS=1 makes each client log
+its LeNet stats rows after every phase of a round.  Used to localise the train-stats corruption of
+tests/test_system_gpu.py (a graph-captured hipMemsetAsync replaying stale host bytes, fixed in the engine)."""
 import sys
 import tempfile
 from pathlib import Path
