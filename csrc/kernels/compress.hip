@@ -13,6 +13,7 @@
 //
 // The compressed payloads are all-gathered over RCCL and folded back with
 // scatter_add_ranked (rank-ordered, atomic-free) / dequant_accum.
+#include <cstdlib>
 #include <algorithm>
 
 #include "common.h"
@@ -654,13 +655,17 @@ void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* resid
   const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g) |
                      reinterpret_cast<uintptr_t>(residual)) & 15) == 0;
   // ~8 float4 per thread, at most 2048 workgroups (their nonzero bins go to the global histogram)
-  const int blocks = (int)std::min<long>(2048, std::max<long>(1, (n + 8 * 1024 - 1) / (8 * 1024)));
+  long hmax = 2048;
+  if (const char* e = std::getenv("FEDMI_TK_HBLOCKS")) hmax = std::max(1L, std::atol(e));   // A/B: histogram grid cap
+  const int blocks = (int)std::min<long>(hmax, std::max<long>(1, (n + 8 * 1024 - 1) / (8 * 1024)));
   if (vec)
     hipLaunchKernelGGL(tk_delta_hist_kernel<true>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s);
   else
     hipLaunchKernelGGL(tk_delta_hist_kernel<false>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s);
   hipLaunchKernelGGL(tk_pick1_kernel, dim3(1), dim3(1024), 0, st, s, k);
-  const int cblocks = (int)std::min<long>(2048, std::max<long>(1, (n + 2 * 2048 - 1) / (2 * 2048)));
+  long cmax = 2048;
+  if (const char* e = std::getenv("FEDMI_TK_CBLOCKS")) cmax = std::max(1L, std::atol(e));   // A/B: compaction grid cap
+  const int cblocks = (int)std::min<long>(cmax, std::max<long>(1, (n + 2 * 2048 - 1) / (2 * 2048)));
   if (n < kTkThreeLevel) {
     hipLaunchKernelGGL(tk_compact1_kernel<false>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx,
                        ckey);
