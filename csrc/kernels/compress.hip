@@ -232,14 +232,50 @@ struct TopKState {
   int b1, n_above, need, out_cnt, cand_cnt, pad[3];
   // 3-level path (large n): level-2 histogram of the candidates' key bits 19..9
   unsigned hist2[kTkBins1];
-  int b2, n_above2, need2, out2_cnt, cand2_cnt, pad2[3];
+  int b2, n_above2, need2, out2_cnt, cand2_cnt;
+  unsigned ticket;                // arrivals of the current tk_delta_hist launch (reset by the last arriver)
+  int pad2[2];
 };
+
+// NT threads: bin b of h[0..nb) (nb = 1024 or 2048, nb >= NT) such that above(b) < k <= above(b) + h[b],
+// scanning from the TOP bin down; above(b) = sum of the bins > b.  Result in res[0..1].
+template <int NT = 1024>
+FEDMI_DEV void tk_find_top(const unsigned* h, int nb, unsigned k, unsigned* scratch, unsigned* res) {
+  constexpr int NW = NT / 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, per = nb / NT;
+  unsigned s = 0u;
+  for (int j = 0; j < per; ++j) s += h[nb - 1 - (t * per + j)];
+  unsigned inc = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned v = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += v;
+  }
+  if (lane == 63) scratch[w] = inc;
+  __syncthreads();
+  if (t == 0) {
+    unsigned a = 0u;
+    for (int q = 0; q < NW; ++q) { const unsigned v = scratch[q]; scratch[16 + q] = a; a += v; }
+  }
+  __syncthreads();
+  const unsigned excl = scratch[16 + w] + inc - s;
+  if (excl < k && k <= excl + s) {
+    unsigned above = excl;
+    for (int j = 0; j < per; ++j) {
+      const int b = nb - 1 - (t * per + j);
+      if (above + h[b] >= k) { res[0] = (unsigned)b; res[1] = above; break; }
+      above += h[b];
+    }
+  }
+  __syncthreads();
+}
 
 FEDMI_DEV void tk_hist_add(unsigned* h, float v) { atomicAdd(&h[key_of(v) >> 20], 1u); }
 
-template <bool VEC>
+template <bool VEC, bool PICK>
 __global__ __launch_bounds__(256) void tk_delta_hist_kernel(const float* __restrict__ x, const float* __restrict__ g,
-                                                            float* __restrict__ r, long n, TopKState* __restrict__ st) {
+                                                            float* __restrict__ r, long n, TopKState* __restrict__ st,
+                                                            int k) {
   __shared__ unsigned h[kTkBins1];
   for (int i = threadIdx.x; i < kTkBins1; i += 256) h[i] = 0u;
   __syncthreads();
@@ -290,37 +326,35 @@ __global__ __launch_bounds__(256) void tk_delta_hist_kernel(const float* __restr
     const int i = (j + (int)blockIdx.x * 64) & (kTkBins1 - 1);
     if (h[i]) atomicAdd(&st->hist[i], h[i]);
   }
-}
-
-// 1024 threads: bin b of h[0..nb) (nb = 1024 or 2048) such that above(b) < k <= above(b) + h[b],
-// scanning from the TOP bin down; above(b) = sum of the bins > b.  Result in res[0..1].
-FEDMI_DEV void tk_find_top(const unsigned* h, int nb, unsigned k, unsigned* scratch, unsigned* res) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, per = nb >> 10;
-  unsigned s = 0u;
-  for (int j = 0; j < per; ++j) s += h[nb - 1 - (t * per + j)];
-  unsigned inc = s;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const unsigned v = __shfl_up(inc, off, 64);
-    if (lane >= off) inc += v;
-  }
-  if (lane == 63) scratch[w] = inc;
+  if (!PICK) return;
+  // tk_pick1's work in the LAST workgroup to arrive (cdna_hip_programming.md Guideline 16: flush retired, one
+  // agent release, relaxed ticket; the last arriver acquires) -- one launch less per call
+  __shared__ int last;
+  __shared__ unsigned scratch[32], res[2];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0) {
-    unsigned a = 0u;
-    for (int q = 0; q < 16; ++q) { const unsigned v = scratch[q]; scratch[16 + q] = a; a += v; }
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1u;
   }
   __syncthreads();
-  const unsigned excl = scratch[16 + w] + inc - s;
-  if (excl < k && k <= excl + s) {
-    unsigned above = excl;
-    for (int j = 0; j < per; ++j) {
-      const int b = nb - 1 - (t * per + j);
-      if (above + h[b] >= k) { res[0] = (unsigned)b; res[1] = above; break; }
-      above += h[b];
-    }
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (int i = threadIdx.x; i < kTkBins1; i += 256) {
+    h[i] = __hip_atomic_load(&st->hist[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st->hist[i] = 0u;                        // zero for the next call (graph-safe: no memset node)
   }
   __syncthreads();
+  tk_find_top<256>(h, kTkBins1, (unsigned)k, scratch, res);
+  if (threadIdx.x == 0) {
+    st->b1 = (int)res[0];
+    st->n_above = (int)res[1];
+    st->need = k - (int)res[1];
+    st->out_cnt = 0;
+    st->cand_cnt = 0;
+    st->ticket = 0u;
+  }
 }
 
 __global__ __launch_bounds__(1024) void tk_pick1_kernel(TopKState* __restrict__ st, int k) {
@@ -361,23 +395,15 @@ __global__ __launch_bounds__(1024) void tk_pick2_kernel(TopKState* __restrict__ 
   }
 }
 
-// wave-aggregated append into a block-local (LDS) counter; returns this lane's slot (valid if flag)
-FEDMI_DEV int tk_append_lds(int* counter, bool flag) {
-  const unsigned long long m = __ballot(flag);
-  if (m == 0ull) return 0;
-  const int lane = threadIdx.x & 63;
-  int base = 0;
-  if (lane == 0) base = atomicAdd(counter, (int)__popcll(m));
-  base = __shfl(base, 0, 64);
-  const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  return base + (int)__popcll(m & lt);
-}
+// workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its outstanding
+// global loads (a __syncthreads() would also drain prefetched loads of the next pass)
+FEDMI_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Winners and candidates are staged in LDS and appended to the global lists once per workgroup (two
 // global atomics per flush): per-wave global atomics on the two list counters serialise at one L2
 // address each (2.4 ms at 11 M entries, measured).
 constexpr int kTkStage = 4096;   // >= 2 iterations' worth (8 x 256 per iteration)
-template <bool H2>
+template <bool H2, bool PICK2 = false>
 __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r, long n, TopKState* __restrict__ st,
                                                           int* __restrict__ idx, float* __restrict__ val,
                                                           int* __restrict__ cidx, unsigned* __restrict__ ckey) {
@@ -392,32 +418,73 @@ __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r,
   if (H2)
     for (int i = threadIdx.x; i < kTkBins1; i += 256) h2[i] = 0u;
   __syncthreads();
-  // uniform trip count per workgroup: every lane takes part in every ballot and barrier; 8 elements per
-  // thread per iteration, loaded before any is used
-  for (long i0 = (long)blockIdx.x * 2048; i0 < n; i0 += stride * 8) {
+  // uniform trip count per workgroup: every lane takes part in every ballot and barrier.  8 elements per
+  // thread per pass; the NEXT pass's 8 loads are issued before this pass is processed, and the pass's
+  // barriers wait for LDS operations only (lds_barrier), so they stay in flight across it
+  // (loads are unconditional -- clamped address, masked value -- so no branch splits them and the compiler can
+  // wait for the older pass only)
+  float nx[8];
+  long i0 = (long)blockIdx.x * 2048;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const long i = i0 + u * 256 + threadIdx.x;
+    const float v = r[i < n ? i : n - 1];
+    nx[u] = i < n ? v : 0.f;
+  }
+  for (; i0 < n; i0 += stride * 8) {
     float dv[8];
 #pragma unroll
+    for (int u = 0; u < 8; ++u) dv[u] = nx[u];
+    const long i1 = i0 + stride * 8;
+#pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const long i = i0 + u * 256 + threadIdx.x;
-      dv[u] = i < n ? r[i] : 0.f;
+      const long i = i1 + u * 256 + threadIdx.x;
+      const float v = r[i < n ? i : n - 1];   // disjoint from this pass's elements (zeroed below when selected)
+      nx[u] = i < n ? v : 0.f;
     }
+    // classify all 8 first, then ONE pair of LDS appends per wave for the whole pass (two independent
+    // returning atomics instead of 16 dependent ones); slots follow from the 8 ballots
+    unsigned key[8];
+    unsigned long long ms[8], mc[8];
+    int ts = 0, tc = 0;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const long i = i0 + u * 256 + threadIdx.x;
       const bool in = i < n;
-      const unsigned key = key_of(dv[u]), bin = key >> 20;
-      const bool sel = in && bin > b1, cand = in && bin == b1;
-      const int ps = tk_append_lds(&n_s, sel);
-      const int pc = tk_append_lds(&n_c, cand);
-      if (sel) { s_si[ps] = (int)i; s_sv[ps] = dv[u]; r[i] = 0.f; }
-      if (cand) {
-        s_ci[pc] = (int)i;
-        s_ck[pc] = key;
-        if (H2) atomicAdd(&h2[(key >> 9) & (kTkBins1 - 1)], 1u);
-      }
+      key[u] = key_of(dv[u]);
+      const unsigned bin = key[u] >> 20;
+      ms[u] = __ballot(in && bin > b1);
+      mc[u] = __ballot(in && bin == b1);
+      ts += (int)__popcll(ms[u]);
+      tc += (int)__popcll(mc[u]);
     }
-    __syncthreads();
-    const bool last = i0 + stride * 8 >= n;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int bs = 0, bc = 0;
+    if (lane == 0) {
+      if (ts) bs = atomicAdd(&n_s, ts);
+      if (tc) bc = atomicAdd(&n_c, tc);
+    }
+    bs = __shfl(bs, 0, 64);
+    bc = __shfl(bc, 0, 64);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long i = i0 + u * 256 + threadIdx.x;
+      if ((ms[u] >> lane) & 1ull) {
+        const int ps = bs + (int)__popcll(ms[u] & lt);
+        s_si[ps] = (int)i; s_sv[ps] = dv[u]; r[i] = 0.f;
+      }
+      if ((mc[u] >> lane) & 1ull) {
+        const int pc = bc + (int)__popcll(mc[u] & lt);
+        s_ci[pc] = (int)i;
+        s_ck[pc] = key[u];
+        if (H2) atomicAdd(&h2[(key[u] >> 9) & (kTkBins1 - 1)], 1u);
+      }
+      bs += (int)__popcll(ms[u]);
+      bc += (int)__popcll(mc[u]);
+    }
+    lds_barrier();
+    const bool last = i1 >= n;
     if (last || n_s > kTkStage - 8 * 256 || n_c > kTkStage - 8 * 256) {
       if (threadIdx.x == 0) {
         b_s = n_s ? atomicAdd(&st->out_cnt, n_s) : 0;
@@ -426,9 +493,9 @@ __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r,
       __syncthreads();
       for (int j = threadIdx.x; j < n_s; j += 256) { idx[b_s + j] = s_si[j]; val[b_s + j] = s_sv[j]; }
       for (int j = threadIdx.x; j < n_c; j += 256) { cidx[b_c + j] = s_ci[j]; ckey[b_c + j] = s_ck[j]; }
-      __syncthreads();
+      lds_barrier();
       if (threadIdx.x == 0) { n_s = 0; n_c = 0; }
-      __syncthreads();
+      lds_barrier();
     }
   }
   if (H2) {
@@ -436,6 +503,35 @@ __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r,
     for (int j = threadIdx.x; j < kTkBins1; j += 256) {
       const int i = (j + (int)blockIdx.x * 64) & (kTkBins1 - 1);
       if (h2[i]) atomicAdd(&st->hist2[i], h2[i]);
+    }
+    if (!PICK2) return;
+    // tk_pick2's work in the last workgroup to arrive (same hand-off as tk_delta_hist_kernel's pick)
+    __shared__ int last;
+    __shared__ unsigned scratch[32], res[2];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const unsigned t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = t == gridDim.x - 1u;
+    }
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (int i = threadIdx.x; i < kTkBins1; i += 256) {
+      h2[i] = __hip_atomic_load(&st->hist2[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st->hist2[i] = 0u;
+    }
+    __syncthreads();
+    const int need = st->need;
+    tk_find_top<256>(h2, kTkBins1, (unsigned)need, scratch, res);
+    if (threadIdx.x == 0) {
+      st->b2 = (int)res[0];
+      st->n_above2 = (int)res[1];
+      st->need2 = need - (int)res[1];
+      st->out2_cnt = 0;
+      st->cand2_cnt = 0;
+      st->ticket = 0u;
     }
   }
 }
@@ -470,15 +566,39 @@ __global__ __launch_bounds__(256) void tk_compact2_kernel(float* __restrict__ r,
       const long j = j0 + u * 256 + threadIdx.x;
       dv[u] = (j < c && ((kk[u] >> 9) & (kTkBins1 - 1)) > b2) ? r[ci[u]] : 0.f;
     }
+    // one pair of LDS appends per wave per pass (see tk_compact1_kernel)
+    unsigned long long ms[8], mc[8];
+    int ts = 0, tc = 0;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const long j = j0 + u * 256 + threadIdx.x;
       const unsigned bin = (kk[u] >> 9) & (kTkBins1 - 1);
-      const bool sel = j < c && bin > b2, cand = j < c && bin == b2;
-      const int ps = tk_append_lds(&n_s, sel);
-      const int pc = tk_append_lds(&n_c, cand);
-      if (sel) { s_si[ps] = ci[u]; s_sv[ps] = dv[u]; r[ci[u]] = 0.f; }
-      if (cand) { s_ci[pc] = ci[u]; s_ck[pc] = kk[u]; }
+      ms[u] = __ballot(j < c && bin > b2);
+      mc[u] = __ballot(j < c && bin == b2);
+      ts += (int)__popcll(ms[u]);
+      tc += (int)__popcll(mc[u]);
+    }
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int bs = 0, bc = 0;
+    if (lane == 0) {
+      if (ts) bs = atomicAdd(&n_s, ts);
+      if (tc) bc = atomicAdd(&n_c, tc);
+    }
+    bs = __shfl(bs, 0, 64);
+    bc = __shfl(bc, 0, 64);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if ((ms[u] >> lane) & 1ull) {
+        const int ps = bs + (int)__popcll(ms[u] & lt);
+        s_si[ps] = ci[u]; s_sv[ps] = dv[u]; r[ci[u]] = 0.f;
+      }
+      if ((mc[u] >> lane) & 1ull) {
+        const int pc = bc + (int)__popcll(mc[u] & lt);
+        s_ci[pc] = ci[u]; s_ck[pc] = kk[u];
+      }
+      bs += (int)__popcll(ms[u]);
+      bc += (int)__popcll(mc[u]);
     }
     __syncthreads();
     const bool last = j0 + stride * 8 >= c;
@@ -658,13 +778,24 @@ void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* resid
   long hmax = 2048;
   if (const char* e = std::getenv("FEDMI_TK_HBLOCKS")) hmax = std::max(1L, std::atol(e));   // A/B: histogram grid cap
   const int blocks = (int)std::min<long>(hmax, std::max<long>(1, (n + 8 * 1024 - 1) / (8 * 1024)));
-  if (vec)
-    hipLaunchKernelGGL(tk_delta_hist_kernel<true>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s);
-  else
-    hipLaunchKernelGGL(tk_delta_hist_kernel<false>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s);
-  hipLaunchKernelGGL(tk_pick1_kernel, dim3(1), dim3(1024), 0, st, s, k);
-  long cmax = 2048;
-  if (const char* e = std::getenv("FEDMI_TK_CBLOCKS")) cmax = std::max(1L, std::atol(e));   // A/B: compaction grid cap
+  // the boundary-bin pick runs in the histogram kernel's last workgroup (FEDMI_TK_FUSE_PICK=0: its own launch)
+  static const bool fuse_pick = [] { const char* e = std::getenv("FEDMI_TK_FUSE_PICK"); return !(e && e[0] == '0'); }();
+  if (fuse_pick) {
+    if (vec)
+      hipLaunchKernelGGL((tk_delta_hist_kernel<true, true>), dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
+    else
+      hipLaunchKernelGGL((tk_delta_hist_kernel<false, true>), dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
+  } else {
+    if (vec)
+      hipLaunchKernelGGL((tk_delta_hist_kernel<true, false>), dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
+    else
+      hipLaunchKernelGGL((tk_delta_hist_kernel<false, false>), dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
+    hipLaunchKernelGGL(tk_pick1_kernel, dim3(1), dim3(1024), 0, st, s, k);
+  }
+  // compaction grid cap: 2 workgroups per CU (512) measured 103.5 vs 128 us at 11.2 M entries (2048: 4x the
+  // per-workgroup flushes of the staged lists and of the level-2 histogram); FEDMI_TK_CBLOCKS overrides
+  long cmax = 512;
+  if (const char* e = std::getenv("FEDMI_TK_CBLOCKS")) cmax = std::max(1L, std::atol(e));
   const int cblocks = (int)std::min<long>(cmax, std::max<long>(1, (n + 2 * 2048 - 1) / (2 * 2048)));
   if (n < kTkThreeLevel) {
     hipLaunchKernelGGL(tk_compact1_kernel<false>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx,
@@ -677,8 +808,14 @@ void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* resid
   // level-3 list of a few hundred for the single-workgroup exact select
   int* cidx2 = cidx + n;                     // second half of the 2n-entry candidate scratch
   unsigned* ckey2 = ckey + n;
-  hipLaunchKernelGGL(tk_compact1_kernel<true>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx, ckey);
-  hipLaunchKernelGGL(tk_pick2_kernel, dim3(1), dim3(1024), 0, st, s);
+  if (fuse_pick) {
+    hipLaunchKernelGGL((tk_compact1_kernel<true, true>), dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val,
+                       cidx, ckey);
+  } else {
+    hipLaunchKernelGGL((tk_compact1_kernel<true, false>), dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val,
+                       cidx, ckey);
+    hipLaunchKernelGGL(tk_pick2_kernel, dim3(1), dim3(1024), 0, st, s);
+  }
   const int c2blocks = (int)std::min<long>(1024, std::max<long>(1, (n / 50 + 2047) / 2048));
   hipLaunchKernelGGL(tk_compact2_kernel, dim3(c2blocks), dim3(256), 0, st, residual, s, cidx, ckey, idx, val, cidx2,
                      ckey2);
