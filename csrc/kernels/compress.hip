@@ -207,21 +207,20 @@ __global__ __launch_bounds__(256) void dequant_accum_kernel(const signed char* _
 }
 
 // ---------------------------------------------------------------------------
-// Fused error-feedback top-k (the default path): 3 launches (5 from 1 M entries), 2 full passes over the state.
+// Fused error-feedback top-k (the default path): 4 launches (6 from 1 M entries), 2 full passes over the state.
 //
 //   K1 tk_delta_hist   r <- x - g + r (the residual buffer holds d from here on), and a
 //                      histogram of the top 11 bits of |d| (key bits 30..20: exponent + 3
 //                      mantissa bits, each bin ~9 % of magnitude), LDS-privatised per
-//                      workgroup, nonzero bins added to the global histogram; the LAST workgroup
-//                      to arrive picks the bin b1 holding the k-th largest key and re-zeroes the
-//                      histogram and the append counters for the next call (tk_pick1 as its own
-//                      launch with FEDMI_TK_FUSE_PICK=0).
+//                      workgroup, nonzero bins added to the global histogram.  tk_pick1 (one
+//                      workgroup) then picks the bin b1 holding the k-th largest key and re-zeroes the
+//                      histogram and the append counters for the next call.
 //   K2 tk_compact1     keys in bins > b1 are selected outright (idx/val appended, r <- 0);
 //                      keys in bin b1 become candidates (index + key appended).  Appends are
 //                      staged in LDS (one pair of LDS atomics per wave per pass) and flushed with
 //                      one global atomic per list per workgroup.  Large n: also the level-2
-//                      histogram of the candidates, whose pick (tk_pick2) runs in the last workgroup;
-//                      tk_compact2 then splits the candidates the same way one level down.
+//                      histogram of the candidates (picked by tk_pick2); tk_compact2 then splits the
+//                      candidates the same way one level down.
 //   K3 tk_select2      one workgroup: exact selection of the remaining `need` among the
 //                      candidates (LDS radix passes over the undecided key bits; exact ties
 //                      resolved by the smallest indices, 3 more passes only when needed).
@@ -743,95 +742,6 @@ __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r,
   tk_select_body<LEVELS>(r, c, nab, m, cidx, ckey, idx, val, &st->pad[0], h, scratch, res, &wcount);
 }
 
-// Small states (n <= kTkSmall, e.g. LeNet's 62 k): the whole error-feedback top-k in ONE 1024-thread workgroup --
-// delta + level-1 histogram, the pick, the compaction (winners straight into idx / val, candidates into
-// cidx / ckey) and the exact select -- one launch instead of three (each launch of the multi-workgroup path
-// costs more than the work at this size).
-constexpr long kTkSmall = 131072;
-__global__ __launch_bounds__(1024) void tk_small_kernel(const float* __restrict__ x, const float* __restrict__ g,
-                                                        float* __restrict__ r, long n, int k, TopKState* __restrict__ st,
-                                                        int* __restrict__ cidx, unsigned* __restrict__ ckey,
-                                                        int* __restrict__ idx, float* __restrict__ val) {
-  __shared__ unsigned h[kTkBins1];
-  __shared__ unsigned scratch[32], res[2];
-  __shared__ int wcount, n_s, n_c;
-  const int t = threadIdx.x, lane = t & 63;
-  for (int i = t; i < kTkBins1; i += 1024) h[i] = 0u;
-  if (t == 0) { n_s = 0; n_c = 0; }
-  __syncthreads();
-  // pass 1: d = x - g + r (into r), histogram of the top key bits; 4 elements per thread per step, loads first
-  for (long i0 = t; i0 < n; i0 += 4 * 1024) {
-    float a[4], b[4], q[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long i = i0 + u * 1024;
-      const long ic = i < n ? i : n - 1;
-      a[u] = x[ic]; b[u] = g[ic]; q[u] = r[ic];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long i = i0 + u * 1024;
-      if (i < n) {
-        const float d = a[u] - b[u] + q[u];
-        r[i] = d;
-        atomicAdd(&h[key_of(d) >> 20], 1u);
-      }
-    }
-  }
-  __syncthreads();
-  tk_find_top<1024>(h, kTkBins1, (unsigned)k, scratch, res);
-  const unsigned b1 = res[0];
-  const int nab = (int)res[1];
-  const unsigned need = (unsigned)k - res[1];
-  // pass 2: bins above b1 win outright, bin b1 holds the candidates (one pair of LDS appends per wave per step)
-  const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (long i0 = 0; i0 < n; i0 += 4 * 1024) {      // uniform trip count: every lane takes part in the ballots
-    float dv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long i = i0 + u * 1024 + t;
-      const float v = r[i < n ? i : n - 1];
-      dv[u] = i < n ? v : 0.f;
-    }
-    unsigned key[4];
-    unsigned long long ms[4], mc[4];
-    int ts = 0, tc = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long i = i0 + u * 1024 + t;
-      key[u] = key_of(dv[u]);
-      const unsigned bin = key[u] >> 20;
-      ms[u] = __ballot(i < n && bin > b1);
-      mc[u] = __ballot(i < n && bin == b1);
-      ts += (int)__popcll(ms[u]);
-      tc += (int)__popcll(mc[u]);
-    }
-    int bs = 0, bc = 0;
-    if (lane == 0) {
-      if (ts) bs = atomicAdd(&n_s, ts);
-      if (tc) bc = atomicAdd(&n_c, tc);
-    }
-    bs = __shfl(bs, 0, 64);
-    bc = __shfl(bc, 0, 64);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long i = i0 + u * 1024 + t;
-      if ((ms[u] >> lane) & 1ull) {
-        const int ps = bs + (int)__popcll(ms[u] & lt);
-        idx[ps] = (int)i; val[ps] = dv[u]; r[i] = 0.f;
-      }
-      if ((mc[u] >> lane) & 1ull) {
-        const int pc = bc + (int)__popcll(mc[u] & lt);
-        cidx[pc] = (int)i; ckey[pc] = key[u];
-      }
-      bs += (int)__popcll(ms[u]);
-      bc += (int)__popcll(mc[u]);
-    }
-  }
-  __syncthreads();                             // the candidate list (global) is complete for every wave
-  tk_select_body<2>(r, n_c, nab, need, cidx, ckey, idx, val, &st->pad[0], h, scratch, res, &wcount);
-}
-
 int grid_for(long n) {
   long b = (n + 255) / 256;
   if (b < 1) b = 1;
@@ -875,19 +785,18 @@ size_t topk_state_bytes() { return sizeof(TopKState); }
 void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* residual, long n, int k, void* state,
                     int* cidx, unsigned* ckey, int* idx, float* val) {
   TopKState* s = reinterpret_cast<TopKState*>(state);
-  static const bool small_on = [] { const char* e = std::getenv("FEDMI_TK_SMALL"); return !(e && e[0] == '0'); }();
-  if (small_on && n <= kTkSmall) {
-    hipLaunchKernelGGL(tk_small_kernel, dim3(1), dim3(1024), 0, st, x, g, residual, n, k, s, cidx, ckey, idx, val);
-    return;
-  }
   const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g) |
                      reinterpret_cast<uintptr_t>(residual)) & 15) == 0;
   // ~8 float4 per thread, at most 2048 workgroups (their nonzero bins go to the global histogram)
   long hmax = 2048;
   if (const char* e = std::getenv("FEDMI_TK_HBLOCKS")) hmax = std::max(1L, std::atol(e));   // A/B: histogram grid cap
   const int blocks = (int)std::min<long>(hmax, std::max<long>(1, (n + 8 * 1024 - 1) / (8 * 1024)));
-  // the boundary-bin pick runs in the histogram kernel's last workgroup (FEDMI_TK_FUSE_PICK=0: its own launch)
-  static const bool fuse_pick = [] { const char* e = std::getenv("FEDMI_TK_FUSE_PICK"); return !(e && e[0] == '0'); }();
+  // opt-in (FEDMI_TK_FUSE_PICK=1): the boundary-bin picks in the last-arriving workgroup of the histogram /
+  // compaction kernels instead of their own launches -- measured SLOWER (132 vs 94.6 us at 11.2 M entries,
+  // 23.4 vs 22.7 us at 62 k: every workgroup pays an agent-scope release and a drained flush for one launch saved).
+  // A one-workgroup kernel for small states (all passes in one launch) measured 38.5 vs 22.7 us at 62 k (one CU's
+  // bandwidth) and was dropped.
+  static const bool fuse_pick = [] { const char* e = std::getenv("FEDMI_TK_FUSE_PICK"); return e && e[0] == '1'; }();
   if (fuse_pick) {
     if (vec)
       hipLaunchKernelGGL((tk_delta_hist_kernel<true, true>), dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
