@@ -538,16 +538,45 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_d
   __syncthreads();
   if (!last) return;
   const int slabs = (int)gridDim.y;
-  for (int cb = 0; cb < C; cb += 64) {
-    const int c = cb + (threadIdx.x & 63);
-    const float a1 = ordered_slab_sum(part, slabs, 2LL * C, c, c < C);
+  // both slab sums of a channel in ONE pass, as many lanes per channel as the 256 threads allow (C <= 128:
+  // 256 / C lanes; wider: 64-channel chunks x 4 lanes), 8 slabs x 2 sums in flight per lane; lane l takes slabs
+  // l, l + L, ... and the lanes are combined in order (deterministic for a given C)
+  __shared__ float fr[2][256];
+  const int t = threadIdx.x;
+  const int L = C <= 128 ? 256 / C : 4, CW = C <= 128 ? C : 64;
+  for (int cb = 0; cb < C; cb += CW) {
+    const int cl = t % CW, l = t / CW, c = cb + cl;
+    const bool valid = l < L && c < C;
+    float v1 = 0.f, v2 = 0.f;
+    if (valid) {
+      int b = l;
+      for (; b + 7 * L < slabs; b += 8 * L) {
+        float x1[8], x2[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float* row = part + (long long)(b + u * L) * 2 * C;
+          x1[u] = row[c];
+          x2[u] = row[C + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { v1 += x1[u]; v2 += x2[u]; }
+      }
+      for (; b < slabs; b += L) {
+        const float* row = part + (long long)b * 2 * C;
+        v1 += row[c];
+        v2 += row[C + c];
+      }
+    }
+    fr[0][t] = v1;
+    fr[1][t] = v2;
     __syncthreads();
-    const float a2 = ordered_slab_sum(part + C, slabs, 2LL * C, c, c < C);
-    __syncthreads();
-    if (!(threadIdx.x >> 6) && c < C) {
+    if (l == 0 && c < C) {
+      float a1 = 0.f, a2 = 0.f;
+      for (int q = 0; q < L; ++q) { a1 += fr[0][q * CW + cl]; a2 += fr[1][q * CW + cl]; }
       if (fin.mode == 1) bn_fwd_fin(fin, c, a1, a2);
       else bn_bwd_fin(fin, c, a1, a2);
     }
+    __syncthreads();
   }
 }
 
@@ -612,7 +641,12 @@ bool bn_rows_fused() {
 int rows_slabs(long long M, int C) {
   const int VL = C / rows_vw(C), vt = VL < 256 ? VL : 256, RL = 256 / vt;
   const long long tiles = (VL + vt - 1) / vt;
-  long long sl = M / ((long long)RL * 16);          // >= 16 rows per row lane
+  static const long long per_lane = [] {           // rows per row lane (A/B: FEDMI_ROWS_PER_LANE)
+    const char* e = std::getenv("FEDMI_ROWS_PER_LANE");
+    const long long v = e ? std::atoll(e) : 16;
+    return v < 1 ? 1LL : v;
+  }();
+  long long sl = M / ((long long)RL * per_lane);    // >= per_lane rows per row lane
   const long long cap = (2048 + tiles - 1) / tiles;  // ~2048 blocks in flight at most
   if (sl > cap) sl = cap;
   if (sl < 1) sl = 1;

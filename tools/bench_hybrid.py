@@ -5,6 +5,7 @@ fedmi's HIP kernels), eager and HIP-graph replayed.
     python tools/bench_hybrid.py [model ...]      -> one JSON line per (model, mode)
 """
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -24,7 +25,10 @@ dev = torch.device("cuda", 0)
 data = make_dataset("synthetic-cifar10", device=dev, n_train=128 * 12, n_test=1000, seed=0)
 for name in MODELS:
     init = build_model(name).state_dict()
-    for mode in ("fp32", "native-eager", "native-graph-nofuse", "native-graph"):
+    modes = ("fp32", "native-eager", "native-graph-nofuse", "native-graph")
+    if os.environ.get("BENCH_MODES"):
+        modes = tuple(os.environ["BENCH_MODES"].split(","))
+    for mode in modes:
         tr = TorchTrainer(name, data, dev, TrainerConfig(seed=1), init_state=init, hybrid=(mode != "fp32"))
         tr.use_graph = "graph" in mode
         if tr.mode is not None:
