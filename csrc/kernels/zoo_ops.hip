@@ -96,6 +96,38 @@ FEDMI_DEV long long zoffset(const ZTensor& shape, const ZTensor& t, long long i6
   return off + (long long)i * t.stride[0];
 }
 
+// The N-d coordinates of linear index i in `shape` (the divisions), computed ONCE per element and shared by
+// every operand of an elementwise op; zoff() is then one multiply-add per dimension per operand (zoffset per
+// operand repeated the divisions: the index math, not memory, bounded the 4-6 operand BN passes).
+struct ZCoord {
+  uint32_t c[ZMAXD];
+};
+
+FEDMI_DEV ZCoord zcoords(const ZTensor& shape, long long i64) {
+  ZCoord k;
+  uint32_t i = (uint32_t)i64;
+#pragma unroll
+  for (int d = ZMAXD - 1; d >= 1; --d) {
+    k.c[d] = 0u;
+    if (d < shape.ndim) {
+      const uint32_t sz = (uint32_t)shape.size[d];
+      const uint32_t q = i / sz;
+      k.c[d] = i - q * sz;
+      i = q;
+    }
+  }
+  k.c[0] = i;
+  return k;
+}
+
+FEDMI_DEV long long zoff(const ZCoord& k, const ZTensor& t, int ndim) {
+  long long off = (long long)k.c[0] * t.stride[0];
+#pragma unroll
+  for (int d = 1; d < ZMAXD; ++d)
+    if (d < ndim) off += (long long)k.c[d] * t.stride[d];
+  return off;
+}
+
 FEDMI_DEV float ew_apply(const EwArgs& a, float x0, float x1, float x2, float x3, float x4, float x5 = 0.f) {
   switch (a.op) {
     case EW_COPY: return x0;
@@ -178,13 +210,14 @@ template <int VW>
 __global__ __launch_bounds__(256) void ew_vec_kernel(EwArgs a, long long nv) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    const ZCoord kc = zcoords(a.o, i);
     float x[6][VW];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       if (a.in[k].p && ((a.vmask >> k) & 1)) {
-        vload<VW>(a.in[k].p, a.in[k].dtype, zoffset(a.o, a.in[k], i), x[k]);
+        vload<VW>(a.in[k].p, a.in[k].dtype, zoff(kc, a.in[k], a.o.ndim), x[k]);
       } else {
-        const float sv = a.in[k].p ? zload(a.in[k], zoffset(a.o, a.in[k], i)) : 0.f;
+        const float sv = a.in[k].p ? zload(a.in[k], zoff(kc, a.in[k], a.o.ndim)) : 0.f;
 #pragma unroll
         for (int u = 0; u < VW; ++u) x[k][u] = sv;
       }
@@ -192,7 +225,7 @@ __global__ __launch_bounds__(256) void ew_vec_kernel(EwArgs a, long long nv) {
     float v[VW];
 #pragma unroll
     for (int u = 0; u < VW; ++u) v[u] = ew_apply(a, x[0][u], x[1][u], x[2][u], x[3][u], x[4][u], x[5][u]);
-    vstore<VW>(a.o.p, a.o.dtype, zoffset(a.o, a.o, i), v);
+    vstore<VW>(a.o.p, a.o.dtype, zoff(kc, a.o, a.o.ndim), v);
   }
 }
 
@@ -200,13 +233,14 @@ __global__ __launch_bounds__(256) void ew_kernel(EwArgs a, long long n) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   const uint32_t ctr = a.ctr ? (uint32_t)a.ctr[0] : 0u;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const ZCoord kc = zcoords(a.o, i);
     float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f, x4 = 0.f, x5 = 0.f;
-    if (a.in[0].p) x0 = zload(a.in[0], zoffset(a.o, a.in[0], i));
-    if (a.in[1].p) x1 = zload(a.in[1], zoffset(a.o, a.in[1], i));
-    if (a.in[2].p) x2 = zload(a.in[2], zoffset(a.o, a.in[2], i));
-    if (a.in[3].p) x3 = zload(a.in[3], zoffset(a.o, a.in[3], i));
-    if (a.in[4].p) x4 = zload(a.in[4], zoffset(a.o, a.in[4], i));
-    if (a.in[5].p) x5 = zload(a.in[5], zoffset(a.o, a.in[5], i));
+    if (a.in[0].p) x0 = zload(a.in[0], zoff(kc, a.in[0], a.o.ndim));
+    if (a.in[1].p) x1 = zload(a.in[1], zoff(kc, a.in[1], a.o.ndim));
+    if (a.in[2].p) x2 = zload(a.in[2], zoff(kc, a.in[2], a.o.ndim));
+    if (a.in[3].p) x3 = zload(a.in[3], zoff(kc, a.in[3], a.o.ndim));
+    if (a.in[4].p) x4 = zload(a.in[4], zoff(kc, a.in[4], a.o.ndim));
+    if (a.in[5].p) x5 = zload(a.in[5], zoff(kc, a.in[5], a.o.ndim));
     float v;
     if (a.op == EW_BERN) {
       const uint32_t h = hash3(a.seed, ctr, (uint32_t)i ^ (uint32_t)(i >> 32));
@@ -214,7 +248,7 @@ __global__ __launch_bounds__(256) void ew_kernel(EwArgs a, long long n) {
     } else {
       v = ew_apply(a, x0, x1, x2, x3, x4, x5);
     }
-    zstore(a.o, zoffset(a.o, a.o, i), v);
+    zstore(a.o, zoff(kc, a.o, a.o.ndim), v);
   }
 }
 
