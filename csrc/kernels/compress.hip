@@ -406,7 +406,12 @@ FEDMI_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" 
 // global atomics per flush): per-wave global atomics on the two list counters serialise at one L2
 // address each (2.4 ms at 11 M entries, measured).
 constexpr int kTkStage = 4096;   // >= 2 iterations' worth (8 x 256 per iteration)
-template <bool H2, bool PICK2 = false>
+template <int LEVELS, int NT>
+FEDMI_DEV void tk_select_body(float* __restrict__ r, int c, int nab, unsigned m, const int* __restrict__ cidx,
+                              const unsigned* __restrict__ ckey, int* __restrict__ idx, float* __restrict__ val,
+                              int* overflow, unsigned* h, unsigned* scratch, unsigned* res, int* wcount_p);
+
+template <bool H2, bool PICK2 = false, bool SEL = false>
 __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r, long n, TopKState* __restrict__ st,
                                                           int* __restrict__ idx, float* __restrict__ val,
                                                           int* __restrict__ cidx, unsigned* __restrict__ ckey) {
@@ -537,6 +542,29 @@ __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r,
       st->ticket = 0u;
     }
   }
+  if (SEL && !H2) {
+    // tk_select2's work in the last-arriving workgroup (below the 3-level threshold the candidate list is a few
+    // thousand entries): one launch less per call
+    __shared__ int last_s, wcount_s;
+    __shared__ unsigned scr_s[32], res_s[2];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const unsigned t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_s = t == gridDim.x - 1u;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int c = __hip_atomic_load(&st->cand_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int nab = st->n_above;
+    const unsigned m = (unsigned)st->need;
+    __syncthreads();
+    if (threadIdx.x == 0) st->ticket = 0u;
+    tk_select_body<2, 256>(r, c, nab, m, cidx, ckey, idx, val, &st->pad[0], reinterpret_cast<unsigned*>(s_si), scr_s,
+                           res_s, &wcount_s);
+  }
 }
 
 // level 2 (large n): candidates with key bits 19..9 above b2 are winners (positions n_above + [0, n_above2)),
@@ -624,7 +652,7 @@ __global__ __launch_bounds__(256) void tk_compact2_kernel(float* __restrict__ r,
 // idx / val [nab, nab + m).  LEVELS == 2: the level-1 candidates (key bits 19..0 undecided, 2 radix passes);
 // LEVELS == 1: the level-3 list of the 3-level path (bits 19..9 decided; one pass over bits 9..0, bit 9 common
 // to all).  h: >= kTkBins1 LDS words, scratch: 32, res: 2.
-template <int LEVELS>
+template <int LEVELS, int NT = 1024>
 FEDMI_DEV void tk_select_body(float* __restrict__ r, int c, int nab, unsigned m, const int* __restrict__ cidx,
                               const unsigned* __restrict__ ckey, int* __restrict__ idx, float* __restrict__ val,
                               int* overflow, unsigned* h, unsigned* scratch, unsigned* res, int* wcount_p) {
@@ -634,34 +662,34 @@ FEDMI_DEV void tk_select_body(float* __restrict__ r, int c, int nab, unsigned m,
   // pass A: key bits 19..10
   unsigned bA = 0u, mA = m;
   if (LEVELS == 2) {
-    for (int i = t; i < 1024; i += 1024) h[i] = 0u;
+    for (int i = t; i < 1024; i += NT) h[i] = 0u;
     __syncthreads();
-    for (int j0 = t; j0 < c; j0 += 8 * 1024) {       // 8 loads in flight per thread
+    for (int j0 = t; j0 < c; j0 += 8 * NT) {         // 8 loads in flight per thread
       unsigned kk[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) kk[u] = j0 + u * 1024 < c ? ckey[j0 + u * 1024] : 0u;
+      for (int u = 0; u < 8; ++u) kk[u] = j0 + u * NT < c ? ckey[j0 + u * NT] : 0u;
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (j0 + u * 1024 < c) atomicAdd(&h[(kk[u] >> 10) & 1023u], 1u);
+        if (j0 + u * NT < c) atomicAdd(&h[(kk[u] >> 10) & 1023u], 1u);
     }
     __syncthreads();
-    tk_find_top(h, 1024, m, scratch, res);
+    tk_find_top<NT>(h, 1024, m, scratch, res);
     bA = res[0];
     mA = m - res[1];
   }
   // pass B: key bits 9..0 of the keys in bin bA
-  h[t] = 0u;
+  for (int i = t; i < 1024; i += NT) h[i] = 0u;
   __syncthreads();
-  for (int j0 = t; j0 < c; j0 += 8 * 1024) {
+  for (int j0 = t; j0 < c; j0 += 8 * NT) {
     unsigned kk[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) kk[u] = j0 + u * 1024 < c ? ckey[j0 + u * 1024] : 0u;
+    for (int u = 0; u < 8; ++u) kk[u] = j0 + u * NT < c ? ckey[j0 + u * NT] : 0u;
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (j0 + u * 1024 < c && (LEVELS == 1 || ((kk[u] >> 10) & 1023u) == bA)) atomicAdd(&h[kk[u] & 1023u], 1u);
+      if (j0 + u * NT < c && (LEVELS == 1 || ((kk[u] >> 10) & 1023u) == bA)) atomicAdd(&h[kk[u] & 1023u], 1u);
   }
   __syncthreads();
-  tk_find_top(h, 1024, mA, scratch, res);
+  tk_find_top<NT>(h, 1024, mA, scratch, res);
   const unsigned bB = res[0];
   const unsigned T = LEVELS == 2 ? ((bA << 10) | bB) : bB;   // undecided low bits of the k-th largest key
   const unsigned ties_take = mA - res[1], ties = h[bB];
@@ -675,14 +703,14 @@ FEDMI_DEV void tk_select_body(float* __restrict__ r, int c, int nab, unsigned m,
     const int widths[3] = {11, 10, 10};
     for (int ps = 0; ps < 3; ++ps) {
       const int nb = 1 << widths[ps], sh = shifts[ps];
-      for (int i = t; i < kTkBins1; i += 1024) h[i] = 0u;
+      for (int i = t; i < kTkBins1; i += NT) h[i] = 0u;
       __syncthreads();
-      for (int j = t; j < c; j += 1024) {
+      for (int j = t; j < c; j += NT) {
         const unsigned ix = (unsigned)cidx[j];
         if ((ckey[j] & LOWMASK) == T && (ix & pmask) == pre) atomicAdd(&h[nb - 1 - ((ix >> sh) & (nb - 1))], 1u);
       }
       __syncthreads();
-      tk_find_top(h, nb < 1024 ? 1024 : nb, kk, scratch, res);
+      tk_find_top<NT>(h, nb < 1024 ? 1024 : nb, kk, scratch, res);
       pre |= (unsigned)(nb - 1 - (int)res[0]) << sh;
       pmask |= (unsigned)(nb - 1) << sh;
       kk -= res[1];
@@ -692,22 +720,22 @@ FEDMI_DEV void tk_select_body(float* __restrict__ r, int c, int nab, unsigned m,
   }
   if (t == 0) wcount = 0;
   __syncthreads();
-  for (int j0 = 0; j0 < c; j0 += 4 * 1024) {      // uniform trip count: every lane takes part in the ballots
+  for (int j0 = 0; j0 < c; j0 += 4 * NT) {      // uniform trip count: every lane takes part in the ballots
     unsigned kk[4];
     int ci[4];
     float dv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int j = j0 + u * 1024 + t;
+      const int j = j0 + u * NT + t;
       kk[u] = j < c ? ckey[j] : 0u;
       ci[u] = j < c ? cidx[j] : 0;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) dv[u] = j0 + u * 1024 + t < c ? r[ci[u]] : 0.f;
+    for (int u = 0; u < 4; ++u) dv[u] = j0 + u * NT + t < c ? r[ci[u]] : 0.f;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const unsigned low = kk[u] & LOWMASK;
-      const bool sel = j0 + u * 1024 + t < c && (low > T || (low == T && (unsigned)ci[u] <= ilim));
+      const bool sel = j0 + u * NT + t < c && (low > T || (low == T && (unsigned)ci[u] <= ilim));
       const unsigned long long msk = __ballot(sel);
       int base = 0;
       if ((t & 63) == 0 && msk) base = atomicAdd(&wcount, (int)__popcll(msk));
@@ -815,9 +843,17 @@ void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* resid
   if (const char* e = std::getenv("FEDMI_TK_CBLOCKS")) cmax = std::max(1L, std::atol(e));
   const int cblocks = (int)std::min<long>(cmax, std::max<long>(1, (n + 2 * 2048 - 1) / (2 * 2048)));
   if (n < kTkThreeLevel) {
-    hipLaunchKernelGGL(tk_compact1_kernel<false>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx,
-                       ckey);
-    hipLaunchKernelGGL(tk_select2_kernel<2>, dim3(1), dim3(1024), 0, st, residual, s, cidx, ckey, idx, val);
+    // opt-in (FEDMI_TK_FUSE_SELECT=1): the exact select in the compaction's last-arriving 256-thread workgroup
+    // instead of its own 1024-thread launch -- correct but measured slower (34 vs 24 us at 62 k entries)
+    static const bool fuse_sel = [] { const char* e = std::getenv("FEDMI_TK_FUSE_SELECT"); return e && e[0] == '1'; }();
+    if (fuse_sel) {
+      hipLaunchKernelGGL((tk_compact1_kernel<false, false, true>), dim3(cblocks), dim3(256), 0, st, residual, n, s, idx,
+                         val, cidx, ckey);
+    } else {
+      hipLaunchKernelGGL(tk_compact1_kernel<false>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx,
+                         ckey);
+      hipLaunchKernelGGL(tk_select2_kernel<2>, dim3(1), dim3(1024), 0, st, residual, s, cidx, ckey, idx, val);
+    }
     return;
   }
   // large n: the boundary bin holds ~1-3 % of the entries -- too many for one workgroup; a second histogram
