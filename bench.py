@@ -62,21 +62,24 @@ def _baseline_rounds(model: str, n: int):
     return table.get(n)
 
 
-def _timed(fn, iters: int, device) -> float:
-    """ms per call (device time, cuda events), MAX over ranks."""
-    for _ in range(3):
-        fn()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        fn()
-    e1.record()
-    torch.cuda.synchronize(device)
-    t = torch.tensor([e0.elapsed_time(e1) / iters], dtype=torch.float64)
-    if dist.get_backend() == "nccl":
-        t = t.to(device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+def _breakdown(marks, phases, t0: float, t1: float, steps: int) -> dict:
+    """Median per-round device ms of each phase (events between the phase boundaries), device busy
+    per round (first -> last boundary), host ms spent issuing each phase, and the wall-clock round."""
+    import statistics
+
+    dev = {p: [] for p in phases}
+    host = {p: [] for p in phases}
+    span = []
+    for row in marks:
+        for i, p in enumerate(phases):
+            dev[p].append(row[i][1].elapsed_time(row[i + 1][1]))
+            host[p].append((row[i + 1][0] - row[i][0]) * 1e3)
+        span.append(row[0][1].elapsed_time(row[-1][1]))
+    gaps = [marks[i][0][1].elapsed_time(marks[i + 1][0][1]) - span[i] for i in range(len(marks) - 1)]
+    med = lambda v: round(statistics.median(v), 4) if v else None  # noqa: E731
+    return {"device_ms": {p: med(v) for p, v in dev.items()}, "host_issue_ms": {p: med(v) for p, v in host.items()},
+            "device_round_span_ms": med(span), "device_idle_between_rounds_ms": med(gaps),
+            "wall_ms_per_round": round((t1 - t0) / steps * 1e3, 4), "rounds": len(marks)}
 
 
 def make_transport(args, trainer, rank: int, world: int, rehearse: bool, device):
@@ -111,48 +114,18 @@ def make_transport(args, trainer, rank: int, world: int, rehearse: bool, device)
         if want != "auto":
             raise RuntimeError("--allreduce peer transport failed on some rank")
         return None, {"chosen": "rccl", "reason": "peer transport unavailable"}
-    g = torch.Generator(device=device).manual_seed(1234 + rank)
-    probe = torch.randn(x.numel(), generator=g, device=device)
-    ref = probe.clone()
-    if rehearse:
-        ref_h = ref.cpu()
-        dist.all_reduce(ref_h)
-        ref = (ref_h / world).to(device)
-    else:
-        dist.all_reduce(ref, op=dist.ReduceOp.AVG)
-    info = {"verified_against": "gloo" if rehearse else "rccl"}
-    times = {}
-    for algo in algos:
-        peer.algo = algo
-        got = probe.clone()
-        peer.allreduce_mean_(got)
-        good = torch.allclose(got, ref, rtol=1e-5, atol=1e-6) and peer.error() == 0
-        okt = torch.tensor([1.0 if good else 0.0], device=device if not rehearse else "cpu")
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        if okt.item() < 1:
-            info[f"{algo}_verified"] = False
-            continue
-        info[f"{algo}_verified"] = True
-        buf = x.detach().clone()
-        times[algo] = _timed(lambda: peer.allreduce_mean_(buf), 20, device)
-    if not rehearse:
-        buf = x.detach().clone()
-        times["rccl"] = _timed(lambda: dist.all_reduce(buf, op=dist.ReduceOp.AVG), 20, device)
-    info["ms"] = {k: round(v, 5) for k, v in times.items()}
-    peer_times = {a: t for a, t in times.items() if a != "rccl"}
-    if not peer_times:
+    from fedmi.parallel.select import verify_and_select
+
+    try:
+        choice, info = verify_and_select(peer, x.numel(), device, algos=algos, compare_group=want == "auto")
+    except RuntimeError:
+        peer.close()
+        raise
+    if choice is None:
         peer.close()
         if want != "auto":
-            raise RuntimeError(f"peer all-reduce ({want}) failed verification")
-        info["chosen"] = "rccl"
+            raise RuntimeError(f"peer all-reduce ({want}) failed verification: {info}")
         return None, info
-    best = min(peer_times, key=peer_times.get)
-    if want == "auto" and "rccl" in times and times["rccl"] < peer_times[best]:
-        peer.close()
-        info["chosen"] = "rccl"
-        return None, info
-    peer.algo = best
-    info["chosen"] = best
     return peer, info
 
 
@@ -180,6 +153,17 @@ def main() -> int:
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--trace", action="store_true",
                     help="print every rank's per-round train/test stats to stderr (synchronising: not for timing)")
+    ap.add_argument("--peer-timeout-ms", type=float, default=30000.0,
+                    help="wall-clock limit of a peer-collective barrier (a lost peer fails the run, never hangs it)")
+    ap.add_argument("--breakdown", action="store_true",
+                    help="per-round device time of each phase (train / allreduce / eval / checkpoint) from events "
+                         "recorded between the phases, and the host-side gaps")
+    ap.add_argument("--project-world", type=int, default=0,
+                    help="PROJECTION (1 GPU, labelled as such): one client runs rank 0's share of an N-client "
+                         "round -- its strided 1/N training shard, a 1/N test shard, the same checkpoint writer -- "
+                         "with NO collective; the per-client critical path of the N-GPU run minus the all-reduce")
+    ap.add_argument("--inject-fault", default="none", choices=["none", "skip-allreduce"],
+                    help="testing the end-of-run guard: the last rank skips the first timed round's FedAvg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,6 +173,10 @@ def main() -> int:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run",
               file=sys.stderr)
         return 2
+    if args.project_world and world != 1:
+        print("[bench] --project-world is a single-process projection", file=sys.stderr)
+        return 2
+    shard_world = args.project_world or world        # the client count whose per-client work this run does
     if not torch.cuda.is_available():
         print("[bench] no GPU visible", file=sys.stderr)
         return 2
@@ -222,13 +210,21 @@ def main() -> int:
         trainer.set_train_data(data.train.subset(shards[rank]))
         trainer.set_schedule(*contiguous_schedule(len(shards[rank]), BATCH))
     else:
-        trainer.set_schedule(*strided_schedule(N_TRAIN, BATCH, rank, world))
+        trainer.set_schedule(*strided_schedule(N_TRAIN, BATCH, rank, shard_world))
     transport, select = None, {}
     if world > 1:
         transport, select = make_transport(args, trainer, rank, world, rehearse, device)
+        if transport is not None:
+            transport.comm.set_timeout_ms(float(args.peer_timeout_ms))
+            transport.timeout_ms = float(args.peer_timeout_ms)
+        elif args.inject_fault != "none":
+            # a rank skipping an RCCL collective hangs its peers inside RCCL: the guard test needs the
+            # peer transport, whose barriers time out
+            print("[bench] --inject-fault needs the peer transport", file=sys.stderr)
+            return 2
     agg = FedAvg(compressor=make_compressor(args.compress, args.topk_ratio, trainer), transport=transport)
-    if world > 1 and not args.eval_full:
-        trainer.set_test_data(eval_shard(data.test, rank, world))
+    if shard_world > 1 and not args.eval_full:
+        trainer.set_test_data(eval_shard(data.test, rank, shard_world))
     hist = EvalHistory(trainer, args.warmup + args.steps)
     if args.trace:
         ys = trainer.train_set.y.long().cpu()
@@ -239,21 +235,40 @@ def main() -> int:
     root = Path(args.ckpt_dir or tempfile.mkdtemp(prefix="fedmi_bench_"))
     prim = mount_dir(root, primary=True) if rank == 0 else None
     cpath = client_ckpt_path(root, f"client{rank}")
-    writer = RoundCheckpointWriter()      # native C++ writer, coalescing (fedmi/ckpt, csrc/runtime/ckpt_writer.cpp)
+    # native C++ writer (fedmi/ckpt, csrc/runtime/ckpt_writer.cpp); every round is written, in order
+    writer = RoundCheckpointWriter()
+    PHASES = ("train", "allreduce", "eval", "checkpoint")
+    marks = []          # --breakdown: per round, (host perf_counter, cuda event) at each phase boundary
+    fault_round = args.warmup if args.inject_fault == "skip-allreduce" and rank == world - 1 else -1
+
+    def stamp(row):
+        if args.breakdown:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            row.append((time.perf_counter(), e))
 
     def one_round(r: int) -> None:
+        row = []
+        stamp(row)
         with phase("local-train"):
             trainer.train_epoch()
+        stamp(row)
         with phase("allreduce"):
-            agg.average(trainer)
+            if r != fault_round:
+                agg.average(trainer)
+        stamp(row)
         if not args.no_eval:
             with phase("eval"):
                 trainer.evaluate()
                 hist.record()
+        stamp(row)
         # global model -> Primary/optimizedModel.pth (rank 0) + this client's checkpoint, one snapshot
         with phase("checkpoint"):
             writer.submit([prim / OPTIMIZED_MODEL, cpath] if prim is not None else cpath, trainer.state_dict(),
                           acc=1, epoch=r + 1)
+        stamp(row)
+        if args.breakdown and r >= args.warmup:
+            marks.append(row)
         if args.trace:
             ts, fs = trainer.train_stats(), trainer.float_state()
             ev = trainer.eval_stats() if not args.no_eval else None
@@ -276,14 +291,26 @@ def main() -> int:
     t0 = time.perf_counter()
     for r in range(args.warmup, args.warmup + args.steps):
         one_round(r)
+    tl = [time.perf_counter()]
     writer.flush()
+    tl.append(time.perf_counter())
     rounds_eval = hist.reduce() if not args.no_eval and not args.eval_full else None
+    tl.append(time.perf_counter())
     barrier()
     t1 = time.perf_counter()
+    tail = {"loop_ms": round((tl[0] - t0) * 1e3, 3), "flush_ms": round((tl[1] - tl[0]) * 1e3, 3),
+            "eval_reduce_ms": round((tl[2] - tl[1]) * 1e3, 3), "barrier_ms": round((t1 - tl[2]) * 1e3, 3)}
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     T = float(elapsed.item())
+
+    # end-of-run guard (outside the timed region): no peer barrier timed out on any rank and every
+    # client holds the bit-identical global model -- else the throughput above is not a FedAvg run
+    from fedmi.parallel.consistency import check_consistency
+
+    consistency = check_consistency(trainer, transport=transport, device=device)
+    breakdown = dict(_breakdown(marks, PHASES, t0, t1, args.steps), tail=tail) if args.breakdown else None
 
     tr_stats = trainer.train_stats()
     if args.no_eval:
@@ -293,11 +320,14 @@ def main() -> int:
     else:
         ev_stats = trainer.eval_stats()
     rounds_per_s = args.steps / T
-    value = rounds_per_s * N_TRAIN
+    value = rounds_per_s * N_TRAIN / (args.project_world or 1)
     base_r = _baseline_rounds(args.model, world)
+    metric = ("rounds/sec + samples/sec/client, 2-conv CNN FedAvg at 1/2/4/8 MI355X clients"
+              if args.model.lower() == "lenet" else f"rounds/sec + samples/sec/client, {args.model} FedAvg")
+    if args.project_world:
+        metric = f"PROJECTION (1 GPU, no collective) of the per-client round at N={args.project_world}: " + metric
     out = {
-        "metric": "rounds/sec + samples/sec/client, 2-conv CNN FedAvg at 1/2/4/8 MI355X clients"
-        if args.model.lower() == "lenet" else f"rounds/sec + samples/sec/client, {args.model} FedAvg",
+        "metric": metric,
         "value": round(value, 3),
         "unit": "samples/s",
         "n_gpus": world,
@@ -310,9 +340,12 @@ def main() -> int:
         "dtype": "bf16",
         "data": "synthetic (CIFAR-shaped uint8 50k/10k, class-structured), random-init weights",
         "config": {"model": args.model, "global_batch": BATCH * world, "seq_len": None,
-                   "parallelism": f"fedavg-dp{world}", "per_client_batch": BATCH,
+                   "parallelism": f"fedavg-dp{world}" if not args.project_world
+                   else f"projection-of-fedavg-dp{args.project_world} (rank 0's share, no collective)",
+                   "per_client_batch": BATCH,
                    "local_epochs_per_round": 1, "eval_per_round": not args.no_eval,
-                   "eval_split": "full-per-client" if args.eval_full or world == 1 else f"1/{world}-per-client",
+                   "eval_split": "full-per-client" if args.eval_full or shard_world == 1
+                   else f"1/{shard_world}-per-client",
                    "data_split": f"noniid-{args.noniid}-shards" if args.noniid else "strided-iid",
                    "aggregation": agg.label() + (" [1-GPU rehearsal]" if rehearse and world > 1 else ""),
                    "hip_graph": not args.no_graph},
@@ -326,6 +359,8 @@ def main() -> int:
         "checkpoint": {"writer": writer.backend, "files_written": writer.written,
                        "rounds_coalesced": writer.coalesced},
         **({"transport_select": select} if select else {}),
+        "consistency": consistency,
+        **({"breakdown": breakdown} if breakdown else {}),
         **({"compression": {"kind": args.compress, "bytes_per_round_per_client":
                             agg.compressor.bytes_sent // max(1, agg.compressor.rounds),
                             "dense_bytes_per_round_per_client": agg.compressor.dense_bytes // max(1, agg.compressor.rounds)}}
@@ -333,15 +368,22 @@ def main() -> int:
     }
     writer.close()
     if transport is not None:
-        transport.close()
+        transport.close()          # store barrier first: no rank unmaps memory a peer's kernel may still read
+    rc = 0
+    if not consistency["ok"]:
+        # no throughput line: a run whose clients diverged did not measure FedAvg
+        print(f"[bench] rank {rank}: CONSISTENCY CHECK FAILED {json.dumps(consistency)}", file=sys.stderr, flush=True)
+        out["value"] = None
+        rc = 3
     if rank == 0:
         line = json.dumps(out)
-        print(line, flush=True)
+        if rc == 0:
+            print(line, flush=True)
         if args.json_out:
             Path(args.json_out).write_text(line + "\n")
     if world > 1:
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 if __name__ == "__main__":

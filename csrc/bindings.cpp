@@ -34,11 +34,9 @@ void launch_lenet_fwd_head(hipStream_t, const uint8_t*, int, int, const bf16*, c
                            int*, const int*, int*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
 void launch_sgd_flat(hipStream_t, float*, const float*, float*, long, float, float, float, float, int, int);
-size_t select_state_bytes();
-int compact_chunk();
 void launch_ef_delta(hipStream_t, const float*, const float*, const float*, float*, long);
-void launch_topk(hipStream_t, const float*, long, int, void*, int*, int*, float*, float*);
 size_t topk_state_bytes();
+size_t topk_overflow_offset();
 void launch_topk_ef(hipStream_t, const float*, const float*, float*, long, int, void*, int*, unsigned*, int*, float*);
 void launch_scatter_add_ranked(hipStream_t, float*, const int*, const float*, int, long, float, long);
 void launch_quant_int8(hipStream_t, const float*, long, signed char*, float*, float*);
@@ -224,8 +222,8 @@ static void fedmi_bind(py::module_& m) {
   });
 
   // ---- compression ---------------------------------------------------------------
-  m.def("select_state_bytes", &select_state_bytes);
   m.def("topk_state_bytes", &topk_state_bytes);
+  m.def("topk_overflow_offset", &topk_overflow_offset);
   m.def("topk_ef", [](uintptr_t st, uintptr_t x, uintptr_t g, uintptr_t residual, long n, int k, uintptr_t state,
                       uintptr_t cidx, uintptr_t ckey, uintptr_t idx, uintptr_t val) {
     if (k <= 0 || k > n) throw std::invalid_argument("topk_ef: need 0 < k <= n");
@@ -235,17 +233,9 @@ static void fedmi_bind(py::module_& m) {
     check_last("topk_ef");
   }, py::arg("stream"), py::arg("x"), py::arg("g"), py::arg("residual"), py::arg("n"), py::arg("k"), py::arg("state"),
      py::arg("cidx"), py::arg("ckey"), py::arg("idx"), py::arg("val"));
-  m.def("compact_chunk", &compact_chunk);
   m.def("ef_delta", [](uintptr_t st, uintptr_t local, uintptr_t global, uintptr_t residual, uintptr_t d, long n) {
     launch_ef_delta(S(st), P<const float>(local), P<const float>(global), P<const float>(residual), P<float>(d), n);
     check_last("ef_delta");
-  });
-  m.def("topk", [](uintptr_t st, uintptr_t d, long n, int k, uintptr_t state, uintptr_t counts, uintptr_t idx,
-                   uintptr_t val, uintptr_t residual) {
-    if (k <= 0 || k > n) throw std::invalid_argument("topk: need 0 < k <= n");
-    launch_topk(S(st), P<const float>(d), n, k, P<void>(state), P<int>(counts), P<int>(idx), P<float>(val),
-                P<float>(residual));
-    check_last("topk");
   });
   m.def("scatter_add_ranked", [](uintptr_t st, uintptr_t out, uintptr_t idx, uintptr_t val, int R, long m_, float scale,
                                  long n) {

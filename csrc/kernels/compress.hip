@@ -6,27 +6,21 @@
 // it mean lossy *update* compression on the data plane:
 //
 //   top-k:  d = (w_local - w_global) + residual      (error feedback)
-//           exact k-th largest |d| by a 4-pass 8-bit radix select
-//           (LDS-privatised histograms, no sort), deterministic compaction
-//           (block scans, ties taken in index order), residual <- d - sparse(d)
+//           exact k-th largest |d|: an 11-bit histogram of the top key bits
+//           fused with the delta pass, one compaction pass that takes the bins
+//           above the boundary outright and keeps the boundary bin as
+//           candidates, an exact LDS radix select among those (ties: smallest
+//           indices); residual <- d - sparse(d)  (the tk_* kernels below)
 //   int8:   per-256-element-chunk absmax scaling, residual <- d - deq(q(d))
 //
 // The compressed payloads are all-gathered over RCCL and folded back with
 // scatter_add_ranked (rank-ordered, atomic-free) / dequant_accum.
-#include <cstdlib>
 #include <algorithm>
+#include <cstddef>
 
 #include "common.h"
 
 namespace {
-
-struct SelectState {
-  unsigned prefix;       // selected high bits of the threshold key so far
-  unsigned mask;         // which bits of prefix are decided
-  int k_rem;             // elements still to take at/below the current prefix
-  int n_gt;              // elements strictly above the final threshold (set by the last pick)
-  unsigned hist[256];
-};
 
 FEDMI_DEV unsigned key_of(float v) { return __float_as_uint(v) & 0x7fffffffu; }
 
@@ -35,130 +29,6 @@ __global__ __launch_bounds__(256) void ef_delta_kernel(const float* __restrict__
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
     d[i] = local[i] - global[i] + (residual ? residual[i] : 0.f);
-}
-
-__global__ void select_init_kernel(SelectState* st, int k) {
-  const int t = threadIdx.x;
-  if (t == 0) { st->prefix = 0u; st->mask = 0u; st->k_rem = k; st->n_gt = 0; }
-  if (t < 256) st->hist[t] = 0u;
-}
-
-__global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict__ d, long n, SelectState* st, int shift) {
-  __shared__ unsigned h[256];
-  h[threadIdx.x] = 0u;
-  __syncthreads();
-  const unsigned prefix = st->prefix, mask = st->mask;
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const unsigned k = key_of(d[i]);
-    if ((k & mask) == prefix) atomicAdd(&h[(k >> shift) & 255u], 1u);
-  }
-  __syncthreads();
-  const unsigned v = h[threadIdx.x];
-  if (v) atomicAdd(&st->hist[threadIdx.x], v);
-}
-
-// One workgroup: choose the digit holding the k_rem-th largest key.
-__global__ __launch_bounds__(256) void radix_pick_kernel(SelectState* st, int shift) {
-  __shared__ unsigned h[256];
-  h[threadIdx.x] = st->hist[threadIdx.x];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int k = st->k_rem;
-    unsigned above = 0u;
-    int digit = 0;
-    for (int b = 255; b >= 0; --b) {
-      if (above + h[b] >= (unsigned)k) { digit = b; break; }
-      above += h[b];
-    }
-    st->k_rem = k - (int)above;
-    st->n_gt += (int)above;
-    st->prefix |= ((unsigned)digit) << shift;
-    st->mask |= 255u << shift;
-  }
-  __syncthreads();
-  st->hist[threadIdx.x] = 0u;
-}
-
-constexpr int kChunk = 2048;   // elements per compaction block (256 thr x 8)
-
-// per-block counts of (key > T) and (key == T)
-__global__ __launch_bounds__(256) void compact_count_kernel(const float* __restrict__ d, long n, const SelectState* st,
-                                                            int* __restrict__ counts) {
-  __shared__ int sg[4], se[4];
-  const unsigned T = st->prefix;
-  const long base = (long)blockIdx.x * kChunk;
-  int gt = 0, eq = 0;
-  for (int j = threadIdx.x; j < kChunk; j += 256) {
-    const long i = base + j;
-    if (i < n) {
-      const unsigned k = key_of(d[i]);
-      gt += k > T;
-      eq += k == T;
-    }
-  }
-  for (int off = 32; off > 0; off >>= 1) { gt += __shfl_xor(gt, off, 64); eq += __shfl_xor(eq, off, 64); }
-  if ((threadIdx.x & 63) == 0) { sg[threadIdx.x >> 6] = gt; se[threadIdx.x >> 6] = eq; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    counts[2 * blockIdx.x] = sg[0] + sg[1] + sg[2] + sg[3];
-    counts[2 * blockIdx.x + 1] = se[0] + se[1] + se[2] + se[3];
-  }
-}
-
-// single workgroup exclusive scan of the per-block counts (in place)
-__global__ __launch_bounds__(256) void compact_scan_kernel(int* __restrict__ counts, int nblocks) {
-  if (threadIdx.x == 0) {
-    int ag = 0, ae = 0;
-    for (int b = 0; b < nblocks; ++b) {
-      const int g = counts[2 * b], e = counts[2 * b + 1];
-      counts[2 * b] = ag;
-      counts[2 * b + 1] = ae;
-      ag += g;
-      ae += e;
-    }
-  }
-}
-
-FEDMI_DEV int block_excl_scan(int flag, int* wsum, int& total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const unsigned long long bal = __ballot(flag);
-  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int in_wave = __popcll(bal & lt);
-  if (lane == 0) wsum[w] = __popcll(bal);
-  __syncthreads();
-  int before = 0;
-  for (int q = 0; q < w; ++q) before += wsum[q];
-  total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  __syncthreads();
-  return before + in_wave;
-}
-
-__global__ __launch_bounds__(256) void compact_write_kernel(const float* __restrict__ d, long n, const SelectState* st,
-                                                            const int* __restrict__ offs, int* __restrict__ idx,
-                                                            float* __restrict__ val, float* __restrict__ residual) {
-  __shared__ int wsum[4];
-  const unsigned T = st->prefix;
-  const int take_eq = st->k_rem, n_gt = st->n_gt;
-  int og = offs[2 * blockIdx.x], oe = offs[2 * blockIdx.x + 1];
-  const long base = (long)blockIdx.x * kChunk;
-  for (int j0 = 0; j0 < kChunk; j0 += 256) {
-    const long i = base + j0 + threadIdx.x;
-    float v = 0.f;
-    unsigned k = 0u;
-    const bool in = i < n;
-    if (in) { v = d[i]; k = key_of(v); }
-    const int fg = in && k > T, fe = in && k == T;
-    int tg, te;
-    const int rg = block_excl_scan(fg, wsum, tg);
-    const int re = block_excl_scan(fe, wsum, te);
-    bool sel = false;
-    if (fg) { idx[og + rg] = (int)i; val[og + rg] = v; sel = true; }
-    if (fe && oe + re < take_eq) { idx[n_gt + oe + re] = (int)i; val[n_gt + oe + re] = v; sel = true; }
-    if (in && residual) residual[i] = sel ? 0.f : v;
-    og += tg;
-    oe += te;
-  }
 }
 
 // out[idx[i]] += scale * val[i] for ONE rank's payload.  Indices are unique within a
@@ -232,12 +102,11 @@ constexpr int kTkBins1 = 2048;
 constexpr long kTkThreeLevel = 1 << 20;   // n at which the 3-level path takes over
 struct TopKState {
   unsigned hist[kTkBins1];
-  int b1, n_above, need, out_cnt, cand_cnt, pad[3];
+  int b1, n_above, need, out_cnt, cand_cnt, pad[3];   // pad[0]: sticky overflow flag (topk_overflow_offset)
   // 3-level path (large n): level-2 histogram of the candidates' key bits 19..9
   unsigned hist2[kTkBins1];
   int b2, n_above2, need2, out2_cnt, cand2_cnt;
-  unsigned ticket;                // arrivals of the current tk_delta_hist launch (reset by the last arriver)
-  int pad2[2];
+  int pad2[3];
 };
 
 // NT threads: bin b of h[0..nb) (nb = 1024 or 2048, nb >= NT) such that above(b) < k <= above(b) + h[b],
@@ -275,7 +144,7 @@ FEDMI_DEV void tk_find_top(const unsigned* h, int nb, unsigned k, unsigned* scra
 
 FEDMI_DEV void tk_hist_add(unsigned* h, float v) { atomicAdd(&h[key_of(v) >> 20], 1u); }
 
-template <bool VEC, bool PICK>
+template <bool VEC>
 __global__ __launch_bounds__(256) void tk_delta_hist_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                             float* __restrict__ r, long n, TopKState* __restrict__ st,
                                                             int k) {
@@ -328,35 +197,6 @@ __global__ __launch_bounds__(256) void tk_delta_hist_kernel(const float* __restr
   for (int j = threadIdx.x; j < kTkBins1; j += 256) {
     const int i = (j + (int)blockIdx.x * 64) & (kTkBins1 - 1);
     if (h[i]) atomicAdd(&st->hist[i], h[i]);
-  }
-  if (!PICK) return;
-  // tk_pick1's work in the LAST workgroup to arrive (cdna_hip_programming.md Guideline 16: flush retired, one
-  // agent release, relaxed ticket; the last arriver acquires) -- one launch less per call
-  __shared__ int last;
-  __shared__ unsigned scratch[32], res[2];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const unsigned t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == gridDim.x - 1u;
-  }
-  __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  for (int i = threadIdx.x; i < kTkBins1; i += 256) {
-    h[i] = __hip_atomic_load(&st->hist[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    st->hist[i] = 0u;                        // zero for the next call (graph-safe: no memset node)
-  }
-  __syncthreads();
-  tk_find_top<256>(h, kTkBins1, (unsigned)k, scratch, res);
-  if (threadIdx.x == 0) {
-    st->b1 = (int)res[0];
-    st->n_above = (int)res[1];
-    st->need = k - (int)res[1];
-    st->out_cnt = 0;
-    st->cand_cnt = 0;
-    st->ticket = 0u;
   }
 }
 
@@ -411,7 +251,7 @@ FEDMI_DEV void tk_select_body(float* __restrict__ r, int c, int nab, unsigned m,
                               const unsigned* __restrict__ ckey, int* __restrict__ idx, float* __restrict__ val,
                               int* overflow, unsigned* h, unsigned* scratch, unsigned* res, int* wcount_p);
 
-template <bool H2, bool PICK2 = false, bool SEL = false>
+template <bool H2>
 __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r, long n, TopKState* __restrict__ st,
                                                           int* __restrict__ idx, float* __restrict__ val,
                                                           int* __restrict__ cidx, unsigned* __restrict__ ckey) {
@@ -512,58 +352,6 @@ __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r,
       const int i = (j + (int)blockIdx.x * 64) & (kTkBins1 - 1);
       if (h2[i]) atomicAdd(&st->hist2[i], h2[i]);
     }
-    if (!PICK2) return;
-    // tk_pick2's work in the last workgroup to arrive (same hand-off as tk_delta_hist_kernel's pick)
-    __shared__ int last;
-    __shared__ unsigned scratch[32], res[2];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      const unsigned t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = t == gridDim.x - 1u;
-    }
-    __syncthreads();
-    if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    for (int i = threadIdx.x; i < kTkBins1; i += 256) {
-      h2[i] = __hip_atomic_load(&st->hist2[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      st->hist2[i] = 0u;
-    }
-    __syncthreads();
-    const int need = st->need;
-    tk_find_top<256>(h2, kTkBins1, (unsigned)need, scratch, res);
-    if (threadIdx.x == 0) {
-      st->b2 = (int)res[0];
-      st->n_above2 = (int)res[1];
-      st->need2 = need - (int)res[1];
-      st->out2_cnt = 0;
-      st->cand2_cnt = 0;
-      st->ticket = 0u;
-    }
-  }
-  if (SEL && !H2) {
-    // tk_select2's work in the last-arriving workgroup (below the 3-level threshold the candidate list is a few
-    // thousand entries): one launch less per call
-    __shared__ int last_s, wcount_s;
-    __shared__ unsigned scr_s[32], res_s[2];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      const unsigned t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last_s = t == gridDim.x - 1u;
-    }
-    __syncthreads();
-    if (!last_s) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const int c = __hip_atomic_load(&st->cand_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int nab = st->n_above;
-    const unsigned m = (unsigned)st->need;
-    __syncthreads();
-    if (threadIdx.x == 0) st->ticket = 0u;
-    tk_select_body<2, 256>(r, c, nab, m, cidx, ckey, idx, val, &st->pad[0], reinterpret_cast<unsigned*>(s_si), scr_s,
-                           res_s, &wcount_s);
   }
 }
 
@@ -781,31 +569,13 @@ int grid_for(long n) {
 
 namespace fedmi {
 
-size_t select_state_bytes() { return sizeof(SelectState); }
-int compact_chunk() { return kChunk; }
-
 void launch_ef_delta(hipStream_t st, const float* local, const float* global, const float* residual, float* d, long n) {
   hipLaunchKernelGGL(ef_delta_kernel, dim3(grid_for(n)), dim3(256), 0, st, local, global, residual, d, n);
 }
 
-// Exact top-k by magnitude.  counts: int[2*ceil(n/kChunk)] scratch.
-// Writes exactly k (idx, val) pairs; residual (optional) keeps the rest.
-void launch_topk(hipStream_t st, const float* d, long n, int k, void* state, int* counts, int* idx, float* val,
-                 float* residual) {
-  SelectState* s = reinterpret_cast<SelectState*>(state);
-  hipLaunchKernelGGL(select_init_kernel, dim3(1), dim3(256), 0, st, s, k);
-  for (int pass = 0; pass < 4; ++pass) {
-    const int shift = 24 - 8 * pass;
-    hipLaunchKernelGGL(radix_hist_kernel, dim3(grid_for(n)), dim3(256), 0, st, d, n, s, shift);
-    hipLaunchKernelGGL(radix_pick_kernel, dim3(1), dim3(256), 0, st, s, shift);
-  }
-  const int nb = (int)((n + kChunk - 1) / kChunk);
-  hipLaunchKernelGGL(compact_count_kernel, dim3(nb), dim3(256), 0, st, d, n, s, counts);
-  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(64), 0, st, counts, nb);
-  hipLaunchKernelGGL(compact_write_kernel, dim3(nb), dim3(256), 0, st, d, n, s, counts, idx, val, residual);
-}
-
 size_t topk_state_bytes() { return sizeof(TopKState); }
+// byte offset of the int overflow word (set if a select ever produced more than k entries; sticky)
+size_t topk_overflow_offset() { return offsetof(TopKState, pad); }
 
 // Fused error-feedback exact top-k (see tk_* kernels).  residual: d is built IN it and the
 // selected entries are zeroed (= the new residual); state: topk_state_bytes(), zero on first
@@ -815,45 +585,25 @@ void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* resid
   TopKState* s = reinterpret_cast<TopKState*>(state);
   const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g) |
                      reinterpret_cast<uintptr_t>(residual)) & 15) == 0;
-  // ~8 float4 per thread, at most 2048 workgroups (their nonzero bins go to the global histogram)
-  long hmax = 2048;
-  if (const char* e = std::getenv("FEDMI_TK_HBLOCKS")) hmax = std::max(1L, std::atol(e));   // A/B: histogram grid cap
-  const int blocks = (int)std::min<long>(hmax, std::max<long>(1, (n + 8 * 1024 - 1) / (8 * 1024)));
-  // opt-in (FEDMI_TK_FUSE_PICK=1): the boundary-bin picks in the last-arriving workgroup of the histogram /
-  // compaction kernels instead of their own launches -- measured SLOWER (132 vs 94.6 us at 11.2 M entries,
-  // 23.4 vs 22.7 us at 62 k: every workgroup pays an agent-scope release and a drained flush for one launch saved).
-  // A one-workgroup kernel for small states (all passes in one launch) measured 38.5 vs 22.7 us at 62 k (one CU's
-  // bandwidth) and was dropped.
-  static const bool fuse_pick = [] { const char* e = std::getenv("FEDMI_TK_FUSE_PICK"); return e && e[0] == '1'; }();
-  if (fuse_pick) {
-    if (vec)
-      hipLaunchKernelGGL((tk_delta_hist_kernel<true, true>), dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
-    else
-      hipLaunchKernelGGL((tk_delta_hist_kernel<false, true>), dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
-  } else {
-    if (vec)
-      hipLaunchKernelGGL((tk_delta_hist_kernel<true, false>), dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
-    else
-      hipLaunchKernelGGL((tk_delta_hist_kernel<false, false>), dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
-    hipLaunchKernelGGL(tk_pick1_kernel, dim3(1), dim3(1024), 0, st, s, k);
-  }
+  // ~8 float4 per thread, at most 2048 workgroups (their nonzero bins go to the global histogram).  The
+  // boundary-bin picks run as their own one-workgroup launches: doing them in the last-arriving workgroup of
+  // the histogram / compaction kernels measured slower (132 vs 94.6 us at 11.2 M entries, 23.4 vs 22.7 us at
+  // 62 k: every workgroup pays an agent-scope release and a drained flush for one launch saved), and so did
+  // the select in the compaction's last workgroup (34 vs 24 us at 62 k) and a one-workgroup kernel for small
+  // states (38.5 vs 22.7 us at 62 k) -- profiles/r3_dataplane/topk_ab.txt.
+  const int blocks = (int)std::min<long>(2048, std::max<long>(1, (n + 8 * 1024 - 1) / (8 * 1024)));
+  if (vec)
+    hipLaunchKernelGGL(tk_delta_hist_kernel<true>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
+  else
+    hipLaunchKernelGGL(tk_delta_hist_kernel<false>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
+  hipLaunchKernelGGL(tk_pick1_kernel, dim3(1), dim3(1024), 0, st, s, k);
   // compaction grid cap: 2 workgroups per CU (512) measured 103.5 vs 128 us at 11.2 M entries (2048: 4x the
-  // per-workgroup flushes of the staged lists and of the level-2 histogram); FEDMI_TK_CBLOCKS overrides
-  long cmax = 512;
-  if (const char* e = std::getenv("FEDMI_TK_CBLOCKS")) cmax = std::max(1L, std::atol(e));
-  const int cblocks = (int)std::min<long>(cmax, std::max<long>(1, (n + 2 * 2048 - 1) / (2 * 2048)));
+  // per-workgroup flushes of the staged lists and of the level-2 histogram)
+  const int cblocks = (int)std::min<long>(512, std::max<long>(1, (n + 2 * 2048 - 1) / (2 * 2048)));
   if (n < kTkThreeLevel) {
-    // opt-in (FEDMI_TK_FUSE_SELECT=1): the exact select in the compaction's last-arriving 256-thread workgroup
-    // instead of its own 1024-thread launch -- correct but measured slower (34 vs 24 us at 62 k entries)
-    static const bool fuse_sel = [] { const char* e = std::getenv("FEDMI_TK_FUSE_SELECT"); return e && e[0] == '1'; }();
-    if (fuse_sel) {
-      hipLaunchKernelGGL((tk_compact1_kernel<false, false, true>), dim3(cblocks), dim3(256), 0, st, residual, n, s, idx,
-                         val, cidx, ckey);
-    } else {
-      hipLaunchKernelGGL(tk_compact1_kernel<false>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx,
-                         ckey);
-      hipLaunchKernelGGL(tk_select2_kernel<2>, dim3(1), dim3(1024), 0, st, residual, s, cidx, ckey, idx, val);
-    }
+    hipLaunchKernelGGL(tk_compact1_kernel<false>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx,
+                       ckey);
+    hipLaunchKernelGGL(tk_select2_kernel<2>, dim3(1), dim3(1024), 0, st, residual, s, cidx, ckey, idx, val);
     return;
   }
   // large n: the boundary bin holds ~1-3 % of the entries -- too many for one workgroup; a second histogram
@@ -861,14 +611,8 @@ void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* resid
   // level-3 list of a few hundred for the single-workgroup exact select
   int* cidx2 = cidx + n;                     // second half of the 2n-entry candidate scratch
   unsigned* ckey2 = ckey + n;
-  if (fuse_pick) {
-    hipLaunchKernelGGL((tk_compact1_kernel<true, true>), dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val,
-                       cidx, ckey);
-  } else {
-    hipLaunchKernelGGL((tk_compact1_kernel<true, false>), dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val,
-                       cidx, ckey);
-    hipLaunchKernelGGL(tk_pick2_kernel, dim3(1), dim3(1024), 0, st, s);
-  }
+  hipLaunchKernelGGL(tk_compact1_kernel<true>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx, ckey);
+  hipLaunchKernelGGL(tk_pick2_kernel, dim3(1), dim3(1024), 0, st, s);
   const int c2blocks = (int)std::min<long>(1024, std::max<long>(1, (n / 50 + 2047) / 2048));
   hipLaunchKernelGGL(tk_compact2_kernel, dim3(c2blocks), dim3(256), 0, st, residual, s, cidx, ckey, idx, val, cidx2,
                      ckey2);

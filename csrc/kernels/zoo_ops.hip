@@ -9,6 +9,7 @@
 // layout (channels-last activations, broadcast operands, channel slices of a
 // concatenation); dtypes are fp32 / bf16 / int64.  Integer index math is 64-bit
 // only where a tensor can exceed 2^31 elements' byte range (never, in practice).
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <stdexcept>
@@ -436,6 +437,7 @@ __global__ __launch_bounds__(256) void pad_rows_kernel(const bf16* __restrict__ 
 struct BnFin {
   int mode;
   int fast;               // 1: the prefetching bf16 row pass (FEDMI_ZOO_FAST=0: the one-row loop)
+  int slot;               // arrival-ticket slot of this launch (g_rows_ticket)
   long long M;
   const float* shift; const float* w; const float* b; float* rmean; float* rvar; float eps, mom;
   float* save_mean; float* save_invstd; float* scale; float* bias;
@@ -471,7 +473,12 @@ FEDMI_DEV void bn_bwd_fin(const BnFin& f, int c, float sg, float sgx) {
   if (f.db) f.db[c] = sg;
 }
 
-__device__ unsigned int g_rows_ticket = 0u;   // arrivals of the current fused BN row pass (reset by the last)
+// Arrival tickets of the fused BN row passes (each reset to 0 by its last arriver).  Every launch takes its
+// own slot (host-side round robin), so passes running concurrently on different streams or from different
+// trainers of one process never share a ticket; a graph node keeps the slot it was captured with.
+constexpr int kRowsTicketSlots = 4096;
+__device__ unsigned int g_rows_ticket[kRowsTicketSlots] = {};
+static std::atomic<unsigned> g_rows_slot{0};
 
 // ---- row reduction of a [M, C] row-major matrix (ld = row stride), C % 8 == 0 ------------------
 // The channels-last case of the BN moments / bias gradients: a thread owns 8 channels (one 16-byte
@@ -562,10 +569,11 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_d
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned total = gridDim.x * gridDim.y;
-    const unsigned prev = __hip_atomic_fetch_add(&g_rows_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned* ticket = &g_rows_ticket[fin.slot];
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = prev + 1 == total;
     if (last) {
-      __hip_atomic_store(&g_rows_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
   }
@@ -1477,6 +1485,7 @@ void launch_bn_rows_fwd(hipStream_t st, const void* x, int x_dt, long long ldx, 
   BnFin fin{};
   fin.fast = zoo_fast();
   if (bn_rows_fused()) {
+    fin.slot = (int)(g_rows_slot.fetch_add(1u) % kRowsTicketSlots);
     fin.mode = 1; fin.M = M; fin.shift = shift; fin.w = w; fin.b = b; fin.rmean = rmean; fin.rvar = rvar;
     fin.eps = eps; fin.mom = mom; fin.save_mean = save_mean; fin.save_invstd = save_invstd; fin.scale = scale;
     fin.bias = bias;
@@ -1506,6 +1515,7 @@ void launch_bn_rows_bwd(hipStream_t st, const void* g, int g_dt, long long ldg, 
   BnFin fin{};
   fin.fast = zoo_fast();
   if (bn_rows_fused()) {
+    fin.slot = (int)(g_rows_slot.fetch_add(1u) % kRowsTicketSlots);
     fin.mode = 2; fin.M = M; fin.mean = mean; fin.invstd = invstd; fin.w = w; fin.k = k; fin.bb = bb; fin.cc = cc;
     fin.dw = dw; fin.db = db;
   }

@@ -11,6 +11,7 @@
 
 namespace fedmi {
 void check_hip(hipError_t e, const char* what);
+uint32_t crc32_fast(uint32_t crc, const uint8_t* p, size_t n);   // crc32_fast.cpp (PCLMULQDQ folding)
 
 namespace {
 
@@ -22,8 +23,9 @@ void put_u32(uint8_t* p, uint32_t v) {
 }
 
 // Write all of `data` to `path` atomically: tmp file in the same directory, then rename.
-void atomic_write(const std::string& path, const uint8_t* data, size_t n) {
-  const std::string tmp = path + ".tmpn" + std::to_string(::getpid());
+std::string tmp_name(const std::string& path) { return path + ".tmpn" + std::to_string(::getpid()); }
+
+void write_tmp(const std::string& tmp, const uint8_t* data, size_t n) {
   const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
   if (fd < 0) throw std::runtime_error("ckpt writer: cannot open " + tmp);
   size_t off = 0;
@@ -37,6 +39,9 @@ void atomic_write(const std::string& path, const uint8_t* data, size_t n) {
     off += (size_t)w;
   }
   if (::close(fd) != 0) throw std::runtime_error("ckpt writer: close failed for " + tmp);
+}
+
+void commit(const std::string& tmp, const std::string& path) {
   if (::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("ckpt writer: rename to " + path);
 }
 
@@ -134,16 +139,22 @@ void CkptWriter::write_one(int slot, int32_t epoch) {
   put_u32(o + epoch_at_, (uint32_t)epoch);        // pickle BININT ('J' + int32 LE)
   for (const auto& r : recs_) {
     if (r.snap_off >= 0) std::memcpy(o + r.data_off, snap_[slot] + r.snap_off, (size_t)r.bytes);
-    uLong crc = crc32(0L, Z_NULL, 0);
-    long long done = 0;
-    while (done < r.bytes) {                        // zlib's length is a uInt
-      const long long chunk = std::min(r.bytes - done, 1LL << 30);
-      crc = crc32(crc, o + r.data_off + done, (uInt)chunk);
-      done += chunk;
-    }
-    for (long long c : r.crc_at) put_u32(o + c, (uint32_t)crc);
+    const uint32_t crc = crc32_fast(0u, o + r.data_off, (size_t)r.bytes);
+    for (long long c : r.crc_at) put_u32(o + c, crc);
   }
-  for (const auto& p : paths_) atomic_write(p, o, out_.size());
+  // the bytes are written ONCE; every further target is a hard link to that file (same archive, e.g.
+  // Primary/optimizedModel.pth and checkpoint/<client>.pth), each committed by its own atomic rename --
+  // a later round's rename replaces the directory entry, never the shared inode's bytes.  Targets on
+  // another filesystem (link fails) get their own copy.
+  const std::string first = tmp_name(paths_[0]);
+  write_tmp(first, o, out_.size());
+  for (size_t i = 1; i < paths_.size(); ++i) {
+    const std::string t = tmp_name(paths_[i]);
+    ::unlink(t.c_str());
+    if (::link(first.c_str(), t.c_str()) != 0) write_tmp(t, o, out_.size());
+    commit(t, paths_[i]);
+  }
+  commit(first, paths_[0]);
 }
 
 void CkptWriter::run() {

@@ -35,6 +35,7 @@ SOURCES = [
     CSRC / "comm" / "peer_comm.hip",
     CSRC / "runtime" / "lenet_engine.cpp",
     CSRC / "runtime" / "ckpt_writer.cpp",
+    CSRC / "runtime" / "crc32_fast.cpp",
     CSRC / "bindings.cpp",
     CSRC / "bindings_cnn.cpp",
     CSRC / "bindings_comm.cpp",

@@ -37,7 +37,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--backend", default="auto", help="dist data-plane backend: nccl (RCCL) | gloo | auto")
     ap.add_argument("--transport", default="auto", choices=["auto", "peer", "dist"],
                     help="FedAvg data plane: peer = hipIpc peer kernels among the node's GPU clients (also "
-                         "several clients on one GPU); dist = torch.distributed (--backend); auto = peer on GPU")
+                         "several clients on one GPU); dist = torch.distributed (--backend); auto (GPU) = verify the "
+                         "peer kernels against the process group's all-reduce at the first multi-client generation, "
+                         "time both, keep the faster (CPU: dist)")
     ap.add_argument("--collective-timeout", type=float, default=20.0,
                     help="seconds before a collective with a lost peer fails (peer barrier / RCCL abort)")
     ap.add_argument("--data", default="synthetic-cifar10",
@@ -84,13 +86,13 @@ def main(argv=None) -> int:
         shards = label_shard_indices(data.train.y.cpu().numpy(), a.num_clients, a.noniid, seed=a.data_seed)
         trainer.set_train_data(data.train.subset(shards[a.client_index]))
     backend = a.backend if a.backend != "auto" else ("nccl" if dev.type == "cuda" else "gloo")
-    transport = a.transport if a.transport != "auto" else ("peer" if dev.type == "cuda" else "dist")
+    transport = a.transport if a.transport != "auto" else ("auto" if dev.type == "cuda" else "dist")
     comp_kind = a.compress if a.compress is not None else ("topk" if gzip else "none")
     fedavg = FedAvg(compressor=make_compressor(comp_kind, a.topk_ratio, trainer))
     n = trainer.float_state().numel()
     cap = max(4 * n, 16 * (int(n * a.topk_ratio) + 64), n + 4 * (n // 256 + 64))
     group = GroupManager(backend, dev, timeout_s=a.collective_timeout, transport=transport, peer_capacity=cap,
-                         peer_timeout_ms=1000.0 * a.collective_timeout)
+                         peer_timeout_ms=1000.0 * a.collective_timeout, model_numel=n)
     agent = ClientAgent(trainer, a.address, root=a.root, agg=a.agg, group=group,
                         fedavg=fedavg, batch_size=a.batch_size, local_shard=a.noniid > 0, resume=a.resume,
                         metrics=MetricsLog(a.metrics), verbose=not a.quiet)

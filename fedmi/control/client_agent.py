@@ -91,6 +91,7 @@ class ClientAgent(P.TrainerServicer):
         self.fault_stall_from = int(os.environ.get("FEDMI_FAULT_STALL_FROM_ROUND", "0") or 0)
         self._round_start = None                # (float, [int]) device copies of the round's starting global model
         self._debug_stats = os.environ.get("FEDMI_DEBUG_STATS", "0") == "1"
+        self._select_logged = False
         if self._debug_stats:
             from ..parallel import compress as _comp
             _comp.PROBE = self._probe
@@ -210,6 +211,9 @@ class ClientAgent(P.TrainerServicer):
                 self._probe("group")
             elif world > 1:
                 context.abort(grpc.StatusCode.FAILED_PRECONDITION, "collective aggregation needs a GroupManager")
+            if changed and self.group is not None and self.group.select_info and not self._select_logged:
+                rec["transport_select"] = self.group.select_info      # the auto data-plane decision, once
+                self._select_logged = True
             if changed and world > 1:
                 # new member set: everyone starts this generation from rank 0's model (one anchor
                 # for the -c Y compressors; undoes any partially applied aborted round)

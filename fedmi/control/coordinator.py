@@ -251,7 +251,14 @@ class Coordinator:
             epoch = int(dict(call.trailing_metadata() or ()).get("x-fedmi-ckpt-epoch", "-1"))
             if reply.reply and epoch > self.installed_epoch:
                 self._install_global(ck.from_b64(reply.reply), epoch)
-            elif epoch < self.round:
+                if epoch > self.round:
+                    # the "aborted" round had completed its all-reduce on rank 0 (a client died after it):
+                    # that model is a full FedAvg result and becomes the committed round, so the round
+                    # counter follows it -- otherwise the next round would report this epoch again and
+                    # _install_global would drop it as not newer
+                    self._log(f"rank 0 committed round {epoch} before the abort: advancing the round counter")
+                    self.round = epoch
+            else:
                 time.sleep(0.02)             # its writer is still serialising the committed round
 
     def flush(self) -> None:

@@ -101,6 +101,18 @@ class TopKCompressor(_EFCompressor):
             self.cidx = torch.empty(2 * self.n, dtype=torch.int32, device=self.dev)
             self.ckey = torch.empty(2 * self.n, dtype=torch.int32, device=self.dev)
 
+    def overflowed(self, clear: bool = True) -> bool:
+        """True if a select ever produced more than k entries (the excess was dropped, never written
+        past the payload; a kernel bug, not a data condition).  Synchronous; read at end of run."""
+        if self._nat is None:
+            return False
+        off = int(self._nat.topk_overflow_offset())
+        word = self.state[off:off + 4].view(torch.int32)
+        hit = bool(word.item())
+        if clear and hit:
+            word.zero_()
+        return hit
+
     def compress(self, x: torch.Tensor) -> None:
         if self._nat is not None:
             # d = x - global + residual is built IN the residual buffer; the winners are zeroed there

@@ -27,6 +27,12 @@ from .. import native
 ALGOS = {"oneshot": 0, "twoshot": 1}
 
 
+def agree_any(store, key: str, rank: int, world: int, mine: bool) -> bool:
+    """OR of a per-rank flag over all ranks, through the rendezvous store (blocks until all have set it)."""
+    store.set(f"{key}/{rank}", b"1" if mine else b"0")
+    return any(store.get(f"{key}/{r}") == b"1" for r in range(world))
+
+
 class PeerAllReduce:
     """IPC-mapped all-reduce / all-gather among ``world`` ranks of one node."""
 
@@ -50,11 +56,13 @@ class PeerAllReduce:
         self._closed = False
         self.calls = 0
         self.timeout_ms = float(timeout_ms)
-        # ranks sharing this GPU (one-GPU rehearsals / drills): a collective kernel spinning in its barrier
+        # ranks sharing a GPU (one-GPU rehearsals / drills): a collective kernel spinning in its barrier
         # can keep a co-located peer's queued kernels from being scheduled until the barrier times out, so
-        # each collective is gated by a host barrier once this rank's stream has drained.  Never taken with
-        # one rank per GPU (the production layout).
-        self.colocated = bool(self.comm.colocated) and world > 1
+        # each collective is gated by a host barrier once this rank's stream has drained.  The gate waits
+        # for all ``world`` ranks, so the decision must be the same on every rank: it is taken if ANY rank
+        # shares its GPU (e.g. 3 ranks on 2 GPUs gate all three).  Never taken with one rank per GPU (the
+        # production layout).
+        self.colocated = agree_any(store, f"{key}/coloc", rank, world, bool(self.comm.colocated)) and world > 1
         self._gate_n = 0
         self._gate_failed = False
 

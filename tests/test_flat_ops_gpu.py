@@ -33,33 +33,6 @@ def test_sgd_flat(nat, gpu_device, n):
     assert torch.allclose(p, pr, rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("n,k", [(62006, 620), (5000, 1), (5000, 5000), (1 << 20, 10000)])
-def test_topk_exact(nat, gpu_device, n, k):
-    torch.manual_seed(k)
-    d = torch.randn(n, device=gpu_device)
-    d[::97] = 0.0
-    state = torch.zeros(nat.select_state_bytes(), dtype=torch.uint8, device=gpu_device)
-    nblk = (n + nat.compact_chunk() - 1) // nat.compact_chunk()
-    counts = torch.zeros(2 * nblk, dtype=torch.int32, device=gpu_device)
-    idx = torch.full((k,), -1, dtype=torch.int32, device=gpu_device)
-    val = torch.zeros(k, device=gpu_device)
-    res = torch.empty(n, device=gpu_device)
-    nat.topk(S(), d.data_ptr(), n, k, state.data_ptr(), counts.data_ptr(), idx.data_ptr(), val.data_ptr(),
-             res.data_ptr())
-    torch.cuda.synchronize()
-    assert int(idx.min()) >= 0
-    assert len(set(idx.tolist())) == k
-    ref_vals = d.abs().topk(k).values
-    got = val.abs().sort(descending=True).values
-    assert torch.equal(got, ref_vals)
-    assert torch.equal(d[idx.long()], val)
-    # residual keeps exactly the unselected entries
-    mask = torch.ones(n, dtype=torch.bool, device=gpu_device)
-    mask[idx.long()] = False
-    assert torch.equal(res[mask], d[mask])
-    assert res[~mask].abs().sum().item() == 0
-
-
 @pytest.mark.parametrize("n,k,ties", [(62006, 620, False), (5000, 1, False), (5000, 5000, False),
                                        (1 << 20, 10000, False), (11173962, 111740, False), (70001, 700, True),
                                        (4099, 17, True), (1 << 21, 5000, "sparse")])
@@ -108,6 +81,8 @@ def test_topk_ef_exact(nat, gpu_device, n, k, ties):
         mask[sel] = False
         assert torch.equal(r[mask], d[mask])
         assert r[~mask].abs().sum().item() == 0
+        off = nat.topk_overflow_offset()
+        assert int(state[off:off + 4].view(torch.int32).item()) == 0      # no select ever exceeded k
 
 
 def test_scatter_add_ranked_is_rank_ordered(nat, gpu_device):

@@ -11,25 +11,26 @@ import torch
 from fedmi import ckpt as ck
 from fedmi.control.coordinator import Coordinator, CoordinatorConfig
 
-from helpers import free_port, spawn_client, stop_proc, wait_heartbeat
+from helpers import free_port, read_jsonl, spawn_client, stop_proc, wait_heartbeat
 
 pytestmark = pytest.mark.gpu
 
 
-def _clients(tmp_path, n, extra=()):
+def _clients(tmp_path, n, extra=(), transport="peer"):
     addrs = [f"127.0.0.1:{free_port()}" for _ in range(n)]
     procs = [spawn_client(a, tmp_path, "--agg", "collective", "--model", "lenet", "--n-train", "2560",
-                          "--n-test", "1000", "--transport", "peer", *extra, log_path=tmp_path / f"client{i}.log",
-                          device="cuda:0")
+                          "--n-test", "1000", "--transport", transport, "--metrics", str(tmp_path / f"client{i}.jsonl"),
+                          *extra, log_path=tmp_path / f"client{i}.log", device="cuda:0")
              for i, a in enumerate(addrs)]
     for a in addrs:
         wait_heartbeat(a, timeout=100)
     return addrs, procs
 
 
-@pytest.mark.parametrize("compress", [False, True], ids=["dense", "topk"])
-def test_grpc_coordinator_drives_gpu_clients(tmp_path, compress):
-    addrs, procs = _clients(tmp_path, 2, ("-c", "Y") if compress else ())
+@pytest.mark.parametrize("compress,transport", [(False, "peer"), (True, "peer"), (False, "auto")],
+                         ids=["dense", "topk", "dense-auto"])
+def test_grpc_coordinator_drives_gpu_clients(tmp_path, compress, transport):
+    addrs, procs = _clients(tmp_path, 2, ("-c", "Y") if compress else (), transport=transport)
     try:
         cfg = CoordinatorConfig(clients=addrs, rounds=3, agg="collective", root=str(tmp_path / "srv"),
                                 gzip=compress, train_timeout_s=90, rpc_timeout_s=20, heartbeat_s=0.5)
@@ -50,6 +51,13 @@ def test_grpc_coordinator_drives_gpu_clients(tmp_path, compress):
             assert c["epoch"] == 3
             for k in g["net"]:
                 assert torch.equal(c["net"][k], g["net"][k]), k     # rank-ordered peer sums: bit-identical
+        if transport == "auto":
+            # product path verify-and-select: two clients on one GPU cannot run RCCL, so the
+            # peer kernel is verified against gloo at the first generation and kept
+            for i in range(2):
+                sel = [r["transport_select"] for r in read_jsonl(tmp_path / f"client{i}.jsonl")
+                       if "transport_select" in r]
+                assert sel and sel[0]["verified_against"] == "gloo" and sel[0]["chosen"] in ("oneshot", "twoshot")
     finally:
         for p in procs:
             stop_proc(p)

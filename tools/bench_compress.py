@@ -2,9 +2,8 @@
 """-c Y kernel timings (csrc/kernels/compress.hip) at the LeNet and ResNet-18 state sizes.
 
 For n = 62,006 (LeNet) and 11,173,962 (ResNet-18): device time of the
-error-feedback delta + exact top-k (k = 1 %: the fused 4-launch path ``topk_us``, round 2's
-ef_delta + 4-pass radix ``topk_r2_radix_us``, and one read+write pass over the state for
-scale ``rw_pass_us``), of the rank-ordered
+error-feedback delta + exact top-k (k = 1 %: the fused 4-launch path ``topk_us``, and one
+read+write pass over the state for scale ``rw_pass_us``), of the rank-ordered
 scatter of 4 ranks' payloads, of int8 quantisation and of a 4-rank dequant
 accumulate; plus payload bytes vs dense fp32.  One JSON line per size.
 """
@@ -48,17 +47,8 @@ def main() -> int:
         glob = torch.randn(n, device=dev)
         resid = torch.zeros(n, device=dev)
         d = torch.empty(n, device=dev)
-        state = torch.zeros(nat.select_state_bytes(), dtype=torch.uint8, device=dev)
-        counts = torch.zeros(2 * ((n + nat.compact_chunk() - 1) // nat.compact_chunk()), dtype=torch.int32, device=dev)
         idx = torch.empty(k, dtype=torch.int32, device=dev)
         val = torch.empty(k, device=dev)
-
-        def topk():
-            nat.ef_delta(S(), local.data_ptr(), glob.data_ptr(), resid.data_ptr(), d.data_ptr(), n)
-            nat.topk(S(), d.data_ptr(), n, k, state.data_ptr(), counts.data_ptr(), idx.data_ptr(), val.data_ptr(),
-                     resid.data_ptr())
-
-        t_topk_old = _time(topk, iters)
         tstate = torch.zeros(nat.topk_state_bytes(), dtype=torch.uint8, device=dev)
         cidx = torch.empty(2 * n, dtype=torch.int32, device=dev)
         ckey = torch.empty(2 * n, dtype=torch.int32, device=dev)
@@ -98,7 +88,6 @@ def main() -> int:
                      iters)
         rec = {"bench": "compress_kernels", "payload": name, "n": n, "k": k,
                "topk_us": round(t_topk, 2), "topk_fresh_update_us": round(t_topk_fresh, 2), "candidates_last": cand,
-               "topk_r2_radix_us": round(t_topk_old, 2),
                "rw_pass_us": round(t_copy, 2), "scatter_ranked_4rank_us": round(t_scatter, 2),
                "quant_int8_us": round(t_q, 2), "dequant_accum_4rank_us": round(t_dq, 2),
                "bytes_dense": 4 * n, "bytes_topk": 8 * k, "bytes_int8": n + 4 * nch,
