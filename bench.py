@@ -77,8 +77,14 @@ def _breakdown(marks, phases, t0: float, t1: float, steps: int) -> dict:
         span.append(row[0][1].elapsed_time(row[-1][1]))
     gaps = [marks[i][0][1].elapsed_time(marks[i + 1][0][1]) - span[i] for i in range(len(marks) - 1)]
     med = lambda v: round(statistics.median(v), 4) if v else None  # noqa: E731
+    mean = lambda v: round(sum(v) / len(v), 4) if v else None  # noqa: E731
     return {"device_ms": {p: med(v) for p, v in dev.items()}, "host_issue_ms": {p: med(v) for p, v in host.items()},
-            "device_round_span_ms": med(span), "device_idle_between_rounds_ms": med(gaps),
+            "device_ms_mean": {p: mean(v) for p, v in dev.items()},
+            "device_ms_max": {p: round(max(v), 4) for p, v in dev.items() if v},
+            "host_issue_ms_mean": {p: mean(v) for p, v in host.items()},
+            "device_round_span_ms": med(span), "device_round_span_ms_mean": mean(span),
+            "device_idle_between_rounds_ms": med(gaps), "device_idle_between_rounds_ms_mean": mean(gaps),
+            "device_idle_between_rounds_ms_max": round(max(gaps), 4) if gaps else None,
             "wall_ms_per_round": round((t1 - t0) / steps * 1e3, 4), "rounds": len(marks)}
 
 
@@ -141,6 +147,7 @@ def main() -> int:
     ap.add_argument("--compress", default="none", choices=["none", "topk", "int8"],
                     help="-c Y data-plane compression of the FedAvg update")
     ap.add_argument("--topk-ratio", type=float, default=0.01)
+    ap.add_argument("--compress-warmup", type=int, default=0, help="dense FedAvg rounds before compression starts")
     ap.add_argument("--allreduce", default="auto", choices=["auto", "rccl", "oneshot", "twoshot"],
                     help="FedAvg transport at N>1: hipIpc peer kernels (oneshot/twoshot), RCCL, or auto = verify "
                          "the peer kernel against RCCL and time both, keep the faster")
@@ -222,7 +229,8 @@ def main() -> int:
             # peer transport, whose barriers time out
             print("[bench] --inject-fault needs the peer transport", file=sys.stderr)
             return 2
-    agg = FedAvg(compressor=make_compressor(args.compress, args.topk_ratio, trainer), transport=transport)
+    agg = FedAvg(compressor=make_compressor(args.compress, args.topk_ratio, trainer, args.compress_warmup),
+                 transport=transport)
     if shard_world > 1 and not args.eval_full:
         trainer.set_test_data(eval_shard(data.test, rank, shard_world))
     hist = EvalHistory(trainer, args.warmup + args.steps)

@@ -19,19 +19,11 @@ namespace py = pybind11;
 namespace fedmi {
 void launch_lenet_conv_fwd(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*, int,
                            bf16*, bf16*, int, bf16*, uint8_t*, uint8_t*, lenet::Stats*);
-void launch_lenet_fc1_fwd(hipStream_t, const bf16*, int, const bf16*, const float*, bf16*);
-void launch_lenet_fc_tail(hipStream_t, const bf16*, const bf16*, const int*, int, int, const bf16*, const float*, float*,
-                          bf16*, float*, lenet::Stats*);
-void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const float*, const bf16*,
-                           const bf16*, const bf16*, const uint8_t*, const uint8_t*, const bf16*, float*, float*);
+void launch_lenet_fc_eval(hipStream_t, const bf16*, const int*, int, const bf16*, const float*, float*, long,
+                          lenet::Stats*);
 bool stamps_enabled();
 void read_stamps(unsigned long long*, bool);
 void set_ks1_diag(int);
-void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, const float*, const float*, int, float,
-                      float, float, int*, int*);
-void launch_lenet_fwd_head(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*, int,
-                           bf16*, bf16*, bf16*, uint8_t*, uint8_t*, const int*, float*, bf16*, float*, lenet::Stats*,
-                           int*, const int*, int*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
 void launch_sgd_flat(hipStream_t, float*, const float*, float*, long, float, float, float, float, int, int);
 void launch_ef_delta(hipStream_t, const float*, const float*, const float*, float*, long);
@@ -69,21 +61,14 @@ static LeNetBuffers buffers_from(const py::dict& d) {
   b.act2_rows = d.contains("act2_rows") ? d["act2_rows"].cast<int>() : 0;
   b.act2T = P<bf16>(get("act2T"));
   b.h1 = P<bf16>(get("h1"));
-  b.pool1 = P<bf16>(get("pool1"));
-  b.am1 = P<uint8_t>(get("am1"));
-  b.am2 = P<uint8_t>(get("am2"));
   b.dact2 = P<float>(get("dact2"));
   b.dZ1T = P<bf16>(get("dZ1T"));
   b.conv_slab = P<float>(get("conv_slab"));
-  b.fc1w_grad = P<float>(get("fc1w_grad"));
-  b.fc_slab = P<float>(get("fc_slab"));
+  b.eval_part = P<float>(get("eval_part"));
+  b.eval_part_floats = d.contains("eval_part_floats") ? d["eval_part_floats"].cast<long>() : 0;
   b.train_stats = P<lenet::Stats>(get("train_stats"));
   b.eval_stats = P<lenet::Stats>(get("eval_stats"));
   b.round_ctr = P<int>(get("round_ctr"));
-  b.done_flags = P<int>(get("done_flags"));
-  b.step_gen = P<int>(get("step_gen"));
-  b.bwd_flags = P<int>(get("bwd_flags"));
-  b.bwd_gen = P<int>(get("bwd_gen"));
   return b;
 }
 
@@ -109,8 +94,8 @@ static void fedmi_bind(py::module_& m) {
     d["P_C1W"] = P_C1W; d["P_C1B"] = P_C1B; d["P_C2W"] = P_C2W; d["P_C2B"] = P_C2B;
     d["P_F1W"] = P_F1W; d["P_F1B"] = P_F1B; d["P_F2W"] = P_F2W; d["P_F2B"] = P_F2B;
     d["P_F3W"] = P_F3W; d["P_F3B"] = P_F3B; d["P_TOTAL"] = P_TOTAL;
-    d["CS"] = CS; d["FS"] = FS; d["F1W_N"] = F1W_N; d["DZ1_LD"] = DZ1_LD; d["N_DW1_WG"] = N_DW1_WG; d["PK_TOTAL"] = PK_TOTAL; d["F0"] = F0; d["F0P"] = F0P; d["NP1"] = NP1;
-    d["MAX_TRAIN_BATCH"] = MAX_TRAIN_BATCH; d["FC_SPW"] = FC_SPW; d["MAX_FC_WG"] = MAX_FC_WG;
+    d["CS"] = CS; d["FS"] = FS; d["F1W_N"] = F1W_N; d["DZ1_LD"] = DZ1_LD; d["PK_TOTAL"] = PK_TOTAL; d["F0"] = F0; d["F0P"] = F0P; d["NP1"] = NP1;
+    d["MAX_TRAIN_BATCH"] = MAX_TRAIN_BATCH; d["FC_SPW"] = FC_SPW;
     d["IMG_BYTES"] = IMG_BYTES; d["STATS_BYTES"] = (int)sizeof(Stats);
     return d;
   });
@@ -138,24 +123,14 @@ static void fedmi_bind(py::module_& m) {
            py::call_guard<py::gil_scoped_release>())
       .def("run_epoch", [](LeNetEngine& e, uintptr_t st, bool use_graph) { e.run_epoch(S(st), use_graph); },
            py::call_guard<py::gil_scoped_release>())
-      .def("eval", [](LeNetEngine& e, uintptr_t st, uintptr_t images, uintptr_t labels, int n, uintptr_t pk,
-                      uintptr_t params) {
-             e.eval(S(st), P<const uint8_t>(images), P<const int>(labels), n, P<const bf16>(pk), P<const float>(params));
-           }, py::arg("st"), py::arg("images"), py::arg("labels"), py::arg("n"), py::arg("pk") = 0,
-           py::arg("params") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("eval", [](LeNetEngine& e, uintptr_t st, uintptr_t images, uintptr_t labels, int n) {
+             e.eval(S(st), P<const uint8_t>(images), P<const int>(labels), n);
+           }, py::arg("st"), py::arg("images"), py::arg("labels"), py::arg("n"), py::call_guard<py::gil_scoped_release>())
       .def("pack", [](LeNetEngine& e, uintptr_t st) { e.pack(S(st)); }, py::call_guard<py::gil_scoped_release>())
-      .def("set_fuse_fc1", &LeNetEngine::set_fuse_fc1)
-      .def("fuse_fc1", &LeNetEngine::fuse_fc1)
       .def("set_sgd", [](LeNetEngine& e, float lr, float m, float wd) {
              SgdConfig c; c.lr = lr; c.momentum = m; c.weight_decay = wd; e.set_sgd(c);
            })
-      .def("graph_ready", &LeNetEngine::graph_ready)
-      .def("set_fuse_head", &LeNetEngine::set_fuse_head)
-      .def("fuse_head", &LeNetEngine::fuse_head)
-      .def("set_fuse_sgd", &LeNetEngine::set_fuse_sgd)
-      .def("fuse_sgd", &LeNetEngine::fuse_sgd)
-      .def("set_sample_path", &LeNetEngine::set_sample_path)
-      .def("sample_path", &LeNetEngine::sample_path);
+      .def("graph_ready", &LeNetEngine::graph_ready);
 
   // ---- raw LeNet kernels (numerics tests drive them one by one) -------------
   m.def("lenet_conv_fwd", [](uintptr_t st, uintptr_t images, int base, int nb, uintptr_t pk, uintptr_t params,
@@ -165,48 +140,6 @@ static void fedmi_bind(py::module_& m) {
                           P<const int>(round_ctr), augment, P<bf16>(act2), P<bf16>(act2T), tstride, P<bf16>(pool1),
                           P<uint8_t>(am1), P<uint8_t>(am2), P<lenet::Stats>(zero_stats));
     check_last("lenet_conv_fwd");
-  });
-  // FC head = fc1 forward (tiled) + FC tail; kept as one entry point for the tests.
-  // h1 == 0: the fused variant (fc1 inside the tail, no K2a launch)
-  m.def("lenet_fc_head", [](uintptr_t st, uintptr_t act2, uintptr_t labels, int nb, int train, uintptr_t pk,
-                            uintptr_t params, uintptr_t h1, uintptr_t dact2, uintptr_t dZ1T, uintptr_t fc_slab,
-                            uintptr_t stats) {
-    if (h1) launch_lenet_fc1_fwd(S(st), P<const bf16>(act2), nb, P<const bf16>(pk), P<const float>(params), P<bf16>(h1));
-    launch_lenet_fc_tail(S(st), P<const bf16>(h1), P<const bf16>(act2), P<const int>(labels), nb, train,
-                         P<const bf16>(pk), P<const float>(params), P<float>(dact2), P<bf16>(dZ1T),
-                         P<float>(fc_slab), P<lenet::Stats>(stats));
-    check_last("lenet_fc_head");
-  });
-  m.def("lenet_conv_bwd", [](uintptr_t st, uintptr_t images, int base, int nb, uint32_t seed, uintptr_t round_ctr,
-                             int augment, uintptr_t dact2, uintptr_t act2T, uintptr_t dZ1T, uintptr_t pool1,
-                             uintptr_t am1, uintptr_t am2, uintptr_t pk, uintptr_t conv_slab, uintptr_t fc1w_grad) {
-    launch_lenet_conv_bwd(S(st), P<const uint8_t>(images), base, nb, seed, P<const int>(round_ctr), augment,
-                          P<const float>(dact2), P<const bf16>(act2T), P<const bf16>(dZ1T), P<const bf16>(pool1),
-                          P<const uint8_t>(am1), P<const uint8_t>(am2), P<const bf16>(pk), P<float>(conv_slab),
-                          P<float>(fc1w_grad));
-    check_last("lenet_conv_bwd");
-  });
-  m.def("lenet_sgd", [](uintptr_t st, uintptr_t params, uintptr_t mom, uintptr_t pk, uintptr_t conv_slab, int n_conv,
-                        uintptr_t fc1w_grad, uintptr_t fc_slab, int n_fc, float lr, float mo, float wd,
-                        uintptr_t round_ctr, uintptr_t step_gen) {
-    launch_lenet_sgd(S(st), P<float>(params), P<float>(mom), P<bf16>(pk), P<const float>(conv_slab), n_conv,
-                     P<const float>(fc1w_grad), P<const float>(fc_slab), n_fc, lr, mo, wd, P<int>(round_ctr),
-                     P<int>(step_gen));
-    check_last("lenet_sgd");
-  }, py::arg("stream"), py::arg("params"), py::arg("mom"), py::arg("pk"), py::arg("conv_slab"), py::arg("n_conv"),
-     py::arg("fc1w_grad"), py::arg("fc_slab"), py::arg("n_fc"), py::arg("lr"), py::arg("mo"), py::arg("wd"),
-     py::arg("round_ctr"), py::arg("step_gen") = 0);
-  // K1 + K2b in one launch (training); flags: int[128] hand-off flags, step_gen: int generation (K4 bumps it)
-  m.def("lenet_fwd_head", [](uintptr_t st, uintptr_t images, int base, int nb, uintptr_t pk, uintptr_t params,
-                             uint32_t seed, uintptr_t round_ctr, int augment, uintptr_t act2, uintptr_t act2T,
-                             uintptr_t pool1, uintptr_t am1, uintptr_t am2, uintptr_t labels, uintptr_t dact2,
-                             uintptr_t dZ1T, uintptr_t fc_slab, uintptr_t stats, uintptr_t flags, uintptr_t step_gen) {
-    launch_lenet_fwd_head(S(st), P<const uint8_t>(images), base, nb, P<const bf16>(pk), P<const float>(params), seed,
-                          P<const int>(round_ctr), augment, P<bf16>(act2), P<bf16>(act2T), P<bf16>(pool1),
-                          P<uint8_t>(am1), P<uint8_t>(am2), P<const int>(labels), P<float>(dact2), P<bf16>(dZ1T),
-                          P<float>(fc_slab), P<lenet::Stats>(stats), P<int>(flags), P<const int>(step_gen),
-                          nullptr);
-    check_last("lenet_fwd_head");
   });
   m.def("lenet_pack", [](uintptr_t st, uintptr_t params, uintptr_t pk) {
     launch_lenet_pack(S(st), P<const float>(params), P<bf16>(pk));

@@ -75,7 +75,7 @@ void launch_bn_coeff(hipStream_t, const BNDesc&, int, int, float, float, int, fl
 long bn_bwd_ws_floats(int, int);
 int bn_bwd_chain_reps(int);
 void launch_head(hipStream_t, const bf16*, const int*, int, const int*, int, int, int, int, const float*,
-                 const float*, float*, float*, bf16*, float*, float*, float*, int, float*, long);
+                 const float*, float*, float*, bf16*, float*, float*, float*, float*, int, float*, long);
 }  // namespace fedmi
 
 using namespace fedmi;
@@ -269,12 +269,13 @@ void fedmi_bind_cnn(py::module_& m) {
   m.def("bn_bwd_chain_reps", [](int C) { return bn_bwd_chain_reps(C); });
   m.def("head", [](uintptr_t st, uintptr_t y, uintptr_t labels, int base, uintptr_t dbase, int N, int HW, int C, int J,
                    uintptr_t W, uintptr_t b, uintptr_t pooled, uintptr_t dlog, uintptr_t dy, uintptr_t stats,
-                   uintptr_t dW, uintptr_t db, int train, uintptr_t zero_buf, long zero_n) {
+                   uintptr_t dW, uintptr_t db, int train, uintptr_t zero_buf, long zero_n, uintptr_t lossv) {
     launch_head(S(st), P<const bf16>(y), P<const int>(labels), base, P<const int>(dbase), N, HW, C, J, P<const float>(W),
-                P<const float>(b), P<float>(pooled), P<float>(dlog), P<bf16>(dy), P<float>(stats), P<float>(dW),
-                P<float>(db), train, P<float>(zero_buf), zero_n);
+                P<const float>(b), P<float>(pooled), P<float>(dlog), P<bf16>(dy), P<float>(stats), P<float>(lossv),
+                P<float>(dW), P<float>(db), train, P<float>(zero_buf), zero_n);
     check("head");
   }, py::arg("st"), py::arg("y"), py::arg("labels"), py::arg("base"), py::arg("dbase"), py::arg("N"), py::arg("HW"),
      py::arg("C"), py::arg("J"), py::arg("W"), py::arg("b"), py::arg("pooled"), py::arg("dlog"), py::arg("dy"),
-     py::arg("stats"), py::arg("dW"), py::arg("db"), py::arg("train"), py::arg("zero_buf") = 0, py::arg("zero_n") = 0);
+     py::arg("stats"), py::arg("dW"), py::arg("db"), py::arg("train"), py::arg("zero_buf") = 0, py::arg("zero_n") = 0,
+     py::arg("lossv") = 0);
 }

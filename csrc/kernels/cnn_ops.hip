@@ -547,8 +547,9 @@ __global__ __launch_bounds__(256) void head_fwd_bwd_kernel(const bf16* __restric
                                                            int base, const int* __restrict__ dbase, int HW, int C, int J, const float* __restrict__ W,
                                                            const float* __restrict__ b, float* __restrict__ pooled,
                                                            float* __restrict__ dlog, bf16* __restrict__ dy,
-                                                           float* __restrict__ stats, int N, int train,
-                                                           float4* __restrict__ zero_buf, long zero_n4) {
+                                                           float* __restrict__ stats, float* __restrict__ lossv,
+                                                           int N, int train, float4* __restrict__ zero_buf,
+                                                           long zero_n4) {
   // the step's BN-backward replica arena (chained mode) is cleared here: the head runs after every
   // BN backward of the previous step and before any of this step
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < zero_n4; i += (long)gridDim.x * 256)
@@ -620,7 +621,7 @@ __global__ __launch_bounds__(256) void head_fwd_bwd_kernel(const bf16* __restric
     float se = 0.f;
     for (int j = 0; j < J; ++j) se += __expf(lg[j] - mx);
     const float lse = mx + __logf(se);
-    atomicAdd(stats, lse - lg[lab]);
+    lossv[n] = lse - lg[lab];   // summed in sample order by head_wgrad / head_loss (no float atomics)
     atomicAdd(reinterpret_cast<int*>(stats) + 1, am == lab ? 1 : 0);
     atomicAdd(reinterpret_cast<int*>(stats) + 2, 1);
     for (int j = 0; j < J; ++j) {
@@ -658,9 +659,29 @@ constexpr int HEAD_MAXN = 512;
 // Block = 64 channels x 4 sample groups (fixed-order LDS combine: deterministic);
 // block 0 also reduces db.  Loads are issued 8 at a time before use (the kernel has
 // C/64 workgroups, so a load-use loop was one memory round trip per sample: 30 us).
+// stats[0] += sum_n lossv[n] in a fixed order (256 strided partials, then an ordered LDS fold): the loss sum
+// is bit-reproducible, unlike a float atomicAdd per sample.  Called by ONE workgroup.
+FEDMI_DEV void ordered_loss_sum(const float* __restrict__ lossv, int N, float* __restrict__ stats, float* red) {
+  float s = 0.f;
+  for (int n = threadIdx.x; n < N; n += 256) s += lossv[n];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) stats[0] += red[0];
+}
+
+__global__ __launch_bounds__(256) void head_loss_kernel(const float* __restrict__ lossv, int N, float* __restrict__ stats) {
+  __shared__ float red[256];
+  ordered_loss_sum(lossv, N, stats, red);
+}
+
 __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict__ pooled, const float* __restrict__ dlog,
                                                          int N, int C, int J, float* __restrict__ dW,
-                                                         float* __restrict__ db) {
+                                                         float* __restrict__ db, const float* __restrict__ lossv,
+                                                         float* __restrict__ stats) {
   __shared__ float part[4][16][64];
   __shared__ float dls[HEAD_MAXN * 16];   // dlog staged once per block, read as LDS broadcasts
   const int cl = threadIdx.x & 63, ng = threadIdx.x >> 6;
@@ -719,6 +740,8 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict
       for (int q = 0; q < 16; ++q) t += red[q * 16 + threadIdx.x];
       db[threadIdx.x] = t;
     }
+    __syncthreads();
+    ordered_loss_sum(lossv, N, stats, red);
   }
 }
 
@@ -1071,18 +1094,22 @@ void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, double* red, int M, int C
 }
 
 void launch_head(hipStream_t st, const bf16* y, const int* labels, int base, const int* dbase, int N, int HW, int C, int J,
-                 const float* W, const float* b, float* pooled, float* dlog, bf16* dy, float* stats, float* dW,
-                 float* db, int train, float* zero_buf, long zero_n) {
+                 const float* W, const float* b, float* pooled, float* dlog, bf16* dy, float* stats, float* lossv,
+                 float* dW, float* db, int train, float* zero_buf, long zero_n) {
+  if (lossv == nullptr) throw std::invalid_argument("head: per-sample loss buffer required");
   if (zero_n % 4 || (reinterpret_cast<uintptr_t>(zero_buf) & 15)) throw std::invalid_argument("head: zero arena alignment");
   if (J > 16) throw std::invalid_argument("head: at most 16 classes");
   if (C % 8 || C > 2048) throw std::invalid_argument("head: need C % 8 == 0 and C <= 2048");
   const int npg = std::max(1, 256 / (C / 8));
   hipLaunchKernelGGL(head_fwd_bwd_kernel, dim3(N), dim3(256), (C + 32 + npg * C) * sizeof(float), st, y, labels, base, dbase, HW, C,
-                     J, W, b, pooled, dlog, dy, stats, N, train,
+                     J, W, b, pooled, dlog, dy, stats, lossv, N, train,
                      reinterpret_cast<float4*>(zero_buf), zero_n / 4);
   if (train && N > HEAD_MAXN) throw std::invalid_argument("head: training batch > 512");
   if (train)
-    hipLaunchKernelGGL(head_wgrad_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pooled, dlog, N, C, J, dW, db);
+    hipLaunchKernelGGL(head_wgrad_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pooled, dlog, N, C, J, dW, db, lossv,
+                       stats);
+  else
+    hipLaunchKernelGGL(head_loss_kernel, dim3(1), dim3(256), 0, st, lossv, N, stats);
 }
 
 }  // namespace fedmi

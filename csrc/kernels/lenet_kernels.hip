@@ -1,33 +1,25 @@
 // fedmi — fused LeNet training/eval kernels for MI355X (gfx950, CDNA4).
 //
-// One local SGD step of the reference (src/main.py:146-151: zero_grad,
-// forward, CE loss, backward, SGD(m=0.9, wd=5e-4)) is FIVE launches:
+// One local SGD step of the reference (src/main.py:146-151: zero_grad, forward, CE loss,
+// backward, SGD(m=0.9, wd=5e-4)) is TWO launches:
 //
-//   K1 lenet_conv_fwd   one 8-wave workgroup per sample: uint8 image ->
-//                       on-device RandomCrop(32,pad4)+HFlip+Normalize
-//                       (src/main.py:37-42) -> conv1 (MFMA, channels-last LDS
-//                       image: one 16-B read per operand fragment) +bias+ReLU
-//                       -> maxpool2 -> conv2 (MFMA) +bias+ReLU -> maxpool2.
-//                       Saves pooled activations + 2-bit argmax codes.
-//   K2a lenet_fc1_fwd   fc1 forward tiled 16 samples x 16 outputs (the fc1
-//                       weight image is streamed by 8 column workgroups).
-//   K2b lenet_fc_tail   16 samples per row group: fc2/fc3 forward, cross-
-//                       entropy + accuracy counters, FC backward (fc2/fc3 wgrad,
-//                       bias grads, dZ1) and dX = dZ1.W1 split 4 ways over
-//                       workgroups.  Also the eval head (train=0).
-//   K3 lenet_conv_bwd   one workgroup per sample: maxpool/ReLU backward by
-//                       argmax, conv2 wgrad + dgrad,
-//                       conv1 wgrad (MFMA; the im2col operands come from
-//                       5 column-shifted LDS copies so every fragment is one
-//                       aligned 16-B read).  25 extra workgroups of the same
-//                       launch compute fc1.weight's gradient (dZ1^T X).
-//   K4 lenet_sgd        combines the gradient slabs (split-K combine at the
-//                       kernel boundary: deterministic, no global atomics),
-//                       applies wd/momentum/lr to the fp32 master weights and
-//                       rewrites the packed bf16 MFMA operand images.
+//   KS1 lenet_sample_step  one 16-wave workgroup per sample runs the sample's whole chain:
+//                          on-device RandomCrop(32,pad4)+HFlip+Normalize (src/main.py:37-42)
+//                          -> conv1 (MFMA) +bias+ReLU -> maxpool2 -> conv2 (MFMA) +bias+ReLU
+//                          -> maxpool2 -> fc1/fc2/fc3 -> CE -> FC backward -> conv backward
+//                          (maxpool/ReLU backward by argmax, conv2 wgrad + dgrad, conv1
+//                          wgrad; im2col operands from 5 column-shifted LDS copies so every
+//                          fragment is one aligned 16-B read) -> the sample's gradient slab.
+//   KS2 lenet_sgd2         fc1/fc2/fc3 weight gradients as MFMA GEMMs over the batch, SGD
+//                          applied to each tile in the workgroup that computed it, the conv
+//                          slab combine, bias sums, loss/accuracy: fixed order, no atomics.
 //
-// The whole local epoch is replayed from a hipGraph built by the native
-// executor (csrc/runtime/lenet_engine.cpp).
+// Evaluation: lenet_conv_fwd (one 8-wave workgroup per sample, the same conv stack as KS1)
+// then lenet_fc_eval (16 samples per workgroup, fc1/fc2/fc3 as MFMA tiles, CE) and
+// lenet_eval_stats (ordered sum of the row groups' partials).
+//
+// The whole local epoch is replayed from a hipGraph built by the native executor
+// (csrc/runtime/lenet_engine.cpp).
 #include <stdexcept>
 
 #include "common.h"
@@ -44,12 +36,11 @@ __device__ int fedmi_ks1_diag;
 
 namespace {
 
-constexpr int NT_FWD = 512;     // conv forward (K1): 8 waves (measured faster than 16)
+constexpr int NT_FWD = 512;     // eval conv forward: 8 waves (measured faster than 16)
 constexpr int NW_FWD = NT_FWD / 64;
-constexpr int NT_CONV = 1024;   // conv backward (K3): 16 waves
+constexpr int NT_CONV = 1024;   // KS1: 16 waves
 constexpr int NW_CONV = NT_CONV / 64;
-constexpr int NT_FC = 512;      // FC tail (K2b): 8 waves
-constexpr int NW_FC = NT_FC / 64;
+constexpr int NT_FC = 512;      // eval FC head: 8 waves
 
 __constant__ float kMean[3] = {0.4914f, 0.4822f, 0.4465f};
 __constant__ float kInvStd[3] = {1.f / 0.2023f, 1.f / 0.1994f, 1.f / 0.2010f};
@@ -103,13 +94,11 @@ FEDMI_DEV void zero_lds(void* p, int bytes) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// K1: conv stack forward, one 8-wave workgroup per sample.
+// lenet_conv_fwd: conv stack forward, one 8-wave workgroup per sample (eval; in "train" mode it
+// also saves act2T / pool1 / argmax codes -- the tests' forward oracle for KS1's backward).
 // ---------------------------------------------------------------------------
-// Body of one sample's workgroup; 'done_flag' (fused fwd+head launch): after act2/act2T
-// are stored, publish 'gen' there for the FC-head workgroups of the same launch.
-template <bool LDSW>
-FEDMI_DEV void conv_fwd_body(
-    int s, const uint8_t* __restrict__ images, int sample_base, int nb,
+__global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
+    const uint8_t* __restrict__ images, int sample_base, int nb,
     const bf16* __restrict__ pk, const float* __restrict__ params,
     uint32_t seed, const int* __restrict__ round_ctr, int augment,
     bf16* __restrict__ act2,        // [nb][F0P]
@@ -118,28 +107,23 @@ FEDMI_DEV void conv_fwd_body(
     bf16* __restrict__ pool1_out,   // [nb][NP1] CHW, or null
     uint8_t* __restrict__ am1_out,  // [nb][NP1] or null
     uint8_t* __restrict__ am2_out,  // [nb][F0]  or null
-    Stats* __restrict__ zero_stats, // stats block to reset before K2 accumulates (or null)
-    int* __restrict__ done_flag, int gen)
+    Stats* __restrict__ zero_stats) // stats block to reset before the FC head accumulates (or null)
 {
   // LDS: raw u8 | x channels-last [36][40][4] bf16 | conv1 out f32 channels-last [784][8]
   //      | pool1 channels-last [14][14][8] bf16 | conv2 out f32 channels-last [100][16]
-  //      | conv1 / conv2 B images (rows padded to 136 / 232 bf16, staged once per workgroup: the
-  //        per-wave register loads of round 1 moved 8 waves x 11 KB of L2 traffic per sample)
-  //        (LDSW: the fused K12 launch, where the fewer workgroups make the LDS cost free; the
-  //        10 000-workgroup eval launch keeps register fragments: its occupancy is worth more)
+  //      (conv weights as register fragments: the 10 000-workgroup eval launch values occupancy over
+  //      the per-wave L2 traffic KS1 avoids by staging them in LDS)
   constexpr int XCL = 36 * 40 * 4, P1CL = 14 * 14 * 8;
   constexpr int O_X = 3072, O_C1 = O_X + XCL * 2, O_P1 = O_C1 + NPOS1 * 8 * 4, O_C2 = O_P1 + P1CL * 2,
-                O_W1 = O_C2 + C2 * NPOS2 * 4, O_W2 = O_W1 + 16 * 136 * 2,
-                O_END = LDSW ? O_W2 + 16 * 232 * 2 : O_W1;
+                O_END = O_C2 + C2 * NPOS2 * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem[O_END];
-  bf16* w1c = reinterpret_cast<bf16*>(smem + O_W1);
-  bf16* w2c = reinterpret_cast<bf16*>(smem + O_W2);
   uint8_t* raw = smem;
   bf16* xcl = reinterpret_cast<bf16*>(smem + O_X);
   float* c1 = reinterpret_cast<float*>(smem + O_C1);
   bf16* p1cl = reinterpret_cast<bf16*>(smem + O_P1);
   float* c2 = reinterpret_cast<float*>(smem + O_C2);
 
+  const int s = blockIdx.x;
   if (s >= nb) return;
   [[maybe_unused]] const int stamp_wg = s;
   const int gidx = sample_base + s;
@@ -153,38 +137,12 @@ FEDMI_DEV void conv_fwd_body(
   // image (192) + conv1 (256) + conv2 (448) weight chunks of 16 B, <= 2 per thread, and every other
   // global read of the kernel start, issued together while the x image is zeroed
   bf16x8 wr1[4], wr2[7];
-  if constexpr (!LDSW) {
-    load_raw(images + (size_t)gidx * IMG_BYTES, raw);
-    zero_lds(xcl, XCL * 2);
+  load_raw(images + (size_t)gidx * IMG_BYTES, raw);
+  zero_lds(xcl, XCL * 2);   // channel 3 and the right/bottom pad stay zero
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) wr1[ks] = ld8(pk + PK_W1C + n16 * K1C + ks * 32 + kq);
+  for (int ks = 0; ks < 4; ++ks) wr1[ks] = ld8(pk + PK_W1C + n16 * K1C + ks * 32 + kq);
 #pragma unroll
-    for (int ks = 0; ks < 7; ++ks) wr2[ks] = ld8(pk + PK_W2C + n16 * K2C + ks * 32 + kq);
-  } else {
-    constexpr int NI = IMG_BYTES / 16, NW1 = 16 * K1C / 8, NW2 = 16 * K2C / 8;
-    uint4 v[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + u * NT_FWD;
-      if (e < NI) v[u] = reinterpret_cast<const uint4*>(images + (size_t)gidx * IMG_BYTES)[e];
-      else if (e < NI + NW1) v[u] = reinterpret_cast<const uint4*>(pk + PK_W1C)[e - NI];
-      else if (e < NI + NW1 + NW2) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2C)[e - NI - NW1];
-    }
-    zero_lds(xcl, XCL * 2);   // channel 3 and the right/bottom pad stay zero
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + u * NT_FWD;
-      if (e < NI) {
-        reinterpret_cast<uint4*>(raw)[e] = v[u];
-      } else if (e < NI + NW1) {
-        const int w = e - NI;
-        reinterpret_cast<uint4*>(w1c + (w / (K1C / 8)) * 136)[w % (K1C / 8)] = v[u];
-      } else if (e < NI + NW1 + NW2) {
-        const int w = e - NI - NW1;
-        reinterpret_cast<uint4*>(w2c + (w / (K2C / 8)) * 232)[w % (K2C / 8)] = v[u];
-      }
-    }
-  }
+  for (int ks = 0; ks < 7; ++ks) wr2[ks] = ld8(pk + PK_W2C + n16 * K2C + ks * 32 + kq);
   int go1[4], go2[7];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
@@ -202,7 +160,7 @@ FEDMI_DEV void conv_fwd_body(
   __syncthreads();
   bf16x8 wb1[4];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) wb1[ks] = LDSW ? ld8(w1c + n16 * 136 + ks * 32 + kq) : wr1[ks];
+  for (int ks = 0; ks < 4; ++ks) wb1[ks] = wr1[ks];
   for (int e = tid; e < IMG_BYTES; e += NT_FWD) {   // lanes walk x: raw reads broadcast within a dword
     const int c = e >> 10, y = (e >> 5) & 31, x = e & 31;
     xcl[(y * 40 + x) * 4 + c] = (bf16)aug_pixel(raw, a, c, y, x);
@@ -277,10 +235,9 @@ FEDMI_DEV void conv_fwd_body(
     if (pos >= NPOS2) pos = 0;
     const int py = pos / O2, px = pos - py * O2;
     const bf16* pb = p1cl + (py * P1 + px) * 8;
-    const bf16* wb = w2c + n16 * 232 + kq;
     f32x4 acc = zero4();
 #pragma unroll
-    for (int ks = 0; ks < 7; ++ks) acc = mfma16(ld8(pb + go2[ks]), LDSW ? ld8(wb + ks * 32) : wr2[ks], acc);
+    for (int ks = 0; ks < 7; ++ks) acc = mfma16(ld8(pb + go2[ks]), wr2[ks], acc);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int p = t * 16 + rq + r;
@@ -303,157 +260,43 @@ FEDMI_DEV void conv_fwd_body(
       mb = (bf16)m;
       if (am2_out) am2_out[(size_t)s * F0 + e] = (uint8_t)am;
     }
-    if (done_flag != nullptr) reinterpret_cast<bf16*>(raw)[e] = mb;   // staged: published write-through below
-    else act2[(size_t)s * F0P + e] = mb;
+    act2[(size_t)s * F0P + e] = mb;
     if (act2T) act2T[(size_t)e * tstride + s] = mb;
-  }
-  if (done_flag != nullptr) {
-    // Hand-off to the FC-head workgroups of this launch without cache maintenance
-    // (MI355X_MICROARCH.md hand-off table, row 1): the act2 row goes out as 8-byte
-    // write-through (sc1) stores, every wave drains them, a workgroup barrier, then ONE
-    // lane's sc1 flag store.  The consumers read the row only with sc1 loads.
-    __syncthreads();
-    if (tid < F0P / 4)
-      __hip_atomic_store(reinterpret_cast<uint64_t*>(act2 + (size_t)s * F0P) + tid,
-                         reinterpret_cast<const uint64_t*>(raw)[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(done_flag + s, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   FEDMI_STAMP(0, 5);
 }
 
-__global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
-    const uint8_t* __restrict__ images, int sample_base, int nb, const bf16* __restrict__ pk,
-    const float* __restrict__ params, uint32_t seed, const int* __restrict__ round_ctr, int augment,
-    bf16* __restrict__ act2, bf16* __restrict__ act2T, int tstride, bf16* __restrict__ pool1_out,
-    uint8_t* __restrict__ am1_out, uint8_t* __restrict__ am2_out, Stats* __restrict__ zero_stats)
+// ---------------------------------------------------------------------------
+// lenet_fc_eval: the eval head, 16 samples per 8-wave workgroup.  fc1 = relu(X W1^T + b1) from
+// the act2 tile in LDS and this wave's 16 W1 rows held as 13 register fragments, fc2 / fc3 as
+// 16x16 MFMA tiles, then CE + argmax on 16 lanes.  The row group's (loss, correct) go to
+// part[2 mt], part[2 mt + 1] for lenet_eval_stats' ordered sum (no float atomics).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT_FC) void lenet_fc_eval(
+    const bf16* __restrict__ act2, const int* __restrict__ labels, int nb,
+    const bf16* __restrict__ pk, const float* __restrict__ params, float* __restrict__ part)
 {
-  conv_fwd_body<false>(blockIdx.x, images, sample_base, nb, pk, params, seed, round_ctr, augment, act2, act2T, tstride,
-                pool1_out, am1_out, am2_out, zero_stats, nullptr, 0);
-}
-
-// ---------------------------------------------------------------------------
-// K2a: fc1 forward, tiled over (16-sample row tile) x (16-output column tile)
-// so the 106 KB fc1 weight image is streamed by 8 column workgroups instead of
-// every row-group workgroup (per-CU bandwidth, not FLOPs, bounds this GEMM).
-// 4 waves split K = 416 (13 steps) and combine through LDS.
-//   H1[s][n] = relu(X[s] . W1[n] + b1[n])   -> global bf16 [rows][128]
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void lenet_fc1_fwd(
-    const bf16* __restrict__ act2,   // [nb][F0P]
-    int nb, const bf16* __restrict__ pk, const float* __restrict__ params,
-    bf16* __restrict__ h1)           // [nb rounded to 16][128]
-{
-  __shared__ float red[4][16][17];
-  const int lane = lane_id(), wave = threadIdx.x >> 6;
-  const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
-  const int nt = blockIdx.x & 7, mt = blockIdx.x >> 3;
-  const int row = mt * 16 + n16;
-  const bool valid = row < nb;
-  const bf16* xa = act2 + (size_t)(valid ? row : 0) * F0P + kq;
-  const bf16* wb = pk + PK_FC1 + (nt * 16 + n16) * F0P + kq;
-  bf16x8 a[4], b[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {                 // k-steps wave, wave+4, wave+8, wave+12 (<13)
-    const int ks = min(wave + 4 * j, 12);
-    a[j] = ld8(xa + ks * 32);
-    b[j] = ld8(wb + ks * 32);
-  }
-  const int n = nt * 16 + (threadIdx.x & 15);
-  const float bias = params[P_F1B + min(n, F1 - 1)];
-  if (!valid) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = zero8();
-  }
-  f32x4 acc = zero4();
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (wave + 4 * j < 13) acc = mfma16(a[j], b[j], acc);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) red[wave][rq + r][n16] = acc[r];
-  __syncthreads();
-  const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
-  const int srow = mt * 16 + r;
-  if (srow < nb) {
-    const float v = red[0][r][c] + red[1][r][c] + red[2][r][c] + red[3][r][c] + bias;
-    h1[(size_t)srow * 128 + n] = (bf16)((n < F1) ? fmaxf(v, 0.f) : 0.f);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// K2b: FC tail, 16 samples per row group, 8 waves; in training each row group
-// is split over 4 workgroups that each produce a quarter of dX = dZ1 . W1
-// (the 100 KB fc1^T image is streamed 4-way in parallel).  The cheap middle of
-// the head (fc2, fc3, CE, fc3/fc2 backward, dZ1) is recomputed by the 4
-// workgroups; only quarter 0 publishes stats, slabs and dZ1^T.
-//   fwd: H2 = relu(H1 W2^T + b2), Z = H2 W3^T + b3; CE + accuracy counters
-//   bwd: dW3/db3, dZ2, dW2/db2, dZ1 (+db1) -> dZ1^T (global), dX (masked by the
-//        pool2 ReLU) -> d(pool2) for K3.
-// Every global operand is prefetched into registers at entry.
-// ---------------------------------------------------------------------------
-// FUSE_FC1: the tail computes H1 = relu(X W1^T + b1) for its 16 samples itself
-// (act2 tile -> LDS, this wave's 16 W1 rows -> 13 register fragments at entry)
-// instead of reading K2a's output: one launch and one H1 round trip fewer.
-// WAIT (fused fwd+head launch): the weight prefetch runs while the same launch's conv
-// workgroups are still computing; act2 is read only after its 16 samples' flags show 'gen'.
-template <bool FUSE_FC1, bool WAIT>
-FEDMI_DEV void fc_tail_body(
-    int bid,
-    const bf16* __restrict__ h1,     // [nb][128]  relu(fc1) from K2a (unused with FUSE_FC1)
-    const bf16* __restrict__ act2,   // [nb][F0P]  (for the dX mask)
-    const int* __restrict__ labels,  // labels of this batch (already offset)
-    int nb, int train,
-    const bf16* __restrict__ pk, const float* __restrict__ params,
-    float* __restrict__ dact2,       // [128][F0]       (train)
-    bf16* __restrict__ dZ1T,         // [128][DZ1_LD]   (train)
-    float* __restrict__ fc_slab,     // [row groups][FS] (train)
-    Stats* __restrict__ stats,
-    const int* __restrict__ done_flags, int gen)
-{
-  __shared__ __attribute__((aligned(16))) bf16 sH1[16 * 128], sH1T[128 * 32];
-  __shared__ __attribute__((aligned(16))) bf16 sH2[16 * 96], sH2T[96 * 32];
-  __shared__ __attribute__((aligned(16))) bf16 sdZ3[16 * 32], sdZ3T[16 * 32];
-  __shared__ __attribute__((aligned(16))) bf16 sdZ2[16 * 96], sdZ2T[96 * 32];
-  __shared__ __attribute__((aligned(16))) bf16 sdZ1[16 * 128];
-  __shared__ float sZ[16 * 16];
-  __shared__ float sdb[128 + 96 + 16];
   constexpr int SX_LD = F0P + 8;                   // act2 tile row stride (bank spread)
-  __shared__ __attribute__((aligned(16))) bf16 sX[FUSE_FC1 ? 16 * SX_LD : 8];
-
+  constexpr int XCH = F0P / 8;                     // 52 16-B chunks per act2 row
+  __shared__ __attribute__((aligned(16))) bf16 sX[16 * SX_LD];
+  __shared__ __attribute__((aligned(16))) bf16 sH1[16 * 128];
+  __shared__ __attribute__((aligned(16))) bf16 sH2[16 * 96];
+  __shared__ float sZ[16 * 16];
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
   const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
-  const int nq = train ? 4 : 1;
-  const int mt = bid / nq, q = bid - mt * nq;
-  [[maybe_unused]] const int stamp_wg = bid;
-  const int s0 = mt * FC_SPW;
+  const int mt = blockIdx.x, s0 = mt * FC_SPW;
   const int ns = min(FC_SPW, nb - s0);
   if (ns <= 0) return;
-  const bool lead = q == 0;                        // publishes stats, slabs and dZ1^T
-  FEDMI_STAMP(1, 0);
 
-  // ---- prefetch: H1 tile (or act2 tile + W1 fragments), fc2/fc3 weights + biases,
-  //      backward weights, dX tile + mask
-  uint4 h1v = make_uint4(0, 0, 0, 0);
-  constexpr int XCH = F0P / 8;                     // 52 16-B chunks per act2 row
-  uint4 xv[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-  bf16x8 w1f[FUSE_FC1 ? 13 : 1];
+  // every global read of the kernel in one wave of requests: W1 / W2 / W3 fragments, biases, act2 tile
   const int nf1 = wave * 16 + n16;
-  float b1 = 0.f;
-  if constexpr (FUSE_FC1) {
+  bf16x8 w1f[13];
 #pragma unroll
-    for (int ks = 0; ks < 13; ++ks) w1f[ks] = ld8(pk + PK_FC1 + nf1 * F0P + ks * 32 + kq);
-    b1 = params[P_F1B + min(nf1, F1 - 1)];
-  } else if (tid < 16 * 128 / 8) {
-    const int r = tid >> 4;
-    h1v = reinterpret_cast<const uint4*>(h1 + (size_t)(s0 + min(r, ns - 1)) * 128)[tid & 15];
-    if (r >= ns) h1v = make_uint4(0, 0, 0, 0);
-  }
+  for (int ks = 0; ks < 13; ++ks) w1f[ks] = ld8(pk + PK_FC1 + nf1 * F0P + ks * 32 + kq);
+  const float b1 = params[P_F1B + min(nf1, F1 - 1)];
   const int nf2 = (wave < 6 ? wave : 0) * 16 + n16;
   const float b2 = params[P_F2B + min(nf2, F2 - 1)];
   const float b3 = params[P_F3B + min(n16, NCLS - 1)];
-  // each wave loads only the fragments it uses (the prefetch is bandwidth-per-CU bound:
-  // 8 waves loading fc3's image for wave 0 alone cost ~0.4 us per step)
   bf16x8 w2f[4], w3f[3];
   if (wave < 6) {
 #pragma unroll
@@ -463,88 +306,28 @@ FEDMI_DEV void fc_tail_body(
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks) w3f[ks] = ld8(pk + PK_FC3 + n16 * 96 + ks * 32 + kq);
   }
-  const int q5 = wave >= 6 ? wave : wave + 8;      // this wave's dH2 task (valid if < 12)
-  // dX tiles of this quarter: 25 tiles split 7/6/6/6
-  const int t0 = q == 0 ? 0 : 7 + 6 * (q - 1), t1 = q == 0 ? 7 : t0 + 6;
-  const int tx = t0 + wave;                        // this wave's dX tile (valid if < t1)
-  const int fx = min(tx, F0 / 16 - 1) * 16 + n16;
-  bf16x8 w3t, w2t[3], wxt[4];
-  float xm[4];
-  if (train) {
-    if (q5 < 12) w3t = ld8(pk + PK_FC3T + ((q5 - 6) * 16 + n16) * 32 + kq);
+  uint4 xv[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
 #pragma unroll
-    for (int ks = 0; ks < 3; ++ks) w2t[ks] = ld8(pk + PK_FC2T + nf1 * 96 + ks * 32 + kq);
-    if (tx < t1) {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) wxt[ks] = ld8(pk + PK_FC1T + fx * 128 + ks * 32 + kq);
+  for (int u = 0; u < 2; ++u) {
+    const int e = tid + u * NT_FC;
+    if (e < 16 * XCH) {
+      const int r = e / XCH;
+      xv[u] = reinterpret_cast<const uint4*>(act2 + (size_t)(s0 + min(r, ns - 1)) * F0P)[e - r * XCH];
+      if (r >= ns) xv[u] = make_uint4(0, 0, 0, 0);
     }
   }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = tid + u * NT_FC;
+    if (e < 16 * XCH) {
+      const int r = e / XCH;
+      *reinterpret_cast<uint4*>(sX + r * SX_LD + (e - r * XCH) * 8) = xv[u];
+    }
+  }
+  __syncthreads();
 
-  zero_lds(sH1T, sizeof(sH1T));
-  zero_lds(sH2T, sizeof(sH2T));
-  zero_lds(sdZ3, sizeof(sdZ3));
-  zero_lds(sdZ3T, sizeof(sdZ3T));
-  zero_lds(sdZ2T, sizeof(sdZ2T));
-  for (int e = tid; e < 240; e += NT_FC) sdb[e] = 0.f;
-  // ---- act2-dependent loads: the act2 tile (fc1 input; in LDS it also gives the dX mask)
-  if constexpr (WAIT) {
-    // consumer side of K12's hand-off: sc1 poll, then ONLY sc1 loads of the act2 rows
-    if (tid < 64) {
-      if (tid < ns) {
-        const unsigned long long t0 = wall_clock64();
-        while (__hip_atomic_load(done_flags + s0 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen) {
-          __builtin_amdgcn_s_sleep(1);
-          if (wall_clock64() - t0 > 100000000ull) {      // 1 s: never hang the GPU on a broken hand-off
-            __hip_atomic_store(&stats->pad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-      }
-    }
-    __syncthreads();
-    FEDMI_STAMP(1, 7);
-    constexpr int XQ = F0P / 4;                  // 104 8-byte words per act2 row
-    for (int e = tid; e < 16 * XQ; e += NT_FC) {
-      const int r = e / XQ, c = e - r * XQ;
-      uint64_t v = 0;
-      if (r < ns)
-        v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(act2 + (size_t)(s0 + r) * F0P) + c, __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-      *reinterpret_cast<uint64_t*>(sX + r * SX_LD + c * 4) = v;
-    }
-    __syncthreads();
-  } else if constexpr (FUSE_FC1) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + u * NT_FC;
-      if (e < 16 * XCH) {
-        const int r = e / XCH;
-        xv[u] = reinterpret_cast<const uint4*>(act2 + (size_t)(s0 + min(r, ns - 1)) * F0P)[e - r * XCH];
-        if (r >= ns) xv[u] = make_uint4(0, 0, 0, 0);
-      }
-    }
-  }
-  if (!FUSE_FC1 && train && tx < t1) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) xm[r] = (float)act2[(size_t)(s0 + min(rq + r, ns - 1)) * F0P + fx];
-  }
-  if constexpr (FUSE_FC1) {
-    if constexpr (!WAIT) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int e = tid + u * NT_FC;
-        if (e < 16 * XCH) {
-          const int r = e / XCH;
-          *reinterpret_cast<uint4*>(sX + r * SX_LD + (e - r * XCH) * 8) = xv[u];
-        }
-      }
-      __syncthreads();
-    }
-    if (train && tx < t1) {                      // pool2-ReLU mask of dX from the LDS tile
-#pragma unroll
-      for (int r = 0; r < 4; ++r) xm[r] = (float)sX[(rq + r) * SX_LD + fx];
-    }
-    // fc1 fwd: wave -> 16 output columns, K = 416 (13 steps)
+  // ---- fc1: wave -> 16 output columns, K = 416 (13 steps)
+  {
     const bf16* xa = sX + n16 * SX_LD + kq;
     f32x4 acc = zero4();
 #pragma unroll
@@ -554,17 +337,9 @@ FEDMI_DEV void fc_tail_body(
       const int sr = rq + r;
       sH1[sr * 128 + nf1] = (bf16)((nf1 < F1 && sr < ns) ? fmaxf(acc[r] + b1, 0.f) : 0.f);
     }
-  } else {
-    if (tid < 16 * 128 / 8) reinterpret_cast<uint4*>(sH1)[tid] = h1v;
   }
   __syncthreads();
-  for (int e = tid; e < 16 * 128; e += NT_FC) {       // sample-contiguous copy for the dW2 GEMM
-    const int r = e >> 7, c = e & 127;
-    sH1T[c * 32 + r] = sH1[e];
-  }
-  FEDMI_STAMP(1, 1);
-
-  // ---- fc2 fwd: waves 0..5 -> 16 outputs each; K = 128 (4 steps)
+  // ---- fc2: waves 0..5 -> 16 outputs each; K = 128 (4 steps)
   if (wave < 6) {
     const bf16* ha = sH1 + n16 * 128 + kq;
     f32x4 acc = zero4();
@@ -573,14 +348,11 @@ FEDMI_DEV void fc_tail_body(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int sr = rq + r;
-      const float hv = (nf2 < F2 && sr < ns) ? fmaxf(acc[r] + b2, 0.f) : 0.f;
-      sH2[sr * 96 + nf2] = (bf16)hv;
-      sH2T[nf2 * 32 + sr] = (bf16)hv;
+      sH2[sr * 96 + nf2] = (bf16)((nf2 < F2 && sr < ns) ? fmaxf(acc[r] + b2, 0.f) : 0.f);
     }
   }
   __syncthreads();
-
-  // ---- fc3 fwd: logits [16 x 16]; K = 96 (3 steps)
+  // ---- fc3: logits [16 x 16]; K = 96 (3 steps)
   if (wave == 0) {
     const bf16* ha = sH2 + n16 * 96 + kq;
     f32x4 acc = zero4();
@@ -590,225 +362,39 @@ FEDMI_DEV void fc_tail_body(
     for (int r = 0; r < 4; ++r) sZ[(rq + r) * 16 + n16] = acc[r] + b3;
   }
   __syncthreads();
-  FEDMI_STAMP(1, 2);
-
-  // ---- cross-entropy (mean over the batch nb), accuracy, dZ3
+  // ---- cross-entropy + accuracy of the row group (lane = sample)
   if (wave == 0) {
     float loss = 0.f, corr = 0.f;
-    if (lane < 16) {
-      const int sr = lane;
-      float dz[NCLS];
-      if (sr < ns) {
-        float z[NCLS];
+    if (lane < ns) {
+      float z[NCLS];
 #pragma unroll
-        for (int n = 0; n < NCLS; ++n) z[n] = sZ[sr * 16 + n];
-        float mx = z[0]; int am = 0;
+      for (int n = 0; n < NCLS; ++n) z[n] = sZ[lane * 16 + n];
+      float mx = z[0]; int am = 0;
 #pragma unroll
-        for (int n = 1; n < NCLS; ++n) if (z[n] > mx) { mx = z[n]; am = n; }
-        float se = 0.f;
+      for (int n = 1; n < NCLS; ++n) if (z[n] > mx) { mx = z[n]; am = n; }
+      float se = 0.f;
 #pragma unroll
-        for (int n = 0; n < NCLS; ++n) se += __expf(z[n] - mx);
-        const float lse = mx + __logf(se);
-        const int y = labels[s0 + sr];
-        float zy = 0.f;
+      for (int n = 0; n < NCLS; ++n) se += __expf(z[n] - mx);
+      const int y = labels[s0 + lane];
+      float zy = 0.f;
 #pragma unroll
-        for (int n = 0; n < NCLS; ++n) zy = (n == y) ? z[n] : zy;
-        loss = lse - zy;
-        corr = (am == y) ? 1.f : 0.f;
-        const float inv = 1.f / (float)nb;
-#pragma unroll
-        for (int n = 0; n < NCLS; ++n) dz[n] = (__expf(z[n] - lse) - (n == y ? 1.f : 0.f)) * inv;
-      } else {
-#pragma unroll
-        for (int n = 0; n < NCLS; ++n) dz[n] = 0.f;
-      }
-      if (train) {   // sdZ3 / sdZ3T were zeroed at entry: write the 10 live entries only
-#pragma unroll
-        for (int n = 0; n < NCLS; ++n) {
-          const bf16 v = (bf16)dz[n];
-          sdZ3[sr * 32 + n] = v;
-          sdZ3T[n * 32 + sr] = v;
-          sZ[sr * 16 + n] = dz[n];   // fp32 dZ3 for db3
-        }
-      }
+      for (int n = 0; n < NCLS; ++n) zy = (n == y) ? z[n] : zy;
+      loss = mx + __logf(se) - zy;
+      corr = (am == y) ? 1.f : 0.f;
     }
     loss = wave_sum(loss);
     corr = wave_sum(corr);
-    if (lane == 0 && lead) {
-      atomicAdd(&stats->loss_sum, loss);
-      atomicAdd(&stats->correct, (int)(corr + 0.5f));
-      atomicAdd(&stats->count, ns);
+    if (lane == 0) {
+      part[2 * mt] = loss;
+      part[2 * mt + 1] = corr;
     }
   }
-  if (!train) return;
-  __syncthreads();
-  FEDMI_STAMP(1, 3);
-
-  float* slab = fc_slab + (size_t)mt * FS;
-  constexpr int OF3W = P_F3W - P_F1B, OF2W = P_F2W - P_F1B;
-
-  if (tid < NCLS && lead) {   // db3
-    float acc = 0.f;
-    for (int sr = 0; sr < 16; ++sr) acc += sZ[sr * 16 + tid];
-    sdb[224 + tid] = acc;
-  }
-
-  // ---- dW3 (tasks 0..5, lead only) and dH2 = dZ3 . W3 (tasks 6..11)
-  for (int qq = wave; qq < 12; qq += NW_FC) {
-    if (qq < 6) {
-      if (!lead) continue;
-      const int ft = qq;
-      const f32x4 acc = mfma16(ld8(sdZ3T + n16 * 32 + kq), ld8(sH2T + (ft * 16 + n16) * 32 + kq), zero4());
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = rq + r, f = ft * 16 + n16;
-        if (n < NCLS && f < F2) slab[OF3W + n * F2 + f] = acc[r];
-      }
-    } else {
-      const int f = (qq - 6) * 16 + n16;
-      const f32x4 acc = mfma16(ld8(sdZ3 + n16 * 32 + kq), w3t, zero4());
-      float colsum = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int sr = rq + r;
-        const float g = (f < F2 && (float)sH2[sr * 96 + f] > 0.f) ? acc[r] : 0.f;
-        sdZ2[sr * 96 + f] = (bf16)g;
-        sdZ2T[f * 32 + sr] = (bf16)g;
-        colsum += g;
-      }
-      colsum += __shfl_xor(colsum, 16, 64);
-      colsum += __shfl_xor(colsum, 32, 64);
-      if (lane < 16 && f < F2) atomicAdd(&sdb[128 + f], colsum);
-    }
-  }
-  __syncthreads();
-  FEDMI_STAMP(1, 4);
-
-  // ---- dW2 = dZ2^T H1 (48 tiles, lead only) and dH1 = dZ2 . W2 (tile = wave) -> dZ1
-  if (lead) {
-    for (int qq = wave; qq < 48; qq += NW_FC) {
-      const int mt2 = qq >> 3, ft = qq & 7;
-      const f32x4 acc = mfma16(ld8(sdZ2T + (mt2 * 16 + n16) * 32 + kq), ld8(sH1T + (ft * 16 + n16) * 32 + kq), zero4());
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = mt2 * 16 + rq + r, f = ft * 16 + n16;
-        if (n < F2 && f < F1) slab[OF2W + n * F1 + f] = acc[r];
-      }
-    }
-  }
-  {
-    const int f = nf1;
-    const bf16* za = sdZ2 + n16 * 96 + kq;
-    f32x4 acc = zero4();
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks) acc = mfma16(ld8(za + ks * 32), w2t[ks], acc);
-    float colsum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int sr = rq + r;
-      const float g = (f < F1 && (float)sH1[sr * 128 + f] > 0.f) ? acc[r] : 0.f;
-      const bf16 gb = (bf16)g;
-      sdZ1[sr * 128 + f] = gb;
-      if (lead) dZ1T[(size_t)f * DZ1_LD + s0 + sr] = gb;
-      colsum += g;
-    }
-    colsum += __shfl_xor(colsum, 16, 64);
-    colsum += __shfl_xor(colsum, 32, 64);
-    if (lane < 16 && f < F1) atomicAdd(&sdb[f], colsum);
-  }
-  __syncthreads();
-  FEDMI_STAMP(1, 5);
-
-  // ---- dX = dZ1 . W1 for this quarter's tiles (K = 128), masked by the pool2 ReLU
-  if (tx < t1) {
-    const bf16* za = sdZ1 + n16 * 128 + kq;
-    f32x4 acc = zero4();
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) acc = mfma16(ld8(za + ks * 32), wxt[ks], acc);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int sr = rq + r;
-      if (sr < ns) dact2[(size_t)(s0 + sr) * F0 + fx] = xm[r] > 0.f ? acc[r] : 0.f;
-    }
-  }
-  if (lead) {
-    for (int e = tid; e < F1; e += NT_FC) slab[e] = sdb[e];                       // fc1.bias
-    for (int e = tid; e < F2; e += NT_FC) slab[P_F2B - P_F1B + e] = sdb[128 + e];
-    if (tid < NCLS) slab[P_F3B - P_F1B + tid] = sdb[224 + tid];
-    // the last row group zeroes dZ1T columns [nb, 128): K-padding of the fc1 wgrad
-    if (s0 + FC_SPW >= nb) {
-      const int pad = DZ1_LD - nb;
-      for (int e = tid; e < 128 * pad; e += NT_FC) {
-        const int f = e / pad, c = nb + (e - f * pad);
-        dZ1T[(size_t)f * DZ1_LD + c] = (bf16)0.f;
-      }
-    }
-  }
-  FEDMI_STAMP(1, 6);
-}
-
-template <bool FUSE_FC1>
-__global__ __launch_bounds__(NT_FC) void lenet_fc_tail(
-    const bf16* __restrict__ h1, const bf16* __restrict__ act2, const int* __restrict__ labels, int nb, int train,
-    const bf16* __restrict__ pk, const float* __restrict__ params, float* __restrict__ dact2,
-    bf16* __restrict__ dZ1T, float* __restrict__ fc_slab, Stats* __restrict__ stats)
-{
-  fc_tail_body<FUSE_FC1, false>(blockIdx.x, h1, act2, labels, nb, train, pk, params, dact2, dZ1T, fc_slab, stats,
-                                nullptr, 0);
 }
 
 // ---------------------------------------------------------------------------
-// K12: K1 + K2b in ONE launch (training).  Workgroups [0, nb) run the conv stack
-// of one sample each and publish it; workgroups [nb, nb + 4*rowgroups) are the FC
-// head: they stream their weight fragments from HBM WHILE the conv workgroups
-// compute, then wait for their 16 samples' flags.  Removes a kernel boundary and
-// takes the FC head's ~5 us weight prefetch off the critical path.  The conv
-// workgroups are dispatched first, so the waiting FC workgroups can never block
-// them (and the wait is wall-clock bounded).  Flags hold a step generation read
-// from 'step_gen' (bumped by K4 every step): no reset between steps.
+// The conv stack backward of one sample (KS1's second half): maxpool/ReLU backward by argmax,
+// conv2 wgrad + dgrad, conv1 wgrad, all operands in LDS.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT_FWD) void lenet_fwd_head(
-    const uint8_t* __restrict__ images, int sample_base, int nb, const bf16* __restrict__ pk,
-    const float* __restrict__ params, uint32_t seed, const int* __restrict__ round_ctr, int augment,
-    bf16* __restrict__ act2, bf16* __restrict__ act2T, bf16* __restrict__ pool1_out,
-    uint8_t* __restrict__ am1_out, uint8_t* __restrict__ am2_out, const int* __restrict__ labels,
-    float* __restrict__ dact2, bf16* __restrict__ dZ1T, float* __restrict__ fc_slab, Stats* __restrict__ stats,
-    int* __restrict__ done_flags, const int* __restrict__ step_gen, int* __restrict__ bwd_gen)
-{
-  static_assert(NT_FWD == NT_FC, "one launch hosts both roles");
-  const int gen = step_gen[0] + 1;
-  if (bwd_gen && blockIdx.x == 0 && threadIdx.x == 0) bwd_gen[0] += 1;   // K34's flag generation (read only by K34)
-  if ((int)blockIdx.x < nb) {
-    conv_fwd_body<true>(blockIdx.x, images, sample_base, nb, pk, params, seed, round_ctr, augment, act2, act2T,
-                  MAX_TRAIN_BATCH, pool1_out, am1_out, am2_out, nullptr, done_flags, gen);
-    return;
-  }
-  fc_tail_body<true, true>(blockIdx.x - nb, nullptr, act2, labels, nb, 1, pk, params, dact2, dZ1T, fc_slab, stats,
-                           done_flags, gen);
-}
-// ---------------------------------------------------------------------------
-// K3: conv stack backward (one workgroup per sample) + fc1 wgrad workgroups.
-// All per-sample inputs and the conv2 dgrad weights are staged into LDS with
-// 16-byte loads at entry; every MFMA operand afterwards is an LDS read.
-// ---------------------------------------------------------------------------
-// PUB (K34, the fused backward + SGD launch): gradient stores go out write-through
-// (sc1) and each producer workgroup then raises its flag -- the SGD workgroups of
-// the same launch consume them with sc1 loads (the K12 hand-off recipe).
-template <bool PUB>
-FEDMI_DEV void put_grad(float* p, float v) {
-  if constexpr (PUB) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-
-template <bool PUB>
-FEDMI_DEV void publish_flag(int* flags, int idx, int gen) {
-  if constexpr (PUB) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(flags + idx, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // Operand images are padded so the 16 lanes of an MFMA fragment read land on
 // distinct 16-byte bank groups (strides in 16-B units: coprime with 16 or
 // chosen so the (c, r, s) im2col column index maps to distinct groups).
@@ -824,10 +410,9 @@ constexpr int BW_WDGS = KDGP + 8;              // conv2 dgrad weight row stride 
 // bytes of the backward's scratch region (shifted copies, out-grads, wgrad partials, bias sums)
 constexpr int BW_O_XSH = 0, BW_O_P1SH = BW_O_XSH + BW_XSH * 2, BW_O_DY2W = BW_O_P1SH + BW_P1SH * 2,
               BW_O_DY2C = BW_O_DY2W + BW_DY2W * 2, BW_O_DY1 = BW_O_DY2C + BW_DY2C * 2,
-              BW_O_DW1 = BW_O_DY1 + BW_DY1 * 2, BW_O_DB = BW_O_DW1 + 3 * 6 * 80 * 4, BW_SCRATCH = BW_O_DB + 32 * 4;
+              BW_O_DW1 = BW_O_DY1 + BW_DY1 * 2, BW_O_DB = BW_O_DW1 + 3 * 6 * 80 * 4, BW_SCRATCH = BW_O_DB + 64 * 4;
 
-// LDS operands of one sample's conv backward (K3 stages them from global memory; the
-// per-sample step kernel KS1 still holds them from its own forward).
+// LDS operands of one sample's conv backward (KS1 still holds them from its own forward).
 struct BwdLds {
   const uint8_t* raw;     // uint8 CHW image
   const bf16* p1r;        // pool1 output, CHW [NP1]
@@ -859,7 +444,7 @@ FEDMI_DEV void bwd_zero(const BwdLds& L) {
   zero_lds(L.dY1, BW_DY1 * 2);
   zero_lds(L.xsh, BW_XSH * 2);
   zero_lds(L.p1sh, BW_P1SH * 2);
-  if (threadIdx.x < 32) L.db[threadIdx.x] = 0.f;
+  if (threadIdx.x < 64) L.db[threadIdx.x] = 0.f;
 }
 
 // each augmented pixel / pooled value is computed once and stored into its 5
@@ -890,10 +475,9 @@ FEDMI_DEV void bwd_build_shifted(const BwdLds& L, const Aug& a) {
 }
 
 // d(pool2) -> conv2 out-grad images + conv2 bias sums, then conv2 wgrad + dgrad, conv1 wgrad,
-// and the sample's gradient slab.  Stamps slots 2..5 of kernel 'sk'.
-template <bool PUB>
-FEDMI_DEV void bwd_main(const BwdLds& L, float* __restrict__ slab, int* __restrict__ flags, int s, int gen,
-                        int sk, int stamp_wg) {
+// and the sample's gradient slab.  Stamps slots 2..5 of kernel 'sk'.  db: [0, 16) conv2 bias,
+// [16, 58) conv1 bias partials of the 7 dgrad waves (combined in wave order: no LDS float atomics).
+FEDMI_DEV void bwd_main(const BwdLds& L, float* __restrict__ slab, int sk, int stamp_wg) {
   (void)sk; (void)stamp_wg;
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
   const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
@@ -936,7 +520,7 @@ FEDMI_DEV void bwd_main(const BwdLds& L, float* __restrict__ slab, int* __restri
     }
     if (kk < 150) {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) put_grad<PUB>(slab + P_C2W + (rq + rr) * 150 + kk, acc[rr]);
+      for (int rr = 0; rr < 4; ++rr) slab[P_C2W + (rq + rr) * 150 + kk] = acc[rr];
     }
   }
 
@@ -964,9 +548,9 @@ FEDMI_DEV void bwd_main(const BwdLds& L, float* __restrict__ slab, int* __restri
       acc[0] = mfma16(ld8(ga + koff[ks]), w, acc[0]);
       acc[1] = mfma16(ld8(gbb + koff[ks]), w, acc[1]);
     }
+    float csum = 0.f;
     if (n16 < C1) {
       const int c = n16;
-      float csum = 0.f;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int t = h ? tb : ta;
@@ -984,8 +568,11 @@ FEDMI_DEV void bwd_main(const BwdLds& L, float* __restrict__ slab, int* __restri
           }
         }
       }
-      atomicAdd(&db[16 + c], csum);
     }
+    // the 4 lane groups (rq) of a channel in a fixed xor order, then one write per (wave, channel)
+    csum += __shfl_xor(csum, 16, 64);
+    csum += __shfl_xor(csum, 32, 64);
+    if (n16 < C1 && lane < 16) db[16 + wave * C1 + n16] = csum;
   }
   __syncthreads();
   FEDMI_STAMP(sk, 3);
@@ -1026,115 +613,18 @@ FEDMI_DEV void bwd_main(const BwdLds& L, float* __restrict__ slab, int* __restri
   FEDMI_STAMP(sk, 4);
   for (int e = tid; e < C1 * 75; e += NT_CONV) {
     const int o = e / 75, kk = e - o * 75;
-    put_grad<PUB>(slab + P_C1W + e, L.w1part[o * 80 + kk] + L.w1part[(6 + o) * 80 + kk] + L.w1part[(12 + o) * 80 + kk]);
+    slab[P_C1W + e] = L.w1part[o * 80 + kk] + L.w1part[(6 + o) * 80 + kk] + L.w1part[(12 + o) * 80 + kk];
   }
-  if (tid < C1) put_grad<PUB>(slab + P_C1B + tid, db[16 + tid]);
-  if (tid < C2) put_grad<PUB>(slab + P_C2B + tid, db[tid]);
-  publish_flag<PUB>(flags, s, gen);
+  if (tid < C1) {
+    float b = 0.f;
+#pragma unroll
+    for (int w = 0; w < 7; ++w) b += db[16 + w * C1 + tid];
+    slab[P_C1B + tid] = b;
+  }
+  if (tid < C2) slab[P_C2B + tid] = db[tid];
   FEDMI_STAMP(sk, 5);
 }
 
-template <bool PUB>
-FEDMI_DEV void conv_bwd_body(
-    int blk, const uint8_t* __restrict__ images, int sample_base, int nb,
-    uint32_t seed, const int* __restrict__ round_ctr, int augment,
-    const float* __restrict__ dact2,       // [nb][F0]   d(pool2), ReLU-masked
-    const bf16* __restrict__ act2T,        // [F0P][128]
-    const bf16* __restrict__ dZ1T,         // [128][128]
-    const bf16* __restrict__ pool1,        // [nb][NP1]
-    const uint8_t* __restrict__ am1,       // [nb][NP1]
-    const uint8_t* __restrict__ am2,       // [nb][F0]
-    const bf16* __restrict__ pk,
-    float* __restrict__ conv_slab,         // [nb][CS]
-    float* __restrict__ fc1w_grad,         // [F1W_N]
-    int* __restrict__ flags, int gen)      // PUB: producer flags [nb + N_DW1_WG]
-{
-  constexpr int O_RAW = 0, O_P1R = 3072, O_AM1 = O_P1R + 2368, O_AM2 = O_AM1 + 1184, O_DX = O_AM2 + 416,
-                O_WDG = O_DX + F0 * 4, O_SCR = O_WDG + 16 * BW_WDGS * 2, O_END = O_SCR + BW_SCRATCH;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[O_END];
-
-  const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
-  const int kq = (lane >> 4) * 8, n16 = lane & 15, rq = (lane >> 4) * 4;
-
-  if (blk >= nb) {
-    // ---- fc1.weight grad: dW1[n][f] = sum_s dZ1[s][n] X[s][f], f in [16e, 16e+16)
-    const int e = blk - nb;
-    if (e >= N_DW1_WG) return;
-    if (wave < 8) {                              // 8 row tiles of 16 outputs
-    const bf16* ap = dZ1T + (wave * 16 + n16) * DZ1_LD + kq;
-    const bf16* bp = act2T + (size_t)(e * 16 + n16) * MAX_TRAIN_BATCH + kq;
-    bf16x8 a[4], b[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {   // always load all 4 k-steps (columns >= nb of dZ1T are zero)
-      a[ks] = ld8(ap + ks * 32);
-      b[ks] = ld8(bp + ks * 32);
-    }
-    f32x4 acc = zero4();
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) acc = mfma16(a[ks], b[ks], acc);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = wave * 16 + rq + r;
-      if (n < F1) put_grad<PUB>(fc1w_grad + n * F0 + e * 16 + n16, acc[r]);
-    }
-    }
-    publish_flag<PUB>(flags, blk, gen);
-    return;
-  }
-
-  uint8_t* raw = smem + O_RAW;
-  bf16* p1r = reinterpret_cast<bf16*>(smem + O_P1R);
-  uint8_t* am1s = smem + O_AM1;
-  uint8_t* am2s = smem + O_AM2;
-  float* dxs = reinterpret_cast<float*>(smem + O_DX);
-  bf16* wdg = reinterpret_cast<bf16*>(smem + O_WDG);
-  const BwdLds L = bwd_lds(smem + O_SCR, raw, p1r, am1s, am2s, dxs, wdg);
-
-  const int s = blk;
-  [[maybe_unused]] const int stamp_wg = s;
-  const int gidx = sample_base + s;
-  FEDMI_STAMP(2, 0);
-
-  // ---- stage everything this sample needs (16-B loads; 8-B for the argmax row)
-  {
-    constexpr int N_RAW = IMG_BYTES / 16, N_P1 = NP1 * 2 / 16, N_AM1 = NP1 / 8, N_AM2 = F0 / 16,
-                  N_DX = F0 * 4 / 16, N_WDG = 16 * KDGP * 2 / 16;
-    constexpr int E1 = N_RAW, E2 = E1 + N_P1, E3 = E2 + N_AM1, E4 = E3 + N_AM2, E5 = E4 + N_DX, E6 = E5 + N_WDG;
-    const uint4* img4 = reinterpret_cast<const uint4*>(images + (size_t)gidx * IMG_BYTES);
-    const uint4* p14 = reinterpret_cast<const uint4*>(pool1 + (size_t)s * NP1);
-    const uint2* am12 = reinterpret_cast<const uint2*>(am1 + (size_t)s * NP1);
-    const uint4* am24 = reinterpret_cast<const uint4*>(am2 + (size_t)s * F0);
-    const uint4* dx4 = reinterpret_cast<const uint4*>(dact2 + (size_t)s * F0);
-    const uint4* wdg4 = reinterpret_cast<const uint4*>(pk + PK_W2DG);
-    for (int e = tid; e < E6; e += NT_CONV) {
-      if (e < E1) reinterpret_cast<uint4*>(raw)[e] = img4[e];
-      else if (e < E2) reinterpret_cast<uint4*>(p1r)[e - E1] = p14[e - E1];
-      else if (e < E3) reinterpret_cast<uint2*>(am1s)[e - E2] = am12[e - E2];
-      else if (e < E4) reinterpret_cast<uint4*>(am2s)[e - E3] = am24[e - E3];
-      else if (e < E5) reinterpret_cast<uint4*>(dxs)[e - E4] = dx4[e - E4];
-      else {   // padded rows: 52 x 16 B per weight row
-        const int w = e - E5, row = w / (KDGP / 8), col = w - row * (KDGP / 8);
-        reinterpret_cast<uint4*>(wdg + row * BW_WDGS)[col] = wdg4[w];
-      }
-    }
-  }
-  bwd_zero(L);
-  const Aug a = aug_params(augment, seed, round_ctr, gidx);
-  __syncthreads();
-  FEDMI_STAMP(2, 1);
-  bwd_build_shifted(L, a);
-  bwd_main<PUB>(L, conv_slab + (size_t)s * CS, flags, s, gen, 2, stamp_wg);
-}
-
-__global__ __launch_bounds__(NT_CONV) void lenet_conv_bwd(
-    const uint8_t* __restrict__ images, int sample_base, int nb, uint32_t seed, const int* __restrict__ round_ctr,
-    int augment, const float* __restrict__ dact2, const bf16* __restrict__ act2T, const bf16* __restrict__ dZ1T,
-    const bf16* __restrict__ pool1, const uint8_t* __restrict__ am1, const uint8_t* __restrict__ am2,
-    const bf16* __restrict__ pk, float* __restrict__ conv_slab, float* __restrict__ fc1w_grad)
-{
-  conv_bwd_body<false>(blockIdx.x, images, sample_base, nb, seed, round_ctr, augment, dact2, act2T, dZ1T, pool1, am1,
-                       am2, pk, conv_slab, fc1w_grad, nullptr, 0);
-}
 // ---------------------------------------------------------------------------
 // KS1 + KS2: the per-sample training step (the default training path).
 //
@@ -1550,7 +1040,7 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
   }
   __syncthreads();             // d(pool2) from every wave before the conv backward scatters it
   FEDMI_STAMP(0, 6);
-  bwd_main<false>(L, conv_slab + (size_t)s * CS, nullptr, s, 0, 2, stamp_wg);
+  bwd_main(L, conv_slab + (size_t)s * CS, 2, stamp_wg);
 }
 
 // ---------------------------------------------------------------------------
@@ -1590,16 +1080,11 @@ __global__ __launch_bounds__(256) void lenet_pack(const float* __restrict__ para
 }
 
 // ---------------------------------------------------------------------------
-// K4: gradient combine + SGD(momentum, weight decay) + repack.
-// torch.optim.SGD semantics (src/main.py:99-100): d = g + wd*p;
-// buf = m*buf + d (buf starts at 0 == torch's clone on first step); p -= lr*buf
-// Workgroup ranges: [0, NA) conv params: 16 params x 16 slab lanes;
-//                   [NA, NA+NB) fc1.weight: 256 params, complete grads;
-//                   [NA+NB, ..) fc tail: 256 params x <= 8 slabs.
+// SGD(momentum, weight decay) + repack, torch.optim.SGD semantics (src/main.py:99-100):
+// d = g + wd*p; buf = m*buf + d (buf starts at 0 == torch's clone on first step); p -= lr*buf.
+// KS2's conv-parameter blocks: 16 params x 16 slab lanes each.
 // ---------------------------------------------------------------------------
 constexpr int SGD_NA = (CS + 15) / 16;           // 180
-constexpr int SGD_NB = (F1W_N + 255) / 256;      // 188
-constexpr int SGD_NC = (FS + 255) / 256;         // 44
 
 FEDMI_DEV void sgd_apply(int i, float grad, float p, float m, float* __restrict__ params, float* __restrict__ mom,
                          bf16* __restrict__ pk, float lr, float momentum, float wd) {
@@ -1609,68 +1094,6 @@ FEDMI_DEV void sgd_apply(int i, float grad, float p, float m, float* __restrict_
   mom[i] = b;
   params[i] = np;
   pack_one(i, np, pk);
-}
-
-__global__ __launch_bounds__(256) void lenet_sgd(
-    float* __restrict__ params, float* __restrict__ mom, bf16* __restrict__ pk,
-    const float* __restrict__ conv_slab, int n_conv,
-    const float* __restrict__ fc1w_grad,
-    const float* __restrict__ fc_slab, int n_fc,
-    float lr, float momentum, float wd, int* __restrict__ round_ctr, int* __restrict__ step_gen)
-{
-  __shared__ float red[16][17];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  [[maybe_unused]] const int stamp_wg = b;
-  FEDMI_STAMP(3, 0);
-  if (b < SGD_NA) {
-    const int pl = tid & 15, g = tid >> 4;
-    const int i = b * 16 + pl;
-    float p = 0.f, m = 0.f;
-    if (g == 0 && i < CS) { p = params[i]; m = mom[i]; }      // issued before the slab sweep
-    float sum = 0.f;
-    if (i < CS) {
-      float v[MAX_TRAIN_BATCH / 16];             // all 8 slab loads in flight before the first add
-#pragma unroll
-      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) {
-        const int q = g + 16 * u;
-        v[u] = q < n_conv ? conv_slab[(size_t)q * CS + i] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) sum += v[u];
-    }
-    red[g][pl] = sum;
-    __syncthreads();
-    if (g == 0 && i < CS) {
-      float tot = 0.f;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) tot += red[q][pl];
-      sgd_apply(i, tot, p, m, params, mom, pk, lr, momentum, wd);
-    }
-  } else if (b < SGD_NA + SGD_NB) {
-    const int j = (b - SGD_NA) * 256 + tid;
-    if (j < F1W_N) {
-      const int i = P_F1W + j;
-      sgd_apply(i, fc1w_grad[j], params[i], mom[i], params, mom, pk, lr, momentum, wd);
-    }
-  } else {
-    const int j = (b - SGD_NA - SGD_NB) * 256 + tid;
-    if (j < FS) {
-      const int i = P_F1B + j;
-      const float p = params[i], m = mom[i];
-      float v[MAX_FC_WG];
-#pragma unroll
-      for (int q = 0; q < MAX_FC_WG; ++q) v[q] = q < n_fc ? fc_slab[(size_t)q * FS + j] : 0.f;
-      float sum = 0.f;
-#pragma unroll
-      for (int q = 0; q < MAX_FC_WG; ++q) sum += v[q];
-      sgd_apply(i, sum, p, m, params, mom, pk, lr, momentum, wd);
-    }
-  }
-  if (b == 0 && tid == 0) {
-    if (round_ctr) atomicAdd(round_ctr, 1);
-    if (step_gen) step_gen[0] += 1;        // generation of K12's hand-off flags (one writer)
-  }
-  FEDMI_STAMP(3, 1);
 }
 
 // Masks the sample columns >= nb of an operand fragment (8 consecutive samples from s0).
@@ -1720,7 +1143,7 @@ __global__ __launch_bounds__(256) void lenet_sgd2(
     const float* __restrict__ conv_slab, int nb,
     const bf16* __restrict__ act2T, const bf16* __restrict__ h1T, const unsigned char* __restrict__ aux,
     const bf16* __restrict__ dZ1T, float lr, float momentum, float wd,
-    int* __restrict__ round_ctr, int* __restrict__ step_gen, Stats* __restrict__ stats)
+    int* __restrict__ round_ctr, Stats* __restrict__ stats)
 {
   __shared__ float red[16][17];
   const int b = blockIdx.x, tid = threadIdx.x, wave = wave_id(), lane = lane_id();
@@ -1847,123 +1270,8 @@ __global__ __launch_bounds__(256) void lenet_sgd2(
       sgd_apply(bi, sum, bp, bm, params, mom, pk, lr, momentum, wd);
     }
   }
-  if (b == 0 && tid == 0) {
-    if (round_ctr) atomicAdd(round_ctr, 1);
-    if (step_gen) step_gen[0] += 1;
-  }
+  if (b == 0 && tid == 0 && round_ctr) atomicAdd(round_ctr, 1);
   FEDMI_STAMP(3, 1);
-}
-
-// ---------------------------------------------------------------------------
-// K34: conv backward (K3's producers) + SGD in ONE launch.  The producer
-// workgroups (nb per-sample conv workgroups, N_DW1_WG fc1-wgrad workgroups) come
-// first in the grid; the SGD workgroups after them either start at once (FC-tail
-// params: their grads come from K12) or wait on the producers' flags (fc1.weight
-// after the fc1-wgrad workgroups, conv params after every sample) and read the
-// published grads with sc1 loads.  The slab combine has K4's order (bit-identical
-// results).  Flags carry 'bwd_gen' (bumped by K12 every step); K34 bumps K12's
-// 'step_gen' and, on a round's last step, the augmentation counter -- each counter
-// is read only by the OTHER kernel.  Waits are wall-clock bounded (stats->pad = 2).
-// ---------------------------------------------------------------------------
-constexpr int K34_NA = (CS + 63) / 64;                    // 45: 64 conv params x 16 slab lanes
-constexpr int K34_NB = (F1W_N + NT_CONV - 1) / NT_CONV;   // 47: fc1.weight
-constexpr int K34_NC = (FS + NT_CONV - 1) / NT_CONV;      // 11: FC tail
-constexpr int K34_SGD_WG = K34_NA + K34_NB + K34_NC;
-
-FEDMI_DEV void wait_flags(const int* flags, int n, int gen, Stats* stats) {
-  if ((int)threadIdx.x < n) {
-    const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(flags + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen) {
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > 100000000ull) {      // 1 s: never hang the GPU on a broken hand-off
-        __hip_atomic_store(&stats->pad, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-}
-
-FEDMI_DEV void sgd_fused_body(int r, int nb, float* __restrict__ params, float* __restrict__ mom,
-                              bf16* __restrict__ pk, const float* __restrict__ conv_slab,
-                              const float* __restrict__ fc1w_grad, const float* __restrict__ fc_slab, int n_fc,
-                              float lr, float momentum, float wd, const int* __restrict__ flags, int gen,
-                              int* __restrict__ round_bump, int* __restrict__ step_gen, Stats* __restrict__ stats) {
-  __shared__ float red[16][65];
-  const int tid = threadIdx.x;
-  if (r < K34_NA) {
-    wait_flags(flags, nb, gen, stats);
-    if (r == 0 && tid == 0) {             // every producer has read both counters by now
-      if (round_bump) atomicAdd(round_bump, 1);
-      step_gen[0] += 1;
-    }
-    const int pl = tid & 63, g = tid >> 6;
-    const int i = r * 64 + pl;
-    float p = 0.f, m = 0.f;
-    if (g == 0 && i < CS) { p = params[i]; m = mom[i]; }
-    float sum = 0.f;
-    if (i < CS) {
-      float v[MAX_TRAIN_BATCH / 16];
-#pragma unroll
-      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) {
-        const int q = g + 16 * u;
-        v[u] = q < nb ? __hip_atomic_load(conv_slab + (size_t)q * CS + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) sum += v[u];
-    }
-    red[g][pl] = sum;
-    __syncthreads();
-    if (g == 0 && i < CS) {
-      float tot = 0.f;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) tot += red[q][pl];
-      sgd_apply(i, tot, p, m, params, mom, pk, lr, momentum, wd);
-    }
-  } else if (r < K34_NA + K34_NB) {
-    const int j = (r - K34_NA) * NT_CONV + tid;
-    const bool ok = j < F1W_N;
-    const int i = P_F1W + (ok ? j : 0);
-    const float p = ok ? params[i] : 0.f, m = ok ? mom[i] : 0.f;    // loaded while the fc1 wgrad runs
-    wait_flags(flags + nb, N_DW1_WG, gen, stats);
-    if (ok)
-      sgd_apply(i, __hip_atomic_load(fc1w_grad + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), p, m, params, mom,
-                pk, lr, momentum, wd);
-  } else {
-    const int j = (r - K34_NA - K34_NB) * NT_CONV + tid;
-    if (j < FS) {                          // grads from K12 (previous launch): plain loads
-      const int i = P_F1B + j;
-      const float p = params[i], m = mom[i];
-      float v[MAX_FC_WG];
-#pragma unroll
-      for (int q = 0; q < MAX_FC_WG; ++q) v[q] = q < n_fc ? fc_slab[(size_t)q * FS + j] : 0.f;
-      float sum = 0.f;
-#pragma unroll
-      for (int q = 0; q < MAX_FC_WG; ++q) sum += v[q];
-      sgd_apply(i, sum, p, m, params, mom, pk, lr, momentum, wd);
-    }
-  }
-}
-
-__global__ __launch_bounds__(NT_CONV) void lenet_bwd_sgd(
-    const uint8_t* __restrict__ images, int sample_base, int nb, uint32_t seed, const int* __restrict__ round_ctr,
-    int augment, const float* __restrict__ dact2, const bf16* __restrict__ act2T, const bf16* __restrict__ dZ1T,
-    const bf16* __restrict__ pool1, const uint8_t* __restrict__ am1, const uint8_t* __restrict__ am2,
-    const bf16* pk_in, float* conv_slab, float* fc1w_grad,   // (pk_in == pk, conv_slab / fc1w_grad: both roles)
-    float* __restrict__ params, float* __restrict__ mom, bf16* pk, const float* __restrict__ fc_slab,
-    int n_fc, float lr, float momentum, float wd, int* __restrict__ flags, const int* __restrict__ bwd_gen,
-    int* __restrict__ round_bump, int* __restrict__ step_gen, Stats* __restrict__ stats)
-{
-  const int gen = bwd_gen[0];
-  const int nprod = nb + N_DW1_WG;
-  if ((int)blockIdx.x < nprod) {
-    conv_bwd_body<true>(blockIdx.x, images, sample_base, nb, seed, round_ctr, augment, dact2, act2T, dZ1T, pool1, am1,
-                        am2, pk_in, conv_slab, fc1w_grad, flags, gen);
-    return;
-  }
-  sgd_fused_body(blockIdx.x - nprod, nb, params, mom, pk, conv_slab, fc1w_grad, fc_slab, n_fc, lr, momentum, wd, flags,
-                 gen, round_bump, step_gen, stats);
 }
 
 // ---------------------------------------------------------------------------
@@ -1980,64 +1288,35 @@ void launch_lenet_conv_fwd(hipStream_t st, const uint8_t* images, int sample_bas
                      seed, round_ctr, augment, act2, act2T, tstride, pool1, am1, am2, zero_stats);
 }
 
-void launch_lenet_fc1_fwd(hipStream_t st, const bf16* act2, int nb, const bf16* pk, const float* params, bf16* h1) {
-  if (nb <= 0) return;
-  const int mtiles = (nb + FC_SPW - 1) / FC_SPW;
-  hipLaunchKernelGGL(lenet_fc1_fwd, dim3(mtiles * 8), dim3(256), 0, st, act2, nb, pk, params, h1);
+// eval loss / correct partials of lenet_fc_eval (one pair per 16-row group) summed in group order: 256
+// strided partials, then an ordered LDS fold -- bit-reproducible eval statistics
+__global__ __launch_bounds__(256) void lenet_eval_stats(const float* __restrict__ part, int groups, int n,
+                                                        Stats* __restrict__ stats) {
+  __shared__ float rl[256], rc[256];
+  float l = 0.f, c = 0.f;
+  for (int g = threadIdx.x; g < groups; g += 256) { l += part[2 * g]; c += part[2 * g + 1]; }
+  rl[threadIdx.x] = l;
+  rc[threadIdx.x] = c;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) { rl[threadIdx.x] += rl[threadIdx.x + w]; rc[threadIdx.x] += rc[threadIdx.x + w]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    stats->loss_sum += rl[0];
+    stats->correct += (int)(rc[0] + 0.5f);
+    stats->count += n;
+  }
 }
 
-// h1 == nullptr: the tail computes fc1 itself (FUSE_FC1 variant, K2a not launched)
-void launch_lenet_fc_tail(hipStream_t st, const bf16* h1, const bf16* act2, const int* labels, int nb, int train,
-                          const bf16* pk, const float* params, float* dact2, bf16* dZ1T, float* fc_slab,
-                          Stats* stats) {
-  if (nb <= 0) return;
-  const int mtiles = (nb + FC_SPW - 1) / FC_SPW;
-  if (h1 == nullptr)
-    hipLaunchKernelGGL(lenet_fc_tail<true>, dim3(mtiles * (train ? 4 : 1)), dim3(NT_FC), 0, st, h1, act2, labels, nb,
-                       train, pk, params, dact2, dZ1T, fc_slab, stats);
-  else
-    hipLaunchKernelGGL(lenet_fc_tail<false>, dim3(mtiles * (train ? 4 : 1)), dim3(NT_FC), 0, st, h1, act2, labels, nb,
-                       train, pk, params, dact2, dZ1T, fc_slab, stats);
-}
-
-void launch_lenet_conv_bwd(hipStream_t st, const uint8_t* images, int sample_base, int nb,
-                           uint32_t seed, const int* round_ctr, int augment, const float* dact2,
-                           const bf16* act2T, const bf16* dZ1T, const bf16* pool1, const uint8_t* am1,
-                           const uint8_t* am2, const bf16* pk, float* conv_slab, float* fc1w_grad) {
-  if (nb <= 0) return;
-  hipLaunchKernelGGL(lenet_conv_bwd, dim3(nb + N_DW1_WG), dim3(NT_CONV), 0, st, images, sample_base, nb, seed,
-                     round_ctr, augment, dact2, act2T, dZ1T, pool1, am1, am2, pk, conv_slab, fc1w_grad);
-}
-
-void launch_lenet_sgd(hipStream_t st, float* params, float* mom, bf16* pk, const float* conv_slab,
-                      int n_conv, const float* fc1w_grad, const float* fc_slab, int n_fc, float lr,
-                      float momentum, float wd, int* round_ctr, int* step_gen) {
-  hipLaunchKernelGGL(lenet_sgd, dim3(SGD_NA + SGD_NB + SGD_NC), dim3(256), 0, st, params, mom, pk,
-                     conv_slab, n_conv, fc1w_grad, fc_slab, n_fc, lr, momentum, wd, round_ctr, step_gen);
-}
-
-void launch_lenet_fwd_head(hipStream_t st, const uint8_t* images, int sample_base, int nb, const bf16* pk,
-                           const float* params, uint32_t seed, const int* round_ctr, int augment, bf16* act2,
-                           bf16* act2T, bf16* pool1, uint8_t* am1, uint8_t* am2, const int* labels, float* dact2,
-                           bf16* dZ1T, float* fc_slab, Stats* stats, int* done_flags, const int* step_gen,
-                           int* bwd_gen) {
-  if (nb <= 0 || nb > MAX_TRAIN_BATCH) return;
-  const int mtiles = (nb + FC_SPW - 1) / FC_SPW;
-  hipLaunchKernelGGL(lenet_fwd_head, dim3(nb + 4 * mtiles), dim3(NT_FWD), 0, st, images, sample_base, nb, pk, params,
-                     seed, round_ctr, augment, act2, act2T, pool1, am1, am2, labels, dact2, dZ1T, fc_slab, stats,
-                     done_flags, step_gen, bwd_gen);
-}
-
-void launch_lenet_bwd_sgd(hipStream_t st, const uint8_t* images, int sample_base, int nb, uint32_t seed,
-                          const int* round_ctr, int augment, const float* dact2, const bf16* act2T, const bf16* dZ1T,
-                          const bf16* pool1, const uint8_t* am1, const uint8_t* am2, float* conv_slab,
-                          float* fc1w_grad, float* params, float* mom, bf16* pk, const float* fc_slab, int n_fc, float lr,
-                          float momentum, float wd, int* flags, const int* bwd_gen, int* round_bump, int* step_gen,
-                          Stats* stats) {
-  if (nb <= 0 || nb > MAX_TRAIN_BATCH) return;
-  hipLaunchKernelGGL(lenet_bwd_sgd, dim3(nb + N_DW1_WG + K34_SGD_WG), dim3(NT_CONV), 0, st, images, sample_base, nb,
-                     seed, round_ctr, augment, dact2, act2T, dZ1T, pool1, am1, am2, pk, conv_slab, fc1w_grad, params,
-                     mom, pk, fc_slab, n_fc, lr, momentum, wd, flags, bwd_gen, round_bump, step_gen, stats);
+// eval head over the act2 rows of n samples; part: >= 2 * ceil(n / 16) floats of scratch
+void launch_lenet_fc_eval(hipStream_t st, const bf16* act2, const int* labels, int n, const bf16* pk,
+                          const float* params, float* part, long part_floats, Stats* stats) {
+  if (n <= 0) return;
+  const int mtiles = (n + FC_SPW - 1) / FC_SPW;
+  if (2L * mtiles > part_floats) throw std::invalid_argument("lenet eval: partials scratch too small");
+  hipLaunchKernelGGL(lenet_fc_eval, dim3(mtiles), dim3(NT_FC), 0, st, act2, labels, n, pk, params, part);
+  hipLaunchKernelGGL(lenet_eval_stats, dim3(1), dim3(256), 0, st, part, mtiles, n, stats);
 }
 
 bool stamps_enabled() {
@@ -2085,7 +1364,6 @@ void launch_lenet_pack(hipStream_t st, const float* params, bf16* pk) {
   hipLaunchKernelGGL(lenet_pack, dim3((P_TOTAL + 255) / 256), dim3(256), 0, st, params, pk);
 }
 
-
 void launch_lenet_sample_step(hipStream_t st, const uint8_t* images, int sample_base, int nb, const bf16* pk,
                               const float* params, uint32_t seed, const int* round_ctr, int augment,
                               const int* labels, bf16* act2T, bf16* h1T, float* aux, bf16* dZ1T, float* conv_slab) {
@@ -2096,10 +1374,10 @@ void launch_lenet_sample_step(hipStream_t st, const uint8_t* images, int sample_
 
 void launch_lenet_sgd2(hipStream_t st, float* params, float* mom, bf16* pk, const float* conv_slab, int nb,
                        const bf16* act2T, const bf16* h1T, const float* aux, const bf16* dZ1T, float lr,
-                       float momentum, float wd, int* round_ctr, int* step_gen, Stats* stats) {
+                       float momentum, float wd, int* round_ctr, Stats* stats) {
   if (nb <= 0 || nb > MAX_TRAIN_BATCH) throw std::invalid_argument("lenet_sgd2: batch must be in [1, 128]");
   hipLaunchKernelGGL(lenet_sgd2, dim3(SGD2_GRID), dim3(256), 0, st, params, mom, pk, conv_slab, nb, act2T, h1T,
-                     reinterpret_cast<const unsigned char*>(aux), dZ1T, lr, momentum, wd, round_ctr, step_gen, stats);
+                     reinterpret_cast<const unsigned char*>(aux), dZ1T, lr, momentum, wd, round_ctr, stats);
 }
 
 }  // namespace fedmi

@@ -43,11 +43,9 @@ constexpr int P_F3W = 61156;             // fc3.weight   [10,84]
 constexpr int P_F3B = 61996;             // fc3.bias     [10]
 constexpr int P_TOTAL = 62006;
 
-// Gradient staging (combined by the SGD kernel at the next kernel boundary:
-// deterministic, no global atomics):
-//   conv_slab [nb][CS]      per-sample grads of params [0, P_F1W)
-//   fc1w_grad [48000]       complete fc1.weight grad (one writer per element)
-//   fc_slab   [nfc][FS]     per-FC-workgroup grads of params [P_F1B, P_TOTAL)
+// Gradient staging (combined by KS2 at the next kernel boundary: deterministic, no global
+// atomics): conv_slab [nb][CS] per-sample grads of params [0, P_F1W); the FC weight grads are
+// KS2's batch GEMMs over KS1's sample-contiguous operands.
 constexpr int CS = P_F1W;                // 2872
 constexpr int FS = P_TOTAL - P_F1B;      // 11134
 constexpr int F1W_N = P_F1B - P_F1W;     // 48000
@@ -68,12 +66,11 @@ constexpr int PK_TOTAL = PK_FC3T + 96 * 32;
 
 // ---- training-step geometry -------------------------------------------------
 constexpr int MAX_TRAIN_BATCH = 128;     // reference batch (src/main.py:140)
-constexpr int FC_SPW = 16;               // samples per FC-head workgroup (one MFMA row tile)
-constexpr int MAX_FC_WG = MAX_TRAIN_BATCH / FC_SPW;
+constexpr int FC_SPW = 16;               // samples per eval FC-head workgroup (one MFMA row tile)
 constexpr int DZ1_LD = 128;              // dZ1 [B][128] and dZ1T [128][B] (B = 128)
-constexpr int N_DW1_WG = F0 / 16;        // 25 fc1-wgrad workgroups appended to the conv-bwd grid
 
-// Stats block written by the FC-head kernel (float/int atomics).
+// Stats block: train row written by KS2 (per-sample losses summed in sample order), eval row by
+// lenet_eval_stats (row-group partials in group order) -- single writers, no atomics.
 struct Stats {
   float loss_sum;   // sum over samples of CE loss
   int correct;      // argmax == label

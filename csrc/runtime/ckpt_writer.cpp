@@ -5,6 +5,7 @@
 #include <unistd.h>
 #include <zlib.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -134,7 +135,17 @@ void CkptWriter::submit(hipStream_t st, int32_t epoch) {
 }
 
 void CkptWriter::write_one(int slot, int32_t epoch) {
-  if (device_) check_hip(hipEventSynchronize(ev_[slot]), "CkptWriter snapshot wait");
+  if (device_) {
+    // poll instead of hipEventSynchronize: a writer thread blocked inside the runtime's event wait was
+    // measured stalling the round loop's own launches/copies on the main thread (host 1.15 ms per
+    // submit at the 8-client LeNet cadence, profiles/r4_scale/README.md)
+    for (;;) {
+      const hipError_t q = hipEventQuery(ev_[slot]);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) check_hip(q, "CkptWriter snapshot wait");
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
   uint8_t* o = out_.data();
   put_u32(o + epoch_at_, (uint32_t)epoch);        // pickle BININT ('J' + int32 LE)
   for (const auto& r : recs_) {

@@ -11,25 +11,14 @@ using lenet::Stats;
 // launchers (csrc/kernels/lenet_kernels.hip)
 void launch_lenet_conv_fwd(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t,
                            const int*, int, bf16*, bf16*, int, bf16*, uint8_t*, uint8_t*, lenet::Stats*);
-void launch_lenet_fc1_fwd(hipStream_t, const bf16*, int, const bf16*, const float*, bf16*);
-void launch_lenet_fc_tail(hipStream_t, const bf16*, const bf16*, const int*, int, int, const bf16*, const float*, float*,
-                          bf16*, float*, Stats*);
-void launch_lenet_conv_bwd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const float*, const bf16*,
-                           const bf16*, const bf16*, const uint8_t*, const uint8_t*, const bf16*, float*, float*);
-void launch_lenet_sgd(hipStream_t, float*, float*, bf16*, const float*, int, const float*, const float*, int, float,
-                      float, float, int*, int*);
-void launch_lenet_fwd_head(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*, int,
-                           bf16*, bf16*, bf16*, uint8_t*, uint8_t*, const int*, float*, bf16*, float*, Stats*, int*,
-                           const int*, int*);
-void launch_lenet_bwd_sgd(hipStream_t, const uint8_t*, int, int, uint32_t, const int*, int, const float*, const bf16*,
-                          const bf16*, const bf16*, const uint8_t*, const uint8_t*, float*, float*, float*, float*, bf16*,
-                          const float*, int, float, float, float, int*, const int*, int*, int*, Stats*);
+void launch_lenet_fc_eval(hipStream_t, const bf16*, const int*, int, const bf16*, const float*, float*, long,
+                          lenet::Stats*);
 void launch_lenet_pack(hipStream_t, const float*, bf16*);
 void launch_lenet_zero_stats(hipStream_t, lenet::Stats*);
 void launch_lenet_sample_step(hipStream_t, const uint8_t*, int, int, const bf16*, const float*, uint32_t, const int*,
                               int, const int*, bf16*, bf16*, float*, bf16*, float*);
 void launch_lenet_sgd2(hipStream_t, float*, float*, bf16*, const float*, int, const bf16*, const bf16*, const float*,
-                       const bf16*, float, float, float, int*, int*, lenet::Stats*);
+                       const bf16*, float, float, float, int*, lenet::Stats*);
 
 void check_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("fedmi HIP error in ") + what + ": " + hipGetErrorString(e));
@@ -37,8 +26,8 @@ void check_hip(hipError_t e, const char* what) {
 
 LeNetEngine::LeNetEngine(const LeNetBuffers& b, SgdConfig sgd, uint32_t seed, bool augment)
     : b_(b), sgd_(sgd), seed_(seed), augment_(augment) {
-  if (!b.params || !b.mom || !b.pk || !b.act2 || !b.act2T || !b.pool1 || !b.am1 || !b.am2 || !b.h1 || !b.dact2 || !b.dZ1T ||
-      !b.conv_slab || !b.fc1w_grad || !b.fc_slab || !b.train_stats || !b.eval_stats || !b.round_ctr)
+  if (!b.params || !b.mom || !b.pk || !b.act2 || !b.act2T || !b.h1 || !b.dact2 || !b.dZ1T || !b.conv_slab ||
+      !b.eval_part || !b.train_stats || !b.eval_stats || !b.round_ctr)
     throw std::invalid_argument("LeNetEngine: missing device buffer");
   if (b.act2_rows < lenet::MAX_TRAIN_BATCH) throw std::invalid_argument("LeNetEngine: act2_rows < 128");
   check_hip(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -67,13 +56,6 @@ void LeNetEngine::set_schedule(const std::vector<int>& starts, const std::vector
   drop_graph();
 }
 
-void LeNetEngine::set_fuse_fc1(bool on) {
-  if (on != fuse_fc1_) {
-    fuse_fc1_ = on;
-    drop_graph();
-  }
-}
-
 void LeNetEngine::set_sgd(SgdConfig sgd) {
   sgd_ = sgd;
   drop_graph();
@@ -84,67 +66,13 @@ void LeNetEngine::step(hipStream_t st, int start, int nb, bool bump_round, bool 
   if (nb <= 0 || nb > MAX_TRAIN_BATCH || start < 0 || start + nb > b_.n_train)
     throw std::invalid_argument("LeNetEngine::step: batch out of range");
   const int aug = augment_ ? 1 : 0;
-  if (sample_path_) {
-    if (reset_stats) launch_lenet_zero_stats(st, b_.train_stats);   // a kernel node, not a memset (graph replay)
-    // the FC side buffers (h2T, dZ2T, dZ3T, bias grads, losses) live in the dact2 buffer, h1T in h1
-    launch_lenet_sample_step(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug,
-                             b_.train_labels + start, b_.act2T, b_.h1, b_.dact2, b_.dZ1T, b_.conv_slab);
-    launch_lenet_sgd2(st, b_.params, b_.mom, b_.pk, b_.conv_slab, nb, b_.act2T, b_.h1, b_.dact2, b_.dZ1T, sgd_.lr,
-                      sgd_.momentum, sgd_.weight_decay, bump_round ? b_.round_ctr : nullptr, b_.step_gen,
-                      b_.train_stats);
-    check_hip(hipGetLastError(), "LeNetEngine::step launch");
-    return;
-  }
-  if (fuse_head_) {
-    if (reset_stats) launch_lenet_zero_stats(st, b_.train_stats);   // a kernel node, not a memset (graph replay)
-    launch_lenet_fwd_head(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug, b_.act2,
-                          b_.act2T, b_.pool1, b_.am1, b_.am2, b_.train_labels + start, b_.dact2, b_.dZ1T, b_.fc_slab,
-                          b_.train_stats, b_.done_flags, b_.step_gen, b_.bwd_gen);
-  } else {
-    launch_lenet_conv_fwd(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug, b_.act2,
-                          b_.act2T, MAX_TRAIN_BATCH, b_.pool1, b_.am1, b_.am2, reset_stats ? b_.train_stats : nullptr);
-    if (!fuse_fc1_) launch_lenet_fc1_fwd(st, b_.act2, nb, b_.pk, b_.params, b_.h1);
-    launch_lenet_fc_tail(st, fuse_fc1_ ? nullptr : b_.h1, b_.act2, b_.train_labels + start, nb, 1, b_.pk, b_.params,
-                         b_.dact2, b_.dZ1T, b_.fc_slab, b_.train_stats);
-  }
-  if (fuse_sgd_ && fuse_head_) {
-    launch_lenet_bwd_sgd(st, b_.train_images, start, nb, seed_, b_.round_ctr, aug, b_.dact2, b_.act2T, b_.dZ1T,
-                         b_.pool1, b_.am1, b_.am2, b_.conv_slab, b_.fc1w_grad, b_.params, b_.mom, b_.pk, b_.fc_slab,
-                         (nb + FC_SPW - 1) / FC_SPW, sgd_.lr, sgd_.momentum, sgd_.weight_decay, b_.bwd_flags, b_.bwd_gen,
-                         bump_round ? b_.round_ctr : nullptr, b_.step_gen, b_.train_stats);
-  } else {
-    launch_lenet_conv_bwd(st, b_.train_images, start, nb, seed_, b_.round_ctr, aug, b_.dact2, b_.act2T, b_.dZ1T,
-                          b_.pool1, b_.am1, b_.am2, b_.pk, b_.conv_slab, b_.fc1w_grad);
-    launch_lenet_sgd(st, b_.params, b_.mom, b_.pk, b_.conv_slab, nb, b_.fc1w_grad, b_.fc_slab,
-                     (nb + FC_SPW - 1) / FC_SPW, sgd_.lr, sgd_.momentum, sgd_.weight_decay,
-                     bump_round ? b_.round_ctr : nullptr, b_.step_gen);
-  }
+  if (reset_stats) launch_lenet_zero_stats(st, b_.train_stats);   // a kernel node, not a memset (graph replay)
+  // the FC side buffers (h2T, dZ2T, dZ3T, bias grads, losses) live in the dact2 buffer, h1T in h1
+  launch_lenet_sample_step(st, b_.train_images, start, nb, b_.pk, b_.params, seed_, b_.round_ctr, aug,
+                           b_.train_labels + start, b_.act2T, b_.h1, b_.dact2, b_.dZ1T, b_.conv_slab);
+  launch_lenet_sgd2(st, b_.params, b_.mom, b_.pk, b_.conv_slab, nb, b_.act2T, b_.h1, b_.dact2, b_.dZ1T, sgd_.lr,
+                    sgd_.momentum, sgd_.weight_decay, bump_round ? b_.round_ctr : nullptr, b_.train_stats);
   check_hip(hipGetLastError(), "LeNetEngine::step launch");
-}
-
-void LeNetEngine::set_sample_path(bool on) {
-  if (on && (!b_.h1 || !b_.dact2 || !b_.dZ1T || !b_.act2T))
-    throw std::invalid_argument("sample path needs h1, dact2, dZ1T and act2T buffers");
-  if (on != sample_path_) {
-    sample_path_ = on;
-    drop_graph();
-  }
-}
-
-void LeNetEngine::set_fuse_head(bool on) {
-  if (on && (!b_.done_flags || !b_.step_gen)) throw std::invalid_argument("fuse_head needs done_flags and step_gen");
-  if (on != fuse_head_) {
-    fuse_head_ = on;
-    drop_graph();
-  }
-}
-
-void LeNetEngine::set_fuse_sgd(bool on) {
-  if (on && (!b_.bwd_flags || !b_.bwd_gen)) throw std::invalid_argument("fuse_sgd needs bwd_flags and bwd_gen");
-  if (on != fuse_sgd_) {
-    fuse_sgd_ = on;
-    drop_graph();
-  }
 }
 
 void LeNetEngine::enqueue_epoch(hipStream_t st) {
@@ -177,17 +105,12 @@ void LeNetEngine::run_epoch(hipStream_t st, bool use_graph) {
   check_hip(hipGraphLaunch(exec_, st), "GraphLaunch");
 }
 
-void LeNetEngine::eval(hipStream_t st, const uint8_t* images, const int* labels, int n, const bf16* pk,
-                       const float* params) {
+void LeNetEngine::eval(hipStream_t st, const uint8_t* images, const int* labels, int n) {
   using namespace lenet;
   if (n <= 0 || n > b_.act2_rows) throw std::invalid_argument("LeNetEngine::eval: n exceeds act2 capacity");
-  if (!pk) pk = b_.pk;
-  if (!params) params = b_.params;
-  launch_lenet_conv_fwd(st, images, 0, n, pk, params, seed_, b_.round_ctr, 0, b_.act2, nullptr, 0,
+  launch_lenet_conv_fwd(st, images, 0, n, b_.pk, b_.params, seed_, b_.round_ctr, 0, b_.act2, nullptr, 0,
                         nullptr, nullptr, nullptr, b_.eval_stats);
-  if (!fuse_fc1_) launch_lenet_fc1_fwd(st, b_.act2, n, pk, params, b_.h1);
-  launch_lenet_fc_tail(st, fuse_fc1_ ? nullptr : b_.h1, b_.act2, labels, n, 0, pk, params, nullptr, nullptr,
-                       nullptr, b_.eval_stats);
+  launch_lenet_fc_eval(st, b_.act2, labels, n, b_.pk, b_.params, b_.eval_part, b_.eval_part_floats, b_.eval_stats);
   check_hip(hipGetLastError(), "LeNetEngine::eval launch");
 }
 

@@ -55,6 +55,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--compress", default=None, choices=["none", "topk", "int8"],
                     help="update compression (default: topk when -c Y)")
     ap.add_argument("--topk-ratio", type=float, default=0.01)
+    ap.add_argument("--compress-warmup", type=int, default=0, help="dense FedAvg rounds before -c Y compression starts")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--root", default=".")
     ap.add_argument("--metrics", default=None)
@@ -88,7 +89,7 @@ def main(argv=None) -> int:
     backend = a.backend if a.backend != "auto" else ("nccl" if dev.type == "cuda" else "gloo")
     transport = a.transport if a.transport != "auto" else ("auto" if dev.type == "cuda" else "dist")
     comp_kind = a.compress if a.compress is not None else ("topk" if gzip else "none")
-    fedavg = FedAvg(compressor=make_compressor(comp_kind, a.topk_ratio, trainer))
+    fedavg = FedAvg(compressor=make_compressor(comp_kind, a.topk_ratio, trainer, a.compress_warmup))
     n = trainer.float_state().numel()
     cap = max(4 * n, 16 * (int(n * a.topk_ratio) + 64), n + 4 * (n // 256 + 64))
     group = GroupManager(backend, dev, timeout_s=a.collective_timeout, transport=transport, peer_capacity=cap,

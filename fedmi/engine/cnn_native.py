@@ -552,6 +552,7 @@ class CNNNativeTrainer(LocalTrainer):
         self.pooled = torch.empty(R, self.head_c, device=device)
         self.head_lin = getattr(self.model, "linear", None) or self.model.classifier
         self.dlog = torch.empty(R, self.head_lin.out_features, device=device)
+        self.lossv = torch.empty(R, device=device)            # per-sample CE losses (ordered sum, no atomics)
         self.stats = torch.zeros(2, 4, device=device)        # [train, eval] x {loss, correct, count, pad}
         self.round_ctr = torch.zeros(4, dtype=torch.int32, device=device)
         self.sched = torch.zeros(1, dtype=torch.int32, device=device)
@@ -684,7 +685,7 @@ class CNNNativeTrainer(LocalTrainer):
         hd = self.dhead[: a.numel()].view_as(a)
         cnn.head(a, labels, 0, lin.weight, lin.bias, self.stats[stats_row], train, self.pooled[:nb], self.dlog[:nb],
                  hd if train else None, lin.weight.grad if train else None, lin.bias.grad if train else None,
-                 dbase=dbase, zero=self.bn_chain if train else None)
+                 dbase=dbase, zero=self.bn_chain if train else None, lossv=self.lossv[:nb])
         return x, hd
 
     def _sums(self, conv_u: _Unit, u: _Unit, nb: int, y, zb: Optional[_Unit] = None,
@@ -792,7 +793,7 @@ class CNNNativeTrainer(LocalTrainer):
         hd = self.dhead[: a.numel()].view_as(a)
         cnn.head(a, labels, 0, lin.weight, lin.bias, self.stats[stats_row], train, self.pooled[:nb], self.dlog[:nb],
                  hd if train else None, lin.weight.grad if train else None, lin.bias.grad if train else None,
-                 dbase=dbase, zero=self.bn_chain if train else None)
+                 dbase=dbase, zero=self.bn_chain if train else None, lossv=self.lossv[:nb])
         return hd
 
     def _forward_preact(self, nb: int, train: bool, images, labels, dbase, stats_row: int):

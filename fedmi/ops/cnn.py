@@ -202,10 +202,16 @@ def bn_bwd_ws_floats(M: int, C: int) -> int:
 
 def head(y: torch.Tensor, labels: torch.Tensor, base: int, W: torch.Tensor, b: torch.Tensor, stats: torch.Tensor,
          train: bool, pooled=None, dlog=None, dy=None, dW=None, db=None, dbase=None,
-         zero: Optional[torch.Tensor] = None) -> None:
+         zero: Optional[torch.Tensor] = None, lossv: Optional[torch.Tensor] = None) -> None:
+    """Global avgpool + linear + CE (+ correct count) of y [N,H,W,C] bf16; with ``train`` also the CE
+    gradient into ``dy`` and the linear layer's ``dW`` / ``db``.  ``lossv``: [N] fp32 scratch for the
+    per-sample losses, summed into ``stats`` in sample order (bit-reproducible; no float atomics)."""
     N, H, Wd, C = y.shape
     J = W.shape[0]
+    if lossv is None:
+        lossv = torch.empty(N, dtype=torch.float32, device=y.device)
     native.require().head(native.stream_handle(y.device), y.data_ptr(), labels.data_ptr(), base, _p(dbase), N,
                           H * Wd, C, J,
                           W.data_ptr(), b.data_ptr(), _p(pooled), _p(dlog), _p(dy), stats.data_ptr(), _p(dW), _p(db),
-                          int(train), _p(zero), zero.numel() * zero.element_size() // 4 if zero is not None else 0)
+                          int(train), _p(zero), zero.numel() * zero.element_size() // 4 if zero is not None else 0,
+                          lossv.data_ptr())

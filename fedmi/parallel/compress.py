@@ -62,7 +62,13 @@ def _all_gather_flat(t: torch.Tensor, group, transport=None) -> torch.Tensor:
 
 
 class _EFCompressor:
-    def __init__(self, trainer):
+    """``warmup``: the first ``warmup`` aggregations are dense FedAvg (the largest updates of a run come
+    first, when a 1 % selection defers most of them); compression starts from the dense global model
+    with an empty residual."""
+
+    def __init__(self, trainer, warmup: int = 0):
+        self.warmup = int(warmup)
+        self.dense_rounds = 0
         x = trainer.float_state()
         self.n = x.numel()
         self.dev = x.device
@@ -79,6 +85,24 @@ class _EFCompressor:
         self.global_ref.copy_(trainer.float_state())
         self.residual.zero_()
 
+    def _dense(self, x: torch.Tensor, group, transport) -> bool:
+        """Dense FedAvg of ``x`` while in warm-up; True if it ran (the anchor follows, residual empty)."""
+        if self.dense_rounds >= self.warmup:
+            return False
+        if transport is not None:
+            transport.allreduce_mean_(x)
+        else:
+            from .fedavg import allreduce_mean_
+
+            allreduce_mean_(x, group)
+        self.global_ref.copy_(x)
+        self.residual.zero_()
+        self.dense_rounds += 1
+        self.bytes_sent += 4 * self.n
+        self.dense_bytes += 4 * self.n
+        self.rounds += 1
+        return True
+
     def _delta(self, x: torch.Tensor) -> None:
         if self._nat is not None:
             self._nat.ef_delta(native.stream_handle(self.dev), x.data_ptr(), self.global_ref.data_ptr(),
@@ -89,8 +113,8 @@ class _EFCompressor:
 
 
 class TopKCompressor(_EFCompressor):
-    def __init__(self, trainer, ratio: float = 0.01):
-        super().__init__(trainer)
+    def __init__(self, trainer, ratio: float = 0.01, warmup: int = 0):
+        super().__init__(trainer, warmup)
         self.k = max(1, min(self.n, int(round(self.n * ratio))))
         self.idx = torch.empty(self.k, dtype=torch.int32, device=self.dev)
         self.val = torch.empty(self.k, dtype=torch.float32, device=self.dev)
@@ -129,6 +153,8 @@ class TopKCompressor(_EFCompressor):
 
     def aggregate(self, trainer, group=None, transport=None) -> None:
         x = trainer.float_state()
+        if self._dense(x, group, transport):
+            return
         self.compress(x)
         _probe("topk")
         w = transport.world if transport is not None else _world(group)
@@ -152,8 +178,8 @@ class TopKCompressor(_EFCompressor):
 class Int8Compressor(_EFCompressor):
     CHUNK = 256
 
-    def __init__(self, trainer):
-        super().__init__(trainer)
+    def __init__(self, trainer, warmup: int = 0):
+        super().__init__(trainer, warmup)
         self.nchunks = (self.n + self.CHUNK - 1) // self.CHUNK
         self.q = torch.empty(self.n, dtype=torch.int8, device=self.dev)
         self.scales = torch.empty(self.nchunks, dtype=torch.float32, device=self.dev)
@@ -176,6 +202,8 @@ class Int8Compressor(_EFCompressor):
 
     def aggregate(self, trainer, group=None, transport=None) -> None:
         x = trainer.float_state()
+        if self._dense(x, group, transport):
+            return
         self.compress(x)
         w = transport.world if transport is not None else _world(group)
         q_all = _all_gather_flat(self.q, group, transport)
@@ -193,11 +221,11 @@ class Int8Compressor(_EFCompressor):
         x.copy_(self.global_ref)
 
 
-def make_compressor(kind: Optional[str], ratio: float, trainer):
+def make_compressor(kind: Optional[str], ratio: float, trainer, warmup: int = 0):
     if kind in (None, "", "none", "n", "N"):
         return None
     if kind in ("topk", "Y", "y"):
-        return TopKCompressor(trainer, ratio)
+        return TopKCompressor(trainer, ratio, warmup)
     if kind == "int8":
-        return Int8Compressor(trainer)
+        return Int8Compressor(trainer, warmup)
     raise ValueError(f"unknown compression {kind!r}")

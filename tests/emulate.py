@@ -346,7 +346,7 @@ def bn_bwd_chain_floats(C):
 
 @torch.no_grad()
 def head(y, labels, base, W, b, stats, train, pooled=None, dlog=None, dy=None, dW=None, db=None, dbase=None,
-         zero=None):
+         zero=None, lossv=None):
     if zero is not None:
         zero.zero_()
     N, H, Wd, C = y.shape

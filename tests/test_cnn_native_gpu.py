@@ -73,8 +73,10 @@ def test_loss_and_tail_grads_match_torch(gpu_device, name, tail):
 @pytest.mark.parametrize("name", ["ResNet18", "MobileNet", "MobileNetV2", "VGG11", "PreActResNet18", "GoogLeNet"])
 def test_engine_is_deterministic(gpu_device, name):
     """Two engines from the same init on the same batch produce bit-identical gradients, batch statistics and
-    running stats: BatchNorm sums go through fp64 atomics (order-independent), every split-K / weight-gradient
-    / head reduction is fixed-order."""
+    running stats.  Every split-K / weight-gradient / head reduction is fixed-order; the BatchNorm sums are fp64
+    atomics, whose arrival order varies -- fp64 sums of these bf16-valued terms come out identical in practice
+    (the terms would have to span ~20 binades to round differently), which this test checks; it is not a
+    guarantee of the arithmetic."""
     from fedmi.engine.cnn_native import CNNNativeTrainer
 
     nb = 64
@@ -97,16 +99,26 @@ def test_engine_is_deterministic(gpu_device, name):
     assert sa.correct == sb.correct and sa.count == sb.count
 
 
-@pytest.mark.parametrize("name,avg_cos", [("ResNet18", 0.75), ("MobileNetV2", 0.35)])
-def test_native_matches_emulated_kernels_on_gpu(gpu_device, name, avg_cos):
-    """Same engine schedule, same bf16 buffers, kernels vs their PyTorch twins (tests/emulate.py)."""
+# Per-tensor margins from profiles/r4_tests/grad_cosines.jsonl (tools/diag_grad_cosines.py, one batch of 64 at
+# random init): the native engine's gradient cosine to fp32 is within 0.022 (ResNet-18) / 0.29 (MobileNetV2) of
+# PyTorch's OWN autocast-bf16 model's at every tensor -- MobileNetV2's deep BN stack makes every bf16 model's
+# early-layer gradient direction chaotic at init (torch-bf16 vs fp32: mean cos 0.51, min -0.25).
+GRAD_MARGIN = {"ResNet18": 0.05, "MobileNetV2": 0.35}
+
+
+@pytest.mark.parametrize("name", ["ResNet18", "MobileNetV2"])
+def test_native_gradients_track_torch_bf16(gpu_device, name):
+    """Per tensor: cos(native grad, fp32 grad) >= cos(torch autocast-bf16 grad, fp32 grad) - margin; the mean
+    over tensors within 0.03 of torch-bf16's; the classifier and the last BN at >= 0.99; the loss within 0.5 %
+    of the emulated-kernel engine's (same schedule and bf16 buffers, tests/emulate.py)."""
     from fedmi.engine.cnn_native import CNNNativeTrainer
     from emulate import emulated
 
     nb = 64
     data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=128, n_test=64, seed=0)
+    torch.manual_seed(0)
     init = build_model(name).state_dict()
-    grads = {}
+    grads, stats = {}, {}
     for kind in ("native", "emulated"):
         cfg = TrainerConfig(batch_size=nb, augment=False, use_graph=False)
         if kind == "native":
@@ -117,16 +129,29 @@ def test_native_matches_emulated_kernels_on_gpu(gpu_device, name, avg_cos):
                 tr = CNNNativeTrainer(name, data, gpu_device, cfg, init_state=init)
                 tr.grads_for_batch(0, nb)
         torch.cuda.synchronize()
-        grads[kind] = ({k: p.grad.clone() for k, p in tr.model.named_parameters()}, tr.train_stats())
-    (gn, sn), (ge, se) = grads["native"], grads["emulated"]
-    assert abs(sn.loss - se.loss) < 5e-3 * se.loss
-    # bf16 at random init: two runs of the SAME engine differ by ~20 % in the gradient (fp32
-    # atomics reorder -> bf16 rounding flips -> BN amplification; tools/diag_graph.py), so
-    # only the head is compared tightly and the rest on average
-    names = list(gn)
-    for k in ("linear.weight", "linear.bias"):
-        assert _cos(gn[k], ge[k]) > 0.99, k
-    assert sum(_cos(gn[k], ge[k]) for k in names) / len(names) > avg_cos
+        grads[kind] = {k: p.grad.detach().float().clone() for k, p in tr.model.named_parameters()}
+        stats[kind] = tr.train_stats()
+    x = augment_normalize(data.train.x[:nb], None, 0, 0)
+    y = data.train.y[:nb].long()
+    for kind in ("fp32", "bf16"):
+        ref = build_model(name).to(gpu_device)
+        ref.load_state_dict(init)
+        ref.train()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=kind == "bf16"):
+            loss = F.cross_entropy(ref(x), y)
+        loss.backward()
+        grads[kind] = {k: p.grad.detach().float().clone() for k, p in ref.named_parameters()}
+    assert abs(stats["native"].loss - stats["emulated"].loss) < 5e-3 * stats["emulated"].loss
+    names = list(grads["native"])
+    cn = {k: _cos(grads["native"][k], grads["fp32"][k]) for k in names}
+    cb = {k: _cos(grads["bf16"][k], grads["fp32"][k]) for k in names}
+    bad = {k: (round(cn[k], 3), round(cb[k], 3)) for k in names if cn[k] < cb[k] - GRAD_MARGIN[name]}
+    assert not bad, bad
+    assert sum(cn.values()) / len(names) > sum(cb.values()) / len(names) - 0.03
+    tail = ["linear.weight", "linear.bias"] + (["layer4.1.bn2.weight", "layer4.1.bn2.bias"] if name == "ResNet18"
+                                               else ["bn2.weight", "bn2.bias"])
+    for k in tail:
+        assert cn[k] > 0.99 and _cos(grads["native"][k], grads["emulated"][k]) > 0.99, (k, cn[k])
 
 
 @pytest.mark.parametrize("name", ["ResNet18", "MobileNet", "VGG11", "PreActResNet18", "GoogLeNet"])

@@ -74,6 +74,18 @@ def _worker(rank, world, port, q):
     i8.flat.add_(delta)
     FedAvg(compressor=c3).average(i8)
     out["int8"] = i8.flat.clone()
+    # warm-up: the first aggregation is dense FedAvg (full delta, residual empty), the second is top-k
+    wu = _Stub(rank)
+    wu.flat.copy_(anchor)
+    c4 = TopKCompressor(wu, ratio=0.1, warmup=1)
+    wu.flat.add_(delta)
+    FedAvg(compressor=c4).average(wu)
+    out["warm_dense"] = wu.flat.clone()
+    out["warm_resid0"] = float(c4.residual.abs().sum())
+    wu.flat.add_(delta)
+    FedAvg(compressor=c4).average(wu)
+    out["warm_resid1"] = float(c4.residual.abs().sum())
+    out["warm_rounds"] = (c4.dense_rounds, c4.rounds)
     # tensors travel by value (numpy pickles): torch's fd-sharing reducer races the worker's exit
     q.put((rank, {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in out.items()}))
     dist.destroy_process_group()
@@ -105,3 +117,7 @@ def test_fedavg_gloo_two_ranks():
         delta_mean = torch.linspace(-1, 1, n) * 1.5
         assert (res[r]["int8"] - (a + delta_mean)).abs().max() < 2.0 / 127 + 1e-6
     assert torch.equal(res[0]["int8"], res[1]["int8"])
+    for r in (0, 1):
+        assert torch.allclose(res[r]["warm_dense"], a + torch.linspace(-1, 1, a.numel()) * 1.5, atol=1e-5)
+        assert res[r]["warm_resid0"] == 0 and res[r]["warm_resid1"] > 0
+        assert tuple(res[r]["warm_rounds"]) == (1, 2)

@@ -34,10 +34,7 @@ def test_lenet_step_launches_only_fedmi_kernels(gpu_device):
     assert names, "profiler saw no kernels"
     bad = [n for n in names if any(f in n for f in FOREIGN)]
     assert not bad, bad[:10]
-    if tr.engine.sample_path():
-        assert any("lenet_sample_step" in n for n in names) and any("lenet_sgd2" in n for n in names), set(names)
-    else:
-        assert any("lenet_fwd_head" in n for n in names) and any("lenet_conv_bwd" in n for n in names), set(names)
+    assert any("lenet_sample_step" in n for n in names) and any("lenet_sgd2" in n for n in names), set(names)
 
 
 @pytest.mark.parametrize("name", ["SimpleDLA", "RegNetX_200MF"])

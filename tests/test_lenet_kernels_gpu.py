@@ -1,11 +1,12 @@
 """Numerics of the fused LeNet HIP kernels vs a plain PyTorch fp32 reference.
 
-Every kernel (K1 conv fwd, K2 FC head fwd+CE+bwd, K3 conv bwd, K4 SGD+pack,
-the pack kernel and the graph-replayed epoch) is checked against the same op
-computed by ``fedmi.models.small.LeNet`` in fp32 with autograd, on the same
-augmented inputs (the host twin of the device RNG, fedmi.engine.data.hash3).
-The kernels take bf16 MFMA operands with fp32 accumulation, so tolerances are
-relative-L2 at the bf16 level.
+The training step (KS1 lenet_sample_step + KS2 lenet_sgd2), the eval kernels
+(lenet_conv_fwd, lenet_fc_eval, lenet_eval_stats), the pack kernel and the
+graph-replayed epoch are checked against the same op computed by
+``fedmi.models.small.LeNet`` in fp32 (autograd or the explicit backward math),
+on the same augmented inputs (the host twin of the device RNG,
+fedmi.engine.data.hash3).  The kernels take bf16 MFMA operands with fp32
+accumulation, so tolerances are relative-L2 at the bf16 level.
 """
 import numpy as np
 import pytest
@@ -46,29 +47,33 @@ def _stream():
     return native.stream_handle()
 
 
-def _run_grad(nat, tr, start, nb, augment, fused=False):
-    """K1+K2+K3 via the raw entry points; returns (flat grad, stats).  ``fused``: fc1 inside the tail."""
+def _forward_oracle(nat, tr, start, nb, augment):
+    """The eval conv stack (lenet_conv_fwd) in "train" mode over the batch: act2 / pool1 / argmax codes
+    (KS1 computes the same forward with the same MFMA order, so its argmaxes are these)."""
     L = tr.L
-    tr.stats.zero_()
-    tr.conv_slab.zero_()
-    tr.fc_slab.zero_()
-    tr.fc1w_grad.zero_()
-    s = _stream()
-    nat.lenet_conv_fwd(s, tr.train_set.x.data_ptr(), start, nb, tr.pk.data_ptr(), tr.params.data_ptr(), SEED,
-                       tr.round_ctr.data_ptr(), int(augment), tr.act2.data_ptr(), tr.act2T.data_ptr(),
-                       L["MAX_TRAIN_BATCH"], tr.pool1.data_ptr(), tr.am1.data_ptr(), tr.am2.data_ptr(),
-                       tr.stats[0].data_ptr())
-    labels = tr.train_set.y[start:]
-    nat.lenet_fc_head(s, tr.act2.data_ptr(), labels.data_ptr(), nb, 1, tr.pk.data_ptr(), tr.params.data_ptr(),
-                      0 if fused else tr.h1.data_ptr(), tr.dact2.data_ptr(), tr.dZ1T.data_ptr(),
-                      tr.fc_slab.data_ptr(), tr.stats[0].data_ptr())
-    nat.lenet_conv_bwd(s, tr.train_set.x.data_ptr(), start, nb, SEED, tr.round_ctr.data_ptr(), int(augment),
-                       tr.dact2.data_ptr(), tr.act2T.data_ptr(), tr.dZ1T.data_ptr(), tr.pool1.data_ptr(),
-                       tr.am1.data_ptr(), tr.am2.data_ptr(), tr.pk.data_ptr(), tr.conv_slab.data_ptr(),
-                       tr.fc1w_grad.data_ptr())
+    dev = tr.params.device
+    pool1 = torch.zeros(nb, L["NP1"], dtype=torch.bfloat16, device=dev)
+    am1 = torch.zeros(nb, L["NP1"], dtype=torch.uint8, device=dev)
+    am2 = torch.zeros(nb, L["F0"], dtype=torch.uint8, device=dev)
+    act2T = torch.zeros(L["F0P"], L["MAX_TRAIN_BATCH"], dtype=torch.bfloat16, device=dev)
+    nat.lenet_conv_fwd(_stream(), tr.train_set.x.data_ptr(), start, nb, tr.pk.data_ptr(), tr.params.data_ptr(), SEED,
+                       tr.round_ctr.data_ptr(), int(augment), tr.act2.data_ptr(), act2T.data_ptr(),
+                       L["MAX_TRAIN_BATCH"], pool1.data_ptr(), am1.data_ptr(), am2.data_ptr(), 0)
     torch.cuda.synchronize()
-    nfc = (nb + L["FC_SPW"] - 1) // L["FC_SPW"]
-    g = torch.cat([tr.conv_slab[:nb].sum(0), tr.fc1w_grad, tr.fc_slab[:nfc].sum(0)])
+    return tr.act2[:nb, :400].float().clone(), pool1, am1, am2
+
+
+def _step_grad(tr, start, nb):
+    """KS1 + KS2 for one batch from zero momentum; returns (flat grad, stats row).  The gradient is
+    recovered from the SGD update: p = p0 - lr * (g + wd * p0)."""
+    lr, wd = tr.cfg.lr, tr.cfg.weight_decay
+    tr.mom.zero_()
+    tr.stats.zero_()
+    p0 = tr.params.clone()
+    tr.train_step(start, nb)
+    torch.cuda.synchronize()
+    g = (p0.double() - tr.params.double()) / lr - wd * p0.double()
+    assert rel(tr.mom.double(), g + wd * p0.double()) < 1e-4   # momentum buffer = d of the first step
     return g, tr.stats[0].clone()
 
 
@@ -188,27 +193,22 @@ def _unpool(g, codes, h, w):
     return out.view(n, c, 2 * h, 2 * w)
 
 
-@pytest.mark.parametrize("fused", [False, True], ids=["fc1-kernel", "fc1-in-tail"])
 @pytest.mark.parametrize("start,nb,augment", [(0, 128, True), (256, 128, False), (896, 80, True), (128, 33, True)])
-def test_step_stagewise_matches_torch(env, start, nb, augment, fused):
-    """K2 and K3 vs fp32 torch math fed with the kernels' own saved forward tensors.
-
-    Using K1's act2/pool1/argmax as inputs removes argmax/ReLU flips, so the only
-    remaining differences are fp32 summation order: tight tolerances.
-    """
+def test_step_matches_torch_math(env, start, nb, augment):
+    """KS1 + KS2 gradients vs fp32 torch math (the explicit backward at the kernels' bf16 rounding
+    points: H1, H2, dZ3, dZ2, dZ1, the conv out-grads) fed with the eval conv stack's saved forward
+    tensors -- no argmax / ReLU flips, so only fp32 summation order differs: tight per-tensor bounds.
+    Also the step's loss sum and correct count."""
     nat, dev, ds, ref, tr = env
     tr.load_state_dict(ref.state_dict())
     tr.round_ctr.zero_()
-    g, stats = _run_grad(nat, tr, start, nb, augment, fused=fused)
-    L = tr.L
+    X, pool1, am1, am2 = _forward_oracle(nat, tr, start, nb, augment)
+    g, stats = _step_grad(tr, start, nb)
     sd = {k: v.float() for k, v in ref.state_dict().items()}
     W1, W2, W3 = _bf(sd["fc1.weight"]), _bf(sd["fc2.weight"]), _bf(sd["fc3.weight"])
-    X = tr.act2[:nb, :400].float()
     y = ds.train.y[start:start + nb].long()
-    # ---- K2: FC head, kernel rounding points (H1, H2, dZ3, dZ2, dZ1 in bf16)
+    # ---- FC head at the kernels' rounding points
     h1 = _bf(torch.relu(X @ W1.t() + sd["fc1.bias"]))
-    if not fused:   # the fused tail keeps H1 in LDS
-        assert rel(tr.h1[:nb, :120].float(), h1) < 1e-2
     h2 = _bf(torch.relu(h1 @ W2.t() + sd["fc2.bias"]))
     z = h2 @ W3.t() + sd["fc3.bias"]
     dz = (torch.softmax(z, 1) - F.one_hot(y, 10).float()) / nb
@@ -227,30 +227,27 @@ def test_step_stagewise_matches_torch(env, start, nb, augment, fused):
     assert int(st[2]) == nb
     assert abs(float(st[0:1].view(torch.float32)) - loss) < 1e-3 * max(1.0, abs(loss))
     assert abs(int(st[1]) - int((z.argmax(1) == y).sum())) <= 1
-    dz1k = tr.dZ1T[:120, :nb].float().t()
-    assert rel(dz1k, dz1b) < 1e-2
-    assert tr.dZ1T[:, nb:].abs().sum().item() == 0                       # K-padding of the fc1 wgrad
-    assert rel(tr.dact2[:nb], (dz1k @ W1) * (X > 0)) < 1e-2
-    # ---- K3: conv backward from the kernel's d(pool2), pool1 and argmax codes
+    # ---- conv backward from d(pool2) and the saved pool1 / argmax codes
+    dX = (dz1b @ W1) * (X > 0)                                            # d(pool2)  [nb, 400]
     C2W, C1W = _bf(sd["conv2.weight"]), _bf(sd["conv1.weight"])
-    dxf = tr.dact2[:nb].clone()                                          # d(pool2)  [nb, 400]
-    dY2 = _unpool(dxf.view(nb, 16, 5, 5), tr.am2[:nb].view(nb, 16, 5, 5), 5, 5)
-    p1 = tr.pool1[:nb].float().view(nb, 6, 14, 14)
+    dY2 = _unpool(dX.view(nb, 16, 5, 5), am2.view(nb, 16, 5, 5), 5, 5)
+    p1 = pool1.float().view(nb, 6, 14, 14)
     dW2 = torch.nn.grad.conv2d_weight(p1, C2W.shape, _bf(dY2))
     dP1 = torch.nn.grad.conv2d_input(p1.shape, C2W, _bf(dY2)) * (p1 > 0)
-    dY1 = _unpool(dP1, tr.am1[:nb].view(nb, 6, 14, 14), 14, 14)
+    dY1 = _unpool(dP1, am1.view(nb, 6, 14, 14), 14, 14)
     gidx = np.arange(start, start + nb) if augment else None
     xin = _bf(augment_normalize(ds.train.x[start:start + nb], gidx, SEED, 0))
     dW1 = torch.nn.grad.conv2d_weight(xin, C1W.shape, _bf(dY1))
-    exp_conv = {"conv1.weight": dW1, "conv1.bias": dY1.sum((0, 2, 3)),
-                "conv2.weight": dW2, "conv2.bias": dY2.sum((0, 2, 3))}
-    exp = {**exp_conv, **exp_fc}
+    exp = {"conv1.weight": dW1, "conv1.bias": dY1.sum((0, 2, 3)),
+           "conv2.weight": dW2, "conv2.bias": dY2.sum((0, 2, 3)), **exp_fc}
     off = 0
     for name, shape in LENET_SPEC:
         k = int(np.prod(shape))
         e = rel(g[off:off + k], exp[name].reshape(-1))
         assert e < 2e-2, f"{name}: rel err {e:.3e}"
         off += k
+    tr.load_state_dict(ref.state_dict())
+    tr.mom.zero_()
 
 
 @pytest.mark.parametrize("start,nb", [(0, 128), (896, 80)])
@@ -259,40 +256,26 @@ def test_step_end_to_end_vs_fp32_autograd(env, start, nb):
     nat, dev, ds, ref, tr = env
     tr.load_state_dict(ref.state_dict())
     tr.round_ctr.zero_()
-    g, stats = _run_grad(nat, tr, start, nb, True)
+    g, stats = _step_grad(tr, start, nb)
     gr, out, loss, y = _ref_grad(ref, ds, start, nb, True)
     assert rel(g, gr) < 0.25
     assert abs(float(stats.cpu()[0:1].view(torch.float32)) / nb - loss.item()) < 2e-2 * max(1.0, loss.item())
+    tr.load_state_dict(ref.state_dict())
+    tr.mom.zero_()
 
 
-def test_sgd_kernel_exact(env):
+def test_step_is_deterministic(env):
+    """Two identical steps give bit-identical parameters, momentum and stats (every cross-wave and
+    cross-sample sum is fixed-order: the conv1 bias partials of the 7 dgrad waves, the slab combine,
+    the FC GEMM tiles, the loss)."""
     nat, dev, ds, ref, tr = env
-    L = tr.L
-    torch.manual_seed(5)
-    p0 = torch.randn(L["P_TOTAL"], device=dev)
-    m0 = torch.randn(L["P_TOTAL"], device=dev) * 0.1
-    tr.params.copy_(p0)
-    tr.mom.copy_(m0)
-    nb = 100
-    nfc = 7
-    tr.conv_slab.normal_()
-    tr.fc_slab.normal_()
-    tr.fc1w_grad.normal_()
-    nat.lenet_sgd(_stream(), tr.params.data_ptr(), tr.mom.data_ptr(), tr.pk.data_ptr(), tr.conv_slab.data_ptr(), nb,
-                  tr.fc1w_grad.data_ptr(), tr.fc_slab.data_ptr(), nfc, 0.1, 0.9, 5e-4, 0)
-    torch.cuda.synchronize()
-    g = torch.cat([tr.conv_slab[:nb].double().sum(0), tr.fc1w_grad.double(), tr.fc_slab[:nfc].double().sum(0)])
-    d = g + 5e-4 * p0.double()
-    b = 0.9 * m0.double() + d
-    p = p0.double() - 0.1 * b
-    assert torch.allclose(tr.mom.double(), b, rtol=1e-5, atol=1e-5)
-    assert torch.allclose(tr.params.double(), p, rtol=1e-5, atol=1e-5)
-    # packed images follow the master weights
-    pk = tr.pk.float()
-    w1 = tr.params[:450].view(6, 3, 5, 5).bfloat16().float()
-    w1c = pk[:16 * 128].view(16, 128)
-    assert torch.equal(w1c[:6, 0:3], w1[:, :, 0, 0])      # group (r=0, s=0..1), channels 0..2
-    assert torch.equal(w1c[:6, 4:7], w1[:, :, 0, 1])
+    res = []
+    for _ in range(2):
+        tr.load_state_dict(ref.state_dict())
+        tr.round_ctr.zero_()
+        res.append(_step_grad(tr, 128, 128) + (tr.params.clone(),))
+    (g0, s0, p0), (g1, s1, p1) = res
+    assert torch.equal(p0, p1) and torch.equal(s0, s1)
     tr.load_state_dict(ref.state_dict())
     tr.mom.zero_()
 
@@ -348,132 +331,3 @@ def test_training_converges(env):
     ev = tr.eval_stats()
     assert ev.count == len(ds.test.y)
     assert ev.acc > 12.0 and accs[-1] > accs[0] + 5.0, (ev, accs)
-
-
-@pytest.mark.parametrize("use_graph", [True, False], ids=["graph", "eager"])
-def test_fused_bwd_sgd_matches_separate_kernels(env, use_graph):
-    """K34 (conv backward + SGD in one launch, producer flags -> SGD workgroups) trains like K3 then K4,
-    across steps (flag generations) and rounds (augmentation counter bumped once per round)."""
-    nat, dev, ds, ref, tr = env
-    starts, sizes = [0, 128, 384, 896], [128, 128, 33, 80]
-    res = []
-    tr.engine.set_sample_path(False)
-    for fuse in (False, True):
-        tr.engine.set_fuse_head(True)
-        tr.engine.set_fuse_sgd(fuse)
-        assert tr.engine.fuse_sgd() == fuse
-        tr.load_state_dict(ref.state_dict())
-        tr.mom.zero_()
-        tr.round_ctr.zero_()
-        tr.stats.zero_()
-        tr.round_idx = 0
-        tr.cfg.use_graph = use_graph
-        tr.set_schedule(starts, sizes)
-        for _ in range(2):
-            tr.train_epoch()
-        torch.cuda.synchronize()
-        res.append((tr.params.clone(), tr.mom.clone(), tr.train_stats(), int(tr.stats[0][3]),
-                    int(tr.round_ctr[0])))
-    (p0, m0, s0, e0, r0), (p1, m1, s1, e1, r1) = res
-    assert e0 == 0 and e1 == 0, "hand-off timed out"
-    assert r0 == r1 == 2
-    assert s0.count == s1.count == sum(sizes) and s0.correct == s1.correct
-    assert abs(s0.loss_sum - s1.loss_sum) <= 1e-4 * abs(s0.loss_sum)
-    assert rel(p1, p0) < 1e-5 and rel(m1, m0) < 1e-5   # only the LDS-atomic order of K3's bias sums differs
-    tr.engine.set_fuse_sgd(False)
-    tr.engine.set_sample_path(True)
-
-
-@pytest.mark.parametrize("use_graph", [True, False], ids=["graph", "eager"])
-def test_fused_fwd_head_matches_separate_kernels(env, use_graph):
-    """K12 (conv stack + FC head in one launch, flag hand-off) trains exactly like K1 then K2b."""
-    nat, dev, ds, ref, tr = env
-    starts, sizes = [0, 128, 384, 896], [128, 128, 33, 80]      # full and partial batches
-    res = []
-    tr.engine.set_sample_path(False)
-    for fuse in (False, True):
-        tr.engine.set_fuse_head(fuse)
-        tr.load_state_dict(ref.state_dict())
-        tr.mom.zero_()
-        tr.round_ctr.zero_()
-        tr.round_idx = 0
-        tr.cfg.use_graph = use_graph
-        tr.set_schedule(starts, sizes)
-        tr.train_epoch()
-        torch.cuda.synchronize()
-        res.append((tr.params.clone(), tr.train_stats(), int(tr.stats[0][3])))
-    (p0, s0, e0), (p1, s1, e1) = res
-    assert e1 == 0, "K12 hand-off timed out"
-    assert s0.count == s1.count == sum(sizes) and s0.correct == s1.correct
-    assert abs(s0.loss_sum - s1.loss_sum) <= 1e-4 * abs(s0.loss_sum)
-    assert rel(p1, p0) < 1e-5          # only the LDS-atomic order of K3's bias sums differs
-    tr.engine.set_fuse_head(True)
-    tr.engine.set_sample_path(True)
-    tr.cfg.use_graph = True
-    tr.load_state_dict(ref.state_dict())
-    tr.mom.zero_()
-
-
-@pytest.mark.parametrize("start,nb", [(0, 128), (896, 80), (128, 33)])
-def test_sample_step_gradients_match_head_kernels(env, start, nb):
-    """KS1 + KS2 (one workgroup per sample, batched FC-gradient GEMMs) compute the same gradients as
-    K1 + K2 + K3 (per-tensor rel. L2 at the bf16 level: the FC GEMVs sum in a different order and a
-    bf16 rounding of an intermediate may land one ulp apart), the same loss and accuracy."""
-    nat, dev, ds, ref, tr = env
-    tr.load_state_dict(ref.state_dict())
-    tr.round_ctr.zero_()
-    g_head, st_head = _run_grad(nat, tr, start, nb, True, fused=True)
-    lr, wd = tr.cfg.lr, tr.cfg.weight_decay
-    tr.engine.set_sample_path(True)
-    tr.load_state_dict(ref.state_dict())
-    tr.mom.zero_()
-    tr.stats.zero_()
-    p0 = tr.params.clone()
-    tr.train_step(start, nb)                    # momentum buffer 0: p = p0 - lr * (g + wd * p0)
-    torch.cuda.synchronize()
-    g = (p0.double() - tr.params.double()) / lr - wd * p0.double()
-    off = 0
-    for name, shape in LENET_SPEC:
-        k = int(np.prod(shape))
-        e = rel(g[off:off + k], g_head[off:off + k])
-        assert e < 1e-2, f"{name}: rel err {e:.3e}"
-        off += k
-    st, sh = tr.stats[0].cpu(), st_head.cpu()
-    assert int(st[2]) == nb
-    assert abs(int(st[1]) - int(sh[1])) <= 1
-    ls, lh = float(st[0:1].view(torch.float32)), float(sh[0:1].view(torch.float32))
-    assert abs(ls - lh) < 1e-3 * max(1.0, abs(lh))
-    assert rel(tr.mom.double(), g + wd * p0.double()) < 1e-4   # g is recovered from fp32 params
-    tr.load_state_dict(ref.state_dict())
-    tr.mom.zero_()
-
-
-@pytest.mark.parametrize("use_graph", [True, False], ids=["graph", "eager"])
-def test_sample_path_trains_like_head_path(env, use_graph):
-    """Two epochs of full and partial batches: the per-sample path and K12 -> K3 -> K4 stay together."""
-    nat, dev, ds, ref, tr = env
-    starts, sizes = [0, 128, 384, 896], [128, 128, 33, 80]
-    res = []
-    for sample in (False, True):
-        tr.engine.set_sample_path(sample)
-        tr.load_state_dict(ref.state_dict())
-        tr.mom.zero_()
-        tr.round_ctr.zero_()
-        tr.stats.zero_()
-        tr.round_idx = 0
-        tr.cfg.use_graph = use_graph
-        tr.set_schedule(starts, sizes)
-        for _ in range(2):
-            tr.train_epoch()
-        torch.cuda.synchronize()
-        res.append((tr.params.clone(), tr.train_stats(), int(tr.round_ctr[0])))
-    (p0, s0, r0), (p1, s1, r1) = res
-    init = torch.cat([v.detach().reshape(-1).float() for v in ref.state_dict().values()])
-    assert r0 == r1 == 2
-    assert s0.count == s1.count == sum(sizes) and abs(s0.correct - s1.correct) <= 2
-    assert abs(s0.loss_sum - s1.loss_sum) <= 2e-3 * abs(s0.loss_sum)
-    assert rel(p1 - init, p0 - init) < 5e-2      # 8 SGD steps of bf16-level differences
-    tr.engine.set_sample_path(True)
-    tr.cfg.use_graph = True
-    tr.load_state_dict(ref.state_dict())
-    tr.mom.zero_()

@@ -2,12 +2,12 @@
 # Host-side AddressSanitizer + UndefinedBehaviorSanitizer build of the native LeNet runtime driver
 # (SURVEY.md §5.2).  Only the host code is instrumented: every -fsanitize= sits behind -Xarch_host, the
 # gfx950 device code is compiled normally.  Run on the GPU box with
-#   ASAN_OPTIONS=verify_asan_link_order=0:detect_leaks=0 ./build/asan/lenet_engine_asan
+#   ASAN_OPTIONS=verify_asan_link_order=0:detect_leaks=0 ./tools/asan/bin/lenet_engine_asan
 # (verify_asan_link_order=0: the box preloads a small library of its own; leaks: the HIP runtime keeps
 # process-lifetime allocations).
 set -eu
 cd "$(dirname "$0")/../.."
-out=build/asan
+out=tools/asan/bin
 mkdir -p "$out"
 SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"
 HIPCC=/opt/rocm/bin/hipcc

@@ -62,23 +62,16 @@ int main() {
   b.act2 = dalloc<bf16>((size_t)rows * F0P);
   b.act2_rows = rows;
   b.act2T = dalloc<bf16>((size_t)F0P * MAX_TRAIN_BATCH);
-  b.h1 = dalloc<bf16>((size_t)(rows + 16) * 128);
-  b.pool1 = dalloc<bf16>((size_t)MAX_TRAIN_BATCH * NP1);
-  b.am1 = dalloc<uint8_t>((size_t)MAX_TRAIN_BATCH * NP1);
-  b.am2 = dalloc<uint8_t>((size_t)MAX_TRAIN_BATCH * F0);
+  b.h1 = dalloc<bf16>((size_t)MAX_TRAIN_BATCH * 128);
   b.dact2 = dalloc<float>((size_t)MAX_TRAIN_BATCH * F0);
   b.dZ1T = dalloc<bf16>((size_t)DZ1_LD * MAX_TRAIN_BATCH);
   b.conv_slab = dalloc<float>((size_t)MAX_TRAIN_BATCH * CS);
-  b.fc1w_grad = dalloc<float>(F1W_N);
-  b.fc_slab = dalloc<float>((size_t)MAX_FC_WG * FS);
+  b.eval_part_floats = 2L * ((rows + FC_SPW - 1) / FC_SPW);
+  b.eval_part = dalloc<float>((size_t)b.eval_part_floats);
   Stats* stats = dalloc<Stats>(2);
   b.train_stats = stats;
   b.eval_stats = stats + 1;
   b.round_ctr = dalloc<int>(4);
-  b.done_flags = dalloc<int>(MAX_TRAIN_BATCH);
-  b.step_gen = dalloc<int>(4);
-  b.bwd_flags = dalloc<int>(MAX_TRAIN_BATCH + N_DW1_WG);
-  b.bwd_gen = dalloc<int>(4);
 
   // small random weights
   std::vector<float> p0(P_TOTAL);
@@ -94,16 +87,11 @@ int main() {
     try { eng.set_schedule({0, 128}, {128}); expect(false, "length mismatch accepted"); } catch (const std::invalid_argument&) {}
     try { eng.step(st, n_train - 10, 64, false); expect(false, "out-of-range batch accepted"); } catch (const std::invalid_argument&) {}
     eng.set_schedule({0, 128, 384, 896}, {128, 128, 33, 80});
-    struct Mode { bool sample, head, sgd; };
-    const Mode modes[] = {{true, true, false}, {false, true, false}, {false, false, false}, {false, true, true},
-                          {true, true, false}};
-    for (const Mode& m : modes) {
-      eng.set_sample_path(m.sample);
-      eng.set_fuse_head(m.head);
-      eng.set_fuse_sgd(m.sgd);
+    for (int rep = 0; rep < 2; ++rep) {       // eager and graph epochs, graph re-capture after a new schedule
       for (int use_graph = 0; use_graph < 2; ++use_graph)
         for (int ep = 0; ep < 2; ++ep) eng.run_epoch(st, use_graph != 0);
       eng.eval(st, images, labels, n_test);
+      eng.set_schedule({0, 128, 384, 896}, {128, 128, 33, 80});
     }
     eng.set_schedule({}, {});
     eng.run_epoch(st, true);           // a rank that owns no batch this round

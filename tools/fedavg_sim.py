@@ -34,14 +34,15 @@ def main() -> int:
     ap.add_argument("--clients", type=int, default=2)
     ap.add_argument("--noniid", type=int, default=0, help="label shards per client (0 = strided IID)")
     ap.add_argument("--rounds", type=int, default=8)
-    ap.add_argument("--engine", choices=["native", "fp32"], default="native")
+    ap.add_argument("--engine", choices=["native", "fp32", "bf16"], default="native",
+                    help="bf16: PyTorch autocast bf16 (torch's own mixed precision of the same model)")
     ap.add_argument("--n-train", type=int, default=N_TRAIN)
     ap.add_argument("--n-test", type=int, default=N_TEST)
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--out", default=None, help="JSONL, one record per round")
     a = ap.parse_args()
-    if a.engine == "fp32":
+    if a.engine in ("fp32", "bf16"):
         os.environ["FEDMI_TORCH_PATH"] = "1"
 
     from fedmi.engine import build_trainer
@@ -56,6 +57,11 @@ def main() -> int:
     init = None
     for r in range(W):
         tr = build_trainer(a.model, data, dev, cfg, init_state=init)
+        if a.engine == "bf16":
+            def run(x, m=tr.model):
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    return m(x).float()
+            tr._run = run
         if init is None:        # one shared init (rank-0 broadcast, reference quirk A7 fixed)
             init = {k: v.detach().cpu().clone() for k, v in tr.state_dict().items()}
         if a.noniid > 0:
