@@ -40,7 +40,6 @@ void launch_conv_pack_multi(hipStream_t, const PackItem*, int);
 void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int);
 long conv_wgrad_ws_floats(const ConvShape&);
 void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int);
-void set_conv_halo_stamps(long long*);
 
 struct BNDesc {
   const double* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
@@ -62,16 +61,15 @@ struct BNBwdDesc {
 struct DwShape {
   int N, H, W, C, R, S, st, pad;
 };
-void launch_dw_fwd(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, double*, const float*, const float*);
+void launch_dw_fwd(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, double*, const float*);
 void launch_dw_dgrad(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, const BnSums*);
 long dw_wgrad_ws_floats(const DwShape&);
-void launch_dw_wgrad(hipStream_t, const DwShape&, const bf16*, const bf16*, float*, float*, long, int, const float*);
+void launch_dw_wgrad(hipStream_t, const DwShape&, const bf16*, const bf16*, float*, float*, long, int);
 void launch_prep_input(hipStream_t, const uint8_t*, int, const int*, int, int, uint32_t, const int*, bf16*);
 void launch_sched_next(hipStream_t, const int*, int*, int*);
 void launch_bn_apply(hipStream_t, const bf16*, const BNDesc&, const bf16*, const BNDesc*, const bf16*, bf16*, int, int,
                      float, float, int, int, int, float*);
 void launch_bn_bwd(hipStream_t, const BNBwdDesc&, double*, int, int, double*, long, int, int, int, int);
-void launch_bn_coeff(hipStream_t, const BNDesc&, int, int, float, float, int, float*);
 long bn_bwd_ws_floats(int, int);
 int bn_bwd_chain_reps(int);
 void launch_head(hipStream_t, const bf16*, const int*, int, const int*, int, int, int, int, const float*,
@@ -127,8 +125,6 @@ BNDesc bn_from(const py::dict& d) {
 
 void fedmi_bind_cnn(py::module_& m) {
   m.attr("STAT_REP") = STAT_REP;
-  // diagnostic: conv_halo writes 8 int64 per workgroup (see the kernel) into this device buffer; 0 = off
-  m.def("conv_halo_stamps", [](uintptr_t p) { set_conv_halo_stamps(reinterpret_cast<long long*>(p)); });
   m.def("conv_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                        uintptr_t shift, uintptr_t ws, long ws_floats, uintptr_t res) {
     launch_conv_fwd(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(w), P<bf16>(y), P<double>(stats),
@@ -184,12 +180,11 @@ void fedmi_bind_cnn(py::module_& m) {
     check("conv_pack");
   });
   m.def("dw_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
-                     uintptr_t shift, uintptr_t isc) {
+                     uintptr_t shift) {
     launch_dw_fwd(S(st), dw_from(shp), P<const bf16>(x), P<const float>(w), P<bf16>(y), P<double>(stats),
-                  P<const float>(shift), P<const float>(isc));
+                  P<const float>(shift));
     check("dw_fwd");
-  }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("shift"),
-     py::arg("isc") = 0);
+  }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("shift"));
   m.def("dw_dgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t dy, uintptr_t w, uintptr_t dx,
                        py::object bsum) {
     BnSums bs{};
@@ -200,12 +195,12 @@ void fedmi_bind_cnn(py::module_& m) {
   }, py::arg("st"), py::arg("shp"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("bsum") = py::none());
   m.def("dw_wgrad_ws_floats", [](const py::tuple& shp) { return dw_wgrad_ws_floats(dw_from(shp)); });
   m.def("dw_wgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws,
-                       long ws_floats, int accumulate, uintptr_t isc) {
+                       long ws_floats, int accumulate) {
     launch_dw_wgrad(S(st), dw_from(shp), P<const bf16>(x), P<const bf16>(dy), P<float>(dw), P<float>(ws), ws_floats,
-                    accumulate, P<const float>(isc));
+                    accumulate);
     check("dw_wgrad");
   }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ws"), py::arg("ws_floats"),
-     py::arg("accumulate"), py::arg("isc") = 0);
+     py::arg("accumulate"));
   m.def("prep_input", [](uintptr_t st, uintptr_t images, int base, uintptr_t dbase, int nb, int augment,
                          uint32_t seed, uintptr_t round_ctr, uintptr_t out) {
     launch_prep_input(S(st), P<const uint8_t>(images), base, P<const int>(dbase), nb, augment, seed,
@@ -245,10 +240,6 @@ void fedmi_bind_cnn(py::module_& m) {
   }, py::arg("st"), py::arg("z"), py::arg("a"), py::arg("z2"), py::arg("b"), py::arg("res"), py::arg("y"), py::arg("M"),
      py::arg("C"), py::arg("eps"), py::arg("mom"), py::arg("train"), py::arg("relu"), py::arg("ldy") = 0,
      py::arg("co_out") = 0);
-  m.def("bn_coeff", [](uintptr_t st, const py::dict& a, int M, int C, float eps, float mom, int train, uintptr_t co) {
-    launch_bn_coeff(S(st), bn_from(a), M, C, eps, mom, train, P<float>(co));
-    check("bn_coeff");
-  });
   m.def("bn_bwd_ws_floats", [](int M, int C) { return bn_bwd_ws_floats(M, C); });
   m.def("bn_bwd", [](uintptr_t st, const py::dict& d, uintptr_t red, int M, int C, uintptr_t ws, long ws_floats,
                      int ldd, int ldy, int chained, int presummed) {

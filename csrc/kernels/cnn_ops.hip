@@ -132,10 +132,6 @@ FEDMI_DEV void bn_coeffs(const BNArgs& a, int C, int M, float eps, float mom, in
 
 // BN scale / shift only ([2][C] fp32), with bn_apply's running-stat / saved-stat commit: for a BN whose
 // consumer applies it on load (bn_apply's output is never written).  One workgroup.
-__global__ __launch_bounds__(256) void bn_coeff_kernel(BNArgs A, int M, int C, float eps, float mom, int train,
-                                                       float* __restrict__ co) {
-  bn_coeffs(A, C, M, eps, mom, train, co, co + C);
-}
 
 // Channel-chunked grid of the apply kernels: blockIdx.y = chunk of CC <= 64 channels, blockIdx.x = chunk
 // of rows.  A block derives the BN coefficients of ITS channels only (16 fp64 replica reads x 2 per
@@ -1007,9 +1003,6 @@ void launch_bn_apply(hipStream_t st, const bf16* z, const BNDesc& a, const bf16*
   }
 }
 
-void launch_bn_coeff(hipStream_t st, const BNDesc& a, int M, int C, float eps, float mom, int train, float* co) {
-  hipLaunchKernelGGL(bn_coeff_kernel, dim3(1), dim3(256), 0, st, to_args(a), M, C, eps, mom, train, co);
-}
 
 struct BNBwdDesc {
   const bf16* dya; const bf16* dyb; const bf16* y;

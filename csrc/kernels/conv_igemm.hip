@@ -35,8 +35,6 @@
 #include <vector>
 #include <stdexcept>
 
-#include <cstdlib>
-
 #include "common.h"
 
 namespace {
@@ -456,9 +454,9 @@ FEDMI_DEV bf16x8 frag_sw(const bf16* img, int i0, int kk, int lane) {
   return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((kc ^ (row & 7)) << 3));
 }
 
-// NST = 3: the DMA runs two K steps ahead (1 workgroup per CU at BN 128, 2 at BN 64); NST = 2: classic
-// double buffer, one step ahead, half the LDS so one more workgroup fits per CU (FEDMI_TAP_STAGES=2).
-template <int BN, int NST = 3>
+// Three LDS stages, the DMA two K steps ahead (1 workgroup per CU at BN 128, 2 at BN 64); a two-stage
+// double buffer (one more workgroup per CU) measured slower and was removed.
+template <int BN>
 __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                 bf16* __restrict__ out, float* __restrict__ part,
                                                 double* __restrict__ stats, const float* __restrict__ shift,
@@ -469,7 +467,7 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
   constexpr int NB = BN / 32;
   constexpr int STAGE = (BM + BN) * 64;  // elements
   constexpr int TM = 4, TN = BN / 32;    // 16x16 fragments per wave: 64 x BN/2
-  static_assert(NST == 2 || NST == 3, "conv_tap: 2 or 3 LDS stages");
+  constexpr int NST = 3;
   // the epilogue reuses the stages for the bf16 tile and its partial sums
   constexpr int EPI = BM * (BN + 8) + 2 * 3 * 256 * 8;
   __shared__ __attribute__((aligned(16))) bf16 smem[NST * STAGE > EPI ? NST * STAGE : EPI];
@@ -540,10 +538,10 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
   // in flight), barrier (step t visible everywhere AND every wave is done reading
   // step t-1's stage), refill that stage with step t+2, then MFMAs on step t.
   if (kb < ke) issue(kb, 0);
-  if (NST == 3 && kb + 1 < ke) issue(kb + 1, 1);
+  if (kb + 1 < ke) issue(kb + 1, 1);
   for (int t = kb; t < ke; ++t) {
     const int stg = (t - kb) % NST;
-    if (NST == 3 && t + 1 < ke) {
+    if (t + 1 < ke) {
       if constexpr (NA + NB == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
@@ -552,10 +550,9 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    // NST 3: refill the stage step t-1 used with step t+2; NST 2: the same stage with step t+1 (every
-    // wave is past step t-1's reads once it passed this barrier)
-    if (NST == 3 && t + 2 < ke) issue(t + 2, (stg + 2) % NST);
-    if (NST == 2 && t + 1 < ke) issue(t + 1, stg ^ 1);
+    // refill the stage step t-1 used with step t+2 (every wave is past step t-1's reads once it
+    // passed this barrier)
+    if (t + 2 < ke) issue(t + 2, (stg + 2) % NST);
     const bf16* As = smem + stg * STAGE;
     const bf16* Bs = As + BM * 64;
 #pragma unroll
@@ -722,24 +719,9 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
 }
 
 // ---------------------------------------------------------------------------
-// Halo-patch implicit GEMM for 3x3 / stride 1 / pad 1 (FWD, and the stride-1
-// DGRAD through its flipped weight image -- also a 3x3 pad-1 convolution).
-//
-// conv_tap re-reads every input pixel once per tap: nine 128-B rows per output
-// pixel per 64-channel chunk go through L2 -> LDS, and at BN 128 that is 32 KiB
-// of LDS-DMA per 512 MFMA cycles -- more than a CU's L2 share delivers.  Here a
-// 128-pixel tile is IMGS images x TH rows x W columns, and its input window
-// (TH + 2 rows x W + 2 columns per image, zero halo) is DMA'd into LDS ONCE per
-// 64-channel chunk; the nine taps of that chunk read shifted rows of the same
-// patch.  Per K step only the weight tile streams (plus 1/7 of the next
-// chunk's patch), 16 + ~3.5 KiB instead of 32.
-//
-// Pipeline: weight tiles in NST stages, NST - 1 steps ahead; chunk c + 1's
-// whole patch is issued at tap 0 of chunk c into the other of two patch
-// buffers (its last reader, chunk c - 1, finished before that barrier), so it
-// has nine steps to land.  Every wait is a counted vmcnt over the groups still
-// allowed in flight.  BatchNorm statistics come straight from the accumulators
-// (bf16-rounded, cross-lane reduced), not from a serial pass over the tile.
+// Halo-patch geometry for 3x3 / stride 1 / pad 1: a 128-pixel tile is IMGS images x TH rows x W
+// columns whose input window (TH + 2 rows x W + 2 columns per image, zero halo) is DMA'd into LDS
+// once per 64-channel chunk; the nine taps read shifted rows of the same patch (conv_wgrad_halo).
 // ---------------------------------------------------------------------------
 struct HaloGeom {
   int N, H, W, C, O;
@@ -759,260 +741,6 @@ FEDMI_DEV void vm_wait_le(int n) {
     if (n >= N) __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
     else vm_wait_le<N - 1>(n);
   }
-}
-
-template <int BN, int PP, int NST>
-__global__ __launch_bounds__(256) void conv_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
-                                                 bf16* __restrict__ out, float* __restrict__ part,
-                                                 double* __restrict__ stats, const float* __restrict__ shift,
-                                                 HaloGeom g, int chunks_per_split, const bf16* __restrict__ res,
-                                                 long long* __restrict__ stamps) {
-  // stamps (diagnostic, null in production): per workgroup [realtime at start, memtime at start, after
-  // the prologue's data landed, after the main loop, at the end]
-  long long st0 = 0, st1 = 0, st2 = 0;
-  const long long rt0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-  if (stamps) st0 = __builtin_amdgcn_s_memtime();
-  constexpr int BM = 128;
-  constexpr int NB = BN / 32;              // weight wave-instructions per step per wave
-  constexpr int TM = 4, TN = BN / 32;
-  constexpr int PCAP = PP == 1 ? 208 : 288;   // patch rows per buffer
-  constexpr int NPS = 7 * PP;                 // patch wave-instructions per chunk per wave (<= 224 * PP rows)
-  constexpr int WST = BN * 64;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * PCAP * 64 + NST * WST + 512];
-  bf16* const wbuf = smem + 2 * PCAP * 64;
-  bf16* const dummy = wbuf + NST * WST;       // landing row block for patch slots past PCAP
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntn = (g.O + BN - 1) / BN;
-  const int tile_n = blockIdx.x % ntn, tile_m = blockIdx.x / ntn;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * (BN / 2);
-  const int HW = g.H * g.W;
-  const int img0 = fdiv(m0, g.dHW), h0 = fdiv(m0 - img0 * HW, g.dW);   // tile origin (IMGS > 1: h0 = 0)
-
-  const int c_begin = blockIdx.z * chunks_per_split;
-  const int c_end = min(g.nchunks, c_begin + chunks_per_split);
-  const int T0 = 9 * c_begin, T1 = 9 * c_end;
-
-  const int lrow = lane >> 3;
-  const int kc = (lane & 7) ^ lrow;          // logical 16-B chunk this lane's DMA carries
-  // patch slot s of this wave covers patch rows (s * 4 + wave) * 8 + [0, 8)
-  int poff[NPS];                             // input element offset of this lane's row (chunk 0), -1 = zero
-  const int per_img = (g.TH + 2) * g.PW;
-#pragma unroll
-  for (int sl = 0; sl < NPS; ++sl) {
-    const int pr = (sl * 4 + wave) * 8 + lrow;
-    const int i = fdiv(pr, g.dPI), rem = pr - i * per_img;
-    const int hh = fdiv(rem, g.dPW), ww = rem - hh * g.PW;
-    const int n = img0 + i, h = h0 - 1 + hh, w = ww - 1;
-    const bool ok = pr < g.NPR && n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-    poff[sl] = ok ? ((n * g.H + h) * g.W + w) * g.C + kc * 8 : -1;
-  }
-  long b_off[NB];
-  bool b_ok[NB];
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const int o = n0 + (wave * NB + i) * 8 + lrow;
-    b_ok[i] = o < g.O;
-    b_off[i] = (long)o * g.K + kc * 8;
-  }
-  // A fragment rows: tile pixel -> patch row at tap (0, 0)
-  int abase[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int ml = wm0 + 16 * i + (lane & 15);
-    const int thw = g.TH * g.W;
-    const int im = fdiv(ml, g.dTHW), rem = ml - im * thw;
-    const int p = fdiv(rem, g.dW), q = rem - p * g.W;
-    abase[i] = (im * (g.TH + 2) + p) * g.PW + q;
-  }
-
-  auto issue_patch = [&](int c) {   // chunk c's whole patch -> buffer c & 1
-    bf16* pb = smem + (c & 1) * PCAP * 64;
-#pragma unroll
-    for (int sl = 0; sl < NPS; ++sl) {
-      const int base = (sl * 4 + wave) * 8;
-      const void* src = poff[sl] >= 0 ? (const void*)(in + poff[sl] + c * 64) : (const void*)g_zero16;
-      glds16(src, base < PCAP ? pb + base * 64 : dummy);
-    }
-  };
-  auto issue_w = [&](int c, int j, int stage) {   // weight tile of step (c, j) -> stage
-    bf16* Bs = wbuf + stage * WST;
-    const long koff = (long)j * g.C + c * 64;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const void* src = b_ok[i] ? (const void*)(wt + b_off[i] + koff) : (const void*)g_zero16;
-      glds16(src, Bs + (wave * NB + i) * 8 * 64);
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
-
-  // DMA groups (per wave): the prologue issues chunk c_begin's patch and the weights of the first
-  // NST - 1 steps; iteration t issues the weights of step t + NST - 1 and, at a chunk's tap 0, the
-  // next chunk's whole patch.  At iteration t the groups of iterations t - NST + 2 .. t - 1 may stay
-  // in flight: NB each while they carried weights (all but the last NST - 1 iterations), plus NPS
-  // when tap 0 of this chunk is among them and a next chunk exists.
-  constexpr int STEADY = (NST - 2) * NB;
-  if (T0 < T1) {
-    issue_patch(c_begin);
-#pragma unroll
-    for (int k = 0; k < NST - 1; ++k)
-      if (T0 + k < T1) issue_w((T0 + k) / 9, (T0 + k) % 9, k);
-  }
-  int c = c_begin, j = 0;                  // step t = 9 c + j
-  int stg = 0;                             // stage holding step t
-  int wc = (T0 + NST - 1) / 9, wj = (T0 + NST - 1) % 9;   // step t + NST - 1
-  for (int t = T0; t < T1; ++t) {
-    const bool pin = j >= 1 && j <= NST - 2 && c + 1 < c_end;   // next chunk's patch in the window
-    const int tail = T1 - 1 - t;
-    if (tail >= NST - 2 && !pin) {
-      vm_wait_le<STEADY>(STEADY);
-    } else {
-      const int younger = NB * min(NST - 2, tail) + (pin ? NPS : 0);
-      vm_wait_le<STEADY + NPS>(younger);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (stamps && t == T0) st1 = __builtin_amdgcn_s_memtime();
-    if (t + NST - 1 < T1) issue_w(wc, wj, stg == 0 ? NST - 1 : stg - 1);
-    if (j == 0 && c + 1 < c_end) issue_patch(c + 1);
-    const int r = j / 3, s = j - 3 * r;
-    const int tap = r * g.PW + s;
-    const bf16* Ps = smem + (c & 1) * PCAP * 64;
-    const bf16* Bs = wbuf + stg * WST;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[TM], bfr[TN];
-      const int kq = kk * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int pr = abase[i] + tap;
-        af[i] = *reinterpret_cast<const bf16x8*>(Ps + pr * 64 + ((kq ^ (pr & 7)) << 3));
-      }
-#pragma unroll
-      for (int jj = 0; jj < TN; ++jj) bfr[jj] = frag_sw(Bs, wn0 + 16 * jj, kk, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int jj = 0; jj < TN; ++jj) acc[i][jj] = mfma16(af[i], bfr[jj], acc[i][jj]);
-    }
-    if (++j == 9) { j = 0; ++c; }
-    if (++wj == 9) { wj = 0; ++wc; }
-    if (++stg == NST) stg = 0;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();   // no DMA in flight, every wave done reading
-  if (stamps) st2 = __builtin_amdgcn_s_memtime();
-  auto put_stamps = [&]() {
-    if (stamps && tid == 0) {
-      long long* d = stamps + 8l * (blockIdx.x + (long)gridDim.x * blockIdx.z);
-      d[0] = rt0; d[1] = st0; d[2] = st1; d[3] = st2; d[4] = __builtin_amdgcn_s_memtime();
-    }
-  };
-
-  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
-  if (part != nullptr) {   // split-K partial -> [split][M][O] fp32
-    float* ws = part + (long)blockIdx.z * g.M * g.O;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wn0 + 16 * j + col_l;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = m0 + wm0 + 16 * i + row_l + e;
-          if (col < g.O) ws[(long)m * g.O + col] = acc[i][j][e];
-        }
-    }
-    put_stamps();
-    return;
-  }
-  constexpr int CT_LD = BN + 8;
-  bf16* ct = smem;
-  float* red = reinterpret_cast<float*>(smem + BM * CT_LD);   // [2 row halves][2][BN]
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        ct[(wm0 + 16 * i + row_l + e) * CT_LD + wn0 + 16 * j + col_l] = (bf16)acc[i][j][e];
-  if (stats != nullptr && res == nullptr) {
-    // sums of bf16(y) - shift over this wave's 64 rows, per column: registers, then the 4 row groups
-    // of the wave (lanes l, l^16, l^32, l^48) by cross-lane adds
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wn0 + 16 * j + col_l;
-      const float sh = (shift != nullptr && col < g.O) ? shift[col] : 0.f;
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float v = (float)(bf16)acc[i][j][e] - sh;
-          s1 += v;
-          s2 += v * v;
-        }
-      s1 += __shfl_xor(s1, 16);
-      s2 += __shfl_xor(s2, 16);
-      s1 += __shfl_xor(s1, 32);
-      s2 += __shfl_xor(s2, 32);
-      if (lane < 16) {
-        red[((wave >> 1) * 2) * BN + wn0 + 16 * j + lane] = s1;
-        red[((wave >> 1) * 2 + 1) * BN + wn0 + 16 * j + lane] = s2;
-      }
-    }
-  }
-  __syncthreads();
-  if (stats != nullptr && res == nullptr && tid < 2 * BN) {
-    const int q = tid / BN, cl = tid % BN;
-    const float tsum = red[q * BN + cl] + red[(2 + q) * BN + cl];
-    if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, (double)tsum);
-  }
-  constexpr int CPR = BN / 8;
-  for (int cidx = tid; cidx < BM * CPR; cidx += 256) {
-    const int row = cidx / CPR, cc = cidx % CPR;
-    const int m = m0 + row, col = n0 + cc * 8;
-    if (col < g.O) {
-      if (res != nullptr) {
-        bf16x8 tv = *reinterpret_cast<const bf16x8*>(ct + row * CT_LD + cc * 8);
-        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + (long)m * g.O + col);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) tv[q] = (bf16)((float)tv[q] + (float)rv[q]);
-        *reinterpret_cast<bf16x8*>(ct + row * CT_LD + cc * 8) = tv;
-      }
-      *reinterpret_cast<uint4*>(out + (long)m * g.O + col) = *reinterpret_cast<const uint4*>(ct + row * CT_LD + cc * 8);
-    }
-  }
-  if (stats != nullptr && res != nullptr) {   // statistics of y = conv + res: from the summed tile
-    __syncthreads();
-    constexpr int PARTS = 256 / BN;
-    const int col = tid % BN, prt = tid / BN;
-    const float sh = (shift != nullptr && n0 + col < g.O) ? shift[n0 + col] : 0.f;
-    float s1 = 0.f, s2 = 0.f;
-    for (int rr = prt; rr < BM; rr += PARTS) {
-      const float v = (float)ct[rr * CT_LD + col] - sh;
-      s1 += v;
-      s2 += v * v;
-    }
-    red[(prt * 2) * BN + col] = s1;
-    red[(prt * 2 + 1) * BN + col] = s2;
-    __syncthreads();
-    if (tid < 2 * BN) {
-      const int q = tid / BN, cl = tid % BN;
-      float tsum = 0.f;
-#pragma unroll
-      for (int pp = 0; pp < PARTS; ++pp) tsum += red[(pp * 2 + q) * BN + cl];
-      if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, (double)tsum);
-    }
-  }
-  put_stamps();
 }
 
 // ---------------------------------------------------------------------------
@@ -1572,14 +1300,10 @@ static TileCfg pick_tiles(int M, int NC) {
 
 // WGRAD always splits K, so the tile count never has to fill the chip: take the 128 x 128 tile
 // (twice the MFMA work per loaded byte) for O >= 256 -- measured 44 -> 38 us (256x256 3x3) and
-// 51 -> 47 us (512x512) at batch 128, but slower at O = 128.  FEDMI_WGRAD_TILE=64 restores 64 x 128.
+// 51 -> 47 us (512x512) at batch 128, but slower at O = 128.
 static TileCfg pick_tiles_wgrad(int M, int NC) {
-  static const int forced = [] {
-    const char* e = std::getenv("FEDMI_WGRAD_TILE");
-    return e ? std::atoi(e) : 0;
-  }();
   TileCfg t = pick_tiles(M, NC);
-  if (forced != 64 && M >= 256 && NC > 64) t.BM = 128;
+  if (M >= 256 && NC > 64) t.BM = 128;
   return t;
 }
 
@@ -1656,13 +1380,9 @@ static int tap_splits(const TapGeom& g, long ws_floats) {
   return (ksteps + kps - 1) / kps;
 }
 
-// conv_halo geometry for a 3x3 / stride-1 / pad-1 problem, or false (then conv_tap runs it).
-// Opt-in (FEDMI_CONV_HALO=1, read per launch so a test can flip it) until it measures faster
-// than conv_tap end to end.
-static bool halo_geom(const TapGeom& g, const RowMap& rm, HaloGeom* h, bool gate = true) {
-  const char* e = std::getenv("FEDMI_CONV_HALO");
-  const bool enabled = !gate || (e && e[0] == '1');
-  if (!enabled || rm.on || g.R != 3 || g.S != 3 || g.st != 1 || g.pad_h != 1 || g.pad_w != 1 || g.P != g.H ||
+// halo geometry of a 3x3 / stride-1 / pad-1 problem (conv_wgrad_halo), or false
+static bool halo_geom(const TapGeom& g, const RowMap& rm, HaloGeom* h) {
+  if (rm.on || g.R != 3 || g.S != 3 || g.st != 1 || g.pad_h != 1 || g.pad_w != 1 || g.P != g.H ||
       g.Q != g.W || g.C % 64 || g.O % 8 || g.M % 128)
     return false;
   const int HW = g.H * g.W;
@@ -1685,69 +1405,10 @@ static bool halo_geom(const TapGeom& g, const RowMap& rm, HaloGeom* h, bool gate
   return true;
 }
 
-static int halo_splits(const HaloGeom& h, long ws_floats) {
-  if (ws_floats <= 0 || h.O > SPLITK_MAX_NC || h.nchunks < 2) return 1;
-  const int bn = tap_bn(h.O);
-  const long tiles = (long)(h.M / 128) * ((h.O + bn - 1) / bn);
-  const long target = (bn == 128 || h.NPR > 208 ? 1l : 2l) * num_cus();
-  if (4 * tiles >= 3 * target) return 1;
-  long sp = std::min<long>((target + tiles / 2) / tiles, h.nchunks);
-  sp = std::min<long>(sp, ws_floats / ((long)h.M * h.O));
-  if (sp < 2) return 1;
-  const int cps = (int)((h.nchunks + sp - 1) / sp);
-  return (h.nchunks + cps - 1) / cps;
-}
-
-static long long* g_halo_stamps = nullptr;   // diagnostic (conv_halo_stamps binding)
-
-static void launch_halo(hipStream_t st, const HaloGeom& h, const bf16* in, const bf16* wt, bf16* out, double* stats,
-                        const float* shift, float* ws, long ws_floats, const bf16* res) {
-  const int BN = tap_bn(h.O);
-  const long tiles = (long)(h.M / 128) * ((h.O + BN - 1) / BN);
-  const int sp = halo_splits(h, ws_floats);
-  const int cps = (h.nchunks + sp - 1) / sp;
-  const int splits = (h.nchunks + cps - 1) / cps;
-  dim3 grid((unsigned)tiles, 1, (unsigned)splits);
-  float* part = splits > 1 ? ws : nullptr;
-  double* stt = part ? nullptr : stats;
-  const bf16* rs = part ? nullptr : res;
-  const bool pp2 = h.NPR > 208;
-  // BN 64 / PP 1: 3 stages keep two workgroups per CU (79 KB LDS); FEDMI_HALO_DEEP64=1 takes 6 (one per CU)
-  const char* d64 = std::getenv("FEDMI_HALO_DEEP64");
-  const bool deep64 = d64 && d64[0] == '1';
-  if (BN == 128) {
-    if (pp2) hipLaunchKernelGGL((conv_halo<128, 2, 5>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs,
-                                g_halo_stamps);
-    else hipLaunchKernelGGL((conv_halo<128, 1, 6>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs,
-                            g_halo_stamps);
-  } else {
-    if (pp2) hipLaunchKernelGGL((conv_halo<64, 2, 6>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs,
-                                g_halo_stamps);
-    else if (deep64) hipLaunchKernelGGL((conv_halo<64, 1, 6>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h,
-                                        cps, rs, g_halo_stamps);
-    else hipLaunchKernelGGL((conv_halo<64, 1, 3>), grid, dim3(256), 0, st, in, wt, out, part, stt, shift, h, cps, rs,
-                            g_halo_stamps);
-  }
-  if (splits > 1) {
-    const int VR = h.O / 8;
-    const int tb = (256 / VR) * VR;
-    const int rstep = tb / VR;
-    const int rows_per_block = stats ? std::max(2 * rstep, (h.M + 255) / 256) : std::max(rstep, (h.M + 1023) / 1024);
-    const int nblk = (h.M + rows_per_block - 1) / rows_per_block;
-    hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, splits, h.M, h.O, RowMap{}, out, stats,
-                       shift, rows_per_block, res, BnSums{});
-  }
-}
-
 static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const bf16* wt, bf16* out, double* stats,
                        const float* shift, const RowMap& rm, float* ws, long ws_floats,
                        const bf16* res = nullptr, const BnSums& bs = BnSums{}) {
   if (g.C % 64 || g.O % 8) throw std::invalid_argument("conv_tap: need C % 64 == 0 and O % 8 == 0");
-  HaloGeom hg;
-  if (!bs.rep && halo_geom(g, rm, &hg)) {
-    launch_halo(st, hg, in, wt, out, stats, shift, ws, ws_floats, res);
-    return;
-  }
   const int BN = tap_bn(g.O);
   const long tiles = (long)((g.M + 127) / 128) * ((g.O + BN - 1) / BN);
   const int ksteps = g.K / 64;
@@ -1757,16 +1418,12 @@ static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const b
   dim3 grid((unsigned)tiles, 1, (unsigned)splits);
   float* part = splits > 1 ? ws : nullptr;
   const BnSums tbs = part ? BnSums{} : bs;
-  static const bool two = [] { const char* e = std::getenv("FEDMI_TAP_STAGES"); return e && e[0] == '2'; }();
   double* tst = part ? nullptr : stats;
   const bf16* trs = part ? nullptr : res;
-  if (BN == 128) {
-    if (two) hipLaunchKernelGGL((conv_tap<128, 2>), grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
-    else hipLaunchKernelGGL((conv_tap<128, 3>), grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
-  } else {
-    if (two) hipLaunchKernelGGL((conv_tap<64, 2>), grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
-    else hipLaunchKernelGGL((conv_tap<64, 3>), grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
-  }
+  if (BN == 128)
+    hipLaunchKernelGGL(conv_tap<128>, grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
+  else
+    hipLaunchKernelGGL(conv_tap<64>, grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
   if (splits > 1) {
     const int VR = g.O / 8;
     const int tb = (256 / VR) * VR;
@@ -1962,11 +1619,6 @@ long conv_fd_ws_floats(const ConvShape& s) {
     const TapGeom t = make_tap(s.N, s.H, s.W, s.C, s.O, s.P, s.Q, s.R, s.S, s.st, s.pad, s.pad);
     const int tsp = tap_splits(t, cap);
     if (tsp > 1) need = std::max(need, (long)tsp * t.M * t.O);
-    HaloGeom h;
-    if (halo_geom(t, RowMap{}, &h)) {
-      const int hsp = halo_splits(h, cap);
-      if (hsp > 1) need = std::max(need, (long)hsp * h.M * h.O);
-    }
   }
   if (s.O % 64 == 0) {
     TapPhase ph[4];
@@ -1975,11 +1627,6 @@ long conv_fd_ws_floats(const ConvShape& s) {
       if (ph[i].empty) continue;
       const int tsp = tap_splits(ph[i].g, cap);
       if (tsp > 1) need = std::max(need, (long)tsp * ph[i].g.M * ph[i].g.O);
-      HaloGeom h;
-      if (halo_geom(ph[i].g, ph[i].rm, &h)) {
-        const int hsp = halo_splits(h, cap);
-        if (hsp > 1) need = std::max(need, (long)hsp * h.M * h.O);
-      }
     }
   }
   ConvGeom d = make_geom(s);
@@ -2008,22 +1655,19 @@ long conv_fd_ws_floats(const ConvShape& s) {
   return need;
 }
 
-// Workspace (floats) launch_conv_wgrad needs for this shape with automatic splits.
-// conv_wgrad_halo applies (3x3 / stride 1 / pad 1, C and O % 64, 128-pixel blocks); FEDMI_WGRAD_HALO=0
-// keeps the generic WGRAD (A/B switch, read per launch).
+// conv_wgrad_halo applies to 3x3 / stride 1 / pad 1 with C and O % 64 and 128-pixel blocks; every other
+// shape takes the generic WGRAD (split-K conv_igemm).
 static bool wgrad_halo_geom(const ConvShape& s, HaloGeom* h) {
-  const char* e = std::getenv("FEDMI_WGRAD_HALO");
-  if ((e && e[0] == '0') || s.R != 3 || s.S != 3 || s.st != 1 || s.pad != 1 || s.C % 64 || s.O % 64) return false;
+  if (s.R != 3 || s.S != 3 || s.st != 1 || s.pad != 1 || s.C % 64 || s.O % 64) return false;
   const TapGeom t = make_tap(s.N, s.H, s.W, s.C, s.O, s.P, s.Q, 3, 3, 1, 1, 1);
   // the 288-row window (4x4 images) would spill the per-lane fragment offset tables: generic path
-  return halo_geom(t, RowMap{}, h, false) && h->NPR <= 208;
+  return halo_geom(t, RowMap{}, h) && h->NPR <= 208;
 }
 
-// K splits of the halo WGRAD: about FEDMI_WGRAD_HALO_WGS (default: one per CU) workgroups over the
-// (O / 64) x (C / 64) tiles -- fewer splits mean fewer fp32 partial bytes to write and reduce.
+// K splits of the halo WGRAD: about one workgroup per CU over the (O / 64) x (C / 64) tiles -- fewer
+// splits mean fewer fp32 partial bytes to write and reduce.
 static int wgrad_halo_splits(const HaloGeom& h, long ws_cap_floats) {
-  const char* e = std::getenv("FEDMI_WGRAD_HALO_WGS");
-  const long want = (e && std::atoi(e) > 0) ? std::atoi(e) : num_cus();
+  const long want = num_cus();
   const long tiles = (long)(h.O / 64) * h.nchunks;
   const int nblk = h.M / 128;
   long sp = std::max<long>(1, (want + tiles / 2) / tiles);
@@ -2142,7 +1786,6 @@ void launch_dgrad_pack_multi(hipStream_t st, const DPackItem* items, int n) {
   }
 }
 
-void set_conv_halo_stamps(long long* p) { g_halo_stamps = p; }
 
 void launch_conv_pack(hipStream_t st, const float* w, bf16* wrsc, int O, int Cw, int C, int RS) {
   const PackItem it{w, wrsc, O, Cw, C, RS};

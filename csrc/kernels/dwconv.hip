@@ -57,18 +57,9 @@ FEDMI_DEV void stage_taps(const float* __restrict__ w, float* wl, int C, int RS)
 
 // one thread per (output pixel, 8-channel group); the block size is a multiple
 // of C/8, so the grid stride is too and a thread's channel group is fixed
-// isc (optional): [2][C] BatchNorm scale / shift of the PRODUCER of x: the kernel reads the producer's
-// pre-BN output z and uses relu(z * sc + sh) as its input (the BN-apply pass and its activation buffer
-// are never materialised; padding stays zero because it is applied to the transformed value).
-FEDMI_DEV void in_bn8(const float* isc, const float* ish, float* v) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * isc[j] + ish[j], 0.f);
-}
-
 __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                      bf16* __restrict__ y, double* __restrict__ stats,
-                                                     const float* __restrict__ shift, DwGeom g,
-                                                     const float* __restrict__ isc) {
+                                                     const float* __restrict__ shift, DwGeom g) {
   extern __shared__ float wl[];   // [RS][C]
   __shared__ float red[2][256][8];
   const int VC = g.C >> 3, RS = g.R * g.S;
@@ -82,12 +73,6 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x,
   float sh[8];   // statistics are of (y - shift): see conv_igemm's epilogue
 #pragma unroll
   for (int j = 0; j < 8; ++j) sh[j] = shift ? shift[c0 + j] : 0.f;
-  float bsc[8], bsh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    bsc[j] = isc ? isc[c0 + j] : 1.f;
-    bsh[j] = isc ? isc[g.C + c0 + j] : 0.f;
-  }
   // 32-bit index math (host guarantees < 2^31 elements): 64-bit div/mod are software loops
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)total; i += gridDim.x * blockDim.x) {
     const uint32_t pix = i / (uint32_t)VC;
@@ -108,7 +93,6 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x,
           const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
           float v[8];
           ld8f(x + (ok ? ((nb + h) * g.W + ww) * g.C + c0 : c0), v);
-          if (isc) in_bn8(bsc, bsh, v);
           const float* wt = wl + (r * 3 + s) * g.C + c0;
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[j] += ok ? v[j] * wt[j] : 0.f;
@@ -123,7 +107,6 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x,
           if ((unsigned)ww >= (unsigned)g.W) continue;
           float v[8];
           ld8f(x + ((nb + h) * g.W + ww) * g.C + c0, v);
-          if (isc) in_bn8(bsc, bsh, v);
           const float* wt = wl + (r * g.S + s) * g.C + c0;
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[j] += v[j] * wt[j];
@@ -160,8 +143,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16* __restrict__ x,
 template <int ST>
 __global__ __launch_bounds__(256) void dw_fwd3_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                       bf16* __restrict__ y, double* __restrict__ stats,
-                                                      const float* __restrict__ shift, DwGeom g,
-                                                      const float* __restrict__ isc) {
+                                                      const float* __restrict__ shift, DwGeom g) {
   constexpr int NCOL = ST == 1 ? 4 : 5;
   extern __shared__ float wl[];   // [9][C]
   __shared__ float red[2][256][8];
@@ -174,13 +156,9 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(const bf16* __restrict__ x
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   const int c0 = (int)(threadIdx.x % VC) * 8;
-  float sh[8], bsc[8], bsh[8];
+  float sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sh[j] = shift ? shift[c0 + j] : 0.f;
-    bsc[j] = isc ? isc[c0 + j] : 1.f;
-    bsh[j] = isc ? isc[g.C + c0 + j] : 0.f;
-  }
+  for (int j = 0; j < 8; ++j) sh[j] = shift ? shift[c0 + j] : 0.f;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)total; i += gridDim.x * blockDim.x) {
     const uint32_t pr = i / (uint32_t)VC;            // pair index
     const uint32_t t2 = pr / (uint32_t)Q2;
@@ -201,7 +179,6 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(const bf16* __restrict__ x
         const int ww = w0 + k;
         const bool ok = hok && (unsigned)ww < (unsigned)g.W;
         ld8f(x + (ok ? ((nb + h) * g.W + ww) * g.C + c0 : c0), v[k]);
-        if (isc) in_bn8(bsc, bsh, v[k]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[k][j] = ok ? v[k][j] : 0.f;
       }
@@ -358,8 +335,7 @@ __device__ __forceinline__ void wgrad_block_reduce(const float (&acc)[RS][8], fl
 // layers still launch ~100+ workgroups (round 1: 8 workgroups for MobileNet's 2x2x1024 layer).
 template <int RS>
 __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
-                                                       float* __restrict__ ws, DwGeom g, int pix_per_block, int VCB,
-                                                       const float* __restrict__ isc) {
+                                                       float* __restrict__ ws, DwGeom g, int pix_per_block, int VCB) {
   const int VC = VCB;        // channel groups of this block's chunk; host: blockDim.x % VCB == 0
   const int cg = threadIdx.x % VC, lane_pix = threadIdx.x / VC, pstep = blockDim.x / VC;
   const int c0 = blockIdx.y * VCB * 8 + cg * 8;
@@ -370,12 +346,6 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16* __restrict__ 
   for (int t = 0; t < RS; ++t)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[t][j] = 0.f;
-  float bsc[8], bsh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    bsc[j] = isc ? isc[c0 + j] : 1.f;
-    bsh[j] = isc ? isc[g.C + c0 + j] : 0.f;
-  }
   for (uint32_t pix = (uint32_t)(pb + lane_pix); pix < (uint32_t)pe; pix += pstep) {
     const uint32_t t2 = pix / (uint32_t)g.Q;
     const int q = (int)(pix - t2 * g.Q);
@@ -389,7 +359,6 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16* __restrict__ 
       const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
       float v[8];
       ld8f(x + (ok ? (((long)n * g.H + h) * g.W + ww) * g.C + c0 : c0), v);
-      if (isc) in_bn8(bsc, bsh, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[t][j] += ok ? v[j] * d[j] : 0.f;
     }
@@ -404,7 +373,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16* __restrict__ 
 template <int ST>
 __global__ __launch_bounds__(256) void dw_wgrad3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                         float* __restrict__ ws, DwGeom g, int pairs_per_block,
-                                                        int VCB, const float* __restrict__ isc) {
+                                                        int VCB) {
   constexpr int NCOL = ST == 1 ? 4 : 5;
   const int VC = VCB;
   const int cg = threadIdx.x % VC, lane_pix = threadIdx.x / VC, pstep = blockDim.x / VC;
@@ -417,12 +386,6 @@ __global__ __launch_bounds__(256) void dw_wgrad3_kernel(const bf16* __restrict__
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[t][j] = 0.f;
-  float bsc[8], bsh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    bsc[j] = isc ? isc[c0 + j] : 1.f;
-    bsh[j] = isc ? isc[g.C + c0 + j] : 0.f;
-  }
   for (uint32_t pr = (uint32_t)(pb + lane_pix); pr < (uint32_t)pe; pr += pstep) {
     const uint32_t t2 = pr / (uint32_t)Q2;
     const int q0 = (int)(pr - t2 * Q2) * 2;
@@ -446,7 +409,6 @@ __global__ __launch_bounds__(256) void dw_wgrad3_kernel(const bf16* __restrict__
         const int ww = w0 + k;
         const bool ok = hok && (unsigned)ww < (unsigned)g.W;
         ld8f(x + (ok ? ((nb + h) * g.W + ww) * g.C + c0 : c0), v[k]);
-        if (isc) in_bn8(bsc, bsh, v[k]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[k][j] = ok ? v[k][j] : 0.f;
       }
@@ -512,21 +474,21 @@ static DwGeom dw_geom(const DwShape& s) {
 
 // w: fp32 [C][1][R][S] (PyTorch depthwise layout, used directly)
 void launch_dw_fwd(hipStream_t st, const DwShape& s, const bf16* x, const float* w, bf16* y, double* stats,
-                   const float* shift, const float* isc) {
+                   const float* shift) {
   const DwGeom g = dw_geom(s);
   const int tb = block_threads(g.C);
   if (g.R == 3 && (g.st == 1 || g.st == 2) && g.pad == 1) {   // the MobileNet family: row-pair kernel
     const long items = (long)g.N * g.P * ((g.Q + 1) / 2) * (g.C / 8);
     const size_t lds = (size_t)g.C * 9 * sizeof(float);
     if (g.st == 1)
-      hipLaunchKernelGGL(dw_fwd3_kernel<1>, dim3(blocks_for(items, tb)), dim3(tb), lds, st, x, w, y, stats, shift, g, isc);
+      hipLaunchKernelGGL(dw_fwd3_kernel<1>, dim3(blocks_for(items, tb)), dim3(tb), lds, st, x, w, y, stats, shift, g);
     else
-      hipLaunchKernelGGL(dw_fwd3_kernel<2>, dim3(blocks_for(items, tb)), dim3(tb), lds, st, x, w, y, stats, shift, g, isc);
+      hipLaunchKernelGGL(dw_fwd3_kernel<2>, dim3(blocks_for(items, tb)), dim3(tb), lds, st, x, w, y, stats, shift, g);
     return;
   }
   const long items = (long)g.N * g.P * g.Q * (g.C / 8);
   hipLaunchKernelGGL(dw_fwd_kernel, dim3(blocks_for(items, tb)), dim3(tb), g.C * g.R * g.S * sizeof(float), st, x, w,
-                     y, stats, shift, g, isc);
+                     y, stats, shift, g);
 }
 
 // bs: optional BN-backward sums of dx's producer (see dw_dgrad_kernel); fewer, longer workgroups then
@@ -552,10 +514,7 @@ static int dw_wgrad_vcb(const DwGeom& g) {   // largest divisor of C/8 that is <
   return 1;
 }
 // stride 1 only: at stride 2 the pair shares 3 of 5 columns, and measured slower (MobileNet 37 -> 64 us)
-static bool dw_wgrad_pair(const DwGeom& g) {
-  static const bool off = [] { const char* e = std::getenv("FEDMI_DW_WGRAD_PAIR"); return e && e[0] == '0'; }();
-  return !off && g.R == 3 && g.st == 1 && g.pad == 1;
-}
+static bool dw_wgrad_pair(const DwGeom& g) { return g.R == 3 && g.st == 1 && g.pad == 1; }
 static long dw_wgrad_items(const DwGeom& g) {   // output pixels, or pixel pairs for the row-pair kernel
   return dw_wgrad_pair(g) ? (long)g.N * g.P * ((g.Q + 1) / 2) : (long)g.N * g.P * g.Q;
 }
@@ -572,7 +531,7 @@ long dw_wgrad_ws_floats(const DwShape& s) {
 }
 
 void launch_dw_wgrad(hipStream_t st, const DwShape& s, const bf16* x, const bf16* dy, float* dw, float* ws,
-                     long ws_floats, int accumulate, const float* isc) {
+                     long ws_floats, int accumulate) {
   const DwGeom g = dw_geom(s);
   const int nblk = dw_wgrad_blocks(g);
   const int n = g.C * g.R * g.S;
@@ -583,10 +542,10 @@ void launch_dw_wgrad(hipStream_t st, const DwShape& s, const bf16* x, const bf16
   const int tb = block_threads(vcb * 8);
   const dim3 grid(nblk, (g.C / 8) / vcb);
   if (dw_wgrad_pair(g))
-    hipLaunchKernelGGL(dw_wgrad3_kernel<1>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb, isc);
-  else if (g.R == 3) hipLaunchKernelGGL(dw_wgrad_kernel<9>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb, isc);
-  else if (g.R == 5) hipLaunchKernelGGL(dw_wgrad_kernel<25>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb, isc);
-  else hipLaunchKernelGGL(dw_wgrad_kernel<49>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb, isc);
+    hipLaunchKernelGGL(dw_wgrad3_kernel<1>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb);
+  else if (g.R == 3) hipLaunchKernelGGL(dw_wgrad_kernel<9>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb);
+  else if (g.R == 5) hipLaunchKernelGGL(dw_wgrad_kernel<25>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb);
+  else hipLaunchKernelGGL(dw_wgrad_kernel<49>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb);
   hipLaunchKernelGGL(dw_wgrad_reduce, dim3((n + 15) / 16), dim3(256), 0, st, ws, nblk, n, dw, accumulate);
 }
 

@@ -436,7 +436,6 @@ __global__ __launch_bounds__(256) void pad_rows_kernel(const bf16* __restrict__ 
 // (mode 1: forward statistics -> coefficients / running stats, 2: backward sums -> coefficients, 0: none)
 struct BnFin {
   int mode;
-  int fast;               // 1: the prefetching bf16 row pass (FEDMI_ZOO_FAST=0: the one-row loop)
   int slot;               // arrival-ticket slot of this launch (g_rows_ticket)
   long long M;
   const float* shift; const float* w; const float* b; float* rmean; float* rvar; float eps, mom;
@@ -509,7 +508,7 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_d
     // U rows per pass, every load of the pass issued before the first use (clamped rows, masked): one
     // memory latency per U rows instead of per row; dtypes / operands are compile-time in the pass
     const bool dot = op != RD_SUM && op != RD_SUMSQ_SHIFT;
-    const bool bf = fin.fast && a_dt == 1 && (!f || f_dt == 1) && (!dot || b_dt == 1);
+    const bool bf = a_dt == 1 && (!f || f_dt == 1) && (!dot || b_dt == 1);   // the prefetching bf16 pass
     const int opk = op == RD_SUM ? 0 : op == RD_SUMSQ_SHIFT ? 1 : 2;
 #define FEDMI_ROWS(BF, HF, OPK) rows_pass<VW, BF, HF, OPK>(a, lda, b, ldb, f, ldf, thr, sh, v, rl, RL, r0, r1, s1, s2)
     if (bf) {
@@ -634,60 +633,14 @@ __global__ __launch_bounds__(256) void reduce_rows_finalize(const float* part, i
   if (two) acc2[c] += t2;
 }
 
-// BatchNorm forward from the reduce_rows slab partials of (x - shift): slab sums in order, then
-// the bn_fwd_coeffs math (one launch instead of finalize + coefficients)
-__global__ __launch_bounds__(256) void bn_rows_fwd_finalize(const float* part, int slabs, int C, long long M,
-                                                            const float* shift, const float* w, const float* b,
-                                                            float* rmean, float* rvar, float eps, float mom,
-                                                            float* save_mean, float* save_invstd, float* scale,
-                                                            float* bias) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const float s1 = ordered_slab_sum(part, slabs, 2LL * C, c, c < C);
-  __syncthreads();
-  const float s2 = ordered_slab_sum(part + C, slabs, 2LL * C, c, c < C);
-  if ((threadIdx.x >> 6) || c >= C) return;
-  BnFin f{};
-  f.M = M; f.shift = shift; f.w = w; f.b = b; f.rmean = rmean; f.rvar = rvar; f.eps = eps; f.mom = mom;
-  f.save_mean = save_mean; f.save_invstd = save_invstd; f.scale = scale; f.bias = bias;
-  bn_fwd_fin(f, c, s1, s2);
-}
 
-// BatchNorm backward from the slab partials of (sum g, sum g * (x - mean)): bn_bwd_coeffs math
-__global__ __launch_bounds__(256) void bn_rows_bwd_finalize(const float* part, int slabs, int C, long long M,
-                                                            const float* mean, const float* invstd, const float* w,
-                                                            float* k, float* bb, float* cc, float* dw, float* db) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const float sg = ordered_slab_sum(part, slabs, 2LL * C, c, c < C);
-  __syncthreads();
-  const float sgx = ordered_slab_sum(part + C, slabs, 2LL * C, c, c < C);
-  if ((threadIdx.x >> 6) || c >= C) return;
-  BnFin f{};
-  f.M = M; f.mean = mean; f.invstd = invstd; f.w = w; f.k = k; f.bb = bb; f.cc = cc; f.dw = dw; f.db = db;
-  bn_bwd_fin(f, c, sg, sgx);
-}
 
 int rows_vw(int C) { return C % 8 == 0 ? 8 : 4; }
-
-// prefetching fast paths of the row pass and the grouped convs (FEDMI_ZOO_FAST=0: the original loops, A/B)
-bool zoo_fast() {
-  static const bool on = [] { const char* e = std::getenv("FEDMI_ZOO_FAST"); return !(e && e[0] == '0'); }();
-  return on;
-}
-
-// BN row passes with the finalize in the last-arriving workgroup (FEDMI_BN_ROWS_FUSED=0: separate launch)
-bool bn_rows_fused() {
-  static const bool on = [] { const char* e = std::getenv("FEDMI_BN_ROWS_FUSED"); return !(e && e[0] == '0'); }();
-  return on;
-}
 
 int rows_slabs(long long M, int C) {
   const int VL = C / rows_vw(C), vt = VL < 256 ? VL : 256, RL = 256 / vt;
   const long long tiles = (VL + vt - 1) / vt;
-  static const long long per_lane = [] {           // rows per row lane (A/B: FEDMI_ROWS_PER_LANE)
-    const char* e = std::getenv("FEDMI_ROWS_PER_LANE");
-    const long long v = e ? std::atoll(e) : 16;
-    return v < 1 ? 1LL : v;
-  }();
+  constexpr long long per_lane = 16;               // rows per row lane
   long long sl = M / ((long long)RL * per_lane);    // >= per_lane rows per row lane
   const long long cap = (2048 + tiles - 1) / tiles;  // ~2048 blocks in flight at most
   if (sl > cap) sl = cap;
@@ -1045,7 +998,6 @@ struct GConv {
   ZTensor x, w, y;
   int G, st_h, st_w, pad_h, pad_w, R, S;
   int vec_x, vec_y;    // channels of x (resp. y) load as aligned bf16x8 vectors (host-checked)
-  int fast;            // prefetching 3x3 / wgrad fast paths (FEDMI_ZOO_FAST)
 };
 
 FEDMI_DEV void load8(const ZTensor& t, long long off, long long cstride, bool vec, float v[8]) {
@@ -1088,7 +1040,7 @@ __global__ __launch_bounds__(256) void gconv_fwd_kernel(GConv g) {
     }
     __syncthreads();
     if (!valid) continue;
-    if (g.fast && g.R == 3 && g.S == 3 && g.vec_x && g.x.dtype == 1 && cn % 8 == 0) {
+    if (g.R == 3 && g.S == 3 && g.vec_x && g.x.dtype == 1 && cn % 8 == 0) {
       // 3x3, bf16 channels-last: per 8-channel group the nine tap vectors are loaded together (clamped
       // addresses, 0/1 masks), then the FMAs -- one memory latency per group instead of one per tap
       const bf16* xp = reinterpret_cast<const bf16*>(g.x.p);
@@ -1181,7 +1133,7 @@ __global__ __launch_bounds__(256) void gconv_dgrad_kernel(GConv g) {
     }
     __syncthreads();
     if (!valid) continue;
-    if (g.fast && g.R == 3 && g.S == 3 && g.vec_y && g.y.dtype == 1 && on % 8 == 0) {
+    if (g.R == 3 && g.S == 3 && g.vec_y && g.y.dtype == 1 && on % 8 == 0) {
       // 3x3, bf16 channels-last dy: the nine tap vectors of an 8-channel group loaded together (see fwd)
       const bf16* yp = reinterpret_cast<const bf16*>(g.y.p);
       long long toff[9];
@@ -1273,7 +1225,7 @@ __global__ __launch_bounds__(256) void gconv_wgrad_kernel(GConv g, float* part, 
   float acc[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) acc[u] = 0.f;
-  if (g.fast && vec && g.y.dtype == 1) {
+  if (vec && g.y.dtype == 1) {
     // bf16 channels-last fast path: 8 output columns per pass, all 16 loads (8 dy scalars, 8 x vectors)
     // issued before the first use -- clamped addresses and a 0/1 mask instead of per-load branches, so the
     // pass costs one memory latency (the scalar loop paid one per pixel: ~300 us per RegNetY launch)
@@ -1461,7 +1413,6 @@ void launch_reduce_rows(hipStream_t st, const void* a, int a_dt, long long lda, 
   const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
   const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
   BnFin fin{};
-  fin.fast = zoo_fast();
   if (vw == 8)
     hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
                        nullptr, 0, 0LL, 0.f, fin);
@@ -1483,22 +1434,16 @@ void launch_bn_rows_fwd(hipStream_t st, const void* x, int x_dt, long long ldx, 
   const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
   const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
   BnFin fin{};
-  fin.fast = zoo_fast();
-  if (bn_rows_fused()) {
-    fin.slot = (int)(g_rows_slot.fetch_add(1u) % kRowsTicketSlots);
-    fin.mode = 1; fin.M = M; fin.shift = shift; fin.w = w; fin.b = b; fin.rmean = rmean; fin.rvar = rvar;
-    fin.eps = eps; fin.mom = mom; fin.save_mean = save_mean; fin.save_invstd = save_invstd; fin.scale = scale;
-    fin.bias = bias;
-  }
+  fin.slot = (int)(g_rows_slot.fetch_add(1u) % kRowsTicketSlots);
+  fin.mode = 1; fin.M = M; fin.shift = shift; fin.w = w; fin.b = b; fin.rmean = rmean; fin.rvar = rvar;
+  fin.eps = eps; fin.mom = mom; fin.save_mean = save_mean; fin.save_invstd = save_invstd; fin.scale = scale;
+  fin.bias = bias;
   if (vw == 8)
     hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, x, x_dt, ldx, nullptr, 0, 0LL, shift, C, M,
                        (int)RD_SUMSQ_SHIFT, part, nullptr, 0, 0LL, 0.f, fin);
   else
     hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, x, x_dt, ldx, nullptr, 0, 0LL, shift, C, M,
                        (int)RD_SUMSQ_SHIFT, part, nullptr, 0, 0LL, 0.f, fin);
-  if (!fin.mode)
-    hipLaunchKernelGGL(bn_rows_fwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C, M,
-                       shift, w, b, rmean, rvar, eps, mom, save_mean, save_invstd, scale, bias);
   check_hip(hipGetLastError(), "bn_rows_fwd");
 }
 
@@ -1513,21 +1458,15 @@ void launch_bn_rows_bwd(hipStream_t st, const void* g, int g_dt, long long ldg, 
   const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
   const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
   BnFin fin{};
-  fin.fast = zoo_fast();
-  if (bn_rows_fused()) {
-    fin.slot = (int)(g_rows_slot.fetch_add(1u) % kRowsTicketSlots);
-    fin.mode = 2; fin.M = M; fin.mean = mean; fin.invstd = invstd; fin.w = w; fin.k = k; fin.bb = bb; fin.cc = cc;
-    fin.dw = dw; fin.db = db;
-  }
+  fin.slot = (int)(g_rows_slot.fetch_add(1u) % kRowsTicketSlots);
+  fin.mode = 2; fin.M = M; fin.mean = mean; fin.invstd = invstd; fin.w = w; fin.k = k; fin.bb = bb; fin.cc = cc;
+  fin.dw = dw; fin.db = db;
   if (vw == 8)
     hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, g, g_dt, ldg, x, x_dt, ldx, mean, C, M,
                        (int)RD_DOT_SHIFT, part, f, f_dt, ldf, thr, fin);
   else
     hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, g, g_dt, ldg, x, x_dt, ldx, mean, C, M,
                        (int)RD_DOT_SHIFT, part, f, f_dt, ldf, thr, fin);
-  if (!fin.mode)
-    hipLaunchKernelGGL(bn_rows_bwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C, M,
-                       mean, invstd, w, k, bb, cc, dw, db);
   check_hip(hipGetLastError(), "bn_rows_bwd");
 }
 
@@ -1634,7 +1573,6 @@ void launch_gconv(hipStream_t st, int mode, const ZTensor& x, const ZTensor& w, 
   };
   g.vec_x = vec_ok(x, Cg);
   g.vec_y = vec_ok(y, Og);
-  g.fast = zoo_fast() ? 1 : 0;
   if (G <= 0 || O % G || x.size[1] != Cg * G || w.size[0] != O || g.R * g.S * GT > GC_LDS)
     throw std::invalid_argument("gconv: inconsistent shapes");
   if (mode == 0) {

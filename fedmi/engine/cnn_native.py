@@ -51,14 +51,6 @@ BN_EPS = 1e-5
 BN_MOM = 0.1
 
 
-class _Lazy:
-    """An activation that was never materialised: relu(BN(z)) with the BN's [2, C] scale / shift
-    ``co``; only a depthwise consumer can take it (it applies the BN on load)."""
-
-    def __init__(self, z: torch.Tensor, co: torch.Tensor):
-        self.z, self.co = z, co
-
-
 class _Unit:
     """conv (dense or depthwise, no bias) + BatchNorm2d (+ ReLU), with its device buffers."""
 
@@ -115,26 +107,18 @@ class _Unit:
     def fwd(self, x: torch.Tensor, nb: int, stats, ws: Optional[torch.Tensor] = None,
             res: Optional[torch.Tensor] = None) -> None:
         sh = self.shift if stats is not None else None
-        in_bn = None
-        if isinstance(x, _Lazy):
-            assert self.depthwise, "only a depthwise conv applies its producer's BN on load"
-            x, in_bn = x.z, x.co
         if self.depthwise:
             assert res is None
             conv.dwconv_fwd(x, self.conv.weight, self.stride, self.pad, stats=stats, out=self.view(self.z, nb),
-                            shift=sh, in_bn=in_bn)
+                            shift=sh)
         else:
             conv.conv2d_fwd(x, self.wr, self.stride, self.pad, Cw=self.Cw, stats=stats, out=self.view(self.z, nb),
                             shift=sh, ws=ws, res=res)
 
     def wgrad(self, x: torch.Tensor, nb: int, ws: torch.Tensor, dz: Optional[torch.Tensor] = None) -> None:
         dz = self.view(self.dz, nb) if dz is None else dz
-        in_bn = None
-        if isinstance(x, _Lazy):
-            assert self.depthwise, "only a depthwise conv applies its producer's BN on load"
-            x, in_bn = x.z, x.co
         if self.depthwise:
-            conv.dwconv_wgrad(x, dz, self.R, self.stride, self.pad, out=self.conv.weight.grad, ws=ws, in_bn=in_bn)
+            conv.dwconv_wgrad(x, dz, self.R, self.stride, self.pad, out=self.conv.weight.grad, ws=ws)
         else:
             conv.conv2d_wgrad(x, dz, self.R, self.S, self.stride, self.pad, Cw=self.Cw, out=self.conv.weight.grad,
                               ws=ws)
@@ -152,14 +136,12 @@ class _Unit:
 
     def dgrad_fusable(self, add: bool = False) -> bool:
         """Whether this conv's DGRAD can take its producer BN's backward sums in the epilogue (dense tap
-        path; the depthwise kernel with FEDMI_CNN_FUSE_DW_BN_BWD=1 -- measured 846 vs 832 ms per MobileNet
-        round with it on) and, ``add``, a second incoming grad (dense tap path only)."""
+        path; the depthwise DGRAD with the sums measured slower, 846 vs 832 ms per MobileNet round) and,
+        ``add``, a second incoming grad."""
         if self.depthwise:
-            import os
-
-            return not add and os.environ.get("FEDMI_CNN_FUSE_DW_BN_BWD", "0") == "1"
+            return False
         if self._fusable is None:
-            self._fusable = (not self.depthwise and self.wd is not None and
+            self._fusable = (self.wd is not None and
                              conv.dgrad_fusable(self.in_shape(1), self.O, self.R, self.S, self.stride, self.pad,
                                                 self.Cw, True))
         return self._fusable
@@ -489,8 +471,6 @@ class CNNNativeTrainer(LocalTrainer):
             last = self.blocks[-1]
             self.head_hw, self.head_c = last.out_hw, last.cout
             self.units = plan.units() if self.preact else [u for b in self.blocks for u in b.units()]
-            if not self.preact:
-                self._mark_deferred_bn(device)
             # units whose data gradient is never needed (they read the network input)
             self._no_dgrad = ({id(self.preact.stem)} if self.preact else
                               {id(u) for u in self.blocks[0].units()} if self.blocks[0].first else set())
@@ -509,16 +489,9 @@ class CNNNativeTrainer(LocalTrainer):
         # one fp32 split-K workspace for every conv launch of a step (fwd / dgrad / wgrad)
         self.wgrad_ws = torch.empty(max(max(u.ws_floats(nb) for u in self.units) for nb in {B, self.eval_bs}),
                                     device=device)
-        # weight gradients on a side stream (FEDMI_CNN_WGRAD_STREAM=0: one stream), with their own workspace
-        import os
-
-        self._side = None
-        self.wgrad_ws2 = None
-        # opt-in: measured slower (ResNet-18 1036 vs 983 ms per round, MobileNet 886 vs 832): the concurrent
-        # kernels compete for CUs / LDS and the split-K sizing assumes the whole chip (profiles/r3_cnn)
-        if device.type == "cuda" and os.environ.get("FEDMI_CNN_WGRAD_STREAM", "0") == "1":
-            self._side = torch.cuda.Stream(device)
-            self.wgrad_ws2 = torch.empty_like(self.wgrad_ws)
+        # (weight gradients on a side stream overlapping the dgrad chain measured slower -- ResNet-18 1036 vs
+        # 983 ms per round, MobileNet 886 vs 832: the concurrent kernels compete for CUs / LDS and the split-K
+        # sizing assumes the whole chip, profiles/r3_cnn -- so everything runs on one stream)
         # BN-backward two-level channel sums (replicated atomics + finalize; kept zero between uses)
         self.bn_ws = torch.zeros(max(cnn.bn_bwd_ws_floats(B * u.P * u.P, u.O) for u in self.units),
                                  dtype=torch.float64, device=device)
@@ -534,10 +507,8 @@ class CNNNativeTrainer(LocalTrainer):
             u.bn_reps = nf // (3 * u.O)
             co += n
         # BN-backward channel sums taken in the epilogue of the DGRAD that writes the BN's output grad
-        # (conv_igemm.hip BnSums): no separate reduce pass over (dy, z, y).  FEDMI_CNN_FUSE_BN_BWD=0: off.
-        import os
-
-        self._fuse_bn_bwd = os.environ.get("FEDMI_CNN_FUSE_BN_BWD", "1") != "0"
+        # (conv_igemm.hip BnSums): no separate reduce pass over (dy, z, y)
+        self._fuse_bn_bwd = True
         # a ReLU'd BN inside a block (no residual): the forward stores its scale / shift, and the backward
         # derives the ReLU mask from z (z * sc + sh > 0) instead of re-reading the materialised y
         for u in self.units:
@@ -620,28 +591,7 @@ class CNNNativeTrainer(LocalTrainer):
         self._starts, self._sizes = [], []
         self._graphs.clear()
 
-    def _mark_deferred_bn(self, device) -> None:
-        """A block whose output feeds ONLY the next block's depthwise conv (no shortcut, no pool, not the
-        network output: MobileNet's pointwise -> depthwise chain) skips its BN-apply pass: the BN's
-        scale / shift are computed by one small launch, the depthwise forward and weight-gradient
-        kernels apply it on load, and its BN backward derives the ReLU mask from z.  Opt-in
-        (FEDMI_CNN_DEFER_BN=1): measured slower on MobileNet (profiles/r2_lenet/experiments.md) -- the
-        per-tap transform made the 9-tap depthwise kernels VALU-bound (+86 / +85 us) and the coefficient
-        launches cost 6.9 us each, more than the 112 us of BN-apply passes they removed."""
-        import os
-
-        on = os.environ.get("FEDMI_CNN_DEFER_BN", "0") == "1"
-        for b, nxt in zip(self.blocks[:-1], self.blocks[1:]):
-            b.defer = bool(on and b.shortcut == "none" and not b.pool and b.out_relu and nxt.main[0].depthwise
-                           and nxt.shortcut == "none" and nxt.proj is None)
-            b.co = torch.empty(2, b.cout, device=device) if b.defer else None
-        self.blocks[-1].defer, self.blocks[-1].co = False, None
-
     def _act(self, b: "_Block", nb: int):
-        """A block's output as its consumer sees it (materialised or lazy)."""
-        if getattr(b, "defer", False):
-            last = b.main[-1]
-            return _Lazy(last.view(last.z, nb), b.co)
         return b.out_view(nb)
 
     # ---- kernel schedule ---------------------------------------------------------------------
@@ -673,9 +623,6 @@ class CNNNativeTrainer(LocalTrainer):
                 self._bn(last, z, out, train, b.out_relu, z2=p.view(p.z, nb), b=p.bn_args(p.stats))
             elif b.shortcut == "identity":
                 self._bn(last, z, out, train, b.out_relu, res=a)
-            elif getattr(b, "defer", False):
-                cnn.bn_coeff(z.numel() // last.O, last.O, last.bn_args(last.stats if train else None), b.co, train,
-                             eps=BN_EPS, momentum=BN_MOM)
             else:
                 self._bn(last, z, out, train, b.out_relu)
             if b.pool:
@@ -700,19 +647,7 @@ class CNNNativeTrainer(LocalTrainer):
         return d
 
     def _wgrad(self, u: _Unit, x, nb: int, dz=None) -> None:
-        """``u``'s weight gradient: nothing else in the backward reads it before the SGD, so with a side
-        stream it runs there (own split-K workspace), overlapping the dgrad / BN chain of the main stream;
-        ``_backward`` joins the streams at its end."""
-        if self._side is None:
-            u.wgrad(x, nb, self.wgrad_ws, dz=dz)
-            return
-        self._side.wait_stream(torch.cuda.current_stream(self._device))
-        with torch.cuda.stream(self._side):
-            u.wgrad(x, nb, self.wgrad_ws2, dz=dz)
-
-    def _join_side(self) -> None:
-        if self._side is not None:
-            torch.cuda.current_stream(self._device).wait_stream(self._side)
+        u.wgrad(x, nb, self.wgrad_ws, dz=dz)
 
     def _bn_bwd(self, u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None, dadd=None,
                 mask_bn=None, presummed: bool = False) -> None:
@@ -743,12 +678,9 @@ class CNNNativeTrainer(LocalTrainer):
             din_b = b.in_view(b.din_b, nb) if b.din_b is not None else None
             if b.pool:   # grad wrt the pooled output -> grad wrt the pre-pool activation
                 dya = cnn.maxpool2_bwd(b.pre_view(nb), dya, out=b.dpre_view(nb))
-            if getattr(b, "defer", False):
-                self._bn_bwd(last, nb, dya, dyb, None, mask_bn=b.co)
-            else:
-                # pres: the next block's first DGRAD wrote dya = (its grad + the shortcut grad) and this BN's sums
-                self._bn_bwd(last, nb, dya, dyb, b.pre_view(nb) if b.out_relu else None, zb=b.proj,
-                             gout=din_b if b.shortcut == "identity" else None, presummed=pres)
+            # pres: the next block's first DGRAD wrote dya = (its grad + the shortcut grad) and this BN's sums
+            self._bn_bwd(last, nb, dya, dyb, b.pre_view(nb) if b.out_relu else None, zb=b.proj,
+                         gout=din_b if b.shortcut == "identity" else None, presummed=pres)
             proj_done = False
             for j in range(len(b.main) - 1, -1, -1):
                 v = b.main[j]
@@ -767,7 +699,7 @@ class CNNNativeTrainer(LocalTrainer):
                 elif not b.first:
                     din_a = b.in_view(b.din_a, nb)
                     bs = None
-                    if not (prev.pool or getattr(prev, "defer", False)):
+                    if not prev.pool:
                         pl = prev.main[-1]
                         bs = self._sums(v, pl, nb, prev.pre_view(nb) if prev.out_relu else None, zb=prev.proj,
                                         add=din_b is not None)
@@ -927,7 +859,6 @@ class CNNNativeTrainer(LocalTrainer):
             self.red_all.zero_()
         x, dh = self._forward(nb, True, self.train_set.x, self.train_set.y, self.cur, 0)
         self._backward(nb, x, dh)
-        self._join_side()          # the side stream's weight gradients before the SGD reads them
 
     def _train_step(self, nb: int) -> None:
         """One SGD step on the batch at sched[counter] (device-side)."""

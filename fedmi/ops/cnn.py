@@ -143,16 +143,6 @@ def bn_apply(z: torch.Tensor, a: BNParams, y: torch.Tensor, train: bool, relu: b
     return y
 
 
-def bn_coeff(z_rows: int, C: int, a: BNParams, co: torch.Tensor, train: bool, eps: float = 1e-5,
-             momentum: float = 0.1) -> torch.Tensor:
-    """BN scale / shift ([2, C] fp32 into ``co``) with bn_apply's running / saved statistics commit, for
-    a BN whose consumer applies it on load (the depthwise conv's ``in_bn``): bn_apply's output pass and
-    its activation buffer are skipped."""
-    native.require().bn_coeff(native.stream_handle(co.device), a.ptrs(), int(z_rows), int(C), eps, momentum,
-                              int(train), co.data_ptr())
-    return co
-
-
 def bn_bwd(dya: torch.Tensor, za: torch.Tensor, a: BNParams, dgamma_a: torch.Tensor, dbeta_a: torch.Tensor,
            dza: torch.Tensor, red: torch.Tensor, dyb: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None,
            zb: Optional[torch.Tensor] = None, b: Optional[BNParams] = None, dgamma_b=None, dbeta_b=None, dzb=None,

@@ -284,10 +284,8 @@ def _dw_shape(x_shape, R: int, stride: int, pad: int):
 
 
 def dwconv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats: Optional[torch.Tensor] = None,
-               out: Optional[torch.Tensor] = None, shift: Optional[torch.Tensor] = None,
-               in_bn: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Depthwise conv (NHWC bf16).  ``in_bn`` ([2, C] fp32 scale / shift): ``x`` is the producer's
-    pre-BN output and the conv reads relu(x * scale + shift)."""
+               out: Optional[torch.Tensor] = None, shift: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Depthwise conv (NHWC bf16), fp32 weights [C, 1, R, R]; optional fused BN statistics of the output."""
     _check(x, torch.bfloat16, "dwconv_fwd.x")
     _check(w, torch.float32, "dwconv_fwd.w")
     C, one, R, S = w.shape
@@ -300,8 +298,7 @@ def dwconv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats: O
         out = torch.empty(shp[0], P, Q, C, dtype=torch.bfloat16, device=x.device)
     native.require().dw_fwd(native.stream_handle(x.device), shp, x.data_ptr(), w.data_ptr(), out.data_ptr(),
                             stats.data_ptr() if stats is not None else 0,
-                            shift.data_ptr() if shift is not None else 0,
-                            in_bn.data_ptr() if in_bn is not None else 0)
+                            shift.data_ptr() if shift is not None else 0)
     return out
 
 
@@ -322,8 +319,7 @@ def dwconv_ws_floats(x_shape, R: int, stride: int, pad: int) -> int:
 
 
 def dwconv_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, stride: int, pad: int, out: Optional[torch.Tensor] = None,
-                 accumulate: bool = False, ws: Optional[torch.Tensor] = None,
-                 in_bn: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 accumulate: bool = False, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     _check(x, torch.bfloat16, "dwconv_wgrad.x")
     _check(dy, torch.bfloat16, "dwconv_wgrad.dy")
     shp = _dw_shape(x.shape, R, stride, pad)
@@ -335,5 +331,5 @@ def dwconv_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, stride: int, pad: in
     if ws is None:
         ws = wgrad_workspace(x.device, nat.dw_wgrad_ws_floats(shp))
     nat.dw_wgrad(native.stream_handle(x.device), shp, x.data_ptr(), dy.data_ptr(), out.data_ptr(), ws.data_ptr(),
-                 ws.numel(), int(accumulate), in_bn.data_ptr() if in_bn is not None else 0)
+                 ws.numel(), int(accumulate))
     return out

@@ -847,13 +847,6 @@ def _conv_kind(C, O, groups, k, stride, pad, dil):
     return "gconv"
 
 
-# A/B switches: FEDMI_NATIVE_CACHE=0 re-packs weights / re-pads inputs in the backward, FEDMI_ZOO_FAST=0 uses
-# the two-launch channel pad (the kernel-side fast paths read the same variable)
-_CACHE = os.environ.get("FEDMI_NATIVE_CACHE", "1") != "0"
-_FAST = os.environ.get("FEDMI_ZOO_FAST", "1") != "0"
-_FAST_PAD = _FAST and os.environ.get("FEDMI_ZOO_FAST_PAD", "1") != "0"
-
-
 def _row_stride(t: torch.Tensor) -> Optional[int]:
     """Row stride (elements) when ``t`` [..., C] is evenly spaced rows of unit-stride channels (a compact tensor
     or a channel slice of one), else None."""
@@ -880,13 +873,12 @@ def _pad_c(t: torch.Tensor, c8: int, cache: bool = False) -> torch.Tensor:
     if C == c8 and t.is_contiguous():
         return t
     mode = NativeMode.current
-    cache = cache and _CACHE
     key = ("pad", t.data_ptr(), tuple(t.shape), tuple(t.stride()), c8)
     if cache and mode is not None and key in mode._wcache:
         return mode._wcache[key][1]
     out = torch.empty(*t.shape[:-1], c8, dtype=torch.bfloat16, device=t.device)
     rows = t.numel() // C if C else 0
-    if _FAST_PAD and t.dtype == torch.bfloat16 and rows and _row_stride(t) is not None:
+    if t.dtype == torch.bfloat16 and rows and _row_stride(t) is not None:
         _nat().z_pad_rows(_st(t.device), t.data_ptr(), _row_stride(t), C, out.data_ptr(), c8, rows)   # one launch
     else:
         if c8 > C:
@@ -922,7 +914,7 @@ def _packed(w32, O8: int, C8: int, st: int, pd: int, need_wd: bool = False):
     NativeMode block: the forward packs, the backward of the same step reuses (the weights only change at
     the SGD, outside the block) -- per conv one pack launch, and the O-padding copies, fewer per step."""
     mode = NativeMode.current
-    cache = mode._wcache if mode is not None and _CACHE else None
+    cache = mode._wcache if mode is not None else None
     key = (w32.data_ptr(), tuple(w32.shape), tuple(w32.stride()), O8, C8, st, pd)
     ent = cache.get(key) if cache is not None else None
     if ent is None:
@@ -1136,17 +1128,14 @@ class NativeMode(TorchDispatchMode):
 
     current: "NativeMode" = None
 
-    def __init__(self, strict: bool = False, seed: int = 0, fuse: Optional[bool] = None):
+    def __init__(self, strict: bool = False, seed: int = 0, fuse: bool = True):
         super().__init__()
         self.strict = strict
         self.seed = seed
         self.fallbacks = collections.Counter()
         self.native_ops = collections.Counter()
         self._ctr = {}
-        # BN -> ReLU (forward) and ReLU-backward -> BN-backward fusion (FEDMI_NATIVE_FUSE=0: off)
-        import os
-
-        self.fuse = (os.environ.get("FEDMI_NATIVE_FUSE", "1") != "0") if fuse is None else bool(fuse)
+        self.fuse = bool(fuse)          # BN -> ReLU (forward) and ReLU-backward -> BN-backward fusion
         self._pend_bn: Optional[_PendingBN] = None
         self._pend_thr: Optional[_PendingThr] = None
         self._dead = {}                 # storage ptr -> materialiser of a tensor a fused op never wrote

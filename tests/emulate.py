@@ -149,17 +149,9 @@ def wgrad_ws_floats(*a, **k):
     return 1
 
 
-@torch.no_grad()
-def _in_bn(x, in_bn):
-    """relu(x * scale + shift) per channel (the kernels' apply-on-load of the producer's BN)."""
-    if in_bn is None:
-        return x
-    return torch.relu(x.float() * in_bn[0] + in_bn[1])
-
-
-def dwconv_fwd(x, w, stride, pad, stats=None, out=None, shift=None, in_bn=None):
+def dwconv_fwd(x, w, stride, pad, stats=None, out=None, shift=None):
     C = x.shape[3]
-    y = F.conv2d(_nchw(_in_bn(x, in_bn)), w.float(), stride=stride, padding=pad, groups=C)
+    y = F.conv2d(_nchw(x), w.float(), stride=stride, padding=pad, groups=C)
     if out is None:
         out = torch.empty(y.shape[0], y.shape[2], y.shape[3], C, dtype=_BF, device=x.device)
     _nhwc_into(out, y)
@@ -177,9 +169,9 @@ def dwconv_dgrad(dy, w, x_shape, stride, pad, out=None, bn_sums=None):
 
 
 @torch.no_grad()
-def dwconv_wgrad(x, dy, R, stride, pad, out=None, accumulate=False, ws=None, in_bn=None):
+def dwconv_wgrad(x, dy, R, stride, pad, out=None, accumulate=False, ws=None):
     C = x.shape[3]
-    dw = torch.nn.grad.conv2d_weight(_nchw(_in_bn(x, in_bn)), (C, 1, R, R), _nchw(dy), stride=stride, padding=pad,
+    dw = torch.nn.grad.conv2d_weight(_nchw(x), (C, 1, R, R), _nchw(dy), stride=stride, padding=pad,
                                      groups=C)
     if out is None:
         return dw
@@ -235,14 +227,6 @@ def _coeffs(p: "cnn.BNParams", M: int, train: bool, eps: float, mom: float):
         mean, inv = p.rmean - (p.cbias if p.cbias is not None else 0.0), torch.rsqrt(p.rvar + eps)
     sc = p.gamma * inv
     return sc, p.beta - mean * sc
-
-
-@torch.no_grad()
-def bn_coeff(z_rows, C, a, co, train, eps=1e-5, momentum=0.1):
-    sc, sh = _coeffs(a, z_rows, train, eps, momentum)
-    co[0].copy_(sc)
-    co[1].copy_(sh)
-    return co
 
 
 @torch.no_grad()
@@ -392,7 +376,7 @@ def emulated():
     for name in ("pack_weight", "pack_weights", "fd_ws_floats", "dgrad_pack_weights", "conv2d_fwd", "conv2d_dgrad", "dgrad_fusable", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
                  "dwconv_dgrad", "dwconv_wgrad", "dwconv_ws_floats"):
         swap(conv, name, globals()[name])
-    for name in ("prep_input", "sched_next", "bn_apply", "bn_coeff", "bn_bwd", "bn_bwd_ws_floats", "bn_bwd_chain_floats", "head", "maxpool2",
+    for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "bn_bwd_ws_floats", "bn_bwd_chain_floats", "head", "maxpool2",
                  "maxpool2_bwd", "maxpool3", "maxpool3_bwd"):
         swap(cnn, name, globals()[name])
     swap(native, "require", lambda: _NativeStub())

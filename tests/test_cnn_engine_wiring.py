@@ -22,13 +22,9 @@ def _cos(a, b):
 
 
 @pytest.mark.parametrize("name", ["ResNet18", "ResNet50", "MobileNet", "MobileNetV2", "VGG11", "PreActResNet18",
-                                  "PreActResNet50", "GoogLeNet", "MobileNet-deferBN"])
-def test_engine_schedule_matches_autograd(name, monkeypatch):
+                                  "PreActResNet50", "GoogLeNet"])
+def test_engine_schedule_matches_autograd(name):
     from fedmi.engine.cnn_native import CNNNativeTrainer
-
-    if name.endswith("-deferBN"):   # the opt-in schedule: pointwise BN applied on load by the depthwise conv
-        name = name[: -len("-deferBN")]
-        monkeypatch.setenv("FEDMI_CNN_DEFER_BN", "1")
 
     torch.manual_seed(0)
     nb = 8

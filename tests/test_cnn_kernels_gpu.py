@@ -301,25 +301,13 @@ def test_depthwise_fwd_dgrad_wgrad(gpu_device, shape):
     assert _rel(dw, wb.grad) < 1e-2
 
 
-def test_depthwise_input_bn_and_z_mask(gpu_device):
-    """Deferred BN (MobileNet pointwise -> depthwise): the depthwise fwd / wgrad read the producer's z and
-    apply relu(z * scale + shift) on load; the producer's BN backward derives its ReLU mask from z."""
+def test_bn_backward_relu_mask_from_z(gpu_device):
+    """A ReLU'd BN inside a block: bn_apply records the scale / shift it applied (co_out) and the BN backward
+    derives the ReLU mask from z (z * scale + shift > 0) instead of re-reading the materialised y."""
     dev = gpu_device
     torch.manual_seed(9)
-    N, H, W, C, R, st = 8, 8, 8, 256, 3, 1
+    N, H, W, C = 8, 8, 8, 256
     z = torch.randn(N, H, W, C, device=dev).bfloat16()
-    co = torch.stack([torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.3]).contiguous()
-    y = torch.relu(z.float() * co[0] + co[1])                       # the activation that is never written
-    w = torch.randn(C, 1, R, R, device=dev) * 0.2
-    out = conv.dwconv_fwd(z, w, st, 1, in_bn=co)
-    ref = F.conv2d(y.permute(0, 3, 1, 2), w, stride=st, padding=1, groups=C)
-    gy = torch.randn(N, H, W, C, device=dev).bfloat16()
-    dw = conv.dwconv_wgrad(z, gy, R, st, 1, in_bn=co)
-    dwr = torch.nn.grad.conv2d_weight(y.permute(0, 3, 1, 2), (C, 1, R, R), gy.float().permute(0, 3, 1, 2),
-                                      stride=st, padding=1, groups=C)
-    torch.cuda.synchronize()
-    assert _rel(out.float(), _nhwc(ref)) < 1e-2
-    assert _rel(dw, dwr) < 1e-2
     # BN backward: mask from z == mask from the materialised y
     M = N * H * W
     zr = z.reshape(M, C)
@@ -331,9 +319,8 @@ def test_depthwise_input_bn_and_z_mask(gpu_device):
     sm, si = torch.empty(C, device=dev), torch.empty(C, device=dev)
     A = cnn.bn_desc(stats, g, b, None, None, None, sm, si)
     co2 = torch.empty(2, C, device=dev)
-    cnn.bn_coeff(M, C, A, co2, True)
     yb = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
-    cnn.bn_apply(zr, A, yb, train=True, relu=True)
+    cnn.bn_apply(zr, A, yb, train=True, relu=True, co_out=co2)
     torch.cuda.synchronize()
     assert _rel(torch.relu(zr.float() * co2[0] + co2[1]), yb.float()) < 1e-2
     dya = torch.randn(M, C, device=dev).bfloat16()
@@ -642,86 +629,14 @@ def test_resnet18_batch128_conv_shapes(gpu_device, shape):
     assert _rel(dw, wr_.grad) < 1e-2
 
 
-# conv_halo (3x3 / stride 1 / pad 1, input window DMA'd once per 64-channel chunk): every tile
-# geometry -- TH rows of one image (W 64 / 32 / 16), whole images per tile (8x8 -> 2, 4x4 -> 8 with the
-# 288-row patch), 3 chunks, O not a multiple of the 128-column tile; forward (+ BN statistics) and the
-# stride-1 DGRAD on the flipped weight image, outputs pre-filled with NaN.
-HALO_SHAPES = [
-    (2, 64, 64, 64, 64, 3, 1, 1),
-    (2, 32, 32, 128, 64, 3, 1, 1),
-    (4, 16, 16, 192, 96, 3, 1, 1),
-    (4, 8, 8, 64, 128, 3, 1, 1),
-    (8, 4, 4, 64, 136, 3, 1, 1),
-]
-
-
-@pytest.mark.parametrize("shape", HALO_SHAPES, ids=[str(s) for s in HALO_SHAPES])
-def test_conv_halo_geometries(gpu_device, shape, monkeypatch):
-    monkeypatch.setenv("FEDMI_CONV_HALO", "1")
-    N, H, W, Cw, O, R, st, pad = shape
-    x, w, wb, xn = _make(shape, gpu_device, seed=21)
-    xr = x.clone().requires_grad_(True)
-    ref = F.conv2d(xr, wb, stride=1, padding=1)
-    gy = torch.randn_like(ref).bfloat16().float()
-    ref.backward(gy)
-    wpk = conv.pack_weight(w)
-    rep = conv.stats_buffer(O, gpu_device)
-    y = torch.full((N, H, W, O), float("nan"), dtype=torch.bfloat16, device=gpu_device)
-    conv.conv2d_fwd(xn, wpk, 1, 1, Cw=Cw, stats=rep, out=y)
-    dyn = _nhwc(gy).bfloat16()
-    dx = None
-    if conv.dgrad_eligible(O):
-        wd = torch.empty(conv.dgrad_image_numel(w.shape, Cw), dtype=torch.bfloat16, device=gpu_device)
-        conv.dgrad_pack_weights([(w, wd, 1, 1, Cw)])
-        dx = torch.full_like(xn, float("nan"))
-        conv.conv2d_dgrad(dyn, wpk, xn.shape, 1, 1, Cw=Cw, out=dx, wd=wd)
-    torch.cuda.synchronize()
-    assert _rel(y.float(), _nhwc(ref.detach())) < 1e-2
-    st_ = conv.stats_total(rep)
-    assert _rel(st_[0], y.float().sum((0, 1, 2))) < 1e-3
-    if dx is not None:
-        assert not torch.isnan(dx.float()).any()
-        assert _rel(dx.float(), _nhwc(xr.grad)) < 1e-2
-
-
-@pytest.mark.parametrize("shape", [(128, 8, 8, 256, 256, 3, 1, 1), (128, 4, 4, 512, 512, 3, 1, 1)],
-                         ids=["layer3", "layer4"])
-def test_conv_halo_splitk_residual(gpu_device, shape, monkeypatch):
-    """conv_halo split over 64-channel chunks (fp32 partials + combine) with fused residual and BN
-    statistics, and the split stride-1 DGRAD."""
-    monkeypatch.setenv("FEDMI_CONV_HALO", "1")
-    N, H, W, Cw, O, R, st, pad = shape
-    x, w, wb, xn = _make(shape, gpu_device, seed=22)
-    xr = x.clone().requires_grad_(True)
-    ref = F.conv2d(xr, wb, stride=1, padding=1)
-    gy = torch.randn_like(ref).bfloat16().float()
-    ref.backward(gy)
-    wpk = conv.pack_weight(w)
-    shp = (xn.shape, O, R, R, st, pad, Cw)
-    need = conv.fd_ws_floats(*shp)
-    assert need > 0
-    ws = torch.full((need,), float("nan"), device=gpu_device)
-    res = torch.randn(N, H, W, O, device=gpu_device).bfloat16()
-    rep = conv.stats_buffer(O, gpu_device)
-    y = conv.conv2d_fwd(xn, wpk, 1, 1, Cw=Cw, stats=rep, ws=ws, res=res)
-    torch.cuda.synchronize()
-    assert _rel(y.float(), _nhwc(ref.detach()) + res.float()) < 1e-2
-    assert _rel(conv.stats_total(rep)[0], y.float().sum((0, 1, 2))) < 1e-3
-    wd = torch.empty(conv.dgrad_image_numel(w.shape, Cw), dtype=torch.bfloat16, device=gpu_device)
-    conv.dgrad_pack_weights([(w, wd, 1, 1, Cw)])
-    ws.fill_(float("nan"))
-    dx = conv.conv2d_dgrad(_nhwc(gy).bfloat16(), wpk, xn.shape, 1, 1, Cw=Cw, ws=ws, wd=wd)
-    torch.cuda.synchronize()
-    assert _rel(dx.float(), _nhwc(xr.grad)) < 1e-2
-
-
 @pytest.mark.parametrize("shape", [(4, 32, 32, 64, 64, 3, 1, 1), (8, 16, 16, 128, 64, 3, 1, 1),
                                    (16, 8, 8, 64, 192, 3, 1, 1), (128, 32, 32, 64, 64, 3, 1, 1),
                                    (128, 8, 8, 256, 256, 3, 1, 1)],
                          ids=["w32", "w16", "w8_o192", "l1_b128", "l3_b128"])
-def test_conv_wgrad_halo(gpu_device, shape, monkeypatch):
-    """Halo-patch WGRAD (3x3 / stride 1, one input window per 128-pixel block for all nine taps) vs torch,
-    and vs the generic WGRAD (FEDMI_WGRAD_HALO=0) on the same inputs."""
+def test_conv_wgrad_halo(gpu_device, shape):
+    """Halo-patch WGRAD (3x3 / stride 1, one input window per 128-pixel block for all nine taps; the automatic
+    choice for these shapes) vs torch, and vs the generic split-K WGRAD (an explicit split count) on the same
+    inputs."""
     N, H, W, Cw, O, R, st, pad = shape
     x, w, wb, xn = _make(shape, gpu_device, seed=23)
     wr_ = wb.clone().requires_grad_(True)
@@ -731,10 +646,9 @@ def test_conv_wgrad_halo(gpu_device, shape, monkeypatch):
     dyn = _nhwc(gy).bfloat16()
     shp = (xn.shape, O, R, R, st, pad, Cw)
     ws = torch.full((conv.wgrad_ws_floats(*shp),), float("nan"), device=gpu_device)
-    monkeypatch.setenv("FEDMI_WGRAD_HALO", "1")
     dw = conv.conv2d_wgrad(xn, dyn, 3, 3, 1, 1, Cw=Cw, ws=ws)
-    monkeypatch.setenv("FEDMI_WGRAD_HALO", "0")
-    dw0 = conv.conv2d_wgrad(xn, dyn, 3, 3, 1, 1, Cw=Cw, ws=ws)
+    ws0 = torch.full((2 * O * 9 * xn.shape[-1],), float("nan"), device=gpu_device)
+    dw0 = conv.conv2d_wgrad(xn, dyn, 3, 3, 1, 1, Cw=Cw, ws=ws0, splits=2)
     torch.cuda.synchronize()
     assert not torch.isnan(dw).any()
     assert _rel(dw, wr_.grad) < 1e-2
