@@ -99,18 +99,22 @@ def test_engine_is_deterministic(gpu_device, name):
     assert sa.correct == sb.correct and sa.count == sb.count
 
 
-# Per-tensor margins from profiles/r4_tests/grad_cosines.jsonl (tools/diag_grad_cosines.py, one batch of 64 at
-# random init): the native engine's gradient cosine to fp32 is within 0.022 (ResNet-18) / 0.29 (MobileNetV2) of
-# PyTorch's OWN autocast-bf16 model's at every tensor -- MobileNetV2's deep BN stack makes every bf16 model's
-# early-layer gradient direction chaotic at init (torch-bf16 vs fp32: mean cos 0.51, min -0.25).
-GRAD_MARGIN = {"ResNet18": 0.05, "MobileNetV2": 0.35}
+# Bounds from profiles/r4_tests/grad_cosines.jsonl (tools/diag_grad_cosines.py, one batch of 64 at random init).
+# A tensor is WELL-CONDITIONED when PyTorch's own autocast-bf16 gradient keeps cos >= 0.9 to fp32: there the
+# native engine must stay within 0.05 of torch-bf16 (ResNet-18: all 62 tensors, worst gap -0.022).  On the
+# rest -- 163 of MobileNetV2's 173 tensors, whose deep BN stack makes every bf16 model's gradient direction
+# chaotic at init (torch-bf16 vs fp32 mean cos 0.48 there, min -0.25) -- a single tensor's cosine is noise
+# (two runs of the diagnostic put the worst gap on different tensors, -0.29 and -0.44), so the bound is on
+# the group: native's mean within 0.05 of torch-bf16's, and no tensor more than 0.6 below it.
+WELL_COND, WELL_MARGIN, ILL_MEAN_MARGIN, ILL_MAX_GAP = 0.9, 0.05, 0.05, 0.6
 
 
 @pytest.mark.parametrize("name", ["ResNet18", "MobileNetV2"])
 def test_native_gradients_track_torch_bf16(gpu_device, name):
-    """Per tensor: cos(native grad, fp32 grad) >= cos(torch autocast-bf16 grad, fp32 grad) - margin; the mean
-    over tensors within 0.03 of torch-bf16's; the classifier and the last BN at >= 0.99; the loss within 0.5 %
-    of the emulated-kernel engine's (same schedule and bf16 buffers, tests/emulate.py)."""
+    """cos(native grad, fp32 grad) against cos(torch autocast-bf16 grad, fp32 grad): per tensor within 0.05
+    where torch-bf16 is well-conditioned, as a group mean elsewhere (see WELL_COND); the mean over all tensors
+    within 0.03 of torch-bf16's; the classifier and the last BN at >= 0.99; the loss within 0.5 % of the
+    emulated-kernel engine's (same schedule and bf16 buffers, tests/emulate.py)."""
     from fedmi.engine.cnn_native import CNNNativeTrainer
     from emulate import emulated
 
@@ -145,8 +149,14 @@ def test_native_gradients_track_torch_bf16(gpu_device, name):
     names = list(grads["native"])
     cn = {k: _cos(grads["native"][k], grads["fp32"][k]) for k in names}
     cb = {k: _cos(grads["bf16"][k], grads["fp32"][k]) for k in names}
-    bad = {k: (round(cn[k], 3), round(cb[k], 3)) for k in names if cn[k] < cb[k] - GRAD_MARGIN[name]}
+    well = [k for k in names if cb[k] >= WELL_COND]
+    ill = [k for k in names if cb[k] < WELL_COND]
+    bad = {k: (round(cn[k], 3), round(cb[k], 3)) for k in well if cn[k] < cb[k] - WELL_MARGIN}
     assert not bad, bad
+    if ill:
+        assert sum(cn[k] for k in ill) / len(ill) > sum(cb[k] for k in ill) / len(ill) - ILL_MEAN_MARGIN
+        bad = {k: (round(cn[k], 3), round(cb[k], 3)) for k in ill if cn[k] < cb[k] - ILL_MAX_GAP}
+        assert not bad, bad
     assert sum(cn.values()) / len(names) > sum(cb.values()) / len(names) - 0.03
     tail = ["linear.weight", "linear.bias"] + (["layer4.1.bn2.weight", "layer4.1.bn2.bias"] if name == "ResNet18"
                                                else ["bn2.weight", "bn2.bias"])

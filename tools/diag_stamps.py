@@ -20,14 +20,6 @@ from fedmi.engine.base import TrainerConfig  # noqa: E402
 from fedmi.engine.data import make_dataset  # noqa: E402
 from fedmi.engine.lenet_native import LeNetNativeTrainer  # noqa: E402
 
-NAMES = {
-    0: ("conv_fwd", ["stage+aug", "conv1", "pool1", "conv2", "pool2+store"]),
-    1: ("fc_tail", ["prefetch+H1", "fc2+fc3", "CE", "dW3/dH2", "dW2/dH1", "dX+slab"]),
-    2: ("conv_bwd", ["stage", "shift+scatter", "c2 wgrad+dgrad", "c1 wgrad", "slab store"]),
-    3: ("sgd", ["all"]),
-}
-NWG = {0: 128, 1: 32, 2: 128, 3: 412}
-
 
 def main():
     nat = native.require()
@@ -43,7 +35,7 @@ def main():
     tr.train_step(0, 128)
     torch.cuda.synchronize()
     st = np.frombuffer(nat.read_stamps(True), dtype=np.uint64).reshape(nat.STAMP_SHAPE).astype(np.int64)
-    if tr.engine.sample_path():
+    if True:   # KS1 + KS2 (the only training path)
         # KS1: forward slots 0..6 under kernel 0, its backward slots 2..5 under kernel 2; KS2 under kernel 3
         ks1 = np.concatenate([st[0, :128, :7], st[2, :128, 2:6]], axis=1)
         phases = ["stage+aug", "conv1", "pool1", "conv2", "pool2+zero+shift", "fc fwd+bwd", "dY2 scatter",
@@ -68,8 +60,6 @@ def main():
             print(f"    fc.dX          med {np.median(k0[:len(f), 6] - prev):8.0f}")
         names = {3: ("sgd2", ["all"])}
         nwg = {3: 249}
-    else:
-        names, nwg = NAMES, NWG
     for k, (name, phases) in names.items():
         a = st[k, :nwg[k], :len(phases) + 1]
         a = a[a[:, 0] > 0]
@@ -80,14 +70,6 @@ def main():
               f"start spread {starts.max():7d} cyc")
         for j, ph in enumerate(phases):
             print(f"    {ph:16s} med {np.median(d[:, j]):8.0f}  max {d[:, j].max():8.0f}")
-    if tr.engine.sample_path():
-        return
-    # fused K12: split the FC head's first phase at the hand-off (slot 7 = flags seen)
-    f = st[1, :NWG[1]]
-    f = f[(f[:, 0] > 0) & (f[:, 7] > 0)]
-    if len(f):
-        print(f"    fc: start->flags seen med {np.median(f[:, 7] - f[:, 0]):8.0f}  max {(f[:, 7] - f[:, 0]).max():8.0f}"
-              f" | flags seen->H1 med {np.median(f[:, 1] - f[:, 7]):8.0f}  max {(f[:, 1] - f[:, 7]).max():8.0f}")
 
 
 if __name__ == "__main__":

@@ -41,6 +41,8 @@ def main() -> int:
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--out", default=None, help="JSONL, one record per round")
+    ap.add_argument("--no-augment", action="store_true", help="no crop/flip (diagnostics)")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of graph replay (diagnostics)")
     a = ap.parse_args()
     if a.engine in ("fp32", "bf16"):
         os.environ["FEDMI_TORCH_PATH"] = "1"
@@ -51,7 +53,7 @@ def main() -> int:
 
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
     data = make_dataset("synthetic-cifar10", device=dev, n_train=a.n_train, n_test=a.n_test, seed=0)
-    cfg = TrainerConfig(seed=a.seed, lr=a.lr)
+    cfg = TrainerConfig(seed=a.seed, lr=a.lr, augment=not a.no_augment, use_graph=not a.no_graph)
     W = a.clients
     clients = []
     init = None
@@ -90,7 +92,8 @@ def main() -> int:
         clients[0].evaluate()
         ev = clients[0].eval_stats()
         torch.cuda.synchronize() if dev.type == "cuda" else None
-        rec = {"round": rnd, "engine": a.engine, "model": a.model, "clients": W,
+        rec = {"round": rnd, "engine": a.engine, "model": a.model, "clients": W, "lr": a.lr, "seed": a.seed,
+               "augment": not a.no_augment, "graph": not a.no_graph,
                "split": f"noniid-{a.noniid}" if a.noniid else "strided-iid",
                "train_loss": [round(s.loss, 4) for s in tstats], "train_acc": [round(s.acc, 2) for s in tstats],
                "test_loss": round(ev.loss, 4), "test_acc": round(ev.acc, 2),
