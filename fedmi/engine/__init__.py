@@ -1,7 +1,6 @@
 """Local training engines (one per federated client)."""
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -21,7 +20,7 @@ def build_trainer(model: str, data: FedDataset, device, cfg: TrainerConfig = Tra
     """On a GPU: LeNet -> fused HIP engine; ResNet / MobileNet / MobileNetV2 -> the implicit-GEMM +
     BN-fused HIP engine (mandatory, no silent fallback).  Other zoo models -> the generic engine with
     every aten op of the step on fedmi's HIP kernels (:class:`fedmi.ops.native_mode.NativeMode`, bf16
-    channels-last activations, graph-replayed; ``FEDMI_HYBRID=0``: plain PyTorch fp32); CPU runs -> the
+    channels-last activations, graph-replayed; ``FEDMI_TORCH_PATH=1``: plain PyTorch fp32); CPU runs -> the
     generic PyTorch engine."""
     device = torch.device(device)
     from ..models import _canon
@@ -42,8 +41,7 @@ def build_trainer(model: str, data: FedDataset, device, cfg: TrainerConfig = Tra
         c, h, w = data.train.x.shape[1:]
         kw = {"in_channels": c} if _canon(model) == "lenet" else {"in_features": c * h * w}
     # zoo models without a whole-network engine: PyTorch autograd over the native aten backend
-    hybrid = (device.type == "cuda" and not native.force_torch_path() and os.environ.get("FEDMI_HYBRID", "1") != "0"
-              and _canon(model) != "lenet")
+    hybrid = device.type == "cuda" and not native.force_torch_path() and _canon(model) != "lenet"
     return TorchTrainer(model, data, device, cfg, init_state=init_state, model_kwargs=kw, hybrid=hybrid)
 
 

@@ -215,3 +215,32 @@ def test_native_round_writer_writes_every_round_in_order(tmp_path, monkeypatch):
     assert seen == [r for r in range(60) if r % 7 == 0]
     ck = load(tmp_path / "m.pth")
     assert ck["epoch"] == 59 and torch.equal(ck["net"]["w"], torch.full((20, 30), 59.0))
+
+
+@pytest.mark.gpu
+def test_device_round_writer_native_vs_python(tmp_path, monkeypatch):
+    """Device tensors: the native writer (default) and the Python writer (FEDMI_NATIVE_CKPT=0) produce
+    archives with the same contents, and each round's file holds the values as of ITS submit even though
+    the stream overwrites the tensors right after (the snapshot copy is stream-ordered)."""
+    from fedmi.ckpt import RoundCheckpointWriter, load
+
+    dev = torch.device("cuda", 0)
+    flat = torch.zeros(62006, device=dev)
+    sd = {"w": flat[:50000].view(100, 500), "b": flat[50000:]}
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("FEDMI_NATIVE_CKPT", mode)
+        w = RoundCheckpointWriter(slots=3)
+        seen = []
+        for r in range(12):
+            flat.fill_(float(r))
+            w.submit(tmp_path / f"m{mode}.pth", sd, epoch=r)
+            flat.add_(1000.0)           # enqueued after the snapshot: must not leak into round r's file
+            if r % 4 == 3:
+                w.flush()
+                ck = load(tmp_path / f"m{mode}.pth")
+                seen.append((ck["epoch"], float(ck["net"]["w"][0, 0]), float(ck["net"]["b"][-1])))
+        w.close()
+        assert w.backend == ("native" if mode == "1" else "python")
+        out[mode] = seen
+    assert out["1"] == out["0"] == [(r, float(r), float(r)) for r in (3, 7, 11)]
