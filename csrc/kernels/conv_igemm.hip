@@ -454,32 +454,36 @@ FEDMI_DEV bf16x8 frag_sw(const bf16* img, int i0, int kk, int lane) {
   return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((kc ^ (row & 7)) << 3));
 }
 
-// Three LDS stages, the DMA two K steps ahead (1 workgroup per CU at BN 128, 2 at BN 64); a two-stage
-// double buffer (one more workgroup per CU) measured slower and was removed.
+// LDS stages: BN 128 keeps 4 (128 KiB, the DMA three K steps ahead: the per-step L2 latency under a
+// full chip exceeds two steps of MFMA work at one workgroup per CU); BN 64 keeps 3 (72 KiB, two
+// workgroups per CU cover each other's latency).  A two-stage double buffer measured slower.
 template <int BN>
-__global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, const bf16* __restrict__ wt,
-                                                bf16* __restrict__ out, float* __restrict__ part,
-                                                double* __restrict__ stats, const float* __restrict__ shift,
-                                                TapGeom g, RowMap rmap, int ksteps_per_split,
-                                                const bf16* __restrict__ res, BnSums bs) {
+FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict__ wt, bf16* __restrict__ out,
+                             float* __restrict__ part, double* __restrict__ stats, const float* __restrict__ shift,
+                             const TapGeom& g, const RowMap& rmap, int ksteps_per_split,
+                             const bf16* __restrict__ res, const BnSums& bs, int tile, int split) {
   constexpr int BM = 128;
   constexpr int NA = BM / 32;            // A wave-instructions per stage per wave (8 rows each)
   constexpr int NB = BN / 32;
   constexpr int STAGE = (BM + BN) * 64;  // elements
   constexpr int TM = 4, TN = BN / 32;    // 16x16 fragments per wave: 64 x BN/2
-  constexpr int NST = 3;
+#ifndef FEDMI_TAP_NST128
+#define FEDMI_TAP_NST128 4
+#endif
+  constexpr int NST = BN == 128 ? FEDMI_TAP_NST128 : 3;
+  constexpr int AHEAD = NST - 1;         // K steps in flight beyond the one being consumed, at most
   // the epilogue reuses the stages for the bf16 tile and its partial sums
   constexpr int EPI = BM * (BN + 8) + 2 * 3 * 256 * 8;
   __shared__ __attribute__((aligned(16))) bf16 smem[NST * STAGE > EPI ? NST * STAGE : EPI];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (g.O + BN - 1) / BN;
-  const int tile_n = blockIdx.x % ntn, tile_m = blockIdx.x / ntn;
+  const int tile_n = tile % ntn, tile_m = tile / ntn;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * (BN / 2);
 
   const int ksteps = g.K / 64;
-  const int kb = blockIdx.z * ksteps_per_split;
+  const int kb = split * ksteps_per_split;
   const int ke = min(ksteps, kb + ksteps_per_split);
 
   // per-lane DMA sources: row (l >> 3) of each 8-row group, logical chunk kc
@@ -534,14 +538,19 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
 
-  // One barrier per K step: wait for this wave's DMA of step t (leaving step t+1's
-  // in flight), barrier (step t visible everywhere AND every wave is done reading
-  // step t-1's stage), refill that stage with step t+2, then MFMAs on step t.
-  if (kb < ke) issue(kb, 0);
-  if (kb + 1 < ke) issue(kb + 1, 1);
+  // One barrier per K step: wait for this wave's DMA of step t (leaving the up to AHEAD-1 later
+  // steps already issued in flight), barrier (step t visible everywhere AND every wave is done
+  // reading step t-1's stage), refill that stage with step t+AHEAD, then MFMAs on step t.
+#pragma unroll
+  for (int a = 0; a < AHEAD; ++a)
+    if (kb + a < ke) issue(kb + a, a);
   for (int t = kb; t < ke; ++t) {
     const int stg = (t - kb) % NST;
-    if (t + 1 < ke) {
+    const int later = min(ke - 1 - t, AHEAD - 1);     // issued steps after t still allowed in flight
+    if (later >= 2) {
+      if constexpr (NA + NB == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else if (later == 1) {
       if constexpr (NA + NB == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
@@ -550,9 +559,9 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    // refill the stage step t-1 used with step t+2 (every wave is past step t-1's reads once it
+    // refill the stage step t-1 used with step t+AHEAD (every wave is past step t-1's reads once it
     // passed this barrier)
-    if (t + 2 < ke) issue(t + 2, (stg + 2) % NST);
+    if (t + AHEAD < ke) issue(t + AHEAD, (stg + AHEAD) % NST);
     const bf16* As = smem + stg * STAGE;
     const bf16* Bs = As + BM * 64;
 #pragma unroll
@@ -572,7 +581,7 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
 
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
   if (part != nullptr) {   // split-K partial -> [split][M][O] fp32
-    float* ws = part + (long)blockIdx.z * g.M * g.O;
+    float* ws = part + (long)split * g.M * g.O;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = n0 + wn0 + 16 * j + col_l;
@@ -716,6 +725,43 @@ __global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, con
       if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, (double)t);
     }
   }
+}
+
+template <int BN>
+__global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+                                                bf16* __restrict__ out, float* __restrict__ part,
+                                                double* __restrict__ stats, const float* __restrict__ shift,
+                                                TapGeom g, RowMap rmap, int ksteps_per_split,
+                                                const bf16* __restrict__ res, BnSums bs) {
+  conv_tap_body<BN>(in, wt, out, part, stats, shift, g, rmap, ksteps_per_split, res, bs, blockIdx.x, blockIdx.z);
+}
+
+// The sub-pixel phases of a stride-2 DGRAD in ONE launch: blockIdx.x walks the phases' tiles in order,
+// blockIdx.z is the K split (phases with fewer splits return early, before any barrier).  Each phase
+// writes its own parity rows of dX (row maps), or its split-K partials into its own workspace slice.
+constexpr int MAX_TAP_PHASES = 4;
+struct TapMulti {
+  TapGeom g[MAX_TAP_PHASES];
+  RowMap rm[MAX_TAP_PHASES];
+  long woff[MAX_TAP_PHASES];       // weight-image offset (elements)
+  long wsoff[MAX_TAP_PHASES];      // workspace offset (floats), -1: no split (the epilogue writes dX)
+  int kps[MAX_TAP_PHASES];         // K steps per split
+  int splits[MAX_TAP_PHASES];
+  int tile0[MAX_TAP_PHASES + 1];   // first tile of each phase; tile0[n] = total
+  int n;
+};
+
+template <int BN>
+__global__ __launch_bounds__(256) void conv_tap_phases(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+                                                       bf16* __restrict__ out, float* __restrict__ ws,
+                                                       TapMulti tm, const bf16* __restrict__ res, BnSums bs) {
+  int p = 0;
+  while (p + 1 < tm.n && (int)blockIdx.x >= tm.tile0[p + 1]) ++p;
+  if ((int)blockIdx.z >= tm.splits[p]) return;
+  const bool split = tm.wsoff[p] >= 0;
+  conv_tap_body<BN>(in, wt + tm.woff[p], out, split ? ws + tm.wsoff[p] : nullptr, nullptr, nullptr, tm.g[p],
+                    tm.rm[p], tm.kps[p], split ? nullptr : res, split ? BnSums{} : bs,
+                    (int)blockIdx.x - tm.tile0[p], blockIdx.z);
 }
 
 // ---------------------------------------------------------------------------
@@ -1405,6 +1451,19 @@ static bool halo_geom(const TapGeom& g, const RowMap& rm, HaloGeom* h) {
   return true;
 }
 
+static void launch_tap_reduce(hipStream_t st, const TapGeom& g, const RowMap& rm, const float* ws, int splits,
+                              bf16* out, double* stats, const float* shift, const bf16* res, const BnSums& bs) {
+  const int VR = g.O / 8;
+  const int tb = (256 / VR) * VR;
+  const int rstep = tb / VR;
+  // with BN statistics / BN-backward sums fewer blocks (their per-channel atomics contend on 2 x O addresses)
+  const int rows_per_block = (stats || bs.rep) ? std::max(2 * rstep, (g.M + 255) / 256)
+                                               : std::max(rstep, (g.M + 1023) / 1024);
+  const int nblk = (g.M + rows_per_block - 1) / rows_per_block;
+  hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, splits, g.M, g.O, rm, out, stats, shift,
+                     rows_per_block, res, bs);
+}
+
 static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const bf16* wt, bf16* out, double* stats,
                        const float* shift, const RowMap& rm, float* ws, long ws_floats,
                        const bf16* res = nullptr, const BnSums& bs = BnSums{}) {
@@ -1424,17 +1483,7 @@ static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const b
     hipLaunchKernelGGL(conv_tap<128>, grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
   else
     hipLaunchKernelGGL(conv_tap<64>, grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
-  if (splits > 1) {
-    const int VR = g.O / 8;
-    const int tb = (256 / VR) * VR;
-    const int rstep = tb / VR;
-    // with BN statistics / BN-backward sums fewer blocks (their per-channel atomics contend on 2 x O addresses)
-    const int rows_per_block = (stats || bs.rep) ? std::max(2 * rstep, (g.M + 255) / 256)
-                                                 : std::max(rstep, (g.M + 1023) / 1024);
-    const int nblk = (g.M + rows_per_block - 1) / rows_per_block;
-    hipLaunchKernelGGL(conv_splitk_reduce, dim3(nblk), dim3(tb), 0, st, ws, splits, g.M, g.O, rm, out, stats, shift,
-                       rows_per_block, res, bs);
-  }
+  if (splits > 1) launch_tap_reduce(st, g, rm, ws, splits, out, stats, shift, res, bs);
 }
 
 // DGRAD phases as conv_tap problems over dY: (geometry, row map, image offset) per phase.
@@ -1474,6 +1523,96 @@ static int dgrad_tap_phases(const ConvShape& s, TapPhase* out) {
       off += (long)s.C * nr * ns * s.O;
     }
   return n;
+}
+
+// One-launch plan for the non-empty phases of a stride-2 DGRAD: no K split while their tiles fill the
+// chip (the phases run side by side instead of one small launch after another); otherwise split the
+// phase with the longest per-split K first (>= 8 K steps per split) until about one wave of workgroups,
+// within the workspace.  ws_need: floats the plan's split phases use.
+struct PhasePlan {
+  TapMulti tm;
+  int idx[MAX_TAP_PHASES];   // TapPhase index of each planned phase
+  int maxsp;
+  long ws_need;
+};
+
+static PhasePlan plan_tap_phases(const TapPhase* ph, int n, long ws_cap) {
+  PhasePlan pl{};
+  TapMulti& tm = pl.tm;
+  long tiles[MAX_TAP_PHASES], total = 0;
+  int ks[MAX_TAP_PHASES];
+  int bn = 0;
+  for (int i = 0; i < n; ++i) {
+    if (ph[i].empty) continue;
+    const int k = tm.n++;
+    pl.idx[k] = i;
+    bn = tap_bn(ph[i].g.O);
+    tiles[k] = (long)((ph[i].g.M + 127) / 128) * ((ph[i].g.O + bn - 1) / bn);
+    ks[k] = ph[i].g.K / 64;
+    tm.splits[k] = 1;
+    total += tiles[k];
+  }
+  auto need = [&](const int* sp) {
+    long w = 0;
+    for (int k = 0; k < tm.n; ++k)
+      if (sp[k] > 1) w += (long)sp[k] * ph[pl.idx[k]].g.M * ph[pl.idx[k]].g.O;
+    return w;
+  };
+  const long target = (bn == 128 ? 1l : 2l) * num_cus();
+  if (4 * total < 3 * target) {
+    long wgs = total;
+    for (;;) {
+      int best = -1;
+      double bestv = 0.0;
+      for (int k = 0; k < tm.n; ++k) {
+        const double v = (double)ks[k] / tm.splits[k];
+        if (ks[k] / (tm.splits[k] + 1) >= 8 && v > bestv) { best = k; bestv = v; }
+      }
+      if (best < 0 || wgs + tiles[best] > target) break;
+      int trial[MAX_TAP_PHASES];
+      for (int k = 0; k < tm.n; ++k) trial[k] = tm.splits[k] + (k == best ? 1 : 0);
+      if (need(trial) > ws_cap) break;
+      tm.splits[best] = trial[best];
+      wgs += tiles[best];
+    }
+  }
+  long off = 0, t0 = 0;
+  pl.maxsp = 1;
+  for (int k = 0; k < tm.n; ++k) {
+    const TapPhase& q = ph[pl.idx[k]];
+    tm.kps[k] = (ks[k] + tm.splits[k] - 1) / tm.splits[k];
+    tm.splits[k] = (ks[k] + tm.kps[k] - 1) / tm.kps[k];
+    tm.g[k] = q.g;
+    tm.rm[k] = q.rm;
+    tm.woff[k] = q.img_off;
+    tm.wsoff[k] = tm.splits[k] > 1 ? off : -1;
+    if (tm.splits[k] > 1) off += (long)tm.splits[k] * q.g.M * q.g.O;
+    tm.tile0[k] = (int)t0;
+    t0 += tiles[k];
+    pl.maxsp = std::max(pl.maxsp, tm.splits[k]);
+  }
+  tm.tile0[tm.n] = (int)t0;
+  pl.ws_need = off;
+  return pl;
+}
+
+// The phases of a stride-2 DGRAD as one conv_tap_phases launch (+ one split-K combine per split phase).
+static void launch_tap_phases(hipStream_t st, const TapPhase* ph, int n, const bf16* dy, const bf16* wd, bf16* dx,
+                              float* ws, long ws_floats, const bf16* res, const BnSums& bs) {
+  const PhasePlan pl = plan_tap_phases(ph, n, ws_floats);
+  const TapMulti& tm = pl.tm;
+  if (tm.n == 0) return;
+  for (int k = 0; k < tm.n; ++k)
+    if (tm.g[k].C % 64 || tm.g[k].O % 8 || tm.g[k].O != tm.g[0].O)
+      throw std::invalid_argument("conv_tap_phases: need C % 64 == 0, O % 8 == 0 and one O");
+  dim3 grid((unsigned)tm.tile0[tm.n], 1, (unsigned)pl.maxsp);
+  if (tap_bn(tm.g[0].O) == 128)
+    hipLaunchKernelGGL(conv_tap_phases<128>, grid, dim3(256), 0, st, dy, wd, dx, ws, tm, res, bs);
+  else
+    hipLaunchKernelGGL(conv_tap_phases<64>, grid, dim3(256), 0, st, dy, wd, dx, ws, tm, res, bs);
+  for (int k = 0; k < tm.n; ++k)
+    if (tm.splits[k] > 1)
+      launch_tap_reduce(st, tm.g[k], tm.rm[k], ws + tm.wsoff[k], tm.splits[k], dx, nullptr, nullptr, res, bs);
 }
 
 // FWD / DGRAD with automatic split-K through ``ws`` (null / 0 floats: never split).
@@ -1559,7 +1698,11 @@ void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const
   if (wd != nullptr && s.O % 64 == 0) {   // tap-major path on the dgrad weight image
     TapPhase ph[4];
     const int n = dgrad_tap_phases(s, ph);
+    if (n > 1) {   // stride 2: the tap phases in one launch, the tap-less parities zeroed below
+      launch_tap_phases(st, ph, n, dy, wd, dx, ws, ws_floats, acc ? dx : add, bs ? *bs : BnSums{});
+    }
     for (int i = 0; i < n; ++i) {
+      if (n > 1 && !ph[i].empty) continue;
       if (ph[i].empty) {   // zero this parity's rows with the generic kernel (K = 0)
         ConvGeom q = make_geom(s);
         q.NC = s.C; q.ph = ph[i].ph; q.pw = ph[i].pw; q.r0 = ph[i].r0; q.s0 = ph[i].s0; q.nr = 0; q.ns = 0;
@@ -1623,10 +1766,14 @@ long conv_fd_ws_floats(const ConvShape& s) {
   if (s.O % 64 == 0) {
     TapPhase ph[4];
     const int n = dgrad_tap_phases(s, ph);
-    for (int i = 0; i < n; ++i) {
-      if (ph[i].empty) continue;
-      const int tsp = tap_splits(ph[i].g, cap);
-      if (tsp > 1) need = std::max(need, (long)tsp * ph[i].g.M * ph[i].g.O);
+    if (n > 1) {
+      need = std::max(need, plan_tap_phases(ph, n, cap).ws_need);
+    } else {
+      for (int i = 0; i < n; ++i) {
+        if (ph[i].empty) continue;
+        const int tsp = tap_splits(ph[i].g, cap);
+        if (tsp > 1) need = std::max(need, (long)tsp * ph[i].g.M * ph[i].g.O);
+      }
     }
   }
   ConvGeom d = make_geom(s);

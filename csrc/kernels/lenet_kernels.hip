@@ -85,10 +85,13 @@ FEDMI_DEV void load_raw(const uint8_t* __restrict__ img, uint8_t* raw) {
     reinterpret_cast<uint4*>(raw)[threadIdx.x] = reinterpret_cast<const uint4*>(img)[threadIdx.x];
 }
 
+// NT = the launch's block size as a constant: blockDim.x is read from the dispatch packet, and the
+// s_waitcnt vmcnt(0) guarding that load would also drain every weight prefetch in flight
+template <int NT>
 FEDMI_DEV void zero_lds(void* p, int bytes) {
   uint4* q = reinterpret_cast<uint4*>(p);
   const uint4 z = make_uint4(0, 0, 0, 0);
-  for (int e = threadIdx.x; e < bytes / 16; e += blockDim.x) q[e] = z;
+  for (int e = threadIdx.x; e < bytes / 16; e += NT) q[e] = z;
 }
 
 }  // namespace
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
   // global read of the kernel start, issued together while the x image is zeroed
   bf16x8 wr1[4], wr2[7];
   load_raw(images + (size_t)gidx * IMG_BYTES, raw);
-  zero_lds(xcl, XCL * 2);   // channel 3 and the right/bottom pad stay zero
+  zero_lds<NT_FWD>(xcl, XCL * 2);   // channel 3 and the right/bottom pad stay zero
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) wr1[ks] = ld8(pk + PK_W1C + n16 * K1C + ks * 32 + kq);
 #pragma unroll
@@ -439,11 +442,11 @@ FEDMI_DEV BwdLds bwd_lds(unsigned char* scratch, const uint8_t* raw, const bf16*
 
 // zero the out-grad images, the shifted copies' tails (x' + s beyond the row) and the bias sums
 FEDMI_DEV void bwd_zero(const BwdLds& L) {
-  zero_lds(L.dY2w, BW_DY2W * 2);
-  zero_lds(L.dY2c, BW_DY2C * 2);
-  zero_lds(L.dY1, BW_DY1 * 2);
-  zero_lds(L.xsh, BW_XSH * 2);
-  zero_lds(L.p1sh, BW_P1SH * 2);
+  zero_lds<NT_CONV>(L.dY2w, BW_DY2W * 2);
+  zero_lds<NT_CONV>(L.dY2c, BW_DY2C * 2);
+  zero_lds<NT_CONV>(L.dY1, BW_DY1 * 2);
+  zero_lds<NT_CONV>(L.xsh, BW_XSH * 2);
+  zero_lds<NT_CONV>(L.p1sh, BW_P1SH * 2);
   if (threadIdx.x < 64) L.db[threadIdx.x] = 0.f;
 }
 
@@ -468,10 +471,6 @@ FEDMI_DEV void bwd_build_shifted_p1(const BwdLds& L, int tid, int nthr) {
     for (int sh = 0; sh < 5; ++sh)
       if (x >= sh) row[sh * (6 * 14 * 16) - sh] = v;
   }
-}
-FEDMI_DEV void bwd_build_shifted(const BwdLds& L, const Aug& a) {
-  bwd_build_shifted_img(L, a, threadIdx.x, NT_CONV);
-  bwd_build_shifted_p1(L, threadIdx.x, NT_CONV);
 }
 
 // d(pool2) -> conv2 out-grad images + conv2 bias sums, then conv2 wgrad + dgrad, conv1 wgrad,
@@ -669,7 +668,11 @@ constexpr int S_O_RAW = 0, S_O_P1R = 3072, S_O_AM1 = S_O_P1R + 2368, S_O_AM2 = S
 constexpr int S_W1C_LD = 136, S_W2C_LD = 232;
 constexpr int S_F_XCL = 0, S_F_C1 = S_F_XCL + 36 * 40 * 4 * 2, S_F_P1 = S_F_C1 + NPOS1 * 8 * 4,
               S_F_C2 = S_F_P1 + 14 * 14 * 8 * 2, S_F_END = S_F_C2 + C2 * NPOS2 * 4;
-constexpr int S_END = S_O_SCR + (S_F_END > BW_SCRATCH ? S_F_END : BW_SCRATCH);
+// fc1 cross-wave partials: [128 n][4 rows] for the forward, [16 waves][F0P] for dX (one region, two uses)
+constexpr int S_O_RED = S_O_SCR + (S_F_END > BW_SCRATCH ? S_F_END : BW_SCRATCH);
+constexpr int S_O_W3 = S_O_RED + NW_CONV * F0P * 4;    // fc3 image [16 n][96 f] bf16, staged with the conv weights
+constexpr int S_END = S_O_W3 + 16 * 96 * 2;
+static_assert(S_END <= 160 * 1024, "KS1 LDS");
 // FC scratch (floats, bf16-rounded values where the old MFMA path used bf16 operands)
 constexpr int SF_H1 = 0, SF_H2 = 128, SF_Z = 224, SF_DZ3 = 240, SF_DZ2 = 256, SF_DZ1 = 352, SF_END = 480;
 static_assert(SF_END * 4 <= 2048, "FC scratch");
@@ -691,6 +694,15 @@ FEDMI_DEV float sum8lanes(float v) {   // over the 8 consecutive lanes of a grou
   return v;
 }
 FEDMI_DEV float bfr(float v) { return (float)(bf16)v; }
+// sum over the 16 lanes of a DPP row (rotations: every lane of the row ends with the row total, each in a
+// fixed order -- deterministic)
+FEDMI_DEV float row_sum16(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x124, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x122, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x121, 0xf, 0xf, false));
+  return v;
+}
 
 __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
     const uint8_t* __restrict__ images, int sample_base, int nb,
@@ -718,6 +730,7 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
   float* dxs = reinterpret_cast<float*>(smem + S_O_DX);
   bf16* wdg = reinterpret_cast<bf16*>(smem + S_O_WDG);
   float* fcs = reinterpret_cast<float*>(smem + S_O_FC);
+  float* red = reinterpret_cast<float*>(smem + S_O_RED);
   unsigned char* scr = smem + S_O_SCR;
   bf16* xcl = reinterpret_cast<bf16*>(scr + S_F_XCL);
   float* c1 = reinterpret_cast<float*>(scr + S_F_C1);
@@ -729,20 +742,22 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
   //      16-B load per thread; both land while the x image is zeroed and the augmentation drawn
   bf16* w1c = reinterpret_cast<bf16*>(smem + S_O_W1C);
   bf16* w2c = reinterpret_cast<bf16*>(smem + S_O_W2C);
+  bf16* w3s = reinterpret_cast<bf16*>(smem + S_O_W3);
   float bias1, bias2;
   Aug a;
   {
-    // 192 image + 832 dgrad-weight + 256 conv1-weight + 448 conv2-weight 16-B chunks (<= 2 per thread)
-    constexpr int NI = IMG_BYTES / 16, NWD = 16 * KDGP / 8, NW1 = 16 * K1C / 8, NW2 = 16 * K2C / 8;
-    constexpr int E1 = NI, E2 = E1 + NWD, E3 = E2 + NW1, E4 = E3 + NW2;
+    // 192 image + 832 dgrad-weight + 256 conv1-weight + 448 conv2-weight + 192 fc3 16-B chunks (<= 2 per thread)
+    constexpr int NI = IMG_BYTES / 16, NWD = 16 * KDGP / 8, NW1 = 16 * K1C / 8, NW2 = 16 * K2C / 8, NW3 = 16 * 96 / 8;
+    constexpr int E1 = NI, E2 = E1 + NWD, E3 = E2 + NW1, E4 = E3 + NW2, E5 = E4 + NW3;
+    static_assert(E5 <= 2 * NT_CONV, "stage: two chunks per thread");
     uint4 v[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
 #ifdef FEDMI_STAMPS
     const int dg = fedmi_ks1_diag;
     const size_t img_sample = (dg & 2) ? 0 : (size_t)gidx;
-    const int lim = (dg & 1) ? E1 : E4;
+    const int lim = (dg & 1) ? E1 : E5;
 #else
     const size_t img_sample = (size_t)gidx;
-    constexpr int lim = E4;
+    constexpr int lim = E5;
 #endif
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -752,13 +767,14 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
       else if (e < E2) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2DG)[e - E1];
       else if (e < E3) v[u] = reinterpret_cast<const uint4*>(pk + PK_W1C)[e - E2];
       else if (e < E4) v[u] = reinterpret_cast<const uint4*>(pk + PK_W2C)[e - E3];
+      else if (e < E5) v[u] = reinterpret_cast<const uint4*>(pk + PK_FC3)[e - E4];
     }
     // the other global reads of the kernel's start go out in the same wave of requests (one
     // memory latency for the whole stage instead of one per dependent group)
     bias1 = n16 < C1 ? params[P_C1B + n16] : 0.f;
     bias2 = params[P_C2B + n16];
     a = aug_params(augment, seed, round_ctr, gidx);
-    zero_lds(xcl, 36 * 40 * 4 * 2);
+    zero_lds<NT_CONV>(xcl, 36 * 40 * 4 * 2);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int e = tid + u * NT_CONV;
@@ -773,6 +789,8 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
       } else if (e < E4) {
         const int w = e - E3, row = w / (K2C / 8), col = w - row * (K2C / 8);
         reinterpret_cast<uint4*>(w2c + row * S_W2C_LD)[col] = v[u];
+      } else if (e < E5) {
+        reinterpret_cast<uint4*>(w3s)[e - E4] = v[u];
       }
     }
   }
@@ -827,13 +845,18 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
       }
     }
   }
-  // fc1 weight chunks of this thread (row n = tid/8, k = q*8 + 64 i): in flight through pool1..pool2
-  const int fn = tid >> 3, fq = tid & 7;
+  // fc1 weights of this thread, in flight through pool1..pool2 and held in registers to the end of the
+  // FC backward: rows n = wave + 16 m (m < 8), columns k = 8 lane .. 8 lane + 7 (lanes >= 52 idle).
+  // The forward reduces over k (lanes: DPP row sums, then 4 rows across LDS), dX over n (in-thread over
+  // m, then 16 waves across LDS) -- one 106 KB read of W1 per sample, no transposed copy.
   // (every weight load below is unconditional from a clamped address and only its USE is guarded:
   //  a select between a loaded value and zero made the compiler wait for the load on the spot)
-  bf16x8 w1v[7];
+  const int fn = tid >> 3, fq = tid & 7;
+  constexpr int KCH = F0P / 8;                     // 52 16-B k chunks
+  const int kc = min(lane, KCH - 1);
+  bf16x8 w1r[8];
 #pragma unroll
-  for (int i = 0; i < 7; ++i) w1v[i] = ld8(pk + PK_FC1 + fn * F0P + min(fq * 8 + 64 * i, F0P - 8));
+  for (int m = 0; m < 8; ++m) w1r[m] = ld8(pk + PK_FC1 + (wave + 16 * m) * F0P + kc * 8);
   __syncthreads();
   FEDMI_STAMP(0, 2);
 
@@ -893,16 +916,13 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
     xrow[e] = mb;
     act2T[(size_t)e * MAX_TRAIN_BATCH + s] = mb;
   }
-  // fc2 / fc3 weight chunks and the FC biases
-  const int n2 = fn < 96 ? fn : 95, n3 = fn < 16 ? fn : 15;
-  bf16x8 w2v[2], w3v[2];
+  // fc2 weight chunks and the FC biases (fc3's 3 KB image is in LDS since the stage)
+  const int n2 = fn < 96 ? fn : 95;
+  bf16x8 w2v[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    w2v[i] = ld8(pk + PK_FC2 + n2 * 128 + fq * 8 + 64 * i);
-    w3v[i] = ld8(pk + PK_FC3 + n3 * 96 + min(fq * 8 + 64 * i, 88));
-  }
+  for (int i = 0; i < 2; ++i) w2v[i] = ld8(pk + PK_FC2 + n2 * 128 + fq * 8 + 64 * i);
   const int label = labels[s];
-  const float fb1 = params[P_F1B + min(fn, F1 - 1)];
+  const float fb1 = params[P_F1B + min(tid & 127, F1 - 1)];
   const float fb2 = params[P_F2B + min(fn, F2 - 1)];
   const float fb3 = params[P_F3B + min(fn, NCLS - 1)];
   __syncthreads();
@@ -914,30 +934,24 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
   unsigned char* auxp = aux;
   float* fcb = reinterpret_cast<float*>(auxp + AUX_FCB) + (size_t)s * FCB_N;
   {
-    float acc = 0.f;
+    const bf16x8 xv = ld8(xrow + kc * 8);
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int k = fq * 8 + 64 * i;
-      if (k < F0P) acc = dot8(ld8(xrow + k), w1v[i], acc);
-    }
-    acc = sum8lanes(acc);
-    if (fq == 0) {
-      const float h = bfr(fn < F1 ? fmaxf(acc + fb1, 0.f) : 0.f);
-      fcs[SF_H1 + fn] = h;
-      h1T[(size_t)fn * MAX_TRAIN_BATCH + s] = (bf16)h;
+    for (int m = 0; m < 8; ++m) {
+      const float p = row_sum16(lane < KCH ? dot8(xv, w1r[m], 0.f) : 0.f);
+      if ((lane & 15) == 0) red[(wave + 16 * m) * 4 + (lane >> 4)] = p;
     }
   }
-  // backward weight chunks: fc1^T rows (dX), fc2^T rows (dH1), fc3^T rows (dH2)
-  const int kx = tid >> 1, hx = tid & 1;
-  bf16x8 w1t[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) w1t[i] = ld8(pk + PK_FC1T + min(kx, F0 - 1) * 128 + hx * 8 + 16 * i);
+  // backward weight chunks: fc2^T rows (dH1)
   bf16x8 w2t[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) w2t[i] = ld8(pk + PK_FC2T + fn * 96 + min(fq * 8 + 64 * i, 88));
-  bf16x8 w3t[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) w3t[i] = ld8(pk + PK_FC3T + min(tid, 95) * 32 + 8 * i);
+  __syncthreads();
+  if (tid < 128) {             // h1[n] = relu(sum of the 4 row partials + b1), rows in order
+    const float* r = red + tid * 4;
+    const float h = bfr(tid < F1 ? fmaxf(((r[0] + r[1]) + r[2]) + r[3] + fb1, 0.f) : 0.f);
+    fcs[SF_H1 + tid] = h;
+    h1T[(size_t)tid * MAX_TRAIN_BATCH + s] = (bf16)h;
+  }
   __syncthreads();
 
   FEDMI_STAMP(1, 0);
@@ -961,7 +975,7 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      if (fq * 8 + 64 * i < 96) acc = dot8f(fcs + SF_H2 + fq * 8 + 64 * i, w3v[i], acc);
+      if (fq * 8 + 64 * i < 96) acc = dot8f(fcs + SF_H2 + fq * 8 + 64 * i, ld8(w3s + fn * 96 + fq * 8 + 64 * i), acc);
     acc = sum8lanes(acc);
     if (fq == 0) fcs[SF_Z + fn] = fn < NCLS ? acc + fb3 : 0.f;
   } else {
@@ -1006,7 +1020,7 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
   if (tid < 96) {
     float acc = 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) acc = dot8f(fcs + SF_DZ3 + 8 * i, w3t[i], acc);
+    for (int n = 0; n < NCLS; ++n) acc += fcs[SF_DZ3 + n] * (float)w3s[n * 96 + tid];   // W3 column tid from LDS
     const float g = (tid < F2 && fcs[SF_H2 + tid] > 0.f) ? acc : 0.f;
     fcs[SF_DZ2 + tid] = bfr(g);
     reinterpret_cast<bf16*>(auxp + AUX_DZ2T)[(size_t)tid * MAX_TRAIN_BATCH + s] = (bf16)g;
@@ -1030,13 +1044,30 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
   }
   __syncthreads();
   FEDMI_STAMP(1, 5);
-  // ---- dX = dZ1 . W1, masked by the pool2 ReLU -> d(pool2) in LDS
+  // ---- dX = dZ1 . W1 from the forward's register fragments: in-thread over the 8 rows, then the 16
+  //      waves' partials in wave order, masked by the pool2 ReLU -> d(pool2) in LDS
   {
+    float d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = 0.f;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const float g = fcs[SF_DZ1 + wave + 16 * m];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] += g * (float)w1r[m][j];
+    }
+    if (lane < KCH) {
+      float4* o = reinterpret_cast<float4*>(red + wave * F0P + lane * 8);
+      o[0] = make_float4(d[0], d[1], d[2], d[3]);
+      o[1] = make_float4(d[4], d[5], d[6], d[7]);
+    }
+  }
+  __syncthreads();
+  if (tid < F0) {
     float acc = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc = dot8f(fcs + SF_DZ1 + hx * 8 + 16 * i, w1t[i], acc);
-    acc += __shfl_xor(acc, 1, 64);
-    if (hx == 0 && kx < F0) dxs[kx] = (float)xrow[kx] > 0.f ? acc : 0.f;
+    for (int w = 0; w < NW_CONV; ++w) acc += red[w * F0P + tid];
+    dxs[tid] = (float)xrow[tid] > 0.f ? acc : 0.f;
   }
   __syncthreads();             // d(pool2) from every wave before the conv backward scatters it
   FEDMI_STAMP(0, 6);
@@ -1060,7 +1091,6 @@ FEDMI_DEV void pack_one(int i, float w, bf16* __restrict__ pk) {
   } else if (i < P_F1B) {
     const int j = i - P_F1W, n = j / F0, f = j - n * F0;
     pk[PK_FC1 + n * F0P + f] = v;
-    pk[PK_FC1T + f * 128 + n] = v;
   } else if (i < P_F2W) {
   } else if (i < P_F2B) {
     const int j = i - P_F2W, n = j / F1, f = j - n * F1;
@@ -1070,7 +1100,6 @@ FEDMI_DEV void pack_one(int i, float w, bf16* __restrict__ pk) {
   } else if (i < P_F3B) {
     const int j = i - P_F3W, n = j / F2, f = j - n * F2;
     pk[PK_FC3 + n * 96 + f] = v;
-    pk[PK_FC3T + f * 32 + n] = v;
   }
 }
 

@@ -57,12 +57,10 @@ constexpr int PK_W1C  = 0;                      // [16 o][128 k]       conv1 B
 constexpr int PK_W2C  = PK_W1C + 16 * K1C;      // [16 o][224 k]       conv2 B
 constexpr int PK_W2DG = PK_W2C + 16 * K2C;      // [16 c][416 (r,s,o)] conv2 dgrad B
 constexpr int PK_FC1  = PK_W2DG + 16 * KDGP;    // [128 n][416 f]      fc1 fwd B
-constexpr int PK_FC1T = PK_FC1 + 128 * F0P;     // [400 f][128 n]      fc1 dgrad B
-constexpr int PK_FC2  = PK_FC1T + F0 * 128;     // [96 n][128 f]       fc2 fwd B
+constexpr int PK_FC2  = PK_FC1 + 128 * F0P;     // [96 n][128 f]       fc2 fwd B (fc1's dX reuses PK_FC1)
 constexpr int PK_FC2T = PK_FC2 + 96 * 128;      // [128 f][96 n]       fc2 dgrad B
-constexpr int PK_FC3  = PK_FC2T + 128 * 96;     // [16 n][96 f]        fc3 fwd B
-constexpr int PK_FC3T = PK_FC3 + 16 * 96;       // [96 f][32 n]        fc3 dgrad B
-constexpr int PK_TOTAL = PK_FC3T + 96 * 32;
+constexpr int PK_FC3  = PK_FC2T + 128 * 96;     // [16 n][96 f]        fc3 fwd + dgrad (KS1 stages it in LDS)
+constexpr int PK_TOTAL = PK_FC3 + 16 * 96;
 
 // ---- training-step geometry -------------------------------------------------
 constexpr int MAX_TRAIN_BATCH = 128;     // reference batch (src/main.py:140)

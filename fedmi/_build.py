@@ -45,7 +45,7 @@ SOURCES = [
 HEADERS = sorted(CSRC.rglob("*.h"))
 
 
-VARIANTS = {"": [], "stamps": ["-DFEDMI_STAMPS"]}
+VARIANTS = {"": [], "stamps": ["-DFEDMI_STAMPS"], "tap3": ["-DFEDMI_TAP_NST128=3"]}   # tap3: A/B build
 
 
 def ext_path(variant: str = "") -> Path:
@@ -120,10 +120,13 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--stamps", action="store_true", help="also build the per-phase timestamp diagnostic variant")
+    ap.add_argument("--variant", default="", choices=[v for v in VARIANTS if v], help="also build this variant")
     a = ap.parse_args(argv)
     build(force=a.force, jobs=a.jobs)
     if a.stamps:
         build(force=a.force, jobs=a.jobs, variant="stamps")
+    if a.variant:
+        build(force=a.force, jobs=a.jobs, variant=a.variant)
     return 0
 
 

@@ -25,9 +25,8 @@ import torch.distributed as dist
 def model_digest(trainer) -> bytes:
     """16-byte blake2b of the bytes of the trainer's flat fp32 state and its integer buffers."""
     h = hashlib.blake2b(digest_size=16)
-    h.update(trainer.float_state().detach().contiguous().cpu().view(torch.uint8).numpy().tobytes())
-    for b in trainer.int_state():
-        h.update(b.detach().contiguous().cpu().view(torch.uint8).numpy().tobytes())
+    for t in [trainer.float_state(), *trainer.int_state()]:      # BN counters are 0-dim int64 tensors
+        h.update(t.detach().reshape(-1).contiguous().cpu().view(torch.uint8).numpy().tobytes())
     return h.digest()
 
 

@@ -22,7 +22,7 @@ class _Stub:
     def __init__(self, n: int = 257, seed: int = 7):
         g = torch.Generator().manual_seed(seed)
         self.flat = torch.randn(n, generator=g)
-        self.ints = [torch.tensor([5], dtype=torch.int64)]
+        self.ints = [torch.tensor(5, dtype=torch.int64), torch.tensor([3], dtype=torch.int64)]   # BN counters: 0-dim
 
     def float_state(self):
         return self.flat

@@ -146,8 +146,16 @@ def test_pack_layout(env):
     assert torch.equal(fc1[:120, :400], bf(sd["fc1.weight"]))
     assert fc1[120:].abs().sum() == 0 and fc1[:, 400:].abs().sum() == 0
     off += 128 * 416
-    fc1t = pk[off:off + 400 * 128].view(400, 128)
-    assert torch.equal(fc1t[:, :120], bf(sd["fc1.weight"].t()))
+    fc2 = pk[off:off + 96 * 128].view(96, 128)
+    assert torch.equal(fc2[:84, :120], bf(sd["fc2.weight"]))
+    off += 96 * 128
+    fc2t = pk[off:off + 128 * 96].view(128, 96)
+    assert torch.equal(fc2t[:120, :84], bf(sd["fc2.weight"].t()))
+    off += 128 * 96
+    fc3 = pk[off:off + 16 * 96].view(16, 96)
+    assert torch.equal(fc3[:10, :84], bf(sd["fc3.weight"]))
+    assert fc3[10:].abs().sum() == 0 and fc3[:, 84:].abs().sum() == 0
+    assert off + 16 * 96 == pk.numel()
 
 
 def test_conv_fwd_matches_torch(env):
@@ -202,8 +210,16 @@ def test_step_matches_torch_math(env, start, nb, augment):
     nat, dev, ds, ref, tr = env
     tr.load_state_dict(ref.state_dict())
     tr.round_ctr.zero_()
+    if not augment:              # the engine's augmentation flag is fixed at binding time: rebind without it
+        tr.cfg.augment = False
+        tr.set_train_data(ds.train)
     X, pool1, am1, am2 = _forward_oracle(nat, tr, start, nb, augment)
-    g, stats = _step_grad(tr, start, nb)
+    try:
+        g, stats = _step_grad(tr, start, nb)
+    finally:
+        if not augment:
+            tr.cfg.augment = True
+            tr.set_train_data(ds.train)
     sd = {k: v.float() for k, v in ref.state_dict().items()}
     W1, W2, W3 = _bf(sd["fc1.weight"]), _bf(sd["fc2.weight"]), _bf(sd["fc3.weight"])
     y = ds.train.y[start:start + nb].long()
@@ -226,7 +242,11 @@ def test_step_matches_torch_math(env, start, nb, augment):
     st = stats.cpu()
     assert int(st[2]) == nb
     assert abs(float(st[0:1].view(torch.float32)) - loss) < 1e-3 * max(1.0, abs(loss))
-    assert abs(int(st[1]) - int((z.argmax(1) == y).sum())) <= 1
+    # argmax flips only where the two top logits are within the kernels' rounding noise: H1 / H2 are bf16
+    # (an fp32 summation-order difference can move a value across a bf16 rounding boundary, 2^-8 relative)
+    top2 = z.topk(2, 1).values
+    ties = int(((top2[:, 0] - top2[:, 1]) < 1e-2 * z.abs().amax(1).clamp_min(1e-3)).sum())
+    assert abs(int(st[1]) - int((z.argmax(1) == y).sum())) <= ties + 1
     # ---- conv backward from d(pool2) and the saved pool1 / argmax codes
     dX = (dz1b @ W1) * (X > 0)                                            # d(pool2)  [nb, 400]
     C2W, C1W = _bf(sd["conv2.weight"]), _bf(sd["conv1.weight"])

@@ -28,32 +28,12 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 N_TRAIN, N_TEST, BATCH = 50000, 10000, 128
 
 
-def main() -> int:
-    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--model", default="resnet18")
-    ap.add_argument("--clients", type=int, default=2)
-    ap.add_argument("--noniid", type=int, default=0, help="label shards per client (0 = strided IID)")
-    ap.add_argument("--rounds", type=int, default=8)
-    ap.add_argument("--engine", choices=["native", "fp32", "bf16"], default="native",
-                    help="bf16: PyTorch autocast bf16 (torch's own mixed precision of the same model)")
-    ap.add_argument("--n-train", type=int, default=N_TRAIN)
-    ap.add_argument("--n-test", type=int, default=N_TEST)
-    ap.add_argument("--lr", type=float, default=0.1)
-    ap.add_argument("--seed", type=int, default=17)
-    ap.add_argument("--out", default=None, help="JSONL, one record per round")
-    ap.add_argument("--no-augment", action="store_true", help="no crop/flip (diagnostics)")
-    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of graph replay (diagnostics)")
-    a = ap.parse_args()
-    if a.engine in ("fp32", "bf16"):
-        os.environ["FEDMI_TORCH_PATH"] = "1"
-
+def _run_seed(a, seed, data, dev, out) -> None:
     from fedmi.engine import build_trainer
     from fedmi.engine.base import TrainerConfig
-    from fedmi.engine.data import contiguous_schedule, label_shard_indices, make_dataset, strided_schedule
+    from fedmi.engine.data import contiguous_schedule, label_shard_indices, strided_schedule
 
-    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
-    data = make_dataset("synthetic-cifar10", device=dev, n_train=a.n_train, n_test=a.n_test, seed=0)
-    cfg = TrainerConfig(seed=a.seed, lr=a.lr, augment=not a.no_augment, use_graph=not a.no_graph)
+    cfg = TrainerConfig(seed=seed, lr=a.lr, augment=not a.no_augment, use_graph=not a.no_graph)
     W = a.clients
     clients = []
     init = None
@@ -73,7 +53,6 @@ def main() -> int:
         else:
             tr.set_schedule(*strided_schedule(a.n_train, BATCH, r, W))
         clients.append(tr)
-    out = open(a.out, "w") if a.out else None
     for rnd in range(1, a.rounds + 1):
         t0 = time.perf_counter()
         tstats = []
@@ -92,7 +71,7 @@ def main() -> int:
         clients[0].evaluate()
         ev = clients[0].eval_stats()
         torch.cuda.synchronize() if dev.type == "cuda" else None
-        rec = {"round": rnd, "engine": a.engine, "model": a.model, "clients": W, "lr": a.lr, "seed": a.seed,
+        rec = {"round": rnd, "engine": a.engine, "model": a.model, "clients": W, "lr": a.lr, "seed": seed,
                "augment": not a.no_augment, "graph": not a.no_graph,
                "split": f"noniid-{a.noniid}" if a.noniid else "strided-iid",
                "train_loss": [round(s.loss, 4) for s in tstats], "train_acc": [round(s.acc, 2) for s in tstats],
@@ -103,6 +82,37 @@ def main() -> int:
         if out:
             out.write(line + "\n")
             out.flush()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--model", default="resnet18")
+    ap.add_argument("--clients", type=int, default=2)
+    ap.add_argument("--noniid", type=int, default=0, help="label shards per client (0 = strided IID)")
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--engine", choices=["native", "fp32", "bf16"], default="native",
+                    help="bf16: PyTorch autocast bf16 (torch's own mixed precision of the same model)")
+    ap.add_argument("--n-train", type=int, default=N_TRAIN)
+    ap.add_argument("--n-test", type=int, default=N_TEST)
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--seed", type=int, default=17)
+    ap.add_argument("--seeds", default="", help="comma list: run each seed in turn (one process)")
+    ap.add_argument("--out", default=None, help="JSONL, one record per round")
+    ap.add_argument("--no-augment", action="store_true", help="no crop/flip (diagnostics)")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of graph replay (diagnostics)")
+    a = ap.parse_args()
+    if a.engine in ("fp32", "bf16"):
+        os.environ["FEDMI_TORCH_PATH"] = "1"
+
+    from fedmi.engine.data import make_dataset
+
+    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    data = make_dataset("synthetic-cifar10", device=dev, n_train=a.n_train, n_test=a.n_test, seed=0)
+    seeds = [int(v) for v in a.seeds.split(",")] if a.seeds else [a.seed]
+    out = open(a.out, "w") if a.out else None
+    for seed in seeds:
+        _run_seed(a, seed, data, dev, out)
+        torch.cuda.empty_cache() if dev.type == "cuda" else None
     return 0
 
 
