@@ -157,6 +157,10 @@ def main() -> int:
                          "the 10k test set is split over the clients and the accumulators summed")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--ckpt-dir", default=None)
+    ap.add_argument("--ckpt-slots", type=int, default=4, help="pinned snapshot slots of the checkpoint writer")
+    ap.add_argument("--ckpt-coalesce", action="store_true",
+                    help="a writer that falls behind by --ckpt-slots rounds supersedes queued rounds (files "
+                         "still end at the newest round) instead of stalling the round loop")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--trace", action="store_true",
                     help="print every rank's per-round train/test stats to stderr (synchronising: not for timing)")
@@ -244,7 +248,7 @@ def main() -> int:
     prim = mount_dir(root, primary=True) if rank == 0 else None
     cpath = client_ckpt_path(root, f"client{rank}")
     # native C++ writer (fedmi/ckpt, csrc/runtime/ckpt_writer.cpp); every round is written, in order
-    writer = RoundCheckpointWriter()
+    writer = RoundCheckpointWriter(slots=args.ckpt_slots, coalesce=args.ckpt_coalesce)
     PHASES = ("train", "allreduce", "eval", "checkpoint")
     marks = []          # --breakdown: per round, (host perf_counter, cuda event) at each phase boundary
     fault_round = args.warmup if args.inject_fault == "skip-allreduce" and rank == world - 1 else -1

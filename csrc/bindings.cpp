@@ -186,8 +186,8 @@ static void fedmi_bind(py::module_& m) {
   });
 }
 
-#ifdef FEDMI_STAMPS
-PYBIND11_MODULE(_fedmi_native_stamps, m) { fedmi_bind(m); }
-#else
-PYBIND11_MODULE(_fedmi_native, m) { fedmi_bind(m); }
+// the module name carries the build variant (fedmi/_build.py VARIANTS): -DFEDMI_MODULE=_fedmi_native_<v>
+#ifndef FEDMI_MODULE
+#define FEDMI_MODULE _fedmi_native
 #endif
+PYBIND11_MODULE(FEDMI_MODULE, m) { fedmi_bind(m); }

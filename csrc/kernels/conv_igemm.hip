@@ -454,9 +454,9 @@ FEDMI_DEV bf16x8 frag_sw(const bf16* img, int i0, int kk, int lane) {
   return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((kc ^ (row & 7)) << 3));
 }
 
-// LDS stages: BN 128 keeps 4 (128 KiB, the DMA three K steps ahead: the per-step L2 latency under a
-// full chip exceeds two steps of MFMA work at one workgroup per CU); BN 64 keeps 3 (72 KiB, two
-// workgroups per CU cover each other's latency).  A two-stage double buffer measured slower.
+// Three LDS stages, the DMA two K steps ahead (1 workgroup per CU at BN 128, 2 at BN 64).  Measured
+// slower: a two-stage double buffer (one more workgroup per CU), and four stages at BN 128 (128 KiB, the
+// DMA three steps ahead: +5..13 % per conv, profiles/r4_cnn/tap_stages_ab.txt).
 template <int BN>
 FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict__ wt, bf16* __restrict__ out,
                              float* __restrict__ part, double* __restrict__ stats, const float* __restrict__ shift,
@@ -467,10 +467,7 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
   constexpr int NB = BN / 32;
   constexpr int STAGE = (BM + BN) * 64;  // elements
   constexpr int TM = 4, TN = BN / 32;    // 16x16 fragments per wave: 64 x BN/2
-#ifndef FEDMI_TAP_NST128
-#define FEDMI_TAP_NST128 4
-#endif
-  constexpr int NST = BN == 128 ? FEDMI_TAP_NST128 : 3;
+  constexpr int NST = 3;
   constexpr int AHEAD = NST - 1;         // K steps in flight beyond the one being consumed, at most
   // the epilogue reuses the stages for the bf16 tile and its partial sums
   constexpr int EPI = BM * (BN + 8) + 2 * 3 * 256 * 8;

@@ -45,7 +45,9 @@ SOURCES = [
 HEADERS = sorted(CSRC.rglob("*.h"))
 
 
-VARIANTS = {"": [], "stamps": ["-DFEDMI_STAMPS"], "tap3": ["-DFEDMI_TAP_NST128=3"]}   # tap3: A/B build
+# build variants: the module name carries the variant (csrc/bindings.cpp FEDMI_MODULE); an A/B build adds
+# its -D switch here for one experiment and is removed with the losing code
+VARIANTS = {"": [], "stamps": ["-DFEDMI_STAMPS", "-DFEDMI_MODULE=_fedmi_native_stamps"]}
 
 
 def ext_path(variant: str = "") -> Path:
