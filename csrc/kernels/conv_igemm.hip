@@ -577,6 +577,9 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
   __syncthreads();   // every wave done with the stages (no DMA in flight) before LDS reuse
 
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  // (Combining the splits in-kernel -- the last-arriving split sums the tile's partials and runs this
+  // epilogue, no combine launch -- measured 1.3-2.2x slower at l3 / l4: each last arriver reads 3 x 64 KB of
+  // partials serially, profiles/r4_cnn/README.md.)
   if (part != nullptr) {   // split-K partial -> [split][M][O] fp32
     float* ws = part + (long)split * g.M * g.O;
 #pragma unroll

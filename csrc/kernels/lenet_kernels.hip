@@ -1149,10 +1149,12 @@ FEDMI_DEV f32x4 batch_tile(const bf16* __restrict__ a, const bf16* __restrict__ 
     av[ks] = ld8(a + n16 * MAX_TRAIN_BATCH + ks * 32 + kq);
     bv[ks] = ld8(b + n16 * MAX_TRAIN_BATCH + ks * 32 + kq);
   }
+  // unconditional loads from a clamped index (the callers only use p / m where idx >= 0): a select between
+  // a loaded value and zero makes the compiler wait for each load on the spot
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    p[r] = idx[r] >= 0 ? params[idx[r]] : 0.f;
-    m[r] = idx[r] >= 0 ? mom[idx[r]] : 0.f;
+    p[r] = params[idx[r] >= 0 ? idx[r] : 0];
+    m[r] = mom[idx[r] >= 0 ? idx[r] : 0];
   }
   f32x4 acc = zero4();
 #pragma unroll
@@ -1186,14 +1188,12 @@ __global__ __launch_bounds__(256) void lenet_sgd2(
     if (g == 0 && i < CS) { p = params[i]; m = mom[i]; }
     float sum = 0.f;
     if (i < CS) {
+      // every load unconditional from a clamped sample (masked after): one memory latency for all 8
       float v[MAX_TRAIN_BATCH / 16];
 #pragma unroll
-      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) {
-        const int q = g + 16 * u;
-        v[u] = q < nb ? conv_slab[(size_t)q * CS + i] : 0.f;
-      }
+      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) v[u] = conv_slab[(size_t)min(g + 16 * u, nb - 1) * CS + i];
 #pragma unroll
-      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) sum += v[u];
+      for (int u = 0; u < MAX_TRAIN_BATCH / 16; ++u) sum += g + 16 * u < nb ? v[u] : 0.f;
     }
     red[g][pl] = sum;
     __syncthreads();
@@ -1268,13 +1268,10 @@ __global__ __launch_bounds__(256) void lenet_sgd2(
     if (e < SGD2_NE && j < 214) {
       float v[32];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) {
-        const int sm = g * 32 + u;
-        v[u] = sm < nb ? fcb[(size_t)sm * FCB_N + j] : 0.f;
-      }
+      for (int u = 0; u < 32; ++u) v[u] = fcb[(size_t)min(g * 32 + u, nb - 1) * FCB_N + j];
       float sum = 0.f;
 #pragma unroll
-      for (int u = 0; u < 32; ++u) sum += v[u];
+      for (int u = 0; u < 32; ++u) sum += g * 32 + u < nb ? v[u] : 0.f;
       bsum[g][tid & 63] = sum;
     } else if (e == SGD2_NE && g == 0 && stats != nullptr) {
       const float* lv = reinterpret_cast<const float*>(aux + AUX_LOSS);

@@ -60,6 +60,15 @@ def main():
             print(f"    fc.dX          med {np.median(k0[:len(f), 6] - prev):8.0f}")
         names = {3: ("sgd2", ["all"])}
         nwg = {3: 249}
+        # KS2 by role (lenet_sgd2 block ranges): conv slab combine, fc1 / fc2 / fc3 weight tiles, biases + loss
+        k2 = st[3, :249, :2]
+        dur = k2[:, 1] - k2[:, 0]
+        t0 = k2[k2[:, 0] > 0, 0].min()
+        for role, lo, hi in (("conv slab", 0, 180), ("fc1 tiles", 180, 230), ("fc2 tiles", 230, 242),
+                             ("fc3 tiles", 242, 244), ("bias+loss", 244, 249)):
+            d = dur[lo:hi]
+            end = k2[lo:hi, 1] - t0
+            print(f"    sgd2 {role:10s} med {np.median(d):8.0f}  max {d.max():8.0f}  last end {end.max():8.0f}")
     for k, (name, phases) in names.items():
         a = st[k, :nwg[k], :len(phases) + 1]
         a = a[a[:, 0] > 0]
