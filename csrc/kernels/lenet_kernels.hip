@@ -1216,9 +1216,11 @@ __global__ __launch_bounds__(256) void lenet_sgd2(
       }
       const f32x4 acc = batch_tile(dZ1T + (size_t)nt * 16 * DZ1_LD, act2T + (size_t)ft * 16 * MAX_TRAIN_BATCH, nb,
                                    params, mom, idx, p, m);
+      FEDMI_STAMP(3, 2);    // operands landed + MFMA (wave 0's tile)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (idx[r] >= 0) sgd_apply(idx[r], acc[r], p[r], m[r], params, mom, pk, lr, momentum, wd);
+      FEDMI_STAMP(3, 3);
     }
   } else if (b < SGD_NA + SGD2_NB + SGD2_NC) {        // fc2.weight [84][120]: 6 x 8 tiles
     const int t = (b - SGD_NA - SGD2_NB) * 4 + wave;

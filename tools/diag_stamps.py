@@ -69,6 +69,11 @@ def main():
             d = dur[lo:hi]
             end = k2[lo:hi, 1] - t0
             print(f"    sgd2 {role:10s} med {np.median(d):8.0f}  max {d.max():8.0f}  last end {end.max():8.0f}")
+        f1 = st[3, 180:230, :4]
+        f1 = f1[f1[:, 2] > 0]
+        if len(f1):
+            print(f"    sgd2 fc1 split: start->operands+MFMA med {np.median(f1[:, 2] - f1[:, 0]):8.0f}  "
+                  f"SGD stores issued med {np.median(f1[:, 3] - f1[:, 2]):8.0f}  -> end med {np.median(f1[:, 1] - f1[:, 3]):8.0f}")
     for k, (name, phases) in names.items():
         a = st[k, :nwg[k], :len(phases) + 1]
         a = a[a[:, 0] > 0]
