@@ -817,13 +817,35 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
   __syncthreads();
   FEDMI_STAMP(0, 1);
 
-  // ---- conv1 (+bias+ReLU): 49 tiles over 16 waves, two tiles per pass
+  // ---- conv1 (+bias+ReLU) with maxpool #1 in registers: a tile's 16 rows are 4 pooling windows x their 4
+  //      positions in argmax-code order (row 4g + r, r = dy * 2 + dx: 0=(0,0) 1=(0,1) 2=(1,0) 3=(1,1)), so the
+  //      lane holding C rows 4g..4g+3 of channel n16 has one whole window -- max and first-max code straight
+  //      from the accumulators, no fp32 conv1 image and no pooling pass (49 tiles over 16 waves, two per pass)
+  auto c1_row = [&](int tt) {                        // A row n16 of tile tt in the channels-last image
+    const int q = tt * 4 + (n16 >> 2), y = 2 * (q / P1) + ((n16 >> 1) & 1), x = 2 * (q % P1) + (n16 & 1);
+    return xcl + (y * 40 + x) * 4;
+  };
+  auto pool1 = [&](const f32x4& v, int tt) {
+    if (n16 < 8) {                                   // channels 6, 7: zero padding of the conv2 operand
+      const int q = tt * 4 + (lane >> 4);
+      float m = fmaxf(v[0] + bias1, 0.f), c;
+      int am = 0;
+      c = fmaxf(v[1] + bias1, 0.f); if (c > m) { m = c; am = 1; }
+      c = fmaxf(v[2] + bias1, 0.f); if (c > m) { m = c; am = 2; }
+      c = fmaxf(v[3] + bias1, 0.f); if (c > m) { m = c; am = 3; }
+      const bf16 mb = (bf16)m;
+      p1cl[q * 8 + n16] = mb;
+      if (n16 < C1) {
+        p1r[n16 * 196 + q] = mb;
+        am1s[n16 * 196 + q] = (uint8_t)am;
+      }
+    }
+  };
   for (int t = wave; t < NPOS1 / 16; t += 2 * NW_CONV) {
     const int tb = t + NW_CONV;
     const bool two = tb < NPOS1 / 16;
-    const int pa = t * 16 + n16, pb = (two ? tb : t) * 16 + n16;
-    const bf16* xa = xcl + ((pa / O1) * 40 + pa % O1) * 4;
-    const bf16* xbb = xcl + ((pb / O1) * 40 + pb % O1) * 4;
+    const bf16* xa = c1_row(t);
+    const bf16* xbb = c1_row(two ? tb : t);
     bf16x8 fa[4], fb[4];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -836,14 +858,8 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
       acc = mfma16(fa[ks], wb1[ks], acc);
       accb = mfma16(fb[ks], wb1[ks], accb);
     }
-    if (n16 < C1) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) c1[(t * 16 + rq + r) * 8 + n16] = fmaxf(acc[r] + bias1, 0.f);
-      if (two) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) c1[(tb * 16 + rq + r) * 8 + n16] = fmaxf(accb[r] + bias1, 0.f);
-      }
-    }
+    pool1(acc, t);
+    if (two) pool1(accb, tb);
   }
   // fc1 weights of this thread, in flight through pool1..pool2 and held in registers to the end of the
   // FC backward: rows n = wave + 16 m (m < 8), columns k = 8 lane .. 8 lane + 7 (lanes >= 52 idle).
@@ -859,63 +875,39 @@ __global__ __launch_bounds__(NT_CONV) void lenet_sample_step(
   for (int m = 0; m < 8; ++m) w1r[m] = ld8(pk + PK_FC1 + (wave + 16 * m) * F0P + kc * 8);
   __syncthreads();
   FEDMI_STAMP(0, 2);
+  FEDMI_STAMP(0, 3);                                 // (pool1 is fused into conv1: empty phase)
 
-  // ---- maxpool2 #1 (+ argmax code: 0=(0,0) 1=(0,1) 2=(1,0) 3=(1,1), first max wins)
-  for (int e = tid; e < 14 * 14 * 8; e += NT_CONV) {
-    const int pos = e >> 3, c = e & 7;
-    bf16 mb = (bf16)0.f;
-    if (c < C1) {
-      const int py = pos / P1, px = pos - py * P1;
-      const float* w = c1 + ((2 * py) * O1 + 2 * px) * 8 + c;
-      float m = w[0]; int am = 0;
-      if (w[8] > m) { m = w[8]; am = 1; }
-      if (w[O1 * 8] > m) { m = w[O1 * 8]; am = 2; }
-      if (w[O1 * 8 + 8] > m) { m = w[O1 * 8 + 8]; am = 3; }
-      mb = (bf16)m;
-      p1r[c * 196 + pos] = mb;
-      am1s[c * 196 + pos] = (uint8_t)am;
-    }
-    p1cl[e] = mb;
-  }
-  __syncthreads();
-  FEDMI_STAMP(0, 3);
-
-  // ---- conv2 (+bias+ReLU): M = 100 positions (7 tiles), N = 16, K = 224
+  // ---- conv2 (+bias+ReLU) with maxpool #2 in registers (rows: 25 windows x 4 positions, 7 tiles) -> act2
+  //      row (torch .view order o * 25 + py * 5 + px) in LDS + act2T column
   if (wave < 7) {
     const int t = wave;
-    int pos = t * 16 + n16;
-    if (pos >= NPOS2) pos = 0;
-    const int py = pos / O2, px = pos - py * O2;
-    const bf16* pb = p1cl + (py * P1 + px) * 8;
+    int q = t * 4 + (n16 >> 2);
+    if (q >= P2 * P2) q = 0;                         // rows past the 25 windows read a valid position
+    const int y = 2 * (q / P2) + ((n16 >> 1) & 1), x = 2 * (q % P2) + (n16 & 1);
+    const bf16* pb = p1cl + (y * P1 + x) * 8;
     const bf16* wb = w2c + n16 * S_W2C_LD + kq;
     f32x4 acc = zero4();
 #pragma unroll
     for (int ks = 0; ks < 7; ++ks) acc = mfma16(ld8(pb + go2[ks]), ld8(wb + ks * 32), acc);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int p = t * 16 + rq + r;
-      if (p < NPOS2) c2[p * 16 + n16] = fmaxf(acc[r] + bias2, 0.f);
-    }
-  }
-  __syncthreads();
-  FEDMI_STAMP(0, 4);
-
-  // ---- maxpool2 #2 -> act2 row (torch .view order o*25 + py*5 + px) in LDS + act2T column
-  for (int e = tid; e < F0P; e += NT_CONV) {
-    bf16 mb = (bf16)0.f;
-    if (e < F0) {
-      const int o = e / 25, rem = e - o * 25, py = rem / P2, px = rem - py * P2;
-      const float* w = c2 + ((2 * py) * O2 + 2 * px) * 16 + o;
-      float m = w[0]; int am = 0;
-      if (w[16] > m) { m = w[16]; am = 1; }
-      if (w[O2 * 16] > m) { m = w[O2 * 16]; am = 2; }
-      if (w[O2 * 16 + 16] > m) { m = w[O2 * 16 + 16]; am = 3; }
-      mb = (bf16)m;
+    const int qo = t * 4 + (lane >> 4);
+    if (qo < P2 * P2) {
+      float m = fmaxf(acc[0] + bias2, 0.f), c;
+      int am = 0;
+      c = fmaxf(acc[1] + bias2, 0.f); if (c > m) { m = c; am = 1; }
+      c = fmaxf(acc[2] + bias2, 0.f); if (c > m) { m = c; am = 2; }
+      c = fmaxf(acc[3] + bias2, 0.f); if (c > m) { m = c; am = 3; }
+      const bf16 mb = (bf16)m;
+      const int e = n16 * (P2 * P2) + qo;
       am2s[e] = (uint8_t)am;
+      xrow[e] = mb;
+      act2T[(size_t)e * MAX_TRAIN_BATCH + s] = mb;
     }
-    xrow[e] = mb;
-    act2T[(size_t)e * MAX_TRAIN_BATCH + s] = mb;
+  } else if (tid >= 7 * 64 && tid < 7 * 64 + (F0P - F0)) {     // act2 row padding 400..415
+    const int e = F0 + tid - 7 * 64;
+    xrow[e] = (bf16)0.f;
+    act2T[(size_t)e * MAX_TRAIN_BATCH + s] = (bf16)0.f;
   }
+  FEDMI_STAMP(0, 4);
   // fc2 weight chunks and the FC biases (fc3's 3 KB image is in LDS since the stage)
   const int n2 = fn < 96 ? fn : 95;
   bf16x8 w2v[2];
