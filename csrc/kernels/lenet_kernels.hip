@@ -547,6 +547,7 @@ FEDMI_DEV void bwd_main(const BwdLds& L, float* __restrict__ slab, int sk, int s
       acc[0] = mfma16(ld8(ga + koff[ks]), w, acc[0]);
       acc[1] = mfma16(ld8(gbb + koff[ks]), w, acc[1]);
     }
+    FEDMI_STAMP(sk, 6);    // wave 0: conv2 dgrad MFMAs done
     float csum = 0.f;
     if (n16 < C1) {
       const int c = n16;
@@ -572,6 +573,7 @@ FEDMI_DEV void bwd_main(const BwdLds& L, float* __restrict__ slab, int sk, int s
     csum += __shfl_xor(csum, 16, 64);
     csum += __shfl_xor(csum, 32, 64);
     if (n16 < C1 && lane < 16) db[16 + wave * C1 + n16] = csum;
+    FEDMI_STAMP(sk, 7);    // wave 0: pool1 backward scatter done
   }
   __syncthreads();
   FEDMI_STAMP(sk, 3);

@@ -58,6 +58,11 @@ def main():
                 print(f"    fc.{nm:14s} med {np.median(f[:, j] - prev):8.0f}")
                 prev = f[:, j]
             print(f"    fc.dX          med {np.median(k0[:len(f), 6] - prev):8.0f}")
+        b2 = st[2, :128]
+        b2 = b2[b2[:, 2] > 0]
+        if len(b2) and (b2[:, 6] > 0).all():
+            print(f"    bwd: dY2 scatter->dgrad MFMAs done (wave 0) med {np.median(b2[:, 6] - b2[:, 2]):8.0f}  "
+                  f"pool1 bwd scatter med {np.median(b2[:, 7] - b2[:, 6]):8.0f}  -> barrier med {np.median(b2[:, 3] - b2[:, 7]):8.0f}")
         names = {3: ("sgd2", ["all"])}
         nwg = {3: 249}
         # KS2 by role (lenet_sgd2 block ranges): conv slab combine, fc1 / fc2 / fc3 weight tiles, biases + loss
