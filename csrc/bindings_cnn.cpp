@@ -35,11 +35,12 @@ struct PackItem {
   const float* w;
   bf16* wr;
   int O, Cw, C, RS;
+  int O8;
 };
 void launch_conv_pack_multi(hipStream_t, const PackItem*, int);
 void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int);
 long conv_wgrad_ws_floats(const ConvShape&);
-void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int);
+void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int, int);
 
 struct BNDesc {
   const double* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
@@ -161,9 +162,9 @@ void fedmi_bind_cnn(py::module_& m) {
     std::vector<PackItem> v;
     for (const auto& it : items) {
       const py::tuple t = it.cast<py::tuple>();
-      if (t.size() != 6) throw std::invalid_argument("conv_pack_multi item: (w, wr, O, Cw, C, RS)");
+      if (t.size() != 6 && t.size() != 7) throw std::invalid_argument("conv_pack_multi item: (w, wr, O, Cw, C, RS[, O8])");
       v.push_back(PackItem{P<const float>(t[0].cast<uintptr_t>()), P<bf16>(t[1].cast<uintptr_t>()), t[2].cast<int>(),
-                           t[3].cast<int>(), t[4].cast<int>(), t[5].cast<int>()});
+                           t[3].cast<int>(), t[4].cast<int>(), t[5].cast<int>(), t.size() == 7 ? t[6].cast<int>() : 0});
     }
     if (!v.empty()) launch_conv_pack_multi(S(st), v.data(), (int)v.size());
     check("conv_pack_multi");
@@ -175,10 +176,11 @@ void fedmi_bind_cnn(py::module_& m) {
     check("conv_wgrad");
   });
   m.def("conv_wgrad_ws_floats", [](const py::tuple& shp) { return conv_wgrad_ws_floats(shape_from(shp)); });
-  m.def("conv_pack", [](uintptr_t st, uintptr_t w, uintptr_t wr, int O, int Cw, int C, int RS) {
-    launch_conv_pack(S(st), P<const float>(w), P<bf16>(wr), O, Cw, C, RS);
+  m.def("conv_pack", [](uintptr_t st, uintptr_t w, uintptr_t wr, int O, int Cw, int C, int RS, int O8) {
+    launch_conv_pack(S(st), P<const float>(w), P<bf16>(wr), O, Cw, C, RS, O8);
     check("conv_pack");
-  });
+  }, py::arg("st"), py::arg("w"), py::arg("wr"), py::arg("O"), py::arg("Cw"), py::arg("C"), py::arg("RS"),
+     py::arg("O8") = 0);
   m.def("dw_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                      uintptr_t shift) {
     launch_dw_fwd(S(st), dw_from(shp), P<const bf16>(x), P<const float>(w), P<bf16>(y), P<double>(stats),

@@ -27,12 +27,13 @@ void launch_ctr_bump(hipStream_t, int*);
 long long reduce_rows_ws_floats(long long, int);
 void launch_pad_rows(hipStream_t, const bf16*, long long, int, bf16*, int, long long);
 void launch_reduce_rows(hipStream_t, const void*, int, long long, const void*, int, long long, const float*, int,
-                        long long, int, float*, long long, float*, float*);
+                        long long, int, float*, long long, float*, float*, void*, int, float);
 void launch_reduce(hipStream_t, const ZTensor&, const ZTensor&, const ZTensor&, const ZTensor&, const void*, int,
-                   const void*, int, const float*, float*, float*, int, float*, long long);
+                   const void*, int, const float*, float*, float*, int, float*, long long, void*, int, float);
 long long reduce_ws_floats(long long, long long);
 void launch_bn_rows_fwd(hipStream_t, const void*, int, long long, const float*, int, long long, float*, long long,
-                        const float*, const float*, float*, float*, float, float, float*, float*, float*, float*);
+                        const float*, const float*, float*, float*, float, float, float*, float*, float*, float*,
+                        long long*);
 void launch_bn_rows_bwd(hipStream_t, const void*, int, long long, const void*, int, long long, const void*, int,
                         long long, float, const float*, const float*, const float*, int, long long, float*, long long,
                         float*, float*, float*, float*, float*);
@@ -91,12 +92,14 @@ void fedmi_bind_zoo(py::module_& m) {
   m.def("z_ctr_bump", [](uintptr_t st, uintptr_t ctr) { fedmi::launch_ctr_bump(S(st), reinterpret_cast<int*>(ctr)); });
   m.def("z_reduce", [](uintptr_t st, py::object outer, py::object inner, py::object outer_b, py::object inner_b,
                        uintptr_t a, int a_dt, uintptr_t b, int b_dt, uintptr_t shift, uintptr_t acc, uintptr_t acc2,
-                       int op, uintptr_t part, long long part_floats) {
+                       int op, uintptr_t part, long long part_floats, uintptr_t out, int out_dt, float scale) {
     fedmi::launch_reduce(S(st), zt(outer), zt(inner), zt(outer_b), zt(inner_b), reinterpret_cast<const void*>(a), a_dt,
                          reinterpret_cast<const void*>(b), b_dt, reinterpret_cast<const float*>(shift),
                          reinterpret_cast<float*>(acc), reinterpret_cast<float*>(acc2), op,
-                         reinterpret_cast<float*>(part), part_floats);
-  });
+                         reinterpret_cast<float*>(part), part_floats, reinterpret_cast<void*>(out), out_dt, scale);
+  }, py::arg("st"), py::arg("outer"), py::arg("inner"), py::arg("outer_b"), py::arg("inner_b"), py::arg("a"),
+     py::arg("a_dt"), py::arg("b"), py::arg("b_dt"), py::arg("shift"), py::arg("acc"), py::arg("acc2"), py::arg("op"),
+     py::arg("part"), py::arg("part_floats"), py::arg("out") = 0, py::arg("out_dt") = 0, py::arg("scale") = 1.f);
   m.def("z_reduce_ws_floats", &fedmi::reduce_ws_floats);
   m.def("z_reduce_rows_ws_floats", &fedmi::reduce_rows_ws_floats);
   m.def("z_pad_rows", [](uintptr_t st, uintptr_t src, long long lds, int C, uintptr_t dst, int C8, long long rows) {
@@ -104,11 +107,14 @@ void fedmi_bind_zoo(py::module_& m) {
   });
   m.def("z_reduce_rows", [](uintptr_t st, uintptr_t a, int a_dt, long long lda, uintptr_t b, int b_dt, long long ldb,
                             uintptr_t shift, int C, long long M, int op, uintptr_t part, long long part_floats,
-                            uintptr_t acc, uintptr_t acc2) {
+                            uintptr_t acc, uintptr_t acc2, uintptr_t out, int out_dt, float scale) {
     fedmi::launch_reduce_rows(S(st), reinterpret_cast<const void*>(a), a_dt, lda, reinterpret_cast<const void*>(b), b_dt,
                               ldb, reinterpret_cast<const float*>(shift), C, M, op, reinterpret_cast<float*>(part),
-                              part_floats, reinterpret_cast<float*>(acc), reinterpret_cast<float*>(acc2));
-  });
+                              part_floats, reinterpret_cast<float*>(acc), reinterpret_cast<float*>(acc2),
+                              reinterpret_cast<void*>(out), out_dt, scale);
+  }, py::arg("st"), py::arg("a"), py::arg("a_dt"), py::arg("lda"), py::arg("b"), py::arg("b_dt"), py::arg("ldb"),
+     py::arg("shift"), py::arg("C"), py::arg("M"), py::arg("op"), py::arg("part"), py::arg("part_floats"),
+     py::arg("acc"), py::arg("acc2"), py::arg("out") = 0, py::arg("out_dt") = 0, py::arg("scale") = 1.f);
   m.def("z_bn_fwd_coeffs", [](uintptr_t st, uintptr_t s1, uintptr_t s2, uintptr_t shift, int C, long long M, uintptr_t w,
                               uintptr_t b, uintptr_t rmean, uintptr_t rvar, float eps, float mom, int train,
                               uintptr_t save_mean, uintptr_t save_invstd, uintptr_t scale, uintptr_t bias) {
@@ -119,11 +125,15 @@ void fedmi_bind_zoo(py::module_& m) {
   m.def("z_bn_rows_fwd", [](uintptr_t st, uintptr_t x, int x_dt, long long ldx, uintptr_t shift, int C, long long M,
                             uintptr_t part, long long part_floats, uintptr_t w, uintptr_t b, uintptr_t rmean,
                             uintptr_t rvar, float eps, float mom, uintptr_t save_mean, uintptr_t save_invstd,
-                            uintptr_t scale, uintptr_t bias) {
+                            uintptr_t scale, uintptr_t bias, uintptr_t ctr) {
     auto f = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
     fedmi::launch_bn_rows_fwd(S(st), reinterpret_cast<const void*>(x), x_dt, ldx, f(shift), C, M, f(part), part_floats,
-                              f(w), f(b), f(rmean), f(rvar), eps, mom, f(save_mean), f(save_invstd), f(scale), f(bias));
-  });
+                              f(w), f(b), f(rmean), f(rvar), eps, mom, f(save_mean), f(save_invstd), f(scale), f(bias),
+                              reinterpret_cast<long long*>(ctr));
+  }, py::arg("st"), py::arg("x"), py::arg("x_dt"), py::arg("ldx"), py::arg("shift"), py::arg("C"), py::arg("M"),
+     py::arg("part"), py::arg("part_floats"), py::arg("w"), py::arg("b"), py::arg("rmean"), py::arg("rvar"),
+     py::arg("eps"), py::arg("mom"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("scale"), py::arg("bias"),
+     py::arg("ctr") = 0);
   m.def("z_bn_rows_bwd", [](uintptr_t st, uintptr_t g, int g_dt, long long ldg, uintptr_t x, int x_dt, long long ldx,
                             uintptr_t fm, int f_dt, long long ldf, float thr, uintptr_t mean, uintptr_t invstd,
                             uintptr_t w, int C, long long M, uintptr_t part, long long part_floats, uintptr_t k,

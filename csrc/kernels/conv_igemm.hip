@@ -1242,9 +1242,10 @@ struct PackEntry {
   const float* w;
   bf16* wr;
   int O, Cw, C, RS;
+  int O8;            // image rows: O..O8 are zero filters (the output-channel pad of odd widths)
   int row0;          // first workgroup (row) of this entry in the launch
 };
-constexpr int MAX_PACK = 24;
+constexpr int MAX_PACK = 64;   // 64 x 40 B of kernel arguments
 constexpr int PACK_ROW_MAX = 8192;   // Cw * R * S floats staged per row (32 KiB)
 struct PackTable {
   PackEntry e[MAX_PACK];
@@ -1257,6 +1258,11 @@ __global__ __launch_bounds__(256) void conv_pack_multi_kernel(PackTable t) {
   while (k + 1 < t.n && (int)blockIdx.x >= t.e[k + 1].row0) ++k;
   const PackEntry& p = t.e[k];
   const int o = blockIdx.x - p.row0;
+  if (o >= p.O) {   // zero filter row (workgroup-uniform)
+    bf16* dst = p.wr + (long)o * p.RS * p.C;
+    for (int i = threadIdx.x; i < p.RS * p.C; i += 256) dst[i] = (bf16)0.f;
+    return;
+  }
   const int n_in = p.Cw * p.RS;
   const float* src = p.w + (long)o * n_in;
   for (int i0 = threadIdx.x; i0 < n_in; i0 += 256 * 8) {   // 8 loads in flight per thread
@@ -1871,6 +1877,7 @@ struct PackItem {
   const float* w;
   bf16* wr;
   int O, Cw, C, RS;
+  int O8;            // <= 0: O (no zero filters)
 };
 
 // All dense-conv weight images of a network from their fp32 masters, <= MAX_PACK per launch.
@@ -1883,8 +1890,9 @@ void launch_conv_pack_multi(hipStream_t st, const PackItem* items, int n) {
       const PackItem& it = items[b + k];
       if (it.C % 8 || it.C < it.Cw) throw std::invalid_argument("conv_pack_multi: bad channel padding");
       if ((long)it.Cw * it.RS > PACK_ROW_MAX) throw std::invalid_argument("conv_pack_multi: row too long");
-      t.e[k] = PackEntry{it.w, it.wr, it.O, it.Cw, it.C, it.RS, rows};
-      rows += it.O;
+      const int o8 = it.O8 > it.O ? it.O8 : it.O;
+      t.e[k] = PackEntry{it.w, it.wr, it.O, it.Cw, it.C, it.RS, o8, rows};
+      rows += o8;
       max_row = std::max(max_row, it.Cw * it.RS);
     }
     hipLaunchKernelGGL(conv_pack_multi_kernel, dim3(rows), dim3(256), max_row * sizeof(float), st, t);
@@ -1934,8 +1942,8 @@ void launch_dgrad_pack_multi(hipStream_t st, const DPackItem* items, int n) {
 }
 
 
-void launch_conv_pack(hipStream_t st, const float* w, bf16* wrsc, int O, int Cw, int C, int RS) {
-  const PackItem it{w, wrsc, O, Cw, C, RS};
+void launch_conv_pack(hipStream_t st, const float* w, bf16* wrsc, int O, int Cw, int C, int RS, int O8) {
+  const PackItem it{w, wrsc, O, Cw, C, RS, O8};
   launch_conv_pack_multi(st, &it, 1);
 }
 

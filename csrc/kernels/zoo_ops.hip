@@ -67,11 +67,16 @@ enum EwOp : int {
   EW_BNB_THR = 17,   // o = (f > s0 ? a : 0) * b + c * d + e   (threshold_backward fused into BN backward)
   EW_FMA_ADD = 18,   // o = r(a * b + c) + d       (BatchNorm apply + residual add; r = bf16 rounding if s1)
   EW_FMA_ADD_RELU = 19,  // o = max(r(a * b + c) + d, 0)  (BatchNorm apply + residual add + ReLU)
+  EW_BNB_ADD = 20,   // o = r(a * b + c * d + e) + f          (BN backward apply + the gradient accumulation add)
+  EW_BNB_THR_ADD = 21,  // o = r((f > s0 ? a : 0) * b + c * d + e) + g
 };
 
+// NIN input descriptors: 6 for every op but the 7-operand BN-backward + accumulation pass, so the common
+// launches do not carry (or unroll over) a seventh descriptor
+template <int NIN>
 struct EwArgs {
   ZTensor o;
-  ZTensor in[6];
+  ZTensor in[NIN];
   float s0, s1;
   int op;
   uint32_t seed;
@@ -129,7 +134,9 @@ FEDMI_DEV long long zoff(const ZCoord& k, const ZTensor& t, int ndim) {
   return off;
 }
 
-FEDMI_DEV float ew_apply(const EwArgs& a, float x0, float x1, float x2, float x3, float x4, float x5 = 0.f) {
+template <class A>
+FEDMI_DEV float ew_apply(const A& a, float x0, float x1, float x2, float x3, float x4, float x5 = 0.f,
+                         float x6 = 0.f) {
   switch (a.op) {
     case EW_COPY: return x0;
     case EW_ADD: return x0 + a.s0 * x1;
@@ -150,6 +157,15 @@ FEDMI_DEV float ew_apply(const EwArgs& a, float x0, float x1, float x2, float x3
     // s1 != 0: the BN output is rounded to bf16 before the add, exactly as the unfused pair stores it
     case EW_FMA_ADD: return (a.s1 != 0.f ? (float)(bf16)(x0 * x1 + x2) : x0 * x1 + x2) + x3;
     case EW_FMA_ADD_RELU: return fmaxf((a.s1 != 0.f ? (float)(bf16)(x0 * x1 + x2) : x0 * x1 + x2) + x3, 0.f);
+    // the BN-backward gradient is rounded (s1) as the unfused pair stores it before autograd's accumulation add
+    case EW_BNB_ADD: {
+      const float gi = x0 * x1 + x2 * x3 + x4;
+      return (a.s1 != 0.f ? (float)(bf16)gi : gi) + x5;
+    }
+    case EW_BNB_THR_ADD: {
+      const float gi = (x5 > a.s0 ? x0 : 0.f) * x1 + x2 * x3 + x4;
+      return (a.s1 != 0.f ? (float)(bf16)gi : gi) + x6;
+    }
     default: return 0.f;
   }
 }
@@ -207,14 +223,16 @@ FEDMI_DEV void vstore(void* p, int dt, long long off, const float* v) {
 // VW consecutive innermost elements per thread (host-checked alignment); the descriptors' innermost
 // size is already divided by VW and unit strides scaled by VW; a broadcast input (vmask bit clear)
 // is one scalar load
-template <int VW>
-__global__ __launch_bounds__(256) void ew_vec_kernel(EwArgs a, long long nv) {
+template <int VW, int NIN>
+__global__ __launch_bounds__(256) void ew_vec_kernel(EwArgs<NIN> a, long long nv) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
     const ZCoord kc = zcoords(a.o, i);
-    float x[6][VW];
+    float x[7][VW];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
+    for (int u = 0; u < VW; ++u) x[6][u] = 0.f;
+#pragma unroll
+    for (int k = 0; k < NIN; ++k) {
       if (a.in[k].p && ((a.vmask >> k) & 1)) {
         vload<VW>(a.in[k].p, a.in[k].dtype, zoff(kc, a.in[k], a.o.ndim), x[k]);
       } else {
@@ -225,29 +243,33 @@ __global__ __launch_bounds__(256) void ew_vec_kernel(EwArgs a, long long nv) {
     }
     float v[VW];
 #pragma unroll
-    for (int u = 0; u < VW; ++u) v[u] = ew_apply(a, x[0][u], x[1][u], x[2][u], x[3][u], x[4][u], x[5][u]);
+    for (int u = 0; u < VW; ++u) v[u] = ew_apply(a, x[0][u], x[1][u], x[2][u], x[3][u], x[4][u], x[5][u], x[6][u]);
     vstore<VW>(a.o.p, a.o.dtype, zoff(kc, a.o, a.o.ndim), v);
   }
 }
 
-__global__ __launch_bounds__(256) void ew_kernel(EwArgs a, long long n) {
+template <int NIN>
+__global__ __launch_bounds__(256) void ew_kernel(EwArgs<NIN> a, long long n) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   const uint32_t ctr = a.ctr ? (uint32_t)a.ctr[0] : 0u;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const ZCoord kc = zcoords(a.o, i);
-    float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f, x4 = 0.f, x5 = 0.f;
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f, x4 = 0.f, x5 = 0.f, x6 = 0.f;
     if (a.in[0].p) x0 = zload(a.in[0], zoff(kc, a.in[0], a.o.ndim));
     if (a.in[1].p) x1 = zload(a.in[1], zoff(kc, a.in[1], a.o.ndim));
     if (a.in[2].p) x2 = zload(a.in[2], zoff(kc, a.in[2], a.o.ndim));
     if (a.in[3].p) x3 = zload(a.in[3], zoff(kc, a.in[3], a.o.ndim));
     if (a.in[4].p) x4 = zload(a.in[4], zoff(kc, a.in[4], a.o.ndim));
     if (a.in[5].p) x5 = zload(a.in[5], zoff(kc, a.in[5], a.o.ndim));
+    if constexpr (NIN > 6) {
+      if (a.in[6].p) x6 = zload(a.in[6], zoff(kc, a.in[6], a.o.ndim));
+    }
     float v;
     if (a.op == EW_BERN) {
       const uint32_t h = hash3(a.seed, ctr, (uint32_t)i ^ (uint32_t)(i >> 32));
       v = ((float)(h >> 8) * (1.f / 16777216.f)) < a.s0 ? 1.f : 0.f;
     } else {
-      v = ew_apply(a, x0, x1, x2, x3, x4, x5);
+      v = ew_apply(a, x0, x1, x2, x3, x4, x5, x6);
     }
     zstore(a.o, zoff(kc, a.o, a.o.ndim), v);
   }
@@ -259,7 +281,8 @@ __global__ void ctr_bump_kernel(int* ctr) {
 
 // ---- reduction: out[outer] (+)= sum over inner of f(in...) ----------------------------
 // outer / inner index spaces with their own sizes and per-tensor strides.
-enum RdOp : int { RD_SUM = 0, RD_SUMSQ_SHIFT = 1, RD_DOT_SHIFT = 2 };
+// RD_DOT_R: sum a, sum bf16(a * b) -- the product rounded as a stored bf16 product would be (exact fusion)
+enum RdOp : int { RD_SUM = 0, RD_SUMSQ_SHIFT = 1, RD_DOT_SHIFT = 2, RD_DOT_R = 3 };
 struct RdArgs {
   ZTensor outer;     // sizes of the kept dims; strides of input a along them
   ZTensor inner;     // sizes of the reduced dims; strides of input a along them
@@ -274,11 +297,19 @@ struct RdArgs {
   float* acc2;          // second accumulator (RD_SUMSQ_SHIFT: sum of squares; RD_DOT_SHIFT: sum a*(b-shift))
   float* part;          // [2][splits][n_outer] per-split partials (splits > 1), summed in split order afterwards
   int op;
+  void* out;            // RD_SUM with out: out[o] = scale * sum, stored in out_dt (overwrite; acc unused)
+  int out_dt;
+  float scale;
 };
 
 FEDMI_DEV float rload(const void* p, int dt, long long off) {
   if (dt == 0) return reinterpret_cast<const float*>(p)[off];
   return (float)reinterpret_cast<const bf16*>(p)[off];
+}
+
+FEDMI_DEV void rstore(void* p, int dt, long long off, float v) {
+  if (dt == 0) reinterpret_cast<float*>(p)[off] = v;
+  else reinterpret_cast<bf16*>(p)[off] = (bf16)v;
 }
 
 // block = 64 outer lanes x 4 inner lanes; grid = (outer tiles, inner splits)
@@ -293,7 +324,23 @@ __global__ __launch_bounds__(256) void reduce_kernel(RdArgs r, long long n_outer
     const float sh = r.shift ? r.shift[o] : 0.f;
     const long long per = (n_inner + gridDim.y - 1) / gridDim.y;
     const long long i0 = (long long)blockIdx.y * per, i1 = i0 + per < n_inner ? i0 + per : n_inner;
-    for (long long i = i0 + li; i < i1; i += 4) {
+    long long i = i0 + li;
+    if (r.op == RD_SUM) {
+      // 8 inner elements per pass, every load issued before the first add (clamped index, masked value):
+      // one memory latency per 8 elements instead of per element
+      constexpr int U = 8;
+      for (; i < i1; i += 4 * U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long iu = i + 4 * u < i1 ? i + 4 * u : i;
+          v[u] = rload(r.a, r.a_dtype, base_a + zoffset(r.inner, r.inner, iu));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) s1 += i + 4 * u < i1 ? v[u] : 0.f;
+      }
+    }
+    for (; i < i1; i += 4) {
       const float va = rload(r.a, r.a_dtype, base_a + zoffset(r.inner, r.inner, i));
       if (r.op == RD_SUM) {
         s1 += va;
@@ -301,6 +348,10 @@ __global__ __launch_bounds__(256) void reduce_kernel(RdArgs r, long long n_outer
         const float d = va - sh;
         s1 += d;
         s2 += d * d;
+      } else if (r.op == RD_DOT_R) {
+        const float vb = rload(r.b, r.b_dtype, base_b + zoffset(r.inner, r.inner_b, i));
+        s1 += va;
+        s2 += (float)(bf16)(va * vb);
       } else {
         const float vb = rload(r.b, r.b_dtype, base_b + zoffset(r.inner, r.inner_b, i));
         s1 += va;
@@ -315,7 +366,9 @@ __global__ __launch_bounds__(256) void reduce_kernel(RdArgs r, long long n_outer
     // no atomics: one writer per (split, outer), so the result does not depend on workgroup order
     const float t1 = red[0][0][lo] + red[0][1][lo] + red[0][2][lo] + red[0][3][lo];
     const float t2 = red[1][0][lo] + red[1][1][lo] + red[1][2][lo] + red[1][3][lo];
-    if (gridDim.y == 1) {
+    if (gridDim.y == 1 && r.out) {
+      rstore(r.out, r.out_dt, o, r.scale * (r.op == RD_SUM ? t1 : t2));
+    } else if (gridDim.y == 1) {
       r.acc[o] += t1;
       if (r.op != RD_SUM) r.acc2[o] += t2;
     } else {
@@ -326,13 +379,18 @@ __global__ __launch_bounds__(256) void reduce_kernel(RdArgs r, long long n_outer
 }
 
 __global__ __launch_bounds__(256) void reduce_splits_kernel(const float* part, int splits, long long n_outer,
-                                                            float* acc, float* acc2) {
+                                                            float* acc, float* acc2, void* out, int out_dt,
+                                                            float scale, int two) {
   const long long o = (long long)blockIdx.x * 256 + threadIdx.x;
   if (o >= n_outer) return;
   float s1 = 0.f, s2 = 0.f;
   for (int y = 0; y < splits; ++y) {
     s1 += part[(long long)y * n_outer + o];
-    if (acc2) s2 += part[((long long)splits + y) * n_outer + o];
+    if (two) s2 += part[((long long)splits + y) * n_outer + o];
+  }
+  if (out) {
+    rstore(out, out_dt, o, scale * (two ? s2 : s1));   // RD_DOT_SHIFT: the dot sums
+    return;
   }
   acc[o] += s1;
   if (acc2) acc2[o] += s2;
@@ -441,6 +499,9 @@ struct BnFin {
   const float* shift; const float* w; const float* b; float* rmean; float* rvar; float eps, mom;
   float* save_mean; float* save_invstd; float* scale; float* bias;
   const float* mean; const float* invstd; float* k; float* bb; float* cc; float* dw; float* db;
+  long long* ctr;         // mode 1: the module's num_batches_tracked, += 1 by the finalizing workgroup (or null)
+  void* out; int out_dt; float out_scale;   // mode 3 (row sums): out[c] = out_scale * sum (dot sum if two), in out_dt
+  int two;
 };
 
 FEDMI_DEV void bn_fwd_fin(const BnFin& f, int c, float s1, float s2) {
@@ -615,10 +676,12 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_d
       float a1 = 0.f, a2 = 0.f;
       for (int q = 0; q < L; ++q) { a1 += fr[0][q * CW + cl]; a2 += fr[1][q * CW + cl]; }
       if (fin.mode == 1) bn_fwd_fin(fin, c, a1, a2);
-      else bn_bwd_fin(fin, c, a1, a2);
+      else if (fin.mode == 2) bn_bwd_fin(fin, c, a1, a2);
+      else rstore(fin.out, fin.out_dt, c, fin.out_scale * (fin.two ? a2 : a1));
     }
     __syncthreads();
   }
+  if (fin.ctr && threadIdx.x == 0) fin.ctr[0] += 1;
 }
 
 // acc[c] += sum_slab part[slab][0][c] (and acc2 from part[slab][1][c]), slab order
@@ -1321,10 +1384,10 @@ int grid1(long long n) {
 
 namespace fedmi {
 
-void launch_ew(hipStream_t st, const ZTensor& o, const ZTensor* ins, int nin, int op, float s0, float s1,
-               uint32_t seed, const int* ctr, int vmask, int vw) {
-  if (nin > 6) throw std::invalid_argument("ew: at most 6 inputs");
-  EwArgs a{};
+template <int NIN>
+static void launch_ew_n(hipStream_t st, const ZTensor& o, const ZTensor* ins, int nin, int op, float s0, float s1,
+                        uint32_t seed, const int* ctr, int vmask, int vw) {
+  EwArgs<NIN> a{};
   a.o = o;
   for (int i = 0; i < nin; ++i) a.in[i] = ins[i];
   a.op = op;
@@ -1339,14 +1402,23 @@ void launch_ew(hipStream_t st, const ZTensor& o, const ZTensor* ins, int nin, in
   if (vmask >= 0) {
     if (op == EW_BERN) throw std::invalid_argument("ew: no vector launch for bernoulli");
     if (vw == 8)
-      hipLaunchKernelGGL(ew_vec_kernel<8>, dim3(grid1(n)), dim3(256), 0, st, a, n);
+      hipLaunchKernelGGL((ew_vec_kernel<8, NIN>), dim3(grid1(n)), dim3(256), 0, st, a, n);
     else if (vw == 4)
-      hipLaunchKernelGGL(ew_vec_kernel<4>, dim3(grid1(n)), dim3(256), 0, st, a, n);
+      hipLaunchKernelGGL((ew_vec_kernel<4, NIN>), dim3(grid1(n)), dim3(256), 0, st, a, n);
     else
       throw std::invalid_argument("ew: vector width 8 or 4");
   } else {
-    hipLaunchKernelGGL(ew_kernel, dim3(grid1(n)), dim3(256), 0, st, a, n);
+    hipLaunchKernelGGL(ew_kernel<NIN>, dim3(grid1(n)), dim3(256), 0, st, a, n);
   }
+}
+
+void launch_ew(hipStream_t st, const ZTensor& o, const ZTensor* ins, int nin, int op, float s0, float s1,
+               uint32_t seed, const int* ctr, int vmask, int vw) {
+  if (nin > 7) throw std::invalid_argument("ew: at most 7 inputs");
+  if (nin > 6)
+    launch_ew_n<7>(st, o, ins, nin, op, s0, s1, seed, ctr, vmask, vw);
+  else
+    launch_ew_n<6>(st, o, ins, nin, op, s0, s1, seed, ctr, vmask, vw);
   check_hip(hipGetLastError(), "ew_kernel");
 }
 
@@ -1371,7 +1443,9 @@ long long reduce_ws_floats(long long no, long long ni) {
 
 void launch_reduce(hipStream_t st, const ZTensor& outer, const ZTensor& inner, const ZTensor& outer_b,
                    const ZTensor& inner_b, const void* a, int a_dt, const void* b, int b_dt, const float* shift,
-                   float* acc, float* acc2, int op, float* part, long long part_floats) {
+                   float* acc, float* acc2, int op, float* part, long long part_floats, void* out, int out_dt,
+                   float scale) {
+  if (out && op == RD_SUMSQ_SHIFT) throw std::invalid_argument("launch_reduce: no direct output of moments");
   long long no = 1, ni = 1;
   for (int d = 0; d < outer.ndim; ++d) no *= outer.size[d];
   for (int d = 0; d < inner.ndim; ++d) ni *= inner.size[d];
@@ -1379,7 +1453,7 @@ void launch_reduce(hipStream_t st, const ZTensor& outer, const ZTensor& inner, c
   RdArgs r{};
   r.outer = outer; r.inner = inner; r.outer_b = outer_b; r.inner_b = inner_b;
   r.a = a; r.a_dtype = a_dt; r.b = b; r.b_dtype = b_dt; r.shift = shift; r.acc = acc; r.acc2 = acc2; r.op = op;
-  r.part = part;
+  r.part = part; r.out = out; r.out_dt = out_dt; r.scale = scale;
   const long long tiles = (no + 63) / 64;
   const long long splits = reduce_splits(no, ni);
   if (splits > 1 && (part == nullptr || part_floats < 2 * splits * no))
@@ -1388,7 +1462,7 @@ void launch_reduce(hipStream_t st, const ZTensor& outer, const ZTensor& inner, c
   check_hip(hipGetLastError(), "reduce_kernel");
   if (splits > 1) {
     hipLaunchKernelGGL(reduce_splits_kernel, dim3((unsigned)((no + 255) / 256)), dim3(256), 0, st, part, (int)splits,
-                       no, acc, op != RD_SUM ? acc2 : nullptr);
+                       no, acc, op != RD_SUM ? acc2 : nullptr, out, out_dt, scale, op != RD_SUM ? 1 : 0);
     check_hip(hipGetLastError(), "reduce_splits_kernel");
   }
 }
@@ -1406,28 +1480,35 @@ long long reduce_rows_ws_floats(long long M, int C) { return (long long)rows_sla
 
 void launch_reduce_rows(hipStream_t st, const void* a, int a_dt, long long lda, const void* b, int b_dt,
                         long long ldb, const float* shift, int C, long long M, int op, float* part, long long part_floats,
-                        float* acc, float* acc2) {
+                        float* acc, float* acc2, void* out, int out_dt, float scale) {
   if (C % 4 || C <= 0 || M <= 0) throw std::invalid_argument("reduce_rows: C % 4 == 0 and M > 0 required");
+  if (out && op == RD_SUMSQ_SHIFT) throw std::invalid_argument("reduce_rows: no direct output of moments");
   const int slabs = rows_slabs(M, C);
   if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("reduce_rows: workspace too small");
   const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
   const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
   BnFin fin{};
+  if (out) {   // the sums stored by the last-arriving workgroup: one launch, no zeroed accumulator, no copy
+    fin.mode = 3; fin.slot = (int)(g_rows_slot.fetch_add(1u) % kRowsTicketSlots);
+    fin.out = out; fin.out_dt = out_dt; fin.out_scale = scale; fin.two = op != RD_SUM;
+  }
   if (vw == 8)
     hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
                        nullptr, 0, 0LL, 0.f, fin);
   else
     hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
                        nullptr, 0, 0LL, 0.f, fin);
-  hipLaunchKernelGGL(reduce_rows_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C,
-                     op != RD_SUM ? 1 : 0, acc, acc2);
+  if (!out)
+    hipLaunchKernelGGL(reduce_rows_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C,
+                       op != RD_SUM ? 1 : 0, acc, acc2);
   check_hip(hipGetLastError(), "reduce_rows");
 }
 
 // BN forward statistics + coefficients of a channels-last [M, C] activation: reduce_rows + one finalize
 void launch_bn_rows_fwd(hipStream_t st, const void* x, int x_dt, long long ldx, const float* shift, int C, long long M,
                         float* part, long long part_floats, const float* w, const float* b, float* rmean, float* rvar,
-                        float eps, float mom, float* save_mean, float* save_invstd, float* scale, float* bias) {
+                        float eps, float mom, float* save_mean, float* save_invstd, float* scale, float* bias,
+                        long long* ctr) {
   if (C % 4 || C <= 0 || M <= 0) throw std::invalid_argument("bn_rows_fwd: C % 4 == 0 and M > 0 required");
   const int slabs = rows_slabs(M, C);
   if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("bn_rows_fwd: workspace too small");
@@ -1437,7 +1518,7 @@ void launch_bn_rows_fwd(hipStream_t st, const void* x, int x_dt, long long ldx, 
   fin.slot = (int)(g_rows_slot.fetch_add(1u) % kRowsTicketSlots);
   fin.mode = 1; fin.M = M; fin.shift = shift; fin.w = w; fin.b = b; fin.rmean = rmean; fin.rvar = rvar;
   fin.eps = eps; fin.mom = mom; fin.save_mean = save_mean; fin.save_invstd = save_invstd; fin.scale = scale;
-  fin.bias = bias;
+  fin.bias = bias; fin.ctr = ctr;
   if (vw == 8)
     hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, x, x_dt, ldx, nullptr, 0, 0LL, shift, C, M,
                        (int)RD_SUMSQ_SHIFT, part, nullptr, 0, 0LL, 0.f, fin);

@@ -99,6 +99,7 @@ class TorchTrainer(LocalTrainer):
 
             self.mode = NativeMode(strict=os.environ.get("FEDMI_NATIVE_STRICT", "0") == "1", seed=cfg.seed)
             self.mode.rng_ctr(self._device)      # allocated here, never inside a captured step
+            self.mode.stable_storage = self.fs.flat.untyped_storage().data_ptr()   # weight images: batched packs
         # hybrid mode replays each full-batch SGD step (zero-grad + forward + autograd backward + SGD +
         # stats) from one captured HIP graph: the Python / launch overhead of ~10^3 small kernels per step
         # goes away.  Round 1's NaN-under-replay (autocast weight-cast cache, bf16 adaptive pooling, host

@@ -65,31 +65,38 @@ def _check(t: torch.Tensor, dtype, name: str):
         raise ValueError(f"{name}: expected contiguous {dtype} CUDA tensor, got {t.dtype} {t.device}")
 
 
-def pack_weight(w: torch.Tensor, c_pad: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """fp32 [O, Cw, R, S] -> bf16 [O, R, S, C] (C = Cw rounded up to 8, zero pad)."""
+def pack_weight(w: torch.Tensor, c_pad: Optional[int] = None, out: Optional[torch.Tensor] = None,
+                o_pad: Optional[int] = None) -> torch.Tensor:
+    """fp32 [O, Cw, R, S] -> bf16 [O8, R, S, C] (C = Cw rounded up to 8, zero pad; ``o_pad`` = O8 >= O: zero
+    filters O..O8 written by the same launch)."""
     O, Cw, R, S = w.shape
     C = c_pad or pad8(Cw)
+    O8 = max(int(o_pad or O), O)
     if out is None:
-        out = torch.empty(O, R, S, C, dtype=torch.bfloat16, device=w.device)
+        out = torch.empty(O8, R, S, C, dtype=torch.bfloat16, device=w.device)
     _check(w, torch.float32, "pack_weight.w")
-    native.require().conv_pack(native.stream_handle(w.device), w.data_ptr(), out.data_ptr(), O, Cw, C, R * S)
+    if tuple(out.shape) != (O8, R, S, C) or not out.is_contiguous():
+        raise ValueError(f"pack_weight: image {tuple(out.shape)} vs {(O8, R, S, C)}")
+    native.require().conv_pack(native.stream_handle(w.device), w.data_ptr(), out.data_ptr(), O, Cw, C, R * S, O8)
     return out
 
 
 def pack_weights(items) -> None:
-    """Pack many ``(w fp32 [O,Cw,R,S], out bf16 [O,R,S,C])`` pairs in one multi-tensor launch."""
+    """Pack many ``(w fp32 [O,Cw,R,S], out bf16 [O8,R,S,C])`` pairs in one multi-tensor launch (``O8 > O``: zero
+    filters O..O8)."""
     items = list(items)
     if not items:
         return
     for w, out in items:
         _check(w, torch.float32, "pack_weights.w")
         _check(out, torch.bfloat16, "pack_weights.out")
-        if out.shape[0] != w.shape[0] or tuple(out.shape[1:3]) != tuple(w.shape[2:]) or out.shape[3] < w.shape[1]:
+        if out.shape[0] < w.shape[0] or tuple(out.shape[1:3]) != tuple(w.shape[2:]) or out.shape[3] < w.shape[1]:
             raise ValueError(f"pack_weights: image {tuple(out.shape)} vs master {tuple(w.shape)}")
     dev = items[0][0].device
     native.require().conv_pack_multi(
         native.stream_handle(dev),
-        [(w.data_ptr(), o.data_ptr(), w.shape[0], w.shape[1], o.shape[3], w.shape[2] * w.shape[3]) for w, o in items])
+        [(w.data_ptr(), o.data_ptr(), w.shape[0], w.shape[1], o.shape[3], w.shape[2] * w.shape[3], o.shape[0])
+         for w, o in items])
 
 
 def fd_ws_floats(x_shape, O: int, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None) -> int:

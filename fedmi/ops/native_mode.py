@@ -49,10 +49,10 @@ _DT = {torch.float32: 0, torch.bfloat16: 1, torch.int64: 2}
 # elementwise op codes (zoo_ops.hip EwOp)
 EW_COPY, EW_ADD, EW_MUL, EW_MULS, EW_RELU, EW_THR_BWD, EW_SIGMOID, EW_SIG_BWD, EW_FILL, EW_FMA = range(10)
 EW_BNB, EW_BERN, EW_SUB, EW_DIV, EW_ADDS, EW_FMA_RELU, EW_BNB_THR = 11, 12, 13, 14, 15, 16, 17
-EW_FMA_ADD, EW_FMA_ADD_RELU = 18, 19
+EW_FMA_ADD, EW_FMA_ADD_RELU, EW_BNB_ADD, EW_BNB_THR_ADD = 18, 19, 20, 21
 # an impl returns ATEN when the op is legitimately ATen's (host copies, scalar reads): not a fallback
 ATEN = object()
-RD_SUM, RD_SUMSQ_SHIFT, RD_DOT_SHIFT = 0, 1, 2
+RD_SUM, RD_SUMSQ_SHIFT, RD_DOT_SHIFT, RD_DOT_R = 0, 1, 2, 3
 
 
 def _nat():
@@ -197,9 +197,27 @@ def _dev(*ts):
     return None
 
 
-def reduce_sum(a: torch.Tensor, dims, acc: torch.Tensor, op: int = RD_SUM, b: Optional[torch.Tensor] = None,
-               shift: Optional[torch.Tensor] = None, acc2: Optional[torch.Tensor] = None) -> None:
-    """acc (fp32, ZEROED, one entry per kept element in order) += sum over ``dims`` of f(a[, b])."""
+def _rowmajor_out(out: torch.Tensor) -> bool:
+    """out's elements sit at their row-major index (size-1 dims ignored): a reduction can store into it by the
+    accumulator index."""
+    if out.dtype not in (torch.float32, torch.bfloat16):
+        return False
+    expect = 1
+    for d in range(out.dim() - 1, -1, -1):
+        if out.shape[d] == 1:
+            continue
+        if out.stride(d) != expect:
+            return False
+        expect *= out.shape[d]
+    return True
+
+
+def reduce_sum(a: torch.Tensor, dims, acc: Optional[torch.Tensor], op: int = RD_SUM, b: Optional[torch.Tensor] = None,
+               shift: Optional[torch.Tensor] = None, acc2: Optional[torch.Tensor] = None,
+               out: Optional[torch.Tensor] = None, scale: float = 1.0) -> None:
+    """acc (fp32, ZEROED, one entry per kept element in order) += sum over ``dims`` of f(a[, b]); or, with
+    ``out`` (RD_SUM, :func:`_rowmajor_out`), out = scale * sum stored directly (no zeroed accumulator, no copy:
+    the bias gradients, spatial means of SE gates, sums of autograd's broadcast backward)."""
     dims = sorted(d % a.dim() for d in dims)
     kept = [d for d in range(a.dim()) if d not in dims]
     ops = [a] if b is None else [a, b]
@@ -220,7 +238,7 @@ def reduce_sum(a: torch.Tensor, dims, acc: torch.Tensor, op: int = RD_SUM, b: Op
 
     oshape, ostr = space(kept, True)
     ishape, istr = space(dims, False)
-    if _rows_ok(oshape, ostr, ishape, istr, ops):
+    if op != RD_DOT_R and _rows_ok(oshape, ostr, ishape, istr, ops):
         # channels-last moments / bias gradients: [M, C] rows, 16-byte channel vectors, deterministic
         C, M = oshape[0], ishape[0]
         nat = _nat()
@@ -228,7 +246,9 @@ def reduce_sum(a: torch.Tensor, dims, acc: torch.Tensor, op: int = RD_SUM, b: Op
         nat.z_reduce_rows(_st(a.device), a.data_ptr(), _DT[a.dtype], istr[0][0],
                           b.data_ptr() if b is not None else 0, _DT[b.dtype] if b is not None else 0,
                           istr[1][0] if b is not None else 0, shift.data_ptr() if shift is not None else 0, C, M, op,
-                          part.data_ptr(), part.numel(), acc.data_ptr(), acc2.data_ptr() if acc2 is not None else 0)
+                          part.data_ptr(), part.numel(), acc.data_ptr() if acc is not None else 0,
+                          acc2.data_ptr() if acc2 is not None else 0, out.data_ptr() if out is not None else 0,
+                          _DT[out.dtype] if out is not None else 0, float(scale))
         return
     outer = (0, 0, oshape, ostr[0])
     inner = (0, 0, ishape, istr[0])
@@ -240,8 +260,9 @@ def reduce_sum(a: torch.Tensor, dims, acc: torch.Tensor, op: int = RD_SUM, b: Op
     part = torch.empty(max(nws, 1), dtype=torch.float32, device=a.device)
     nat.z_reduce(_st(a.device), outer, inner, outer_b, inner_b, a.data_ptr(), _DT[a.dtype],
                  b.data_ptr() if b is not None else 0, _DT[b.dtype] if b is not None else 0,
-                 shift.data_ptr() if shift is not None else 0, acc.data_ptr(),
-                 acc2.data_ptr() if acc2 is not None else 0, op, part.data_ptr(), nws)
+                 shift.data_ptr() if shift is not None else 0, acc.data_ptr() if acc is not None else 0,
+                 acc2.data_ptr() if acc2 is not None else 0, op, part.data_ptr(), nws,
+                 out.data_ptr() if out is not None else 0, _DT[out.dtype] if out is not None else 0, float(scale))
 
 
 def _rows_ok(oshape, ostr, ishape, istr, ops) -> bool:
@@ -280,6 +301,15 @@ def _add(func, self, other, alpha=1):
             mode._defer(pend.out, pend.materialize)
             mode.fused["bn+add"] += 1
             return out
+    if func is aten.add.Tensor and mode is not None and mode._pend_bnb is not None:
+        o = _bnb_add_partner(mode._pend_bnb, (self, other), {"alpha": alpha})
+        if o is not None:           # BN-backward gradient + the other incoming gradient: one pass
+            pend, mode._pend_bnb = mode._pend_bnb, None
+            out = _alloc_like_meta(func, (self, other), {"alpha": alpha}, self.device)
+            pend.add(out, o)
+            mode._defer(pend.out, pend.materialize)
+            mode.fused["bn_bwd+grad_add"] += 1
+            return out
     sign = -1.0 if func is aten.sub.Tensor else 1.0
     s = _scalar(other)
     if s is not None:
@@ -292,9 +322,40 @@ def _add(func, self, other, alpha=1):
 def _add_(func, self, other, alpha=1):
     sign = -1.0 if func is aten.sub_.Tensor else 1.0
     s = _scalar(other)
+    mode = NativeMode.current
+    if (s is not None and mode is not None and mode.fuse and func is aten.add_.Tensor and sign * alpha * s == 1.0
+            and self.dtype == torch.int64 and self.numel() == 1):
+        # BatchNorm's num_batches_tracked += 1 (torch.nn.modules.batchnorm, right before the batch_norm call): the
+        # BN forward's finalizing workgroup bumps it, so it costs no launch of its own
+        mode._flush_ctr()
+        mode._pend_ctr = self
+        mode.fused["bn_counter"] += 1
+        return self
+    if func is aten.add_.Tensor and mode is not None and mode._pend_bnb is not None:
+        o = _bnb_add_partner(mode._pend_bnb, (self, other), {"alpha": alpha})
+        if o is not None:           # in-place accumulation into either operand: one pass
+            pend, mode._pend_bnb = mode._pend_bnb, None
+            pend.add(self, o)
+            if o is self:
+                mode._defer(pend.out, pend.materialize)
+            mode.fused["bn_bwd+grad_add"] += 1
+            return self
     if s is not None:
         return ew(self, [self], EW_ADDS, sign * alpha * s)
     return ew(self, [self, other], EW_ADD, sign * alpha)
+
+
+class _PendingMul:
+    """a * b (same shapes) not computed yet: if the next op sums it over some dims (autograd's backward of a
+    broadcast multiply -- the SE gate's gradient), the product is folded into that reduction (RD_DOT_SHIFT,
+    no shift) and never stored; any other op materialises it."""
+    __slots__ = ("out", "a", "b")
+
+    def __init__(self, out, a, b):
+        self.out, self.a, self.b = out, a, b
+
+    def materialize(self):
+        ew(self.out, [self.a, self.b], EW_MUL)
 
 
 @impl(aten.mul.Tensor)
@@ -306,6 +367,11 @@ def _mul(func, self, other):
     if s is not None:
         return ew(torch.empty_like(other), [other], EW_MULS, s)
     out = _alloc_like_meta(func, (self, other), {}, _dev(self, other))
+    mode = NativeMode.current
+    if (mode is not None and mode.fuse and self.shape == other.shape == out.shape and self.dtype == other.dtype
+            and out.dim() >= 2):
+        mode._pend_mul = _PendingMul(out, self, other)
+        return out
     return ew(out, [self, other], EW_MUL)
 
 
@@ -362,6 +428,37 @@ def _relu_(func, self):
     return ew(self, [self], EW_RELU)
 
 
+class _PendingBNB:
+    """A BatchNorm input gradient whose apply pass has not run: when autograd next sums it with the tensor's
+    other incoming gradient (DenseNet: the concat's slice; residual nets: the shortcut), the sum joins the
+    pass (EW_BNB[_THR]_ADD, the gradient rounded as the unfused pair stores it); any other op materialises it."""
+    __slots__ = ("out", "ins", "thr")
+
+    def __init__(self, out, ins, thr):
+        self.out, self.ins, self.thr = out, ins, thr
+
+    def materialize(self):
+        ew(self.out, self.ins, EW_BNB_THR if len(self.ins) == 6 else EW_BNB, self.thr)
+
+    def add(self, out, other):
+        rnd = 1.0 if self.out.dtype == torch.bfloat16 else 0.0
+        return ew(out, self.ins + [other], EW_BNB_THR_ADD if len(self.ins) == 6 else EW_BNB_ADD, self.thr, rnd)
+
+
+def _bnb_add_partner(pend, args, kwargs=None):
+    """The other operand of ``add(a, b)`` / ``a.add_(b)`` when one operand is the pending BN-backward gradient
+    (plain sum, same shape and dtype); else None."""
+    if pend is None or len(args) != 2 or (kwargs and kwargs.get("alpha", 1) != 1):
+        return None
+    a, b = args
+    if not (isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor)):
+        return None
+    o = b if _same(a, pend.out) else a if _same(b, pend.out) else None
+    if o is None or o.shape != pend.out.shape or o.dtype != pend.out.dtype:
+        return None
+    return o
+
+
 class _PendingThr:
     """threshold_backward(grad, relu_out) not yet computed: its consumer (BN backward) masks on the fly."""
     __slots__ = ("out", "grad", "relu_out", "thr")
@@ -378,7 +475,7 @@ def _thr_bwd(func, grad_output, self, threshold):
     out = _alloc_like_meta(func, (grad_output, self, threshold), {}, grad_output.device)
     mode = NativeMode.current
     if (mode is not None and mode.fuse and _cl_rows(grad_output) and _cl_rows(self) and _cl_rows(out)
-            and _same_geom(grad_output, self) and _same_geom(out, self)):
+            and grad_output.shape == self.shape):
         mode._pend_thr = _PendingThr(out, grad_output, self, float(threshold))
         return out
     return ew(out, [grad_output, self], EW_THR_BWD, float(threshold))
@@ -441,9 +538,67 @@ def _zero_(func, self):
 
 
 # ---- concat / slicing -------------------------------------------------------------
+class _CatBuf:
+    """A reverse-filled concat buffer: NHWC [N, H, W, K], channels [front, K) live.  ``cat([y, x], 1)`` with x
+    the live tail writes y in front of it and returns the longer tail -- x is never copied again (DenseNet's
+    growing feature map, /root/reference/src/models/densenet.py:20-24: the reference copies the whole map per
+    layer)."""
+    __slots__ = ("buf", "front", "head")
+
+    def __init__(self, buf, front, head):
+        self.buf, self.front, self.head = buf, front, head
+
+    def tail(self):
+        return _nchw(self.buf[..., self.front:])
+
+
+def _cat_chain(mode, y: torch.Tensor, x: torch.Tensor):
+    """``cat([y, x], 1)`` of 4-D activations through a concat buffer, or None (the plain copy path).
+
+    A chain is a run of such cats, each taking the previous one's output as x.  The first block that runs a
+    chain only learns its final width (``mode._cat_plan``, keyed by the head cat's shapes); from then on the
+    head cat allocates a buffer of that width and every later cat of the chain copies only its y.  Aliasing is
+    safe because nothing writes a cat output in place (:meth:`NativeMode.__torch_dispatch__` refuses in-place
+    ops on a buffer) and each buffer hands out only ever-longer tails."""
+    if x.dim() != 4 or y.dim() != 4 or x.dtype != y.dtype or x.shape[0] != y.shape[0] or x.shape[2:] != y.shape[2:]:
+        return None
+    N, Cy, H, W = y.shape
+    Cx = x.shape[1]
+    ent = mode._catbufs.get(x.untyped_storage().data_ptr())
+    if ent is not None and ent.front >= Cy and _same(x, ent.tail()):
+        ew(_nchw(ent.buf[..., ent.front - Cy:ent.front]), [y], EW_COPY)
+        ent.front -= Cy
+        out = ent.tail()
+        mode._cat_plan[ent.head] = max(mode._cat_plan.get(ent.head, 0), Cx + Cy)
+        mode.fused["cat_in_place"] += 1
+        return out
+    head = mode._cat_src.get((x.data_ptr(), tuple(x.shape)))
+    if head is not None:                 # learning: x is an earlier cat's output, the chain grows
+        mode._cat_plan[head] = max(mode._cat_plan.get(head, 0), Cx + Cy)
+        return None
+    head = (N, H, W, Cx, Cy, x.dtype)
+    K = CV.pad8(mode._cat_plan.get(head, 0))
+    if K <= Cx + Cy:
+        return head                      # not (yet) known to be a chain head: plain copy, remember the head
+    buf = torch.empty(N, H, W, K, dtype=x.dtype, device=x.device)
+    ent = _CatBuf(buf, K - Cx, head)
+    ew(ent.tail(), [x], EW_COPY)
+    ew(_nchw(buf[..., ent.front - Cy:ent.front]), [y], EW_COPY)
+    ent.front -= Cy
+    mode._catbufs[buf.untyped_storage().data_ptr()] = ent
+    return ent.tail()
+
+
 @impl(aten.cat.default)
 def _cat(func, tensors, dim=0):
     tensors = [t for t in tensors if t.numel() > 0 or t.dim() > 1]
+    mode = NativeMode.current
+    head = None
+    if mode is not None and mode.fuse and len(tensors) == 2 and tensors[0].dim() == 4 and dim % 4 == 1:
+        r = _cat_chain(mode, tensors[0], tensors[1])
+        if isinstance(r, torch.Tensor):
+            return r
+        head = r
     out = _alloc_like_meta(func, (tensors,), {"dim": dim}, _dev(tensors))
     d = dim % out.dim()
     off = 0
@@ -451,6 +606,10 @@ def _cat(func, tensors, dim=0):
         if t.numel():
             ew(out.narrow(d, off, t.shape[d]), [t], EW_COPY)
         off += t.shape[d] if t.dim() else 0
+    if mode is not None and mode.fuse and len(tensors) == 2 and tensors[0].dim() == 4 and dim % 4 == 1:
+        x = tensors[1]
+        src = mode._cat_src.get((x.data_ptr(), tuple(x.shape)))
+        mode._cat_src[(out.data_ptr(), tuple(out.shape))] = src if src is not None else head
     return out
 
 
@@ -469,12 +628,30 @@ def _sum_like(func, self, dim, keepdim, dtype, scale_by_count: bool):
     if dtype is not None:
         kw["dtype"] = dtype
     out = _alloc_like_meta(func, (self, dim), kw, self.device)
-    acc = torch.empty(out.shape, dtype=torch.float32, device=self.device)
-    fill_(acc, 0.0)
-    reduce_sum(self, dims, acc)
     cnt = 1
     for d in dims:
         cnt *= self.shape[d]
+    mode = NativeMode.current
+    pend = mode._pend_mul if mode is not None else None
+    if pend is not None and _same(self, pend.out):
+        mode._pend_mul = None
+        kept = [d for d in range(self.dim()) if d not in dims and self.shape[d] > 1]
+        # per-(sample, channel) sums (SE gates): the generic reduction, which the unfused sum takes too
+        if out.numel() and _rowmajor_out(out) and len(kept) >= 2:   # sum(a * b): one dot reduction, the product never stored
+            # bf16 operands: each product rounded as the unfused multiply stores it (fused == unfused, bitwise)
+            rd = RD_DOT_R if pend.out.dtype == torch.bfloat16 else RD_DOT_SHIFT
+            reduce_sum(pend.a, dims, None, rd, b=pend.b, out=out,
+                       scale=1.0 / max(cnt, 1) if scale_by_count else 1.0)
+            mode._defer(pend.out, pend.materialize)
+            mode.fused["mul+sum"] += 1
+            return out
+        pend.materialize()
+    if out.numel() and _rowmajor_out(out):
+        reduce_sum(self, dims, None, out=out, scale=1.0 / max(cnt, 1) if scale_by_count else 1.0)
+        return out
+    acc = torch.empty(out.shape, dtype=torch.float32, device=self.device)
+    fill_(acc, 0.0)
+    reduce_sum(self, dims, acc)
     if scale_by_count:
         return ew(out, [acc], EW_MULS, 1.0 / max(cnt, 1))
     return ew(out, [acc], EW_COPY)
@@ -500,18 +677,27 @@ def _sum_all(func, self, dtype=None):
 
 
 # ---- BatchNorm -------------------------------------------------------------------
-def _cl_rows(t: torch.Tensor) -> bool:
-    """t is a [M, C] row matrix in memory (channels-last 4-D or contiguous 2-D), 16-B channel vectors."""
+def _rows_ld(t: torch.Tensor) -> Optional[int]:
+    """Row stride (elements) when t is an [M, C] row matrix in memory -- channels-last 4-D or 2-D with unit-stride
+    channels, compact or a channel slice of a wider one (a concat buffer's tail, a padded conv output's first C
+    channels) -- with 16-B channel vectors (8-B for bf16 C % 8 != 0); else None."""
     if t.dim() == 4:
-        if not t.is_contiguous(memory_format=torch.channels_last):
-            return False
-    elif t.dim() != 2 or not t.is_contiguous():
-        return False
+        ld = _row_stride(t.permute(0, 2, 3, 1))
+    elif t.dim() == 2 and t.stride(1) == 1:
+        ld = t.stride(0) if t.shape[0] > 1 else t.shape[1]
+    else:
+        return None
     C = t.shape[1]
-    if C % 4 or t.dtype not in (torch.float32, torch.bfloat16) or t.numel() == 0:
-        return False
+    if ld is None or C % 4 or ld < C or t.dtype not in (torch.float32, torch.bfloat16) or t.numel() == 0:
+        return None
     align = 16 if (t.dtype == torch.float32 or C % 8 == 0) else 8
-    return t.data_ptr() % align == 0
+    if t.data_ptr() % align or (ld * t.element_size()) % align:
+        return None
+    return int(ld)
+
+
+def _cl_rows(t: torch.Tensor) -> bool:
+    return _rows_ld(t) is not None
 
 
 def _same_geom(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -578,17 +764,21 @@ def _bn(func, input, weight, bias, running_mean, running_var, training, momentum
     scale, shift_out = torch.empty(C, **f32), torch.empty(C, **f32)
     nat = _nat()
     mode = NativeMode.current
-    rows = _cl_rows(x)
+    ldx = _rows_ld(x)
+    rows = ldx is not None
+    if mode is not None and not (training and rows):
+        mode._flush_ctr()
     if training and rows:
         # channels-last rows: moments (slab partials) + ONE finalize that also derives the coefficients and
         # the running stats (2 launches; the generic path below takes 4)
         save_mean, save_invstd = torch.empty(C, **f32), torch.empty(C, **f32)
         p = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
         part = torch.empty(int(nat.z_reduce_rows_ws_floats(M, C)), **f32)
-        nat.z_bn_rows_fwd(_st(dev), x.data_ptr(), _DT[x.dtype], C, p(running_mean), C, M, part.data_ptr(), part.numel(),
+        ctr = mode._take_ctr() if mode is not None else None
+        nat.z_bn_rows_fwd(_st(dev), x.data_ptr(), _DT[x.dtype], ldx, p(running_mean), C, M, part.data_ptr(), part.numel(),
                           p(weight), p(bias), p(running_mean), p(running_var), float(eps),
                           float(momentum if momentum is not None else 0.1), save_mean.data_ptr(), save_invstd.data_ptr(),
-                          scale.data_ptr(), shift_out.data_ptr())
+                          scale.data_ptr(), shift_out.data_ptr(), p(ctr))
     elif training:
         acc = torch.empty(2 * C, **f32)
         fill_(acc, 0.0)
@@ -607,8 +797,8 @@ def _bn(func, input, weight, bias, running_mean, running_var, training, momentum
         save_mean = torch.empty(0, **f32)
         save_invstd = torch.empty(0, **f32)
     bshape = [1, C] + [1] * (x.dim() - 2)
-    out = torch.empty_like(x)
-    if mode is not None and mode.fuse and rows and _same_geom(out, x):
+    out = torch.empty_like(x)      # channels-last compact even for a row-strided x (empty_like of a non-dense view)
+    if mode is not None and mode.fuse and rows and _cl_rows(out):
         mode._pend_bn = _PendingBN(out, x, scale.view(bshape), shift_out.view(bshape))
     else:
         ew(out, [x, scale.view(bshape), shift_out.view(bshape)], EW_FMA)
@@ -649,11 +839,13 @@ def _bn_bwd(func, grad_out, input, weight, running_mean, running_var, save_mean,
         mode._defer(thr.out, thr.materialize)
         mode.fused["relu_bwd+bn_bwd"] += 1
         g = thr.grad
-    if _cl_rows(g) and _cl_rows(x) and _same_geom(g, x):
+    ldg, ldx = _rows_ld(g), _rows_ld(x)
+    ldf = _rows_ld(thr.relu_out) if thr else 0
+    if ldg is not None and ldx is not None and ldf is not None and g.shape == x.shape:
         nat = _nat()
         part = torch.empty(int(nat.z_reduce_rows_ws_floats(M, C)), **f32)
-        nat.z_bn_rows_bwd(_st(dev), g.data_ptr(), _DT[g.dtype], C, x.data_ptr(), _DT[x.dtype], C,
-                          thr.relu_out.data_ptr() if thr else 0, _DT[thr.relu_out.dtype] if thr else 0, C,
+        nat.z_bn_rows_bwd(_st(dev), g.data_ptr(), _DT[g.dtype], ldg, x.data_ptr(), _DT[x.dtype], ldx,
+                          thr.relu_out.data_ptr() if thr else 0, _DT[thr.relu_out.dtype] if thr else 0, ldf,
                           thr.thr if thr else 0.0, save_mean.data_ptr(), save_invstd.data_ptr(), p(weight), C, M,
                           part.data_ptr(), part.numel(), k.data_ptr(), bb.data_ptr(), cc.data_ptr(), p(gw), p(gb))
     else:
@@ -671,10 +863,12 @@ def _bn_bwd(func, grad_out, input, weight, running_mean, running_var, save_mean,
     if output_mask[0]:
         bshape = [1, C] + [1] * (x.dim() - 2)
         gi = torch.empty_like(x)
-        if thr is not None:
-            ew(gi, [g, k.view(bshape), x, bb.view(bshape), cc.view(bshape), thr.relu_out], EW_BNB_THR, thr.thr)
+        ins = [g, k.view(bshape), x, bb.view(bshape), cc.view(bshape)] + ([thr.relu_out] if thr is not None else [])
+        pend = _PendingBNB(gi, ins, thr.thr if thr is not None else 0.0)
+        if mode is not None and mode.fuse:
+            mode._pend_bnb = pend            # autograd's accumulation add of this gradient may join the pass
         else:
-            ew(gi, [g, k.view(bshape), x, bb.view(bshape), cc.view(bshape)], EW_BNB)
+            pend.materialize()
     if gw is not None and weight is not None and gw.dtype != weight.dtype:
         gw = ew(torch.empty_like(weight), [gw], EW_COPY)
     return gi, gw, gb
@@ -826,9 +1020,13 @@ def _native_dropout_bwd(func, grad_output, mask, scale):
 
 
 # ---- convolution ----------------------------------------------------------------------
-def _cl_bf16(x: torch.Tensor) -> torch.Tensor:
-    """channels-last contiguous bf16 (NCHW-shaped) -- a no-op for the engine's activations."""
+def _cl_bf16(x: torch.Tensor, rows: bool = False) -> torch.Tensor:
+    """channels-last contiguous bf16 (NCHW-shaped) -- a no-op for the engine's activations.  ``rows``: a
+    row-strided channels-last view (a channel slice) passes as is too (the MFMA conv paths pad / copy it
+    through :func:`_pad_c`, which reads row strides)."""
     if x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last):
+        return x
+    if rows and x.dtype == torch.bfloat16 and x.dim() == 4 and _row_stride(_nhwc(x)) is not None:
         return x
     out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
     return ew(out, [x], EW_COPY)
@@ -890,10 +1088,11 @@ def _pad_c(t: torch.Tensor, c8: int, cache: bool = False) -> torch.Tensor:
 
 
 def _unpad_c(t: torch.Tensor, c: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The first ``c`` channels of a channel-padded NHWC result: copied into ``out`` when given, else the
+    row-strided view itself -- its consumers (BN row passes, elementwise / concat copies, the next conv's
+    channel pad) all read row strides, so the compacting copy is not needed."""
     if out is None:
-        if t.shape[-1] == c:
-            return t
-        out = torch.empty(*t.shape[:-1], c, dtype=t.dtype, device=t.device)
+        return t if t.shape[-1] == c else t[..., :c]
     return ew(out, [t[..., :c]], EW_COPY)
 
 
@@ -912,10 +1111,23 @@ def _pad_o(w32: torch.Tensor, o8: int) -> torch.Tensor:
 def _packed(w32, O8: int, C8: int, st: int, pd: int, need_wd: bool = False):
     """bf16 [O8, R, S, C8] conv image of fp32 ``w32`` (and with ``need_wd`` its DGRAD image), packed once per
     NativeMode block: the forward packs, the backward of the same step reuses (the weights only change at
-    the SGD, outside the block) -- per conv one pack launch, and the O-padding copies, fewer per step."""
+    the SGD, outside the block).  Weights living in the trainer's flat parameter storage
+    (:attr:`NativeMode.stable_storage`) are remembered: the next block packs all of them in one multi-tensor
+    launch at its first conv (and all DGRAD images at its first conv backward) instead of one launch each."""
     mode = NativeMode.current
     cache = mode._wcache if mode is not None else None
     key = (w32.data_ptr(), tuple(w32.shape), tuple(w32.stride()), O8, C8, st, pd)
+    if mode is not None:
+        if not mode._prepacked:
+            mode._prepacked = True
+            mode._prepack(wd=False)
+        if need_wd and not mode._prepacked_wd:
+            mode._prepacked_wd = True
+            mode._prepack(wd=True)
+        if mode.stable_storage and w32.untyped_storage().data_ptr() == mode.stable_storage:
+            mode._pack_plan.setdefault(key, w32)
+            if need_wd:
+                mode._wd_plan.setdefault(key, w32)
     ent = cache.get(key) if cache is not None else None
     if ent is None:
         ent = {}
@@ -923,21 +1135,17 @@ def _packed(w32, O8: int, C8: int, st: int, pd: int, need_wd: bool = False):
             cache[key] = (w32, ent)          # holds w32: the pointer key stays valid for the block
     else:
         ent = ent[1]
-    O, Cw, R, S = w32.shape
     if "wp" not in ent:
-        if O8 == O and w32.is_contiguous():
-            ent["wp"] = CV.pack_weight(w32, c_pad=C8)
-        else:
-            wp = torch.empty(O8, R, S, C8, dtype=torch.bfloat16, device=w32.device)
-            fill_(wp[O:], 0.0)
-            CV.pack_weight(w32.contiguous(), c_pad=C8, out=wp[:O])
-            ent["wp"] = wp
+        ent["wp"] = CV.pack_weight(w32.contiguous(), c_pad=C8, o_pad=O8)   # zero filters O..O8: same launch
     if need_wd and "wd" not in ent:
-        w8 = _pad_o(w32, O8)
-        wd = torch.empty(CV.dgrad_image_numel(w8.shape, C8), dtype=torch.bfloat16, device=w32.device)
-        CV.dgrad_pack_weights([(w8, wd, st, pd, C8)])
-        ent["wd"] = wd
+        ent["wd"] = _wd_image(w32, O8, C8, st, pd)
+        CV.dgrad_pack_weights([(_pad_o(w32, O8), ent["wd"], st, pd, C8)])
     return ent["wp"], ent.get("wd")
+
+
+def _wd_image(w32, O8, C8, st, pd):
+    return torch.empty(CV.dgrad_image_numel((O8,) + tuple(w32.shape[1:]), C8), dtype=torch.bfloat16,
+                       device=w32.device)
 
 
 def _dense_fwd(xh, w32, st, pd, out=None):
@@ -996,7 +1204,7 @@ def _conv(func, input, weight, bias, stride, padding, dilation, transposed, outp
     dev = input.device
     w32 = weight if weight.dtype == torch.float32 else ew(torch.empty(weight.shape, device=dev), [weight], EW_COPY)
     if kind in ("mfma", "dw"):
-        xh = _nhwc(_cl_bf16(input))
+        xh = _nhwc(_cl_bf16(input, rows=kind == "mfma"))
         if kind == "dw":
             y = CV.dwconv_fwd(xh, w32.contiguous(), st[0], pd[0])
         elif groups == 1:
@@ -1036,8 +1244,8 @@ def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dil
     w32 = weight if weight.dtype == torch.float32 else ew(torch.empty(weight.shape, device=dev), [weight], EW_COPY)
     gi = gw = gb = None
     if kind in ("mfma", "dw"):
-        xh = _nhwc(_cl_bf16(input))
-        gy = _nhwc(_cl_bf16(grad_output))
+        xh = _nhwc(_cl_bf16(input, rows=kind == "mfma"))
+        gy = _nhwc(_cl_bf16(grad_output, rows=kind == "mfma"))
         if kind == "dw":
             if output_mask[0]:
                 gi = _nchw(CV.dwconv_dgrad(gy, w32.contiguous(), xh.shape, st[0], pd[0]))
@@ -1075,10 +1283,13 @@ def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dil
         gw = ew(torch.empty_like(weight), [gw], EW_COPY)
     if output_mask[2]:
         gb = torch.empty(O, dtype=weight.dtype, device=dev)
-        acc = torch.empty(O, dtype=torch.float32, device=dev)
-        fill_(acc, 0.0)
-        reduce_sum(grad_output, [0, 2, 3], acc)
-        ew(gb, [acc], EW_COPY)
+        if _rowmajor_out(gb):
+            reduce_sum(grad_output, [0, 2, 3], None, out=gb)
+        else:
+            acc = torch.empty(O, dtype=torch.float32, device=dev)
+            fill_(acc, 0.0)
+            reduce_sum(grad_output, [0, 2, 3], acc)
+            ew(gb, [acc], EW_COPY)
     return gi, gw, gb
 
 
@@ -1100,6 +1311,12 @@ _PASSTHROUGH = _ops(
     "new_empty_strided", "reshape", "flatten.using_ints", "_reshape_alias", "lift_fresh", "narrow", "unflatten.int",
     "_local_scalar_dense", "is_same_size", "as_strided_", "view.dtype", "set_.source_Storage_storage_offset",
 )
+
+
+_BN_FWD = _ops("native_batch_norm", "miopen_batch_norm")
+# in-place ops among the native impls (their first argument is written)
+_INPLACE = _ops("add_.Tensor", "sub_.Tensor", "mul_.Tensor", "div_.Scalar", "relu_", "copy_", "fill_.Scalar",
+                "zero_", "bernoulli_.float")
 
 
 class _MixedDtypeConv(TorchFunctionMode):
@@ -1140,12 +1357,58 @@ class NativeMode(TorchDispatchMode):
         self._pend_thr: Optional[_PendingThr] = None
         self._dead = {}                 # storage ptr -> materialiser of a tensor a fused op never wrote
         self.fused = collections.Counter()
+        self.packs = collections.Counter()   # weight images packed by the batched per-block launches
         self._wcache = {}               # packed conv weights of the current block (see _packed)
+        self._pend_ctr: Optional[torch.Tensor] = None   # a BN counter increment waiting for its BN forward
+        self._pend_bnb: Optional[_PendingBNB] = None    # a BN input gradient waiting for its accumulation add
+        self._pend_mul: Optional[_PendingMul] = None    # a product waiting for the reduction that sums it
+        self.stable_storage = 0         # data_ptr of the trainer's flat parameter storage (set by the trainer)
+        self._pack_plan, self._wd_plan = {}, {}   # weight-image keys of stable weights -> fp32 master (kept)
+        self._prepacked = self._prepacked_wd = False
+        self._cat_plan = {}             # concat-chain head shapes -> final width (kept across blocks)
+        self._catbufs = {}              # storage ptr -> _CatBuf of the current block
+        self._cat_src = {}              # (ptr, shape) of a plain cat output of this block -> its chain head
 
     def _defer(self, t: torch.Tensor, materialize) -> None:
         self._dead[t.untyped_storage().data_ptr()] = materialize
 
+    def _prepack(self, wd: bool) -> None:
+        """Pack every remembered weight image (``wd``: DGRAD images) of the trainer's parameters in as few
+        launches as the multi-tensor pack kernels take (see :func:`_packed`)."""
+        plan = self._wd_plan if wd else self._pack_plan
+        items = []
+        for key, w32 in plan.items():
+            O8, C8, st, pd = key[3:]
+            ent = self._wcache.setdefault(key, (w32, {}))[1]
+            if wd:
+                if "wd" not in ent and w32.shape[0] == O8 and w32.is_contiguous():
+                    ent["wd"] = _wd_image(w32, O8, C8, st, pd)
+                    items.append((w32, ent["wd"], st, pd, C8))
+            elif "wp" not in ent and w32.is_contiguous():
+                O, _, R, S = w32.shape
+                ent["wp"] = torch.empty(O8, R, S, C8, dtype=torch.bfloat16, device=w32.device)
+                items.append((w32, ent["wp"]))
+        if items:
+            (CV.dgrad_pack_weights if wd else CV.pack_weights)(items)
+            self.packs["wd" if wd else "wp"] += len(items)
+
+    def _flush_ctr(self) -> None:
+        if self._pend_ctr is not None:
+            t, self._pend_ctr = self._pend_ctr, None
+            ew(t, [t], EW_ADDS, 1.0)
+
+    def _take_ctr(self) -> Optional[torch.Tensor]:
+        t, self._pend_ctr = self._pend_ctr, None
+        return t
+
     def _flush(self) -> None:
+        self._flush_ctr()
+        if self._pend_mul is not None:
+            pend, self._pend_mul = self._pend_mul, None
+            pend.materialize()
+        if self._pend_bnb is not None:
+            pend, self._pend_bnb = self._pend_bnb, None
+            pend.materialize()
         if self._pend_bn is not None:
             pend, self._pend_bn = self._pend_bn, None
             pend.materialize()
@@ -1156,6 +1419,16 @@ class NativeMode(TorchDispatchMode):
     def _touch(self, args, kwargs) -> None:
         """Before an op runs: materialise a pending result it does not fuse with, and any deferred tensor
         it reads (a fused op left it unwritten)."""
+        if self._pend_ctr is not None and self._func not in _BN_FWD:
+            self._flush_ctr()
+        if self._pend_mul is not None and not (self._func in (aten.sum.dim_IntList, aten.mean.dim) and args
+                                               and _same(args[0], self._pend_mul.out)):
+            pend, self._pend_mul = self._pend_mul, None
+            pend.materialize()
+        if self._pend_bnb is not None and not (self._func in (aten.add.Tensor, aten.add_.Tensor)
+                                               and _bnb_add_partner(self._pend_bnb, args, kwargs) is not None):
+            pend, self._pend_bnb = self._pend_bnb, None
+            pend.materialize()
         if self._pend_bn is not None and not self._fuses_bn(args, kwargs):
             pend, self._pend_bn = self._pend_bn, None
             pend.materialize()
@@ -1195,6 +1468,8 @@ class NativeMode(TorchDispatchMode):
         self._prev = NativeMode.current
         NativeMode.current = self
         self._wcache = {}
+        self._prepacked = self._prepacked_wd = False
+        self._catbufs, self._cat_src = {}, {}
         self._fn_mode = _MixedDtypeConv()
         self._fn_mode.__enter__()
         return super().__enter__()
@@ -1205,6 +1480,7 @@ class NativeMode(TorchDispatchMode):
         finally:
             self._dead.clear()
             self._wcache = {}
+            self._catbufs, self._cat_src = {}, {}
         NativeMode.current = self._prev
         try:
             return super().__exit__(*exc)
@@ -1219,6 +1495,10 @@ class NativeMode(TorchDispatchMode):
                 self._touch(args, kwargs)
             return func(*args, **kwargs)
         self._func = func
+        if self._catbufs and func in _INPLACE and isinstance(args[0], torch.Tensor) and args[0].is_cuda \
+                and args[0].untyped_storage().data_ptr() in self._catbufs:
+            raise RuntimeError(f"native_mode: {func} writes in place into a shared concat buffer (a cat output "
+                               "aliases the inputs of later cats); run this model with NativeMode(fuse=False)")
         self._touch(args, kwargs)
         fn = _IMPL.get(func)
         on_gpu = _dev(args, tuple(kwargs.values())) is not None

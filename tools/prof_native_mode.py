@@ -22,4 +22,4 @@ tr.model.train()
 for i in range(steps):
     tr.train_step(128 * (i % 4), 128)
 torch.cuda.synchronize()
-print(name, "fallbacks", dict(tr.mode.fallbacks), flush=True)
+print(name, "fallbacks", dict(tr.mode.fallbacks), "fused", dict(tr.mode.fused), flush=True)
