@@ -490,11 +490,10 @@ __global__ __launch_bounds__(256) void pad_rows_kernel(const bf16* __restrict__ 
   }
 }
 
-// Finalize arguments of a BatchNorm row pass folded into the reduction's last-arriving workgroup
+// Finalize arguments of a row pass, applied per channel by rows_fin_kernel
 // (mode 1: forward statistics -> coefficients / running stats, 2: backward sums -> coefficients, 0: none)
 struct BnFin {
   int mode;
-  int slot;               // arrival-ticket slot of this launch (g_rows_ticket)
   long long M;
   const float* shift; const float* w; const float* b; float* rmean; float* rvar; float eps, mom;
   float* save_mean; float* save_invstd; float* scale; float* bias;
@@ -533,28 +532,27 @@ FEDMI_DEV void bn_bwd_fin(const BnFin& f, int c, float sg, float sgx) {
   if (f.db) f.db[c] = sg;
 }
 
-// Arrival tickets of the fused BN row passes (each reset to 0 by its last arriver).  Every launch takes its
-// own slot (host-side round robin), so passes running concurrently on different streams or from different
-// trainers of one process never share a ticket; a graph node keeps the slot it was captured with.
-constexpr int kRowsTicketSlots = 4096;
-__device__ unsigned int g_rows_ticket[kRowsTicketSlots] = {};
-static std::atomic<unsigned> g_rows_slot{0};
+constexpr int kRowsTileC = 64;   // channels per workgroup column tile
 
-// ---- row reduction of a [M, C] row-major matrix (ld = row stride), C % 8 == 0 ------------------
-// The channels-last case of the BN moments / bias gradients: a thread owns 8 channels (one 16-byte
-// load per row), RL = 256 / (C/8) row lanes per block, grid.y row slabs; per-slab partials go to
-// `part` [slabs][2][C] and a finalize pass adds them in slab order (deterministic).
+// ---- row reduction of a [M, C] row-major matrix (ld = row stride), C % 4 == 0 ------------------
+// The channels-last case of the BN moments / bias gradients.  Grid = (64-channel column tiles, row slabs): a
+// thread owns VW channels (one 16- / 8-byte load per row), RL = 256 / (tile vectors) row lanes per block, the
+// row lanes are combined by a fixed-order LDS tree and each block stores its slab's sums to `part`
+// [slabs][2][C]; rows_fin_kernel then adds the slabs in slab order (deterministic) and applies the BN
+// finalize.  A kernel boundary publishes the partials: the one-launch form, whose last-arriving workgroups
+// summed the slabs after an agent-scope release per workgroup, measured 1.1-2x slower at every zoo BN shape
+// (profiles/r4_zoo/rows_ab).
 template <int VW>
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_dt, long long lda, const void* b,
                                                           int b_dt, long long ldb, const float* shift, int C,
                                                           long long M, int op, float* part, const void* f = nullptr,
-                                                          int f_dt = 0, long long ldf = 0, float thr = 0.f,
-                                                          BnFin fin = BnFin{}) {
+                                                          int f_dt = 0, long long ldf = 0, float thr = 0.f) {
   __shared__ float red[2][256 * VW];
   const int VL = C / VW;
-  const int vt = min(VL, 256);
+  const int vt = min(VL, kRowsTileC / VW);
   const int RL = 256 / vt;
-  const int v = blockIdx.x * vt + (threadIdx.x % vt);
+  const int vl = threadIdx.x % vt;
+  const int v = blockIdx.x * vt + vl;
   const int rl = threadIdx.x / vt;
   const bool act = rl < RL && v < VL;
   float s1[VW], s2[VW];
@@ -601,108 +599,68 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_d
     }
 #undef FEDMI_ROWS
   }
-  // tree over the row lanes of each channel vector
+  // fixed-order tree over the row lanes of each channel vector: fold lanes >= P2 (largest power of two <= RL)
+  // onto lanes < RL - P2, then halve
+  auto put = [&]() {
 #pragma unroll
-  for (int u = 0; u < VW; ++u) {
-    red[0][threadIdx.x * VW + u] = s1[u];
-    red[1][threadIdx.x * VW + u] = s2[u];
-  }
+    for (int u = 0; u < VW; ++u) { red[0][threadIdx.x * VW + u] = s1[u]; red[1][threadIdx.x * VW + u] = s2[u]; }
+  };
+  auto take = [&](int src_rl) {
+    const int t = (src_rl * vt + vl) * VW;
+#pragma unroll
+    for (int u = 0; u < VW; ++u) { s1[u] += red[0][t + u]; s2[u] += red[1][t + u]; }
+  };
+  int P2 = 1;
+  while (P2 * 2 <= RL) P2 *= 2;
+  put();
   __syncthreads();
+  if (rl < RL - P2) { take(rl + P2); put(); }
+  __syncthreads();
+  for (int sstep = P2 / 2; sstep >= 1; sstep /= 2) {
+    if (rl < sstep) { take(rl + sstep); put(); }
+    __syncthreads();
+  }
   if (rl == 0 && v < VL) {
-    for (int k = 1; k < RL; ++k) {
-      const int t = k * vt + (threadIdx.x % vt);
-#pragma unroll
-      for (int u = 0; u < VW; ++u) { s1[u] += red[0][t * VW + u]; s2[u] += red[1][t * VW + u]; }
-    }
     float* dst = part + (long long)blockIdx.y * 2 * C;
 #pragma unroll
     for (int u = 0; u < VW; ++u) { dst[v * VW + u] = s1[u]; dst[C + v * VW + u] = s2[u]; }
   }
-  if (!fin.mode) return;
-  // BatchNorm finalize in the LAST workgroup to arrive (cdna_hip_programming.md Guideline 16: stores retired,
-  // one agent release, relaxed ticket; the last arriver acquires and reads every slab in slab order) -- one
-  // launch per BN pass instead of reduce + finalize
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned total = gridDim.x * gridDim.y;
-    unsigned* ticket = &g_rows_ticket[fin.slot];
-    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev + 1 == total;
-    if (last) {
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  const int slabs = (int)gridDim.y;
-  // both slab sums of a channel in ONE pass, as many lanes per channel as the 256 threads allow (C <= 128:
-  // 256 / C lanes; wider: 64-channel chunks x 4 lanes), 8 slabs x 2 sums in flight per lane; lane l takes slabs
-  // l, l + L, ... and the lanes are combined in order (deterministic for a given C)
-  __shared__ float fr[2][256];
-  const int t = threadIdx.x;
-  const int L = C <= 128 ? 256 / C : 4, CW = C <= 128 ? C : 64;
-  for (int cb = 0; cb < C; cb += CW) {
-    const int cl = t % CW, l = t / CW, c = cb + cl;
-    const bool valid = l < L && c < C;
-    float v1 = 0.f, v2 = 0.f;
-    if (valid) {
-      int b = l;
-      for (; b + 7 * L < slabs; b += 8 * L) {
-        float x1[8], x2[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const float* row = part + (long long)(b + u * L) * 2 * C;
-          x1[u] = row[c];
-          x2[u] = row[C + c];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) { v1 += x1[u]; v2 += x2[u]; }
-      }
-      for (; b < slabs; b += L) {
-        const float* row = part + (long long)b * 2 * C;
-        v1 += row[c];
-        v2 += row[C + c];
-      }
-    }
-    fr[0][t] = v1;
-    fr[1][t] = v2;
-    __syncthreads();
-    if (l == 0 && c < C) {
-      float a1 = 0.f, a2 = 0.f;
-      for (int q = 0; q < L; ++q) { a1 += fr[0][q * CW + cl]; a2 += fr[1][q * CW + cl]; }
-      if (fin.mode == 1) bn_fwd_fin(fin, c, a1, a2);
-      else if (fin.mode == 2) bn_bwd_fin(fin, c, a1, a2);
-      else rstore(fin.out, fin.out_dt, c, fin.out_scale * (fin.two ? a2 : a1));
-    }
-    __syncthreads();
-  }
-  if (fin.ctr && threadIdx.x == 0) fin.ctr[0] += 1;
 }
 
-// acc[c] += sum_slab part[slab][0][c] (and acc2 from part[slab][1][c]), slab order
-__global__ __launch_bounds__(256) void reduce_rows_finalize(const float* part, int slabs, int C, int two, float* acc,
-                                                            float* acc2) {
+// the slab sums of 64 channels per block (4 lanes per channel, combined in order), then per channel: the BN
+// forward finalize (fin.mode 1), the BN backward coefficients (2), a direct store (3), or acc += sums (0)
+__global__ __launch_bounds__(256) void rows_fin_kernel(const float* part, int slabs, int C, int two, float* acc,
+                                                       float* acc2, BnFin fin) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const float t1 = ordered_slab_sum(part, slabs, 2LL * C, c, c < C);
   __syncthreads();
   const float t2 = two ? ordered_slab_sum(part + C, slabs, 2LL * C, c, c < C) : 0.f;
+  if (fin.ctr && blockIdx.x == 0 && threadIdx.x == 0) fin.ctr[0] += 1;
   if ((threadIdx.x >> 6) || c >= C) return;
-  acc[c] += t1;
-  if (two) acc2[c] += t2;
+  if (fin.mode == 1) bn_fwd_fin(fin, c, t1, t2);
+  else if (fin.mode == 2) bn_bwd_fin(fin, c, t1, t2);
+  else if (fin.mode == 3) rstore(fin.out, fin.out_dt, c, fin.out_scale * (fin.two ? t2 : t1));
+  else {
+    acc[c] += t1;
+    if (two) acc2[c] += t2;
+  }
 }
-
-
 
 int rows_vw(int C) { return C % 8 == 0 ? 8 : 4; }
 
+int rows_tile_vecs(int C) {
+  const int VL = C / rows_vw(C), tv = kRowsTileC / rows_vw(C);
+  return VL < tv ? VL : tv;
+}
+
+int rows_tiles(int C) {
+  const int VL = C / rows_vw(C), vt = rows_tile_vecs(C);
+  return (VL + vt - 1) / vt;
+}
+
 int rows_slabs(long long M, int C) {
-  const int VL = C / rows_vw(C), vt = VL < 256 ? VL : 256, RL = 256 / vt;
-  const long long tiles = (VL + vt - 1) / vt;
+  const int RL = 256 / rows_tile_vecs(C);
+  const long long tiles = rows_tiles(C);
   constexpr long long per_lane = 16;               // rows per row lane
   long long sl = M / ((long long)RL * per_lane);    // >= per_lane rows per row lane
   const long long cap = (2048 + tiles - 1) / tiles;  // ~2048 blocks in flight at most
@@ -1478,54 +1436,49 @@ void launch_pad_rows(hipStream_t st, const bf16* src, long long lds, int C, bf16
 
 long long reduce_rows_ws_floats(long long M, int C) { return (long long)rows_slabs(M, C) * 2 * C; }
 
+// phase 1 (row slabs -> part) + rows_fin_kernel (slab sums -> fin / out / acc)
+static void rows_launch(hipStream_t st, const void* a, int a_dt, long long lda, const void* b, int b_dt, long long ldb,
+                        const float* shift, int C, long long M, int op, float* part, long long part_floats,
+                        const void* f, int f_dt, long long ldf, float thr, float* acc, float* acc2, const BnFin& fin,
+                        const char* what) {
+  if (C % 4 || C <= 0 || M <= 0) throw std::invalid_argument(std::string(what) + ": C % 4 == 0 and M > 0 required");
+  const int slabs = rows_slabs(M, C);
+  if (part_floats < reduce_rows_ws_floats(M, C)) throw std::invalid_argument(std::string(what) + ": workspace too small");
+  const dim3 grid((unsigned)rows_tiles(C), (unsigned)slabs);
+  if (rows_vw(C) == 8)
+    hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
+                       f, f_dt, ldf, thr);
+  else
+    hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
+                       f, f_dt, ldf, thr);
+  hipLaunchKernelGGL(rows_fin_kernel, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C,
+                     op != RD_SUM ? 1 : 0, acc, acc2, fin);
+  check_hip(hipGetLastError(), what);
+}
+
 void launch_reduce_rows(hipStream_t st, const void* a, int a_dt, long long lda, const void* b, int b_dt,
                         long long ldb, const float* shift, int C, long long M, int op, float* part, long long part_floats,
                         float* acc, float* acc2, void* out, int out_dt, float scale) {
-  if (C % 4 || C <= 0 || M <= 0) throw std::invalid_argument("reduce_rows: C % 4 == 0 and M > 0 required");
   if (out && op == RD_SUMSQ_SHIFT) throw std::invalid_argument("reduce_rows: no direct output of moments");
-  const int slabs = rows_slabs(M, C);
-  if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("reduce_rows: workspace too small");
-  const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
-  const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
   BnFin fin{};
-  if (out) {   // the sums stored by the last-arriving workgroup: one launch, no zeroed accumulator, no copy
-    fin.mode = 3; fin.slot = (int)(g_rows_slot.fetch_add(1u) % kRowsTicketSlots);
-    fin.out = out; fin.out_dt = out_dt; fin.out_scale = scale; fin.two = op != RD_SUM;
+  if (out) {   // the sums stored directly: no zeroed accumulator, no copy
+    fin.mode = 3; fin.out = out; fin.out_dt = out_dt; fin.out_scale = scale; fin.two = op != RD_SUM;
   }
-  if (vw == 8)
-    hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
-                       nullptr, 0, 0LL, 0.f, fin);
-  else
-    hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
-                       nullptr, 0, 0LL, 0.f, fin);
-  if (!out)
-    hipLaunchKernelGGL(reduce_rows_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C,
-                       op != RD_SUM ? 1 : 0, acc, acc2);
-  check_hip(hipGetLastError(), "reduce_rows");
+  rows_launch(st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part, part_floats, nullptr, 0, 0LL, 0.f, acc, acc2, fin,
+              "reduce_rows");
 }
 
-// BN forward statistics + coefficients of a channels-last [M, C] activation: reduce_rows + one finalize
+// BN forward statistics + coefficients of a channels-last [M, C] activation
 void launch_bn_rows_fwd(hipStream_t st, const void* x, int x_dt, long long ldx, const float* shift, int C, long long M,
                         float* part, long long part_floats, const float* w, const float* b, float* rmean, float* rvar,
                         float eps, float mom, float* save_mean, float* save_invstd, float* scale, float* bias,
                         long long* ctr) {
-  if (C % 4 || C <= 0 || M <= 0) throw std::invalid_argument("bn_rows_fwd: C % 4 == 0 and M > 0 required");
-  const int slabs = rows_slabs(M, C);
-  if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("bn_rows_fwd: workspace too small");
-  const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
-  const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
   BnFin fin{};
-  fin.slot = (int)(g_rows_slot.fetch_add(1u) % kRowsTicketSlots);
   fin.mode = 1; fin.M = M; fin.shift = shift; fin.w = w; fin.b = b; fin.rmean = rmean; fin.rvar = rvar;
   fin.eps = eps; fin.mom = mom; fin.save_mean = save_mean; fin.save_invstd = save_invstd; fin.scale = scale;
   fin.bias = bias; fin.ctr = ctr;
-  if (vw == 8)
-    hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, x, x_dt, ldx, nullptr, 0, 0LL, shift, C, M,
-                       (int)RD_SUMSQ_SHIFT, part, nullptr, 0, 0LL, 0.f, fin);
-  else
-    hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, x, x_dt, ldx, nullptr, 0, 0LL, shift, C, M,
-                       (int)RD_SUMSQ_SHIFT, part, nullptr, 0, 0LL, 0.f, fin);
-  check_hip(hipGetLastError(), "bn_rows_fwd");
+  rows_launch(st, x, x_dt, ldx, nullptr, 0, 0LL, shift, C, M, (int)RD_SUMSQ_SHIFT, part, part_floats, nullptr, 0, 0LL,
+              0.f, nullptr, nullptr, fin, "bn_rows_fwd");
 }
 
 // BN backward sums + coefficients; f (optional): the ReLU output whose threshold_backward is fused in
@@ -1533,22 +1486,11 @@ void launch_bn_rows_bwd(hipStream_t st, const void* g, int g_dt, long long ldg, 
                         const void* f, int f_dt, long long ldf, float thr, const float* mean, const float* invstd,
                         const float* w, int C, long long M, float* part, long long part_floats, float* k, float* bb,
                         float* cc, float* dw, float* db) {
-  if (C % 4 || C <= 0 || M <= 0) throw std::invalid_argument("bn_rows_bwd: C % 4 == 0 and M > 0 required");
-  const int slabs = rows_slabs(M, C);
-  if (part_floats < (long long)slabs * 2 * C) throw std::invalid_argument("bn_rows_bwd: workspace too small");
-  const int vw = rows_vw(C), VL = C / vw, vt = VL < 256 ? VL : 256;
-  const dim3 grid((unsigned)((VL + vt - 1) / vt), (unsigned)slabs);
   BnFin fin{};
-  fin.slot = (int)(g_rows_slot.fetch_add(1u) % kRowsTicketSlots);
   fin.mode = 2; fin.M = M; fin.mean = mean; fin.invstd = invstd; fin.w = w; fin.k = k; fin.bb = bb; fin.cc = cc;
   fin.dw = dw; fin.db = db;
-  if (vw == 8)
-    hipLaunchKernelGGL(reduce_rows_kernel<8>, grid, dim3(256), 0, st, g, g_dt, ldg, x, x_dt, ldx, mean, C, M,
-                       (int)RD_DOT_SHIFT, part, f, f_dt, ldf, thr, fin);
-  else
-    hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, g, g_dt, ldg, x, x_dt, ldx, mean, C, M,
-                       (int)RD_DOT_SHIFT, part, f, f_dt, ldf, thr, fin);
-  check_hip(hipGetLastError(), "bn_rows_bwd");
+  rows_launch(st, g, g_dt, ldg, x, x_dt, ldx, mean, C, M, (int)RD_DOT_SHIFT, part, part_floats, f, f_dt, ldf, thr,
+              nullptr, nullptr, fin, "bn_rows_bwd");
 }
 
 void launch_bn_fwd_coeffs(hipStream_t st, const float* s1, const float* s2, const float* shift, int C, long long M,

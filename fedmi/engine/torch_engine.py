@@ -48,8 +48,10 @@ class FlatState:
         self.grad = torch.zeros(n, dtype=torch.float32, device=device)
         self.mom = torch.zeros(n, dtype=torch.float32, device=device)
         off = 0
+        self.offsets = []
         for p in params:
             k = p.numel()
+            self.offsets.append(off)
             self.flat[off:off + k].copy_(p.data.reshape(-1))
             p.data = self.flat[off:off + k].view_as(p)
             p.grad = self.grad[off:off + k].view_as(p)
@@ -100,6 +102,15 @@ class TorchTrainer(LocalTrainer):
             self.mode = NativeMode(strict=os.environ.get("FEDMI_NATIVE_STRICT", "0") == "1", seed=cfg.seed)
             self.mode.rng_ctr(self._device)      # allocated here, never inside a captured step
             self.mode.stable_storage = self.fs.flat.untyped_storage().data_ptr()   # weight images: batched packs
+            # parameter gradients written straight into the flat gradient buffer (see native_mode._param_grad)
+            self.mode.grad_flat = self.fs.grad
+            self._params = list(self.model.parameters())
+            self._grad_views = [self.fs.grad[o:o + p.numel()].view_as(p) for o, p in zip(self.fs.offsets, self._params)]
+            off_of = {id(p): o for o, p in zip(self.fs.offsets, self._params)}
+            for m in self.model.modules():
+                w, b = getattr(m, "weight", None), getattr(m, "bias", None)
+                if isinstance(w, nn.Parameter) and isinstance(b, nn.Parameter) and id(w) in off_of and id(b) in off_of:
+                    self.mode.bias_of[off_of[id(w)]] = (off_of[id(b)], b.numel())
         # hybrid mode replays each full-batch SGD step (zero-grad + forward + autograd backward + SGD +
         # stats) from one captured HIP graph: the Python / launch overhead of ~10^3 small kernels per step
         # goes away.  Round 1's NaN-under-replay (autocast weight-cast cache, bf16 adaptive pooling, host
@@ -216,9 +227,15 @@ class TorchTrainer(LocalTrainer):
 
             with self.mode:
                 self.fs.grad.zero_()
+                for p in self._params:        # AccumulateGrad adopts the native backward's flat-buffer gradients
+                    p.grad = None
                 out = self._run(x)
                 loss = F.cross_entropy(out, y)
                 loss.backward()
+                for p, g in zip(self._params, self._grad_views):
+                    if p.grad is not None and p.grad.data_ptr() != g.data_ptr():
+                        g.copy_(p.grad)       # a gradient not produced in place (classifier GEMM, ATen op)
+                    p.grad = g
             self._sgd()
             ce_stats_(out.detach(), y, self._tstats)
             return loss

@@ -132,6 +132,11 @@ def ew(out: torch.Tensor, ins, op: int, s0: float = 0.0, s1: float = 0.0, seed: 
     if vmask >= 0:
         nshape = nshape[:-1] + [nshape[-1] // vw]
         nstr = [st[:-1] + [st[-1] * vw] for st in nstr]
+    if NativeMode.current is not None:   # diagnostics: passes per op code, and which miss the vector launch
+        NativeMode.current.ew_ops[(NativeMode.current._func_name(), op)] += 1
+        if vmask < 0:
+            NativeMode.current.scalar_ew[(op, tuple(out.shape), tuple(out.stride()),
+                                          tuple(tuple(t.stride()) for t in ts))] += 1
     descs = [(t.data_ptr(), _DT[t.dtype], nshape, st) for t, st in zip(allt, nstr)]
     _nat().z_ew(_st(out.device), descs[0], descs[1:], op, float(s0), float(s1), int(seed) & 0xFFFFFFFF,
                 0 if ctr is None else ctr.data_ptr(), vmask, vw)
@@ -600,6 +605,11 @@ def _cat(func, tensors, dim=0):
             return r
         head = r
     out = _alloc_like_meta(func, (tensors,), {"dim": dim}, _dev(tensors))
+    if (out.dim() == 4 and dim % 4 == 1 and not out.is_contiguous(memory_format=torch.channels_last)
+            and all(t.dim() == 4 and t.stride(1) == 1 for t in tensors)):
+        # channel slices of channels-last activations (DPN's dual path) make ATen's meta pick NCHW: keep the
+        # activations channels-last (vector copies here, no layout transposes in the next conv)
+        out = torch.empty(out.shape, dtype=out.dtype, device=out.device, memory_format=torch.channels_last)
     d = dim % out.dim()
     off = 0
     for t in tensors:
@@ -616,6 +626,10 @@ def _cat(func, tensors, dim=0):
 @impl(aten.slice_backward.default)
 def _slice_bwd(func, grad_output, input_sizes, dim, start, end, step):
     out = _alloc_like_meta(func, (grad_output, input_sizes, dim, start, end, step), {}, grad_output.device)
+    if out.dim() == 4 and grad_output.stride(1) == 1 and not out.is_contiguous(memory_format=torch.channels_last):
+        # the meta function allocates NCHW zeros: keep a channels-last gradient channels-last (DPN's dual-path
+        # slices would otherwise turn every upstream BN backward and conv gradient into layout transposes)
+        out = torch.empty(out.shape, dtype=out.dtype, device=out.device, memory_format=torch.channels_last)
     fill_(out, 0.0)
     ew(aten.slice.Tensor(out, dim, start, end, step), [grad_output], EW_COPY)
     return out
@@ -829,8 +843,10 @@ def _bn_bwd(func, grad_out, input, weight, running_mean, running_var, save_mean,
     M = x.numel() // C
     f32 = dict(dtype=torch.float32, device=dev)
     k, bb, cc = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(C, **f32)
-    gw = torch.empty(C, **f32) if output_mask[1] else None
-    gb = torch.empty(C, **f32) if output_mask[2] else None
+    gw = (_param_grad(weight) if output_mask[1] else None) if weight is not None else None
+    gw = gw if gw is not None else (torch.empty(C, **f32) if output_mask[1] else None)
+    gb = (_param_grad(weight, bias=True) if output_mask[2] else None) if weight is not None else None
+    gb = gb if gb is not None and gb.shape[0] == C else (torch.empty(C, **f32) if output_mask[2] else None)
     p = lambda t: 0 if t is None else t.data_ptr()   # noqa: E731
     mode = NativeMode.current
     thr = None
@@ -1192,6 +1208,29 @@ def _ws(dev, floats):
     return CV.wgrad_workspace(dev, floats) if floats > 0 else None
 
 
+def _param_grad(w: Optional[torch.Tensor], bias: bool = False) -> Optional[torch.Tensor]:
+    """The trainer's flat-gradient slot of parameter ``w`` (``bias``: of the bias that belongs to weight ``w``), a
+    view of :attr:`NativeMode.grad_flat` shaped like the parameter, handed out once per block.  A native backward
+    writes the parameter gradient straight into it and autograd's AccumulateGrad adopts the tensor as ``p.grad``
+    (the trainer clears ``p.grad`` before backward, :meth:`fedmi.engine.torch_engine.TorchTrainer._step_body`):
+    no accumulation pass per parameter (~360 launches per DenseNet step).  None: allocate as usual."""
+    mode = NativeMode.current
+    if (mode is None or mode.grad_flat is None or not isinstance(w, torch.Tensor) or not w.is_cuda
+            or w.dtype != torch.float32 or not w.is_contiguous() or w.untyped_storage().data_ptr() != mode.stable_storage):
+        return None
+    off, n, shape = w.storage_offset(), w.numel(), w.shape
+    if bias:
+        ent = mode.bias_of.get(off)
+        if ent is None:
+            return None
+        off, n = ent
+        shape = (n,)
+    if off + n > mode.grad_flat.numel() or off in mode._grad_taken:
+        return None
+    mode._grad_taken.add(off)
+    return mode.grad_flat[off:off + n].view(shape)
+
+
 @impl(aten.convolution.default)
 def _conv(func, input, weight, bias, stride, padding, dilation, transposed, output_padding, groups):
     if transposed or input.dim() != 4:
@@ -1243,6 +1282,7 @@ def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dil
     dev = input.device
     w32 = weight if weight.dtype == torch.float32 else ew(torch.empty(weight.shape, device=dev), [weight], EW_COPY)
     gi = gw = gb = None
+    gw_slot = _param_grad(weight) if output_mask[1] else None
     if kind in ("mfma", "dw"):
         xh = _nhwc(_cl_bf16(input, rows=kind == "mfma"))
         gy = _nhwc(_cl_bf16(grad_output, rows=kind == "mfma"))
@@ -1250,14 +1290,15 @@ def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dil
             if output_mask[0]:
                 gi = _nchw(CV.dwconv_dgrad(gy, w32.contiguous(), xh.shape, st[0], pd[0]))
             if output_mask[1]:
-                gw = CV.dwconv_wgrad(xh, gy, k[0], st[0], pd[0])
+                gw = CV.dwconv_wgrad(xh, gy, k[0], st[0], pd[0], out=gw_slot)
         elif groups == 1:
-            dx, gw = _dense_bwd(xh, gy, w32, st[0], pd[0], output_mask[0], output_mask[1])
+            dx, gw = _dense_bwd(xh, gy, w32, st[0], pd[0], output_mask[0], output_mask[1], dw_out=gw_slot)
             gi = _nchw(dx) if dx is not None else None
         else:
             Cg, Og = C // groups, O // groups
             gih = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dev) if output_mask[0] else None
-            gw = torch.empty(O, Cg, k[0], k[1], dtype=torch.float32, device=dev) if output_mask[1] else None
+            gw = (gw_slot if gw_slot is not None else torch.empty(O, Cg, k[0], k[1], dtype=torch.float32, device=dev)) \
+                if output_mask[1] else None
             for g in range(groups):
                 _dense_bwd(xh[..., g * Cg:(g + 1) * Cg], gy[..., g * Og:(g + 1) * Og], w32[g * Og:(g + 1) * Og],
                            st[0], pd[0], output_mask[0], output_mask[1],
@@ -1273,7 +1314,7 @@ def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dil
             gi = torch.empty_like(input)
             _nat().z_gconv(_st(dev), 1, zd(gi), zd(w32), zd(grad_output), int(groups), st[0], st[1], pd[0], pd[1])
         if output_mask[1]:
-            gw = torch.empty(w32.shape, dtype=torch.float32, device=dev)
+            gw = gw_slot if gw_slot is not None else torch.empty(w32.shape, dtype=torch.float32, device=dev)
             P, Q = grad_output.shape[2], grad_output.shape[3]
             wsf = int(_nat().z_gconv_wgrad_ws_floats(N, P, Q, gw.numel()))
             ws = CV.wgrad_workspace(dev, wsf)
@@ -1282,7 +1323,9 @@ def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dil
     if gw is not None and gw.dtype != weight.dtype:
         gw = ew(torch.empty_like(weight), [gw], EW_COPY)
     if output_mask[2]:
-        gb = torch.empty(O, dtype=weight.dtype, device=dev)
+        gb = _param_grad(weight, bias=True)
+        if gb is None or gb.shape[0] != O:
+            gb = torch.empty(O, dtype=weight.dtype, device=dev)
         if _rowmajor_out(gb):
             reduce_sum(grad_output, [0, 2, 3], None, out=gb)
         else:
@@ -1358,12 +1401,17 @@ class NativeMode(TorchDispatchMode):
         self._dead = {}                 # storage ptr -> materialiser of a tensor a fused op never wrote
         self.fused = collections.Counter()
         self.packs = collections.Counter()   # weight images packed by the batched per-block launches
+        self.scalar_ew = collections.Counter()   # (op, shape, strides) of elementwise passes on the scalar kernel
+        self.ew_ops = collections.Counter()      # (aten op, elementwise op code) -> passes
         self._wcache = {}               # packed conv weights of the current block (see _packed)
         self._pend_ctr: Optional[torch.Tensor] = None   # a BN counter increment waiting for its BN forward
         self._pend_bnb: Optional[_PendingBNB] = None    # a BN input gradient waiting for its accumulation add
         self._pend_mul: Optional[_PendingMul] = None    # a product waiting for the reduction that sums it
         self.stable_storage = 0         # data_ptr of the trainer's flat parameter storage (set by the trainer)
         self._pack_plan, self._wd_plan = {}, {}   # weight-image keys of stable weights -> fp32 master (kept)
+        self.grad_flat: Optional[torch.Tensor] = None   # the trainer's flat gradient buffer (see _param_grad)
+        self.bias_of = {}               # weight storage offset -> (bias offset, numel) of the same module
+        self._grad_taken = set()
         self._prepacked = self._prepacked_wd = False
         self._cat_plan = {}             # concat-chain head shapes -> final width (kept across blocks)
         self._catbufs = {}              # storage ptr -> _CatBuf of the current block
@@ -1443,6 +1491,9 @@ class NativeMode(TorchDispatchMode):
 
     _func = None
 
+    def _func_name(self) -> str:
+        return str(self._func).replace("aten.", "") if self._func is not None else "?"
+
     def _fuses_bn(self, args, kwargs=None) -> bool:
         if self._func is aten.add.Tensor:
             return _bn_add_partner(self._pend_bn, args, kwargs) is not None
@@ -1470,6 +1521,7 @@ class NativeMode(TorchDispatchMode):
         self._wcache = {}
         self._prepacked = self._prepacked_wd = False
         self._catbufs, self._cat_src = {}, {}
+        self._grad_taken = set()
         self._fn_mode = _MixedDtypeConv()
         self._fn_mode.__enter__()
         return super().__enter__()

@@ -23,3 +23,7 @@ for i in range(steps):
     tr.train_step(128 * (i % 4), 128)
 torch.cuda.synchronize()
 print(name, "fallbacks", dict(tr.mode.fallbacks), "fused", dict(tr.mode.fused), flush=True)
+for k, v in tr.mode.scalar_ew.most_common(12):
+    print("scalar ew", v, k, flush=True)
+for k, v in tr.mode.ew_ops.most_common(24):
+    print("ew op", v, k, flush=True)
