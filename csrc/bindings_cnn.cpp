@@ -38,7 +38,7 @@ struct PackItem {
   int O8;
 };
 void launch_conv_pack_multi(hipStream_t, const PackItem*, int);
-void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int);
+void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int, int);
 long conv_wgrad_ws_floats(const ConvShape&);
 void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int, int);
 
@@ -170,11 +170,12 @@ void fedmi_bind_cnn(py::module_& m) {
     check("conv_pack_multi");
   });
   m.def("conv_wgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws,
-                         long ws_floats, int splits, int accumulate) {
+                         long ws_floats, int splits, int accumulate, int Ow) {
     launch_conv_wgrad(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(dy), P<float>(dw), P<float>(ws),
-                      ws_floats, splits, accumulate);
+                      ws_floats, splits, accumulate, Ow);
     check("conv_wgrad");
-  });
+  }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ws"), py::arg("ws_floats"),
+     py::arg("splits"), py::arg("accumulate"), py::arg("Ow") = 0);
   m.def("conv_wgrad_ws_floats", [](const py::tuple& shp) { return conv_wgrad_ws_floats(shape_from(shp)); });
   m.def("conv_pack", [](uintptr_t st, uintptr_t w, uintptr_t wr, int O, int Cw, int C, int RS, int O8) {
     launch_conv_pack(S(st), P<const float>(w), P<bf16>(wr), O, Cw, C, RS, O8);

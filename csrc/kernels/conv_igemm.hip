@@ -1053,12 +1053,13 @@ __global__ __launch_bounds__(256) void dgrad_pack_kernel(DPackTable t) {
 // layout scattered every 4-byte store RS floats apart).
 constexpr int WRED_MAX_RS = 49;
 __global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict__ ws, int splits, int O, int C, int Cw,
-                                                         int RS, float* __restrict__ dw, int accumulate) {
+                                                         int RS, float* __restrict__ dw, int accumulate, int Ow) {
   extern __shared__ float part_[];                 // [4][RS][65], sized by the launch
   auto part = [&](int zg, int rs, int ci) -> float& { return part_[(zg * RS + rs) * 65 + ci]; };
   const long plane = (long)O * RS * C;
   const int ncb = (C + 63) / 64;
   const int o = blockIdx.x / ncb, c0 = (blockIdx.x % ncb) * 64;
+  if (o >= Ow) return;                             // zero-padded filters: no output row (workgroup-uniform)
   const int cl = threadIdx.x & 63, zg = threadIdx.x >> 6;
   const int c = c0 + cl;
   for (int rs = 0; rs < RS; ++rs) {
@@ -1094,7 +1095,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict
 // coalesced), the 4 groups are combined in LDS, and the 64 sums are written to
 // their permuted [O][Cw][R][S] positions.  Deterministic (fixed order).
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_cols(const float* __restrict__ ws, int splits, int O, int C, int Cw,
-                                                         int RS, float* __restrict__ dw, int accumulate) {
+                                                         int RS, float* __restrict__ dw, int accumulate, int Ow) {
   __shared__ float part[4][64];
   const long plane = (long)O * RS * C;
   const long e = (long)blockIdx.x * 64 + (threadIdx.x & 63);
@@ -1115,9 +1116,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_cols(const float* __res
   if (threadIdx.x < 64 && e < plane) {
     const float s = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
     const int c = (int)(e % C);
-    if (c < Cw) {
-      const long t = e / C;
-      const int rs = (int)(t % RS), o = (int)(t / RS);
+    const long t = e / C;
+    const int rs = (int)(t % RS), o = (int)(t / RS);
+    if (c < Cw && o < Ow) {
       const long i = ((long)o * Cw + c) * RS + rs;
       dw[i] = accumulate ? dw[i] + s : s;
     }
@@ -1841,8 +1842,10 @@ long conv_wgrad_ws_floats(const ConvShape& s) {
 
 // dW[O][Cw][R][S] (fp32, PyTorch layout) = (or +=) X^T dY.  ``ws`` holds
 // ws_floats floats; splits <= 0 picks automatically within that capacity.
+// dw: [Ow][Cw][R][S] (Ow <= 0: O) -- the first Ow filters of an O-padded conv land in the unpadded gradient
 void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const bf16* dy, float* dw, float* ws,
-                       long ws_floats, int splits, int accumulate) {
+                       long ws_floats, int splits, int accumulate, int Ow) {
+  if (Ow <= 0 || Ow > s.O) Ow = s.O;
   const ConvGeom g = wgrad_geom(s);
   const long plane = (long)g.M * g.NC;
   if (ws_floats < plane) throw std::invalid_argument("conv_wgrad: workspace smaller than one O x RSC plane");
@@ -1866,10 +1869,10 @@ void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const 
   const long blocks = (long)s.O * ((s.C + 63) / 64);
   if (blocks >= 1024) {      // enough (o, channel-block) tiles: coalesced tile writes
     hipLaunchKernelGGL(conv_wgrad_reduce, dim3((unsigned)blocks), dim3(256), 4 * s.R * s.S * 65 * sizeof(float), st,
-                       ws, splits, s.O, s.C, s.Cw, s.R * s.S, dw, accumulate);
+                       ws, splits, s.O, s.C, s.Cw, s.R * s.S, dw, accumulate, Ow);
   } else {
     hipLaunchKernelGGL(conv_wgrad_reduce_cols, dim3((unsigned)((plane + 63) / 64)), dim3(256), 0, st, ws, splits, s.O,
-                       s.C, s.Cw, s.R * s.S, dw, accumulate);
+                       s.C, s.Cw, s.R * s.S, dw, accumulate, Ow);
   }
 }
 

@@ -254,8 +254,9 @@ def wgrad_ws_floats(x_shape, O: int, R: int, S: int, stride: int, pad: int, Cw: 
 
 def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None,
                  out: Optional[torch.Tensor] = None, accumulate: bool = False, splits: int = 0,
-                 ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 ws: Optional[torch.Tensor] = None, Ow: Optional[int] = None) -> torch.Tensor:
     """dW fp32 [O, Cw, R, S] (PyTorch layout).  ``accumulate`` adds into ``out`` instead of overwriting.
+    ``Ow`` < O: dy carries zero-padded filters; only the first Ow land in ``out`` ([Ow, Cw, R, S]).
 
     Split-K partials go to a workspace (plain stores) and one reduce launch sums
     them into ``out`` — no fp32 atomics on the gradient.
@@ -266,17 +267,20 @@ def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int,
     shp = shape_tuple(x.shape, O, R, S, stride, pad, Cw)
     if tuple(dy.shape) != (shp[0], shp[6], shp[7], O):
         raise ValueError("conv2d_wgrad: dy shape mismatch")
+    Ow = O if Ow is None else int(Ow)
+    if not 0 < Ow <= O:
+        raise ValueError("conv2d_wgrad: 0 < Ow <= O")
     if out is None:
-        out = torch.empty(O, shp[4], R, S, dtype=torch.float32, device=x.device)
+        out = torch.empty(Ow, shp[4], R, S, dtype=torch.float32, device=x.device)
         accumulate = False
-    if tuple(out.shape) != (O, shp[4], R, S) or out.dtype != torch.float32:
-        raise ValueError("conv2d_wgrad: out must be fp32 [O, Cw, R, S]")
+    if tuple(out.shape) != (Ow, shp[4], R, S) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("conv2d_wgrad: out must be contiguous fp32 [Ow, Cw, R, S]")
     nat = native.require()
     if ws is None:
         need = max(nat.conv_wgrad_ws_floats(shp), splits * O * R * S * shp[3])
         ws = wgrad_workspace(x.device, need)
     nat.conv_wgrad(native.stream_handle(x.device), shp, x.data_ptr(), dy.data_ptr(), out.data_ptr(), ws.data_ptr(),
-                   ws.numel(), splits, int(accumulate))
+                   ws.numel(), splits, int(accumulate), Ow)
     return out
 
 

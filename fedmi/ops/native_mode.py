@@ -1186,13 +1186,11 @@ def _dense_bwd(xh, gy, w32, st, pd, need_dx, need_dw, dx_out=None, dw_out=None):
         xs = (N, H, W, C8)
         d = CV.conv2d_dgrad(gyp, wp, xs, st, pd, wd=wd, ws=_ws(xh.device, CV.fd_ws_floats(xs, O8, R, S, st, pd)))
         dx = _unpad_c(d, Cg, dx_out)
-    if need_dw:
-        if dw_out is not None and O8 == Og:
-            dw = CV.conv2d_wgrad(_pad_c(xh, C8, cache=True), gyp, R, S, st, pd, Cw=Cg, out=dw_out)
-        else:
-            dw = CV.conv2d_wgrad(_pad_c(xh, C8, cache=True), gyp, R, S, st, pd, Cw=Cg)[:Og]
-            if dw_out is not None:
-                dw = ew(dw_out, [dw], EW_COPY)
+    if need_dw:   # the padded filters O..O8 never leave the reduction (Ow): no slice copy
+        dw = CV.conv2d_wgrad(_pad_c(xh, C8, cache=True), gyp, R, S, st, pd, Cw=Cg, Ow=Og,
+                             out=dw_out if dw_out is not None and dw_out.is_contiguous() else None)
+        if dw_out is not None and dw.data_ptr() != dw_out.data_ptr():
+            dw = ew(dw_out, [dw], EW_COPY)
     return dx, dw
 
 
