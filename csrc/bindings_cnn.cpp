@@ -36,11 +36,12 @@ struct PackItem {
   bf16* wr;
   int O, Cw, C, RS;
   int O8;
+  int G;
 };
 void launch_conv_pack_multi(hipStream_t, const PackItem*, int);
-void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int, int);
+void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int, int, int);
 long conv_wgrad_ws_floats(const ConvShape&);
-void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int, int);
+void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int, int, int);
 
 struct BNDesc {
   const double* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
@@ -162,26 +163,27 @@ void fedmi_bind_cnn(py::module_& m) {
     std::vector<PackItem> v;
     for (const auto& it : items) {
       const py::tuple t = it.cast<py::tuple>();
-      if (t.size() != 6 && t.size() != 7) throw std::invalid_argument("conv_pack_multi item: (w, wr, O, Cw, C, RS[, O8])");
+      if (t.size() < 6 || t.size() > 8) throw std::invalid_argument("conv_pack_multi item: (w, wr, O, Cw, C, RS[, O8[, G]])");
       v.push_back(PackItem{P<const float>(t[0].cast<uintptr_t>()), P<bf16>(t[1].cast<uintptr_t>()), t[2].cast<int>(),
-                           t[3].cast<int>(), t[4].cast<int>(), t[5].cast<int>(), t.size() == 7 ? t[6].cast<int>() : 0});
+                           t[3].cast<int>(), t[4].cast<int>(), t[5].cast<int>(), t.size() >= 7 ? t[6].cast<int>() : 0,
+                           t.size() >= 8 ? t[7].cast<int>() : 1});
     }
     if (!v.empty()) launch_conv_pack_multi(S(st), v.data(), (int)v.size());
     check("conv_pack_multi");
   });
   m.def("conv_wgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws,
-                         long ws_floats, int splits, int accumulate, int Ow) {
+                         long ws_floats, int splits, int accumulate, int Ow, int G) {
     launch_conv_wgrad(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(dy), P<float>(dw), P<float>(ws),
-                      ws_floats, splits, accumulate, Ow);
+                      ws_floats, splits, accumulate, Ow, G);
     check("conv_wgrad");
   }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ws"), py::arg("ws_floats"),
-     py::arg("splits"), py::arg("accumulate"), py::arg("Ow") = 0);
+     py::arg("splits"), py::arg("accumulate"), py::arg("Ow") = 0, py::arg("G") = 1);
   m.def("conv_wgrad_ws_floats", [](const py::tuple& shp) { return conv_wgrad_ws_floats(shape_from(shp)); });
-  m.def("conv_pack", [](uintptr_t st, uintptr_t w, uintptr_t wr, int O, int Cw, int C, int RS, int O8) {
-    launch_conv_pack(S(st), P<const float>(w), P<bf16>(wr), O, Cw, C, RS, O8);
+  m.def("conv_pack", [](uintptr_t st, uintptr_t w, uintptr_t wr, int O, int Cw, int C, int RS, int O8, int G) {
+    launch_conv_pack(S(st), P<const float>(w), P<bf16>(wr), O, Cw, C, RS, O8, G);
     check("conv_pack");
   }, py::arg("st"), py::arg("w"), py::arg("wr"), py::arg("O"), py::arg("Cw"), py::arg("C"), py::arg("RS"),
-     py::arg("O8") = 0);
+     py::arg("O8") = 0, py::arg("G") = 1);
   m.def("dw_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                      uintptr_t shift) {
     launch_dw_fwd(S(st), dw_from(shp), P<const bf16>(x), P<const float>(w), P<bf16>(y), P<double>(stats),

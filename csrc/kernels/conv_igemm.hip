@@ -1053,7 +1053,7 @@ __global__ __launch_bounds__(256) void dgrad_pack_kernel(DPackTable t) {
 // layout scattered every 4-byte store RS floats apart).
 constexpr int WRED_MAX_RS = 49;
 __global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict__ ws, int splits, int O, int C, int Cw,
-                                                         int RS, float* __restrict__ dw, int accumulate, int Ow) {
+                                                         int RS, float* __restrict__ dw, int accumulate, int Ow, int G) {
   extern __shared__ float part_[];                 // [4][RS][65], sized by the launch
   auto part = [&](int zg, int rs, int ci) -> float& { return part_[(zg * RS + rs) * 65 + ci]; };
   const long plane = (long)O * RS * C;
@@ -1077,11 +1077,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict
     part(zg, rs, cl) = v;
   }
   __syncthreads();
-  const int cn = min(64, Cw - c0);
-  if (cn <= 0) return;
-  float* out = dw + ((long)o * Cw + c0) * RS;
-  for (int e = threadIdx.x; e < cn * RS; e += 256) {
-    const int ci = e / RS, rs = e - ci * RS;
+  // this filter's channels: [cg0, cg0 + Cw) (G > 1: the block-diagonal group of a densified grouped conv)
+  const int cg0 = G > 1 ? (o / (O / G)) * Cw : 0;
+  const int lo = max(c0, cg0), hi = min(c0 + 64, cg0 + Cw);
+  if (hi <= lo) return;
+  float* out = dw + ((long)o * Cw + (lo - cg0)) * RS;
+  for (int e = threadIdx.x; e < (hi - lo) * RS; e += 256) {
+    const int ci = e / RS + (lo - c0), rs = e - (e / RS) * RS;
     const float s = (part(0, rs, ci) + part(1, rs, ci)) + (part(2, rs, ci) + part(3, rs, ci));
     out[e] = accumulate ? out[e] + s : s;
   }
@@ -1095,7 +1097,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict
 // coalesced), the 4 groups are combined in LDS, and the 64 sums are written to
 // their permuted [O][Cw][R][S] positions.  Deterministic (fixed order).
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_cols(const float* __restrict__ ws, int splits, int O, int C, int Cw,
-                                                         int RS, float* __restrict__ dw, int accumulate, int Ow) {
+                                                         int RS, float* __restrict__ dw, int accumulate, int Ow, int G) {
   __shared__ float part[4][64];
   const long plane = (long)O * RS * C;
   const long e = (long)blockIdx.x * 64 + (threadIdx.x & 63);
@@ -1115,10 +1117,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_cols(const float* __res
   __syncthreads();
   if (threadIdx.x < 64 && e < plane) {
     const float s = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
-    const int c = (int)(e % C);
     const long t = e / C;
     const int rs = (int)(t % RS), o = (int)(t / RS);
-    if (c < Cw && o < Ow) {
+    const int c = (int)(e % C) - (G > 1 ? (o / (O / G)) * Cw : 0);   // channel within filter o's group
+    if (c >= 0 && c < Cw && o < Ow) {
       const long i = ((long)o * Cw + c) * RS + rs;
       dw[i] = accumulate ? dw[i] + s : s;
     }
@@ -1244,6 +1246,7 @@ struct PackEntry {
   bf16* wr;
   int O, Cw, C, RS;
   int O8;            // image rows: O..O8 are zero filters (the output-channel pad of odd widths)
+  int G;             // groups > 1: block-diagonal image of a grouped conv (filter o reads channels of its group)
   int row0;          // first workgroup (row) of this entry in the launch
 };
 constexpr int MAX_PACK = 64;   // 64 x 40 B of kernel arguments
@@ -1277,9 +1280,10 @@ __global__ __launch_bounds__(256) void conv_pack_multi_kernel(PackTable t) {
   __syncthreads();
   bf16* dst = p.wr + (long)o * p.RS * p.C;
   const int n_out = p.RS * p.C;
+  const int cg0 = p.G > 1 ? (o / (p.O / p.G)) * p.Cw : 0;   // first input channel of filter o's group
   for (int i = threadIdx.x; i < n_out; i += 256) {
-    const int rs = i / p.C, c = i - rs * p.C;
-    dst[i] = c < p.Cw ? (bf16)row[c * p.RS + rs] : (bf16)0.f;
+    const int rs = i / p.C, c = i - rs * p.C - cg0;
+    dst[i] = c >= 0 && c < p.Cw ? (bf16)row[c * p.RS + rs] : (bf16)0.f;
   }
 }
 
@@ -1842,10 +1846,15 @@ long conv_wgrad_ws_floats(const ConvShape& s) {
 
 // dW[O][Cw][R][S] (fp32, PyTorch layout) = (or +=) X^T dY.  ``ws`` holds
 // ws_floats floats; splits <= 0 picks automatically within that capacity.
-// dw: [Ow][Cw][R][S] (Ow <= 0: O) -- the first Ow filters of an O-padded conv land in the unpadded gradient
+// dw: [Ow][Cw][R][S] (Ow <= 0: O) -- the first Ow filters of an O-padded conv land in the unpadded gradient.
+// G > 1: a grouped conv run densely with a block-diagonal weight image; filter o keeps only its group's Cw
+// channels of the dense gradient.
 void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const bf16* dy, float* dw, float* ws,
-                       long ws_floats, int splits, int accumulate, int Ow) {
+                       long ws_floats, int splits, int accumulate, int Ow, int G) {
   if (Ow <= 0 || Ow > s.O) Ow = s.O;
+  if (G < 1) G = 1;
+  if (G > 1 && (s.O % G || s.C < G * s.Cw || Ow != s.O))
+    throw std::invalid_argument("conv_wgrad: grouped gradient needs O % G == 0, C >= G * Cw, no O pad");
   const ConvGeom g = wgrad_geom(s);
   const long plane = (long)g.M * g.NC;
   if (ws_floats < plane) throw std::invalid_argument("conv_wgrad: workspace smaller than one O x RSC plane");
@@ -1869,10 +1878,10 @@ void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const 
   const long blocks = (long)s.O * ((s.C + 63) / 64);
   if (blocks >= 1024) {      // enough (o, channel-block) tiles: coalesced tile writes
     hipLaunchKernelGGL(conv_wgrad_reduce, dim3((unsigned)blocks), dim3(256), 4 * s.R * s.S * 65 * sizeof(float), st,
-                       ws, splits, s.O, s.C, s.Cw, s.R * s.S, dw, accumulate, Ow);
+                       ws, splits, s.O, s.C, s.Cw, s.R * s.S, dw, accumulate, Ow, G);
   } else {
     hipLaunchKernelGGL(conv_wgrad_reduce_cols, dim3((unsigned)((plane + 63) / 64)), dim3(256), 0, st, ws, splits, s.O,
-                       s.C, s.Cw, s.R * s.S, dw, accumulate, Ow);
+                       s.C, s.Cw, s.R * s.S, dw, accumulate, Ow, G);
   }
 }
 
@@ -1881,6 +1890,7 @@ struct PackItem {
   bf16* wr;
   int O, Cw, C, RS;
   int O8;            // <= 0: O (no zero filters)
+  int G;             // <= 1: dense; > 1: block-diagonal image of a grouped conv (C = G * Cw channels)
 };
 
 // All dense-conv weight images of a network from their fp32 masters, <= MAX_PACK per launch.
@@ -1892,9 +1902,11 @@ void launch_conv_pack_multi(hipStream_t st, const PackItem* items, int n) {
     for (int k = 0; k < t.n; ++k) {
       const PackItem& it = items[b + k];
       if (it.C % 8 || it.C < it.Cw) throw std::invalid_argument("conv_pack_multi: bad channel padding");
+      if (it.G > 1 && (it.O % it.G || it.C < it.G * it.Cw || (it.O8 > it.O)))
+        throw std::invalid_argument("conv_pack_multi: grouped image needs O % G == 0, C >= G * Cw, no O pad");
       if ((long)it.Cw * it.RS > PACK_ROW_MAX) throw std::invalid_argument("conv_pack_multi: row too long");
       const int o8 = it.O8 > it.O ? it.O8 : it.O;
-      t.e[k] = PackEntry{it.w, it.wr, it.O, it.Cw, it.C, it.RS, o8, rows};
+      t.e[k] = PackEntry{it.w, it.wr, it.O, it.Cw, it.C, it.RS, o8, it.G > 1 ? it.G : 1, rows};
       rows += o8;
       max_row = std::max(max_row, it.Cw * it.RS);
     }
@@ -1945,8 +1957,8 @@ void launch_dgrad_pack_multi(hipStream_t st, const DPackItem* items, int n) {
 }
 
 
-void launch_conv_pack(hipStream_t st, const float* w, bf16* wrsc, int O, int Cw, int C, int RS, int O8) {
-  const PackItem it{w, wrsc, O, Cw, C, RS, O8};
+void launch_conv_pack(hipStream_t st, const float* w, bf16* wrsc, int O, int Cw, int C, int RS, int O8, int G) {
+  const PackItem it{w, wrsc, O, Cw, C, RS, O8, G};
   launch_conv_pack_multi(st, &it, 1);
 }
 

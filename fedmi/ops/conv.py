@@ -66,28 +66,30 @@ def _check(t: torch.Tensor, dtype, name: str):
 
 
 def pack_weight(w: torch.Tensor, c_pad: Optional[int] = None, out: Optional[torch.Tensor] = None,
-                o_pad: Optional[int] = None) -> torch.Tensor:
+                o_pad: Optional[int] = None, groups: int = 1) -> torch.Tensor:
     """fp32 [O, Cw, R, S] -> bf16 [O8, R, S, C] (C = Cw rounded up to 8, zero pad; ``o_pad`` = O8 >= O: zero
-    filters O..O8 written by the same launch)."""
+    filters O..O8 written by the same launch).  ``groups`` > 1: the block-diagonal dense image of a grouped conv
+    (C = groups * Cw channels, filter o holds its group's Cw channels and zeros elsewhere)."""
     O, Cw, R, S = w.shape
-    C = c_pad or pad8(Cw)
+    C = c_pad or pad8(Cw * groups)
     O8 = max(int(o_pad or O), O)
     if out is None:
         out = torch.empty(O8, R, S, C, dtype=torch.bfloat16, device=w.device)
     _check(w, torch.float32, "pack_weight.w")
     if tuple(out.shape) != (O8, R, S, C) or not out.is_contiguous():
         raise ValueError(f"pack_weight: image {tuple(out.shape)} vs {(O8, R, S, C)}")
-    native.require().conv_pack(native.stream_handle(w.device), w.data_ptr(), out.data_ptr(), O, Cw, C, R * S, O8)
+    native.require().conv_pack(native.stream_handle(w.device), w.data_ptr(), out.data_ptr(), O, Cw, C, R * S, O8,
+                               int(groups))
     return out
 
 
 def pack_weights(items) -> None:
-    """Pack many ``(w fp32 [O,Cw,R,S], out bf16 [O8,R,S,C])`` pairs in one multi-tensor launch (``O8 > O``: zero
-    filters O..O8)."""
-    items = list(items)
+    """Pack many ``(w fp32 [O,Cw,R,S], out bf16 [O8,R,S,C][, groups])`` items in one multi-tensor launch (``O8 >
+    O``: zero filters O..O8; groups > 1: block-diagonal image, see :func:`pack_weight`)."""
+    items = [tuple(it) if len(it) == 3 else (it[0], it[1], 1) for it in items]
     if not items:
         return
-    for w, out in items:
+    for w, out, _ in items:
         _check(w, torch.float32, "pack_weights.w")
         _check(out, torch.bfloat16, "pack_weights.out")
         if out.shape[0] < w.shape[0] or tuple(out.shape[1:3]) != tuple(w.shape[2:]) or out.shape[3] < w.shape[1]:
@@ -95,8 +97,8 @@ def pack_weights(items) -> None:
     dev = items[0][0].device
     native.require().conv_pack_multi(
         native.stream_handle(dev),
-        [(w.data_ptr(), o.data_ptr(), w.shape[0], w.shape[1], o.shape[3], w.shape[2] * w.shape[3], o.shape[0])
-         for w, o in items])
+        [(w.data_ptr(), o.data_ptr(), w.shape[0], w.shape[1], o.shape[3], w.shape[2] * w.shape[3], o.shape[0], int(g))
+         for w, o, g in items])
 
 
 def fd_ws_floats(x_shape, O: int, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None) -> int:
@@ -254,9 +256,10 @@ def wgrad_ws_floats(x_shape, O: int, R: int, S: int, stride: int, pad: int, Cw: 
 
 def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None,
                  out: Optional[torch.Tensor] = None, accumulate: bool = False, splits: int = 0,
-                 ws: Optional[torch.Tensor] = None, Ow: Optional[int] = None) -> torch.Tensor:
+                 ws: Optional[torch.Tensor] = None, Ow: Optional[int] = None, groups: int = 1) -> torch.Tensor:
     """dW fp32 [O, Cw, R, S] (PyTorch layout).  ``accumulate`` adds into ``out`` instead of overwriting.
     ``Ow`` < O: dy carries zero-padded filters; only the first Ow land in ``out`` ([Ow, Cw, R, S]).
+    ``groups`` > 1: a grouped conv run densely (block-diagonal image): filter o keeps its group's Cw channels.
 
     Split-K partials go to a workspace (plain stores) and one reduce launch sums
     them into ``out`` — no fp32 atomics on the gradient.
@@ -280,7 +283,7 @@ def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int,
         need = max(nat.conv_wgrad_ws_floats(shp), splits * O * R * S * shp[3])
         ws = wgrad_workspace(x.device, need)
     nat.conv_wgrad(native.stream_handle(x.device), shp, x.data_ptr(), dy.data_ptr(), out.data_ptr(), ws.data_ptr(),
-                   ws.numel(), splits, int(accumulate), Ow)
+                   ws.numel(), splits, int(accumulate), Ow, int(groups))
     return out
 
 

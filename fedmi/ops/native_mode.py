@@ -1058,6 +1058,11 @@ def _conv_kind(C, O, groups, k, stride, pad, dil):
         # one MFMA implicit GEMM per group; channel counts off the 8-grid (stems, DenseNet growth widths,
         # ShuffleNet g2/g3 widths) are zero-padded
         return "mfma"
+    if C % 8 == 0 and O % 8 == 0 and C // groups <= 32 and C <= 1024 and O <= 1024:
+        # many narrow groups (DPN cardinality 32, ResNeXt 32x4d, RegNet group width 8): one dense MFMA conv over a
+        # block-diagonal weight image does groups-times the FLOPs but runs on the matrix cores -- the direct VALU
+        # kernel (gconv) spent 8.9 of DPN26's 17 ms per step on its 3- / 6- / 12-channel groups
+        return "gdense"
     return "gconv"
 
 
@@ -1124,7 +1129,7 @@ def _pad_o(w32: torch.Tensor, o8: int) -> torch.Tensor:
     return out
 
 
-def _packed(w32, O8: int, C8: int, st: int, pd: int, need_wd: bool = False):
+def _packed(w32, O8: int, C8: int, st: int, pd: int, need_wd: bool = False, groups: int = 1):
     """bf16 [O8, R, S, C8] conv image of fp32 ``w32`` (and with ``need_wd`` its DGRAD image), packed once per
     NativeMode block: the forward packs, the backward of the same step reuses (the weights only change at
     the SGD, outside the block).  Weights living in the trainer's flat parameter storage
@@ -1132,7 +1137,7 @@ def _packed(w32, O8: int, C8: int, st: int, pd: int, need_wd: bool = False):
     launch at its first conv (and all DGRAD images at its first conv backward) instead of one launch each."""
     mode = NativeMode.current
     cache = mode._wcache if mode is not None else None
-    key = (w32.data_ptr(), tuple(w32.shape), tuple(w32.stride()), O8, C8, st, pd)
+    key = (w32.data_ptr(), tuple(w32.shape), tuple(w32.stride()), O8, C8, st, pd, groups)
     if mode is not None:
         if not mode._prepacked:
             mode._prepacked = True
@@ -1151,8 +1156,8 @@ def _packed(w32, O8: int, C8: int, st: int, pd: int, need_wd: bool = False):
             cache[key] = (w32, ent)          # holds w32: the pointer key stays valid for the block
     else:
         ent = ent[1]
-    if "wp" not in ent:
-        ent["wp"] = CV.pack_weight(w32.contiguous(), c_pad=C8, o_pad=O8)   # zero filters O..O8: same launch
+    if "wp" not in ent:   # zero filters O..O8 (and a grouped conv's off-diagonal blocks): same launch
+        ent["wp"] = CV.pack_weight(w32.contiguous(), c_pad=C8, o_pad=O8, groups=groups)
     if need_wd and "wd" not in ent:
         ent["wd"] = _wd_image(w32, O8, C8, st, pd)
         CV.dgrad_pack_weights([(_pad_o(w32, O8), ent["wd"], st, pd, C8)])
@@ -1164,30 +1169,33 @@ def _wd_image(w32, O8, C8, st, pd):
                        device=w32.device)
 
 
-def _dense_fwd(xh, w32, st, pd, out=None):
-    """One group: y [N,P,Q,Og] = conv(xh [N,H,W,Cg] NHWC bf16 (a view is fine), w32 [Og,Cg,R,S])."""
+def _dense_fwd(xh, w32, st, pd, out=None, groups: int = 1):
+    """One group: y [N,P,Q,Og] = conv(xh [N,H,W,Cg] NHWC bf16 (a view is fine), w32 [Og,Cg,R,S]).  ``groups`` > 1:
+    the whole grouped conv as one dense MFMA conv over a block-diagonal weight image (xh holds all channels)."""
     Og, Cg, R, S = w32.shape
-    C8, O8 = CV.pad8(Cg), CV.pad8(Og)
+    C8, O8 = CV.pad8(Cg * groups), CV.pad8(Og)
     xp = _pad_c(xh, C8, cache=True)
-    wp, _ = _packed(w32, O8, C8, st, pd)
+    wp, _ = _packed(w32, O8, C8, st, pd, groups=groups)
     y = CV.conv2d_fwd(xp, wp, st, pd, ws=_ws(xh.device, CV.fd_ws_floats(xp.shape, O8, R, S, st, pd)))
     return _unpad_c(y, Og, out)
 
 
-def _dense_bwd(xh, gy, w32, st, pd, need_dx, need_dw, dx_out=None, dw_out=None):
-    """One group's data / weight gradients; dx written into ``dx_out`` (NHWC view) when given."""
+def _dense_bwd(xh, gy, w32, st, pd, need_dx, need_dw, dx_out=None, dw_out=None, groups: int = 1):
+    """One group's data / weight gradients; dx written into ``dx_out`` (NHWC view) when given.  ``groups`` > 1:
+    the densified grouped conv of :func:`_dense_fwd` (the DGRAD reads the block-diagonal image; the WGRAD
+    reduction keeps each filter's own group of the dense gradient)."""
     Og, Cg, R, S = w32.shape
     N, H, W = xh.shape[:3]
-    C8, O8 = CV.pad8(Cg), CV.pad8(Og)
+    C8, O8 = CV.pad8(Cg * groups), CV.pad8(Og)
     gyp = _pad_c(gy, O8)
     dx = dw = None
     if need_dx:
-        wp, wd = _packed(w32, O8, C8, st, pd, need_wd=CV.dgrad_eligible(O8))
+        wp, wd = _packed(w32, O8, C8, st, pd, need_wd=groups == 1 and CV.dgrad_eligible(O8), groups=groups)
         xs = (N, H, W, C8)
         d = CV.conv2d_dgrad(gyp, wp, xs, st, pd, wd=wd, ws=_ws(xh.device, CV.fd_ws_floats(xs, O8, R, S, st, pd)))
-        dx = _unpad_c(d, Cg, dx_out)
+        dx = _unpad_c(d, Cg * groups, dx_out)
     if need_dw:   # the padded filters O..O8 never leave the reduction (Ow): no slice copy
-        dw = CV.conv2d_wgrad(_pad_c(xh, C8, cache=True), gyp, R, S, st, pd, Cw=Cg, Ow=Og,
+        dw = CV.conv2d_wgrad(_pad_c(xh, C8, cache=True), gyp, R, S, st, pd, Cw=Cg, Ow=Og, groups=groups,
                              out=dw_out if dw_out is not None and dw_out.is_contiguous() else None)
         if dw_out is not None and dw.data_ptr() != dw_out.data_ptr():
             dw = ew(dw_out, [dw], EW_COPY)
@@ -1240,10 +1248,12 @@ def _conv(func, input, weight, bias, stride, padding, dilation, transposed, outp
     kind = _conv_kind(C, O, groups, k, st, pd, dl)
     dev = input.device
     w32 = weight if weight.dtype == torch.float32 else ew(torch.empty(weight.shape, device=dev), [weight], EW_COPY)
-    if kind in ("mfma", "dw"):
-        xh = _nhwc(_cl_bf16(input, rows=kind == "mfma"))
+    if kind in ("mfma", "dw", "gdense"):
+        xh = _nhwc(_cl_bf16(input, rows=kind != "dw"))
         if kind == "dw":
             y = CV.dwconv_fwd(xh, w32.contiguous(), st[0], pd[0])
+        elif kind == "gdense":
+            y = _dense_fwd(xh, w32, st[0], pd[0], groups=groups)
         elif groups == 1:
             y = _dense_fwd(xh, w32, st[0], pd[0])
         else:
@@ -1281,10 +1291,14 @@ def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dil
     w32 = weight if weight.dtype == torch.float32 else ew(torch.empty(weight.shape, device=dev), [weight], EW_COPY)
     gi = gw = gb = None
     gw_slot = _param_grad(weight) if output_mask[1] else None
-    if kind in ("mfma", "dw"):
-        xh = _nhwc(_cl_bf16(input, rows=kind == "mfma"))
-        gy = _nhwc(_cl_bf16(grad_output, rows=kind == "mfma"))
-        if kind == "dw":
+    if kind in ("mfma", "dw", "gdense"):
+        xh = _nhwc(_cl_bf16(input, rows=kind != "dw"))
+        gy = _nhwc(_cl_bf16(grad_output, rows=kind != "dw"))
+        if kind == "gdense":
+            dx, gw = _dense_bwd(xh, gy, w32, st[0], pd[0], output_mask[0], output_mask[1], dw_out=gw_slot,
+                                groups=groups)
+            gi = _nchw(dx) if dx is not None else None
+        elif kind == "dw":
             if output_mask[0]:
                 gi = _nchw(CV.dwconv_dgrad(gy, w32.contiguous(), xh.shape, st[0], pd[0]))
             if output_mask[1]:
@@ -1424,16 +1438,16 @@ class NativeMode(TorchDispatchMode):
         plan = self._wd_plan if wd else self._pack_plan
         items = []
         for key, w32 in plan.items():
-            O8, C8, st, pd = key[3:]
+            O8, C8, st, pd, groups = key[3:]
             ent = self._wcache.setdefault(key, (w32, {}))[1]
             if wd:
-                if "wd" not in ent and w32.shape[0] == O8 and w32.is_contiguous():
+                if "wd" not in ent and w32.shape[0] == O8 and w32.is_contiguous() and groups == 1:
                     ent["wd"] = _wd_image(w32, O8, C8, st, pd)
                     items.append((w32, ent["wd"], st, pd, C8))
             elif "wp" not in ent and w32.is_contiguous():
                 O, _, R, S = w32.shape
                 ent["wp"] = torch.empty(O8, R, S, C8, dtype=torch.bfloat16, device=w32.device)
-                items.append((w32, ent["wp"]))
+                items.append((w32, ent["wp"], groups))
         if items:
             (CV.dgrad_pack_weights if wd else CV.pack_weights)(items)
             self.packs["wd" if wd else "wp"] += len(items)
