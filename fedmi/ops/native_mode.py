@@ -306,6 +306,14 @@ def _add(func, self, other, alpha=1):
             mode._defer(pend.out, pend.materialize)
             mode.fused["bn+add"] += 1
             return out
+    pair = _sb_pair(mode, (self, other), {"alpha": alpha}) if func is aten.add.Tensor else None
+    if pair is not None:            # slice_backward(g1, [0, a)) + slice_backward(g2, [a, n)): two copies
+        lo, hi = pair
+        out = torch.empty_like(lo.out)
+        ew(out.narrow(lo.dim, lo.start, lo.end - lo.start), [lo.grad], EW_COPY)
+        ew(out.narrow(hi.dim, hi.start, hi.end - hi.start), [hi.grad], EW_COPY)
+        mode.fused["slice_bwd+add"] += 1
+        return out
     if func is aten.add.Tensor and mode is not None and mode._pend_bnb is not None:
         o = _bnb_add_partner(mode._pend_bnb, (self, other), {"alpha": alpha})
         if o is not None:           # BN-backward gradient + the other incoming gradient: one pass
@@ -623,6 +631,40 @@ def _cat(func, tensors, dim=0):
     return out
 
 
+class _PendingSliceBwd:
+    """slice_backward not computed yet (zeros + the gradient in its slice): autograd's sum of two of them that
+    tile the sliced dim (DPN's dual path: y[:, :d] and y[:, d:]) becomes two copies into one tensor -- no zero
+    fills, no add pass; any other read materialises it."""
+    __slots__ = ("out", "grad", "dim", "start", "end", "done")
+
+    def __init__(self, out, grad, dim, start, end):
+        self.out, self.grad, self.dim, self.start, self.end = out, grad, dim, start, end
+        self.done = False
+
+    def materialize(self):
+        self.done = True
+        fill_(self.out, 0.0)
+        ew(self.out.narrow(self.dim, self.start, self.end - self.start), [self.grad], EW_COPY)
+
+
+def _sb_pair(mode, args, kwargs=None):
+    """The two pending slice_backwards an ``add(a, b)`` sums when their slices tile the dim exactly, else None."""
+    if mode is None or not mode._pend_sb or len(args) != 2 or (kwargs and kwargs.get("alpha", 1) != 1):
+        return None
+    a, b = args
+    if not (isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor)) or not (a.is_cuda and b.is_cuda):
+        return None
+    pa = mode._pend_sb.get(a.untyped_storage().data_ptr())
+    pb = mode._pend_sb.get(b.untyped_storage().data_ptr())
+    if (pa is None or pb is None or pa is pb or pa.done or pb.done or not (_same(a, pa.out) and _same(b, pb.out))
+            or pa.dim != pb.dim):
+        return None
+    lo, hi = (pa, pb) if pa.start <= pb.start else (pb, pa)
+    if lo.start != 0 or lo.end != hi.start or hi.end != pa.out.shape[pa.dim]:
+        return None
+    return lo, hi
+
+
 @impl(aten.slice_backward.default)
 def _slice_bwd(func, grad_output, input_sizes, dim, start, end, step):
     out = _alloc_like_meta(func, (grad_output, input_sizes, dim, start, end, step), {}, grad_output.device)
@@ -630,6 +672,15 @@ def _slice_bwd(func, grad_output, input_sizes, dim, start, end, step):
         # the meta function allocates NCHW zeros: keep a channels-last gradient channels-last (DPN's dual-path
         # slices would otherwise turn every upstream BN backward and conv gradient into layout transposes)
         out = torch.empty(out.shape, dtype=out.dtype, device=out.device, memory_format=torch.channels_last)
+    d = dim % out.dim()
+    lo = max(0, min(start, out.shape[d])) if start is not None else 0
+    hi = max(lo, min(end, out.shape[d])) if end is not None else out.shape[d]
+    mode = NativeMode.current
+    if mode is not None and mode.fuse and step == 1 and hi - lo == grad_output.shape[d]:
+        pend = _PendingSliceBwd(out, grad_output, d, lo, hi)
+        mode._pend_sb[out.untyped_storage().data_ptr()] = pend
+        mode._defer(out, pend.materialize)
+        return out
     fill_(out, 0.0)
     ew(aten.slice.Tensor(out, dim, start, end, step), [grad_output], EW_COPY)
     return out
@@ -1419,6 +1470,7 @@ class NativeMode(TorchDispatchMode):
         self._pend_ctr: Optional[torch.Tensor] = None   # a BN counter increment waiting for its BN forward
         self._pend_bnb: Optional[_PendingBNB] = None    # a BN input gradient waiting for its accumulation add
         self._pend_mul: Optional[_PendingMul] = None    # a product waiting for the reduction that sums it
+        self._pend_sb = {}              # storage ptr -> _PendingSliceBwd (deferred; see _sb_pair)
         self.stable_storage = 0         # data_ptr of the trainer's flat parameter storage (set by the trainer)
         self._pack_plan, self._wd_plan = {}, {}   # weight-image keys of stable weights -> fp32 master (kept)
         self.grad_flat: Optional[torch.Tensor] = None   # the trainer's flat gradient buffer (see _param_grad)
@@ -1495,6 +1547,8 @@ class NativeMode(TorchDispatchMode):
         if self._pend_thr is not None and not self._fuses_thr(args):
             pend, self._pend_thr = self._pend_thr, None
             pend.materialize()
+        if self._dead and self._pend_sb and self._func is aten.add.Tensor and _sb_pair(self, args, kwargs):
+            return                          # the add reads both pending slice gradients' sources itself
         if self._dead:
             for t in _iter_tensors(args, kwargs):
                 fn = self._dead.pop(t.untyped_storage().data_ptr(), None) if t.is_cuda else None
@@ -1531,6 +1585,7 @@ class NativeMode(TorchDispatchMode):
         self._prev = NativeMode.current
         NativeMode.current = self
         self._wcache = {}
+        self._pend_sb = {}
         self._prepacked = self._prepacked_wd = False
         self._catbufs, self._cat_src = {}, {}
         self._grad_taken = set()
@@ -1543,6 +1598,7 @@ class NativeMode(TorchDispatchMode):
             self._flush()
         finally:
             self._dead.clear()
+            self._pend_sb = {}
             self._wcache = {}
             self._catbufs, self._cat_src = {}, {}
         NativeMode.current = self._prev

@@ -293,16 +293,19 @@ def test_family_step_native_only(gpu_device, name):
     assert abs(losses["native"] - losses["fp32"]) < 0.05 * losses["fp32"] + 0.02, losses
 
 
-@pytest.mark.parametrize("name", ["densenet_cifar", "SENet18", "DPN26", "ResNeXt29_2x64d", "EfficientNetB0",
-                                  "RegNetY_400MF"])
-def test_family_trains_like_fp32(gpu_device, name):
+# RegNetY_400MF's first epoch at lr 0.02 is chaotic on BOTH engines (it blows up to a loss of 7-15 and the
+# fp32 seeds alone end between 48 and 100 % accuracy, profiles/r3_zoo/README.md "Learning parity"): the
+# first-epoch comparison is meaningless there, so it is compared at lr 0.005, where both engines are stable
+@pytest.mark.parametrize("name,lr", [("densenet_cifar", 0.02), ("SENet18", 0.02), ("DPN26", 0.02),
+                                     ("ResNeXt29_2x64d", 0.02), ("EfficientNetB0", 0.02), ("RegNetY_400MF", 0.005)])
+def test_family_trains_like_fp32(gpu_device, name, lr):
     """Three short epochs, graph-replayed: the trajectory tracks the fp32 engine (round 1's hybrid
     EfficientNet / RegNetY went NaN under replay)."""
     from fedmi.engine import build_trainer
     from fedmi.engine.torch_engine import TorchTrainer
 
     data = make_dataset("synthetic-cifar10-easy", device=gpu_device, n_train=1280, n_test=500, seed=0)
-    cfg = TrainerConfig(batch_size=128, lr=0.02, seed=7)
+    cfg = TrainerConfig(batch_size=128, lr=lr, seed=7)
     init = build_model(name).state_dict()
     res = {}
     for kind in ("native", "fp32"):
@@ -353,7 +356,8 @@ def test_graph_replay_matches_eager(gpu_device):
     assert lg == le, out
 
 
-@pytest.mark.parametrize("name", ["densenet_cifar", "ResNeXt29_2x64d", "DLA"])
+# DPN26: paired slice gradients summed as copies; SENet18: SE-gate multiply + sum as one dot reduction
+@pytest.mark.parametrize("name", ["densenet_cifar", "ResNeXt29_2x64d", "DLA", "DPN26", "SENet18"])
 def test_bn_relu_fusion_is_exact(gpu_device, name):
     """BN -> [residual add ->] ReLU (one pass) and ReLU-backward -> BN-backward (masked sums and apply)
     fusion: relu(bf16(BN(x))) == bf16(relu(BN(x))), the fused add rounds the BN output to bf16 where the
