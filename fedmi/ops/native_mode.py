@@ -1105,6 +1105,10 @@ def _conv_kind(C, O, groups, k, stride, pad, dil):
         return "gconv"
     if groups == C == O and C % 8 == 0 and C <= 2048 and k[0] in (3, 5, 7) and C * k[0] * k[0] * 4 <= 128 * 1024:
         return "dw"
+    if groups == C == O and C % 4 == 0 and C <= 2040 and k[0] in (3, 5, 7) and CV.pad8(C) * k[0] * k[0] * 4 <= 128 * 1024:
+        # depthwise on an off-grid width (PNASNetA's 44 / 88 / 176 channels): the depthwise kernels on channels
+        # zero-padded to 8 (input, weights, output gradient), results read back as row-strided views
+        return "dwpad"
     if groups <= 8:
         # one MFMA implicit GEMM per group; channel counts off the 8-grid (stems, DenseNet growth widths,
         # ShuffleNet g2/g3 widths) are zero-padded
@@ -1253,6 +1257,18 @@ def _dense_bwd(xh, gy, w32, st, pd, need_dx, need_dw, dx_out=None, dw_out=None, 
     return dx, dw
 
 
+def _dw_padded_weight(w32: torch.Tensor, C8: int) -> torch.Tensor:
+    """fp32 [C8, 1, R, R] depthwise weights with zero channels C..C8, made once per NativeMode block."""
+    mode = NativeMode.current
+    key = ("dwpad", w32.data_ptr(), tuple(w32.shape), C8)
+    if mode is not None and key in mode._wcache:
+        return mode._wcache[key][1]
+    wp = _pad_o(w32.contiguous(), C8)
+    if mode is not None:
+        mode._wcache[key] = (w32, wp)
+    return wp
+
+
 def _nchw(t_nhwc: torch.Tensor) -> torch.Tensor:
     return t_nhwc.permute(0, 3, 1, 2)
 
@@ -1299,9 +1315,12 @@ def _conv(func, input, weight, bias, stride, padding, dilation, transposed, outp
     kind = _conv_kind(C, O, groups, k, st, pd, dl)
     dev = input.device
     w32 = weight if weight.dtype == torch.float32 else ew(torch.empty(weight.shape, device=dev), [weight], EW_COPY)
-    if kind in ("mfma", "dw", "gdense"):
+    if kind in ("mfma", "dw", "gdense", "dwpad"):
         xh = _nhwc(_cl_bf16(input, rows=kind != "dw"))
-        if kind == "dw":
+        if kind == "dwpad":
+            C8 = CV.pad8(C)
+            y = CV.dwconv_fwd(_pad_c(xh, C8, cache=True), _dw_padded_weight(w32, C8), st[0], pd[0])[..., :C]
+        elif kind == "dw":
             y = CV.dwconv_fwd(xh, w32.contiguous(), st[0], pd[0])
         elif kind == "gdense":
             y = _dense_fwd(xh, w32, st[0], pd[0], groups=groups)
@@ -1342,10 +1361,18 @@ def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dil
     w32 = weight if weight.dtype == torch.float32 else ew(torch.empty(weight.shape, device=dev), [weight], EW_COPY)
     gi = gw = gb = None
     gw_slot = _param_grad(weight) if output_mask[1] else None
-    if kind in ("mfma", "dw", "gdense"):
+    if kind in ("mfma", "dw", "gdense", "dwpad"):
         xh = _nhwc(_cl_bf16(input, rows=kind != "dw"))
         gy = _nhwc(_cl_bf16(grad_output, rows=kind != "dw"))
-        if kind == "gdense":
+        if kind == "dwpad":
+            C8 = CV.pad8(C)
+            gyp = _pad_c(gy, C8)
+            if output_mask[0]:
+                gi = _nchw(CV.dwconv_dgrad(gyp, _dw_padded_weight(w32, C8), (N, H, W, C8), st[0], pd[0])[..., :C])
+            if output_mask[1]:
+                gw8 = CV.dwconv_wgrad(_pad_c(xh, C8, cache=True), gyp, k[0], st[0], pd[0])
+                gw = ew(gw_slot, [gw8[:C]], EW_COPY) if gw_slot is not None else gw8[:C]
+        elif kind == "gdense":
             dx, gw = _dense_bwd(xh, gy, w32, st[0], pd[0], output_mask[0], output_mask[1], dw_out=gw_slot,
                                 groups=groups)
             gi = _nchw(dx) if dx is not None else None

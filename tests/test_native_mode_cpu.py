@@ -78,6 +78,7 @@ def test_conv_kind_routing():
     assert nm._conv_kind(128, 128, 32, k3, s1, p1, d1) == "gdense"      # many narrow groups: block-diagonal MFMA
     assert nm._conv_kind(2048, 2048, 32, k3, s1, p1, d1) == "gconv"     # wide groups / channels: direct kernel
     assert nm._conv_kind(60, 60, 12, k3, s1, p1, d1) == "gconv"         # channels off the 8-grid
+    assert nm._conv_kind(44, 44, 44, (7, 7), s1, (3, 3), d1) == "dwpad"  # PNASNetA: depthwise on padded channels
     assert nm._conv_kind(60, 60, 3, (1, 1), s1, (0, 0), d1) == "mfma"   # ShuffleNet g3 widths, padded
     assert nm._conv_kind(96, 96, 32, k3, s1, p1, d1) == "gdense"        # DPN cardinality 32
     assert nm._conv_kind(64, 64, 1, k3, (3, 3), p1, d1) == "gconv"      # stride 3

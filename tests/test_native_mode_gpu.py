@@ -83,7 +83,8 @@ CONVS = [(8, 16, 24, 48, 1, 1, 0, 1, False), (8, 16, 48, 16, 3, 1, 1, 1, False),
          (4, 16, 64, 64, 3, 1, 1, 4, False), (4, 16, 200, 200, 1, 1, 0, 2, False),    # 4 x 16 groups, ShuffleNet
          (4, 8, 96, 96, 3, 1, 1, 32, False), (4, 8, 192, 192, 3, 2, 1, 32, False),     # DPN: 3- / 6- / 12-channel
          (2, 8, 384, 384, 3, 1, 1, 32, False),                                          # groups: block-diagonal MFMA
-         (4, 8, 60, 60, 3, 1, 1, 12, False)]                                            # off-grid widths: direct gconv
+         (4, 8, 60, 60, 3, 1, 1, 12, False),                                            # off-grid widths: direct gconv
+         (4, 16, 44, 44, 7, 1, 3, 44, False), (4, 16, 44, 44, 3, 2, 1, 44, False)]     # PNASNetA depthwise, padded
 
 
 @pytest.mark.parametrize("shape", CONVS, ids=[str(s) for s in CONVS])
