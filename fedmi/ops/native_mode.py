@@ -132,7 +132,7 @@ def ew(out: torch.Tensor, ins, op: int, s0: float = 0.0, s1: float = 0.0, seed: 
     if vmask >= 0:
         nshape = nshape[:-1] + [nshape[-1] // vw]
         nstr = [st[:-1] + [st[-1] * vw] for st in nstr]
-    if NativeMode.current is not None:   # diagnostics: passes per op code, and which miss the vector launch
+    if NativeMode.current is not None and NativeMode.current.diag:   # passes per op code, and which miss the vector launch
         NativeMode.current.ew_ops[(NativeMode.current._func_name(), op)] += 1
         if vmask < 0:
             NativeMode.current.scalar_ew[(op, tuple(out.shape), tuple(out.stride()),
@@ -1493,6 +1493,7 @@ class NativeMode(TorchDispatchMode):
         self.packs = collections.Counter()   # weight images packed by the batched per-block launches
         self.scalar_ew = collections.Counter()   # (op, shape, strides) of elementwise passes on the scalar kernel
         self.ew_ops = collections.Counter()      # (aten op, elementwise op code) -> passes
+        self.diag = False                        # collect scalar_ew / ew_ops (tools/prof_native_mode.py)
         self._wcache = {}               # packed conv weights of the current block (see _packed)
         self._pend_ctr: Optional[torch.Tensor] = None   # a BN counter increment waiting for its BN forward
         self._pend_bnb: Optional[_PendingBNB] = None    # a BN input gradient waiting for its accumulation add

@@ -18,6 +18,7 @@ steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 dev = torch.device("cuda", 0)
 data = make_dataset("synthetic-cifar10", device=dev, n_train=128 * 4, n_test=128, seed=0)
 tr = TorchTrainer(name, data, dev, TrainerConfig(seed=1, augment=False), hybrid=True)
+tr.mode.diag = True
 tr.model.train()
 for i in range(steps):
     tr.train_step(128 * (i % 4), 128)
