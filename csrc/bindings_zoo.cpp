@@ -25,6 +25,7 @@ struct ZTensor {
 void launch_ew(hipStream_t, const ZTensor&, const ZTensor*, int, int, float, float, uint32_t, const int*, int, int);
 void launch_ctr_bump(hipStream_t, int*);
 long long reduce_rows_ws_floats(long long, int);
+int rows_tune(int);
 void launch_pad_rows(hipStream_t, const bf16*, long long, int, bf16*, int, long long);
 void launch_reduce_rows(hipStream_t, const void*, int, long long, const void*, int, long long, const float*, int,
                         long long, int, float*, long long, float*, float*, void*, int, float);
@@ -102,6 +103,7 @@ void fedmi_bind_zoo(py::module_& m) {
      py::arg("part"), py::arg("part_floats"), py::arg("out") = 0, py::arg("out_dt") = 0, py::arg("scale") = 1.f);
   m.def("z_reduce_ws_floats", &fedmi::reduce_ws_floats);
   m.def("z_reduce_rows_ws_floats", &fedmi::reduce_rows_ws_floats);
+  m.def("z_rows_tune", &fedmi::rows_tune);   // rows per row lane of the row reductions (benchmark sweeps)
   m.def("z_pad_rows", [](uintptr_t st, uintptr_t src, long long lds, int C, uintptr_t dst, int C8, long long rows) {
     fedmi::launch_pad_rows(S(st), reinterpret_cast<const bf16*>(src), lds, C, reinterpret_cast<bf16*>(dst), C8, rows);
   });

@@ -658,10 +658,12 @@ int rows_tiles(int C) {
   return (VL + vt - 1) / vt;
 }
 
+int g_rows_per_lane = 16;   // rows per row lane (tools/bench_rows.py sweeps it through fedmi::rows_tune)
+
 int rows_slabs(long long M, int C) {
   const int RL = 256 / rows_tile_vecs(C);
   const long long tiles = rows_tiles(C);
-  constexpr long long per_lane = 16;               // rows per row lane
+  const long long per_lane = g_rows_per_lane;
   long long sl = M / ((long long)RL * per_lane);    // >= per_lane rows per row lane
   const long long cap = (2048 + tiles - 1) / tiles;  // ~2048 blocks in flight at most
   if (sl > cap) sl = cap;
@@ -1435,6 +1437,12 @@ void launch_pad_rows(hipStream_t st, const bf16* src, long long lds, int C, bf16
 }
 
 long long reduce_rows_ws_floats(long long M, int C) { return (long long)rows_slabs(M, C) * 2 * C; }
+
+int rows_tune(int per_lane) {
+  const int prev = g_rows_per_lane;
+  if (per_lane > 0) g_rows_per_lane = per_lane;
+  return prev;
+}
 
 // phase 1 (row slabs -> part) + rows_fin_kernel (slab sums -> fin / out / acc)
 static void rows_launch(hipStream_t st, const void* a, int a_dt, long long lda, const void* b, int b_dt, long long ldb,
