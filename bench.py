@@ -321,7 +321,7 @@ def main() -> int:
     # client holds the bit-identical global model -- else the throughput above is not a FedAvg run
     from fedmi.parallel.consistency import check_consistency
 
-    consistency = check_consistency(trainer, transport=transport, device=device)
+    consistency = check_consistency(trainer, transport=transport, device=device, compressor=agg.compressor)
     breakdown = dict(_breakdown(marks, PHASES, t0, t1, args.steps), tail=tail) if args.breakdown else None
 
     tr_stats = trainer.train_stats()

@@ -473,7 +473,9 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
   constexpr int EPI = BM * (BN + 8) + 2 * 3 * 256 * 8;
   __shared__ __attribute__((aligned(16))) bf16 smem[NST * STAGE > EPI ? NST * STAGE : EPI];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // uniform (SGPR) wave index: the LDS-DMA destinations (M0) are scalar, no readfirstlane per piece
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = (g.O + BN - 1) / BN;
   const int tile_n = tile % ntn, tile_m = tile / ntn;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
@@ -508,16 +510,24 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
     b_off[i] = (long)o * g.K + kc * 8;
   }
 
-  auto issue = [&](int t, int stage) {
-    const int k0 = t * 64;
-    const int rs = k0 / g.C, c0 = k0 - rs * g.C;
-    const int r = rs / g.S, sx = rs - r * g.S;
-    const long tap = ((long)r * g.W + sx) * g.C + c0;
+  // tap state of the next K step to issue, advanced incrementally (scalar; no per-step division):
+  // K step t = tap (r, s), channels [c0, c0 + 64)
+  int is_c0, is_s, is_r;
+  {
+    const int k0 = kb * 64;
+    const int rs = k0 / g.C;
+    is_c0 = k0 - rs * g.C;
+    is_r = rs / g.S;
+    is_s = rs - is_r * g.S;
+  }
+  auto issue = [&](int stage) {
+    const long tap = ((long)is_r * g.W + is_s) * g.C + is_c0;
+    const long k0 = ((long)is_r * g.S + is_s) * g.C + is_c0;
     bf16* As = smem + stage * STAGE;
     bf16* Bs = As + BM * 64;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int h = a_h[i] + r, w = a_w[i] + sx;
+      const int h = a_h[i] + is_r, w = a_w[i] + is_s;
       const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
       const void* src = ok ? (const void*)(in + a_off[i] + tap) : (const void*)g_zero16;
       glds16(src, As + (wave * NA + i) * 8 * 64);
@@ -526,6 +536,11 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
     for (int i = 0; i < NB; ++i) {
       const void* src = b_ok[i] ? (const void*)(wt + b_off[i] + k0) : (const void*)g_zero16;
       glds16(src, Bs + (wave * NB + i) * 8 * 64);
+    }
+    is_c0 += 64;
+    if (is_c0 == g.C) {
+      is_c0 = 0;
+      if (++is_s == g.S) { is_s = 0; ++is_r; }
     }
   };
 
@@ -540,7 +555,7 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
   // reading step t-1's stage), refill that stage with step t+AHEAD, then MFMAs on step t.
 #pragma unroll
   for (int a = 0; a < AHEAD; ++a)
-    if (kb + a < ke) issue(kb + a, a);
+    if (kb + a < ke) issue(a);
   for (int t = kb; t < ke; ++t) {
     const int stg = (t - kb) % NST;
     const int later = min(ke - 1 - t, AHEAD - 1);     // issued steps after t still allowed in flight
@@ -556,23 +571,30 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    // refill the stage step t-1 used with step t+AHEAD (every wave is past step t-1's reads once it
-    // passed this barrier)
-    if (t + AHEAD < ke) issue(t + AHEAD, (stg + AHEAD) % NST);
     const bf16* As = smem + stg * STAGE;
     const bf16* Bs = As + BM * 64;
+    // every fragment of the step (both 32-deep halves) requested at once, THEN the refill DMA and the
+    // MFMAs: one LDS latency per step instead of one per half (the compiler otherwise reuses the
+    // fragment registers and waits for lgkmcnt(0) before each MFMA group)
+    bf16x8 af[2][TM], bfr[2][TN];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag_sw(As, wm0 + 16 * i, kk, lane);
+      for (int i = 0; i < TM; ++i) af[kk][i] = frag_sw(As, wm0 + 16 * i, kk, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = frag_sw(Bs, wn0 + 16 * j, kk, lane);
+      for (int j = 0; j < TN; ++j) bfr[kk][j] = frag_sw(Bs, wn0 + 16 * j, kk, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // refill the stage step t-1 used with step t+AHEAD (every wave is past step t-1's reads once it
+    // passed this barrier)
+    if (t + AHEAD < ke) issue((stg + AHEAD) % NST);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-    }
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[kk][i], bfr[kk][j], acc[i][j]);
   }
   __syncthreads();   // every wave done with the stages (no DMA in flight) before LDS reuse
 
@@ -581,17 +603,25 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
   // epilogue, no combine launch -- measured 1.3-2.2x slower at l3 / l4: each last arriver reads 3 x 64 KB of
   // partials serially, profiles/r4_cnn/README.md.)
   if (part != nullptr) {   // split-K partial -> [split][M][O] fp32
+    // staged through LDS (free after the K loop) so every global store is a 16-byte row segment instead of
+    // a guarded 4-byte scatter per accumulator element
+    constexpr int PLD = BN + 4;
+    float* pt = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pt[(wm0 + 16 * i + row_l + e) * PLD + wn0 + 16 * j + col_l] = acc[i][j][e];
+    __syncthreads();
     float* ws = part + (long)split * g.M * g.O;
+    constexpr int C4 = BN / 4;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wn0 + 16 * j + col_l;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = m0 + wm0 + 16 * i + row_l + e;
-          if (m < g.M && col < g.O) ws[(long)m * g.O + col] = acc[i][j][e];
-        }
+    for (int k = 0; k < BM * C4 / 256; ++k) {
+      const int c = tid + k * 256, row = c / C4, c4 = c % C4;
+      const int m = m0 + row, col = n0 + c4 * 4;
+      if (m < g.M && col < g.O)
+        *reinterpret_cast<float4*>(ws + (long)m * g.O + col) = *reinterpret_cast<const float4*>(pt + row * PLD + c4 * 4);
     }
     return;
   }

@@ -49,9 +49,10 @@ void commit(const std::string& tmp, const std::string& path) {
 }  // namespace
 
 CkptWriter::CkptWriter(std::vector<uint8_t> tmpl, std::vector<CkptSegment> segs, std::vector<CkptRecord> recs,
-                       long long epoch_at, std::vector<std::string> paths, bool device, int slots, bool coalesce)
+                       long long epoch_at, std::vector<std::string> paths, bool device, int slots, bool coalesce,
+                       bool link)
     : tmpl_(std::move(tmpl)), segs_(std::move(segs)), recs_(std::move(recs)), epoch_at_(epoch_at),
-      paths_(std::move(paths)), device_(device), coalesce_(coalesce) {
+      paths_(std::move(paths)), device_(device), coalesce_(coalesce), link_(link) {
   const long long n = (long long)tmpl_.size();
   if (slots < 1 || slots > 64) throw std::invalid_argument("CkptWriter: slots must be in [1, 64]");
   if (epoch_at_ < 0 || epoch_at_ + 4 > n) throw std::invalid_argument("CkptWriter: epoch offset outside template");
@@ -153,16 +154,19 @@ void CkptWriter::write_one(int slot, int32_t epoch) {
     const uint32_t crc = crc32_fast(0u, o + r.data_off, (size_t)r.bytes);
     for (long long c : r.crc_at) put_u32(o + c, crc);
   }
-  // the bytes are written ONCE; every further target is a hard link to that file (same archive, e.g.
-  // Primary/optimizedModel.pth and checkpoint/<client>.pth), each committed by its own atomic rename --
-  // a later round's rename replaces the directory entry, never the shared inode's bytes.  Targets on
-  // another filesystem (link fails) get their own copy.
+  // Default: every target is its own file (tmp + atomic rename), so a peer that rewrites one of them in
+  // place (the reference's torch.save, src/server.py:179, src/main.py:165) never touches another.  With
+  // link_ (opt-in, for target sets in directories fedmi owns alone) the bytes are written ONCE and every
+  // further target is a hard link to that file, committed by its own rename; a link that fails (another
+  // filesystem) falls back to a copy.  Stale temp names are unlinked first: a temp left behind by a failed
+  // round may share an inode with a committed target, and O_TRUNC on it would rewrite that file in place.
   const std::string first = tmp_name(paths_[0]);
+  ::unlink(first.c_str());
   write_tmp(first, o, out_.size());
   for (size_t i = 1; i < paths_.size(); ++i) {
     const std::string t = tmp_name(paths_[i]);
     ::unlink(t.c_str());
-    if (::link(first.c_str(), t.c_str()) != 0) write_tmp(t, o, out_.size());
+    if (!link_ || ::link(first.c_str(), t.c_str()) != 0) write_tmp(t, o, out_.size());
     commit(t, paths_[i]);
   }
   commit(first, paths_[0]);

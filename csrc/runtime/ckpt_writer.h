@@ -55,7 +55,8 @@ class CkptWriter {
   // device: true = segments are device pointers copied on a stream (pinned snapshots);
   //         false = host pointers copied synchronously (CPU hosts / tests).
   CkptWriter(std::vector<uint8_t> tmpl, std::vector<CkptSegment> segs, std::vector<CkptRecord> recs,
-             long long epoch_at, std::vector<std::string> paths, bool device, int slots = 4, bool coalesce = false);
+             long long epoch_at, std::vector<std::string> paths, bool device, int slots = 4, bool coalesce = false,
+             bool link = false);   // link: extra targets are hard links to the first (opt-in, see write_one)
   ~CkptWriter();
   CkptWriter(const CkptWriter&) = delete;
   CkptWriter& operator=(const CkptWriter&) = delete;
@@ -78,6 +79,7 @@ class CkptWriter {
   std::vector<std::string> paths_;
   bool device_;
   bool coalesce_;
+  bool link_;
   long long snap_bytes_ = 0;
   std::vector<uint8_t*> snap_;
   std::vector<hipEvent_t> ev_;

@@ -341,7 +341,7 @@ class NativeCheckpointWriter:
     (mixed devices, non-contiguous tensors); :class:`RoundCheckpointWriter` then
     uses Python."""
 
-    def __init__(self, paths, state_dict, acc=1, slots: int = 4, coalesce: bool = False):
+    def __init__(self, paths, state_dict, acc=1, slots: int = 4, coalesce: bool = False, link: bool = False):
         from .. import native
 
         nat = native.require()
@@ -400,7 +400,8 @@ class NativeCheckpointWriter:
         self.paths = [str(Path(p)) for p in paths]
         for p in self.paths:
             Path(p).parent.mkdir(parents=True, exist_ok=True)
-        self.w = nat.CkptWriter(blob, segs, recs, at + 1, self.paths, self.device, int(slots), bool(coalesce))
+        self.w = nat.CkptWriter(blob, segs, recs, at + 1, self.paths, self.device, int(slots), bool(coalesce),
+                                bool(link))
         self._stream = native.stream_handle if self.device else None
 
     @staticmethod
@@ -431,10 +432,13 @@ class RoundCheckpointWriter:
     """Per-round checkpoints (same files every round): the native writer where the state dict
     maps onto it, else :class:`AsyncCheckpointWriter`.  Every round is written unless
     ``coalesce`` (then a host that outruns the writer by ``slots`` rounds supersedes queued
-    rounds instead of waiting).  FEDMI_NATIVE_CKPT=0 forces the Python writer."""
+    rounds instead of waiting).  Every target is an independent file unless ``link`` (opt-in, only
+    for target sets in directories fedmi owns alone): then the native writer writes the bytes once
+    and hard-links the other targets -- a peer that rewrites one of them in place (the reference's
+    torch.save) would then change the others too.  FEDMI_NATIVE_CKPT=0 forces the Python writer."""
 
-    def __init__(self, slots: int = 4, coalesce: bool = False):
-        self.slots, self.coalesce = slots, coalesce
+    def __init__(self, slots: int = 4, coalesce: bool = False, link: bool = False):
+        self.slots, self.coalesce, self.link = slots, coalesce, link
         self._native: Dict[tuple, NativeCheckpointWriter] = {}
         self._py: Optional[AsyncCheckpointWriter] = None
         self.backend = None
@@ -459,7 +463,7 @@ class RoundCheckpointWriter:
                 w = None
             if w is None:
                 try:
-                    w = NativeCheckpointWriter(paths, state_dict, acc, self.slots, self.coalesce)
+                    w = NativeCheckpointWriter(paths, state_dict, acc, self.slots, self.coalesce, self.link)
                     self._native[paths] = w
                 except (ValueError, RuntimeError):
                     w = None

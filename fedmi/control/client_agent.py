@@ -15,6 +15,14 @@ Reference: src/client.py:15-35 (+ the import-time trainer in src/main.py).
         usually the previous round's) unless the coordinator asks for this
         round's (``x-fedmi-sync-ckpt: 1``, e.g. on the final round).
         A new membership generation starts with a resync from rank 0.
+        Round lease (``x-fedmi-lease: K``, fedmi extension): one StartTrain runs K
+        consecutive synchronous rounds (round numbers x-fedmi-round .. +K-1, one
+        data-plane generation), each fenced, averaged, evaluated and checkpointed
+        exactly like a single round; per-round stats return in the trailing
+        metadata, so the gRPC round trip is paid once per K rounds instead of once
+        per round (control plane off the critical path).  A collective
+        that fails inside a lease rolls this client back to the last committed
+        round (the previous lease round) and ends the call with ABORTED.
   SendModel(b64 checkpoint) -> install it (resync / grpc-mode broadcast), persist,
       evaluate.
   HeartBeat() -> status 1.
@@ -26,6 +34,7 @@ checkpoints are never ``module.``-prefixed, the checkpoint dir is created.
 """
 from __future__ import annotations
 
+import json
 import os
 import threading
 import time
@@ -51,6 +60,8 @@ META_STORE = "x-fedmi-store"
 META_SYNC = "x-fedmi-sync-ckpt"        # "1": the reply must carry THIS round's checkpoint
 META_UPLOAD = "x-fedmi-upload"         # "0": leave the checkpoint out of the StartTrain reply (fetched later)
 META_FETCH = "x-fedmi-fetch"           # on SendModel: "1" = return the newest checkpoint instead of installing
+META_HAVE = "x-fedmi-have-epoch"       # on a fetch: the coordinator already holds this epoch (reply empty unless newer)
+META_LEASE = "x-fedmi-lease"           # on StartTrain: "K" = run K consecutive synchronous rounds in this call
 
 
 def metadata_dict(context) -> dict:
@@ -92,6 +103,8 @@ class ClientAgent(P.TrainerServicer):
         self._round_start = None                # (float, [int]) device copies of the round's starting global model
         self._debug_stats = os.environ.get("FEDMI_DEBUG_STATS", "0") == "1"
         self._select_logged = False
+        self._overflow_logged = False
+        self._newest_term = 0                   # highest term any StartTrain carried (read without the lock)
         if self._debug_stats:
             from ..parallel import compress as _comp
             _comp.PROBE = self._probe
@@ -177,6 +190,9 @@ class ClientAgent(P.TrainerServicer):
         t_enter = time.time()
         meta = metadata_dict(context)
         gen = int(meta.get(META_GEN, "0") or 0)
+        term = int(meta.get(META_TERM, "0") or 0)
+        if term > self._newest_term:
+            self._newest_term = term            # seen before the lock: a running lease stops at its next round
         busy = self._busy_gen
         if self.group is not None and busy is not None and gen > busy:
             # a newer membership while an older round is still blocked in its collective
@@ -191,13 +207,15 @@ class ClientAgent(P.TrainerServicer):
 
     def _start_train(self, request, context, meta: dict, gen: int, t_enter: float = 0.0):
         self._fence(meta, context)
+        term = int(meta.get(META_TERM, "0") or 0)
         rank, world = int(request.rank), int(request.world)
         if world <= 0 or not 0 <= rank < world:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"bad rank/world {rank}/{world}")
         rnd = int(meta.get(META_ROUND, self.round + 1) or self.round + 1)
+        lease = max(1, int(meta.get(META_LEASE, "1") or 1)) if self.agg == "collective" else 1
         t = Timer()
-        rec = {"role": "client", "address": self.address, "round": rnd, "rank": rank, "world": world,
-               "agg": self.agg, "generation": gen}
+        rec0 = {"role": "client", "address": self.address, "rank": rank, "world": world, "agg": self.agg,
+                "generation": gen}
         if self.agg == "collective":
             host, _, port = (meta.get(META_STORE) or "127.0.0.1:0").rpartition(":")
             changed = False
@@ -212,17 +230,51 @@ class ClientAgent(P.TrainerServicer):
             elif world > 1:
                 context.abort(grpc.StatusCode.FAILED_PRECONDITION, "collective aggregation needs a GroupManager")
             if changed and self.group is not None and self.group.select_info and not self._select_logged:
-                rec["transport_select"] = self.group.select_info      # the auto data-plane decision, once
+                rec0["transport_select"] = self.group.select_info      # the auto data-plane decision, once
                 self._select_logged = True
             if changed and world > 1:
                 # new member set: everyone starts this generation from rank 0's model (one anchor
                 # for the -c Y compressors; undoes any partially applied aborted round)
                 self.fedavg.resync(self.trainer, 0)
-                rec["resync"] = True
+                rec0["resync"] = True
                 self._probe("resync")
             elif changed and self.fedavg.compressor is not None:
                 self.fedavg.compressor.reset(self.trainer)
-            rec["group_ms"] = t.ms()
+            rec0["group_ms"] = t.ms()
+        lease_stats = []
+        ck_epoch, message = -1, ""
+        for i in range(lease):
+            r = rnd + i
+            if i > 0 and term and term < max(self.max_term, self._newest_term):
+                # a newer coordinator reached this client mid-lease: stop at the committed round
+                self._lease_trailer(context, lease_stats, -1)
+                context.abort(grpc.StatusCode.FAILED_PRECONDITION,
+                              f"lease of term {term} superseded by term {self._newest_term} after round {self.round}")
+            rec = dict(rec0, round=r, lease=lease, lease_index=i) if i == 0 else dict(
+                {k: v for k, v in rec0.items() if k not in ("group_ms", "resync", "transport_select")},
+                round=r, lease=lease, lease_index=i)
+            last = i == lease - 1
+            tr, ck_epoch, message = self._one_round(rank, world, r, meta, gen, context, rec, lease_stats,
+                                                    t_enter if i == 0 else time.time(), last)
+            lease_stats.append((r, round(tr.loss, 6), round(rec.get("test_acc", -1.0), 4), round(time.time(), 6)))
+        self._lease_trailer(context, lease_stats, ck_epoch)
+        return P.TrainReply(message=message)
+
+    def _lease_trailer(self, context, lease_stats, ck_epoch: int) -> None:
+        last = lease_stats[-1] if lease_stats else (self.round, -1.0, -1.0, time.time())
+        try:
+            context.set_trailing_metadata((("x-fedmi-client-round", str(self.round)),
+                                           ("x-fedmi-ckpt-epoch", str(ck_epoch)),
+                                           ("x-fedmi-train-loss", f"{last[1]:.6f}"),
+                                           ("x-fedmi-test-acc", f"{last[2]:.4f}"),
+                                           ("x-fedmi-lease-stats", json.dumps(lease_stats, separators=(",", ":")))))
+        except Exception:
+            pass
+
+    def _one_round(self, rank: int, world: int, rnd: int, meta: dict, gen: int, context, rec: dict, lease_stats,
+                   t_enter: float, last: bool):
+        """One synchronous round (local epoch, FedAvg, eval, checkpoint) of a StartTrain lease."""
+        t = Timer()
         if self.agg == "collective" and world > 1:
             self._snapshot_round_start()
         t1 = Timer()
@@ -253,9 +305,12 @@ class ClientAgent(P.TrainerServicer):
                 digest = self._restore_round_start()
                 self.metrics.write(role="client", address=self.address, event="round_aborted", round=rnd,
                                    generation=gen, error=err[:200], restored_sum=digest)
+                # the lease's earlier rounds are committed: report how far this client got
+                self._lease_trailer(context, lease_stats, -1)
                 # ABORTED (not UNAVAILABLE): this client is alive, only the round is void
                 context.abort(grpc.StatusCode.ABORTED, err[:500])
             rec["allreduce_ms"] = t2.ms()
+            self._check_compressor()
             t3 = Timer()
             with phase("eval"):
                 self.trainer.evaluate()
@@ -267,10 +322,10 @@ class ClientAgent(P.TrainerServicer):
             t4 = Timer()
             with phase("checkpoint"):
                 self._persist_async(ev.acc, rnd, keep=(rank == 0))
-                sync = meta.get(META_SYNC) == "1"
+                sync = last and meta.get(META_SYNC) == "1"
                 if rank == 0 and sync:
                     self.writer.flush()
-                upload = rank == 0 and (sync or meta.get(META_UPLOAD) != "0")
+                upload = last and rank == 0 and (sync or meta.get(META_UPLOAD) != "0")
                 ck_epoch, message = self._take_ready() if upload else (-1, "")
             rec["ckpt_ms"] = t4.ms()
             self._probe("ckpt")
@@ -287,14 +342,19 @@ class ClientAgent(P.TrainerServicer):
         self.metrics.write(**rec)
         self._log(f"round {rnd} rank {rank}/{world}: train loss {tr.loss:.4f} acc {tr.acc:.2f}%"
                   + (f" | test acc {rec['test_acc']:.2f}%" if "test_acc" in rec else ""))
-        try:
-            context.set_trailing_metadata((("x-fedmi-client-round", str(self.round)),
-                                           ("x-fedmi-ckpt-epoch", str(ck_epoch)),
-                                           ("x-fedmi-train-loss", f"{tr.loss:.6f}"),
-                                           ("x-fedmi-test-acc", f"{rec.get('test_acc', -1):.4f}")))
-        except Exception:
-            pass
-        return P.TrainReply(message=message)
+        return tr, ck_epoch, message
+
+    def _check_compressor(self) -> None:
+        """-c Y top-k: log the kernel's sticky overflow flag once (it is a kernel bug, never a data condition);
+        checked every 64 rounds (the read synchronises)."""
+        comp = getattr(self.fedavg, "compressor", None)
+        over = getattr(comp, "overflowed", None)
+        if over is None or self._overflow_logged or self.round % 64:
+            return
+        if over(clear=False):
+            self._overflow_logged = True
+            self._log("WARNING: top-k select overflowed (entries beyond k were dropped on every rank)")
+            self.metrics.write(role="client", address=self.address, event="topk_overflow", round=self.round)
 
     def SendModel(self, request, context):
         meta = metadata_dict(context)
@@ -325,10 +385,13 @@ class ClientAgent(P.TrainerServicer):
         term = int(meta.get(META_TERM, "0") or 0)
         if term and term < self.max_term:
             context.abort(grpc.StatusCode.FAILED_PRECONDITION, f"stale coordinator term {term} < {self.max_term}")
+        have = int(meta.get(META_HAVE, "-1") or -1)
         with self._ready_lock:
             ready = self._ready
         if ready is None:
             epoch, b64 = -1, ""
+        elif ready[0] <= have:
+            epoch, b64 = ready[0], ""           # nothing newer than what the coordinator holds
         else:
             epoch, b64 = ready[0], ck.to_b64(ready[1])
         try:

@@ -26,6 +26,7 @@ is a daemon thread that stops with the coordinator.
 from __future__ import annotations
 
 import concurrent.futures as cf
+import json
 import threading
 import time
 from collections import OrderedDict
@@ -41,7 +42,8 @@ from ..parallel.group import StoreHost
 from ..utils.metrics import MetricsLog, Timer, log
 from ..utils.trace import phase
 from ..wire import proto as P
-from .client_agent import META_FETCH, META_GEN, META_ROUND, META_STORE, META_SYNC, META_TERM, META_UPLOAD
+from .client_agent import (META_FETCH, META_GEN, META_HAVE, META_LEASE, META_ROUND, META_STORE, META_SYNC, META_TERM,
+                           META_UPLOAD)
 
 
 @dataclass
@@ -64,6 +66,10 @@ class CoordinatorConfig:
     # collective mode with fedmi clients: the per-round model upload leaves the StartTrain reply and a
     # background fetcher pulls rank 0's newest checkpoint at most this often (<= 0: upload every reply)
     ckpt_fetch_interval_s: float = 0.05
+    # collective mode: one StartTrain runs this many consecutive rounds on the clients (x-fedmi-lease), so the
+    # fan-out / gather round trip is paid once per lease; 1 = one RPC per round (the reference's cadence; always
+    # the case for agg="grpc")
+    lease_rounds: int = 16
 
 
 def fedavg_state_dicts(sds: List[dict], weights: Optional[List[float]] = None) -> "OrderedDict[str, torch.Tensor]":
@@ -141,6 +147,7 @@ class Coordinator:
         self._persist_thread.start()
         self._fetch_thread: Optional[threading.Thread] = None
         self._fetches = 0
+        self._lease_end = 0                  # last round of the StartTrain lease in flight (0: none)
         if cfg.agg == "collective" and cfg.ckpt_fetch_interval_s > 0:
             self._fetch_thread = threading.Thread(target=self._fetcher, name="fedmi-fetch", daemon=True)
             self._fetch_thread.start()
@@ -164,10 +171,23 @@ class Coordinator:
         with self._lock:
             return {a: m.active for a, m in self.members.items()}
 
-    def _meta(self, round_no: int, live: List[str]):
+    def _lease(self, rnd: int) -> int:
+        """Rounds the next StartTrain covers: the configured lease, never past the last round, and ending on
+        a ``ckpt_sync_every`` boundary (those rounds upload their own checkpoint)."""
+        if self.cfg.agg != "collective":
+            return 1
+        k = max(1, min(int(self.cfg.lease_rounds), self.cfg.rounds - rnd + 1))
+        if self.cfg.ckpt_sync_every > 0:
+            k = min(k, self.cfg.ckpt_sync_every - (rnd - 1) % self.cfg.ckpt_sync_every)
+        return k
+
+    def _meta(self, round_no: int, live: List[str], lease: int = 1):
         md = [(META_TERM, str(self.term)), (META_ROUND, str(round_no)), (META_GEN, str(self.generation))]
+        if lease > 1:
+            md.append((META_LEASE, str(lease)))
         k = self.cfg.ckpt_sync_every
-        sync = round_no >= self.cfg.rounds or (k > 0 and round_no % k == 0)
+        end = round_no + lease - 1
+        sync = end >= self.cfg.rounds or (k > 0 and end % k == 0)
         if sync:
             md.append((META_SYNC, "1"))
         elif (self._fetch_thread is not None and live and self.members[live[0]].fedmi):
@@ -218,12 +238,14 @@ class Coordinator:
         without a model upload inside each StartTrain reply."""
         while not self.stop_event.wait(self.cfg.ckpt_fetch_interval_s):
             live = self.live()
-            if not live or self.round <= self.installed_epoch or not self.members[live[0]].fedmi:
+            behind = self.round > self.installed_epoch or self._lease_end > max(self.round, self.installed_epoch)
+            if not live or not behind or not self.members[live[0]].fedmi:
                 continue
             m = self.members[live[0]]
             try:
                 call = m.stub.SendModel.with_call(P.SendModelRequest(model=""), timeout=self.cfg.rpc_timeout_s,
-                                                  metadata=[(META_TERM, str(self.term)), (META_FETCH, "1")])
+                                                  metadata=[(META_TERM, str(self.term)), (META_FETCH, "1"),
+                                                            (META_HAVE, str(self.installed_epoch))])
             except grpc.RpcError:
                 continue                     # membership changes are the round loop's business
             reply, call = call
@@ -232,34 +254,35 @@ class Coordinator:
                 self._fetches += 1
                 self._install_global(ck.from_b64(reply.reply), epoch)
 
-    def _catch_up_committed(self, addr: str, wait_s: float = 2.0) -> None:
+    def _catch_up_committed(self, addr: str, target: Optional[int] = None, wait_s: float = 2.0) -> None:
         """Synchronously pull the newest COMMITTED global model from ``addr`` (the aborted round's rank 0,
-        which keeps the checkpoint of its last successful round) until it covers ``self.round``: the
-        background fetcher may be several rounds behind.  Best effort -- an unreachable rank 0 leaves
-        ``latest_model`` as it is."""
+        which keeps the checkpoint of its last successful round) until it covers ``target`` (the round rank 0
+        reported as committed in its ABORTED trailer; default ``self.round``): the background fetcher may be
+        several rounds behind.  A model newer than ``self.round`` -- rounds of a lease that completed their
+        all-reduce before the failure, or an aborted round whose all-reduce had finished on rank 0 -- is a
+        full FedAvg result and becomes the committed round: the round counter follows it (otherwise the next
+        round would report that epoch again and _install_global would drop it as not newer).  Best effort:
+        an unreachable rank 0 leaves ``latest_model`` as it is."""
         m = self.members.get(addr)
         if m is None or not m.fedmi or self.cfg.agg != "collective":
             return
+        want = self.round if target is None else max(self.round, int(target))
         deadline = time.monotonic() + wait_s
-        while self.installed_epoch < self.round and time.monotonic() < deadline:
+        while self.installed_epoch < want and time.monotonic() < deadline:
             try:
                 reply, call = m.stub.SendModel.with_call(
                     P.SendModelRequest(model=""), timeout=self.cfg.rpc_timeout_s,
-                    metadata=[(META_TERM, str(self.term)), (META_FETCH, "1")])
+                    metadata=[(META_TERM, str(self.term)), (META_FETCH, "1"), (META_HAVE, str(self.installed_epoch))])
             except grpc.RpcError:
-                return
+                break
             epoch = int(dict(call.trailing_metadata() or ()).get("x-fedmi-ckpt-epoch", "-1"))
             if reply.reply and epoch > self.installed_epoch:
                 self._install_global(ck.from_b64(reply.reply), epoch)
-                if epoch > self.round:
-                    # the "aborted" round had completed its all-reduce on rank 0 (a client died after it):
-                    # that model is a full FedAvg result and becomes the committed round, so the round
-                    # counter follows it -- otherwise the next round would report this epoch again and
-                    # _install_global would drop it as not newer
-                    self._log(f"rank 0 committed round {epoch} before the abort: advancing the round counter")
-                    self.round = epoch
             else:
                 time.sleep(0.02)             # its writer is still serialising the committed round
+        if self.installed_epoch > self.round:
+            self._log(f"rank 0 committed round {self.installed_epoch} before the abort: advancing the round counter")
+            self.round = self.installed_epoch
 
     def flush(self) -> None:
         """Wait until the newest installed model is on disk (and offered to the backup)."""
@@ -294,42 +317,62 @@ class Coordinator:
             self._last_live = tuple(live)
         world = len(live)
         rnd = self.round + 1
-        self._log(f"Starting round {rnd} with {world} client(s) (gen {self.generation})")
+        lease = self._lease(rnd)
+        end = rnd + lease - 1
+        self._log(f"Starting round {rnd}" + (f"-{end}" if lease > 1 else "")
+                  + f" with {world} client(s) (gen {self.generation})")
         t = Timer()
-        md = self._meta(rnd, live)
+        md = self._meta(rnd, live, lease)
         t_send = time.time()
+        self._lease_end = end
         futs = {}
+        # blocking unary calls on the coordinator's pool (a grpc ``.future()`` call starts a channel spin thread
+        # per call: ~1 ms per client per round on the control plane)
         for rank, addr in enumerate(live):
             stub = self.members[addr].stub
-            futs[addr] = (rank, stub.StartTrain.future(P.TrainRequest(rank=rank, world=world),
-                                                       timeout=self.cfg.train_timeout_s, metadata=md))
-        replies, failed, client_rounds, ckpt_epochs = {}, [], [], {}
+            futs[addr] = (rank, self._pool.submit(stub.StartTrain.with_call, P.TrainRequest(rank=rank, world=world),
+                                                  timeout=self.cfg.train_timeout_s * lease, metadata=md))
+        replies, failed, client_rounds, ckpt_epochs, lease_stats, committed = {}, [], [], {}, None, {}
         for addr, (rank, f) in futs.items():
             try:
-                replies[rank] = f.result().message
-                tm = dict(f.trailing_metadata() or ())
+                reply, call = f.result()
+                replies[rank] = reply.message
+                tm = dict(call.trailing_metadata() or ())
                 if "x-fedmi-client-round" in tm:
                     client_rounds.append(int(tm["x-fedmi-client-round"]))
                     self.members[addr].fedmi = True
                 if "x-fedmi-ckpt-epoch" in tm:
                     ckpt_epochs[rank] = int(tm["x-fedmi-ckpt-epoch"])
+                if rank == 0 and "x-fedmi-lease-stats" in tm:
+                    lease_stats = tm["x-fedmi-lease-stats"]
             except grpc.RpcError as e:
                 self._log(f"StartTrain on {addr} failed: {e.code().name} {e.details() or ''}".strip())
                 failed.append(addr)
+                try:   # an aborted lease reports the rounds it committed before the failure
+                    tm = dict(e.trailing_metadata() or ())
+                    if "x-fedmi-client-round" in tm:
+                        committed[rank] = int(tm["x-fedmi-client-round"])
+                        self.members[addr].fedmi = True      # a fedmi client (it serves the fetch path)
+                    if rank == 0 and "x-fedmi-lease-stats" in tm:
+                        lease_stats = tm["x-fedmi-lease-stats"]
+                except Exception:
+                    pass
                 # ABORTED / FAILED_PRECONDITION: the client answered (its collective lost a peer, or it
                 # fenced us); only an unreachable or silent client leaves the membership
                 if e.code() not in (grpc.StatusCode.ABORTED, grpc.StatusCode.FAILED_PRECONDITION):
                     self._mark(addr, False)
+        self._lease_end = 0
         t_train = t.ms()
         t_recv = time.time()
         ok = False
         if self.cfg.agg == "collective":
             if failed:
                 # the survivors' all-reduce for this round is not trustworthy: roll them back to the
-                # last committed global model, then regroup (new generation) next round
+                # last committed global model, then regroup (new generation) next round.  Lease rounds that
+                # completed before the failure stay committed (rank 0 checkpointed them).
                 self._log(f"round {rnd} aborted ({len(failed)} client(s) lost); rolling back survivors, regrouping")
                 self._last_live = None           # force a new generation even if every member answered ABORTED
-                self._catch_up_committed(live[0])
+                self._catch_up_committed(live[0], committed.get(0))
                 if self.latest_model is not None:
                     if self.installed_epoch >= 0 and self.installed_epoch < self.round:
                         # rank 0's newest committed round was not reachable: the round counter follows
@@ -349,7 +392,7 @@ class Coordinator:
             else:
                 msg = replies.get(0, "")
                 if msg:
-                    self._install_global(ck.from_b64(msg), ckpt_epochs.get(0, rnd))
+                    self._install_global(ck.from_b64(msg), ckpt_epochs.get(0, end))
                 ok = True
         else:
             good = {r: ck.from_b64(m) for r, m in replies.items() if m}
@@ -366,15 +409,41 @@ class Coordinator:
                     s_.result()
                 ok = True
         if ok:
-            self.round = max([rnd] + client_rounds)
+            self.round = max([end] + client_rounds)
         dt = t.ms()
-        self.round_times.append(dt)
-        self.metrics.write(role=self.role, event="round", round=rnd, ok=ok, world=world, generation=self.generation,
-                           failed=failed, train_ms=t_train, round_ms=dt, term=self.term, t_send=t_send, t_recv=t_recv,
-                           t_done=time.time())
+        self.round_times.append(dt / lease)
+        t_done = time.time()
+        if ok:
+            per = [(r_, True, lo, ac, tr_) for r_, lo, ac, tr_ in self._lease_rows(lease_stats, rnd, end)]
+        else:
+            # an aborted lease: the rounds before the failure are committed (the round counter now covers them),
+            # the failing round is the one after them
+            done = [row for row in self._lease_rows(lease_stats, rnd, self.round) if row[0] <= self.round]
+            per = [(r_, True, lo, ac, tr_) for r_, lo, ac, tr_ in done]
+            per.append((max(rnd, self.round + 1), False, None, None, t_done))
+        for r_, ok_r, loss, acc, t_r in per:
+            self.metrics.write(role=self.role, event="round", round=r_, ok=ok_r, world=world, generation=self.generation,
+                               failed=[] if ok_r else failed, train_ms=t_train / lease, round_ms=dt / lease,
+                               term=self.term, t_send=t_send, t_recv=t_recv, t_done=t_done, lease=lease, t_round=t_r,
+                               **({"train_loss": loss, "test_acc": acc} if loss is not None else {}))
         if self.cfg.round_pause_s:
             time.sleep(self.cfg.round_pause_s)
         return ok
+
+    @staticmethod
+    def _lease_rows(raw: Optional[str], rnd: int, end: int):
+        """(round, train_loss, test_acc, t_done) per round of a lease from rank 0's x-fedmi-lease-stats
+        trailer (reference peers send none: one row per round with no stats)."""
+        rows = []
+        if raw:
+            try:
+                rows = [(int(r[0]), float(r[1]), float(r[2]), float(r[3])) for r in json.loads(raw)]
+            except (ValueError, TypeError, IndexError):
+                rows = []
+        have = {r[0] for r in rows}
+        now = time.time()
+        rows += [(r, None, None, now) for r in range(rnd, end + 1) if r not in have]
+        return sorted(rows)
 
     # ---- rejoin tracker (src/server.py:78-101) --------------------------------------
     def _track(self) -> None:
@@ -405,6 +474,11 @@ class Coordinator:
         self._log(f"term {self.term}, resuming at round {self.round}, clients {list(self.members)}")
         while self.round < self.cfg.rounds and not self.stop_event.is_set():
             self.run_round()
+        live = self.live()
+        if live and self.installed_epoch < self.round:
+            # a lease ended without uploading its last round (pipelined upload, fetcher stopped): pull rank 0's
+            # newest committed model so Primary/optimizedModel.pth and the backup replica cover every round run
+            self._catch_up_committed(live[0], self.round)
         self._log(f"finished at round {self.round}")
 
     def stop(self) -> None:

@@ -30,14 +30,21 @@ def model_digest(trainer) -> bytes:
     return h.digest()
 
 
-def check_consistency(trainer, group=None, transport=None, device: Optional[torch.device] = None) -> dict:
-    """Collective over ``group``: every rank's (transport error, model digest).
+def check_consistency(trainer, group=None, transport=None, device: Optional[torch.device] = None,
+                      compressor=None) -> dict:
+    """Collective over ``group``: every rank's (error word, model digest).
 
     Returns ``{"ok", "ranks", "transport_errors", "distinct_digests", "digest"}``; ``ok`` is
     identical on every rank.  ``transport`` is the peer transport (``error()`` != 0 after a
-    barrier timeout); ``None`` for RCCL / gloo, whose failures raise instead.
+    barrier timeout); ``None`` for RCCL / gloo, whose failures raise instead.  ``compressor``
+    (``-c Y`` top-k) contributes its sticky overflow flag as bit 30 of the error word: a select
+    that produced more than k entries drops the excess identically on every rank, so the digests
+    would still agree although the sparse update was wrong.
     """
     err = int(transport.error()) if transport is not None else 0
+    over = getattr(compressor, "overflowed", None)
+    if over is not None and over(clear=False):
+        err |= 1 << 30
     dig = model_digest(trainer)
     words = [err] + [int.from_bytes(dig[i:i + 8], "little", signed=True) for i in (0, 8)]
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1

@@ -79,7 +79,8 @@ def test_checkpoint_fetched_off_the_round_path(tmp_path):
     addrs, procs = _start_clients(tmp_path, 1)
     try:
         cfg = CoordinatorConfig(clients=addrs, rounds=12, agg="collective", root=str(tmp_path / "srv"),
-                                train_timeout_s=120, rpc_timeout_s=10, heartbeat_s=0.2, ckpt_fetch_interval_s=0.01)
+                                train_timeout_s=120, rpc_timeout_s=10, heartbeat_s=0.2, ckpt_fetch_interval_s=0.01,
+                                lease_rounds=1)
         coord = Coordinator(cfg)
         seen = []
         orig = coord._install_global

@@ -217,6 +217,37 @@ def test_native_round_writer_writes_every_round_in_order(tmp_path, monkeypatch):
     assert ck["epoch"] == 59 and torch.equal(ck["net"]["w"], torch.full((20, 30), 59.0))
 
 
+def test_native_writer_targets_are_independent_files(tmp_path):
+    """Default: Primary/optimizedModel.pth and checkpoint/<client>.pth are separate inodes, so a peer that
+    rewrites one of them IN PLACE (the reference's torch.save: truncate + write, src/server.py:179) leaves
+    the other intact.  ``link=True`` (opt-in) shares one inode."""
+    import os
+
+    from fedmi import native
+    from fedmi.ckpt import RoundCheckpointWriter, load
+
+    if not native.available():
+        pytest.skip("native extension not built")
+    sd = {"w": torch.arange(12.0).view(3, 4)}
+    paths = [tmp_path / "Primary" / "optimizedModel.pth", tmp_path / "checkpoint" / "c0.pth"]
+    w = RoundCheckpointWriter(slots=2)
+    for r in range(3):
+        w.submit(paths, sd, epoch=r + 1)
+    w.close()
+    assert w.backend == "native"
+    assert os.stat(paths[0]).st_ino != os.stat(paths[1]).st_ino
+    with open(paths[0], "r+b") as f:     # in-place rewrite of one target
+        f.truncate(0)
+        f.write(b"garbage")
+    ck = load(paths[1])
+    assert ck["epoch"] == 3 and torch.equal(ck["net"]["w"], sd["w"])
+    lk = RoundCheckpointWriter(slots=2, link=True)
+    lp = [tmp_path / "own" / "a.pth", tmp_path / "own" / "b.pth"]
+    lk.submit(lp, sd, epoch=7)
+    lk.close()
+    assert os.stat(lp[0]).st_ino == os.stat(lp[1]).st_ino and load(lp[1])["epoch"] == 7
+
+
 @pytest.mark.gpu
 def test_device_round_writer_native_vs_python(tmp_path, monkeypatch):
     """Device tensors: the native writer (default) and the Python writer (FEDMI_NATIVE_CKPT=0) produce

@@ -154,11 +154,15 @@ def _client_killed_mid_collective(tmp_path, device, n_clients=3):
         t = threading.Thread(target=coord.run, daemon=True)
         t.start()
         # rounds 1-2 commit; from round 3 on the victim stalls 4 s before the collective: the survivors
-        # are inside it when it dies
-        wait_for(lambda: len(_rounds(tmp_path / "coord.jsonl")) >= 2, timeout=60)
+        # are inside it when it dies.  The coordinator runs round leases (one StartTrain for many rounds), so
+        # committed rounds are read off the clients' own per-round records.
+        def client_rounds(i=0):
+            return [r for r in read_jsonl(tmp_path / f"client{i}.jsonl") if "train_ms" in r and "round" in r]
+
+        wait_for(lambda: len(client_rounds()) >= 2, timeout=60)
         time.sleep(2.0)
         t_kill = kill9(procs[victim])
-        committed = max(r["round"] for r in _rounds(tmp_path / "coord.jsonl") if r["ts"] < t_kill)
+        committed = max(r["round"] for r in client_rounds() if r["ts"] < t_kill)
         # survivors fail fast, the round is aborted; the next round runs with the survivors only
         ok2 = wait_for(lambda: [r for r in _rounds(tmp_path / "coord.jsonl") if r["world"] == surv], timeout=90)
         recovery = ok2[0]["ts"] - t_kill
