@@ -148,6 +148,7 @@ def main() -> int:
                     help="-c Y data-plane compression of the FedAvg update")
     ap.add_argument("--topk-ratio", type=float, default=0.01)
     ap.add_argument("--compress-warmup", type=int, default=0, help="dense FedAvg rounds before compression starts")
+    ap.add_argument("--seed", type=int, default=17, help="model-init / augmentation seed (same on every rank)")
     ap.add_argument("--allreduce", default="auto", choices=["auto", "rccl", "oneshot", "twoshot"],
                     help="FedAvg transport at N>1: hipIpc peer kernels (oneshot/twoshot), RCCL, or auto = verify "
                          "the peer kernel against RCCL and time both, keep the faster")
@@ -211,7 +212,7 @@ def main() -> int:
     from fedmi.utils.trace import phase
 
     data = make_dataset("synthetic-cifar10", device=device, n_train=N_TRAIN, n_test=N_TEST, seed=0)
-    cfg = TrainerConfig(seed=17, use_graph=not args.no_graph)
+    cfg = TrainerConfig(seed=args.seed, use_graph=not args.no_graph)
     trainer = build_trainer(args.model, data, device, cfg)
     broadcast_state_(trainer, 0)                     # one shared init (reference quirk A7 fixed)
     if args.noniid > 0:     # McMahan-style label shards: each client trains only its own shard

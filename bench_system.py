@@ -93,6 +93,8 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=None, help="GPUs to spread clients over (default: all visible)")
     ap.add_argument("--no-backup", action="store_true")
     ap.add_argument("--ckpt-sync-every", type=int, default=0)
+    ap.add_argument("--lease", type=int, default=16,
+                    help="rounds per StartTrain (round lease); 1 = one StartTrain per round (reference cadence)")
     ap.add_argument("--keep", default=None, help="keep the run directory here")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--startup-timeout", type=float, default=300.0)
@@ -127,7 +129,8 @@ def main() -> int:
             _wait_heartbeat(addr, a.startup_timeout, procs)
         prim = _spawn([str(ROOT / "server.py"), "--p", "y", "--backupPort", str(bport), "--clients", ",".join(addrs),
                        "--rounds", str(total), "--agg", a.agg, "--root", str(run / "srv"), "--train-timeout", "600",
-                       "--metrics", str(run / "primary.jsonl"), "--ckpt-sync-every", str(a.ckpt_sync_every), *comp],
+                       "--metrics", str(run / "primary.jsonl"), "--ckpt-sync-every", str(a.ckpt_sync_every),
+                       "--lease", str(a.lease), *comp],
                       run, run / "primary.log", env)
         procs.append(prim)
         deadline = time.time() + 600 + 60 * total
@@ -150,7 +153,9 @@ def main() -> int:
     if len(rounds) < total:
         print(f"[bench_system] only {len(rounds)} ok rounds of {total}; see {run}", file=sys.stderr)
         return 1
-    t0, t1 = rounds[a.warmup - 1]["ts"], rounds[total - 1]["ts"]
+    # per-round completion time: the client-reported end of each leased round (t_round), else the event time
+    tk = "t_round" if all("t_round" in r for r in rounds) else "ts"
+    t0, t1 = rounds[a.warmup - 1][tk], rounds[total - 1][tk]
     rps = a.rounds / (t1 - t0)
     timed = {r["round"] for r in rounds[a.warmup:total]}
 
@@ -173,7 +178,9 @@ def main() -> int:
     # client handler work outside its timed round, reply latency (handler exit -> coordinator has the
     # reply), coordinator bookkeeping after the replies, and the gap to the next round's send
     by_round = {r["round"]: r for r in rounds}
-    c0 = {r["round"]: r for r in _jsonl(run / "client0.jsonl") if r.get("round") in timed and "t_enter" in r}
+    # request / reply latency only where a StartTrain begins or ends (the first / last round of a lease)
+    c0 = {r["round"]: r for r in _jsonl(run / "client0.jsonl") if r.get("round") in timed and "t_enter" in r
+          and r.get("lease_index", 0) == 0 and r.get("lease", 1) == 1}
     req, rep, post, gap, hnd = [], [], [], [], []
     for rnd_, cr in c0.items():
         pr = by_round.get(rnd_)
@@ -202,7 +209,7 @@ def main() -> int:
         "warmup": a.warmup,
         "ms_per_round": round(1e3 / rps, 4),
         "config": {"model": a.model, "agg": a.agg, "transport": a.transport, "compress": a.compressFlag,
-                   "backup": not a.no_backup, "ckpt_sync_every": a.ckpt_sync_every,
+                   "backup": not a.no_backup, "ckpt_sync_every": a.ckpt_sync_every, "lease": a.lease,
                    "batch": 128, "eval_per_round": True, "data": "synthetic CIFAR-shaped 50k/10k"},
         "phases_ms": phases,
         "last_round": {k: last_rec[0].get(k) for k in ("train_loss", "train_acc", "test_loss", "test_acc")}

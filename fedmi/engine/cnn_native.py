@@ -555,7 +555,7 @@ class CNNNativeTrainer(LocalTrainer):
         return self.fs.flat
 
     def int_state(self) -> List[torch.Tensor]:
-        return [b for _, _, b in self.fs.ibufs]
+        return self.fs.int_state()
 
     def momentum_state(self) -> torch.Tensor:
         return self.fs.mom

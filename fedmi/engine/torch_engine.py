@@ -61,8 +61,26 @@ class FlatState:
             self.flat[off:off + k].copy_(b.reshape(-1))
             m._buffers[key] = self.flat[off:off + k].view_as(b)
             off += k
-        self.ibufs = [(m, k, b) for m in model.modules() for k, b in m._buffers.items()
-                      if b is not None and not b.is_floating_point()]
+        # integer buffers (BN num_batches_tracked) re-homed into ONE int64 vector as well: FedAvg averages
+        # them in one collective instead of one per BatchNorm
+        ibufs = [(m, k, b) for m in model.modules() for k, b in m._buffers.items()
+                 if b is not None and not b.is_floating_point()]
+        self.iflat = None
+        if ibufs and all(b.dtype == torch.int64 for _, _, b in ibufs):
+            self.iflat = torch.zeros(sum(b.numel() for _, _, b in ibufs), dtype=torch.int64, device=device)
+            off = 0
+            for m, key, b in ibufs:
+                k = b.numel()
+                self.iflat[off:off + k].copy_(b.reshape(-1))
+                m._buffers[key] = self.iflat[off:off + k].view_as(b)
+                off += k
+        self.ibufs = [(m, k, m._buffers[k]) for m, k, _ in ibufs]
+
+    def int_state(self) -> list:
+        """The integer buffers as averaged by FedAvg: the one packed int64 vector (or the buffers themselves)."""
+        if self.iflat is not None:
+            return [self.iflat]
+        return [b for _, _, b in self.ibufs]
 
     @property
     def params(self) -> torch.Tensor:
@@ -99,7 +117,9 @@ class TorchTrainer(LocalTrainer):
         if self.hybrid:
             from ..ops.native_mode import NativeMode
 
-            self.mode = NativeMode(strict=os.environ.get("FEDMI_NATIVE_STRICT", "0") == "1", seed=cfg.seed)
+            # discard_unread: the step copies every p.grad inside the block, nothing reads a deferred tensor after it
+            self.mode = NativeMode(strict=os.environ.get("FEDMI_NATIVE_STRICT", "0") == "1", seed=cfg.seed,
+                                   discard_unread=True)
             self.mode.rng_ctr(self._device)      # allocated here, never inside a captured step
             self.mode.stable_storage = self.fs.flat.untyped_storage().data_ptr()   # weight images: batched packs
             # parameter gradients written straight into the flat gradient buffer (see native_mode._param_grad)
@@ -139,7 +159,7 @@ class TorchTrainer(LocalTrainer):
         return self.fs.flat
 
     def int_state(self) -> List[torch.Tensor]:
-        return [b for _, _, b in self.fs.ibufs]
+        return self.fs.int_state()
 
     def momentum_state(self) -> torch.Tensor:
         return self.fs.mom

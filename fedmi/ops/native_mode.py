@@ -1478,9 +1478,14 @@ class NativeMode(TorchDispatchMode):
 
     current: "NativeMode" = None
 
-    def __init__(self, strict: bool = False, seed: int = 0, fuse: bool = True):
+    def __init__(self, strict: bool = False, seed: int = 0, fuse: bool = True, discard_unread: bool = False):
         super().__init__()
         self.strict = strict
+        # at exit, tensors a fused op left unwritten (deferred: nothing inside the block read them) are
+        # materialised, because code after the block may still read them (e.g. a gradient AccumulateGrad adopted
+        # as p.grad without dispatching an op).  A caller that provably reads nothing after the block (the
+        # trainer: it copies every p.grad inside the block) sets discard_unread and saves those launches.
+        self.discard_unread = bool(discard_unread)
         self.seed = seed
         self.fallbacks = collections.Counter()
         self.native_ops = collections.Counter()
@@ -1624,6 +1629,9 @@ class NativeMode(TorchDispatchMode):
     def __exit__(self, *exc):
         try:
             self._flush()
+            if not self.discard_unread and exc[0] is None:
+                for fn in list(self._dead.values()):
+                    fn()
         finally:
             self._dead.clear()
             self._pend_sb = {}

@@ -72,6 +72,7 @@ def _run_seed(a, seed, data, dev, out) -> None:
         ev = clients[0].eval_stats()
         torch.cuda.synchronize() if dev.type == "cuda" else None
         rec = {"round": rnd, "engine": a.engine, "model": a.model, "clients": W, "lr": a.lr, "seed": seed,
+               "deterministic": bool(a.deterministic),
                "augment": not a.no_augment, "graph": not a.no_graph,
                "split": f"noniid-{a.noniid}" if a.noniid else "strided-iid",
                "train_loss": [round(s.loss, 4) for s in tstats], "train_acc": [round(s.acc, 2) for s in tstats],
@@ -100,9 +101,16 @@ def main() -> int:
     ap.add_argument("--out", default=None, help="JSONL, one record per round")
     ap.add_argument("--no-augment", action="store_true", help="no crop/flip (diagnostics)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of graph replay (diagnostics)")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="PyTorch engines: deterministic algorithms (MIOpen / rocBLAS deterministic kernels), so two "
+                         "runs of the fp32 reference agree and a parity gap is the engine's, not reference noise")
     a = ap.parse_args()
     if a.engine in ("fp32", "bf16"):
         os.environ["FEDMI_TORCH_PATH"] = "1"
+    if a.deterministic:
+        from fedmi.utils.stats import make_deterministic
+
+        make_deterministic()
 
     from fedmi.engine.data import make_dataset
 
