@@ -144,9 +144,10 @@ def main() -> int:
                     help="lenet (headline) | resnet18 | mobilenet | ... (native HIP engines on GPU)")
     ap.add_argument("--noniid", type=int, default=0,
                     help="non-IID label shards per client (BASELINE config 3: ResNet-18, 2 shards); 0 = strided IID")
-    ap.add_argument("--compress", default="none", choices=["none", "topk", "int8"],
-                    help="-c Y data-plane compression of the FedAvg update")
-    ap.add_argument("--topk-ratio", type=float, default=0.01)
+    ap.add_argument("--compress", default="none", choices=["none", "Y", "topk", "int8"],
+                    help="-c Y data-plane compression of the FedAvg update (Y = the product default, int8 + error "
+                         "feedback)")
+    ap.add_argument("--topk-ratio", type=float, default=0.2)
     ap.add_argument("--compress-warmup", type=int, default=0, help="dense FedAvg rounds before compression starts")
     ap.add_argument("--seed", type=int, default=17, help="model-init / augmentation seed (same on every rank)")
     ap.add_argument("--allreduce", default="auto", choices=["auto", "rccl", "oneshot", "twoshot"],
@@ -373,6 +374,10 @@ def main() -> int:
                        "rounds_coalesced": writer.coalesced},
         **({"transport_select": select} if select else {}),
         "consistency": consistency,
+        **({"native_backend": {"aten_fallbacks": sum(trainer.mode.fallbacks.values()),
+                               "fallback_ops": dict(trainer.mode.fallbacks),
+                               "native_ops": sum(trainer.mode.native_ops.values())}}
+           if getattr(trainer, "mode", None) is not None and hasattr(trainer.mode, "fallbacks") else {}),
         **({"breakdown": breakdown} if breakdown else {}),
         **({"compression": {"kind": args.compress, "bytes_per_round_per_client":
                             agg.compressor.bytes_sent // max(1, agg.compressor.rounds),

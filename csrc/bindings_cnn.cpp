@@ -125,7 +125,15 @@ BNDesc bn_from(const py::dict& d) {
 }
 }  // namespace
 
+void read_conv_stamps(unsigned long long* host, bool clear);
+
 void fedmi_bind_cnn(py::module_& m) {
+  m.def("read_conv_stamps", [](bool clear) {
+    const size_t n = (size_t)FEDMI_STAMP_WGS * FEDMI_STAMP_SLOTS;
+    std::vector<unsigned long long> buf(n, 0ull);
+    read_conv_stamps(buf.data(), clear);
+    return py::bytes(reinterpret_cast<const char*>(buf.data()), n * sizeof(unsigned long long));
+  }, py::arg("clear") = true);
   m.attr("STAT_REP") = STAT_REP;
   m.def("conv_fwd", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats,
                        uintptr_t shift, uintptr_t ws, long ws_floats, uintptr_t res) {

@@ -77,14 +77,15 @@ __global__ __launch_bounds__(256) void dequant_accum_kernel(const signed char* _
 }
 
 // ---------------------------------------------------------------------------
-// Fused error-feedback top-k (the default path): 4 launches (6 from 1 M entries), 2 full passes over the state.
+// Fused error-feedback top-k (the default path): 3 launches (6 from 1 M entries), 2 full passes over the state.
 //
 //   K1 tk_delta_hist   r <- x - g + r (the residual buffer holds d from here on), and a
 //                      histogram of the top 11 bits of |d| (key bits 30..20: exponent + 3
 //                      mantissa bits, each bin ~9 % of magnitude), LDS-privatised per
-//                      workgroup, nonzero bins added to the global histogram.  tk_pick1 (one
-//                      workgroup) then picks the bin b1 holding the k-th largest key and re-zeroes the
-//                      histogram and the append counters for the next call.
+//                      workgroup, nonzero bins added to the global histogram.  The bin b1 holding the
+//                      k-th largest key is picked by every K2 workgroup from that histogram (n < 1 M; a
+//                      one-workgroup tk_pick1 launch from 1 M entries); tk_select2 / tk_pick1 leave the
+//                      histogram and the append counters zero for the next call.
 //   K2 tk_compact1     keys in bins > b1 are selected outright (idx/val appended, r <- 0);
 //                      keys in bin b1 become candidates (index + key appended).  Appends are
 //                      staged in LDS (one pair of LDS atomics per wave per pass) and flushed with
@@ -251,16 +252,35 @@ FEDMI_DEV void tk_select_body(float* __restrict__ r, int c, int nab, unsigned m,
                               const unsigned* __restrict__ ckey, int* __restrict__ idx, float* __restrict__ val,
                               int* overflow, unsigned* h, unsigned* scratch, unsigned* res, int* wcount_p);
 
-template <bool H2>
+// PICK (2-level path, n < kTkThreeLevel): every workgroup finds the boundary bin b1 itself from the global
+// histogram (one 8 KB read + an LDS scan) instead of a one-workgroup tk_pick1 launch in between; workgroup 0
+// publishes (b1, n_above, need) for tk_select2, which also re-zeroes the histogram and the list counters for the
+// next call once every compaction workgroup has read them.
+template <bool H2, bool PICK>
 __global__ __launch_bounds__(256) void tk_compact1_kernel(float* __restrict__ r, long n, TopKState* __restrict__ st,
                                                           int* __restrict__ idx, float* __restrict__ val,
-                                                          int* __restrict__ cidx, unsigned* __restrict__ ckey) {
+                                                          int* __restrict__ cidx, unsigned* __restrict__ ckey, int k) {
   __shared__ int s_si[kTkStage], s_ci[kTkStage];   // 4 x 16 KB of LDS
   __shared__ float s_sv[kTkStage];
   __shared__ unsigned s_ck[kTkStage];
-  __shared__ unsigned h2[H2 ? kTkBins1 : 1];
+  __shared__ unsigned h2[(H2 || PICK) ? kTkBins1 : 1];
   __shared__ int n_s, n_c, b_s, b_c;
-  const unsigned b1 = (unsigned)st->b1;
+  __shared__ unsigned pscr[32], pres[2];
+  unsigned b1;
+  if constexpr (PICK) {
+    for (int i = threadIdx.x; i < kTkBins1; i += 256) h2[i] = st->hist[i];
+    __syncthreads();
+    tk_find_top<256>(h2, kTkBins1, (unsigned)k, pscr, pres);
+    b1 = pres[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->b1 = (int)pres[0];
+      st->n_above = (int)pres[1];
+      st->need = k - (int)pres[1];
+    }
+    __syncthreads();      // h2 is reused as the level-2 histogram only when H2 (never together with PICK)
+  } else {
+    b1 = (unsigned)st->b1;
+  }
   const long stride = (long)gridDim.x * 256;
   if (threadIdx.x == 0) { n_s = 0; n_c = 0; }
   if (H2)
@@ -556,6 +576,10 @@ __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r,
   const int nab = LEVELS == 2 ? st->n_above : st->n_above + st->n_above2;
   const unsigned m = (unsigned)(LEVELS == 2 ? st->need : st->need2);
   tk_select_body<LEVELS>(r, c, nab, m, cidx, ckey, idx, val, &st->pad[0], h, scratch, res, &wcount);
+  if (LEVELS == 2) {      // 2-level path: leave the histogram and the list counters zero for the next call
+    for (int i = threadIdx.x; i < kTkBins1; i += blockDim.x) st->hist[i] = 0u;
+    if (threadIdx.x == 0) { st->out_cnt = 0; st->cand_cnt = 0; }
+  }
 }
 
 int grid_for(long n) {
@@ -596,22 +620,23 @@ void launch_topk_ef(hipStream_t st, const float* x, const float* g, float* resid
     hipLaunchKernelGGL(tk_delta_hist_kernel<true>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
   else
     hipLaunchKernelGGL(tk_delta_hist_kernel<false>, dim3(blocks), dim3(256), 0, st, x, g, residual, n, s, k);
-  hipLaunchKernelGGL(tk_pick1_kernel, dim3(1), dim3(1024), 0, st, s, k);
   // compaction grid cap: 2 workgroups per CU (512) measured 103.5 vs 128 us at 11.2 M entries (2048: 4x the
   // per-workgroup flushes of the staged lists and of the level-2 histogram)
   const int cblocks = (int)std::min<long>(512, std::max<long>(1, (n + 2 * 2048 - 1) / (2 * 2048)));
-  if (n < kTkThreeLevel) {
-    hipLaunchKernelGGL(tk_compact1_kernel<false>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx,
-                       ckey);
+  if (n < kTkThreeLevel) {   // 3 launches: the bin pick runs inside every compaction workgroup
+    hipLaunchKernelGGL((tk_compact1_kernel<false, true>), dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val,
+                       cidx, ckey, k);
     hipLaunchKernelGGL(tk_select2_kernel<2>, dim3(1), dim3(1024), 0, st, residual, s, cidx, ckey, idx, val);
     return;
   }
+  hipLaunchKernelGGL(tk_pick1_kernel, dim3(1), dim3(1024), 0, st, s, k);
   // large n: the boundary bin holds ~1-3 % of the entries -- too many for one workgroup; a second histogram
   // level over the candidates (built by compact1) and a multi-workgroup compaction of them leave a
   // level-3 list of a few hundred for the single-workgroup exact select
   int* cidx2 = cidx + n;                     // second half of the 2n-entry candidate scratch
   unsigned* ckey2 = ckey + n;
-  hipLaunchKernelGGL(tk_compact1_kernel<true>, dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx, ckey);
+  hipLaunchKernelGGL((tk_compact1_kernel<true, false>), dim3(cblocks), dim3(256), 0, st, residual, n, s, idx, val, cidx,
+                     ckey, k);
   hipLaunchKernelGGL(tk_pick2_kernel, dim3(1), dim3(1024), 0, st, s);
   const int c2blocks = (int)std::min<long>(1024, std::max<long>(1, (n / 50 + 2047) / 2048));
   hipLaunchKernelGGL(tk_compact2_kernel, dim3(c2blocks), dim3(256), 0, st, residual, s, cidx, ckey, idx, val, cidx2,

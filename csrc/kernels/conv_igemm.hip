@@ -31,11 +31,38 @@
 // Reference parity: these are the convolution / convolution_backward ops of
 // every zoo model (src/models/resnet.py:14-104 etc.).
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 #include <stdexcept>
 
 #include "common.h"
+
+// diagnostic build (-DFEDMI_STAMPS): s_memtime per conv_tap phase, lane 0 of each workgroup
+// (tools/diag_conv_stamps.py); device code is per translation unit, so conv stamps have their own array
+#ifdef FEDMI_STAMPS
+__device__ unsigned long long fedmi_conv_stamps[FEDMI_STAMP_WGS][FEDMI_STAMP_SLOTS];
+#define CONV_STAMP(i)                                                                       \
+  do {                                                                                      \
+    if (threadIdx.x == 0 && stamp_wg >= 0 && stamp_wg < FEDMI_STAMP_WGS)                    \
+      fedmi_conv_stamps[stamp_wg][i] = __builtin_amdgcn_s_memtime();                        \
+  } while (0)
+#else
+#define CONV_STAMP(i) do {} while (0)
+#endif
+
+void read_conv_stamps(unsigned long long* host, bool clear) {
+#ifdef FEDMI_STAMPS
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(fedmi_conv_stamps), sizeof(fedmi_conv_stamps), 0, hipMemcpyDeviceToHost);
+  if (clear) {
+    static unsigned long long zeros[FEDMI_STAMP_WGS][FEDMI_STAMP_SLOTS];
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(fedmi_conv_stamps), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
+  }
+#else
+  (void)host;
+  (void)clear;
+#endif
+}
 
 namespace {
 
@@ -447,6 +474,24 @@ FEDMI_DEV void glds16(const void* g, bf16* lds_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_base, 16, 0, 0);
 }
 
+// Raw buffer resource over [base, base + bytes): a lane whose byte offset is >= bytes reads zeros (the
+// hardware range check), so halo / tail lanes need no select and no zero block.  gfx9 descriptor word 3.
+constexpr uint32_t BUF_OOB = 0x80000000u;   // a byte offset every resource here is shorter than
+FEDMI_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+// 16 bytes per lane from rsrc + voffset into LDS at lds_base + 16 * lane (M0 = lds_base, uniform)
+FEDMI_DEV void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voffset, bf16* lds_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_base, 16, (int)voffset, 0, 0, 0);
+}
+
+// s_waitcnt vmcnt(N) with expcnt / lgkmcnt left at their maxima (gfx9 encoding: vmcnt bits 3:0 + 15:14)
+template <int N>
+FEDMI_DEV void vmcnt_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
 // fragment of rows [i0, i0+16), k block kk (0/1) from a swizzled [rows][64] image
 FEDMI_DEV bf16x8 frag_sw(const bf16* img, int i0, int kk, int lane) {
   const int row = i0 + (lane & 15);
@@ -457,39 +502,51 @@ FEDMI_DEV bf16x8 frag_sw(const bf16* img, int i0, int kk, int lane) {
 // Three LDS stages, the DMA two K steps ahead (1 workgroup per CU at BN 128, 2 at BN 64).  Measured
 // slower: a two-stage double buffer (one more workgroup per CU), and four stages at BN 128 (128 KiB, the
 // DMA three steps ahead: +5..13 % per conv, profiles/r4_cnn/tap_stages_ab.txt).
-template <int BN>
+// NW waves per workgroup (4 or 8) in an (NW / 2) x 2 grid over the 128 x BN tile: with 8 waves every SIMD
+// holds two waves, so one wave's barrier / LDS / DMA latency is covered by its partner's MFMAs.
+template <int BN, int NW>
 FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict__ wt, bf16* __restrict__ out,
                              float* __restrict__ part, double* __restrict__ stats, const float* __restrict__ shift,
                              const TapGeom& g, const RowMap& rmap, int ksteps_per_split,
                              const bf16* __restrict__ res, const BnSums& bs, int tile, int split) {
   constexpr int BM = 128;
-  constexpr int NA = BM / 32;            // A wave-instructions per stage per wave (8 rows each)
-  constexpr int NB = BN / 32;
+  constexpr int NT = 64 * NW;            // threads
+  constexpr int RW = NW / 2;             // row waves
+  constexpr int WMR = BM / RW;           // rows per wave
+  constexpr int NA = BM / 8 / NW;        // A wave-instructions per stage per wave (8 rows each)
+  constexpr int NB = BN / 8 / NW;
+  static_assert(NA >= 1 && NB >= 1, "tile too small for the wave count");
   constexpr int STAGE = (BM + BN) * 64;  // elements
-  constexpr int TM = 4, TN = BN / 32;    // 16x16 fragments per wave: 64 x BN/2
-  constexpr int NST = 3;
-  constexpr int AHEAD = NST - 1;         // K steps in flight beyond the one being consumed, at most
+  constexpr int TM = WMR / 16, TN = BN / 32;    // 16x16 fragments per wave: WMR x BN/2
+  constexpr int NST = 3;                 // LDS stages: step t being read, t+1 and t+2 in flight
   // the epilogue reuses the stages for the bf16 tile and its partial sums
-  constexpr int EPI = BM * (BN + 8) + 2 * 3 * 256 * 8;
+  constexpr int EPI = BM * (BN + 8) + 2 * 3 * NT * 8;
   __shared__ __attribute__((aligned(16))) bf16 smem[NST * STAGE > EPI ? NST * STAGE : EPI];
 
+  [[maybe_unused]] const int stamp_wg = (int)(blockIdx.x + gridDim.x * blockIdx.z);
+  CONV_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63;
   // uniform (SGPR) wave index: the LDS-DMA destinations (M0) are scalar, no readfirstlane per piece
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = (g.O + BN - 1) / BN;
   const int tile_n = tile % ntn, tile_m = tile / ntn;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * (BN / 2);
+  const int wm0 = (wave >> 1) * WMR, wn0 = (wave & 1) * (BN / 2);
 
   const int ksteps = g.K / 64;
   const int kb = split * ksteps_per_split;
   const int ke = min(ksteps, kb + ksteps_per_split);
 
-  // per-lane DMA sources: row (l >> 3) of each 8-row group, logical chunk kc
+  // per-lane DMA sources: row (l >> 3) of each 8-row group, logical chunk kc.  Operands are read through
+  // buffer resources (the host keeps them < 2 GiB): an A row is valid at tap (r, s) iff bit r * S + s of
+  // its tap mask is set (the input pixel (p*st - pad + r, q*st - pad + s) is inside the image); invalid
+  // rows / filters get an out-of-range offset and land as zeros.
   const int lrow = lane >> 3;
   const int kc = (lane & 7) ^ lrow;
-  long a_off[NA];
-  int a_h[NA], a_w[NA];
+  const __amdgpu_buffer_rsrc_t rin = buf_rsrc(in, (uint32_t)((long)g.N * g.H * g.W * g.C * 2));
+  const __amdgpu_buffer_rsrc_t rwt = buf_rsrc(wt, (uint32_t)((long)g.O * g.K * 2));
+  int a_off[NA];              // element offset of the row's pixel at tap (0, 0) (may be negative: halo)
+  uint64_t a_mask[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     const int m = m0 + (wave * NA + i) * 8 + lrow;
@@ -497,17 +554,19 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
     const uint32_t mm = ok ? m : 0;
     const uint32_t n = fdiv(mm, g.dPQ), pq = mm - n * g.P * g.Q;
     const uint32_t p = fdiv(pq, g.dQ), q = pq - p * g.Q;
-    a_h[i] = ok ? (int)(p * g.st) - g.pad_h : -(1 << 20);   // invalid rows never pass the bounds test
-    a_w[i] = (int)(q * g.st) - g.pad_w;
-    a_off[i] = (((long)n * g.H + a_h[i]) * g.W + a_w[i]) * g.C + kc * 8;
+    const int h0 = (int)(p * g.st) - g.pad_h, w0 = (int)(q * g.st) - g.pad_w;
+    uint64_t mk = 0;
+    for (int r = 0; r < g.R; ++r)
+      for (int x = 0; x < g.S; ++x)
+        if (ok && (unsigned)(h0 + r) < (unsigned)g.H && (unsigned)(w0 + x) < (unsigned)g.W) mk |= 1ull << (r * g.S + x);
+    a_mask[i] = mk;
+    a_off[i] = ((n * g.H + h0) * g.W + w0) * g.C + kc * 8;
   }
-  long b_off[NB];
-  bool b_ok[NB];
+  uint32_t b_off[NB];         // byte offset of the filter row's chunk at k = 0 (BUF_OOB: o >= O)
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int o = n0 + (wave * NB + i) * 8 + lrow;
-    b_ok[i] = o < g.O;
-    b_off[i] = (long)o * g.K + kc * 8;
+    b_off[i] = o < g.O ? (uint32_t)(o * g.K + kc * 8) * 2u : BUF_OOB;
   }
 
   // tap state of the next K step to issue, advanced incrementally (scalar; no per-step division):
@@ -521,22 +580,18 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
     is_s = rs - is_r * g.S;
   }
   auto issue = [&](int stage) {
-    const long tap = ((long)is_r * g.W + is_s) * g.C + is_c0;
-    const long k0 = ((long)is_r * g.S + is_s) * g.C + is_c0;
+    const int rs = is_r * g.S + is_s;
+    const int tap = (is_r * g.W + is_s) * g.C + is_c0;
+    const uint32_t k0b = (uint32_t)(rs * g.C + is_c0) * 2u;
     bf16* As = smem + stage * STAGE;
     bf16* Bs = As + BM * 64;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int h = a_h[i] + is_r, w = a_w[i] + is_s;
-      const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-      const void* src = ok ? (const void*)(in + a_off[i] + tap) : (const void*)g_zero16;
-      glds16(src, As + (wave * NA + i) * 8 * 64);
+      const bool ok = (a_mask[i] >> rs) & 1;
+      blds16(rin, ok ? (uint32_t)(a_off[i] + tap) * 2u : BUF_OOB, As + (wave * NA + i) * 8 * 64);
     }
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const void* src = b_ok[i] ? (const void*)(wt + b_off[i] + k0) : (const void*)g_zero16;
-      glds16(src, Bs + (wave * NB + i) * 8 * 64);
-    }
+    for (int i = 0; i < NB; ++i) blds16(rwt, b_off[i] == BUF_OOB ? BUF_OOB : b_off[i] + k0b, Bs + (wave * NB + i) * 8 * 64);
     is_c0 += 64;
     if (is_c0 == g.C) {
       is_c0 = 0;
@@ -552,25 +607,28 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
 
   // One barrier per K step: wait for this wave's DMA of step t (leaving the up to AHEAD-1 later
   // steps already issued in flight), barrier (step t visible everywhere AND every wave is done
-  // reading step t-1's stage), refill that stage with step t+AHEAD, then MFMAs on step t.
+  // reading step t-1's stage), read every fragment of step t, refill step t-1's stage with step
+  // t+AHEAD, MFMAs on step t.  (Measured slower with 8 waves: a software-pipelined loop that reads step
+  // t+1's fragments into a second register set during step t's MFMAs, +2..8 % per conv -- the partner wave
+  // on the SIMD already covers the LDS latency; profiles/r5_cnn/README.md.)
+  constexpr int AHEAD = NST - 1;
 #pragma unroll
   for (int a = 0; a < AHEAD; ++a)
     if (kb + a < ke) issue(a);
+  CONV_STAMP(1);
   for (int t = kb; t < ke; ++t) {
     const int stg = (t - kb) % NST;
     const int later = min(ke - 1 - t, AHEAD - 1);     // issued steps after t still allowed in flight
-    if (later >= 2) {
-      if constexpr (NA + NB == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    } else if (later == 1) {
-      if constexpr (NA + NB == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (later >= 2) vmcnt_wait<2 * (NA + NB)>();
+    else if (later == 1) vmcnt_wait<NA + NB>();
+    else vmcnt_wait<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+#ifdef FEDMI_STAMPS
+    if (t == kb) CONV_STAMP(2);
+    if (t == kb + (ke - kb) / 2) CONV_STAMP(3);
+#endif
     const bf16* As = smem + stg * STAGE;
     const bf16* Bs = As + BM * 64;
     // every fragment of the step (both 32-deep halves) requested at once, THEN the refill DMA and the
@@ -585,8 +643,6 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
       for (int j = 0; j < TN; ++j) bfr[kk][j] = frag_sw(Bs, wn0 + 16 * j, kk, lane);
     }
     __builtin_amdgcn_sched_barrier(0);
-    // refill the stage step t-1 used with step t+AHEAD (every wave is past step t-1's reads once it
-    // passed this barrier)
     if (t + AHEAD < ke) issue((stg + AHEAD) % NST);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -597,6 +653,7 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[kk][i], bfr[kk][j], acc[i][j]);
   }
   __syncthreads();   // every wave done with the stages (no DMA in flight) before LDS reuse
+  CONV_STAMP(4);
 
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
   // (Combining the splits in-kernel -- the last-arriving split sums the tile's partials and runs this
@@ -617,12 +674,13 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
     float* ws = part + (long)split * g.M * g.O;
     constexpr int C4 = BN / 4;
 #pragma unroll
-    for (int k = 0; k < BM * C4 / 256; ++k) {
-      const int c = tid + k * 256, row = c / C4, c4 = c % C4;
+    for (int k = 0; k < BM * C4 / NT; ++k) {
+      const int c = tid + k * NT, row = c / C4, c4 = c % C4;
       const int m = m0 + row, col = n0 + c4 * 4;
       if (m < g.M && col < g.O)
         *reinterpret_cast<float4*>(ws + (long)m * g.O + col) = *reinterpret_cast<const float4*>(pt + row * PLD + c4 * 4);
     }
+    CONV_STAMP(5);
     return;
   }
   constexpr int CT_LD = BN + 8;
@@ -637,7 +695,7 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
         ct[(wm0 + 16 * i + row_l + e) * CT_LD + wn0 + 16 * j + col_l] = (bf16)acc[i][j][e];
   if (stats != nullptr && res == nullptr) {
     // BN statistics of bf16(y) - shift straight from the accumulators (rows past M masked), the wave's
-    // 4 row groups combined by cross-lane adds, the two row halves of the tile through LDS
+    // 4 row groups combined by cross-lane adds, the RW row parts of the tile through LDS
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = n0 + wn0 + 16 * j + col_l;
@@ -664,12 +722,14 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
   __syncthreads();
   if (stats != nullptr && res == nullptr && tid < 2 * BN) {
     const int q = tid / BN, cl = tid % BN;
-    const float tsum = red[q * BN + cl] + red[(2 + q) * BN + cl];
+    float tsum = 0.f;
+#pragma unroll
+    for (int rw = 0; rw < RW; ++rw) tsum += red[(rw * 2 + q) * BN + cl];
     if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, (double)tsum);
   }
   constexpr int CPR = BN / 8;
-  constexpr int RPT = BM * CPR / 256;      // output rows (8-channel vectors) per thread
-  // DGRAD: BN-backward sums of the producer BN (each thread keeps one 8-channel group: 256 % CPR == 0)
+  constexpr int RPT = BM * CPR / NT;      // output rows (8-channel vectors) per thread
+  // DGRAD: BN-backward sums of the producer BN (each thread keeps one 8-channel group: NT % CPR == 0)
   const bool bsum = bs.rep != nullptr;
   float bq[3][8], bm[3][8], bi[3][8];
   if (bsum) bnsum_coeffs(bs, n0 + (tid % CPR) * 8, n0 + (tid % CPR) * 8 < g.O, bm, bi, bq);
@@ -680,7 +740,7 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
   bool pok[RPT];
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
-    const int c = tid + k * 256, row = c / CPR, cc = c % CPR;
+    const int c = tid + k * NT, row = c / CPR, cc = c % CPR;
     const int m = m0 + row, col = n0 + cc * 8;
     pok[k] = m < g.M && col < g.O;
     pidx[k] = pok[k] ? map_row(rmap, m) * g.O + col : 0;
@@ -704,7 +764,7 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
   }
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
-    const int c = tid + k * 256, row = c / CPR, cc = c % CPR;
+    const int c = tid + k * NT, row = c / CPR, cc = c % CPR;
     if (pok[k]) {
       bf16x8 t = *reinterpret_cast<const bf16x8*>(ct + row * CT_LD + cc * 8);
       if (res != nullptr) {   // fused residual add (pre-activation fwd) / second incoming grad (DGRAD)
@@ -717,24 +777,24 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
     }
   }
   if (bsum) {
-    // [3][256][8] partials behind the ct tile, then one (quantity, channel) per thread -> fp64 replica atomics
+    // [3][NT][8] partials behind the ct tile, then one (quantity, channel) per thread -> fp64 replica atomics
     float* rs = red;
     const int nq = bs.zb ? 3 : 2;
 #pragma unroll
     for (int q = 0; q < 3; ++q)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) rs[(q * 256 + tid) * 8 + j] = bq[q][j];
+      for (int j = 0; j < 8; ++j) rs[(q * NT + tid) * 8 + j] = bq[q][j];
     __syncthreads();
-    for (int e = tid; e < nq * BN; e += 256) {
+    for (int e = tid; e < nq * BN; e += NT) {
       const int q = e / BN, cl = e % BN, grp = cl >> 3, j = cl & 7;
       float s = 0.f;
-      for (int th = grp; th < 256; th += CPR) s += rs[(q * 256 + th) * 8 + j];
+      for (int th = grp; th < NT; th += CPR) s += rs[(q * NT + th) * 8 + j];
       if (n0 + cl < g.O) unsafeAtomicAdd(bs.rep + ((long)(blockIdx.x % bs.reps) * 3 + q) * g.O + n0 + cl, (double)s);
     }
   }
   if (stats != nullptr && res != nullptr) {   // statistics of y = conv + res, from the summed tile
     __syncthreads();
-    constexpr int PARTS = 256 / BN;
+    constexpr int PARTS = NT / BN;
     const int col = tid % BN, prt = tid / BN;
     const int rows = min(BM, g.M - m0);
     const float sh = (shift != nullptr && n0 + col < g.O) ? shift[n0 + col] : 0.f;
@@ -755,15 +815,16 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
       if (n0 + cl < g.O) unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + q) * g.O + n0 + cl, (double)t);
     }
   }
+  CONV_STAMP(5);
 }
 
-template <int BN>
-__global__ __launch_bounds__(256) void conv_tap(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+template <int BN, int NW>
+__global__ __launch_bounds__(64 * NW) void conv_tap(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                 bf16* __restrict__ out, float* __restrict__ part,
                                                 double* __restrict__ stats, const float* __restrict__ shift,
                                                 TapGeom g, RowMap rmap, int ksteps_per_split,
                                                 const bf16* __restrict__ res, BnSums bs) {
-  conv_tap_body<BN>(in, wt, out, part, stats, shift, g, rmap, ksteps_per_split, res, bs, blockIdx.x, blockIdx.z);
+  conv_tap_body<BN, NW>(in, wt, out, part, stats, shift, g, rmap, ksteps_per_split, res, bs, blockIdx.x, blockIdx.z);
 }
 
 // The sub-pixel phases of a stride-2 DGRAD in ONE launch: blockIdx.x walks the phases' tiles in order,
@@ -781,15 +842,15 @@ struct TapMulti {
   int n;
 };
 
-template <int BN>
-__global__ __launch_bounds__(256) void conv_tap_phases(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+template <int BN, int NW>
+__global__ __launch_bounds__(64 * NW) void conv_tap_phases(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                        bf16* __restrict__ out, float* __restrict__ ws,
                                                        TapMulti tm, const bf16* __restrict__ res, BnSums bs) {
   int p = 0;
   while (p + 1 < tm.n && (int)blockIdx.x >= tm.tile0[p + 1]) ++p;
   if ((int)blockIdx.z >= tm.splits[p]) return;
   const bool split = tm.wsoff[p] >= 0;
-  conv_tap_body<BN>(in, wt + tm.woff[p], out, split ? ws + tm.wsoff[p] : nullptr, nullptr, nullptr, tm.g[p],
+  conv_tap_body<BN, NW>(in, wt + tm.woff[p], out, split ? ws + tm.wsoff[p] : nullptr, nullptr, nullptr, tm.g[p],
                     tm.rm[p], tm.kps[p], split ? nullptr : res, split ? BnSums{} : bs,
                     (int)blockIdx.x - tm.tile0[p], blockIdx.z);
 }
@@ -1451,16 +1512,45 @@ static TapGeom make_tap(int N, int H, int W, int C, int O, int P, int Q, int R, 
 
 static int tap_bn(int O) { return O <= 64 ? 64 : 128; }
 
+// waves per conv_tap workgroup: 8 (two per SIMD, default: 8-15 % faster per conv, profiles/r5_cnn/) or 4 (one
+// per SIMD); FEDMI_TAP_WAVES overrides (A/B runs)
+static int tap_waves() {
+  static int w = [] {
+    const char* e = std::getenv("FEDMI_TAP_WAVES");
+    const int v = e ? std::atoi(e) : 8;
+    return v == 8 ? 8 : 4;
+  }();
+  return w;
+}
+
+// conv_tap reads its operands through 32-bit buffer offsets (out-of-range lanes read zeros) and keeps a
+// per-row tap-validity mask of R * S <= 64 bits
+static bool tap_fits(long in_elems, long w_elems, int R, int S) {
+  return in_elems * 2 < (1l << 31) && w_elems * 2 < (1l << 31) && R * S <= 64;
+}
+
 // Split K only to fill one wave of workgroups: conv_tap keeps 1 (BN 128, 96 KiB
 // LDS) or 2 (BN 64) workgroups per CU, and a split costs an fp32 round trip.
+// With 8-wave workgroups a half-filled chip without split-K beats split-K + combine (ResNet-18 l3 forward:
+// 24.7 vs 28.8 us, profiles/r5_cnn/): split only when the tiles fill at most a quarter of one wave of
+// workgroups.  FEDMI_TAP_SPLITS=n forces n splits where a split applies (A/B runs).
+static int tap_split_override() {
+  static int v = [] {
+    const char* e = std::getenv("FEDMI_TAP_SPLITS");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 static int tap_splits(const TapGeom& g, long ws_floats) {
   if (ws_floats <= 0 || g.O > SPLITK_MAX_NC) return 1;
   const int bn = tap_bn(g.O);
   const long tiles = (long)((g.M + 127) / 128) * ((g.O + bn - 1) / bn);
   const long target = (bn == 128 ? 1l : 2l) * num_cus();
   const int ksteps = g.K / 64;
-  if (4 * tiles >= 3 * target || ksteps < 16) return 1;
+  if (4 * tiles > target || ksteps < 16) return 1;
   long sp = std::min<long>((target + tiles / 2) / tiles, ksteps / 8);
+  if (tap_split_override() > 0) sp = std::min<long>(tap_split_override(), ksteps / 8);
   sp = std::min<long>(sp, ws_floats / ((long)g.M * g.O));
   if (sp < 2) return 1;
   const int kps = (int)((ksteps + sp - 1) / sp);
@@ -1509,6 +1599,8 @@ static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const b
                        const float* shift, const RowMap& rm, float* ws, long ws_floats,
                        const bf16* res = nullptr, const BnSums& bs = BnSums{}) {
   if (g.C % 64 || g.O % 8) throw std::invalid_argument("conv_tap: need C % 64 == 0 and O % 8 == 0");
+  if (!tap_fits((long)g.N * g.H * g.W * g.C, (long)g.O * g.K, g.R, g.S))
+    throw std::invalid_argument("conv_tap: operands over 2 GiB or R * S > 64");
   const int BN = tap_bn(g.O);
   const long tiles = (long)((g.M + 127) / 128) * ((g.O + BN - 1) / BN);
   const int ksteps = g.K / 64;
@@ -1521,9 +1613,14 @@ static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const b
   double* tst = part ? nullptr : stats;
   const bf16* trs = part ? nullptr : res;
   if (BN == 128)
-    hipLaunchKernelGGL(conv_tap<128>, grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
+    if (tap_waves() == 8)
+      hipLaunchKernelGGL((conv_tap<128, 8>), grid, dim3(512), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
+    else
+      hipLaunchKernelGGL((conv_tap<128, 4>), grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
+  else if (tap_waves() == 8)
+    hipLaunchKernelGGL((conv_tap<64, 8>), grid, dim3(512), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
   else
-    hipLaunchKernelGGL(conv_tap<64>, grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
+    hipLaunchKernelGGL((conv_tap<64, 4>), grid, dim3(256), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
   if (splits > 1) launch_tap_reduce(st, g, rm, ws, splits, out, stats, shift, res, bs);
 }
 
@@ -1643,14 +1740,22 @@ static void launch_tap_phases(hipStream_t st, const TapPhase* ph, int n, const b
   const PhasePlan pl = plan_tap_phases(ph, n, ws_floats);
   const TapMulti& tm = pl.tm;
   if (tm.n == 0) return;
-  for (int k = 0; k < tm.n; ++k)
+  for (int k = 0; k < tm.n; ++k) {
     if (tm.g[k].C % 64 || tm.g[k].O % 8 || tm.g[k].O != tm.g[0].O)
       throw std::invalid_argument("conv_tap_phases: need C % 64 == 0, O % 8 == 0 and one O");
+    if (!tap_fits((long)tm.g[k].N * tm.g[k].H * tm.g[k].W * tm.g[k].C, (long)tm.g[k].O * tm.g[k].K, tm.g[k].R, tm.g[k].S))
+      throw std::invalid_argument("conv_tap_phases: operands over 2 GiB or R * S > 64");
+  }
   dim3 grid((unsigned)tm.tile0[tm.n], 1, (unsigned)pl.maxsp);
   if (tap_bn(tm.g[0].O) == 128)
-    hipLaunchKernelGGL(conv_tap_phases<128>, grid, dim3(256), 0, st, dy, wd, dx, ws, tm, res, bs);
+    if (tap_waves() == 8)
+      hipLaunchKernelGGL((conv_tap_phases<128, 8>), grid, dim3(512), 0, st, dy, wd, dx, ws, tm, res, bs);
+    else
+      hipLaunchKernelGGL((conv_tap_phases<128, 4>), grid, dim3(256), 0, st, dy, wd, dx, ws, tm, res, bs);
+  else if (tap_waves() == 8)
+    hipLaunchKernelGGL((conv_tap_phases<64, 8>), grid, dim3(512), 0, st, dy, wd, dx, ws, tm, res, bs);
   else
-    hipLaunchKernelGGL(conv_tap_phases<64>, grid, dim3(256), 0, st, dy, wd, dx, ws, tm, res, bs);
+    hipLaunchKernelGGL((conv_tap_phases<64, 4>), grid, dim3(256), 0, st, dy, wd, dx, ws, tm, res, bs);
   for (int k = 0; k < tm.n; ++k)
     if (tm.splits[k] > 1)
       launch_tap_reduce(st, tm.g[k], tm.rm[k], ws + tm.wsoff[k], tm.splits[k], dx, nullptr, nullptr, res, bs);
@@ -1701,7 +1806,7 @@ void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf
   check_shape(s);
   ConvGeom g = make_geom(s);
   g.M = s.N * s.P * s.Q; g.NC = s.O; g.K = s.R * s.S * s.C;
-  if (s.C % 64 == 0) {
+  if (s.C % 64 == 0 && tap_fits((long)s.N * s.H * s.W * s.C, (long)s.O * g.K, s.R, s.S)) {
     const TapGeom t = make_tap(s.N, s.H, s.W, s.C, s.O, s.P, s.Q, s.R, s.S, s.st, s.pad, s.pad);
     launch_tap(st, t, x, wrsc, y, stats, shift, RowMap{}, ws, ws_floats, res);
     return;
@@ -1717,9 +1822,13 @@ void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf
 // add: dx = result + add (a second incoming grad, e.g. the shortcut branch's; != dx) and bs: the
 // producer BN's backward sums taken in the epilogue -- both only on the tap path without empty
 // phases (conv_dgrad_fusable).
+static bool dgrad_tap_ok(const ConvShape& s) {
+  return s.O % 64 == 0 && tap_fits((long)s.N * s.P * s.Q * s.O, (long)s.C * s.R * s.S * s.O, s.R, s.S);
+}
+
 int conv_dgrad_fusable(const ConvShape& s, int has_wd) {
   check_shape(s);
-  if (!has_wd || s.O % 64) return 0;
+  if (!has_wd || !dgrad_tap_ok(s)) return 0;
   TapPhase ph[4];
   const int n = dgrad_tap_phases(s, ph);
   for (int i = 0; i < n; ++i)
@@ -1736,7 +1845,7 @@ void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const
   if (bs && (!bs->rep || !bs->z || !bs->mean || !bs->inv || bs->reps < 1 || (bs->zb && (!bs->meanb || !bs->invb)) ||
              (bs->msc && (bs->y || bs->msc_ld <= 0))))
     throw std::invalid_argument("conv_dgrad: incomplete BN sums descriptor");
-  if (wd != nullptr && s.O % 64 == 0) {   // tap-major path on the dgrad weight image
+  if (wd != nullptr && dgrad_tap_ok(s)) {   // tap-major path on the dgrad weight image
     TapPhase ph[4];
     const int n = dgrad_tap_phases(s, ph);
     if (n > 1) {   // stride 2: the tap phases in one launch, the tap-less parities zeroed below

@@ -27,7 +27,7 @@ from ..utils.metrics import MetricsLog, log
 
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description="fedmi federated client (one GPU)")
-    ap.add_argument("-c", "--compressFlag", help="'Y': gzip gRPC + compressed (top-k) FedAvg updates")
+    ap.add_argument("-c", "--compressFlag", help="'Y': gzip gRPC + compressed FedAvg updates (int8 + error feedback)")
     ap.add_argument("-a", "--address", default="temp", help="listen address host:port (also the checkpoint name)")
     ap.add_argument("-r", "--resume", action="store_true", help="resume from checkpoint/<address>.pth")
     ap.add_argument("--lr", type=float, default=0.1)
@@ -53,8 +53,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--client-index", type=int, default=0)
     ap.add_argument("--num-clients", type=int, default=1)
     ap.add_argument("--compress", default=None, choices=["none", "topk", "int8"],
-                    help="update compression (default: topk when -c Y)")
-    ap.add_argument("--topk-ratio", type=float, default=0.01)
+                    help="update compression (default with -c Y: int8 + error feedback, see "
+                         "fedmi.parallel.compress.DEFAULT_Y)")
+    ap.add_argument("--topk-ratio", type=float, default=0.2)
     ap.add_argument("--compress-warmup", type=int, default=0, help="dense FedAvg rounds before -c Y compression starts")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--root", default=".")
@@ -88,7 +89,7 @@ def main(argv=None) -> int:
         trainer.set_train_data(data.train.subset(shards[a.client_index]))
     backend = a.backend if a.backend != "auto" else ("nccl" if dev.type == "cuda" else "gloo")
     transport = a.transport if a.transport != "auto" else ("auto" if dev.type == "cuda" else "dist")
-    comp_kind = a.compress if a.compress is not None else ("topk" if gzip else "none")
+    comp_kind = a.compress if a.compress is not None else ("Y" if gzip else "none")
     fedavg = FedAvg(compressor=make_compressor(comp_kind, a.topk_ratio, trainer, a.compress_warmup))
     n = trainer.float_state().numel()
     cap = max(4 * n, 16 * (int(n * a.topk_ratio) + 64), n + 4 * (n // 256 + 64))

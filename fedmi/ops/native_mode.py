@@ -30,6 +30,7 @@ max_pool2d_with_indices, sigmoid, mul, mean, slice_backward, bernoulli_, ...).
 from __future__ import annotations
 
 import collections
+import sys
 import os
 import math
 from typing import Optional
@@ -1666,9 +1667,12 @@ class NativeMode(TorchDispatchMode):
                 self.native_ops[str(func)] += 1
                 return out
         if on_gpu:
-            self.fallbacks[str(func)] += 1
             if self.strict:
                 raise RuntimeError(f"native_mode: no native kernel for {func}")
+            if not self.fallbacks[str(func)]:   # never silent: once per op, counted in .fallbacks (bench JSON)
+                print(f"[fedmi native_mode] ATen fallback for {func} (FEDMI_NATIVE_STRICT=1 makes it an error)",
+                      file=sys.stderr, flush=True)
+            self.fallbacks[str(func)] += 1
         return func(*args, **kwargs)
 
 

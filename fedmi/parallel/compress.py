@@ -221,10 +221,19 @@ class Int8Compressor(_EFCompressor):
         x.copy_(self.global_ref)
 
 
+# What ``-c Y`` selects: the compressor that stays within 3 points of dense FedAvg at the fewest bytes on the
+# 8-rank rehearsal (profiles/r5_dataplane/: 3 seeds x 23 rounds) -- int8 + error feedback, a quarter of the dense
+# bytes; top-k needs ~20 % of the entries (40 % of the dense bytes: 8 B per kept entry) to get as close.
+DEFAULT_Y = "int8"
+DEFAULT_TOPK_RATIO = 0.2
+
+
 def make_compressor(kind: Optional[str], ratio: float, trainer, warmup: int = 0):
     if kind in (None, "", "none", "n", "N"):
         return None
-    if kind in ("topk", "Y", "y"):
+    if kind in ("Y", "y"):
+        kind = DEFAULT_Y
+    if kind == "topk":
         return TopKCompressor(trainer, ratio, warmup)
     if kind == "int8":
         return Int8Compressor(trainer, warmup)

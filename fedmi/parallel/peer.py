@@ -16,6 +16,7 @@ GPU (same-device IPC), which is how it is tested on a single-GPU box.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Optional
 
@@ -63,6 +64,10 @@ class PeerAllReduce:
         # shares its GPU (e.g. 3 ranks on 2 GPUs gate all three).  Never taken with one rank per GPU (the
         # production layout).
         self.colocated = agree_any(store, f"{key}/coloc", rank, world, bool(self.comm.colocated)) and world > 1
+        # diagnostics only (tools/bench_peer.py --no-gate): the kernels' own cost without the host gate, as
+        # round 2 measured it before the gate existed -- the barrier timeout still bounds a non-co-scheduled peer
+        if os.environ.get("FEDMI_PEER_GATE", "1") == "0":
+            self.colocated = False
         self._gate_n = 0
         self._gate_failed = False
 

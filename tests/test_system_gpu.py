@@ -27,13 +27,14 @@ def _clients(tmp_path, n, extra=(), transport="peer"):
     return addrs, procs
 
 
-@pytest.mark.parametrize("compress,transport", [(False, "peer"), (True, "peer"), (False, "auto")],
-                         ids=["dense", "topk", "dense-auto"])
+@pytest.mark.parametrize("compress,transport", [(None, "peer"), ("Y", "peer"), ("topk", "peer"), (None, "auto")],
+                         ids=["dense", "c-Y-int8", "topk", "dense-auto"])
 def test_grpc_coordinator_drives_gpu_clients(tmp_path, compress, transport):
-    addrs, procs = _clients(tmp_path, 2, ("-c", "Y") if compress else (), transport=transport)
+    extra = {None: (), "Y": ("-c", "Y"), "topk": ("-c", "Y", "--compress", "topk")}[compress]
+    addrs, procs = _clients(tmp_path, 2, extra, transport=transport)
     try:
         cfg = CoordinatorConfig(clients=addrs, rounds=3, agg="collective", root=str(tmp_path / "srv"),
-                                gzip=compress, train_timeout_s=90, rpc_timeout_s=20, heartbeat_s=0.5)
+                                gzip=compress is not None, train_timeout_s=90, rpc_timeout_s=20, heartbeat_s=0.5)
         coord = Coordinator(cfg)
         coord.run()
         coord.close()

@@ -2,7 +2,7 @@
 """-c Y kernel timings (csrc/kernels/compress.hip) at the LeNet and ResNet-18 state sizes.
 
 For n = 62,006 (LeNet) and 11,173,962 (ResNet-18): device time of the
-error-feedback delta + exact top-k (k = 1 %: the fused 4-launch path ``topk_us``, and one
+error-feedback delta + exact top-k (k = 1 % and 20 % of n, FEDMI_TOPK_RATIOS: the fused path ``topk_us``, and one
 read+write pass over the state for scale ``rw_pass_us``), of the rank-ordered
 scatter of 4 ranks' payloads, of int8 quantisation and of a 4-rank dequant
 accumulate; plus payload bytes vs dense fp32.  One JSON line per size.
@@ -10,6 +10,7 @@ accumulate; plus payload bytes vs dense fp32.  One JSON line per size.
 from __future__ import annotations
 
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -39,9 +40,10 @@ def main() -> int:
     dev = torch.device("cuda", 0)
     S = lambda: native.stream_handle(dev)   # noqa: E731
     out = []
-    for name, n in (("lenet", 62006), ("resnet18", 11173962)):
+    ratios = [float(v) for v in os.environ.get("FEDMI_TOPK_RATIOS", "0.01,0.2").split(",")]
+    for (name, n), ratio in [(p, r) for p in (("lenet", 62006), ("resnet18", 11173962)) for r in ratios]:
         iters = 200 if n < 1e6 else 20
-        k = max(1, int(round(n * 0.01)))
+        k = max(1, int(round(n * ratio)))
         R = 4
         local = torch.randn(n, device=dev)
         glob = torch.randn(n, device=dev)
@@ -86,7 +88,7 @@ def main() -> int:
         s_all = sc.repeat(R)
         t_dq = _time(lambda: nat.dequant_accum(S(), q_all.data_ptr(), s_all.data_ptr(), R, n, acc.data_ptr(), 1.0 / R),
                      iters)
-        rec = {"bench": "compress_kernels", "payload": name, "n": n, "k": k,
+        rec = {"bench": "compress_kernels", "payload": name, "n": n, "k": k, "ratio": ratio,
                "topk_us": round(t_topk, 2), "topk_fresh_update_us": round(t_topk_fresh, 2), "candidates_last": cand,
                "rw_pass_us": round(t_copy, 2), "scatter_ranked_4rank_us": round(t_scatter, 2),
                "quant_int8_us": round(t_q, 2), "dequant_accum_4rank_us": round(t_dq, 2),

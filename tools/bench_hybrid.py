@@ -1,6 +1,7 @@
 """Per-step time of the generic engine on zoo models without a whole-network native engine:
-PyTorch fp32 (MIOpen / rocBLAS / ATen) vs the native aten backend (fedmi.ops.native_mode: every op on
-fedmi's HIP kernels), eager and HIP-graph replayed.
+PyTorch fp32 (MIOpen / rocBLAS / ATen), PyTorch autocast-bf16 (the same-precision vendor baseline:
+MIOpen / hipBLASLt bf16 kernels, mode ``torch-bf16``) vs the native aten backend (fedmi.ops.native_mode:
+every op on fedmi's HIP kernels), eager and HIP-graph replayed.
 
     python tools/bench_hybrid.py [model ...]      -> one JSON line per (model, mode)
 """
@@ -25,12 +26,17 @@ dev = torch.device("cuda", 0)
 data = make_dataset("synthetic-cifar10", device=dev, n_train=128 * 12, n_test=1000, seed=0)
 for name in MODELS:
     init = build_model(name).state_dict()
-    modes = ("fp32", "native-eager", "native-graph-nofuse", "native-graph")
+    modes = ("fp32", "torch-bf16", "native-eager", "native-graph-nofuse", "native-graph")
     if os.environ.get("BENCH_MODES"):
         modes = tuple(os.environ["BENCH_MODES"].split(","))
     for mode in modes:
-        tr = TorchTrainer(name, data, dev, TrainerConfig(seed=1), init_state=init, hybrid=(mode != "fp32"))
+        tr = TorchTrainer(name, data, dev, TrainerConfig(seed=1), init_state=init, hybrid=mode.startswith("native"))
         tr.use_graph = "graph" in mode
+        if mode == "torch-bf16":
+            def run(x, m=tr.model):
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    return m(x).float()
+            tr._run = run
         if tr.mode is not None:
             tr.mode.fuse = not mode.endswith("nofuse")     # BN -> ReLU / ReLU-bwd -> BN-bwd fusion
         tr.model.train()

@@ -36,6 +36,7 @@ def _worker(rank, world, path, iters, q):
     torch.cuda.set_device(dev)
     store = dist.FileStore(path, world)
     pc = PeerAllReduce(rank, world, 4 * max(SIZES.values()) + 4096, store, tag="bench", device=dev)
+    pc.comm.set_timeout_ms(float(os.environ.get("FEDMI_BENCH_PEER_TIMEOUT_MS", "30000")))
     res = []
     for name, n in SIZES.items():
         x = torch.randn(n, device=dev)
@@ -62,7 +63,14 @@ def main() -> int:
     ap.add_argument("--world", type=int, nargs="+", default=[2, 4])
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--no-gate", action="store_true",
+                    help="ranks sharing a GPU skip the host gate before each collective (FEDMI_PEER_GATE=0): the "
+                         "kernels' own barrier + copy cost, the round-2 measurement; a 2 s barrier timeout bounds "
+                         "a peer whose kernel is not co-scheduled")
     a = ap.parse_args()
+    if a.no_gate:
+        os.environ["FEDMI_PEER_GATE"] = "0"
+        os.environ["FEDMI_BENCH_PEER_TIMEOUT_MS"] = "2000"
     lines = []
     for world in a.world:
         ctx = mp.get_context("spawn")
@@ -80,7 +88,7 @@ def main() -> int:
             us = max(g[1][i][3] for g in got)
             rec = {"bench": "peer_allreduce", "world": world, "payload": name, "numel": n, "bytes": 4 * n,
                    "algo": algo, "us_per_call": round(us, 2), "alg_GBps": round(4 * n / us / 1e3, 2),
-                   "gpus": torch.cuda.device_count(), "errors": errs}
+                   "gpus": torch.cuda.device_count(), "errors": errs, "host_gate": not a.no_gate}
             print(json.dumps(rec), flush=True)
             lines.append(rec)
     if a.out:
