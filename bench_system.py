@@ -87,7 +87,7 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=30, help="timed rounds")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="lenet")
-    ap.add_argument("-c", "--compressFlag", default=None, help="'Y': gzip control channel + top-k updates")
+    ap.add_argument("-c", "--compressFlag", default=None, help="'Y': gzip control channel + int8 error-feedback updates")
     ap.add_argument("--transport", default="auto", choices=["auto", "peer", "dist"])
     ap.add_argument("--agg", default="collective", choices=["collective", "grpc"])
     ap.add_argument("--gpus", type=int, default=None, help="GPUs to spread clients over (default: all visible)")

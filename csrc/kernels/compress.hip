@@ -576,10 +576,12 @@ __global__ __launch_bounds__(1024) void tk_select2_kernel(float* __restrict__ r,
   const int nab = LEVELS == 2 ? st->n_above : st->n_above + st->n_above2;
   const unsigned m = (unsigned)(LEVELS == 2 ? st->need : st->need2);
   tk_select_body<LEVELS>(r, c, nab, m, cidx, ckey, idx, val, &st->pad[0], h, scratch, res, &wcount);
-  if (LEVELS == 2) {      // 2-level path: leave the histogram and the list counters zero for the next call
+  // leave the level-1 histogram and list counters zero for the next call, on BOTH paths: the 2-level path has
+  // no pick launch that would reset them, so a 3-level call followed by a 2-level one must not leave its
+  // counters behind (the 2-level compaction would append past the end of idx / cidx)
+  if (LEVELS == 2)
     for (int i = threadIdx.x; i < kTkBins1; i += blockDim.x) st->hist[i] = 0u;
-    if (threadIdx.x == 0) { st->out_cnt = 0; st->cand_cnt = 0; }
-  }
+  if (threadIdx.x == 0) { st->out_cnt = 0; st->cand_cnt = 0; }
 }
 
 int grid_for(long n) {

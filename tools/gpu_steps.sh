@@ -1,7 +1,7 @@
 #!/bin/bash
 # Run named GPU steps, each under its own time limit, logging to gpurun_out/<tag>/.
-# A step that fails normally (rc 1/2: a failing test) does not stop the script;
-# a fault, abort, segfault or time limit (rc >= 124) ends it right there.
+# Any failing step ends the script right there: a failing GPU test may be a device fault (an illegal
+# address surfaces as an ordinary pytest failure), and nothing more runs on the GPU after a fault.
 #   usage: bash tools/gpu_steps.sh <tag> <name> <seconds> <command> [<name> <seconds> <command> ...]
 set -u
 tag=$1; shift
@@ -16,7 +16,7 @@ while [ $# -ge 3 ]; do
   rc=$?
   echo "=== $name rc=$rc wall=$(( $(date +%s) - start ))s" | tee -a "$out/steps.txt"
   tail -5 "$out/$name.log"
-  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+  if [ $rc -ne 0 ]; then
     echo "=== stopping after $name (rc=$rc)" | tee -a "$out/steps.txt"
     exit $rc
   fi
