@@ -97,7 +97,7 @@ def main(argv=None) -> int:
                          peer_timeout_ms=1000.0 * a.collective_timeout, model_numel=n)
     agent = ClientAgent(trainer, a.address, root=a.root, agg=a.agg, group=group,
                         fedavg=fedavg, batch_size=a.batch_size, local_shard=a.noniid > 0, resume=a.resume,
-                        metrics=MetricsLog(a.metrics), verbose=not a.quiet)
+                        metrics=MetricsLog(a.metrics, background=True), verbose=not a.quiet)
     server, port = serve_client(agent, a.address, gzip=gzip)
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())

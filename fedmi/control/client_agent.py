@@ -405,6 +405,7 @@ class ClientAgent(P.TrainerServicer):
 
     def close(self) -> None:
         self.writer.close()
+        self.metrics.close()
 
 
 def serve_client(agent: ClientAgent, address: str, gzip: bool = False, max_workers: int = 10):

@@ -28,6 +28,28 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 N_TRAIN, N_TEST, BATCH = 50000, 10000, 128
 
 
+def _eval_batch_bn(tr) -> None:
+    """Diagnostic (PyTorch engines): evaluate the global model with batch-statistics BN instead of the averaged
+    running statistics (train-mode BN at momentum 0, so the running buffers are left as they are)."""
+    from torch.nn.modules.batchnorm import _BatchNorm
+
+    m = tr.model
+    bns = [b for b in m.modules() if isinstance(b, _BatchNorm)]
+    mom = [b.momentum for b in bns]
+    for b in bns:
+        b.momentum = 0.0
+    orig_eval = m.eval
+    m.eval = lambda: m.train()
+    try:
+        with torch.no_grad():
+            tr.evaluate()
+    finally:
+        m.eval = orig_eval
+        for b, v in zip(bns, mom):
+            b.momentum = v
+        m.eval()
+
+
 def _run_seed(a, seed, data, dev, out) -> None:
     from fedmi.engine import build_trainer
     from fedmi.engine.base import TrainerConfig
@@ -68,13 +90,17 @@ def _run_seed(a, seed, data, dev, out) -> None:
                 for b, v in zip(tr.int_state(), ints):
                     b.copy_(v)
                 tr.after_aggregate()
-        clients[0].evaluate()
+        if a.bn_eval == "batch":
+            _eval_batch_bn(clients[0])
+        else:
+            clients[0].evaluate()
         ev = clients[0].eval_stats()
         torch.cuda.synchronize() if dev.type == "cuda" else None
         rec = {"round": rnd, "engine": a.engine, "model": a.model, "clients": W, "lr": a.lr, "seed": seed,
+               "data": a.data,
                "deterministic": bool(a.deterministic),
                "augment": not a.no_augment, "graph": not a.no_graph,
-               "split": f"noniid-{a.noniid}" if a.noniid else "strided-iid",
+               "split": f"noniid-{a.noniid}" if a.noniid else "strided-iid", "bn_eval": a.bn_eval,
                "train_loss": [round(s.loss, 4) for s in tstats], "train_acc": [round(s.acc, 2) for s in tstats],
                "test_loss": round(ev.loss, 4), "test_acc": round(ev.acc, 2),
                "finite": bool(torch.isfinite(mean).all()), "round_s": round(time.perf_counter() - t0, 3)}
@@ -93,6 +119,8 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--engine", choices=["native", "fp32", "bf16"], default="native",
                     help="bf16: PyTorch autocast bf16 (torch's own mixed precision of the same model)")
+    ap.add_argument("--data", default="synthetic-cifar10",
+                    help="dataset spec (fedmi.engine.data.make_dataset): synthetic-cifar10 | synthetic-cifar10-easy | ...")
     ap.add_argument("--n-train", type=int, default=N_TRAIN)
     ap.add_argument("--n-test", type=int, default=N_TEST)
     ap.add_argument("--lr", type=float, default=0.1)
@@ -104,7 +132,11 @@ def main() -> int:
     ap.add_argument("--deterministic", action="store_true",
                     help="PyTorch engines: deterministic algorithms (MIOpen / rocBLAS deterministic kernels), so two "
                          "runs of the fp32 reference agree and a parity gap is the engine's, not reference noise")
+    ap.add_argument("--bn-eval", choices=["running", "batch"], default="running",
+                    help="batch: evaluate the global model with batch-statistics BN (diagnostic, PyTorch engines)")
     a = ap.parse_args()
+    if a.bn_eval == "batch" and a.engine == "native":
+        ap.error("--bn-eval batch needs a PyTorch engine (fp32 / bf16)")
     if a.engine in ("fp32", "bf16"):
         os.environ["FEDMI_TORCH_PATH"] = "1"
     if a.deterministic:
@@ -115,7 +147,7 @@ def main() -> int:
     from fedmi.engine.data import make_dataset
 
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
-    data = make_dataset("synthetic-cifar10", device=dev, n_train=a.n_train, n_test=a.n_test, seed=0)
+    data = make_dataset(a.data, device=dev, n_train=a.n_train, n_test=a.n_test, seed=0)
     seeds = [int(v) for v in a.seeds.split(",")] if a.seeds else [a.seed]
     out = open(a.out, "w") if a.out else None
     for seed in seeds:
