@@ -206,12 +206,21 @@ class ClientAgent(P.TrainerServicer):
                 self._busy_gen = None
 
     def _start_train(self, request, context, meta: dict, gen: int, t_enter: float = 0.0):
-        self._fence(meta, context)
         term = int(meta.get(META_TERM, "0") or 0)
+        first_of_term = term > self.max_term and self.max_term > 0
+        self._fence(meta, context)
         rank, world = int(request.rank), int(request.world)
         if world <= 0 or not 0 <= rank < world:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"bad rank/world {rank}/{world}")
         rnd = int(meta.get(META_ROUND, self.round + 1) or self.round + 1)
+        if self.agg == "collective" and first_of_term and rnd <= self.round:
+            # a newly promoted coordinator resumes from its replica, which can trail the rounds this client
+            # committed under the previous term (a lease keeps running until the new term reaches it): report
+            # the committed round instead of re-running it; the coordinator pulls rank 0's model of that round
+            # and continues after it (once per term, so a coordinator that cannot reach that model rolls back)
+            self._lease_trailer(context, [], -1)
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION,
+                          f"round {rnd} of term {term}: this client already committed round {self.round}")
         lease = max(1, int(meta.get(META_LEASE, "1") or 1)) if self.agg == "collective" else 1
         t = Timer()
         rec0 = {"role": "client", "address": self.address, "rank": rank, "world": world, "agg": self.agg,

@@ -418,7 +418,10 @@ class Coordinator:
         else:
             # an aborted lease: the rounds before the failure are committed (the round counter now covers them),
             # the failing round is the one after them
-            done = [row for row in self._lease_rows(lease_stats, rnd, self.round) if row[0] <= self.round]
+            # (rows with rank 0's stats only: a committed round this call did not run -- a client fencing a new
+            # term off rounds it committed under the previous one -- is not this coordinator's round)
+            done = [row for row in self._lease_rows(lease_stats, rnd, self.round)
+                    if row[0] <= self.round and row[1] is not None]
             per = [(r_, True, lo, ac, tr_) for r_, lo, ac, tr_ in done]
             per.append((max(rnd, self.round + 1), False, None, None, t_done))
         for r_, ok_r, loss, acc, t_r in per:
