@@ -294,12 +294,13 @@ def test_family_step_native_only(gpu_device, name):
     assert abs(losses["native"] - losses["fp32"]) < 0.05 * losses["fp32"] + 0.02, losses
 
 
-# RegNetY_400MF's first epoch at lr 0.02 is chaotic on BOTH engines (it blows up to a loss of 7-15 and the
-# fp32 seeds alone end between 48 and 100 % accuracy, profiles/r3_zoo/README.md "Learning parity"): the
-# first-epoch comparison is meaningless there, so it is compared at lr 0.005, where both engines are stable
+# Against the deterministic fp32 reference (conftest.deterministic_reference).  RegNetY_400MF stays at lr 0.005:
+# at 0.02 its first epoch diverges on BOTH engines even with a reproducible reference (epoch losses native
+# 6.54 / 3.47 / 2.42 vs fp32 8.13 / 4.12 / 2.46, round-5 GPU run) -- the first-epoch gap measures that chaos,
+# not the engine, and the third epochs agree within 2 %
 @pytest.mark.parametrize("name,lr", [("densenet_cifar", 0.02), ("SENet18", 0.02), ("DPN26", 0.02),
                                      ("ResNeXt29_2x64d", 0.02), ("EfficientNetB0", 0.02), ("RegNetY_400MF", 0.005)])
-def test_family_trains_like_fp32(gpu_device, name, lr):
+def test_family_trains_like_fp32(gpu_device, deterministic_reference, name, lr):
     """Three short epochs, graph-replayed: the trajectory tracks the fp32 engine (round 1's hybrid
     EfficientNet / RegNetY went NaN under replay)."""
     from fedmi.engine import build_trainer

@@ -10,21 +10,13 @@ pytestmark = [pytest.mark.gpu, pytest.mark.slow, pytest.mark.timeout(420)]
 
 
 @pytest.fixture(autouse=True)
-def deterministic_reference():
-    """The fp32 reference runs PyTorch's deterministic algorithms (deterministic MIOpen solvers, no benchmark
-    search): run to run it is bit-stable, so a parity gap below is the native engine's and not reference noise
-    (VERDICT r4 weak #3 -- the one-sided bounds of round 4 came from a non-deterministic reference)."""
-    from fedmi.utils.stats import make_deterministic
-
-    prev = (torch.are_deterministic_algorithms_enabled(), torch.backends.cudnn.deterministic,
-            torch.backends.cudnn.benchmark)
-    make_deterministic()
+def _deterministic(deterministic_reference):
+    """Every test here compares against the deterministic fp32 reference (conftest.deterministic_reference)."""
     yield
-    torch.use_deterministic_algorithms(prev[0])
-    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev[1], prev[2]
 
 
-def _run(engine: str, rounds: int, monkeypatch, lr: float = 0.02, augment: bool = True, seed: int = 17):
+def _run(engine: str, rounds: int, monkeypatch, lr: float = 0.02, augment: bool = True, seed: int = 17,
+         clients: int = 2, data_spec: str = "synthetic-cifar10", n_train: int = 50000, n_test: int = 10000):
     if engine == "fp32":
         monkeypatch.setenv("FEDMI_TORCH_PATH", "1")
     else:
@@ -34,11 +26,12 @@ def _run(engine: str, rounds: int, monkeypatch, lr: float = 0.02, augment: bool 
     from fedmi.engine.data import contiguous_schedule, label_shard_indices, make_dataset
 
     dev = torch.device("cuda", 0)
-    data = make_dataset("synthetic-cifar10", device=dev, n_train=50000, n_test=10000, seed=0)
+    data = make_dataset(data_spec, device=dev, n_train=n_train, n_test=n_test, seed=0)
     cfg = TrainerConfig(seed=seed, lr=lr, augment=augment)
-    shards = label_shard_indices(data.train.y.cpu().numpy(), 2, 2, seed=0)
+    W = clients
+    shards = label_shard_indices(data.train.y.cpu().numpy(), W, 2, seed=0)
     clients, init = [], None
-    for r in range(2):
+    for r in range(W):
         tr = build_trainer("resnet18", data, dev, cfg, init_state=init)
         if init is None:
             init = {k: v.detach().cpu().clone() for k, v in tr.state_dict().items()}
@@ -52,8 +45,8 @@ def _run(engine: str, rounds: int, monkeypatch, lr: float = 0.02, augment: bool 
         train_accs.append([tr.train_stats().acc for tr in clients])
         with torch.no_grad():
             mean = torch.stack([tr.float_state() for tr in clients]).mean(0)
-            ints = [torch.div(a + b, 2, rounding_mode="floor")
-                    for a, b in zip(clients[0].int_state(), clients[1].int_state())]
+            ints = [torch.div(sum(bs), W, rounding_mode="floor")
+                    for bs in zip(*[[b.clone() for b in tr.int_state()] for tr in clients])]
             for tr in clients:
                 tr.float_state().copy_(mean)
                 for b, v in zip(tr.int_state(), ints):
@@ -91,3 +84,21 @@ def test_native_tracks_fp32_at_reference_lr_without_augmentation(monkeypatch):
     for a, b in zip(nat_tr[-1], ref_tr[-1]):
         assert a > 50.0 and b > 50.0, (nat_tr, ref_tr)
         assert abs(a - b) < 10.0, (nat_tr, ref_tr)
+
+
+def test_config3_scale_global_model_learns(monkeypatch):
+    """Config 3 at its client count: 8 clients x 2 label shards (each client sees ~2 classes), reduced size
+    (16k training images, 2k test, 12 rounds, lr 0.02), on the high-contrast synthetic set.  On the default
+    low-contrast set every engine's averaged model -- deterministic fp32 PyTorch included -- stays at chance for
+    20 rounds at every lr from 0.002 to 0.1 (profiles/r5_noniid/README.md); here FedAvg's global model rises
+    clearly above chance in both engines, and the native engine's late-round accuracy stays within 10 points of
+    the deterministic fp32 reference (both engines are run-to-run deterministic, so this pins one outcome)."""
+    kw = dict(clients=8, data_spec="synthetic-cifar10-easy", n_train=16000, n_test=2000, lr=0.02)
+    rounds = 12
+    nat, _ = _run("native", rounds, monkeypatch, **kw)
+    ref, _ = _run("fp32", rounds, monkeypatch, **kw)
+    print("native", nat, "fp32", ref)
+    assert max(nat) > 20.0 and max(ref) > 20.0, (nat, ref)            # chance is 10 %
+    late = rounds // 2
+    mn, mr = sum(nat[late:]) / (rounds - late), sum(ref[late:]) / (rounds - late)
+    assert abs(mn - mr) < 10.0, (mn, mr, nat, ref)
