@@ -93,8 +93,11 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=None, help="GPUs to spread clients over (default: all visible)")
     ap.add_argument("--no-backup", action="store_true")
     ap.add_argument("--ckpt-sync-every", type=int, default=0)
-    ap.add_argument("--lease", type=int, default=16,
-                    help="rounds per StartTrain (round lease); 1 = one StartTrain per round (reference cadence)")
+    ap.add_argument("--lease", type=int, default=64,
+                    help="at most this many rounds per StartTrain (round lease); 1 = one StartTrain per round "
+                         "(reference cadence)")
+    ap.add_argument("--lease-s", type=float, default=0.25,
+                    help="target lease duration (s); 0 = always --lease rounds (server.py --lease-s)")
     ap.add_argument("--keep", default=None, help="keep the run directory here")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--startup-timeout", type=float, default=300.0)
@@ -130,7 +133,7 @@ def main() -> int:
         prim = _spawn([str(ROOT / "server.py"), "--p", "y", "--backupPort", str(bport), "--clients", ",".join(addrs),
                        "--rounds", str(total), "--agg", a.agg, "--root", str(run / "srv"), "--train-timeout", "600",
                        "--metrics", str(run / "primary.jsonl"), "--ckpt-sync-every", str(a.ckpt_sync_every),
-                       "--lease", str(a.lease), *comp],
+                       "--lease", str(a.lease), "--lease-s", str(a.lease_s), *comp],
                       run, run / "primary.log", env)
         procs.append(prim)
         deadline = time.time() + 600 + 60 * total
@@ -210,6 +213,7 @@ def main() -> int:
         "ms_per_round": round(1e3 / rps, 4),
         "config": {"model": a.model, "agg": a.agg, "transport": a.transport, "compress": a.compressFlag,
                    "backup": not a.no_backup, "ckpt_sync_every": a.ckpt_sync_every, "lease": a.lease,
+                   "lease_s": a.lease_s,
                    "batch": 128, "eval_per_round": True, "data": "synthetic CIFAR-shaped 50k/10k"},
         "phases_ms": phases,
         "last_round": {k: last_rec[0].get(k) for k in ("train_loss", "train_acc", "test_loss", "test_acc")}

@@ -46,9 +46,13 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--ckpt-sync-every", type=int, default=0,
                     help="rank 0 uploads THAT round's checkpoint every k rounds (0: pipelined by one round, "
                          "synchronous on the final round)")
-    ap.add_argument("--lease", type=int, default=16,
-                    help="collective mode: rounds per StartTrain (round lease; the gRPC round trip is paid once per "
-                         "lease); 1 = one StartTrain per round like the reference")
+    ap.add_argument("--lease", type=int, default=64,
+                    help="collective mode: at most this many rounds per StartTrain (round lease; the gRPC round trip "
+                         "is paid once per lease); 1 = one StartTrain per round like the reference")
+    ap.add_argument("--lease-s", type=float, default=0.25,
+                    help="target duration of one lease (s): the lease length follows the measured round time "
+                         "(fast rounds: long leases; rounds slower than this: one round per StartTrain); 0 = always "
+                         "--lease rounds")
     return ap
 
 
@@ -61,6 +65,7 @@ def main(argv=None) -> int:
                             rpc_timeout_s=a.rpc_timeout, heartbeat_s=a.heartbeat, store_host=a.store_host,
                             store_port=a.store_port, min_clients=a.min_clients, ckpt_sync_every=a.ckpt_sync_every,
                             ckpt_fetch_interval_s=a.ckpt_fetch_interval, lease_rounds=max(1, a.lease),
+                            lease_s=max(0.0, a.lease_s),
                             backup_address=f"{a.backupAddress}:{a.backupPort}")
     metrics = MetricsLog(a.metrics)
     stop = threading.Event()

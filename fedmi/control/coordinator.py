@@ -66,10 +66,15 @@ class CoordinatorConfig:
     # collective mode with fedmi clients: the per-round model upload leaves the StartTrain reply and a
     # background fetcher pulls rank 0's newest checkpoint at most this often (<= 0: upload every reply)
     ckpt_fetch_interval_s: float = 0.05
-    # collective mode: one StartTrain runs this many consecutive rounds on the clients (x-fedmi-lease), so the
-    # fan-out / gather round trip is paid once per lease; 1 = one RPC per round (the reference's cadence; always
-    # the case for agg="grpc")
-    lease_rounds: int = 16
+    # collective mode: one StartTrain runs up to this many consecutive rounds on the clients (x-fedmi-lease), so
+    # the fan-out / gather round trip is paid once per lease; 1 = one RPC per round (the reference's cadence;
+    # always the case for agg="grpc")
+    lease_rounds: int = 64
+    # target duration of one lease (s): the lease length follows the measured round time, so fast rounds
+    # (LeNet, ~10 ms) amortise the round trip over ~25 rounds while slow rounds (ResNet-18, ~0.9 s) keep one
+    # StartTrain per round and the coordinator reacts to joins / failures at that cadence.  The first lease is
+    # one round (the round time is not known yet).  0: always lease_rounds
+    lease_s: float = 0.25
 
 
 def fedavg_state_dicts(sds: List[dict], weights: Optional[List[float]] = None) -> "OrderedDict[str, torch.Tensor]":
@@ -137,6 +142,7 @@ class Coordinator:
             self._backup = P.TrainerStub(P.make_channel(cfg.backup_address))
         self._tracker: Optional[threading.Thread] = None
         self.round_times: List[float] = []
+        self._round_s: Optional[float] = None     # smoothed seconds per round (sizes the lease, cfg.lease_s)
         self.installed_epoch = ck.read_epoch(self.model_path) or -1
         self._persist_cv = threading.Condition()
         self._to_persist: Optional[bytes] = None
@@ -176,7 +182,10 @@ class Coordinator:
         a ``ckpt_sync_every`` boundary (those rounds upload their own checkpoint)."""
         if self.cfg.agg != "collective":
             return 1
-        k = max(1, min(int(self.cfg.lease_rounds), self.cfg.rounds - rnd + 1))
+        k = int(self.cfg.lease_rounds)
+        if self.cfg.lease_s > 0:
+            k = 1 if self._round_s is None else min(k, max(1, int(self.cfg.lease_s / max(self._round_s, 1e-6))))
+        k = max(1, min(k, self.cfg.rounds - rnd + 1))
         if self.cfg.ckpt_sync_every > 0:
             k = min(k, self.cfg.ckpt_sync_every - (rnd - 1) % self.cfg.ckpt_sync_every)
         return k
@@ -412,6 +421,9 @@ class Coordinator:
             self.round = max([end] + client_rounds)
         dt = t.ms()
         self.round_times.append(dt / lease)
+        if ok:   # per-round wall time, smoothed (the lease length follows it)
+            per_s = dt / lease / 1e3
+            self._round_s = per_s if self._round_s is None else 0.7 * self._round_s + 0.3 * per_s
         t_done = time.time()
         if ok:
             per = [(r_, True, lo, ac, tr_) for r_, lo, ac, tr_ in self._lease_rows(lease_stats, rnd, end)]

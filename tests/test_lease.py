@@ -61,7 +61,7 @@ def _spawn_fakes(tmp_path, n):
 def _overhead_per_round(addrs, root, lease: int, rounds: int = 64) -> float:
     if True:
         cfg = CoordinatorConfig(clients=addrs, rounds=rounds, agg="collective", root=str(root),
-                                rpc_timeout_s=10, train_timeout_s=30, heartbeat_s=5.0, lease_rounds=lease,
+                                rpc_timeout_s=10, train_timeout_s=30, heartbeat_s=5.0, lease_rounds=lease, lease_s=0,
                                 ckpt_fetch_interval_s=0)
         coord = Coordinator(cfg)
         coord.run_round()                        # warm the channels (first call carries the connection setup)
@@ -101,7 +101,7 @@ def test_aborted_lease_advances_to_rank0_committed_round(tmp_path):
     fakes, servers, addrs = _serve(2)
     try:
         cfg = CoordinatorConfig(clients=addrs, rounds=40, agg="collective", root=str(tmp_path / "srv"),
-                                rpc_timeout_s=10, train_timeout_s=30, heartbeat_s=5.0, lease_rounds=8,
+                                rpc_timeout_s=10, train_timeout_s=30, heartbeat_s=5.0, lease_rounds=8, lease_s=0,
                                 ckpt_fetch_interval_s=0)
         coord = Coordinator(cfg)
         assert coord.run_round() and coord.round == 8
@@ -167,7 +167,7 @@ def test_lease_with_real_clients(tmp_path):
             wait_heartbeat(a, timeout=120)
         metrics = MetricsLog(tmp_path / "primary.jsonl")
         cfg = CoordinatorConfig(clients=addrs, rounds=12, agg="collective", root=str(tmp_path / "srv"),
-                                train_timeout_s=120, rpc_timeout_s=10, heartbeat_s=0.2, lease_rounds=5)
+                                train_timeout_s=120, rpc_timeout_s=10, heartbeat_s=0.2, lease_rounds=5, lease_s=0)
         coord = Coordinator(cfg, metrics=metrics)
         calls = []
         orig = coord._meta
@@ -191,3 +191,33 @@ def test_lease_with_real_clients(tmp_path):
     finally:
         for p in procs:
             stop_proc(p)
+
+
+def test_lease_length_follows_round_time(tmp_path):
+    """cfg.lease_s: the first StartTrain covers one round (the round time is unknown), then the lease covers
+    about lease_s of rounds -- ~10 ms rounds get long leases (capped at lease_rounds), rounds slower than lease_s
+    keep one StartTrain per round (the coordinator reacts at that cadence)."""
+    def leases(work_s, lease_s, cap, rounds):
+        fakes, servers, addrs = _serve(1, work_s=work_s)
+        try:
+            cfg = CoordinatorConfig(clients=addrs, rounds=rounds, agg="collective", root=str(tmp_path / f"s{work_s}"),
+                                    rpc_timeout_s=10, train_timeout_s=30, heartbeat_s=5.0, lease_rounds=cap,
+                                    lease_s=lease_s, ckpt_fetch_interval_s=0)
+            coord = Coordinator(cfg)
+            seen = []
+            orig = coord._meta
+            coord._meta = lambda rnd, live, lease=1: (seen.append(lease), orig(rnd, live, lease))[1]
+            while coord.round < rounds:
+                assert coord.run_round()
+            coord.close()
+            return seen
+        finally:
+            for s in servers:
+                s.stop(grace=0)
+
+    fast = leases(0.005, 0.1, 64, 120)              # ~5-6 ms rounds: ~16-20 rounds per lease
+    assert fast[0] == 1 and all(8 <= k <= 20 for k in fast[2:-1]), fast
+    capped = leases(0.002, 1.0, 12, 60)             # a long target is capped at lease_rounds
+    assert capped[0] == 1 and max(capped) == 12, capped
+    slow = leases(0.03, 0.02, 64, 6)                # rounds slower than the target: one round per StartTrain
+    assert slow == [1] * 6, slow

@@ -46,7 +46,7 @@ def main() -> int:
         for n in a.clients:
             for lease in a.leases:
                 cfg = CoordinatorConfig(clients=addrs[:n], rounds=a.rounds, agg="collective",
-                                        root=str(tmp / f"s{n}_{lease}"), lease_rounds=lease, ckpt_fetch_interval_s=0,
+                                        root=str(tmp / f"s{n}_{lease}"), lease_rounds=lease, lease_s=0, ckpt_fetch_interval_s=0,
                                         heartbeat_s=5.0, rpc_timeout_s=10, train_timeout_s=30)
                 with contextlib.redirect_stdout(io.StringIO()):
                     c = Coordinator(cfg)
