@@ -421,9 +421,11 @@ class Coordinator:
             self.round = max([end] + client_rounds)
         dt = t.ms()
         self.round_times.append(dt / lease)
-        if ok:   # per-round wall time, smoothed (the lease length follows it)
+        if ok:   # per-round wall time (the lease length follows it): a faster round is taken at once (the first
+            # rounds carry group setup and warm-up), a slower one is smoothed in
             per_s = dt / lease / 1e3
-            self._round_s = per_s if self._round_s is None else 0.7 * self._round_s + 0.3 * per_s
+            self._round_s = (per_s if self._round_s is None or per_s < self._round_s
+                             else 0.7 * self._round_s + 0.3 * per_s)
         t_done = time.time()
         if ok:
             per = [(r_, True, lo, ac, tr_) for r_, lo, ac, tr_ in self._lease_rows(lease_stats, rnd, end)]
