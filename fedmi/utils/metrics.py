@@ -78,7 +78,12 @@ class MetricsLog:
                     return
                 batch = list(self._q)
                 self._q.clear()
-            lines = [json.dumps(r, default=float) for r in batch]
+            lines = []
+            for r in batch:
+                try:
+                    lines.append(json.dumps(r, default=float))
+                except (TypeError, ValueError) as e:   # never let one bad record stop the writer
+                    lines.append(json.dumps({"event": "metrics_error", "error": str(e)[:200], "ts": r.get("ts")}))
             with self._lock:
                 for line in lines:
                     self._emit(line)
