@@ -1510,7 +1510,15 @@ static TapGeom make_tap(int N, int H, int W, int C, int O, int P, int Q, int R, 
   return g;
 }
 
-static int tap_bn(int O) { return O <= 64 ? 64 : 128; }
+// conv_tap tile width: 128 columns (1 workgroup per CU: 96 KiB of LDS stages) or 64 (2 per CU); FEDMI_TAP_BN=64
+// forces the narrow tile for every O (A/B runs)
+static int tap_bn(int O) {
+  static const int force = [] {
+    const char* e = std::getenv("FEDMI_TAP_BN");
+    return e ? std::atoi(e) : 0;
+  }();
+  return (O <= 64 || force == 64) ? 64 : 128;
+}
 
 // waves per conv_tap workgroup: 8 (two per SIMD, default: 8-15 % faster per conv, profiles/r5_cnn/) or 4 (one
 // per SIMD); FEDMI_TAP_WAVES overrides (A/B runs)
