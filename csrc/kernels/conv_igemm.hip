@@ -1510,15 +1510,20 @@ static TapGeom make_tap(int N, int H, int W, int C, int O, int P, int Q, int R, 
   return g;
 }
 
-// conv_tap tile width: 128 columns (1 workgroup per CU: 96 KiB of LDS stages) or 64 (2 per CU); FEDMI_TAP_BN=64
-// forces the narrow tile for every O (A/B runs)
-static int tap_bn(int O) {
+// conv_tap tile width: 128 columns (96 KiB of LDS stages, 1 workgroup per CU) while the 128-wide tiles fill the
+// chip; 64 (72 KiB, 2 per CU) for O <= 64 and for problems whose 128-wide tiles would leave CUs idle (ResNet-18 l3 /
+// l4: 128 / 64 tiles -> 256 / 128; -19 % / -8 % per conv, while l2's 256 tiles stay faster at 128: +7 % at 64,
+// profiles/r5_cnn/).  FEDMI_TAP_BN=64|128 forces one width (A/B runs).  m_tiles: 128-row tiles of the problem.
+static int tap_bn_for(int O, long m_tiles) {
   static const int force = [] {
     const char* e = std::getenv("FEDMI_TAP_BN");
     return e ? std::atoi(e) : 0;
   }();
-  return (O <= 64 || force == 64) ? 64 : 128;
+  if (O <= 64) return 64;
+  if (force == 64 || force == 128) return force;
+  return m_tiles * ((O + 127) / 128) < num_cus() ? 64 : 128;
 }
+static int tap_bn(const TapGeom& g) { return tap_bn_for(g.O, (g.M + 127) / 128); }
 
 // waves per conv_tap workgroup: 8 (two per SIMD, default: 8-15 % faster per conv, profiles/r5_cnn/) or 4 (one
 // per SIMD); FEDMI_TAP_WAVES overrides (A/B runs)
@@ -1552,7 +1557,7 @@ static int tap_split_override() {
 
 static int tap_splits(const TapGeom& g, long ws_floats) {
   if (ws_floats <= 0 || g.O > SPLITK_MAX_NC) return 1;
-  const int bn = tap_bn(g.O);
+  const int bn = tap_bn(g);
   const long tiles = (long)((g.M + 127) / 128) * ((g.O + bn - 1) / bn);
   const long target = (bn == 128 ? 1l : 2l) * num_cus();
   const int ksteps = g.K / 64;
@@ -1609,7 +1614,7 @@ static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const b
   if (g.C % 64 || g.O % 8) throw std::invalid_argument("conv_tap: need C % 64 == 0 and O % 8 == 0");
   if (!tap_fits((long)g.N * g.H * g.W * g.C, (long)g.O * g.K, g.R, g.S))
     throw std::invalid_argument("conv_tap: operands over 2 GiB or R * S > 64");
-  const int BN = tap_bn(g.O);
+  const int BN = tap_bn(g);
   const long tiles = (long)((g.M + 127) / 128) * ((g.O + BN - 1) / BN);
   const int ksteps = g.K / 64;
   const int sp = tap_splits(g, ws_floats);
@@ -1680,6 +1685,7 @@ struct PhasePlan {
   int idx[MAX_TAP_PHASES];   // TapPhase index of each planned phase
   int maxsp;
   long ws_need;
+  int bn;                    // tile width of the one launch (all phases share O)
 };
 
 static PhasePlan plan_tap_phases(const TapPhase* ph, int n, long ws_cap) {
@@ -1687,12 +1693,17 @@ static PhasePlan plan_tap_phases(const TapPhase* ph, int n, long ws_cap) {
   TapMulti& tm = pl.tm;
   long tiles[MAX_TAP_PHASES], total = 0;
   int ks[MAX_TAP_PHASES];
-  int bn = 0;
+  long m_tiles = 0;
+  for (int i = 0; i < n; ++i)
+    if (!ph[i].empty) m_tiles += (ph[i].g.M + 127) / 128;
+  int bn = 64;
+  for (int i = 0; i < n; ++i)
+    if (!ph[i].empty) { bn = tap_bn_for(ph[i].g.O, m_tiles); break; }
+  pl.bn = bn;
   for (int i = 0; i < n; ++i) {
     if (ph[i].empty) continue;
     const int k = tm.n++;
     pl.idx[k] = i;
-    bn = tap_bn(ph[i].g.O);
     tiles[k] = (long)((ph[i].g.M + 127) / 128) * ((ph[i].g.O + bn - 1) / bn);
     ks[k] = ph[i].g.K / 64;
     tm.splits[k] = 1;
@@ -1755,7 +1766,7 @@ static void launch_tap_phases(hipStream_t st, const TapPhase* ph, int n, const b
       throw std::invalid_argument("conv_tap_phases: operands over 2 GiB or R * S > 64");
   }
   dim3 grid((unsigned)tm.tile0[tm.n], 1, (unsigned)pl.maxsp);
-  if (tap_bn(tm.g[0].O) == 128)
+  if (pl.bn == 128)
     if (tap_waves() == 8)
       hipLaunchKernelGGL((conv_tap_phases<128, 8>), grid, dim3(512), 0, st, dy, wd, dx, ws, tm, res, bs);
     else
