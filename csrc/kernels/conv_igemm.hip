@@ -1561,10 +1561,9 @@ static int tap_splits(const TapGeom& g, long ws_floats) {
   const long tiles = (long)((g.M + 127) / 128) * ((g.O + bn - 1) / bn);
   const long target = (bn == 128 ? 1l : 2l) * num_cus();
   const int ksteps = g.K / 64;
-  // below 40 K steps the split's fp32 round trip and combine launch cost more than the idle CUs (ResNet-18
-  // layer-4 stride-2 forward, 36 steps on 128 tiles: 18.5 us unsplit vs 20.8 split in 4; l4's 72 steps still
-  // gain: 28.7 vs 32.2, profiles/r5_cnn/)
-  if (4 * tiles > target || ksteps < 40) return 1;
+  // (a 40-step threshold saved 2.4 us on ResNet-18's layer-4 stride-2 forward but moved EfficientNetB0's
+  // 3-epoch trajectory outside its parity bound -- profiles/r5_cnn/splits/; kept at 16)
+  if (4 * tiles > target || ksteps < 16) return 1;
   long sp = std::min<long>((target + tiles / 2) / tiles, ksteps / 8);
   if (tap_split_override() > 0) sp = std::min<long>(tap_split_override(), ksteps / 8);
   sp = std::min<long>(sp, ws_floats / ((long)g.M * g.O));

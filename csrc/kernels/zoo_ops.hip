@@ -627,16 +627,41 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const void* a, int a_d
   }
 }
 
-// the slab sums of 64 channels per block (4 lanes per channel, combined in order), then per channel: the BN
-// forward finalize (fin.mode 1), the BN backward coefficients (2), a direct store (3), or acc += sums (0)
+// the slab sums of kFinCB channels per block, 256 / kFinCB lanes per channel (a lane's slab loads all in flight:
+// one memory latency, where 4 lanes per channel walked the slabs in ~slabs / 32 dependent rounds), both sums in
+// the same pass, lanes combined by a fixed-order LDS tree (deterministic); then per channel: the BN forward
+// finalize (fin.mode 1), the BN backward coefficients (2), a direct store (3), or acc += sums (0)
+constexpr int kFinCB = 16;
 __global__ __launch_bounds__(256) void rows_fin_kernel(const float* part, int slabs, int C, int two, float* acc,
                                                        float* acc2, BnFin fin) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const float t1 = ordered_slab_sum(part, slabs, 2LL * C, c, c < C);
+  constexpr int L = 256 / kFinCB;
+  __shared__ float red[2][256];
+  const int l = threadIdx.x / kFinCB, el = threadIdx.x % kFinCB;
+  const int c = blockIdx.x * kFinCB + el;
+  const bool ok = c < C;
+  const long long pitch = 2LL * C;
+  float v1 = 0.f, v2 = 0.f;
+  if (ok) {
+#pragma unroll 4
+    for (int b = l; b < slabs; b += L) {
+      v1 += part[(long long)b * pitch + c];
+      if (two) v2 += part[(long long)b * pitch + C + c];
+    }
+  }
+  red[0][threadIdx.x] = v1;
+  red[1][threadIdx.x] = v2;
   __syncthreads();
-  const float t2 = two ? ordered_slab_sum(part + C, slabs, 2LL * C, c, c < C) : 0.f;
+#pragma unroll
+  for (int sstep = L / 2; sstep >= 1; sstep /= 2) {
+    if (l < sstep) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + sstep * kFinCB];
+      red[1][threadIdx.x] += red[1][threadIdx.x + sstep * kFinCB];
+    }
+    __syncthreads();
+  }
   if (fin.ctr && blockIdx.x == 0 && threadIdx.x == 0) fin.ctr[0] += 1;
-  if ((threadIdx.x >> 6) || c >= C) return;
+  if (l != 0 || !ok) return;
+  const float t1 = red[0][el], t2 = two ? red[1][el] : 0.f;
   if (fin.mode == 1) bn_fwd_fin(fin, c, t1, t2);
   else if (fin.mode == 2) bn_bwd_fin(fin, c, t1, t2);
   else if (fin.mode == 3) rstore(fin.out, fin.out_dt, c, fin.out_scale * (fin.two ? t2 : t1));
@@ -1459,7 +1484,7 @@ static void rows_launch(hipStream_t st, const void* a, int a_dt, long long lda, 
   else
     hipLaunchKernelGGL(reduce_rows_kernel<4>, grid, dim3(256), 0, st, a, a_dt, lda, b, b_dt, ldb, shift, C, M, op, part,
                        f, f_dt, ldf, thr);
-  hipLaunchKernelGGL(rows_fin_kernel, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, st, part, slabs, C,
+  hipLaunchKernelGGL(rows_fin_kernel, dim3((unsigned)((C + kFinCB - 1) / kFinCB)), dim3(256), 0, st, part, slabs, C,
                      op != RD_SUM ? 1 : 0, acc, acc2, fin);
   check_hip(hipGetLastError(), what);
 }

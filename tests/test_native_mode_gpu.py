@@ -311,6 +311,9 @@ def test_family_trains_like_fp32(gpu_device, deterministic_reference, name, lr):
     init = build_model(name).state_dict()
     res = {}
     for kind in ("native", "fp32"):
+        # the same RNG stream for both engines (EfficientNet's drop-connect / dropout masks), independent of the
+        # tests that ran before in this process
+        torch.manual_seed(1234)
         tr = (build_trainer(name, data, gpu_device, cfg, init_state=init) if kind == "native"
               else TorchTrainer(name, data, gpu_device, cfg, init_state=init))
         if kind == "native":
