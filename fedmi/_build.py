@@ -47,8 +47,7 @@ HEADERS = sorted(CSRC.rglob("*.h"))
 
 # build variants: the module name carries the variant (csrc/bindings.cpp FEDMI_MODULE); an A/B build adds
 # its -D switch here for one experiment and is removed with the losing code
-VARIANTS = {"": [], "stamps": ["-DFEDMI_STAMPS", "-DFEDMI_MODULE=_fedmi_native_stamps"],
-            "ab": ["-DFEDMI_MODULE=_fedmi_native_ab"]}
+VARIANTS = {"": [], "stamps": ["-DFEDMI_STAMPS", "-DFEDMI_MODULE=_fedmi_native_stamps"]}
 
 
 def ext_path(variant: str = "") -> Path:
