@@ -42,6 +42,19 @@ void launch_conv_pack_multi(hipStream_t, const PackItem*, int);
 void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int, int, int);
 long conv_wgrad_ws_floats(const ConvShape&);
 void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int, int, int);
+struct SgdPackConv {
+  long off;
+  bf16* wr;
+  bf16* wd;
+  int O, Cw, C, R, S, st, pad;
+};
+struct SgdPackPlan {
+  std::vector<char> table;
+  int n_entries, n_blocks, lds_bytes;
+};
+SgdPackPlan build_sgd_pack_plan(const SgdPackConv*, int, const long*, int);
+void launch_sgd_pack(hipStream_t, const void*, int, int, int, float*, const float*, float*, float, float, float, float,
+                     int, int);
 
 struct BNDesc {
   const double* stats; const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
@@ -167,6 +180,33 @@ void fedmi_bind_cnn(py::module_& m) {
     check("dgrad_pack_multi");
   });
   m.def("conv_fd_ws_floats", [](const py::tuple& shp) { return conv_fd_ws_floats(shape_from(shp)); });
+  // fused SGD + weight images: convs (off, wr, wd, O, Cw, C, R, S, stride, pad) inside the flat master and flat
+  // segments (off, len) -> (table bytes for device memory, entries, workgroups, LDS bytes)
+  m.def("sgd_pack_plan", [](const py::list& convs, const py::list& segs) {
+    std::vector<SgdPackConv> cv;
+    for (const auto& it : convs) {
+      const py::tuple t = it.cast<py::tuple>();
+      if (t.size() != 10) throw std::invalid_argument("sgd_pack_plan conv: (off, wr, wd, O, Cw, C, R, S, stride, pad)");
+      cv.push_back(SgdPackConv{t[0].cast<long>(), P<bf16>(t[1].cast<uintptr_t>()), P<bf16>(t[2].cast<uintptr_t>()),
+                               t[3].cast<int>(), t[4].cast<int>(), t[5].cast<int>(), t[6].cast<int>(),
+                               t[7].cast<int>(), t[8].cast<int>(), t[9].cast<int>()});
+    }
+    std::vector<long> sg;
+    for (const auto& it : segs) {
+      const py::tuple t = it.cast<py::tuple>();
+      if (t.size() != 2) throw std::invalid_argument("sgd_pack_plan segment: (off, len)");
+      sg.push_back(t[0].cast<long>());
+      sg.push_back(t[1].cast<long>());
+    }
+    const SgdPackPlan p = build_sgd_pack_plan(cv.data(), (int)cv.size(), sg.data(), (int)(sg.size() / 2));
+    return py::make_tuple(py::bytes(p.table.data(), p.table.size()), p.n_entries, p.n_blocks, p.lds_bytes);
+  });
+  m.def("sgd_pack", [](uintptr_t st, uintptr_t table, int n_entries, int n_blocks, int lds_bytes, uintptr_t p,
+                       uintptr_t g, uintptr_t b, float lr, float mom, float wd, float damp, int nesterov, int first) {
+    launch_sgd_pack(S(st), reinterpret_cast<const void*>(table), n_entries, n_blocks, lds_bytes, P<float>(p),
+                    P<const float>(g), P<float>(b), lr, mom, wd, damp, nesterov, first);
+    check("sgd_pack");
+  });
   m.def("conv_pack_multi", [](uintptr_t st, const py::list& items) {
     std::vector<PackItem> v;
     for (const auto& it : items) {

@@ -144,4 +144,17 @@ FEDMI_DEV void bnsum_coeffs(const BnSums& bs, int c0, bool ok, float (*bm)[8], f
   }
 }
 
+// torch.optim.SGD on one element (momentum buffer b): d = g + wd * p, b = m * b + (1 - dampening) * d (d on the
+// first step), d = nesterov ? d + m * b : b, p -= lr * d.  sgd_flat_kernel and the fused SGD + weight-image pack
+// (sgd_pack_kernel) both use it, so the two paths are bit-identical.
+FEDMI_DEV void sgd_elem(float& p, float g, float& b, float lr, float m, float wd, float dampening, int nesterov,
+                        int first) {
+  float d = g + wd * p;
+  if (m != 0.f) {
+    b = first ? d : m * b + (1.f - dampening) * d;
+    d = nesterov ? d + m * b : b;
+  }
+  p -= lr * d;
+}
+
 }  // namespace fedmi

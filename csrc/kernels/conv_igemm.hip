@@ -32,6 +32,7 @@
 // every zoo model (src/models/resnet.py:14-104 etc.).
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 #include <stdexcept>
@@ -1136,6 +1137,151 @@ __global__ __launch_bounds__(256) void dgrad_pack_kernel(DPackTable t) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused SGD step + weight images (the CNN engines' per-step tail): one launch updates every parameter of the
+// flat fp32 master (torch.optim.SGD with momentum / weight decay, fedmi::sgd_elem -- bit-identical to
+// sgd_flat_kernel) and, for each dense conv, writes the forward image wr[o][r][s][c] and the DGRAD phase
+// images wd[c][i][j][o] from the UPDATED values while they are still in LDS.  The unfused tail read the fp32
+// weights three times (sgd_flat, conv_pack_multi, dgrad_pack) in 3-4 launches.
+// Workgroup = one conv block of 64 filters x cb input channels (dgrad_pack_kernel's tiling: the image rows
+// wd[c][i][j][o0:o0+64] are 128-B runs, the forward rows wr[o][rs][c0:c0+cb] 32-B runs) or SP_SEG elements of
+// a flat segment (BatchNorm affine, classifier, depthwise filters: SGD only).  The table lives in device
+// memory (built once per engine: all pointers are fixed), sorted by first workgroup.
+// ---------------------------------------------------------------------------
+constexpr int SP_SEG = 2048;   // flat-segment elements per workgroup (8 per thread)
+struct SgdPackEntry {
+  long off;                    // element offset into the flat params / grads / momentum
+  bf16* wr;                    // kind 0: forward image [O][R][S][C] (nullptr: none)
+  bf16* wd[4];                 // kind 0: DGRAD phase images (nph of them)
+  int kind;                    // 0: conv weight [O][Cw][R][S]; 1: flat segment of O elements
+  int O, Cw, C, R, S, cb, nph, step;
+  int blk0;                    // first workgroup of this entry
+  int r0[4], s0[4], nr[4], ns[4];
+};
+
+template <int RU>
+__global__ __launch_bounds__(256) void sgd_pack_kernel(const SgdPackEntry* __restrict__ tab, int n,
+                                                       float* __restrict__ P, const float* __restrict__ G,
+                                                       float* __restrict__ B, float lr, float mom, float wdecay,
+                                                       float damp, int nesterov, int first) {
+  extern __shared__ float tile_[];   // [64][cb * R*S + 1] (conv blocks), sized by the launch
+  const int bid = blockIdx.x;
+  int lo = 0, hi = n - 1;            // last entry with blk0 <= bid (workgroup-uniform)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].blk0 <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const SgdPackEntry& e = tab[lo];
+  const int b = bid - e.blk0;
+  const int tid = threadIdx.x;
+  if (e.kind == 1) {                 // flat segment: all loads of the chunk in flight, then update + store
+    constexpr int U = SP_SEG / 256;
+    const long base = e.off + (long)b * SP_SEG;
+    const long end = e.off + e.O;
+    float pv[U], gv[U], bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = base + tid + 256 * u;
+      const bool ok = i < end;
+      pv[u] = ok ? P[i] : 0.f;
+      gv[u] = ok ? G[i] : 0.f;
+      bv[u] = ok ? B[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = base + tid + 256 * u;
+      if (i < end) {
+        fedmi::sgd_elem(pv[u], gv[u], bv[u], lr, mom, wdecay, damp, nesterov, first);
+        P[i] = pv[u];
+        B[i] = bv[u];
+      }
+    }
+    return;
+  }
+  const int CB = e.cb, RS = e.R * e.S;
+  const int ncb = (e.C + CB - 1) / CB;
+  const int o0 = (b / ncb) * 64, c0 = (b % ncb) * CB;
+  const int cw = max(0, min(CB, e.Cw - c0));                // real input channels of this block
+  const int span = CB * RS, ld = span + 1, live = cw * RS;
+  const int lane = tid & 63, wave = tid >> 6;
+  // SGD on rows o0..o0+63 (wave w: rows w, w+4, ..): row o's channels [c0, c0+cw) are cw*RS contiguous floats
+  // at a wave-uniform base; updated values -> LDS, channels past Cw as zeros.  8 rows x 3 row chunks x 3 operands
+  // in flight per lane (RU = 4 rows per pass: 2 measured the same, 8 18-28 % slower -- its VGPRs cost occupancy;
+  // profiles/r5_cnn/sgdpack/).
+  for (int k0 = 0; k0 < 16; k0 += RU) {
+    for (int f0 = lane; f0 < span; f0 += 64 * 3) {
+      float pv[RU][3], gv[RU][3], bv[RU][3];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int o = o0 + wave + 4 * (k0 + u);
+        const long rb = e.off + ((long)o * e.Cw + c0) * RS;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int f = f0 + 64 * q;
+          const bool ok = o < e.O && f < live;
+          pv[u][q] = ok ? P[rb + f] : 0.f;
+          gv[u][q] = ok ? G[rb + f] : 0.f;
+          bv[u][q] = ok ? B[rb + f] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int o = o0 + wave + 4 * (k0 + u);
+        const long rb = e.off + ((long)o * e.Cw + c0) * RS;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int f = f0 + 64 * q;
+          if (o < e.O && f < live) {
+            fedmi::sgd_elem(pv[u][q], gv[u][q], bv[u][q], lr, mom, wdecay, damp, nesterov, first);
+            P[rb + f] = pv[u][q];
+            B[rb + f] = bv[u][q];
+          }
+          if (f < span) tile_[(wave + 4 * (k0 + u)) * ld + f] = pv[u][q];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // DGRAD phase images (dgrad_pack_kernel's write loop per phase)
+  const int o = o0 + lane;
+  for (int ph = 0; ph < e.nph; ++ph) {
+    const int nr = e.nr[ph], ns = e.ns[ph], r0 = e.r0[ph], s0 = e.s0[ph], taps = nr * ns;
+    bf16* wd = e.wd[ph];
+    for (int idx = wave; idx < CB * taps; idx += 4) {
+      const int ci = idx / taps, ij = idx - ci * taps;
+      const int i = ij / ns, j = ij - i * ns;
+      const int c = c0 + ci;
+      if (c >= e.C || o >= e.O) continue;
+      const int r = r0 + e.step * (nr - 1 - i), sx = s0 + e.step * (ns - 1 - j);
+      wd[(((long)c * nr + i) * ns + j) * e.O + o] = (bf16)tile_[lane * ld + ci * RS + r * e.S + sx];
+    }
+  }
+  // forward image rows wr[o][rs][c0 : c0 + cwr) (cwr: 8 / 16 at cb 16 since C % 8 == 0; 4 at cb 4)
+  if (e.wr != nullptr) {
+    const int cwr = min(CB, e.C - c0);
+    for (int q = tid; q < 64 * RS; q += 256) {
+      const int ol = q / RS, rs = q - ol * RS;
+      if (o0 + ol >= e.O) continue;
+      bf16* dst = e.wr + ((long)(o0 + ol) * RS + rs) * e.C + c0;
+      const float* src = tile_ + ol * ld + rs;
+      if (cwr == 4) {
+        bf16x4 t;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = (bf16)src[k * RS];
+        *reinterpret_cast<bf16x4*>(dst) = t;
+      } else {
+        for (int v0 = 0; v0 < cwr; v0 += 8) {
+          bf16x8 t;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) t[k] = (bf16)src[(v0 + k) * RS];
+          *reinterpret_cast<bf16x8*>(dst + v0) = t;
+        }
+      }
+    }
+  }
+}
+
 // dW[o][c][r][s] (+)= sum_z ws[z][o][(r*S + s)*C + c]     (c < Cw)
 // Block = one output channel o x 64 input channels, all R*S taps, 4 split groups:
 // each wave reads 256 contiguous bytes per (tap, split), the groups combine in
@@ -2114,6 +2260,77 @@ void launch_dgrad_pack_multi(hipStream_t st, const DPackItem* items, int n) {
     }
     hipLaunchKernelGGL(dgrad_pack_kernel, dim3(blk), dim3(256), 64 * (t.cb * max_rs + 1) * sizeof(float), st, t);
   }
+}
+
+// Fused SGD + weight images (sgd_pack_kernel): the host builds the table once per engine (convs first, then the
+// flat segments, in workgroup order); the caller copies `table` to device memory and launches with it.
+struct SgdPackConv {
+  long off;          // element offset of the fp32 weight [O][Cw][R][S] in the flat master
+  bf16* wr;          // forward image [O][R][S][C] (nullptr: none)
+  bf16* wd;          // DGRAD image, phases concatenated (nullptr: none; needs O % 64 == 0)
+  int O, Cw, C, R, S, st, pad;
+};
+struct SgdPackPlan {
+  std::vector<char> table;
+  int n_entries, n_blocks, lds_bytes;
+};
+
+SgdPackPlan build_sgd_pack_plan(const SgdPackConv* convs, int nc, const long* segs, int nseg) {
+  std::vector<SgdPackEntry> v;
+  int blk = 0, lds = 0;
+  for (int k = 0; k < nc; ++k) {
+    const SgdPackConv& c = convs[k];
+    if (c.C % 8 || c.C < c.Cw || c.Cw < 1 || c.O < 1 || c.R * c.S > 49 || (c.wd && c.O % 64))
+      throw std::invalid_argument("sgd_pack: unsupported conv (C % 8, C >= Cw, R*S <= 49, O % 64 with a DGRAD image)");
+    SgdPackEntry e{};
+    e.kind = 0; e.off = c.off; e.wr = c.wr;
+    e.O = c.O; e.Cw = c.Cw; e.C = c.C; e.R = c.R; e.S = c.S; e.step = c.st;
+    // input channels per block: about 144 floats per filter row (3x3: 16, 1x1: 128), 4 for windows past 3x3
+    e.cb = c.R * c.S > 9 ? 4 : c.R * c.S > 4 ? DP_CB : c.R * c.S > 1 ? 32 : 128;
+    if (c.wd) {
+      ConvShape s{};
+      s.N = 1; s.H = 8; s.W = 8; s.P = 4; s.Q = 4;   // spatial sizes only gate empty phases (launch_dgrad_pack_multi)
+      s.C = c.C; s.Cw = c.Cw; s.O = c.O; s.R = c.R; s.S = c.S; s.st = c.st; s.pad = c.pad;
+      TapPhase ph[4];
+      const int np = dgrad_tap_phases(s, ph);
+      for (int i = 0; i < np; ++i) {
+        if (ph[i].empty) continue;
+        e.wd[e.nph] = c.wd + ph[i].img_off;
+        e.r0[e.nph] = ph[i].r0; e.s0[e.nph] = ph[i].s0; e.nr[e.nph] = ph[i].nr; e.ns[e.nph] = ph[i].ns;
+        ++e.nph;
+      }
+    }
+    e.blk0 = blk;
+    blk += ((c.O + 63) / 64) * ((c.C + e.cb - 1) / e.cb);
+    lds = std::max(lds, (int)(64 * (e.cb * c.R * c.S + 1) * sizeof(float)));
+    v.push_back(e);
+  }
+  for (int k = 0; k < nseg; ++k) {
+    const long off = segs[2 * k], len = segs[2 * k + 1];
+    if (len <= 0) continue;
+    for (long s0 = 0; s0 < len; s0 += (1l << 30)) {   // entries count O in 32 bits
+      SgdPackEntry e{};
+      e.kind = 1; e.off = off + s0; e.O = (int)std::min<long>(len - s0, 1l << 30);
+      e.blk0 = blk;
+      blk += (e.O + SP_SEG - 1) / SP_SEG;
+      v.push_back(e);
+    }
+  }
+  if (v.empty()) throw std::invalid_argument("sgd_pack: empty plan");
+  SgdPackPlan p;
+  p.table.resize(v.size() * sizeof(SgdPackEntry));
+  std::memcpy(p.table.data(), v.data(), p.table.size());
+  p.n_entries = (int)v.size();
+  p.n_blocks = blk;
+  p.lds_bytes = lds;
+  return p;
+}
+
+void launch_sgd_pack(hipStream_t st, const void* table, int n_entries, int n_blocks, int lds_bytes, float* P,
+                     const float* G, float* B, float lr, float m, float wd, float dampening, int nesterov, int first) {
+  if (n_entries <= 0 || n_blocks <= 0) return;
+  hipLaunchKernelGGL(sgd_pack_kernel<4>, dim3((unsigned)n_blocks), dim3(256), lds_bytes, st,
+                     static_cast<const SgdPackEntry*>(table), n_entries, P, G, B, lr, m, wd, dampening, nesterov, first);
 }
 
 

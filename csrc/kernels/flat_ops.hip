@@ -22,25 +22,16 @@ __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, co
     const float* gg = reinterpret_cast<const float*>(&gv);
     float* bb = reinterpret_cast<float*>(&bv);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float d = gg[j] + wd * pp[j];
-      if (m != 0.f) {
-        bb[j] = first ? d : m * bb[j] + (1.f - dampening) * d;
-        d = nesterov ? d + m * bb[j] : bb[j];
-      }
-      pp[j] -= lr * d;
-    }
+    for (int j = 0; j < 4; ++j) fedmi::sgd_elem(pp[j], gg[j], bb[j], lr, m, wd, dampening, nesterov, first);
     reinterpret_cast<float4*>(p)[i] = pv;
     reinterpret_cast<float4*>(buf)[i] = bv;
   }
   // tail
   for (long i = (n4 << 2) + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float d = g[i] + wd * p[i];
-    if (m != 0.f) {
-      buf[i] = first ? d : m * buf[i] + (1.f - dampening) * d;
-      d = nesterov ? d + m * buf[i] : buf[i];
-    }
-    p[i] -= lr * d;
+    float pv = p[i], bv = buf[i];
+    fedmi::sgd_elem(pv, g[i], bv, lr, m, wd, dampening, nesterov, first);
+    p[i] = pv;
+    buf[i] = bv;
   }
 }
 

@@ -31,6 +31,7 @@ resident, sized for max(train batch, eval batch) rows.
 from __future__ import annotations
 
 import dataclasses
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional
 
@@ -535,6 +536,14 @@ class CNNNativeTrainer(LocalTrainer):
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self.round_idx = 0
         self.pack()
+        # the step's tail in ONE launch: SGD on the flat master + every conv's forward / DGRAD image from the
+        # updated weights (conv.SgdPack; FEDMI_SGD_PACK=0: sgd_flat, then the two pack launches)
+        self._sgdpack = None
+        if os.environ.get("FEDMI_SGD_PACK", "1") != "0":
+            self._sgdpack = conv.SgdPack(
+                self.fs.params, self.fs.grad, self.fs.mom,
+                [(u.conv.weight.data, u.wr, None if id(u) in self._no_dgrad else u.wd, u.stride, u.pad, u.C)
+                 for u in self.units if not u.depthwise])
 
     # ---- state ---------------------------------------------------------------------
     @property
@@ -848,6 +857,9 @@ class CNNNativeTrainer(LocalTrainer):
 
     def _sgd(self) -> None:
         c, fs = self.cfg, self.fs
+        if self._sgdpack is not None:
+            self._sgdpack.step(c.lr, c.momentum, c.weight_decay)
+            return
         self._nat.sgd_flat(native.stream_handle(self._device), fs.params.data_ptr(), fs.grad.data_ptr(),
                            fs.mom.data_ptr(), fs.n_params, c.lr, c.momentum, c.weight_decay, 0.0, False, False)
         self.pack()

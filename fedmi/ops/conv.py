@@ -168,6 +168,63 @@ def dgrad_pack_weights(items) -> None:
     native.require().dgrad_pack_multi(native.stream_handle(items[0][0].device), rows)
 
 
+class SgdPack:
+    """One launch per step for a flat fp32 master: torch.optim.SGD on every element (bit-identical to
+    ``sgd_flat``) and, for each dense conv, its forward image (:func:`pack_weights`) and DGRAD image
+    (:func:`dgrad_pack_weights`) written from the updated values (``sgd_pack_kernel``).  The unfused tail reads
+    the fp32 weights three times in 3-4 launches.
+
+    ``convs``: ``(w, wr, wd, stride, pad, C)`` per conv -- ``w`` a view of ``params`` (the fp32 master [O, Cw, R, S]),
+    ``wr`` its bf16 [O, R, S, C] image or None, ``wd`` its DGRAD image or None.  ``grad`` / ``mom`` share
+    ``params``' layout.  The device table holds raw pointers: every tensor here must outlive the plan."""
+
+    def __init__(self, params: torch.Tensor, grad: torch.Tensor, mom: torch.Tensor, convs) -> None:
+        for t, nm in ((params, "params"), (grad, "grad"), (mom, "mom")):
+            _check(t, torch.float32, f"SgdPack.{nm}")
+        n = params.numel()
+        if grad.numel() != n or mom.numel() != n:
+            raise ValueError("SgdPack: params / grad / mom sizes differ")
+        base = params.data_ptr()
+        rows, cover, keep = [], [], [params, grad, mom]
+        for w, wr, wd, stride, pad, C in convs:
+            O, Cw, R, S = (int(v) for v in w.shape)
+            d = w.data_ptr() - base
+            if not w.is_contiguous() or w.dtype != torch.float32 or d % 4 or d < 0 or d // 4 + w.numel() > n:
+                raise ValueError("SgdPack: a conv weight is not a contiguous fp32 view of params")
+            if wr is not None:
+                _check(wr, torch.bfloat16, "SgdPack.wr")
+                if tuple(wr.shape) != (O, R, S, int(C)):
+                    raise ValueError(f"SgdPack: image {tuple(wr.shape)} vs {(O, R, S, int(C))}")
+            if wd is not None:
+                _check(wd, torch.bfloat16, "SgdPack.wd")
+                if wd.numel() < dgrad_image_numel(w.shape, C) or not dgrad_eligible(O):
+                    raise ValueError("SgdPack: DGRAD image too small or O % 64 != 0")
+            rows.append((d // 4, wr.data_ptr() if wr is not None else 0, wd.data_ptr() if wd is not None else 0,
+                         O, Cw, int(C), R, S, int(stride), int(pad)))
+            cover.append((d // 4, d // 4 + w.numel()))
+            keep += [t for t in (wr, wd) if t is not None]
+        segs, at = [], 0
+        for a, b in sorted(cover):
+            if a < at:
+                raise ValueError("SgdPack: conv weights overlap")
+            if a > at:
+                segs.append((at, a - at))
+            at = b
+        if at < n:
+            segs.append((at, n - at))
+        tab, self.n_entries, self.n_blocks, self.lds = native.require().sgd_pack_plan(rows, segs)
+        self.table = torch.frombuffer(bytearray(tab), dtype=torch.uint8).to(params.device)
+        self._keep = keep
+        self.n_convs, self.n_segs = len(rows), len(segs)
+
+    def step(self, lr: float, momentum: float, weight_decay: float, dampening: float = 0.0,
+             nesterov: bool = False, first: bool = False) -> None:
+        p, g, b = self._keep[:3]
+        native.require().sgd_pack(native.stream_handle(p.device), self.table.data_ptr(), self.n_entries,
+                                  self.n_blocks, self.lds, p.data_ptr(), g.data_ptr(), b.data_ptr(), float(lr),
+                                  float(momentum), float(weight_decay), float(dampening), int(nesterov), int(first))
+
+
 def conv2d_dgrad(dy: torch.Tensor, wrsc: torch.Tensor, x_shape, stride: int, pad: int, Cw: Optional[int] = None,
                  out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
                  wd: Optional[torch.Tensor] = None, accumulate: bool = False, add: Optional[torch.Tensor] = None,

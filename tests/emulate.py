@@ -63,6 +63,26 @@ def dgrad_pack_weights(items):
     pass
 
 
+class SgdPack:
+    """conv.SgdPack under emulation: the torch SGD update of the flat master, then the forward images."""
+
+    def __init__(self, params, grad, mom, convs):
+        self.p, self.g, self.m = params, grad, mom
+        self.convs = [(w, wr) for w, wr, *_rest in convs]
+        self.n_convs = len(self.convs)
+
+    @torch.no_grad()
+    def step(self, lr, momentum, weight_decay, dampening=0.0, nesterov=False, first=False):
+        d = self.g + weight_decay * self.p
+        if momentum != 0:
+            self.m.copy_(d if first else momentum * self.m + (1 - dampening) * d)
+            d = d + momentum * self.m if nesterov else self.m
+        self.p.sub_(lr * d)
+        for w, wr in self.convs:
+            if wr is not None:
+                pack_weight(w, wr.shape[3], out=wr)
+
+
 def _w_from_img(wr: torch.Tensor, Cw: Optional[int]) -> torch.Tensor:
     m = _MASTER.get(wr.data_ptr())
     w = m.float() if m is not None and m.shape[2:] == wr.shape[1:3] else wr.permute(0, 3, 1, 2).float()
@@ -373,7 +393,7 @@ def emulated():
         saved.append((mod, name, getattr(mod, name)))
         setattr(mod, name, fn)
 
-    for name in ("pack_weight", "pack_weights", "fd_ws_floats", "dgrad_pack_weights", "conv2d_fwd", "conv2d_dgrad", "dgrad_fusable", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
+    for name in ("pack_weight", "pack_weights", "SgdPack", "fd_ws_floats", "dgrad_pack_weights", "conv2d_fwd", "conv2d_dgrad", "dgrad_fusable", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
                  "dwconv_dgrad", "dwconv_wgrad", "dwconv_ws_floats"):
         swap(conv, name, globals()[name])
     for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "bn_bwd_ws_floats", "bn_bwd_chain_floats", "head", "maxpool2",
