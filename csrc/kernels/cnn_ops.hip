@@ -372,6 +372,36 @@ struct BwdOut {
   const bf16* dadd;       // optional grad added to dza (a residual edge that bypasses this BN)
 };
 
+// Raw operands of one 8-channel vector of the BN backward (row r, channel offset c; i = the compact element index
+// r * C + c), all loads issued together; bwd_g then forms load_g's g from them.  The apply kernels issue their
+// first vector this way BEFORE the coefficient prologue, so its latency overlaps the fp64 channel-sum reads.
+struct BwdRaw {
+  float z[8], g[8], gb[8], ym[8], zb[8], da[8];
+};
+FEDMI_DEV void bwd_issue(const BwdIn& in, const BwdOut& out, long r, int c, long i, BwdRaw& x) {
+  load8f(in.za + i, x.z);
+  const long od = r * in.ldd + c;
+  load8f(in.dya + od, x.g);
+  if (in.dyb) load8f(in.dyb + od, x.gb);
+  if (in.y) load8f(in.y + r * in.ldy + c, x.ym);
+  if (in.zb) load8f(in.zb + i, x.zb);
+  if (out.dadd) load8f(out.dadd + i, x.da);
+}
+FEDMI_DEV void bwd_g(const BwdIn& in, int c, BwdRaw& x) {
+  if (in.dyb) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x.g[j] += x.gb[j];
+  }
+  if (in.y) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x.g[j] = x.ym[j] > 0.f ? x.g[j] : 0.f;
+  } else if (in.msc) {
+    const int C = in.ldd;   // msc mode: compact rows (host checks ldd == C)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x.g[j] = x.z[j] * in.msc[c + j] + in.msc[C + c + j] > 0.f ? x.g[j] : 0.f;
+  }
+}
+
 // Flat grid variant (see bn_apply_kernel).
 // partials != null (chained mode): the channel sums are read straight from the reduce kernel's
 // 'reps' atomic replicas (no finalize launch); the caller zeroes them before the next step.
@@ -380,6 +410,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_flat_kernel(BwdIn in, BwdOut
                                                            int reps) {
   extern __shared__ float co[];   // [6][C]: kA, bA, cA, kB, bB, cB  (dz = k*g + b*xhat + c)
   const float invM = 1.f / (float)M;
+  const int VR = C >> 3;
+  const int nv = M * VR;          // host: < 2^31
+  const int stride = gridDim.x * blockDim.x;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  BwdRaw x;
+  if (i < nv) {
+    const int row = i / VR;
+    bwd_issue(in, out, row, (i - row * VR) * 8, (long)i * 8, x);
+  }
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     double dg = 0.0, dgx = 0.0, dgx2 = 0.0;
     if (partials) {
@@ -418,28 +457,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_flat_kernel(BwdIn in, BwdOut
     }
   }
   __syncthreads();
-  const int VR = C >> 3;
-  const long nv = (long)M * VR;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % VR) * 8;
-    float g[8], z[8], d[8];
-    load8f(in.za + i * 8, z);
-    load_g(in, i / VR, c0 >> 3, g, z);
-    if (out.gout) store8f(out.gout + i * 8, g);
+  for (bool first = true; i < nv; i += stride, first = false) {
+    const int row = i / VR, c0 = (i - row * VR) * 8;
+    if (!first) bwd_issue(in, out, row, c0, (long)i * 8, x);
+    bwd_g(in, c0, x);
+    if (out.gout) store8f(out.gout + (long)i * 8, x.g);
+    float d[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = co[c0 + j] * g[j] + co[C + c0 + j] * z[j] + co[2 * C + c0 + j];
+    for (int j = 0; j < 8; ++j) d[j] = co[c0 + j] * x.g[j] + co[C + c0 + j] * x.z[j] + co[2 * C + c0 + j];
     if (out.dadd) {
-      float t[8];
-      load8f(out.dadd + i * 8, t);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] += t[j];
+      for (int j = 0; j < 8; ++j) d[j] += x.da[j];
     }
-    store8f(out.dza + i * 8, d);
+    store8f(out.dza + (long)i * 8, d);
     if (in.zb) {
-      load8f(in.zb + i * 8, z);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = co[3 * C + c0 + j] * g[j] + co[4 * C + c0 + j] * z[j] + co[5 * C + c0 + j];
-      store8f(out.dzb + i * 8, d);
+      for (int j = 0; j < 8; ++j) d[j] = co[3 * C + c0 + j] * x.g[j] + co[4 * C + c0 + j] * x.zb[j] + co[5 * C + c0 + j];
+      store8f(out.dzb + (long)i * 8, d);
     }
   }
 }
@@ -453,6 +487,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_chunk_kernel(BwdIn in, BwdOu
   __shared__ float co[6][kBnChunk];   // kA, bA, cA, kB, bB, cB  (dz = k*g + b*z + c)
   const int CC = min(kBnChunk, C), c_lo = blockIdx.y * CC;
   const float invM = 1.f / (float)M;
+  const int VC = CC >> 3, rstep = 256 / VC;
+  const int cv = threadIdx.x % VC, c0 = cv * 8, cg = c_lo + c0;
+  const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
+  const bool lane_ok = (int)threadIdx.x < rstep * VC;
+  // two rows per thread-slot, every load issued before the first use; the first pair before the prologue
+  BwdRaw x[2];
+  auto issue_pair = [&](int r0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + u * rstep;
+      if (r < re) bwd_issue(in, out, r, cg, (long)r * C + cg, x[u]);
+    }
+  };
+  int r0 = rb + (int)threadIdx.x / VC;
+  if (lane_ok) issue_pair(r0);
   for (int cc = threadIdx.x; cc < CC; cc += blockDim.x) {
     const int c = c_lo + cc;
     double dg = 0.0, dgx = 0.0, dgx2 = 0.0;
@@ -492,44 +541,26 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_chunk_kernel(BwdIn in, BwdOu
     }
   }
   __syncthreads();
-  const int VC = CC >> 3, rstep = 256 / VC;
-  const int cv = threadIdx.x % VC, c0 = cv * 8, cg = c_lo + c0;
-  const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
-  if ((int)threadIdx.x >= rstep * VC) return;
-  // two rows per thread-slot, every load issued before the first use
-  for (int r0 = rb + (int)threadIdx.x / VC; r0 < re; r0 += 2 * rstep) {
-    float z[2][8], g[2][8], zb[2][8], da[2][8];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int r = r0 + u * rstep;
-      if (r < re) {
-        const long i = (long)r * C + cg;
-        load8f(in.za + i, z[u]);
-        if (in.zb) load8f(in.zb + i, zb[u]);
-        if (out.dadd) load8f(out.dadd + i, da[u]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int r = r0 + u * rstep;
-      if (r < re) load_g(in, r, cg >> 3, g[u], z[u]);
-    }
+  if (!lane_ok) return;
+  for (bool first = true; r0 < re; r0 += 2 * rstep, first = false) {
+    if (!first) issue_pair(r0);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int r = r0 + u * rstep;
       if (r >= re) continue;
       const long i = (long)r * C + cg;
-      if (out.gout) store8f(out.gout + i, g[u]);
+      bwd_g(in, cg, x[u]);
+      if (out.gout) store8f(out.gout + i, x[u].g);
       float d[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        d[j] = co[0][c0 + j] * g[u][j] + co[1][c0 + j] * z[u][j] + co[2][c0 + j];
-        if (out.dadd) d[j] += da[u][j];
+        d[j] = co[0][c0 + j] * x[u].g[j] + co[1][c0 + j] * x[u].z[j] + co[2][c0 + j];
+        if (out.dadd) d[j] += x[u].da[j];
       }
       store8f(out.dza + i, d);
       if (in.zb) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = co[3][c0 + j] * g[u][j] + co[4][c0 + j] * zb[u][j] + co[5][c0 + j];
+        for (int j = 0; j < 8; ++j) d[j] = co[3][c0 + j] * x[u].g[j] + co[4][c0 + j] * x[u].zb[j] + co[5][c0 + j];
         store8f(out.dzb + i, d);
       }
     }
@@ -991,6 +1022,7 @@ void launch_bn_apply(hipStream_t st, const bf16* z, const BNDesc& a, const bf16*
   if (C % 8) throw std::invalid_argument("bn_apply: C % 8 != 0");
   if (ldy <= 0) ldy = C;
   if (ldy < C || ldy % 8) throw std::invalid_argument("bn_apply: bad output row stride");
+  if ((long)M * (C / 8) >= (1l << 31)) throw std::invalid_argument("bn_apply: tensor too large for 32-bit indexing");
   const int res_mode = b ? 2 : (res ? 1 : 0);
   const BNArgs bb = b ? to_args(*b) : BNArgs{};
   if (use_chunked(C)) {
@@ -1046,6 +1078,7 @@ void launch_bn_bwd(hipStream_t st, const BNBwdDesc& d, double* red, int M, int C
   if (ldd <= 0) ldd = C;
   if (ldy <= 0) ldy = C;
   if (ldd < C || ldy < C || ldd % 8 || ldy % 8) throw std::invalid_argument("bn_bwd: bad row strides");
+  if ((long)M * VR >= (1l << 31)) throw std::invalid_argument("bn_bwd: tensor too large for 32-bit indexing");
   if (d.msc && (d.y || ldd != C)) throw std::invalid_argument("bn_bwd: the z-derived ReLU mask needs y == null, compact rows");
   BwdIn in{d.dya, d.dyb, d.y, d.za, d.meanA, d.invA, d.zb, d.meanB, d.invB, ldd, ldy, d.msc};
   BwdOut out{d.dza, d.dzb, d.gout, d.dgammaA, d.dbetaA, d.dgammaB, d.dbetaB, d.gammaA, d.gammaB, d.shiftA, d.shiftB,

@@ -1848,14 +1848,15 @@ static PhasePlan plan_tap_phases(const TapPhase* ph, int n, long ws_cap) {
   for (int i = 0; i < n; ++i)
     if (!ph[i].empty) { bn = tap_bn_for(ph[i].g.O, m_tiles); break; }
   pl.bn = bn;
+  // tap-less parities (1x1 stride 2) ride along as K = 0 phases: their tiles only write zeros (or leave an
+  // accumulated dX as it is) -- one launch instead of one zero-fill launch per empty parity
   for (int i = 0; i < n; ++i) {
-    if (ph[i].empty) continue;
     const int k = tm.n++;
     pl.idx[k] = i;
     tiles[k] = (long)((ph[i].g.M + 127) / 128) * ((ph[i].g.O + bn - 1) / bn);
-    ks[k] = ph[i].g.K / 64;
+    ks[k] = ph[i].empty ? 0 : ph[i].g.K / 64;
     tm.splits[k] = 1;
-    total += tiles[k];
+    if (!ph[i].empty) total += tiles[k];
   }
   auto need = [&](const int* sp) {
     long w = 0;
@@ -1885,9 +1886,10 @@ static PhasePlan plan_tap_phases(const TapPhase* ph, int n, long ws_cap) {
   pl.maxsp = 1;
   for (int k = 0; k < tm.n; ++k) {
     const TapPhase& q = ph[pl.idx[k]];
-    tm.kps[k] = (ks[k] + tm.splits[k] - 1) / tm.splits[k];
-    tm.splits[k] = (ks[k] + tm.kps[k] - 1) / tm.kps[k];
+    tm.kps[k] = std::max(1, (ks[k] + tm.splits[k] - 1) / tm.splits[k]);
+    tm.splits[k] = std::max(1, (ks[k] + tm.kps[k] - 1) / tm.kps[k]);
     tm.g[k] = q.g;
+    if (q.empty) tm.g[k].K = 0;
     tm.rm[k] = q.rm;
     tm.woff[k] = q.img_off;
     tm.wsoff[k] = tm.splits[k] > 1 ? off : -1;
@@ -2015,23 +2017,11 @@ void launch_conv_dgrad(hipStream_t st, const ConvShape& s, const bf16* dy, const
   if (wd != nullptr && dgrad_tap_ok(s)) {   // tap-major path on the dgrad weight image
     TapPhase ph[4];
     const int n = dgrad_tap_phases(s, ph);
-    if (n > 1) {   // stride 2: the tap phases in one launch, the tap-less parities zeroed below
+    if (n > 1)   // stride 2: every parity in one launch (tap-less parities as K = 0 phases that write zeros)
       launch_tap_phases(st, ph, n, dy, wd, dx, ws, ws_floats, acc ? dx : add, bs ? *bs : BnSums{});
-    }
-    for (int i = 0; i < n; ++i) {
-      if (n > 1 && !ph[i].empty) continue;
-      if (ph[i].empty) {   // zero this parity's rows with the generic kernel (K = 0)
-        ConvGeom q = make_geom(s);
-        q.NC = s.C; q.ph = ph[i].ph; q.pw = ph[i].pw; q.r0 = ph[i].r0; q.s0 = ph[i].s0; q.nr = 0; q.ns = 0;
-        q.Hp = ph[i].g.P; q.Wp = ph[i].g.Q;
-        q.dNS = make_div(1); q.dWp = make_div(q.Wp); q.dHWp = make_div(q.Hp * q.Wp);
-        q.M = s.N * q.Hp * q.Wp; q.K = 0;
-        launch_mode<DGRAD>(st, q, nullptr, wrsc, dy, dx, nullptr, nullptr, 1, nullptr, acc ? 2 : 0);
-        continue;
-      }
-      launch_tap(st, ph[i].g, dy, wd + ph[i].img_off, dx, nullptr, nullptr, ph[i].rm, ws, ws_floats,
+    else
+      launch_tap(st, ph[0].g, dy, wd + ph[0].img_off, dx, nullptr, nullptr, ph[0].rm, ws, ws_floats,
                  acc ? dx : add, bs ? *bs : BnSums{});
-    }
     return;
   }
   ConvGeom g = make_geom(s);
@@ -2285,8 +2275,9 @@ SgdPackPlan build_sgd_pack_plan(const SgdPackConv* convs, int nc, const long* se
     SgdPackEntry e{};
     e.kind = 0; e.off = c.off; e.wr = c.wr;
     e.O = c.O; e.Cw = c.Cw; e.C = c.C; e.R = c.R; e.S = c.S; e.step = c.st;
-    // input channels per block: about 144 floats per filter row (3x3: 16, 1x1: 128), 4 for windows past 3x3
-    e.cb = c.R * c.S > 9 ? 4 : c.R * c.S > 4 ? DP_CB : c.R * c.S > 1 ? 32 : 128;
+    // input channels per block: 16 for 3x3 (144 floats per filter row), 4 past 3x3 (LDS), 64 for 1x1 (cold-cache
+    // tail, MobileNet: 16 -> 53 us, 64 -> 37, 128 -> 40; profiles/r5_cnn/sgdpack/)
+    e.cb = c.R * c.S > 9 ? 4 : c.R * c.S > 4 ? DP_CB : c.R * c.S > 1 ? 32 : 64;
     if (c.wd) {
       ConvShape s{};
       s.N = 1; s.H = 8; s.W = 8; s.P = 4; s.Q = 4;   // spatial sizes only gate empty phases (launch_dgrad_pack_multi)

@@ -772,3 +772,26 @@ def test_dwconv_dgrad_fused_bn_sums(gpu_device, shape):
     scale = gm.abs().sum(0) + 1.0
     assert float(((got[0] - s0).abs() / scale).max()) < 1e-5
     assert float(((got[1] - s1).abs() / (scale * 4)).max()) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(4, 16, 16, 64, 128, 1, 2, 0), (128, 8, 8, 256, 512, 1, 2, 0)])
+def test_conv_dgrad_1x1_stride2_zeroes_tapless_parities(gpu_device, shape):
+    """1x1 / stride 2: three of the four dX parities get no tap.  They ride in the one tap-phases launch as K = 0
+    phases that write zeros -- every element of a NaN-filled output must be overwritten."""
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device, seed=23)
+    xr = x.clone().requires_grad_(True)
+    out = F.conv2d(xr, wb, stride=st, padding=pad)
+    gy = torch.randn_like(out).bfloat16().float()
+    out.backward(gy)
+    C = xn.shape[-1]
+    wd = torch.empty(conv.dgrad_image_numel(w.shape, C), dtype=torch.bfloat16, device=gpu_device)
+    conv.dgrad_pack_weights([(w, wd, st, pad, C)])
+    shp = (xn.shape, O, R, R, st, pad, Cw)
+    wsp = torch.empty(max(conv.fd_ws_floats(*shp), 1), device=gpu_device)
+    dx = torch.full_like(xn, float("nan"))
+    conv.conv2d_dgrad(_nhwc(gy).bfloat16(), conv.pack_weight(w), xn.shape, st, pad, Cw=Cw, out=dx, ws=wsp, wd=wd)
+    torch.cuda.synchronize()
+    assert not torch.isnan(dx.float()).any()
+    assert torch.equal(dx[:, 1::2].float(), torch.zeros_like(dx[:, 1::2].float()))
+    assert _rel(dx[..., :Cw].float(), _nhwc(xr.grad)) < 1e-2
