@@ -1953,15 +1953,14 @@ static void launch_fd(hipStream_t st, const ConvGeom& g, const bf16* x, const bf
                      rows_per_block, acc ? out : nullptr, BnSums{});
 }
 
-// K-split count for the weight gradient: about two workgroups per CU, at least
-// 8 K steps per split, and a bounded workspace.
-// K-split count for the weight gradient: about two workgroups per CU, at least
-// 8 K steps per split, and a bounded workspace.
+// K-split count for the weight gradient: at most one wave of two workgroups per CU (rounded down: ResNet-18's
+// layer-4 3x3 WGRAD, 144 tiles, 48.0 -> 40.5 us with 3 splits instead of 4 -- the fourth made a second, 64-workgroup
+// wave; profiles/r5_cnn/experiments/wgrad_splits.jsonl), at least 8 K steps per split, a bounded workspace.
 static int wgrad_splits(const ConvGeom& g, long ws_cap_floats) {
   const TileCfg t = pick_tiles_wgrad(g.M, g.NC);
   const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
   const int ksteps = (g.K + BK - 1) / BK;
-  long sp = (2l * num_cus() + tiles - 1) / tiles;
+  long sp = std::max<long>(1, 2l * num_cus() / tiles);
   sp = std::min<long>(sp, std::max(1, ksteps / 8));
   if (ws_cap_floats > 0) sp = std::min<long>(sp, ws_cap_floats / ((long)g.M * g.NC));
   sp = std::max<long>(1, sp);
