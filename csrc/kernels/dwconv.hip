@@ -307,6 +307,167 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16* __restrict__ 
   }
 }
 
+// 3x3 / stride 2 / pad 1 DGRAD, one thread per (2x2 block of dX, 8-channel group): the block's four input
+// pixels draw on the same four dY pixels (i, j), (i, j+1), (i+1, j), (i+1, j+1) --
+//   dx[2i][2j]     = dy[i][j] w11
+//   dx[2i][2j+1]   = dy[i][j+1] w10 + dy[i][j] w12
+//   dx[2i+1][2j]   = dy[i+1][j] w01 + dy[i][j] w21
+//   dx[2i+1][2j+1] = dy[i+1][j+1] w00 + dy[i+1][j] w02 + dy[i][j+1] w20 + dy[i][j] w22
+// -- so 4 loads feed 4 outputs with no per-tap parity test (dw_dgrad_kernel's generic path walks all 9 taps
+// per output behind divergent stride checks: 4x the forward's time).  Taps are summed in dw_dgrad_kernel's
+// (r, s) order; same BN-sums epilogue.
+__global__ __launch_bounds__(256) void dw_dgrad3s2_kernel(const bf16* __restrict__ dy, const float* __restrict__ w,
+                                                          bf16* __restrict__ dx, DwGeom g, fedmi::BnSums bs) {
+  extern __shared__ float wl[];
+  const int VC = g.C >> 3;
+  stage_taps(w, wl, g.C, 9);
+  __syncthreads();
+  const bool bsum = bs.rep != nullptr;
+  float bq[3][8], bm[3][8], bi[3][8];
+  const int c0 = (int)(threadIdx.x % VC) * 8;
+  fedmi::bnsum_coeffs(bs, c0, bsum, bm, bi, bq);
+  const float* wc = wl + c0;   // tap t, channel k: wc[t * C + k]
+  const uint32_t total = (uint32_t)g.N * g.P * g.Q * VC;
+  for (uint32_t it = blockIdx.x * blockDim.x + threadIdx.x; it < total; it += gridDim.x * blockDim.x) {
+    const uint32_t cell = it / (uint32_t)VC;
+    const uint32_t t2 = cell / (uint32_t)g.Q;
+    const int j = (int)(cell - t2 * g.Q);
+    const int n = (int)(t2 / (uint32_t)g.P), i = (int)(t2 - (uint32_t)n * g.P);
+    const bool okr = i + 1 < g.P, okc = j + 1 < g.Q;
+    const long b00 = (((long)n * g.P + i) * g.Q + j) * g.C + c0;
+    float d00[8], d01[8], d10[8], d11[8];
+    ld8f(dy + b00, d00);
+    ld8f(dy + (okc ? b00 + g.C : b00), d01);
+    ld8f(dy + (okr ? b00 + (long)g.Q * g.C : b00), d10);
+    ld8f(dy + (okr && okc ? b00 + (long)(g.Q + 1) * g.C : b00), d11);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      d01[k] = okc ? d01[k] : 0.f;
+      d10[k] = okr ? d10[k] : 0.f;
+      d11[k] = okr && okc ? d11[k] : 0.f;
+    }
+    // taps: t = r * 3 + s
+    const int C = g.C;
+    float a[4][8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a[0][k] = 0.f + d00[k] * wc[4 * C + k];
+      a[1][k] = 0.f + d01[k] * wc[3 * C + k];
+      a[1][k] += d00[k] * wc[5 * C + k];
+      a[2][k] = 0.f + d10[k] * wc[1 * C + k];
+      a[2][k] += d00[k] * wc[7 * C + k];
+      a[3][k] = 0.f + d11[k] * wc[0 * C + k];
+      a[3][k] += d10[k] * wc[2 * C + k];
+      a[3][k] += d01[k] * wc[6 * C + k];
+      a[3][k] += d00[k] * wc[8 * C + k];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int h = 2 * i + (q >> 1), ww = 2 * j + (q & 1);
+      if (h >= g.H || ww >= g.W) continue;
+      const long pix = ((long)n * g.H + h) * g.W + ww;
+      bf16x8v o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = (bf16)a[q][k];
+      *reinterpret_cast<bf16x8v*>(dx + pix * g.C + c0) = o;
+      if (bsum) fedmi::bnsum_acc(bs, pix * g.C + c0, o, bm, bi, bq);
+    }
+  }
+  if (!bsum) return;
+  float* red = wl + g.C * 9;   // [3][blockDim][8]
+  const int tb = blockDim.x;
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[(q * tb + threadIdx.x) * 8 + k] = bq[q][k];
+  __syncthreads();
+  const int nq = bs.zb ? 3 : 2;
+  for (int e = threadIdx.x; e < nq * g.C; e += tb) {
+    const int q = e / g.C, c = e - q * g.C, grp = c >> 3, k = c & 7;
+    float sum = 0.f;
+    for (int t = grp; t < tb; t += VC) sum += red[(q * tb + t) * 8 + k];
+    unsafeAtomicAdd(bs.rep + ((long)(blockIdx.x % bs.reps) * 3 + q) * g.C + c, (double)sum);
+  }
+}
+
+// 3x3 / stride 1 / pad 1 DGRAD, register-blocked like dw_fwd3_kernel<1>: one thread per (2 horizontally adjacent
+// dX pixels, 8-channel group); the 3 x 4 dY pixels they draw on are loaded once (6 loads per output instead of
+// 9).  dx[h][w] = sum_{r,s} dy[h+1-r][w+1-s] w[r][s], taps summed in dw_dgrad_kernel's (r, s) order; same BN-sums
+// epilogue.
+__global__ __launch_bounds__(256) void dw_dgrad3s1_kernel(const bf16* __restrict__ dy, const float* __restrict__ w,
+                                                          bf16* __restrict__ dx, DwGeom g, fedmi::BnSums bs) {
+  extern __shared__ float wl[];
+  const int VC = g.C >> 3;
+  stage_taps(w, wl, g.C, 9);
+  __syncthreads();
+  const bool bsum = bs.rep != nullptr;
+  float bq[3][8], bm[3][8], bi[3][8];
+  const int c0 = (int)(threadIdx.x % VC) * 8;
+  fedmi::bnsum_coeffs(bs, c0, bsum, bm, bi, bq);
+  const int W2 = (g.W + 1) >> 1;
+  const uint32_t total = (uint32_t)g.N * g.H * W2 * VC;
+  for (uint32_t it = blockIdx.x * blockDim.x + threadIdx.x; it < total; it += gridDim.x * blockDim.x) {
+    const uint32_t pr = it / (uint32_t)VC;
+    const uint32_t t2 = pr / (uint32_t)W2;
+    const int w0 = (int)(pr - t2 * W2) * 2;
+    const int n = (int)(t2 / (uint32_t)g.H), h = (int)(t2 - (uint32_t)n * g.H);
+    float a0[8], a1[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a0[k] = a1[k] = 0.f;
+    const long nb = (long)n * g.P;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int yy = h + 1 - r;
+      const bool rok = (unsigned)yy < (unsigned)g.P;
+      float v[4][8];   // dY columns w0-1 .. w0+2
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int xx = w0 - 1 + k;
+        const bool ok = rok && (unsigned)xx < (unsigned)g.Q;
+        ld8f(dy + (ok ? ((nb + yy) * g.Q + xx) * g.C + c0 : c0), v[k]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = ok ? v[k][j] : 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const float* wt = wl + (r * 3 + s) * g.C + c0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a0[j] += v[2 - s][j] * wt[j];
+          a1[j] += v[3 - s][j] * wt[j];
+        }
+      }
+    }
+    const long pix0 = ((long)n * g.H + h) * g.W + w0;
+    bf16x8v o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)a0[j];
+    *reinterpret_cast<bf16x8v*>(dx + pix0 * g.C + c0) = o;
+    if (bsum) fedmi::bnsum_acc(bs, pix0 * g.C + c0, o, bm, bi, bq);
+    if (w0 + 1 < g.W) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)a1[j];
+      *reinterpret_cast<bf16x8v*>(dx + (pix0 + 1) * g.C + c0) = o;
+      if (bsum) fedmi::bnsum_acc(bs, (pix0 + 1) * g.C + c0, o, bm, bi, bq);
+    }
+  }
+  if (!bsum) return;
+  float* red = wl + g.C * 9;   // [3][blockDim][8]
+  const int tb = blockDim.x;
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[(q * tb + threadIdx.x) * 8 + k] = bq[q][k];
+  __syncthreads();
+  const int nq = bs.zb ? 3 : 2;
+  for (int e = threadIdx.x; e < nq * g.C; e += tb) {
+    const int q = e / g.C, c = e - q * g.C, grp = c >> 3, k = c & 7;
+    float sum = 0.f;
+    for (int t = grp; t < tb; t += VC) sum += red[(q * tb + t) * 8 + k];
+    unsafeAtomicAdd(bs.rep + ((long)(blockIdx.x % bs.reps) * 3 + q) * g.C + c, (double)sum);
+  }
+}
+
 // Sum acc over the pstep threads of the block that share a channel group (LDS, one tap at a
 // time) and write this block's partial ws[blockIdx.x][C][RS] for the chunk's channels.
 template <int RS>
@@ -499,10 +660,22 @@ void launch_dw_dgrad(hipStream_t st, const DwShape& s, const bf16* dy, const flo
   if (bs && (!bs->rep || !bs->z || !bs->mean || !bs->inv || bs->reps < 1 || (bs->zb && (!bs->meanb || !bs->invb)) ||
              (bs->msc && (bs->y || bs->msc_ld <= 0))))
     throw std::invalid_argument("dw_dgrad: incomplete BN sums descriptor");
-  const long items = (long)g.N * g.H * g.W * (g.C / 8);
   const int tb = block_threads(g.C);
-  const int nblk = bs ? std::min(blocks_for(items, tb), 2048) : blocks_for(items, tb);
   const size_t lds = g.C * g.R * g.S * sizeof(float) + (bs ? 3 * tb * 8 * sizeof(float) : 0);
+  if (g.R == 3 && g.st == 2 && g.pad == 1) {   // 2x2 dX blocks (dw_dgrad3s2_kernel): H <= 2P, W <= 2Q always
+    const long items = (long)g.N * g.P * g.Q * (g.C / 8);
+    const int nblk = bs ? std::min(blocks_for(items, tb), 2048) : blocks_for(items, tb);
+    hipLaunchKernelGGL(dw_dgrad3s2_kernel, dim3(nblk), dim3(tb), lds, st, dy, w, dx, g, bs ? *bs : BnSums{});
+    return;
+  }
+  if (g.R == 3 && g.st == 1 && g.pad == 1) {   // row pairs (dw_dgrad3s1_kernel)
+    const long items = (long)g.N * g.H * ((g.W + 1) / 2) * (g.C / 8);
+    const int nblk = bs ? std::min(blocks_for(items, tb), 2048) : blocks_for(items, tb);
+    hipLaunchKernelGGL(dw_dgrad3s1_kernel, dim3(nblk), dim3(tb), lds, st, dy, w, dx, g, bs ? *bs : BnSums{});
+    return;
+  }
+  const long items = (long)g.N * g.H * g.W * (g.C / 8);
+  const int nblk = bs ? std::min(blocks_for(items, tb), 2048) : blocks_for(items, tb);
   hipLaunchKernelGGL(dw_dgrad_kernel, dim3(nblk), dim3(tb), lds, st, dy, w, dx, g, bs ? *bs : BnSums{});
 }
 
