@@ -137,7 +137,8 @@ class _Unit:
 
     def dgrad_fusable(self, add: bool = False) -> bool:
         """Whether this conv's DGRAD can take its producer BN's backward sums in the epilogue (dense tap
-        path; the depthwise DGRAD with the sums measured slower, 846 vs 832 ms per MobileNet round) and,
+        path; the depthwise DGRAD with the sums measured slower, 846 vs 832 ms per MobileNet round, and with
+        round 5's blocked depthwise DGRAD kernels a wash, 695.8 / 694.7 vs 695.9 / 693.5 ms) and,
         ``add``, a second incoming grad."""
         if self.depthwise:
             return False
