@@ -44,6 +44,8 @@ void fedmi_bind_comm(py::module_& m) {
       .def("error", &PeerComm::error)
       .def("epochs", &PeerComm::epochs)
       .def("clear_error", &PeerComm::clear_error)
+      .def("request_abort", &PeerComm::request_abort)
+      .def("abort_requested", &PeerComm::abort_requested)
       .def("set_timeout_ms", &PeerComm::set_timeout_ms)
       .def("disconnect", &PeerComm::disconnect, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("connected", &PeerComm::connected)

@@ -48,6 +48,8 @@ struct PeerArgs {
   int world;
   long long cap;                    // bytes per region
   long long timeout_ticks;          // s_memrealtime ticks (100 MHz)
+  const uint32_t* abort_flag;       // host-pinned coherent word (device view): nonzero = the coordinator
+                                    // reported a lost client, every barrier of this communicator fails now
 };
 
 enum PeerAlgo { kPeerOneShot = 0, kPeerTwoShot = 1 };
@@ -77,6 +79,11 @@ class PeerComm {
   void allgather(hipStream_t st, const void* in, void* out, long long nbytes, int blocks);
 
   uint32_t error() const;           // synchronous read of the timeout flag
+  // Host-side abort (a watchdog thread, while a collective may be spinning on the stream): a plain store
+  // into host-pinned coherent memory the barrier polls -- no stream, no HIP call, never blocks.  Sticky:
+  // the communicator belongs to one data-plane generation, which the coordinator replaces after a loss.
+  void request_abort();
+  bool abort_requested() const;
   std::vector<uint32_t> epochs() const;   // synchronous read of the per-block call counters (tests)
   void clear_error();
   void set_timeout_ms(double ms);
@@ -91,6 +98,7 @@ class PeerComm {
   PeerArgs a_{};
   PeerSignal* sig_ = nullptr;       // own (uncached)
   char* data_ = nullptr;            // own staging
+  uint32_t* abort_host_ = nullptr;  // host-pinned abort word (a_.abort_flag is its device view)
   bool connected_ = false;
   bool colocated_ = false;
   int device_ = 0;

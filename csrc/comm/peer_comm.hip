@@ -8,7 +8,11 @@
 //   [phase][block][p]; a SYSTEM-scope acquire (L1/L2 invalidate) follows, then a
 //   workgroup barrier releases the other waves to read peer data.
 //   Flags live in uncached memory; polls are bounded by a wall-clock timeout that
-//   sets PeerSignal::error instead of hanging when a peer died mid-collective.
+//   sets PeerSignal::error instead of hanging when a peer died mid-collective, and
+//   by a host-pinned abort word (PeerArgs::abort_flag) that the client's watchdog
+//   sets as soon as the coordinator reports the loss (reference: a dead client is
+//   dropped at its next failed RPC, src/server.py:59-62, 72-75) -- the survivors
+//   then leave the barrier within one poll period instead of the full timeout.
 //
 // Buffer reuse: call k uses staging slot k & 1.  A rank rewrites slot k & 1 only
 // in call k + 2, after call k + 1's barrier, which every peer enters only once
@@ -75,9 +79,12 @@ PDEV bool peer_barrier(const PeerArgs& a, int phase, int b, uint32_t ep) {
       st_sys(&a.sig[p]->flags[phase][b][a.rank], ep);
       const uint32_t* mine = &a.sig[a.rank]->flags[phase][b][p];
       const unsigned long long t0 = wall_clock64();
+      uint32_t polls = 0;
       while (ld_sys(mine) < ep) {
         __builtin_amdgcn_s_sleep(1);
-        if ((long long)(wall_clock64() - t0) > a.timeout_ticks) {
+        // the abort word lives in host memory (one PCIe read): looked at every 256 polls only
+        const bool aborted = ((++polls & 255u) == 0u) && ld_sys(a.abort_flag) != 0u;
+        if (aborted || (long long)(wall_clock64() - t0) > a.timeout_ticks) {
           st_sys(&a.sig[a.rank]->error, 1u);
           ok = false;
           break;
@@ -235,6 +242,13 @@ PeerComm::PeerComm(int rank, int world, long long cap_bytes) {
   check_hip(hipExtMallocWithFlags(reinterpret_cast<void**>(&data_), data_bytes, hipDeviceMallocUncached),
             "PeerComm staging alloc");
   check_hip(hipMemset(data_, 0, 4 * cap_bytes), "PeerComm staging memset");
+  // abort word: host-pinned, coherent (device reads see host stores without any cache maintenance)
+  check_hip(hipHostMalloc(reinterpret_cast<void**>(&abort_host_), 64, hipHostMallocMapped | hipHostMallocCoherent),
+            "PeerComm abort word alloc");
+  *reinterpret_cast<volatile uint32_t*>(abort_host_) = 0u;
+  void* abort_dev = nullptr;
+  check_hip(hipHostGetDevicePointer(&abort_dev, abort_host_, 0), "PeerComm abort word device pointer");
+  a_.abort_flag = reinterpret_cast<const uint32_t*>(abort_dev);
   check_hip(hipDeviceSynchronize(), "PeerComm init sync");
   a_.rank = rank;
   a_.world = world;
@@ -251,6 +265,7 @@ PeerComm::~PeerComm() {
   }
   (void)hipFree(data_);
   (void)hipFree(sig_);
+  (void)hipHostFree(abort_host_);
 }
 
 // Handle blob: [signal IPC handle][staging IPC handle][PCI bus id of the owner's GPU, 64 bytes].
@@ -333,6 +348,12 @@ std::vector<uint32_t> PeerComm::epochs() const {
             "PeerComm::epochs");
   return e;
 }
+
+void PeerComm::request_abort() {
+  __atomic_store_n(abort_host_, 1u, __ATOMIC_RELEASE);
+}
+
+bool PeerComm::abort_requested() const { return __atomic_load_n(abort_host_, __ATOMIC_ACQUIRE) != 0u; }
 
 void PeerComm::clear_error() { check_hip(hipMemset(&sig_->error, 0, sizeof(uint32_t)), "PeerComm::clear_error"); }
 

@@ -95,6 +95,8 @@ class ClientAgent(P.TrainerServicer):
         self._ready_lock = threading.Lock()
         self._ready: Optional[tuple] = None     # (epoch, bytes) newest serialised global checkpoint
         self._sent_epoch = -1
+        self._ready_branch = 0                  # bumped when SendModel installs a model (rollback / resync):
+                                                # checkpoints serialised on the abandoned branch are dropped
         self.ckpt_path = ck.client_ckpt_path(root, address.replace("/", "_"))
         # fault injection (tests / drills): stall this many seconds right before the FedAvg
         # collective, so a kill lands while the other clients wait inside it
@@ -147,8 +149,10 @@ class ClientAgent(P.TrainerServicer):
     def _persist_async(self, acc, epoch: int, keep: bool) -> None:
         """Checkpoint off the RPC thread (pinned snapshot + writer thread); with ``keep`` the
         serialised bytes are also kept for the coordinator's upload."""
-        def _keep(_path, data, _epoch=epoch):
+        def _keep(_path, data, _epoch=epoch, _branch=self._ready_branch):
             with self._ready_lock:
+                if _branch != self._ready_branch:
+                    return                      # serialised before a rollback: not the committed history
                 if self._ready is None or _epoch >= self._ready[0]:
                     self._ready = (_epoch, data)
 
@@ -176,6 +180,17 @@ class ClientAgent(P.TrainerServicer):
         if comp is not None:
             comp.reset(self.trainer)
         return ck.state_digest(self.trainer.state_dict())
+
+    def _reset_ready(self, epoch: int, data: bytes) -> None:
+        """A model installed by the coordinator (rollback, rejoin resync) is the committed history from now
+        on: the ready buffer holds it, uploads restart after its epoch, and writer callbacks of checkpoints
+        serialised before it (a branch the coordinator discarded, possibly labelled with HIGHER epochs) are
+        ignored -- otherwise the fetcher would install the abandoned model and the re-run rounds up to that
+        epoch would never be uploaded."""
+        with self._ready_lock:
+            self._ready_branch += 1
+            self._ready = (epoch, data)
+            self._sent_epoch = epoch
 
     def _take_ready(self) -> tuple:
         """(epoch, b64) of the newest serialised checkpoint not uploaded yet, or (-1, '')."""
@@ -235,6 +250,7 @@ class ClientAgent(P.TrainerServicer):
                     except Exception as e:      # rendezvous failed (a member never showed up)
                         context.abort(grpc.StatusCode.ABORTED, f"data-plane group failed: {e}"[:500])
                 self.fedavg.transport = self.group.transport
+                self.fedavg.abort = self.group.abort_event
                 self._probe("group")
             elif world > 1:
                 context.abort(grpc.StatusCode.FAILED_PRECONDITION, "collective aggregation needs a GroupManager")
@@ -306,28 +322,25 @@ class ClientAgent(P.TrainerServicer):
                     self._probe("average")
                     tp = self.fedavg.transport
                     err = "peer collective timed out (a client was lost)" if tp is not None and tp.error() else ""
+                    err = err or self._lost_peer()
                 except Exception as e:          # gloo / RCCL error: a peer was lost mid-collective
                     err = f"collective failed: {e}"
             if err:
-                # the round is void: back to the global model it started from (identical on every survivor;
-                # a peer collective may have written the mean into part of the model before failing)
-                digest = self._restore_round_start()
-                self.metrics.write(role="client", address=self.address, event="round_aborted", round=rnd,
-                                   generation=gen, error=err[:200], restored_sum=digest)
-                # the lease's earlier rounds are committed: report how far this client got
-                self._lease_trailer(context, lease_stats, -1)
-                # ABORTED (not UNAVAILABLE): this client is alive, only the round is void
-                context.abort(grpc.StatusCode.ABORTED, err[:500])
+                self._void_round(rnd, gen, err, context, lease_stats)
             rec["allreduce_ms"] = t2.ms()
-            self._check_compressor()
             t3 = Timer()
             with phase("eval"):
                 self.trainer.evaluate()
                 ev = self.trainer.eval_stats()
             self._probe("eval")
+            # a stream-ordered collective (RCCL) the watchdog aborted surfaces only here, after the eval's sync
+            err = self._lost_peer() if world > 1 else ""
+            if err:
+                self._void_round(rnd, gen, err, context, lease_stats)
             rec["eval_ms"] = t3.ms()
             rec.update(ev.as_dict("test"))
             self.round = rnd
+            self._check_compressor(rnd)
             t4 = Timer()
             with phase("checkpoint"):
                 self._persist_async(ev.acc, rnd, keep=(rank == 0))
@@ -353,17 +366,35 @@ class ClientAgent(P.TrainerServicer):
                   + (f" | test acc {rec['test_acc']:.2f}%" if "test_acc" in rec else ""))
         return tr, ck_epoch, message
 
-    def _check_compressor(self) -> None:
+    def _lost_peer(self) -> str:
+        """The coordinator reported a lost client for this generation (abort watchdog)."""
+        g = self.group
+        if g is not None and g.abort_event.is_set():
+            return "collective aborted: the coordinator reported a lost client"
+        return ""
+
+    def _void_round(self, rnd: int, gen: int, err: str, context, lease_stats) -> None:
+        """The round is void: back to the global model it started from (identical on every survivor; a peer
+        collective may have written the mean into part of the model before failing), then ABORTED."""
+        digest = self._restore_round_start()
+        self.metrics.write(role="client", address=self.address, event="round_aborted", round=rnd,
+                           generation=gen, error=err[:200], restored_sum=digest)
+        # the lease's earlier rounds are committed: report how far this client got
+        self._lease_trailer(context, lease_stats, -1)
+        # ABORTED (not UNAVAILABLE): this client is alive, only the round is void
+        context.abort(grpc.StatusCode.ABORTED, err[:500])
+
+    def _check_compressor(self, rnd: int) -> None:
         """-c Y top-k: log the kernel's sticky overflow flag once (it is a kernel bug, never a data condition);
         checked every 64 rounds (the read synchronises)."""
         comp = getattr(self.fedavg, "compressor", None)
         over = getattr(comp, "overflowed", None)
-        if over is None or self._overflow_logged or self.round % 64:
+        if over is None or self._overflow_logged or rnd % 64:
             return
         if over(clear=False):
             self._overflow_logged = True
             self._log("WARNING: top-k select overflowed (entries beyond k were dropped on every rank)")
-            self.metrics.write(role="client", address=self.address, event="topk_overflow", round=self.round)
+            self.metrics.write(role="client", address=self.address, event="topk_overflow", round=rnd)
 
     def SendModel(self, request, context):
         meta = metadata_dict(context)
@@ -378,7 +409,9 @@ class ClientAgent(P.TrainerServicer):
             if comp is not None:
                 comp.reset(self.trainer)
             self.writer.submit_bytes(self.ckpt_path, data)
-            self.round = max(self.round, int(c.get("epoch", 0) or 0))
+            epoch = int(c.get("epoch", 0) or 0)
+            self._reset_ready(epoch, data)
+            self.round = max(self.round, epoch)
             self.trainer.evaluate()
             ev = self.trainer.eval_stats()
             self.metrics.write(role="client", address=self.address, event="send_model", round=self.round,

@@ -335,13 +335,18 @@ class Coordinator:
         t_send = time.time()
         self._lease_end = end
         futs = {}
+        timeout = self._train_deadline(lease)
+        gen = self.generation
         # blocking unary calls on the coordinator's pool (a grpc ``.future()`` call starts a channel spin thread
         # per call: ~1 ms per client per round on the control plane)
         for rank, addr in enumerate(live):
             stub = self.members[addr].stub
-            futs[addr] = (rank, self._pool.submit(stub.StartTrain.with_call, P.TrainRequest(rank=rank, world=world),
-                                                  timeout=self.cfg.train_timeout_s * lease, metadata=md))
-        replies, failed, client_rounds, ckpt_epochs, lease_stats, committed = {}, [], [], {}, None, {}
+            f = self._pool.submit(stub.StartTrain.with_call, P.TrainRequest(rank=rank, world=world),
+                                  timeout=timeout, metadata=md)
+            if world > 1 and self.store is not None:
+                f.add_done_callback(lambda f_, a_=addr: self._propagate_loss(f_, a_, gen))
+            futs[addr] = (rank, f)
+        replies, failed, client_rounds, ckpt_epochs, lease_stats, committed, ok_rounds = {}, [], [], {}, None, {}, {}
         for addr, (rank, f) in futs.items():
             try:
                 reply, call = f.result()
@@ -349,6 +354,7 @@ class Coordinator:
                 tm = dict(call.trailing_metadata() or ())
                 if "x-fedmi-client-round" in tm:
                     client_rounds.append(int(tm["x-fedmi-client-round"]))
+                    ok_rounds[rank] = int(tm["x-fedmi-client-round"])
                     self.members[addr].fedmi = True
                 if "x-fedmi-ckpt-epoch" in tm:
                     ckpt_epochs[rank] = int(tm["x-fedmi-ckpt-epoch"])
@@ -381,7 +387,14 @@ class Coordinator:
                 # completed before the failure stay committed (rank 0 checkpointed them).
                 self._log(f"round {rnd} aborted ({len(failed)} client(s) lost); rolling back survivors, regrouping")
                 self._last_live = None           # force a new generation even if every member answered ABORTED
-                self._catch_up_committed(live[0], committed.get(0))
+                target = committed.get(0)
+                if 0 in replies:
+                    # rank 0 finished the whole call: every round it ran completed its all-reduce (all members
+                    # contributed), so they are committed even though another rank failed afterwards
+                    target = ok_rounds.get(0, end)
+                    if replies[0]:
+                        self._install_global(ck.from_b64(replies[0]), ckpt_epochs.get(0, target))
+                self._catch_up_committed(live[0], target)
                 if self.latest_model is not None:
                     if self.installed_epoch >= 0 and self.installed_epoch < self.round:
                         # rank 0's newest committed round was not reachable: the round counter follows
@@ -461,6 +474,35 @@ class Coordinator:
         now = time.time()
         rows += [(r, None, None, now) for r in range(rnd, end + 1) if r not in have]
         return sorted(rows)
+
+    def _train_deadline(self, lease: int) -> float:
+        """StartTrain deadline: the per-round timeout plus the lease's expected run time with headroom (a
+        multiple of the per-round timeout would let a stuck-but-alive client hold a lease for hours)."""
+        if lease <= 1:
+            return self.cfg.train_timeout_s
+        if self._round_s is None:
+            return self.cfg.train_timeout_s * lease
+        return self.cfg.train_timeout_s + 4.0 * lease * self._round_s
+
+    def _propagate_loss(self, f, addr: str, gen: int) -> None:
+        """Done-callback of a StartTrain future: an unreachable client (not ABORTED / FAILED_PRECONDITION,
+        which are answers from a live client) aborts its generation's collective on every survivor at once
+        -- they would otherwise wait out the collective timeout inside the barrier (reference: the dead client
+        is marked inactive at its failed RPC, src/server.py:59-62)."""
+        if f.cancelled():
+            return
+        e = f.exception()
+        if not isinstance(e, grpc.RpcError):
+            return
+        code = e.code() if callable(getattr(e, "code", None)) else None
+        if code in (grpc.StatusCode.ABORTED, grpc.StatusCode.FAILED_PRECONDITION):
+            return
+        try:
+            self.store.abort_generation(gen, addr)
+            self.metrics.write(role=self.role, event="loss_propagated", generation=gen, client=addr,
+                               code=getattr(code, "name", str(code)))
+        except Exception as err:  # pragma: no cover - the store is ours; best effort
+            self._log(f"could not propagate the loss of {addr}: {err!r}")
 
     # ---- rejoin tracker (src/server.py:78-101) --------------------------------------
     def _track(self) -> None:

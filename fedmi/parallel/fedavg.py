@@ -13,6 +13,7 @@ disappears from the steady state.
 """
 from __future__ import annotations
 
+import threading
 import time
 from dataclasses import dataclass, field
 from typing import Optional
@@ -36,7 +37,19 @@ def _supports_avg(group) -> bool:
         return False
 
 
-def allreduce_mean_(t: torch.Tensor, group=None) -> torch.Tensor:
+def _run(fn, t: torch.Tensor, group, abort: Optional[threading.Event], **kw) -> None:
+    """One collective.  RCCL is stream-ordered (an abort is ncclCommAbort from the watchdog); a host-blocking
+    backend (gloo) runs it ``async_op`` and stops waiting when ``abort`` is set
+    (:func:`fedmi.parallel.group.wait_work`)."""
+    if abort is None or _supports_avg(group):
+        fn(t, group=group, **kw)
+        return
+    from .group import wait_work
+
+    wait_work(fn(t, group=group, async_op=True, **kw), abort, fn.__name__)
+
+
+def allreduce_mean_(t: torch.Tensor, group=None, abort: Optional[threading.Event] = None) -> torch.Tensor:
     """In-place mean over the group (RCCL ncclAvg; SUM+scale on gloo)."""
     w = _world(group)
     if w == 1:
@@ -44,28 +57,28 @@ def allreduce_mean_(t: torch.Tensor, group=None) -> torch.Tensor:
     if _supports_avg(group):
         dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group)
     else:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        _run(dist.all_reduce, t, group, abort, op=dist.ReduceOp.SUM)
         t.div_(w)
     return t
 
 
-def allreduce_int_mean_(t: torch.Tensor, group=None) -> torch.Tensor:
+def allreduce_int_mean_(t: torch.Tensor, group=None, abort: Optional[threading.Event] = None) -> torch.Tensor:
     """Integer buffers: sum then floor-divide (== reference float mean + int64 truncation)."""
     w = _world(group)
     if w == 1:
         return t
-    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    _run(dist.all_reduce, t, group, abort, op=dist.ReduceOp.SUM)
     t.div_(w, rounding_mode="floor")
     return t
 
 
-def broadcast_state_(trainer: LocalTrainer, src: int = 0, group=None) -> None:
+def broadcast_state_(trainer: LocalTrainer, src: int = 0, group=None, abort: Optional[threading.Event] = None) -> None:
     """Give every client rank ``src``'s model (fixes reference quirk A7: independent random inits)."""
     if _world(group) == 1:
         return
-    dist.broadcast(trainer.float_state(), src=src, group=group)
+    _run(dist.broadcast, trainer.float_state(), group, abort, src=src)
     for b in trainer.int_state():
-        dist.broadcast(b, src=src, group=group)
+        _run(dist.broadcast, b, group, abort, src=src)
     trainer.after_aggregate()
 
 
@@ -89,6 +102,7 @@ class FedAvg:
     compressor: Optional[object] = None      # fedmi.parallel.compress.Compressor
     transport: Optional[object] = None       # fedmi.parallel.peer.PeerAllReduce
     timer: AggregationTimer = field(default_factory=AggregationTimer)
+    abort: Optional[threading.Event] = None  # the generation's loss flag (GroupManager.abort_event)
 
     def world(self) -> int:
         if self.transport is not None:
@@ -116,12 +130,12 @@ class FedAvg:
             elif self.transport is not None:
                 self.transport.allreduce_mean_(trainer.float_state())
             else:
-                allreduce_mean_(trainer.float_state(), self.group)
+                allreduce_mean_(trainer.float_state(), self.group, self.abort)
             for b in trainer.int_state():
                 if self.transport is not None:
                     self.transport.allreduce_mean_(b)
                 else:
-                    allreduce_int_mean_(b, self.group)
+                    allreduce_int_mean_(b, self.group, self.abort)
         elif self.compressor is not None:
             # a client training alone holds the global model: it becomes the new anchor
             self.compressor.reset(trainer)
@@ -140,7 +154,7 @@ class FedAvg:
                     self.transport.broadcast_(b, src)
             trainer.after_aggregate()
         else:
-            broadcast_state_(trainer, src, self.group)
+            broadcast_state_(trainer, src, self.group, self.abort)
         if self.compressor is not None:
             self.compressor.reset(trainer)
 

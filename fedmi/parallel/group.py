@@ -19,6 +19,12 @@ Two data planes:
   GPUs, ``gloo`` on CPU hosts).  A broken RCCL communicator is ABORTED
   (``ncclCommAbort`` via the process group), never destroyed: destroy would
   block on the dead peer.  The collective timeout is short (``timeout_s``).
+* Loss propagation: the coordinator learns of a dead client within milliseconds (its StartTrain fails with
+  UNAVAILABLE) and sets ``abort`` in the generation's store namespace.  Every member runs a watchdog
+  thread on that key; on it, the peer barriers fail at their next poll (host-pinned abort word), an RCCL
+  communicator is aborted (``ncclCommAbort``) and a gloo collective stops waiting -- the survivors leave
+  the collective at once instead of after ``timeout_s`` (reference: a dead client is dropped at its next
+  failed RPC, src/server.py:59-62, 72-75).
 * ``auto`` (GPU clients' default): at the first generation with world > 1 the
   client forms BOTH, verifies the peer kernels against the process group's
   all-reduce on random data and times both on a model-sized buffer
@@ -30,6 +36,7 @@ from __future__ import annotations
 
 import datetime
 import threading
+import time
 from dataclasses import dataclass
 from typing import Optional
 
@@ -46,10 +53,63 @@ class Membership:
     store_port: int
 
 
-def abort_default_group() -> None:
-    """Tear down the default process group without talking to (possibly dead) peers."""
-    if not dist.is_initialized():
+ABORT_KEY = "abort"          # per generation, under the client's "fedmi/gen<g>" store prefix
+ABORT_POLL_S = 0.02
+
+
+class CollectiveAborted(RuntimeError):
+    """A collective was abandoned because the coordinator reported a lost client."""
+
+
+def wait_work(work, abort: Optional[threading.Event], what: str = "collective") -> None:
+    """Wait for an ``async_op`` collective, giving up as soon as ``abort`` is set.  Used for host-blocking
+    backends (gloo): an abandoned gloo work keeps its worker thread until its own timeout, so the group
+    it belongs to is detached, not destroyed (:func:`_detach_default_group`)."""
+    if abort is None:
+        work.wait()
         return
+    while not work.is_completed():
+        if abort.is_set():
+            raise CollectiveAborted(f"{what} abandoned: the coordinator reported a lost client")
+        time.sleep(0.0002)
+    work.wait()               # completed: surfaces its error, if any
+
+
+def _detach_default_group() -> bool:
+    """Forget the default gloo group WITHOUT shutting it down (its destructor would join a worker thread
+    still blocked on the dead peer until the gloo timeout).  The object stays referenced by the caller's
+    retired list.  Private c10d state: returns False (caller destroys normally) if the layout differs."""
+    c = dist.distributed_c10d
+    w = getattr(c, "_world", None)
+    pg = getattr(w, "default_pg", None) if w is not None else None
+    if pg is None:
+        return False
+    try:
+        for name in ("pg_map", "pg_names", "pg_group_ranks", "pg_backend_config", "pg_to_tag",
+                     "pg_coalesce_state", "pg_default_device"):
+            d = getattr(w, name, None)
+            if isinstance(d, dict):
+                d.pop(pg, None)
+        tags = getattr(w, "tags_to_pg", None)
+        if isinstance(tags, dict):
+            for k in list(tags):
+                tags[k] = [g for g in tags[k] if g is not pg]
+        w.default_pg = None
+    except Exception:  # pragma: no cover - torch internals moved
+        return False
+    return True
+
+
+def abort_default_group(pending: bool = False) -> object:
+    """Tear down the default process group without talking to (possibly dead) peers.  ``pending``: a gloo
+    collective was abandoned on it -- detach instead of destroy.  Returns the detached group (keep it
+    referenced) or None."""
+    if not dist.is_initialized():
+        return None
+    if pending and dist.get_backend() == "gloo":
+        pg = dist.distributed_c10d._get_default_group()
+        if _detach_default_group():
+            return pg
     try:
         if dist.get_backend() == "nccl":
             dist.distributed_c10d._abort_process_group()     # ncclCommAbort: never blocks on a dead peer
@@ -60,6 +120,7 @@ def abort_default_group() -> None:
             dist.destroy_process_group()
         except Exception:
             pass
+    return None
 
 
 class GroupManager:
@@ -86,8 +147,17 @@ class GroupManager:
         self.generations_joined = 0
         self.selected: Optional[str] = None   # auto: "peer" | "dist" once decided
         self.select_info: dict = {}
+        # loss propagation: set by the watchdog when the coordinator reports a lost client for the current
+        # generation (a fresh Event per generation; FedAvg polls it around host-blocking collectives)
+        self.abort_event = threading.Event()
+        self.aborts_seen = 0
+        self._watch_stop: Optional[threading.Event] = None
+        self._detached: list = []            # gloo groups left with an abandoned collective (never destroyed)
 
     def _drop(self) -> None:
+        if self._watch_stop is not None:
+            self._watch_stop.set()
+            self._watch_stop = None
         if self.transport is not None:
             try:
                 self.transport.close(barrier=False)
@@ -95,8 +165,45 @@ class GroupManager:
                 pass
             self._retired = (self._retired + [self.transport])[-4:]
             self.transport = None
-        abort_default_group()
+        pg = abort_default_group(pending=self.abort_event.is_set())
+        if pg is not None:
+            self._detached.append(pg)
         self.current = None
+        self.abort_event = threading.Event()
+
+    def _watch(self, m: Membership, stop: threading.Event, ev: threading.Event) -> None:
+        """Watchdog of generation ``m``: its own store connection (the main thread's is not shared across
+        threads), one ``check`` of the abort key every ABORT_POLL_S."""
+        try:
+            store = dist.TCPStore(m.store_host, m.store_port, world_size=None, is_master=False,
+                                  timeout=self.timeout, wait_for_workers=False)
+            pstore = dist.PrefixStore(f"fedmi/gen{m.generation}", store)
+        except Exception:  # pragma: no cover - the coordinator is gone; the collective timeout still bounds us
+            return
+        while not stop.wait(ABORT_POLL_S):
+            try:
+                hit = pstore.check([ABORT_KEY])
+            except Exception:
+                return
+            if hit:
+                self._on_abort(ev)
+                return
+
+    def _on_abort(self, ev: threading.Event) -> None:
+        if ev is not self.abort_event or ev.is_set():
+            return                              # a later generation already replaced this one
+        ev.set()
+        self.aborts_seen += 1
+        tp = self.transport
+        if tp is not None:
+            tp.request_abort()
+        elif dist.is_initialized() and self.backend == "nccl":
+            abort_default_group()               # ncclCommAbort: the spinning RCCL kernel exits
+        # gloo: FedAvg's wait_work() sees the event and abandons the work
+
+    def request_abort(self) -> None:
+        """Abort the current generation's collectives locally (tests; the watchdog's action)."""
+        self._on_abort(self.abort_event)
 
     def ensure(self, m: Membership) -> bool:
         """Join (or re-join) the data-plane group described by ``m``; True if it changed."""
@@ -116,6 +223,9 @@ class GroupManager:
                     self.transport = self._peer(m, pstore)
                 else:
                     self._init_group(self.backend, m, pstore)
+                self._watch_stop = threading.Event()
+                threading.Thread(target=self._watch, args=(m, self._watch_stop, self.abort_event),
+                                 name=f"fedmi-abort-watch-g{m.generation}", daemon=True).start()
             self.current = m
             self.generations_joined += 1
             return True
@@ -162,10 +272,8 @@ class GroupManager:
 
     def interrupt(self) -> None:
         """Called WITHOUT the agent lock when a newer generation arrives while an old round is
-        still blocked in a collective: abort the RCCL communicator so that round fails fast.
-        (Peer collectives need nothing: their barriers time out on their own.)"""
-        if self.transport is None and dist.is_initialized() and self.backend == "nccl":
-            abort_default_group()
+        still blocked in a collective: that round fails fast (the same action as the abort watchdog)."""
+        self._on_abort(self.abort_event)
 
     def shutdown(self) -> None:
         with self._lock:
@@ -180,3 +288,9 @@ class StoreHost:
                                    timeout=datetime.timedelta(seconds=timeout_s), wait_for_workers=False)
         self.host = host
         self.port = self.store.port
+        self._lock = threading.Lock()
+
+    def abort_generation(self, generation: int, reason: str = "") -> None:
+        """Tell every member of ``generation`` that a client was lost (their watchdogs abort the collective)."""
+        with self._lock:
+            self.store.set(f"fedmi/gen{generation}/{ABORT_KEY}", (reason or "lost").encode()[:200])

@@ -70,9 +70,20 @@ class PeerAllReduce:
             self.colocated = False
         self._gate_n = 0
         self._gate_failed = False
+        self._abort = False
+
+    def request_abort(self) -> None:
+        """Called from a watchdog thread when the coordinator reports a lost client: every barrier of this
+        communicator -- the kernel's (host-pinned abort word) and the co-located host gate -- fails at its
+        next poll instead of waiting out ``timeout_ms``.  Sticky for this generation's communicator."""
+        self._abort = True
+        self.comm.request_abort()
 
     def _gate(self) -> bool:
         """False: a peer never reached this collective (its kernel must not be launched; ``error()`` is set)."""
+        if self._abort:
+            self._gate_failed = True
+            return False
         if not self.colocated:
             return True
         if self._gate_failed:
@@ -83,7 +94,7 @@ class PeerAllReduce:
         self.store.add(key, 1)
         deadline = time.monotonic() + self.timeout_ms / 1e3
         while int(self.store.add(key, 0)) < self.world:
-            if time.monotonic() > deadline:
+            if self._abort or time.monotonic() > deadline:
                 self._gate_failed = True
                 return False
             time.sleep(0.0002)

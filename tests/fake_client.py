@@ -32,6 +32,7 @@ class FakeClient(P.TrainerServicer):
         self.ready = None            # (epoch, None): serialised on demand, like the writer's ready buffer
         self.installed = []          # epochs installed by SendModel (rollbacks / resyncs)
         self.abort_at = None
+        self.lost_after_lease = False    # finish every round of the call, then fail UNAVAILABLE (died before replying)
         self.work_s = work_s
         self.lock = threading.Lock()
 
@@ -54,6 +55,8 @@ class FakeClient(P.TrainerServicer):
             self.rounds = r
             stats.append((r, 1.0 / r, 10.0 + r, time.time()))
         self.ready = (self.rounds, None)
+        if self.lost_after_lease:
+            context.abort(grpc.StatusCode.UNAVAILABLE, "Socket closed")
         context.set_trailing_metadata((("x-fedmi-client-round", str(self.rounds)),
                                        ("x-fedmi-ckpt-epoch", "-1"),
                                        ("x-fedmi-lease-stats", json.dumps(stats))))
@@ -68,6 +71,7 @@ class FakeClient(P.TrainerServicer):
             context.set_trailing_metadata((("x-fedmi-ckpt-epoch", str(epoch)),))
             return P.SendModelReply(reply=ck.to_b64(model_bytes(epoch, epoch)) if ready and epoch > have else "")
         self.installed.append(ck.from_bytes(ck.from_b64(request.model))["epoch"])
+        self.ready = (self.installed[-1], None)
         return P.SendModelReply(reply="success")
 
     def HeartBeat(self, request, context):

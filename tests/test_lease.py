@@ -154,6 +154,91 @@ def test_single_round_abort_with_rank0_ahead(tmp_path):
             s.stop(grace=0)
 
 
+def test_nonzero_rank_lost_after_final_round_keeps_rank0_lease(tmp_path):
+    """rank 0 finished the whole lease and replied OK, a non-zero rank died after the last collective
+    (UNAVAILABLE before its reply landed).  Every round of the lease completed its all-reduce, so the coordinator
+    commits up to rank 0's round instead of rolling every survivor back a whole lease; the loss is propagated to
+    the generation's store (abort key) at once."""
+    fakes, servers, addrs = _serve(2)
+    try:
+        metrics = MetricsLog(tmp_path / "coord.jsonl")
+        cfg = CoordinatorConfig(clients=addrs, rounds=40, agg="collective", root=str(tmp_path / "srv"),
+                                rpc_timeout_s=10, train_timeout_s=30, heartbeat_s=5.0, lease_rounds=8, lease_s=0,
+                                ckpt_fetch_interval_s=0)
+        coord = Coordinator(cfg, metrics=metrics)
+        assert coord.run_round() and coord.round == 8
+        gen = coord.generation
+        fakes[1].lost_after_lease = True         # rounds 9-16 all run on both, then rank 1 dies
+        assert not coord.run_round()
+        assert coord.round == 16 and coord.installed_epoch == 16, (coord.round, coord.installed_epoch)
+        assert fakes[0].installed[-1:] == [16], fakes[0].installed          # rolled to rank 0's round, not to 8
+        assert coord.client_status()[addrs[1]] is False
+        assert coord.store.store.check([f"fedmi/gen{gen}/abort"])        # survivors' watchdogs see the loss
+        metrics.flush()
+        ev = [json.loads(x) for x in (tmp_path / "coord.jsonl").read_text().splitlines()]
+        assert [r["client"] for r in ev if r.get("event") == "loss_propagated"] == [addrs[1]]
+        seen = []
+        orig = coord._meta
+        coord._meta = lambda rnd, live, lease=1: (seen.append(rnd), orig(rnd, live, lease))[1]
+        assert coord.run_round() and seen[0] == 17
+        coord.close()
+    finally:
+        for s in servers:
+            s.stop(grace=0)
+
+
+def test_lease_deadline_follows_round_time(tmp_path):
+    """a lease's StartTrain deadline is the per-round timeout plus the lease's expected run time, not
+    lease x the per-round timeout (a stuck-but-alive client would otherwise hold a 64-round lease for hours)."""
+    cfg = CoordinatorConfig(clients=[], rounds=10, agg="grpc", root=str(tmp_path / "srv"), train_timeout_s=600)
+    coord = Coordinator(cfg)
+    try:
+        assert coord._train_deadline(1) == 600
+        coord._round_s = 0.01
+        assert coord._train_deadline(64) == pytest.approx(600 + 4 * 64 * 0.01)
+        coord._round_s = None
+        assert coord._train_deadline(4) == 2400          # no measured round yet: the old bound
+    finally:
+        coord.close()
+
+
+def test_rollback_below_rank0_checkpoint_resets_upload_buffer(tmp_path):
+    """rank 0 serialised rounds up to 5, then the coordinator rolls it back to round 3 (SendModel).  The
+    fetch path must serve the installed round-3 model (nothing newer than have=3), and after the re-run round 4 the
+    fetched model is the NEW round 4 -- never the abandoned branch's round 5 labelled with a higher epoch."""
+    from fedmi.control.client_agent import META_FETCH, META_HAVE, META_LEASE, META_ROUND, ClientAgent, serve_client
+    from helpers import small_trainer
+
+    addr = f"127.0.0.1:{free_port()}"
+    ag = ClientAgent(small_trainer("mlp", seed=0), addr, root=tmp_path / "c0", agg="collective", verbose=False)
+    srv, _ = serve_client(ag, addr)
+    stub = P.TrainerStub(P.make_channel(addr))
+
+    def fetch(have):
+        reply, call = stub.SendModel.with_call(P.SendModelRequest(model=""), timeout=30,
+                                               metadata=[(META_FETCH, "1"), (META_HAVE, str(have))])
+        return int(dict(call.trailing_metadata())["x-fedmi-ckpt-epoch"]), reply.reply
+
+    try:
+        stub.StartTrain(P.TrainRequest(rank=0, world=1), timeout=120, metadata=[(META_ROUND, "1"), (META_LEASE, "3")])
+        committed3 = ck.to_bytes(ck.make_checkpoint(ag.trainer.state_dict(), acc=1, epoch=3))
+        stub.StartTrain(P.TrainRequest(rank=0, world=1), timeout=120, metadata=[(META_ROUND, "4"), (META_LEASE, "2")])
+        ag.writer.flush()
+        assert fetch(-1)[0] == 5
+        stub.SendModel(P.SendModelRequest(model=ck.to_b64(committed3)), timeout=60)        # rollback to round 3
+        epoch, b64 = fetch(3)
+        assert epoch == 3 and b64 == "", epoch                       # not the abandoned round 5
+        stub.StartTrain(P.TrainRequest(rank=0, world=1), timeout=120, metadata=[(META_ROUND, "4")])
+        ag.writer.flush()
+        epoch, b64 = fetch(3)
+        assert epoch == 4 and b64
+        got = ck.from_bytes(ck.from_b64(b64))["net"]
+        assert ck.state_digest(got) == ck.state_digest(ag.trainer.state_dict())
+    finally:
+        srv.stop(None)
+        ag.close()
+
+
 @pytest.mark.slow
 def test_lease_with_real_clients(tmp_path):
     from helpers import spawn_client, wait_heartbeat
