@@ -12,11 +12,14 @@ A *step* is one federated round with the reference's semantics
   2. FedAvg of the full model across clients   [hand-written hipIpc peer all-reduce
      over xGMI (csrc/comm/peer_comm.hip) or RCCL -- ``--allreduce auto`` verifies
      both against each other at start-up and keeps the faster]
-  3. the global model is evaluated on the full 10,000-image test set: split
-     over the N clients (they all hold the same averaged model), per-round
-     (loss, correct, count) kept on device and summed over clients in one
-     collective -- the same numbers as every client evaluating all of it
-     (``--eval-full`` runs that reference-literal redundant variant)
+  3. every client evaluates the global model on the full 10,000-image test set
+     (reference-literal: src/client.py:30 -> src/main.py:167-191).  At N>1 a
+     second timed loop of the same length re-runs the round with the test set
+     split over the clients (they all hold the same averaged model; per-round
+     (loss, correct, count) summed over clients in one collective -- the same
+     numbers, 1/N of the eval work) and reports it as
+     ``rounds_per_sec_eval_split``; ``--eval-split`` makes that the headline
+     ``value`` instead (labelled in ``config.eval_split``)
   4. the global model is persisted as Primary/optimizedModel.pth (rank 0) and
      every client checkpoint as checkpoint/<client>.pth ({'net','acc','epoch'}),
      by the native C++ writer (csrc/runtime/ckpt_writer.cpp: async device->pinned
@@ -155,8 +158,12 @@ def main() -> int:
                          "the peer kernel against RCCL and time both, keep the faster")
     ap.add_argument("--no-eval", action="store_true", help="skip per-round eval (NOT the headline config)")
     ap.add_argument("--eval-full", action="store_true",
-                    help="every client evaluates the whole test set (reference-literal, redundant); default: "
-                         "the 10k test set is split over the clients and the accumulators summed")
+                    help="(the default) every client evaluates the whole test set, as the reference does")
+    ap.add_argument("--eval-split", action="store_true",
+                    help="headline loop with the 10k test set split over the clients and the accumulators summed "
+                         "(same numbers, 1/N of the eval work); labelled in config.eval_split")
+    ap.add_argument("--no-split-compare", action="store_true",
+                    help="N>1: skip the second timed loop that measures the split-eval round")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--ckpt-dir", default=None)
     ap.add_argument("--ckpt-slots", type=int, default=4, help="pinned snapshot slots of the checkpoint writer")
@@ -237,9 +244,12 @@ def main() -> int:
             return 2
     agg = FedAvg(compressor=make_compressor(args.compress, args.topk_ratio, trainer, args.compress_warmup),
                  transport=transport)
-    if shard_world > 1 and not args.eval_full:
+    split_eval = shard_world > 1 and args.eval_split
+    if split_eval:
         trainer.set_test_data(eval_shard(data.test, rank, shard_world))
-    hist = EvalHistory(trainer, args.warmup + args.steps)
+    # N>1 with full per-client eval: a second timed loop measures the split-eval round (reported, not headline)
+    compare_split = shard_world > 1 and not split_eval and not args.no_split_compare and not args.no_eval
+    hist = EvalHistory(trainer, args.warmup + args.steps + (args.steps + 1 if compare_split else 0))
     if args.trace:
         ys = trainer.train_set.y.long().cpu()
         print(f"[trace] rank {rank} start: {len(ys)} train samples, labels {torch.bincount(ys, minlength=10).tolist()}, "
@@ -308,7 +318,7 @@ def main() -> int:
     tl = [time.perf_counter()]
     writer.flush()
     tl.append(time.perf_counter())
-    rounds_eval = hist.reduce() if not args.no_eval and not args.eval_full else None
+    rounds_eval = hist.reduce() if not args.no_eval and split_eval else None
     tl.append(time.perf_counter())
     barrier()
     t1 = time.perf_counter()
@@ -318,6 +328,24 @@ def main() -> int:
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     T = float(elapsed.item())
+    full_eval_stats = trainer.eval_stats() if not args.no_eval and not split_eval else None
+    T_split = None
+    if compare_split:
+        # the same rounds with the test set split over the clients (after the headline's timed region)
+        trainer.set_test_data(eval_shard(data.test, rank, shard_world))
+        one_round(args.warmup + args.steps)              # untimed: the eval graph re-captures for the shard
+        writer.flush()
+        barrier()
+        t2 = time.perf_counter()
+        for r in range(args.warmup + args.steps + 1, args.warmup + 2 * args.steps + 1):
+            one_round(r)
+        writer.flush()
+        hist.reduce()
+        barrier()
+        el2 = torch.tensor([time.perf_counter() - t2], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(el2, op=dist.ReduceOp.MAX)
+        T_split = float(el2.item())
 
     # end-of-run guard (outside the timed region): no peer barrier timed out on any rank and every
     # client holds the bit-identical global model -- else the throughput above is not a FedAvg run
@@ -332,7 +360,7 @@ def main() -> int:
     elif rounds_eval is not None:
         ev_stats = rounds_eval[-1]
     else:
-        ev_stats = trainer.eval_stats()
+        ev_stats = full_eval_stats
     rounds_per_s = args.steps / T
     value = rounds_per_s * N_TRAIN / (args.project_world or 1)
     base_r = _baseline_rounds(args.model, world)
@@ -358,13 +386,21 @@ def main() -> int:
                    else f"projection-of-fedavg-dp{args.project_world} (rank 0's share, no collective)",
                    "per_client_batch": BATCH,
                    "local_epochs_per_round": 1, "eval_per_round": not args.no_eval,
-                   "eval_split": "full-per-client" if args.eval_full or shard_world == 1
-                   else f"1/{shard_world}-per-client",
+                   "eval_split": "full-per-client" if not split_eval else f"1/{shard_world}-per-client",
                    "data_split": f"noniid-{args.noniid}-shards" if args.noniid else "strided-iid",
                    "aggregation": agg.label() + (" [1-GPU rehearsal]" if rehearse and world > 1 else ""),
                    "hip_graph": not args.no_graph},
         "rounds_per_sec": round(rounds_per_s, 4),
+        **({"rounds_per_sec_eval_split": round(args.steps / T_split, 4),
+            "value_eval_split": round(args.steps / T_split * N_TRAIN / (args.project_world or 1), 3)}
+           if T_split else {}),
         "samples_per_sec_per_client": round(value / world, 3),
+        # what actually carried FedAvg, and among how many ranks
+        "data_plane": {"aggregation": agg.label(), "world": agg.world(),
+                       "collective_world": (transport.world if transport is not None
+                                            else (dist.get_world_size() if dist.is_initialized() else 1)),
+                       "backend": ("peer-hipipc" if transport is not None
+                                   else (dist.get_backend() if dist.is_initialized() else "none"))},
         "baseline_rounds_per_sec": base_r,
         "last_round": {"train_loss": round(tr_stats.loss, 4), "train_acc": round(tr_stats.acc, 3),
                        **({"test_loss": round(ev_stats.loss, 4), "test_acc": round(ev_stats.acc, 3)}

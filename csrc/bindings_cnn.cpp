@@ -81,7 +81,7 @@ void launch_dw_dgrad(hipStream_t, const DwShape&, const bf16*, const float*, bf1
 long dw_wgrad_ws_floats(const DwShape&);
 void launch_dw_wgrad(hipStream_t, const DwShape&, const bf16*, const bf16*, float*, float*, long, int);
 void launch_prep_input(hipStream_t, const uint8_t*, int, const int*, int, int, uint32_t, const int*, bf16*);
-void launch_sched_next(hipStream_t, const int*, int*, int*);
+void launch_sched_next(hipStream_t, const int*, int*, int*, double*, long);
 void launch_bn_apply(hipStream_t, const bf16*, const BNDesc&, const bf16*, const BNDesc*, const bf16*, bf16*, int, int,
                      float, float, int, int, int, float*);
 void launch_bn_bwd(hipStream_t, const BNBwdDesc&, double*, int, int, double*, long, int, int, int, int);
@@ -277,8 +277,8 @@ void fedmi_bind_cnn(py::module_& m) {
     launch_maxpool2_bwd(S(st), P<const bf16>(x), P<const bf16>(dy), P<bf16>(dx), N, H, W, C);
     check("maxpool2_bwd");
   });
-  m.def("sched_next", [](uintptr_t st, uintptr_t sched, uintptr_t counter, uintptr_t cur) {
-    launch_sched_next(S(st), P<const int>(sched), P<int>(counter), P<int>(cur));
+  m.def("sched_next", [](uintptr_t st, uintptr_t sched, uintptr_t counter, uintptr_t cur, uintptr_t zero, long n) {
+    launch_sched_next(S(st), P<const int>(sched), P<int>(counter), P<int>(cur), P<double>(zero), n);
     check("sched_next");
   });
   m.def("bn_apply", [](uintptr_t st, uintptr_t z, const py::dict& a, uintptr_t z2, py::object b, uintptr_t res,

@@ -936,13 +936,19 @@ __global__ __launch_bounds__(256) void maxpool3_bwd_kernel(const bf16* __restric
   }
 }
 
-// cur[0] = sched[counter[0]++]  (first node of a captured training step)
-__global__ void sched_next_kernel(const int* __restrict__ sched, int* __restrict__ counter, int* __restrict__ cur) {
-  if (threadIdx.x == 0) {
+// cur[0] = sched[counter[0]++]  (first node of a captured training step); the other lanes / workgroups zero the
+// step's fp64 BN-statistics accumulators (n doubles, 16-B stores): one fedmi launch instead of sched + an ATen fill
+__global__ __launch_bounds__(256) void sched_next_kernel(const int* __restrict__ sched, int* __restrict__ counter,
+                                                         int* __restrict__ cur, double* __restrict__ zero, long n) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     const int i = counter[0];
     cur[0] = sched[i];
     counter[0] = i + 1;
   }
+  const long n2 = n >> 1;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n2; i += (long)gridDim.x * 256)
+    reinterpret_cast<double2*>(zero)[i] = make_double2(0.0, 0.0);
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 64) zero[n - 1] = 0.0;
 }
 
 int grid_for(long nv) { return (int)std::min<long>((nv + 255) / 256, 2048); }
@@ -1012,8 +1018,10 @@ void launch_prep_input(hipStream_t st, const uint8_t* images, int base, const in
                      augment, seed, round_ctr, out);
 }
 
-void launch_sched_next(hipStream_t st, const int* sched, int* counter, int* cur) {
-  hipLaunchKernelGGL(sched_next_kernel, dim3(1), dim3(64), 0, st, sched, counter, cur);
+void launch_sched_next(hipStream_t st, const int* sched, int* counter, int* cur, double* zero, long n) {
+  if (zero == nullptr) n = 0;
+  const int grid = (int)std::max<long>(1, std::min<long>(((n >> 1) + 255) / 256, 256));
+  hipLaunchKernelGGL(sched_next_kernel, dim3(grid), dim3(256), 0, st, sched, counter, cur, zero, n);
 }
 
 // co_out (optional): BN-A's scale / shift [2][C] as applied (a backward that derives the ReLU mask from z)

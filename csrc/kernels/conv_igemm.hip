@@ -1138,6 +1138,115 @@ __global__ __launch_bounds__(256) void dgrad_pack_kernel(DPackTable t) {
 }
 
 // ---------------------------------------------------------------------------
+// Network-input ("stem") 3x3 / stride 1 / pad 1 conv on the 8-channel padded image (3 real channels), O = 16 * OT
+// output channels (ResNet / VGG / PreAct: 64, MobileNet(V2): 32).  K = 9 taps x 8 channels is tiny, so the
+// generic implicit GEMM (128-row tiles, LDS staging, 2 K steps) spent 16-17 us on a memory-bound 0.45 GFLOP
+// conv.  Here every MFMA fragment is ONE 16-byte load: with the product transposed (A = filters [o][k],
+// B = im2col^T [k][pixel]) a lane's 8 consecutive k are one tap's 8 channels -- of filter o (A, kept in registers
+// for the whole kernel) or of one input pixel (B, straight from global memory, zero in the halo).  A wave takes
+// 16 output pixels per step: 3 B loads per lane, 3 * OT MFMAs (taps 0-3, 4-7, 8 + zero pad), and the 16x16 output
+// tiles land as 4 consecutive channels of one pixel per lane (8-byte stores).  BatchNorm statistics of
+// bf16(y) - shift as in the other epilogues: per-lane sums, 16-lane shuffles, a workgroup LDS combine, fp64
+// replica atomics.
+// ---------------------------------------------------------------------------
+struct StemGeom {
+  int N, H, W, O, M;   // input [N][H][W][8], output [N][H][W][O], M = N * H * W
+};
+
+template <int OT>
+__global__ __launch_bounds__(256) void conv_stem_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wr,
+                                                        bf16* __restrict__ y, double* __restrict__ stats,
+                                                        const float* __restrict__ shift, StemGeom g) {
+  constexpr int O = 16 * OT;
+  __shared__ float red[4][2][O];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kq = lane >> 4;        // k block of this lane: taps ks * 4 + kq
+  const int col = lane & 15;       // A row (filter) / B column (pixel) of this lane
+  bf16x8 a[OT][3];
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const int tap = ks * 4 + kq;
+      a[ot][ks] = tap < 9 ? *reinterpret_cast<const bf16x8*>(wr + ((ot * 16 + col) * 9 + tap) * 8) : zero8();
+    }
+  float sh[OT][4], s1[OT][4], s2[OT][4];
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sh[ot][e] = shift != nullptr ? shift[ot * 16 + kq * 4 + e] : 0.f;
+      s1[ot][e] = s2[ot][e] = 0.f;
+    }
+  const int ntiles = (g.M + 15) >> 4;
+  const int nwaves = gridDim.x * 4;
+  for (int t = blockIdx.x * 4 + wave; t < ntiles; t += nwaves) {
+    const int m = t * 16 + col;
+    const bool mok = m < g.M;
+    const int mm = mok ? m : 0;
+    const int n = mm / (g.H * g.W), pq = mm - n * g.H * g.W;
+    const int p = pq / g.W, q = pq - p * g.W;
+    bf16x8 b[3];
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const int tap = ks * 4 + kq;
+      const int r = tap / 3, s = tap - (tap / 3) * 3;
+      const int h = p + r - 1, w = q + s - 1;
+      const bool ok = mok && tap < 9 && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (ok ? ((long)(n * g.H + h) * g.W + w) * 8 : 0));
+      b[ks] = ok ? v : zero8();
+    }
+    f32x4 acc[OT];
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) {
+      acc[ot] = zero4();
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) acc[ot] = mfma16(a[ot][ks], b[ks], acc[ot]);
+    }
+    if (mok) {
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot) {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = (bf16)acc[ot][e];
+          const float v = (float)o[e] - sh[ot][e];
+          s1[ot][e] += v;
+          s2[ot][e] += v * v;
+        }
+        *reinterpret_cast<bf16x4*>(y + (long)m * O + ot * 16 + kq * 4) = o;
+      }
+    }
+  }
+  if (stats == nullptr) return;
+  // the 16 lanes of a k block hold the same 4 channels of 16 different pixels
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int d = 1; d < 16; d <<= 1) {
+        s1[ot][e] += __shfl_xor(s1[ot][e], d);
+        s2[ot][e] += __shfl_xor(s2[ot][e], d);
+      }
+  if (col == 0) {
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        red[wave][0][ot * 16 + kq * 4 + e] = s1[ot][e];
+        red[wave][1][ot * 16 + kq * 4 + e] = s2[ot][e];
+      }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < 2 * O) {
+    const int qn = threadIdx.x / O, c = threadIdx.x - qn * O;
+    const float v = (red[0][qn][c] + red[1][qn][c]) + (red[2][qn][c] + red[3][qn][c]);
+    unsafeAtomicAdd(stats + ((blockIdx.x % STAT_REP) * 2 + qn) * O + c, (double)v);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Fused SGD step + weight images (the CNN engines' per-step tail): one launch updates every parameter of the
 // flat fp32 master (torch.optim.SGD with momentum / weight decay, fedmi::sgd_elem -- bit-identical to
 // sgd_flat_kernel) and, for each dense conv, writes the forward image wr[o][r][s][c] and the DGRAD phase
@@ -1953,15 +2062,14 @@ static void launch_fd(hipStream_t st, const ConvGeom& g, const bf16* x, const bf
                      rows_per_block, acc ? out : nullptr, BnSums{});
 }
 
-// K-split count for the weight gradient: about two workgroups per CU, at least 8 K steps per split, and a bounded
-// workspace.  (Rounding down to one wave -- ResNet-18's layer-4 3x3 WGRAD 48.0 -> 40.5 us, 847.6 -> 831.3 ms per
-// round -- changes the summation order and moved the lr-0.02 non-IID parity run 11 points off deterministic fp32
-// (tests/test_noniid_gpu.py); kept at the rounded-up count: profiles/r5_cnn/experiments/wgrad_splits.jsonl.)
+// K-split count for the weight gradient: at most one wave of two workgroups per CU (rounded down: ResNet-18's
+// layer-4 3x3 WGRAD, 144 tiles, 48.0 -> 40.5 us with 3 splits instead of 4 -- the fourth made a second, 64-workgroup
+// wave; profiles/r5_cnn/experiments/wgrad_splits.jsonl), at least 8 K steps per split, a bounded workspace.
 static int wgrad_splits(const ConvGeom& g, long ws_cap_floats) {
   const TileCfg t = pick_tiles_wgrad(g.M, g.NC);
   const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
   const int ksteps = (g.K + BK - 1) / BK;
-  long sp = (2l * num_cus() + tiles - 1) / tiles;
+  long sp = std::max<long>(1, 2l * num_cus() / tiles);
   sp = std::min<long>(sp, std::max(1, ksteps / 8));
   if (ws_cap_floats > 0) sp = std::min<long>(sp, ws_cap_floats / ((long)g.M * g.NC));
   sp = std::max<long>(1, sp);
@@ -1981,6 +2089,17 @@ void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf
     return;
   }
   if (res) throw std::invalid_argument("conv_fwd: a fused residual needs the tap path (C % 64 == 0)");
+  if (s.C == 8 && s.R == 3 && s.S == 3 && s.st == 1 && s.pad == 1 && (s.O == 32 || s.O == 64)) {
+    // the network-input conv (conv_stem_kernel): ~4 pixel tiles of 16 per wave
+    const StemGeom sg{s.N, s.H, s.W, s.O, s.N * s.H * s.W};
+    const long ntiles = (sg.M + 15) / 16;
+    const unsigned nblk = (unsigned)std::max<long>(1, std::min<long>(2048, (ntiles + 15) / 16));
+    if (s.O == 64)
+      hipLaunchKernelGGL(conv_stem_kernel<4>, dim3(nblk), dim3(256), 0, st, x, wrsc, y, stats, shift, sg);
+    else
+      hipLaunchKernelGGL(conv_stem_kernel<2>, dim3(nblk), dim3(256), 0, st, x, wrsc, y, stats, shift, sg);
+    return;
+  }
   launch_fd<FWD>(st, g, x, wrsc, nullptr, y, stats, shift, ws, ws_floats);
 }
 

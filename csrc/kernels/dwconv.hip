@@ -390,6 +390,84 @@ __global__ __launch_bounds__(256) void dw_dgrad3s2_kernel(const bf16* __restrict
   }
 }
 
+// 3x3 / stride 1 / pad 1 DGRAD, register-blocked like dw_fwd3_kernel<1>: one thread per (2 horizontally adjacent
+// dX pixels, 8-channel group); the 3 x 4 dY pixels they draw on are loaded once (6 loads per output instead of
+// 9).  dx[h][w] = sum_{r,s} dy[h+1-r][w+1-s] w[r][s], taps summed in dw_dgrad_kernel's (r, s) order; same BN-sums
+// epilogue.
+__global__ __launch_bounds__(256) void dw_dgrad3s1_kernel(const bf16* __restrict__ dy, const float* __restrict__ w,
+                                                          bf16* __restrict__ dx, DwGeom g, fedmi::BnSums bs) {
+  extern __shared__ float wl[];
+  const int VC = g.C >> 3;
+  stage_taps(w, wl, g.C, 9);
+  __syncthreads();
+  const bool bsum = bs.rep != nullptr;
+  float bq[3][8], bm[3][8], bi[3][8];
+  const int c0 = (int)(threadIdx.x % VC) * 8;
+  fedmi::bnsum_coeffs(bs, c0, bsum, bm, bi, bq);
+  const int W2 = (g.W + 1) >> 1;
+  const uint32_t total = (uint32_t)g.N * g.H * W2 * VC;
+  for (uint32_t it = blockIdx.x * blockDim.x + threadIdx.x; it < total; it += gridDim.x * blockDim.x) {
+    const uint32_t pr = it / (uint32_t)VC;
+    const uint32_t t2 = pr / (uint32_t)W2;
+    const int w0 = (int)(pr - t2 * W2) * 2;
+    const int n = (int)(t2 / (uint32_t)g.H), h = (int)(t2 - (uint32_t)n * g.H);
+    float a0[8], a1[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a0[k] = a1[k] = 0.f;
+    const long nb = (long)n * g.P;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int yy = h + 1 - r;
+      const bool rok = (unsigned)yy < (unsigned)g.P;
+      float v[4][8];   // dY columns w0-1 .. w0+2
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int xx = w0 - 1 + k;
+        const bool ok = rok && (unsigned)xx < (unsigned)g.Q;
+        ld8f(dy + (ok ? ((nb + yy) * g.Q + xx) * g.C + c0 : c0), v[k]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = ok ? v[k][j] : 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const float* wt = wl + (r * 3 + s) * g.C + c0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a0[j] += v[2 - s][j] * wt[j];
+          a1[j] += v[3 - s][j] * wt[j];
+        }
+      }
+    }
+    const long pix0 = ((long)n * g.H + h) * g.W + w0;
+    bf16x8v o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)a0[j];
+    *reinterpret_cast<bf16x8v*>(dx + pix0 * g.C + c0) = o;
+    if (bsum) fedmi::bnsum_acc(bs, pix0 * g.C + c0, o, bm, bi, bq);
+    if (w0 + 1 < g.W) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)a1[j];
+      *reinterpret_cast<bf16x8v*>(dx + (pix0 + 1) * g.C + c0) = o;
+      if (bsum) fedmi::bnsum_acc(bs, (pix0 + 1) * g.C + c0, o, bm, bi, bq);
+    }
+  }
+  if (!bsum) return;
+  float* red = wl + g.C * 9;   // [3][blockDim][8]
+  const int tb = blockDim.x;
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[(q * tb + threadIdx.x) * 8 + k] = bq[q][k];
+  __syncthreads();
+  const int nq = bs.zb ? 3 : 2;
+  for (int e = threadIdx.x; e < nq * g.C; e += tb) {
+    const int q = e / g.C, c = e - q * g.C, grp = c >> 3, k = c & 7;
+    float sum = 0.f;
+    for (int t = grp; t < tb; t += VC) sum += red[(q * tb + t) * 8 + k];
+    unsafeAtomicAdd(bs.rep + ((long)(blockIdx.x % bs.reps) * 3 + q) * g.C + c, (double)sum);
+  }
+}
+
 // Sum acc over the pstep threads of the block that share a channel group (LDS, one tap at a
 // time) and write this block's partial ws[blockIdx.x][C][RS] for the chunk's channels.
 template <int RS>
@@ -588,6 +666,12 @@ void launch_dw_dgrad(hipStream_t st, const DwShape& s, const bf16* dy, const flo
     const long items = (long)g.N * g.P * g.Q * (g.C / 8);
     const int nblk = bs ? std::min(blocks_for(items, tb), 2048) : blocks_for(items, tb);
     hipLaunchKernelGGL(dw_dgrad3s2_kernel, dim3(nblk), dim3(tb), lds, st, dy, w, dx, g, bs ? *bs : BnSums{});
+    return;
+  }
+  if (g.R == 3 && g.st == 1 && g.pad == 1) {   // row pairs (dw_dgrad3s1_kernel)
+    const long items = (long)g.N * g.H * ((g.W + 1) / 2) * (g.C / 8);
+    const int nblk = bs ? std::min(blocks_for(items, tb), 2048) : blocks_for(items, tb);
+    hipLaunchKernelGGL(dw_dgrad3s1_kernel, dim3(nblk), dim3(tb), lds, st, dy, w, dx, g, bs ? *bs : BnSums{});
     return;
   }
   const long items = (long)g.N * g.H * g.W * (g.C / 8);

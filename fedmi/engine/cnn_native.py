@@ -865,9 +865,11 @@ class CNNNativeTrainer(LocalTrainer):
                            fs.mom.data_ptr(), fs.n_params, c.lr, c.momentum, c.weight_decay, 0.0, False, False)
         self.pack()
 
-    def _forward_backward(self, nb: int) -> None:
-        # every gradient entry is overwritten (wgrad reduce, BN dgamma/dbeta, head): no grad zeroing
-        self.stats_all.zero_()
+    def _forward_backward(self, nb: int, zeroed: bool = False) -> None:
+        # every gradient entry is overwritten (wgrad reduce, BN dgamma/dbeta, head): no grad zeroing;
+        # the BN statistics accumulators are zeroed by the step's first kernel (sched_next) unless ``zeroed``
+        if not zeroed:
+            self.stats_all.zero_()
         if not self.bn_ws.numel():     # atomic BN-backward sums (emulation) need zeroed accumulators
             self.red_all.zero_()
         x, dh = self._forward(nb, True, self.train_set.x, self.train_set.y, self.cur, 0)
@@ -875,8 +877,8 @@ class CNNNativeTrainer(LocalTrainer):
 
     def _train_step(self, nb: int) -> None:
         """One SGD step on the batch at sched[counter] (device-side)."""
-        cnn.sched_next(self.sched, self.counter, self.cur)
-        self._forward_backward(nb)
+        cnn.sched_next(self.sched, self.counter, self.cur, zero=self.stats_all)
+        self._forward_backward(nb, zeroed=True)
         self._sgd()
 
     def grads_for_batch(self, start: int, nb: int) -> None:

@@ -33,10 +33,13 @@ def prep_input(images_u8: torch.Tensor, base: int, nb: int, augment: bool, seed:
     return out
 
 
-def sched_next(sched: torch.Tensor, counter: torch.Tensor, cur: torch.Tensor) -> None:
-    """cur = sched[counter++] on the device."""
+def sched_next(sched: torch.Tensor, counter: torch.Tensor, cur: torch.Tensor, zero: torch.Tensor = None) -> None:
+    """cur = sched[counter++] on the device; ``zero`` (fp64, contiguous, 16-B aligned): zeroed in the same launch."""
+    if zero is not None:
+        assert zero.dtype == torch.float64 and zero.is_contiguous() and zero.data_ptr() % 16 == 0
     native.require().sched_next(native.stream_handle(sched.device), sched.data_ptr(), counter.data_ptr(),
-                                cur.data_ptr())
+                                cur.data_ptr(), zero.data_ptr() if zero is not None else 0,
+                                zero.numel() if zero is not None else 0)
 
 
 class BNParams:

@@ -223,7 +223,9 @@ def prep_input(images_u8, base, nb, augment, seed, round_ctr, out=None, dbase=No
 
 
 @torch.no_grad()
-def sched_next(sched, counter, cur):
+def sched_next(sched, counter, cur, zero=None):
+    if zero is not None:
+        zero.zero_()
     i = int(counter.view(-1)[0])
     cur.view(-1)[0] = sched.view(-1)[i]
     counter.view(-1)[0] = i + 1

@@ -795,3 +795,26 @@ def test_conv_dgrad_1x1_stride2_zeroes_tapless_parities(gpu_device, shape):
     assert not torch.isnan(dx.float()).any()
     assert torch.equal(dx[:, 1::2].float(), torch.zeros_like(dx[:, 1::2].float()))
     assert _rel(dx[..., :Cw].float(), _nhwc(xr.grad)) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(3, 7, 5, 3, 32, 3, 1, 1), (2, 32, 32, 3, 64, 3, 1, 1), (5, 9, 9, 3, 64, 3, 1, 1),
+                                   (500, 32, 32, 3, 32, 3, 1, 1)],
+                         ids=["odd_o32", "b2_o64", "b5_9x9", "eval500_o32"])
+def test_conv_stem_kernel(gpu_device, shape):
+    """The network-input conv kernel (conv_stem_kernel: C = 8 padded, 3x3 / stride 1, O = 32 | 64) vs torch fp32,
+    with BatchNorm statistics of bf16(y) - shift (M not a multiple of 16 included), and without statistics."""
+    N, H, W, Cw, O, R, st, pad = shape
+    x, w, wb, xn = _make(shape, gpu_device, seed=31)
+    wr = conv.pack_weight(w)
+    shift = (torch.randn(O, device=gpu_device) * 0.1)
+    rep = conv.stats_buffer(O, gpu_device)
+    y = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=rep, shift=shift)
+    y2 = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw)
+    ref = F.conv2d(x, wb, stride=st, padding=pad)
+    torch.cuda.synchronize()
+    assert _rel(y.float(), _nhwc(ref)) < 1e-2
+    assert torch.equal(y, y2)
+    d = y.float().reshape(-1, O) - shift
+    stats = conv.stats_total(rep)
+    assert torch.allclose(stats[0], d.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(stats[1], (d * d).sum(0), rtol=1e-3, atol=1e-2)

@@ -50,3 +50,20 @@ def test_native_mode_step_launches_only_fedmi_kernels(gpu_device, name):
     assert not bad, sorted(set(bad))[:10]
     assert not tr.mode.fallbacks
     assert any("conv_igemm" in n or "conv_tap" in n for n in names)
+
+
+@pytest.mark.parametrize("name", ["resnet18", "mobilenet"])
+def test_cnn_engine_step_launches_only_fedmi_kernels(gpu_device, name):
+    """the whole-network CNN engines' captured step (eager here, same launches) is fedmi
+    kernels only -- the per-step BN-statistics zeroing rides in sched_next, no ATen fill."""
+    data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=256, n_test=128, seed=0)
+    tr = build_trainer(name, data, gpu_device, TrainerConfig(seed=1, use_graph=False))
+    tr.set_schedule(*contiguous_schedule(256, 128))
+    tr.train_epoch()                                   # warm-up (weight images, first-touch)
+    tr.counter.zero_()                                 # (epoch bookkeeping fills stay outside the profiled step)
+    torch.cuda.synchronize()
+    names = _kernels(lambda: tr._train_step(128))      # exactly what one graph replay launches
+    assert names, "profiler saw no kernels"
+    bad = [n for n in names if any(f in n for f in FOREIGN)]
+    assert not bad, sorted(set(bad))[:10]
+    assert any("conv_tap" in n for n in names) and any("sgd_pack" in n for n in names), sorted(set(names))[:20]
