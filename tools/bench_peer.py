@@ -53,6 +53,32 @@ def _worker(rank, world, path, iters, q):
             e1.record()
             torch.cuda.synchronize()
             res.append((name, algo, n, e0.elapsed_time(e1) * 1e3 / it))
+        # -c Y int8 + error feedback: the fused one-launch collective vs the unfused chain (delta, quantise, two
+        # all-gathers, dequantise-accumulate), same data
+        from fedmi.parallel.compress import Int8Compressor
+
+        class _F:
+            def __init__(self, t):
+                self.t = t
+
+            def float_state(self):
+                return self.t
+
+        for fused in (True, False):
+            xs = x.clone()
+            comp = Int8Compressor(_F(xs))
+            comp.fused = fused
+            it = iters if n < 1_000_000 else max(10, iters // 10)
+            for _ in range(5):
+                comp.aggregate(_F(xs), transport=pc)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(it):
+                comp.aggregate(_F(xs), transport=pc)
+            e1.record()
+            torch.cuda.synchronize()
+            res.append((name, "int8_fused" if fused else "int8_unfused", n, e0.elapsed_time(e1) * 1e3 / it))
     err = pc.error()
     pc.close()
     q.put((rank, res, err))
