@@ -35,6 +35,12 @@ void fedmi_bind_comm(py::module_& m) {
                              blocks);
            }, py::arg("stream"), py::arg("src"), py::arg("dst"), py::arg("n"), py::arg("scale"), py::arg("algo") = 0,
            py::arg("blocks") = 0)
+      .def("allreduce_int8_ef", [](PeerComm& c, uintptr_t st, uintptr_t x, uintptr_t g, uintptr_t r, long long n,
+                                   float scale, int blocks) {
+             c.allreduce_int8_ef(S(st), reinterpret_cast<float*>(x), reinterpret_cast<float*>(g),
+                                 reinterpret_cast<float*>(r), n, scale, blocks);
+           }, py::arg("stream"), py::arg("x"), py::arg("g"), py::arg("r"), py::arg("n"), py::arg("scale"),
+           py::arg("blocks") = 0)
       .def("allreduce_i64_mean_floor", [](PeerComm& c, uintptr_t st, uintptr_t in, uintptr_t out, long long n) {
         c.allreduce_i64_mean_floor(S(st), reinterpret_cast<const int64_t*>(in), reinterpret_cast<int64_t*>(out), n);
       })

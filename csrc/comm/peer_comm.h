@@ -73,6 +73,9 @@ class PeerComm {
 
   // out = scale * sum_p in_p  (fp32; in == out allowed)
   void allreduce_f32(hipStream_t st, const float* in, float* out, long long n, float scale, int algo, int blocks);
+  // -c Y int8 + error feedback in ONE launch: d = x - g + r quantised per 256-chunk (r <- quantisation error),
+  // g += scale * sum_p deq(q_p), x = g  (bit-identical to ef_delta + quant_int8 + all-gathers + dequant_accum)
+  void allreduce_int8_ef(hipStream_t st, float* x, float* g, float* r, long long n, float scale, int blocks);
   // out = floor(sum_p in_p / world)  (int64 BN counters: reference float mean + int64 truncation)
   void allreduce_i64_mean_floor(hipStream_t st, const int64_t* in, int64_t* out, long long n);
   // out[p * nbytes .. ) = in_p  (nbytes % 16 == 0)

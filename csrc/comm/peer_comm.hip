@@ -27,6 +27,7 @@
 // every block of this one has retired.
 #include "peer_comm.h"
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -217,6 +218,91 @@ __global__ __launch_bounds__(256) void peer_allgather_kernel(PeerArgs a, const u
   end_call(a, b, ep);
 }
 
+// -c Y (int8 + error feedback) fused into the collective: ONE launch per FedAvg instead of delta + quantise +
+// two all-gathers + dequantise-accumulate.  One WAVE owns one 256-entry chunk (4 consecutive entries per lane,
+// 16-byte loads / stores, the chunk's absmax by wave shuffles only -- no workgroup barrier per chunk); block b's
+// waves take chunks 4b + w, 4b + w + 4G, ... on every rank.  Phase 1: d = x - g + r, scale s = absmax / 127,
+// q = rint(d / s) clamped to +-127, r <- d - q * s; q (int8) and s go to this rank's staging slot.  Peer barrier of
+// block b.  Phase 2, same chunks: acc = sum over ranks 0..W-1 of q_p * s_p, g += scale * acc, x = g.  The formulas
+// and the summation order are those of ef_delta / quant_int8 / dequant_accum (compress.hip), so the result is
+// bit-identical to the unfused path and to every other rank.  Staging: q bytes [0, n16), scales (fp32) from n16.
+// x, g, r: 16-byte aligned (the host checks); the tail chunk's lanes past n go element by element.
+PDEV void i8_load4(const float* p, long long i, long long n, float v[4]) {
+  if (i + 3 < n) {
+    const float4 t = *reinterpret_cast<const float4*>(p + i);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = i + e < n ? p[i + e] : 0.f;
+  }
+}
+PDEV void i8_store4(float* p, long long i, long long n, const float v[4]) {
+  if (i + 3 < n) {
+    *reinterpret_cast<float4*>(p + i) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (i + e < n) p[i + e] = v[e];
+  }
+}
+
+__global__ __launch_bounds__(256) void peer_int8_ef_kernel(PeerArgs a, float* __restrict__ x, float* __restrict__ g,
+                                                           float* __restrict__ r, long long n, float scale) {
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t ep = begin_call(a, b);
+  const int slot = ep & 1;
+  const long long nchunks = (n + 255) >> 8, n16 = (n + 15) & ~15LL;
+  const long long cstep = (long long)gridDim.x * 4;
+  char* mine = region(a, a.rank, slot, 0);
+  float* mys = reinterpret_cast<float*>(mine + n16);
+  for (long long c = (long long)b * 4 + wave; c < nchunks; c += cstep) {
+    const long long i = c * 256 + 4 * lane;
+    float xv[4], gv[4], rv[4], v[4];
+    i8_load4(x, i, n, xv);
+    i8_load4(g, i, n, gv);
+    i8_load4(r, i, n, rv);
+    float am = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = i + e < n ? (xv[e] - gv[e]) + rv[e] : 0.f;
+      am = fmaxf(am, fabsf(v[e]));
+    }
+    for (int off = 32; off > 0; off >>= 1) am = fmaxf(am, __shfl_xor(am, off, 64));
+    const float sc = am > 0.f ? am / 127.f : 1.f;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float rq = rintf(v[e] / sc);
+      const int qi = (int)fminf(fmaxf(rq, -127.f), 127.f);
+      packed |= (uint32_t)(qi & 0xff) << (8 * e);
+      rv[e] = v[e] - (float)qi * sc;
+    }
+    i8_store4(r, i, n, rv);
+    if (i < n16) *reinterpret_cast<uint32_t*>(mine + i) = packed;     // (n16 % 4 == 0: whole words)
+    if (lane == 0) mys[c] = sc;
+  }
+  if (!peer_barrier(a, 0, b, ep)) return;
+  for (long long c = (long long)b * 4 + wave; c < nchunks; c += cstep) {
+    const long long i = c * 256 + 4 * lane;
+    if (i >= n) continue;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < a.world; ++p) {
+      const char* base = region(a, p, slot, 0);
+      const uint32_t qw = *reinterpret_cast<const uint32_t*>(base + i);
+      const float sp = reinterpret_cast<const float*>(base + n16)[c];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += (float)(signed char)((qw >> (8 * e)) & 0xff) * sp;
+    }
+    float gv[4];
+    i8_load4(g, i, n, gv);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gv[e] = gv[e] + scale * acc[e];
+    i8_store4(g, i, n, gv);
+    i8_store4(x, i, n, gv);
+  }
+  end_call(a, b, ep);
+}
+
 }  // namespace
 
 namespace fedmi {
@@ -384,6 +470,19 @@ void PeerComm::allreduce_f32(hipStream_t st, const float* in, float* out, long l
   else
     hipLaunchKernelGGL(peer_oneshot_f32_kernel, dim3(blocks), dim3(256), 0, st, a_, in, out, n, scale);
   check_hip(hipGetLastError(), "peer allreduce_f32 launch");
+}
+
+void PeerComm::allreduce_int8_ef(hipStream_t st, float* x, float* g, float* r, long long n, float scale, int blocks) {
+  need(connected_ || a_.world == 1, "PeerComm: not connected");
+  const long long nchunks = (n + 255) / 256, n16 = (n + 15) & ~15LL;
+  need(n >= 0 && n16 + 4 * nchunks <= a_.cap, "PeerComm::allreduce_int8_ef: payload exceeds capacity");
+  if (n == 0) return;
+  need(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(r)) & 15) == 0,
+       "PeerComm::allreduce_int8_ef: x, g, r must be 16-byte aligned");
+  if (blocks <= 0) blocks = (int)std::min<long long>((nchunks + 3) / 4, kPeerMaxBlocks);   // a chunk per wave
+  need(blocks <= kPeerMaxBlocks, "PeerComm: too many blocks");
+  hipLaunchKernelGGL(peer_int8_ef_kernel, dim3(blocks), dim3(256), 0, st, a_, x, g, r, n, scale);
+  check_hip(hipGetLastError(), "peer int8_ef launch");
 }
 
 void PeerComm::allreduce_i64_mean_floor(hipStream_t st, const int64_t* in, int64_t* out, long long n) {

@@ -843,49 +843,9 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const bf16* __restric
 // windows covering each input pixel (no atomics), optionally accumulating into
 // dx (the branch's share of a fan-in gradient).
 // stride as a template parameter: the window / phase index math compiles to shifts instead of
-// runtime integer divisions (GoogLeNet's inception pools: 63 us per backward launch with runtime st)
-template <int ST>
-__global__ __launch_bounds__(256) void maxpool3_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
-                                                           uint8_t* __restrict__ idx, int N, int H, int W, int C,
-                                                           int P, int Q) {
-  constexpr int st = ST;
-  const int VC = C >> 3;
-  const uint32_t total = (uint32_t)N * P * Q * VC;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const uint32_t pix = i / VC;
-    const int c0 = (int)(i - pix * VC) * 8;
-    const uint32_t t = pix / Q;
-    const int q = (int)(pix - t * Q);
-    const int n = (int)(t / P), p = (int)(t - (uint32_t)n * P);
-    float best[8];
-    int am[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; am[j] = 0; }
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int h = p * st - 1 + r;
-#pragma unroll
-      for (int s2 = 0; s2 < 3; ++s2) {
-        const int w = q * st - 1 + s2;
-        if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) continue;
-        const bf16x8v v = *reinterpret_cast<const bf16x8v*>(x + (((long)n * H + h) * W + w) * C + c0);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if ((float)v[j] > best[j]) { best[j] = (float)v[j]; am[j] = r * 3 + s2; }
-      }
-    }
-    bf16x8v o;
-    uint64_t packed = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      o[j] = (bf16)best[j];
-      packed |= (uint64_t)am[j] << (8 * j);
-    }
-    *reinterpret_cast<bf16x8v*>(y + (long)pix * C + c0) = o;
-    *reinterpret_cast<uint64_t*>(idx + (long)pix * C + c0) = packed;
-  }
-}
-
+// runtime integer divisions (GoogLeNet's inception pools: 63 us per backward launch with runtime st).
+// maxpool3_bwd_kernel serves stride 2; the forward and the stride-1 backward are the register-blocked
+// kernels below.
 template <int ST>
 __global__ __launch_bounds__(256) void maxpool3_bwd_kernel(const bf16* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                            bf16* __restrict__ dx, int N, int H, int W, int C,
@@ -977,15 +937,146 @@ static BNArgs to_args(const BNDesc& d) {
   return BNArgs{d.stats, d.gamma, d.beta, d.rmean, d.rvar, d.nbt, d.smean, d.sinv, d.shift, d.cbias};
 }
 
+// Register-blocked forms (QB horizontally adjacent outputs per thread): the (QB - 1) * ST + 3 input columns of
+// the QB windows are loaded once (stride 1, QB 4: 18 loads for 4 outputs instead of 36), and every output scans its
+// window in the same (r, s) order with the same strict '>' as maxpool3_fwd_kernel -- bit-identical values and
+// argmax codes.  GoogLeNet's 32x32x192/256 branch pools spent 40 us (fwd) / 53 us (bwd) per call re-reading each
+// input vector 9 times.
+template <int ST, int QB>
+__global__ __launch_bounds__(256) void maxpool3_fwd_blk_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                               uint8_t* __restrict__ idx, int N, int H, int W, int C,
+                                                               int P, int Q) {
+  constexpr int NCOL = (QB - 1) * ST + 3;
+  const int VC = C >> 3;
+  const int QBk = (Q + QB - 1) / QB;
+  const uint32_t total = (uint32_t)N * P * QBk * VC;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t pb = i / VC;
+    const int c0 = (int)(i - pb * VC) * 8;
+    const uint32_t t = pb / QBk;
+    const int q0 = (int)(pb - t * QBk) * QB;
+    const int n = (int)(t / P), p = (int)(t - (uint32_t)n * P);
+    const int w0 = q0 * ST - 1;
+    float best[QB][8];
+    int am[QB][8];
+#pragma unroll
+    for (int k = 0; k < QB; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { best[k][j] = -INFINITY; am[k][j] = 0; }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int h = p * ST - 1 + r;
+      const bool hok = (unsigned)h < (unsigned)H;
+      bf16x8v v[NCOL];
+      bool ok[NCOL];
+#pragma unroll
+      for (int cc = 0; cc < NCOL; ++cc) {
+        const int w = w0 + cc;
+        ok[cc] = hok && (unsigned)w < (unsigned)W;
+        v[cc] = *reinterpret_cast<const bf16x8v*>(x + (ok[cc] ? (((long)n * H + h) * W + w) * C + c0 : c0));
+      }
+#pragma unroll
+      for (int k = 0; k < QB; ++k)
+#pragma unroll
+        for (int s2 = 0; s2 < 3; ++s2) {
+          const int cc = k * ST + s2;
+          if (!ok[cc]) continue;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if ((float)v[cc][j] > best[k][j]) { best[k][j] = (float)v[cc][j]; am[k][j] = r * 3 + s2; }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < QB; ++k) {
+      if (q0 + k >= Q) break;
+      bf16x8v o;
+      uint64_t packed = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = (bf16)best[k][j];
+        packed |= (uint64_t)am[k][j] << (8 * j);
+      }
+      const long pix = ((long)n * P + p) * Q + q0 + k;
+      *reinterpret_cast<bf16x8v*>(y + pix * C + c0) = o;
+      *reinterpret_cast<uint64_t*>(idx + pix * C + c0) = packed;
+    }
+  }
+}
+
+// stride-1 backward, QB adjacent input pixels per thread: the (QB + 2) x 3 covering windows' (code, grad) pairs are
+// loaded once; each pixel sums its windows in maxpool3_bwd_kernel's (r, s) order (bit-identical)
+template <int QB>
+__global__ __launch_bounds__(256) void maxpool3_bwd1_blk_kernel(const bf16* __restrict__ dy,
+                                                                const uint8_t* __restrict__ idx, bf16* __restrict__ dx,
+                                                                int N, int H, int W, int C, int acc) {
+  constexpr int NCOL = QB + 2;
+  const int VC = C >> 3;
+  const int WBk = (W + QB - 1) / QB;
+  const uint32_t total = (uint32_t)N * H * WBk * VC;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t pb = i / VC;
+    const int c0 = (int)(i - pb * VC) * 8;
+    const uint32_t t = pb / WBk;
+    const int w0 = (int)(pb - t * WBk) * QB;
+    const int n = (int)(t / H), h = (int)(t - (uint32_t)n * H);
+    float g[QB][8];
+#pragma unroll
+    for (int k = 0; k < QB; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[k][j] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int p = h + 1 - r;                // output row whose window holds input row h at tap row r
+      if ((unsigned)p >= (unsigned)H) continue;
+      uint64_t pk[NCOL];
+      bf16x8v d[NCOL];
+      bool ok[NCOL];
+#pragma unroll
+      for (int cc = 0; cc < NCOL; ++cc) {     // output columns q = w0 - 1 + cc
+        const int q = w0 - 1 + cc;
+        ok[cc] = (unsigned)q < (unsigned)W;
+        const long o = ok[cc] ? (((long)n * H + p) * W + q) * C + c0 : c0;
+        pk[cc] = *reinterpret_cast<const uint64_t*>(idx + o);
+        d[cc] = *reinterpret_cast<const bf16x8v*>(dy + o);
+      }
+#pragma unroll
+      for (int k = 0; k < QB; ++k)
+#pragma unroll
+        for (int s2 = 0; s2 < 3; ++s2) {
+          const int cc = k + 2 - s2;          // q = (w0 + k) + 1 - s2
+          if (!ok[cc]) continue;
+          const int tap = r * 3 + s2;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if ((int)((pk[cc] >> (8 * j)) & 0xff) == tap) g[k][j] += (float)d[cc][j];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < QB; ++k) {
+      if (w0 + k >= W) break;
+      bf16* dst = dx + (((long)n * H + h) * W + w0 + k) * C + c0;
+      if (acc) {
+        const bf16x8v e = *reinterpret_cast<const bf16x8v*>(dst);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[k][j] += (float)e[j];
+      }
+      bf16x8v o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)g[k][j];
+      *reinterpret_cast<bf16x8v*>(dst) = o;
+    }
+  }
+}
+
 void launch_maxpool3(hipStream_t st, const bf16* x, bf16* y, uint8_t* idx, int N, int H, int W, int C, int stride) {
   if (C % 8 || (stride != 1 && stride != 2)) throw std::invalid_argument("maxpool3: need C % 8 == 0, stride 1|2");
   const int P = (H + 2 - 3) / stride + 1, Q = (W + 2 - 3) / stride + 1;
   if (stride == 1)
-    hipLaunchKernelGGL(maxpool3_fwd_kernel<1>, dim3(grid_for((long)N * P * Q * (C / 8))), dim3(256), 0, st, x, y, idx, N,
-                       H, W, C, P, Q);
+    hipLaunchKernelGGL((maxpool3_fwd_blk_kernel<1, 4>), dim3(grid_for((long)N * P * ((Q + 3) / 4) * (C / 8))),
+                       dim3(256), 0, st, x, y, idx, N, H, W, C, P, Q);
   else
-    hipLaunchKernelGGL(maxpool3_fwd_kernel<2>, dim3(grid_for((long)N * P * Q * (C / 8))), dim3(256), 0, st, x, y, idx, N,
-                       H, W, C, P, Q);
+    hipLaunchKernelGGL((maxpool3_fwd_blk_kernel<2, 2>), dim3(grid_for((long)N * P * ((Q + 1) / 2) * (C / 8))),
+                       dim3(256), 0, st, x, y, idx, N, H, W, C, P, Q);
 }
 
 void launch_maxpool3_bwd(hipStream_t st, const bf16* dy, const uint8_t* idx, bf16* dx, int N, int H, int W, int C,
@@ -993,8 +1084,8 @@ void launch_maxpool3_bwd(hipStream_t st, const bf16* dy, const uint8_t* idx, bf1
   if (C % 8 || (stride != 1 && stride != 2)) throw std::invalid_argument("maxpool3_bwd: need C % 8 == 0, stride 1|2");
   const int P = (H + 2 - 3) / stride + 1, Q = (W + 2 - 3) / stride + 1;
   if (stride == 1)
-    hipLaunchKernelGGL(maxpool3_bwd_kernel<1>, dim3(grid_for((long)N * H * W * (C / 8))), dim3(256), 0, st, dy, idx, dx,
-                       N, H, W, C, P, Q, acc);
+    hipLaunchKernelGGL(maxpool3_bwd1_blk_kernel<4>, dim3(grid_for((long)N * H * ((W + 3) / 4) * (C / 8))), dim3(256), 0,
+                       st, dy, idx, dx, N, H, W, C, acc);
   else
     hipLaunchKernelGGL(maxpool3_bwd_kernel<2>, dim3(grid_for((long)N * H * W * (C / 8))), dim3(256), 0, st, dy, idx, dx,
                        N, H, W, C, P, Q, acc);

@@ -505,7 +505,12 @@ FEDMI_DEV bf16x8 frag_sw(const bf16* img, int i0, int kk, int lane) {
 // DMA three steps ahead: +5..13 % per conv, profiles/r4_cnn/tap_stages_ab.txt).
 // NW waves per workgroup (4 or 8) in an (NW / 2) x 2 grid over the 128 x BN tile: with 8 waves every SIMD
 // holds two waves, so one wave's barrier / LDS / DMA latency is covered by its partner's MFMAs.
-template <int BN, int NW>
+// GEN: input channels C % 8 == 0 but not % 64 (GoogLeNet's 16 / 24 / 32 / 48 / 96 / 112 / 144 / 160-channel inception
+// branches, DenseNet's growth): a 64-deep K step then spans several taps, so every DMA lane tracks the (tap, channel)
+// of its own 16-byte chunk (k = 64 t + 8 kc, incrementally, no division in the loop) and the last step's chunks
+// past K = R * S * C read zeros on both operands.  The weight rows are K-contiguous for any C, so the B side only
+// gains the K-tail mask.
+template <int BN, int NW, bool GEN = false>
 FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict__ wt, bf16* __restrict__ out,
                              float* __restrict__ part, double* __restrict__ stats, const float* __restrict__ shift,
                              const TapGeom& g, const RowMap& rmap, int ksteps_per_split,
@@ -534,7 +539,7 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int wm0 = (wave >> 1) * WMR, wn0 = (wave & 1) * (BN / 2);
 
-  const int ksteps = g.K / 64;
+  const int ksteps = GEN ? (g.K + 63) / 64 : g.K / 64;
   const int kb = split * ksteps_per_split;
   const int ke = min(ksteps, kb + ksteps_per_split);
 
@@ -561,7 +566,7 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
       for (int x = 0; x < g.S; ++x)
         if (ok && (unsigned)(h0 + r) < (unsigned)g.H && (unsigned)(w0 + x) < (unsigned)g.W) mk |= 1ull << (r * g.S + x);
     a_mask[i] = mk;
-    a_off[i] = ((n * g.H + h0) * g.W + w0) * g.C + kc * 8;
+    a_off[i] = ((n * g.H + h0) * g.W + w0) * g.C + (GEN ? 0 : kc * 8);
   }
   uint32_t b_off[NB];         // byte offset of the filter row's chunk at k = 0 (BUF_OOB: o >= O)
 #pragma unroll
@@ -572,20 +577,51 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
 
   // tap state of the next K step to issue, advanced incrementally (scalar; no per-step division):
   // K step t = tap (r, s), channels [c0, c0 + 64)
-  int is_c0, is_s, is_r;
-  {
+  int is_c0 = 0, is_s = 0, is_r = 0;
+  if constexpr (!GEN) {
     const int k0 = kb * 64;
     const int rs = k0 / g.C;
     is_c0 = k0 - rs * g.C;
     is_r = rs / g.S;
     is_s = rs - is_r * g.S;
   }
+  // GEN: this lane's chunk of the next K step to issue: k = 64 t + 8 kc -> tap (gr, gs), channel gc
+  int gr = 0, gs = 0, gc = 0;
+  uint32_t gk0b = 0;                      // byte offset of the step's first k along a weight row
+  if constexpr (GEN) {
+    const int k = kb * 64 + kc * 8;
+    const int tp = k / g.C;
+    gc = k - tp * g.C;
+    gr = tp / g.S;
+    gs = tp - gr * g.S;
+    gk0b = (uint32_t)kb * 128u;
+  }
   auto issue = [&](int stage) {
+    bf16* As = smem + stage * STAGE;
+    bf16* Bs = As + BM * 64;
+    if constexpr (GEN) {
+      const bool kok = gr < g.R;          // k < K (the last step's tail chunks read zeros on both sides)
+      const int rs = kok ? gr * g.S + gs : 0;
+      const int tap = (gr * g.W + gs) * g.C + gc;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const bool ok = kok && ((a_mask[i] >> rs) & 1);
+        blds16(rin, ok ? (uint32_t)(a_off[i] + tap) * 2u : BUF_OOB, As + (wave * NA + i) * 8 * 64);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        blds16(rwt, (b_off[i] == BUF_OOB || !kok) ? BUF_OOB : b_off[i] + gk0b, Bs + (wave * NB + i) * 8 * 64);
+      gk0b += 128u;
+      gc += 64;
+      while (gc >= g.C) {
+        gc -= g.C;
+        if (++gs == g.S) { gs = 0; ++gr; }
+      }
+      return;
+    }
     const int rs = is_r * g.S + is_s;
     const int tap = (is_r * g.W + is_s) * g.C + is_c0;
     const uint32_t k0b = (uint32_t)(rs * g.C + is_c0) * 2u;
-    bf16* As = smem + stage * STAGE;
-    bf16* Bs = As + BM * 64;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const bool ok = (a_mask[i] >> rs) & 1;
@@ -819,13 +855,14 @@ FEDMI_DEV void conv_tap_body(const bf16* __restrict__ in, const bf16* __restrict
   CONV_STAMP(5);
 }
 
-template <int BN, int NW>
+template <int BN, int NW, bool GEN = false>
 __global__ __launch_bounds__(64 * NW) void conv_tap(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                 bf16* __restrict__ out, float* __restrict__ part,
                                                 double* __restrict__ stats, const float* __restrict__ shift,
                                                 TapGeom g, RowMap rmap, int ksteps_per_split,
                                                 const bf16* __restrict__ res, BnSums bs) {
-  conv_tap_body<BN, NW>(in, wt, out, part, stats, shift, g, rmap, ksteps_per_split, res, bs, blockIdx.x, blockIdx.z);
+  conv_tap_body<BN, NW, GEN>(in, wt, out, part, stats, shift, g, rmap, ksteps_per_split, res, bs, blockIdx.x,
+                             blockIdx.z);
 }
 
 // The sub-pixel phases of a stride-2 DGRAD in ONE launch: blockIdx.x walks the phases' tiles in order,
@@ -1815,7 +1852,7 @@ static int tap_splits(const TapGeom& g, long ws_floats) {
   const int bn = tap_bn(g);
   const long tiles = (long)((g.M + 127) / 128) * ((g.O + bn - 1) / bn);
   const long target = (bn == 128 ? 1l : 2l) * num_cus();
-  const int ksteps = g.K / 64;
+  const int ksteps = (g.K + 63) / 64;
   // (a 40-step threshold saved 2.4 us on ResNet-18's layer-4 stride-2 forward but moved EfficientNetB0's
   // 3-epoch trajectory outside its parity bound -- profiles/r5_cnn/splits/; kept at 16)
   if (4 * tiles > target || ksteps < 16) return 1;
@@ -1868,12 +1905,13 @@ static void launch_tap_reduce(hipStream_t st, const TapGeom& g, const RowMap& rm
 static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const bf16* wt, bf16* out, double* stats,
                        const float* shift, const RowMap& rm, float* ws, long ws_floats,
                        const bf16* res = nullptr, const BnSums& bs = BnSums{}) {
-  if (g.C % 64 || g.O % 8) throw std::invalid_argument("conv_tap: need C % 64 == 0 and O % 8 == 0");
+  if (g.C % 8 || g.C < 16 || g.O % 8) throw std::invalid_argument("conv_tap: need C % 8 == 0, C >= 16, O % 8 == 0");
   if (!tap_fits((long)g.N * g.H * g.W * g.C, (long)g.O * g.K, g.R, g.S))
     throw std::invalid_argument("conv_tap: operands over 2 GiB or R * S > 64");
+  const bool gen = g.C % 64 != 0;         // several taps per K step (conv_tap_body GEN)
   const int BN = tap_bn(g);
   const long tiles = (long)((g.M + 127) / 128) * ((g.O + BN - 1) / BN);
-  const int ksteps = g.K / 64;
+  const int ksteps = (g.K + 63) / 64;
   const int sp = tap_splits(g, ws_floats);
   const int kps = (ksteps + sp - 1) / sp;
   const int splits = (ksteps + kps - 1) / kps;
@@ -1882,7 +1920,14 @@ static void launch_tap(hipStream_t st, const TapGeom& g, const bf16* in, const b
   const BnSums tbs = part ? BnSums{} : bs;
   double* tst = part ? nullptr : stats;
   const bf16* trs = part ? nullptr : res;
-  if (BN == 128)
+  if (gen) {   // 8 waves only (the default shape)
+    if (BN == 128)
+      hipLaunchKernelGGL((conv_tap<128, 8, true>), grid, dim3(512), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs,
+                         tbs);
+    else
+      hipLaunchKernelGGL((conv_tap<64, 8, true>), grid, dim3(512), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs,
+                         tbs);
+  } else if (BN == 128)
     if (tap_waves() == 8)
       hipLaunchKernelGGL((conv_tap<128, 8>), grid, dim3(512), 0, st, in, wt, out, part, tst, shift, g, rm, kps, trs, tbs);
     else
@@ -2077,18 +2122,33 @@ static int wgrad_splits(const ConvGeom& g, long ws_cap_floats) {
   return (ksteps + kps - 1) / kps;
 }
 
+// the forward runs on conv_tap for C % 64 == 0, and (GEN) for any C % 8 == 0 from 16 channels with O % 8 == 0;
+// FEDMI_TAP_GEN=0 keeps those on the generic implicit GEMM (A/B runs, tests)
+static bool tap_gen_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("FEDMI_TAP_GEN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+static bool fwd_tap_ok(const ConvShape& s) {
+  const long K = (long)s.R * s.S * s.C;
+  return s.O % 8 == 0 && (s.C % 64 == 0 || (tap_gen_enabled() && s.C % 8 == 0 && s.C >= 16)) &&
+         tap_fits((long)s.N * s.H * s.W * s.C, (long)s.O * K, s.R, s.S);
+}
+
 // Y[N,P,Q,O] = conv(X[N,H,W,C], W_rsc); stats (optional) += [sum | sumsq] of (Y - shift) per output channel.
 void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf16* wrsc, bf16* y, double* stats,
                      const float* shift, float* ws, long ws_floats, const bf16* res) {
   check_shape(s);
   ConvGeom g = make_geom(s);
   g.M = s.N * s.P * s.Q; g.NC = s.O; g.K = s.R * s.S * s.C;
-  if (s.C % 64 == 0 && tap_fits((long)s.N * s.H * s.W * s.C, (long)s.O * g.K, s.R, s.S)) {
+  if (fwd_tap_ok(s)) {
     const TapGeom t = make_tap(s.N, s.H, s.W, s.C, s.O, s.P, s.Q, s.R, s.S, s.st, s.pad, s.pad);
     launch_tap(st, t, x, wrsc, y, stats, shift, RowMap{}, ws, ws_floats, res);
     return;
   }
-  if (res) throw std::invalid_argument("conv_fwd: a fused residual needs the tap path (C % 64 == 0)");
+  if (res) throw std::invalid_argument("conv_fwd: a fused residual needs the tap path (C % 8 == 0, C >= 16)");
   if (s.C == 8 && s.R == 3 && s.S == 3 && s.st == 1 && s.pad == 1 && (s.O == 32 || s.O == 64)) {
     // the network-input conv (conv_stem_kernel): ~4 pixel tiles of 16 per wave
     const StemGeom sg{s.N, s.H, s.W, s.O, s.N * s.H * s.W};
@@ -2184,7 +2244,7 @@ long conv_fd_ws_floats(const ConvShape& s) {
   const long cap = 1l << 40;
   int sp = fd_splits(g, cap);
   if (sp > 1) need = std::max(need, (long)sp * g.M * g.NC);
-  if (s.C % 64 == 0) {
+  if (fwd_tap_ok(s)) {
     const TapGeom t = make_tap(s.N, s.H, s.W, s.C, s.O, s.P, s.Q, s.R, s.S, s.st, s.pad, s.pad);
     const int tsp = tap_splits(t, cap);
     if (tsp > 1) need = std::max(need, (long)tsp * t.M * t.O);

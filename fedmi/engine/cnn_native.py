@@ -493,7 +493,9 @@ class CNNNativeTrainer(LocalTrainer):
                                     device=device)
         # (weight gradients on a side stream overlapping the dgrad chain measured slower -- ResNet-18 1036 vs
         # 983 ms per round, MobileNet 886 vs 832: the concurrent kernels compete for CUs / LDS and the split-K
-        # sizing assumes the whole chip, profiles/r3_cnn -- so everything runs on one stream)
+        # sizing assumes the whole chip, profiles/r3_cnn.  Round 6 re-measured it as two graph branches with the
+        # side stream's split count divided by 1 / 2 / 4 (sized for the CUs the DGRAD chain leaves): ResNet-18
+        # 847 / 837 / 925 vs 823-827 ms, MobileNet 733 / 752 / 789 vs 690-692, profiles/r6_cnn/ -- one stream)
         # BN-backward two-level channel sums (replicated atomics + finalize; kept zero between uses)
         self.bn_ws = torch.zeros(max(cnn.bn_bwd_ws_floats(B * u.P * u.P, u.O) for u in self.units),
                                  dtype=torch.float64, device=device)
@@ -842,9 +844,13 @@ class CNNNativeTrainer(LocalTrainer):
                     v = br[j]
                     if j > 0:
                         w = br[j - 1]
-                        self._wgrad(v, w.view(w.y, nb), nb)
-                        v.dgrad(nb, w.view(w.dy, nb), ws)
-                        self._bn_bwd(w, nb, w.view(w.dy, nb), None, w.view(w.y, nb))
+                        wy = w.view(w.y, nb)
+                        self._wgrad(v, wy, nb)
+                        # the inner BN's backward sums in this DGRAD's epilogue where it runs on conv_tap
+                        # (no separate reduce pass over (dy, z, y))
+                        bs = self._sums(v, w, nb, wy)
+                        v.dgrad(nb, w.view(w.dy, nb), ws, bn_sums=bs)
+                        self._bn_bwd(w, nb, w.view(w.dy, nb), None, wy, presummed=bs is not None)
                     elif k < 3:                            # branch heads: the module input's grad fan-in
                         self._wgrad(v, a, nb)
                         v.dgrad(nb, dx, ws, accumulate=k > 0)

@@ -200,9 +200,19 @@ class Int8Compressor(_EFCompressor):
             self.scales.copy_(s)
             self.residual.copy_(self.d - (q * s[:, None]).view(-1)[:self.n])
 
+    # the fused peer kernel (quantise + exchange + dequantise-average in one launch); False: the unfused
+    # reference path (tests compare the two bit for bit)
+    fused = True
+
     def aggregate(self, trainer, group=None, transport=None) -> None:
         x = trainer.float_state()
         if self._dense(x, group, transport):
+            return
+        if self.fused and transport is not None and hasattr(transport, "int8_ef_allreduce_"):
+            transport.int8_ef_allreduce_(x, self.global_ref, self.residual)
+            self.bytes_sent += self.n + 4 * self.nchunks
+            self.dense_bytes += 4 * self.n
+            self.rounds += 1
             return
         self.compress(x)
         w = transport.world if transport is not None else _world(group)

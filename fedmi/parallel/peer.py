@@ -131,6 +131,16 @@ class PeerAllReduce:
         self.calls += 1
         return dst
 
+    def int8_ef_allreduce_(self, x: torch.Tensor, g: torch.Tensor, r: torch.Tensor) -> None:
+        """-c Y fused into the collective (one launch): x - g + r is quantised to int8 per 256-entry chunk with the
+        quantisation error kept in ``r``, every rank's int8 payload is dequantised and averaged in rank order into
+        ``g``, and ``x`` becomes the new global model ``g`` (fp32, contiguous, same length)."""
+        if not self._gate():
+            return
+        self.comm.allreduce_int8_ef(self._stream(), x.data_ptr(), g.data_ptr(), r.data_ptr(), x.numel(),
+                                    1.0 / self.world)
+        self.calls += 1
+
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[world, *t.shape] with rank r's tensor in row r."""
         t = t.contiguous()

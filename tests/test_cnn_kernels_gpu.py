@@ -18,6 +18,11 @@ SHAPES = [
     (16, 4, 4, 512, 512, 3, 1, 1),     # layer4
     (3, 7, 5, 24, 40, 3, 1, 1),        # odd spatial, partial tiles
     (2, 9, 9, 16, 8, 5, 2, 2),         # 5x5 stride 2
+    # GoogLeNet inception branches: C % 64 != 0 runs the forward on conv_tap<GEN> (several taps per K step)
+    (4, 32, 32, 96, 128, 3, 1, 1),     # a3 3x3 branch
+    (4, 16, 16, 48, 48, 3, 1, 1),      # a4 double-3x3 branch
+    (4, 16, 16, 480, 192, 1, 1, 0),    # a4 1x1 (C % 64 == 32)
+    (16, 4, 4, 160, 320, 3, 1, 1),     # small M, long K (split-K of the GEN path)
 ]
 
 
@@ -479,11 +484,18 @@ def test_conv_fwd_fused_residual(gpu_device, shape):
     assert torch.allclose(tot[0], yb.sum((0, 1, 2)), rtol=1e-3, atol=1e-1)
 
 
-@pytest.mark.parametrize("stride,shape", [(1, (4, 9, 7, 24)), (2, (3, 16, 16, 64)), (2, (2, 9, 11, 16))])
-def test_maxpool3_fwd_bwd_accumulate(gpu_device, stride, shape):
-    """MaxPool2d(3, stride, 1) (GoogLeNet) vs torch: forward, gather backward (overlapping windows sum), +=."""
+@pytest.mark.parametrize("stride,shape,ties", [(1, (4, 9, 7, 24), False), (2, (3, 16, 16, 64), False),
+                                               (2, (2, 9, 11, 16), False), (1, (2, 32, 32, 16), True),
+                                               (1, (3, 6, 5, 8), True), (2, (2, 15, 13, 8), True)])
+def test_maxpool3_fwd_bwd_accumulate(gpu_device, stride, shape, ties):
+    """MaxPool2d(3, stride, 1) (GoogLeNet) vs torch: forward, gather backward (overlapping windows sum), +=.
+    ``ties``: values on a coarse grid, so windows hold equal maxima -- the first maximum in (r, s) order must win,
+    as in max_pool2d_with_indices (the register-blocked kernels scan each window in that order)."""
     torch.manual_seed(15)
-    x = torch.randn(*shape, device=gpu_device).bfloat16()
+    x = torch.randn(*shape, device=gpu_device)
+    if ties:
+        x = torch.round(x * 2) / 2
+    x = x.bfloat16()
     y, idx = cnn.maxpool3(x, stride)
     xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
     ref = F.max_pool2d(xr, 3, stride, 1)
@@ -818,3 +830,34 @@ def test_conv_stem_kernel(gpu_device, shape):
     stats = conv.stats_total(rep)
     assert torch.allclose(stats[0], d.sum(0), rtol=1e-3, atol=1e-2)
     assert torch.allclose(stats[1], (d * d).sum(0), rtol=1e-3, atol=1e-2)
+
+
+def test_conv_fwd_tap_gen_sweep(gpu_device):
+    """conv_tap<GEN> (C % 8, several taps per 64-deep K step) against fp32 over random shapes: channel counts
+    off the 64 grid (DenseNet / DPN / GoogLeNet widths), 1x1 / 3x3 / 5x5, stride 1 / 2, partial row tiles, K
+    shorter than one step, and long K (split-K)."""
+    g = torch.Generator().manual_seed(77)
+    shapes = [(2, 4, 4, 16, 16, 1, 1, 0), (2, 5, 5, 24, 8, 1, 2, 0), (4, 8, 8, 304, 96, 1, 1, 0),
+              (4, 8, 8, 336, 200, 1, 2, 0), (3, 16, 16, 96, 96, 3, 2, 1), (2, 7, 9, 40, 72, 3, 1, 1),
+              (16, 4, 4, 600, 256, 1, 1, 0), (8, 4, 4, 648, 512, 3, 1, 1), (2, 11, 11, 56, 24, 5, 1, 2)]
+    for _ in range(8):
+        R = [1, 3, 5][int(torch.randint(0, 3, (1,), generator=g))]
+        C = 8 * int(torch.randint(2, 90 if R < 5 else 40, (1,), generator=g))    # (weight pack: C * R * S rows)
+        if C % 64 == 0:
+            C += 8
+        O = 8 * int(torch.randint(1, 40, (1,), generator=g))
+        st = int(torch.randint(1, 3, (1,), generator=g))
+        H = int(torch.randint(3, 17, (1,), generator=g))
+        shapes.append((int(torch.randint(1, 6, (1,), generator=g)), H, H, C, O, R, st, R // 2))
+    for shape in shapes:
+        N, H, W, Cw, O, R, st, pad = shape
+        x, w, wb, xn = _make(shape, gpu_device, seed=5)
+        wr = conv.pack_weight(w)
+        rep = conv.stats_buffer(O, gpu_device)
+        y = conv.conv2d_fwd(xn, wr, st, pad, Cw=Cw, stats=rep, ws=conv.wgrad_workspace(gpu_device, 1 << 24))
+        ref = F.conv2d(x, wb, stride=st, padding=pad)
+        torch.cuda.synchronize()
+        assert _rel(y.float(), _nhwc(ref)) < 1e-2, shape
+        stats = conv.stats_total(rep)
+        yb = y.float()
+        assert torch.allclose(stats[0], yb.sum((0, 1, 2)), rtol=1e-3, atol=5e-2), shape

@@ -262,3 +262,68 @@ def test_peer_barrier_leaves_on_host_abort_word():
     err, dt = out[0]
     assert err == 1 and out[1][0] == 0, out
     assert 0.25 < dt < 2.0, dt          # not the 20 s timeout
+
+
+class _Flat:
+    def __init__(self, t):
+        self.t = t
+
+    def float_state(self):
+        return self.t
+
+
+def _int8_worker(rank, world, path, q):
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    from fedmi.parallel.compress import Int8Compressor
+    from fedmi.parallel.peer import PeerAllReduce
+
+    store = dist.FileStore(path, world)
+    dev = torch.device("cuda", 0)
+    res = {"ok": True, "msgs": []}
+    n = 62006                                          # LeNet's flat state (odd tail chunk)
+    pc = PeerAllReduce(rank, world, 4 * n + 4096, store, tag="i8")
+    g0 = torch.randn(n, generator=torch.Generator().manual_seed(5)).to(dev)
+    outs = {}
+    for fused in (True, False):
+        x = (g0 + 0.01 * _data(rank, 3, n).to(dev)).contiguous()
+        comp = Int8Compressor(_Flat(x))
+        comp.global_ref.copy_(g0)
+        comp.residual.copy_(1e-3 * _data(rank, 4, n).to(dev))
+        comp.fused = fused
+        for _ in range(3):                              # error feedback carried over rounds
+            x.add_(0.01 * _data(rank, 7 + _, n).to(dev))
+            comp.aggregate(_Flat(x), transport=pc)
+        torch.cuda.synchronize()
+        outs[fused] = (x.cpu(), comp.global_ref.cpu(), comp.residual.cpu())
+    for a, b, name in zip(outs[True], outs[False], ("x", "g", "r")):
+        if not torch.equal(a, b):
+            res["ok"] = False
+            res["msgs"].append(f"{name} fused != unfused: max {(a - b).abs().max().item():.3e}")
+    import hashlib
+
+    res["x"] = hashlib.sha256(outs[True][0].numpy().tobytes()).hexdigest()   # (no tensors through the queue)
+    res["err"] = pc.error()
+    pc.close()
+    q.put((rank, res))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_int8_ef_fused_matches_unfused_bit_exact(world):
+    """the one-launch int8 + error-feedback peer collective equals the unfused path (delta,
+    quantise, two all-gathers, dequantise-accumulate) bit for bit -- x, the new global model and the residual --
+    and every rank ends on the same model."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "store")
+        procs = [ctx.Process(target=_int8_worker, args=(r, world, path, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        out = dict(q.get(timeout=200) for _ in procs)
+        for p in procs:
+            p.join(timeout=60)
+    for r in range(world):
+        assert out[r]["ok"] and out[r]["err"] == 0, (r, out[r]["msgs"])
+        assert out[r]["x"] == out[0]["x"], r
