@@ -2114,7 +2114,11 @@ static int wgrad_splits(const ConvGeom& g, long ws_cap_floats) {
   const TileCfg t = pick_tiles_wgrad(g.M, g.NC);
   const long tiles = (long)((g.M + t.BM - 1) / t.BM) * ((g.NC + t.BN - 1) / t.BN);
   const int ksteps = (g.K + BK - 1) / BK;
-  long sp = std::max<long>(1, 2l * num_cus() / tiles);
+  static const bool up = [] {
+    const char* e = std::getenv("FEDMI_WGRAD_SPLITS_UP");   // A/B: round 5's rounded-up count
+    return e && e[0] == '1';
+  }();
+  long sp = up ? (2l * num_cus() + tiles - 1) / tiles : std::max<long>(1, 2l * num_cus() / tiles);
   sp = std::min<long>(sp, std::max(1, ksteps / 8));
   if (ws_cap_floats > 0) sp = std::min<long>(sp, ws_cap_floats / ((long)g.M * g.NC));
   sp = std::max<long>(1, sp);
@@ -2149,7 +2153,11 @@ void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf
     return;
   }
   if (res) throw std::invalid_argument("conv_fwd: a fused residual needs the tap path (C % 8 == 0, C >= 16)");
-  if (s.C == 8 && s.R == 3 && s.S == 3 && s.st == 1 && s.pad == 1 && (s.O == 32 || s.O == 64)) {
+  static const bool stem_on = [] {
+    const char* e = std::getenv("FEDMI_STEM");                // A/B: 0 = the generic implicit GEMM for the stem
+    return !(e && e[0] == '0');
+  }();
+  if (stem_on && s.C == 8 && s.R == 3 && s.S == 3 && s.st == 1 && s.pad == 1 && (s.O == 32 || s.O == 64)) {
     // the network-input conv (conv_stem_kernel): ~4 pixel tiles of 16 per wave
     const StemGeom sg{s.N, s.H, s.W, s.O, s.N * s.H * s.W};
     const long ntiles = (sg.M + 15) / 16;
