@@ -495,15 +495,9 @@ class CNNNativeTrainer(LocalTrainer):
         # 983 ms per round, MobileNet 886 vs 832: the concurrent kernels compete for CUs / LDS and the split-K
         # sizing assumes the whole chip, profiles/r3_cnn.  Round 6 re-measured it as two graph branches with the
         # side stream's split count divided by 1 / 2 / 4 (sized for the CUs the DGRAD chain leaves): ResNet-18
-        # 847 / 837 / 925 vs 823-827 ms, MobileNet 733 / 752 / 789 vs 690-692, profiles/r6_cnn/ -- one stream)
-        # FEDMI_WGRAD_SIDE_MAXPIX=n (A/B): weight gradients of layers with at most n output pixels per batch on a
-        # second stream (own split-K workspace), beside the DGRAD chain
-        self._wside = None
-        self._wside_maxpix = int(os.environ.get("FEDMI_WGRAD_SIDE_MAXPIX", "0") or 0)
-        self.wgrad_ws2 = None
-        if self._wside_maxpix > 0 and device.type == "cuda" and self.preact is None and self.goog is None:
-            self._wside = torch.cuda.Stream(device)
-            self.wgrad_ws2 = torch.empty_like(self.wgrad_ws)
+        # 847 / 837 / 925 vs 823-827 ms, MobileNet 733 / 752 / 789 vs 690-692; and only for the small layers (<= 2048 /
+        # 8192 output pixels per batch, whose kernels fill a fraction of the chip): ResNet-18 859 / 849 vs 826-829,
+        # MobileNet 739 / 749 vs 691-692, profiles/r6_cnn/ -- one stream)
         # BN-backward two-level channel sums (replicated atomics + finalize; kept zero between uses)
         self.bn_ws = torch.zeros(max(cnn.bn_bwd_ws_floats(B * u.P * u.P, u.O) for u in self.units),
                                  dtype=torch.float64, device=device)
@@ -667,17 +661,7 @@ class CNNNativeTrainer(LocalTrainer):
         return d
 
     def _wgrad(self, u: _Unit, x, nb: int, dz=None) -> None:
-        side = self._wside
-        if side is None or nb * u.P * u.P > self._wside_maxpix:
-            u.wgrad(x, nb, self.wgrad_ws, dz=dz)
-            return
-        # a SMALL layer's weight gradient (few-pixel planes: its kernels fill a fraction of the chip) as a second
-        # graph branch: it needs only dz(u) and u's input, which nothing on the main stream rewrites before the
-        # step's join (_forward_backward), so the DGRAD chain runs on beside it
-        main = torch.cuda.current_stream(self._device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            u.wgrad(x, nb, self.wgrad_ws2, dz=dz)
+        u.wgrad(x, nb, self.wgrad_ws, dz=dz)
 
     def _bn_bwd(self, u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None, dadd=None,
                 mask_bn=None, presummed: bool = False) -> None:
@@ -898,8 +882,6 @@ class CNNNativeTrainer(LocalTrainer):
             self.red_all.zero_()
         x, dh = self._forward(nb, True, self.train_set.x, self.train_set.y, self.cur, 0)
         self._backward(nb, x, dh)
-        if self._wside is not None:                 # join the weight-gradient branch before the update
-            torch.cuda.current_stream(self._device).wait_stream(self._wside)
 
     def _train_step(self, nb: int) -> None:
         """One SGD step on the batch at sched[counter] (device-side)."""
