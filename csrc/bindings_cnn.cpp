@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "kernels/common.h"
+#include "kernels/wgrad_reduce.h"
 
 namespace py = pybind11;
 
@@ -39,7 +40,8 @@ struct PackItem {
   int G;
 };
 void launch_conv_pack_multi(hipStream_t, const PackItem*, int);
-void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int, int, int);
+void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int, int, int,
+                       WredItem*);
 long conv_wgrad_ws_floats(const ConvShape&);
 void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int, int, int);
 struct SgdPackConv {
@@ -79,7 +81,7 @@ struct DwShape {
 void launch_dw_fwd(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, double*, const float*);
 void launch_dw_dgrad(hipStream_t, const DwShape&, const bf16*, const float*, bf16*, const BnSums*);
 long dw_wgrad_ws_floats(const DwShape&);
-void launch_dw_wgrad(hipStream_t, const DwShape&, const bf16*, const bf16*, float*, float*, long, int);
+void launch_dw_wgrad(hipStream_t, const DwShape&, const bf16*, const bf16*, float*, float*, long, int, WredItem*);
 void launch_prep_input(hipStream_t, const uint8_t*, int, const int*, int, int, uint32_t, const int*, bf16*);
 void launch_sched_next(hipStream_t, const int*, int*, int*, double*, long);
 void launch_bn_apply(hipStream_t, const bf16*, const BNDesc&, const bf16*, const BNDesc*, const bf16*, bf16*, int, int,
@@ -121,6 +123,24 @@ DwShape dw_from(const py::tuple& t) {
   int* f = &s.N;
   for (int i = 0; i < 8; ++i) f[i] = t[i].cast<int>();
   return s;
+}
+
+// deferred WGRAD reduction <-> (ws, dw, kind, splits, O, C, Cw, RS, accumulate, Ow, G)
+py::object wred_tuple(const WredItem& e) {
+  return py::make_tuple(reinterpret_cast<uintptr_t>(e.ws), reinterpret_cast<uintptr_t>(e.dw), e.kind, e.splits, e.O,
+                        e.C, e.Cw, e.RS, e.accumulate, e.Ow, e.G);
+}
+
+WredItem wred_from(const py::tuple& t) {
+  if (t.size() != 11) throw std::invalid_argument("wgrad reduce item: (ws, dw, kind, splits, O, C, Cw, RS, acc, Ow, G)");
+  WredItem e{};
+  e.ws = P<const float>(t[0].cast<uintptr_t>());
+  e.dw = P<float>(t[1].cast<uintptr_t>());
+  e.kind = t[2].cast<int>();
+  if (e.kind < WRED_TILE || e.kind > WRED_DW || !e.ws || !e.dw) throw std::invalid_argument("wgrad reduce item: bad kind / pointers");
+  e.splits = t[3].cast<int>(); e.O = t[4].cast<int>(); e.C = t[5].cast<int>(); e.Cw = t[6].cast<int>();
+  e.RS = t[7].cast<int>(); e.accumulate = t[8].cast<int>(); e.Ow = t[9].cast<int>(); e.G = t[10].cast<int>();
+  return e;
 }
 
 BnSums bnsums_from(const py::dict& d) {
@@ -219,13 +239,22 @@ void fedmi_bind_cnn(py::module_& m) {
     if (!v.empty()) launch_conv_pack_multi(S(st), v.data(), (int)v.size());
     check("conv_pack_multi");
   });
+  // defer != 0: the partial reduction is not launched; its descriptor comes back (wred_tuple) for wgrad_reduce_multi
   m.def("conv_wgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws,
-                         long ws_floats, int splits, int accumulate, int Ow, int G) {
+                         long ws_floats, int splits, int accumulate, int Ow, int G, int defer) -> py::object {
+    WredItem it{};
     launch_conv_wgrad(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(dy), P<float>(dw), P<float>(ws),
-                      ws_floats, splits, accumulate, Ow, G);
+                      ws_floats, splits, accumulate, Ow, G, defer ? &it : nullptr);
     check("conv_wgrad");
+    return defer ? wred_tuple(it) : py::object(py::none());
   }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ws"), py::arg("ws_floats"),
-     py::arg("splits"), py::arg("accumulate"), py::arg("Ow") = 0, py::arg("G") = 1);
+     py::arg("splits"), py::arg("accumulate"), py::arg("Ow") = 0, py::arg("G") = 1, py::arg("defer") = 0);
+  m.def("wgrad_reduce_multi", [](uintptr_t st, const py::list& items) {
+    std::vector<WredItem> v;
+    for (const auto& o : items) v.push_back(wred_from(o.cast<py::tuple>()));
+    if (!v.empty()) launch_wgrad_reduce_multi(S(st), v.data(), (int)v.size());
+    check("wgrad_reduce_multi");
+  });
   m.def("conv_wgrad_ws_floats", [](const py::tuple& shp) { return conv_wgrad_ws_floats(shape_from(shp)); });
   m.def("conv_pack", [](uintptr_t st, uintptr_t w, uintptr_t wr, int O, int Cw, int C, int RS, int O8, int G) {
     launch_conv_pack(S(st), P<const float>(w), P<bf16>(wr), O, Cw, C, RS, O8, G);
@@ -248,12 +277,14 @@ void fedmi_bind_cnn(py::module_& m) {
   }, py::arg("st"), py::arg("shp"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("bsum") = py::none());
   m.def("dw_wgrad_ws_floats", [](const py::tuple& shp) { return dw_wgrad_ws_floats(dw_from(shp)); });
   m.def("dw_wgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws,
-                       long ws_floats, int accumulate) {
+                       long ws_floats, int accumulate, int defer) -> py::object {
+    WredItem it{};
     launch_dw_wgrad(S(st), dw_from(shp), P<const bf16>(x), P<const bf16>(dy), P<float>(dw), P<float>(ws), ws_floats,
-                    accumulate);
+                    accumulate, defer ? &it : nullptr);
     check("dw_wgrad");
+    return defer ? wred_tuple(it) : py::object(py::none());
   }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ws"), py::arg("ws_floats"),
-     py::arg("accumulate"));
+     py::arg("accumulate"), py::arg("defer") = 0);
   m.def("prep_input", [](uintptr_t st, uintptr_t images, int base, uintptr_t dbase, int nb, int augment,
                          uint32_t seed, uintptr_t round_ctr, uintptr_t out) {
     launch_prep_input(S(st), P<const uint8_t>(images), base, P<const int>(dbase), nb, augment, seed,

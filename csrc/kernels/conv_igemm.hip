@@ -38,6 +38,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "wgrad_reduce.h"
 
 // diagnostic build (-DFEDMI_STAMPS): s_memtime per conv_tap phase, lane 0 of each workgroup
 // (tools/diag_conv_stamps.py); device code is per translation unit, so conv stamps have their own array
@@ -1428,86 +1429,42 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(const SgdPackEntry* __res
   }
 }
 
-// dW[o][c][r][s] (+)= sum_z ws[z][o][(r*S + s)*C + c]     (c < Cw)
-// Block = one output channel o x 64 input channels, all R*S taps, 4 split groups:
-// each wave reads 256 contiguous bytes per (tap, split), the groups combine in
-// LDS in a fixed order (deterministic), and the block writes its 64 x RS results
-// as ONE contiguous run of dW[o][c0:c0+64][:][:] (the former one-lane-per-column
-// layout scattered every 4-byte store RS floats apart).
+// Split-K WGRAD reductions (bodies in wgrad_reduce.h, shared with the deferred wgrad_reduce_multi below).
 constexpr int WRED_MAX_RS = 49;
 __global__ __launch_bounds__(256) void conv_wgrad_reduce(const float* __restrict__ ws, int splits, int O, int C, int Cw,
                                                          int RS, float* __restrict__ dw, int accumulate, int Ow, int G) {
   extern __shared__ float part_[];                 // [4][RS][65], sized by the launch
-  auto part = [&](int zg, int rs, int ci) -> float& { return part_[(zg * RS + rs) * 65 + ci]; };
-  const long plane = (long)O * RS * C;
-  const int ncb = (C + 63) / 64;
-  const int o = blockIdx.x / ncb, c0 = (blockIdx.x % ncb) * 64;
-  if (o >= Ow) return;                             // zero-padded filters: no output row (workgroup-uniform)
-  const int cl = threadIdx.x & 63, zg = threadIdx.x >> 6;
-  const int c = c0 + cl;
-  for (int rs = 0; rs < RS; ++rs) {
-    float v = 0.f;
-    if (c < C) {
-      const float* p = ws + ((long)o * RS + rs) * C + c;
-      int z = zg;
-      for (; z + 12 < splits; z += 16) {   // 4 independent loads in flight per lane
-        const float a = p[(long)z * plane], b = p[(long)(z + 4) * plane];
-        const float cc = p[(long)(z + 8) * plane], d = p[(long)(z + 12) * plane];
-        v += (a + b) + (cc + d);
-      }
-      for (; z < splits; z += 4) v += p[(long)z * plane];
-    }
-    part(zg, rs, cl) = v;
-  }
-  __syncthreads();
-  // this filter's channels: [cg0, cg0 + Cw) (G > 1: the block-diagonal group of a densified grouped conv)
-  const int cg0 = G > 1 ? (o / (O / G)) * Cw : 0;
-  const int lo = max(c0, cg0), hi = min(c0 + 64, cg0 + Cw);
-  if (hi <= lo) return;
-  float* out = dw + ((long)o * Cw + (lo - cg0)) * RS;
-  for (int e = threadIdx.x; e < (hi - lo) * RS; e += 256) {
-    const int ci = e / RS + (lo - c0), rs = e - (e / RS) * RS;
-    const float s = (part(0, rs, ci) + part(1, rs, ci)) + (part(2, rs, ci) + part(3, rs, ci));
-    out[e] = accumulate ? out[e] + s : s;
-  }
+  fedmi::wred_tile_body(part_, blockIdx.x, ws, splits, O, C, Cw, RS, dw, accumulate, Ow, G);
 }
 
-// Column-mapped variant (one lane per workspace column, scattered stores): more workgroups, so
-// it wins when the plane is small and the split count large (ResNet-18's 64-channel layers).
-// dW[o][c][r][s] (+)= sum_z ws[z][o][(r*S + s)*C + c]     (c < Cw)
-// Block = 64 consecutive workspace columns x 4 split groups: every wave reads
-// 256 contiguous bytes per split (the workspace is read exactly once, fully
-// coalesced), the 4 groups are combined in LDS, and the 64 sums are written to
-// their permuted [O][Cw][R][S] positions.  Deterministic (fixed order).
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_cols(const float* __restrict__ ws, int splits, int O, int C, int Cw,
                                                          int RS, float* __restrict__ dw, int accumulate, int Ow, int G) {
-  __shared__ float part[4][64];
-  const long plane = (long)O * RS * C;
-  const long e = (long)blockIdx.x * 64 + (threadIdx.x & 63);
-  const int zg = threadIdx.x >> 6;
-  float v = 0.f;
-  if (e < plane) {
-    const float* p = ws + e;
-    int z = zg;
-    for (; z + 12 < splits; z += 16) {   // 4 independent loads in flight per lane
-      const float a = p[(long)z * plane], b = p[(long)(z + 4) * plane];
-      const float c = p[(long)(z + 8) * plane], d = p[(long)(z + 12) * plane];
-      v += (a + b) + (c + d);
-    }
-    for (; z < splits; z += 4) v += p[(long)z * plane];
-  }
-  part[zg][threadIdx.x & 63] = v;
-  __syncthreads();
-  if (threadIdx.x < 64 && e < plane) {
-    const float s = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
-    const long t = e / C;
-    const int rs = (int)(t % RS), o = (int)(t / RS);
-    const int c = (int)(e % C) - (G > 1 ? (o / (O / G)) * Cw : 0);   // channel within filter o's group
-    if (c >= 0 && c < Cw && o < Ow) {
-      const long i = ((long)o * Cw + c) * RS + rs;
-      dw[i] = accumulate ? dw[i] + s : s;
-    }
-  }
+  __shared__ float part[4 * 64];
+  fedmi::wred_cols_body(part, blockIdx.x, ws, splits, O, C, Cw, RS, dw, accumulate, Ow, G);
+}
+
+// Deferred WGRAD reductions: every split-K / depthwise partial reduction of a backward pass in one launch
+// (the engines run them all after the last WGRAD, before the SGD step).  Workgroup bid belongs to the last item
+// with blk0 <= bid; each item runs its standalone kernel's body, so the result is bit-identical.
+constexpr int WRED_MULTI_MAX = 32;
+struct WredTable {
+  fedmi::WredItem it[WRED_MULTI_MAX];
+  int blk0[WRED_MULTI_MAX];
+  int n;
+};
+__global__ __launch_bounds__(256) void wgrad_reduce_multi(const WredTable t) {
+  extern __shared__ float lds_[];
+  const int bid = blockIdx.x;
+  int k = 0;
+  while (k + 1 < t.n && t.blk0[k + 1] <= bid) ++k;   // workgroup-uniform
+  const fedmi::WredItem& e = t.it[k];
+  const int b = bid - t.blk0[k];
+  if (e.kind == fedmi::WRED_TILE)
+    fedmi::wred_tile_body(lds_, b, e.ws, e.splits, e.O, e.C, e.Cw, e.RS, e.dw, e.accumulate, e.Ow, e.G);
+  else if (e.kind == fedmi::WRED_COLS)
+    fedmi::wred_cols_body(lds_, b, e.ws, e.splits, e.O, e.C, e.Cw, e.RS, e.dw, e.accumulate, e.Ow, e.G);
+  else
+    fedmi::wred_dw_body(lds_, b, e.ws, e.splits, e.C, e.dw, e.accumulate);
 }
 
 // Split-K FWD / DGRAD combine: out[row][c] = bf16(sum_z ws[z][m][c]); FWD also
@@ -2333,7 +2290,7 @@ long conv_wgrad_ws_floats(const ConvShape& s) {
 // G > 1: a grouped conv run densely with a block-diagonal weight image; filter o keeps only its group's Cw
 // channels of the dense gradient.
 void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const bf16* dy, float* dw, float* ws,
-                       long ws_floats, int splits, int accumulate, int Ow, int G) {
+                       long ws_floats, int splits, int accumulate, int Ow, int G, WredItem* defer) {
   if (Ow <= 0 || Ow > s.O) Ow = s.O;
   if (G < 1) G = 1;
   if (G > 1 && (s.O % G || s.C < G * s.Cw || Ow != s.O))
@@ -2359,12 +2316,45 @@ void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const 
   }
   if (s.R * s.S > WRED_MAX_RS) throw std::invalid_argument("conv_wgrad: window larger than 7x7");
   const long blocks = (long)s.O * ((s.C + 63) / 64);
-  if (blocks >= 1024) {      // enough (o, channel-block) tiles: coalesced tile writes
-    hipLaunchKernelGGL(conv_wgrad_reduce, dim3((unsigned)blocks), dim3(256), 4 * s.R * s.S * 65 * sizeof(float), st,
-                       ws, splits, s.O, s.C, s.Cw, s.R * s.S, dw, accumulate, Ow, G);
-  } else {
-    hipLaunchKernelGGL(conv_wgrad_reduce_cols, dim3((unsigned)((plane + 63) / 64)), dim3(256), 0, st, ws, splits, s.O,
-                       s.C, s.Cw, s.R * s.S, dw, accumulate, Ow, G);
+  // enough (o, channel-block) tiles: coalesced tile writes; else one lane per workspace column
+  const WredItem it{ws, dw, blocks >= 1024 ? WRED_TILE : WRED_COLS, splits, s.O, s.C, s.Cw, s.R * s.S, accumulate, Ow, G};
+  if (defer) {               // the caller runs it later in launch_wgrad_reduce_multi
+    *defer = it;
+    return;
+  }
+  launch_wgrad_reduce_multi(st, &it, 1);
+}
+
+// Deferred reductions (WredItem, filled by launch_conv_wgrad / launch_dw_wgrad with a `defer` slot): one launch
+// per WRED_MULTI_MAX items; a single item launches its standalone kernel.
+void launch_wgrad_reduce_multi(hipStream_t st, const WredItem* items, int n) {
+  for (int i0 = 0; i0 < n; i0 += WRED_MULTI_MAX) {
+    const int m = std::min(WRED_MULTI_MAX, n - i0);
+    if (m == 1) {
+      const WredItem& e = items[i0];
+      const unsigned g = (unsigned)wred_blocks(e);
+      if (e.kind == WRED_TILE)
+        hipLaunchKernelGGL(conv_wgrad_reduce, dim3(g), dim3(256), wred_lds_bytes(e), st, e.ws, e.splits, e.O, e.C, e.Cw,
+                           e.RS, e.dw, e.accumulate, e.Ow, e.G);
+      else if (e.kind == WRED_COLS)
+        hipLaunchKernelGGL(conv_wgrad_reduce_cols, dim3(g), dim3(256), 0, st, e.ws, e.splits, e.O, e.C, e.Cw, e.RS,
+                           e.dw, e.accumulate, e.Ow, e.G);
+      else
+        launch_dw_wgrad_reduce(st, e);
+      continue;
+    }
+    WredTable t{};
+    long blk = 0;
+    size_t lds = 0;
+    for (int k = 0; k < m; ++k) {
+      t.it[k] = items[i0 + k];
+      t.blk0[k] = (int)blk;
+      blk += wred_blocks(items[i0 + k]);
+      lds = std::max(lds, wred_lds_bytes(items[i0 + k]));
+    }
+    t.n = m;
+    if (blk >= (1l << 31)) throw std::invalid_argument("wgrad_reduce_multi: grid too large");
+    hipLaunchKernelGGL(wgrad_reduce_multi, dim3((unsigned)blk), dim3(256), lds, st, t);
   }
 }
 

@@ -18,6 +18,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "wgrad_reduce.h"
 
 namespace {
 
@@ -582,32 +583,11 @@ __global__ __launch_bounds__(256) void dw_wgrad3_kernel(const bf16* __restrict__
   wgrad_block_reduce<9>(acc, ws, g, VCB);
 }
 
-// dw[i] (+)= sum_b ws[b][i]: block = 16 outputs x 16 partial groups (each thread
-// sums nblk/16 partials, 4 loads in flight), fixed-order LDS combine.
+// dw[i] (+)= sum_b ws[b][i] (body: wgrad_reduce.h wred_dw_body)
 __global__ __launch_bounds__(256) void dw_wgrad_reduce(const float* __restrict__ ws, int nblk, int n,
                                                        float* __restrict__ dw, int accumulate) {
-  __shared__ float part[16][17];
-  const int col = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const int i = blockIdx.x * 16 + col;
-  float a = 0.f, b = 0.f, c = 0.f, d = 0.f;
-  if (i < n) {
-    int k = grp;
-    for (; k + 48 < nblk; k += 64) {
-      a += ws[(long)k * n + i];
-      b += ws[(long)(k + 16) * n + i];
-      c += ws[(long)(k + 32) * n + i];
-      d += ws[(long)(k + 48) * n + i];
-    }
-    for (; k < nblk; k += 16) a += ws[(long)k * n + i];
-  }
-  part[grp][col] = (a + b) + (c + d);
-  __syncthreads();
-  if (threadIdx.x < 16 && i < n) {
-    float v = 0.f;
-#pragma unroll
-    for (int g2 = 0; g2 < 16; ++g2) v += part[g2][col];
-    dw[i] = accumulate ? dw[i] + v : v;
-  }
+  __shared__ float part[16 * 17];
+  fedmi::wred_dw_body(part, blockIdx.x, ws, nblk, n, dw, accumulate);
 }
 
 int blocks_for(long items, int tb = 256) { return (int)std::max<long>(1, std::min<long>((items + tb - 1) / tb, 4096)); }
@@ -703,8 +683,14 @@ long dw_wgrad_ws_floats(const DwShape& s) {
   return (long)dw_wgrad_blocks(g) * g.C * g.R * g.S;
 }
 
+void launch_dw_wgrad_reduce(hipStream_t st, const WredItem& e) {
+  hipLaunchKernelGGL(dw_wgrad_reduce, dim3((unsigned)wred_blocks(e)), dim3(256), 0, st, e.ws, e.splits, e.C, e.dw,
+                     e.accumulate);
+}
+
+// defer: fill the reduction's WredItem instead of launching it (see launch_wgrad_reduce_multi)
 void launch_dw_wgrad(hipStream_t st, const DwShape& s, const bf16* x, const bf16* dy, float* dw, float* ws,
-                     long ws_floats, int accumulate) {
+                     long ws_floats, int accumulate, WredItem* defer) {
   const DwGeom g = dw_geom(s);
   const int nblk = dw_wgrad_blocks(g);
   const int n = g.C * g.R * g.S;
@@ -719,7 +705,10 @@ void launch_dw_wgrad(hipStream_t st, const DwShape& s, const bf16* x, const bf16
   else if (g.R == 3) hipLaunchKernelGGL(dw_wgrad_kernel<9>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb);
   else if (g.R == 5) hipLaunchKernelGGL(dw_wgrad_kernel<25>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb);
   else hipLaunchKernelGGL(dw_wgrad_kernel<49>, grid, dim3(tb), 0, st, x, dy, ws, g, ppb, vcb);
-  hipLaunchKernelGGL(dw_wgrad_reduce, dim3((n + 15) / 16), dim3(256), 0, st, ws, nblk, n, dw, accumulate);
+  WredItem it{};
+  it.ws = ws; it.dw = dw; it.kind = WRED_DW; it.splits = nblk; it.C = n; it.accumulate = accumulate;
+  if (defer) *defer = it;
+  else launch_dw_wgrad_reduce(st, it);
 }
 
 }  // namespace fedmi

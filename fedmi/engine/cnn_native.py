@@ -116,13 +116,21 @@ class _Unit:
             conv.conv2d_fwd(x, self.wr, self.stride, self.pad, Cw=self.Cw, stats=stats, out=self.view(self.z, nb),
                             shift=sh, ws=ws, res=res)
 
-    def wgrad(self, x: torch.Tensor, nb: int, ws: torch.Tensor, dz: Optional[torch.Tensor] = None) -> None:
+    def wgrad_floats(self, nb: int) -> int:
+        """Partial-sum floats this conv's WGRAD writes (its own buffer when the reduction is deferred)."""
+        if self.depthwise:
+            return conv.dwconv_ws_floats(self.in_shape(nb), self.R, self.stride, self.pad)
+        return conv.wgrad_ws_floats(self.in_shape(nb), self.O, self.R, self.S, self.stride, self.pad, self.Cw)
+
+    def wgrad(self, x: torch.Tensor, nb: int, ws: torch.Tensor, dz: Optional[torch.Tensor] = None,
+              deferred: Optional[list] = None) -> None:
         dz = self.view(self.dz, nb) if dz is None else dz
         if self.depthwise:
-            conv.dwconv_wgrad(x, dz, self.R, self.stride, self.pad, out=self.conv.weight.grad, ws=ws)
+            conv.dwconv_wgrad(x, dz, self.R, self.stride, self.pad, out=self.conv.weight.grad, ws=ws,
+                              deferred=deferred)
         else:
             conv.conv2d_wgrad(x, dz, self.R, self.S, self.stride, self.pad, Cw=self.Cw, out=self.conv.weight.grad,
-                              ws=ws)
+                              ws=ws, deferred=deferred)
 
     def dgrad(self, nb: int, out: torch.Tensor, ws: Optional[torch.Tensor] = None,
               dz: Optional[torch.Tensor] = None, accumulate: bool = False, add: Optional[torch.Tensor] = None,
@@ -498,6 +506,22 @@ class CNNNativeTrainer(LocalTrainer):
         # 847 / 837 / 925 vs 823-827 ms, MobileNet 733 / 752 / 789 vs 690-692; and only for the small layers (<= 2048 /
         # 8192 output pixels per batch, whose kernels fill a fraction of the chip): ResNet-18 859 / 849 vs 826-829,
         # MobileNet 739 / 749 vs 691-692, profiles/r6_cnn/ -- one stream)
+        # Deferred WGRAD reductions: every conv's WGRAD writes its split-K / depthwise partials into a buffer of its
+        # own and ONE launch after the backward pass sums them all (conv.wgrad_reduce_multi; bit-identical to the
+        # per-conv reduce launches it replaces, most of them latency-bound).  FEDMI_WRED_DEFER=0: per-conv
+        # reductions in the shared workspace (A/B).
+        self._wred: Optional[list] = None
+        self._wpart = {}
+        if os.environ.get("FEDMI_WRED_DEFER", "1") != "0":
+            # sized for every batch size a schedule can hold: the automatic split count is capped by the
+            # workspace, and it is not monotone in the batch (a partial last batch of 80 takes 160 splits of a
+            # GoogLeNet 3x3 conv where 128 take 158) -- a binding cap would change the rounding
+            sizes = [(max(u.wgrad_floats(nb) for nb in range(1, B + 1)) + 63) // 64 * 64 for u in self.units]
+            self.wgrad_parts = torch.empty(sum(sizes), device=device)
+            off = 0
+            for u, n in zip(self.units, sizes):
+                self._wpart[id(u)] = self.wgrad_parts[off:off + n]
+                off += n
         # BN-backward two-level channel sums (replicated atomics + finalize; kept zero between uses)
         self.bn_ws = torch.zeros(max(cnn.bn_bwd_ws_floats(B * u.P * u.P, u.O) for u in self.units),
                                  dtype=torch.float64, device=device)
@@ -661,7 +685,11 @@ class CNNNativeTrainer(LocalTrainer):
         return d
 
     def _wgrad(self, u: _Unit, x, nb: int, dz=None) -> None:
-        u.wgrad(x, nb, self.wgrad_ws, dz=dz)
+        part = self._wpart.get(id(u)) if self._wred is not None else None
+        if part is None:
+            u.wgrad(x, nb, self.wgrad_ws, dz=dz)
+        else:
+            u.wgrad(x, nb, part, dz=dz, deferred=self._wred)
 
     def _bn_bwd(self, u: _Unit, nb: int, dya, dyb, y, zb: Optional[_Unit] = None, gout=None, dadd=None,
                 mask_bn=None, presummed: bool = False) -> None:
@@ -881,7 +909,13 @@ class CNNNativeTrainer(LocalTrainer):
         if not self.bn_ws.numel():     # atomic BN-backward sums (emulation) need zeroed accumulators
             self.red_all.zero_()
         x, dh = self._forward(nb, True, self.train_set.x, self.train_set.y, self.cur, 0)
-        self._backward(nb, x, dh)
+        self._wred = [] if self._wpart else None
+        try:
+            self._backward(nb, x, dh)
+            if self._wred:
+                conv.wgrad_reduce_multi(self._wred, self._device)
+        finally:
+            self._wred = None
 
     def _train_step(self, nb: int) -> None:
         """One SGD step on the batch at sched[counter] (device-side)."""

@@ -12,6 +12,7 @@ Reference ops: ``convolution`` / ``convolution_backward`` of every zoo model
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -311,10 +312,19 @@ def wgrad_ws_floats(x_shape, O: int, R: int, S: int, stride: int, pad: int, Cw: 
     return int(native.require().conv_wgrad_ws_floats(shape_tuple(x_shape, O, R, S, stride, pad, Cw)))
 
 
+# Pixel count (N*H*W) up to which a 1x1 / stride-1 WGRAD goes to the library GEMM; FEDMI_WGRAD_GEMM=0 keeps every
+# WGRAD native (A/B switch).
+WGRAD_GEMM_PIXELS = 2048 if os.environ.get("FEDMI_WGRAD_GEMM", "1") != "0" else 0
+
+
 def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None,
                  out: Optional[torch.Tensor] = None, accumulate: bool = False, splits: int = 0,
-                 ws: Optional[torch.Tensor] = None, Ow: Optional[int] = None, groups: int = 1) -> torch.Tensor:
+                 ws: Optional[torch.Tensor] = None, Ow: Optional[int] = None, groups: int = 1,
+                 deferred: Optional[list] = None) -> torch.Tensor:
     """dW fp32 [O, Cw, R, S] (PyTorch layout).  ``accumulate`` adds into ``out`` instead of overwriting.
+    ``deferred`` (a list): the split-K reduction is not launched but appended as a descriptor, for ONE
+    :func:`wgrad_reduce_multi` launch after the backward pass -- ``ws`` must then stay untouched until that launch
+    (``out`` is not written before it).
     ``Ow`` < O: dy carries zero-padded filters; only the first Ow land in ``out`` ([Ow, Cw, R, S]).
     ``groups`` > 1: a grouped conv run densely (block-diagonal image): filter o keeps its group's Cw channels.
 
@@ -335,13 +345,33 @@ def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int,
         accumulate = False
     if tuple(out.shape) != (Ow, shp[4], R, S) or out.dtype != torch.float32 or not out.is_contiguous():
         raise ValueError("conv2d_wgrad: out must be contiguous fp32 [Ow, Cw, R, S]")
+    if (WGRAD_GEMM_PIXELS and R == 1 and S == 1 and stride == 1 and pad == 0 and groups == 1 and Ow == O
+            and not accumulate and not splits and shp[4] == shp[3] and shp[0] * shp[1] * shp[2] <= WGRAD_GEMM_PIXELS):
+        # 1x1 / stride 1 over at most 2048 pixels (MobileNet's 4x4 / 2x2 pointwise layers): a plain GEMM
+        # dW[O, C] = dY^T X, where one library launch beats split-K + reduce (15.5-15.8 vs 17.3-20.1 us at 4x4,
+        # 8.1-8.6 vs 21.8-28.5 us at 2x2; the native kernel wins from 8x8 up: profiles/r6_cnn/wgrad1x1.jsonl).
+        # The library result is bit-stable run to run.
+        C = shp[3]
+        torch.mm(dy.view(-1, O).t(), x.view(-1, C), out_dtype=torch.float32, out=out.view(O, C))
+        return out
     nat = native.require()
+    if deferred is not None and ws is None:
+        raise ValueError("conv2d_wgrad: a deferred reduction needs its own workspace")
     if ws is None:
         need = max(nat.conv_wgrad_ws_floats(shp), splits * O * R * S * shp[3])
         ws = wgrad_workspace(x.device, need)
-    nat.conv_wgrad(native.stream_handle(x.device), shp, x.data_ptr(), dy.data_ptr(), out.data_ptr(), ws.data_ptr(),
-                   ws.numel(), splits, int(accumulate), Ow, int(groups))
+    item = nat.conv_wgrad(native.stream_handle(x.device), shp, x.data_ptr(), dy.data_ptr(), out.data_ptr(),
+                          ws.data_ptr(), ws.numel(), splits, int(accumulate), Ow, int(groups), int(deferred is not None))
+    if item is not None:
+        deferred.append(item)
     return out
+
+
+def wgrad_reduce_multi(items: list, device) -> None:
+    """Run the WGRAD partial reductions collected by ``conv2d_wgrad`` / ``dwconv_wgrad`` (``deferred=``) in one
+    launch (per 32 items); each item sums exactly as its immediate reduction would (bit-identical)."""
+    if items:
+        native.require().wgrad_reduce_multi(native.stream_handle(device), list(items))
 
 
 # ---------------------------------------------------------------------------
@@ -390,7 +420,9 @@ def dwconv_ws_floats(x_shape, R: int, stride: int, pad: int) -> int:
 
 
 def dwconv_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, stride: int, pad: int, out: Optional[torch.Tensor] = None,
-                 accumulate: bool = False, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 accumulate: bool = False, ws: Optional[torch.Tensor] = None,
+                 deferred: Optional[list] = None) -> torch.Tensor:
+    """Depthwise dW fp32 [C, 1, R, R]; ``deferred``: as :func:`conv2d_wgrad`."""
     _check(x, torch.bfloat16, "dwconv_wgrad.x")
     _check(dy, torch.bfloat16, "dwconv_wgrad.dy")
     shp = _dw_shape(x.shape, R, stride, pad)
@@ -399,8 +431,12 @@ def dwconv_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, stride: int, pad: in
         out = torch.empty(C, 1, R, R, dtype=torch.float32, device=x.device)
         accumulate = False
     nat = native.require()
+    if deferred is not None and ws is None:
+        raise ValueError("dwconv_wgrad: a deferred reduction needs its own workspace")
     if ws is None:
         ws = wgrad_workspace(x.device, nat.dw_wgrad_ws_floats(shp))
-    nat.dw_wgrad(native.stream_handle(x.device), shp, x.data_ptr(), dy.data_ptr(), out.data_ptr(), ws.data_ptr(),
-                 ws.numel(), int(accumulate))
+    item = nat.dw_wgrad(native.stream_handle(x.device), shp, x.data_ptr(), dy.data_ptr(), out.data_ptr(),
+                        ws.data_ptr(), ws.numel(), int(accumulate), int(deferred is not None))
+    if item is not None:
+        deferred.append(item)
     return out

@@ -152,7 +152,8 @@ def dgrad_fusable(x_shape, O, R, S, stride, pad, Cw=None, has_wd=True):
 
 
 @torch.no_grad()
-def conv2d_wgrad(x, dy, R, S, stride, pad, Cw=None, out=None, accumulate=False, splits=0, ws=None):
+def conv2d_wgrad(x, dy, R, S, stride, pad, Cw=None, out=None, accumulate=False, splits=0, ws=None, deferred=None):
+    # deferred: the emulation reduces immediately (nothing to append)
     Cw = Cw or x.shape[3]
     O = dy.shape[3]
     dw = torch.nn.grad.conv2d_weight(_nchw(x)[:, :Cw], (O, Cw, R, S), _nchw(dy), stride=stride, padding=pad)
@@ -167,6 +168,10 @@ def conv2d_wgrad(x, dy, R, S, stride, pad, Cw=None, out=None, accumulate=False, 
 
 def wgrad_ws_floats(*a, **k):
     return 1
+
+
+def wgrad_reduce_multi(items, device):
+    assert not items, "the emulated WGRAD reduces immediately"
 
 
 def dwconv_fwd(x, w, stride, pad, stats=None, out=None, shift=None):
@@ -189,7 +194,7 @@ def dwconv_dgrad(dy, w, x_shape, stride, pad, out=None, bn_sums=None):
 
 
 @torch.no_grad()
-def dwconv_wgrad(x, dy, R, stride, pad, out=None, accumulate=False, ws=None):
+def dwconv_wgrad(x, dy, R, stride, pad, out=None, accumulate=False, ws=None, deferred=None):
     C = x.shape[3]
     dw = torch.nn.grad.conv2d_weight(_nchw(x), (C, 1, R, R), _nchw(dy), stride=stride, padding=pad,
                                      groups=C)
@@ -395,7 +400,7 @@ def emulated():
         saved.append((mod, name, getattr(mod, name)))
         setattr(mod, name, fn)
 
-    for name in ("pack_weight", "pack_weights", "SgdPack", "fd_ws_floats", "dgrad_pack_weights", "conv2d_fwd", "conv2d_dgrad", "dgrad_fusable", "conv2d_wgrad", "wgrad_ws_floats", "dwconv_fwd",
+    for name in ("pack_weight", "pack_weights", "SgdPack", "fd_ws_floats", "dgrad_pack_weights", "conv2d_fwd", "conv2d_dgrad", "dgrad_fusable", "conv2d_wgrad", "wgrad_ws_floats", "wgrad_reduce_multi", "dwconv_fwd",
                  "dwconv_dgrad", "dwconv_wgrad", "dwconv_ws_floats"):
         swap(conv, name, globals()[name])
     for name in ("prep_input", "sched_next", "bn_apply", "bn_bwd", "bn_bwd_ws_floats", "bn_bwd_chain_floats", "head", "maxpool2",

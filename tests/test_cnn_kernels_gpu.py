@@ -124,6 +124,25 @@ def test_conv_wgrad_split_invariance(gpu_device):
     assert _rel(a, b) < 1e-4
 
 
+@pytest.mark.parametrize("shape", [(128, 4, 4, 512, 512), (128, 2, 2, 1024, 1024), (16, 4, 4, 256, 512),
+                                   (64, 8, 8, 128, 256)])
+def test_conv_wgrad_1x1_library_route(gpu_device, shape, monkeypatch):
+    """1x1 / stride-1 WGRAD over <= 2048 pixels goes to the library GEMM (conv.WGRAD_GEMM_PIXELS); both routes
+    match fp32 and each other, and the library route is bit-stable run to run."""
+    N, H, W, C, O = shape
+    torch.manual_seed(11)
+    xn = torch.randn(N, H, W, C, device=gpu_device).bfloat16()
+    dy = torch.randn(N, H, W, O, device=gpu_device).bfloat16()
+    ref = (dy.float().view(-1, O).t() @ xn.float().view(-1, C)).view(O, C, 1, 1)
+    lib = conv.conv2d_wgrad(xn, dy, 1, 1, 1, 0)
+    lib2 = conv.conv2d_wgrad(xn, dy, 1, 1, 1, 0)
+    monkeypatch.setattr(conv, "WGRAD_GEMM_PIXELS", 0)
+    nat = conv.conv2d_wgrad(xn, dy, 1, 1, 1, 0)
+    torch.cuda.synchronize()
+    assert _rel(lib, ref) < 1e-5 and _rel(nat, ref) < 1e-5
+    assert torch.equal(lib, lib2)
+
+
 def _bn_ref(z, gamma, beta, eps=1e-5):
     mean = z.mean(0)
     var = z.var(0, unbiased=False)

@@ -99,6 +99,32 @@ def test_engine_is_deterministic(gpu_device, name):
     assert sa.correct == sb.correct and sa.count == sb.count
 
 
+@pytest.mark.parametrize("name", ["ResNet18", "MobileNet", "GoogLeNet", "PreActResNet18"])
+def test_deferred_wgrad_reductions_are_bit_identical(gpu_device, name, monkeypatch):
+    """The deferred WGRAD reductions (one wgrad_reduce_multi launch after the backward pass, every conv's
+    partials in a buffer of its own) give bit-identical weight gradients to the per-conv reduce launches
+    (FEDMI_WRED_DEFER=0), at the full batch and at a partial last batch."""
+    from fedmi.engine.cnn_native import CNNNativeTrainer
+
+    data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=256, n_test=64, seed=0)
+    init = build_model(name).state_dict()
+    runs = []
+    for defer in ("1", "0"):
+        monkeypatch.setenv("FEDMI_WRED_DEFER", defer)
+        tr = CNNNativeTrainer(name, data, gpu_device, TrainerConfig(batch_size=128, augment=False, use_graph=False),
+                              init_state=init)
+        assert bool(tr._wpart) == (defer == "1")
+        grads = []
+        for start, nb in ((0, 128), (128, 80)):
+            tr.grads_for_batch(start, nb)
+            torch.cuda.synchronize()
+            grads.append({k: p.grad.clone() for k, p in tr.model.named_parameters()})
+        runs.append(grads)
+    for a, b in zip(*runs):
+        bad = [k for k in a if not torch.equal(a[k], b[k])]
+        assert not bad, f"{len(bad)} / {len(a)} gradients differ: {bad[:5]}"
+
+
 # Bounds from profiles/r4_tests/grad_cosines.jsonl (tools/diag_grad_cosines.py, one batch of 64 at random init).
 # A tensor is WELL-CONDITIONED when PyTorch's own autocast-bf16 gradient keeps cos >= 0.9 to fp32: there the
 # native engine must stay within 0.05 of torch-bf16 (ResNet-18: all 62 tensors, worst gap -0.022).  On the
