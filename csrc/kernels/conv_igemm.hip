@@ -2135,8 +2135,11 @@ void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf
 // add: dx = result + add (a second incoming grad, e.g. the shortcut branch's; != dx) and bs: the
 // producer BN's backward sums taken in the epilogue -- both only on the tap path without empty
 // phases (conv_dgrad_fusable).
+// O % 64 == 0 (every stride: conv_tap / conv_tap_phases), or stride 1 with O % 8 == 0 from 16 channels: one phase, a
+// plain conv_tap problem over dY with O input channels -> conv_tap<GEN> (the GoogLeNet / zoo narrow branches)
 static bool dgrad_tap_ok(const ConvShape& s) {
-  return s.O % 64 == 0 && tap_fits((long)s.N * s.P * s.Q * s.O, (long)s.C * s.R * s.S * s.O, s.R, s.S);
+  const bool gen = s.st == 1 && tap_gen_enabled() && s.O % 8 == 0 && s.O >= 16;
+  return (s.O % 64 == 0 || gen) && tap_fits((long)s.N * s.P * s.Q * s.O, (long)s.C * s.R * s.S * s.O, s.R, s.S);
 }
 
 int conv_dgrad_fusable(const ConvShape& s, int has_wd) {
@@ -2214,7 +2217,7 @@ long conv_fd_ws_floats(const ConvShape& s) {
     const int tsp = tap_splits(t, cap);
     if (tsp > 1) need = std::max(need, (long)tsp * t.M * t.O);
   }
-  if (s.O % 64 == 0) {
+  if (dgrad_tap_ok(s)) {
     TapPhase ph[4];
     const int n = dgrad_tap_phases(s, ph);
     if (n > 1) {
@@ -2447,8 +2450,9 @@ SgdPackPlan build_sgd_pack_plan(const SgdPackConv* convs, int nc, const long* se
   int blk = 0, lds = 0;
   for (int k = 0; k < nc; ++k) {
     const SgdPackConv& c = convs[k];
-    if (c.C % 8 || c.C < c.Cw || c.Cw < 1 || c.O < 1 || c.R * c.S > 49 || (c.wd && c.O % 64))
-      throw std::invalid_argument("sgd_pack: unsupported conv (C % 8, C >= Cw, R*S <= 49, O % 64 with a DGRAD image)");
+    if (c.C % 8 || c.C < c.Cw || c.Cw < 1 || c.O < 1 || c.R * c.S > 49 || (c.wd && (c.O % 8 || (c.O % 64 && c.st != 1))))
+      throw std::invalid_argument("sgd_pack: unsupported conv (C % 8, C >= Cw, R*S <= 49; a DGRAD image needs O % 64, "
+                                  "or O % 8 at stride 1)");
     SgdPackEntry e{};
     e.kind = 0; e.off = c.off; e.wr = c.wr;
     e.O = c.O; e.Cw = c.Cw; e.C = c.C; e.R = c.R; e.S = c.S; e.step = c.st;

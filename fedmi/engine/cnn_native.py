@@ -75,9 +75,9 @@ class _Unit:
         bf = dict(dtype=act_dtype, device=dev)
         self.wr = None if self.depthwise else torch.empty(self.O, self.R, self.S, self.C, dtype=torch.bfloat16,
                                                           device=dev)
-        # flipped/transposed weight image for the tap-major DGRAD kernel (O % 64 == 0)
+        # flipped/transposed weight image for the tap-major DGRAD kernel (O % 64 == 0; stride 1: O % 8 == 0)
         self.wd = (torch.empty(conv.dgrad_image_numel(c.weight.shape, self.C), dtype=torch.bfloat16, device=dev)
-                   if not self.depthwise and conv.dgrad_eligible(self.O) else None)
+                   if not self.depthwise and conv.dgrad_eligible(self.O, self.stride) else None)
         self.z = torch.empty(n_out, **bf)                            # conv output (pre-BN)
         self.y = torch.empty(n_out, **bf) if need_y else None        # BN(+ReLU) output inside a block
         self.dz = torch.empty(n_out, **bf)                           # grad wrt z

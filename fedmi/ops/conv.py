@@ -147,9 +147,16 @@ def dgrad_image_numel(w_shape, c_pad: Optional[int] = None) -> int:
     return O * R * S * (c_pad or pad8(Cw))
 
 
-def dgrad_eligible(O: int) -> bool:
-    """The tap-major DGRAD reads dY as its input operand: needs O % 64 == 0."""
-    return O % 64 == 0
+# FEDMI_TAP_GEN=0: convs with C % 64 != 0 (forward) / O % 64 != 0 (stride-1 DGRAD) stay on the generic implicit
+# GEMM (conv_igemm.hip tap_gen_enabled; A/B runs)
+TAP_GEN = os.environ.get("FEDMI_TAP_GEN", "1") != "0"
+
+
+def dgrad_eligible(O: int, stride: Optional[int] = None) -> bool:
+    """The tap-major DGRAD reads dY as its input operand (O input channels): O % 64 == 0, or, at stride 1 (one
+    phase: a plain conv_tap problem), any O % 8 == 0 from 16 channels on ``conv_tap<GEN>`` (several taps per K
+    step).  ``stride`` None: the stride-independent condition."""
+    return O % 64 == 0 or (stride == 1 and TAP_GEN and O % 8 == 0 and O >= 16)
 
 
 def dgrad_pack_weights(items) -> None:
@@ -163,8 +170,8 @@ def dgrad_pack_weights(items) -> None:
         _check(w, torch.float32, "dgrad_pack_weights.w")
         _check(img, torch.bfloat16, "dgrad_pack_weights.img")
         O, Cw, R, S = w.shape
-        if img.numel() < dgrad_image_numel(w.shape, c_pad) or not dgrad_eligible(O):
-            raise ValueError("dgrad_pack_weights: image too small or O % 64 != 0")
+        if img.numel() < dgrad_image_numel(w.shape, c_pad) or not dgrad_eligible(O, int(stride)):
+            raise ValueError("dgrad_pack_weights: image too small or O not DGRAD-eligible at this stride")
         rows.append((w.data_ptr(), img.data_ptr(), O, Cw, c_pad, R, S, int(stride), int(pad)))
     native.require().dgrad_pack_multi(native.stream_handle(items[0][0].device), rows)
 
@@ -198,8 +205,8 @@ class SgdPack:
                     raise ValueError(f"SgdPack: image {tuple(wr.shape)} vs {(O, R, S, int(C))}")
             if wd is not None:
                 _check(wd, torch.bfloat16, "SgdPack.wd")
-                if wd.numel() < dgrad_image_numel(w.shape, C) or not dgrad_eligible(O):
-                    raise ValueError("SgdPack: DGRAD image too small or O % 64 != 0")
+                if wd.numel() < dgrad_image_numel(w.shape, C) or not dgrad_eligible(O, int(stride)):
+                    raise ValueError("SgdPack: DGRAD image too small or O not DGRAD-eligible at this stride")
             rows.append((d // 4, wr.data_ptr() if wr is not None else 0, wd.data_ptr() if wd is not None else 0,
                          O, Cw, int(C), R, S, int(stride), int(pad)))
             cover.append((d // 4, d // 4 + w.numel()))

@@ -1246,7 +1246,7 @@ def _dense_bwd(xh, gy, w32, st, pd, need_dx, need_dw, dx_out=None, dw_out=None, 
     gyp = _pad_c(gy, O8)
     dx = dw = None
     if need_dx:
-        wp, wd = _packed(w32, O8, C8, st, pd, need_wd=groups == 1 and CV.dgrad_eligible(O8), groups=groups)
+        wp, wd = _packed(w32, O8, C8, st, pd, need_wd=groups == 1 and CV.dgrad_eligible(O8, st), groups=groups)
         xs = (N, H, W, C8)
         d = CV.conv2d_dgrad(gyp, wp, xs, st, pd, wd=wd, ws=_ws(xh.device, CV.fd_ws_floats(xs, O8, R, S, st, pd)))
         dx = _unpad_c(d, Cg * groups, dx_out)

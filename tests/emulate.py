@@ -136,8 +136,9 @@ def conv2d_dgrad(dy, wrsc, x_shape, stride, pad, Cw=None, out=None, ws=None, wd=
 
 
 def dgrad_fusable(x_shape, O, R, S, stride, pad, Cw=None, has_wd=True):
-    """Mirror of conv_igemm.hip conv_dgrad_fusable: tap path (a DGRAD image, O % 64), no empty phase."""
-    if not has_wd or O % 64:
+    """Mirror of conv_igemm.hip conv_dgrad_fusable: tap path (a DGRAD image; O % 64, or stride 1 and O % 8 from 16
+    channels), no empty phase."""
+    if not has_wd or not (O % 64 == 0 or (stride == 1 and O % 8 == 0 and O >= 16)):
         return False
     if stride == 1:
         return True

@@ -23,6 +23,10 @@ SHAPES = [
     (4, 16, 16, 48, 48, 3, 1, 1),      # a4 double-3x3 branch
     (4, 16, 16, 480, 192, 1, 1, 0),    # a4 1x1 (C % 64 == 32)
     (16, 4, 4, 160, 320, 3, 1, 1),     # small M, long K (split-K of the GEN path)
+    # O % 64 != 0 at stride 1: the DGRAD runs on conv_tap<GEN> over dY (O input channels)
+    (4, 32, 32, 192, 16, 1, 1, 0),     # a3 1x1 -> 16 (K = 16: one masked K step)
+    (4, 32, 32, 16, 32, 3, 1, 1),      # a3 16 -> 32 3x3
+    (4, 8, 8, 832, 48, 1, 1, 0),       # b5 1x1 -> 48
 ]
 
 
@@ -80,7 +84,7 @@ def test_conv_dgrad_wgrad(gpu_device, shape):
     if Cw < dx.shape[-1]:   # padded input channels see zero weights
         assert float(dx[..., Cw:].float().abs().max()) == 0.0
     assert _rel(dw, wr_.grad) < 1e-2
-    if conv.dgrad_eligible(O):   # tap-major DGRAD on the flipped weight image, every sub-pixel phase
+    if conv.dgrad_eligible(O, st):   # tap-major DGRAD on the flipped weight image (stride 1: any O % 8 via GEN)
         wd = torch.full((conv.dgrad_image_numel(w.shape, xn.shape[-1]),), float("nan"), dtype=torch.bfloat16,
                         device=gpu_device)
         conv.dgrad_pack_weights([(w, wd, st, pad, xn.shape[-1])])
@@ -575,7 +579,7 @@ def test_conv_dgrad_accumulate(gpu_device, shape):
     shp = (xn.shape, O, R, R, st, pad, Cw)
     wsp = torch.empty(max(conv.fd_ws_floats(*shp), 1), device=gpu_device)
     wds = [None]
-    if conv.dgrad_eligible(O):
+    if conv.dgrad_eligible(O, st):
         wd = torch.empty(conv.dgrad_image_numel(w.shape, C), dtype=torch.bfloat16, device=gpu_device)
         conv.dgrad_pack_weights([(w, wd, st, pad, C)])
         wds.append(wd)
@@ -645,7 +649,7 @@ def test_resnet18_batch128_conv_shapes(gpu_device, shape):
     y = conv.conv2d_fwd(xn, wpk, st, pad, Cw=Cw, stats=rep, ws=ws)
     dyn = _nhwc(gy).bfloat16()
     wd = None
-    if conv.dgrad_eligible(O):
+    if conv.dgrad_eligible(O, st):
         wd = torch.empty(conv.dgrad_image_numel(w.shape, C), dtype=torch.bfloat16, device=gpu_device)
         conv.dgrad_pack_weights([(w, wd, st, pad, C)])
     dx = conv.conv2d_dgrad(dyn, wpk, xn.shape, st, pad, Cw=Cw, ws=ws, wd=wd)
@@ -689,7 +693,9 @@ def test_conv_wgrad_halo(gpu_device, shape):
 # DGRAD epilogue with a second incoming grad and the producer BN's backward sums (conv_igemm.hip BnSums):
 # single-pass tap kernel, split-K combine, and the four stride-2 sub-pixel phases
 FUSE_SHAPES = [(8, 16, 16, 64, 64, 3, 1, 1), (128, 32, 32, 64, 64, 3, 1, 1), (128, 8, 8, 256, 256, 3, 1, 1),
-               (128, 4, 4, 512, 512, 3, 1, 1), (16, 16, 16, 64, 128, 3, 2, 1), (16, 8, 8, 128, 256, 1, 1, 0)]
+               (128, 4, 4, 512, 512, 3, 1, 1), (16, 16, 16, 64, 128, 3, 2, 1), (16, 8, 8, 128, 256, 1, 1, 0),
+               # stride-1 DGRAD on conv_tap<GEN> (O % 64 != 0): GoogLeNet's narrow branches
+               (16, 32, 32, 16, 32, 3, 1, 1), (16, 16, 16, 96, 48, 1, 1, 0)]
 
 
 @pytest.mark.parametrize("shape", FUSE_SHAPES, ids=[str(s) for s in FUSE_SHAPES])
