@@ -2137,8 +2137,15 @@ void launch_conv_fwd(hipStream_t st, const ConvShape& s, const bf16* x, const bf
 // phases (conv_dgrad_fusable).
 // O % 64 == 0 (every stride: conv_tap / conv_tap_phases), or stride 1 with O % 8 == 0 from 16 channels: one phase, a
 // plain conv_tap problem over dY with O input channels -> conv_tap<GEN> (the GoogLeNet / zoo narrow branches)
+static bool dgrad_gen_enabled() {   // FEDMI_DGRAD_GEN=0: the GEN DGRAD only off (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("FEDMI_DGRAD_GEN");
+    return !(e && e[0] == '0');
+  }();
+  return on && tap_gen_enabled();
+}
 static bool dgrad_tap_ok(const ConvShape& s) {
-  const bool gen = s.st == 1 && tap_gen_enabled() && s.O % 8 == 0 && s.O >= 16;
+  const bool gen = s.st == 1 && dgrad_gen_enabled() && s.O % 8 == 0 && s.O >= 16;
   return (s.O % 64 == 0 || gen) && tap_fits((long)s.N * s.P * s.Q * s.O, (long)s.C * s.R * s.S * s.O, s.R, s.S);
 }
 

@@ -150,13 +150,14 @@ def dgrad_image_numel(w_shape, c_pad: Optional[int] = None) -> int:
 # FEDMI_TAP_GEN=0: convs with C % 64 != 0 (forward) / O % 64 != 0 (stride-1 DGRAD) stay on the generic implicit
 # GEMM (conv_igemm.hip tap_gen_enabled; A/B runs)
 TAP_GEN = os.environ.get("FEDMI_TAP_GEN", "1") != "0"
+DGRAD_GEN = TAP_GEN and os.environ.get("FEDMI_DGRAD_GEN", "1") != "0"     # the stride-1 GEN DGRAD only (A/B)
 
 
 def dgrad_eligible(O: int, stride: Optional[int] = None) -> bool:
     """The tap-major DGRAD reads dY as its input operand (O input channels): O % 64 == 0, or, at stride 1 (one
     phase: a plain conv_tap problem), any O % 8 == 0 from 16 channels on ``conv_tap<GEN>`` (several taps per K
     step).  ``stride`` None: the stride-independent condition."""
-    return O % 64 == 0 or (stride == 1 and TAP_GEN and O % 8 == 0 and O >= 16)
+    return O % 64 == 0 or (stride == 1 and DGRAD_GEN and O % 8 == 0 and O >= 16)
 
 
 def dgrad_pack_weights(items) -> None:
@@ -327,11 +328,11 @@ WGRAD_GEMM_PIXELS = 2048 if os.environ.get("FEDMI_WGRAD_GEMM", "1") != "0" else 
 def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int, pad: int, Cw: Optional[int] = None,
                  out: Optional[torch.Tensor] = None, accumulate: bool = False, splits: int = 0,
                  ws: Optional[torch.Tensor] = None, Ow: Optional[int] = None, groups: int = 1,
-                 deferred: Optional[list] = None) -> torch.Tensor:
+                 deferred: Optional[list] = None, lib_gemm: bool = True) -> torch.Tensor:
     """dW fp32 [O, Cw, R, S] (PyTorch layout).  ``accumulate`` adds into ``out`` instead of overwriting.
     ``deferred`` (a list): the split-K reduction is not launched but appended as a descriptor, for ONE
     :func:`wgrad_reduce_multi` launch after the backward pass -- ``ws`` must then stay untouched until that launch
-    (``out`` is not written before it).
+    (``out`` is not written before it).  ``lib_gemm`` False: never the library GEMM route (WGRAD_GEMM_PIXELS).
     ``Ow`` < O: dy carries zero-padded filters; only the first Ow land in ``out`` ([Ow, Cw, R, S]).
     ``groups`` > 1: a grouped conv run densely (block-diagonal image): filter o keeps its group's Cw channels.
 
@@ -352,7 +353,7 @@ def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int,
         accumulate = False
     if tuple(out.shape) != (Ow, shp[4], R, S) or out.dtype != torch.float32 or not out.is_contiguous():
         raise ValueError("conv2d_wgrad: out must be contiguous fp32 [Ow, Cw, R, S]")
-    if (WGRAD_GEMM_PIXELS and R == 1 and S == 1 and stride == 1 and pad == 0 and groups == 1 and Ow == O
+    if (lib_gemm and WGRAD_GEMM_PIXELS and R == 1 and S == 1 and stride == 1 and pad == 0 and groups == 1 and Ow == O
             and not accumulate and not splits and shp[4] == shp[3] and shp[0] * shp[1] * shp[2] <= WGRAD_GEMM_PIXELS):
         # 1x1 / stride 1 over at most 2048 pixels (MobileNet's 4x4 / 2x2 pointwise layers): a plain GEMM
         # dW[O, C] = dY^T X, where one library launch beats split-K + reduce (15.5-15.8 vs 17.3-20.1 us at 4x4,

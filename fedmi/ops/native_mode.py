@@ -1246,16 +1246,37 @@ def _dense_bwd(xh, gy, w32, st, pd, need_dx, need_dw, dx_out=None, dw_out=None, 
     gyp = _pad_c(gy, O8)
     dx = dw = None
     if need_dx:
-        wp, wd = _packed(w32, O8, C8, st, pd, need_wd=groups == 1 and CV.dgrad_eligible(O8, st), groups=groups)
+        # (O % 64 only: the stride-1 GEN DGRAD of the CNN engine measured 14 % slower on densenet_cifar here, where
+        # no BN sums ride in its epilogue -- profiles/r6_zoo/routing_ab/)
+        wp, wd = _packed(w32, O8, C8, st, pd, need_wd=groups == 1 and CV.dgrad_eligible(O8), groups=groups)
         xs = (N, H, W, C8)
         d = CV.conv2d_dgrad(gyp, wp, xs, st, pd, wd=wd, ws=_ws(xh.device, CV.fd_ws_floats(xs, O8, R, S, st, pd)))
         dx = _unpad_c(d, Cg * groups, dx_out)
     if need_dw:   # the padded filters O..O8 never leave the reduction (Ow): no slice copy
-        dw = CV.conv2d_wgrad(_pad_c(xh, C8, cache=True), gyp, R, S, st, pd, Cw=Cg, Ow=Og, groups=groups,
-                             out=dw_out if dw_out is not None and dw_out.is_contiguous() else None)
+        out = dw_out if dw_out is not None and dw_out.is_contiguous() else None
+        xp = _pad_c(xh, C8, cache=True)
+        part, wred = _wred_part(out, CV.wgrad_ws_floats(xp.shape, O8, R, S, st, pd, Cg))
+        # (no library-GEMM route here: 1-2.5 % slower on RegNetX / SimpleDLA / DenseNet121, profiles/r6_zoo/routing_ab/)
+        dw = CV.conv2d_wgrad(xp, gyp, R, S, st, pd, Cw=Cg, Ow=Og, groups=groups, out=out, ws=part, deferred=wred,
+                             lib_gemm=False)
         if dw_out is not None and dw.data_ptr() != dw_out.data_ptr():
             dw = ew(dw_out, [dw], EW_COPY)
     return dx, dw
+
+
+def _wred_part(out: Optional[torch.Tensor], floats: int):
+    """(workspace, deferred list) for a WGRAD into ``out``: while a mode runs, a WGRAD that writes a trainer's flat
+    gradient slot keeps its split-K partials in a buffer of its own and appends its reduction to the mode's list --
+    ONE wgrad_reduce_multi launch (per 32) sums them all when anything reads a pending slot, or at the mode's flush
+    (bit-identical to the per-conv reduce: conv_igemm.hip wgrad_reduce.h; ~120 launches per DenseNet step).
+    (None, None): reduce right away in the shared workspace."""
+    mode = NativeMode.current
+    if mode is None or not mode.defer_wred or out is None or floats <= 0:
+        return None, None
+    part = torch.empty(floats, dtype=torch.float32, device=out.device)
+    mode._wred_keep.append(part)
+    mode._wred_ptrs.add(out.data_ptr())
+    return part, mode._wred
 
 
 def _dw_padded_weight(w32: torch.Tensor, C8: int) -> torch.Tensor:
@@ -1381,7 +1402,8 @@ def _conv_bwd(func, grad_output, input, weight, bias_sizes, stride, padding, dil
             if output_mask[0]:
                 gi = _nchw(CV.dwconv_dgrad(gy, w32.contiguous(), xh.shape, st[0], pd[0]))
             if output_mask[1]:
-                gw = CV.dwconv_wgrad(xh, gy, k[0], st[0], pd[0], out=gw_slot)
+                part, wred = _wred_part(gw_slot, CV.dwconv_ws_floats(xh.shape, k[0], st[0], pd[0]))
+                gw = CV.dwconv_wgrad(xh, gy, k[0], st[0], pd[0], out=gw_slot, ws=part, deferred=wred)
         elif groups == 1:
             dx, gw = _dense_bwd(xh, gy, w32, st[0], pd[0], output_mask[0], output_mask[1], dw_out=gw_slot)
             gi = _nchw(dx) if dx is not None else None
@@ -1514,6 +1536,9 @@ class NativeMode(TorchDispatchMode):
         self._cat_plan = {}             # concat-chain head shapes -> final width (kept across blocks)
         self._catbufs = {}              # storage ptr -> _CatBuf of the current block
         self._cat_src = {}              # (ptr, shape) of a plain cat output of this block -> its chain head
+        # deferred WGRAD reductions (see _wred_part): FEDMI_WRED_DEFER=0 reduces each right away (A/B)
+        self.defer_wred = os.environ.get("FEDMI_WRED_DEFER", "1") != "0"
+        self._wred, self._wred_keep, self._wred_ptrs = [], [], set()
 
     def _defer(self, t: torch.Tensor, materialize) -> None:
         self._dead[t.untyped_storage().data_ptr()] = materialize
@@ -1547,7 +1572,14 @@ class NativeMode(TorchDispatchMode):
         t, self._pend_ctr = self._pend_ctr, None
         return t
 
+    def _flush_wred(self) -> None:
+        if self._wred:
+            items, self._wred = self._wred, []
+            CV.wgrad_reduce_multi(items, self._wred_keep[0].device)
+        self._wred_keep, self._wred_ptrs = [], set()
+
     def _flush(self) -> None:
+        self._flush_wred()
         self._flush_ctr()
         if self._pend_mul is not None:
             pend, self._pend_mul = self._pend_mul, None
@@ -1581,6 +1613,8 @@ class NativeMode(TorchDispatchMode):
         if self._pend_thr is not None and not self._fuses_thr(args):
             pend, self._pend_thr = self._pend_thr, None
             pend.materialize()
+        if self._wred_ptrs and any(t.data_ptr() in self._wred_ptrs for t in _iter_tensors(args, kwargs)):
+            self._flush_wred()              # an op reads a weight gradient whose reduction is still pending
         if self._dead and self._pend_sb and self._func is aten.add.Tensor and _sb_pair(self, args, kwargs):
             return                          # the add reads both pending slice gradients' sources itself
         if self._dead:

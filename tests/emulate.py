@@ -153,7 +153,8 @@ def dgrad_fusable(x_shape, O, R, S, stride, pad, Cw=None, has_wd=True):
 
 
 @torch.no_grad()
-def conv2d_wgrad(x, dy, R, S, stride, pad, Cw=None, out=None, accumulate=False, splits=0, ws=None, deferred=None):
+def conv2d_wgrad(x, dy, R, S, stride, pad, Cw=None, out=None, accumulate=False, splits=0, ws=None, deferred=None,
+                 lib_gemm=True):
     # deferred: the emulation reduces immediately (nothing to append)
     Cw = Cw or x.shape[3]
     O = dy.shape[3]

@@ -426,6 +426,29 @@ def test_native_backend_is_deterministic(gpu_device, name):
     assert outs[0][1] == outs[1][1]
 
 
+@pytest.mark.parametrize("name", ["densenet_cifar", "RegNetX_200MF", "EfficientNetB0", "ResNeXt29_2x64d"])
+def test_deferred_wgrad_reductions_are_bit_identical(gpu_device, name):
+    """The aten backend's deferred WGRAD reductions (every WGRAD into a flat-gradient slot keeps its partials; one
+    wgrad_reduce_multi launch per 32 at the first read / the mode's flush) give the same weights, bit for bit, as
+    reducing each right away (defer_wred off), over graph-replayed steps: same reduce bodies, same split counts."""
+    from fedmi.engine import build_trainer
+
+    data = make_dataset("synthetic-cifar10-easy", device=gpu_device, n_train=384, n_test=64, seed=0)
+    cfg = TrainerConfig(batch_size=128, lr=0.02, seed=7)
+    init = build_model(name).state_dict()
+    outs = []
+    for defer in (True, False):
+        tr = build_trainer(name, data, gpu_device, cfg, init_state=init)
+        assert tr.mode is not None, "the zoo family runs on the native aten backend"
+        tr.mode.defer_wred = defer
+        tr.set_schedule(*contiguous_schedule(len(data.train), 128))
+        tr.train_epoch()
+        torch.cuda.synchronize()
+        outs.append((tr.float_state().clone(), tr.train_stats().loss))
+    assert torch.equal(outs[0][0], outs[1][0]), float((outs[0][0] - outs[1][0]).abs().max())
+    assert outs[0][1] == outs[1][1]
+
+
 @pytest.mark.parametrize("C", [24, 36, 48, 252])
 @pytest.mark.parametrize("M", [1000, 4096])
 def test_bn_rows_bwd_fused_mask_matches_premasked(gpu_device, C, M):
