@@ -114,11 +114,12 @@ def wait_for(pred, timeout: float = 60.0, step: float = 0.05):
     raise TimeoutError("condition not reached")
 
 
-def seed_band(native, fp32, floor: float, k: float = 2.0):
+def seed_band(native, fp32, floor: float, k: float = 2.0, lower_only: bool = False):
     """Multi-seed parity gate: a chaotic few-epoch trajectory is not an oracle for ONE seed
     (any rounding change moves it), but the MEAN over seeds must agree with the fp32 engine's mean within
     ``k`` x the fp32 engine's own seed-to-seed standard deviation (never tighter than ``floor``).  Returns
-    (gap, tolerance, details) and asserts."""
+    (gap, tolerance, details) and asserts.  ``lower_only``: only a native mean BELOW fp32's by more than the
+    tolerance fails (a gate on "learns no worse than fp32" where fp32 itself stays at chance in some seeds)."""
     import statistics
 
     assert len(native) == len(fp32) >= 3, (native, fp32)
@@ -127,5 +128,5 @@ def seed_band(native, fp32, floor: float, k: float = 2.0):
     tol = max(floor, k * sd)
     info = {"native": [round(v, 4) for v in native], "fp32": [round(v, 4) for v in fp32],
             "mean_native": round(mn, 4), "mean_fp32": round(mf, 4), "fp32_sd": round(sd, 4), "tol": round(tol, 4)}
-    assert abs(mn - mf) <= tol, info
+    assert (mn >= mf - tol) if lower_only else (abs(mn - mf) <= tol), info
     return abs(mn - mf), tol, info

@@ -121,8 +121,9 @@ def test_config3_scale_global_model_learns(monkeypatch):
     (16k training images, 2k test, 12 rounds, lr 0.02), on the high-contrast synthetic set.  On the default
     low-contrast set every engine's averaged model -- deterministic fp32 PyTorch included -- stays at chance for
     20 rounds at every lr from 0.002 to 0.1 (profiles/r5_noniid/README.md); here FedAvg's global model rises
-    clearly above chance in both engines (seed mean of the peak), and the native engine's late-round accuracy, averaged
-    over 3 seeds, stays within 10 points (or twice the fp32 seed spread) of the deterministic fp32 reference."""
+    clearly above chance in the native engine (seed mean of the peak) and in at least one seed of fp32, and the native
+    engine's late-round accuracy, averaged over 3 seeds, is not below the deterministic fp32 reference's by more than
+    10 points (or twice the fp32 seed spread)."""
     from helpers import seed_band
 
     kw = dict(clients=8, data_spec="synthetic-cifar10-easy", n_train=16000, n_test=2000, lr=0.02)
@@ -136,7 +137,10 @@ def test_config3_scale_global_model_learns(monkeypatch):
             print(seed, eng, accs)
             peaks[eng].append(max(accs))
             tails[eng].append(sum(accs[late:]) / (rounds - late))
-    # above chance (10 %) on the seed mean: a seed of either engine can stay at chance (fp32 seed 18 peaked at 19.4 %)
-    for eng in ("native", "fp32"):
-        assert sum(peaks[eng]) / len(SEEDS) > 20.0, (eng, peaks)
-    print(seed_band(tails["native"], tails["fp32"], floor=10.0)[2])
+    # the native engine learns (seed-mean peak above 20 %; chance is 10 %).  The deterministic fp32 reference is
+    # itself seed- AND process-dependent here: one suite run had it at chance in 2 of 3 seeds (peaks 11.4 / 11.35 /
+    # 30.05, native 46.55 / 31.95 / 26.3), another peaked at 19.4 % in seed 18 -- so fp32 must learn in at least one
+    # seed, and the band is one-sided: the native late-round accuracy may not fall below fp32's by more than the band
+    assert sum(peaks["native"]) / len(SEEDS) > 20.0, peaks
+    assert max(peaks["fp32"]) > 20.0, peaks
+    print(seed_band(tails["native"], tails["fp32"], floor=10.0, lower_only=True)[2])
