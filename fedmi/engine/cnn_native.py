@@ -515,11 +515,18 @@ class CNNNativeTrainer(LocalTrainer):
         if os.environ.get("FEDMI_WRED_DEFER", "1") != "0":
             # sized for every batch size a schedule can hold: the automatic split count is capped by the
             # workspace, and it is not monotone in the batch (a partial last batch of 80 takes 160 splits of a
-            # GoogLeNet 3x3 conv where 128 take 158) -- a binding cap would change the rounding
-            sizes = [(max(u.wgrad_floats(nb) for nb in range(1, B + 1)) + 63) // 64 * 64 for u in self.units]
-            self.wgrad_parts = torch.empty(sum(sizes), device=device)
+            # GoogLeNet 3x3 conv where 128 take 158) -- a binding cap would change the rounding.
+            # FEDMI_WRED_DEFER_MB=n: defer only WGRADs with at most n MB of partials, reducing the larger sets right
+            # away while they may still sit in the 256 MB infinity cache (ResNet-18's 3x3 halo WGRADs write ~38 MB
+            # each, ~480 MB per step).  Measured a wash -- ResNet-18 816.6 / 819.2 ms at 8 MB, 815.3 at 64, 815.6 all
+            # deferred; GoogLeNet 3338 vs 3325 (profiles/r6_cnn/wgrad_defer/cap_*) -- so everything is deferred.
+            cap = float(os.environ.get("FEDMI_WRED_DEFER_MB", "inf")) * (1 << 20) / 4
+            need = {id(u): max(u.wgrad_floats(nb) for nb in range(1, B + 1)) for u in self.units}
+            units = [u for u in self.units if need[id(u)] <= cap]
+            sizes = [(need[id(u)] + 63) // 64 * 64 for u in units]
+            self.wgrad_parts = torch.empty(max(sum(sizes), 1), device=device)
             off = 0
-            for u, n in zip(self.units, sizes):
+            for u, n in zip(units, sizes):
                 self._wpart[id(u)] = self.wgrad_parts[off:off + n]
                 off += n
         # BN-backward two-level channel sums (replicated atomics + finalize; kept zero between uses)
@@ -912,8 +919,8 @@ class CNNNativeTrainer(LocalTrainer):
         self._wred = [] if self._wpart else None
         try:
             self._backward(nb, x, dh)
-            if self._wred:
-                conv.wgrad_reduce_multi(self._wred, self._device)
+            if self._wred:      # the most recently written partials first (the likeliest still cache-resident)
+                conv.wgrad_reduce_multi(self._wred[::-1], self._device)
         finally:
             self._wred = None
 

@@ -109,8 +109,9 @@ def test_deferred_wgrad_reductions_are_bit_identical(gpu_device, name, monkeypat
     data = make_dataset("synthetic-cifar10", device=gpu_device, n_train=256, n_test=64, seed=0)
     init = build_model(name).state_dict()
     runs = []
-    for defer in ("1", "0"):
+    for defer, cap_mb in (("1", "inf"), ("1", "8"), ("0", "inf")):   # all deferred (default) / a size split / none
         monkeypatch.setenv("FEDMI_WRED_DEFER", defer)
+        monkeypatch.setenv("FEDMI_WRED_DEFER_MB", cap_mb)
         tr = CNNNativeTrainer(name, data, gpu_device, TrainerConfig(batch_size=128, augment=False, use_graph=False),
                               init_state=init)
         assert bool(tr._wpart) == (defer == "1")
@@ -120,9 +121,10 @@ def test_deferred_wgrad_reductions_are_bit_identical(gpu_device, name, monkeypat
             torch.cuda.synchronize()
             grads.append({k: p.grad.clone() for k, p in tr.model.named_parameters()})
         runs.append(grads)
-    for a, b in zip(*runs):
-        bad = [k for k in a if not torch.equal(a[k], b[k])]
-        assert not bad, f"{len(bad)} / {len(a)} gradients differ: {bad[:5]}"
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            bad = [k for k in a if not torch.equal(a[k], b[k])]
+            assert not bad, f"{len(bad)} / {len(a)} gradients differ: {bad[:5]}"
 
 
 # Bounds from profiles/r4_tests/grad_cosines.jsonl (tools/diag_grad_cosines.py, one batch of 64 at random init).
