@@ -100,7 +100,9 @@ FEDMI_DEV void zero_lds(void* p, int bytes) {
 // lenet_conv_fwd: conv stack forward, one 8-wave workgroup per sample (eval; in "train" mode it
 // also saves act2T / pool1 / argmax codes -- the tests' forward oracle for KS1's backward).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT_FWD) void lenet_conv_fwd(
+// (at least 6 waves per SIMD: 76 VGPRs, three 49 KB workgroups per CU instead of two at 82 -- the eval launch is
+// 10 000 latency-bound workgroups, so images in flight per CU set its throughput)
+__global__ __launch_bounds__(NT_FWD, 6) void lenet_conv_fwd(
     const uint8_t* __restrict__ images, int sample_base, int nb,
     const bf16* __restrict__ pk, const float* __restrict__ params,
     uint32_t seed, const int* __restrict__ round_ctr, int augment,
