@@ -88,7 +88,9 @@ def _breakdown(marks, phases, t0: float, t1: float, steps: int) -> dict:
             "device_round_span_ms": med(span), "device_round_span_ms_mean": mean(span),
             "device_idle_between_rounds_ms": med(gaps), "device_idle_between_rounds_ms_mean": mean(gaps),
             "device_idle_between_rounds_ms_max": round(max(gaps), 4) if gaps else None,
-            "wall_ms_per_round": round((t1 - t0) / steps * 1e3, 4), "rounds": len(marks)}
+            "wall_ms_per_round": round((t1 - t0) / steps * 1e3, 4), "rounds": len(marks),
+            "device_round_span_ms_each": [round(v, 3) for v in span],
+            "device_train_ms_each": [round(v, 3) for v in dev[phases[0]]] if phases else []}
 
 
 def make_transport(args, trainer, rank: int, world: int, rehearse: bool, device):
@@ -166,7 +168,11 @@ def main() -> int:
                     help="N>1: skip the second timed loop that measures the split-eval round")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--ckpt-dir", default=None)
-    ap.add_argument("--ckpt-slots", type=int, default=4, help="pinned snapshot slots of the checkpoint writer")
+    # 2 slots: the writer takes 0.22 ms per LeNet round (profiles/r6_lenet/ckpt_write_probe.jsonl), so 2 keep it off
+    # the critical path at every N; with 4 the host ran 4 rounds ahead and timed rounds 2-4 after a 3-round warmup
+    # trained ~0.9 ms slower (16 slots: every round; 1-2 slots or a 10-round warmup: none) -- 107.8 vs 109.2
+    # rounds/s (profiles/r6_lenet/slots.md)
+    ap.add_argument("--ckpt-slots", type=int, default=2, help="pinned snapshot slots of the checkpoint writer")
     ap.add_argument("--ckpt-coalesce", action="store_true",
                     help="a writer that falls behind by --ckpt-slots rounds supersedes queued rounds (files "
                          "still end at the newest round) instead of stalling the round loop")
