@@ -1471,6 +1471,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_multi(const WredTable t) {
 // accumulates the BatchNorm batch statistics (sum / sum of squares of
 // bf16(y) - shift[c]) like the single-pass epilogue.  Each thread owns one
 // 8-channel group (two 16-B loads per split) of rows r0, r0 + rstep, ...
+// rows per thread per pass x splits' loads in flight per step (2: ResNet-18 814-816 vs 816-822 ms per round,
+// GoogLeNet 3322 vs 3325-3338, MobileNet 643 vs 645-648; same VGPR count -- profiles/r6_cnn/splitk_z2/)
+#ifndef SPLITK_U
+#define SPLITK_U 4
+#endif
+#ifndef SPLITK_Z
+#define SPLITK_Z 2
+#endif
 __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restrict__ ws, int splits, int M, int NC,
                                                           RowMap rmap, bf16* __restrict__ out,
                                                           double* __restrict__ stats, const float* __restrict__ shift,
@@ -1489,7 +1497,7 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restric
   const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
   // U rows per thread per pass, every load of the pass issued before the first use (the partials of all
   // splits, the residual / second grad, the BN-sums operands): one memory latency per U rows
-  constexpr int U = 4;
+  constexpr int U = SPLITK_U;
   for (int m0 = rb + r0; m0 < re; m0 += U * rstep) {
     float v[U][8];
     bf16x8 rr[U], pz[U], py[U], pzb[U];
@@ -1506,19 +1514,26 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const float* __restric
       v[u][0] = a.x; v[u][1] = a.y; v[u][2] = a.z; v[u][3] = a.w;
       v[u][4] = b.x; v[u][5] = b.y; v[u][6] = b.z; v[u][7] = b.w;
     }
-    for (int z = 1; z < splits; ++z) {
-      float4 ua[U], ub[U];
+    // SPLITK_Z splits' loads in flight per step (the adds stay in split order: bit-identical for any SPLITK_Z)
+    for (int z = 1; z < splits; z += SPLITK_Z) {
+      float4 ua[SPLITK_Z][U], ub[SPLITK_Z][U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int mm = ok[u] ? m0 + u * rstep : rb + r0;
-        const float* p = ws + (long)mm * NC + c0 + z * plane;
-        ua[u] = *reinterpret_cast<const float4*>(p);
-        ub[u] = *reinterpret_cast<const float4*>(p + 4);
-      }
+      for (int q = 0; q < SPLITK_Z; ++q)
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        v[u][0] += ua[u].x; v[u][1] += ua[u].y; v[u][2] += ua[u].z; v[u][3] += ua[u].w;
-        v[u][4] += ub[u].x; v[u][5] += ub[u].y; v[u][6] += ub[u].z; v[u][7] += ub[u].w;
+        for (int u = 0; u < U; ++u) {
+          const int mm = ok[u] ? m0 + u * rstep : rb + r0;
+          const float* p = ws + (long)mm * NC + c0 + (long)min(z + q, splits - 1) * plane;
+          ua[q][u] = *reinterpret_cast<const float4*>(p);
+          ub[q][u] = *reinterpret_cast<const float4*>(p + 4);
+        }
+#pragma unroll
+      for (int q = 0; q < SPLITK_Z; ++q) {
+        if (z + q >= splits) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          v[u][0] += ua[q][u].x; v[u][1] += ua[q][u].y; v[u][2] += ua[q][u].z; v[u][3] += ua[q][u].w;
+          v[u][4] += ub[q][u].x; v[u][5] += ub[q][u].y; v[u][6] += ub[q][u].z; v[u][7] += ub[q][u].w;
+        }
       }
     }
     if (res != nullptr) {
