@@ -934,11 +934,14 @@ FEDMI_DEV void vm_wait_le(int n) {
 // to ws[split][o][(r, s, c)] -- the generic WGRAD's layout, so its reduce kernels
 // sum the splits and permute into [O][Cw][3][3].
 // ---------------------------------------------------------------------------
-template <int PP>
+// KR = 1: the same kernel for a 1x1 / stride-1 conv -- the "patch" is the block's own 128 pixel rows (no halo,
+// one tap), dW[o][c] = sum_m dY[m][o] X[m][c]: a plain GEMM over the pixels with both operands pixel-major.
+template <int PP, int KR = 3>
 __global__ __launch_bounds__(256) void conv_wgrad_halo(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                        float* __restrict__ ws, HaloGeom g, int blocks_per_split) {
-  constexpr int PCAP = PP == 1 ? 208 : 288;
-  constexpr int NPS = 7 * PP;             // patch wave-instructions per block per wave
+  constexpr int TAPS = KR * KR;
+  constexpr int PCAP = KR == 1 ? 128 : PP == 1 ? 208 : 288;
+  constexpr int NPS = KR == 1 ? 4 : 7 * PP;   // patch wave-instructions per block per wave
   constexpr int DYE = 128 * 64;           // dY stage elements
   constexpr int PTE = PCAP * 64;          // patch stage elements
   constexpr int NST = 3;
@@ -974,9 +977,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo(const bf16* __restrict__ 
 #pragma unroll
   for (int q = 0; q < NPS; ++q) {
     const int pr = (q * 4 + wave) * 8 + lr;
-    const int i = fdiv(pr, g.dPI), rem = pr - i * per_img;
-    const int hh = fdiv(rem, g.dPW), ww = rem - hh * g.PW;
-    pk[q] = pr < g.NPR ? (i << 16) | (hh << 8) | ww : -1;
+    if constexpr (KR == 1) {
+      pk[q] = pr;                                  // the block's pixel row (NPS * 32 == 128)
+    } else {
+      const int i = fdiv(pr, g.dPI), rem = pr - i * per_img;
+      const int hh = fdiv(rem, g.dPW), ww = rem - hh * g.PW;
+      pk[q] = pr < g.NPR ? (i << 16) | (hh << 8) | ww : -1;
+    }
   }
   auto issue = [&](int b, int stage) {
     bf16* Ds = smem + stage * (DYE + PTE);
@@ -985,15 +992,23 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo(const bf16* __restrict__ 
 #pragma unroll
     for (int u = 0; u < 4; ++u) glds16(dy + mb * g.O + dyo[u], Ds + (u * 4 + wave) * 512);
     const int m0 = b * 128;
-    const int img0 = fdiv(m0, g.dHW), h0 = fdiv(m0 - img0 * HW, g.dW);
+    if constexpr (KR == 1) {
 #pragma unroll
-    for (int q = 0; q < NPS; ++q) {
-      const int base = (q * 4 + wave) * 8;
-      const int n = img0 + (pk[q] >> 16), h = h0 + ((pk[q] >> 8) & 255) - 1, w = (pk[q] & 255) - 1;
-      const bool ok = pk[q] >= 0 && n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-      const void* src = ok ? (const void*)(x + (((long)n * g.H + h) * g.W + w) * g.C + c0 + lcol(base + lr))
-                           : (const void*)g_zero16;
-      glds16(src, base < PCAP ? Ps + base * 64 : dummy);
+      for (int q = 0; q < NPS; ++q) {
+        const int base = (q * 4 + wave) * 8;
+        glds16(x + ((long)m0 + pk[q]) * g.C + c0 + lcol(base + lr), Ps + base * 64);
+      }
+    } else {
+      const int img0 = fdiv(m0, g.dHW), h0 = fdiv(m0 - img0 * HW, g.dW);
+#pragma unroll
+      for (int q = 0; q < NPS; ++q) {
+        const int base = (q * 4 + wave) * 8;
+        const int n = img0 + (pk[q] >> 16), h = h0 + ((pk[q] >> 8) & 255) - 1, w = (pk[q] & 255) - 1;
+        const bool ok = pk[q] >= 0 && n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+        const void* src = ok ? (const void*)(x + (((long)n * g.H + h) * g.W + w) * g.C + c0 + lcol(base + lr))
+                             : (const void*)g_zero16;
+        glds16(src, base < PCAP ? Ps + base * 64 : dummy);
+      }
     }
   };
 
@@ -1005,7 +1020,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo(const bf16* __restrict__ 
   // q4 = (lane & 15) >> 2, p4 = lane & 3; rows kk * 32 + 8 g4 + q4 and + 4; columns col0 + 4 p4.
   const int g4 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
   int aoff[4][4][2];        // [kk][o block][row half] in the dY image
-  int boff[4][9][2];        // [kk][tap][row half] in the patch image
+  int boff[4][TAPS][2];     // [kk][tap][row half] in the patch image
   const int thw = g.TH * g.W;
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk)
@@ -1014,12 +1029,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo(const bf16* __restrict__ 
       const int k = kk * 32 + 8 * g4 + q4 + 4 * h2;        // pixel of the block
 #pragma unroll
       for (int i = 0; i < 4; ++i) aoff[kk][i][h2] = mnc_off<64>(k, 16 * i + 4 * p4);
-      const int im = fdiv(k, g.dTHW), rem = k - im * thw;
-      const int pp = fdiv(rem, g.dW), qq = rem - pp * g.W;
-      const int prow = (im * (g.TH + 2) + pp) * g.PW + qq;  // patch row at tap (0, 0)
+      if constexpr (KR == 1) {
+        boff[kk][0][h2] = mnc_off<64>(k, wave * 16 + 4 * p4);
+      } else {
+        const int im = fdiv(k, g.dTHW), rem = k - im * thw;
+        const int pp = fdiv(rem, g.dW), qq = rem - pp * g.W;
+        const int prow = (im * (g.TH + 2) + pp) * g.PW + qq;  // patch row at tap (0, 0)
 #pragma unroll
-      for (int t = 0; t < 9; ++t)
-        boff[kk][t][h2] = mnc_off<64>(prow + (t / 3) * g.PW + (t % 3), wave * 16 + 4 * p4);
+        for (int t = 0; t < 9; ++t)
+          boff[kk][t][h2] = mnc_off<64>(prow + (t / 3) * g.PW + (t % 3), wave * 16 + 4 * p4);
+      }
     }
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
   auto tr = [&](const bf16* base, int o0_, int o1_) {
@@ -1030,11 +1049,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo(const bf16* __restrict__ 
     return (bf16x8)__builtin_shufflevector(l4, h4, 0, 1, 2, 3, 4, 5, 6, 7);
   };
 
-  f32x4 acc[4][9];
+  f32x4 acc[4][TAPS];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) acc[i][t] = zero4();
+    for (int t = 0; t < TAPS; ++t) acc[i][t] = zero4();
 
   constexpr int GRP = 4 + NPS;            // DMA instructions per block per wave
   auto step = [&](int it, auto stg) {
@@ -1053,7 +1072,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo(const bf16* __restrict__ 
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = tr(Ds, aoff[kk][i][0], aoff[kk][i][1]);
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
+      for (int t = 0; t < TAPS; ++t) {
         const bf16x8 bfr = tr(Ps, boff[kk][t][0], boff[kk][t][1]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][t] = mfma16(af[i], bfr, acc[i][t]);
@@ -1072,9 +1091,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo(const bf16* __restrict__ 
   // values of a column as one 16-B LDS write into a [576 col][32 o (+1 pad)] tile, then each thread
   // gathers 4 consecutive columns of one o and stores them as a float4.
   constexpr int TLD = 33;
-  float* tile = reinterpret_cast<float*>(smem);    // 576 x 33 floats = 76 KB
+  float* tile = reinterpret_cast<float*>(smem);    // (TAPS * 64) x 33 floats (76 KB at 9 taps)
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
-  const long NC = 9l * g.C;
+  const long NC = (long)TAPS * g.C;
   float* wsp = ws + (long)blockIdx.z * g.O * NC;
   __syncthreads();
 #pragma unroll
@@ -1083,16 +1102,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo(const bf16* __restrict__ 
     for (int ii = 0; ii < 2; ++ii) {
       const int i = 2 * half + ii;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
+      for (int t = 0; t < TAPS; ++t) {
         const int col = t * 64 + wave * 16 + col_l;     // column within the tile (tap, c)
         float* d = tile + col * TLD + 16 * ii + row_l;
         d[0] = acc[i][t][0]; d[1] = acc[i][t][1]; d[2] = acc[i][t][2]; d[3] = acc[i][t][3];
       }
     }
     __syncthreads();
-    // 32 o x 144 column quads
-    for (int idx = tid; idx < 32 * 144; idx += 256) {
-      const int ol = idx / 144, cq = idx - ol * 144;
+    // 32 o x (16 * TAPS) column quads
+    for (int idx = tid; idx < 32 * 16 * TAPS; idx += 256) {
+      const int ol = idx / (16 * TAPS), cq = idx - ol * (16 * TAPS);
       const int col = cq * 4;
       float4 v;
       v.x = tile[(col + 0) * TLD + ol];
@@ -2280,7 +2299,28 @@ long conv_fd_ws_floats(const ConvShape& s) {
 
 // conv_wgrad_halo applies to 3x3 / stride 1 / pad 1 with C and O % 64 and 128-pixel blocks; every other
 // shape takes the generic WGRAD (split-K conv_igemm).
+static bool wgrad_1x1_enabled() {   // FEDMI_WGRAD_1X1=0: 1x1 WGRADs on the generic split-K kernel (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("FEDMI_WGRAD_1X1");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 static bool wgrad_halo_geom(const ConvShape& s, HaloGeom* h) {
+  if (s.R == 1 && s.S == 1 && s.st == 1 && s.pad == 0 && s.C % 64 == 0 && s.O % 64 == 0 && wgrad_1x1_enabled()) {
+    // 1x1 / stride 1: conv_wgrad_halo<1, 1> over 128-pixel blocks (K = C marks the one-tap form).  Its 64 x 64
+    // tiles re-read each operand chunk twice as often as the generic kernel's 128 x 128 ones, which the L2 absorbs
+    // only for small problems: 1.3-2x faster at MobileNet's 16x16 / 8x8 pointwise shapes, 7-65 % slower from
+    // M * (C + O) ~ 2e7 on (GoogLeNet 32x32 256 -> 128, 16x16 512 -> 192, 8x8 832 -> 256;
+    // profiles/r6_cnn/wgrad1x1_halo/)
+    const long M = (long)s.N * s.H * s.W;
+    if (M % 128 || M >= (1l << 31) || M * (s.C + s.O) > 3l * (1l << 22)) return false;
+    HaloGeom x{};
+    x.N = s.N; x.H = s.H; x.W = s.W; x.C = s.C; x.O = s.O; x.M = (int)M; x.K = s.C;
+    x.NPR = 128; x.nchunks = s.C / 64;
+    *h = x;
+    return true;
+  }
   if (s.R != 3 || s.S != 3 || s.st != 1 || s.pad != 1 || s.C % 64 || s.O % 64) return false;
   const TapGeom t = make_tap(s.N, s.H, s.W, s.C, s.O, s.P, s.Q, 3, 3, 1, 1, 1);
   // the 288-row window (4x4 images) would spill the per-lane fragment offset tables: generic path
@@ -2295,7 +2335,7 @@ static int wgrad_halo_splits(const HaloGeom& h, long ws_cap_floats) {
   const int nblk = h.M / 128;
   long sp = std::max<long>(1, (want + tiles / 2) / tiles);
   sp = std::min<long>(sp, nblk);
-  if (ws_cap_floats > 0) sp = std::min<long>(sp, ws_cap_floats / ((long)h.O * 9 * h.C));
+  if (ws_cap_floats > 0) sp = std::min<long>(sp, ws_cap_floats / ((long)h.O * h.K));   // K = taps * C
   sp = std::max<long>(1, sp);
   const int bps = (int)((nblk + sp - 1) / sp);
   return (nblk + bps - 1) / bps;
@@ -2329,7 +2369,10 @@ void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const 
     const int nblk = h.M / 128;
     const int bps = (nblk + splits - 1) / splits;
     dim3 grid((unsigned)((h.O / 64) * h.nchunks), 1, (unsigned)splits);
-    hipLaunchKernelGGL(conv_wgrad_halo<1>, grid, dim3(256), 0, st, x, dy, ws, h, bps);
+    if (h.K == h.C)
+      hipLaunchKernelGGL((conv_wgrad_halo<1, 1>), grid, dim3(256), 0, st, x, dy, ws, h, bps);
+    else
+      hipLaunchKernelGGL(conv_wgrad_halo<1>, grid, dim3(256), 0, st, x, dy, ws, h, bps);
   } else {
     if (splits <= 0) splits = wgrad_splits(g, ws_floats);
     const int ksteps = (g.K + BK - 1) / BK;
