@@ -41,7 +41,7 @@ struct PackItem {
 };
 void launch_conv_pack_multi(hipStream_t, const PackItem*, int);
 void launch_conv_wgrad(hipStream_t, const ConvShape&, const bf16*, const bf16*, float*, float*, long, int, int, int, int,
-                       WredItem*);
+                       WredItem*, int);
 long conv_wgrad_ws_floats(const ConvShape&);
 void launch_conv_pack(hipStream_t, const float*, bf16*, int, int, int, int, int, int);
 struct SgdPackConv {
@@ -241,14 +241,15 @@ void fedmi_bind_cnn(py::module_& m) {
   });
   // defer != 0: the partial reduction is not launched; its descriptor comes back (wred_tuple) for wgrad_reduce_multi
   m.def("conv_wgrad", [](uintptr_t st, const py::tuple& shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws,
-                         long ws_floats, int splits, int accumulate, int Ow, int G, int defer) -> py::object {
+                         long ws_floats, int splits, int accumulate, int Ow, int G, int defer, int allow_1x1) -> py::object {
     WredItem it{};
     launch_conv_wgrad(S(st), shape_from(shp), P<const bf16>(x), P<const bf16>(dy), P<float>(dw), P<float>(ws),
-                      ws_floats, splits, accumulate, Ow, G, defer ? &it : nullptr);
+                      ws_floats, splits, accumulate, Ow, G, defer ? &it : nullptr, allow_1x1);
     check("conv_wgrad");
     return defer ? wred_tuple(it) : py::object(py::none());
   }, py::arg("st"), py::arg("shp"), py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ws"), py::arg("ws_floats"),
-     py::arg("splits"), py::arg("accumulate"), py::arg("Ow") = 0, py::arg("G") = 1, py::arg("defer") = 0);
+     py::arg("splits"), py::arg("accumulate"), py::arg("Ow") = 0, py::arg("G") = 1, py::arg("defer") = 0,
+     py::arg("allow_1x1") = 1);
   m.def("wgrad_reduce_multi", [](uintptr_t st, const py::list& items) {
     std::vector<WredItem> v;
     for (const auto& o : items) v.push_back(wred_from(o.cast<py::tuple>()));

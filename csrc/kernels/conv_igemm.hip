@@ -2306,8 +2306,9 @@ static bool wgrad_1x1_enabled() {   // FEDMI_WGRAD_1X1=0: 1x1 WGRADs on the gene
   }();
   return on;
 }
-static bool wgrad_halo_geom(const ConvShape& s, HaloGeom* h) {
-  if (s.R == 1 && s.S == 1 && s.st == 1 && s.pad == 0 && s.C % 64 == 0 && s.O % 64 == 0 && wgrad_1x1_enabled()) {
+static bool wgrad_halo_geom(const ConvShape& s, HaloGeom* h, bool allow_1x1 = true) {
+  if (allow_1x1 && s.R == 1 && s.S == 1 && s.st == 1 && s.pad == 0 && s.C % 64 == 0 && s.O % 64 == 0 &&
+      wgrad_1x1_enabled()) {
     // 1x1 / stride 1: conv_wgrad_halo<1, 1> over 128-pixel blocks (K = C marks the one-tap form).  Its 64 x 64
     // tiles re-read each operand chunk twice as often as the generic kernel's 128 x 128 ones, which the L2 absorbs
     // only for small problems: 1.3-2x faster at MobileNet's 16x16 / 8x8 pointwise shapes, 7-65 % slower from
@@ -2354,8 +2355,9 @@ long conv_wgrad_ws_floats(const ConvShape& s) {
 // dw: [Ow][Cw][R][S] (Ow <= 0: O) -- the first Ow filters of an O-padded conv land in the unpadded gradient.
 // G > 1: a grouped conv run densely with a block-diagonal weight image; filter o keeps only its group's Cw
 // channels of the dense gradient.
+// allow_1x1 = 0: no conv_wgrad_halo<1, 1> route (the aten backend: mixed results across the zoo families)
 void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const bf16* dy, float* dw, float* ws,
-                       long ws_floats, int splits, int accumulate, int Ow, int G, WredItem* defer) {
+                       long ws_floats, int splits, int accumulate, int Ow, int G, WredItem* defer, int allow_1x1) {
   if (Ow <= 0 || Ow > s.O) Ow = s.O;
   if (G < 1) G = 1;
   if (G > 1 && (s.O % G || s.C < G * s.Cw || Ow != s.O))
@@ -2364,7 +2366,7 @@ void launch_conv_wgrad(hipStream_t st, const ConvShape& s, const bf16* x, const 
   const long plane = (long)g.M * g.NC;
   if (ws_floats < plane) throw std::invalid_argument("conv_wgrad: workspace smaller than one O x RSC plane");
   HaloGeom h;
-  if (splits <= 0 && wgrad_halo_geom(s, &h)) {
+  if (splits <= 0 && wgrad_halo_geom(s, &h, allow_1x1 != 0)) {
     splits = wgrad_halo_splits(h, ws_floats);
     const int nblk = h.M / 128;
     const int bps = (nblk + splits - 1) / splits;

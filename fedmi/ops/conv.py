@@ -332,7 +332,8 @@ def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int,
     """dW fp32 [O, Cw, R, S] (PyTorch layout).  ``accumulate`` adds into ``out`` instead of overwriting.
     ``deferred`` (a list): the split-K reduction is not launched but appended as a descriptor, for ONE
     :func:`wgrad_reduce_multi` launch after the backward pass -- ``ws`` must then stay untouched until that launch
-    (``out`` is not written before it).  ``lib_gemm`` False: never the library GEMM route (WGRAD_GEMM_PIXELS).
+    (``out`` is not written before it).  ``lib_gemm`` False: neither the library GEMM route (WGRAD_GEMM_PIXELS) nor
+    the 1x1 halo-kernel route (the CNN engine's; the aten backend keeps the generic kernel).
     ``Ow`` < O: dy carries zero-padded filters; only the first Ow land in ``out`` ([Ow, Cw, R, S]).
     ``groups`` > 1: a grouped conv run densely (block-diagonal image): filter o keeps its group's Cw channels.
 
@@ -369,7 +370,8 @@ def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int,
         need = max(nat.conv_wgrad_ws_floats(shp), splits * O * R * S * shp[3])
         ws = wgrad_workspace(x.device, need)
     item = nat.conv_wgrad(native.stream_handle(x.device), shp, x.data_ptr(), dy.data_ptr(), out.data_ptr(),
-                          ws.data_ptr(), ws.numel(), splits, int(accumulate), Ow, int(groups), int(deferred is not None))
+                          ws.data_ptr(), ws.numel(), splits, int(accumulate), Ow, int(groups), int(deferred is not None),
+                          int(lib_gemm))
     if item is not None:
         deferred.append(item)
     return out

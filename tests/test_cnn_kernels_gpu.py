@@ -149,16 +149,21 @@ def test_conv_wgrad_1x1_library_route(gpu_device, shape, monkeypatch):
 
 @pytest.mark.parametrize("shape", [(8, 16, 16, 64, 128), (4, 32, 32, 192, 64), (16, 8, 8, 256, 256), (2, 8, 8, 128, 64),
                                    (128, 8, 8, 832, 256)])
-def test_conv_wgrad_1x1_halo_kernel(gpu_device, shape):
-    """1x1 / stride-1 WGRAD with C, O % 64 over > 2048 pixels runs on conv_wgrad_halo<1, 1> (the block's own pixel
-    rows as the one-tap patch); against fp32, and split-count invariant."""
+def test_conv_wgrad_1x1_halo_kernel(gpu_device, shape, monkeypatch):
+    """1x1 / stride-1 WGRAD with C, O % 64 (M (C + O) <= 12.6 M) runs on conv_wgrad_halo<1, 1> (the block's own
+    pixel rows as the one-tap patch); against fp32 and the generic kernel (explicit splits, and lib_gemm=False --
+    the aten backend's route -- both take it)."""
     N, H, W, C, O = shape
     torch.manual_seed(13)
     xn = torch.randn(N, H, W, C, device=gpu_device).bfloat16()
     dy = torch.randn(N, H, W, O, device=gpu_device).bfloat16()
     ref = (dy.float().view(-1, O).t() @ xn.float().view(-1, C)).view(O, C, 1, 1)
-    dw = conv.conv2d_wgrad(xn, dy, 1, 1, 1, 0, lib_gemm=False)
-    dw1 = conv.conv2d_wgrad(xn, dy, 1, 1, 1, 0, lib_gemm=False, splits=1)   # explicit splits: generic kernel
+    monkeypatch.setattr(conv, "WGRAD_GEMM_PIXELS", 0)                         # no library route at small M
+    dw = conv.conv2d_wgrad(xn, dy, 1, 1, 1, 0)
+    dw1 = conv.conv2d_wgrad(xn, dy, 1, 1, 1, 0, splits=1)                     # explicit splits: generic kernel
+    dw2 = conv.conv2d_wgrad(xn, dy, 1, 1, 1, 0, lib_gemm=False)               # generic, automatic splits
+    torch.cuda.synchronize()
+    assert _rel(dw2, ref) < 1e-4
     torch.cuda.synchronize()
     assert _rel(dw, ref) < 1e-4 and _rel(dw1, ref) < 1e-4
     assert _rel(dw, dw1) < 1e-4

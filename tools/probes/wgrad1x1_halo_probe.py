@@ -26,6 +26,7 @@ SHAPES = [(16, 64, 128), (16, 128, 128), (8, 128, 256), (8, 256, 256),
 def main():
     dev = torch.device("cuda:0")
     mode = os.environ.get("FEDMI_WGRAD_1X1", "1")
+    conv.WGRAD_GEMM_PIXELS = 0          # CNN-engine routing (lib_gemm=True) minus the small-M library GEMM
     for H, C, O in SHAPES:
         if C % 64 or O % 64:
             continue
@@ -36,7 +37,7 @@ def main():
         dw = torch.empty(O, C, 1, 1, device=dev)
 
         def run():
-            conv.conv2d_wgrad(x, dy, 1, 1, 1, 0, out=dw, ws=ws, lib_gemm=False)
+            conv.conv2d_wgrad(x, dy, 1, 1, 1, 0, out=dw, ws=ws)
         print(json.dumps({"H": H, "C": C, "O": O, "halo1": mode, "us": round(timed(run), 2),
                           "splits": ws.numel() // (O * C)}), flush=True)
 
