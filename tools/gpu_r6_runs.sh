@@ -452,6 +452,16 @@ case "$run" in
     rm -f $(find $out/lenet -name 'run_kernel_trace.csv')
     cat $out/lenet_kernels.txt | head -20
     ;;
+  final)
+    # round 6: headline + CNN benches at the final HEAD (LeNet x2, ResNet-18, MobileNet, MobileNetV2, GoogLeNet)
+    bash tools/gpu_steps.sh r6_final \
+      lenet1 200 "python -u bench.py --json-out gpurun_out/r6_final/lenet1.json" \
+      lenet2 200 "python -u bench.py --json-out gpurun_out/r6_final/lenet2.json" \
+      r18 200 "python -u bench.py --model resnet18 --steps 3 --warmup 1 --json-out gpurun_out/r6_final/resnet18.json" \
+      mbn 200 "python -u bench.py --model mobilenet --steps 3 --warmup 1 --json-out gpurun_out/r6_final/mobilenet.json" \
+      mbv2 200 "python -u bench.py --model mobilenetv2 --steps 3 --warmup 1 --json-out gpurun_out/r6_final/mobilenetv2.json" \
+      goog 250 "python -u bench.py --model googlenet --steps 3 --warmup 1 --json-out gpurun_out/r6_final/googlenet.json"
+    ;;
   list) awk '/^  [a-z]+\)$/ {n=$1; getline; sub(/^ *# round 6: /, ""); print n, $0}' "$0" ;;
   *) echo "unknown run: $run (try: list)" >&2; exit 2 ;;
 esac
