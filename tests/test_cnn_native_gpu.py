@@ -134,7 +134,14 @@ def test_deferred_wgrad_reductions_are_bit_identical(gpu_device, name, monkeypat
 # chaotic at init (torch-bf16 vs fp32 mean cos 0.48 there, min -0.25) -- a single tensor's cosine is noise
 # (two runs of the diagnostic put the worst gap on different tensors, -0.29 and -0.44), so the bound is on
 # the group: native's mean within 0.05 of torch-bf16's, and no tensor more than 0.6 below it.
+# STRUCTURAL ZEROS are left out of every cosine: a BN bias whose output reaches the loss only through train-mode
+# BNs (MobileNetV2's every bn3.bias / shortcut.1.bias) has an exactly-zero gradient -- fp64 RMS ~1e-18 against a
+# median tensor's 1.8e-3, fp32 1e-10..1e-7 of pure rounding -- so its cosine to fp32 is a coin flip for any
+# engine (native -0.69 vs torch-bf16 0.12 on layers.0.bn3.bias in one run).  They are found with an fp64 CPU
+# reference; instead of a cosine, the native rounding residue on them (group RMS) must stay within
+# STRUCT_ZERO_VS_BF16 of torch-bf16's. (measured: 21 tensors, native 1.6e-4 vs torch-bf16 2.4e-4 vs fp32 1.1e-7).
 WELL_COND, WELL_MARGIN, ILL_MEAN_MARGIN, ILL_MAX_GAP = 0.9, 0.05, 0.05, 0.6
+STRUCT_ZERO_REL, STRUCT_ZERO_VS_BF16 = 1e-9, 2.0
 
 
 @pytest.mark.parametrize("name", ["ResNet18", "MobileNetV2"])
@@ -173,8 +180,21 @@ def test_native_gradients_track_torch_bf16(gpu_device, name):
             loss = F.cross_entropy(ref(x), y)
         loss.backward()
         grads[kind] = {k: p.grad.detach().float().clone() for k, p in ref.named_parameters()}
+    ref64 = build_model(name).double()
+    ref64.load_state_dict(init)
+    ref64.train()
+    F.cross_entropy(ref64(x.double().cpu()), y.cpu()).backward()
+    rms64 = {k: p.grad.pow(2).mean().sqrt().item() for k, p in ref64.named_parameters()}
+    med = sorted(rms64.values())[len(rms64) // 2]
+    zero = [k for k in rms64 if rms64[k] < STRUCT_ZERO_REL * med]
+    assert len(zero) <= (0 if name == "ResNet18" else 40), zero
+    if zero:
+        res = {kind: (sum(grads[kind][k].pow(2).mean().item() for k in zero) / len(zero)) ** 0.5
+               for kind in ("native", "bf16", "fp32")}
+        print(f"structural zeros: {len(zero)} tensors, residue RMS {res} (median tensor RMS {med:.3e})")
+        assert res["native"] < STRUCT_ZERO_VS_BF16 * res["bf16"], res
     assert abs(stats["native"].loss - stats["emulated"].loss) < 5e-3 * stats["emulated"].loss
-    names = list(grads["native"])
+    names = [k for k in grads["native"] if k not in zero]
     cn = {k: _cos(grads["native"][k], grads["fp32"][k]) for k in names}
     cb = {k: _cos(grads["bf16"][k], grads["fp32"][k]) for k in names}
     well = [k for k in names if cb[k] >= WELL_COND]

@@ -462,6 +462,48 @@ case "$run" in
       mbv2 200 "python -u bench.py --model mobilenetv2 --steps 3 --warmup 1 --json-out gpurun_out/r6_final/mobilenetv2.json" \
       goog 250 "python -u bench.py --model googlenet --steps 3 --warmup 1 --json-out gpurun_out/r6_final/googlenet.json"
     ;;
+  kfinal)
+    # round 6: kernel breakdowns at the final HEAD (MobileNet / MobileNetV2 with the 1x1 halo WGRAD, ResNet-18)
+    set -e
+    export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+    out=gpurun_out/r6_kfinal
+    mkdir -p $out
+    for m in mobilenet mobilenetv2 resnet18; do
+      timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $out/$m -o run -- python3 bench.py --model $m --steps 1 --warmup 1 > $out/${m}_bench.log 2>&1
+      tr=$(find $out/$m -name 'run_kernel_trace.csv' | head -n 1)
+      st=$(find $out/$m -name 'run_kernel_stats.csv' | head -n 1)
+      python3 tools/prof_summary.py "$st" sched_next 40 > $out/${m}_kernels.txt
+      python3 tools/prof_step.py "$tr" 300 > $out/${m}_step.txt
+      rm -f "$tr"
+      tail -n 2 $out/${m}_step.txt
+    done
+    ;;
+  au)
+    # round 6: MobileNet 4x4 / 2x2 1x1 WGRADs -- library GEMM vs conv_wgrad_halo<1, 1> vs generic, per shape
+    bash tools/gpu_steps.sh r6_au \
+      lib 200 "python -u tools/probes/wgrad1x1_halo_probe.py --lib" \
+      halo 200 "python -u tools/probes/wgrad1x1_halo_probe.py" \
+      gen 200 "env FEDMI_WGRAD_1X1=0 python -u tools/probes/wgrad1x1_halo_probe.py"
+    ;;
+  av)
+    # round 6: halo1-eligible 4x4 1x1 WGRADs off the library GEMM (WGRAD_GEMM_PIXELS_HALO 512) -- tests + MobileNet A/B
+    bash tools/gpu_steps.sh r6_av \
+      kern 300 "python -u -m pytest tests/test_cnn_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k 'wgrad_1x1'" \
+      eng 400 "python -u -m pytest tests/test_kernel_list_gpu.py tests/test_cnn_native_gpu.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k 'launches or mobilenet or deferred'" \
+      mbn1 200 "python -u bench.py --model mobilenet --steps 3 --warmup 1 --json-out gpurun_out/r6_av/mbn1.json" \
+      mbn_lib 200 "python -u -c 'import sys; import fedmi.ops.conv as c; c.WGRAD_GEMM_PIXELS_HALO = 2048; sys.argv = [\"bench.py\", \"--model\", \"mobilenet\", \"--steps\", \"3\", \"--warmup\", \"1\", \"--json-out\", \"gpurun_out/r6_av/mbn_lib.json\"]; import runpy; runpy.run_path(\"bench.py\", run_name=\"__main__\")'" \
+      mbn2 200 "python -u bench.py --model mobilenet --steps 3 --warmup 1 --json-out gpurun_out/r6_av/mbn2.json"
+    ;;
+  aw)
+    # round 6: which MobileNetV2 gradients change when its 4x4 1x1 WGRADs leave the library GEMM (test failure in av)
+    bash tools/gpu_steps.sh r6_aw \
+      diff 200 "python -u tools/probes/halo_lib_grad_diff.py MobileNetV2"
+    ;;
+  ax)
+    # round 6: structural-zero gradients in the MobileNetV2 tracking test (residue vs torch-bf16), then the av A/B
+    bash tools/gpu_steps.sh r6_ax \
+      track 300 "python -u -m pytest tests/test_cnn_native_gpu.py -x -q -s --timeout 300 --timeout-method thread -p no:cacheprovider -k 'track'"
+    ;;
   list) awk '/^  [a-z]+\)$/ {n=$1; getline; sub(/^ *# round 6: /, ""); print n, $0}' "$0" ;;
   *) echo "unknown run: $run (try: list)" >&2; exit 2 ;;
 esac
