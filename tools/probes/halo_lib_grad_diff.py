@@ -1,6 +1,7 @@
-"""Probe: one MobileNetV2 step's gradients (nb = 64, the gradient-tracking test's setup) with the 4x4 1x1 WGRADs on
-the library GEMM (WGRAD_GEMM_PIXELS_HALO = 2048) vs conv_wgrad_halo<1, 1> (= 512): which tensors differ.  Only the
-routed convs' weight gradients may.
+"""Probe: one MobileNetV2 step's gradients (nb = 64, the gradient-tracking test's setup) with the small 1x1 WGRADs
+on the library GEMM (conv.WGRAD_GEMM_PIXELS = 2048) vs the native kernels (= 0): which tensors differ, and is each
+route bit-stable run to run.  Only the routed convs' weight gradients may differ.  (Round 6 ran it against a
+since-reverted 512-pixel library threshold for halo-eligible shapes: profiles/r6_cnn/wgrad1x1_halo/small_shapes/.)
 
     python tools/probes/halo_lib_grad_diff.py [model]
 """
@@ -25,8 +26,8 @@ def main():
     torch.manual_seed(0)
     init = build_model(name).state_dict()
     grads = {}
-    for halo in (2048, 512, 512, 2048):
-        conv.WGRAD_GEMM_PIXELS_HALO = halo
+    for halo in (2048, 0, 0, 2048):
+        conv.WGRAD_GEMM_PIXELS = halo
         tr = CNNNativeTrainer(name, data, dev, TrainerConfig(batch_size=64, augment=False, use_graph=False),
                               init_state=init)
         tr.grads_for_batch(0, 64)
@@ -37,7 +38,7 @@ def main():
             print(f"halo={halo} rerun: {len(same)} tensors differ from the first run {same[:6]}", flush=True)
         else:
             grads[halo] = g
-    a, b = grads[2048], grads[512]
+    a, b = grads[2048], grads[0]
     for k in a:
         if not torch.equal(a[k], b[k]):
             d = (a[k] - b[k]).abs().max().item()
