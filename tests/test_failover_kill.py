@@ -46,7 +46,12 @@ def _report(**rec):
 
 
 def _keep_logs(tmp_path, tag):
-    """On failure, copy the drill's logs next to FEDMI_FAILOVER_REPORT (read back from the GPU box)."""
+    """On failure, copy the drill's logs next to FEDMI_FAILOVER_REPORT (read back from the GPU box), and print each
+    client log's tail into the captured output (a suite run without the report path still records them)."""
+    for f in sorted(tmp_path.glob("client*.log")):
+        lines = f.read_text(errors="replace").splitlines()
+        print(f"----- {tag}: {f.name} (last 15 of {len(lines)} lines)")
+        print("\n".join(lines[-15:]))
     path = os.environ.get("FEDMI_FAILOVER_REPORT")
     if path:
         import shutil
