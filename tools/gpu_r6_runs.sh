@@ -504,6 +504,11 @@ case "$run" in
     bash tools/gpu_steps.sh r6_ax \
       track 300 "python -u -m pytest tests/test_cnn_native_gpu.py -x -q -s --timeout 300 --timeout-method thread -p no:cacheprovider -k 'track'"
     ;;
+  ay)
+    # round 6: the failover drills (GPU) with client-log tails on failure, after the suite's one 8-client drill failure
+    bash tools/gpu_steps.sh r6_ay \
+      drills 600 "env FEDMI_FAILOVER_REPORT=gpurun_out/r6_ay/drills.jsonl python -u -m pytest tests/test_failover_kill.py tests/test_failover_collective.py -m gpu -x -v --timeout 420 --timeout-method thread -p no:cacheprovider"
+    ;;
   list) awk '/^  [a-z]+\)$/ {n=$1; getline; sub(/^ *# round 6: /, ""); print n, $0}' "$0" ;;
   *) echo "unknown run: $run (try: list)" >&2; exit 2 ;;
 esac
